@@ -1,0 +1,187 @@
+/*
+ * nmmo_hip.h — C-ABI of the MI355X-native Neural MMO env stepper (libnmmo_hip.so).
+ *
+ * This is the drop-in boundary for the reference's hot path. The reference (Meeso1/nmmo,
+ * NeurIPS-2023 baselines) reaches the simulator only through Python protocols — there is no
+ * FFI in the reference to bind against — so each entry point below names the reference call
+ * site whose behaviour it replaces:
+ *
+ *   nmmo_create   <- nmmo.Env(Config(...))            reinforcement_learning/environment.py:57
+ *                    + pufferlib pool construction     reinforcement_learning/clean_pufferl.py:106-114
+ *   nmmo_reset    <- pool.async_reset(seed)            clean_pufferl.py:175
+ *                    -> env.reset(seed=...)            reinforcement_learning/stat_wrapper.py:51
+ *   nmmo_step     <- pool.send(actions); pool.recv()   clean_pufferl.py:357, :293
+ *                    -> env.step(actions)              stat_wrapper.py:64
+ *   nmmo_layout   <- pool.single_observation_space / driver_env.unflatten_context
+ *                                                      clean_pufferl.py:116, baseline_policy.py:28,41
+ *   nmmo_get_state / nmmo_set_state  <- env.realm.{players,npcs,map,tick} reads
+ *                                                      stat_wrapper.py:122-185, train_helper.py:133-166
+ *   nmmo_scripted_actions  <- (bench/test helper) masked-uniform actions, the behaviour of an
+ *                    untrained masked policy           agent_zoo/neurips23_start_kit/baseline_policy.py:228-264
+ *
+ * Conventions: every call returns 0 on success or a negative NMMO_E_* code (never aborts);
+ * nmmo_last_error() returns a thread-local message. Every I/O buffer passed to step/reset is a
+ * caller-owned DEVICE pointer (e.g. torch tensor .data_ptr()); the handle owns the env state in
+ * HBM. Work is enqueued on `stream` (a hipStream_t, NULL = default stream) with no implicit
+ * device synchronisation and no allocation inside step (graph-capturable). One host thread per
+ * handle; handles are independent (one per GPU rank).
+ *
+ * The game semantics these calls implement are frozen in SPEC.md (v1); the state layout below
+ * is shared bit-for-bit with the CPU oracle under oracle/ (test infrastructure only).
+ */
+#ifndef NMMO_HIP_H
+#define NMMO_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NMMO_API __attribute__((visibility("default")))
+#define NMMO_ABI_VERSION 1
+
+/* ---- error codes ---- */
+#define NMMO_OK 0
+#define NMMO_E_INVALID (-1)   /* bad argument / config */
+#define NMMO_E_HIP (-2)       /* HIP runtime error */
+#define NMMO_E_NOMEM (-3)     /* device allocation failed */
+#define NMMO_E_SIZE (-4)      /* buffer size mismatch */
+
+/* ---- systems bitmask (mirrors the Config mixins, environment.py:14-25) ---- */
+#define NMMO_SYS_RESOURCE (1u << 0)
+#define NMMO_SYS_COMBAT (1u << 1)
+#define NMMO_SYS_NPC (1u << 2)
+#define NMMO_SYS_PROGRESSION (1u << 3)
+#define NMMO_SYS_ITEM (1u << 4)
+#define NMMO_SYS_EQUIPMENT (1u << 5)
+#define NMMO_SYS_PROFESSION (1u << 6)
+#define NMMO_SYS_EXCHANGE (1u << 7)
+#define NMMO_SYS_ALL 0xFFu
+
+/* ---- observation layouts ---- */
+#define NMMO_OBS_NONE 0   /* C2/C3 benchmark configs: state only */
+#define NMMO_OBS_FLAT 1   /* pufferlib-0.7.3 flat float32 vector, 23,987 / agent */
+
+/* ---- fixed geometry (nmmo 2.1 defaults, SPEC.md §1) ---- */
+#define NMMO_MAP_SIZE 160          /* MAP_CENTER 128 + 2 * MAP_BORDER 16 */
+#define NMMO_MAP_TILES (NMMO_MAP_SIZE * NMMO_MAP_SIZE)
+#define NMMO_N_MATERIALS 16
+#define NMMO_N_ENTITY_COLS 31      /* Entity obs columns (baseline_policy.py:118) */
+#define NMMO_N_ACTION_HEADS 12     /* takeru/policy.py:293-307 */
+
+/* Entity table fields: int16 [n_envs][NMMO_NF][slots]; fields 0..30 ARE the Entity obs
+ * columns, in nmmo EntityState order (id col 0, npc_type col 1: baseline_policy.py:118-129). */
+enum NmmoField {
+  F_ID = 0, F_NPC_TYPE, F_ROW, F_COL, F_DAMAGE, F_TIME_ALIVE, F_FREEZE, F_ITEM_LEVEL,
+  F_ATTACKER_ID, F_LATEST_COMBAT_TICK, F_MESSAGE, F_GOLD, F_HEALTH, F_FOOD, F_WATER,
+  F_MELEE_LEVEL, F_MELEE_EXP, F_RANGE_LEVEL, F_RANGE_EXP, F_MAGE_LEVEL, F_MAGE_EXP,
+  F_FISHING_LEVEL, F_FISHING_EXP, F_HERBALISM_LEVEL, F_HERBALISM_EXP,
+  F_PROSPECTING_LEVEL, F_PROSPECTING_EXP, F_CARVING_LEVEL, F_CARVING_EXP,
+  F_ALCHEMY_LEVEL, F_ALCHEMY_EXP,
+  /* --- internal (not observed) --- */
+  F_ALIVE = 31,        /* 1 while in the realm */
+  F_DS_ROW,            /* datastore row (1-based; obs Entity rows are listed in this order) */
+  F_RESILIENT,         /* RESOURCE_RESILIENT_POPULATION draw */
+  F_EXPLORATION,       /* history.exploration (GO_FARTHEST record) */
+  F_STYLE,             /* NPC combat style 0 melee 1 range 2 mage */
+  F_TARGET_ID,         /* NPC AI target (player id, 0 = none) */
+  F_NPC_LEVEL,         /* NPC spawn level */
+  F_EQUIP_OFFENSE,     /* NPC equipment offense (equipment system) */
+  F_EQUIP_DEFENSE,     /* NPC equipment defense */
+  F_PLAYER_KILLS,
+  F_HEALTH_RESTORE,    /* Resources.health_restore of the last update */
+  F_DIED_TICK,         /* tick at which the player was culled (0 = alive) */
+  NMMO_NF_USED,
+  NMMO_NF = 48
+};
+
+/* Env scalar fields: int32 [n_envs][NMMO_NE]. */
+enum NmmoEnvField {
+  E_TICK = 0, E_MAP_ID, E_DONE, E_EPISODE, E_NPC_COUNT, E_NPC_NEXT_ID, E_FREE_HEAD,
+  E_FREE_COUNT, E_SEED_LO, E_SEED_HI, E_PLAYERS_ALIVE, E_ENV_INDEX,
+  NMMO_NE_USED,
+  NMMO_NE = 16
+};
+
+typedef struct NmmoConfig {
+  int32_t abi_version;        /* must be NMMO_ABI_VERSION */
+  int32_t player_n;           /* PLAYER_N 128 (environment.py:35, config.yaml:76); <= 128 */
+  int32_t npc_n;              /* NPC_N 256 (environment.py:43, config.yaml:77); <= 256 */
+  int32_t horizon;            /* HORIZON 1024 (environment.py:35) */
+  int32_t map_n;              /* MAP_N 256 (environment.py:36) */
+  int32_t spawn_immunity;     /* COMBAT_SPAWN_IMMUNITY 20 (environment.py:48) */
+  int32_t early_stop_agent_num; /* BaseStatWrapper early stop (stat_wrapper.py:68-69), 0 = off */
+  uint32_t resilient_u32;     /* RESOURCE_RESILIENT_POPULATION as a u32 threshold (0.2 -> 0x33333333) */
+  uint32_t systems;           /* NMMO_SYS_* bitmask (environment.py:14-25) */
+  int32_t obs_layout;         /* NMMO_OBS_* */
+  int32_t task_embed_dim;     /* TASK_EMBED_DIM 2048 (environment.py:44) */
+  int32_t task_num_tick;      /* default task TickGE(num_tick) (manual_curriculum.py:56) */
+  uint64_t map_seed;          /* map-bank generator seed */
+  uint64_t env_index_base;    /* global index of env 0 of this handle (rank sharding) */
+} NmmoConfig;
+
+typedef struct NmmoLayout {
+  int32_t obs_elems;          /* per-agent elements of the flat obs (23,987) */
+  int32_t act_heads;          /* 12 */
+  int32_t act_dims[NMMO_N_ACTION_HEADS];
+  /* flat obs offsets (pufferlib sorted-key order) */
+  int32_t off_mask_attack_style, off_mask_attack_target, off_mask_buy, off_mask_destroy,
+      off_mask_give_item, off_mask_give_target, off_mask_givegold_price, off_mask_givegold_target,
+      off_mask_move, off_mask_sell_item, off_mask_sell_price, off_mask_use;
+  int32_t off_agent_id, off_current_tick, off_entity, off_inventory, off_market, off_task, off_tile;
+  int32_t entity_rows, entity_cols, inventory_rows, item_cols, market_rows, tile_rows, tile_cols;
+  /* state blob geometry */
+  int32_t slots;              /* player_n + npc_n */
+  int32_t nf, ne;
+  size_t state_bytes_per_env; /* see nmmo_get_state */
+} NmmoLayout;
+
+typedef struct NmmoHandle NmmoHandle;
+
+/* Fill cfg with the reference defaults (environment.py:31-49 + config.yaml env:). */
+NMMO_API void nmmo_default_config(NmmoConfig* cfg);
+NMMO_API int nmmo_layout(const NmmoConfig* cfg, NmmoLayout* out);
+
+/* Allocate the SoA state for n_envs envs on `device` and generate the map bank.
+ * task_embedding: host fp16[task_embed_dim] used as every agent's Task obs (may be NULL). */
+NMMO_API int nmmo_create(const NmmoConfig* cfg, int32_t n_envs, uint64_t seed, int32_t device,
+                const uint16_t* task_embedding, NmmoHandle** out);
+NMMO_API void nmmo_destroy(NmmoHandle* h);
+
+/* Reset every env (env_seeds: host uint64[n_envs] or NULL = derive from the create seed). */
+NMMO_API int nmmo_reset(NmmoHandle* h, const uint64_t* env_seeds, void* obs, uint8_t* mask, void* stream);
+
+/* One tick of every env. actions: device int32 [n_envs][player_n][12]. Envs whose previous
+ * step ended the episode are reset instead (pufferlib auto-reset), with rewards/flags 0.
+ * obs: device float32 [n_envs][player_n][obs_elems] (NMMO_OBS_FLAT) or NULL (NMMO_OBS_NONE).
+ * rew f32, term/trunc/mask u8: device [n_envs][player_n]. */
+NMMO_API int nmmo_step(NmmoHandle* h, const int32_t* actions, void* obs, float* rew, uint8_t* term,
+              uint8_t* trunc, uint8_t* mask, void* stream);
+
+/* Masked-uniform scripted actions from the current state (bench / tests). */
+NMMO_API int nmmo_scripted_actions(NmmoHandle* h, uint64_t policy_seed, int32_t* actions, void* stream);
+
+/* State blob: per env, [NMMO_NE int32 env fields][NF*slots int16 entity table]
+ * [slots int16 free-row ring][MAP_TILES u8 material]; envs concatenated. Synchronous. */
+NMMO_API int nmmo_get_state(NmmoHandle* h, void* host_buf, size_t nbytes);
+NMMO_API int nmmo_set_state(NmmoHandle* h, const void* host_buf, size_t nbytes);
+/* The generated map bank: host u8 [map_n][MAP_TILES]. Synchronous. */
+NMMO_API int nmmo_get_map_bank(NmmoHandle* h, uint8_t* host_buf, size_t nbytes);
+
+/* Kernel timing with HIP events recorded on the launch stream around each kernel of
+ * nmmo_step (bench/profiling; off by default, up to 8192 steps buffered).
+ * nmmo_read_timing synchronises, returns the summed milliseconds of the tick and obs kernels
+ * over the buffered steps in ms[0], ms[1], their count in *n, and clears the buffer. */
+NMMO_API int nmmo_set_timing(NmmoHandle* h, int32_t enable);
+NMMO_API int nmmo_read_timing(NmmoHandle* h, double* ms /* [2] */, int32_t* n);
+
+NMMO_API int32_t nmmo_n_envs(const NmmoHandle* h);
+NMMO_API const char* nmmo_last_error(void);
+NMMO_API int32_t nmmo_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NMMO_HIP_H */

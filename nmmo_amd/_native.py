@@ -1,0 +1,74 @@
+"""Loader for libnmmo_hip.so (the HIP path). Fails loudly: there is no CPU fallback.
+
+torch is imported first so that the library's libamdhip64.so.7 dependency binds to the HIP
+runtime torch already loaded (one runtime per process: device pointers from the torch caching
+allocator and streams from torch.cuda are then valid inside the library).
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+
+from . import abi
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libnmmo_hip.so")
+_lib = None
+
+SYMBOLS = [
+    "nmmo_default_config", "nmmo_layout", "nmmo_create", "nmmo_destroy", "nmmo_reset",
+    "nmmo_step", "nmmo_scripted_actions", "nmmo_get_state", "nmmo_set_state",
+    "nmmo_get_map_bank", "nmmo_set_timing", "nmmo_read_timing", "nmmo_n_envs",
+    "nmmo_last_error", "nmmo_abi_version",
+]
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    import torch  # noqa: F401  (bind the HIP runtime torch ships, see module docstring)
+
+    if not os.path.exists(LIB_PATH):
+        raise NativeError(
+            f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+            " (there is no CPU fallback for the HIP stepper)")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, i32, u64, sz = ctypes.c_void_p, ctypes.c_int32, ctypes.c_uint64, ctypes.c_size_t
+    cfgp = ctypes.POINTER(abi.NmmoConfig)
+    L.nmmo_default_config.argtypes = [cfgp]
+    L.nmmo_default_config.restype = None
+    L.nmmo_layout.argtypes = [cfgp, ctypes.POINTER(abi.NmmoLayout)]
+    L.nmmo_create.argtypes = [cfgp, i32, u64, i32, vp, ctypes.POINTER(vp)]
+    L.nmmo_destroy.argtypes = [vp]
+    L.nmmo_destroy.restype = None
+    L.nmmo_reset.argtypes = [vp, vp, vp, vp, vp]
+    L.nmmo_step.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp]
+    L.nmmo_scripted_actions.argtypes = [vp, u64, vp, vp]
+    L.nmmo_get_state.argtypes = [vp, vp, sz]
+    L.nmmo_set_state.argtypes = [vp, vp, sz]
+    L.nmmo_get_map_bank.argtypes = [vp, vp, sz]
+    L.nmmo_set_timing.argtypes = [vp, i32]
+    L.nmmo_read_timing.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i32)]
+    L.nmmo_n_envs.argtypes = [vp]
+    L.nmmo_last_error.restype = ctypes.c_char_p
+    L.nmmo_abi_version.restype = i32
+    if L.nmmo_abi_version() != abi.ABI_VERSION:
+        raise NativeError(f"ABI mismatch: lib {L.nmmo_abi_version()} != python {abi.ABI_VERSION}")
+    _lib = L
+    return L
+
+
+def check(rc: int, what: str):
+    if rc != abi.NMMO_OK:
+        raise NativeError(f"{what} failed ({rc}): {lib().nmmo_last_error().decode()}")
+
+
+def layout(cfg: abi.NmmoConfig) -> abi.NmmoLayout:
+    out = abi.NmmoLayout()
+    check(lib().nmmo_layout(ctypes.byref(cfg), ctypes.byref(out)), "nmmo_layout")
+    return out

@@ -1,0 +1,99 @@
+"""ctypes mirror of include/nmmo_hip.h (the C-ABI boundary).
+
+Field enums and struct layouts must match the header exactly; tests/test_abi.py checks the
+struct sizes against the compiled library and the enum values against the header text.
+"""
+
+import ctypes
+
+ABI_VERSION = 1
+
+NMMO_OK = 0
+NMMO_E_INVALID = -1
+NMMO_E_HIP = -2
+NMMO_E_NOMEM = -3
+NMMO_E_SIZE = -4
+
+SYS_RESOURCE = 1 << 0
+SYS_COMBAT = 1 << 1
+SYS_NPC = 1 << 2
+SYS_PROGRESSION = 1 << 3
+SYS_ITEM = 1 << 4
+SYS_EQUIPMENT = 1 << 5
+SYS_PROFESSION = 1 << 6
+SYS_EXCHANGE = 1 << 7
+SYS_ALL = 0xFF
+
+OBS_NONE = 0
+OBS_FLAT = 1
+
+MAP_SIZE = 160
+MAP_TILES = MAP_SIZE * MAP_SIZE
+N_ENTITY_COLS = 31
+N_ACTION_HEADS = 12
+NF = 48
+NE = 16
+
+# Entity table fields (int16 [n_envs][NF][slots]); 0..30 are the Entity obs columns.
+ENTITY_FIELDS = [
+    "id", "npc_type", "row", "col", "damage", "time_alive", "freeze", "item_level",
+    "attacker_id", "latest_combat_tick", "message", "gold", "health", "food", "water",
+    "melee_level", "melee_exp", "range_level", "range_exp", "mage_level", "mage_exp",
+    "fishing_level", "fishing_exp", "herbalism_level", "herbalism_exp",
+    "prospecting_level", "prospecting_exp", "carving_level", "carving_exp",
+    "alchemy_level", "alchemy_exp",
+    # internal
+    "alive", "ds_row", "resilient", "exploration", "style", "target_id", "npc_level",
+    "equip_offense", "equip_defense", "player_kills", "health_restore", "died_tick",
+]
+F = {name: i for i, name in enumerate(ENTITY_FIELDS)}
+
+ENV_FIELDS = [
+    "tick", "map_id", "done", "episode", "npc_count", "npc_next_id", "free_head",
+    "free_count", "seed_lo", "seed_hi", "players_alive", "env_index",
+]
+E = {name: i for i, name in enumerate(ENV_FIELDS)}
+
+
+class NmmoConfig(ctypes.Structure):
+    _fields_ = [
+        ("abi_version", ctypes.c_int32),
+        ("player_n", ctypes.c_int32),
+        ("npc_n", ctypes.c_int32),
+        ("horizon", ctypes.c_int32),
+        ("map_n", ctypes.c_int32),
+        ("spawn_immunity", ctypes.c_int32),
+        ("early_stop_agent_num", ctypes.c_int32),
+        ("resilient_u32", ctypes.c_uint32),
+        ("systems", ctypes.c_uint32),
+        ("obs_layout", ctypes.c_int32),
+        ("task_embed_dim", ctypes.c_int32),
+        ("task_num_tick", ctypes.c_int32),
+        ("map_seed", ctypes.c_uint64),
+        ("env_index_base", ctypes.c_uint64),
+    ]
+
+
+_MASK_NAMES = [
+    "mask_attack_style", "mask_attack_target", "mask_buy", "mask_destroy", "mask_give_item",
+    "mask_give_target", "mask_givegold_price", "mask_givegold_target", "mask_move",
+    "mask_sell_item", "mask_sell_price", "mask_use",
+]
+
+
+class NmmoLayout(ctypes.Structure):
+    _fields_ = (
+        [("obs_elems", ctypes.c_int32), ("act_heads", ctypes.c_int32),
+         ("act_dims", ctypes.c_int32 * N_ACTION_HEADS)]
+        + [("off_" + n, ctypes.c_int32) for n in _MASK_NAMES]
+        + [("off_" + n, ctypes.c_int32) for n in
+           ["agent_id", "current_tick", "entity", "inventory", "market", "task", "tile"]]
+        + [(n, ctypes.c_int32) for n in
+           ["entity_rows", "entity_cols", "inventory_rows", "item_cols", "market_rows",
+            "tile_rows", "tile_cols", "slots", "nf", "ne"]]
+        + [("state_bytes_per_env", ctypes.c_size_t)]
+    )
+
+
+def state_bytes_per_env(slots: int) -> int:
+    return NE * 4 + NF * slots * 2 + slots * 2 + MAP_TILES

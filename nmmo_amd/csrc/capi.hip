@@ -1,0 +1,349 @@
+// capi.hip — the C-ABI of libnmmo_hip.so (include/nmmo_hip.h). Host side only: owns the
+// device state (SoA over env x slot in HBM), enqueues the gfx950 kernels on the caller's
+// stream, never synchronises inside nmmo_step (graph-capturable, no allocation).
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "kernels.h"
+
+
+
+using namespace nmmo;
+
+static thread_local std::string g_err;
+
+static int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+static int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+#define HIP_TRY(expr)                                                                    \
+  do {                                                                                   \
+    hipError_t _e = (expr);                                                              \
+    if (_e != hipSuccess) return fail(NMMO_E_HIP, "%s: %s", #expr, hipGetErrorString(_e)); \
+  } while (0)
+
+struct NmmoHandle {
+  NmmoConfig cfg;
+  NmmoLayout layout;
+  DevState st;
+  int device;
+  int32_t* d_env = nullptr;
+  int16_t* d_ent = nullptr;
+  int16_t* d_ring = nullptr;
+  uint8_t* d_mat = nullptr;
+  uint32_t* d_dep = nullptr;
+  uint8_t* d_bank = nullptr;
+  float* d_task = nullptr;
+  uint64_t* d_seeds = nullptr;
+  // bench timing (nmmo_set_timing): event pairs around the tick and obs kernels
+  bool timing = false;
+  int t_count = 0;
+  std::vector<hipEvent_t> ev;  // [kTimingCap][4]: tick begin/end, obs begin/end
+};
+static constexpr int kTimingCap = 8192;
+
+static float half_to_float(uint16_t h) {
+  uint32_t s = (uint32_t)(h >> 15) << 31, e = (h >> 10) & 31, m = h & 1023, bits;
+  if (e == 0) {
+    if (m == 0) {
+      bits = s;
+    } else {
+      int sh = 0;
+      while (!(m & 1024)) { m <<= 1; sh++; }
+      m &= 1023;
+      bits = s | ((uint32_t)(127 - 15 - sh + 1) << 23) | (m << 13);
+    }
+  } else if (e == 31) {
+    bits = s | 0x7F800000u | (m << 13);
+  } else {
+    bits = s | ((e + 112) << 23) | (m << 13);
+  }
+  float f;
+  memcpy(&f, &bits, 4);
+  return f;
+}
+
+extern "C" {
+
+int32_t nmmo_abi_version(void) { return NMMO_ABI_VERSION; }
+const char* nmmo_last_error(void) { return g_err.c_str(); }
+
+void nmmo_default_config(NmmoConfig* c) {
+  memset(c, 0, sizeof(*c));
+  c->abi_version = NMMO_ABI_VERSION;
+  c->player_n = 128;
+  c->npc_n = 256;
+  c->horizon = 1024;
+  c->map_n = 256;
+  c->spawn_immunity = 20;
+  c->early_stop_agent_num = 0;
+  c->resilient_u32 = 858993459u;  // 0.2 * 2^32
+  c->systems = NMMO_SYS_ALL;
+  c->obs_layout = NMMO_OBS_FLAT;
+  c->task_embed_dim = 2048;
+  c->task_num_tick = 1024;
+  c->map_seed = 0;
+  c->env_index_base = 0;
+}
+
+int nmmo_layout(const NmmoConfig* cfg, NmmoLayout* L) {
+  if (!cfg || !L) return fail(NMMO_E_INVALID, "null argument");
+  memset(L, 0, sizeof(*L));
+  const int dims[NMMO_N_ACTION_HEADS] = {3, 101, 1025, 13, 13, 101, 99, 101, 5, 13, 99, 13};
+  L->act_heads = NMMO_N_ACTION_HEADS;
+  int o = 0;
+  int* offs[NMMO_N_ACTION_HEADS] = {
+      &L->off_mask_attack_style, &L->off_mask_attack_target, &L->off_mask_buy,
+      &L->off_mask_destroy, &L->off_mask_give_item, &L->off_mask_give_target,
+      &L->off_mask_givegold_price, &L->off_mask_givegold_target, &L->off_mask_move,
+      &L->off_mask_sell_item, &L->off_mask_sell_price, &L->off_mask_use};
+  for (int h = 0; h < NMMO_N_ACTION_HEADS; h++) {
+    L->act_dims[h] = dims[h];
+    *offs[h] = o;
+    o += dims[h];
+  }
+  L->off_agent_id = o; o += 1;
+  L->off_current_tick = o; o += 1;
+  L->off_entity = o; o += 100 * NMMO_N_ENTITY_COLS;
+  L->off_inventory = o; o += 12 * 16;
+  L->off_market = o; o += 1024 * 16;
+  L->off_task = o; o += cfg->task_embed_dim;
+  L->off_tile = o; o += 225 * 3;
+  L->obs_elems = o;
+  L->entity_rows = 100; L->entity_cols = NMMO_N_ENTITY_COLS;
+  L->inventory_rows = 12; L->item_cols = 16; L->market_rows = 1024;
+  L->tile_rows = 225; L->tile_cols = 3;
+  const int npc = (cfg->systems & NMMO_SYS_NPC) ? cfg->npc_n : 0;
+  L->slots = cfg->player_n + npc;
+  L->nf = NMMO_NF;
+  L->ne = NMMO_NE;
+  L->state_bytes_per_env = (size_t)NMMO_NE * 4 + (size_t)NMMO_NF * L->slots * 2 +
+                           (size_t)L->slots * 2 + NMMO_MAP_TILES;
+  return NMMO_OK;
+}
+
+int32_t nmmo_n_envs(const NmmoHandle* h) { return h ? h->st.n_envs : 0; }
+
+void nmmo_destroy(NmmoHandle* h) {
+  if (!h) return;
+  (void)hipSetDevice(h->device);
+  for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
+  void* bufs[] = {h->d_env, h->d_ent, h->d_ring, h->d_mat, h->d_dep, h->d_bank, h->d_task, h->d_seeds};
+  for (void* b : bufs)
+    if (b) (void)hipFree(b);
+  delete h;
+}
+
+int nmmo_create(const NmmoConfig* cfg, int32_t n_envs, uint64_t seed, int32_t device,
+                const uint16_t* task_embedding, NmmoHandle** out) {
+  if (!cfg || !out) return fail(NMMO_E_INVALID, "null argument");
+  *out = nullptr;
+  if (cfg->abi_version != NMMO_ABI_VERSION)
+    return fail(NMMO_E_INVALID, "abi_version %d != %d", cfg->abi_version, NMMO_ABI_VERSION);
+  if (n_envs <= 0) return fail(NMMO_E_INVALID, "n_envs must be > 0");
+  if (cfg->player_n <= 0 || cfg->player_n > 128) return fail(NMMO_E_INVALID, "player_n in 1..128");
+  if (cfg->npc_n < 0 || cfg->npc_n > 256) return fail(NMMO_E_INVALID, "npc_n in 0..256");
+  if (cfg->map_n <= 0) return fail(NMMO_E_INVALID, "map_n must be > 0");
+  if (cfg->horizon <= 0 || cfg->task_num_tick <= 0) return fail(NMMO_E_INVALID, "horizon/task_num_tick");
+  if (cfg->task_embed_dim < 0 || cfg->task_embed_dim > 65536) return fail(NMMO_E_INVALID, "task_embed_dim");
+  if (cfg->obs_layout != NMMO_OBS_NONE && cfg->obs_layout != NMMO_OBS_FLAT)
+    return fail(NMMO_E_INVALID, "obs_layout %d", cfg->obs_layout);
+  NmmoHandle* h = new NmmoHandle();
+  h->cfg = *cfg;
+  h->device = device;
+  nmmo_layout(cfg, &h->layout);
+  const int P = cfg->player_n, N = (cfg->systems & NMMO_SYS_NPC) ? cfg->npc_n : 0, S = P + N;
+  auto cleanup_fail = [&](int code) { nmmo_destroy(h); return code; };
+  if (hipSetDevice(device) != hipSuccess) return cleanup_fail(fail(NMMO_E_HIP, "hipSetDevice(%d)", device));
+  const size_t n = (size_t)n_envs;
+#define ALLOC(ptr, bytes)                                                               \
+  if (hipMalloc((void**)&(ptr), (bytes)) != hipSuccess)                                  \
+    return cleanup_fail(fail(NMMO_E_NOMEM, "hipMalloc %zu bytes for %s", (size_t)(bytes), #ptr)); \
+  if (hipMemset((ptr), 0, (bytes)) != hipSuccess) return cleanup_fail(fail(NMMO_E_HIP, "hipMemset"));
+  ALLOC(h->d_env, n * NMMO_NE * 4);
+  ALLOC(h->d_ent, n * NMMO_NF * S * 2);
+  ALLOC(h->d_ring, n * S * 2);
+  ALLOC(h->d_mat, n * NMMO_MAP_TILES);
+  ALLOC(h->d_dep, n * kBitmapWords * 4);
+  ALLOC(h->d_bank, (size_t)cfg->map_n * NMMO_MAP_TILES);
+  ALLOC(h->d_task, (size_t)(cfg->task_embed_dim > 0 ? cfg->task_embed_dim : 1) * 4);
+  ALLOC(h->d_seeds, n * 8);
+#undef ALLOC
+  if (task_embedding && cfg->task_embed_dim > 0) {
+    std::vector<float> t(cfg->task_embed_dim);
+    for (int k = 0; k < cfg->task_embed_dim; k++) t[k] = half_to_float(task_embedding[k]);
+    if (hipMemcpy(h->d_task, t.data(), t.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+      return cleanup_fail(fail(NMMO_E_HIP, "task upload"));
+  }
+  h->st = DevState{h->d_env, h->d_ent, h->d_ring, h->d_mat, h->d_dep, h->d_bank,
+                   n_envs, P, N, S, seed, *cfg};
+  if (launch_mapgen(cfg->map_seed, cfg->map_n, h->d_bank, nullptr) != hipSuccess ||
+      hipDeviceSynchronize() != hipSuccess)
+    return cleanup_fail(fail(NMMO_E_HIP, "map generation failed: %s", hipGetErrorString(hipGetLastError())));
+  *out = h;
+  return NMMO_OK;
+}
+
+static ObsParams obs_params(NmmoHandle* h, float* obs) {
+  const NmmoLayout& L = h->layout;
+  ObsParams p;
+  p.env = h->d_env; p.ent = h->d_ent; p.mat = h->d_mat; p.task = h->d_task; p.obs = obs;
+  p.n_envs = h->st.n_envs; p.P = h->st.P; p.S = h->st.S; p.elems = L.obs_elems;
+  p.task_dim = h->cfg.task_embed_dim; p.systems = h->cfg.systems;
+  p.spawn_immunity = h->cfg.spawn_immunity;
+  p.o_style = L.off_mask_attack_style; p.o_target = L.off_mask_attack_target;
+  p.o_buy = L.off_mask_buy; p.o_destroy = L.off_mask_destroy;
+  p.o_give_item = L.off_mask_give_item; p.o_give_target = L.off_mask_give_target;
+  p.o_gg_price = L.off_mask_givegold_price; p.o_gg_target = L.off_mask_givegold_target;
+  p.o_move = L.off_mask_move; p.o_sell_item = L.off_mask_sell_item;
+  p.o_sell_price = L.off_mask_sell_price; p.o_use = L.off_mask_use;
+  p.o_agent_id = L.off_agent_id; p.o_tick = L.off_current_tick; p.o_entity = L.off_entity;
+  p.o_inventory = L.off_inventory; p.o_market = L.off_market; p.o_task = L.off_task;
+  p.o_tile = L.off_tile;
+  return p;
+}
+
+int nmmo_reset(NmmoHandle* h, const uint64_t* env_seeds, void* obs, uint8_t* mask, void* stream) {
+  if (!h) return fail(NMMO_E_INVALID, "null handle");
+  hipStream_t s = (hipStream_t)stream;
+  HIP_TRY(hipSetDevice(h->device));
+  if (env_seeds) {
+    HIP_TRY(hipMemcpyAsync(h->d_seeds, env_seeds, (size_t)h->st.n_envs * 8, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipStreamSynchronize(s));  // host seeds may go away after return
+  }
+  HIP_TRY(launch_tick(h->st, nullptr, env_seeds ? h->d_seeds : nullptr, nullptr, nullptr, nullptr,
+                      mask, 1, s));
+  if (obs && h->cfg.obs_layout == NMMO_OBS_FLAT) HIP_TRY(launch_obs(obs_params(h, (float*)obs), s));
+  return NMMO_OK;
+}
+
+int nmmo_step(NmmoHandle* h, const int32_t* actions, void* obs, float* rew, uint8_t* term,
+              uint8_t* trunc, uint8_t* mask, void* stream) {
+  if (!h) return fail(NMMO_E_INVALID, "null handle");
+  if (!actions || !rew || !term || !trunc || !mask)
+    return fail(NMMO_E_INVALID, "actions/rew/term/trunc/mask must be device pointers");
+  hipStream_t s = (hipStream_t)stream;
+  const bool rec = h->timing && h->t_count < kTimingCap;
+  hipEvent_t* ev = rec ? &h->ev[(size_t)h->t_count * 4] : nullptr;
+  if (rec) HIP_TRY(hipEventRecord(ev[0], s));
+  HIP_TRY(launch_tick(h->st, actions, nullptr, rew, term, trunc, mask, 0, s));
+  if (rec) HIP_TRY(hipEventRecord(ev[1], s));
+  const bool do_obs = obs && h->cfg.obs_layout == NMMO_OBS_FLAT;
+  if (do_obs) HIP_TRY(launch_obs(obs_params(h, (float*)obs), s));
+  if (rec) {
+    HIP_TRY(hipEventRecord(ev[2], s));  // obs span = ev[1]..ev[2] (empty when no obs)
+    h->t_count++;
+  }
+  return NMMO_OK;
+}
+
+int nmmo_set_timing(NmmoHandle* h, int32_t enable) {
+  if (!h) return fail(NMMO_E_INVALID, "null handle");
+  HIP_TRY(hipSetDevice(h->device));
+  if (enable && h->ev.empty()) {
+    h->ev.resize((size_t)kTimingCap * 4);
+    for (auto& e : h->ev) HIP_TRY(hipEventCreate(&e));
+  }
+  h->timing = enable != 0;
+  h->t_count = 0;
+  return NMMO_OK;
+}
+
+int nmmo_read_timing(NmmoHandle* h, double* ms, int32_t* n) {
+  if (!h || !ms || !n) return fail(NMMO_E_INVALID, "null argument");
+  ms[0] = ms[1] = 0.0;
+  *n = h->t_count;
+  for (int i = 0; i < h->t_count; i++) {
+    hipEvent_t* ev = &h->ev[(size_t)i * 4];
+    float a = 0.f, b = 0.f;
+    HIP_TRY(hipEventSynchronize(ev[2]));
+    HIP_TRY(hipEventElapsedTime(&a, ev[0], ev[1]));
+    HIP_TRY(hipEventElapsedTime(&b, ev[1], ev[2]));
+    ms[0] += a;
+    ms[1] += b;
+  }
+  h->t_count = 0;
+  return NMMO_OK;
+}
+
+int nmmo_scripted_actions(NmmoHandle* h, uint64_t policy_seed, int32_t* actions, void* stream) {
+  if (!h || !actions) return fail(NMMO_E_INVALID, "null argument");
+  PolicyParams p;
+  p.env = h->d_env; p.ent = h->d_ent; p.mat = h->d_mat; p.actions = actions;
+  p.n_envs = h->st.n_envs; p.P = h->st.P; p.S = h->st.S; p.systems = h->cfg.systems;
+  p.spawn_immunity = h->cfg.spawn_immunity; p.seed = policy_seed;
+  HIP_TRY(launch_policy(p, (hipStream_t)stream));
+  return NMMO_OK;
+}
+
+int nmmo_get_state(NmmoHandle* h, void* host_buf, size_t nbytes) {
+  if (!h || !host_buf) return fail(NMMO_E_INVALID, "null argument");
+  const size_t n = (size_t)h->st.n_envs, S = (size_t)h->st.S;
+  const size_t per = h->layout.state_bytes_per_env;
+  if (nbytes != per * n) return fail(NMMO_E_SIZE, "state buffer %zu != %zu", nbytes, per * n);
+  HIP_TRY(hipSetDevice(h->device));
+  HIP_TRY(hipDeviceSynchronize());
+  std::vector<int32_t> env(n * NMMO_NE);
+  std::vector<int16_t> ent(n * NMMO_NF * S), ring(n * S);
+  std::vector<uint8_t> mat(n * NMMO_MAP_TILES);
+  HIP_TRY(hipMemcpy(env.data(), h->d_env, env.size() * 4, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(ent.data(), h->d_ent, ent.size() * 2, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(ring.data(), h->d_ring, ring.size() * 2, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(mat.data(), h->d_mat, mat.size(), hipMemcpyDeviceToHost));
+  uint8_t* b = (uint8_t*)host_buf;
+  for (size_t e = 0; e < n; e++) {
+    memcpy(b, env.data() + e * NMMO_NE, NMMO_NE * 4); b += NMMO_NE * 4;
+    memcpy(b, ent.data() + e * NMMO_NF * S, NMMO_NF * S * 2); b += NMMO_NF * S * 2;
+    memcpy(b, ring.data() + e * S, S * 2); b += S * 2;
+    memcpy(b, mat.data() + e * NMMO_MAP_TILES, NMMO_MAP_TILES); b += NMMO_MAP_TILES;
+  }
+  return NMMO_OK;
+}
+
+int nmmo_set_state(NmmoHandle* h, const void* host_buf, size_t nbytes) {
+  if (!h || !host_buf) return fail(NMMO_E_INVALID, "null argument");
+  const size_t n = (size_t)h->st.n_envs, S = (size_t)h->st.S;
+  const size_t per = h->layout.state_bytes_per_env;
+  if (nbytes != per * n) return fail(NMMO_E_SIZE, "state buffer %zu != %zu", nbytes, per * n);
+  std::vector<int32_t> env(n * NMMO_NE);
+  std::vector<int16_t> ent(n * NMMO_NF * S), ring(n * S);
+  std::vector<uint8_t> mat(n * NMMO_MAP_TILES);
+  const uint8_t* b = (const uint8_t*)host_buf;
+  for (size_t e = 0; e < n; e++) {
+    memcpy(env.data() + e * NMMO_NE, b, NMMO_NE * 4); b += NMMO_NE * 4;
+    memcpy(ent.data() + e * NMMO_NF * S, b, NMMO_NF * S * 2); b += NMMO_NF * S * 2;
+    memcpy(ring.data() + e * S, b, S * 2); b += S * 2;
+    memcpy(mat.data() + e * NMMO_MAP_TILES, b, NMMO_MAP_TILES); b += NMMO_MAP_TILES;
+  }
+  HIP_TRY(hipSetDevice(h->device));
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(h->d_env, env.data(), env.size() * 4, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(h->d_ent, ent.data(), ent.size() * 2, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(h->d_ring, ring.data(), ring.size() * 2, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(h->d_mat, mat.data(), mat.size(), hipMemcpyHostToDevice));
+  HIP_TRY(launch_rebuild_dep(h->st, nullptr));
+  HIP_TRY(hipDeviceSynchronize());
+  return NMMO_OK;
+}
+
+int nmmo_get_map_bank(NmmoHandle* h, uint8_t* host_buf, size_t nbytes) {
+  if (!h || !host_buf) return fail(NMMO_E_INVALID, "null argument");
+  const size_t need = (size_t)h->cfg.map_n * NMMO_MAP_TILES;
+  if (nbytes != need) return fail(NMMO_E_SIZE, "map bank buffer %zu != %zu", nbytes, need);
+  HIP_TRY(hipSetDevice(h->device));
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(host_buf, h->d_bank, need, hipMemcpyDeviceToHost));
+  return NMMO_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,133 @@
+// common.h — device-side constants and primitives of the gfx950 stepper (SPEC.md §1-§3).
+// Product code: the oracle under oracle/ restates these independently (it shares nothing but
+// include/nmmo_hip.h), so a wrong constant here shows up as a parity failure.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/nmmo_hip.h"
+
+namespace nmmo {
+
+constexpr int kSize = NMMO_MAP_SIZE;  // 160
+constexpr int kTiles = NMMO_MAP_TILES;
+constexpr int kLo = 16, kHi = 143, kCenter = 128, kVision = 7, kNObs = 100;
+constexpr int kBitmapWords = kTiles / 32;  // 800 depleted-tile bitmap words per env
+constexpr int kNFLive = F_DIED_TICK + 1;   // entity fields carried through LDS (43)
+constexpr int kMaxSlots = 384;
+constexpr int kHeads = NMMO_N_ACTION_HEADS;
+
+enum Material : int {
+  M_VOID, M_WATER, M_GRASS, M_SCRUB, M_FOILAGE, M_STONE, M_SLAG, M_ORE, M_STUMP, M_TREE,
+  M_FRAGMENT, M_CRYSTAL, M_WEEDS, M_HERB, M_OCEAN, M_FISH
+};
+enum Purpose : uint32_t {
+  P_MAPSEL = 1, P_SPAWN_OFFSET = 2, P_RESILIENT = 3, P_NPC_SPAWN = 4, P_NPC_MOVE = 5,
+  P_RESPAWN = 6
+};
+
+// bit m set <=> material m is impassable (Void, Water, Stone, Ocean, Fish)
+constexpr uint32_t kImpassableMask = (1u << M_VOID) | (1u << M_WATER) | (1u << M_STONE) |
+                                     (1u << M_OCEAN) | (1u << M_FISH);
+__host__ __device__ inline bool impassable(int m) { return (kImpassableMask >> m) & 1u; }
+
+__host__ __device__ inline uint32_t respawn_u32(int base) {
+  switch (base) {
+    case M_FOILAGE: return 107374182u;
+    case M_TREE: case M_ORE: case M_CRYSTAL: return 429496729u;
+    case M_HERB: case M_FISH: return 85899345u;
+    default: return 0u;
+  }
+}
+
+__host__ __device__ inline int level_at_exp(int exp) {
+  const int thr[10] = {0, 90, 250, 500, 900, 1500, 2400, 3700, 5500, 8000};
+  int l = 0;
+#pragma unroll
+  for (int i = 0; i < 10; i++) l += exp >= thr[i];
+  return l;
+}
+__host__ __device__ inline int exp_at_level(int level) {
+  const int thr[10] = {0, 90, 250, 500, 900, 1500, 2400, 3700, 5500, 8000};
+  return thr[level - 1];
+}
+
+__host__ __device__ inline int dir_dr(int d) { return d == 0 ? -1 : d == 1 ? 1 : 0; }
+__host__ __device__ inline int dir_dc(int d) { return d == 2 ? 1 : d == 3 ? -1 : 0; }
+
+__host__ __device__ inline int iabs(int x) { return x < 0 ? -x : x; }
+__host__ __device__ inline int linf(int r0, int c0, int r1, int c1) {
+  int a = iabs(r0 - r1), b = iabs(c0 - c1);
+  return a > b ? a : b;
+}
+
+// ---------------------------------------------------------------- RNG (SPEC §2)
+__host__ __device__ inline uint64_t splitmix64(uint64_t x) {
+  uint64_t z = x + 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+struct U4 { uint32_t x, y, z, w; };
+
+__host__ __device__ inline U4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                     uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; r++) {
+    uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+    uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+    uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+    uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+    c1 = (uint32_t)p1;
+    c3 = (uint32_t)p0;
+    c0 = n0;
+    c2 = n2;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return U4{c0, c1, c2, c3};
+}
+__host__ __device__ inline U4 draw(uint64_t seed, uint32_t tick, uint32_t purpose,
+                                   uint32_t index, uint32_t sub) {
+  return philox(tick, purpose, index, sub, (uint32_t)seed, (uint32_t)(seed >> 32));
+}
+__host__ __device__ inline uint32_t uniform_n(uint32_t u, uint32_t n) {
+  return (uint32_t)(((uint64_t)u * n) >> 32);
+}
+
+// ---------------------------------------------------------------- map hash (SPEC §3)
+__host__ __device__ inline uint32_t h32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+
+// ---------------------------------------------------------------- LDS/wave helpers
+__device__ inline int lane_id() { return threadIdx.x & 63; }
+__device__ inline int wave_id() { return threadIdx.x >> 6; }
+__device__ inline uint64_t lanes_below() { return (1ull << lane_id()) - 1ull; }
+
+// Block-wide exclusive prefix count of a 0/1 predicate in thread order (<= 16 waves).
+// `wave_tot` is LDS scratch of >= 17 ints. Returns the exclusive count; *total gets the sum.
+__device__ inline int block_prefix_count(bool pred, int* wave_tot, int* total) {
+  const uint64_t b = __ballot(pred);
+  const int w = wave_id(), nw = (blockDim.x + 63) >> 6;
+  if (lane_id() == 0) wave_tot[w] = __popcll(b);
+  __syncthreads();
+  int base = 0, sum = 0;
+  for (int i = 0; i < nw; i++) {
+    int v = wave_tot[i];
+    base += i < w ? v : 0;
+    sum += v;
+  }
+  __syncthreads();
+  *total = sum;
+  return base + __popcll(b & lanes_below());
+}
+
+}  // namespace nmmo

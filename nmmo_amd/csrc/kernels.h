@@ -1,0 +1,54 @@
+// kernels.h — launch interface shared by the kernel translation units and the C-ABI host code.
+#pragma once
+
+#include "common.h"
+
+namespace nmmo {
+
+struct DevState {
+  int32_t* env;          // [n][NMMO_NE]
+  int16_t* ent;          // [n][NMMO_NF][S]
+  int16_t* ring;         // [n][S]
+  uint8_t* mat;          // [n][kTiles]
+  uint32_t* dep;         // [n][kBitmapWords]
+  const uint8_t* bank;   // [map_n][kTiles]
+  int n_envs, P, N, S;   // N = NPC capacity (0 when the NPC system is off), S = P + N
+  uint64_t seed;         // create seed (first-episode seeds)
+  NmmoConfig cfg;
+};
+
+struct ObsParams {
+  const int32_t* env;   // [n][NE]
+  const int16_t* ent;   // [n][NF][S]
+  const uint8_t* mat;   // [n][kTiles]
+  const float* task;    // [task_dim]
+  float* obs;           // [n][P][elems]
+  int n_envs, P, S, elems, task_dim;
+  uint32_t systems;
+  int spawn_immunity;
+  // flat offsets (NmmoLayout)
+  int o_style, o_target, o_buy, o_destroy, o_give_item, o_give_target, o_gg_price, o_gg_target,
+      o_move, o_sell_item, o_sell_price, o_use, o_agent_id, o_tick, o_entity, o_inventory,
+      o_market, o_task, o_tile;
+};
+
+struct PolicyParams {
+  const int32_t* env;
+  const int16_t* ent;
+  const uint8_t* mat;
+  int32_t* actions;  // [n][P][12]
+  int n_envs, P, S;
+  uint32_t systems;
+  int spawn_immunity;
+  uint64_t seed;
+};
+
+hipError_t launch_mapgen(uint64_t seed, int map_n, uint8_t* bank, hipStream_t stream);
+hipError_t launch_tick(const DevState& st, const int32_t* actions, const uint64_t* env_seeds,
+                       float* rew, uint8_t* term, uint8_t* trunc, uint8_t* mask, int mode,
+                       hipStream_t stream);
+hipError_t launch_rebuild_dep(const DevState& st, hipStream_t stream);
+hipError_t launch_obs(const ObsParams& p, hipStream_t stream);
+hipError_t launch_policy(const PolicyParams& p, hipStream_t stream);
+
+}  // namespace nmmo

@@ -1,0 +1,135 @@
+"""NmmoEngine — a batch of envs stepped in lockstep on one GPU through libnmmo_hip.so.
+
+This is the MI355X replacement for the reference's whole env stack below the trainer:
+`nmmo.Env` x num_envs + `pufferlib.vectorization.*` (clean_pufferl.py:106-114). State lives in
+HBM as SoA over (env x slot); I/O buffers are torch tensors on the same device, passed to the
+C-ABI as raw device pointers, and every call is enqueued on torch's current stream.
+"""
+
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import abi
+from ._native import check, layout, lib
+
+
+class NmmoEngine:
+    def __init__(self, config, n_envs: int, seed: int = 0, device=None, task_embedding=None,
+                 env_index_base: int = 0):
+        self.config = config
+        self.n_envs = int(n_envs)
+        self.device = torch.device("cuda", torch.cuda.current_device()) if device is None \
+            else torch.device(device)
+        if self.device.type != "cuda":
+            raise ValueError("NmmoEngine runs on a HIP device only")
+        self.cfg = config.to_c(env_index_base)
+        self.layout = layout(self.cfg)
+        self.P = config.PLAYER_N
+        self.S = self.layout.slots
+        self.obs_elems = self.layout.obs_elems
+        task = None
+        if task_embedding is not None:
+            task = np.ascontiguousarray(np.asarray(task_embedding, dtype=np.float16)).view(np.uint16)
+            if task.size != config.TASK_EMBED_DIM:
+                raise ValueError("task embedding size != TASK_EMBED_DIM")
+        self._task = task
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            check(lib().nmmo_create(ctypes.byref(self.cfg), self.n_envs, seed & (2**64 - 1),
+                                    self.device.index,
+                                    None if task is None else task.ctypes.data_as(ctypes.c_void_p),
+                                    ctypes.byref(h)), "nmmo_create")
+        self.h = h
+        d = self.device
+        n, P = self.n_envs, self.P
+        self.actions = torch.zeros((n, P, abi.N_ACTION_HEADS), dtype=torch.int32, device=d)
+        self.obs = (torch.empty((n, P, self.obs_elems), dtype=torch.float32, device=d)
+                    if config.obs_layout == abi.OBS_FLAT else None)
+        self.rew = torch.zeros((n, P), dtype=torch.float32, device=d)
+        self.term = torch.zeros((n, P), dtype=torch.uint8, device=d)
+        self.trunc = torch.zeros((n, P), dtype=torch.uint8, device=d)
+        self.mask = torch.zeros((n, P), dtype=torch.uint8, device=d)
+
+    def close(self):
+        if getattr(self, "h", None) is not None and self.h.value:
+            torch.cuda.synchronize(self.device)
+            lib().nmmo_destroy(self.h)
+        self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @staticmethod
+    def _ptr(t):
+        return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def reset(self, env_seeds=None):
+        seeds = None
+        if env_seeds is not None:
+            seeds = np.ascontiguousarray(env_seeds, dtype=np.uint64)
+            assert seeds.shape == (self.n_envs,)
+        with torch.cuda.device(self.device):
+            check(lib().nmmo_reset(self.h, None if seeds is None else seeds.ctypes.data_as(ctypes.c_void_p),
+                                   self._ptr(self.obs), self._ptr(self.mask), self._stream()),
+                  "nmmo_reset")
+        self.rew.zero_()
+        self.term.zero_()
+        self.trunc.zero_()
+        return self.obs, self.mask
+
+    def step(self, actions=None):
+        """One tick of every env; `actions` int32 [n_envs, P, 12] on the device (default: the
+        engine's own action buffer). Outputs are the engine's tensors (overwritten in place)."""
+        a = self.actions if actions is None else actions
+        if a.dtype != torch.int32 or not a.is_contiguous() or a.device != self.device:
+            a = a.to(device=self.device, dtype=torch.int32).contiguous()
+        assert tuple(a.shape) == (self.n_envs, self.P, abi.N_ACTION_HEADS)
+        with torch.cuda.device(self.device):
+            check(lib().nmmo_step(self.h, self._ptr(a), self._ptr(self.obs), self._ptr(self.rew),
+                                  self._ptr(self.term), self._ptr(self.trunc), self._ptr(self.mask),
+                                  self._stream()), "nmmo_step")
+        return self.obs, self.rew, self.term, self.trunc, self.mask
+
+    def scripted_actions(self, policy_seed: int, out=None):
+        out = self.actions if out is None else out
+        with torch.cuda.device(self.device):
+            check(lib().nmmo_scripted_actions(self.h, policy_seed & (2**64 - 1), self._ptr(out),
+                                              self._stream()), "nmmo_scripted_actions")
+        return out
+
+    def set_timing(self, enable: bool):
+        check(lib().nmmo_set_timing(self.h, 1 if enable else 0), "nmmo_set_timing")
+
+    def read_timing(self):
+        """(tick_ms_sum, obs_ms_sum, n_steps) from HIP events on the launch stream."""
+        ms = (ctypes.c_double * 2)()
+        n = ctypes.c_int32()
+        check(lib().nmmo_read_timing(self.h, ms, ctypes.byref(n)), "nmmo_read_timing")
+        return ms[0], ms[1], n.value
+
+    def get_state(self) -> np.ndarray:
+        n = self.layout.state_bytes_per_env * self.n_envs
+        buf = np.zeros(n, np.uint8)
+        check(lib().nmmo_get_state(self.h, buf.ctypes.data_as(ctypes.c_void_p), n), "nmmo_get_state")
+        return buf
+
+    def set_state(self, buf: np.ndarray):
+        buf = np.ascontiguousarray(buf, dtype=np.uint8)
+        check(lib().nmmo_set_state(self.h, buf.ctypes.data_as(ctypes.c_void_p), buf.nbytes),
+              "nmmo_set_state")
+
+    def map_bank(self) -> np.ndarray:
+        buf = np.zeros((self.config.MAP_N, abi.MAP_SIZE, abi.MAP_SIZE), np.uint8)
+        check(lib().nmmo_get_map_bank(self.h, buf.ctypes.data_as(ctypes.c_void_p), buf.nbytes),
+              "nmmo_get_map_bank")
+        return buf

@@ -1,0 +1,134 @@
+"""TEST INFRASTRUCTURE ONLY — ctypes wrapper of the CPU oracle (oracle/nmmo_oracle.c).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module.
+Parity vs the real nmmo 2.1 is UNPINNED (see nmmo_oracle.c header and SPEC.md).
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+from nmmo_amd import abi
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "build", "libnmmo_oracle.so")
+_lib = None
+
+
+def build(force: bool = False) -> str:
+    if force or not os.path.exists(LIB_PATH):
+        subprocess.check_call(["make", "-s", "-C", _HERE])
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        vp, i32, u64, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64, ctypes.c_size_t
+        L.oracle_create.restype = vp
+        L.oracle_create.argtypes = [ctypes.POINTER(abi.NmmoConfig), i32, u64, vp]
+        L.oracle_destroy.argtypes = [vp]
+        L.oracle_reset.argtypes = [vp, vp, vp, vp]
+        L.oracle_step.argtypes = [vp, vp, vp, vp, vp, vp, vp]
+        L.oracle_step_range.argtypes = [vp, i32, i32, vp, vp, vp, vp, vp, vp]
+        L.oracle_scripted_actions.argtypes = [vp, u64, vp]
+        L.oracle_scripted_actions_range.argtypes = [vp, i32, i32, u64, vp]
+        L.oracle_get_state.argtypes = [vp, vp, sz]
+        L.oracle_set_state.argtypes = [vp, vp, sz]
+        L.oracle_get_map_bank.argtypes = [vp, vp, sz]
+        L.oracle_obs_elems.argtypes = [i32]
+        L.oracle_flat_offsets.argtypes = [i32, vp]
+        L.oracle_state_bytes_per_env.restype = sz
+        L.oracle_state_bytes_per_env.argtypes = [i32]
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+class OracleEnvs:
+    """n_envs independent envs stepped serially on the host, same API shape as the HIP engine."""
+
+    def __init__(self, config, n_envs: int, seed: int, task_embedding=None, env_index_base=0):
+        self.config = config
+        self.cfg = config.to_c(env_index_base)
+        self.n_envs = n_envs
+        self.P = config.PLAYER_N
+        self.S = config.PLAYER_N + (config.NPC_N if "NPC" in config.systems else 0)
+        self.obs_elems = lib().oracle_obs_elems(config.TASK_EMBED_DIM)
+        self._task = None
+        if task_embedding is not None:
+            self._task = np.ascontiguousarray(np.asarray(task_embedding, dtype=np.float16)).view(np.uint16)
+        self.h = lib().oracle_create(ctypes.byref(self.cfg), n_envs, seed, _p(self._task))
+        if not self.h:
+            raise ValueError("oracle_create failed")
+        with_obs = config.obs_layout == abi.OBS_FLAT
+        self.obs = np.zeros((n_envs, self.P, self.obs_elems), np.float32) if with_obs else None
+        self.rew = np.zeros((n_envs, self.P), np.float32)
+        self.term = np.zeros((n_envs, self.P), np.uint8)
+        self.trunc = np.zeros((n_envs, self.P), np.uint8)
+        self.mask = np.zeros((n_envs, self.P), np.uint8)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().oracle_destroy(self.h)
+            self.h = None
+
+    def reset(self, env_seeds=None):
+        seeds = None if env_seeds is None else np.ascontiguousarray(env_seeds, dtype=np.uint64)
+        lib().oracle_reset(self.h, _p(seeds), _p(self.obs), _p(self.mask))
+
+    def step(self, actions):
+        actions = np.ascontiguousarray(actions, dtype=np.int32)
+        assert actions.shape == (self.n_envs, self.P, abi.N_ACTION_HEADS)
+        lib().oracle_step(self.h, _p(actions), _p(self.obs), _p(self.rew), _p(self.term),
+                          _p(self.trunc), _p(self.mask))
+
+    def step_range(self, lo, hi, actions):
+        lib().oracle_step_range(self.h, lo, hi, _p(actions), _p(self.obs), _p(self.rew),
+                                _p(self.term), _p(self.trunc), _p(self.mask))
+
+    def scripted_actions(self, policy_seed: int, out=None):
+        out = np.zeros((self.n_envs, self.P, abi.N_ACTION_HEADS), np.int32) if out is None else out
+        lib().oracle_scripted_actions(self.h, policy_seed, _p(out))
+        return out
+
+    def get_state(self) -> np.ndarray:
+        n = lib().oracle_state_bytes_per_env(self.S) * self.n_envs
+        buf = np.zeros(n, np.uint8)
+        rc = lib().oracle_get_state(self.h, _p(buf), n)
+        assert rc == 0, rc
+        return buf
+
+    def set_state(self, buf: np.ndarray):
+        buf = np.ascontiguousarray(buf, dtype=np.uint8)
+        rc = lib().oracle_set_state(self.h, _p(buf), buf.nbytes)
+        assert rc == 0, rc
+
+    def map_bank(self) -> np.ndarray:
+        buf = np.zeros((self.config.MAP_N, abi.MAP_SIZE, abi.MAP_SIZE), np.uint8)
+        rc = lib().oracle_get_map_bank(self.h, _p(buf), buf.nbytes)
+        assert rc == 0, rc
+        return buf
+
+
+def split_state(buf: np.ndarray, n_envs: int, slots: int) -> dict:
+    """View a state blob as named arrays (env [n,NE] i32, ent [n,NF,S] i16, ring, mat)."""
+    per = abi.state_bytes_per_env(slots)
+    b = buf.reshape(n_envs, per)
+    o = 0
+    env = b[:, o:o + abi.NE * 4].copy().view(np.int32); o += abi.NE * 4
+    ent = b[:, o:o + abi.NF * slots * 2].copy().view(np.int16).reshape(n_envs, abi.NF, slots)
+    o += abi.NF * slots * 2
+    ring = b[:, o:o + slots * 2].copy().view(np.int16); o += slots * 2
+    mat = b[:, o:o + abi.MAP_TILES].reshape(n_envs, abi.MAP_SIZE, abi.MAP_SIZE)
+    return {"env": env, "ent": ent, "ring": ring, "mat": mat}
