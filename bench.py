@@ -1,0 +1,251 @@
+#!/usr/bin/env python3
+"""bench.py — agent-steps/sec of the MI355X Neural MMO stepper (BASELINE.json metric).
+
+One "step" = one tick of every env on this GPU: the scripted masked-uniform policy kernel
+(SPEC.md §9, the synthetic action input) + nmmo_step (tick kernel [+ obs kernel]).
+Inputs/state are resident in HBM before the timed region. Envs shard across ranks with no
+data-path collective (weak scaling: envs per GPU fixed); each rank times K steps between a
+barrier + device sync, rank 0 reports the max over ranks.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2|C3|C4] [--envs E]
+  torchrun --nproc-per-node N bench.py --gpus N ...
+
+value = alive agent-steps/s over the whole job (the reference's agent_SPS = sum(mask)/time,
+reinforcement_learning/clean_pufferl.py:306,365); slot-steps/s (envs x 128 x ticks / s, the
+padded count, :307,364) is reported beside it. cpu_baseline = the CPU oracle (a port of the
+same semantics, not nmmo 2.1, which is absent) on the host's cores, rank 0 at N=1 only.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import threading
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "agent-steps/sec (whole node), 128-agent envs at 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+WORKLOADS = {
+    # BASELINE.json configs[1..3]; early stop 8 = config.yaml reward_wrapper.early_stop_agent_num
+    "C2": dict(envs=256, preset="C2", obs=False,
+               desc="C2: 256 envs x 128 agents, movement + food/water (Resource)"),
+    "C3": dict(envs=1024, preset="C3", obs=False,
+               desc="C3: 1024 envs x 128 agents, + melee/range/mage combat, NPC spawn/AI, progression"),
+    "C4": dict(envs=1024, preset="C4", obs=True,
+               desc="C4: 1024 envs x 128 agents, all systems + per-agent flat obs gather"),
+}
+
+
+def tick_bytes_per_env(S: int, P: int) -> int:
+    """Algorithmic HBM bytes of one tick of one env: the env state read and
+    written once (43 int16 entity fields x slots, free-row ring, depleted-tile bitmap, env
+    scalars), the actions read, the outputs written and the map tiles a player touches
+    (own tile + 4 neighbours for harvest/drink, 1 move target)."""
+    state = 43 * S * 2 + S * 2 + 800 * 4 + 16 * 4
+    return 2 * state + P * 12 * 4 + P * (4 + 1 + 1 + 1) + P * 6
+
+
+def obs_bytes_per_env(S: int, P: int, elems: int) -> int:
+    """Flat fp32 obs rows written + the entity columns staged once per 16-agent workgroup +
+    the 15x15 tile window read per agent."""
+    return P * elems * 4 + (P // 16) * (33 * S * 2) + P * 225
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=300)
+    ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--config", default="C2", choices=sorted(WORKLOADS))
+    ap.add_argument("--envs", type=int, default=None, help="envs per GPU (default: config's)")
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(cfg, seconds: float):
+    """The CPU oracle (oracle/, a port of SPEC.md) on the host cores: one Python thread per core,
+    each stepping its own env range through ctypes (the GIL is released inside the C calls)."""
+    import numpy as np
+
+    from oracle.oracle import OracleEnvs
+
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    threads = max(1, min(cores, 16))
+    per = 4
+    n = threads * per
+    o = OracleEnvs(cfg, n, seed=7)
+    o.reset()
+    acts = np.zeros((n, cfg.PLAYER_N, 12), np.int32)
+    from oracle.oracle import lib as olib
+
+    def worker(k, counter, stop_at):
+        lo, hi = k * per, (k + 1) * per
+        t = 0
+        while time.perf_counter() < stop_at:
+            olib().oracle_scripted_actions_range(o.h, lo, hi, 1000 + t, acts.ctypes.data)
+            o.step_range(lo, hi, acts)
+            counter[k] += int(o.mask[lo:hi].sum())
+            t += 1
+
+    counter = [0] * threads
+    stop_at = time.perf_counter() + 1.0  # warmup
+    ths = [threading.Thread(target=worker, args=(k, [0] * threads, stop_at)) for k in range(threads)]
+    [t.start() for t in ths]
+    [t.join() for t in ths]
+    t0 = time.perf_counter()
+    stop_at = t0 + seconds
+    ths = [threading.Thread(target=worker, args=(k, counter, stop_at)) for k in range(threads)]
+    [t.start() for t in ths]
+    [t.join() for t in ths]
+    dt = time.perf_counter() - t0
+    return {
+        "value": round(sum(counter) / dt, 1),
+        "unit": "agent-steps/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"CPU oracle (SPEC.md port, not nmmo 2.1) on {threads} host threads x {per} envs "
+                  f"= {n} envs x {cfg.PLAYER_N} agents, same systems/obs as the GPU workload, "
+                  f"{dt:.1f} s wall incl. the scripted policy",
+    }
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    from nmmo_amd import abi
+    from nmmo_amd.config import Config
+    from nmmo_amd.engine import NmmoEngine
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    wl = WORKLOADS[args.config]
+    envs = args.envs or wl["envs"]
+    cfg = Config.preset(wl["preset"], early_stop_agent_num=8,
+                        obs_layout=abi.OBS_FLAT if wl["obs"] else abi.OBS_NONE)
+    import numpy as np
+
+    task = None
+    gpath = os.path.join(ROOT, "tests", "golden", "task_embeddings.npz")
+    if os.path.exists(gpath):
+        task = np.load(gpath)["heldout_emb"][0]  # TickGE(1024) task, SURVEY §8d
+    eng = NmmoEngine(cfg, envs, seed=args.seed, device=dev, task_embedding=task,
+                     env_index_base=rank * envs)
+    eng.reset()
+    alive = torch.zeros((), dtype=torch.int64, device=dev)
+
+    def one(t):
+        eng.scripted_actions(args.seed * 1_000_003 + t)
+        eng.step()
+
+    for t in range(args.warmup):
+        one(t)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    eng.set_timing(True)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for t in range(args.steps):
+        one(args.warmup + t)
+        alive += eng.mask.sum()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    tick_ms, obs_ms, n_timed = eng.read_timing()
+
+    vals = torch.tensor([elapsed, float(alive.item()), float(envs * cfg.PLAYER_N * args.steps)],
+                        dtype=torch.float64, device=dev)
+    if world > 1:
+        t_max = vals[0:1].clone()
+        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+        sums = vals[1:3].clone()
+        dist.all_reduce(sums, op=dist.ReduceOp.SUM)
+        elapsed = float(t_max.item())
+        alive_total, slots_total = float(sums[0].item()), float(sums[1].item())
+    else:
+        alive_total, slots_total = float(vals[1].item()), float(vals[2].item())
+
+    if rank == 0:
+        S, P = eng.S, cfg.PLAYER_N
+        tick_avg_ms = tick_ms / max(n_timed, 1)
+        obs_avg_ms = obs_ms / max(n_timed, 1)
+        tick_b = tick_bytes_per_env(S, P) * envs
+        obs_b = obs_bytes_per_env(S, P, eng.obs_elems) * envs if wl["obs"] else 0
+        if wl["obs"] and obs_avg_ms > tick_avg_ms:
+            kern, byts, ms = "obs_kernel", obs_b, obs_avg_ms
+        else:
+            kern, byts, ms = "tick_kernel", tick_b, tick_avg_ms
+        achieved = byts / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(Config.preset(wl["preset"], early_stop_agent_num=8,
+                                             obs_layout=abi.OBS_FLAT if wl["obs"] else abi.OBS_NONE),
+                               args.cpu_seconds)
+        line = {
+            "metric": METRIC,
+            "value": round(alive_total / elapsed, 1),
+            "unit": "agent-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int16",
+            "data": "synthetic: generated map bank (SPEC §3), masked-uniform scripted actions (SPEC §9)",
+            "config": {
+                "workload": wl["desc"],
+                "envs_per_gpu": envs,
+                "agents_per_env": P,
+                "npcs_per_env": S - P,
+                "systems": list(cfg.systems),
+                "obs": "pufferlib-flat fp32 (23,987/agent)" if wl["obs"] else "none",
+                "early_stop_agent_num": 8,
+                "parallelism": f"env-shard x{world}",
+            },
+            "slot_steps_per_sec": round(slots_total / elapsed, 1),
+            "alive_fraction": round(alive_total / slots_total, 4),
+            "kernel_ms": {"tick": round(tick_avg_ms, 5), "obs": round(obs_avg_ms, 5)},
+            "roofline": {
+                "kernel": kern,
+                "bound": "hbm",
+                "achieved": round(achieved, 2),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 5),
+                "traffic": None,
+                "bytes_per_launch": byts,
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
