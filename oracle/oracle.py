@@ -132,3 +132,15 @@ def split_state(buf: np.ndarray, n_envs: int, slots: int) -> dict:
     ring = b[:, o:o + slots * 2].copy().view(np.int16); o += slots * 2
     mat = b[:, o:o + abi.MAP_TILES].reshape(n_envs, abi.MAP_SIZE, abi.MAP_SIZE)
     return {"env": env, "ent": ent, "ring": ring, "mat": mat}
+
+
+def join_state(d: dict) -> np.ndarray:
+    """Inverse of split_state."""
+    n = d["env"].shape[0]
+    parts = []
+    for e in range(n):
+        parts += [np.ascontiguousarray(d["env"][e], np.int32).view(np.uint8),
+                  np.ascontiguousarray(d["ent"][e], np.int16).reshape(-1).view(np.uint8),
+                  np.ascontiguousarray(d["ring"][e], np.int16).view(np.uint8),
+                  np.ascontiguousarray(d["mat"][e], np.uint8).reshape(-1)]
+    return np.concatenate(parts)

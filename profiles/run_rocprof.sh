@@ -1,0 +1,21 @@
+#!/bin/bash
+# Collects the rocprofv3 summaries committed under profiles/ (run on the GPU box via gpurun).
+#   kernel trace + stats per config, then FETCH_SIZE and WRITE_SIZE in separate --pmc passes
+#   (MI355X_MICROARCH.md: TCC slots: FETCH_SIZE costs 3, WRITE_SIZE 2 -> one per pass).
+# Usage: bash profiles/run_rocprof.sh <round-tag> [configs...]
+set -e -o pipefail
+TAG=${1:-r01}; shift || true
+CONFIGS=${@:-C2 C3 C4}
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+OUT=gpurun_out/prof_$TAG
+mkdir -p $OUT
+for c in $CONFIGS; do
+  mkdir -p $OUT/$c
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/$c/trace -o run -- \
+    python3 bench.py --config $c --steps 100 --warmup 20 --no-cpu-baseline > $OUT/$c/bench.json
+  timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/$c/fetch -o run -- \
+    python3 bench.py --config $c --steps 30 --warmup 5 --no-cpu-baseline > /dev/null
+  timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/$c/write -o run -- \
+    python3 bench.py --config $c --steps 30 --warmup 5 --no-cpu-baseline > /dev/null
+done

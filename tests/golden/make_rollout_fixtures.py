@@ -1,0 +1,74 @@
+"""Golden rollout hashes (self-generated from the oracle; parity vs nmmo 2.1 unpinned).
+
+sha256 of the state blob and of the step outputs after selected ticks of a seeded
+scripted-action rollout. Used by tests/test_oracle.py (oracle regression) and
+tests/test_gpu_parity.py (HIP path vs the same fixture).
+Run: python -m tests.golden.make_rollout_fixtures
+"""
+
+import hashlib
+import json
+import os
+
+import numpy as np
+
+from nmmo_amd.config import Config
+
+CHECKPOINTS = (0, 1, 5, 20, 60)
+OUT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "rollout_hashes.json")
+
+
+def _h(*arrays):
+    m = hashlib.sha256()
+    for a in arrays:
+        m.update(np.ascontiguousarray(a).tobytes())
+    return m.hexdigest()[:24]
+
+
+def rollout(stepper, preset):
+    """Drive `stepper` (oracle or HIP engine wrapper exposing reset/step/scripted_actions/
+    get_state/rew/term/trunc/mask as numpy) and hash at CHECKPOINTS."""
+    out = {}
+    stepper.reset()
+    out["reset"] = _h(stepper.get_state())
+    for t in range(max(CHECKPOINTS) + 1):
+        a = stepper.scripted_actions(77 + t)
+        stepper.step(a)
+        if t in CHECKPOINTS:
+            out[str(t)] = _h(stepper.get_state(), *stepper.outputs())
+    return out
+
+
+def config(preset):
+    return Config.preset(preset, MAP_N=4, early_stop_agent_num=8)
+
+
+class _OracleStepper:
+    def __init__(self, preset):
+        from oracle.oracle import OracleEnvs
+
+        self.o = OracleEnvs(config(preset), 4, seed=2024)
+
+    def reset(self):
+        self.o.reset()
+
+    def step(self, a):
+        self.o.step(a)
+
+    def scripted_actions(self, s):
+        return self.o.scripted_actions(s)
+
+    def get_state(self):
+        return self.o.get_state()
+
+    def outputs(self):
+        return self.o.rew, self.o.term, self.o.trunc, self.o.mask
+
+
+def rollout_hashes(preset):
+    return rollout(_OracleStepper(preset), preset)
+
+
+if __name__ == "__main__":
+    json.dump({p: rollout_hashes(p) for p in ("C2", "C3")}, open(OUT, "w"), indent=1)
+    print("wrote", OUT)

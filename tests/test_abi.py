@@ -1,0 +1,111 @@
+"""The C-ABI library loads and exports every symbol include/nmmo_hip.h declares; the ctypes
+mirror (nmmo_amd/abi.py) matches the header's structs and enums; argument errors are reported
+through the return code + nmmo_last_error without touching a GPU. CPU only."""
+
+import ctypes
+import os
+import re
+import subprocess
+import tempfile
+
+import pytest
+
+from nmmo_amd import abi
+from nmmo_amd.config import Config
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "nmmo_hip.h")
+
+
+def header_text():
+    return open(HEADER).read()
+
+
+@pytest.fixture(scope="module")
+def native():
+    from nmmo_amd import _native
+
+    return _native.lib()
+
+
+def test_every_declared_symbol_is_exported(native):
+    decl = re.findall(r"NMMO_API\s+[\w\s\*]+?\b(nmmo_\w+)\s*\(", header_text())
+    assert len(decl) >= 14
+    out = subprocess.check_output(["nm", "-D", "--defined-only",
+                                   os.path.join(ROOT, "nmmo_amd", "lib", "libnmmo_hip.so")]).decode()
+    exported = set(re.findall(r"\sT\s(nmmo_\w+)", out))
+    assert set(decl) == exported, (set(decl) ^ exported)
+    from nmmo_amd import _native
+
+    assert set(_native.SYMBOLS) == set(decl)
+    for name in decl:
+        getattr(native, name)
+
+
+def test_enums_match_header():
+    text = header_text()
+    ent = re.search(r"enum NmmoField \{(.*?)\};", text, re.S).group(1)
+    names = [n.strip().split("=")[0].strip() for n in re.sub(r"/\*.*?\*/", "", ent, flags=re.S).split(",")]
+    names = [n for n in names if n.startswith("F_")]
+    assert [n[2:].lower() for n in names] == abi.ENTITY_FIELDS
+    env = re.search(r"enum NmmoEnvField \{(.*?)\};", text, re.S).group(1)
+    enames = [n.strip().split("=")[0].strip() for n in env.split(",")]
+    assert [n[2:].lower() for n in enames if n.startswith("E_")] == abi.ENV_FIELDS
+    for macro, val in [("NMMO_SYS_RESOURCE", abi.SYS_RESOURCE), ("NMMO_SYS_EXCHANGE", abi.SYS_EXCHANGE),
+                       ("NMMO_OBS_FLAT", abi.OBS_FLAT), ("NMMO_ABI_VERSION", abi.ABI_VERSION)]:
+        m = re.search(rf"#define {macro} (.*?)(?:/\*|$)", text, re.M)
+        assert eval(m.group(1).replace("u", "").strip()) == val, macro
+
+
+def test_struct_layout_matches_c_compiler():
+    src = r"""
+#include <stdio.h>
+#include <stddef.h>
+#include "nmmo_hip.h"
+int main(void) {
+  printf("%zu %zu %zu %zu %zu\n", sizeof(NmmoConfig), offsetof(NmmoConfig, map_seed),
+         sizeof(NmmoLayout), offsetof(NmmoLayout, off_tile), offsetof(NmmoLayout, state_bytes_per_env));
+  return 0;
+}
+"""
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "t.c")
+        open(c, "w").write(src)
+        exe = os.path.join(d, "t")
+        subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), c, "-o", exe])
+        got = list(map(int, subprocess.check_output([exe]).split()))
+    want = [ctypes.sizeof(abi.NmmoConfig), abi.NmmoConfig.map_seed.offset,
+            ctypes.sizeof(abi.NmmoLayout), abi.NmmoLayout.off_tile.offset,
+            abi.NmmoLayout.state_bytes_per_env.offset]
+    assert got == want
+
+
+def test_default_config_matches_python(native):
+    c = abi.NmmoConfig()
+    native.nmmo_default_config(ctypes.byref(c))
+    py = Config().to_c()
+    for name, _ in abi.NmmoConfig._fields_:
+        assert getattr(c, name) == getattr(py, name), name
+
+
+def test_invalid_arguments_report_errors(native):
+    bad = Config().to_c()
+    bad.player_n = 500
+    h = ctypes.c_void_p()
+    rc = native.nmmo_create(ctypes.byref(bad), 4, 0, 0, None, ctypes.byref(h))
+    assert rc == abi.NMMO_E_INVALID and not h.value
+    assert b"player_n" in native.nmmo_last_error()
+    bad = Config().to_c()
+    bad.abi_version = 99
+    assert native.nmmo_create(ctypes.byref(bad), 4, 0, 0, None, ctypes.byref(h)) == abi.NMMO_E_INVALID
+    assert native.nmmo_step(None, None, None, None, None, None, None, None) == abi.NMMO_E_INVALID
+    assert native.nmmo_get_state(None, None, 0) == abi.NMMO_E_INVALID
+
+
+def test_state_blob_size(native):
+    from nmmo_amd import _native
+
+    for preset, slots in [("C2", 128), ("C3", 384)]:
+        lay = _native.layout(Config.preset(preset).to_c())
+        assert lay.slots == slots
+        assert lay.state_bytes_per_env == abi.state_bytes_per_env(slots)

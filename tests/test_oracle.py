@@ -1,0 +1,270 @@
+"""Known-answer tests of the CPU oracle against SPEC.md, one rule per test, on hand-built states
+(numbers computed by hand from the SPEC constants, not from the oracle). CPU only."""
+
+import numpy as np
+import pytest
+
+from nmmo_amd import abi
+from nmmo_amd.config import Config
+from oracle.oracle import OracleEnvs, join_state, split_state
+
+F, E = abi.F, abi.E
+FOILAGE, WATER, GRASS, SCRUB, STONE = 4, 1, 2, 3, 5
+
+
+def make(systems, P=4, seed=3):
+    cfg = Config(systems=systems, PLAYER_N=P, MAP_N=1, early_stop_agent_num=0)
+    o = OracleEnvs(cfg, 1, seed=seed)
+    o.reset()
+    return o, split_state(o.get_state(), 1, o.S)
+
+
+def put(o, d):
+    o.set_state(join_state(d))
+
+
+def noop_actions(o):
+    a = np.zeros((1, o.P, 12), np.int32)
+    a[..., 1] = 100  # Attack.Target noop
+    a[..., 8] = 4    # Stay
+    return a
+
+
+def find_tile(mat, pred, avoid=()):
+    for r in range(24, 136):
+        for c in range(24, 136):
+            if (r, c) not in avoid and pred(mat, r, c):
+                return r, c
+    raise AssertionError("no such tile")
+
+
+def nbrs(mat, r, c):
+    return [mat[r - 1, c], mat[r + 1, c], mat[r, c - 1], mat[r, c + 1]]
+
+
+def plain(mat, r, c):  # grass, no water around, not foilage
+    return mat[r, c] == GRASS and WATER not in nbrs(mat, r, c)
+
+
+def place(d, slot, r, c, **fields):
+    d["ent"][0, F["row"], slot] = r
+    d["ent"][0, F["col"], slot] = c
+    for k, v in fields.items():
+        d["ent"][0, F[k], slot] = v
+
+
+def park_others(d, keep, mat):
+    """Move players not in `keep` to distinct plain tiles far from the scenario."""
+    spots = [(r, c) for r in range(120, 140) for c in range(120, 140) if plain(mat, r, c)]
+    k = 0
+    for s in range(d["ent"].shape[2]):
+        if s in keep or d["ent"][0, F["alive"], s] == 0 or d["ent"][0, F["id"], s] <= 0:
+            continue
+        place(d, s, *spots[k])
+        k += 1
+
+
+def visible_index(d, p, target):
+    ent = d["ent"][0]
+    r, c = ent[F["row"], p], ent[F["col"], p]
+    rows = sorted((ent[F["ds_row"], s], s) for s in range(ent.shape[1])
+                  if ent[F["alive"], s] and max(abs(ent[F["row"], s] - r), abs(ent[F["col"], s] - c)) <= 7)
+    return [s for _, s in rows].index(target)
+
+
+def test_starvation_and_dehydration():
+    o, d = make(("Resource",))
+    mat = d["mat"][0]
+    r, c = find_tile(mat, plain)
+    park_others(d, {0}, mat)
+    place(d, 0, r, c, food=0, water=0, health=50, resilient=0)
+    place(d, 1, *find_tile(mat, plain, avoid=[(r, c)] + [(x, y) for x in range(120, 140) for y in range(120, 140)]),
+          food=0, water=0, health=50, resilient=1)
+    put(o, d)
+    o.step(noop_actions(o))
+    s = split_state(o.get_state(), 1, o.S)["ent"][0]
+    assert s[F["health"], 0] == 30 and s[F["health_restore"], 0] == -20  # 10 + 10
+    assert s[F["health"], 1] == 40  # resilient: int(10 * 0.5) each
+    assert s[F["food"], 0] == 0 and s[F["water"], 0] == 0
+
+
+def test_regen_and_depletion():
+    o, d = make(("Resource",))
+    mat = d["mat"][0]
+    park_others(d, {0}, mat)
+    place(d, 0, *find_tile(mat, plain), food=60, water=60, health=50)
+    put(o, d)
+    o.step(noop_actions(o))
+    s = split_state(o.get_state(), 1, o.S)["ent"][0]
+    assert (s[F["health"], 0], s[F["food"], 0], s[F["water"], 0]) == (60, 55, 55)
+
+
+def test_first_player_on_foilage_eats():
+    o, d = make(("Resource",))
+    mat = d["mat"][0]
+    r, c = find_tile(mat, lambda m, r, c: m[r, c] == FOILAGE and WATER not in nbrs(m, r, c))
+    park_others(d, {0, 1}, mat)
+    place(d, 0, r, c, food=40, water=40)
+    place(d, 1, r, c, food=40, water=40)
+    put(o, d)
+    o.step(noop_actions(o))
+    s = split_state(o.get_state(), 1, o.S)
+    assert s["ent"][0][F["food"], 0] == 100  # slot 0 harvests
+    assert s["ent"][0][F["food"], 1] == 35   # slot 1 sees Scrub
+    assert s["mat"][0][r, c] in (SCRUB, FOILAGE)  # Scrub unless the 2.5 % respawn fired
+
+
+def test_drink_adjacent_water():
+    o, d = make(("Resource",))
+    mat = d["mat"][0]
+    park_others(d, {0}, mat)
+    place(d, 0, *find_tile(mat, lambda m, r, c: m[r, c] == GRASS and WATER in nbrs(m, r, c)), water=10)
+    put(o, d)
+    o.step(noop_actions(o))
+    assert split_state(o.get_state(), 1, o.S)["ent"][0][F["water"], 0] == 100
+
+
+COMBAT = ("Resource", "Combat", "Progression")
+
+
+def duel(dist=2, t_fields=None, style=0, both_attack=False, x_fields=None):
+    o, d = make(COMBAT)
+    mat = d["mat"][0]
+    r, c = find_tile(mat, lambda m, r, c: all(plain(m, r, c + k) for k in range(0, 5)))
+    park_others(d, {0, 1}, mat)
+    place(d, 0, r, c, **{"time_alive": 50, **(x_fields or {})})
+    place(d, 1, r, c + dist, **{"time_alive": 50, **(t_fields or {})})
+    put(o, d)
+    a = noop_actions(o)
+    a[0, 0, 0], a[0, 0, 1] = style, visible_index(d, 0, 1)
+    if both_attack:
+        a[0, 1, 0], a[0, 1, 1] = 0, visible_index(d, 1, 0)
+    o.step(a)
+    return o, split_state(o.get_state(), 1, o.S)
+
+
+def test_melee_damage_equal_skills():
+    o, s = duel()
+    ent = s["ent"][0]
+    # offense 10+5*1 = 15, defense 5*1 = 5, mult 1.0 -> 10
+    assert ent[F["health"], 1] == 90 and ent[F["damage"], 1] == 10 and ent[F["attacker_id"], 1] == 1
+    assert ent[F["melee_exp"], 0] == 6 and ent[F["melee_level"], 0] == 1
+    tick = s["env"][0, E["tick"]]
+    assert ent[F["latest_combat_tick"], 0] == tick and ent[F["latest_combat_tick"], 1] == tick
+
+
+def test_weakness_multiplier():
+    # target dominant skill = range (exp 90 -> level 2): melee beats range -> 1.5*15 - 10 = 12.5 -> 12
+    _, s = duel(t_fields=dict(range_exp=90, range_level=2))
+    assert s["ent"][0][F["health"], 1] == 88
+    # mage is not range's weakness: max(15 - 10, 3.75) -> 5
+    _, s = duel(t_fields=dict(range_exp=90, range_level=2), style=2)
+    assert s["ent"][0][F["health"], 1] == 95
+
+
+def test_minimum_damage_proportion():
+    lv = {f"{k}_level": 10 for k in ["melee", "range", "mage", "fishing", "herbalism",
+                                       "prospecting", "carving", "alchemy"]}
+    _, s = duel(t_fields=lv)  # defense 50 -> int(0.25 * 15) = 3
+    assert s["ent"][0][F["health"], 1] == 97
+
+
+def test_spawn_immunity_and_reach():
+    _, s = duel(t_fields=dict(time_alive=5))  # 6 after the update, < 20
+    assert s["ent"][0][F["health"], 1] == 100 and s["ent"][0][F["melee_exp"], 0] == 0
+    _, s = duel(dist=4)
+    assert s["ent"][0][F["health"], 1] == 100
+
+
+def test_kill_cull_and_serial_order():
+    # slot 0 acts first and kills slot 1 (health 5, no regen at food/water 40) -> slot 1's
+    # counter-attack never executes (Realm.step serial order)
+    o, s = duel(t_fields=dict(health=5, food=40, water=40), both_attack=True,
+                x_fields=dict(food=40, water=40, health=70))
+    ent, env = s["ent"][0], s["env"][0]
+    assert ent[F["alive"], 1] == 0 and ent[F["died_tick"], 1] == env[E["tick"]]
+    assert ent[F["health"], 0] == 70 and ent[F["player_kills"], 0] == 1
+    assert o.term[0, 1] == 1 and o.rew[0, 1] == -1.0 and o.mask[0, 1] == 1
+    assert o.rew[0, 0] == np.float32(1 / 1024)
+    assert env[E["players_alive"]] == o.P - 1
+    ring = s["ring"][0]
+    assert ring[(env[E["free_head"]] + env[E["free_count"]] - 1) % o.S] == ent[F["ds_row"], 1]
+
+
+def test_move_blocked_by_stone():
+    o, d = make(("Resource",))
+    mat = d["mat"][0]
+    passable = (GRASS, SCRUB, FOILAGE)
+    r, c = find_tile(mat, lambda m, r, c: m[r, c] in passable and m[r - 1, c] == STONE
+                     and m[r + 1, c] in passable)
+    park_others(d, {0}, mat)
+    place(d, 0, r, c)
+    put(o, d)
+    a = noop_actions(o)
+    a[0, 0, 8] = 0  # North into stone
+    o.step(a)
+    ent = split_state(o.get_state(), 1, o.S)["ent"][0]
+    assert (ent[F["row"], 0], ent[F["col"], 0]) == (r, c)
+    a[0, 0, 8] = 1  # South onto grass
+    o.step(a)
+    ent = split_state(o.get_state(), 1, o.S)["ent"][0]
+    assert (ent[F["row"], 0], ent[F["col"], 0]) == (r + 1, c)
+
+
+def test_horizon_truncation_then_auto_reset():
+    o, d = make(("Resource",))
+    d["env"][0, E["tick"]] = 1023
+    put(o, d)
+    o.step(noop_actions(o))
+    env = split_state(o.get_state(), 1, o.S)["env"][0]
+    assert env[E["done"]] == 1 and env[E["tick"]] == 1024
+    assert o.trunc[0].sum() == o.P
+    o.step(noop_actions(o))  # pufferlib auto-reset
+    env = split_state(o.get_state(), 1, o.S)["env"][0]
+    assert env[E["tick"]] == 0 and env[E["episode"]] == 1 and env[E["done"]] == 0
+    assert o.mask[0].sum() == o.P and o.rew[0].sum() == 0
+
+
+def test_npc_bookkeeping_invariants():
+    cfg = Config.preset("C3", MAP_N=2, early_stop_agent_num=8)
+    o = OracleEnvs(cfg, 3, seed=9)
+    o.reset()
+    for t in range(80):
+        o.step(o.scripted_actions(t))
+        s = split_state(o.get_state(), 3, o.S)
+        for e in range(3):
+            ent, env, ring = s["ent"][e], s["env"][e], s["ring"][e]
+            alive = ent[F["alive"]] == 1
+            n_npc = env[E["npc_count"]]
+            assert 0 <= n_npc <= 256
+            assert np.all(alive[128:128 + n_npc]) and not np.any(alive[128 + n_npc:])  # compacted
+            ids = ent[F["id"], 128:128 + n_npc]
+            assert np.all(np.diff(ids) < 0)  # spawn order = decreasing ids
+            rows = list(ent[F["ds_row"]][alive])
+            fr = [ring[(env[E["free_head"]] + k) % o.S] for k in range(env[E["free_count"]])]
+            assert sorted(rows + fr) == list(range(1, o.S + 1))  # every datastore row exactly once
+            assert env[E["players_alive"]] == alive[:128].sum()
+
+
+def test_determinism_and_seed_sensitivity():
+    cfg = Config.preset("C3", MAP_N=2)
+    runs = []
+    for seed in (4, 4, 5):
+        o = OracleEnvs(cfg, 2, seed=seed)
+        o.reset()
+        for t in range(25):
+            o.step(o.scripted_actions(t))
+        runs.append(o.get_state())
+    assert np.array_equal(runs[0], runs[1]) and not np.array_equal(runs[0], runs[2])
+
+
+@pytest.mark.parametrize("preset", ["C2", "C3"])
+def test_golden_rollout_hashes(preset):
+    """Regression pin: the committed hashes were produced by tests/golden/make_rollout_fixtures.py
+    (self-generated from the oracle — parity vs nmmo 2.1 is unpinned, SPEC.md)."""
+    import json
+
+    from tests.golden.make_rollout_fixtures import rollout_hashes
+
+    golden = json.load(open("tests/golden/rollout_hashes.json"))[preset]
+    assert rollout_hashes(preset) == golden
