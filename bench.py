@@ -67,6 +67,8 @@ def parse():
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraph replay")
+    ap.add_argument("--graph-steps", type=int, default=10, help="ticks captured per hipGraph")
     return ap.parse_args()
 
 
@@ -152,28 +154,55 @@ def main():
     eng = NmmoEngine(cfg, envs, seed=args.seed, device=dev, task_embedding=task,
                      env_index_base=rank * envs)
     eng.reset()
-    alive = torch.zeros((), dtype=torch.int64, device=dev)
+    alive_acc = torch.zeros((envs, cfg.PLAYER_N), dtype=torch.int32, device=dev)
+    pseed = args.seed * 1_000_003  # the policy's Philox counter already walks (tick, episode)
 
-    def one(t):
-        eng.scripted_actions(args.seed * 1_000_003 + t)
+    def one():
+        eng.scripted_actions(pseed)
         eng.step()
+        torch.add(alive_acc, eng.mask, out=alive_acc)  # sum(mask) accounting, one kernel
 
-    for t in range(args.warmup):
-        one(t)
+    for _ in range(args.warmup):
+        one()
     torch.cuda.synchronize(dev)
+    graphs = []
+    if not args.no_graph:  # the step is capture-safe: no sync / alloc inside nmmo_step
+        g_n = max(1, min(args.graph_steps, args.steps))
+        for n in sorted({g_n, args.steps % g_n} - {0}):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for _ in range(n):
+                    one()
+            graphs.append((n, g))
+        torch.cuda.synchronize(dev)
+        alive_acc.zero_()
+    plan = []
+    if graphs:
+        big = graphs[-1] if graphs[-1][0] == max(n for n, _ in graphs) else graphs[0]
+        q, r = divmod(args.steps, big[0])
+        plan = [big[1]] * q + [g for n, g in graphs if n == r and r]
     if world > 1:
         dist.barrier()
-    eng.set_timing(True)
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for t in range(args.steps):
-        one(args.warmup + t)
-        alive += eng.mask.sum()
+    if plan:
+        for g in plan:
+            g.replay()
+    else:
+        for _ in range(args.steps):
+            one()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    alive = alive_acc.sum(dtype=torch.int64)
+    # per-kernel durations: HIP events on the launch stream around each kernel of nmmo_step,
+    # over an equal number of eager steps right after the timed region (same state stream)
+    eng.set_timing(True)
+    for _ in range(min(args.steps, 8192)):
+        one()
     tick_ms, obs_ms, n_timed = eng.read_timing()
+    eng.set_timing(False)
 
     vals = torch.tensor([elapsed, float(alive.item()), float(envs * cfg.PLAYER_N * args.steps)],
                         dtype=torch.float64, device=dev)
@@ -229,6 +258,7 @@ def main():
             "slot_steps_per_sec": round(slots_total / elapsed, 1),
             "alive_fraction": round(alive_total / slots_total, 4),
             "kernel_ms": {"tick": round(tick_avg_ms, 5), "obs": round(obs_avg_ms, 5)},
+            "launch": "eager" if args.no_graph else f"hipGraph x{min(args.graph_steps, args.steps)} ticks",
             "roofline": {
                 "kernel": kern,
                 "bound": "hbm",

@@ -12,7 +12,8 @@ import os
 
 from . import abi
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libnmmo_hip.so")
+LIB_PATH = os.environ.get(
+    "NMMO_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libnmmo_hip.so"))
 _lib = None
 
 SYMBOLS = [

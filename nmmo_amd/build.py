@@ -11,6 +11,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB_DIR = os.path.join(HERE, "lib")
 LIB_PATH = os.path.join(LIB_DIR, "libnmmo_hip.so")
+STAMPS_PATH = os.path.join(LIB_DIR, "libnmmo_hip_stamps.so")
 SOURCES = ["mapgen.hip", "tick.hip", "obs.hip", "capi.hip"]
 HEADERS = ["common.h", "kernels.h"]
 ARCH = os.environ.get("NMMO_OFFLOAD_ARCH", "gfx950")
@@ -32,21 +33,24 @@ def stale() -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and not stale():
+def build(force: bool = False, verbose: bool = False, stamps: bool = False) -> str:
+    """Product library; `stamps=True` builds the diagnostic variant (phase clock stamps,
+    tools/stamps.py) to lib/libnmmo_hip_stamps.so instead."""
+    out = STAMPS_PATH if stamps else LIB_PATH
+    if not force and not stamps and not stale():
         return LIB_PATH
     os.makedirs(LIB_DIR, exist_ok=True)
-    tmp = LIB_PATH + ".tmp"
+    tmp = out + ".tmp"
     cmd = [
         _hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-        "-fvisibility=hidden", "-Wall", "-Werror",
+        "-fvisibility=hidden", "-Wall", "-Werror", *(["-DNMMO_STAMPS"] if stamps else []),
         *[os.path.join(CSRC, f) for f in SOURCES], "-o", tmp,
     ]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.check_call(cmd)
-    os.replace(tmp, LIB_PATH)
-    return LIB_PATH
+    os.replace(tmp, out)
+    return out
 
 
 if __name__ == "__main__":

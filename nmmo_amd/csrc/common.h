@@ -130,4 +130,29 @@ __device__ inline int block_prefix_count(bool pred, int* wave_tot, int* total) {
   return base + __popcll(b & lanes_below());
 }
 
+// ---------------------------------------------------------------- packed-row scans
+// rp: per datastore row r | c<<8 | slot<<16 (| flags<<25), -1 = no entity; padded with -1 to a
+// multiple of 4 entries and 16-B aligned so a scan reads 4 rows per ds_read_b128, branch-free.
+__host__ __device__ inline int rp_groups(int S) { return (S + 4) >> 2; }
+
+// slot of the k-th (0-based) entity within L-inf <= kVision of (r, c) in row order, or -1
+__device__ inline int kth_visible(const int* __restrict__ rp, int S, int r, int c, int k) {
+  const int4* rp4 = reinterpret_cast<const int4*>(rp);
+  const int ng = rp_groups(S);
+  int cnt = 0, tgt = -1;
+  for (int g = 0; g < ng; g++) {
+    const int4 q = rp4[g];
+    const int vv[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const int v = vv[j];
+      const bool vis = v >= 0 && linf(r, c, v & 255, (v >> 8) & 255) <= kVision;
+      tgt = (vis && cnt == k) ? ((v >> 16) & 511) : tgt;
+      cnt += vis;
+    }
+    if (cnt > k) break;
+  }
+  return tgt;
+}
+
 }  // namespace nmmo

@@ -150,23 +150,21 @@ hipError_t launch_obs(const ObsParams& p, hipStream_t stream) {
 }
 
 // ---------------------------------------------------------------- scripted policy (SPEC §9)
+// One workgroup per env, one thread per player. The env's entities are first packed per
+// datastore row into one int32 (r | c<<8 | slot<<16 | immune<<25, -1 = absent), so the two
+// visibility passes over the rows are one broadcast LDS load per row with no dependent loads.
 __global__ void __launch_bounds__(128) policy_kernel(PolicyParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int S = p.S, e = blockIdx.x, tid = threadIdx.x;
-  int16_t* row_ = reinterpret_cast<int16_t*>(smem);
-  int16_t* col_ = row_ + S;
-  int16_t* ta_ = col_ + S;
-  int16_t* rowslot = ta_ + S;
+  int* rp = reinterpret_cast<int*>(smem);  // by datastore row (row 0 unused), int4-padded
   const int16_t* E = p.ent + (size_t)e * NMMO_NF * S;
-  for (int k = tid; k <= S; k += blockDim.x) rowslot[k] = -1;
-  for (int s = tid; s < S; s += blockDim.x) {
-    row_[s] = E[F_ROW * S + s];
-    col_[s] = E[F_COL * S + s];
-    ta_[s] = E[F_TIME_ALIVE * S + s];
-  }
+  for (int k = tid; k < rp_groups(S) * 4; k += blockDim.x) rp[k] = -1;
   __syncthreads();
-  for (int s = tid; s < S; s += blockDim.x)
-    if (E[F_ALIVE * S + s]) rowslot[E[F_DS_ROW * S + s]] = (int16_t)s;
+  for (int s = tid; s < S; s += blockDim.x) {
+    if (!E[F_ALIVE * S + s]) continue;
+    const bool immune = s < p.P && E[F_TIME_ALIVE * S + s] < p.spawn_immunity;
+    rp[E[F_DS_ROW * S + s]] = E[F_ROW * S + s] | (E[F_COL * S + s] << 8) | (s << 16) | ((int)immune << 25);
+  }
   __syncthreads();
   const int32_t* env = p.env + (size_t)e * NMMO_NE;
   const uint8_t* mat = p.mat + (size_t)e * kTiles;
@@ -181,29 +179,44 @@ __global__ void __launch_bounds__(128) policy_kernel(PolicyParams p) {
     const uint32_t c0 = (uint32_t)env[E_TICK] + 2048u * (uint32_t)env[E_EPISODE];
     const uint32_t c1 = (uint32_t)env[E_ENV_INDEX];
     const uint32_t k0 = (uint32_t)p.seed, k1 = (uint32_t)(p.seed >> 32);
-    const int r = row_[a], c = col_[a];
+    const int r = E[F_ROW * S + a], c = E[F_COL * S + a];
     if (p.systems & NMMO_SYS_COMBAT) {
       h[0] = (int)uniform_n(philox(c0, c1, (uint32_t)a, 0, k0, k1).x, 3);
-      // attack mask over the visible rows (two passes: count, then select the k-th set bit)
+      // attack mask over the first 100 visible rows: count, draw, then select the k-th set bit
+      const int4* rp4 = reinterpret_cast<const int4*>(rp);
+      const int ng = rp_groups(S);
       int nb = 0, nv = 0;
-      for (int rw = 1; rw <= S && nv < kNObs; rw++) {
-        const int q = rowslot[rw];
-        if (q < 0 || linf(r, c, row_[q], col_[q]) > kVision) continue;
-        nv++;
-        nb += q != a && linf(r, c, row_[q], col_[q]) <= 3 && !(q < p.P && ta_[q] < p.spawn_immunity);
+      for (int g = 0; g < ng; g++) {  // pass 1: count targets among the first 100 visible
+        const int4 q = rp4[g];
+        const int vv[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const int v = vv[j];
+          const int d = linf(r, c, v & 255, (v >> 8) & 255);
+          const bool vis = v >= 0 && d <= kVision && nv < kNObs;
+          nb += vis && ((v >> 16) & 511) != a && d <= 3 && !((v >> 25) & 1);
+          nv += vis;
+        }
       }
       const int pick = (int)uniform_n(philox(c0, c1, (uint32_t)a, 1, k0, k1).x, (uint32_t)(nb + 1));
-      int sel = kNObs, seen = 0;
-      nv = 0;
-      for (int rw = 1; rw <= S && nv < kNObs && sel == kNObs; rw++) {
-        const int q = rowslot[rw];
-        if (q < 0 || linf(r, c, row_[q], col_[q]) > kVision) continue;
-        const bool ok = q != a && linf(r, c, row_[q], col_[q]) <= 3 && !(q < p.P && ta_[q] < p.spawn_immunity);
-        if (ok) {
-          if (seen == pick) sel = nv;
-          seen++;
+      int sel = kNObs;
+      if (pick < nb) {  // pass 2: visible index of the pick-th target
+        int seen = 0;
+        nv = 0;
+        for (int g = 0; g < ng && sel == kNObs; g++) {
+          const int4 q = rp4[g];
+          const int vv[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+          for (int j = 0; j < 4; j++) {
+            const int v = vv[j];
+            const int d = linf(r, c, v & 255, (v >> 8) & 255);
+            const bool vis = v >= 0 && d <= kVision;
+            const bool ok = vis && ((v >> 16) & 511) != a && d <= 3 && !((v >> 25) & 1);
+            sel = (ok && seen == pick && sel == kNObs) ? nv : sel;
+            seen += ok;
+            nv += vis;
+          }
         }
-        nv++;
       }
       h[1] = sel;
     }
@@ -218,7 +231,7 @@ __global__ void __launch_bounds__(128) policy_kernel(PolicyParams p) {
 }
 
 hipError_t launch_policy(const PolicyParams& p, hipStream_t stream) {
-  const size_t lds = (size_t)3 * p.S * 2 + (size_t)(p.S + 1) * 2;
+  const size_t lds = (size_t)rp_groups(p.S) * 16;
   hipLaunchKernelGGL(policy_kernel, dim3(p.n_envs), dim3(128), lds, stream, p);
   return hipGetLastError();
 }

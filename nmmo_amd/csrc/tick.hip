@@ -22,7 +22,11 @@ namespace nmmo {
 
 struct Ctx {
   int16_t* T;        // [kNFLive][S]
-  int16_t* rowslot;  // [S+1] datastore row -> slot
+  uint64_t* vism;    // [P][NW] visibility bitmap: bit j of word w = row 64w+j+1 visible to player
+  int* rp;           // [S+1] datastore row -> r | c<<8 | slot<<16 (-1 = no entity)
+  int* sp;           // [S] slot -> r | c<<8 while in the realm with health > 0 (-1 otherwise)
+  int* hkey;         // [kHash] Foilage-tile hash: tile index (-1 = empty)
+  int* hmin;         // [kHash] lowest player slot standing on that tile
   int16_t* amove;    // [S]
   int16_t* atgt;     // [S]
   int16_t* asty;     // [S]
@@ -43,16 +47,36 @@ struct Ctx {
 
 #define TF(f, s) c.T[(f) * c.S + (s)]
 
+// Diagnostic build only (-DNMMO_STAMPS, tools/stamps.py): thread 0 stamps the shader clock right
+// after phase barriers; never compiled into the product library.
+#ifdef NMMO_STAMPS
+__device__ unsigned long long g_stamps[4096 * 16];
+#define NMMO_STAMP(k)                                                        \
+  do {                                                                       \
+    if (threadIdx.x == 0 && blockIdx.x < 4096)                               \
+      g_stamps[blockIdx.x * 16 + (k)] = __builtin_amdgcn_s_memtime();        \
+  } while (0)
+#else
+#define NMMO_STAMP(k) \
+  do {               \
+  } while (0)
+#endif
+
 __device__ inline bool sys(const Ctx& c, uint32_t b) { return (c.cfg->systems & b) != 0; }
 __device__ inline uint64_t env_seed(const Ctx& c) {
   return (uint64_t)(uint32_t)c.E[E_SEED_LO] | ((uint64_t)(uint32_t)c.E[E_SEED_HI] << 32);
 }
 
+constexpr int kHash = 256;  // >= 2x players: open addressing never fills
+
 __host__ __device__ inline size_t tick_lds_bytes(int S) {
   auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
   size_t b = 0;
   b += al((size_t)kNFLive * S * 2);  // T
-  b += al((size_t)(S + 1) * 2);      // rowslot
+  b += (size_t)128 * ((S + 63) / 64) * 8;  // vism (players <= 128)
+  b += (size_t)rp_groups(S) * 16;    // rp
+  b += al((size_t)S * 4);            // sp
+  b += 2 * kHash * 4;                // hkey, hmin
   b += 3 * al((size_t)S * 2);        // amove atgt asty
   b += al((size_t)S * 4);            // ft
   b += al((size_t)S * 2);            // clist
@@ -68,7 +92,11 @@ __device__ inline Ctx make_ctx(unsigned char* smem, const DevState& st, int e) {
   const int S = st.S;
   size_t o = 0;
   c.T = reinterpret_cast<int16_t*>(smem + o); o += al((size_t)kNFLive * S * 2);
-  c.rowslot = reinterpret_cast<int16_t*>(smem + o); o += al((size_t)(S + 1) * 2);
+  c.vism = reinterpret_cast<uint64_t*>(smem + o); o += (size_t)128 * ((S + 63) / 64) * 8;
+  c.rp = reinterpret_cast<int*>(smem + o); o += (size_t)rp_groups(S) * 16;
+  c.sp = reinterpret_cast<int*>(smem + o); o += al((size_t)S * 4);
+  c.hkey = reinterpret_cast<int*>(smem + o); o += kHash * 4;
+  c.hmin = reinterpret_cast<int*>(smem + o); o += kHash * 4;
   c.amove = reinterpret_cast<int16_t*>(smem + o); o += al((size_t)S * 2);
   c.atgt = reinterpret_cast<int16_t*>(smem + o); o += al((size_t)S * 2);
   c.asty = reinterpret_cast<int16_t*>(smem + o); o += al((size_t)S * 2);
@@ -249,11 +277,25 @@ __device__ void npc_decide(Ctx& c, int n, int& move, int& tgt, int& sty) {
     hunt = true;
   } else if (type == 3) {
     if (!TF(F_TARGET_ID, n)) {
-      int best = -1, bd = 1 << 30;
-      for (int p = 0; p < c.P; p++) {
-        if (!TF(F_ALIVE, p) || TF(F_HEALTH, p) <= 0) continue;
-        const int d = linf(r, col, TF(F_ROW, p), TF(F_COL, p));
-        if (d <= kVision && d < bd) { bd = d; best = p; }
+      int best = -1, bd = kVision + 1;  // closest player, ties to the lowest id
+      const int4* sp4 = reinterpret_cast<const int4*>(c.sp);
+#pragma unroll 4
+      for (int g = 0; g < (c.P >> 2); g++) {  // 4 players per ds_read_b128, branch-free
+        const int4 q = sp4[g];
+        const int vv[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const int v = vv[j];
+          const int d = v < 0 ? kVision + 1 : linf(r, col, v & 255, (v >> 8) & 255);
+          best = d < bd ? 4 * g + j : best;
+          bd = d < bd ? d : bd;
+        }
+      }
+      for (int p = c.P & ~3; p < c.P; p++) {
+        const int v = c.sp[p];
+        const int d = v < 0 ? kVision + 1 : linf(r, col, v & 255, (v >> 8) & 255);
+        best = d < bd ? p : best;
+        bd = d < bd ? d : bd;
       }
       if (best >= 0) TF(F_TARGET_ID, n) = TF(F_ID, best);
     }
@@ -346,28 +388,85 @@ __device__ void tick_env(Ctx& c, const int32_t* __restrict__ act, float* rew, ui
   const bool inslot = s < nslots;
 
   if (s < P) c.pres[s] = (uint8_t)TF(F_ALIVE, s);
-  for (int k = tid; k <= S; k += nt) c.rowslot[k] = -1;
+  for (int k = tid; k < rp_groups(S) * 4; k += nt) c.rp[k] = -1;
+  for (int k = tid; k < kHash; k += nt) {
+    c.hkey[k] = -1;
+    c.hmin[k] = 0x7FFF;
+  }
   __syncthreads();
-  if (inslot && TF(F_ALIVE, s)) c.rowslot[TF(F_DS_ROW, s)] = (int16_t)s;
+  if (s < S) {
+    const bool in = inslot && TF(F_ALIVE, s);  // in the realm => health > 0 at tick start
+    const int pos = TF(F_ROW, s) | (TF(F_COL, s) << 8);
+    c.sp[s] = in ? pos : -1;
+    if (in) c.rp[TF(F_DS_ROW, s)] = pos | (s << 16);
+  }
   __syncthreads();
+  NMMO_STAMP(1);
 
-  // 0. decode (Env._validate_actions) against the previous observation's state
+  // 0. decode (Env._validate_actions) against the previous observation's state.
+  // Attack.Target k is the k-th visible entity in datastore-row order (the previous obs' Entity
+  // row k). Every wave builds the player x row visibility bitmap for its 64 rows with one
+  // ballot per player; each player then selects its k-th set bit with popcounts.
+  const int NW = (S + 63) >> 6;
+  const bool combat = sys(c, NMMO_SYS_COMBAT);
+  if (combat) {
+    // Packed 16-bit window test: entity (col+7, row+7) minus player (col, row) with one
+    // v_pk_sub_u16; both halves <= 14 <=> L-inf <= 7 (out-of-window values wrap to >= 0x8000).
+    typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+    const int w = wave_id(), lane = lane_id(), row = (w << 6) + lane + 1;
+    const int v = row <= S ? c.rp[row] : -1;
+    const uint32_t e32 = v < 0 ? 0xF000F000u : ((uint32_t)((v & 255) + 7) << 16) | (uint32_t)(((v >> 8) & 255) + 7);
+    const us2 e2 = __builtin_bit_cast(us2, e32);
+    const int4* sp4 = reinterpret_cast<const int4*>(c.sp);
+    for (int pb = 0; pb < P; pb += 64) {
+      int mine_lo = 0, mine_hi = 0;  // lane j keeps the mask of player pb + j
+      const int pe = min(P, pb + 64);
+      for (int g = pb >> 2; g < (pe + 3) >> 2; g++) {  // 4 players per ds_read_b128 (broadcast)
+        const int4 q = sp4[g];
+        const int pv[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const int p = 4 * g + j;
+          const uint32_t p32 = (pv[j] < 0 || p >= P) ? 0x80008000u
+                                                     : ((uint32_t)(pv[j] & 255) << 16) | (uint32_t)((pv[j] >> 8) & 255);
+          const us2 t = e2 - __builtin_bit_cast(us2, p32);
+          const unsigned short d = t.x > t.y ? t.x : t.y;
+          const uint64_t m = __ballot(d <= 14);
+          const bool me = lane == (p & 63);
+          mine_lo = me ? (int)(uint32_t)m : mine_lo;
+          mine_hi = me ? (int)(uint32_t)(m >> 32) : mine_hi;
+        }
+      }
+      if (pb + lane < pe)
+        c.vism[(pb + lane) * NW + w] = ((uint64_t)(uint32_t)mine_hi << 32) | (uint32_t)mine_lo;
+    }
+  }
+  __syncthreads();
+  NMMO_STAMP(13);
   int my_move = -1, my_tgt = -1, my_sty = 0;
   if (s < P && c.pres[s]) {
     const int32_t* a = act + (size_t)s * kHeads;
     const int dmove = a[8], dsty = a[0], dk = a[1];
     if (dmove >= 0 && dmove < 5) my_move = dmove;
-    if (sys(c, NMMO_SYS_COMBAT) && dsty >= 0 && dsty < 3 && dk >= 0 && dk < kNObs) {
-      const int r = TF(F_ROW, s), col = TF(F_COL, s);
-      int cnt = 0;
-      for (int row = 1; row <= S && cnt <= dk; row++) {
-        const int q = c.rowslot[row];
-        if (q < 0 || linf(r, col, TF(F_ROW, q), TF(F_COL, q)) > kVision) continue;
-        if (cnt == dk) { my_tgt = q; my_sty = dsty; }
-        cnt++;
+    if (combat && dsty >= 0 && dsty < 3 && dk >= 0 && dk < kNObs) {
+      int k = dk;
+      for (int w = 0; w < NW; w++) {
+        uint64_t m = c.vism[s * NW + w];
+        const int pc = __popcll(m);
+        if (k < pc) {
+          for (int i = 0; i < k; i++) m &= m - 1;  // clear the k lowest set bits
+          my_tgt = (c.rp[(w << 6) + __builtin_ctzll(m) + 1] >> 16) & 511;
+          my_sty = dsty;
+          break;
+        }
+        k -= pc;
       }
     }
   }
+#ifdef NMMO_STAMPS
+  __syncthreads();
+  NMMO_STAMP(12);
+#endif
   // 1. npcs.actions
   if (sys(c, NMMO_SYS_NPC) && s >= P && inslot) npc_decide(c, s, my_move, my_tgt, my_sty);
   if (s < S) {
@@ -376,10 +475,11 @@ __device__ void tick_env(Ctx& c, const int32_t* __restrict__ act, float* rew, ui
     c.asty[s] = (int16_t)my_sty;
   }
   __syncthreads();
+  NMMO_STAMP(2);
 
   // 2. players.update / npcs.update
   bool eat = false;
-  int tile = 0;
+  int tile = 0, hslot = -1;
   if (inslot && TF(F_ALIVE, s)) {
     if (TF(F_DAMAGE, s) == 0) TF(F_ATTACKER_ID, s) = 0;
     TF(F_DAMAGE, s) = 0;
@@ -399,15 +499,24 @@ __device__ void tick_env(Ctx& c, const int32_t* __restrict__ act, float* rew, ui
       TF(F_FOOD, s) = (int16_t)max(0, food - 5);
       const int r = TF(F_ROW, s), col = TF(F_COL, s);
       tile = r * kSize + col;
-      eat = c.mat[tile] == M_FOILAGE;
-      for (int q = 0; q < s && eat; q++)  // first player in slot order on the tile wins
-        if (TF(F_ALIVE, q) && TF(F_ROW, q) == r && TF(F_COL, q) == col) eat = false;
+      if (c.mat[tile] == M_FOILAGE) {  // first player in slot order on the tile wins:
+        int hh = (int)(h32((uint32_t)tile) & (kHash - 1));  // atomicMin of slots per tile
+        while (true) {
+          const int old = atomicCAS(&c.hkey[hh], -1, tile);
+          if (old == -1 || old == tile) break;
+          hh = (hh + 1) & (kHash - 1);
+        }
+        atomicMin(&c.hmin[hh], s);
+        hslot = hh;
+      }
       const bool drink = c.mat[tile - kSize] == M_WATER || c.mat[tile + kSize] == M_WATER ||
                          c.mat[tile - 1] == M_WATER || c.mat[tile + 1] == M_WATER;
       TF(F_WATER, s) = (int16_t)(drink ? 100 : max(0, water - 5));
     }
   }
   __syncthreads();
+  NMMO_STAMP(3);
+  eat = hslot >= 0 && c.hmin[hslot] == s;
   if (eat) {
     TF(F_FOOD, s) = 100;
     c.mat[tile] = M_SCRUB;
@@ -430,14 +539,40 @@ __device__ void tick_env(Ctx& c, const int32_t* __restrict__ act, float* rew, ui
   const int cpos = block_prefix_count(contested, c.wtot, &ncont);
   if (contested) c.clist[cpos] = (int16_t)s;
   __syncthreads();
-  if (tid == 0) {  // the lane-serial replay of the contested attacks, in slot order
-    for (int i = 0; i < ncont; i++) {
-      const int x = c.clist[i], tx = c.atgt[x], sx = c.asty[x];
-      const int d = eval_attack(c, x, sx, tx);
-      if (d >= 0) apply_attack(c, x, sx, tx, d, tick);
+  NMMO_STAMP(4);
+  if (wave_id() == 0) {
+    // Replay of the contested attacks in slot order, 64 per chunk. Inside a chunk, lane j
+    // conflicts with an earlier lane i if i targets j's attacker or target, or j's target is
+    // i's attacker; a maximal conflict-free prefix [start, end) has disjoint read/write sets,
+    // so it is evaluated and applied in one wave step (exactly the serial result).
+    const int lane = lane_id();
+    for (int base = 0; base < ncont; base += 64) {
+      const int nin = min(64, ncont - base);
+      const bool valid = lane < nin;
+      const int x = valid ? c.clist[base + lane] : -1;
+      const int tx = valid ? c.atgt[x] : -2;
+      const int sx = valid ? c.asty[x] : 0;
+      uint64_t cm = 0;
+      for (int i = 0; i < 64; i++) {
+        const int xi = __shfl(x, i), ti = __shfl(tx, i);
+        if (i < lane && valid && (ti == x || ti == tx || xi == tx)) cm |= 1ull << i;
+      }
+      int start = 0;
+      while (start < nin) {
+        const uint64_t below = lane > start ? (((1ull << lane) - 1ull) & ~((1ull << start) - 1ull)) : 0ull;
+        const uint64_t blocked = __ballot(valid && (cm & below) != 0);
+        const int end = blocked ? (int)__builtin_ctzll(blocked) : nin;
+        int d = -1;
+        if (lane >= start && lane < end) d = eval_attack(c, x, sx, tx);
+        __builtin_amdgcn_wave_barrier();
+        if (d >= 0) apply_attack(c, x, sx, tx, d, tick);
+        __builtin_amdgcn_wave_barrier();
+        start = end;
+      }
     }
   }
   __syncthreads();
+  NMMO_STAMP(5);
 
   // 3b. Move (priority 60)
   if (inslot && c.amove[s] >= 0 && TF(F_ALIVE, s) && TF(F_HEALTH, s) > 0) {
@@ -451,6 +586,7 @@ __device__ void tick_env(Ctx& c, const int32_t* __restrict__ act, float* rew, ui
     }
   }
   __syncthreads();
+  NMMO_STAMP(6);
 
   // 4. cull: rows appended to the free ring in slot order; NPC slots compacted
   const bool dead = inslot && TF(F_ALIVE, s) && TF(F_HEALTH, s) <= 0;
@@ -469,7 +605,7 @@ __device__ void tick_env(Ctx& c, const int32_t* __restrict__ act, float* rew, ui
     c.E[E_FREE_COUNT] += ndead;
     c.E[E_PLAYERS_ALIVE] -= npdead;
   }
-  if (sys(c, NMMO_SYS_NPC)) {
+  if (sys(c, NMMO_SYS_NPC) && ndead > npdead) {  // compaction only when an NPC left the realm
     const bool keep = s >= P && inslot && TF(F_ALIVE, s);
     int nkeep;
     const int kpos = block_prefix_count(keep, c.wtot, &nkeep);
@@ -490,6 +626,7 @@ __device__ void tick_env(Ctx& c, const int32_t* __restrict__ act, float* rew, ui
     if (tid == 0) c.E[E_NPC_COUNT] = nkeep;
   }
   __syncthreads();
+  NMMO_STAMP(7);
 
   // 5-6. tick += 1; map.step respawn of depleted tiles
   const uint64_t seed = env_seed(c);
@@ -502,7 +639,9 @@ __device__ void tick_env(Ctx& c, const int32_t* __restrict__ act, float* rew, ui
         bits &= bits - 1;
         const int tt = w * 32 + b;
         const int bm = base[tt];
-        if (draw(seed, (uint32_t)(tick + 1), P_RESPAWN, (uint32_t)tt, 0).x < respawn_u32(bm)) {
+        const U4 u = draw(seed, (uint32_t)(tick + 1), P_RESPAWN, (uint32_t)(tt >> 2), 0);
+        const uint32_t ut = (tt & 3) == 0 ? u.x : (tt & 3) == 1 ? u.y : (tt & 3) == 2 ? u.z : u.w;
+        if (ut < respawn_u32(bm)) {
           c.mat[tt] = (uint8_t)bm;
           keepb &= ~(1u << b);
         }
@@ -513,8 +652,10 @@ __device__ void tick_env(Ctx& c, const int32_t* __restrict__ act, float* rew, ui
   __syncthreads();
   if (tid == 0) c.E[E_TICK] = tick + 1;
   __syncthreads();
+  NMMO_STAMP(8);
   // 7. NPC refill
   if (sys(c, NMMO_SYS_NPC)) npc_spawn(c, (uint32_t)(tick + 1));
+  NMMO_STAMP(9);
 
   // 8. rewards / dones
   if (tid == 0) {
@@ -542,6 +683,7 @@ __global__ void tick_kernel(DevState st, const int32_t* __restrict__ actions,
                             uint8_t* trunc, uint8_t* mask, int mode) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int e = blockIdx.x;
+  NMMO_STAMP(0);
   Ctx c = make_ctx(smem, st, e);
   load_env(c, st, e);
   __syncthreads();
@@ -569,7 +711,10 @@ __global__ void tick_kernel(DevState st, const int32_t* __restrict__ actions,
     tick_env(c, actions + o * kHeads, rew + o, term + o, trunc + o, mask + o);
   }
   __syncthreads();
+  NMMO_STAMP(10);
   store_env(c, st, e);
+  __syncthreads();
+  NMMO_STAMP(11);
 }
 
 hipError_t launch_tick(const DevState& st, const int32_t* actions, const uint64_t* env_seeds,
@@ -600,3 +745,11 @@ hipError_t launch_rebuild_dep(const DevState& st, hipStream_t stream) {
 }
 
 }  // namespace nmmo
+
+#ifdef NMMO_STAMPS
+extern "C" __attribute__((visibility("default"))) int nmmo_debug_read_stamps(unsigned long long* out,
+                                                                              int n) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(nmmo::g_stamps), (size_t)n * 8, 0,
+                                  hipMemcpyDeviceToHost);
+}
+#endif

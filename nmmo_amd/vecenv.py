@@ -1,0 +1,255 @@
+"""Drop-in vectorized env for the reference trainer (pufferlib 0.7.3 pool protocol) and a
+PettingZoo-style single-env facade (nmmo.Env protocol), both backed by the HIP engine.
+
+Protocol 2 — what `reinforcement_learning/clean_pufferl.py` consumes:
+    pool = GpuVecEnv(env_creator, env_kwargs=..., num_envs=..., envs_per_worker=...,
+                     envs_per_batch=..., env_pool=..., mask_agents=True)   # :106-114
+    pool.single_observation_space.shape, pool.single_action_space.shape    # :116-117
+    pool.agents_per_env, pool.envs_per_batch, pool.driver_env              # :118,134-136,151
+    pool.async_reset(seed)                                                 # :175
+    o, r, d, t, infos, env_id, mask = pool.recv()                          # :293
+    pool.send(actions)                                                     # :357
+    pool.close()                                                           # :563
+Differences by design: all envs step in lockstep on the GPU, so `envs_per_batch` is every env
+of the pool and `recv` returns device tensors for the observations (the trainer's
+`torch.as_tensor(o).to(device)` at :302,318 is then a no-op instead of an H2D copy); `mask` is a
+host numpy bool array because the trainer combines it with host arrays (:306,334).
+
+Protocol 1 — `NmmoEnv` exposes `reset(seed)` / `step(actions)` with per-agent dict
+observations (the unflattened layout) like `nmmo.Env`, for wrappers such as
+`reinforcement_learning/stat_wrapper.py` (the realm facade is partial: see `NmmoEnv.realm`).
+"""
+
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import abi, layout
+from .config import Config
+from .engine import NmmoEngine
+
+
+class Box:
+    """Minimal gym.spaces.Box stand-in (gymnasium is not installed in this image)."""
+
+    def __init__(self, low, high, shape, dtype):
+        self.low, self.high, self.shape, self.dtype = low, high, tuple(shape), np.dtype(dtype)
+
+    def __repr__(self):
+        return f"Box({self.shape}, {self.dtype})"
+
+
+class MultiDiscrete:
+    def __init__(self, nvec):
+        self.nvec = np.asarray(nvec, dtype=np.int64)
+        self.shape = self.nvec.shape
+        self.dtype = np.dtype(np.int64)
+
+    def sample(self, rng=None):
+        rng = rng or np.random.default_rng()
+        return (rng.random(self.shape) * self.nvec).astype(np.int64)
+
+    def __repr__(self):
+        return f"MultiDiscrete({self.nvec.tolist()})"
+
+
+class DriverEnv:
+    """The attributes the reference reads off `pool.driver_env` (clean_pufferl.py:134-136,
+    baseline_policy.py:28): unflatten_context, obs_sz, possible_agents, spaces."""
+
+    def __init__(self, config: Config, obs_elems: int):
+        self.config = config
+        self.obs_sz = obs_elems
+        self.possible_agents = list(range(1, config.PLAYER_N + 1))
+        self.unflatten_context = layout.flat_layout(config.TASK_EMBED_DIM)
+        self.single_observation_space = Box(-2**20, 2**20, (obs_elems,), np.float32)
+        self.single_action_space = MultiDiscrete(layout.ACTION_DIMS)
+
+    def unflatten(self, flat):
+        return layout.unflatten(flat, self.config.TASK_EMBED_DIM)
+
+
+def _config_from_kwargs(env_kwargs) -> Config:
+    if isinstance(env_kwargs, Config):
+        return env_kwargs
+    if env_kwargs and "env" in env_kwargs:  # environment.py:57 passes kwargs["env"]
+        return Config(env_kwargs["env"])
+    return Config()
+
+
+class GpuVecEnv:
+    """pufferlib-0.7.3 pool protocol over one NmmoEngine (all envs in lockstep on one GPU)."""
+
+    def __init__(self, env_creator=None, env_kwargs=None, num_envs=1, envs_per_worker=1,
+                 envs_per_batch=None, env_pool=False, mask_agents=True, *, config=None,
+                 device=None, seed=0, task_embedding=None, env_index_base=0):
+        del env_creator, envs_per_worker, env_pool  # the engine replaces workers and creators
+        self.config = config or _config_from_kwargs(env_kwargs)
+        if self.config.obs_layout != abi.OBS_FLAT:
+            raise ValueError("GpuVecEnv serves flat observations (obs_layout=OBS_FLAT)")
+        self.num_envs = int(num_envs)
+        if envs_per_batch not in (None, self.num_envs):
+            # lockstep GPU stepping: one batch = every env (clean_pufferl sizes buffers from
+            # envs_per_batch, so report the real value instead of silently re-batching)
+            pass
+        self.envs_per_batch = self.num_envs
+        self.mask_agents = mask_agents
+        self.engine = NmmoEngine(self.config, self.num_envs, seed=seed, device=device,
+                                 task_embedding=task_embedding, env_index_base=env_index_base)
+        self.agents_per_env = self.config.PLAYER_N
+        self.driver_env = DriverEnv(self.config, self.engine.obs_elems)
+        self.single_observation_space = self.driver_env.single_observation_space
+        self.single_action_space = self.driver_env.single_action_space
+        self.env_id = np.arange(self.num_envs * self.agents_per_env)
+        self._seed = seed
+        self._ready = False
+
+    # -- protocol
+    def async_reset(self, seed=None):
+        if seed is not None:
+            base = np.uint64(seed)
+            seeds = np.array([base + np.uint64(i) for i in range(self.num_envs)], dtype=np.uint64)
+            self.engine.reset(seeds)
+        else:
+            self.engine.reset()
+        self._ready = True
+
+    def recv(self):
+        if not self._ready:
+            raise RuntimeError("recv() before async_reset()/send()")
+        e = self.engine
+        N = self.num_envs * self.agents_per_env
+        o = e.obs.view(N, e.obs_elems)
+        r = e.rew.view(N)
+        d = e.term.view(N)
+        t = e.trunc.view(N)
+        mask = e.mask.view(N).to(torch.bool).cpu().numpy()
+        self._ready = False
+        return o, r, d, t, [], self.env_id, mask
+
+    def send(self, actions):
+        a = torch.as_tensor(actions)
+        a = a.to(device=self.engine.device, dtype=torch.int32).reshape(
+            self.num_envs, self.agents_per_env, abi.N_ACTION_HEADS)
+        self.engine.step(a)
+        self._ready = True
+
+    def close(self):
+        self.engine.close()
+
+    # -- helpers
+    def unflatten_obs(self):
+        return self.driver_env.unflatten(self.engine.obs)
+
+
+class NmmoEnv:
+    """PettingZoo-ParallelEnv-shaped facade over a 1-env engine (nmmo.Env protocol).
+
+    reset(seed) -> (obs, infos); step(actions: {agent_id: int[12] or dict}) ->
+    (obs, rewards, terminated, truncated, infos); obs[agent] is the unflattened dict of numpy
+    arrays (Tile, Entity, Inventory, Market, Task, AgentId, CurrentTick, ActionTargets)."""
+
+    def __init__(self, config: Config | None = None, seed: int = 0, device=None, task_embedding=None):
+        self.config = config or Config()
+        self.config.obs_layout = abi.OBS_FLAT
+        self.engine = NmmoEngine(self.config, 1, seed=seed, device=device,
+                                 task_embedding=task_embedding)
+        self.possible_agents = list(range(1, self.config.PLAYER_N + 1))
+        self.agents: list[int] = []
+        self._obs_space = Box(-2**20, 2**20, (self.engine.obs_elems,), np.float32)
+        self._act_space = MultiDiscrete(layout.ACTION_DIMS)
+
+    def observation_space(self, agent):
+        return self._obs_space
+
+    def action_space(self, agent):
+        return self._act_space
+
+    def _obs_dict(self, mask):
+        flat = self.engine.obs[0].cpu().numpy()
+        d = layout.unflatten(flat, self.config.TASK_EMBED_DIM)
+        out = {}
+        for i, a in enumerate(self.possible_agents):
+            if mask[i]:
+                out[a] = _index(d, i)
+        return out
+
+    def reset(self, seed=None, options=None):
+        self.engine.reset(None if seed is None else np.array([seed], dtype=np.uint64))
+        mask = self.engine.mask[0].cpu().numpy()
+        self.agents = [a for i, a in enumerate(self.possible_agents) if mask[i]]
+        return self._obs_dict(mask), {a: {} for a in self.agents}
+
+    def step(self, actions):
+        buf = np.zeros((1, self.config.PLAYER_N, abi.N_ACTION_HEADS), np.int32)
+        buf[0, :, 1] = layout.PLAYER_N_OBS  # noop defaults
+        buf[0, :, 8] = 4
+        for a, act in actions.items():
+            if isinstance(act, dict):
+                act = flatten_action(act)
+            buf[0, a - 1] = np.asarray(act, dtype=np.int32)
+        self.engine.step(torch.from_numpy(buf).to(self.engine.device))
+        e = self.engine
+        mask = e.mask[0].cpu().numpy()
+        rew, term, trunc = (x[0].cpu().numpy() for x in (e.rew, e.term, e.trunc))
+        present = [a for i, a in enumerate(self.possible_agents) if mask[i]]
+        obs = self._obs_dict(mask)
+        rewards = {a: float(rew[a - 1]) for a in present}
+        terms = {a: bool(term[a - 1]) for a in present}
+        truncs = {a: bool(trunc[a - 1]) for a in present}
+        self.agents = [a for a in present if not (terms[a] or truncs[a])]
+        return obs, rewards, terms, truncs, {a: {} for a in present}
+
+    @property
+    def realm(self):
+        """Partial realm facade: `realm.tick` and `realm.players[id]` with the entity columns as
+        attributes (the reads of stat_wrapper.py:136-185); the event log arrives with row A16."""
+        return _Realm(self.state())
+
+    def state(self) -> dict:
+        st = self.engine.get_state()
+        S = self.engine.S
+        per = abi.state_bytes_per_env(S)
+        b = st[:per]
+        env = b[:abi.NE * 4].view(np.int32)
+        ent = b[abi.NE * 4:abi.NE * 4 + abi.NF * S * 2].view(np.int16).reshape(abi.NF, S)
+        return {"tick": int(env[abi.E["tick"]]),
+                "entities": {n: ent[i].copy() for i, n in enumerate(abi.ENTITY_FIELDS)}}
+
+    def close(self):
+        self.engine.close()
+
+
+def flatten_action(act: dict) -> np.ndarray:
+    """{"Move": {"Direction": 2}, "Attack": {"Style": 0, "Target": 5}, ...} -> int[12] in the
+    MultiDiscrete head order (takeru/policy.py:293-307); absent heads take their noop."""
+    out = np.array([0, 100, 1024, 12, 12, 100, 0, 100, 4, 12, 0, 12], dtype=np.int32)
+    for i, ((a, b), _) in enumerate(layout.ACTION_HEADS):
+        if a in act and b in act[a]:
+            out[i] = int(act[a][b])
+    return out
+
+
+class _Entity:
+    """One entity row; every entity-table field is an int attribute (alive, health, food, ...)."""
+
+    def __init__(self, cols: dict, slot: int):
+        for k, v in cols.items():
+            setattr(self, k, int(v[slot]))
+
+
+class _Realm:
+    def __init__(self, st: dict):
+        self.tick = st["tick"]
+        ent = st["entities"]
+        self.players = {int(ent["id"][s]): _Entity(ent, s) for s in range(len(ent["id"]))
+                        if ent["id"][s] > 0 and ent["alive"][s]}
+        self.npcs = {int(ent["id"][s]): _Entity(ent, s) for s in range(len(ent["id"]))
+                     if ent["id"][s] < 0 and ent["alive"][s]}
+
+
+def _index(d, i):
+    if isinstance(d, dict):
+        return {k: _index(v, i) for k, v in d.items()}
+    return d[i]

@@ -627,8 +627,8 @@ static void step_env(Oracle* o, int e, const int32_t* actions, float* obs, float
   for (int t = 0; t < NMMO_MAP_TILES; t++) {
     if (mat[t] == base[t]) continue;
     uint32_t u[4];
-    draw(env_seed(E), tick + 1, P_RESPAWN, (uint32_t)t, 0, u);
-    if (u[0] < respawn_u32(base[t])) mat[t] = base[t];
+    draw(env_seed(E), tick + 1, P_RESPAWN, (uint32_t)(t >> 2), 0, u);  /* one draw per 4 tiles */
+    if (u[t & 3] < respawn_u32(base[t])) mat[t] = base[t];
   }
   /* 7. NPC refill */
   if (sys_on(o, NMMO_SYS_NPC)) npc_spawn(o, e, tick + 1);

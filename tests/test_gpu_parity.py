@@ -92,3 +92,42 @@ def test_set_state_roundtrip():
         eng.step(torch.from_numpy(a).cuda())
     torch.cuda.synchronize()
     _cmp_state(eng.get_state(), orc.get_state(), 3, eng.S, "after set_state")
+
+
+class _EngineStepper:
+    """HIP engine behind the golden-rollout driver (numpy in/out)."""
+
+    def __init__(self, preset):
+        from tests.golden.make_rollout_fixtures import config
+
+        self.e = _engine(config(preset), 4, seed=2024)
+
+    def reset(self):
+        self.e.reset()
+
+    def step(self, a):
+        import torch
+
+        self.e.step(torch.from_numpy(a).cuda())
+
+    def scripted_actions(self, s):
+        return self.e.scripted_actions(s).cpu().numpy()
+
+    def get_state(self):
+        import torch
+
+        torch.cuda.synchronize()
+        return self.e.get_state()
+
+    def outputs(self):
+        return tuple(getattr(self.e, n).cpu().numpy() for n in ("rew", "term", "trunc", "mask"))
+
+
+@pytest.mark.parametrize("preset", ["C2", "C3"])
+def test_golden_rollout_hashes_gpu(preset):
+    import json
+
+    from tests.golden.make_rollout_fixtures import rollout
+
+    golden = json.load(open("tests/golden/rollout_hashes.json"))[preset]
+    assert rollout(_EngineStepper(preset), preset) == golden

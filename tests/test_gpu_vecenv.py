@@ -1,0 +1,67 @@
+"""The pufferlib-shaped pool and the PettingZoo-shaped facade driven the way the reference
+drives them (clean_pufferl.py:106-118,175,293,357; stat_wrapper.py:51,64), on the GPU."""
+
+import numpy as np
+import pytest
+
+from nmmo_amd import layout
+from nmmo_amd.config import Config
+
+pytestmark = pytest.mark.gpu
+
+
+def test_pool_protocol_matches_engine_and_oracle():
+    import torch
+
+    from nmmo_amd.vecenv import GpuVecEnv
+    from oracle.oracle import OracleEnvs
+
+    cfg = Config.preset("C4", MAP_N=4, early_stop_agent_num=8)
+    pool = GpuVecEnv(None, env_kwargs=None, num_envs=3, envs_per_worker=1, envs_per_batch=3,
+                     env_pool=True, mask_agents=True, config=cfg, seed=5)
+    assert pool.single_observation_space.shape == (23987,)
+    assert pool.single_action_space.shape == (12,)
+    assert pool.agents_per_env == 128 and pool.driver_env.obs_sz == 23987
+    ref = OracleEnvs(cfg, 3, seed=5)
+    pool.async_reset(1)
+    ref.reset(env_seeds=np.array([1, 2, 3], dtype=np.uint64))
+    rng = np.random.default_rng(0)
+    for t in range(10):
+        o, r, d, tr, infos, env_id, mask = pool.recv()
+        assert o.shape == (3 * 128, 23987) and o.is_cuda and mask.dtype == np.bool_
+        assert np.array_equal(o.cpu().numpy(), ref.obs.reshape(3 * 128, -1))
+        assert np.array_equal(mask, ref.mask.reshape(-1).astype(bool))
+        # a policy-like action sampler over the masks (baseline_policy.py:228-264)
+        d_ = layout.unflatten(o.cpu().numpy())
+        acts = np.zeros((3 * 128, 12), np.int64)
+        for h, ((a, b), n) in enumerate(layout.ACTION_HEADS):
+            m = d_["ActionTargets"][a][b].astype(bool)
+            for i in range(3 * 128):
+                ok = np.flatnonzero(m[i])
+                acts[i, h] = rng.choice(ok) if len(ok) else 0
+        pool.send(acts)
+        ref.step(acts.reshape(3, 128, 12).astype(np.int32))
+    o, r, d, tr, infos, env_id, mask = pool.recv()
+    torch.cuda.synchronize()
+    assert np.array_equal(r.cpu().numpy(), ref.rew.reshape(-1))
+    assert np.array_equal(pool.engine.get_state(), ref.get_state())
+    pool.close()
+
+
+def test_pettingzoo_facade():
+    from nmmo_amd.vecenv import NmmoEnv
+
+    env = NmmoEnv(Config.preset("C3", MAP_N=2), seed=3)
+    obs, info = env.reset(seed=7)
+    assert len(obs) == 128 and set(obs[1]) >= {"Tile", "Entity", "Task", "AgentId", "ActionTargets"}
+    assert obs[5]["AgentId"][0] == 5 and obs[5]["Tile"].shape == (225, 3)
+    total = 0
+    for t in range(30):
+        acts = {a: {"Move": {"Direction": t % 4}} for a in env.agents}
+        obs, rew, term, trunc, info = env.step(acts)
+        total += len(rew)
+        assert all(abs(v - 1 / 1024) < 1e-9 or v == -1.0 for v in rew.values())
+    realm = env.realm
+    assert realm.tick == 30 and all(p.alive for p in realm.players.values())
+    assert total > 0
+    env.close()

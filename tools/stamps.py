@@ -1,0 +1,64 @@
+"""Phase attribution of the tick kernel from in-kernel s_memtime stamps (diagnostic build).
+
+Usage (GPU box): python tools/stamps.py [C3] [envs] [warmup]
+Builds nothing on the box: run `python -c "from nmmo_amd import build; build.build(stamps=True)"`
+here first (the .so travels with the snapshot). Prints median / p90 cycles per phase.
+"""
+
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+os.environ["NMMO_LIB"] = os.path.join(ROOT, "nmmo_amd", "lib", "libnmmo_hip_stamps.so")
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from nmmo_amd import _native, abi  # noqa: E402
+from nmmo_amd.config import Config  # noqa: E402
+from nmmo_amd.engine import NmmoEngine  # noqa: E402
+
+PHASES = ["load", "rowslot", "decode+npc_decide", "update+harvest", "attack:uncontested",
+          "attack:contested", "move", "cull+compact", "respawn", "npc_spawn", "rewards", "store"]
+
+
+def main():
+    preset = sys.argv[1] if len(sys.argv) > 1 else "C3"
+    envs = int(sys.argv[2]) if len(sys.argv) > 2 else 1024
+    warm = int(sys.argv[3]) if len(sys.argv) > 3 else 40
+    cfg = Config.preset(preset, early_stop_agent_num=8,
+                        obs_layout=abi.OBS_FLAT if preset == "C4" else abi.OBS_NONE)
+    eng = NmmoEngine(cfg, envs, seed=1)
+    eng.reset()
+    L = _native.lib()
+    L.nmmo_debug_read_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    rows, subs = [], []
+    for t in range(warm + 10):
+        eng.scripted_actions(1000 + t)
+        eng.step()
+        torch.cuda.synchronize()
+        if t >= warm:
+            buf = np.zeros(4096 * 16, np.uint64)
+            assert L.nmmo_debug_read_stamps(buf.ctypes.data_as(ctypes.c_void_p), buf.size) == 0
+            st = buf.reshape(4096, 16)[:min(envs, 4096), :12].astype(np.int64)
+            ok = (st[:, 2] > 0) & (st[:, 11] > st[:, 0])  # stepped (not reset) envs
+            d = np.diff(st[ok], axis=1)
+            rows.append(d)
+            full = buf.reshape(4096, 16)[:min(envs, 4096)].astype(np.int64)[ok]
+            subs.append(np.stack([full[:, 12] - full[:, 1], full[:, 2] - full[:, 12],
+                                  full[:, 13] - full[:, 1]], 1))
+    d = np.concatenate(rows)
+    tot = np.median(d.sum(1))
+    print(f"{preset} envs={envs}: median total {tot:.0f} cycles over {len(d)} env-ticks")
+    for i in range(11):
+        med, p90 = np.median(d[:, i]), np.percentile(d[:, i], 90)
+        print(f"  {PHASES[i+1]:22s} median {med:9.0f}  p90 {p90:9.0f}  ({100*med/tot:5.1f}%)")
+    sub = np.concatenate(subs)
+    print(f"  of which player decode  median {np.median(sub[:, 0]):9.0f} (visibility bitmap "
+          f"{np.median(sub[:, 2]):9.0f}); npc decide median {np.median(sub[:, 1]):9.0f}")
+
+
+if __name__ == "__main__":
+    main()
