@@ -2,7 +2,7 @@
 """bench.py — agent-steps/sec of the MI355X Neural MMO stepper (BASELINE.json metric).
 
 One "step" = one tick of every env on this GPU: the scripted masked-uniform policy kernel
-(SPEC.md §9, the synthetic action input) + nmmo_step (tick kernel [+ obs kernel]).
+(SPEC.md §10, the synthetic action input) + nmmo_step (tick kernel [+ obs kernel]).
 Inputs/state are resident in HBM before the timed region. Envs shard across ranks with no
 data-path collective (weak scaling: envs per GPU fixed); each rank times K steps between a
 barrier + device sync, rank 0 reports the max over ranks.
@@ -244,7 +244,7 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "int16",
-            "data": "synthetic: generated map bank (SPEC §3), masked-uniform scripted actions (SPEC §9)",
+            "data": "synthetic: generated map bank (SPEC §3), masked-uniform scripted actions (SPEC §10)",
             "config": {
                 "workload": wl["desc"],
                 "envs_per_gpu": envs,

@@ -64,6 +64,13 @@ extern "C" {
 #define NMMO_OBS_NONE 0   /* C2/C3 benchmark configs: state only */
 #define NMMO_OBS_FLAT 1   /* pufferlib-0.7.3 flat float32 vector, 23,987 / agent */
 
+/* ---- items (SPEC.md §9): per player NMMO_INV_SLOTS inventory slots in ascending item-row
+ * order, each item two u32 words: w0 = type | level<<5 | equipped<<9 | listed_price<<10 |
+ * listed_tick<<17 ; w1 = quantity | row<<16 (type 0 = empty slot). Item rows come from a FIFO
+ * ring of NMMO_INV_SLOTS * player_n rows. ---- */
+#define NMMO_INV_SLOTS 12
+#define NMMO_MARKET_ROWS 1024
+
 /* ---- fixed geometry (nmmo 2.1 defaults, SPEC.md §1) ---- */
 #define NMMO_MAP_SIZE 160          /* MAP_CENTER 128 + 2 * MAP_BORDER 16 */
 #define NMMO_MAP_TILES (NMMO_MAP_SIZE * NMMO_MAP_SIZE)
@@ -93,6 +100,8 @@ enum NmmoField {
   F_PLAYER_KILLS,
   F_HEALTH_RESTORE,    /* Resources.health_restore of the last update */
   F_DIED_TICK,         /* tick at which the player was culled (0 = alive) */
+  F_DROP_ARMOR,        /* NPC drop: armor type - 2 (Hat/Top/Bottom) */
+  F_DROP_TOOL,         /* NPC drop: tool type - 8 (Rod..Chisel) */
   NMMO_NF_USED,
   NMMO_NF = 48
 };
@@ -101,6 +110,7 @@ enum NmmoField {
 enum NmmoEnvField {
   E_TICK = 0, E_MAP_ID, E_DONE, E_EPISODE, E_NPC_COUNT, E_NPC_NEXT_ID, E_FREE_HEAD,
   E_FREE_COUNT, E_SEED_LO, E_SEED_HI, E_PLAYERS_ALIVE, E_ENV_INDEX,
+  E_ITEM_FREE_HEAD, E_ITEM_FREE_COUNT,
   NMMO_NE_USED,
   NMMO_NE = 16
 };
@@ -164,7 +174,8 @@ NMMO_API int nmmo_step(NmmoHandle* h, const int32_t* actions, void* obs, float* 
 NMMO_API int nmmo_scripted_actions(NmmoHandle* h, uint64_t policy_seed, int32_t* actions, void* stream);
 
 /* State blob: per env, [NMMO_NE int32 env fields][NF*slots int16 entity table]
- * [slots int16 free-row ring][MAP_TILES u8 material]; envs concatenated. Synchronous. */
+ * [slots int16 free-row ring][MAP_TILES u8 material][player_n*12 x 2 u32 items]
+ * [12*player_n int16 item-row ring]; envs concatenated. Synchronous. */
 NMMO_API int nmmo_get_state(NmmoHandle* h, void* host_buf, size_t nbytes);
 NMMO_API int nmmo_set_state(NmmoHandle* h, const void* host_buf, size_t nbytes);
 /* The generated map bank: host u8 [map_n][MAP_TILES]. Synchronous. */

@@ -45,12 +45,14 @@ ENTITY_FIELDS = [
     # internal
     "alive", "ds_row", "resilient", "exploration", "style", "target_id", "npc_level",
     "equip_offense", "equip_defense", "player_kills", "health_restore", "died_tick",
+    "drop_armor", "drop_tool",
 ]
 F = {name: i for i, name in enumerate(ENTITY_FIELDS)}
 
 ENV_FIELDS = [
     "tick", "map_id", "done", "episode", "npc_count", "npc_next_id", "free_head",
     "free_count", "seed_lo", "seed_hi", "players_alive", "env_index",
+    "item_free_head", "item_free_count",
 ]
 E = {name: i for i, name in enumerate(ENV_FIELDS)}
 
@@ -95,5 +97,10 @@ class NmmoLayout(ctypes.Structure):
     )
 
 
-def state_bytes_per_env(slots: int) -> int:
-    return NE * 4 + NF * slots * 2 + slots * 2 + MAP_TILES
+INV_SLOTS = 12
+MARKET_ROWS = 1024
+
+
+def state_bytes_per_env(slots: int, players: int = 128) -> int:
+    return NE * 4 + NF * slots * 2 + slots * 2 + MAP_TILES + players * INV_SLOTS * 8 \
+        + INV_SLOTS * players * 2

@@ -1,5 +1,5 @@
 // obs.hip — per-agent observation gather (SPEC.md §8) and the scripted masked-uniform policy
-// (SPEC.md §9).
+// (SPEC.md §10).
 //
 // Replaces Env._compute_observations + pufferlib's flatten/pad (the buffer the reference
 // receives from pool.recv(), clean_pufferl.py:293, and decodes with unpack_batched_obs,
@@ -149,7 +149,7 @@ hipError_t launch_obs(const ObsParams& p, hipStream_t stream) {
   return hipGetLastError();
 }
 
-// ---------------------------------------------------------------- scripted policy (SPEC §9)
+// ---------------------------------------------------------------- scripted policy (SPEC §10)
 // One workgroup per env, one thread per player. The env's entities are first packed per
 // datastore row into one int32 (r | c<<8 | slot<<16 | immune<<25, -1 = absent), so the two
 // visibility passes over the rows are one broadcast LDS load per row with no dependent loads.

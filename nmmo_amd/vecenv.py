@@ -210,7 +210,7 @@ class NmmoEnv:
     def state(self) -> dict:
         st = self.engine.get_state()
         S = self.engine.S
-        per = abi.state_bytes_per_env(S)
+        per = abi.state_bytes_per_env(S, self.config.PLAYER_N)
         b = st[:per]
         env = b[:abi.NE * 4].view(np.int32)
         ent = b[abi.NE * 4:abi.NE * 4 + abi.NF * S * 2].view(np.int16).reshape(abi.NF, S)

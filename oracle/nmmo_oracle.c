@@ -184,12 +184,16 @@ typedef struct {
   int16_t* ring;       /* [n_envs][S] */
   uint8_t* mat;        /* [n_envs][TILES] */
   uint8_t* bank;       /* [map_n][TILES] */
+  uint32_t* items;     /* [n_envs][P][INV][2] (SPEC §9 item words) */
+  int16_t* iring;      /* [n_envs][INV*P] free item rows */
   float task[4096];
 } Oracle;
 
 #define ENV(o, e) ((o)->env + (size_t)(e) * NMMO_NE)
 #define ENT(o, e) ((o)->ent + (size_t)(e) * NMMO_NF * (o)->S)
 #define FLD(t, f, s) (t)[(size_t)(f) * S + (s)]
+#define INV NMMO_INV_SLOTS
+#define INVP(o, e, p) ((o)->items + (((size_t)(e) * (o)->P + (p)) * INV) * 2)
 
 static int sys_on(const Oracle* o, uint32_t s) { return (o->cfg.systems & s) != 0; }
 static int level_at_exp(int exp) {
@@ -219,6 +223,143 @@ static float half_to_float(uint16_t h) {
   float f;
   memcpy(&f, &bits, 4);
   return f;
+}
+
+/* ------------------------------------------------------------------ items (SPEC §9) */
+enum { T_HAT = 2, T_TOP, T_BOTTOM, T_SPEAR, T_BOW, T_WAND, T_ROD, T_GLOVES, T_PICKAXE, T_AXE,
+       T_CHISEL, T_WHETSTONE, T_ARROW, T_RUNES, T_RATION, T_POTION };
+enum { P_BUY_ORDER = 7 };
+#define IT_TYPE(w) ((int)((w)[0] & 31))
+#define IT_LEVEL(w) ((int)(((w)[0] >> 5) & 15))
+#define IT_EQUIPPED(w) ((int)(((w)[0] >> 9) & 1))
+#define IT_PRICE(w) ((int)(((w)[0] >> 10) & 127))
+#define IT_LTICK(w) ((int)(((w)[0] >> 17) & 2047))
+#define IT_QTY(w) ((int)((w)[1] & 0xFFFF))
+#define IT_ROW(w) ((int)((w)[1] >> 16))
+
+static int item_attack(int type, int level, int style) {
+  if (type == T_SPEAR + style || type == T_WHETSTONE + style) return 5 + 5 * level;
+  return 0;
+}
+static int item_defense(int type, int level) {
+  if (type >= T_HAT && type <= T_BOTTOM) return 3 * level;
+  if (type >= T_ROD && type <= T_CHISEL) return 2 * level;
+  return 0;
+}
+static int equip_slot(int type) { /* hat top bottom held ammo; -1 consumable */
+  if (type >= T_HAT && type <= T_BOTTOM) return type - T_HAT;
+  if (type >= T_SPEAR && type <= T_CHISEL) return 3;
+  if (type >= T_WHETSTONE && type <= T_RUNES) return 4;
+  return -1;
+}
+static int inv_count(const uint32_t* inv) {
+  int n = 0;
+  while (n < INV && IT_TYPE(inv + 2 * n)) n++;
+  return n;
+}
+static int inv_find(const uint32_t* inv, int row) {
+  for (int k = 0; k < INV && IT_TYPE(inv + 2 * k); k++)
+    if (IT_ROW(inv + 2 * k) == row) return k;
+  return -1;
+}
+static void inv_remove(uint32_t* inv, int k) {
+  for (int j = k; j < INV - 1; j++) { inv[2 * j] = inv[2 * j + 2]; inv[2 * j + 1] = inv[2 * j + 3]; }
+  inv[2 * INV - 2] = inv[2 * INV - 1] = 0;
+}
+static void inv_insert_sorted(uint32_t* inv, uint32_t w0, uint32_t w1) { /* caller checked room */
+  int n = inv_count(inv), k = n;
+  while (k > 0 && IT_ROW(inv + 2 * (k - 1)) > (int)(w1 >> 16)) {
+    inv[2 * k] = inv[2 * k - 2]; inv[2 * k + 1] = inv[2 * k - 1]; k--;
+  }
+  inv[2 * k] = w0; inv[2 * k + 1] = w1;
+}
+static int inv_stack_slot(const uint32_t* inv, int type, int level) {
+  if (type < T_WHETSTONE || type > T_RUNES) return -1;
+  for (int k = 0; k < INV && IT_TYPE(inv + 2 * k); k++)
+    if (IT_TYPE(inv + 2 * k) == type && IT_LEVEL(inv + 2 * k) == level) return k;
+  return -1;
+}
+static void free_item_row(Oracle* o, int e, int row) {
+  int32_t* E = ENV(o, e);
+  int16_t* ir = o->iring + (size_t)e * INV * o->P;
+  ir[(E[E_ITEM_FREE_HEAD] + E[E_ITEM_FREE_COUNT]) % (INV * o->P)] = (int16_t)row;
+  E[E_ITEM_FREE_COUNT]++;
+}
+static int alloc_item_row(Oracle* o, int e) {
+  int32_t* E = ENV(o, e);
+  int16_t* ir = o->iring + (size_t)e * INV * o->P;
+  int row = ir[E[E_ITEM_FREE_HEAD]];
+  E[E_ITEM_FREE_HEAD] = (E[E_ITEM_FREE_HEAD] + 1) % (INV * o->P);
+  E[E_ITEM_FREE_COUNT]--;
+  return row;
+}
+/* a brand-new item (harvest, NPC drop): stacks onto ammo, else a new row if there is room */
+static void receive_new(Oracle* o, int e, int p, int type, int level) {
+  uint32_t* inv = INVP(o, e, p);
+  int k = inv_stack_slot(inv, type, level);
+  if (k >= 0) { inv[2 * k + 1] += 1; return; }
+  if (inv_count(inv) >= INV) return;
+  int row = alloc_item_row(o, e);
+  inv_insert_sorted(inv, (uint32_t)type | ((uint32_t)level << 5), 1u | ((uint32_t)row << 16));
+}
+/* an existing item moving into p's inventory (loot, give, buy), already unequipped/unlisted */
+static void receive_moved(Oracle* o, int e, int p, uint32_t w0, uint32_t w1) {
+  uint32_t* inv = INVP(o, e, p);
+  uint32_t it[2] = {w0, w1};
+  int k = inv_stack_slot(inv, IT_TYPE(it), IT_LEVEL(it));
+  if (k >= 0) { inv[2 * k + 1] += (uint32_t)IT_QTY(it); free_item_row(o, e, IT_ROW(it)); return; }
+  if (inv_count(inv) >= INV) { free_item_row(o, e, IT_ROW(it)); return; }
+  inv_insert_sorted(inv, w0, w1);
+}
+static int has_room(Oracle* o, int e, int p, const uint32_t* it) {
+  const uint32_t* inv = INVP(o, e, p);
+  return inv_stack_slot(inv, IT_TYPE(it), IT_LEVEL(it)) >= 0 || inv_count(inv) < INV;
+}
+static void update_item_level(Oracle* o, int e, int p) {
+  const int S = o->S;
+  int16_t* T = ENT(o, e);
+  const uint32_t* inv = INVP(o, e, p);
+  int l = 0;
+  for (int k = 0; k < INV && IT_TYPE(inv + 2 * k); k++)
+    if (IT_EQUIPPED(inv + 2 * k)) l += IT_LEVEL(inv + 2 * k);
+  FLD(T, F_ITEM_LEVEL, p) = (int16_t)l;
+}
+static int player_offense(Oracle* o, int e, int p, int style) {
+  const uint32_t* inv = INVP(o, e, p);
+  int a = 0;
+  for (int k = 0; k < INV && IT_TYPE(inv + 2 * k); k++)
+    if (IT_EQUIPPED(inv + 2 * k)) a += item_attack(IT_TYPE(inv + 2 * k), IT_LEVEL(inv + 2 * k), style);
+  return a;
+}
+static int player_defense(Oracle* o, int e, int p) {
+  const uint32_t* inv = INVP(o, e, p);
+  int d = 0;
+  for (int k = 0; k < INV && IT_TYPE(inv + 2 * k); k++)
+    if (IT_EQUIPPED(inv + 2 * k)) d += item_defense(IT_TYPE(inv + 2 * k), IT_LEVEL(inv + 2 * k));
+  return d;
+}
+/* level an item requires of its user (SPEC §9) */
+static int requirement_level(const int16_t* T, int S, int p, int type) {
+  if (type >= T_SPEAR && type <= T_WAND) return FLD(T, F_MELEE_LEVEL + 2 * (type - T_SPEAR), p);
+  if (type >= T_WHETSTONE && type <= T_RUNES) return FLD(T, F_MELEE_LEVEL + 2 * (type - T_WHETSTONE), p);
+  if (type >= T_ROD && type <= T_CHISEL) return FLD(T, F_FISHING_LEVEL + 2 * (type - T_ROD), p);
+  if (type == T_RATION) return FLD(T, F_FISHING_LEVEL, p);
+  if (type == T_POTION) return FLD(T, F_HERBALISM_LEVEL, p);
+  int m = FLD(T, F_MELEE_LEVEL, p); /* armor: max combat level */
+  if (FLD(T, F_RANGE_LEVEL, p) > m) m = FLD(T, F_RANGE_LEVEL, p);
+  if (FLD(T, F_MAGE_LEVEL, p) > m) m = FLD(T, F_MAGE_LEVEL, p);
+  return m;
+}
+static int usable(const int16_t* T, int S, int p, const uint32_t* it) {
+  if (IT_PRICE(it)) return 0;
+  if (equip_slot(IT_TYPE(it)) >= 0 && IT_EQUIPPED(it)) return 1;
+  return IT_LEVEL(it) <= requirement_level(T, S, p, IT_TYPE(it));
+}
+static void add_skill_exp(int16_t* T, int S, int p, int f_exp, int xp) {
+  int ex = FLD(T, f_exp, p) + xp;
+  FLD(T, f_exp, p) = (int16_t)ex;
+  int nl = level_at_exp(ex);
+  if (nl > FLD(T, f_exp - 1, p)) FLD(T, f_exp - 1, p) = (int16_t)nl;
 }
 
 /* ------------------------------------------------------------------ reset (SPEC §4) */
@@ -264,6 +405,11 @@ static void reset_env(Oracle* o, int e, uint64_t seed, int episode) {
   E[E_FREE_COUNT] = o->N;
   E[E_NPC_NEXT_ID] = -1;
   E[E_PLAYERS_ALIVE] = P;
+  memset(INVP(o, e, 0), 0, (size_t)P * INV * 8);
+  int16_t* ir = o->iring + (size_t)e * INV * P;
+  for (int k = 0; k < INV * P; k++) ir[k] = (int16_t)(k + 1);
+  E[E_ITEM_FREE_HEAD] = 0;
+  E[E_ITEM_FREE_COUNT] = INV * P;
   if (sys_on(o, NMMO_SYS_NPC)) npc_spawn(o, e, 0);
 }
 
@@ -307,6 +453,12 @@ static void npc_spawn(Oracle* o, int e, uint32_t tick) {
     FLD(T, F_DS_ROW, s) = ring[E[E_FREE_HEAD]];
     FLD(T, F_STYLE, s) = (int16_t)style;
     FLD(T, F_NPC_LEVEL, s) = (int16_t)level;
+    FLD(T, F_DROP_ARMOR, s) = (int16_t)U(u[3], 3);
+    FLD(T, F_DROP_TOOL, s) = (int16_t)U(u[3] >> 2, 5);
+    if (sys_on(o, NMMO_SYS_EQUIPMENT) && level > 0) { /* int(8 * (level - U[0,1))) */
+      int eq = (int)((((uint64_t)level << 32) - u[3]) * 8 >> 32);
+      FLD(T, F_EQUIP_OFFENSE, s) = FLD(T, F_EQUIP_DEFENSE, s) = (int16_t)eq;
+    }
     E[E_FREE_HEAD] = (E[E_FREE_HEAD] + 1) % S;
     E[E_FREE_COUNT]--;
     E[E_NPC_NEXT_ID]--;
@@ -405,6 +557,31 @@ static int combat_level(const Oracle* o, const int16_t* T, int s) {
   return l;
 }
 
+/* a player killed its target: gold, then the victim's items (player) or its drops (NPC) */
+static void loot(Oracle* o, int e, int x, int t) {
+  const int S = o->S, P = o->P;
+  int16_t* T = ENT(o, e);
+  if (sys_on(o, NMMO_SYS_EXCHANGE)) {
+    FLD(T, F_GOLD, x) = (int16_t)(FLD(T, F_GOLD, x) + FLD(T, F_GOLD, t));
+    FLD(T, F_GOLD, t) = 0;
+  }
+  if (!sys_on(o, NMMO_SYS_ITEM)) return;
+  if (t < P) {
+    uint32_t* inv = INVP(o, e, t);
+    while (IT_TYPE(inv)) {
+      uint32_t w0 = inv[0] & 0x1FFu, w1 = inv[1]; /* unequipped, unlisted */
+      w0 &= ~(1u << 9);
+      inv_remove(inv, 0);
+      receive_moved(o, e, x, w0, w1);
+    }
+    update_item_level(o, e, t);
+  } else {
+    int lvl = FLD(T, F_NPC_LEVEL, t) > 0 ? FLD(T, F_NPC_LEVEL, t) : 1;
+    if (sys_on(o, NMMO_SYS_EQUIPMENT)) receive_new(o, e, x, T_HAT + FLD(T, F_DROP_ARMOR, t), lvl);
+    if (sys_on(o, NMMO_SYS_PROFESSION)) receive_new(o, e, x, T_ROD + FLD(T, F_DROP_TOOL, t), lvl);
+  }
+}
+
 static void attack_call(Oracle* o, int e, int x, int style, int t) {
   const int S = o->S, P = o->P;
   int16_t* T = ENT(o, e);
@@ -419,8 +596,10 @@ static void attack_call(Oracle* o, int e, int x, int style, int t) {
   int offense = prog ? 10 + 5 * FLD(T, F_MELEE_LEVEL + 2 * style, x) : 30;
   int defense = prog ? 5 * combat_level(o, T, t) : 0;
   if (sys_on(o, NMMO_SYS_EQUIPMENT)) {
-    offense += FLD(T, F_EQUIP_OFFENSE, x);
-    defense += FLD(T, F_EQUIP_DEFENSE, t);
+    offense += x < P ? (sys_on(o, NMMO_SYS_ITEM) ? player_offense(o, e, x, style) : 0)
+                     : FLD(T, F_EQUIP_OFFENSE, x);
+    defense += t < P ? (sys_on(o, NMMO_SYS_ITEM) ? player_defense(o, e, t) : 0)
+                     : FLD(T, F_EQUIP_DEFENSE, t);
   }
   /* combat.damage_multiplier: dominant = np.argmax of target exp; 1.0 when all equal */
   int e0 = FLD(T, F_MELEE_EXP, t), e1 = FLD(T, F_RANGE_EXP, t), e2 = FLD(T, F_MAGE_EXP, t);
@@ -441,10 +620,26 @@ static void attack_call(Oracle* o, int e, int x, int style, int t) {
     int nl = level_at_exp(FLD(T, f, x));
     if (nl > FLD(T, f - 1, x)) FLD(T, f - 1, x) = (int16_t)nl;
   }
+  if (x < P && sys_on(o, NMMO_SYS_EQUIPMENT) && sys_on(o, NMMO_SYS_ITEM)) {
+    uint32_t* inv = INVP(o, e, x); /* fire one unit of the equipped ammunition of this style */
+    for (int k = 0; k < INV && IT_TYPE(inv + 2 * k); k++) {
+      if (!IT_EQUIPPED(inv + 2 * k) || IT_TYPE(inv + 2 * k) != T_WHETSTONE + style) continue;
+      inv[2 * k + 1] -= 1;
+      if (IT_QTY(inv + 2 * k) == 0) {
+        free_item_row(o, e, IT_ROW(inv + 2 * k));
+        inv_remove(inv, k);
+        update_item_level(o, e, x);
+      }
+      break;
+    }
+  }
   FLD(T, F_DAMAGE, t) = (int16_t)dmg;
   int h = FLD(T, F_HEALTH, t) - dmg;
   FLD(T, F_HEALTH, t) = (int16_t)(h < 0 ? 0 : h);
-  if (FLD(T, F_HEALTH, t) == 0) FLD(T, F_PLAYER_KILLS, x)++;
+  if (FLD(T, F_HEALTH, t) == 0) {
+    FLD(T, F_PLAYER_KILLS, x)++;
+    if (x < P) loot(o, e, x, t);
+  }
   FLD(T, F_LATEST_COMBAT_TICK, x) = FLD(T, F_LATEST_COMBAT_TICK, t) = (int16_t)(E[E_TICK] + 1);
 }
 
@@ -462,7 +657,90 @@ static void move_call(Oracle* o, int e, int x, int d) {
   if (progress > FLD(T, F_EXPLORATION, x)) FLD(T, F_EXPLORATION, x) = (int16_t)progress;
 }
 
-/* ------------------------------------------------------------------ observation (SPEC §8) */
+/* ------------------------------------------------------------------ observation (SPEC §8, §9) */
+/* Item.Query.for_sale: every listed item, ascending item row (owner slot, inventory slot) */
+static int market_list(Oracle* o, int e, int* own, int* slot) {
+  int n = 0;
+  for (int p = 0; p < o->P; p++) {
+    const uint32_t* inv = INVP(o, e, p);
+    for (int k = 0; k < INV && IT_TYPE(inv + 2 * k); k++) {
+      if (!IT_PRICE(inv + 2 * k)) continue;
+      int j = n++; /* insertion by row */
+      while (j > 0 && IT_ROW(INVP(o, e, own[j - 1]) + 2 * slot[j - 1]) > IT_ROW(inv + 2 * k)) {
+        own[j] = own[j - 1]; slot[j] = slot[j - 1]; j--;
+      }
+      own[j] = p; slot[j] = k;
+    }
+  }
+  return n;
+}
+
+/* ActionTargets of player p as int8 in flat order (SPEC §8, §9) */
+static void compute_masks(Oracle* o, int e, int p, const int* vis, int nv, const int* mown,
+                          const int* mslot, int nm, int8_t* m /* [1586] */) {
+  const FlatLayout L = flat_layout(0);
+  const int S = o->S, P = o->P;
+  const int16_t* T = ENT(o, e);
+  const uint8_t* mat = o->mat + (size_t)e * NMMO_MAP_TILES;
+  const uint32_t* inv = INVP(o, e, p);
+  const int r = FLD(T, F_ROW, p), c = FLD(T, F_COL, p), gold = FLD(T, F_GOLD, p);
+  const int item = sys_on(o, NMMO_SYS_ITEM), exch = sys_on(o, NMMO_SYS_EXCHANGE) && item;
+  memset(m, 0, (size_t)L.agent_id);
+  if (sys_on(o, NMMO_SYS_COMBAT))
+    for (int k = 0; k < 3; k++) m[L.mask_attack_style + k] = 1;
+  for (int i = 0; i < nv; i++) {
+    int s = vis[i], d = linf(r, c, FLD(T, F_ROW, s), FLD(T, F_COL, s));
+    if (sys_on(o, NMMO_SYS_COMBAT))
+      m[L.mask_attack_target + i] = s != p && d <= 3 && !(s < P && FLD(T, F_TIME_ALIVE, s) < o->cfg.spawn_immunity);
+    int same = s < P && s != p && d == 0;
+    if (item) m[L.mask_give_target + i] = (int8_t)same;
+    if (exch) m[L.mask_givegold_target + i] = (int8_t)same;
+  }
+  m[L.mask_attack_target + N_OBS] = 1;
+  m[L.mask_give_target + N_OBS] = 1;
+  m[L.mask_givegold_target + N_OBS] = 1;
+  for (int d = 0; d < 5; d++)
+    m[L.mask_move + d] = !impassable(mat[(r + DR[d]) * SIZE + c + DC[d]]);
+  for (int k = 0; k < INV && IT_TYPE(inv + 2 * k); k++) {
+    const uint32_t* it = inv + 2 * k;
+    int free_ = !IT_EQUIPPED(it) && !IT_PRICE(it);
+    if (item) {
+      m[L.mask_use + k] = (int8_t)usable(T, S, p, it);
+      m[L.mask_destroy + k] = (int8_t)free_;
+      m[L.mask_give_item + k] = (int8_t)free_;
+    }
+    if (exch) m[L.mask_sell_item + k] = !IT_EQUIPPED(it);
+  }
+  m[L.mask_use + 12] = m[L.mask_destroy + 12] = m[L.mask_give_item + 12] = m[L.mask_sell_item + 12] = 1;
+  if (exch) {
+    for (int q = 0; q < 99; q++) {
+      m[L.mask_givegold_price + q] = q < gold;
+      m[L.mask_sell_price + q] = 1;
+    }
+    for (int j = 0; j < nm && j < 1024; j++) {
+      const uint32_t* it = INVP(o, e, mown[j]) + 2 * mslot[j];
+      m[L.mask_buy + j] = IT_PRICE(it) <= gold && mown[j] != p;
+    }
+  }
+  m[L.mask_buy + 1024] = 1;
+}
+
+static void item_row16(const uint32_t* it, int owner_id, float* out) {
+  int type = IT_TYPE(it), lvl = IT_LEVEL(it);
+  out[0] = (float)IT_ROW(it);
+  out[1] = (float)type;
+  out[2] = (float)owner_id;
+  out[3] = (float)lvl;
+  out[4] = 0.f;
+  out[5] = (float)IT_QTY(it);
+  for (int st = 0; st < 3; st++) out[6 + st] = (float)item_attack(type, lvl, st);
+  for (int st = 0; st < 3; st++) out[9 + st] = (float)item_defense(type, lvl);
+  out[12] = type == T_POTION ? (float)(50 + 5 * lvl) : 0.f;
+  out[13] = type == T_RATION ? (float)(50 + 5 * lvl) : 0.f;
+  out[14] = (float)IT_EQUIPPED(it);
+  out[15] = (float)IT_PRICE(it);
+}
+
 static void write_obs(Oracle* o, int e, float* obs_env /* [P][obs_elems] or NULL */) {
   if (!obs_env) return;
   const FlatLayout L = flat_layout(o->cfg.task_embed_dim);
@@ -470,7 +748,9 @@ static void write_obs(Oracle* o, int e, float* obs_env /* [P][obs_elems] or NULL
   const int16_t* T = ENT(o, e);
   const int32_t* E = ENV(o, e);
   const uint8_t* mat = o->mat + (size_t)e * NMMO_MAP_TILES;
-  int vis[512];
+  int vis[512], mown[INV * 128], mslot[INV * 128];
+  int8_t m[1586];
+  int nm = market_list(o, e, mown, mslot);
   for (int p = 0; p < P; p++) {
     float* ob = obs_env + (size_t)p * L.elems;
     memset(ob, 0, sizeof(float) * (size_t)L.elems);
@@ -478,30 +758,18 @@ static void write_obs(Oracle* o, int e, float* obs_env /* [P][obs_elems] or NULL
     int r = FLD(T, F_ROW, p), c = FLD(T, F_COL, p);
     int nv = visible_slots(o, e, p, vis);
     if (nv > N_OBS) nv = N_OBS;
-    /* ActionTargets */
-    if (sys_on(o, NMMO_SYS_COMBAT))
-      for (int k = 0; k < 3; k++) ob[L.mask_attack_style + k] = 1.f;
-    for (int i = 0; i < nv && sys_on(o, NMMO_SYS_COMBAT); i++) {
-      int s = vis[i];
-      int ok = s != p && linf(r, c, FLD(T, F_ROW, s), FLD(T, F_COL, s)) <= 3 &&
-               !(s < P && FLD(T, F_TIME_ALIVE, s) < o->cfg.spawn_immunity);
-      ob[L.mask_attack_target + i] = ok ? 1.f : 0.f;
-    }
-    ob[L.mask_attack_target + N_OBS] = 1.f;
-    ob[L.mask_buy + 1024] = 1.f;
-    ob[L.mask_destroy + 12] = 1.f;
-    ob[L.mask_give_item + 12] = 1.f;
-    ob[L.mask_give_target + N_OBS] = 1.f;
-    ob[L.mask_givegold_target + N_OBS] = 1.f;
-    for (int d = 0; d < 5; d++)
-      ob[L.mask_move + d] = impassable(mat[(r + DR[d]) * SIZE + c + DC[d]]) ? 0.f : 1.f;
-    ob[L.mask_sell_item + 12] = 1.f;
-    ob[L.mask_use + 12] = 1.f;
+    compute_masks(o, e, p, vis, nv, mown, mslot, nm, m);
+    for (int k = 0; k < L.agent_id; k++) ob[k] = (float)m[k];
     ob[L.agent_id] = (float)FLD(T, F_ID, p);
     ob[L.current_tick] = (float)E[E_TICK];
     for (int i = 0; i < nv; i++)
       for (int f = 0; f < NMMO_N_ENTITY_COLS; f++)
         ob[L.entity + i * NMMO_N_ENTITY_COLS + f] = (float)FLD(T, f, vis[i]);
+    const uint32_t* inv = INVP(o, e, p);
+    for (int k = 0; k < INV && IT_TYPE(inv + 2 * k); k++)
+      item_row16(inv + 2 * k, FLD(T, F_ID, p), ob + L.inventory + 16 * k);
+    for (int j = 0; j < nm && j < 1024; j++)
+      item_row16(INVP(o, e, mown[j]) + 2 * mslot[j], FLD(T, F_ID, mown[j]), ob + L.market + 16 * j);
     for (int k = 0; k < o->cfg.task_embed_dim; k++) ob[L.task + k] = o->task[k];
     int w = 0;
     for (int dr = -VISION; dr <= VISION; dr++)
@@ -525,6 +793,14 @@ static void reset_outputs(Oracle* o, int e, float* rew, uint8_t* term, uint8_t* 
   }
 }
 
+static int acts(const int16_t* T, int S, int s) { return FLD(T, F_ALIVE, s) && FLD(T, F_HEALTH, s) > 0; }
+
+/* the item row an InventoryItem index of the previous observation refers to (-1: none) */
+static int decode_item(Oracle* o, int e, int p, int k) {
+  const uint32_t* inv = INVP(o, e, p);
+  return (k >= 0 && k < inv_count(inv)) ? IT_ROW(inv + 2 * k) : -1;
+}
+
 static void step_env(Oracle* o, int e, const int32_t* actions, float* obs, float* rew,
                      uint8_t* term, uint8_t* trunc, uint8_t* mask) {
   const int S = o->S, P = o->P;
@@ -540,20 +816,42 @@ static void step_env(Oracle* o, int e, const int32_t* actions, float* obs, float
     return;
   }
   const uint32_t tick = (uint32_t)E[E_TICK];
+  const int item = sys_on(o, NMMO_SYS_ITEM), exch = item && sys_on(o, NMMO_SYS_EXCHANGE);
+  const int prof = item && sys_on(o, NMMO_SYS_PROFESSION);
   int present[128], move_dir[512], atk_t[512], atk_s[512], vis[512];
+  int use_row[128], destroy_row[128], give_row[128], give_t[128], gg_t[128], gg_amt[128];
+  int sell_row[128], sell_price[128], buy_row[128];
+  int mown[INV * 128], mslot[INV * 128];
   for (int s = 0; s < S; s++) move_dir[s] = atk_t[s] = -1, atk_s[s] = 0;
-  for (int p = 0; p < P; p++) present[p] = FLD(T, F_ALIVE, p);
+  for (int p = 0; p < P; p++) {
+    present[p] = FLD(T, F_ALIVE, p);
+    use_row[p] = destroy_row[p] = give_row[p] = give_t[p] = gg_t[p] = sell_row[p] = buy_row[p] = -1;
+    gg_amt[p] = sell_price[p] = 0;
+  }
+  const int nm = exch ? market_list(o, e, mown, mslot) : 0;
 
   /* 0. Env._validate_actions: deserialize against the previous observation's state */
   for (int p = 0; p < P; p++) {
     if (!present[p]) continue;
     const int32_t* a = actions + ((size_t)e * P + p) * NMMO_N_ACTION_HEADS;
     if (a[8] >= 0 && a[8] < 5) move_dir[p] = a[8];
-    if (sys_on(o, NMMO_SYS_COMBAT) && a[0] >= 0 && a[0] < 3 && a[1] >= 0 && a[1] < N_OBS) {
-      int nv = visible_slots(o, e, p, vis);
-      if (nv > N_OBS) nv = N_OBS;
-      if (a[1] < nv) { atk_t[p] = vis[a[1]]; atk_s[p] = a[0]; }
+    int nv = visible_slots(o, e, p, vis);
+    if (nv > N_OBS) nv = N_OBS;
+    if (sys_on(o, NMMO_SYS_COMBAT) && a[0] >= 0 && a[0] < 3 && a[1] >= 0 && a[1] < nv) {
+      atk_t[p] = vis[a[1]];
+      atk_s[p] = a[0];
     }
+    if (!item) continue;
+    use_row[p] = decode_item(o, e, p, a[11]);
+    destroy_row[p] = decode_item(o, e, p, a[3]);
+    if (a[5] >= 0 && a[5] < nv) {
+      give_row[p] = decode_item(o, e, p, a[4]);
+      give_t[p] = give_row[p] >= 0 ? vis[a[5]] : -1;
+    }
+    if (!exch) continue;
+    if (a[7] >= 0 && a[7] < nv && a[6] >= 0 && a[6] < 99) { gg_t[p] = vis[a[7]]; gg_amt[p] = a[6] + 1; }
+    if (a[10] >= 0 && a[10] < 99) { sell_row[p] = decode_item(o, e, p, a[9]); sell_price[p] = a[10] + 1; }
+    if (a[2] >= 0 && a[2] < nm && a[2] < 1024) buy_row[p] = IT_ROW(INVP(o, e, mown[a[2]]) + 2 * mslot[a[2]]);
   }
   /* 1. npcs.actions */
   if (sys_on(o, NMMO_SYS_NPC))
@@ -570,32 +868,155 @@ static void step_env(Oracle* o, int e, const int32_t* actions, float* obs, float
       FLD(T, F_HEALTH, s) = (int16_t)(h > 100 ? 100 : h);
       continue;
     }
-    if (!sys_on(o, NMMO_SYS_RESOURCE)) continue;
-    int org = FLD(T, F_HEALTH, s), h = org;
-    if (FLD(T, F_FOOD, s) > 50 && FLD(T, F_WATER, s) > 50) h = h + 10 > 100 ? 100 : h + 10;
-    int dmg = FLD(T, F_RESILIENT, s) ? 5 : 10;
-    if (FLD(T, F_FOOD, s) == 0) h = h - dmg < 0 ? 0 : h - dmg;
-    if (FLD(T, F_WATER, s) == 0) h = h - dmg < 0 ? 0 : h - dmg;
-    FLD(T, F_HEALTH, s) = (int16_t)h;
-    FLD(T, F_HEALTH_RESTORE, s) = (int16_t)(h - org);
-    int r = FLD(T, F_ROW, s), c = FLD(T, F_COL, s);
-    int fd = FLD(T, F_FOOD, s) - 5;
-    FLD(T, F_FOOD, s) = (int16_t)(fd < 0 ? 0 : fd);
-    if (mat[r * SIZE + c] == M_FOILAGE) { /* Food.update -> harvest (depletes) */
-      FLD(T, F_FOOD, s) = 100;
-      mat[r * SIZE + c] = M_SCRUB;
+    int r = FLD(T, F_ROW, s), c = FLD(T, F_COL, s), tile = r * SIZE + c;
+    if (sys_on(o, NMMO_SYS_RESOURCE)) {
+      int org = FLD(T, F_HEALTH, s), h = org;
+      if (FLD(T, F_FOOD, s) > 50 && FLD(T, F_WATER, s) > 50) h = h + 10 > 100 ? 100 : h + 10;
+      int dmg = FLD(T, F_RESILIENT, s) ? 5 : 10;
+      if (FLD(T, F_FOOD, s) == 0) h = h - dmg < 0 ? 0 : h - dmg;
+      if (FLD(T, F_WATER, s) == 0) h = h - dmg < 0 ? 0 : h - dmg;
+      FLD(T, F_HEALTH, s) = (int16_t)h;
+      FLD(T, F_HEALTH_RESTORE, s) = (int16_t)(h - org);
+      int fd = FLD(T, F_FOOD, s) - 5;
+      FLD(T, F_FOOD, s) = (int16_t)(fd < 0 ? 0 : fd);
+      if (mat[tile] == M_FOILAGE) { /* Food.update -> harvest (depletes) */
+        FLD(T, F_FOOD, s) = 100;
+        mat[tile] = M_SCRUB;
+      }
+      int wt = FLD(T, F_WATER, s) - 5;
+      FLD(T, F_WATER, s) = (int16_t)(wt < 0 ? 0 : wt);
+      if (mat[tile - SIZE] == M_WATER || mat[tile + SIZE] == M_WATER ||
+          mat[tile - 1] == M_WATER || mat[tile + 1] == M_WATER)
+        FLD(T, F_WATER, s) = 100;
     }
-    int wt = FLD(T, F_WATER, s) - 5;
-    FLD(T, F_WATER, s) = (int16_t)(wt < 0 ? 0 : wt);
-    if (mat[(r - 1) * SIZE + c] == M_WATER || mat[(r + 1) * SIZE + c] == M_WATER ||
-        mat[r * SIZE + c - 1] == M_WATER || mat[r * SIZE + c + 1] == M_WATER)
-      FLD(T, F_WATER, s) = 100;
+    if (prof) { /* fishing, herbalism, prospecting, carving, alchemy (SPEC §9) */
+      const uint32_t* inv = INVP(o, e, s);
+      int held = -1, held_lvl = 1;
+      for (int k = 0; k < INV && IT_TYPE(inv + 2 * k); k++)
+        if (IT_EQUIPPED(inv + 2 * k) && equip_slot(IT_TYPE(inv + 2 * k)) == 3) {
+          held = IT_TYPE(inv + 2 * k);
+          held_lvl = IT_LEVEL(inv + 2 * k);
+        }
+      int nb[4] = {tile - SIZE, tile + SIZE, tile - 1, tile + 1}, got = 0;
+      for (int q = 0; q < 4; q++)
+        if (mat[nb[q]] == M_FISH) { mat[nb[q]] = M_OCEAN; got = 1; }
+      if (got) {
+        int lvl = held == T_ROD ? held_lvl : 1;
+        receive_new(o, e, s, T_RATION, lvl);
+        add_skill_exp(T, S, s, F_FISHING_EXP, 30 * lvl);
+      }
+      static const int from[4] = {M_HERB, M_ORE, M_TREE, M_CRYSTAL};
+      static const int to[4] = {M_WEEDS, M_SLAG, M_STUMP, M_FRAGMENT};
+      static const int out[4] = {T_POTION, T_WHETSTONE, T_ARROW, T_RUNES};
+      static const int tool[4] = {T_GLOVES, T_PICKAXE, T_AXE, T_CHISEL};
+      static const int fexp[4] = {F_HERBALISM_EXP, F_PROSPECTING_EXP, F_CARVING_EXP, F_ALCHEMY_EXP};
+      for (int q = 0; q < 4; q++) {
+        if (mat[tile] != from[q]) continue;
+        mat[tile] = (uint8_t)to[q];
+        int lvl = held == tool[q] ? held_lvl : 1;
+        receive_new(o, e, s, out[q], lvl);
+        add_skill_exp(T, S, s, fexp[q], (q == 0 ? 30 : 15) * lvl);
+      }
+    }
   }
-  /* 3. actions by priority: Attack (50) then Move (60), slot order */
-  for (int s = 0; s < P + E[E_NPC_COUNT]; s++)
+  /* 3. actions by priority, slot order (Buy: shuffled) */
+  for (int p = 0; p < P && item; p++) { /* Use (10) */
+    if (use_row[p] < 0 || !acts(T, S, p)) continue;
+    uint32_t* inv = INVP(o, e, p);
+    int k = inv_find(inv, use_row[p]);
+    if (k < 0 || IT_PRICE(inv + 2 * k)) continue;
+    uint32_t* it = inv + 2 * k;
+    int type = IT_TYPE(it), lvl = IT_LEVEL(it), slot = equip_slot(type);
+    if (slot >= 0) {
+      if (IT_EQUIPPED(it)) it[0] &= ~(1u << 9);
+      else if (lvl <= requirement_level(T, S, p, type)) {
+        for (int j = 0; j < INV && IT_TYPE(inv + 2 * j); j++)
+          if (IT_EQUIPPED(inv + 2 * j) && equip_slot(IT_TYPE(inv + 2 * j)) == slot) inv[2 * j] &= ~(1u << 9);
+        it[0] |= 1u << 9;
+      }
+      update_item_level(o, e, p);
+    } else if (lvl <= requirement_level(T, S, p, type)) {
+      int rs = 50 + 5 * lvl;
+      if (type == T_RATION) {
+        FLD(T, F_FOOD, p) = (int16_t)(FLD(T, F_FOOD, p) + rs > 100 ? 100 : FLD(T, F_FOOD, p) + rs);
+        FLD(T, F_WATER, p) = (int16_t)(FLD(T, F_WATER, p) + rs > 100 ? 100 : FLD(T, F_WATER, p) + rs);
+      } else {
+        FLD(T, F_HEALTH, p) = (int16_t)(FLD(T, F_HEALTH, p) + rs > 100 ? 100 : FLD(T, F_HEALTH, p) + rs);
+      }
+      it[1] -= 1;
+      if (IT_QTY(it) == 0) { free_item_row(o, e, IT_ROW(it)); inv_remove(inv, k); }
+    }
+  }
+  if (exch) { /* Buy (20): players in shuffled order */
+    int order[128], key[128], n = 0;
+    for (int p = 0; p < P; p++) {
+      if (buy_row[p] < 0) continue;
+      uint32_t u[4];
+      draw(env_seed(E), tick, P_BUY_ORDER, (uint32_t)(p + 1), 0, u);
+      int j = n++;
+      while (j > 0 && ((uint32_t)key[j - 1] > u[0] || ((uint32_t)key[j - 1] == u[0] && order[j - 1] > p))) {
+        key[j] = key[j - 1]; order[j] = order[j - 1]; j--;
+      }
+      key[j] = (int)u[0]; order[j] = p;
+    }
+    for (int i = 0; i < n; i++) {
+      int b = order[i];
+      if (!acts(T, S, b)) continue;
+      int owner = -1, k = -1;
+      for (int q = 0; q < P && owner < 0; q++) {
+        int kk = inv_find(INVP(o, e, q), buy_row[b]);
+        if (kk >= 0) { owner = q; k = kk; }
+      }
+      if (owner < 0 || owner == b) continue;
+      uint32_t* it = INVP(o, e, owner) + 2 * k;
+      int price = IT_PRICE(it);
+      if (!price || FLD(T, F_GOLD, b) < price || !has_room(o, e, b, it)) continue;
+      FLD(T, F_GOLD, b) = (int16_t)(FLD(T, F_GOLD, b) - price);
+      FLD(T, F_GOLD, owner) = (int16_t)(FLD(T, F_GOLD, owner) + price);
+      uint32_t w0 = it[0] & 0x1FFu, w1 = it[1];
+      inv_remove(INVP(o, e, owner), k);
+      receive_moved(o, e, b, w0, w1);
+    }
+  }
+  for (int p = 0; p < P && item; p++) { /* Give, GiveGold (30) */
+    if (!acts(T, S, p)) continue;
+    int t = give_t[p];
+    if (give_row[p] >= 0 && t >= 0 && t < P && t != p && acts(T, S, t) &&
+        FLD(T, F_ROW, t) == FLD(T, F_ROW, p) && FLD(T, F_COL, t) == FLD(T, F_COL, p)) {
+      uint32_t* inv = INVP(o, e, p);
+      int k = inv_find(inv, give_row[p]);
+      if (k >= 0 && !IT_EQUIPPED(inv + 2 * k) && !IT_PRICE(inv + 2 * k) && has_room(o, e, t, inv + 2 * k)) {
+        uint32_t w0 = inv[2 * k], w1 = inv[2 * k + 1];
+        inv_remove(inv, k);
+        receive_moved(o, e, t, w0, w1);
+      }
+    }
+    t = gg_t[p];
+    if (exch && t >= 0 && t < P && t != p && acts(T, S, t) && gg_amt[p] <= FLD(T, F_GOLD, p) &&
+        FLD(T, F_ROW, t) == FLD(T, F_ROW, p) && FLD(T, F_COL, t) == FLD(T, F_COL, p)) {
+      FLD(T, F_GOLD, p) = (int16_t)(FLD(T, F_GOLD, p) - gg_amt[p]);
+      FLD(T, F_GOLD, t) = (int16_t)(FLD(T, F_GOLD, t) + gg_amt[p]);
+    }
+  }
+  for (int p = 0; p < P && item; p++) { /* Destroy (40) */
+    if (destroy_row[p] < 0 || !acts(T, S, p)) continue;
+    uint32_t* inv = INVP(o, e, p);
+    int k = inv_find(inv, destroy_row[p]);
+    if (k < 0 || IT_EQUIPPED(inv + 2 * k) || IT_PRICE(inv + 2 * k)) continue;
+    free_item_row(o, e, IT_ROW(inv + 2 * k));
+    inv_remove(inv, k);
+  }
+  for (int s = 0; s < P + E[E_NPC_COUNT]; s++) /* Attack (50) */
     if (atk_t[s] >= 0) attack_call(o, e, s, atk_s[s], atk_t[s]);
-  for (int s = 0; s < P + E[E_NPC_COUNT]; s++)
+  for (int s = 0; s < P + E[E_NPC_COUNT]; s++) /* Move (60) */
     if (move_dir[s] >= 0) move_call(o, e, s, move_dir[s]);
+  for (int p = 0; p < P && exch; p++) { /* Sell (70) */
+    if (sell_row[p] < 0 || !acts(T, S, p)) continue;
+    uint32_t* inv = INVP(o, e, p);
+    int k = inv_find(inv, sell_row[p]);
+    if (k < 0 || IT_EQUIPPED(inv + 2 * k)) continue;
+    inv[2 * k] = (inv[2 * k] & 0x3FFu) | ((uint32_t)sell_price[p] << 10) | (tick << 17);
+  }
   /* 4. cull (players then NPCs), rows appended to the free ring; compact NPC slots */
   int16_t* ring = o->ring + (size_t)e * S;
   int died[128] = {0};
@@ -609,6 +1030,12 @@ static void step_env(Oracle* o, int e, const int32_t* actions, float* obs, float
       FLD(T, F_DIED_TICK, s) = (int16_t)(tick + 1);
       E[E_PLAYERS_ALIVE]--;
     }
+  }
+  for (int p = 0; p < P && item; p++) { /* unlooted items of the dead are destroyed */
+    if (!died[p]) continue;
+    uint32_t* inv = INVP(o, e, p);
+    while (IT_TYPE(inv)) { free_item_row(o, e, IT_ROW(inv)); inv_remove(inv, 0); }
+    FLD(T, F_ITEM_LEVEL, p) = 0;
   }
   int w = P;
   for (int s = P; s < P + E[E_NPC_COUNT]; s++) {
@@ -629,6 +1056,12 @@ static void step_env(Oracle* o, int e, const int32_t* actions, float* obs, float
     uint32_t u[4];
     draw(env_seed(E), tick + 1, P_RESPAWN, (uint32_t)(t >> 2), 0, u);  /* one draw per 4 tiles */
     if (u[t & 3] < respawn_u32(base[t])) mat[t] = base[t];
+  }
+  /* exchange.step: listings older than 5 ticks expire */
+  for (int p = 0; p < P && exch; p++) {
+    uint32_t* inv = INVP(o, e, p);
+    for (int k = 0; k < INV && IT_TYPE(inv + 2 * k); k++)
+      if (IT_PRICE(inv + 2 * k) && (int)(tick + 1) - IT_LTICK(inv + 2 * k) > 5) inv[2 * k] &= 0x3FFu;
   }
   /* 7. NPC refill */
   if (sys_on(o, NMMO_SYS_NPC)) npc_spawn(o, e, tick + 1);
@@ -652,45 +1085,35 @@ static void step_env(Oracle* o, int e, const int32_t* actions, float* obs, float
   write_obs(o, e, obs_env);
 }
 
-/* ------------------------------------------------------------------ scripted policy (SPEC §9) */
+/* ------------------------------------------------------------------ scripted policy (SPEC §10) */
 static void scripted_env(Oracle* o, int e, uint64_t pseed, int32_t* actions) {
+  static const int seg_off[12] = {0, 3, 104, 1129, 1142, 1155, 1256, 1355, 1456, 1461, 1474, 1573};
+  static const int seg_len[12] = {3, 101, 1025, 13, 13, 101, 99, 101, 5, 13, 99, 13};
   const int S = o->S, P = o->P;
   const int16_t* T = ENT(o, e);
   const int32_t* E = ENV(o, e);
-  const uint8_t* mat = o->mat + (size_t)e * NMMO_MAP_TILES;
-  int vis[512];
+  int vis[512], mown[INV * 128], mslot[INV * 128];
+  int8_t m[1586];
+  int nm = market_list(o, e, mown, mslot);
   for (int p = 0; p < P; p++) {
     int32_t* a = actions + ((size_t)e * P + p) * NMMO_N_ACTION_HEADS;
     for (int h = 0; h < NMMO_N_ACTION_HEADS; h++) a[h] = 0;
     if (!FLD(T, F_ALIVE, p)) continue;
+    int nv = visible_slots(o, e, p, vis);
+    if (nv > N_OBS) nv = N_OBS;
+    compute_masks(o, e, p, vis, nv, mown, mslot, nm, m);
     uint32_t ctr[4] = {(uint32_t)E[E_TICK] + 2048u * (uint32_t)E[E_EPISODE],
                        (uint32_t)E[E_ENV_INDEX], (uint32_t)p, 0}, u[4];
-    int r = FLD(T, F_ROW, p), c = FLD(T, F_COL, p);
-    a[1] = N_OBS; a[2] = 1024; a[3] = 12; a[4] = 12; a[5] = N_OBS; a[6] = 0; a[7] = N_OBS;
-    a[9] = 12; a[10] = 0; a[11] = 12;
-    if (sys_on(o, NMMO_SYS_COMBAT)) {
-      ctr[3] = 0;
+    for (int h = 0; h < NMMO_N_ACTION_HEADS; h++) { /* uniform over the head's set mask bits */
+      int n = 0;
+      for (int k = 0; k < seg_len[h]; k++) n += m[seg_off[h] + k];
+      if (n == 0) continue;
+      ctr[3] = (uint32_t)h;
       philox(ctr, (uint32_t)pseed, (uint32_t)(pseed >> 32), u);
-      a[0] = (int32_t)U(u[0], 3);
-      int nv = visible_slots(o, e, p, vis), bits[N_OBS + 1], nb = 0;
-      if (nv > N_OBS) nv = N_OBS;
-      for (int i = 0; i < nv; i++) {
-        int s = vis[i];
-        if (s != p && linf(r, c, FLD(T, F_ROW, s), FLD(T, F_COL, s)) <= 3 &&
-            !(s < P && FLD(T, F_TIME_ALIVE, s) < o->cfg.spawn_immunity))
-          bits[nb++] = i;
-      }
-      bits[nb++] = N_OBS;
-      ctr[3] = 1;
-      philox(ctr, (uint32_t)pseed, (uint32_t)(pseed >> 32), u);
-      a[1] = bits[U(u[0], (uint32_t)nb)];
+      int pick = (int)U(u[0], (uint32_t)n);
+      for (int k = 0; k < seg_len[h]; k++)
+        if (m[seg_off[h] + k] && pick-- == 0) { a[h] = k; break; }
     }
-    int mv[5], nm = 0;
-    for (int d = 0; d < 5; d++)
-      if (!impassable(mat[(r + DR[d]) * SIZE + c + DC[d]])) mv[nm++] = d;
-    ctr[3] = 8;
-    philox(ctr, (uint32_t)pseed, (uint32_t)(pseed >> 32), u);
-    a[8] = mv[U(u[0], (uint32_t)nm)];
   }
 }
 
@@ -703,8 +1126,9 @@ EXPORT int oracle_flat_offsets(int task_dim, int32_t* out /* [20] */) {
   memcpy(out, &L, sizeof(L));
   return (int)(sizeof(L) / sizeof(int));
 }
-EXPORT size_t oracle_state_bytes_per_env(int slots) {
-  return NMMO_NE * 4 + (size_t)NMMO_NF * slots * 2 + (size_t)slots * 2 + NMMO_MAP_TILES;
+EXPORT size_t oracle_state_bytes_per_env(int slots, int players) {
+  return NMMO_NE * 4 + (size_t)NMMO_NF * slots * 2 + (size_t)slots * 2 + NMMO_MAP_TILES +
+         (size_t)players * INV * 8 + (size_t)INV * players * 2;
 }
 
 EXPORT void* oracle_create(const NmmoConfig* cfg, int n_envs, uint64_t seed,
@@ -724,6 +1148,8 @@ EXPORT void* oracle_create(const NmmoConfig* cfg, int n_envs, uint64_t seed,
   o->ring = (int16_t*)calloc((size_t)n_envs * o->S, 2);
   o->mat = (uint8_t*)calloc((size_t)n_envs * NMMO_MAP_TILES, 1);
   o->bank = (uint8_t*)malloc((size_t)cfg->map_n * NMMO_MAP_TILES);
+  o->items = (uint32_t*)calloc((size_t)n_envs * o->P * INV * 2, 4);
+  o->iring = (int16_t*)calloc((size_t)n_envs * INV * o->P, 2);
   for (int m = 0; m < cfg->map_n; m++)
     generate_map(cfg->map_seed, (uint32_t)m, o->bank + (size_t)m * NMMO_MAP_TILES);
   for (int k = 0; k < cfg->task_embed_dim; k++) o->task[k] = task_emb ? half_to_float(task_emb[k]) : 0.f;
@@ -733,7 +1159,8 @@ EXPORT void* oracle_create(const NmmoConfig* cfg, int n_envs, uint64_t seed,
 EXPORT void oracle_destroy(void* h) {
   Oracle* o = (Oracle*)h;
   if (!o) return;
-  free(o->env); free(o->ent); free(o->ring); free(o->mat); free(o->bank); free(o);
+  free(o->env); free(o->ent); free(o->ring); free(o->mat); free(o->bank);
+  free(o->items); free(o->iring); free(o);
 }
 
 EXPORT int oracle_reset(void* h, const uint64_t* env_seeds, float* obs, uint8_t* mask) {
@@ -773,7 +1200,7 @@ EXPORT int oracle_scripted_actions(void* h, uint64_t pseed, int32_t* actions) {
 
 EXPORT int oracle_get_state(void* h, void* buf, size_t nbytes) {
   Oracle* o = (Oracle*)h;
-  size_t per = oracle_state_bytes_per_env(o->S);
+  size_t per = oracle_state_bytes_per_env(o->S, o->P);
   if (nbytes != per * (size_t)o->n_envs) return NMMO_E_SIZE;
   uint8_t* b = (uint8_t*)buf;
   for (int e = 0; e < o->n_envs; e++) {
@@ -781,12 +1208,14 @@ EXPORT int oracle_get_state(void* h, void* buf, size_t nbytes) {
     memcpy(b, ENT(o, e), (size_t)NMMO_NF * o->S * 2); b += (size_t)NMMO_NF * o->S * 2;
     memcpy(b, o->ring + (size_t)e * o->S, (size_t)o->S * 2); b += (size_t)o->S * 2;
     memcpy(b, o->mat + (size_t)e * NMMO_MAP_TILES, NMMO_MAP_TILES); b += NMMO_MAP_TILES;
+    memcpy(b, INVP(o, e, 0), (size_t)o->P * INV * 8); b += (size_t)o->P * INV * 8;
+    memcpy(b, o->iring + (size_t)e * INV * o->P, (size_t)INV * o->P * 2); b += (size_t)INV * o->P * 2;
   }
   return 0;
 }
 EXPORT int oracle_set_state(void* h, const void* buf, size_t nbytes) {
   Oracle* o = (Oracle*)h;
-  size_t per = oracle_state_bytes_per_env(o->S);
+  size_t per = oracle_state_bytes_per_env(o->S, o->P);
   if (nbytes != per * (size_t)o->n_envs) return NMMO_E_SIZE;
   const uint8_t* b = (const uint8_t*)buf;
   for (int e = 0; e < o->n_envs; e++) {
@@ -794,6 +1223,8 @@ EXPORT int oracle_set_state(void* h, const void* buf, size_t nbytes) {
     memcpy(ENT(o, e), b, (size_t)NMMO_NF * o->S * 2); b += (size_t)NMMO_NF * o->S * 2;
     memcpy(o->ring + (size_t)e * o->S, b, (size_t)o->S * 2); b += (size_t)o->S * 2;
     memcpy(o->mat + (size_t)e * NMMO_MAP_TILES, b, NMMO_MAP_TILES); b += NMMO_MAP_TILES;
+    memcpy(INVP(o, e, 0), b, (size_t)o->P * INV * 8); b += (size_t)o->P * INV * 8;
+    memcpy(o->iring + (size_t)e * INV * o->P, b, (size_t)INV * o->P * 2); b += (size_t)INV * o->P * 2;
   }
   return 0;
 }

@@ -46,7 +46,7 @@ def lib():
         L.oracle_obs_elems.argtypes = [i32]
         L.oracle_flat_offsets.argtypes = [i32, vp]
         L.oracle_state_bytes_per_env.restype = sz
-        L.oracle_state_bytes_per_env.argtypes = [i32]
+        L.oracle_state_bytes_per_env.argtypes = [i32, i32]
         _lib = L
     return _lib
 
@@ -103,7 +103,7 @@ class OracleEnvs:
         return out
 
     def get_state(self) -> np.ndarray:
-        n = lib().oracle_state_bytes_per_env(self.S) * self.n_envs
+        n = lib().oracle_state_bytes_per_env(self.S, self.P) * self.n_envs
         buf = np.zeros(n, np.uint8)
         rc = lib().oracle_get_state(self.h, _p(buf), n)
         assert rc == 0, rc
@@ -121,17 +121,22 @@ class OracleEnvs:
         return buf
 
 
-def split_state(buf: np.ndarray, n_envs: int, slots: int) -> dict:
-    """View a state blob as named arrays (env [n,NE] i32, ent [n,NF,S] i16, ring, mat)."""
-    per = abi.state_bytes_per_env(slots)
+def split_state(buf: np.ndarray, n_envs: int, slots: int, players: int = 128) -> dict:
+    """View a state blob as named arrays (env [n,NE] i32, ent [n,NF,S] i16, ring, mat,
+    items [n,P,12,2] u32, iring [n,12P] i16)."""
+    per = abi.state_bytes_per_env(slots, players)
     b = buf.reshape(n_envs, per)
     o = 0
     env = b[:, o:o + abi.NE * 4].copy().view(np.int32); o += abi.NE * 4
     ent = b[:, o:o + abi.NF * slots * 2].copy().view(np.int16).reshape(n_envs, abi.NF, slots)
     o += abi.NF * slots * 2
     ring = b[:, o:o + slots * 2].copy().view(np.int16); o += slots * 2
-    mat = b[:, o:o + abi.MAP_TILES].reshape(n_envs, abi.MAP_SIZE, abi.MAP_SIZE)
-    return {"env": env, "ent": ent, "ring": ring, "mat": mat}
+    mat = b[:, o:o + abi.MAP_TILES].reshape(n_envs, abi.MAP_SIZE, abi.MAP_SIZE); o += abi.MAP_TILES
+    ni = players * abi.INV_SLOTS
+    items = b[:, o:o + ni * 8].copy().view(np.uint32).reshape(n_envs, players, abi.INV_SLOTS, 2)
+    o += ni * 8
+    iring = b[:, o:o + ni * 2].copy().view(np.int16)
+    return {"env": env, "ent": ent, "ring": ring, "mat": mat, "items": items, "iring": iring}
 
 
 def join_state(d: dict) -> np.ndarray:
@@ -142,5 +147,7 @@ def join_state(d: dict) -> np.ndarray:
         parts += [np.ascontiguousarray(d["env"][e], np.int32).view(np.uint8),
                   np.ascontiguousarray(d["ent"][e], np.int16).reshape(-1).view(np.uint8),
                   np.ascontiguousarray(d["ring"][e], np.int16).view(np.uint8),
-                  np.ascontiguousarray(d["mat"][e], np.uint8).reshape(-1)]
+                  np.ascontiguousarray(d["mat"][e], np.uint8).reshape(-1),
+                  np.ascontiguousarray(d["items"][e], np.uint32).reshape(-1).view(np.uint8),
+                  np.ascontiguousarray(d["iring"][e], np.int16).view(np.uint8)]
     return np.concatenate(parts)

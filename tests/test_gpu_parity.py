@@ -20,10 +20,10 @@ def _engine(cfg, n_envs, seed, task=None):
     return NmmoEngine(cfg, n_envs, seed=seed, task_embedding=task)
 
 
-def _cmp_state(ga, oa, n, S, where):
-    g = split_state(ga, n, S)
-    o = split_state(oa, n, S)
-    for key in ("env", "ring", "mat"):
+def _cmp_state(ga, oa, n, S, where, P=128):
+    g = split_state(ga, n, S, P)
+    o = split_state(oa, n, S, P)
+    for key in ("env", "ring", "mat", "items", "iring"):
         if not np.array_equal(g[key], o[key]):
             bad = np.argwhere(g[key] != o[key])[:5]
             raise AssertionError(f"{where}: {key} differs at {bad.tolist()}")

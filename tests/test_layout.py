@@ -121,7 +121,7 @@ def rollout():
 def test_obs_tile_window(rollout):
     o, _ = rollout
     d = layout.unflatten(o.obs)
-    st = split_state(o.get_state(), o.n_envs, o.S)
+    st = split_state(o.get_state(), o.n_envs, o.S, o.P)
     tile = d["Tile"]
     for e in range(o.n_envs):
         for p in range(o.P):
@@ -178,7 +178,7 @@ def test_obs_task_is_heldout_embedding(rollout):
 
 def test_ids_and_materials(rollout):
     o, _ = rollout
-    st = split_state(o.get_state(), o.n_envs, o.S)
+    st = split_state(o.get_state(), o.n_envs, o.S, o.P)
     ids = st["ent"][:, abi.F["id"]]
     assert np.array_equal(ids[:, :128], np.tile(np.arange(1, 129), (o.n_envs, 1)))  # train_helper.py:147
     npc = ids[:, 128:]

@@ -16,18 +16,18 @@ def make(systems, P=4, seed=3):
     cfg = Config(systems=systems, PLAYER_N=P, MAP_N=1, early_stop_agent_num=0)
     o = OracleEnvs(cfg, 1, seed=seed)
     o.reset()
-    return o, split_state(o.get_state(), 1, o.S)
+    return o, split_state(o.get_state(), 1, o.S, o.P)
 
 
 def put(o, d):
     o.set_state(join_state(d))
 
 
+NOOP = [0, 100, 1024, 12, 12, 100, 0, 100, 4, 12, 0, 12]  # last index of every target/item head
+
+
 def noop_actions(o):
-    a = np.zeros((1, o.P, 12), np.int32)
-    a[..., 1] = 100  # Attack.Target noop
-    a[..., 8] = 4    # Stay
-    return a
+    return np.tile(np.array(NOOP, np.int32), (1, o.P, 1))
 
 
 def find_tile(mat, pred, avoid=()):
@@ -82,7 +82,7 @@ def test_starvation_and_dehydration():
           food=0, water=0, health=50, resilient=1)
     put(o, d)
     o.step(noop_actions(o))
-    s = split_state(o.get_state(), 1, o.S)["ent"][0]
+    s = split_state(o.get_state(), 1, o.S, o.P)["ent"][0]
     assert s[F["health"], 0] == 30 and s[F["health_restore"], 0] == -20  # 10 + 10
     assert s[F["health"], 1] == 40  # resilient: int(10 * 0.5) each
     assert s[F["food"], 0] == 0 and s[F["water"], 0] == 0
@@ -95,7 +95,7 @@ def test_regen_and_depletion():
     place(d, 0, *find_tile(mat, plain), food=60, water=60, health=50)
     put(o, d)
     o.step(noop_actions(o))
-    s = split_state(o.get_state(), 1, o.S)["ent"][0]
+    s = split_state(o.get_state(), 1, o.S, o.P)["ent"][0]
     assert (s[F["health"], 0], s[F["food"], 0], s[F["water"], 0]) == (60, 55, 55)
 
 
@@ -108,7 +108,7 @@ def test_first_player_on_foilage_eats():
     place(d, 1, r, c, food=40, water=40)
     put(o, d)
     o.step(noop_actions(o))
-    s = split_state(o.get_state(), 1, o.S)
+    s = split_state(o.get_state(), 1, o.S, o.P)
     assert s["ent"][0][F["food"], 0] == 100  # slot 0 harvests
     assert s["ent"][0][F["food"], 1] == 35   # slot 1 sees Scrub
     assert s["mat"][0][r, c] in (SCRUB, FOILAGE)  # Scrub unless the 2.5 % respawn fired
@@ -121,7 +121,7 @@ def test_drink_adjacent_water():
     place(d, 0, *find_tile(mat, lambda m, r, c: m[r, c] == GRASS and WATER in nbrs(m, r, c)), water=10)
     put(o, d)
     o.step(noop_actions(o))
-    assert split_state(o.get_state(), 1, o.S)["ent"][0][F["water"], 0] == 100
+    assert split_state(o.get_state(), 1, o.S, o.P)["ent"][0][F["water"], 0] == 100
 
 
 COMBAT = ("Resource", "Combat", "Progression")
@@ -140,7 +140,7 @@ def duel(dist=2, t_fields=None, style=0, both_attack=False, x_fields=None):
     if both_attack:
         a[0, 1, 0], a[0, 1, 1] = 0, visible_index(d, 1, 0)
     o.step(a)
-    return o, split_state(o.get_state(), 1, o.S)
+    return o, split_state(o.get_state(), 1, o.S, o.P)
 
 
 def test_melee_damage_equal_skills():
@@ -203,11 +203,11 @@ def test_move_blocked_by_stone():
     a = noop_actions(o)
     a[0, 0, 8] = 0  # North into stone
     o.step(a)
-    ent = split_state(o.get_state(), 1, o.S)["ent"][0]
+    ent = split_state(o.get_state(), 1, o.S, o.P)["ent"][0]
     assert (ent[F["row"], 0], ent[F["col"], 0]) == (r, c)
     a[0, 0, 8] = 1  # South onto grass
     o.step(a)
-    ent = split_state(o.get_state(), 1, o.S)["ent"][0]
+    ent = split_state(o.get_state(), 1, o.S, o.P)["ent"][0]
     assert (ent[F["row"], 0], ent[F["col"], 0]) == (r + 1, c)
 
 
@@ -216,11 +216,11 @@ def test_horizon_truncation_then_auto_reset():
     d["env"][0, E["tick"]] = 1023
     put(o, d)
     o.step(noop_actions(o))
-    env = split_state(o.get_state(), 1, o.S)["env"][0]
+    env = split_state(o.get_state(), 1, o.S, o.P)["env"][0]
     assert env[E["done"]] == 1 and env[E["tick"]] == 1024
     assert o.trunc[0].sum() == o.P
     o.step(noop_actions(o))  # pufferlib auto-reset
-    env = split_state(o.get_state(), 1, o.S)["env"][0]
+    env = split_state(o.get_state(), 1, o.S, o.P)["env"][0]
     assert env[E["tick"]] == 0 and env[E["episode"]] == 1 and env[E["done"]] == 0
     assert o.mask[0].sum() == o.P and o.rew[0].sum() == 0
 
@@ -231,7 +231,7 @@ def test_npc_bookkeeping_invariants():
     o.reset()
     for t in range(80):
         o.step(o.scripted_actions(t))
-        s = split_state(o.get_state(), 3, o.S)
+        s = split_state(o.get_state(), 3, o.S, o.P)
         for e in range(3):
             ent, env, ring = s["ent"][e], s["env"][e], s["ring"][e]
             alive = ent[F["alive"]] == 1
@@ -268,3 +268,117 @@ def test_golden_rollout_hashes(preset):
 
     golden = json.load(open("tests/golden/rollout_hashes.json"))[preset]
     assert rollout_hashes(preset) == golden
+
+
+# ---------------------------------------------------------------- items (SPEC §9)
+ITEMS = ("Resource", "Combat", "Progression", "Item", "Equipment", "Profession", "Exchange")
+ORE, SLAG = 7, 6
+
+
+def item_words(typ, level=1, qty=1, row=1, equipped=0, price=0, ltick=0):
+    return [typ | (level << 5) | (equipped << 9) | (price << 10) | (ltick << 17), qty | (row << 16)]
+
+
+def give_item(d, p, k, words):
+    d["items"][0, p, k] = words
+    # take the row out of the free ring (rows 1..12P start in order; use the last ones)
+
+
+def test_harvest_ore_without_tool():
+    o, d = make(ITEMS)
+    mat = d["mat"][0]
+    r, c = find_tile(mat, lambda m, r, c: m[r, c] in (GRASS, SCRUB) and WATER not in nbrs(m, r, c))
+    d["mat"][0][r, c] = ORE
+    park_others(d, {0}, mat)
+    place(d, 0, r, c)
+    put(o, d)
+    o.step(noop_actions(o))
+    s = split_state(o.get_state(), 1, o.S, o.P)
+    it = s["items"][0, 0, 0]
+    assert (it[0] & 31, (it[0] >> 5) & 15, it[1] & 0xFFFF) == (13, 1, 1)  # Whetstone L1 x1
+    assert it[1] >> 16 == 1  # first row of the FIFO ring
+    assert s["ent"][0][F["prospecting_exp"], 0] == 15
+    assert s["mat"][0][r, c] in (SLAG, ORE)  # depleted (unless the 10 % respawn fired)
+    assert s["env"][0, E["item_free_count"]] == 12 * o.P - 1
+
+
+def _with_item(words, slot=0, **fields):
+    o, d = make(ITEMS)
+    mat = d["mat"][0]
+    park_others(d, {0}, mat)
+    place(d, 0, *find_tile(mat, plain), **fields)
+    row = words[1] >> 16
+    d["items"][0, 0, slot] = words
+    ring = d["iring"][0]
+    # remove `row` from the free ring: rows are 1..12P in order, head 0
+    keep = [x for x in ring if x != row]
+    d["iring"][0] = keep + [0]
+    d["env"][0, E["item_free_count"]] -= 1
+    put(o, d)
+    return o, d
+
+
+def test_use_ration_restores_food_and_water():
+    o, d = _with_item(item_words(16, level=1, row=7), food=20, water=30, health=100)
+    a = noop_actions(o)
+    a[0, 0, 11] = 0  # Use.InventoryItem 0
+    o.step(a)
+    s = split_state(o.get_state(), 1, o.S, o.P)
+    # update first: 20-5, 30-5; then +55 each (50 + 5*1)
+    assert (s["ent"][0][F["food"], 0], s["ent"][0][F["water"], 0]) == (70, 80)
+    assert s["items"][0, 0, 0, 0] == 0  # consumed
+    ring, env = s["iring"][0], s["env"][0]
+    assert ring[(env[E["item_free_head"]] + env[E["item_free_count"]] - 1) % (12 * o.P)] == 7
+
+
+def test_equip_weapon_adds_offense():
+    o, d = _with_item(item_words(5, level=1, row=3), time_alive=50)  # Spear L1: +10 melee attack
+    a = noop_actions(o)
+    a[0, 0, 11] = 0
+    o.step(a)
+    s = split_state(o.get_state(), 1, o.S, o.P)
+    assert (s["items"][0, 0, 0, 0] >> 9) & 1 == 1 and s["ent"][0][F["item_level"], 0] == 1
+    # now attack a player 2 tiles away: offense 15 + 10 = 25, defense 5 -> 20
+    d = split_state(o.get_state(), 1, o.S, o.P)
+    r, c = d["ent"][0][F["row"], 0], d["ent"][0][F["col"], 0]
+    place(d, 1, r, c + 2, time_alive=50)
+    put(o, d)
+    a = noop_actions(o)
+    a[0, 0, 0], a[0, 0, 1] = 0, visible_index(d, 0, 1)
+    o.step(a)
+    s = split_state(o.get_state(), 1, o.S, o.P)
+    assert s["ent"][0][F["damage"], 1] == 20
+
+
+def test_sell_then_buy_moves_gold_and_item():
+    o, d = _with_item(item_words(2, level=1, row=9), gold=0)  # a Hat
+    d = split_state(o.get_state(), 1, o.S, o.P)
+    r, c = d["ent"][0][F["row"], 0], d["ent"][0][F["col"], 0]
+    place(d, 1, r, c + 1, gold=50)
+    put(o, d)
+    a = noop_actions(o)
+    a[0, 0, 9], a[0, 0, 10] = 0, 9  # Sell item 0 at price 10
+    o.step(a)
+    s = split_state(o.get_state(), 1, o.S, o.P)
+    assert (s["items"][0, 0, 0, 0] >> 10) & 127 == 10
+    a = noop_actions(o)
+    a[0, 1, 2] = 0  # Buy market listing 0
+    o.step(a)
+    s = split_state(o.get_state(), 1, o.S, o.P)
+    assert s["ent"][0][F["gold"], 0] == 10 and s["ent"][0][F["gold"], 1] == 40
+    assert s["items"][0, 0, 0, 0] == 0 and (s["items"][0, 1, 0, 0] & 31) == 2
+    assert (s["items"][0, 1, 0, 0] >> 10) & 127 == 0 and s["items"][0, 1, 0, 1] >> 16 == 9
+
+
+def test_give_requires_same_tile():
+    for dist, moved in [(0, True), (1, False)]:
+        o, d = _with_item(item_words(17, level=1, row=5))
+        d = split_state(o.get_state(), 1, o.S, o.P)
+        r, c = d["ent"][0][F["row"], 0], d["ent"][0][F["col"], 0]
+        place(d, 1, r, c + dist)
+        put(o, d)
+        a = noop_actions(o)
+        a[0, 0, 4], a[0, 0, 5] = 0, visible_index(d, 0, 1)  # Give item 0 to player 2
+        o.step(a)
+        s = split_state(o.get_state(), 1, o.S, o.P)
+        assert ((s["items"][0, 1, 0, 0] & 31) == 17) == moved
