@@ -45,6 +45,10 @@ struct NmmoHandle {
   uint8_t* d_bank = nullptr;
   float* d_task = nullptr;
   uint64_t* d_seeds = nullptr;
+  uint2* d_items = nullptr;
+  int16_t* d_iring = nullptr;
+  int32_t* d_mlist = nullptr;
+  int32_t* d_mcount = nullptr;
   // bench timing (nmmo_set_timing): event pairs around the tick and obs kernels
   bool timing = false;
   int t_count = 0;
@@ -128,7 +132,9 @@ int nmmo_layout(const NmmoConfig* cfg, NmmoLayout* L) {
   L->nf = NMMO_NF;
   L->ne = NMMO_NE;
   L->state_bytes_per_env = (size_t)NMMO_NE * 4 + (size_t)NMMO_NF * L->slots * 2 +
-                           (size_t)L->slots * 2 + NMMO_MAP_TILES;
+                           (size_t)L->slots * 2 + NMMO_MAP_TILES +
+                           (size_t)cfg->player_n * NMMO_INV_SLOTS * 8 +
+                           (size_t)NMMO_INV_SLOTS * cfg->player_n * 2;
   return NMMO_OK;
 }
 
@@ -138,7 +144,8 @@ void nmmo_destroy(NmmoHandle* h) {
   if (!h) return;
   (void)hipSetDevice(h->device);
   for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
-  void* bufs[] = {h->d_env, h->d_ent, h->d_ring, h->d_mat, h->d_dep, h->d_bank, h->d_task, h->d_seeds};
+  void* bufs[] = {h->d_env,  h->d_ent,   h->d_ring,  h->d_mat,   h->d_dep,   h->d_bank,
+                  h->d_task, h->d_seeds, h->d_items, h->d_iring, h->d_mlist, h->d_mcount};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   delete h;
@@ -178,15 +185,21 @@ int nmmo_create(const NmmoConfig* cfg, int32_t n_envs, uint64_t seed, int32_t de
   ALLOC(h->d_bank, (size_t)cfg->map_n * NMMO_MAP_TILES);
   ALLOC(h->d_task, (size_t)(cfg->task_embed_dim > 0 ? cfg->task_embed_dim : 1) * 4);
   ALLOC(h->d_seeds, n * 8);
+  ALLOC(h->d_items, n * P * NMMO_INV_SLOTS * 8);
+  ALLOC(h->d_iring, n * NMMO_INV_SLOTS * P * 2);
+  ALLOC(h->d_mlist, n * NMMO_MARKET_ROWS * 4);
+  ALLOC(h->d_mcount, n * 4);
 #undef ALLOC
+  if (init_kernels() != hipSuccess) return cleanup_fail(fail(NMMO_E_HIP, "kernel attributes"));
   if (task_embedding && cfg->task_embed_dim > 0) {
     std::vector<float> t(cfg->task_embed_dim);
     for (int k = 0; k < cfg->task_embed_dim; k++) t[k] = half_to_float(task_embedding[k]);
     if (hipMemcpy(h->d_task, t.data(), t.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
       return cleanup_fail(fail(NMMO_E_HIP, "task upload"));
   }
-  h->st = DevState{h->d_env, h->d_ent, h->d_ring, h->d_mat, h->d_dep, h->d_bank,
-                   n_envs, P, N, S, seed, *cfg};
+  h->st = DevState{h->d_env,   h->d_ent,   h->d_ring,  h->d_mat,    h->d_dep, h->d_bank,
+                   h->d_items, h->d_iring, h->d_mlist, h->d_mcount, n_envs,   P,
+                   N,          S,          seed,       *cfg};
   if (launch_mapgen(cfg->map_seed, cfg->map_n, h->d_bank, nullptr) != hipSuccess ||
       hipDeviceSynchronize() != hipSuccess)
     return cleanup_fail(fail(NMMO_E_HIP, "map generation failed: %s", hipGetErrorString(hipGetLastError())));
@@ -198,6 +211,7 @@ static ObsParams obs_params(NmmoHandle* h, float* obs) {
   const NmmoLayout& L = h->layout;
   ObsParams p;
   p.env = h->d_env; p.ent = h->d_ent; p.mat = h->d_mat; p.task = h->d_task; p.obs = obs;
+  p.items = h->d_items; p.mlist = h->d_mlist; p.mcount = h->d_mcount;
   p.n_envs = h->st.n_envs; p.P = h->st.P; p.S = h->st.S; p.elems = L.obs_elems;
   p.task_dim = h->cfg.task_embed_dim; p.systems = h->cfg.systems;
   p.spawn_immunity = h->cfg.spawn_immunity;
@@ -280,6 +294,7 @@ int nmmo_scripted_actions(NmmoHandle* h, uint64_t policy_seed, int32_t* actions,
   if (!h || !actions) return fail(NMMO_E_INVALID, "null argument");
   PolicyParams p;
   p.env = h->d_env; p.ent = h->d_ent; p.mat = h->d_mat; p.actions = actions;
+  p.items = h->d_items; p.mlist = h->d_mlist; p.mcount = h->d_mcount;
   p.n_envs = h->st.n_envs; p.P = h->st.P; p.S = h->st.S; p.systems = h->cfg.systems;
   p.spawn_immunity = h->cfg.spawn_immunity; p.seed = policy_seed;
   HIP_TRY(launch_policy(p, (hipStream_t)stream));
@@ -296,6 +311,11 @@ int nmmo_get_state(NmmoHandle* h, void* host_buf, size_t nbytes) {
   std::vector<int32_t> env(n * NMMO_NE);
   std::vector<int16_t> ent(n * NMMO_NF * S), ring(n * S);
   std::vector<uint8_t> mat(n * NMMO_MAP_TILES);
+  const size_t IP = (size_t)NMMO_INV_SLOTS * h->st.P;  // items per env
+  std::vector<uint32_t> items(n * IP * 2);
+  std::vector<int16_t> iring(n * IP);
+  HIP_TRY(hipMemcpy(items.data(), h->d_items, items.size() * 4, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(iring.data(), h->d_iring, iring.size() * 2, hipMemcpyDeviceToHost));
   HIP_TRY(hipMemcpy(env.data(), h->d_env, env.size() * 4, hipMemcpyDeviceToHost));
   HIP_TRY(hipMemcpy(ent.data(), h->d_ent, ent.size() * 2, hipMemcpyDeviceToHost));
   HIP_TRY(hipMemcpy(ring.data(), h->d_ring, ring.size() * 2, hipMemcpyDeviceToHost));
@@ -306,6 +326,8 @@ int nmmo_get_state(NmmoHandle* h, void* host_buf, size_t nbytes) {
     memcpy(b, ent.data() + e * NMMO_NF * S, NMMO_NF * S * 2); b += NMMO_NF * S * 2;
     memcpy(b, ring.data() + e * S, S * 2); b += S * 2;
     memcpy(b, mat.data() + e * NMMO_MAP_TILES, NMMO_MAP_TILES); b += NMMO_MAP_TILES;
+    memcpy(b, items.data() + e * IP * 2, IP * 8); b += IP * 8;
+    memcpy(b, iring.data() + e * IP, IP * 2); b += IP * 2;
   }
   return NMMO_OK;
 }
@@ -318,12 +340,17 @@ int nmmo_set_state(NmmoHandle* h, const void* host_buf, size_t nbytes) {
   std::vector<int32_t> env(n * NMMO_NE);
   std::vector<int16_t> ent(n * NMMO_NF * S), ring(n * S);
   std::vector<uint8_t> mat(n * NMMO_MAP_TILES);
+  const size_t IP = (size_t)NMMO_INV_SLOTS * h->st.P;
+  std::vector<uint32_t> items(n * IP * 2);
+  std::vector<int16_t> iring(n * IP);
   const uint8_t* b = (const uint8_t*)host_buf;
   for (size_t e = 0; e < n; e++) {
     memcpy(env.data() + e * NMMO_NE, b, NMMO_NE * 4); b += NMMO_NE * 4;
     memcpy(ent.data() + e * NMMO_NF * S, b, NMMO_NF * S * 2); b += NMMO_NF * S * 2;
     memcpy(ring.data() + e * S, b, S * 2); b += S * 2;
     memcpy(mat.data() + e * NMMO_MAP_TILES, b, NMMO_MAP_TILES); b += NMMO_MAP_TILES;
+    memcpy(items.data() + e * IP * 2, b, IP * 8); b += IP * 8;
+    memcpy(iring.data() + e * IP, b, IP * 2); b += IP * 2;
   }
   HIP_TRY(hipSetDevice(h->device));
   HIP_TRY(hipDeviceSynchronize());
@@ -331,6 +358,8 @@ int nmmo_set_state(NmmoHandle* h, const void* host_buf, size_t nbytes) {
   HIP_TRY(hipMemcpy(h->d_ent, ent.data(), ent.size() * 2, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(h->d_ring, ring.data(), ring.size() * 2, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(h->d_mat, mat.data(), mat.size(), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(h->d_items, items.data(), items.size() * 4, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(h->d_iring, iring.data(), iring.size() * 2, hipMemcpyHostToDevice));
   HIP_TRY(launch_rebuild_dep(h->st, nullptr));
   HIP_TRY(hipDeviceSynchronize());
   return NMMO_OK;

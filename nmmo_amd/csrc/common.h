@@ -14,7 +14,7 @@ constexpr int kSize = NMMO_MAP_SIZE;  // 160
 constexpr int kTiles = NMMO_MAP_TILES;
 constexpr int kLo = 16, kHi = 143, kCenter = 128, kVision = 7, kNObs = 100;
 constexpr int kBitmapWords = kTiles / 32;  // 800 depleted-tile bitmap words per env
-constexpr int kNFLive = F_DIED_TICK + 1;   // entity fields carried through LDS (43)
+constexpr int kNFLive = F_DROP_TOOL + 1;   // entity fields carried through LDS (45)
 constexpr int kMaxSlots = 384;
 constexpr int kHeads = NMMO_N_ACTION_HEADS;
 
@@ -24,8 +24,44 @@ enum Material : int {
 };
 enum Purpose : uint32_t {
   P_MAPSEL = 1, P_SPAWN_OFFSET = 2, P_RESILIENT = 3, P_NPC_SPAWN = 4, P_NPC_MOVE = 5,
-  P_RESPAWN = 6
+  P_RESPAWN = 6, P_BUY_ORDER = 7
 };
+
+// ---------------------------------------------------------------- items (SPEC §9)
+constexpr int kInv = NMMO_INV_SLOTS;
+enum ItemType : int {
+  T_HAT = 2, T_TOP, T_BOTTOM, T_SPEAR, T_BOW, T_WAND, T_ROD, T_GLOVES, T_PICKAXE, T_AXE, T_CHISEL,
+  T_WHETSTONE, T_ARROW, T_RUNES, T_RATION, T_POTION
+};
+// item = uint2: x = type | level<<5 | equipped<<9 | listed_price<<10 | listed_tick<<17,
+//               y = quantity | row<<16 ; type 0 = empty slot
+__host__ __device__ inline int it_type(uint2 w) { return (int)(w.x & 31u); }
+__host__ __device__ inline int it_level(uint2 w) { return (int)((w.x >> 5) & 15u); }
+__host__ __device__ inline int it_equipped(uint2 w) { return (int)((w.x >> 9) & 1u); }
+__host__ __device__ inline int it_price(uint2 w) { return (int)((w.x >> 10) & 127u); }
+__host__ __device__ inline int it_ltick(uint2 w) { return (int)((w.x >> 17) & 2047u); }
+__host__ __device__ inline int it_qty(uint2 w) { return (int)(w.y & 0xFFFFu); }
+__host__ __device__ inline int it_row(uint2 w) { return (int)(w.y >> 16); }
+__host__ __device__ inline int item_attack(int type, int level, int style) {
+  return (type == T_SPEAR + style || type == T_WHETSTONE + style) ? 5 + 5 * level : 0;
+}
+__host__ __device__ inline int item_defense(int type, int level) {
+  return (type >= T_HAT && type <= T_BOTTOM) ? 3 * level : (type >= T_ROD && type <= T_CHISEL) ? 2 * level : 0;
+}
+// level an item requires of its user; T is field-major with stride S (SPEC §9)
+__device__ inline int requirement_level(const int16_t* T, int S, int p, int type) {
+  if (type >= T_SPEAR && type <= T_WAND) return T[(F_MELEE_LEVEL + 2 * (type - T_SPEAR)) * S + p];
+  if (type >= T_WHETSTONE && type <= T_RUNES) return T[(F_MELEE_LEVEL + 2 * (type - T_WHETSTONE)) * S + p];
+  if (type >= T_ROD && type <= T_CHISEL) return T[(F_FISHING_LEVEL + 2 * (type - T_ROD)) * S + p];
+  if (type == T_RATION) return T[F_FISHING_LEVEL * S + p];
+  if (type == T_POTION) return T[F_HERBALISM_LEVEL * S + p];
+  return max((int)T[F_MELEE_LEVEL * S + p], max((int)T[F_RANGE_LEVEL * S + p], (int)T[F_MAGE_LEVEL * S + p]));
+}
+__host__ __device__ inline int equip_slot(int type) {  // hat top bottom held ammo; -1 consumable
+  return (type >= T_HAT && type <= T_BOTTOM) ? type - T_HAT
+         : (type >= T_SPEAR && type <= T_CHISEL) ? 3
+         : (type >= T_WHETSTONE && type <= T_RUNES) ? 4 : -1;
+}
 
 // bit m set <=> material m is impassable (Void, Water, Stone, Ocean, Fish)
 constexpr uint32_t kImpassableMask = (1u << M_VOID) | (1u << M_WATER) | (1u << M_STONE) |
@@ -111,6 +147,87 @@ __host__ __device__ inline uint32_t h32(uint32_t x) {
 __device__ inline int lane_id() { return threadIdx.x & 63; }
 __device__ inline int wave_id() { return threadIdx.x >> 6; }
 __device__ inline uint64_t lanes_below() { return (1ull << lane_id()) - 1ull; }
+
+__device__ inline bool item_usable(const int16_t* T, int S, int p, uint2 w) {
+  if (it_price(w)) return false;
+  if (equip_slot(it_type(w)) >= 0 && it_equipped(w)) return true;
+  return it_level(w) <= requirement_level(T, S, p, it_type(w));
+}
+// column col of an Inventory / Market obs row (nmmo ItemState order, SPEC §9)
+__device__ inline float item_col(uint2 w, int owner_id, int col) {
+  const int type = it_type(w), lvl = it_level(w);
+  switch (col) {
+    case 0: return (float)it_row(w);
+    case 1: return (float)type;
+    case 2: return (float)owner_id;
+    case 3: return (float)lvl;
+    case 4: return 0.f;
+    case 5: return (float)it_qty(w);
+    case 6: case 7: case 8: return (float)item_attack(type, lvl, col - 6);
+    case 9: case 10: case 11: return (float)item_defense(type, lvl);
+    case 12: return type == T_POTION ? (float)(50 + 5 * lvl) : 0.f;
+    case 13: return type == T_RATION ? (float)(50 + 5 * lvl) : 0.f;
+    case 14: return (float)it_equipped(w);
+    default: return (float)it_price(w);
+  }
+}
+// inventory of one player: kInv slots, occupied prefix in ascending row order
+__device__ inline int inv_count(const uint2* inv) {
+  int n = 0;
+  while (n < kInv && it_type(inv[n])) n++;
+  return n;
+}
+__device__ inline int inv_find(const uint2* inv, int row) {
+  for (int k = 0; k < kInv; k++) {
+    const uint2 w = inv[k];
+    if (!it_type(w)) break;
+    if (it_row(w) == row) return k;
+  }
+  return -1;
+}
+__device__ inline void inv_remove(uint2* inv, int k) {
+  for (int j = k; j < kInv - 1; j++) inv[j] = inv[j + 1];
+  inv[kInv - 1] = make_uint2(0u, 0u);
+}
+__device__ inline void inv_insert(uint2* inv, uint2 w) {  // caller checked room
+  int k = inv_count(inv);
+  while (k > 0 && it_row(inv[k - 1]) > it_row(w)) {
+    inv[k] = inv[k - 1];
+    k--;
+  }
+  inv[k] = w;
+}
+__device__ inline int inv_stack(const uint2* inv, int type, int level) {  // ammunition stacks
+  if (type < T_WHETSTONE || type > T_RUNES) return -1;
+  for (int k = 0; k < kInv; k++) {
+    const uint2 w = inv[k];
+    if (!it_type(w)) break;
+    if (it_type(w) == type && it_level(w) == level) return k;
+  }
+  return -1;
+}
+
+// Block-wide exclusive prefix sum of an int in thread order (<= 16 waves); *total gets the sum.
+__device__ inline int block_prefix_sum(int v, int* wave_tot, int* total) {
+  const int lane = lane_id(), w = wave_id(), nw = (blockDim.x + 63) >> 6;
+  int x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int y = __shfl_up(x, d);
+    if (lane >= d) x += y;
+  }
+  if (lane == 63) wave_tot[w] = x;
+  __syncthreads();
+  int base = 0, sum = 0;
+  for (int i = 0; i < nw; i++) {
+    const int t = wave_tot[i];
+    base += i < w ? t : 0;
+    sum += t;
+  }
+  __syncthreads();
+  *total = sum;
+  return base + x - v;
+}
 
 // Block-wide exclusive prefix count of a 0/1 predicate in thread order (<= 16 waves).
 // `wave_tot` is LDS scratch of >= 17 ints. Returns the exclusive count; *total gets the sum.

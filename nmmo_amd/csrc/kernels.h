@@ -12,6 +12,10 @@ struct DevState {
   uint8_t* mat;          // [n][kTiles]
   uint32_t* dep;         // [n][kBitmapWords]
   const uint8_t* bank;   // [map_n][kTiles]
+  uint2* items;          // [n][P][kInv] (SPEC §9)
+  int16_t* iring;        // [n][kInv*P] free item rows
+  int32_t* mlist;        // [n][NMMO_MARKET_ROWS] end-of-tick listings, ascending row: row | owner<<16 | slot<<24
+  int* mcount;           // [n] listings in mlist (<= NMMO_MARKET_ROWS)
   int n_envs, P, N, S;   // N = NPC capacity (0 when the NPC system is off), S = P + N
   uint64_t seed;         // create seed (first-episode seeds)
   NmmoConfig cfg;
@@ -21,6 +25,9 @@ struct ObsParams {
   const int32_t* env;   // [n][NE]
   const int16_t* ent;   // [n][NF][S]
   const uint8_t* mat;   // [n][kTiles]
+  const uint2* items;   // [n][P][kInv]
+  const int32_t* mlist; // [n][NMMO_MARKET_ROWS] row | owner<<16 | slot<<24
+  const int* mcount;    // [n]
   const float* task;    // [task_dim]
   float* obs;           // [n][P][elems]
   int n_envs, P, S, elems, task_dim;
@@ -36,6 +43,9 @@ struct PolicyParams {
   const int32_t* env;
   const int16_t* ent;
   const uint8_t* mat;
+  const uint2* items;
+  const int32_t* mlist;
+  const int* mcount;
   int32_t* actions;  // [n][P][12]
   int n_envs, P, S;
   uint32_t systems;
@@ -43,6 +53,7 @@ struct PolicyParams {
   uint64_t seed;
 };
 
+hipError_t init_kernels();  // one-time function attributes (dynamic LDS above 64 KB)
 hipError_t launch_mapgen(uint64_t seed, int map_n, uint8_t* bank, hipStream_t stream);
 hipError_t launch_tick(const DevState& st, const int32_t* actions, const uint64_t* env_seeds,
                        float* rew, uint8_t* term, uint8_t* trunc, uint8_t* mask, int mode,

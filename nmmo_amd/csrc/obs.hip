@@ -19,9 +19,10 @@ constexpr int kObsAgentsPerBlock = 16;
 constexpr int kObsWaves = 4;
 constexpr int kObsFields = F_DS_ROW + 1;  // 0..30 obs columns, alive, ds_row
 
+// LDS: entity fields | row->slot | per-wave visible list | per-wave inventory | market listings
 __host__ __device__ inline size_t obs_lds_bytes(int S) {
   return (((size_t)kObsFields * S * 2 + 15) & ~(size_t)15) + (((size_t)(S + 1) * 2 + 15) & ~(size_t)15) +
-         (size_t)kObsWaves * 128 * 2;
+         (size_t)kObsWaves * 128 * 2 + (size_t)kObsWaves * kInv * 8 + (size_t)NMMO_MARKET_ROWS * 12;
 }
 
 // zero [lo, hi) of a row with 16-byte stores on the aligned body (wave-cooperative)
@@ -44,8 +45,18 @@ __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
   int16_t* T = reinterpret_cast<int16_t*>(smem);
   int16_t* rowslot = reinterpret_cast<int16_t*>(smem + (((size_t)kObsFields * S * 2 + 15) & ~(size_t)15));
   int16_t* vis_all = rowslot + ((((size_t)(S + 1) * 2 + 15) & ~(size_t)15) / 2);
+  uint2* inv_all = reinterpret_cast<uint2*>(vis_all + kObsWaves * 128);
+  uint2* mitem = inv_all + kObsWaves * kInv;                       // listed item words
+  int* mown = reinterpret_cast<int*>(mitem + NMMO_MARKET_ROWS);    // listing owner slot
   const int e = blockIdx.x, g = blockIdx.y;
   const int tid = threadIdx.x;
+  const int nm = p.mcount[e];
+  for (int j = tid; j < nm; j += blockDim.x) {  // end-of-tick listings, ascending row
+    const int v = p.mlist[(size_t)e * NMMO_MARKET_ROWS + j];
+    const int own = (v >> 16) & 255, slot = (v >> 24) & 15;
+    mown[j] = own;
+    mitem[j] = p.items[((size_t)e * p.P + own) * kInv + slot];
+  }
   {
     const int16_t* src = p.ent + (size_t)e * NMMO_NF * S;
     const int n16 = kObsFields * S;
@@ -68,6 +79,9 @@ __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
   const uint8_t* mat = p.mat + (size_t)e * kTiles;
   const int tick = p.env[(size_t)e * NMMO_NE + E_TICK];
   const bool combat = (p.systems & NMMO_SYS_COMBAT) != 0;
+  const bool item = (p.systems & NMMO_SYS_ITEM) != 0;
+  const bool exch = item && (p.systems & NMMO_SYS_EXCHANGE) != 0;
+  uint2* inv = inv_all + w * kInv;
   for (int i = w; i < kObsAgentsPerBlock; i += kObsWaves) {
     const int a = g * kObsAgentsPerBlock + i;
     if (a >= p.P) break;
@@ -77,6 +91,8 @@ __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
       continue;
     }
     const int r = T[F_ROW * S + a], c = T[F_COL * S + a];
+    const int gold = T[F_GOLD * S + a];
+    if (lane < kInv) inv[lane] = p.items[((size_t)e * p.P + a) * kInv + lane];
     // Entity.Query.window: ascending datastore rows within L-inf <= 7, first 100
     int nv = 0;
     for (int base = 1; base <= S; base += 64) {
@@ -96,32 +112,49 @@ __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
 
-    // ActionTargets [0, o_agent_id)
+    const int ninv = inv_count(inv);
+    // ActionTargets [0, o_agent_id) (SPEC §8, §9)
     for (int j = lane; j < p.o_agent_id; j += 64) {
-      float v = 0.f;
+      bool v = false;
       if (j < p.o_target) {
-        v = combat ? 1.f : 0.f;
+        v = combat;
       } else if (j < p.o_buy) {
         const int k = j - p.o_target;
-        if (k == kNObs) v = 1.f;
+        if (k == kNObs) v = true;
         else if (combat && k < nv) {
           const int q = vis[k];
-          const bool ok = q != a && linf(r, c, T[F_ROW * S + q], T[F_COL * S + q]) <= 3 &&
-                          !(q < p.P && T[F_TIME_ALIVE * S + q] < p.spawn_immunity);
-          v = ok ? 1.f : 0.f;
+          v = q != a && linf(r, c, T[F_ROW * S + q], T[F_COL * S + q]) <= 3 &&
+              !(q < p.P && T[F_TIME_ALIVE * S + q] < p.spawn_immunity);
         }
-      } else if (j >= p.o_move && j < p.o_sell_item) {
+      } else if (j < p.o_destroy) {
+        const int k = j - p.o_buy;
+        v = k == NMMO_MARKET_ROWS || (exch && k < nm && it_price(mitem[k]) <= gold && mown[k] != a);
+      } else if (j < p.o_give_target) {  // Destroy.InventoryItem, Give.InventoryItem
+        const int k = j < p.o_give_item ? j - p.o_destroy : j - p.o_give_item;
+        v = k == kInv || (item && k < ninv && !it_equipped(inv[k]) && !it_price(inv[k]));
+      } else if (j < p.o_gg_price || (j >= p.o_gg_target && j < p.o_move)) {  // Give/GiveGold.Target
+        const bool on = j < p.o_gg_price ? item : exch;
+        const int k = j < p.o_gg_price ? j - p.o_give_target : j - p.o_gg_target;
+        if (k == kNObs) v = true;
+        else if (on && k < nv) {
+          const int q = vis[k];
+          v = q < p.P && q != a && T[F_ROW * S + q] == r && T[F_COL * S + q] == c;
+        }
+      } else if (j < p.o_gg_target) {
+        v = exch && j - p.o_gg_price < gold;
+      } else if (j < p.o_sell_item) {
         const int d = j - p.o_move;
-        v = impassable(mat[(r + dir_dr(d)) * kSize + c + dir_dc(d)]) ? 0.f : 1.f;
+        v = !impassable(mat[(r + dir_dr(d)) * kSize + c + dir_dc(d)]);
+      } else if (j < p.o_sell_price) {
+        const int k = j - p.o_sell_item;
+        v = k == kInv || (exch && k < ninv && !it_equipped(inv[k]));
+      } else if (j < p.o_use) {
+        v = exch;
       } else {
-        // noop (last) index of every other Target / InventoryItem / MarketItem mask
-        v = (j == p.o_destroy - 1 || j == p.o_give_item - 1 || j == p.o_give_target - 1 ||
-             j == p.o_gg_price - 1 || j == p.o_move - 1 || j == p.o_sell_price - 1 ||
-             j == p.o_agent_id - 1)
-                ? 1.f
-                : 0.f;
+        const int k = j - p.o_use;
+        v = k == kInv || (item && k < ninv && item_usable(T, S, a, inv[k]));
       }
-      row[j] = v;
+      row[j] = v ? 1.f : 0.f;
     }
     if (lane == 0) row[p.o_agent_id] = (float)T[F_ID * S + a];
     if (lane == 1) row[p.o_tick] = (float)tick;
@@ -131,8 +164,14 @@ __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
       const int k = j / NMMO_N_ENTITY_COLS, f = j - k * NMMO_N_ENTITY_COLS;
       row[p.o_entity + j] = k < nv ? (float)T[f * S + vis[k]] : 0.f;
     }
-    // Inventory + Market (v1: no items, no listings)
-    wave_zero(row, p.o_inventory, p.o_task);
+    // Inventory (own items, owner = self) and Market (env listings, ascending row)
+    const int aid = T[F_ID * S + a];
+    for (int j = lane; j < kInv * 16; j += 64) {
+      const int k = j >> 4;
+      row[p.o_inventory + j] = k < ninv ? item_col(inv[k], aid, j & 15) : 0.f;
+    }
+    for (int j = lane; j < nm * 16; j += 64) row[p.o_market + j] = item_col(mitem[j >> 4], mown[j >> 4] + 1, j & 15);
+    wave_zero(row, p.o_market + nm * 16, p.o_task);
     for (int j = lane; j < p.task_dim; j += 64) row[p.o_task + j] = p.task[j];
     for (int j = lane; j < 225 * 3; j += 64) {
       const int t = j / 3, comp = j - 3 * t;
@@ -150,15 +189,33 @@ hipError_t launch_obs(const ObsParams& p, hipStream_t stream) {
 }
 
 // ---------------------------------------------------------------- scripted policy (SPEC §10)
-// One workgroup per env, one thread per player. The env's entities are first packed per
-// datastore row into one int32 (r | c<<8 | slot<<16 | immune<<25, -1 = absent), so the two
+// One workgroup per env, one thread per player: for every head, a uniform draw over the set
+// bits of that head's mask (identical to the obs masks). The env's entities are first packed
+// per datastore row into one int32 (r | c<<8 | slot<<16 | immune<<25, -1 = absent), so the two
 // visibility passes over the rows are one broadcast LDS load per row with no dependent loads.
+__host__ __device__ inline size_t policy_lds_bytes(int S, int P) {
+  return (size_t)rp_groups(S) * 16 + (size_t)P * kInv * 8 + (size_t)NMMO_MARKET_ROWS * 12;
+}
+
 __global__ void __launch_bounds__(128) policy_kernel(PolicyParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int S = p.S, e = blockIdx.x, tid = threadIdx.x;
   int* rp = reinterpret_cast<int*>(smem);  // by datastore row (row 0 unused), int4-padded
+  uint2* invs = reinterpret_cast<uint2*>(smem + (size_t)rp_groups(S) * 16);
+  uint2* mitem = invs + p.P * kInv;
+  int* mown = reinterpret_cast<int*>(mitem + NMMO_MARKET_ROWS);
   const int16_t* E = p.ent + (size_t)e * NMMO_NF * S;
+  const bool combat = (p.systems & NMMO_SYS_COMBAT) != 0;
+  const bool item = (p.systems & NMMO_SYS_ITEM) != 0;
+  const bool exch = item && (p.systems & NMMO_SYS_EXCHANGE) != 0;
+  const int nm = exch ? p.mcount[e] : 0;
   for (int k = tid; k < rp_groups(S) * 4; k += blockDim.x) rp[k] = -1;
+  for (int k = tid; k < p.P * kInv; k += blockDim.x) invs[k] = p.items[(size_t)e * p.P * kInv + k];
+  for (int j = tid; j < nm; j += blockDim.x) {
+    const int v = p.mlist[(size_t)e * NMMO_MARKET_ROWS + j];
+    mown[j] = (v >> 16) & 255;
+    mitem[j] = p.items[((size_t)e * p.P + ((v >> 16) & 255)) * kInv + ((v >> 24) & 15)];
+  }
   __syncthreads();
   for (int s = tid; s < S; s += blockDim.x) {
     if (!E[F_ALIVE * S + s]) continue;
@@ -170,7 +227,7 @@ __global__ void __launch_bounds__(128) policy_kernel(PolicyParams p) {
   const uint8_t* mat = p.mat + (size_t)e * kTiles;
   for (int a = tid; a < p.P; a += blockDim.x) {
     int32_t* out = p.actions + ((size_t)e * p.P + a) * kHeads;
-    int32_t h[kHeads] = {0, kNObs, 1024, 12, 12, kNObs, 0, kNObs, 0, 12, 0, 12};
+    int32_t h[kHeads] = {0, kNObs, NMMO_MARKET_ROWS, kInv, kInv, kNObs, 0, kNObs, 0, kInv, 0, kInv};
     if (!E[F_ALIVE * S + a]) {
 #pragma unroll
       for (int k = 0; k < kHeads; k++) out[k] = 0;
@@ -179,60 +236,124 @@ __global__ void __launch_bounds__(128) policy_kernel(PolicyParams p) {
     const uint32_t c0 = (uint32_t)env[E_TICK] + 2048u * (uint32_t)env[E_EPISODE];
     const uint32_t c1 = (uint32_t)env[E_ENV_INDEX];
     const uint32_t k0 = (uint32_t)p.seed, k1 = (uint32_t)(p.seed >> 32);
-    const int r = E[F_ROW * S + a], c = E[F_COL * S + a];
-    if (p.systems & NMMO_SYS_COMBAT) {
-      h[0] = (int)uniform_n(philox(c0, c1, (uint32_t)a, 0, k0, k1).x, 3);
-      // attack mask over the first 100 visible rows: count, draw, then select the k-th set bit
+    auto draw_n = [&](int head, int n) {
+      return (int)uniform_n(philox(c0, c1, (uint32_t)a, (uint32_t)head, k0, k1).x, (uint32_t)n);
+    };
+    const int r = E[F_ROW * S + a], c = E[F_COL * S + a], gold = E[F_GOLD * S + a];
+    if (combat) h[0] = draw_n(0, 3);
+    // Attack / Give / GiveGold targets over the first 100 visible rows: count, draw, then
+    // select the pick-th set bit of each mask in one more pass
+    const bool tgt_any = combat || item;
+    if (tgt_any) {
       const int4* rp4 = reinterpret_cast<const int4*>(rp);
       const int ng = rp_groups(S);
-      int nb = 0, nv = 0;
-      for (int g = 0; g < ng; g++) {  // pass 1: count targets among the first 100 visible
+      int na = 0, nt = 0, nv = 0;
+      for (int g = 0; g < ng; g++) {  // pass 1: counts among the first 100 visible
         const int4 q = rp4[g];
         const int vv[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
         for (int j = 0; j < 4; j++) {
           const int v = vv[j];
           const int d = linf(r, c, v & 255, (v >> 8) & 255);
+          const int sl = (v >> 16) & 511;
           const bool vis = v >= 0 && d <= kVision && nv < kNObs;
-          nb += vis && ((v >> 16) & 511) != a && d <= 3 && !((v >> 25) & 1);
+          na += vis && sl != a && d <= 3 && !((v >> 25) & 1);
+          nt += vis && sl != a && sl < p.P && d == 0;
           nv += vis;
         }
       }
-      const int pick = (int)uniform_n(philox(c0, c1, (uint32_t)a, 1, k0, k1).x, (uint32_t)(nb + 1));
-      int sel = kNObs;
-      if (pick < nb) {  // pass 2: visible index of the pick-th target
-        int seen = 0;
+      const int pa = combat ? draw_n(1, na + 1) : na;
+      const int pg = draw_n(5, (item ? nt : 0) + 1);
+      const int pgg = draw_n(7, (exch ? nt : 0) + 1);
+      int sa = kNObs, sg = kNObs, sgg = kNObs;
+      const bool want_a = combat && pa < na, want_g = item && pg < nt, want_gg = exch && pgg < nt;
+      if (want_a || want_g || want_gg) {  // pass 2: visible index of each pick
+        int seen_a = 0, seen_t = 0;
         nv = 0;
-        for (int g = 0; g < ng && sel == kNObs; g++) {
+        for (int g = 0; g < ng && nv < kNObs; g++) {
           const int4 q = rp4[g];
           const int vv[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
           for (int j = 0; j < 4; j++) {
             const int v = vv[j];
             const int d = linf(r, c, v & 255, (v >> 8) & 255);
-            const bool vis = v >= 0 && d <= kVision;
-            const bool ok = vis && ((v >> 16) & 511) != a && d <= 3 && !((v >> 25) & 1);
-            sel = (ok && seen == pick && sel == kNObs) ? nv : sel;
-            seen += ok;
+            const int sl = (v >> 16) & 511;
+            const bool vis = v >= 0 && d <= kVision && nv < kNObs;
+            const bool oka = vis && sl != a && d <= 3 && !((v >> 25) & 1);
+            const bool okt = vis && sl != a && sl < p.P && d == 0;
+            sa = (want_a && oka && seen_a == pa && sa == kNObs) ? nv : sa;
+            sg = (want_g && okt && seen_t == pg && sg == kNObs) ? nv : sg;
+            sgg = (want_gg && okt && seen_t == pgg && sgg == kNObs) ? nv : sgg;
+            seen_a += oka;
+            seen_t += okt;
             nv += vis;
           }
         }
       }
-      h[1] = sel;
+      if (combat) h[1] = sa;
+      h[5] = sg;
+      h[7] = sgg;
     }
-    int mv[5], nm = 0;
+    // Buy.MarketItem: listings with price <= gold not owned by self
+    {
+      int nb = 0;
+      for (int j = 0; j < nm; j++) nb += it_price(mitem[j]) <= gold && mown[j] != a;
+      const int pick = draw_n(2, nb + 1);
+      int sel = NMMO_MARKET_ROWS;
+      for (int j = 0, seen = 0; j < nm && sel == NMMO_MARKET_ROWS; j++) {
+        const bool ok = it_price(mitem[j]) <= gold && mown[j] != a;
+        sel = (ok && seen == pick) ? j : sel;
+        seen += ok;
+      }
+      h[2] = sel;
+    }
+    // InventoryItem heads: Destroy (3), Give (4), Sell (9), Use (11)
+    {
+      const uint2* inv = invs + a * kInv;
+      const int n = inv_count(inv);
+      int nf = 0, ns = 0, nu = 0;
+      for (int k = 0; k < n; k++) {
+        const uint2 w = inv[k];
+        nf += !it_equipped(w) && !it_price(w);
+        ns += !it_equipped(w);
+        nu += item_usable(E, S, a, w);
+      }
+      const int pd = draw_n(3, (item ? nf : 0) + 1), pgv = draw_n(4, (item ? nf : 0) + 1);
+      const int ps = draw_n(9, (exch ? ns : 0) + 1), pu = draw_n(11, (item ? nu : 0) + 1);
+      int sd = kInv, sgv = kInv, ss = kInv, su = kInv;
+      for (int k = 0, cf = 0, cs = 0, cu = 0; k < n; k++) {
+        const uint2 w = inv[k];
+        const bool f = !it_equipped(w) && !it_price(w), sll = !it_equipped(w), us = item_usable(E, S, a, w);
+        sd = (item && f && cf == pd && sd == kInv) ? k : sd;
+        sgv = (item && f && cf == pgv && sgv == kInv) ? k : sgv;
+        ss = (exch && sll && cs == ps && ss == kInv) ? k : ss;
+        su = (item && us && cu == pu && su == kInv) ? k : su;
+        cf += f;
+        cs += sll;
+        cu += us;
+      }
+      h[3] = sd;
+      h[4] = sgv;
+      h[9] = ss;
+      h[11] = su;
+    }
+    if (exch) {
+      const int ng = min(gold, 99);
+      h[6] = ng > 0 ? draw_n(6, ng) : 0;
+      h[10] = draw_n(10, 99);
+    }
+    int mv[5], nmv = 0;
 #pragma unroll
     for (int d = 0; d < 5; d++)
-      if (!impassable(mat[(r + dir_dr(d)) * kSize + c + dir_dc(d)])) mv[nm++] = d;
-    h[8] = mv[uniform_n(philox(c0, c1, (uint32_t)a, 8, k0, k1).x, (uint32_t)nm)];
+      if (!impassable(mat[(r + dir_dr(d)) * kSize + c + dir_dc(d)])) mv[nmv++] = d;
+    h[8] = nmv ? mv[draw_n(8, nmv)] : 0;
 #pragma unroll
     for (int k = 0; k < kHeads; k++) out[k] = h[k];
   }
 }
 
 hipError_t launch_policy(const PolicyParams& p, hipStream_t stream) {
-  const size_t lds = (size_t)rp_groups(p.S) * 16;
-  hipLaunchKernelGGL(policy_kernel, dim3(p.n_envs), dim3(128), lds, stream, p);
+  hipLaunchKernelGGL(policy_kernel, dim3(p.n_envs), dim3(128), policy_lds_bytes(p.S, p.P), stream, p);
   return hipGetLastError();
 }
 

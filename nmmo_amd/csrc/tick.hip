@@ -15,7 +15,14 @@
 //     target, or its target attacked earlier. Uncontested attacks read only phase-start state
 //     and have disjoint write sets, so they are applied in parallel first; contested ones are
 //     then replayed lane-serially in slot order (the only serial part of the tick);
-//   * cull, free-row FIFO, NPC compaction and NPC spawn use wave ballots + block prefix counts.
+//   * cull, free-row FIFO, NPC compaction and NPC spawn use wave ballots + block prefix counts;
+//   * items (SPEC §9): every player's 12-slot inventory, the item-row FIFO, a listed-row bitmap
+//     and row->owner map live in LDS too. Per-player item work (harvest, Use, Destroy, Sell,
+//     expiry, death cleanup) runs in parallel and touches the item FIFO through block prefix
+//     sums, so rows are allocated/freed in exactly the serial slot order; the cross-player
+//     steps (Buy in shuffled order, Give/GiveGold, and ammunition + loot of executed attacks,
+//     deferred to after the attack phase — equipment sums cannot change inside it) are
+//     replayed by thread 0 in serial order.
 #include "kernels.h"
 
 namespace nmmo {
@@ -41,7 +48,22 @@ struct Ctx {
   uint8_t* died;     // [128]
   uint8_t* mat;      // global, this env
   const uint8_t* bank;
-  int S, P, N;
+  // items (SPEC §9), allocated only when the Item system is on
+  uint2* inv;        // [P][kInv]
+  int16_t* iring;    // [IC] free item rows (FIFO)
+  int16_t* rmap;     // [IC+1] listed row -> owner | slot<<8
+  uint64_t* lbits;   // [kLWords] listed-row bitmap (bit = row)
+  int16_t* a_buy;    // [128] decoded Buy row
+  int16_t* a_give;   // [128] decoded Give item row
+  int16_t* a_givet;  // [128] Give target slot
+  int16_t* a_ggt;    // [128] GiveGold target slot
+  int16_t* a_gga;    // [128] GiveGold amount
+  int16_t* kill;     // [128] slot killed by this player's attack (deferred loot)
+  int16_t* order;    // [128] Buy order / serial replay lists
+  uint8_t* fired;    // [128] executed attack (ammunition)
+  uint32_t* ikey;    // [128] Buy sort keys
+  int S, P, N, IC;
+  bool items, exch, prof, equip;
   const NmmoConfig* cfg;
 };
 
@@ -62,16 +84,24 @@ __device__ unsigned long long g_stamps[4096 * 16];
   } while (0)
 #endif
 
-__device__ inline bool sys(const Ctx& c, uint32_t b) { return (c.cfg->systems & b) != 0; }
-__device__ inline uint64_t env_seed(const Ctx& c) {
+__device__ __forceinline__ bool sys(const Ctx& c, uint32_t b) { return (c.cfg->systems & b) != 0; }
+__device__ __forceinline__ uint64_t env_seed(const Ctx& c) {
   return (uint64_t)(uint32_t)c.E[E_SEED_LO] | ((uint64_t)(uint32_t)c.E[E_SEED_HI] << 32);
 }
 
 constexpr int kHash = 256;  // >= 2x players: open addressing never fills
+constexpr int kLWords = 32;  // listed-row bitmap words (rows 1..12*128)
 
-__host__ __device__ inline size_t tick_lds_bytes(int S) {
+__host__ __device__ inline size_t item_lds_bytes(int P) {
   auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
-  size_t b = 0;
+  const size_t ic = (size_t)kInv * P;
+  return (size_t)P * kInv * 8 + al(ic * 2) + al((ic + 1) * 2) + kLWords * 8;
+}
+constexpr size_t kPlayerArrBytes = 7 * 256 + 128 + 512;  // per-player action / replay arrays
+
+__host__ __device__ inline size_t tick_lds_bytes(int S, int P, bool items) {
+  auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
+  size_t b = (items ? item_lds_bytes(P) : 0) + kPlayerArrBytes;
   b += al((size_t)kNFLive * S * 2);  // T
   b += (size_t)128 * ((S + 63) / 64) * 8;  // vism (players <= 128)
   b += (size_t)rp_groups(S) * 16;    // rp
@@ -86,11 +116,34 @@ __host__ __device__ inline size_t tick_lds_bytes(int S) {
   return b;
 }
 
-__device__ inline Ctx make_ctx(unsigned char* smem, const DevState& st, int e) {
+__device__ __forceinline__ Ctx make_ctx(unsigned char* smem, const DevState& st, int e) {
   auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
   Ctx c;
   const int S = st.S;
   size_t o = 0;
+  const uint32_t sy = st.cfg.systems;
+  c.items = (sy & NMMO_SYS_ITEM) != 0;
+  c.exch = c.items && (sy & NMMO_SYS_EXCHANGE) != 0;
+  c.prof = c.items && (sy & NMMO_SYS_PROFESSION) != 0;
+  c.equip = c.items && (sy & NMMO_SYS_EQUIPMENT) != 0;
+  c.IC = kInv * st.P;
+  if (c.items) {  // 16-B aligned block first (inventories are copied with 16-B accesses)
+    c.inv = reinterpret_cast<uint2*>(smem + o); o += (size_t)st.P * kInv * 8;
+    c.iring = reinterpret_cast<int16_t*>(smem + o); o += al((size_t)c.IC * 2);
+    c.rmap = reinterpret_cast<int16_t*>(smem + o); o += al((size_t)(c.IC + 1) * 2);
+    c.lbits = reinterpret_cast<uint64_t*>(smem + o); o += kLWords * 8;
+  }
+  {
+    c.a_buy = reinterpret_cast<int16_t*>(smem + o); o += 256;
+    c.a_give = reinterpret_cast<int16_t*>(smem + o); o += 256;
+    c.a_givet = reinterpret_cast<int16_t*>(smem + o); o += 256;
+    c.a_ggt = reinterpret_cast<int16_t*>(smem + o); o += 256;
+    c.a_gga = reinterpret_cast<int16_t*>(smem + o); o += 256;
+    c.kill = reinterpret_cast<int16_t*>(smem + o); o += 256;
+    c.order = reinterpret_cast<int16_t*>(smem + o); o += 256;
+    c.fired = smem + o; o += 128;
+    c.ikey = reinterpret_cast<uint32_t*>(smem + o); o += 512;
+  }
   c.T = reinterpret_cast<int16_t*>(smem + o); o += al((size_t)kNFLive * S * 2);
   c.vism = reinterpret_cast<uint64_t*>(smem + o); o += (size_t)128 * ((S + 63) / 64) * 8;
   c.rp = reinterpret_cast<int*>(smem + o); o += (size_t)rp_groups(S) * 16;
@@ -119,7 +172,7 @@ __device__ inline Ctx make_ctx(unsigned char* smem, const DevState& st, int e) {
 }
 
 // ---------------------------------------------------------------- load / store
-__device__ void load_env(Ctx& c, const DevState& st, int e) {
+__device__ __forceinline__ void load_env(Ctx& c, const DevState& st, int e) {
   const int tid = threadIdx.x, nt = blockDim.x, S = c.S;
   if (tid < NMMO_NE) c.E[tid] = st.env[(size_t)e * NMMO_NE + tid];
   const int16_t* src = st.ent + (size_t)e * NMMO_NF * S;
@@ -133,9 +186,15 @@ __device__ void load_env(Ctx& c, const DevState& st, int e) {
   }
   for (int i = tid; i < S; i += nt) c.ring[i] = st.ring[(size_t)e * S + i];
   for (int i = tid; i < kBitmapWords; i += nt) c.dep[i] = st.dep[(size_t)e * kBitmapWords + i];
+  if (c.items) {
+    const uint4* s4 = reinterpret_cast<const uint4*>(st.items + (size_t)e * c.P * kInv);
+    uint4* d4 = reinterpret_cast<uint4*>(c.inv);
+    for (int i = tid; i < c.P * kInv / 2; i += nt) d4[i] = s4[i];
+    for (int i = tid; i < c.IC; i += nt) c.iring[i] = st.iring[(size_t)e * c.IC + i];
+  }
 }
 
-__device__ void store_env(const Ctx& c, const DevState& st, int e) {
+__device__ __forceinline__ void store_env(const Ctx& c, const DevState& st, int e) {
   const int tid = threadIdx.x, nt = blockDim.x, S = c.S;
   if (tid < NMMO_NE) st.env[(size_t)e * NMMO_NE + tid] = c.E[tid];
   int16_t* dst = st.ent + (size_t)e * NMMO_NF * S;
@@ -149,16 +208,140 @@ __device__ void store_env(const Ctx& c, const DevState& st, int e) {
   }
   for (int i = tid; i < S; i += nt) st.ring[(size_t)e * S + i] = c.ring[i];
   for (int i = tid; i < kBitmapWords; i += nt) st.dep[(size_t)e * kBitmapWords + i] = c.dep[i];
+  if (c.items) {
+    const uint4* s4 = reinterpret_cast<const uint4*>(c.inv);
+    uint4* d4 = reinterpret_cast<uint4*>(st.items + (size_t)e * c.P * kInv);
+    for (int i = tid; i < c.P * kInv / 2; i += nt) d4[i] = s4[i];
+    for (int i = tid; i < c.IC; i += nt) st.iring[(size_t)e * c.IC + i] = c.iring[i];
+  }
+}
+
+// ---------------------------------------------------------------- items (SPEC §9)
+// Serial item-row FIFO operations (one thread at a time).
+__device__ __forceinline__ void ifree(Ctx& c, int row) {
+  c.iring[(c.E[E_ITEM_FREE_HEAD] + c.E[E_ITEM_FREE_COUNT]) % c.IC] = (int16_t)row;
+  c.E[E_ITEM_FREE_COUNT] += 1;
+}
+__device__ __forceinline__ int ialloc(Ctx& c) {
+  const int row = c.iring[c.E[E_ITEM_FREE_HEAD]];
+  c.E[E_ITEM_FREE_HEAD] = (c.E[E_ITEM_FREE_HEAD] + 1) % c.IC;
+  c.E[E_ITEM_FREE_COUNT] -= 1;
+  return row;
+}
+__device__ __forceinline__ void update_item_level(Ctx& c, int p) {
+  const uint2* inv = c.inv + p * kInv;
+  int l = 0;
+  for (int k = 0; k < kInv; k++) {
+    const uint2 w = inv[k];
+    if (!it_type(w)) break;
+    l += it_equipped(w) ? it_level(w) : 0;
+  }
+  TF(F_ITEM_LEVEL, p) = (int16_t)l;
+}
+// a brand-new item (NPC drop): stacks onto ammunition, else a new row if there is room
+__device__ __forceinline__ void receive_new(Ctx& c, int p, int type, int level) {
+  uint2* inv = c.inv + p * kInv;
+  const int k = inv_stack(inv, type, level);
+  if (k >= 0) {
+    inv[k].y += 1u;
+    return;
+  }
+  if (inv_count(inv) >= kInv) return;
+  const int row = ialloc(c);
+  inv_insert(inv, make_uint2((uint32_t)type | ((uint32_t)level << 5), 1u | ((uint32_t)row << 16)));
+}
+// an existing (unequipped, unlisted) item moving into p's inventory; returns false if its row was freed
+__device__ __forceinline__ bool receive_moved(Ctx& c, int p, uint2 w) {
+  uint2* inv = c.inv + p * kInv;
+  const int k = inv_stack(inv, it_type(w), it_level(w));
+  if (k >= 0) {
+    inv[k].y += (uint32_t)it_qty(w);
+    ifree(c, it_row(w));
+    return false;
+  }
+  if (inv_count(inv) >= kInv) {
+    ifree(c, it_row(w));
+    return false;
+  }
+  inv_insert(inv, w);
+  return true;
+}
+__device__ __forceinline__ bool has_room(const Ctx& c, int p, uint2 w) {
+  const uint2* inv = c.inv + p * kInv;
+  return inv_stack(inv, it_type(w), it_level(w)) >= 0 || inv_count(inv) < kInv;
+}
+__device__ __forceinline__ int inv_offense(const Ctx& c, int p, int style) {
+  const uint2* inv = c.inv + p * kInv;
+  int a = 0;
+  for (int k = 0; k < kInv; k++) {
+    const uint2 w = inv[k];
+    if (!it_type(w)) break;
+    a += it_equipped(w) ? item_attack(it_type(w), it_level(w), style) : 0;
+  }
+  return a;
+}
+__device__ __forceinline__ int inv_defense(const Ctx& c, int p) {
+  const uint2* inv = c.inv + p * kInv;
+  int d = 0;
+  for (int k = 0; k < kInv; k++) {
+    const uint2 w = inv[k];
+    if (!it_type(w)) break;
+    d += it_equipped(w) ? item_defense(it_type(w), it_level(w)) : 0;
+  }
+  return d;
+}
+// Frees up to one row per thread (row < 0: none), appended to the item FIFO in thread order.
+// Every thread of the block must call this.
+__device__ __forceinline__ void ring_append_ordered(Ctx& c, int row) {
+  int tot;
+  const int pre = block_prefix_sum(row >= 0 ? 1 : 0, c.wtot, &tot);
+  if (row >= 0) c.iring[(c.E[E_ITEM_FREE_HEAD] + c.E[E_ITEM_FREE_COUNT] + pre) % c.IC] = (int16_t)row;
+  __syncthreads();
+  if (threadIdx.x == 0) c.E[E_ITEM_FREE_COUNT] += tot;
+  __syncthreads();
+}
+// Item.Query.for_sale: listed-row bitmap + row -> owner | slot<<8 (block-wide, barriers inside)
+__device__ __forceinline__ void build_market(Ctx& c) {
+  const int tid = threadIdx.x;
+  if (tid < kLWords) c.lbits[tid] = 0;
+  __syncthreads();
+  if (tid < c.P) {
+    const uint2* inv = c.inv + tid * kInv;
+    for (int k = 0; k < kInv; k++) {
+      const uint2 w = inv[k];
+      if (!it_type(w)) break;
+      if (it_price(w)) {
+        const int row = it_row(w);
+        c.rmap[row] = (int16_t)(tid | (k << 8));
+        atomicOr((unsigned long long*)&c.lbits[row >> 6], 1ull << (row & 63));
+      }
+    }
+  }
+  __syncthreads();
+}
+// row of the k-th listing (ascending row), or -1
+__device__ __forceinline__ int kth_listed(const Ctx& c, int k) {
+  for (int w = 0; w < kLWords; w++) {
+    uint64_t m = c.lbits[w];
+    const int pc = __popcll(m);
+    if (k < pc) {
+      for (int i = 0; i < k; i++) m &= m - 1;
+      return (w << 6) + __builtin_ctzll(m);
+    }
+    k -= pc;
+  }
+  return -1;
 }
 
 // ---------------------------------------------------------------- NPC spawn (SPEC §5.7)
 // 25 attempts evaluated by lanes 0..24 of wave 0; accepted in attempt order up to capacity.
-__device__ void npc_spawn(Ctx& c, uint32_t tick) {
+__device__ __forceinline__ void npc_spawn(Ctx& c, uint32_t tick) {
   if (wave_id() == 0) {
     const int a = lane_id();
     const uint64_t seed = env_seed(c);
     bool valid = false;
     int r = 0, col = 0, type = 0, style = 0, level = 0;
+    uint32_t u3 = 0;
     if (a < 25) {
       const U4 u = draw(seed, tick, P_NPC_SPAWN, (uint32_t)a, 0);
       r = kLo + (int)uniform_n(u.x, kCenter);
@@ -171,6 +354,7 @@ __device__ void npc_spawn(Ctx& c, uint32_t tick) {
       type = 20 * dist >= 1024 ? 3 : 20 * dist >= 640 ? 2 : 1;
       style = (int)uniform_n(u.z, 3);
       level = sys(c, NMMO_SYS_PROGRESSION) ? (9 * dist) / 64 + 1 : 0;
+      u3 = u.w;
     }
     const uint64_t b = __ballot(valid);
     const int rank = __popcll(b & lanes_below());
@@ -198,6 +382,13 @@ __device__ void npc_spawn(Ctx& c, uint32_t tick) {
       TF(F_DS_ROW, s) = c.ring[(head + rank) % c.S];
       TF(F_STYLE, s) = (int16_t)style;
       TF(F_NPC_LEVEL, s) = (int16_t)level;
+      TF(F_DROP_ARMOR, s) = (int16_t)uniform_n(u3, 3);
+      TF(F_DROP_TOOL, s) = (int16_t)uniform_n(u3 >> 2, 5);
+      if (sys(c, NMMO_SYS_EQUIPMENT) && level > 0) {  // int(8 * (level - U[0,1)))
+        const int eq = (int)(((((uint64_t)level << 32) - u3) * 8) >> 32);
+        TF(F_EQUIP_OFFENSE, s) = (int16_t)eq;
+        TF(F_EQUIP_DEFENSE, s) = (int16_t)eq;
+      }
     }
     if (lane_id() == 0 && nacc > 0) {
       c.E[E_FREE_HEAD] = (head + nacc) % c.S;
@@ -210,12 +401,16 @@ __device__ void npc_spawn(Ctx& c, uint32_t tick) {
 }
 
 // ---------------------------------------------------------------- reset (SPEC §4)
-__device__ void reset_env(Ctx& c, uint64_t seed, int episode, int env_global) {
+__device__ __forceinline__ void reset_env(Ctx& c, uint64_t seed, int episode, int env_global) {
   const int tid = threadIdx.x, nt = blockDim.x, S = c.S, P = c.P;
   for (int i = tid; i < kNFLive * S; i += nt) c.T[i] = 0;
   for (int i = tid; i < kBitmapWords; i += nt) c.dep[i] = 0;
   for (int i = tid; i < S; i += nt) c.ring[i] = i < c.N ? (int16_t)(P + 1 + i) : (int16_t)0;
   if (tid < NMMO_NE) c.E[tid] = 0;
+  if (c.items) {
+    for (int i = tid; i < P * kInv; i += nt) c.inv[i] = make_uint2(0u, 0u);
+    for (int i = tid; i < c.IC; i += nt) c.iring[i] = (int16_t)(i + 1);
+  }
   __syncthreads();
   if (tid == 0) {
     c.E[E_SEED_LO] = (int)(uint32_t)seed;
@@ -226,6 +421,7 @@ __device__ void reset_env(Ctx& c, uint64_t seed, int episode, int env_global) {
     c.E[E_FREE_COUNT] = c.N;
     c.E[E_NPC_NEXT_ID] = -1;
     c.E[E_PLAYERS_ALIVE] = P;
+    c.E[E_ITEM_FREE_COUNT] = c.IC;
   }
   __syncthreads();
   {  // copy the bank map into the env's mutable map (16 B per lane)
@@ -256,13 +452,13 @@ __device__ void reset_env(Ctx& c, uint64_t seed, int episode, int env_global) {
 }
 
 // ---------------------------------------------------------------- NPC AI (SPEC §6)
-__device__ inline bool player_valid(const Ctx& c, int id, int r, int col) {
+__device__ __forceinline__ bool player_valid(const Ctx& c, int id, int r, int col) {
   if (id <= 0 || id > c.P) return false;
   const int s = id - 1;
   return TF(F_ALIVE, s) && TF(F_HEALTH, s) > 0 && linf(r, col, TF(F_ROW, s), TF(F_COL, s)) <= kVision;
 }
 
-__device__ void npc_decide(Ctx& c, int n, int& move, int& tgt, int& sty) {
+__device__ __forceinline__ void npc_decide(Ctx& c, int n, int& move, int& tgt, int& sty) {
   const int r = TF(F_ROW, n), col = TF(F_COL, n), id = TF(F_ID, n);
   const U4 u = draw(env_seed(c), (uint32_t)c.E[E_TICK], P_NPC_MOVE, (uint32_t)(-id), 0);
   move = -1;
@@ -328,7 +524,7 @@ __device__ void npc_decide(Ctx& c, int n, int& move, int& tgt, int& sty) {
 }
 
 // ---------------------------------------------------------------- combat (SPEC §5.3)
-__device__ inline int combat_level(const Ctx& c, int s) {
+__device__ __forceinline__ int combat_level(const Ctx& c, int s) {
   const int nsk = s < c.P ? 8 : 3;
   int l = 0;
   for (int k = 0; k < nsk; k++) l = max(l, (int)TF(F_MELEE_LEVEL + 2 * k, s));
@@ -336,7 +532,7 @@ __device__ inline int combat_level(const Ctx& c, int s) {
 }
 
 // Attack.call validity + combat.attack damage on the current LDS state; -1 = no attack.
-__device__ int eval_attack(const Ctx& c, int x, int sty, int t) {
+__device__ __forceinline__ int eval_attack(const Ctx& c, int x, int sty, int t) {
   if (!TF(F_ALIVE, x) || TF(F_HEALTH, x) <= 0) return -1;
   if (!TF(F_ALIVE, t) || TF(F_HEALTH, t) <= 0 || t == x) return -1;
   if (x < c.P && t < c.P && TF(F_TIME_ALIVE, t) < c.cfg->spawn_immunity) return -1;
@@ -345,9 +541,9 @@ __device__ int eval_attack(const Ctx& c, int x, int sty, int t) {
   const bool prog = sys(c, NMMO_SYS_PROGRESSION);
   int offense = prog ? 10 + 5 * TF(F_MELEE_LEVEL + 2 * sty, x) : 30;
   int defense = prog ? 5 * combat_level(c, t) : 0;
-  if (sys(c, NMMO_SYS_EQUIPMENT)) {
-    offense += TF(F_EQUIP_OFFENSE, x);
-    defense += TF(F_EQUIP_DEFENSE, t);
+  if (sys(c, NMMO_SYS_EQUIPMENT)) {  // players: equipped items; NPCs: spawn-time equipment
+    offense += x < c.P ? (c.items ? inv_offense(c, x, sty) : 0) : TF(F_EQUIP_OFFENSE, x);
+    defense += t < c.P ? (c.items ? inv_defense(c, t) : 0) : TF(F_EQUIP_DEFENSE, t);
   }
   const int e0 = TF(F_MELEE_EXP, t), e1 = TF(F_RANGE_EXP, t), e2 = TF(F_MAGE_EXP, t);
   const int mx = max(e0, max(e1, e2)), mn = min(e0, min(e1, e2));
@@ -361,7 +557,7 @@ __device__ int eval_attack(const Ctx& c, int x, int sty, int t) {
   return d4 >> 2;
 }
 
-__device__ void apply_attack(Ctx& c, int x, int sty, int t, int dmg, int tick) {
+__device__ __forceinline__ void apply_attack(Ctx& c, int x, int sty, int t, int dmg, int tick) {
   TF(F_ATTACKER_ID, t) = TF(F_ID, x);
   if (x < c.P && sys(c, NMMO_SYS_PROGRESSION)) {
     const int f = F_MELEE_EXP + 2 * sty;
@@ -376,16 +572,90 @@ __device__ void apply_attack(Ctx& c, int x, int sty, int t, int dmg, int tick) {
   if (h == 0) TF(F_PLAYER_KILLS, x) += 1;
   TF(F_LATEST_COMBAT_TICK, x) = (int16_t)(tick + 1);
   TF(F_LATEST_COMBAT_TICK, t) = (int16_t)(tick + 1);
+  if (x < c.P) {  // ammunition and loot are applied after the phase, in slot order
+    if (c.equip) c.fired[x] = 1;
+    if (h == 0) c.kill[x] = (int16_t)t;
+  }
+}
+
+// fire one unit of x's equipped ammunition of this style (serial)
+__device__ __forceinline__ void fire_ammo(Ctx& c, int x, int style) {
+  uint2* inv = c.inv + x * kInv;
+  for (int k = 0; k < kInv; k++) {
+    const uint2 w = inv[k];
+    if (!it_type(w)) break;
+    if (!it_equipped(w) || it_type(w) != T_WHETSTONE + style) continue;
+    inv[k].y -= 1u;
+    if (it_qty(inv[k]) == 0) {
+      ifree(c, it_row(w));
+      inv_remove(inv, k);
+      update_item_level(c, x);
+    }
+    break;
+  }
+}
+
+// a player killed t: gold, then t's items (player) or drops (NPC) (serial; SPEC §9 Death)
+__device__ __forceinline__ void loot(Ctx& c, int x, int t) {
+  if (sys(c, NMMO_SYS_EXCHANGE)) {
+    TF(F_GOLD, x) = (int16_t)(TF(F_GOLD, x) + TF(F_GOLD, t));
+    TF(F_GOLD, t) = 0;
+  }
+  if (!c.items) return;
+  if (t < c.P) {
+    uint2* inv = c.inv + t * kInv;
+    while (it_type(inv[0])) {
+      uint2 w = inv[0];
+      w.x &= 0x1FFu;  // unequipped, unlisted
+      inv_remove(inv, 0);
+      receive_moved(c, x, w);
+    }
+    update_item_level(c, t);
+  } else {
+    const int lvl = TF(F_NPC_LEVEL, t) > 0 ? TF(F_NPC_LEVEL, t) : 1;
+    if (sys(c, NMMO_SYS_EQUIPMENT)) receive_new(c, x, T_HAT + TF(F_DROP_ARMOR, t), lvl);
+    if (sys(c, NMMO_SYS_PROFESSION)) receive_new(c, x, T_ROD + TF(F_DROP_TOOL, t), lvl);
+  }
 }
 
 // ---------------------------------------------------------------- the tick (SPEC §5)
-__device__ void tick_env(Ctx& c, const int32_t* __restrict__ act, float* rew, uint8_t* term,
+__device__ __forceinline__ bool acts(const Ctx& c, int s) { return TF(F_ALIVE, s) && TF(F_HEALTH, s) > 0; }
+__device__ __forceinline__ bool same_tile(const Ctx& c, int a, int b) {
+  return TF(F_ROW, a) == TF(F_ROW, b) && TF(F_COL, a) == TF(F_COL, b);
+}
+// slot of player s's k-th visible entity (previous obs' Entity row k), or -1
+__device__ __forceinline__ int vis_kth(const Ctx& c, int s, int NW, int k) {
+  for (int w = 0; w < NW; w++) {
+    uint64_t m = c.vism[s * NW + w];
+    const int pc = __popcll(m);
+    if (k < pc) {
+      for (int i = 0; i < k; i++) m &= m - 1;  // clear the k lowest set bits
+      return (c.rp[(w << 6) + __builtin_ctzll(m) + 1] >> 16) & 511;
+    }
+    k -= pc;
+  }
+  return -1;
+}
+// lowest player slot standing on `tile` (position hash), 0x7FFF if none
+__device__ __forceinline__ int hash_min(const Ctx& c, int tile) {
+  int hh = (int)(h32((uint32_t)tile) & (kHash - 1));
+  while (true) {
+    const int k = c.hkey[hh];
+    if (k == tile) return c.hmin[hh];
+    if (k == -1) return 0x7FFF;
+    hh = (hh + 1) & (kHash - 1);
+  }
+}
+
+__device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act, float* rew, uint8_t* term,
                          uint8_t* trunc, uint8_t* mask) {
   const int tid = threadIdx.x, nt = blockDim.x, S = c.S, P = c.P;
   const int s = tid;
   const int tick = c.E[E_TICK];
   const int nslots = P + c.E[E_NPC_COUNT];
   const bool inslot = s < nslots;
+  const bool items = c.items;
+  const uint64_t seed = env_seed(c);
 
   if (s < P) c.pres[s] = (uint8_t)TF(F_ALIVE, s);
   for (int k = tid; k < rp_groups(S) * 4; k += nt) c.rp[k] = -1;
@@ -393,6 +663,7 @@ __device__ void tick_env(Ctx& c, const int32_t* __restrict__ act, float* rew, ui
     c.hkey[k] = -1;
     c.hmin[k] = 0x7FFF;
   }
+  if (c.exch && tid < kLWords) c.lbits[tid] = 0;
   __syncthreads();
   if (s < S) {
     const bool in = inslot && TF(F_ALIVE, s);  // in the realm => health > 0 at tick start
@@ -400,16 +671,28 @@ __device__ void tick_env(Ctx& c, const int32_t* __restrict__ act, float* rew, ui
     c.sp[s] = in ? pos : -1;
     if (in) c.rp[TF(F_DS_ROW, s)] = pos | (s << 16);
   }
+  if (c.exch && s < P) {  // listings of the previous observation (Buy.MarketItem index space)
+    const uint2* inv = c.inv + s * kInv;
+    for (int k = 0; k < kInv; k++) {
+      const uint2 w = inv[k];
+      if (!it_type(w)) break;
+      if (it_price(w)) {
+        const int row = it_row(w);
+        c.rmap[row] = (int16_t)(s | (k << 8));
+        atomicOr((unsigned long long*)&c.lbits[row >> 6], 1ull << (row & 63));
+      }
+    }
+  }
   __syncthreads();
   NMMO_STAMP(1);
 
   // 0. decode (Env._validate_actions) against the previous observation's state.
-  // Attack.Target k is the k-th visible entity in datastore-row order (the previous obs' Entity
-  // row k). Every wave builds the player x row visibility bitmap for its 64 rows with one
+  // Target indices select the k-th visible entity in datastore-row order (the previous obs'
+  // Entity row k). Every wave builds the player x row visibility bitmap for its 64 rows with one
   // ballot per player; each player then selects its k-th set bit with popcounts.
   const int NW = (S + 63) >> 6;
   const bool combat = sys(c, NMMO_SYS_COMBAT);
-  if (combat) {
+  if (combat || items) {
     // Packed 16-bit window test: entity (col+7, row+7) minus player (col, row) with one
     // v_pk_sub_u16; both halves <= 14 <=> L-inf <= 7 (out-of-window values wrap to >= 0x8000).
     typedef unsigned short us2 __attribute__((ext_vector_type(2)));
@@ -444,22 +727,48 @@ __device__ void tick_env(Ctx& c, const int32_t* __restrict__ act, float* rew, ui
   __syncthreads();
   NMMO_STAMP(13);
   int my_move = -1, my_tgt = -1, my_sty = 0;
+  int use_row = -1, destroy_row = -1, sell_row = -1, sell_price = 0;
+  if (s < P) {
+    c.a_buy[s] = c.a_give[s] = c.a_givet[s] = c.a_ggt[s] = -1;
+    c.a_gga[s] = 0;
+    c.kill[s] = -1;
+    c.fired[s] = 0;
+  }
   if (s < P && c.pres[s]) {
     const int32_t* a = act + (size_t)s * kHeads;
     const int dmove = a[8], dsty = a[0], dk = a[1];
     if (dmove >= 0 && dmove < 5) my_move = dmove;
     if (combat && dsty >= 0 && dsty < 3 && dk >= 0 && dk < kNObs) {
-      int k = dk;
-      for (int w = 0; w < NW; w++) {
-        uint64_t m = c.vism[s * NW + w];
-        const int pc = __popcll(m);
-        if (k < pc) {
-          for (int i = 0; i < k; i++) m &= m - 1;  // clear the k lowest set bits
-          my_tgt = (c.rp[(w << 6) + __builtin_ctzll(m) + 1] >> 16) & 511;
-          my_sty = dsty;
-          break;
+      my_tgt = vis_kth(c, s, NW, dk);
+      my_sty = my_tgt >= 0 ? dsty : 0;
+    }
+    if (items) {  // InventoryItem k -> item row of the previous obs' inventory slot k
+      const uint2* inv = c.inv + s * kInv;
+      const int n = inv_count(inv);
+      auto row_of = [&](int k) { return (k >= 0 && k < n) ? it_row(inv[k]) : -1; };
+      use_row = row_of(a[11]);
+      destroy_row = row_of(a[3]);
+      if (a[5] >= 0 && a[5] < kNObs) {
+        const int gr = row_of(a[4]);
+        const int t = gr >= 0 ? vis_kth(c, s, NW, a[5]) : -1;
+        if (t >= 0) {
+          c.a_give[s] = (int16_t)gr;
+          c.a_givet[s] = (int16_t)t;
         }
-        k -= pc;
+      }
+      if (c.exch) {
+        if (a[7] >= 0 && a[7] < kNObs && a[6] >= 0 && a[6] < 99) {
+          const int t = vis_kth(c, s, NW, a[7]);
+          if (t >= 0) {
+            c.a_ggt[s] = (int16_t)t;
+            c.a_gga[s] = (int16_t)(a[6] + 1);
+          }
+        }
+        if (a[10] >= 0 && a[10] < 99) {
+          sell_row = row_of(a[9]);
+          sell_price = a[10] + 1;
+        }
+        if (a[2] >= 0 && a[2] < NMMO_MARKET_ROWS) c.a_buy[s] = (int16_t)kth_listed(c, a[2]);
       }
     }
   }
@@ -477,8 +786,9 @@ __device__ void tick_env(Ctx& c, const int32_t* __restrict__ act, float* rew, ui
   __syncthreads();
   NMMO_STAMP(2);
 
-  // 2. players.update / npcs.update
-  bool eat = false;
+  // 2. players.update / npcs.update. Every player in the realm registers its tile in the
+  // position hash (lowest slot per tile via atomicMin): first-in-slot-order harvests.
+  const bool resource = sys(c, NMMO_SYS_RESOURCE);
   int tile = 0, hslot = -1;
   if (inslot && TF(F_ALIVE, s)) {
     if (TF(F_DAMAGE, s) == 0) TF(F_ATTACKER_ID, s) = 0;
@@ -486,21 +796,26 @@ __device__ void tick_env(Ctx& c, const int32_t* __restrict__ act, float* rew, ui
     TF(F_TIME_ALIVE, s) += 1;
     if (s >= P) {
       TF(F_HEALTH, s) = (int16_t)min(100, TF(F_HEALTH, s) + 1);
-    } else if (sys(c, NMMO_SYS_RESOURCE)) {
-      const int org = TF(F_HEALTH, s);
-      int h = org;
-      const int food = TF(F_FOOD, s), water = TF(F_WATER, s);
-      if (food > 50 && water > 50) h = min(100, h + 10);
-      const int dmg = TF(F_RESILIENT, s) ? 5 : 10;
-      if (food == 0) h = max(0, h - dmg);
-      if (water == 0) h = max(0, h - dmg);
-      TF(F_HEALTH, s) = (int16_t)h;
-      TF(F_HEALTH_RESTORE, s) = (int16_t)(h - org);
-      TF(F_FOOD, s) = (int16_t)max(0, food - 5);
+    } else {
       const int r = TF(F_ROW, s), col = TF(F_COL, s);
       tile = r * kSize + col;
-      if (c.mat[tile] == M_FOILAGE) {  // first player in slot order on the tile wins:
-        int hh = (int)(h32((uint32_t)tile) & (kHash - 1));  // atomicMin of slots per tile
+      if (resource) {
+        const int org = TF(F_HEALTH, s);
+        int h = org;
+        const int food = TF(F_FOOD, s), water = TF(F_WATER, s);
+        if (food > 50 && water > 50) h = min(100, h + 10);
+        const int dmg = TF(F_RESILIENT, s) ? 5 : 10;
+        if (food == 0) h = max(0, h - dmg);
+        if (water == 0) h = max(0, h - dmg);
+        TF(F_HEALTH, s) = (int16_t)h;
+        TF(F_HEALTH_RESTORE, s) = (int16_t)(h - org);
+        TF(F_FOOD, s) = (int16_t)max(0, food - 5);
+        const bool drink = c.mat[tile - kSize] == M_WATER || c.mat[tile + kSize] == M_WATER ||
+                           c.mat[tile - 1] == M_WATER || c.mat[tile + 1] == M_WATER;
+        TF(F_WATER, s) = (int16_t)(drink ? 100 : max(0, water - 5));
+      }
+      if ((resource && c.mat[tile] == M_FOILAGE) || c.prof) {
+        int hh = (int)(h32((uint32_t)tile) & (kHash - 1));
         while (true) {
           const int old = atomicCAS(&c.hkey[hh], -1, tile);
           if (old == -1 || old == tile) break;
@@ -509,18 +824,225 @@ __device__ void tick_env(Ctx& c, const int32_t* __restrict__ act, float* rew, ui
         atomicMin(&c.hmin[hh], s);
         hslot = hh;
       }
-      const bool drink = c.mat[tile - kSize] == M_WATER || c.mat[tile + kSize] == M_WATER ||
-                         c.mat[tile - 1] == M_WATER || c.mat[tile + 1] == M_WATER;
-      TF(F_WATER, s) = (int16_t)(drink ? 100 : max(0, water - 5));
     }
   }
   __syncthreads();
   NMMO_STAMP(3);
-  eat = hslot >= 0 && c.hmin[hslot] == s;
-  if (eat) {
+  const bool first_on_tile = hslot >= 0 && c.hmin[hslot] == s;
+  if (resource && first_on_tile && c.mat[tile] == M_FOILAGE) {
     TF(F_FOOD, s) = 100;
     c.mat[tile] = M_SCRUB;
     atomicOr(&c.dep[tile >> 5], 1u << (tile & 31));
+  }
+  if (c.prof) {
+    // Professions: adjacent Fish (depleted by the lowest adjacent slot; every Fish 4-neighbour
+    // of a player is depleted) then the on-tile Herb/Ore/Tree/Crystal (first on the tile).
+    int fishm = 0, q_on = -1;
+    bool got = false;
+    if (hslot >= 0) {
+      const int nb[4] = {tile - kSize, tile + kSize, tile - 1, tile + 1};
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        if (c.mat[nb[q]] != M_FISH) continue;
+        fishm |= 1 << q;
+        const int f = nb[q];
+        const int w = min(min(hash_min(c, f - kSize), hash_min(c, f + kSize)),
+                          min(hash_min(c, f - 1), hash_min(c, f + 1)));
+        got = got || w == s;
+      }
+      if (first_on_tile) {
+        const int m = c.mat[tile];
+        q_on = m == M_HERB ? 0 : m == M_ORE ? 1 : m == M_TREE ? 2 : m == M_CRYSTAL ? 3 : -1;
+      }
+    }
+    int held = -1, held_lvl = 1, need = 0, n = 0;
+    uint2* inv = c.inv + (s < P ? s : 0) * kInv;
+    const int out_type = q_on == 0 ? T_POTION : q_on == 1 ? T_WHETSTONE : q_on == 2 ? T_ARROW : T_RUNES;
+    if (got || q_on >= 0) {
+      for (int k = 0; k < kInv; k++) {
+        const uint2 w = inv[k];
+        if (!it_type(w)) break;
+        n++;
+        if (it_equipped(w) && equip_slot(it_type(w)) == 3) {
+          held = it_type(w);
+          held_lvl = it_level(w);
+        }
+      }
+    }
+    const int lvl_f = held == T_ROD ? held_lvl : 1;
+    const int lvl_on = q_on >= 0 && held == T_GLOVES + q_on ? held_lvl : 1;
+    const bool new_f = got && n < kInv;
+    const bool stack_on = q_on >= 0 && inv_stack(inv, out_type, lvl_on) >= 0;
+    const bool new_on = q_on >= 0 && !stack_on && n + (new_f ? 1 : 0) < kInv;
+    need = (new_f ? 1 : 0) + (new_on ? 1 : 0);
+    int tot;
+    const int pre = block_prefix_sum(need, c.wtot, &tot);  // rows in slot order (barriers inside)
+    const int head = c.E[E_ITEM_FREE_HEAD];
+    if (fishm) {
+      const int nb[4] = {tile - kSize, tile + kSize, tile - 1, tile + 1};
+#pragma unroll
+      for (int q = 0; q < 4; q++)
+        if (fishm & (1 << q)) {
+          c.mat[nb[q]] = M_OCEAN;
+          atomicOr(&c.dep[nb[q] >> 5], 1u << (nb[q] & 31));
+        }
+    }
+    int ri = pre;
+    if (got) {
+      if (new_f) {
+        const int row = c.iring[(head + ri++) % c.IC];
+        inv_insert(inv, make_uint2((uint32_t)T_RATION | ((uint32_t)lvl_f << 5), 1u | ((uint32_t)row << 16)));
+      }
+      const int ex = TF(F_FISHING_EXP, s) + 30 * lvl_f;
+      TF(F_FISHING_EXP, s) = (int16_t)ex;
+      const int nl = level_at_exp(ex);
+      if (nl > TF(F_FISHING_LEVEL, s)) TF(F_FISHING_LEVEL, s) = (int16_t)nl;
+    }
+    if (q_on >= 0) {
+      const int to = q_on == 0 ? M_WEEDS : q_on == 1 ? M_SLAG : q_on == 2 ? M_STUMP : M_FRAGMENT;
+      c.mat[tile] = (uint8_t)to;
+      atomicOr(&c.dep[tile >> 5], 1u << (tile & 31));
+      if (stack_on) {
+        inv[inv_stack(inv, out_type, lvl_on)].y += 1u;
+      } else if (new_on) {
+        const int row = c.iring[(head + ri++) % c.IC];
+        inv_insert(inv, make_uint2((uint32_t)out_type | ((uint32_t)lvl_on << 5), 1u | ((uint32_t)row << 16)));
+      }
+      const int fe = F_HERBALISM_EXP + 2 * q_on;
+      const int ex = TF(fe, s) + (q_on == 0 ? 30 : 15) * lvl_on;
+      TF(fe, s) = (int16_t)ex;
+      const int nl = level_at_exp(ex);
+      if (nl > TF(fe - 1, s)) TF(fe - 1, s) = (int16_t)nl;
+    }
+    __syncthreads();
+    if (tid == 0 && tot) {
+      c.E[E_ITEM_FREE_HEAD] = (head + tot) % c.IC;
+      c.E[E_ITEM_FREE_COUNT] -= tot;
+    }
+  }
+  __syncthreads();
+
+  if (items) {
+    // 3. Use (priority 10): own inventory only -> parallel; consumed rows freed in slot order
+    int freed = -1;
+    if (s < P && use_row >= 0 && acts(c, s)) {
+      uint2* inv = c.inv + s * kInv;
+      const int k = inv_find(inv, use_row);
+      if (k >= 0 && !it_price(inv[k])) {
+        const uint2 w = inv[k];
+        const int type = it_type(w), lvl = it_level(w), slot = equip_slot(type);
+        if (slot >= 0) {
+          if (it_equipped(w)) {
+            inv[k].x &= ~(1u << 9);
+          } else if (lvl <= requirement_level(c.T, S, s, type)) {
+            for (int j = 0; j < kInv; j++) {
+              if (!it_type(inv[j])) break;
+              if (it_equipped(inv[j]) && equip_slot(it_type(inv[j])) == slot) inv[j].x &= ~(1u << 9);
+            }
+            inv[k].x |= 1u << 9;
+          }
+          update_item_level(c, s);
+        } else if (lvl <= requirement_level(c.T, S, s, type)) {
+          const int rs = 50 + 5 * lvl;
+          if (type == T_RATION) {
+            TF(F_FOOD, s) = (int16_t)min(100, TF(F_FOOD, s) + rs);
+            TF(F_WATER, s) = (int16_t)min(100, TF(F_WATER, s) + rs);
+          } else {
+            TF(F_HEALTH, s) = (int16_t)min(100, TF(F_HEALTH, s) + rs);
+          }
+          inv[k].y -= 1u;
+          if (it_qty(inv[k]) == 0) {
+            freed = it_row(w);
+            inv_remove(inv, k);
+          }
+        }
+      }
+    }
+    ring_append_ordered(c, freed);
+
+    // Buy (priority 20): buyers in shuffled order (key draw(tick, BUY_ORDER, id), ties by id),
+    // replayed by thread 0 against the row -> owner map of the tick-start listings
+    if (c.exch) {
+      const bool isb = s < P && c.a_buy[s] >= 0;
+      int nbuy;
+      block_prefix_count(isb, c.wtot, &nbuy);
+      if (nbuy > 0) {
+        if (isb) c.ikey[s] = draw(seed, (uint32_t)tick, P_BUY_ORDER, (uint32_t)(s + 1), 0).x;
+        __syncthreads();
+        if (isb) {
+          const uint32_t key = c.ikey[s];
+          int rank = 0;
+          for (int q = 0; q < P; q++)
+            if (c.a_buy[q] >= 0) rank += (c.ikey[q] < key || (c.ikey[q] == key && q < s)) ? 1 : 0;
+          c.order[rank] = (int16_t)s;
+        }
+        __syncthreads();
+        if (tid == 0) {
+          for (int i = 0; i < nbuy; i++) {
+            const int b = c.order[i];
+            if (!acts(c, b)) continue;
+            const int row = c.a_buy[b];
+            const int owner = c.rmap[row] < 0 ? -1 : (c.rmap[row] & 255);
+            if (owner < 0 || owner == b) continue;
+            uint2* oinv = c.inv + owner * kInv;
+            const int k = inv_find(oinv, row);
+            if (k < 0) continue;
+            uint2 w = oinv[k];
+            const int price = it_price(w);
+            if (!price || TF(F_GOLD, b) < price || !has_room(c, b, w)) continue;
+            TF(F_GOLD, b) = (int16_t)(TF(F_GOLD, b) - price);
+            TF(F_GOLD, owner) = (int16_t)(TF(F_GOLD, owner) + price);
+            w.x &= 0x1FFu;
+            inv_remove(oinv, k);
+            c.rmap[row] = receive_moved(c, b, w) ? (int16_t)b : (int16_t)-1;
+          }
+        }
+        __syncthreads();
+      }
+    }
+
+    // Give / GiveGold (priority 30): cross-player, replayed by thread 0 in slot order
+    {
+      const bool isg = s < P && (c.a_givet[s] >= 0 || c.a_ggt[s] >= 0);
+      int ng;
+      const int gpos = block_prefix_count(isg, c.wtot, &ng);
+      if (isg) c.order[gpos] = (int16_t)s;
+      __syncthreads();
+      if (tid == 0) {
+        for (int i = 0; i < ng; i++) {
+          const int p = c.order[i];
+          if (!acts(c, p)) continue;
+          int t = c.a_givet[p];
+          if (t >= 0 && t < P && t != p && acts(c, t) && same_tile(c, t, p)) {
+            uint2* inv = c.inv + p * kInv;
+            const int k = inv_find(inv, c.a_give[p]);
+            if (k >= 0 && !it_equipped(inv[k]) && !it_price(inv[k]) && has_room(c, t, inv[k])) {
+              const uint2 w = inv[k];
+              inv_remove(inv, k);
+              receive_moved(c, t, w);
+            }
+          }
+          t = c.a_ggt[p];
+          if (t >= 0 && t < P && t != p && acts(c, t) && c.a_gga[p] <= TF(F_GOLD, p) && same_tile(c, t, p)) {
+            TF(F_GOLD, p) = (int16_t)(TF(F_GOLD, p) - c.a_gga[p]);
+            TF(F_GOLD, t) = (int16_t)(TF(F_GOLD, t) + c.a_gga[p]);
+          }
+        }
+      }
+      __syncthreads();
+    }
+
+    // Destroy (priority 40): own inventory, rows freed in slot order
+    freed = -1;
+    if (s < P && destroy_row >= 0 && acts(c, s)) {
+      uint2* inv = c.inv + s * kInv;
+      const int k = inv_find(inv, destroy_row);
+      if (k >= 0 && !it_equipped(inv[k]) && !it_price(inv[k])) {
+        freed = destroy_row;
+        inv_remove(inv, k);
+      }
+    }
+    ring_append_ordered(c, freed);
   }
 
   // 3a. Attack (priority 50)
@@ -572,6 +1094,23 @@ __device__ void tick_env(Ctx& c, const int32_t* __restrict__ act, float* rew, ui
     }
   }
   __syncthreads();
+  if (items || sys(c, NMMO_SYS_EXCHANGE)) {
+    // ammunition and loot of the executed player attacks, in slot order (equipment sums and
+    // every attack's validity are unaffected by them, so deferring is exact)
+    const bool nd = s < P && (c.fired[s] || c.kill[s] >= 0);
+    int nn;
+    const int pos = block_prefix_count(nd, c.wtot, &nn);
+    if (nd) c.order[pos] = (int16_t)s;
+    __syncthreads();
+    if (tid == 0) {
+      for (int i = 0; i < nn; i++) {
+        const int x = c.order[i];
+        if (c.fired[x]) fire_ammo(c, x, c.asty[x]);
+        if (c.kill[x] >= 0) loot(c, x, c.kill[x]);
+      }
+    }
+    __syncthreads();
+  }
   NMMO_STAMP(5);
 
   // 3b. Move (priority 60)
@@ -584,6 +1123,13 @@ __device__ void tick_env(Ctx& c, const int32_t* __restrict__ act, float* rew, ui
       const int progress = 64 - linf(80, 80, nr, nc);
       if (progress > TF(F_EXPLORATION, s)) TF(F_EXPLORATION, s) = (int16_t)progress;
     }
+  }
+  // Sell (priority 70): own inventory
+  if (c.exch && s < P && sell_row >= 0 && acts(c, s)) {
+    uint2* inv = c.inv + s * kInv;
+    const int k = inv_find(inv, sell_row);
+    if (k >= 0 && !it_equipped(inv[k]))
+      inv[k].x = (inv[k].x & 0x3FFu) | ((uint32_t)sell_price << 10) | ((uint32_t)tick << 17);
   }
   __syncthreads();
   NMMO_STAMP(6);
@@ -599,6 +1145,22 @@ __device__ void tick_env(Ctx& c, const int32_t* __restrict__ act, float* rew, ui
     c.ring[(c.E[E_FREE_HEAD] + c.E[E_FREE_COUNT] + dpos) % S] = TF(F_DS_ROW, s);
     TF(F_ALIVE, s) = 0;
     if (s < P) TF(F_DIED_TICK, s) = (int16_t)(tick + 1);
+  }
+  if (items) {  // unlooted items of the dead are destroyed: rows freed in (slot, inventory) order
+    uint2* inv = c.inv + (s < P ? s : 0) * kInv;
+    const int n = (dead && s < P) ? inv_count(inv) : 0;
+    int tot;
+    const int pre = block_prefix_sum(n, c.wtot, &tot);
+    if (n) {
+      const int base = c.E[E_ITEM_FREE_HEAD] + c.E[E_ITEM_FREE_COUNT] + pre;
+      for (int k = 0; k < n; k++) {
+        c.iring[(base + k) % c.IC] = (int16_t)it_row(inv[k]);
+        inv[k] = make_uint2(0u, 0u);
+      }
+      TF(F_ITEM_LEVEL, s) = 0;
+    }
+    __syncthreads();
+    if (tid == 0) c.E[E_ITEM_FREE_COUNT] += tot;
   }
   __syncthreads();
   if (tid == 0) {
@@ -628,8 +1190,7 @@ __device__ void tick_env(Ctx& c, const int32_t* __restrict__ act, float* rew, ui
   __syncthreads();
   NMMO_STAMP(7);
 
-  // 5-6. tick += 1; map.step respawn of depleted tiles
-  const uint64_t seed = env_seed(c);
+  // 5-6. tick += 1; map.step respawn of depleted tiles; exchange.step listing expiry
   {
     const uint8_t* base = c.bank + (size_t)c.E[E_MAP_ID] * kTiles;
     for (int w = tid; w < kBitmapWords; w += nt) {
@@ -647,6 +1208,13 @@ __device__ void tick_env(Ctx& c, const int32_t* __restrict__ act, float* rew, ui
         }
       }
       c.dep[w] = keepb;
+    }
+  }
+  if (c.exch && s < P) {
+    uint2* inv = c.inv + s * kInv;
+    for (int k = 0; k < kInv; k++) {
+      if (!it_type(inv[k])) break;
+      if (it_price(inv[k]) && tick + 1 - it_ltick(inv[k]) > 5) inv[k].x &= 0x3FFu;
     }
   }
   __syncthreads();
@@ -676,6 +1244,33 @@ __device__ void tick_env(Ctx& c, const int32_t* __restrict__ act, float* rew, ui
   }
 }
 
+// End-of-tick listings for the obs and policy kernels (Market rows, Buy mask): ascending row.
+__device__ __forceinline__ void store_market(Ctx& c, const DevState& st, int e) {
+  const int tid = threadIdx.x;
+  if (!c.exch) {
+    if (tid == 0) st.mcount[e] = 0;
+    return;
+  }
+  build_market(c);
+  int32_t* ml = st.mlist + (size_t)e * NMMO_MARKET_ROWS;
+  for (int row = tid + 1; row <= c.IC; row += blockDim.x) {
+    const int w = row >> 6;
+    const uint64_t m = c.lbits[w];
+    if (!((m >> (row & 63)) & 1)) continue;
+    int rank = __popcll(m & ((1ull << (row & 63)) - 1ull));
+    for (int j = 0; j < w; j++) rank += __popcll(c.lbits[j]);
+    if (rank < NMMO_MARKET_ROWS) {
+      const int rm = c.rmap[row];
+      ml[rank] = row | ((rm & 255) << 16) | ((rm >> 8) << 24);
+    }
+  }
+  if (tid == 0) {
+    int n = 0;
+    for (int j = 0; j < kLWords; j++) n += __popcll(c.lbits[j]);
+    st.mcount[e] = min(n, NMMO_MARKET_ROWS);
+  }
+}
+
 // ---------------------------------------------------------------- kernel
 // mode 0: step (auto-reset envs that are done); mode 1: reset every env.
 __global__ void tick_kernel(DevState st, const int32_t* __restrict__ actions,
@@ -701,6 +1296,10 @@ __global__ void tick_kernel(DevState st, const int32_t* __restrict__ actions,
     }
     __syncthreads();
     reset_env(c, seed, episode, env_global);
+    if (!c.items) {  // item state is not staged in LDS without the Item system; reset it in HBM
+      for (int i = threadIdx.x; i < c.P * kInv; i += blockDim.x) st.items[(size_t)e * c.P * kInv + i] = make_uint2(0u, 0u);
+      for (int i = threadIdx.x; i < c.IC; i += blockDim.x) st.iring[(size_t)e * c.IC + i] = (int16_t)(i + 1);
+    }
     for (int p = threadIdx.x; p < c.P; p += blockDim.x) {
       if (rew) rew[o + p] = 0.f;
       if (term) term[o + p] = 0;
@@ -712,6 +1311,7 @@ __global__ void tick_kernel(DevState st, const int32_t* __restrict__ actions,
   }
   __syncthreads();
   NMMO_STAMP(10);
+  store_market(c, st, e);
   store_env(c, st, e);
   __syncthreads();
   NMMO_STAMP(11);
@@ -721,21 +1321,53 @@ hipError_t launch_tick(const DevState& st, const int32_t* actions, const uint64_
                        float* rew, uint8_t* term, uint8_t* trunc, uint8_t* mask, int mode,
                        hipStream_t stream) {
   const int threads = ((st.S + 63) / 64) * 64;
-  hipLaunchKernelGGL(tick_kernel, dim3(st.n_envs), dim3(threads), tick_lds_bytes(st.S), stream,
+  const size_t lds = tick_lds_bytes(st.S, st.P, (st.cfg.systems & NMMO_SYS_ITEM) != 0);
+  hipLaunchKernelGGL(tick_kernel, dim3(st.n_envs), dim3(threads), lds, stream,
                      st, actions, env_seeds, rew, term, trunc, mask, mode);
   return hipGetLastError();
 }
 
-// set_state support: the depleted-tile bitmap is derived state (bit <=> material != bank).
+hipError_t init_kernels() {
+  return hipFuncSetAttribute(reinterpret_cast<const void*>(tick_kernel),
+                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+}
+
+// set_state support: derived state is rebuilt from the blob — the depleted-tile bitmap
+// (bit <=> material != bank) and the end-of-tick market list (listed rows, ascending).
 __global__ void rebuild_dep_kernel(DevState st) {
-  const int e = blockIdx.x;
+  __shared__ uint64_t lbits[kLWords];
+  __shared__ int16_t rmap[kInv * 128 + 1];
+  const int e = blockIdx.x, tid = threadIdx.x;
   const int32_t* E = st.env + (size_t)e * NMMO_NE;
   const uint8_t* mat = st.mat + (size_t)e * kTiles;
   const uint8_t* base = st.bank + (size_t)E[E_MAP_ID] * kTiles;
-  for (int w = threadIdx.x; w < kBitmapWords; w += blockDim.x) {
+  for (int w = tid; w < kBitmapWords; w += blockDim.x) {
     uint32_t bits = 0;
     for (int b = 0; b < 32; b++) bits |= (mat[w * 32 + b] != base[w * 32 + b] ? 1u : 0u) << b;
     st.dep[(size_t)e * kBitmapWords + w] = bits;
+  }
+  if (tid < kLWords) lbits[tid] = 0;
+  __syncthreads();
+  const bool exch = (st.cfg.systems & NMMO_SYS_ITEM) && (st.cfg.systems & NMMO_SYS_EXCHANGE);
+  if (exch && tid < st.P) {
+    const uint2* inv = st.items + ((size_t)e * st.P + tid) * kInv;
+    for (int k = 0; k < kInv && it_type(inv[k]); k++)
+      if (it_price(inv[k])) {
+        const int row = it_row(inv[k]);
+        rmap[row] = (int16_t)(tid | (k << 8));
+        atomicOr((unsigned long long*)&lbits[row >> 6], 1ull << (row & 63));
+      }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int n = 0;
+    for (int row = 1; row <= kInv * st.P; row++)
+      if ((lbits[row >> 6] >> (row & 63)) & 1) {
+        if (n < NMMO_MARKET_ROWS)
+          st.mlist[(size_t)e * NMMO_MARKET_ROWS + n] = row | ((rmap[row] & 255) << 16) | ((rmap[row] >> 8) << 24);
+        n++;
+      }
+    st.mcount[e] = min(n, NMMO_MARKET_ROWS);
   }
 }
 

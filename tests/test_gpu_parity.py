@@ -131,3 +131,74 @@ def test_golden_rollout_hashes_gpu(preset):
 
     golden = json.load(open("tests/golden/rollout_hashes.json"))[preset]
     assert rollout(_EngineStepper(preset), preset) == golden
+
+
+def _stress_items(d, rng, P):
+    """Random inventories (rows taken from the front of the item FIFO), equipment, listings,
+    gold and same-tile player pairs, so Use/Buy/Give/GiveGold/Destroy/Sell, ammunition and loot
+    all fire in the first ticks (SPEC §9)."""
+    n = d["env"].shape[0]
+    IC = abi.INV_SLOTS * P
+    E, F = abi.E, abi.F
+    for e in range(n):
+        row = 1
+        for p in range(P):
+            used = set()
+            for k in range(int(rng.integers(0, abi.INV_SLOTS + 1))):
+                typ = int(rng.integers(2, 18))
+                lvl = int(rng.integers(1, 4))
+                slot = {2: 0, 3: 1, 4: 2}.get(typ, 3 if 5 <= typ <= 12 else 4 if 13 <= typ <= 15 else -1)
+                eq = int(slot >= 0 and slot not in used and rng.random() < 0.4)
+                if eq:
+                    used.add(slot)
+                price = int(rng.integers(1, 40)) if (not eq and rng.random() < 0.3) else 0
+                qty = int(rng.integers(1, 4)) if 13 <= typ <= 15 else 1
+                d["items"][e, p, k] = [typ | (lvl << 5) | (eq << 9) | (price << 10), qty | (row << 16)]
+                row += 1
+            d["ent"][e, F["item_level"], p] = sum(
+                (int(w0) >> 5) & 15 for w0 in d["items"][e, p, :, 0] if (w0 & 31) and (w0 >> 9) & 1)
+        d["iring"][e, :] = 0
+        d["iring"][e, :IC - row + 1] = np.arange(row, IC + 1)
+        d["env"][e, E["item_free_head"]] = 0
+        d["env"][e, E["item_free_count"]] = IC - row + 1
+        d["ent"][e, F["gold"], :P] = rng.integers(0, 60, P)
+        for p in range(1, P, 2):  # pairs on one tile: Give / GiveGold targets
+            d["ent"][e, F["row"], p] = d["ent"][e, F["row"], p - 1]
+            d["ent"][e, F["col"], p] = d["ent"][e, F["col"], p - 1]
+        d["ent"][e, F["time_alive"], :P] = 30  # past spawn immunity: kills (loot) early
+
+
+def test_item_stress_parity():
+    import torch
+
+    from oracle.oracle import join_state
+
+    n, steps = 4, 60
+    cfg = Config.preset("C4", MAP_N=4, early_stop_agent_num=0)
+    orc = OracleEnvs(cfg, n, seed=17)
+    orc.reset()
+    d = split_state(orc.get_state(), n, orc.S, orc.P)
+    _stress_items(d, np.random.default_rng(5), orc.P)
+    orc.set_state(join_state(d))
+    eng = _engine(cfg, n, seed=0)
+    eng.set_state(orc.get_state())
+    busy = 0
+    for t in range(steps):
+        acts = orc.scripted_actions(500 + t)
+        g_acts = eng.scripted_actions(500 + t)
+        if not np.array_equal(g_acts.cpu().numpy(), acts):
+            bad = np.argwhere(g_acts.cpu().numpy() != acts)[:5]
+            raise AssertionError(f"policy differs at step {t}: {bad.tolist()}")
+        busy += int((acts[..., [2, 3, 4, 6, 9, 11]] != [1024, 12, 12, 0, 12, 12]).sum())
+        orc.step(acts)
+        eng.step(torch.from_numpy(acts).cuda())
+        torch.cuda.synchronize()
+        _cmp_state(eng.get_state(), orc.get_state(), n, eng.S, f"stress step {t}")
+        for name in ("rew", "term", "trunc", "mask"):
+            assert np.array_equal(getattr(eng, name).cpu().numpy(), getattr(orc, name)), f"{name} @ {t}"
+        if t % 5 == 0:
+            go = eng.obs.cpu().numpy()
+            if not np.array_equal(go, orc.obs):
+                bad = np.argwhere(go != orc.obs)[:5]
+                raise AssertionError(f"stress obs differs at step {t}: {bad.tolist()}")
+    assert busy > 1000  # item heads were actually exercised
