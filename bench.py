@@ -42,13 +42,34 @@ WORKLOADS = {
 }
 
 
-def tick_bytes_per_env(S: int, P: int) -> int:
-    """Algorithmic HBM bytes of one tick of one env (DESIGN.md §4): the env state read and
-    written once (43 int16 entity fields x slots, free-row ring, depleted-tile bitmap, env
-    scalars), the actions read, the outputs written and the map tiles a player touches
-    (own tile + 4 neighbours for harvest/drink, 1 move target)."""
-    state = 43 * S * 2 + S * 2 + 800 * 4 + 16 * 4
+def tick_bytes_per_env(S: int, P: int, items: bool) -> int:
+    """Algorithmic HBM bytes of one tick of one env (DESIGN.md §3.1): the env state read and
+    written once (45 int16 entity fields x slots, free-row ring, depleted-tile bitmap, env
+    scalars; with the Item system the 12-slot inventories and the item-row ring), the actions
+    read, the outputs written and the map tiles a player touches (own tile + 4 neighbours for
+    harvest/drink, 1 move target)."""
+    state = 45 * S * 2 + S * 2 + 800 * 4 + 16 * 4
+    if items:
+        state += P * 12 * 8 + 12 * P * 2
     return 2 * state + P * 12 * 4 + P * (4 + 1 + 1 + 1) + P * 6
+
+
+def pmc_traffic(cfg_name: str, kernel: str, envs: int):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of the same
+    bench command (profiles/<round>/<cfg>/pmc.json, tools/pmc_summary.py): 2 x FETCH_SIZE +
+    WRITE_SIZE, gfx950-corrected. None when no summary matches this workload."""
+    import glob
+
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", cfg_name, "pmc.json")), reverse=True):
+        try:
+            d = json.load(open(path))
+            k = d["kernels"][kernel]
+            if d.get("bench", {}).get("config", {}).get("envs_per_gpu") != envs:
+                continue
+            return k["hbm_bytes_per_dispatch"], os.path.relpath(path, ROOT)
+        except (KeyError, ValueError, OSError):
+            continue
+    return None, None
 
 
 def obs_bytes_per_env(S: int, P: int, elems: int) -> int:
@@ -154,13 +175,14 @@ def main():
     eng = NmmoEngine(cfg, envs, seed=args.seed, device=dev, task_embedding=task,
                      env_index_base=rank * envs)
     eng.reset()
-    alive_acc = torch.zeros((envs, cfg.PLAYER_N), dtype=torch.int32, device=dev)
+    # device counters the tick kernel adds into: [0] = sum(mask) (agent-steps), [1] = episodes
+    counters = torch.zeros(2, dtype=torch.int64, device=dev)
+    eng.set_counters(counters)
     pseed = args.seed * 1_000_003  # the policy's Philox counter already walks (tick, episode)
 
     def one():
         eng.scripted_actions(pseed)
         eng.step()
-        torch.add(alive_acc, eng.mask, out=alive_acc)  # sum(mask) accounting, one kernel
 
     for _ in range(args.warmup):
         one()
@@ -175,12 +197,12 @@ def main():
                     one()
             graphs.append((n, g))
         torch.cuda.synchronize(dev)
-        alive_acc.zero_()
     plan = []
     if graphs:
         big = graphs[-1] if graphs[-1][0] == max(n for n, _ in graphs) else graphs[0]
         q, r = divmod(args.steps, big[0])
         plan = [big[1]] * q + [g for n, g in graphs if n == r and r]
+    counters.zero_()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -195,7 +217,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    alive = alive_acc.sum(dtype=torch.int64)
+    alive = counters[0].clone()
     # per-kernel durations: HIP events on the launch stream around each kernel of nmmo_step,
     # over an equal number of eager steps right after the timed region (same state stream)
     eng.set_timing(True)
@@ -220,13 +242,14 @@ def main():
         S, P = eng.S, cfg.PLAYER_N
         tick_avg_ms = tick_ms / max(n_timed, 1)
         obs_avg_ms = obs_ms / max(n_timed, 1)
-        tick_b = tick_bytes_per_env(S, P) * envs
+        tick_b = tick_bytes_per_env(S, P, "Item" in cfg.systems) * envs
         obs_b = obs_bytes_per_env(S, P, eng.obs_elems) * envs if wl["obs"] else 0
         if wl["obs"] and obs_avg_ms > tick_avg_ms:
             kern, byts, ms = "obs_kernel", obs_b, obs_avg_ms
         else:
             kern, byts, ms = "tick_kernel", tick_b, tick_avg_ms
         achieved = byts / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
+        traffic, traffic_src = pmc_traffic(args.config, kern, envs)
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(Config.preset(wl["preset"], early_stop_agent_num=8,
@@ -266,7 +289,8 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5),
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_source": traffic_src,
                 "bytes_per_launch": byts,
             },
             "cpu_baseline": cpu,

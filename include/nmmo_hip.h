@@ -186,6 +186,11 @@ NMMO_API int nmmo_get_map_bank(NmmoHandle* h, uint8_t* host_buf, size_t nbytes);
  * nmmo_read_timing synchronises, returns the summed milliseconds of the tick and obs kernels
  * over the buffered steps in ms[0], ms[1], their count in *n, and clears the buffer. */
 NMMO_API int nmmo_set_timing(NmmoHandle* h, int32_t enable);
+/* Device-side rollout counters (the trainer's agent_SPS numerator, clean_pufferl.py:306):
+ * when set, every nmmo_step / nmmo_reset adds into dev_counters (device u64 [2]):
+ * [0] += sum of the mask it writes (agent-steps), [1] += envs whose episode ended.
+ * NULL disables. The caller owns and zeroes the buffer; capture-safe. */
+NMMO_API int nmmo_set_counters(NmmoHandle* h, uint64_t* dev_counters);
 NMMO_API int nmmo_read_timing(NmmoHandle* h, double* ms /* [2] */, int32_t* n);
 
 NMMO_API int32_t nmmo_n_envs(const NmmoHandle* h);

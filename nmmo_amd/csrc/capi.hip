@@ -199,7 +199,7 @@ int nmmo_create(const NmmoConfig* cfg, int32_t n_envs, uint64_t seed, int32_t de
   }
   h->st = DevState{h->d_env,   h->d_ent,   h->d_ring,  h->d_mat,    h->d_dep, h->d_bank,
                    h->d_items, h->d_iring, h->d_mlist, h->d_mcount, n_envs,   P,
-                   N,          S,          seed,       *cfg};
+                   N,          S,          seed,       nullptr,     *cfg};
   if (launch_mapgen(cfg->map_seed, cfg->map_n, h->d_bank, nullptr) != hipSuccess ||
       hipDeviceSynchronize() != hipSuccess)
     return cleanup_fail(fail(NMMO_E_HIP, "map generation failed: %s", hipGetErrorString(hipGetLastError())));
@@ -270,6 +270,12 @@ int nmmo_set_timing(NmmoHandle* h, int32_t enable) {
   }
   h->timing = enable != 0;
   h->t_count = 0;
+  return NMMO_OK;
+}
+
+int nmmo_set_counters(NmmoHandle* h, uint64_t* dev_counters) {
+  if (!h) return fail(NMMO_E_INVALID, "null handle");
+  h->st.counters = reinterpret_cast<unsigned long long*>(dev_counters);
   return NMMO_OK;
 }
 

@@ -207,6 +207,13 @@ __device__ inline int inv_stack(const uint2* inv, int type, int level) {  // amm
   return -1;
 }
 
+// lane `lane` of `old` <- the wave-uniform `val`: v_cmp + v_cndmask. (An inline-asm
+// v_writelane_b32 with the lane select in M0 is one op cheaper but mis-set ~1 in 10^3 masks on
+// gfx950 — a hazard the compiler's recognizer cannot see inside asm — so it is not used.)
+__device__ inline uint32_t writelane_u32(uint32_t old, uint32_t val, uint32_t lane) {
+  return lane_id() == (int)lane ? val : old;
+}
+
 // Block-wide exclusive prefix sum of an int in thread order (<= 16 waves); *total gets the sum.
 __device__ inline int block_prefix_sum(int v, int* wave_tot, int* total) {
   const int lane = lane_id(), w = wave_id(), nw = (blockDim.x + 63) >> 6;

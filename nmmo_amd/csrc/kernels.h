@@ -18,6 +18,7 @@ struct DevState {
   int* mcount;           // [n] listings in mlist (<= NMMO_MARKET_ROWS)
   int n_envs, P, N, S;   // N = NPC capacity (0 when the NPC system is off), S = P + N
   uint64_t seed;         // create seed (first-episode seeds)
+  unsigned long long* counters;  // optional device u64 [2]: agent-steps, finished episodes
   NmmoConfig cfg;
 };
 

@@ -189,44 +189,114 @@ hipError_t launch_obs(const ObsParams& p, hipStream_t stream) {
 }
 
 // ---------------------------------------------------------------- scripted policy (SPEC §10)
-// One workgroup per env, one thread per player: for every head, a uniform draw over the set
-// bits of that head's mask (identical to the obs masks). The env's entities are first packed
-// per datastore row into one int32 (r | c<<8 | slot<<16 | immune<<25, -1 = absent), so the two
-// visibility passes over the rows are one broadcast LDS load per row with no dependent loads.
+// One workgroup per env: for every head, a uniform draw over the set bits of that head's mask
+// (identical to the obs masks). Phase A (all waves, rows across lanes): for each player one
+// packed 16-bit window test per row (entity (r+7, c+7) minus player (r, c), one v_pk_sub_u16)
+// and three ballots give the visible / attackable / same-tile row bitmaps. Phase B (thread per
+// player): the first-100-visible cut, counts, draws and k-th-set-bit selections with popcounts.
+__host__ __device__ inline int policy_threads(int S, int P) {
+  const int t = ((S + 63) / 64) * 64;
+  return t < P ? ((P + 63) / 64) * 64 : t;
+}
 __host__ __device__ inline size_t policy_lds_bytes(int S, int P) {
-  return (size_t)rp_groups(S) * 16 + (size_t)P * kInv * 8 + (size_t)NMMO_MARKET_ROWS * 12;
+  const int NW = (S + 63) / 64;
+  return (size_t)3 * P * NW * 8 + (size_t)((P + 3) & ~3) * 4 + (size_t)NMMO_MARKET_ROWS * 12;
 }
 
-__global__ void __launch_bounds__(128) policy_kernel(PolicyParams p) {
+__global__ void __launch_bounds__(512) policy_kernel(PolicyParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int S = p.S, e = blockIdx.x, tid = threadIdx.x;
-  int* rp = reinterpret_cast<int*>(smem);  // by datastore row (row 0 unused), int4-padded
-  uint2* invs = reinterpret_cast<uint2*>(smem + (size_t)rp_groups(S) * 16);
-  uint2* mitem = invs + p.P * kInv;
+  typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+  const int S = p.S, P = p.P, e = blockIdx.x, tid = threadIdx.x;
+  const int NW = (S + 63) >> 6;
+  uint64_t* vism = reinterpret_cast<uint64_t*>(smem);  // [P][NW] visible rows
+  uint64_t* atkm = vism + P * NW;                      // [P][NW] attackable rows
+  uint64_t* samm = atkm + P * NW;                      // [P][NW] other players on the same tile
+  uint32_t* ppos = reinterpret_cast<uint32_t*>(samm + P * NW);  // [P] r<<16 | c, or sentinel
+  uint2* mitem = reinterpret_cast<uint2*>(ppos + ((P + 3) & ~3));
   int* mown = reinterpret_cast<int*>(mitem + NMMO_MARKET_ROWS);
   const int16_t* E = p.ent + (size_t)e * NMMO_NF * S;
   const bool combat = (p.systems & NMMO_SYS_COMBAT) != 0;
   const bool item = (p.systems & NMMO_SYS_ITEM) != 0;
   const bool exch = item && (p.systems & NMMO_SYS_EXCHANGE) != 0;
   const int nm = exch ? p.mcount[e] : 0;
-  for (int k = tid; k < rp_groups(S) * 4; k += blockDim.x) rp[k] = -1;
-  for (int k = tid; k < p.P * kInv; k += blockDim.x) invs[k] = p.items[(size_t)e * p.P * kInv + k];
   for (int j = tid; j < nm; j += blockDim.x) {
     const int v = p.mlist[(size_t)e * NMMO_MARKET_ROWS + j];
     mown[j] = (v >> 16) & 255;
-    mitem[j] = p.items[((size_t)e * p.P + ((v >> 16) & 255)) * kInv + ((v >> 24) & 15)];
+    mitem[j] = p.items[((size_t)e * P + ((v >> 16) & 255)) * kInv + ((v >> 24) & 15)];
+  }
+  for (int a = tid; a < ((P + 3) & ~3); a += blockDim.x)
+    ppos[a] = (a < P && E[F_ALIVE * S + a]) ? ((uint32_t)E[F_ROW * S + a] << 16) | (uint32_t)E[F_COL * S + a]
+                                            : 0x80008000u;
+  // the entity of datastore row (64w + lane + 1): found by the slot that owns it
+  __shared__ int rowslot[512];
+  for (int k = tid; k <= S; k += blockDim.x) rowslot[k] = -1;
+  __syncthreads();
+  for (int s = tid; s < S; s += blockDim.x)
+    if (E[F_ALIVE * S + s]) rowslot[E[F_DS_ROW * S + s]] = s;
+  __syncthreads();
+  const bool tgt_any = combat || item;
+  if (tgt_any) {
+    // per player: pk_sub + packed max + compare per row-lane, three ballots, writelanes.
+    // Row-constant conditions (immune target, player entity) are folded into masks once; the
+    // player's own row is cleared in phase B.
+    const int w = wave_id(), lane = lane_id(), row = (w << 6) + lane + 1;
+    if (w < NW) {
+      const int q = row <= S ? rowslot[row] : -1;
+      const uint32_t e32 = q < 0 ? 0xF000F000u
+                                 : ((uint32_t)(E[F_ROW * S + q] + 7) << 16) | (uint32_t)(E[F_COL * S + q] + 7);
+      const bool immune = q >= 0 && q < P && E[F_TIME_ALIVE * S + q] < p.spawn_immunity;
+      const uint64_t not_immune = __ballot(!immune), is_player = __ballot(q >= 0 && q < P);
+      const us2 e2 = __builtin_bit_cast(us2, e32);
+      const us2 four = {4, 4};
+      const uint4* pp4 = reinterpret_cast<const uint4*>(ppos);
+      for (int pb = 0; pb < P; pb += 64) {
+        uint32_t v_lo = 0, v_hi = 0, a_lo = 0, a_hi = 0, s_lo = 0, s_hi = 0;
+        const int pe = min(P, pb + 64);
+        for (int g = pb >> 2; g < (pe + 3) >> 2; g++) {
+          const uint4 pq = pp4[g];
+          const uint32_t pv[4] = {(uint32_t)__builtin_amdgcn_readfirstlane((int)pq.x),
+                                  (uint32_t)__builtin_amdgcn_readfirstlane((int)pq.y),
+                                  (uint32_t)__builtin_amdgcn_readfirstlane((int)pq.z),
+                                  (uint32_t)__builtin_amdgcn_readfirstlane((int)pq.w)};
+#pragma unroll
+          for (int j = 0; j < 4; j++) {
+            const us2 t = e2 - __builtin_bit_cast(us2, pv[j]);
+            const us2 t4 = t - four;
+            const us2 mx = __builtin_elementwise_max(t, t.yx);
+            const us2 m4 = __builtin_elementwise_max(t4, t4.yx);
+            const uint64_t mv = __ballot(mx.x <= 14);
+            const uint64_t ma = __ballot(m4.x <= 6) & not_immune;
+            const uint64_t ms = __ballot(__builtin_bit_cast(uint32_t, t) == 0x00070007u) & is_player;
+            const uint32_t l = (uint32_t)((4 * g + j) & 63);
+            v_lo = writelane_u32(v_lo, (uint32_t)mv, l);
+            v_hi = writelane_u32(v_hi, (uint32_t)(mv >> 32), l);
+            a_lo = writelane_u32(a_lo, (uint32_t)ma, l);
+            a_hi = writelane_u32(a_hi, (uint32_t)(ma >> 32), l);
+            s_lo = writelane_u32(s_lo, (uint32_t)ms, l);
+            s_hi = writelane_u32(s_hi, (uint32_t)(ms >> 32), l);
+          }
+        }
+        if (pb + lane < pe) {
+          const int a = pb + lane;
+          vism[a * NW + w] = ((uint64_t)v_hi << 32) | v_lo;
+          atkm[a * NW + w] = ((uint64_t)a_hi << 32) | a_lo;
+          samm[a * NW + w] = ((uint64_t)s_hi << 32) | s_lo;
+        }
+      }
+    }
   }
   __syncthreads();
-  for (int s = tid; s < S; s += blockDim.x) {
-    if (!E[F_ALIVE * S + s]) continue;
-    const bool immune = s < p.P && E[F_TIME_ALIVE * S + s] < p.spawn_immunity;
-    rp[E[F_DS_ROW * S + s]] = E[F_ROW * S + s] | (E[F_COL * S + s] << 8) | (s << 16) | ((int)immune << 25);
+  for (int a = tid; a < P && tgt_any; a += blockDim.x) {  // a player never targets itself
+    if (!E[F_ALIVE * S + a]) continue;
+    const int r0 = E[F_DS_ROW * S + a] - 1;
+    atkm[a * NW + (r0 >> 6)] &= ~(1ull << (r0 & 63));
+    samm[a * NW + (r0 >> 6)] &= ~(1ull << (r0 & 63));
   }
   __syncthreads();
   const int32_t* env = p.env + (size_t)e * NMMO_NE;
   const uint8_t* mat = p.mat + (size_t)e * kTiles;
-  for (int a = tid; a < p.P; a += blockDim.x) {
-    int32_t* out = p.actions + ((size_t)e * p.P + a) * kHeads;
+  for (int a = tid; a < P; a += blockDim.x) {
+    int32_t* out = p.actions + ((size_t)e * P + a) * kHeads;
     int32_t h[kHeads] = {0, kNObs, NMMO_MARKET_ROWS, kInv, kInv, kNObs, 0, kNObs, 0, kInv, 0, kInv};
     if (!E[F_ALIVE * S + a]) {
 #pragma unroll
@@ -241,58 +311,42 @@ __global__ void __launch_bounds__(128) policy_kernel(PolicyParams p) {
     };
     const int r = E[F_ROW * S + a], c = E[F_COL * S + a], gold = E[F_GOLD * S + a];
     if (combat) h[0] = draw_n(0, 3);
-    // Attack / Give / GiveGold targets over the first 100 visible rows: count, draw, then
-    // select the pick-th set bit of each mask in one more pass
-    const bool tgt_any = combat || item;
     if (tgt_any) {
-      const int4* rp4 = reinterpret_cast<const int4*>(rp);
-      const int ng = rp_groups(S);
-      int na = 0, nt = 0, nv = 0;
-      for (int g = 0; g < ng; g++) {  // pass 1: counts among the first 100 visible
-        const int4 q = rp4[g];
-        const int vv[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-          const int v = vv[j];
-          const int d = linf(r, c, v & 255, (v >> 8) & 255);
-          const int sl = (v >> 16) & 511;
-          const bool vis = v >= 0 && d <= kVision && nv < kNObs;
-          na += vis && sl != a && d <= 3 && !((v >> 25) & 1);
-          nt += vis && sl != a && sl < p.P && d == 0;
-          nv += vis;
+      // Entity rows beyond the first 100 visible are not in the obs: cut the masks there
+      int na = 0, nt = 0, cum = 0;
+      for (int w = 0; w < NW; w++) {
+        uint64_t cut = vism[a * NW + w];
+        const int pc = __popcll(cut);
+        if (cum + pc > kNObs) {
+          for (int i = 0; i < cum + pc - kNObs; i++) cut &= ~(1ull << (63 - __builtin_clzll(cut)));
         }
+        cum = min(cum + pc, kNObs);
+        na += __popcll(atkm[a * NW + w] & cut);
+        nt += __popcll(samm[a * NW + w] & cut);
       }
       const int pa = combat ? draw_n(1, na + 1) : na;
       const int pg = draw_n(5, (item ? nt : 0) + 1);
       const int pgg = draw_n(7, (exch ? nt : 0) + 1);
-      int sa = kNObs, sg = kNObs, sgg = kNObs;
-      const bool want_a = combat && pa < na, want_g = item && pg < nt, want_gg = exch && pgg < nt;
-      if (want_a || want_g || want_gg) {  // pass 2: visible index of each pick
-        int seen_a = 0, seen_t = 0;
-        nv = 0;
-        for (int g = 0; g < ng && nv < kNObs; g++) {
-          const int4 q = rp4[g];
-          const int vv[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-          for (int j = 0; j < 4; j++) {
-            const int v = vv[j];
-            const int d = linf(r, c, v & 255, (v >> 8) & 255);
-            const int sl = (v >> 16) & 511;
-            const bool vis = v >= 0 && d <= kVision && nv < kNObs;
-            const bool oka = vis && sl != a && d <= 3 && !((v >> 25) & 1);
-            const bool okt = vis && sl != a && sl < p.P && d == 0;
-            sa = (want_a && oka && seen_a == pa && sa == kNObs) ? nv : sa;
-            sg = (want_g && okt && seen_t == pg && sg == kNObs) ? nv : sg;
-            sgg = (want_gg && okt && seen_t == pgg && sgg == kNObs) ? nv : sgg;
-            seen_a += oka;
-            seen_t += okt;
-            nv += vis;
+      // visible index of the k-th set bit of mask m (within the cut)
+      auto select = [&](const uint64_t* m, int k) {
+        int before = 0;
+        for (int w = 0; w < NW; w++) {
+          const uint64_t vm = vism[a * NW + w];
+          uint64_t mm = m[a * NW + w] & vm;
+          const int pc = __popcll(mm);
+          if (k < pc) {
+            for (int i = 0; i < k; i++) mm &= mm - 1;
+            const int b = __builtin_ctzll(mm);
+            return before + (int)__popcll(vm & ((1ull << b) - 1ull));
           }
+          k -= pc;
+          before += (int)__popcll(vm);
         }
-      }
-      if (combat) h[1] = sa;
-      h[5] = sg;
-      h[7] = sgg;
+        return (int)kNObs;
+      };
+      if (combat && pa < na) h[1] = select(atkm, pa);
+      if (item && pg < nt) h[5] = select(samm, pg);
+      if (exch && pgg < nt) h[7] = select(samm, pgg);
     }
     // Buy.MarketItem: listings with price <= gold not owned by self
     {
@@ -309,33 +363,42 @@ __global__ void __launch_bounds__(128) policy_kernel(PolicyParams p) {
     }
     // InventoryItem heads: Destroy (3), Give (4), Sell (9), Use (11)
     {
-      const uint2* inv = invs + a * kInv;
-      const int n = inv_count(inv);
+      uint2 inv[kInv];
+      const uint4* src = reinterpret_cast<const uint4*>(p.items + ((size_t)e * P + a) * kInv);
+#pragma unroll
+      for (int k = 0; k < kInv / 2; k++) {
+        const uint4 q = item ? src[k] : make_uint4(0u, 0u, 0u, 0u);
+        inv[2 * k] = make_uint2(q.x, q.y);
+        inv[2 * k + 1] = make_uint2(q.z, q.w);
+      }
       int nf = 0, ns = 0, nu = 0;
-      for (int k = 0; k < n; k++) {
+      uint32_t mf = 0, msl = 0, mu = 0;
+#pragma unroll
+      for (int k = 0; k < kInv; k++) {
         const uint2 w = inv[k];
-        nf += !it_equipped(w) && !it_price(w);
-        ns += !it_equipped(w);
-        nu += item_usable(E, S, a, w);
+        const bool present = it_type(w) != 0;
+        const bool f = present && !it_equipped(w) && !it_price(w);
+        const bool sl = present && !it_equipped(w);
+        const bool us = present && item_usable(E, S, a, w);
+        mf |= (uint32_t)f << k;
+        msl |= (uint32_t)sl << k;
+        mu |= (uint32_t)us << k;
       }
-      const int pd = draw_n(3, (item ? nf : 0) + 1), pgv = draw_n(4, (item ? nf : 0) + 1);
-      const int ps = draw_n(9, (exch ? ns : 0) + 1), pu = draw_n(11, (item ? nu : 0) + 1);
-      int sd = kInv, sgv = kInv, ss = kInv, su = kInv;
-      for (int k = 0, cf = 0, cs = 0, cu = 0; k < n; k++) {
-        const uint2 w = inv[k];
-        const bool f = !it_equipped(w) && !it_price(w), sll = !it_equipped(w), us = item_usable(E, S, a, w);
-        sd = (item && f && cf == pd && sd == kInv) ? k : sd;
-        sgv = (item && f && cf == pgv && sgv == kInv) ? k : sgv;
-        ss = (exch && sll && cs == ps && ss == kInv) ? k : ss;
-        su = (item && us && cu == pu && su == kInv) ? k : su;
-        cf += f;
-        cs += sll;
-        cu += us;
-      }
-      h[3] = sd;
-      h[4] = sgv;
-      h[9] = ss;
-      h[11] = su;
+      if (!item) mf = mu = 0;
+      if (!exch) msl = 0;
+      nf = __popc(mf);
+      ns = __popc(msl);
+      nu = __popc(mu);
+      auto kth = [](uint32_t m, int k) {
+        for (int i = 0; i < k; i++) m &= m - 1;
+        return (int)__builtin_ctz(m);
+      };
+      const int pd = draw_n(3, nf + 1), pgv = draw_n(4, nf + 1);
+      const int ps = draw_n(9, ns + 1), pu = draw_n(11, nu + 1);
+      h[3] = pd < nf ? kth(mf, pd) : kInv;
+      h[4] = pgv < nf ? kth(mf, pgv) : kInv;
+      h[9] = ps < ns ? kth(msl, ps) : kInv;
+      h[11] = pu < nu ? kth(mu, pu) : kInv;
     }
     if (exch) {
       const int ng = min(gold, 99);
@@ -353,7 +416,9 @@ __global__ void __launch_bounds__(128) policy_kernel(PolicyParams p) {
 }
 
 hipError_t launch_policy(const PolicyParams& p, hipStream_t stream) {
-  hipLaunchKernelGGL(policy_kernel, dim3(p.n_envs), dim3(128), policy_lds_bytes(p.S, p.P), stream, p);
+  if (p.S > 511) return hipErrorInvalidValue;  // rowslot[512]
+  hipLaunchKernelGGL(policy_kernel, dim3(p.n_envs), dim3(policy_threads(p.S, p.P)),
+                     policy_lds_bytes(p.S, p.P), stream, p);
   return hipGetLastError();
 }
 

@@ -32,6 +32,7 @@ struct Ctx {
   uint64_t* vism;    // [P][NW] visibility bitmap: bit j of word w = row 64w+j+1 visible to player
   int* rp;           // [S+1] datastore row -> r | c<<8 | slot<<16 (-1 = no entity)
   int* sp;           // [S] slot -> r | c<<8 while in the realm with health > 0 (-1 otherwise)
+  uint32_t* pp;      // [128] player -> r<<16 | c (0x80008000 when not in the realm): window tests
   int* hkey;         // [kHash] Foilage-tile hash: tile index (-1 = empty)
   int* hmin;         // [kHash] lowest player slot standing on that tile
   int16_t* amove;    // [S]
@@ -106,6 +107,7 @@ __host__ __device__ inline size_t tick_lds_bytes(int S, int P, bool items) {
   b += (size_t)128 * ((S + 63) / 64) * 8;  // vism (players <= 128)
   b += (size_t)rp_groups(S) * 16;    // rp
   b += al((size_t)S * 4);            // sp
+  b += 128 * 4;                      // pp
   b += 2 * kHash * 4;                // hkey, hmin
   b += 3 * al((size_t)S * 2);        // amove atgt asty
   b += al((size_t)S * 4);            // ft
@@ -148,6 +150,7 @@ __device__ __forceinline__ Ctx make_ctx(unsigned char* smem, const DevState& st,
   c.vism = reinterpret_cast<uint64_t*>(smem + o); o += (size_t)128 * ((S + 63) / 64) * 8;
   c.rp = reinterpret_cast<int*>(smem + o); o += (size_t)rp_groups(S) * 16;
   c.sp = reinterpret_cast<int*>(smem + o); o += al((size_t)S * 4);
+  c.pp = reinterpret_cast<uint32_t*>(smem + o); o += 128 * 4;
   c.hkey = reinterpret_cast<int*>(smem + o); o += kHash * 4;
   c.hmin = reinterpret_cast<int*>(smem + o); o += kHash * 4;
   c.amove = reinterpret_cast<int16_t*>(smem + o); o += al((size_t)S * 2);
@@ -671,6 +674,8 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
     c.sp[s] = in ? pos : -1;
     if (in) c.rp[TF(F_DS_ROW, s)] = pos | (s << 16);
   }
+  if (tid < 128) c.pp[tid] = (tid < P && TF(F_ALIVE, tid)) ? ((uint32_t)TF(F_ROW, tid) << 16) | (uint32_t)TF(F_COL, tid)
+                                                        : 0x80008000u;
   if (c.exch && s < P) {  // listings of the previous observation (Buy.MarketItem index space)
     const uint2* inv = c.inv + s * kInv;
     for (int k = 0; k < kInv; k++) {
@@ -700,28 +705,27 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
     const int v = row <= S ? c.rp[row] : -1;
     const uint32_t e32 = v < 0 ? 0xF000F000u : ((uint32_t)((v & 255) + 7) << 16) | (uint32_t)(((v >> 8) & 255) + 7);
     const us2 e2 = __builtin_bit_cast(us2, e32);
-    const int4* sp4 = reinterpret_cast<const int4*>(c.sp);
+    const uint4* pp4 = reinterpret_cast<const uint4*>(c.pp);
     for (int pb = 0; pb < P; pb += 64) {
-      int mine_lo = 0, mine_hi = 0;  // lane j keeps the mask of player pb + j
+      uint32_t mine_lo = 0, mine_hi = 0;  // lane j keeps the mask of player pb + j
       const int pe = min(P, pb + 64);
       for (int g = pb >> 2; g < (pe + 3) >> 2; g++) {  // 4 players per ds_read_b128 (broadcast)
-        const int4 q = sp4[g];
-        const int pv[4] = {q.x, q.y, q.z, q.w};
+        const uint4 q = pp4[g];
+        const uint32_t pv[4] = {(uint32_t)__builtin_amdgcn_readfirstlane((int)q.x),
+                                (uint32_t)__builtin_amdgcn_readfirstlane((int)q.y),
+                                (uint32_t)__builtin_amdgcn_readfirstlane((int)q.z),
+                                (uint32_t)__builtin_amdgcn_readfirstlane((int)q.w)};
 #pragma unroll
         for (int j = 0; j < 4; j++) {
-          const int p = 4 * g + j;
-          const uint32_t p32 = (pv[j] < 0 || p >= P) ? 0x80008000u
-                                                     : ((uint32_t)(pv[j] & 255) << 16) | (uint32_t)((pv[j] >> 8) & 255);
-          const us2 t = e2 - __builtin_bit_cast(us2, p32);
-          const unsigned short d = t.x > t.y ? t.x : t.y;
-          const uint64_t m = __ballot(d <= 14);
-          const bool me = lane == (p & 63);
-          mine_lo = me ? (int)(uint32_t)m : mine_lo;
-          mine_hi = me ? (int)(uint32_t)(m >> 32) : mine_hi;
+          const us2 t = e2 - __builtin_bit_cast(us2, pv[j]);
+          const us2 mx = __builtin_elementwise_max(t, t.yx);
+          const uint64_t m = __ballot(mx.x <= 14);
+          const uint32_t l = (uint32_t)((4 * g + j) & 63);
+          mine_lo = writelane_u32(mine_lo, (uint32_t)m, l);
+          mine_hi = writelane_u32(mine_hi, (uint32_t)(m >> 32), l);
         }
       }
-      if (pb + lane < pe)
-        c.vism[(pb + lane) * NW + w] = ((uint64_t)(uint32_t)mine_hi << 32) | (uint32_t)mine_lo;
+      if (pb + lane < pe) c.vism[(pb + lane) * NW + w] = ((uint64_t)mine_hi << 32) | mine_lo;
     }
   }
   __syncthreads();
@@ -921,6 +925,7 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
     }
   }
   __syncthreads();
+  NMMO_STAMP(15);
 
   if (items) {
     // 3. Use (priority 10): own inventory only -> parallel; consumed rows freed in slot order
@@ -1045,6 +1050,7 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
     ring_append_ordered(c, freed);
   }
 
+  NMMO_STAMP(14);
   // 3a. Attack (priority 50)
   for (int k = tid; k < S; k += nt) c.ft[k] = 0x7FFF;
   __syncthreads();
@@ -1283,7 +1289,8 @@ __global__ void tick_kernel(DevState st, const int32_t* __restrict__ actions,
   load_env(c, st, e);
   __syncthreads();
   const size_t o = (size_t)e * c.P;
-  if (mode == 1 || c.E[E_DONE]) {
+  const bool reset_path = mode == 1 || c.E[E_DONE];
+  if (reset_path) {
     const int env_global = (int)(st.cfg.env_index_base + (uint64_t)e);
     uint64_t seed;
     int episode;
@@ -1310,6 +1317,15 @@ __global__ void tick_kernel(DevState st, const int32_t* __restrict__ actions,
     tick_env(c, actions + o * kHeads, rew + o, term + o, trunc + o, mask + o);
   }
   __syncthreads();
+  if (st.counters) {  // sum(mask) of this launch (pres, or all players on a reset) + done envs
+    const bool reset = mode == 1 || reset_path;
+    int n;
+    block_prefix_count(threadIdx.x < c.P && (reset || c.pres[threadIdx.x]), c.wtot, &n);
+    if (threadIdx.x == 0) {
+      atomicAdd(&st.counters[0], (unsigned long long)n);
+      if (!reset && c.E[E_DONE]) atomicAdd(&st.counters[1], 1ull);
+    }
+  }
   NMMO_STAMP(10);
   store_market(c, st, e);
   store_env(c, st, e);

@@ -110,6 +110,13 @@ class NmmoEngine:
     def set_timing(self, enable: bool):
         check(lib().nmmo_set_timing(self.h, 1 if enable else 0), "nmmo_set_timing")
 
+    def set_counters(self, counters):
+        """Device u64 [2] (torch int64 tensor on this device) the kernels add into: agent-steps
+        (sum of mask) and finished episodes; None disables."""
+        ptr = None if counters is None else ctypes.c_void_p(counters.data_ptr())
+        self._counters = counters
+        check(lib().nmmo_set_counters(self.h, ptr), "nmmo_set_counters")
+
     def read_timing(self):
         """(tick_ms_sum, obs_ms_sum, n_steps) from HIP events on the launch stream."""
         ms = (ctypes.c_double * 2)()

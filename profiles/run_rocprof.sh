@@ -1,7 +1,9 @@
 #!/bin/bash
-# Collects the rocprofv3 summaries committed under profiles/ (run on the GPU box via gpurun).
-#   kernel trace + stats per config, then FETCH_SIZE and WRITE_SIZE in separate --pmc passes
-#   (MI355X_MICROARCH.md: TCC slots: FETCH_SIZE costs 3, WRITE_SIZE 2 -> one per pass).
+# Collects the rocprofv3 summaries committed under profiles/<tag>/ (run on the GPU box via
+# gpurun; outputs go to gpurun_out/prof_<tag>/, which gpurun merges back).
+#   per config: kernel trace + stats, then FETCH_SIZE and WRITE_SIZE in separate --pmc passes
+#   (MI355X_MICROARCH.md: TCC slots: FETCH_SIZE costs 3, WRITE_SIZE 2 -> one per pass), and a
+#   JSON summary (tools/pmc_summary.py) that bench.py reads for roofline.traffic.
 # Usage: bash profiles/run_rocprof.sh <round-tag> [configs...]
 set -e -o pipefail
 TAG=${1:-r01}; shift || true
@@ -18,4 +20,6 @@ for c in $CONFIGS; do
     python3 bench.py --config $c --steps 30 --warmup 5 --no-cpu-baseline > /dev/null
   timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/$c/write -o run -- \
     python3 bench.py --config $c --steps 30 --warmup 5 --no-cpu-baseline > /dev/null
+  python3 tools/pmc_summary.py $OUT/$c > $OUT/$c/pmc.json
+  echo "profiled $c"
 done

@@ -1,0 +1,62 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 output of profiles/run_rocprof.sh into one JSON per config.
+
+Per kernel: dispatch count and mean duration (kernel trace), mean FETCH_SIZE / WRITE_SIZE per
+dispatch (separate --pmc passes) and the HBM bytes per dispatch corrected as
+MI355X_MICROARCH.md §HBM prescribes: rocprofv3 reports both counters in KiB; on gfx950
+FETCH_SIZE counts half the bytes of wide coalesced reads (doubled here), WRITE_SIZE is exact
+for 16-B-per-lane stores.
+
+  python tools/pmc_summary.py <prof_dir/cfg> > pmc.json
+"""
+
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+
+def _rows(pattern):
+    for path in sorted(glob.glob(pattern, recursive=True)):
+        with open(path, newline="") as f:
+            yield from csv.DictReader(f)
+
+
+def _short(name):
+    name = name.split("(")[0]
+    return name.split("::")[-1].strip()
+
+
+def summarise(d):
+    out = defaultdict(dict)
+    for r in _rows(os.path.join(d, "trace", "**", "*kernel_stats.csv")):
+        k = _short(r["Name"])
+        out[k]["dispatches"] = int(r["Calls"])
+        out[k]["avg_ns"] = float(r["AverageNs"])
+    for sub, ctr in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
+        acc = defaultdict(list)
+        for r in _rows(os.path.join(d, sub, "**", "*counter_collection.csv")):
+            if r.get("Counter_Name") == ctr:
+                acc[_short(r["Kernel_Name"])].append(float(r["Counter_Value"]))
+        for k, v in acc.items():
+            out[k][ctr.lower() + "_kib_per_dispatch"] = sum(v) / len(v)
+            out[k][ctr.lower() + "_dispatches"] = len(v)
+    for k, v in out.items():
+        if "fetch_size_kib_per_dispatch" in v and "write_size_kib_per_dispatch" in v:
+            v["hbm_bytes_per_dispatch"] = round(
+                2 * v["fetch_size_kib_per_dispatch"] * 1024 + v["write_size_kib_per_dispatch"] * 1024)
+    return dict(out)
+
+
+if __name__ == "__main__":
+    d = sys.argv[1]
+    res = {"kernels": summarise(d)}
+    bj = os.path.join(d, "bench.json")
+    if os.path.exists(bj):
+        lines = [ln for ln in open(bj) if ln.strip().startswith("{")]
+        if lines:
+            res["bench"] = json.loads(lines[-1])
+    json.dump(res, sys.stdout, indent=1)
+    print()

@@ -48,7 +48,8 @@ def main():
             rows.append(d)
             full = buf.reshape(4096, 16)[:min(envs, 4096)].astype(np.int64)[ok]
             subs.append(np.stack([full[:, 12] - full[:, 1], full[:, 2] - full[:, 12],
-                                  full[:, 13] - full[:, 1]], 1))
+                                  full[:, 13] - full[:, 1], full[:, 15] - full[:, 3],
+                                  full[:, 14] - full[:, 15], full[:, 4] - full[:, 14]], 1))
     d = np.concatenate(rows)
     tot = np.median(d.sum(1))
     print(f"{preset} envs={envs}: median total {tot:.0f} cycles over {len(d)} env-ticks")
@@ -58,6 +59,9 @@ def main():
     sub = np.concatenate(subs)
     print(f"  of which player decode  median {np.median(sub[:, 0]):9.0f} (visibility bitmap "
           f"{np.median(sub[:, 2]):9.0f}); npc decide median {np.median(sub[:, 1]):9.0f}")
+    print(f"  update+harvest = resource {np.median(d[:, 2]):9.0f} + professions "
+          f"{np.median(sub[:, 3]):9.0f}; item actions (Use..Destroy) {np.median(sub[:, 4]):9.0f}; "
+          f"uncontested attacks {np.median(sub[:, 5]):9.0f}")
 
 
 if __name__ == "__main__":
