@@ -40,7 +40,7 @@ extern "C" {
 #endif
 
 #define NMMO_API __attribute__((visibility("default")))
-#define NMMO_ABI_VERSION 1
+#define NMMO_ABI_VERSION 2
 
 /* ---- error codes ---- */
 #define NMMO_OK 0
@@ -111,8 +111,20 @@ enum NmmoEnvField {
   E_TICK = 0, E_MAP_ID, E_DONE, E_EPISODE, E_NPC_COUNT, E_NPC_NEXT_ID, E_FREE_HEAD,
   E_FREE_COUNT, E_SEED_LO, E_SEED_HI, E_PLAYERS_ALIVE, E_ENV_INDEX,
   E_ITEM_FREE_HEAD, E_ITEM_FREE_COUNT,
+  E_EVENT_COUNT,       /* events logged in this episode (SPEC.md §11) */
   NMMO_NE_USED,
   NMMO_NE = 16
+};
+
+/* ---- event log (SPEC.md §11; nmmo.lib.event_log): per env a ring of event_cap rows of
+ * NMMO_EVENT_COLS int32: id, ent_id, tick, event, type, level, number, gold, target_ent
+ * (stat_wrapper.py:219-300 reads cols event/item_type/level/distance/gold/damage/target_ent). */
+#define NMMO_EVENT_COLS 9
+enum NmmoEventCode {
+  EV_EAT_FOOD = 1, EV_DRINK_WATER = 2, EV_GO_FARTHEST = 3, EV_SCORE_HIT = 11, EV_PLAYER_KILL = 12,
+  EV_CONSUME_ITEM = 21, EV_GIVE_ITEM = 22, EV_DESTROY_ITEM = 23, EV_HARVEST_ITEM = 24,
+  EV_EQUIP_ITEM = 25, EV_LOOT_ITEM = 26, EV_GIVE_GOLD = 31, EV_LIST_ITEM = 32, EV_EARN_GOLD = 33,
+  EV_BUY_ITEM = 34, EV_LEVEL_UP = 41, EV_AGENT_CULLED = 91
 };
 
 typedef struct NmmoConfig {
@@ -128,6 +140,8 @@ typedef struct NmmoConfig {
   int32_t obs_layout;         /* NMMO_OBS_* */
   int32_t task_embed_dim;     /* TASK_EMBED_DIM 2048 (environment.py:44) */
   int32_t task_num_tick;      /* default task TickGE(num_tick) (manual_curriculum.py:56) */
+  int32_t event_cap;          /* event-log ring rows per env (SPEC.md §11); 0 = no event log */
+  int32_t reserved0;
   uint64_t map_seed;          /* map-bank generator seed */
   uint64_t env_index_base;    /* global index of env 0 of this handle (rank sharding) */
 } NmmoConfig;
@@ -192,6 +206,12 @@ NMMO_API int nmmo_set_timing(NmmoHandle* h, int32_t enable);
  * NULL disables. The caller owns and zeroes the buffer; capture-safe. */
 NMMO_API int nmmo_set_counters(NmmoHandle* h, uint64_t* dev_counters);
 NMMO_API int nmmo_read_timing(NmmoHandle* h, double* ms /* [2] */, int32_t* n);
+
+/* The event log of env `env` (realm.event_log.get_data): copies the most recent
+ * min(retained, max_rows) rows, oldest first, into host_rows [max_rows][NMMO_EVENT_COLS] and
+ * their count into *n_rows (retained = min(E_EVENT_COUNT, event_cap)). Synchronous. */
+NMMO_API int nmmo_get_events(NmmoHandle* h, int32_t env, int32_t* host_rows, int32_t max_rows,
+                             int32_t* n_rows);
 
 NMMO_API int32_t nmmo_n_envs(const NmmoHandle* h);
 NMMO_API const char* nmmo_last_error(void);

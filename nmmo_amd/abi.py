@@ -6,7 +6,7 @@ struct sizes against the compiled library and the enum values against the header
 
 import ctypes
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 NMMO_OK = 0
 NMMO_E_INVALID = -1
@@ -52,9 +52,37 @@ F = {name: i for i, name in enumerate(ENTITY_FIELDS)}
 ENV_FIELDS = [
     "tick", "map_id", "done", "episode", "npc_count", "npc_next_id", "free_head",
     "free_count", "seed_lo", "seed_hi", "players_alive", "env_index",
-    "item_free_head", "item_free_count",
+    "item_free_head", "item_free_count", "event_count",
 ]
 E = {name: i for i, name in enumerate(ENV_FIELDS)}
+
+# Event log (SPEC.md §11): int32 rows of EVENT_ATTRS; nmmo's column aliases (ATTR_TO_COL) as read
+# by the reference (stat_wrapper.py:219-300).
+EVENT_COLS = 9
+EVENT_ATTRS = ["id", "ent_id", "tick", "event", "type", "level", "number", "gold", "target_ent"]
+ATTR_TO_COL = {a: i for i, a in enumerate(EVENT_ATTRS)}
+ATTR_TO_COL.update(item_type=4, combat_style=4, quantity=6, damage=6, distance=6, price=7)
+
+
+class EventCode:
+    """nmmo.lib.event_code.EventCode (nmmo 2.1, SPEC.md §11)."""
+    EAT_FOOD = 1
+    DRINK_WATER = 2
+    GO_FARTHEST = 3
+    SCORE_HIT = 11
+    PLAYER_KILL = 12
+    CONSUME_ITEM = 21
+    GIVE_ITEM = 22
+    DESTROY_ITEM = 23
+    HARVEST_ITEM = 24
+    EQUIP_ITEM = 25
+    LOOT_ITEM = 26
+    GIVE_GOLD = 31
+    LIST_ITEM = 32
+    EARN_GOLD = 33
+    BUY_ITEM = 34
+    LEVEL_UP = 41
+    AGENT_CULLED = 91
 
 
 class NmmoConfig(ctypes.Structure):
@@ -71,6 +99,8 @@ class NmmoConfig(ctypes.Structure):
         ("obs_layout", ctypes.c_int32),
         ("task_embed_dim", ctypes.c_int32),
         ("task_num_tick", ctypes.c_int32),
+        ("event_cap", ctypes.c_int32),
+        ("reserved0", ctypes.c_int32),
         ("map_seed", ctypes.c_uint64),
         ("env_index_base", ctypes.c_uint64),
     ]

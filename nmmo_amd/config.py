@@ -50,6 +50,7 @@ class Config:
     systems: tuple = tuple(SYSTEM_BITS)
     early_stop_agent_num: int = 0        # BaseStatWrapper (stat_wrapper.py:68-69)
     task_num_tick: int = 1024            # default task TickGE(num_tick)
+    event_cap: int = 4096                # event-log ring rows per env (SPEC §11), 0 = off
     obs_layout: int = abi.OBS_FLAT
     map_seed: int = 0
 
@@ -119,6 +120,7 @@ class Config:
         c.obs_layout = self.obs_layout
         c.task_embed_dim = self.TASK_EMBED_DIM
         c.task_num_tick = self.task_num_tick
+        c.event_cap = self.event_cap
         c.map_seed = self.map_seed
         c.env_index_base = env_index_base
         return c

@@ -49,6 +49,7 @@ struct NmmoHandle {
   int16_t* d_iring = nullptr;
   int32_t* d_mlist = nullptr;
   int32_t* d_mcount = nullptr;
+  int32_t* d_events = nullptr;
   // bench timing (nmmo_set_timing): event pairs around the tick and obs kernels
   bool timing = false;
   int t_count = 0;
@@ -96,6 +97,7 @@ void nmmo_default_config(NmmoConfig* c) {
   c->obs_layout = NMMO_OBS_FLAT;
   c->task_embed_dim = 2048;
   c->task_num_tick = 1024;
+  c->event_cap = 4096;
   c->map_seed = 0;
   c->env_index_base = 0;
 }
@@ -145,7 +147,8 @@ void nmmo_destroy(NmmoHandle* h) {
   (void)hipSetDevice(h->device);
   for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
   void* bufs[] = {h->d_env,  h->d_ent,   h->d_ring,  h->d_mat,   h->d_dep,   h->d_bank,
-                  h->d_task, h->d_seeds, h->d_items, h->d_iring, h->d_mlist, h->d_mcount};
+                  h->d_task, h->d_seeds, h->d_items, h->d_iring, h->d_mlist, h->d_mcount,
+                  h->d_events};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   delete h;
@@ -163,6 +166,7 @@ int nmmo_create(const NmmoConfig* cfg, int32_t n_envs, uint64_t seed, int32_t de
   if (cfg->map_n <= 0) return fail(NMMO_E_INVALID, "map_n must be > 0");
   if (cfg->horizon <= 0 || cfg->task_num_tick <= 0) return fail(NMMO_E_INVALID, "horizon/task_num_tick");
   if (cfg->task_embed_dim < 0 || cfg->task_embed_dim > 65536) return fail(NMMO_E_INVALID, "task_embed_dim");
+  if (cfg->event_cap < 0 || cfg->event_cap > (1 << 24)) return fail(NMMO_E_INVALID, "event_cap in 0..2^24");
   if (cfg->obs_layout != NMMO_OBS_NONE && cfg->obs_layout != NMMO_OBS_FLAT)
     return fail(NMMO_E_INVALID, "obs_layout %d", cfg->obs_layout);
   NmmoHandle* h = new NmmoHandle();
@@ -189,6 +193,7 @@ int nmmo_create(const NmmoConfig* cfg, int32_t n_envs, uint64_t seed, int32_t de
   ALLOC(h->d_iring, n * NMMO_INV_SLOTS * P * 2);
   ALLOC(h->d_mlist, n * NMMO_MARKET_ROWS * 4);
   ALLOC(h->d_mcount, n * 4);
+  if (cfg->event_cap > 0) ALLOC(h->d_events, n * (size_t)cfg->event_cap * NMMO_EVENT_COLS * 4);
 #undef ALLOC
   if (init_kernels() != hipSuccess) return cleanup_fail(fail(NMMO_E_HIP, "kernel attributes"));
   if (task_embedding && cfg->task_embed_dim > 0) {
@@ -198,7 +203,7 @@ int nmmo_create(const NmmoConfig* cfg, int32_t n_envs, uint64_t seed, int32_t de
       return cleanup_fail(fail(NMMO_E_HIP, "task upload"));
   }
   h->st = DevState{h->d_env,   h->d_ent,   h->d_ring,  h->d_mat,    h->d_dep, h->d_bank,
-                   h->d_items, h->d_iring, h->d_mlist, h->d_mcount, n_envs,   P,
+                   h->d_items, h->d_iring, h->d_mlist, h->d_mcount, h->d_events, n_envs, P,
                    N,          S,          seed,       nullptr,     *cfg};
   if (launch_mapgen(cfg->map_seed, cfg->map_n, h->d_bank, nullptr) != hipSuccess ||
       hipDeviceSynchronize() != hipSuccess)
@@ -368,6 +373,30 @@ int nmmo_set_state(NmmoHandle* h, const void* host_buf, size_t nbytes) {
   HIP_TRY(hipMemcpy(h->d_iring, iring.data(), iring.size() * 2, hipMemcpyHostToDevice));
   HIP_TRY(launch_rebuild_dep(h->st, nullptr));
   HIP_TRY(hipDeviceSynchronize());
+  return NMMO_OK;
+}
+
+int nmmo_get_events(NmmoHandle* h, int32_t env, int32_t* host_rows, int32_t max_rows, int32_t* n_rows) {
+  if (!h || !n_rows || (max_rows > 0 && !host_rows)) return fail(NMMO_E_INVALID, "null argument");
+  if (env < 0 || env >= h->st.n_envs) return fail(NMMO_E_INVALID, "env %d out of range", env);
+  *n_rows = 0;
+  const int cap = h->cfg.event_cap;
+  if (cap <= 0 || max_rows <= 0) return NMMO_OK;
+  HIP_TRY(hipSetDevice(h->device));
+  HIP_TRY(hipDeviceSynchronize());
+  int32_t cnt = 0;
+  HIP_TRY(hipMemcpy(&cnt, h->d_env + (size_t)env * NMMO_NE + E_EVENT_COUNT, 4, hipMemcpyDeviceToHost));
+  int n = cnt < cap ? cnt : cap;
+  if (n > max_rows) n = max_rows;
+  const int32_t* ring = h->d_events + (size_t)env * cap * NMMO_EVENT_COLS;
+  const int first = (int)((cnt - n) % cap);  // ring index of the oldest copied row
+  const int n1 = n < cap - first ? n : cap - first;
+  HIP_TRY(hipMemcpy(host_rows, ring + (size_t)first * NMMO_EVENT_COLS, (size_t)n1 * NMMO_EVENT_COLS * 4,
+                    hipMemcpyDeviceToHost));
+  if (n > n1)
+    HIP_TRY(hipMemcpy(host_rows + (size_t)n1 * NMMO_EVENT_COLS, ring, (size_t)(n - n1) * NMMO_EVENT_COLS * 4,
+                      hipMemcpyDeviceToHost));
+  *n_rows = n;
   return NMMO_OK;
 }
 

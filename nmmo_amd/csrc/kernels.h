@@ -16,6 +16,7 @@ struct DevState {
   int16_t* iring;        // [n][kInv*P] free item rows
   int32_t* mlist;        // [n][NMMO_MARKET_ROWS] end-of-tick listings, ascending row: row | owner<<16 | slot<<24
   int* mcount;           // [n] listings in mlist (<= NMMO_MARKET_ROWS)
+  int32_t* events;       // [n][cfg.event_cap][NMMO_EVENT_COLS] event-log rings (SPEC §11)
   int n_envs, P, N, S;   // N = NPC capacity (0 when the NPC system is off), S = P + N
   uint64_t seed;         // create seed (first-episode seeds)
   unsigned long long* counters;  // optional device u64 [2]: agent-steps, finished episodes

@@ -63,6 +63,10 @@ struct Ctx {
   int16_t* order;    // [128] Buy order / serial replay lists
   uint8_t* fired;    // [128] executed attack (ammunition)
   uint32_t* ikey;    // [128] Buy sort keys
+  int16_t* ev_dmg;   // [128] damage of the player's executed attack (-1 none): SCORE_HIT
+  int16_t* ev_lvl;   // [128] combat level reached by that attack's XP (0 none): LEVEL_UP
+  int32_t* evg;      // this env's event ring (global), evcap rows (SPEC §11)
+  int evcap, tick1;  // ring rows (0 = no event log); tick + 1 (the events' tick column)
   int S, P, N, IC;
   bool items, exch, prof, equip;
   const NmmoConfig* cfg;
@@ -98,7 +102,7 @@ __host__ __device__ inline size_t item_lds_bytes(int P) {
   const size_t ic = (size_t)kInv * P;
   return (size_t)P * kInv * 8 + al(ic * 2) + al((ic + 1) * 2) + kLWords * 8;
 }
-constexpr size_t kPlayerArrBytes = 7 * 256 + 128 + 512;  // per-player action / replay arrays
+constexpr size_t kPlayerArrBytes = 9 * 256 + 128 + 512;  // per-player action / replay arrays
 
 __host__ __device__ inline size_t tick_lds_bytes(int S, int P, bool items) {
   auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
@@ -145,6 +149,8 @@ __device__ __forceinline__ Ctx make_ctx(unsigned char* smem, const DevState& st,
     c.order = reinterpret_cast<int16_t*>(smem + o); o += 256;
     c.fired = smem + o; o += 128;
     c.ikey = reinterpret_cast<uint32_t*>(smem + o); o += 512;
+    c.ev_dmg = reinterpret_cast<int16_t*>(smem + o); o += 256;
+    c.ev_lvl = reinterpret_cast<int16_t*>(smem + o); o += 256;
   }
   c.T = reinterpret_cast<int16_t*>(smem + o); o += al((size_t)kNFLive * S * 2);
   c.vism = reinterpret_cast<uint64_t*>(smem + o); o += (size_t)128 * ((S + 63) / 64) * 8;
@@ -167,6 +173,9 @@ __device__ __forceinline__ Ctx make_ctx(unsigned char* smem, const DevState& st,
   c.died = smem + o; o += 128;
   c.mat = st.mat + (size_t)e * kTiles;
   c.bank = st.bank;
+  c.evcap = st.cfg.event_cap > 0 ? st.cfg.event_cap : 0;
+  c.evg = c.evcap ? st.events + (size_t)e * c.evcap * NMMO_EVENT_COLS : nullptr;
+  c.tick1 = 0;
   c.S = S;
   c.P = st.P;
   c.N = st.N;
@@ -334,6 +343,31 @@ __device__ __forceinline__ int kth_listed(const Ctx& c, int k) {
     k -= pc;
   }
   return -1;
+}
+
+// ---------------------------------------------------------------- event log (SPEC §11)
+// Row of the episode's event `idx` (0-based) for player p.
+__device__ __forceinline__ void ev_put(const Ctx& c, int idx, int p, int code, int type, int level,
+                                       int number, int gold, int target) {
+  int32_t* r = c.evg + (size_t)(idx % c.evcap) * NMMO_EVENT_COLS;
+  r[0] = idx + 1;
+  r[1] = p + 1;
+  r[2] = c.tick1;
+  r[3] = code;
+  r[4] = type;
+  r[5] = level;
+  r[6] = number;
+  r[7] = gold;
+  r[8] = target;
+}
+// Appends each thread's n events in thread (= slot) order: emit(first_index) writes them.
+// evn is the block-uniform running count. Every thread must call (barriers inside).
+template <typename F>
+__device__ __forceinline__ void ev_append(Ctx& c, int& evn, int n, F&& emit) {
+  int tot;
+  const int pre = block_prefix_sum(n, c.wtot, &tot);
+  if (n) emit(evn + pre);
+  evn += tot;
 }
 
 // ---------------------------------------------------------------- NPC spawn (SPEC §5.7)
@@ -562,12 +596,16 @@ __device__ __forceinline__ int eval_attack(const Ctx& c, int x, int sty, int t) 
 
 __device__ __forceinline__ void apply_attack(Ctx& c, int x, int sty, int t, int dmg, int tick) {
   TF(F_ATTACKER_ID, t) = TF(F_ID, x);
+  int lvl_up = 0;
   if (x < c.P && sys(c, NMMO_SYS_PROGRESSION)) {
     const int f = F_MELEE_EXP + 2 * sty;
     const int ex = TF(f, x) + 6;
     TF(f, x) = (int16_t)ex;
     const int nl = level_at_exp(ex);
-    if (nl > TF(f - 1, x)) TF(f - 1, x) = (int16_t)nl;
+    if (nl > TF(f - 1, x)) {
+      TF(f - 1, x) = (int16_t)nl;
+      lvl_up = nl;
+    }
   }
   TF(F_DAMAGE, t) = (int16_t)dmg;
   const int h = max(0, (int)TF(F_HEALTH, t) - dmg);
@@ -575,9 +613,11 @@ __device__ __forceinline__ void apply_attack(Ctx& c, int x, int sty, int t, int 
   if (h == 0) TF(F_PLAYER_KILLS, x) += 1;
   TF(F_LATEST_COMBAT_TICK, x) = (int16_t)(tick + 1);
   TF(F_LATEST_COMBAT_TICK, t) = (int16_t)(tick + 1);
-  if (x < c.P) {  // ammunition and loot are applied after the phase, in slot order
+  if (x < c.P) {  // ammunition, loot and the events are applied after the phase, in slot order
     if (c.equip) c.fired[x] = 1;
     if (h == 0) c.kill[x] = (int16_t)t;
+    c.ev_dmg[x] = (int16_t)dmg;
+    c.ev_lvl[x] = (int16_t)lvl_up;
   }
 }
 
@@ -599,7 +639,7 @@ __device__ __forceinline__ void fire_ammo(Ctx& c, int x, int style) {
 }
 
 // a player killed t: gold, then t's items (player) or drops (NPC) (serial; SPEC §9 Death)
-__device__ __forceinline__ void loot(Ctx& c, int x, int t) {
+__device__ __forceinline__ void loot(Ctx& c, int x, int t, int& evn) {
   if (sys(c, NMMO_SYS_EXCHANGE)) {
     TF(F_GOLD, x) = (int16_t)(TF(F_GOLD, x) + TF(F_GOLD, t));
     TF(F_GOLD, t) = 0;
@@ -609,6 +649,7 @@ __device__ __forceinline__ void loot(Ctx& c, int x, int t) {
     uint2* inv = c.inv + t * kInv;
     while (it_type(inv[0])) {
       uint2 w = inv[0];
+      if (c.evcap) ev_put(c, evn++, x, EV_LOOT_ITEM, it_type(w), it_level(w), it_qty(w), 0, TF(F_ID, t));
       w.x &= 0x1FFu;  // unequipped, unlisted
       inv_remove(inv, 0);
       receive_moved(c, x, w);
@@ -616,8 +657,14 @@ __device__ __forceinline__ void loot(Ctx& c, int x, int t) {
     update_item_level(c, t);
   } else {
     const int lvl = TF(F_NPC_LEVEL, t) > 0 ? TF(F_NPC_LEVEL, t) : 1;
-    if (sys(c, NMMO_SYS_EQUIPMENT)) receive_new(c, x, T_HAT + TF(F_DROP_ARMOR, t), lvl);
-    if (sys(c, NMMO_SYS_PROFESSION)) receive_new(c, x, T_ROD + TF(F_DROP_TOOL, t), lvl);
+    if (sys(c, NMMO_SYS_EQUIPMENT)) {
+      receive_new(c, x, T_HAT + TF(F_DROP_ARMOR, t), lvl);
+      if (c.evcap) ev_put(c, evn++, x, EV_LOOT_ITEM, T_HAT + TF(F_DROP_ARMOR, t), lvl, 1, 0, TF(F_ID, t));
+    }
+    if (sys(c, NMMO_SYS_PROFESSION)) {
+      receive_new(c, x, T_ROD + TF(F_DROP_TOOL, t), lvl);
+      if (c.evcap) ev_put(c, evn++, x, EV_LOOT_ITEM, T_ROD + TF(F_DROP_TOOL, t), lvl, 1, 0, TF(F_ID, t));
+    }
   }
 }
 
@@ -659,6 +706,9 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
   const bool inslot = s < nslots;
   const bool items = c.items;
   const uint64_t seed = env_seed(c);
+  c.tick1 = tick + 1;
+  const bool evon = c.evcap > 0;
+  int evn = c.E[E_EVENT_COUNT];  // block-uniform running event count (SPEC §11)
 
   if (s < P) c.pres[s] = (uint8_t)TF(F_ALIVE, s);
   for (int k = tid; k < rp_groups(S) * 4; k += nt) c.rp[k] = -1;
@@ -737,6 +787,8 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
     c.a_gga[s] = 0;
     c.kill[s] = -1;
     c.fired[s] = 0;
+    c.ev_dmg[s] = -1;
+    c.ev_lvl[s] = 0;
   }
   if (s < P && c.pres[s]) {
     const int32_t* a = act + (size_t)s * kHeads;
@@ -794,6 +846,9 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
   // position hash (lowest slot per tile via atomicMin): first-in-slot-order harvests.
   const bool resource = sys(c, NMMO_SYS_RESOURCE);
   int tile = 0, hslot = -1;
+  // this player's update-phase events: EAT_FOOD, DRINK_WATER, harvests and level-ups
+  bool e_eat = false, e_drink = false;
+  int e_fish = 0, e_fish_nl = 0, e_on_q = -1, e_on_type = 0, e_on_lvl = 0, e_on_nl = 0;
   if (inslot && TF(F_ALIVE, s)) {
     if (TF(F_DAMAGE, s) == 0) TF(F_ATTACKER_ID, s) = 0;
     TF(F_DAMAGE, s) = 0;
@@ -817,6 +872,7 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
         const bool drink = c.mat[tile - kSize] == M_WATER || c.mat[tile + kSize] == M_WATER ||
                            c.mat[tile - 1] == M_WATER || c.mat[tile + 1] == M_WATER;
         TF(F_WATER, s) = (int16_t)(drink ? 100 : max(0, water - 5));
+        e_drink = drink;
       }
       if ((resource && c.mat[tile] == M_FOILAGE) || c.prof) {
         int hh = (int)(h32((uint32_t)tile) & (kHash - 1));
@@ -834,6 +890,7 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
   NMMO_STAMP(3);
   const bool first_on_tile = hslot >= 0 && c.hmin[hslot] == s;
   if (resource && first_on_tile && c.mat[tile] == M_FOILAGE) {
+    e_eat = true;
     TF(F_FOOD, s) = 100;
     c.mat[tile] = M_SCRUB;
     atomicOr(&c.dep[tile >> 5], 1u << (tile & 31));
@@ -900,7 +957,11 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
       const int ex = TF(F_FISHING_EXP, s) + 30 * lvl_f;
       TF(F_FISHING_EXP, s) = (int16_t)ex;
       const int nl = level_at_exp(ex);
-      if (nl > TF(F_FISHING_LEVEL, s)) TF(F_FISHING_LEVEL, s) = (int16_t)nl;
+      if (nl > TF(F_FISHING_LEVEL, s)) {
+        TF(F_FISHING_LEVEL, s) = (int16_t)nl;
+        e_fish_nl = nl;
+      }
+      e_fish = lvl_f;
     }
     if (q_on >= 0) {
       const int to = q_on == 0 ? M_WEEDS : q_on == 1 ? M_SLAG : q_on == 2 ? M_STUMP : M_FRAGMENT;
@@ -916,7 +977,13 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
       const int ex = TF(fe, s) + (q_on == 0 ? 30 : 15) * lvl_on;
       TF(fe, s) = (int16_t)ex;
       const int nl = level_at_exp(ex);
-      if (nl > TF(fe - 1, s)) TF(fe - 1, s) = (int16_t)nl;
+      if (nl > TF(fe - 1, s)) {
+        TF(fe - 1, s) = (int16_t)nl;
+        e_on_nl = nl;
+      }
+      e_on_q = q_on;
+      e_on_type = out_type;
+      e_on_lvl = lvl_on;
     }
     __syncthreads();
     if (tid == 0 && tot) {
@@ -926,10 +993,21 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
   }
   __syncthreads();
   NMMO_STAMP(15);
+  if (evon) {
+    const int n = (int)e_eat + (int)e_drink + (e_fish > 0) + (e_fish_nl > 0) + (e_on_q >= 0) + (e_on_nl > 0);
+    ev_append(c, evn, n, [&](int i) {
+      if (e_eat) ev_put(c, i++, s, EV_EAT_FOOD, 0, 0, 0, 0, 0);
+      if (e_drink) ev_put(c, i++, s, EV_DRINK_WATER, 0, 0, 0, 0, 0);
+      if (e_fish) ev_put(c, i++, s, EV_HARVEST_ITEM, T_RATION, e_fish, 1, 0, 0);
+      if (e_fish_nl) ev_put(c, i++, s, EV_LEVEL_UP, 4, e_fish_nl, 0, 0, 0);
+      if (e_on_q >= 0) ev_put(c, i++, s, EV_HARVEST_ITEM, e_on_type, e_on_lvl, 1, 0, 0);
+      if (e_on_nl) ev_put(c, i++, s, EV_LEVEL_UP, 5 + e_on_q, e_on_nl, 0, 0, 0);
+    });
+  }
 
   if (items) {
     // 3. Use (priority 10): own inventory only -> parallel; consumed rows freed in slot order
-    int freed = -1;
+    int freed = -1, u_code = 0, u_type = 0, u_lvl = 0, u_num = 0;
     if (s < P && use_row >= 0 && acts(c, s)) {
       uint2* inv = c.inv + s * kInv;
       const int k = inv_find(inv, use_row);
@@ -945,6 +1023,10 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
               if (it_equipped(inv[j]) && equip_slot(it_type(inv[j])) == slot) inv[j].x &= ~(1u << 9);
             }
             inv[k].x |= 1u << 9;
+            u_code = EV_EQUIP_ITEM;
+            u_type = type;
+            u_lvl = lvl;
+            u_num = it_qty(w);
           }
           update_item_level(c, s);
         } else if (lvl <= requirement_level(c.T, S, s, type)) {
@@ -956,6 +1038,10 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
             TF(F_HEALTH, s) = (int16_t)min(100, TF(F_HEALTH, s) + rs);
           }
           inv[k].y -= 1u;
+          u_code = EV_CONSUME_ITEM;
+          u_type = type;
+          u_lvl = lvl;
+          u_num = 1;
           if (it_qty(inv[k]) == 0) {
             freed = it_row(w);
             inv_remove(inv, k);
@@ -964,6 +1050,7 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
       }
     }
     ring_append_ordered(c, freed);
+    if (evon) ev_append(c, evn, u_code ? 1 : 0, [&](int i) { ev_put(c, i, s, u_code, u_type, u_lvl, u_num, 0, 0); });
 
     // Buy (priority 20): buyers in shuffled order (key draw(tick, BUY_ORDER, id), ties by id),
     // replayed by thread 0 against the row -> owner map of the tick-start listings
@@ -997,12 +1084,18 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
             if (!price || TF(F_GOLD, b) < price || !has_room(c, b, w)) continue;
             TF(F_GOLD, b) = (int16_t)(TF(F_GOLD, b) - price);
             TF(F_GOLD, owner) = (int16_t)(TF(F_GOLD, owner) + price);
+            if (evon) {
+              ev_put(c, evn++, b, EV_BUY_ITEM, it_type(w), it_level(w), it_qty(w), price, 0);
+              ev_put(c, evn++, owner, EV_EARN_GOLD, 0, 0, 0, price, 0);
+            }
             w.x &= 0x1FFu;
             inv_remove(oinv, k);
             c.rmap[row] = receive_moved(c, b, w) ? (int16_t)b : (int16_t)-1;
           }
+          c.E[E_EVENT_COUNT] = evn;
         }
         __syncthreads();
+        evn = c.E[E_EVENT_COUNT];
       }
     }
 
@@ -1023,6 +1116,7 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
             const int k = inv_find(inv, c.a_give[p]);
             if (k >= 0 && !it_equipped(inv[k]) && !it_price(inv[k]) && has_room(c, t, inv[k])) {
               const uint2 w = inv[k];
+              if (evon) ev_put(c, evn++, p, EV_GIVE_ITEM, it_type(w), it_level(w), it_qty(w), 0, TF(F_ID, t));
               inv_remove(inv, k);
               receive_moved(c, t, w);
             }
@@ -1031,23 +1125,31 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
           if (t >= 0 && t < P && t != p && acts(c, t) && c.a_gga[p] <= TF(F_GOLD, p) && same_tile(c, t, p)) {
             TF(F_GOLD, p) = (int16_t)(TF(F_GOLD, p) - c.a_gga[p]);
             TF(F_GOLD, t) = (int16_t)(TF(F_GOLD, t) + c.a_gga[p]);
+            if (evon) ev_put(c, evn++, p, EV_GIVE_GOLD, 0, 0, 0, c.a_gga[p], TF(F_ID, t));
           }
         }
+        c.E[E_EVENT_COUNT] = evn;
       }
       __syncthreads();
+      evn = c.E[E_EVENT_COUNT];
     }
 
     // Destroy (priority 40): own inventory, rows freed in slot order
     freed = -1;
+    uint2 dw = make_uint2(0u, 0u);
     if (s < P && destroy_row >= 0 && acts(c, s)) {
       uint2* inv = c.inv + s * kInv;
       const int k = inv_find(inv, destroy_row);
       if (k >= 0 && !it_equipped(inv[k]) && !it_price(inv[k])) {
         freed = destroy_row;
+        dw = inv[k];
         inv_remove(inv, k);
       }
     }
     ring_append_ordered(c, freed);
+    if (evon)
+      ev_append(c, evn, freed >= 0 ? 1 : 0,
+                [&](int i) { ev_put(c, i, s, EV_DESTROY_ITEM, it_type(dw), it_level(dw), it_qty(dw), 0, 0); });
   }
 
   NMMO_STAMP(14);
@@ -1100,6 +1202,18 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
     }
   }
   __syncthreads();
+  if (evon) {  // SCORE_HIT, LEVEL_UP, PLAYER_KILL per player attacker in slot order
+    const int dm = s < P ? c.ev_dmg[s] : -1, lv = s < P ? c.ev_lvl[s] : 0, kv = s < P ? c.kill[s] : -1;
+    ev_append(c, evn, (dm >= 0) + (lv > 0) + (kv >= 0), [&](int i) {
+      const int sk = c.asty[s] + 1;
+      if (dm >= 0) ev_put(c, i++, s, EV_SCORE_HIT, sk, 0, dm, 0, 0);
+      if (lv > 0) ev_put(c, i++, s, EV_LEVEL_UP, sk, lv, 0, 0, 0);
+      if (kv >= 0) {
+        const int vl = max((int)TF(F_MELEE_LEVEL, kv), max((int)TF(F_RANGE_LEVEL, kv), (int)TF(F_MAGE_LEVEL, kv)));
+        ev_put(c, i++, s, EV_PLAYER_KILL, 0, vl, 0, 0, TF(F_ID, kv));
+      }
+    });
+  }
   if (items || sys(c, NMMO_SYS_EXCHANGE)) {
     // ammunition and loot of the executed player attacks, in slot order (equipment sums and
     // every attack's validity are unaffected by them, so deferring is exact)
@@ -1112,14 +1226,17 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
       for (int i = 0; i < nn; i++) {
         const int x = c.order[i];
         if (c.fired[x]) fire_ammo(c, x, c.asty[x]);
-        if (c.kill[x] >= 0) loot(c, x, c.kill[x]);
+        if (c.kill[x] >= 0) loot(c, x, c.kill[x], evn);
       }
+      c.E[E_EVENT_COUNT] = evn;
     }
     __syncthreads();
+    evn = c.E[E_EVENT_COUNT];
   }
   NMMO_STAMP(5);
 
   // 3b. Move (priority 60)
+  int gf = 0;  // GO_FARTHEST record
   if (inslot && c.amove[s] >= 0 && TF(F_ALIVE, s) && TF(F_HEALTH, s) > 0) {
     const int d = c.amove[s];
     const int nr = TF(F_ROW, s) + dir_dr(d), nc = TF(F_COL, s) + dir_dc(d);
@@ -1127,15 +1244,31 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
       TF(F_ROW, s) = (int16_t)nr;
       TF(F_COL, s) = (int16_t)nc;
       const int progress = 64 - linf(80, 80, nr, nc);
-      if (progress > TF(F_EXPLORATION, s)) TF(F_EXPLORATION, s) = (int16_t)progress;
+      if (progress > TF(F_EXPLORATION, s)) {
+        TF(F_EXPLORATION, s) = (int16_t)progress;
+        gf = s < P ? progress : 0;
+      }
     }
   }
   // Sell (priority 70): own inventory
+  uint2 sw = make_uint2(0u, 0u);
   if (c.exch && s < P && sell_row >= 0 && acts(c, s)) {
     uint2* inv = c.inv + s * kInv;
     const int k = inv_find(inv, sell_row);
-    if (k >= 0 && !it_equipped(inv[k]))
+    if (k >= 0 && !it_equipped(inv[k])) {
       inv[k].x = (inv[k].x & 0x3FFu) | ((uint32_t)sell_price << 10) | ((uint32_t)tick << 17);
+      sw = inv[k];
+    }
+  }
+  if (evon) {  // GO_FARTHEST (Move) events, then LIST_ITEM (Sell) events: both counts in one scan
+    const int nl = it_type(sw) ? 1 : 0;
+    int tot;
+    const int pre = block_prefix_sum((gf > 0 ? 1 : 0) | (nl << 16), c.wtot, &tot);
+    if (gf > 0) ev_put(c, evn + (pre & 0xFFFF), s, EV_GO_FARTHEST, 0, 0, gf, 0, 0);
+    if (nl)
+      ev_put(c, evn + (tot & 0xFFFF) + (pre >> 16), s, EV_LIST_ITEM, it_type(sw), it_level(sw), it_qty(sw),
+             sell_price, 0);
+    evn += (tot & 0xFFFF) + (tot >> 16);
   }
   __syncthreads();
   NMMO_STAMP(6);
@@ -1147,6 +1280,7 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
   int npdead;
   block_prefix_count(dead && s < P, c.wtot, &npdead);
   if (s < P) c.died[s] = dead ? 1 : 0;
+  if (evon) ev_append(c, evn, dead && s < P ? 1 : 0, [&](int i) { ev_put(c, i, s, EV_AGENT_CULLED, 0, 0, 0, 0, 0); });
   if (dead) {
     c.ring[(c.E[E_FREE_HEAD] + c.E[E_FREE_COUNT] + dpos) % S] = TF(F_DS_ROW, s);
     TF(F_ALIVE, s) = 0;
@@ -1236,6 +1370,7 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
     const int alive = c.E[E_PLAYERS_ALIVE];
     const int done = alive == 0 || tick + 1 >= c.cfg->horizon || alive <= c.cfg->early_stop_agent_num;
     c.E[E_DONE] = done;
+    c.E[E_EVENT_COUNT] = evn;
   }
   __syncthreads();
   if (s < P) {

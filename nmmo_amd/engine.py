@@ -135,6 +135,17 @@ class NmmoEngine:
         check(lib().nmmo_set_state(self.h, buf.ctypes.data_as(ctypes.c_void_p), buf.nbytes),
               "nmmo_set_state")
 
+    def events(self, env: int, max_rows: int | None = None) -> np.ndarray:
+        """Retained event-log rows of `env`, oldest first: int32 [n, 9] (SPEC §11 columns
+        id, ent_id, tick, event, type, level, number, gold, target_ent). Synchronous."""
+        cap = self.config.event_cap
+        m = cap if max_rows is None else min(max_rows, cap)
+        buf = np.zeros((max(m, 1), abi.EVENT_COLS), np.int32)
+        n = ctypes.c_int32()
+        check(lib().nmmo_get_events(self.h, env, buf.ctypes.data_as(ctypes.c_void_p), m, ctypes.byref(n)),
+              "nmmo_get_events")
+        return buf[:n.value].copy()
+
     def map_bank(self) -> np.ndarray:
         buf = np.zeros((self.config.MAP_N, abi.MAP_SIZE, abi.MAP_SIZE), np.uint8)
         check(lib().nmmo_get_map_bank(self.h, buf.ctypes.data_as(ctypes.c_void_p), buf.nbytes),

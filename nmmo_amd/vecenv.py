@@ -203,9 +203,9 @@ class NmmoEnv:
 
     @property
     def realm(self):
-        """Partial realm facade: `realm.tick` and `realm.players[id]` with the entity columns as
-        attributes (the reads of stat_wrapper.py:136-185); the event log arrives with row A16."""
-        return _Realm(self.state())
+        """Partial realm facade: `realm.tick`, `realm.players[id]` with the entity columns as
+        attributes and `realm.event_log` (the reads of stat_wrapper.py:122-185, 216-285)."""
+        return _Realm(self.state(), self.engine.events(0))
 
     def state(self) -> dict:
         st = self.engine.get_state()
@@ -239,9 +239,32 @@ class _Entity:
             setattr(self, k, int(v[slot]))
 
 
+class EventLog:
+    """realm.event_log facade (nmmo.lib.event_log.EventLogger as read by stat_wrapper.py:123,
+    218-219): get_data(agents=[...], tick=None|-1|t) and attr_to_col over the engine's ring."""
+
+    def __init__(self, rows: np.ndarray, tick: int):
+        self._rows = rows
+        self._tick = tick
+        self.attr_to_col = dict(abi.ATTR_TO_COL)
+
+    def get_data(self, agents=None, event_code=None, tick=None) -> np.ndarray:
+        r = self._rows
+        if agents is not None:
+            r = r[np.isin(r[:, abi.ATTR_TO_COL["ent_id"]], list(agents))]
+        if event_code is not None:
+            r = r[r[:, abi.ATTR_TO_COL["event"]] == event_code]
+        if tick is not None:
+            t = self._tick if tick == -1 else tick
+            r = r[r[:, abi.ATTR_TO_COL["tick"]] == t]
+        return r
+
+
 class _Realm:
-    def __init__(self, st: dict):
+    def __init__(self, st: dict, events: np.ndarray | None = None):
         self.tick = st["tick"]
+        self.event_log = EventLog(np.zeros((0, abi.EVENT_COLS), np.int32) if events is None else events,
+                                  self.tick)
         ent = st["entities"]
         self.players = {int(ent["id"][s]): _Entity(ent, s) for s in range(len(ent["id"]))
                         if ent["id"][s] > 0 and ent["alive"][s]}

@@ -186,6 +186,7 @@ typedef struct {
   uint8_t* bank;       /* [map_n][TILES] */
   uint32_t* items;     /* [n_envs][P][INV][2] (SPEC §9 item words) */
   int16_t* iring;      /* [n_envs][INV*P] free item rows */
+  int32_t* events;     /* [n_envs][event_cap][NMMO_EVENT_COLS] event-log rings (SPEC §11) */
   float task[4096];
 } Oracle;
 
@@ -355,11 +356,45 @@ static int usable(const int16_t* T, int S, int p, const uint32_t* it) {
   if (equip_slot(IT_TYPE(it)) >= 0 && IT_EQUIPPED(it)) return 1;
   return IT_LEVEL(it) <= requirement_level(T, S, p, IT_TYPE(it));
 }
-static void add_skill_exp(int16_t* T, int S, int p, int f_exp, int xp) {
+/* returns the new level on a level-up, else 0 */
+static int add_skill_exp(int16_t* T, int S, int p, int f_exp, int xp) {
   int ex = FLD(T, f_exp, p) + xp;
   FLD(T, f_exp, p) = (int16_t)ex;
   int nl = level_at_exp(ex);
-  if (nl > FLD(T, f_exp - 1, p)) FLD(T, f_exp - 1, p) = (int16_t)nl;
+  if (nl > FLD(T, f_exp - 1, p)) { FLD(T, f_exp - 1, p) = (int16_t)nl; return nl; }
+  return 0;
+}
+
+/* ------------------------------------------------------------------ event log (SPEC §11) */
+/* EventLogger.record: players only; row k of the episode at ring index (k-1) mod event_cap */
+static void log_event(Oracle* o, int e, int p, int code, int type, int level, int number, int gold,
+                      int target) {
+  const int cap = o->cfg.event_cap;
+  if (cap <= 0 || p < 0 || p >= o->P) return;
+  int32_t* E = ENV(o, e);
+  const int32_t id = ++E[E_EVENT_COUNT];
+  int32_t* r = o->events + ((size_t)e * cap + (size_t)((id - 1) % cap)) * NMMO_EVENT_COLS;
+  r[0] = id; r[1] = p + 1; r[2] = E[E_TICK] + 1; r[3] = code; r[4] = type; r[5] = level;
+  r[6] = number; r[7] = gold; r[8] = target;
+}
+/* loot events are appended after all attack events of the tick (SPEC §11 order (7)) */
+static __thread int32_t g_pend[128 * 16][7];
+static __thread int g_npend;
+static void pend_event(int p, int code, int type, int level, int number, int gold, int target) {
+  int32_t* r = g_pend[g_npend++];
+  r[0] = p; r[1] = code; r[2] = type; r[3] = level; r[4] = number; r[5] = gold; r[6] = target;
+}
+static void flush_pending(Oracle* o, int e) {
+  for (int i = 0; i < g_npend; i++)
+    log_event(o, e, g_pend[i][0], g_pend[i][1], g_pend[i][2], g_pend[i][3], g_pend[i][4],
+              g_pend[i][5], g_pend[i][6]);
+  g_npend = 0;
+}
+static int max_combat_level(const int16_t* T, int S, int s) {
+  int l = FLD(T, F_MELEE_LEVEL, s);
+  if (FLD(T, F_RANGE_LEVEL, s) > l) l = FLD(T, F_RANGE_LEVEL, s);
+  if (FLD(T, F_MAGE_LEVEL, s) > l) l = FLD(T, F_MAGE_LEVEL, s);
+  return l;
 }
 
 /* ------------------------------------------------------------------ reset (SPEC §4) */
@@ -571,14 +606,21 @@ static void loot(Oracle* o, int e, int x, int t) {
     while (IT_TYPE(inv)) {
       uint32_t w0 = inv[0] & 0x1FFu, w1 = inv[1]; /* unequipped, unlisted */
       w0 &= ~(1u << 9);
+      pend_event(x, EV_LOOT_ITEM, IT_TYPE(inv), IT_LEVEL(inv), IT_QTY(inv), 0, FLD(T, F_ID, t));
       inv_remove(inv, 0);
       receive_moved(o, e, x, w0, w1);
     }
     update_item_level(o, e, t);
   } else {
     int lvl = FLD(T, F_NPC_LEVEL, t) > 0 ? FLD(T, F_NPC_LEVEL, t) : 1;
-    if (sys_on(o, NMMO_SYS_EQUIPMENT)) receive_new(o, e, x, T_HAT + FLD(T, F_DROP_ARMOR, t), lvl);
-    if (sys_on(o, NMMO_SYS_PROFESSION)) receive_new(o, e, x, T_ROD + FLD(T, F_DROP_TOOL, t), lvl);
+    if (sys_on(o, NMMO_SYS_EQUIPMENT)) {
+      receive_new(o, e, x, T_HAT + FLD(T, F_DROP_ARMOR, t), lvl);
+      pend_event(x, EV_LOOT_ITEM, T_HAT + FLD(T, F_DROP_ARMOR, t), lvl, 1, 0, FLD(T, F_ID, t));
+    }
+    if (sys_on(o, NMMO_SYS_PROFESSION)) {
+      receive_new(o, e, x, T_ROD + FLD(T, F_DROP_TOOL, t), lvl);
+      pend_event(x, EV_LOOT_ITEM, T_ROD + FLD(T, F_DROP_TOOL, t), lvl, 1, 0, FLD(T, F_ID, t));
+    }
   }
 }
 
@@ -613,12 +655,12 @@ static void attack_call(Oracle* o, int e, int x, int style, int t) {
   }
   int d4 = mult4 * offense - 4 * defense;
   if (d4 < offense) d4 = offense;
-  int dmg = d4 >> 2;
+  int dmg = d4 >> 2, lvl_up = 0;
   if (x < P && prog) { /* Player.apply_damage -> skill.add_xp */
     int f = F_MELEE_EXP + 2 * style;
     FLD(T, f, x) = (int16_t)(FLD(T, f, x) + 6);
     int nl = level_at_exp(FLD(T, f, x));
-    if (nl > FLD(T, f - 1, x)) FLD(T, f - 1, x) = (int16_t)nl;
+    if (nl > FLD(T, f - 1, x)) { FLD(T, f - 1, x) = (int16_t)nl; lvl_up = nl; }
   }
   if (x < P && sys_on(o, NMMO_SYS_EQUIPMENT) && sys_on(o, NMMO_SYS_ITEM)) {
     uint32_t* inv = INVP(o, e, x); /* fire one unit of the equipped ammunition of this style */
@@ -636,8 +678,11 @@ static void attack_call(Oracle* o, int e, int x, int style, int t) {
   FLD(T, F_DAMAGE, t) = (int16_t)dmg;
   int h = FLD(T, F_HEALTH, t) - dmg;
   FLD(T, F_HEALTH, t) = (int16_t)(h < 0 ? 0 : h);
+  log_event(o, e, x, EV_SCORE_HIT, style + 1, 0, dmg, 0, 0);
+  if (lvl_up) log_event(o, e, x, EV_LEVEL_UP, style + 1, lvl_up, 0, 0, 0);
   if (FLD(T, F_HEALTH, t) == 0) {
     FLD(T, F_PLAYER_KILLS, x)++;
+    log_event(o, e, x, EV_PLAYER_KILL, 0, max_combat_level(T, S, t), 0, 0, FLD(T, F_ID, t));
     if (x < P) loot(o, e, x, t);
   }
   FLD(T, F_LATEST_COMBAT_TICK, x) = FLD(T, F_LATEST_COMBAT_TICK, t) = (int16_t)(E[E_TICK] + 1);
@@ -654,7 +699,10 @@ static void move_call(Oracle* o, int e, int x, int d) {
   FLD(T, F_ROW, x) = (int16_t)nr;
   FLD(T, F_COL, x) = (int16_t)nc;
   int progress = 64 - linf(80, 80, nr, nc);
-  if (progress > FLD(T, F_EXPLORATION, x)) FLD(T, F_EXPLORATION, x) = (int16_t)progress;
+  if (progress > FLD(T, F_EXPLORATION, x)) {
+    FLD(T, F_EXPLORATION, x) = (int16_t)progress;
+    log_event(o, e, x, EV_GO_FARTHEST, 0, 0, progress, 0, 0);
+  }
 }
 
 /* ------------------------------------------------------------------ observation (SPEC §8, §9) */
@@ -882,12 +930,15 @@ static void step_env(Oracle* o, int e, const int32_t* actions, float* obs, float
       if (mat[tile] == M_FOILAGE) { /* Food.update -> harvest (depletes) */
         FLD(T, F_FOOD, s) = 100;
         mat[tile] = M_SCRUB;
+        log_event(o, e, s, EV_EAT_FOOD, 0, 0, 0, 0, 0);
       }
       int wt = FLD(T, F_WATER, s) - 5;
       FLD(T, F_WATER, s) = (int16_t)(wt < 0 ? 0 : wt);
       if (mat[tile - SIZE] == M_WATER || mat[tile + SIZE] == M_WATER ||
-          mat[tile - 1] == M_WATER || mat[tile + 1] == M_WATER)
+          mat[tile - 1] == M_WATER || mat[tile + 1] == M_WATER) {
         FLD(T, F_WATER, s) = 100;
+        log_event(o, e, s, EV_DRINK_WATER, 0, 0, 0, 0, 0);
+      }
     }
     if (prof) { /* fishing, herbalism, prospecting, carving, alchemy (SPEC §9) */
       const uint32_t* inv = INVP(o, e, s);
@@ -903,7 +954,9 @@ static void step_env(Oracle* o, int e, const int32_t* actions, float* obs, float
       if (got) {
         int lvl = held == T_ROD ? held_lvl : 1;
         receive_new(o, e, s, T_RATION, lvl);
-        add_skill_exp(T, S, s, F_FISHING_EXP, 30 * lvl);
+        log_event(o, e, s, EV_HARVEST_ITEM, T_RATION, lvl, 1, 0, 0);
+        int nl = add_skill_exp(T, S, s, F_FISHING_EXP, 30 * lvl);
+        if (nl) log_event(o, e, s, EV_LEVEL_UP, 4, nl, 0, 0, 0);
       }
       static const int from[4] = {M_HERB, M_ORE, M_TREE, M_CRYSTAL};
       static const int to[4] = {M_WEEDS, M_SLAG, M_STUMP, M_FRAGMENT};
@@ -915,7 +968,9 @@ static void step_env(Oracle* o, int e, const int32_t* actions, float* obs, float
         mat[tile] = (uint8_t)to[q];
         int lvl = held == tool[q] ? held_lvl : 1;
         receive_new(o, e, s, out[q], lvl);
-        add_skill_exp(T, S, s, fexp[q], (q == 0 ? 30 : 15) * lvl);
+        log_event(o, e, s, EV_HARVEST_ITEM, out[q], lvl, 1, 0, 0);
+        int nl = add_skill_exp(T, S, s, fexp[q], (q == 0 ? 30 : 15) * lvl);
+        if (nl) log_event(o, e, s, EV_LEVEL_UP, 5 + q, nl, 0, 0, 0);
       }
     }
   }
@@ -933,6 +988,7 @@ static void step_env(Oracle* o, int e, const int32_t* actions, float* obs, float
         for (int j = 0; j < INV && IT_TYPE(inv + 2 * j); j++)
           if (IT_EQUIPPED(inv + 2 * j) && equip_slot(IT_TYPE(inv + 2 * j)) == slot) inv[2 * j] &= ~(1u << 9);
         it[0] |= 1u << 9;
+        log_event(o, e, p, EV_EQUIP_ITEM, type, lvl, IT_QTY(it), 0, 0);
       }
       update_item_level(o, e, p);
     } else if (lvl <= requirement_level(T, S, p, type)) {
@@ -944,6 +1000,7 @@ static void step_env(Oracle* o, int e, const int32_t* actions, float* obs, float
         FLD(T, F_HEALTH, p) = (int16_t)(FLD(T, F_HEALTH, p) + rs > 100 ? 100 : FLD(T, F_HEALTH, p) + rs);
       }
       it[1] -= 1;
+      log_event(o, e, p, EV_CONSUME_ITEM, type, lvl, 1, 0, 0);
       if (IT_QTY(it) == 0) { free_item_row(o, e, IT_ROW(it)); inv_remove(inv, k); }
     }
   }
@@ -974,6 +1031,8 @@ static void step_env(Oracle* o, int e, const int32_t* actions, float* obs, float
       FLD(T, F_GOLD, b) = (int16_t)(FLD(T, F_GOLD, b) - price);
       FLD(T, F_GOLD, owner) = (int16_t)(FLD(T, F_GOLD, owner) + price);
       uint32_t w0 = it[0] & 0x1FFu, w1 = it[1];
+      log_event(o, e, b, EV_BUY_ITEM, IT_TYPE(it), IT_LEVEL(it), IT_QTY(it), price, 0);
+      log_event(o, e, owner, EV_EARN_GOLD, 0, 0, 0, price, 0);
       inv_remove(INVP(o, e, owner), k);
       receive_moved(o, e, b, w0, w1);
     }
@@ -987,6 +1046,8 @@ static void step_env(Oracle* o, int e, const int32_t* actions, float* obs, float
       int k = inv_find(inv, give_row[p]);
       if (k >= 0 && !IT_EQUIPPED(inv + 2 * k) && !IT_PRICE(inv + 2 * k) && has_room(o, e, t, inv + 2 * k)) {
         uint32_t w0 = inv[2 * k], w1 = inv[2 * k + 1];
+        log_event(o, e, p, EV_GIVE_ITEM, IT_TYPE(inv + 2 * k), IT_LEVEL(inv + 2 * k), IT_QTY(inv + 2 * k), 0,
+                  FLD(T, F_ID, t));
         inv_remove(inv, k);
         receive_moved(o, e, t, w0, w1);
       }
@@ -996,6 +1057,7 @@ static void step_env(Oracle* o, int e, const int32_t* actions, float* obs, float
         FLD(T, F_ROW, t) == FLD(T, F_ROW, p) && FLD(T, F_COL, t) == FLD(T, F_COL, p)) {
       FLD(T, F_GOLD, p) = (int16_t)(FLD(T, F_GOLD, p) - gg_amt[p]);
       FLD(T, F_GOLD, t) = (int16_t)(FLD(T, F_GOLD, t) + gg_amt[p]);
+      log_event(o, e, p, EV_GIVE_GOLD, 0, 0, 0, gg_amt[p], FLD(T, F_ID, t));
     }
   }
   for (int p = 0; p < P && item; p++) { /* Destroy (40) */
@@ -1003,11 +1065,14 @@ static void step_env(Oracle* o, int e, const int32_t* actions, float* obs, float
     uint32_t* inv = INVP(o, e, p);
     int k = inv_find(inv, destroy_row[p]);
     if (k < 0 || IT_EQUIPPED(inv + 2 * k) || IT_PRICE(inv + 2 * k)) continue;
+    log_event(o, e, p, EV_DESTROY_ITEM, IT_TYPE(inv + 2 * k), IT_LEVEL(inv + 2 * k), IT_QTY(inv + 2 * k), 0, 0);
     free_item_row(o, e, IT_ROW(inv + 2 * k));
     inv_remove(inv, k);
   }
+  g_npend = 0;
   for (int s = 0; s < P + E[E_NPC_COUNT]; s++) /* Attack (50) */
     if (atk_t[s] >= 0) attack_call(o, e, s, atk_s[s], atk_t[s]);
+  flush_pending(o, e); /* loot events after all attack events */
   for (int s = 0; s < P + E[E_NPC_COUNT]; s++) /* Move (60) */
     if (move_dir[s] >= 0) move_call(o, e, s, move_dir[s]);
   for (int p = 0; p < P && exch; p++) { /* Sell (70) */
@@ -1016,6 +1081,8 @@ static void step_env(Oracle* o, int e, const int32_t* actions, float* obs, float
     int k = inv_find(inv, sell_row[p]);
     if (k < 0 || IT_EQUIPPED(inv + 2 * k)) continue;
     inv[2 * k] = (inv[2 * k] & 0x3FFu) | ((uint32_t)sell_price[p] << 10) | (tick << 17);
+    log_event(o, e, p, EV_LIST_ITEM, IT_TYPE(inv + 2 * k), IT_LEVEL(inv + 2 * k), IT_QTY(inv + 2 * k),
+              sell_price[p], 0);
   }
   /* 4. cull (players then NPCs), rows appended to the free ring; compact NPC slots */
   int16_t* ring = o->ring + (size_t)e * S;
@@ -1029,6 +1096,7 @@ static void step_env(Oracle* o, int e, const int32_t* actions, float* obs, float
       died[s] = 1;
       FLD(T, F_DIED_TICK, s) = (int16_t)(tick + 1);
       E[E_PLAYERS_ALIVE]--;
+      log_event(o, e, s, EV_AGENT_CULLED, 0, 0, 0, 0, 0);
     }
   }
   for (int p = 0; p < P && item; p++) { /* unlooted items of the dead are destroyed */
@@ -1150,6 +1218,7 @@ EXPORT void* oracle_create(const NmmoConfig* cfg, int n_envs, uint64_t seed,
   o->bank = (uint8_t*)malloc((size_t)cfg->map_n * NMMO_MAP_TILES);
   o->items = (uint32_t*)calloc((size_t)n_envs * o->P * INV * 2, 4);
   o->iring = (int16_t*)calloc((size_t)n_envs * INV * o->P, 2);
+  o->events = (int32_t*)calloc((size_t)n_envs * (cfg->event_cap > 0 ? cfg->event_cap : 1) * NMMO_EVENT_COLS, 4);
   for (int m = 0; m < cfg->map_n; m++)
     generate_map(cfg->map_seed, (uint32_t)m, o->bank + (size_t)m * NMMO_MAP_TILES);
   for (int k = 0; k < cfg->task_embed_dim; k++) o->task[k] = task_emb ? half_to_float(task_emb[k]) : 0.f;
@@ -1160,7 +1229,7 @@ EXPORT void oracle_destroy(void* h) {
   Oracle* o = (Oracle*)h;
   if (!o) return;
   free(o->env); free(o->ent); free(o->ring); free(o->mat); free(o->bank);
-  free(o->items); free(o->iring); free(o);
+  free(o->items); free(o->iring); free(o->events); free(o);
 }
 
 EXPORT int oracle_reset(void* h, const uint64_t* env_seeds, float* obs, uint8_t* mask) {
@@ -1228,6 +1297,22 @@ EXPORT int oracle_set_state(void* h, const void* buf, size_t nbytes) {
   }
   return 0;
 }
+/* the env's retained event rows, oldest first (as nmmo_get_events) */
+EXPORT int oracle_get_events(void* h, int env, int32_t* rows, int max_rows, int* n_rows) {
+  Oracle* o = (Oracle*)h;
+  const int cap = o->cfg.event_cap;
+  const int cnt = ENV(o, env)[E_EVENT_COUNT];
+  int n = cap > 0 ? (cnt < cap ? cnt : cap) : 0;
+  if (n > max_rows) n = max_rows;
+  for (int i = 0; i < n; i++) {
+    const int id = cnt - n + 1 + i;
+    memcpy(rows + (size_t)i * NMMO_EVENT_COLS,
+           o->events + ((size_t)env * cap + (size_t)((id - 1) % cap)) * NMMO_EVENT_COLS, NMMO_EVENT_COLS * 4);
+  }
+  *n_rows = n;
+  return 0;
+}
+
 EXPORT int oracle_get_map_bank(void* h, uint8_t* buf, size_t nbytes) {
   Oracle* o = (Oracle*)h;
   if (nbytes != (size_t)o->cfg.map_n * NMMO_MAP_TILES) return NMMO_E_SIZE;

@@ -43,6 +43,7 @@ def lib():
         L.oracle_get_state.argtypes = [vp, vp, sz]
         L.oracle_set_state.argtypes = [vp, vp, sz]
         L.oracle_get_map_bank.argtypes = [vp, vp, sz]
+        L.oracle_get_events.argtypes = [vp, i32, vp, i32, ctypes.POINTER(i32)]
         L.oracle_obs_elems.argtypes = [i32]
         L.oracle_flat_offsets.argtypes = [i32, vp]
         L.oracle_state_bytes_per_env.restype = sz
@@ -113,6 +114,15 @@ class OracleEnvs:
         buf = np.ascontiguousarray(buf, dtype=np.uint8)
         rc = lib().oracle_set_state(self.h, _p(buf), buf.nbytes)
         assert rc == 0, rc
+
+    def events(self, env: int, max_rows: int = 1 << 20) -> np.ndarray:
+        """Retained event-log rows of `env`, oldest first: int32 [n, 9] (SPEC §11)."""
+        cap = max(self.config.event_cap, 1)
+        buf = np.zeros((min(max_rows, cap), abi.EVENT_COLS), np.int32)
+        n = ctypes.c_int()
+        rc = lib().oracle_get_events(self.h, env, _p(buf), buf.shape[0], ctypes.byref(n))
+        assert rc == 0, rc
+        return buf[:n.value].copy()
 
     def map_bank(self) -> np.ndarray:
         buf = np.zeros((self.config.MAP_N, abi.MAP_SIZE, abi.MAP_SIZE), np.uint8)

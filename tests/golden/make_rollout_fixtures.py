@@ -1,6 +1,6 @@
 """Golden rollout hashes (self-generated from the oracle; parity vs nmmo 2.1 unpinned).
 
-sha256 of the state blob and of the step outputs after selected ticks of a seeded
+sha256 of the state blob, the step outputs and the event logs (SPEC §11) after selected ticks of a seeded
 scripted-action rollout. Used by tests/test_oracle.py (oracle regression) and
 tests/test_gpu_parity.py (HIP path vs the same fixture).
 Run: python -m tests.golden.make_rollout_fixtures
@@ -35,7 +35,7 @@ def rollout(stepper, preset):
         a = stepper.scripted_actions(77 + t)
         stepper.step(a)
         if t in CHECKPOINTS:
-            out[str(t)] = _h(stepper.get_state(), *stepper.outputs())
+            out[str(t)] = _h(stepper.get_state(), *stepper.outputs(), *[stepper.events(e) for e in range(4)])
     return out
 
 
@@ -57,6 +57,9 @@ class _OracleStepper:
 
     def scripted_actions(self, s):
         return self.o.scripted_actions(s)
+
+    def events(self, e):
+        return self.o.events(e)
 
     def get_state(self):
         return self.o.get_state()

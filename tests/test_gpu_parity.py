@@ -34,6 +34,16 @@ def _cmp_state(ga, oa, n, S, where, P=128):
         raise AssertionError(f"{where}: entity fields differ (env, field, slot, gpu, oracle): {names}")
 
 
+def _cmp_events(eng, orc, n, where):
+    for e in range(n):
+        g, o = eng.events(e), orc.events(e)
+        if g.shape != o.shape or not np.array_equal(g, o):
+            k = next((i for i in range(min(len(g), len(o))) if not np.array_equal(g[i], o[i])), None)
+            raise AssertionError(f"{where}: env {e} event log differs (gpu {len(g)} rows, oracle "
+                                 f"{len(o)}); first differing row {k}: gpu {g[k].tolist() if k is not None else None} "
+                                 f"oracle {o[k].tolist() if k is not None else None}")
+
+
 def test_map_bank_parity():
     cfg = Config.preset("C2", MAP_N=16, map_seed=123)
     eng = _engine(cfg, 1, seed=0)
@@ -69,6 +79,7 @@ def test_rollout_parity(preset):
             gv = getattr(eng, name).cpu().numpy()
             ov = getattr(orc, name)
             assert np.array_equal(gv, ov), f"{name} differs at step {t}"
+        _cmp_events(eng, orc, n, f"step {t}")
         if orc.obs is not None and (t % 10 == 0 or t == steps - 1):
             go = eng.obs.cpu().numpy()
             if not np.array_equal(go, orc.obs):
@@ -121,6 +132,9 @@ class _EngineStepper:
 
     def outputs(self):
         return tuple(getattr(self.e, n).cpu().numpy() for n in ("rew", "term", "trunc", "mask"))
+
+    def events(self, e):
+        return self.e.events(e)
 
 
 @pytest.mark.parametrize("preset", ["C2", "C3"])
@@ -196,6 +210,7 @@ def test_item_stress_parity():
         _cmp_state(eng.get_state(), orc.get_state(), n, eng.S, f"stress step {t}")
         for name in ("rew", "term", "trunc", "mask"):
             assert np.array_equal(getattr(eng, name).cpu().numpy(), getattr(orc, name)), f"{name} @ {t}"
+        _cmp_events(eng, orc, n, f"stress step {t}")
         if t % 5 == 0:
             go = eng.obs.cpu().numpy()
             if not np.array_equal(go, orc.obs):

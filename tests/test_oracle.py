@@ -382,3 +382,73 @@ def test_give_requires_same_tile():
         o.step(a)
         s = split_state(o.get_state(), 1, o.S, o.P)
         assert ((s["items"][0, 1, 0, 0] & 31) == 17) == moved
+
+
+# ---------------------------------------------------------------- event log (SPEC §11)
+EV = abi.EventCode
+C = abi.ATTR_TO_COL
+
+
+def test_event_log_eat_and_drink():
+    o, d = make(("Resource",))
+    mat = d["mat"][0]
+    r, c = find_tile(mat, lambda m, r, c: m[r, c] in (GRASS, SCRUB) and WATER in nbrs(m, r, c))
+    d["mat"][0][r, c] = FOILAGE
+    park_others(d, {0}, mat)
+    place(d, 0, r, c)
+    put(o, d)
+    a = noop_actions(o)
+    o.step(a)
+    ev = o.events(0)
+    mine = ev[ev[:, C["ent_id"]] == 1]
+    # update phase (eat, drink), then Move (Stay still sets the first exploration record)
+    assert [tuple(x) for x in mine[:, [C["event"], C["tick"]]]] == [
+        (EV.EAT_FOOD, 1), (EV.DRINK_WATER, 1), (EV.GO_FARTHEST, 1)]
+    assert mine[2, C["distance"]] == 64 - max(abs(r - 80), abs(c - 80))
+    assert np.array_equal(ev[:, C["id"]], np.arange(1, len(ev) + 1))  # running ids
+    assert split_state(o.get_state(), 1, o.S, o.P)["env"][0, E["event_count"]] == len(ev)
+
+
+def test_event_log_hit_kill_and_cull():
+    o, s = duel(t_fields=dict(health=5, food=40, water=40), x_fields=dict(food=40, water=40))
+    ev = o.events(0)
+    codes = [int(x) for x in ev[:, C["event"]]]
+    hit = ev[ev[:, C["event"]] == EV.SCORE_HIT][0]
+    assert hit[C["ent_id"]] == 1 and hit[C["combat_style"]] == 1 and hit[C["damage"]] == 10
+    kill = ev[ev[:, C["event"]] == EV.PLAYER_KILL][0]
+    assert kill[C["ent_id"]] == 1 and kill[C["target_ent"]] == 2 and kill[C["level"]] == 1
+    culled = ev[ev[:, C["event"]] == EV.AGENT_CULLED]
+    assert culled[:, C["ent_id"]].tolist() == [2]
+    # phase order: attack events, then the cull
+    assert codes.index(EV.SCORE_HIT) < codes.index(EV.PLAYER_KILL) < codes.index(EV.AGENT_CULLED)
+
+
+def test_event_log_ring_keeps_latest_rows():
+    cfg = Config.preset("C2", MAP_N=1, early_stop_agent_num=0, event_cap=16)
+    o = OracleEnvs(cfg, 1, seed=4)
+    o.reset()
+    for t in range(6):
+        o.step(o.scripted_actions(t))
+    n = split_state(o.get_state(), 1, o.S, o.P)["env"][0, E["event_count"]]
+    assert n > 16
+    ev = o.events(0)
+    assert len(ev) == 16 and ev[-1, C["id"]] == n and np.all(np.diff(ev[:, C["id"]]) == 1)
+    off = OracleEnvs(Config.preset("C2", MAP_N=1, event_cap=0), 1, seed=4)
+    off.reset()
+    off.step(off.scripted_actions(0))
+    assert len(off.events(0)) == 0
+    assert split_state(off.get_state(), 1, off.S, off.P)["env"][0, E["event_count"]] == 0
+
+
+def test_event_log_harvest_item():
+    o, d = make(ITEMS)
+    mat = d["mat"][0]
+    r, c = find_tile(mat, lambda m, r, c: m[r, c] in (GRASS, SCRUB) and WATER not in nbrs(m, r, c))
+    d["mat"][0][r, c] = ORE
+    park_others(d, {0}, mat)
+    place(d, 0, r, c)
+    put(o, d)
+    o.step(noop_actions(o))
+    ev = o.events(0)
+    h = ev[(ev[:, C["event"]] == EV.HARVEST_ITEM) & (ev[:, C["ent_id"]] == 1)]
+    assert h.shape[0] == 1 and (h[0, C["item_type"]], h[0, C["level"]], h[0, C["quantity"]]) == (13, 1, 1)
