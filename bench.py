@@ -225,6 +225,18 @@ def main():
         one()
     tick_ms, obs_ms, n_timed = eng.read_timing()
     eng.set_timing(False)
+    # practical HBM write ceiling on THIS box: the vendor fill kernel over the same obs buffer
+    # (the same byte count the obs kernel writes per launch), HIP events on the current stream
+    fill_gbs = None
+    if wl["obs"]:
+        s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        eng.obs.zero_()
+        s0.record()
+        for _ in range(10):
+            eng.obs.zero_()
+        s1.record()
+        torch.cuda.synchronize(dev)
+        fill_gbs = eng.obs.numel() * 4 / (s0.elapsed_time(s1) / 10 * 1e-3) / 1e9
 
     vals = torch.tensor([elapsed, float(alive.item()), float(envs * cfg.PLAYER_N * args.steps)],
                         dtype=torch.float64, device=dev)
@@ -292,6 +304,8 @@ def main():
                 "traffic": traffic,
                 "traffic_source": traffic_src,
                 "bytes_per_launch": byts,
+                "write_ceiling_gbs": None if fill_gbs is None else round(fill_gbs, 1),
+                "frac_of_write_ceiling": None if not fill_gbs or kern != "obs_kernel" else round(achieved / fill_gbs, 4),
             },
             "cpu_baseline": cpu,
         }

@@ -25,18 +25,25 @@ __host__ __device__ inline size_t obs_lds_bytes(int S) {
          (size_t)kObsWaves * 128 * 2 + (size_t)kObsWaves * kInv * 8 + (size_t)NMMO_MARKET_ROWS * 12;
 }
 
+// Plain (temporal) stores. Measured on MI355X (same-box A/B): __builtin_nontemporal_store
+// ("nt") made the C4 obs kernel 33% slower (3.52 vs 2.65 ms per launch); building every row
+// from 16-byte stores (4 consecutive elements per lane) was 54% slower (3.25 vs 2.11 ms: the
+// per-element section dispatch doubled the VGPRs and halved occupancy).
+__device__ __forceinline__ void obs_st(float* p, float v) { *p = v; }
+__device__ __forceinline__ void obs_st4(float4* p, float4 v) { *p = v; }
+
 // zero [lo, hi) of a row with 16-byte stores on the aligned body (wave-cooperative)
 __device__ inline void wave_zero(float* row, int lo, int hi) {
   const int lane = lane_id();
   const uintptr_t a = reinterpret_cast<uintptr_t>(row + lo);
   int head = (int)(((16 - (a & 15)) & 15) >> 2);
   if (head > hi - lo) head = hi - lo;
-  if (lane < head) row[lo + lane] = 0.f;
+  if (lane < head) obs_st(&row[lo + lane], 0.f);
   const int body = (hi - lo - head) >> 2;
   float4* p4 = reinterpret_cast<float4*>(row + lo + head);
-  for (int i = lane; i < body; i += 64) p4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int i = lane; i < body; i += 64) obs_st4(&p4[i], make_float4(0.f, 0.f, 0.f, 0.f));
   const int tail0 = lo + head + body * 4;
-  if (tail0 + lane < hi) row[tail0 + lane] = 0.f;
+  if (tail0 + lane < hi) obs_st(&row[tail0 + lane], 0.f);
 }
 
 __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
@@ -113,8 +120,9 @@ __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
 
     const int ninv = inv_count(inv);
+    const int aid = T[F_ID * S + a];
     // ActionTargets [0, o_agent_id) (SPEC §8, §9)
-    for (int j = lane; j < p.o_agent_id; j += 64) {
+    auto mask_val = [&](int j) -> bool {
       bool v = false;
       if (j < p.o_target) {
         v = combat;
@@ -154,29 +162,30 @@ __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
         const int k = j - p.o_use;
         v = k == kInv || (item && k < ninv && item_usable(T, S, a, inv[k]));
       }
-      row[j] = v ? 1.f : 0.f;
-    }
-    if (lane == 0) row[p.o_agent_id] = (float)T[F_ID * S + a];
-    if (lane == 1) row[p.o_tick] = (float)tick;
+      return v;
+    };
+    for (int j = lane; j < p.o_agent_id; j += 64) obs_st(&row[j], mask_val(j) ? 1.f : 0.f);
+    if (lane == 0) obs_st(&row[p.o_agent_id], (float)aid);
+    if (lane == 1) obs_st(&row[p.o_tick], (float)tick);
     // Entity rows (31 columns each)
     const int ne = kNObs * NMMO_N_ENTITY_COLS;
     for (int j = lane; j < ne; j += 64) {
       const int k = j / NMMO_N_ENTITY_COLS, f = j - k * NMMO_N_ENTITY_COLS;
-      row[p.o_entity + j] = k < nv ? (float)T[f * S + vis[k]] : 0.f;
+      obs_st(&row[p.o_entity + j], k < nv ? (float)T[f * S + vis[k]] : 0.f);
     }
     // Inventory (own items, owner = self) and Market (env listings, ascending row)
-    const int aid = T[F_ID * S + a];
     for (int j = lane; j < kInv * 16; j += 64) {
       const int k = j >> 4;
-      row[p.o_inventory + j] = k < ninv ? item_col(inv[k], aid, j & 15) : 0.f;
+      obs_st(&row[p.o_inventory + j], k < ninv ? item_col(inv[k], aid, j & 15) : 0.f);
     }
-    for (int j = lane; j < nm * 16; j += 64) row[p.o_market + j] = item_col(mitem[j >> 4], mown[j >> 4] + 1, j & 15);
+    for (int j = lane; j < nm * 16; j += 64)
+      obs_st(&row[p.o_market + j], item_col(mitem[j >> 4], mown[j >> 4] + 1, j & 15));
     wave_zero(row, p.o_market + nm * 16, p.o_task);
-    for (int j = lane; j < p.task_dim; j += 64) row[p.o_task + j] = p.task[j];
+    for (int j = lane; j < p.task_dim; j += 64) obs_st(&row[p.o_task + j], p.task[j]);
     for (int j = lane; j < 225 * 3; j += 64) {
       const int t = j / 3, comp = j - 3 * t;
       const int tr = r + t / 15 - kVision, tc = c + t % 15 - kVision;
-      row[p.o_tile + j] = comp == 0 ? (float)tr : comp == 1 ? (float)tc : (float)mat[tr * kSize + tc];
+      obs_st(&row[p.o_tile + j], comp == 0 ? (float)tr : comp == 1 ? (float)tc : (float)mat[tr * kSize + tc]);
     }
     __builtin_amdgcn_wave_barrier();
   }

@@ -1278,9 +1278,12 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
   int ndead;
   const int dpos = block_prefix_count(dead, c.wtot, &ndead);
   int npdead;
-  block_prefix_count(dead && s < P, c.wtot, &npdead);
+  const int ppos = block_prefix_count(dead && s < P, c.wtot, &npdead);
   if (s < P) c.died[s] = dead ? 1 : 0;
-  if (evon) ev_append(c, evn, dead && s < P ? 1 : 0, [&](int i) { ev_put(c, i, s, EV_AGENT_CULLED, 0, 0, 0, 0, 0); });
+  if (evon) {  // AGENT_CULLED in slot order (players are slots 0..P-1: the same prefix)
+    if (dead && s < P) ev_put(c, evn + ppos, s, EV_AGENT_CULLED, 0, 0, 0, 0, 0);
+    evn += npdead;
+  }
   if (dead) {
     c.ring[(c.E[E_FREE_HEAD] + c.E[E_FREE_COUNT] + dpos) % S] = TF(F_DS_ROW, s);
     TF(F_ALIVE, s) = 0;
