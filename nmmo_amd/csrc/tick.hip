@@ -138,6 +138,11 @@ __device__ __forceinline__ Ctx make_ctx(unsigned char* smem, const DevState& st,
     c.iring = reinterpret_cast<int16_t*>(smem + o); o += al((size_t)c.IC * 2);
     c.rmap = reinterpret_cast<int16_t*>(smem + o); o += al((size_t)(c.IC + 1) * 2);
     c.lbits = reinterpret_cast<uint64_t*>(smem + o); o += kLWords * 8;
+  } else {
+    c.inv = nullptr;
+    c.iring = nullptr;
+    c.rmap = nullptr;
+    c.lbits = nullptr;
   }
   {
     c.a_buy = reinterpret_cast<int16_t*>(smem + o); o += 256;
@@ -184,18 +189,68 @@ __device__ __forceinline__ Ctx make_ctx(unsigned char* smem, const DevState& st,
 }
 
 // ---------------------------------------------------------------- load / store
+// HBM -> LDS copy of up to 5 segments of 16-byte words as one flat index space, 8 loads in
+// flight per thread before their LDS stores (a plain strided copy loop keeps one dependent
+// load in flight per iteration: the state load was a quarter of a C2 tick).
+struct Seg16 {
+  uint4* d;
+  const uint4* s;
+  int n;
+};
+__device__ __forceinline__ void copy_segs(const Seg16 (&sg)[5], int tid, int nt) {
+  // segment lookup by selects (a runtime index into sg[] would put the array in scratch)
+  const int e0 = sg[0].n, e1 = e0 + sg[1].n, e2 = e1 + sg[2].n, e3 = e2 + sg[3].n, total = e3 + sg[4].n;
+  auto src = [&](int i) -> const uint4* {
+    return i < e0 ? sg[0].s + i
+           : i < e1 ? sg[1].s + (i - e0)
+           : i < e2 ? sg[2].s + (i - e1)
+           : i < e3 ? sg[3].s + (i - e2)
+                    : sg[4].s + (i - e3);
+  };
+  auto dst = [&](int i) -> uint4* {
+    return i < e0 ? sg[0].d + i
+           : i < e1 ? sg[1].d + (i - e0)
+           : i < e2 ? sg[2].d + (i - e1)
+           : i < e3 ? sg[3].d + (i - e2)
+                    : sg[4].d + (i - e3);
+  };
+  constexpr int U = 8;
+  int b = tid;
+  for (; b + (U - 1) * nt < total; b += U * nt) {  // full batches: U loads in flight
+    uint4 r0 = *src(b), r1 = *src(b + nt), r2 = *src(b + 2 * nt), r3 = *src(b + 3 * nt);
+    uint4 r4 = *src(b + 4 * nt), r5 = *src(b + 5 * nt), r6 = *src(b + 6 * nt), r7 = *src(b + 7 * nt);
+    *dst(b) = r0;
+    *dst(b + nt) = r1;
+    *dst(b + 2 * nt) = r2;
+    *dst(b + 3 * nt) = r3;
+    *dst(b + 4 * nt) = r4;
+    *dst(b + 5 * nt) = r5;
+    *dst(b + 6 * nt) = r6;
+    *dst(b + 7 * nt) = r7;
+  }
+  for (; b < total; b += nt) *dst(b) = *src(b);
+}
+
 __device__ __forceinline__ void load_env(Ctx& c, const DevState& st, int e) {
   const int tid = threadIdx.x, nt = blockDim.x, S = c.S;
   if (tid < NMMO_NE) c.E[tid] = st.env[(size_t)e * NMMO_NE + tid];
   const int16_t* src = st.ent + (size_t)e * NMMO_NF * S;
   const int n16 = kNFLive * S;
-  if ((S & 7) == 0) {
-    const uint4* s4 = reinterpret_cast<const uint4*>(src);
-    uint4* d4 = reinterpret_cast<uint4*>(c.T);
-    for (int i = tid; i < n16 / 8; i += nt) d4[i] = s4[i];
-  } else {
-    for (int i = tid; i < n16; i += nt) c.T[i] = src[i];
+  const bool v16 = (S & 7) == 0 && (c.IC & 7) == 0;  // every segment a whole number of 16-B words
+  if (v16) {
+    Seg16 sg[5] = {
+        {reinterpret_cast<uint4*>(c.T), reinterpret_cast<const uint4*>(src), n16 / 8},
+        {reinterpret_cast<uint4*>(c.ring), reinterpret_cast<const uint4*>(st.ring + (size_t)e * S), S / 8},
+        {reinterpret_cast<uint4*>(c.dep), reinterpret_cast<const uint4*>(st.dep + (size_t)e * kBitmapWords),
+         kBitmapWords / 4},
+        {reinterpret_cast<uint4*>(c.inv), reinterpret_cast<const uint4*>(st.items + (size_t)e * c.P * kInv),
+         c.items ? c.P * kInv / 2 : 0},
+        {reinterpret_cast<uint4*>(c.iring), reinterpret_cast<const uint4*>(st.iring + (size_t)e * c.IC),
+         c.items ? c.IC / 8 : 0}};
+    copy_segs(sg, tid, nt);
+    return;
   }
+  for (int i = tid; i < n16; i += nt) c.T[i] = src[i];
   for (int i = tid; i < S; i += nt) c.ring[i] = st.ring[(size_t)e * S + i];
   for (int i = tid; i < kBitmapWords; i += nt) c.dep[i] = st.dep[(size_t)e * kBitmapWords + i];
   if (c.items) {
@@ -1333,24 +1388,72 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
   __syncthreads();
   NMMO_STAMP(7);
 
-  // 5-6. tick += 1; map.step respawn of depleted tiles; exchange.step listing expiry
+  // 5-6. tick += 1; map.step respawn of depleted tiles; exchange.step listing expiry.
+  // One Philox call serves a group of 4 consecutive tiles (SPEC §5.6). The groups holding a
+  // depleted tile are compacted into a list (in LDS space the decode bitmap no longer needs)
+  // and drawn one group per lane, so the phase costs ~one Philox per lane instead of the
+  // busiest lane's tile count; beyond the list's capacity the per-word loop is used.
   {
     const uint8_t* base = c.bank + (size_t)c.E[E_MAP_ID] * kTiles;
+    int ng_mine = 0;
     for (int w = tid; w < kBitmapWords; w += nt) {
-      uint32_t bits = c.dep[w], keepb = bits;
-      while (bits) {
-        const int b = __builtin_ctz(bits);
-        bits &= bits - 1;
-        const int tt = w * 32 + b;
-        const int bm = base[tt];
-        const U4 u = draw(seed, (uint32_t)(tick + 1), P_RESPAWN, (uint32_t)(tt >> 2), 0);
-        const uint32_t ut = (tt & 3) == 0 ? u.x : (tt & 3) == 1 ? u.y : (tt & 3) == 2 ? u.z : u.w;
-        if (ut < respawn_u32(bm)) {
-          c.mat[tt] = (uint8_t)bm;
-          keepb &= ~(1u << b);
+      uint32_t nz = c.dep[w];
+      nz |= nz >> 1;
+      nz |= nz >> 2;
+      ng_mine += __popc(nz & 0x11111111u);
+    }
+    int ngroups;
+    const int gpos = block_prefix_sum(ng_mine, c.wtot, &ngroups);
+    int16_t* glist = reinterpret_cast<int16_t*>(c.vism);  // dead after decode
+    const int gcap = 128 * NW * 4;                         // int16 entries in vism's bytes
+    const uint32_t rtick = (uint32_t)(tick + 1);
+    if (ngroups <= gcap) {
+      int k = gpos;
+      for (int w = tid; w < kBitmapWords; w += nt) {
+        uint32_t nz = c.dep[w];
+        nz |= nz >> 1;
+        nz |= nz >> 2;
+        nz &= 0x11111111u;
+        while (nz) {
+          const int b = __builtin_ctz(nz);
+          nz &= nz - 1;
+          glist[k++] = (int16_t)(w * 8 + (b >> 2));
         }
       }
-      c.dep[w] = keepb;
+      __syncthreads();
+      for (int i = tid; i < ngroups; i += nt) {
+        const int g = glist[i], w = g >> 3, sh = (g & 7) * 4;
+        const uint32_t nib = (c.dep[w] >> sh) & 15u;
+        const U4 u = draw(seed, rtick, P_RESPAWN, (uint32_t)g, 0);
+        const uint32_t uu[4] = {u.x, u.y, u.z, u.w};
+        uint32_t clear = 0;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const int tt = 4 * g + j;
+          if (((nib >> j) & 1u) && uu[j] < respawn_u32(base[tt])) {
+            c.mat[tt] = base[tt];
+            clear |= 1u << (sh + j);
+          }
+        }
+        if (clear) atomicAnd(&c.dep[w], ~clear);
+      }
+    } else {
+      for (int w = tid; w < kBitmapWords; w += nt) {
+        uint32_t bits = c.dep[w], keepb = bits;
+        while (bits) {
+          const int b = __builtin_ctz(bits);
+          bits &= bits - 1;
+          const int tt = w * 32 + b;
+          const int bm = base[tt];
+          const U4 u = draw(seed, rtick, P_RESPAWN, (uint32_t)(tt >> 2), 0);
+          const uint32_t ut = (tt & 3) == 0 ? u.x : (tt & 3) == 1 ? u.y : (tt & 3) == 2 ? u.z : u.w;
+          if (ut < respawn_u32(bm)) {
+            c.mat[tt] = (uint8_t)bm;
+            keepb &= ~(1u << b);
+          }
+        }
+        c.dep[w] = keepb;
+      }
     }
   }
   if (c.exch && s < P) {
