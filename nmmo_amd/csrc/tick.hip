@@ -11,10 +11,9 @@
 // resolved exactly:
 //   * food harvest: a player eats iff its tile is Foilage at phase start and no lower slot in
 //     the realm stands on it (first-in-slot-order wins, later ones see Scrub);
-//   * attacks: an attack is *contested* iff an earlier attack targets its attacker or its
-//     target, or its target attacked earlier. Uncontested attacks read only phase-start state
-//     and have disjoint write sets, so they are applied in parallel first; contested ones are
-//     then replayed lane-serially in slot order (the only serial part of the tick);
+//   * attacks: two attacks conflict iff their {attacker, target} sets intersect; rounds run, in
+//     parallel, every remaining attack that is the lowest-slot remaining attack on both of its
+//     entities, which is exactly the serial result (no earlier conflicting attack is pending);
 //   * cull, free-row FIFO, NPC compaction and NPC spawn use wave ballots + block prefix counts;
 //   * items (SPEC §9): every player's 12-slot inventory, the item-row FIFO, a listed-row bitmap
 //     and row->owner map live in LDS too. Per-player item work (harvest, Use, Destroy, Sell,
@@ -38,8 +37,8 @@ struct Ctx {
   int16_t* amove;    // [S]
   int16_t* atgt;     // [S]
   int16_t* asty;     // [S]
-  int* ft;           // [S] first attacker slot targeting each slot
-  int16_t* clist;    // [S] contested attackers
+  int* ft;           // [S] per-entity scratch (closest-player keys, attack-round keys)
+  int16_t* clist;    // [S] scratch list (hostile NPCs searching for a target)
   int16_t* ring;     // [S]
   uint32_t* dep;     // [kBitmapWords]
   int* E;            // [NMMO_NE]
@@ -97,25 +96,32 @@ __device__ __forceinline__ uint64_t env_seed(const Ctx& c) {
 constexpr int kHash = 256;  // >= 2x players: open addressing never fills
 constexpr int kLWords = 32;  // listed-row bitmap words (rows 1..12*128)
 
+// item system: inventories, item FIFO, row map, listed bitmap, decoded Buy/Give actions
 __host__ __device__ inline size_t item_lds_bytes(int P) {
   auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
   const size_t ic = (size_t)kInv * P;
-  return (size_t)P * kInv * 8 + al(ic * 2) + al((ic + 1) * 2) + kLWords * 8;
+  return (size_t)P * kInv * 8 + al(ic * 2) + al((ic + 1) * 2) + kLWords * 8 + 5 * 256 + 512;
 }
-constexpr size_t kPlayerArrBytes = 9 * 256 + 128 + 512;  // per-player action / replay arrays
+constexpr size_t kPlayerArrBytes = 4 * 256 + 128;  // kill, order, ev_dmg, ev_lvl, fired
+// One LDS region, three lifetimes: the decode bitmap (phase 0; reused as the respawn group list
+// in phase 6), the position hash (update/harvest) and the attack first-touch arrays.
+__host__ __device__ inline size_t union_lds_bytes(int S) {
+  auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
+  size_t u = (size_t)128 * ((S + 63) / 64) * 8;
+  u = u > 2 * kHash * 4 ? u : 2 * kHash * 4;
+  const size_t atk = al((size_t)S * 4) + al((size_t)S * 2);
+  return u > atk ? u : atk;
+}
 
 __host__ __device__ inline size_t tick_lds_bytes(int S, int P, bool items) {
   auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
   size_t b = (items ? item_lds_bytes(P) : 0) + kPlayerArrBytes;
   b += al((size_t)kNFLive * S * 2);  // T
-  b += (size_t)128 * ((S + 63) / 64) * 8;  // vism (players <= 128)
+  b += union_lds_bytes(S);           // vism | hkey,hmin | ft,clist
   b += (size_t)rp_groups(S) * 16;    // rp
   b += al((size_t)S * 4);            // sp
   b += 128 * 4;                      // pp
-  b += 2 * kHash * 4;                // hkey, hmin
   b += 3 * al((size_t)S * 2);        // amove atgt asty
-  b += al((size_t)S * 4);            // ft
-  b += al((size_t)S * 2);            // clist
   b += al((size_t)S * 2);            // ring
   b += (size_t)kBitmapWords * 4;     // dep
   b += NMMO_NE * 4 + 32 * 4 + 16 * 4 + 128 + 128;
@@ -138,37 +144,41 @@ __device__ __forceinline__ Ctx make_ctx(unsigned char* smem, const DevState& st,
     c.iring = reinterpret_cast<int16_t*>(smem + o); o += al((size_t)c.IC * 2);
     c.rmap = reinterpret_cast<int16_t*>(smem + o); o += al((size_t)(c.IC + 1) * 2);
     c.lbits = reinterpret_cast<uint64_t*>(smem + o); o += kLWords * 8;
-  } else {
-    c.inv = nullptr;
-    c.iring = nullptr;
-    c.rmap = nullptr;
-    c.lbits = nullptr;
-  }
-  {
     c.a_buy = reinterpret_cast<int16_t*>(smem + o); o += 256;
     c.a_give = reinterpret_cast<int16_t*>(smem + o); o += 256;
     c.a_givet = reinterpret_cast<int16_t*>(smem + o); o += 256;
     c.a_ggt = reinterpret_cast<int16_t*>(smem + o); o += 256;
     c.a_gga = reinterpret_cast<int16_t*>(smem + o); o += 256;
-    c.kill = reinterpret_cast<int16_t*>(smem + o); o += 256;
-    c.order = reinterpret_cast<int16_t*>(smem + o); o += 256;
-    c.fired = smem + o; o += 128;
     c.ikey = reinterpret_cast<uint32_t*>(smem + o); o += 512;
-    c.ev_dmg = reinterpret_cast<int16_t*>(smem + o); o += 256;
-    c.ev_lvl = reinterpret_cast<int16_t*>(smem + o); o += 256;
+  } else {
+    c.inv = nullptr;
+    c.iring = nullptr;
+    c.rmap = nullptr;
+    c.lbits = nullptr;
+    c.a_buy = c.a_give = c.a_givet = c.a_ggt = c.a_gga = nullptr;
+    c.ikey = nullptr;
   }
+  c.kill = reinterpret_cast<int16_t*>(smem + o); o += 256;
+  c.order = reinterpret_cast<int16_t*>(smem + o); o += 256;
+  c.ev_dmg = reinterpret_cast<int16_t*>(smem + o); o += 256;
+  c.ev_lvl = reinterpret_cast<int16_t*>(smem + o); o += 256;
+  c.fired = smem + o; o += 128;
   c.T = reinterpret_cast<int16_t*>(smem + o); o += al((size_t)kNFLive * S * 2);
-  c.vism = reinterpret_cast<uint64_t*>(smem + o); o += (size_t)128 * ((S + 63) / 64) * 8;
+  {  // the union region (see union_lds_bytes)
+    unsigned char* u = smem + o;
+    c.vism = reinterpret_cast<uint64_t*>(u);
+    c.hkey = reinterpret_cast<int*>(u);
+    c.hmin = reinterpret_cast<int*>(u + kHash * 4);
+    c.ft = reinterpret_cast<int*>(u);
+    c.clist = reinterpret_cast<int16_t*>(u + al((size_t)S * 4));
+    o += union_lds_bytes(S);
+  }
   c.rp = reinterpret_cast<int*>(smem + o); o += (size_t)rp_groups(S) * 16;
   c.sp = reinterpret_cast<int*>(smem + o); o += al((size_t)S * 4);
   c.pp = reinterpret_cast<uint32_t*>(smem + o); o += 128 * 4;
-  c.hkey = reinterpret_cast<int*>(smem + o); o += kHash * 4;
-  c.hmin = reinterpret_cast<int*>(smem + o); o += kHash * 4;
   c.amove = reinterpret_cast<int16_t*>(smem + o); o += al((size_t)S * 2);
   c.atgt = reinterpret_cast<int16_t*>(smem + o); o += al((size_t)S * 2);
   c.asty = reinterpret_cast<int16_t*>(smem + o); o += al((size_t)S * 2);
-  c.ft = reinterpret_cast<int*>(smem + o); o += al((size_t)S * 4);
-  c.clist = reinterpret_cast<int16_t*>(smem + o); o += al((size_t)S * 2);
   c.ring = reinterpret_cast<int16_t*>(smem + o); o += al((size_t)S * 2);
   c.dep = reinterpret_cast<uint32_t*>(smem + o); o += (size_t)kBitmapWords * 4;
   c.E = reinterpret_cast<int*>(smem + o); o += NMMO_NE * 4;
@@ -550,43 +560,30 @@ __device__ __forceinline__ bool player_valid(const Ctx& c, int id, int r, int co
   return TF(F_ALIVE, s) && TF(F_HEALTH, s) > 0 && linf(r, col, TF(F_ROW, s), TF(F_COL, s)) <= kVision;
 }
 
-__device__ __forceinline__ void npc_decide(Ctx& c, int n, int& move, int& tgt, int& sty) {
+// behavior.update: drop an attacker/target that is gone, dead or out of vision; true if this
+// NPC is hostile with no target (it then needs the closest-player search)
+__device__ __forceinline__ bool npc_validate(Ctx& c, int n) {
+  const int r = TF(F_ROW, n), col = TF(F_COL, n);
+  if (!player_valid(c, TF(F_ATTACKER_ID, n), r, col)) TF(F_ATTACKER_ID, n) = 0;
+  if (!player_valid(c, TF(F_TARGET_ID, n), r, col)) TF(F_TARGET_ID, n) = 0;
+  return TF(F_NPC_TYPE, n) == 3 && !TF(F_TARGET_ID, n);
+}
+
+// closest: slot of the closest player within vision (ties to the lowest id) for a hostile NPC
+// without a target (computed block-wide by the caller), else -1
+__device__ __forceinline__ void npc_decide(Ctx& c, int n, int closest, int& move, int& tgt, int& sty) {
   const int r = TF(F_ROW, n), col = TF(F_COL, n), id = TF(F_ID, n);
   const U4 u = draw(env_seed(c), (uint32_t)c.E[E_TICK], P_NPC_MOVE, (uint32_t)(-id), 0);
   move = -1;
   tgt = -1;
   sty = TF(F_STYLE, n);
-  if (!player_valid(c, TF(F_ATTACKER_ID, n), r, col)) TF(F_ATTACKER_ID, n) = 0;
-  if (!player_valid(c, TF(F_TARGET_ID, n), r, col)) TF(F_TARGET_ID, n) = 0;
   const int type = TF(F_NPC_TYPE, n);
   bool hunt = false;
   if (type == 2 && TF(F_ATTACKER_ID, n)) {
     TF(F_TARGET_ID, n) = TF(F_ATTACKER_ID, n);
     hunt = true;
   } else if (type == 3) {
-    if (!TF(F_TARGET_ID, n)) {
-      int best = -1, bd = kVision + 1;  // closest player, ties to the lowest id
-      const int4* sp4 = reinterpret_cast<const int4*>(c.sp);
-#pragma unroll 4
-      for (int g = 0; g < (c.P >> 2); g++) {  // 4 players per ds_read_b128, branch-free
-        const int4 q = sp4[g];
-        const int vv[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-          const int v = vv[j];
-          const int d = v < 0 ? kVision + 1 : linf(r, col, v & 255, (v >> 8) & 255);
-          best = d < bd ? 4 * g + j : best;
-          bd = d < bd ? d : bd;
-        }
-      }
-      for (int p = c.P & ~3; p < c.P; p++) {
-        const int v = c.sp[p];
-        const int d = v < 0 ? kVision + 1 : linf(r, col, v & 255, (v >> 8) & 255);
-        best = d < bd ? p : best;
-        bd = d < bd ? d : bd;
-      }
-      if (best >= 0) TF(F_TARGET_ID, n) = TF(F_ID, best);
-    }
+    if (!TF(F_TARGET_ID, n) && closest >= 0) TF(F_TARGET_ID, n) = TF(F_ID, closest);
     hunt = TF(F_TARGET_ID, n) != 0;
   }
   if (!hunt) {
@@ -767,10 +764,6 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
 
   if (s < P) c.pres[s] = (uint8_t)TF(F_ALIVE, s);
   for (int k = tid; k < rp_groups(S) * 4; k += nt) c.rp[k] = -1;
-  for (int k = tid; k < kHash; k += nt) {
-    c.hkey[k] = -1;
-    c.hmin[k] = 0x7FFF;
-  }
   if (c.exch && tid < kLWords) c.lbits[tid] = 0;
   __syncthreads();
   if (s < S) {
@@ -838,8 +831,10 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
   int my_move = -1, my_tgt = -1, my_sty = 0;
   int use_row = -1, destroy_row = -1, sell_row = -1, sell_price = 0;
   if (s < P) {
-    c.a_buy[s] = c.a_give[s] = c.a_givet[s] = c.a_ggt[s] = -1;
-    c.a_gga[s] = 0;
+    if (items) {
+      c.a_buy[s] = c.a_give[s] = c.a_givet[s] = c.a_ggt[s] = -1;
+      c.a_gga[s] = 0;
+    }
     c.kill[s] = -1;
     c.fired[s] = 0;
     c.ev_dmg[s] = -1;
@@ -887,8 +882,34 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
   __syncthreads();
   NMMO_STAMP(12);
 #endif
-  // 1. npcs.actions
-  if (sys(c, NMMO_SYS_NPC) && s >= P && inslot) npc_decide(c, s, my_move, my_tgt, my_sty);
+  // 1. npcs.actions. The closest-player search of hostile NPCs without a target is spread over
+  // the whole block: (NPC, player) pairs -> LDS atomicMin of (L-inf << 8 | player slot).
+  const bool npc_on = sys(c, NMMO_SYS_NPC);
+  const bool need = npc_on && s >= P && inslot && npc_validate(c, s);
+  int closest = -1;
+  if (npc_on) {
+    int nneed;
+    const int npos = block_prefix_count(need, c.wtot, &nneed);  // its barriers end the decode
+    if (nneed > 0) {
+      int* best = c.ft;            // union region: the decode bitmap is dead past the barrier
+      int16_t* nlist = c.clist;
+      for (int j = tid; j < nneed; j += nt) best[j] = 0x7FFFFFFF;
+      if (need) nlist[npos] = (int16_t)s;
+      __syncthreads();
+      for (int i = tid; i < nneed * P; i += nt) {
+        const int j = (int)((unsigned)i / (unsigned)P), p = i - j * P;
+        const int v = c.sp[p];
+        if (v >= 0) {
+          const int n = nlist[j];
+          const int d = linf(TF(F_ROW, n), TF(F_COL, n), v & 255, (v >> 8) & 255);
+          if (d <= kVision) atomicMin(&best[j], (d << 8) | p);
+        }
+      }
+      __syncthreads();
+      if (need) closest = best[npos] == 0x7FFFFFFF ? -1 : (best[npos] & 255);
+    }
+  }
+  if (npc_on && s >= P && inslot) npc_decide(c, s, closest, my_move, my_tgt, my_sty);
   if (s < S) {
     c.amove[s] = (int16_t)my_move;
     c.atgt[s] = (int16_t)my_tgt;
@@ -896,6 +917,11 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
   }
   __syncthreads();
   NMMO_STAMP(2);
+  for (int k = tid; k < kHash; k += nt) {  // position hash (its LDS held the decode bitmap)
+    c.hkey[k] = -1;
+    c.hmin[k] = 0x7FFF;
+  }
+  __syncthreads();
 
   // 2. players.update / npcs.update. Every player in the realm registers its tile in the
   // position hash (lowest slot per tile via atomicMin): first-in-slot-order harvests.
@@ -1208,52 +1234,33 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
   }
 
   NMMO_STAMP(14);
-  // 3a. Attack (priority 50)
-  for (int k = tid; k < S; k += nt) c.ft[k] = 0x7FFF;
-  __syncthreads();
-  const int t = s < S ? c.atgt[s] : -1;
-  const bool ev = inslot && t >= 0;
-  if (ev) atomicMin(&c.ft[t], s);
-  __syncthreads();
-  const bool contested = ev && (c.ft[s] < s || c.ft[t] < s || (c.atgt[t] >= 0 && t < s));
-  int dmg = -1;
-  if (ev && !contested) dmg = eval_attack(c, s, c.asty[s], t);
-  __syncthreads();
-  if (dmg >= 0) apply_attack(c, s, c.asty[s], t, dmg, tick);
-  int ncont;
-  const int cpos = block_prefix_count(contested, c.wtot, &ncont);
-  if (contested) c.clist[cpos] = (int16_t)s;
+  // 3a. Attack (priority 50), in rounds. An attack (attacker slot s -> target t) touches the
+  // entities {s, t}; two attacks with disjoint sets have disjoint read/write sets. Each round
+  // runs every remaining attack that is the lowest-slot remaining attack on both of its
+  // entities (so it follows every earlier attack it conflicts with), all in parallel; round 1
+  // is all attacks no earlier attack conflicts with. The per-entity minimum is an atomicMax of
+  // round << 16 | (0xFFFF - slot), so no reset between rounds is needed.
+  int* mi = c.ft;
+  for (int k = tid; k < S; k += nt) mi[k] = 0;
   __syncthreads();
   NMMO_STAMP(4);
-  if (wave_id() == 0) {
-    // Replay of the contested attacks in slot order, 64 per chunk. Inside a chunk, lane j
-    // conflicts with an earlier lane i if i targets j's attacker or target, or j's target is
-    // i's attacker; a maximal conflict-free prefix [start, end) has disjoint read/write sets,
-    // so it is evaluated and applied in one wave step (exactly the serial result).
-    const int lane = lane_id();
-    for (int base = 0; base < ncont; base += 64) {
-      const int nin = min(64, ncont - base);
-      const bool valid = lane < nin;
-      const int x = valid ? c.clist[base + lane] : -1;
-      const int tx = valid ? c.atgt[x] : -2;
-      const int sx = valid ? c.asty[x] : 0;
-      uint64_t cm = 0;
-      for (int i = 0; i < 64; i++) {
-        const int xi = __shfl(x, i), ti = __shfl(tx, i);
-        if (i < lane && valid && (ti == x || ti == tx || xi == tx)) cm |= 1ull << i;
+  {
+    const int t = s < S ? c.atgt[s] : -1;
+    bool active = inslot && t >= 0;
+    const int sty = s < S ? c.asty[s] : 0;
+    for (int round = 1;; round++) {
+      const int key = (round << 16) | (0xFFFF - s);
+      if (active) {
+        atomicMax(&mi[s], key);
+        atomicMax(&mi[t], key);
       }
-      int start = 0;
-      while (start < nin) {
-        const uint64_t below = lane > start ? (((1ull << lane) - 1ull) & ~((1ull << start) - 1ull)) : 0ull;
-        const uint64_t blocked = __ballot(valid && (cm & below) != 0);
-        const int end = blocked ? (int)__builtin_ctzll(blocked) : nin;
-        int d = -1;
-        if (lane >= start && lane < end) d = eval_attack(c, x, sx, tx);
-        __builtin_amdgcn_wave_barrier();
-        if (d >= 0) apply_attack(c, x, sx, tx, d, tick);
-        __builtin_amdgcn_wave_barrier();
-        start = end;
+      __syncthreads();
+      if (active && mi[s] == key && mi[t] == key) {
+        const int dmg = eval_attack(c, s, sty, t);
+        if (dmg >= 0) apply_attack(c, s, sty, t, dmg, tick);
+        active = false;
       }
+      if (!__syncthreads_or(active)) break;
     }
   }
   __syncthreads();
@@ -1585,8 +1592,12 @@ hipError_t launch_tick(const DevState& st, const int32_t* actions, const uint64_
 }
 
 hipError_t init_kernels() {
+  // dynamic LDS may use what the kernel's static LDS (e.g. __syncthreads_or) leaves of 160 KB
+  hipFuncAttributes fa;
+  hipError_t err = hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(tick_kernel));
+  if (err != hipSuccess) return err;
   return hipFuncSetAttribute(reinterpret_cast<const void*>(tick_kernel),
-                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)(160 * 1024 - fa.sharedSizeBytes));
 }
 
 // set_state support: derived state is rebuilt from the blob — the depleted-tile bitmap

@@ -20,8 +20,8 @@ from nmmo_amd import _native, abi  # noqa: E402
 from nmmo_amd.config import Config  # noqa: E402
 from nmmo_amd.engine import NmmoEngine  # noqa: E402
 
-PHASES = ["load", "rowslot", "decode+npc_decide", "update+harvest", "attack:uncontested",
-          "attack:contested", "move", "cull+compact", "respawn", "npc_spawn", "rewards", "store"]
+PHASES = ["load", "rowslot", "decode+npc_decide", "update+harvest", "professions+items",
+          "attack rounds+loot", "move", "cull+compact", "respawn", "npc_spawn", "rewards", "store"]
 
 
 def main():
@@ -61,7 +61,7 @@ def main():
           f"{np.median(sub[:, 2]):9.0f}); npc decide median {np.median(sub[:, 1]):9.0f}")
     print(f"  update+harvest = resource {np.median(d[:, 2]):9.0f} + professions "
           f"{np.median(sub[:, 3]):9.0f}; item actions (Use..Destroy) {np.median(sub[:, 4]):9.0f}; "
-          f"uncontested attacks {np.median(sub[:, 5]):9.0f}")
+          f"attack init {np.median(sub[:, 5]):9.0f}")
 
 
 if __name__ == "__main__":
