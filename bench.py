@@ -39,6 +39,10 @@ WORKLOADS = {
                desc="C3: 1024 envs x 128 agents, + melee/range/mage combat, NPC spawn/AI, progression"),
     "C4": dict(envs=1024, preset="C4", obs=True,
                desc="C4: 1024 envs x 128 agents, all systems + per-agent flat obs gather"),
+    # BASELINE.json configs[4]: C4 per GPU (8192 envs on 8) + the learner gather every step
+    "C5": dict(envs=1024, preset="C4", obs=True, gather=True,
+               desc="C5: 1024 envs x 128 agents per GPU, all systems + flat obs, RCCL gather of "
+                    "obs/reward/dones/mask to the learner (rank 0) every step"),
 }
 
 
@@ -145,6 +149,11 @@ def cpu_baseline(cfg, seconds: float):
 
 def main():
     args = parse()
+    # The JSON line is the only thing on stdout: native libraries (RCCL prints a version banner
+    # on stdout when a communicator is created) are sent to stderr by pointing fd 1 at fd 2.
+    json_out = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
     import torch
     import torch.distributed as dist
 
@@ -180,15 +189,33 @@ def main():
     eng.set_counters(counters)
     pseed = args.seed * 1_000_003  # the policy's Philox counter already walks (tick, episode)
 
+    gather = wl.get("gather", False)
+    if gather:
+        # learner-side receive buffers on rank 0 (one gather per tick over xGMI);
+        # the four small outputs travel packed in one buffer with the obs in another
+        small = torch.empty((envs, cfg.PLAYER_N, 8), dtype=torch.uint8, device=dev)
+        recv_obs = [torch.empty_like(eng.obs) for _ in range(world)] if rank == 0 else None
+        recv_small = [torch.empty_like(small) for _ in range(world)] if rank == 0 else None
+        if world == 1:  # a one-rank RCCL group: the gather degenerates to the root's own copy
+            dist.init_process_group("nccl", init_method="tcp://127.0.0.1:29533", rank=0, world_size=1,
+                                    device_id=dev)
+
     def one():
         eng.scripted_actions(pseed)
         eng.step()
+        if gather:
+            small[..., 0:4] = eng.rew.view(torch.uint8).view(envs, cfg.PLAYER_N, 4)
+            small[..., 4] = eng.term
+            small[..., 5] = eng.trunc
+            small[..., 6] = eng.mask
+            dist.gather(eng.obs, recv_obs, dst=0)
+            dist.gather(small, recv_small, dst=0)
 
     for _ in range(args.warmup):
         one()
     torch.cuda.synchronize(dev)
     graphs = []
-    if not args.no_graph:  # the step is capture-safe: no sync / alloc inside nmmo_step
+    if not args.no_graph and not gather:  # the step is capture-safe: no sync / alloc inside nmmo_step
         g_n = max(1, min(args.graph_steps, args.steps))
         for n in sorted({g_n, args.steps % g_n} - {0}):
             g = torch.cuda.CUDAGraph()
@@ -293,7 +320,8 @@ def main():
             "slot_steps_per_sec": round(slots_total / elapsed, 1),
             "alive_fraction": round(alive_total / slots_total, 4),
             "kernel_ms": {"tick": round(tick_avg_ms, 5), "obs": round(obs_avg_ms, 5)},
-            "launch": "eager" if args.no_graph else f"hipGraph x{min(args.graph_steps, args.steps)} ticks",
+            "launch": "eager" if (args.no_graph or gather) else f"hipGraph x{min(args.graph_steps, args.steps)} ticks",
+            "gather": f"RCCL gather of {eng.obs.numel() * 4 + envs * cfg.PLAYER_N * 8} B/rank/step to rank 0" if gather else None,
             "roofline": {
                 "kernel": kern,
                 "bound": "hbm",
@@ -309,9 +337,9 @@ def main():
             },
             "cpu_baseline": cpu,
         }
-        print(json.dumps(line), flush=True)
+        print(json.dumps(line), file=json_out, flush=True)
     eng.close()
-    if world > 1:
+    if world > 1 or gather:
         dist.destroy_process_group()
 
 
