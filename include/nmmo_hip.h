@@ -40,7 +40,7 @@ extern "C" {
 #endif
 
 #define NMMO_API __attribute__((visibility("default")))
-#define NMMO_ABI_VERSION 2
+#define NMMO_ABI_VERSION 3
 
 /* ---- error codes ---- */
 #define NMMO_OK 0
@@ -127,6 +127,38 @@ enum NmmoEventCode {
   EV_BUY_ITEM = 34, EV_LEVEL_UP = 41, EV_AGENT_CULLED = 91
 };
 
+/* ---- tasks (SPEC.md §12; nmmo.task base predicates): a task program is up to two predicate
+ * terms combined as SINGLE / SUM (w0*p0 + w1*p1) / PRODUCT (p0*p1); each player runs one. ---- */
+enum NmmoPredicate {
+  PRED_NONE = 0, PRED_TICK_GE = 1, PRED_COUNT_EVENT, PRED_SCORE_HIT, PRED_HARVEST_ITEM,
+  PRED_CONSUME_ITEM, PRED_LIST_ITEM, PRED_BUY_ITEM, PRED_EARN_GOLD, PRED_SPEND_GOLD,
+  PRED_MAKE_PROFIT, PRED_DEFEAT_ENTITY, PRED_HOARD_GOLD, PRED_ATTAIN_SKILL, PRED_GAIN_EXPERIENCE,
+  PRED_EQUIP_ITEM, PRED_OWN_ITEM, PRED_INVENTORY_SPACE_GE, PRED_OCCUPY_TILE, PRED_CAN_SEE_TILE,
+  PRED_FULLY_ARMED, NMMO_N_PREDICATES
+};
+#define NMMO_TASK_SINGLE 0
+#define NMMO_TASK_SUM 1
+#define NMMO_TASK_PRODUCT 2
+#define NMMO_MAX_TASKS 4096
+typedef struct NmmoTaskTerm {
+  int32_t pred;               /* NmmoPredicate */
+  int32_t a, b, c;            /* predicate arguments, SPEC.md §12 table */
+  float weight;               /* SUM weight */
+  int32_t reserved;
+} NmmoTaskTerm;
+typedef struct NmmoTask {
+  NmmoTaskTerm term[2];
+  int32_t combine;            /* NMMO_TASK_* */
+  int32_t reserved;
+} NmmoTask;
+/* per player task state (part of the state blob): previous / max progress, event accumulators,
+ * positive-reward count (task.reward_signal_count), tick of first progress >= 1 (0 = none) */
+typedef struct NmmoTaskState {
+  double last, max_progress;
+  int32_t acc[4];             /* term k uses acc[2k], acc[2k+1] */
+  int32_t signals, completed_tick;
+} NmmoTaskState;
+
 typedef struct NmmoConfig {
   int32_t abi_version;        /* must be NMMO_ABI_VERSION */
   int32_t player_n;           /* PLAYER_N 128 (environment.py:35, config.yaml:76); <= 128 */
@@ -184,12 +216,22 @@ NMMO_API int nmmo_reset(NmmoHandle* h, const uint64_t* env_seeds, void* obs, uin
 NMMO_API int nmmo_step(NmmoHandle* h, const int32_t* actions, void* obs, float* rew, uint8_t* term,
               uint8_t* trunc, uint8_t* mask, void* stream);
 
+/* Task table and per-player assignment (SPEC.md §12; nmmo.Env.reset(make_task_fn) /
+ * agent_task_map). tasks: host [n_tasks] (1..NMMO_MAX_TASKS); embeddings: host fp16
+ * [n_tasks][task_embed_dim] used as each player's Task obs (NULL = keep the create-time
+ * embedding for every task); assign: host int32 [n_envs][player_n] task indices (NULL = all 0).
+ * Takes effect for progress from the next step; call before nmmo_reset for whole episodes.
+ * Synchronous. Default after create: one task TickGE(task_num_tick). */
+NMMO_API int nmmo_set_tasks(NmmoHandle* h, const NmmoTask* tasks, int32_t n_tasks,
+                            const uint16_t* embeddings, const int32_t* assign);
+
 /* Masked-uniform scripted actions from the current state (bench / tests). */
 NMMO_API int nmmo_scripted_actions(NmmoHandle* h, uint64_t policy_seed, int32_t* actions, void* stream);
 
 /* State blob: per env, [NMMO_NE int32 env fields][NF*slots int16 entity table]
  * [slots int16 free-row ring][MAP_TILES u8 material][player_n*12 x 2 u32 items]
- * [12*player_n int16 item-row ring]; envs concatenated. Synchronous. */
+ * [12*player_n int16 item-row ring][player_n int32 task index][player_n NmmoTaskState];
+ * envs concatenated. Synchronous. */
 NMMO_API int nmmo_get_state(NmmoHandle* h, void* host_buf, size_t nbytes);
 NMMO_API int nmmo_set_state(NmmoHandle* h, const void* host_buf, size_t nbytes);
 /* The generated map bank: host u8 [map_n][MAP_TILES]. Synchronous. */

@@ -6,7 +6,7 @@ struct sizes against the compiled library and the enum values against the header
 
 import ctypes
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 NMMO_OK = 0
 NMMO_E_INVALID = -1
@@ -62,6 +62,40 @@ EVENT_COLS = 9
 EVENT_ATTRS = ["id", "ent_id", "tick", "event", "type", "level", "number", "gold", "target_ent"]
 ATTR_TO_COL = {a: i for i, a in enumerate(EVENT_ATTRS)}
 ATTR_TO_COL.update(item_type=4, combat_style=4, quantity=6, damage=6, distance=6, price=7)
+
+
+# Tasks (SPEC.md §12)
+PREDICATES = [
+    "NONE", "TickGE", "CountEvent", "ScoreHit", "HarvestItem", "ConsumeItem", "ListItem", "BuyItem",
+    "EarnGold", "SpendGold", "MakeProfit", "DefeatEntity", "HoardGold", "AttainSkill",
+    "GainExperience", "EquipItem", "OwnItem", "InventorySpaceGE", "OccupyTile", "CanSeeTile",
+    "FullyArmed",
+]
+PRED = {n: i for i, n in enumerate(PREDICATES)}
+TASK_SINGLE, TASK_SUM, TASK_PRODUCT = 0, 1, 2
+MAX_TASKS = 4096
+
+
+class NmmoTaskTerm(ctypes.Structure):
+    _fields_ = [("pred", ctypes.c_int32), ("a", ctypes.c_int32), ("b", ctypes.c_int32),
+                ("c", ctypes.c_int32), ("weight", ctypes.c_float), ("reserved", ctypes.c_int32)]
+
+
+class NmmoTask(ctypes.Structure):
+    _fields_ = [("term", NmmoTaskTerm * 2), ("combine", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+class NmmoTaskState(ctypes.Structure):
+    _fields_ = [("last", ctypes.c_double), ("max_progress", ctypes.c_double),
+                ("acc", ctypes.c_int32 * 4), ("signals", ctypes.c_int32),
+                ("completed_tick", ctypes.c_int32)]
+
+
+def task_state_dtype():
+    import numpy as np
+
+    return np.dtype([("last", "<f8"), ("max_progress", "<f8"), ("acc", "<i4", (4,)),
+                     ("signals", "<i4"), ("completed_tick", "<i4")])
 
 
 class EventCode:
@@ -131,6 +165,9 @@ INV_SLOTS = 12
 MARKET_ROWS = 1024
 
 
+TASK_STATE_BYTES = 40
+
+
 def state_bytes_per_env(slots: int, players: int = 128) -> int:
     return NE * 4 + NF * slots * 2 + slots * 2 + MAP_TILES + players * INV_SLOTS * 8 \
-        + INV_SLOTS * players * 2
+        + INV_SLOTS * players * 2 + players * 4 + players * TASK_STATE_BYTES

@@ -50,6 +50,9 @@ struct NmmoHandle {
   int32_t* d_mlist = nullptr;
   int32_t* d_mcount = nullptr;
   int32_t* d_events = nullptr;
+  NmmoTask* d_tasks = nullptr;
+  int32_t* d_assign = nullptr;
+  NmmoTaskState* d_tstate = nullptr;
   // bench timing (nmmo_set_timing): event pairs around the tick and obs kernels
   bool timing = false;
   int t_count = 0;
@@ -136,7 +139,8 @@ int nmmo_layout(const NmmoConfig* cfg, NmmoLayout* L) {
   L->state_bytes_per_env = (size_t)NMMO_NE * 4 + (size_t)NMMO_NF * L->slots * 2 +
                            (size_t)L->slots * 2 + NMMO_MAP_TILES +
                            (size_t)cfg->player_n * NMMO_INV_SLOTS * 8 +
-                           (size_t)NMMO_INV_SLOTS * cfg->player_n * 2;
+                           (size_t)NMMO_INV_SLOTS * cfg->player_n * 2 + (size_t)cfg->player_n * 4 +
+                           (size_t)cfg->player_n * sizeof(NmmoTaskState);
   return NMMO_OK;
 }
 
@@ -148,7 +152,7 @@ void nmmo_destroy(NmmoHandle* h) {
   for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
   void* bufs[] = {h->d_env,  h->d_ent,   h->d_ring,  h->d_mat,   h->d_dep,   h->d_bank,
                   h->d_task, h->d_seeds, h->d_items, h->d_iring, h->d_mlist, h->d_mcount,
-                  h->d_events};
+                  h->d_events, h->d_tasks, h->d_assign, h->d_tstate};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   delete h;
@@ -194,6 +198,9 @@ int nmmo_create(const NmmoConfig* cfg, int32_t n_envs, uint64_t seed, int32_t de
   ALLOC(h->d_mlist, n * NMMO_MARKET_ROWS * 4);
   ALLOC(h->d_mcount, n * 4);
   if (cfg->event_cap > 0) ALLOC(h->d_events, n * (size_t)cfg->event_cap * NMMO_EVENT_COLS * 4);
+  ALLOC(h->d_tasks, sizeof(NmmoTask));
+  ALLOC(h->d_assign, n * P * 4);
+  ALLOC(h->d_tstate, n * P * sizeof(NmmoTaskState));
 #undef ALLOC
   if (init_kernels() != hipSuccess) return cleanup_fail(fail(NMMO_E_HIP, "kernel attributes"));
   if (task_embedding && cfg->task_embed_dim > 0) {
@@ -203,8 +210,17 @@ int nmmo_create(const NmmoConfig* cfg, int32_t n_envs, uint64_t seed, int32_t de
       return cleanup_fail(fail(NMMO_E_HIP, "task upload"));
   }
   h->st = DevState{h->d_env,   h->d_ent,   h->d_ring,  h->d_mat,    h->d_dep, h->d_bank,
-                   h->d_items, h->d_iring, h->d_mlist, h->d_mcount, h->d_events, n_envs, P,
+                   h->d_items, h->d_iring, h->d_mlist, h->d_mcount, h->d_events,
+                   h->d_tasks, h->d_assign, h->d_tstate, 1,            0,           n_envs, P,
                    N,          S,          seed,       nullptr,     *cfg};
+  {  // default task table: everyone runs TickGE(task_num_tick) (SPEC §12)
+    NmmoTask t;
+    memset(&t, 0, sizeof(t));
+    t.term[0].pred = PRED_TICK_GE;
+    t.term[0].a = cfg->task_num_tick;
+    if (hipMemcpy(h->d_tasks, &t, sizeof(t), hipMemcpyHostToDevice) != hipSuccess)
+      return cleanup_fail(fail(NMMO_E_HIP, "task table upload"));
+  }
   if (launch_mapgen(cfg->map_seed, cfg->map_n, h->d_bank, nullptr) != hipSuccess ||
       hipDeviceSynchronize() != hipSuccess)
     return cleanup_fail(fail(NMMO_E_HIP, "map generation failed: %s", hipGetErrorString(hipGetLastError())));
@@ -216,7 +232,7 @@ static ObsParams obs_params(NmmoHandle* h, float* obs) {
   const NmmoLayout& L = h->layout;
   ObsParams p;
   p.env = h->d_env; p.ent = h->d_ent; p.mat = h->d_mat; p.task = h->d_task; p.obs = obs;
-  p.items = h->d_items; p.mlist = h->d_mlist; p.mcount = h->d_mcount;
+  p.items = h->d_items; p.mlist = h->d_mlist; p.mcount = h->d_mcount; p.assign = h->d_assign;
   p.n_envs = h->st.n_envs; p.P = h->st.P; p.S = h->st.S; p.elems = L.obs_elems;
   p.task_dim = h->cfg.task_embed_dim; p.systems = h->cfg.systems;
   p.spawn_immunity = h->cfg.spawn_immunity;
@@ -325,8 +341,13 @@ int nmmo_get_state(NmmoHandle* h, void* host_buf, size_t nbytes) {
   const size_t IP = (size_t)NMMO_INV_SLOTS * h->st.P;  // items per env
   std::vector<uint32_t> items(n * IP * 2);
   std::vector<int16_t> iring(n * IP);
+  const size_t P = (size_t)h->st.P;
+  std::vector<int32_t> assign(n * P);
+  std::vector<NmmoTaskState> tstate(n * P);
   HIP_TRY(hipMemcpy(items.data(), h->d_items, items.size() * 4, hipMemcpyDeviceToHost));
   HIP_TRY(hipMemcpy(iring.data(), h->d_iring, iring.size() * 2, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(assign.data(), h->d_assign, assign.size() * 4, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(tstate.data(), h->d_tstate, tstate.size() * sizeof(NmmoTaskState), hipMemcpyDeviceToHost));
   HIP_TRY(hipMemcpy(env.data(), h->d_env, env.size() * 4, hipMemcpyDeviceToHost));
   HIP_TRY(hipMemcpy(ent.data(), h->d_ent, ent.size() * 2, hipMemcpyDeviceToHost));
   HIP_TRY(hipMemcpy(ring.data(), h->d_ring, ring.size() * 2, hipMemcpyDeviceToHost));
@@ -339,6 +360,8 @@ int nmmo_get_state(NmmoHandle* h, void* host_buf, size_t nbytes) {
     memcpy(b, mat.data() + e * NMMO_MAP_TILES, NMMO_MAP_TILES); b += NMMO_MAP_TILES;
     memcpy(b, items.data() + e * IP * 2, IP * 8); b += IP * 8;
     memcpy(b, iring.data() + e * IP, IP * 2); b += IP * 2;
+    memcpy(b, assign.data() + e * P, P * 4); b += P * 4;
+    memcpy(b, tstate.data() + e * P, P * sizeof(NmmoTaskState)); b += P * sizeof(NmmoTaskState);
   }
   return NMMO_OK;
 }
@@ -354,6 +377,9 @@ int nmmo_set_state(NmmoHandle* h, const void* host_buf, size_t nbytes) {
   const size_t IP = (size_t)NMMO_INV_SLOTS * h->st.P;
   std::vector<uint32_t> items(n * IP * 2);
   std::vector<int16_t> iring(n * IP);
+  const size_t P = (size_t)h->st.P;
+  std::vector<int32_t> assign(n * P);
+  std::vector<NmmoTaskState> tstate(n * P);
   const uint8_t* b = (const uint8_t*)host_buf;
   for (size_t e = 0; e < n; e++) {
     memcpy(env.data() + e * NMMO_NE, b, NMMO_NE * 4); b += NMMO_NE * 4;
@@ -362,7 +388,11 @@ int nmmo_set_state(NmmoHandle* h, const void* host_buf, size_t nbytes) {
     memcpy(mat.data() + e * NMMO_MAP_TILES, b, NMMO_MAP_TILES); b += NMMO_MAP_TILES;
     memcpy(items.data() + e * IP * 2, b, IP * 8); b += IP * 8;
     memcpy(iring.data() + e * IP, b, IP * 2); b += IP * 2;
+    memcpy(assign.data() + e * P, b, P * 4); b += P * 4;
+    memcpy(tstate.data() + e * P, b, P * sizeof(NmmoTaskState)); b += P * sizeof(NmmoTaskState);
   }
+  for (int32_t a : assign)
+    if (a < 0 || a >= h->st.n_tasks) return fail(NMMO_E_INVALID, "state blob: task index %d outside the task table", a);
   HIP_TRY(hipSetDevice(h->device));
   HIP_TRY(hipDeviceSynchronize());
   HIP_TRY(hipMemcpy(h->d_env, env.data(), env.size() * 4, hipMemcpyHostToDevice));
@@ -371,8 +401,56 @@ int nmmo_set_state(NmmoHandle* h, const void* host_buf, size_t nbytes) {
   HIP_TRY(hipMemcpy(h->d_mat, mat.data(), mat.size(), hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(h->d_items, items.data(), items.size() * 4, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(h->d_iring, iring.data(), iring.size() * 2, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(h->d_assign, assign.data(), assign.size() * 4, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(h->d_tstate, tstate.data(), tstate.size() * sizeof(NmmoTaskState), hipMemcpyHostToDevice));
   HIP_TRY(launch_rebuild_dep(h->st, nullptr));
   HIP_TRY(hipDeviceSynchronize());
+  return NMMO_OK;
+}
+
+int nmmo_set_tasks(NmmoHandle* h, const NmmoTask* tasks, int32_t n_tasks, const uint16_t* embeddings,
+                   const int32_t* assign) {
+  if (!h || !tasks) return fail(NMMO_E_INVALID, "null argument");
+  if (n_tasks < 1 || n_tasks > NMMO_MAX_TASKS) return fail(NMMO_E_INVALID, "n_tasks %d not in 1..%d", n_tasks, NMMO_MAX_TASKS);
+  int tev = 0;
+  for (int i = 0; i < n_tasks; i++)
+    for (int k = 0; k < 2; k++) {
+      const int pr = tasks[i].term[k].pred;
+      if (pr < 0 || pr >= NMMO_N_PREDICATES) return fail(NMMO_E_INVALID, "task %d term %d: predicate %d", i, k, pr);
+      tev |= pr >= PRED_COUNT_EVENT && pr <= PRED_DEFEAT_ENTITY;
+    }
+  const size_t nP = (size_t)h->st.n_envs * h->st.P;
+  if (assign)
+    for (size_t i = 0; i < nP; i++)
+      if (assign[i] < 0 || assign[i] >= n_tasks) return fail(NMMO_E_INVALID, "assign[%zu] = %d", i, assign[i]);
+  HIP_TRY(hipSetDevice(h->device));
+  HIP_TRY(hipDeviceSynchronize());
+  const int D = h->cfg.task_embed_dim > 0 ? h->cfg.task_embed_dim : 1;
+  std::vector<float> emb((size_t)n_tasks * D);
+  std::vector<float> first(D);
+  HIP_TRY(hipMemcpy(first.data(), h->d_task, (size_t)D * 4, hipMemcpyDeviceToHost));
+  for (int i = 0; i < n_tasks; i++)
+    for (int k = 0; k < D; k++)
+      emb[(size_t)i * D + k] = embeddings && h->cfg.task_embed_dim > 0 ? half_to_float(embeddings[(size_t)i * D + k])
+                                                                       : first[k];
+  float* d_task = nullptr;
+  NmmoTask* d_tasks = nullptr;
+  if (hipMalloc((void**)&d_task, emb.size() * 4) != hipSuccess ||
+      hipMalloc((void**)&d_tasks, (size_t)n_tasks * sizeof(NmmoTask)) != hipSuccess) {
+    if (d_task) (void)hipFree(d_task);
+    return fail(NMMO_E_NOMEM, "task table allocation");
+  }
+  HIP_TRY(hipMemcpy(d_task, emb.data(), emb.size() * 4, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(d_tasks, tasks, (size_t)n_tasks * sizeof(NmmoTask), hipMemcpyHostToDevice));
+  if (assign) HIP_TRY(hipMemcpy(h->d_assign, assign, nP * 4, hipMemcpyHostToDevice));
+  else HIP_TRY(hipMemset(h->d_assign, 0, nP * 4));
+  (void)hipFree(h->d_task);
+  (void)hipFree(h->d_tasks);
+  h->d_task = d_task;
+  h->d_tasks = d_tasks;
+  h->st.tasks = d_tasks;
+  h->st.n_tasks = n_tasks;
+  h->st.tev = tev;
   return NMMO_OK;
 }
 

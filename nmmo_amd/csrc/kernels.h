@@ -17,6 +17,10 @@ struct DevState {
   int32_t* mlist;        // [n][NMMO_MARKET_ROWS] end-of-tick listings, ascending row: row | owner<<16 | slot<<24
   int* mcount;           // [n] listings in mlist (<= NMMO_MARKET_ROWS)
   int32_t* events;       // [n][cfg.event_cap][NMMO_EVENT_COLS] event-log rings (SPEC §11)
+  const NmmoTask* tasks; // [n_tasks] task programs (SPEC §12)
+  int32_t* assign;       // [n][P] task index of each player
+  NmmoTaskState* tstate; // [n][P] progress / event accumulators
+  int n_tasks, tev;      // tev: some task term counts events
   int n_envs, P, N, S;   // N = NPC capacity (0 when the NPC system is off), S = P + N
   uint64_t seed;         // create seed (first-episode seeds)
   unsigned long long* counters;  // optional device u64 [2]: agent-steps, finished episodes
@@ -30,7 +34,8 @@ struct ObsParams {
   const uint2* items;   // [n][P][kInv]
   const int32_t* mlist; // [n][NMMO_MARKET_ROWS] row | owner<<16 | slot<<24
   const int* mcount;    // [n]
-  const float* task;    // [task_dim]
+  const float* task;    // [n_tasks][task_dim] Task obs per task
+  const int32_t* assign; // [n][P]
   float* obs;           // [n][P][elems]
   int n_envs, P, S, elems, task_dim;
   uint32_t systems;

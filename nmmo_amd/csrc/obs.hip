@@ -181,7 +181,8 @@ __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
     for (int j = lane; j < nm * 16; j += 64)
       obs_st(&row[p.o_market + j], item_col(mitem[j >> 4], mown[j >> 4] + 1, j & 15));
     wave_zero(row, p.o_market + nm * 16, p.o_task);
-    for (int j = lane; j < p.task_dim; j += 64) obs_st(&row[p.o_task + j], p.task[j]);
+    const float* temb = p.task + (size_t)p.assign[(size_t)e * p.P + a] * p.task_dim;  // this player's task
+    for (int j = lane; j < p.task_dim; j += 64) obs_st(&row[p.o_task + j], temb[j]);
     for (int j = lane; j < 225 * 3; j += 64) {
       const int t = j / 3, comp = j - 3 * t;
       const int tr = r + t / 15 - kVision, tc = c + t % 15 - kVision;

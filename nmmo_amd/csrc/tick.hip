@@ -65,6 +65,12 @@ struct Ctx {
   int16_t* ev_dmg;   // [128] damage of the player's executed attack (-1 none): SCORE_HIT
   int16_t* ev_lvl;   // [128] combat level reached by that attack's XP (0 none): LEVEL_UP
   int32_t* evg;      // this env's event ring (global), evcap rows (SPEC §11)
+  // tasks (SPEC §12)
+  const NmmoTask* tasks;   // global task table
+  const int32_t* assign;   // global [P] task index of this env's players
+  NmmoTaskState* ts;       // LDS [P] task state of this env's players (loaded/stored with the state)
+  int4* tdesc;             // LDS [128][2] (pred, a, b, c) of each player's terms (when tev)
+  bool tev;
   int evcap, tick1;  // ring rows (0 = no event log); tick + 1 (the events' tick column)
   int S, P, N, IC;
   bool items, exch, prof, equip;
@@ -113,9 +119,10 @@ __host__ __device__ inline size_t union_lds_bytes(int S) {
   return u > atk ? u : atk;
 }
 
-__host__ __device__ inline size_t tick_lds_bytes(int S, int P, bool items) {
+__host__ __device__ inline size_t tick_lds_bytes(int S, int P, bool items, bool tev) {
   auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
-  size_t b = (items ? item_lds_bytes(P) : 0) + kPlayerArrBytes;
+  size_t b = (items ? item_lds_bytes(P) : 0) + kPlayerArrBytes + (tev ? 128 * 2 * 16 : 0) +
+             al((size_t)P * sizeof(NmmoTaskState));
   b += al((size_t)kNFLive * S * 2);  // T
   b += union_lds_bytes(S);           // vism | hkey,hmin | ft,clist
   b += (size_t)rp_groups(S) * 16;    // rp
@@ -157,6 +164,15 @@ __device__ __forceinline__ Ctx make_ctx(unsigned char* smem, const DevState& st,
     c.lbits = nullptr;
     c.a_buy = c.a_give = c.a_givet = c.a_ggt = c.a_gga = nullptr;
     c.ikey = nullptr;
+  }
+  c.tev = st.tev != 0;
+  c.tasks = st.tasks;
+  c.assign = st.assign + (size_t)e * st.P;
+  c.ts = reinterpret_cast<NmmoTaskState*>(smem + o); o += al((size_t)st.P * sizeof(NmmoTaskState));
+  if (c.tev) {
+    c.tdesc = reinterpret_cast<int4*>(smem + o); o += 128 * 2 * 16;
+  } else {
+    c.tdesc = nullptr;
   }
   c.kill = reinterpret_cast<int16_t*>(smem + o); o += 256;
   c.order = reinterpret_cast<int16_t*>(smem + o); o += 256;
@@ -207,22 +223,25 @@ struct Seg16 {
   const uint4* s;
   int n;
 };
-__device__ __forceinline__ void copy_segs(const Seg16 (&sg)[5], int tid, int nt) {
+__device__ __forceinline__ void copy_segs(const Seg16 (&sg)[6], int tid, int nt) {
   // segment lookup by selects (a runtime index into sg[] would put the array in scratch)
-  const int e0 = sg[0].n, e1 = e0 + sg[1].n, e2 = e1 + sg[2].n, e3 = e2 + sg[3].n, total = e3 + sg[4].n;
+  const int e0 = sg[0].n, e1 = e0 + sg[1].n, e2 = e1 + sg[2].n, e3 = e2 + sg[3].n, e4 = e3 + sg[4].n,
+            total = e4 + sg[5].n;
   auto src = [&](int i) -> const uint4* {
     return i < e0 ? sg[0].s + i
            : i < e1 ? sg[1].s + (i - e0)
            : i < e2 ? sg[2].s + (i - e1)
            : i < e3 ? sg[3].s + (i - e2)
-                    : sg[4].s + (i - e3);
+           : i < e4 ? sg[4].s + (i - e3)
+                    : sg[5].s + (i - e4);
   };
   auto dst = [&](int i) -> uint4* {
     return i < e0 ? sg[0].d + i
            : i < e1 ? sg[1].d + (i - e0)
            : i < e2 ? sg[2].d + (i - e1)
            : i < e3 ? sg[3].d + (i - e2)
-                    : sg[4].d + (i - e3);
+           : i < e4 ? sg[4].d + (i - e3)
+                    : sg[5].d + (i - e4);
   };
   constexpr int U = 8;
   int b = tid;
@@ -246,9 +265,11 @@ __device__ __forceinline__ void load_env(Ctx& c, const DevState& st, int e) {
   if (tid < NMMO_NE) c.E[tid] = st.env[(size_t)e * NMMO_NE + tid];
   const int16_t* src = st.ent + (size_t)e * NMMO_NF * S;
   const int n16 = kNFLive * S;
-  const bool v16 = (S & 7) == 0 && (c.IC & 7) == 0;  // every segment a whole number of 16-B words
+  // every segment a whole number of 16-B words (task state: 40 B per player)
+  const bool v16 = (S & 7) == 0 && (c.IC & 7) == 0 && (c.P & 1) == 0;
+  NmmoTaskState* tsg = st.tstate + (size_t)e * c.P;
   if (v16) {
-    Seg16 sg[5] = {
+    Seg16 sg[6] = {
         {reinterpret_cast<uint4*>(c.T), reinterpret_cast<const uint4*>(src), n16 / 8},
         {reinterpret_cast<uint4*>(c.ring), reinterpret_cast<const uint4*>(st.ring + (size_t)e * S), S / 8},
         {reinterpret_cast<uint4*>(c.dep), reinterpret_cast<const uint4*>(st.dep + (size_t)e * kBitmapWords),
@@ -256,10 +277,14 @@ __device__ __forceinline__ void load_env(Ctx& c, const DevState& st, int e) {
         {reinterpret_cast<uint4*>(c.inv), reinterpret_cast<const uint4*>(st.items + (size_t)e * c.P * kInv),
          c.items ? c.P * kInv / 2 : 0},
         {reinterpret_cast<uint4*>(c.iring), reinterpret_cast<const uint4*>(st.iring + (size_t)e * c.IC),
-         c.items ? c.IC / 8 : 0}};
+         c.items ? c.IC / 8 : 0},
+        {reinterpret_cast<uint4*>(c.ts), reinterpret_cast<const uint4*>(tsg),
+         c.P * (int)sizeof(NmmoTaskState) / 16}};
     copy_segs(sg, tid, nt);
     return;
   }
+  for (int i = tid; i < c.P * (int)sizeof(NmmoTaskState) / 4; i += nt)
+    reinterpret_cast<int*>(c.ts)[i] = reinterpret_cast<const int*>(tsg)[i];
   for (int i = tid; i < n16; i += nt) c.T[i] = src[i];
   for (int i = tid; i < S; i += nt) c.ring[i] = st.ring[(size_t)e * S + i];
   for (int i = tid; i < kBitmapWords; i += nt) c.dep[i] = st.dep[(size_t)e * kBitmapWords + i];
@@ -290,6 +315,11 @@ __device__ __forceinline__ void store_env(const Ctx& c, const DevState& st, int 
     uint4* d4 = reinterpret_cast<uint4*>(st.items + (size_t)e * c.P * kInv);
     for (int i = tid; i < c.P * kInv / 2; i += nt) d4[i] = s4[i];
     for (int i = tid; i < c.IC; i += nt) st.iring[(size_t)e * c.IC + i] = c.iring[i];
+  }
+  {  // task state (SPEC §12)
+    int* dsti = reinterpret_cast<int*>(st.tstate + (size_t)e * c.P);
+    const int* srci = reinterpret_cast<const int*>(c.ts);
+    for (int i = tid; i < c.P * (int)sizeof(NmmoTaskState) / 4; i += nt) dsti[i] = srci[i];
   }
 }
 
@@ -412,8 +442,43 @@ __device__ __forceinline__ int kth_listed(const Ctx& c, int k) {
 
 // ---------------------------------------------------------------- event log (SPEC §11)
 // Row of the episode's event `idx` (0-based) for player p.
+// an event of player p feeds the event accumulators of p's task terms (SPEC §12)
+__device__ __forceinline__ void task_accumulate(const Ctx& c, int p, int code, int type, int level, int number,
+                                                int gold, int target) {
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    const int4 q = c.tdesc[p * 2 + k];  // pred, a, b, c
+    int* acc = c.ts[p].acc + 2 * k;
+    int add0 = 0, add1 = 0;
+    switch (q.x) {
+      case PRED_COUNT_EVENT: add0 = code == q.y; break;
+      case PRED_SCORE_HIT: add0 = code == EV_SCORE_HIT && type == q.y; break;
+      case PRED_HARVEST_ITEM: add0 = code == EV_HARVEST_ITEM && type == q.y && level >= q.z ? number : 0; break;
+      case PRED_CONSUME_ITEM: add0 = code == EV_CONSUME_ITEM && type == q.y && level >= q.z ? number : 0; break;
+      case PRED_LIST_ITEM: add0 = code == EV_LIST_ITEM && type == q.y && level >= q.z ? number : 0; break;
+      case PRED_BUY_ITEM: add0 = code == EV_BUY_ITEM && type == q.y && level >= q.z ? number : 0; break;
+      case PRED_EARN_GOLD: add0 = code == EV_EARN_GOLD ? gold : 0; break;
+      case PRED_SPEND_GOLD: add0 = code == EV_BUY_ITEM ? gold : 0; break;
+      case PRED_MAKE_PROFIT:
+        add0 = code == EV_EARN_GOLD ? gold : 0;
+        add1 = code == EV_BUY_ITEM ? gold : 0;
+        break;
+      case PRED_DEFEAT_ENTITY:
+        add0 = code == EV_PLAYER_KILL && ((q.y == 0 && target < 0) || (q.y == 1 && target > 0)) && level >= q.z;
+        break;
+      default: break;
+    }
+    if (add0) atomicAdd(&acc[0], add0);
+    if (add1) atomicAdd(&acc[1], add1);
+  }
+}
+
+// Event `idx` (0-based in the episode) of player p: written to the ring when the log is on, and
+// counted by p's task when some task counts events.
 __device__ __forceinline__ void ev_put(const Ctx& c, int idx, int p, int code, int type, int level,
                                        int number, int gold, int target) {
+  if (c.tev) task_accumulate(c, p, code, type, level, number, gold, target);
+  if (!c.evcap) return;
   int32_t* r = c.evg + (size_t)(idx % c.evcap) * NMMO_EVENT_COLS;
   r[0] = idx + 1;
   r[1] = p + 1;
@@ -720,6 +785,69 @@ __device__ __forceinline__ void loot(Ctx& c, int x, int t, int& evn) {
   }
 }
 
+// ---------------------------------------------------------------- task progress (SPEC §12)
+__device__ __forceinline__ double per_d(int num, int den) { return (double)num / (double)(den > 0 ? den : 1); }
+__device__ __forceinline__ double clip01(double x) { return x < 0.0 ? 0.0 : x > 1.0 ? 1.0 : x; }
+
+__device__ __forceinline__ double term_progress(const Ctx& c, int p, const NmmoTaskTerm& q, const int* acc) {
+  const int sk = q.a >= 1 && q.a <= 8 ? q.a - 1 : -1;
+  const uint2* inv = c.items ? c.inv + p * kInv : nullptr;
+  switch (q.pred) {
+    case PRED_TICK_GE: return per_d(c.tick1, q.a);
+    case PRED_COUNT_EVENT: case PRED_SCORE_HIT: return per_d(acc[0], q.b);
+    case PRED_HARVEST_ITEM: case PRED_CONSUME_ITEM: case PRED_LIST_ITEM: case PRED_BUY_ITEM:
+    case PRED_DEFEAT_ENTITY: return per_d(acc[0], q.c);
+    case PRED_EARN_GOLD: case PRED_SPEND_GOLD: return per_d(acc[0], q.a);
+    case PRED_MAKE_PROFIT: return per_d(acc[0] - acc[1], q.a);
+    case PRED_HOARD_GOLD: return per_d(TF(F_GOLD, p), q.a);
+    case PRED_ATTAIN_SKILL: return sk >= 0 && TF(F_MELEE_LEVEL + 2 * sk, p) >= q.b ? 1.0 : 0.0;
+    case PRED_GAIN_EXPERIENCE: return sk >= 0 ? per_d(TF(F_MELEE_EXP + 2 * sk, p), q.b) : 0.0;
+    case PRED_EQUIP_ITEM:
+      for (int k = 0; inv && k < kInv && it_type(inv[k]); k++)
+        if (it_equipped(inv[k]) && it_type(inv[k]) == q.a && it_level(inv[k]) >= q.b) return 1.0;
+      return 0.0;
+    case PRED_OWN_ITEM: {
+      int n = 0;
+      for (int k = 0; inv && k < kInv && it_type(inv[k]); k++)
+        if (it_type(inv[k]) == q.a && it_level(inv[k]) >= q.b) n += it_qty(inv[k]);
+      return per_d(n, q.c);
+    }
+    case PRED_INVENTORY_SPACE_GE: return kInv - (inv ? inv_count(inv) : 0) >= q.a ? 1.0 : 0.0;
+    case PRED_OCCUPY_TILE: return TF(F_ROW, p) == q.a && TF(F_COL, p) == q.b ? 1.0 : 0.0;
+    case PRED_CAN_SEE_TILE: {
+      const int r = TF(F_ROW, p), col = TF(F_COL, p);
+      for (int dr = -kVision; dr <= kVision; dr++)
+        for (int dc = -kVision; dc <= kVision; dc++)
+          if (c.mat[(r + dr) * kSize + col + dc] == q.a) return 1.0;
+      return 0.0;
+    }
+    case PRED_FULLY_ARMED: {
+      if (q.a < 1 || q.a > 3 || !inv) return 0.0;
+      const int need[5] = {T_HAT, T_TOP, T_BOTTOM, T_SPEAR + q.a - 1, T_WHETSTONE + q.a - 1};
+      for (int j = 0; j < 5; j++) {
+        bool ok = false;
+        for (int k = 0; k < kInv && it_type(inv[k]); k++)
+          ok = ok || (it_equipped(inv[k]) && it_type(inv[k]) == need[j] && it_level(inv[k]) >= q.b);
+        if (!ok) return 0.0;
+      }
+      return 1.0;
+    }
+    default: return 0.0;
+  }
+}
+
+// clipped progress of player p's task; SUM without fused multiply-adds (bit-exact with the oracle)
+__device__ __forceinline__ double task_progress(const Ctx& c, int p, const int* acc) {
+  const NmmoTask& t = c.tasks[c.assign[p]];
+  const double p0 = clip01(term_progress(c, p, t.term[0], acc));
+  if (t.combine == NMMO_TASK_SINGLE) return p0;
+  const double p1 = clip01(term_progress(c, p, t.term[1], acc + 2));
+  const double v = t.combine == NMMO_TASK_SUM
+                       ? __dadd_rn(__dmul_rn((double)t.term[0].weight, p0), __dmul_rn((double)t.term[1].weight, p1))
+                       : __dmul_rn(p0, p1);
+  return clip01(v);
+}
+
 // ---------------------------------------------------------------- the tick (SPEC §5)
 __device__ __forceinline__ bool acts(const Ctx& c, int s) { return TF(F_ALIVE, s) && TF(F_HEALTH, s) > 0; }
 __device__ __forceinline__ bool same_tile(const Ctx& c, int a, int b) {
@@ -759,12 +887,17 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
   const bool items = c.items;
   const uint64_t seed = env_seed(c);
   c.tick1 = tick + 1;
-  const bool evon = c.evcap > 0;
+  const bool evon = c.evcap > 0 || c.tev;
   int evn = c.E[E_EVENT_COUNT];  // block-uniform running event count (SPEC §11)
 
   if (s < P) c.pres[s] = (uint8_t)TF(F_ALIVE, s);
   for (int k = tid; k < rp_groups(S) * 4; k += nt) c.rp[k] = -1;
   if (c.exch && tid < kLWords) c.lbits[tid] = 0;
+  if (c.tev && s < P) {  // this player's task terms and event accumulators
+    const NmmoTask& tk = c.tasks[c.assign[s]];
+#pragma unroll
+    for (int k = 0; k < 2; k++) c.tdesc[s * 2 + k] = make_int4(tk.term[k].pred, tk.term[k].a, tk.term[k].b, tk.term[k].c);
+  }
   __syncthreads();
   if (s < S) {
     const bool in = inslot && TF(F_ALIVE, s);  // in the realm => health > 0 at tick start
@@ -1483,14 +1616,22 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
     const int alive = c.E[E_PLAYERS_ALIVE];
     const int done = alive == 0 || tick + 1 >= c.cfg->horizon || alive <= c.cfg->early_stop_agent_num;
     c.E[E_DONE] = done;
-    c.E[E_EVENT_COUNT] = evn;
+    if (c.evcap) c.E[E_EVENT_COUNT] = evn;
   }
   __syncthreads();
-  if (s < P) {
-    const double nt_ = (double)c.cfg->task_num_tick;
-    const double pn = fmin((double)(tick + 1) / nt_, 1.0), po = fmin((double)tick / nt_, 1.0);
+  if (s < P) {  // Task.compute_rewards: progress delta, death penalty (SPEC §12)
     float rw = 0.f;
-    if (c.pres[s]) rw = c.died[s] ? -1.f : (float)(pn - po);
+    if (c.pres[s] && c.died[s]) {
+      rw = -1.f;
+    } else if (c.pres[s]) {
+      NmmoTaskState& ts = c.ts[s];
+      const double np = task_progress(c, s, ts.acc), d = np - ts.last;
+      ts.last = np;
+      if (np > ts.max_progress) ts.max_progress = np;
+      if (d > 0.0) ts.signals += 1;
+      if (np >= 1.0 && ts.completed_tick == 0) ts.completed_tick = tick + 1;
+      rw = (float)d;
+    }
     rew[s] = rw;
     term[s] = c.died[s];
     trunc[s] = (uint8_t)(c.E[E_DONE] && TF(F_ALIVE, s));
@@ -1551,6 +1692,8 @@ __global__ void tick_kernel(DevState st, const int32_t* __restrict__ actions,
     }
     __syncthreads();
     reset_env(c, seed, episode, env_global);
+    for (int i = threadIdx.x; i < c.P * (int)sizeof(NmmoTaskState) / 4; i += blockDim.x)
+      reinterpret_cast<int*>(c.ts)[i] = 0;  // task progress restarts with the episode
     if (!c.items) {  // item state is not staged in LDS without the Item system; reset it in HBM
       for (int i = threadIdx.x; i < c.P * kInv; i += blockDim.x) st.items[(size_t)e * c.P * kInv + i] = make_uint2(0u, 0u);
       for (int i = threadIdx.x; i < c.IC; i += blockDim.x) st.iring[(size_t)e * c.IC + i] = (int16_t)(i + 1);
@@ -1585,7 +1728,7 @@ hipError_t launch_tick(const DevState& st, const int32_t* actions, const uint64_
                        float* rew, uint8_t* term, uint8_t* trunc, uint8_t* mask, int mode,
                        hipStream_t stream) {
   const int threads = ((st.S + 63) / 64) * 64;
-  const size_t lds = tick_lds_bytes(st.S, st.P, (st.cfg.systems & NMMO_SYS_ITEM) != 0);
+  const size_t lds = tick_lds_bytes(st.S, st.P, (st.cfg.systems & NMMO_SYS_ITEM) != 0, st.tev != 0);
   hipLaunchKernelGGL(tick_kernel, dim3(st.n_envs), dim3(threads), lds, stream,
                      st, actions, env_seeds, rew, term, trunc, mask, mode);
   return hipGetLastError();

@@ -135,6 +135,18 @@ class NmmoEngine:
         check(lib().nmmo_set_state(self.h, buf.ctypes.data_as(ctypes.c_void_p), buf.nbytes),
               "nmmo_set_state")
 
+    def set_tasks(self, tasks, embeddings=None, assign=None):
+        """Task table (sequence of abi.NmmoTask, e.g. from nmmo_amd.tasks), optional fp16
+        embeddings [n_tasks, task_embed_dim] for the Task obs, and int32 assign [n_envs, P]
+        (None = task 0 for everyone). SPEC §12; call before reset() for whole episodes."""
+        arr = (abi.NmmoTask * len(tasks))(*tasks)
+        emb = None if embeddings is None else np.ascontiguousarray(embeddings, np.float16)
+        asg = None if assign is None else np.ascontiguousarray(assign, np.int32)
+        check(lib().nmmo_set_tasks(self.h, ctypes.cast(arr, ctypes.c_void_p), len(tasks),
+                                   None if emb is None else emb.ctypes.data_as(ctypes.c_void_p),
+                                   None if asg is None else asg.ctypes.data_as(ctypes.c_void_p)),
+              "nmmo_set_tasks")
+
     def events(self, env: int, max_rows: int | None = None) -> np.ndarray:
         """Retained event-log rows of `env`, oldest first: int32 [n, 9] (SPEC §11 columns
         id, ent_id, tick, event, type, level, number, gold, target_ent). Synchronous."""

@@ -187,7 +187,11 @@ typedef struct {
   uint32_t* items;     /* [n_envs][P][INV][2] (SPEC §9 item words) */
   int16_t* iring;      /* [n_envs][INV*P] free item rows */
   int32_t* events;     /* [n_envs][event_cap][NMMO_EVENT_COLS] event-log rings (SPEC §11) */
-  float task[4096];
+  NmmoTask* tasks;     /* [n_tasks] task programs (SPEC §12) */
+  int n_tasks, tev;    /* tev: some task term counts events */
+  float* task_emb;     /* [n_tasks][task_embed_dim] Task obs per task */
+  int32_t* assign;     /* [n_envs][P] task index of each player */
+  NmmoTaskState* tstate; /* [n_envs][P] */
 } Oracle;
 
 #define ENV(o, e) ((o)->env + (size_t)(e) * NMMO_NE)
@@ -367,10 +371,45 @@ static int add_skill_exp(int16_t* T, int S, int p, int f_exp, int xp) {
 
 /* ------------------------------------------------------------------ event log (SPEC §11) */
 /* EventLogger.record: players only; row k of the episode at ring index (k-1) mod event_cap */
+/* ------------------------------------------------------------------ tasks (SPEC §12) */
+static int pred_counts_events(int pred) { return pred >= PRED_COUNT_EVENT && pred <= PRED_DEFEAT_ENTITY; }
+
+/* an event of player p feeds the event accumulators of p's task terms */
+static void task_accumulate(Oracle* o, int e, int p, int code, int type, int level, int number,
+                            int gold, int target) {
+  const NmmoTask* t = &o->tasks[o->assign[(size_t)e * o->P + p]];
+  NmmoTaskState* ts = &o->tstate[(size_t)e * o->P + p];
+  for (int k = 0; k < 2; k++) {
+    const NmmoTaskTerm* q = &t->term[k];
+    int32_t* acc = ts->acc + 2 * k;
+    switch (q->pred) {
+      case PRED_COUNT_EVENT: if (code == q->a) acc[0] += 1; break;
+      case PRED_SCORE_HIT: if (code == EV_SCORE_HIT && type == q->a) acc[0] += 1; break;
+      case PRED_HARVEST_ITEM: if (code == EV_HARVEST_ITEM && type == q->a && level >= q->b) acc[0] += number; break;
+      case PRED_CONSUME_ITEM: if (code == EV_CONSUME_ITEM && type == q->a && level >= q->b) acc[0] += number; break;
+      case PRED_LIST_ITEM: if (code == EV_LIST_ITEM && type == q->a && level >= q->b) acc[0] += number; break;
+      case PRED_BUY_ITEM: if (code == EV_BUY_ITEM && type == q->a && level >= q->b) acc[0] += number; break;
+      case PRED_EARN_GOLD: if (code == EV_EARN_GOLD) acc[0] += gold; break;
+      case PRED_SPEND_GOLD: if (code == EV_BUY_ITEM) acc[0] += gold; break;
+      case PRED_MAKE_PROFIT:
+        if (code == EV_EARN_GOLD) acc[0] += gold;
+        if (code == EV_BUY_ITEM) acc[1] += gold;
+        break;
+      case PRED_DEFEAT_ENTITY:
+        if (code == EV_PLAYER_KILL && ((q->a == 0 && target < 0) || (q->a == 1 && target > 0)) && level >= q->b)
+          acc[0] += 1;
+        break;
+      default: break;
+    }
+  }
+}
+
 static void log_event(Oracle* o, int e, int p, int code, int type, int level, int number, int gold,
                       int target) {
   const int cap = o->cfg.event_cap;
-  if (cap <= 0 || p < 0 || p >= o->P) return;
+  if (p < 0 || p >= o->P) return;
+  if (o->tev) task_accumulate(o, e, p, code, type, level, number, gold, target);
+  if (cap <= 0) return;
   int32_t* E = ENV(o, e);
   const int32_t id = ++E[E_EVENT_COUNT];
   int32_t* r = o->events + ((size_t)e * cap + (size_t)((id - 1) % cap)) * NMMO_EVENT_COLS;
@@ -445,6 +484,7 @@ static void reset_env(Oracle* o, int e, uint64_t seed, int episode) {
   for (int k = 0; k < INV * P; k++) ir[k] = (int16_t)(k + 1);
   E[E_ITEM_FREE_HEAD] = 0;
   E[E_ITEM_FREE_COUNT] = INV * P;
+  memset(&o->tstate[(size_t)e * P], 0, (size_t)P * sizeof(NmmoTaskState));
   if (sys_on(o, NMMO_SYS_NPC)) npc_spawn(o, e, 0);
 }
 
@@ -818,7 +858,8 @@ static void write_obs(Oracle* o, int e, float* obs_env /* [P][obs_elems] or NULL
       item_row16(inv + 2 * k, FLD(T, F_ID, p), ob + L.inventory + 16 * k);
     for (int j = 0; j < nm && j < 1024; j++)
       item_row16(INVP(o, e, mown[j]) + 2 * mslot[j], FLD(T, F_ID, mown[j]), ob + L.market + 16 * j);
-    for (int k = 0; k < o->cfg.task_embed_dim; k++) ob[L.task + k] = o->task[k];
+    const float* emb = o->task_emb + (size_t)o->assign[(size_t)e * P + p] * o->cfg.task_embed_dim;
+    for (int k = 0; k < o->cfg.task_embed_dim; k++) ob[L.task + k] = emb[k];
     int w = 0;
     for (int dr = -VISION; dr <= VISION; dr++)
       for (int dc = -VISION; dc <= VISION; dc++, w++) {
@@ -827,6 +868,72 @@ static void write_obs(Oracle* o, int e, float* obs_env /* [P][obs_elems] or NULL
         ob[L.tile + 3 * w + 2] = (float)mat[(r + dr) * SIZE + (c + dc)];
       }
   }
+}
+
+/* ------------------------------------------------------------------ task progress (SPEC §12) */
+static double clip01(double x) { return x < 0.0 ? 0.0 : x > 1.0 ? 1.0 : x; }
+static double per(int num, int den) { return (double)num / (double)(den > 0 ? den : 1); }
+
+static double term_progress(Oracle* o, int e, int p, const NmmoTaskTerm* q, const int32_t* acc) {
+  const int S = o->S;
+  const int16_t* T = ENT(o, e);
+  const int32_t* E = ENV(o, e);
+  const uint32_t* inv = INVP(o, e, p);
+  const int sk = q->a >= 1 && q->a <= 8 ? q->a - 1 : -1; /* skill id -> 0..7 */
+  switch (q->pred) {
+    case PRED_TICK_GE: return per(E[E_TICK], q->a);
+    case PRED_COUNT_EVENT: case PRED_SCORE_HIT: return per(acc[0], q->b);
+    case PRED_HARVEST_ITEM: case PRED_CONSUME_ITEM: case PRED_LIST_ITEM: case PRED_BUY_ITEM:
+    case PRED_DEFEAT_ENTITY: return per(acc[0], q->c);
+    case PRED_EARN_GOLD: case PRED_SPEND_GOLD: return per(acc[0], q->a);
+    case PRED_MAKE_PROFIT: return per(acc[0] - acc[1], q->a);
+    case PRED_HOARD_GOLD: return per(FLD(T, F_GOLD, p), q->a);
+    case PRED_ATTAIN_SKILL: return sk >= 0 && FLD(T, F_MELEE_LEVEL + 2 * sk, p) >= q->b ? 1.0 : 0.0;
+    case PRED_GAIN_EXPERIENCE: return sk >= 0 ? per(FLD(T, F_MELEE_EXP + 2 * sk, p), q->b) : 0.0;
+    case PRED_EQUIP_ITEM:
+      for (int k = 0; k < INV && IT_TYPE(inv + 2 * k); k++)
+        if (IT_EQUIPPED(inv + 2 * k) && IT_TYPE(inv + 2 * k) == q->a && IT_LEVEL(inv + 2 * k) >= q->b) return 1.0;
+      return 0.0;
+    case PRED_OWN_ITEM: {
+      int n = 0;
+      for (int k = 0; k < INV && IT_TYPE(inv + 2 * k); k++)
+        if (IT_TYPE(inv + 2 * k) == q->a && IT_LEVEL(inv + 2 * k) >= q->b) n += IT_QTY(inv + 2 * k);
+      return per(n, q->c);
+    }
+    case PRED_INVENTORY_SPACE_GE: return INV - inv_count(inv) >= q->a ? 1.0 : 0.0;
+    case PRED_OCCUPY_TILE: return FLD(T, F_ROW, p) == q->a && FLD(T, F_COL, p) == q->b ? 1.0 : 0.0;
+    case PRED_CAN_SEE_TILE: {
+      const uint8_t* mat = o->mat + (size_t)e * NMMO_MAP_TILES;
+      const int r = FLD(T, F_ROW, p), c = FLD(T, F_COL, p);
+      for (int dr = -VISION; dr <= VISION; dr++)
+        for (int dc = -VISION; dc <= VISION; dc++)
+          if (mat[(r + dr) * SIZE + c + dc] == q->a) return 1.0;
+      return 0.0;
+    }
+    case PRED_FULLY_ARMED: {
+      if (q->a < 1 || q->a > 3) return 0.0;
+      const int need[5] = {T_HAT, T_TOP, T_BOTTOM, T_SPEAR + q->a - 1, T_WHETSTONE + q->a - 1};
+      for (int j = 0; j < 5; j++) {
+        int ok = 0;
+        for (int k = 0; k < INV && IT_TYPE(inv + 2 * k); k++)
+          ok |= IT_EQUIPPED(inv + 2 * k) && IT_TYPE(inv + 2 * k) == need[j] && IT_LEVEL(inv + 2 * k) >= q->b;
+        if (!ok) return 0.0;
+      }
+      return 1.0;
+    }
+    default: return 0.0;
+  }
+}
+
+static double task_progress(Oracle* o, int e, int p) {
+  const NmmoTask* t = &o->tasks[o->assign[(size_t)e * o->P + p]];
+  const NmmoTaskState* ts = &o->tstate[(size_t)e * o->P + p];
+  const double p0 = clip01(term_progress(o, e, p, &t->term[0], ts->acc));
+  if (t->combine == NMMO_TASK_SINGLE) return p0;
+  const double p1 = clip01(term_progress(o, e, p, &t->term[1], ts->acc + 2));
+  const double v = t->combine == NMMO_TASK_SUM ? (double)t->term[0].weight * p0 + (double)t->term[1].weight * p1
+                                               : p0 * p1;
+  return clip01(v);
 }
 
 /* ------------------------------------------------------------------ step (SPEC §5) */
@@ -1136,14 +1243,20 @@ static void step_env(Oracle* o, int e, const int32_t* actions, float* obs, float
   /* 8. rewards, dones */
   int alive = E[E_PLAYERS_ALIVE];
   int done = alive == 0 || (int)(tick + 1) >= o->cfg.horizon || alive <= o->cfg.early_stop_agent_num;
-  double nt = (double)o->cfg.task_num_tick;
-  double p_new = (double)(tick + 1) / nt, p_old = (double)tick / nt;
-  if (p_new > 1.0) p_new = 1.0;
-  if (p_old > 1.0) p_old = 1.0;
   for (int p = 0; p < P; p++) {
     size_t i = (size_t)e * P + p;
     float rw = 0.f;
-    if (present[p]) rw = died[p] ? -1.f : (float)(p_new - p_old);
+    if (present[p] && died[p]) {
+      rw = -1.f;
+    } else if (present[p]) { /* Task.compute_rewards: progress delta (SPEC §12) */
+      NmmoTaskState* ts = &o->tstate[i];
+      const double np = task_progress(o, e, p), d = np - ts->last;
+      ts->last = np;
+      if (np > ts->max_progress) ts->max_progress = np;
+      if (d > 0.0) ts->signals++;
+      if (np >= 1.0 && ts->completed_tick == 0) ts->completed_tick = E[E_TICK];
+      rw = (float)d;
+    }
     if (rew) rew[i] = rw;
     if (term) term[i] = (uint8_t)died[p];
     if (trunc) trunc[i] = (uint8_t)(done && FLD(T, F_ALIVE, p));
@@ -1196,7 +1309,8 @@ EXPORT int oracle_flat_offsets(int task_dim, int32_t* out /* [20] */) {
 }
 EXPORT size_t oracle_state_bytes_per_env(int slots, int players) {
   return NMMO_NE * 4 + (size_t)NMMO_NF * slots * 2 + (size_t)slots * 2 + NMMO_MAP_TILES +
-         (size_t)players * INV * 8 + (size_t)INV * players * 2;
+         (size_t)players * INV * 8 + (size_t)INV * players * 2 + (size_t)players * 4 +
+         (size_t)players * sizeof(NmmoTaskState);
 }
 
 EXPORT void* oracle_create(const NmmoConfig* cfg, int n_envs, uint64_t seed,
@@ -1221,7 +1335,14 @@ EXPORT void* oracle_create(const NmmoConfig* cfg, int n_envs, uint64_t seed,
   o->events = (int32_t*)calloc((size_t)n_envs * (cfg->event_cap > 0 ? cfg->event_cap : 1) * NMMO_EVENT_COLS, 4);
   for (int m = 0; m < cfg->map_n; m++)
     generate_map(cfg->map_seed, (uint32_t)m, o->bank + (size_t)m * NMMO_MAP_TILES);
-  for (int k = 0; k < cfg->task_embed_dim; k++) o->task[k] = task_emb ? half_to_float(task_emb[k]) : 0.f;
+  o->n_tasks = 1; /* default: everyone runs TickGE(task_num_tick) */
+  o->tasks = (NmmoTask*)calloc(1, sizeof(NmmoTask));
+  o->tasks[0].term[0].pred = PRED_TICK_GE;
+  o->tasks[0].term[0].a = cfg->task_num_tick;
+  o->task_emb = (float*)calloc((size_t)(cfg->task_embed_dim > 0 ? cfg->task_embed_dim : 1), 4);
+  for (int k = 0; k < cfg->task_embed_dim; k++) o->task_emb[k] = task_emb ? half_to_float(task_emb[k]) : 0.f;
+  o->assign = (int32_t*)calloc((size_t)n_envs * o->P, 4);
+  o->tstate = (NmmoTaskState*)calloc((size_t)n_envs * o->P, sizeof(NmmoTaskState));
   return o;
 }
 
@@ -1229,7 +1350,8 @@ EXPORT void oracle_destroy(void* h) {
   Oracle* o = (Oracle*)h;
   if (!o) return;
   free(o->env); free(o->ent); free(o->ring); free(o->mat); free(o->bank);
-  free(o->items); free(o->iring); free(o->events); free(o);
+  free(o->items); free(o->iring); free(o->events);
+  free(o->tasks); free(o->task_emb); free(o->assign); free(o->tstate); free(o);
 }
 
 EXPORT int oracle_reset(void* h, const uint64_t* env_seeds, float* obs, uint8_t* mask) {
@@ -1279,6 +1401,9 @@ EXPORT int oracle_get_state(void* h, void* buf, size_t nbytes) {
     memcpy(b, o->mat + (size_t)e * NMMO_MAP_TILES, NMMO_MAP_TILES); b += NMMO_MAP_TILES;
     memcpy(b, INVP(o, e, 0), (size_t)o->P * INV * 8); b += (size_t)o->P * INV * 8;
     memcpy(b, o->iring + (size_t)e * INV * o->P, (size_t)INV * o->P * 2); b += (size_t)INV * o->P * 2;
+    memcpy(b, o->assign + (size_t)e * o->P, (size_t)o->P * 4); b += (size_t)o->P * 4;
+    memcpy(b, o->tstate + (size_t)e * o->P, (size_t)o->P * sizeof(NmmoTaskState));
+    b += (size_t)o->P * sizeof(NmmoTaskState);
   }
   return 0;
 }
@@ -1294,9 +1419,40 @@ EXPORT int oracle_set_state(void* h, const void* buf, size_t nbytes) {
     memcpy(o->mat + (size_t)e * NMMO_MAP_TILES, b, NMMO_MAP_TILES); b += NMMO_MAP_TILES;
     memcpy(INVP(o, e, 0), b, (size_t)o->P * INV * 8); b += (size_t)o->P * INV * 8;
     memcpy(o->iring + (size_t)e * INV * o->P, b, (size_t)INV * o->P * 2); b += (size_t)INV * o->P * 2;
+    memcpy(o->assign + (size_t)e * o->P, b, (size_t)o->P * 4); b += (size_t)o->P * 4;
+    memcpy(o->tstate + (size_t)e * o->P, b, (size_t)o->P * sizeof(NmmoTaskState));
+    b += (size_t)o->P * sizeof(NmmoTaskState);
   }
   return 0;
 }
+/* as nmmo_set_tasks (SPEC §12) */
+EXPORT int oracle_set_tasks(void* h, const NmmoTask* tasks, int n_tasks, const uint16_t* emb,
+                            const int32_t* assign) {
+  Oracle* o = (Oracle*)h;
+  if (!tasks || n_tasks < 1 || n_tasks > NMMO_MAX_TASKS) return NMMO_E_INVALID;
+  for (int i = 0; i < n_tasks; i++)
+    for (int k = 0; k < 2; k++)
+      if (tasks[i].term[k].pred < 0 || tasks[i].term[k].pred >= NMMO_N_PREDICATES) return NMMO_E_INVALID;
+  if (assign)
+    for (size_t i = 0; i < (size_t)o->n_envs * o->P; i++)
+      if (assign[i] < 0 || assign[i] >= n_tasks) return NMMO_E_INVALID;
+  const int D = o->cfg.task_embed_dim;
+  float* ne = (float*)calloc((size_t)n_tasks * (D > 0 ? D : 1), 4);
+  for (int i = 0; i < n_tasks; i++)
+    for (int k = 0; k < D; k++) ne[(size_t)i * D + k] = emb ? half_to_float(emb[(size_t)i * D + k]) : o->task_emb[k];
+  free(o->task_emb);
+  o->task_emb = ne;
+  free(o->tasks);
+  o->tasks = (NmmoTask*)malloc((size_t)n_tasks * sizeof(NmmoTask));
+  memcpy(o->tasks, tasks, (size_t)n_tasks * sizeof(NmmoTask));
+  o->n_tasks = n_tasks;
+  o->tev = 0;
+  for (int i = 0; i < n_tasks; i++)
+    for (int k = 0; k < 2; k++) o->tev |= pred_counts_events(tasks[i].term[k].pred);
+  for (size_t i = 0; i < (size_t)o->n_envs * o->P; i++) o->assign[i] = assign ? assign[i] : 0;
+  return 0;
+}
+
 /* the env's retained event rows, oldest first (as nmmo_get_events) */
 EXPORT int oracle_get_events(void* h, int env, int32_t* rows, int max_rows, int* n_rows) {
   Oracle* o = (Oracle*)h;

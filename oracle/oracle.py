@@ -44,6 +44,7 @@ def lib():
         L.oracle_set_state.argtypes = [vp, vp, sz]
         L.oracle_get_map_bank.argtypes = [vp, vp, sz]
         L.oracle_get_events.argtypes = [vp, i32, vp, i32, ctypes.POINTER(i32)]
+        L.oracle_set_tasks.argtypes = [vp, vp, i32, vp, vp]
         L.oracle_obs_elems.argtypes = [i32]
         L.oracle_flat_offsets.argtypes = [i32, vp]
         L.oracle_state_bytes_per_env.restype = sz
@@ -115,6 +116,16 @@ class OracleEnvs:
         rc = lib().oracle_set_state(self.h, _p(buf), buf.nbytes)
         assert rc == 0, rc
 
+    def set_tasks(self, tasks, embeddings=None, assign=None):
+        """tasks: sequence of abi.NmmoTask; embeddings fp16 [n_tasks, dim] or None;
+        assign int32 [n_envs, P] or None (SPEC §12, as nmmo_set_tasks)."""
+        arr = (abi.NmmoTask * len(tasks))(*tasks)
+        emb = None if embeddings is None else np.ascontiguousarray(embeddings, np.float16)
+        asg = None if assign is None else np.ascontiguousarray(assign, np.int32)
+        rc = lib().oracle_set_tasks(self.h, ctypes.cast(arr, ctypes.c_void_p), len(tasks),
+                                    None if emb is None else emb.ctypes.data_as(ctypes.c_void_p), _p(asg))
+        assert rc == 0, rc
+
     def events(self, env: int, max_rows: int = 1 << 20) -> np.ndarray:
         """Retained event-log rows of `env`, oldest first: int32 [n, 9] (SPEC §11)."""
         cap = max(self.config.event_cap, 1)
@@ -133,7 +144,7 @@ class OracleEnvs:
 
 def split_state(buf: np.ndarray, n_envs: int, slots: int, players: int = 128) -> dict:
     """View a state blob as named arrays (env [n,NE] i32, ent [n,NF,S] i16, ring, mat,
-    items [n,P,12,2] u32, iring [n,12P] i16)."""
+    items [n,P,12,2] u32, iring [n,12P] i16, tasks [n,P] i32, tstate [n,P] NmmoTaskState)."""
     per = abi.state_bytes_per_env(slots, players)
     b = buf.reshape(n_envs, per)
     o = 0
@@ -146,7 +157,12 @@ def split_state(buf: np.ndarray, n_envs: int, slots: int, players: int = 128) ->
     items = b[:, o:o + ni * 8].copy().view(np.uint32).reshape(n_envs, players, abi.INV_SLOTS, 2)
     o += ni * 8
     iring = b[:, o:o + ni * 2].copy().view(np.int16)
-    return {"env": env, "ent": ent, "ring": ring, "mat": mat, "items": items, "iring": iring}
+    o += ni * 2
+    tasks = b[:, o:o + players * 4].copy().view(np.int32)
+    o += players * 4
+    tstate = b[:, o:o + players * abi.TASK_STATE_BYTES].copy().view(abi.task_state_dtype())
+    return {"env": env, "ent": ent, "ring": ring, "mat": mat, "items": items, "iring": iring,
+            "tasks": tasks, "tstate": tstate}
 
 
 def join_state(d: dict) -> np.ndarray:
@@ -159,5 +175,7 @@ def join_state(d: dict) -> np.ndarray:
                   np.ascontiguousarray(d["ring"][e], np.int16).view(np.uint8),
                   np.ascontiguousarray(d["mat"][e], np.uint8).reshape(-1),
                   np.ascontiguousarray(d["items"][e], np.uint32).reshape(-1).view(np.uint8),
-                  np.ascontiguousarray(d["iring"][e], np.int16).view(np.uint8)]
+                  np.ascontiguousarray(d["iring"][e], np.int16).view(np.uint8),
+                  np.ascontiguousarray(d["tasks"][e], np.int32).view(np.uint8),
+                  np.ascontiguousarray(d["tstate"][e]).view(np.uint8)]
     return np.concatenate(parts)

@@ -217,3 +217,61 @@ def test_item_stress_parity():
                 bad = np.argwhere(go != orc.obs)[:5]
                 raise AssertionError(f"stress obs differs at step {t}: {bad.tolist()}")
     assert busy > 1000  # item heads were actually exercised
+
+
+def _all_predicate_tasks():
+    from nmmo_amd import tasks as T
+
+    return [
+        T.task("TickGE", num_tick=40), T.task("CountEvent", event="DRINK_WATER", N=5),
+        T.task("CountEvent", event="GO_FARTHEST", N=3), T.task("ScoreHit", combat_style="Melee", N=2),
+        T.task("HarvestItem", item="Ration", level=1, quantity=2),
+        T.task("ConsumeItem", item="Potion", level=1, quantity=1),
+        T.task("ListItem", item="Hat", level=1, quantity=1), T.task("BuyItem", item="Top", level=1, quantity=1),
+        T.task("EarnGold", amount=20), T.task("SpendGold", amount=20), T.task("MakeProfit", amount=10),
+        T.task("DefeatEntity", agent_type="npc", level=1, num_agent=1),
+        T.task("DefeatEntity", agent_type="player", level=1, num_agent=1),
+        T.task("HoardGold", amount=50), T.task("AttainSkill", skill="Melee", level=2),
+        T.task("GainExperience", skill="Range", experience=30), T.task("EquipItem", item="Spear", level=1),
+        T.task("OwnItem", item="Whetstone", level=1, quantity=4), T.task("InventorySpaceGE", space=6),
+        T.task("OccupyTile", row=80, col=80), T.task("CanSeeTile", tile_type="Fish"),
+        T.task("FullyArmed", combat_style="Melee", level=1),
+        T.practice_skill_with_tool("Fishing", 60), T.practice_inventory_management(4, 30),
+    ]
+
+
+def test_task_parity_all_predicates():
+    """Every predicate and both combinators, randomly assigned, on the item-stress scenario:
+    rewards and per-player task state (progress, max, accumulators, signals, completion) bit-exact."""
+    import torch
+
+    from oracle.oracle import join_state
+
+    n, steps = 4, 50
+    cfg = Config.preset("C4", MAP_N=4, early_stop_agent_num=0)
+    orc = OracleEnvs(cfg, n, seed=23)
+    tl = _all_predicate_tasks()
+    rng = np.random.default_rng(9)
+    assign = rng.integers(0, len(tl), (n, orc.P)).astype(np.int32)
+    emb = rng.standard_normal((len(tl), cfg.TASK_EMBED_DIM)).astype(np.float16)
+    orc.set_tasks(tl, emb, assign)
+    orc.reset()
+    d = split_state(orc.get_state(), n, orc.S, orc.P)
+    _stress_items(d, np.random.default_rng(6), orc.P)
+    orc.set_state(join_state(d))
+    eng = _engine(cfg, n, seed=0)
+    eng.set_tasks(tl, emb, assign)
+    eng.set_state(orc.get_state())
+    for t in range(steps):
+        acts = orc.scripted_actions(900 + t)
+        orc.step(acts)
+        eng.step(torch.from_numpy(acts).cuda())
+        torch.cuda.synchronize()
+        g, o = split_state(eng.get_state(), n, eng.S, eng.P), split_state(orc.get_state(), n, orc.S, orc.P)
+        assert np.array_equal(g["tstate"].view(np.uint8), o["tstate"].view(np.uint8)), f"task state @ {t}"
+        _cmp_state(eng.get_state(), orc.get_state(), n, eng.S, f"task step {t}")
+        assert np.array_equal(eng.rew.cpu().numpy(), orc.rew), f"rewards @ {t}"
+        if t % 10 == 0:
+            assert np.array_equal(eng.obs.cpu().numpy(), orc.obs), f"obs @ {t}"
+    st = split_state(orc.get_state(), n, orc.S, orc.P)["tstate"]
+    assert (st["signals"] > 0).mean() > 0.15 and (st["completed_tick"] > 0).any()

@@ -1,0 +1,107 @@
+"""Task programs and rewards (SPEC.md §12): known answers on the CPU oracle, hand-computed from
+the SPEC formulas. CPU only."""
+
+import numpy as np
+import pytest
+
+from nmmo_amd import abi, tasks
+from nmmo_amd.config import Config
+from oracle.oracle import OracleEnvs, join_state, split_state
+from tests.test_oracle import GRASS, SCRUB, WATER, find_tile, nbrs, noop_actions, park_others, place, put
+
+F, E = abi.F, abi.E
+
+
+def make(systems=("Resource",), P=4):
+    cfg = Config(systems=systems, PLAYER_N=P, MAP_N=1, early_stop_agent_num=0)
+    o = OracleEnvs(cfg, 1, seed=3)
+    o.reset()
+    return o, split_state(o.get_state(), 1, o.S, o.P)
+
+
+def tstate(o):
+    return split_state(o.get_state(), 1, o.S, o.P)["tstate"][0]
+
+
+def test_count_event_progress_reward_and_completion():
+    o, d = make()
+    mat = d["mat"][0]
+    r, c = find_tile(mat, lambda m, r, c: m[r, c] in (GRASS, SCRUB) and WATER in nbrs(m, r, c))
+    park_others(d, {0}, mat)
+    place(d, 0, r, c)
+    put(o, d)
+    o.set_tasks([tasks.task("CountEvent", event="DRINK_WATER", N=4)])
+    rewards = []
+    for _ in range(6):
+        o.step(noop_actions(o))
+        rewards.append(float(o.rew[0, 0]))
+    assert rewards == [0.25, 0.25, 0.25, 0.25, 0.0, 0.0]  # one DRINK_WATER per tick, N = 4
+    ts = tstate(o)[0]
+    assert ts["last"] == 1.0 and ts["max_progress"] == 1.0 and ts["signals"] == 4
+    assert ts["completed_tick"] == 4 and ts["acc"][0] == 6
+
+
+def test_hoard_gold_can_go_down():
+    o, d = make(systems=("Resource", "Item", "Exchange"))
+    mat = d["mat"][0]
+    r, c = find_tile(mat, lambda m, r, c: m[r, c] in (GRASS, SCRUB) and WATER not in nbrs(m, r, c))
+    park_others(d, {0, 1}, mat)
+    place(d, 0, r, c, gold=5)
+    place(d, 1, r, c, gold=0)
+    put(o, d)
+    o.set_tasks([tasks.task("HoardGold", amount=10)])
+    o.step(noop_actions(o))
+    assert o.rew[0, 0] == np.float32(0.5)
+    a = noop_actions(o)
+    a[0, 0, 6] = 2  # GiveGold price index 2 -> amount 3, to player 1 (its visible row below)
+    ent = split_state(o.get_state(), 1, o.S, o.P)["ent"][0]
+    rows = sorted((ent[F["ds_row"], s], s) for s in range(o.S) if ent[F["alive"], s]
+                  and max(abs(ent[F["row"], s] - r), abs(ent[F["col"], s] - c)) <= 7)
+    a[0, 0, 7] = [s for _, s in rows].index(1)
+    o.step(a)
+    assert o.rew[0, 0] == np.float32(0.2 - 0.5)  # gold 5 -> 2: progress 0.5 -> 0.2
+    assert o.rew[0, 1] == np.float32(0.3)         # player 1 also hoards: 0 -> 3
+
+
+def test_weighted_sum_without_fma():
+    o, d = make(systems=("Resource", "Item", "Equipment", "Profession"))
+    mat = d["mat"][0]
+    r, c = find_tile(mat, lambda m, r, c: m[r, c] in (GRASS, SCRUB) and WATER not in nbrs(m, r, c))
+    park_others(d, {0}, mat)
+    place(d, 0, r, c, fishing_exp=13)
+    d["items"][0, 0, 0] = [8 | (1 << 5) | (1 << 9), 1 | (1 << 16)]  # Rod L1, equipped, row 1
+    d["iring"][0, :] = np.r_[np.arange(2, 12 * o.P + 1), 0]
+    d["env"][0, E["item_free_count"]] = 12 * o.P - 1
+    put(o, d)
+    o.set_tasks([tasks.practice_skill_with_tool("Fishing", 30)])
+    o.step(noop_actions(o))
+    want = np.float64(np.float32(0.3)) * 1.0 + np.float64(np.float32(0.7)) * (13 / 30)
+    assert o.rew[0, 0] == np.float32(want)
+
+
+def test_product_and_per_player_assignment_and_task_obs():
+    cfg = Config.preset("C2", MAP_N=1, early_stop_agent_num=0, PLAYER_N=8)
+    cfg.obs_layout = abi.OBS_FLAT
+    o = OracleEnvs(cfg, 1, seed=5)
+    emb = np.stack([np.full(cfg.TASK_EMBED_DIM, 0.5, np.float16), np.full(cfg.TASK_EMBED_DIM, -1, np.float16)])
+    assign = np.array([[0, 1] * 4], np.int32)
+    o.set_tasks([tasks.task("TickGE", num_tick=8), tasks.practice_inventory_management(12, 4)], emb, assign)
+    o.reset()
+    from nmmo_amd import layout
+
+    t = layout.unflatten(o.obs)["Task"][0]
+    assert np.all(t[0::2] == 0.5) and np.all(t[1::2] == -1.0)
+    o.step(o.scripted_actions(0))
+    alive = o.mask[0] == 1
+    for p in range(8):
+        if alive[p] and not o.term[0, p]:
+            assert o.rew[0, p] == np.float32(1 / 8 if p % 2 == 0 else 1 / 4)
+
+
+def test_builder_rejects_team_tasks_and_unknown_predicates():
+    with pytest.raises(ValueError):
+        tasks.task("AttainSkill", skill="Melee", level=3, num_agent=2)
+    with pytest.raises(ValueError):
+        tasks.task("CanSeeGroup", target="left_team")
+    t = tasks.task("HarvestItem", item="Whetstone", level=2, quantity=3)
+    assert (t.term[0].pred, t.term[0].a, t.term[0].b, t.term[0].c) == (abi.PRED["HarvestItem"], 13, 2, 3)
