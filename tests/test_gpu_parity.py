@@ -23,7 +23,8 @@ def _engine(cfg, n_envs, seed, task=None):
 def _cmp_state(ga, oa, n, S, where, P=128):
     g = split_state(ga, n, S, P)
     o = split_state(oa, n, S, P)
-    for key in ("env", "ring", "mat", "items", "iring"):
+    g["tstate"], o["tstate"] = g["tstate"].view(np.uint8), o["tstate"].view(np.uint8)
+    for key in ("env", "ring", "mat", "items", "iring", "tasks", "tstate"):
         if not np.array_equal(g[key], o[key]):
             bad = np.argwhere(g[key] != o[key])[:5]
             raise AssertionError(f"{where}: {key} differs at {bad.tolist()}")
@@ -275,3 +276,30 @@ def test_task_parity_all_predicates():
             assert np.array_equal(eng.obs.cpu().numpy(), orc.obs), f"obs @ {t}"
     st = split_state(orc.get_state(), n, orc.S, orc.P)["tstate"]
     assert (st["signals"] > 0).mean() > 0.15 and (st["completed_tick"] > 0).any()
+
+
+@pytest.mark.parametrize("P,N,preset", [(100, 50, "C4"), (13, 0, "C3"), (64, 256, "C4"), (1, 7, "C4")])
+def test_rollout_parity_odd_sizes(P, N, preset):
+    """Player/NPC counts that are not multiples of 8/16/64: scalar state-copy fallbacks, partial
+    waves, partial 16-agent obs groups, tiny envs."""
+    import torch
+
+    n, steps = 3, 60
+    cfg = Config.preset(preset, MAP_N=4, early_stop_agent_num=0, PLAYER_N=P, NPC_N=N)
+    eng = _engine(cfg, n, seed=31)
+    orc = OracleEnvs(cfg, n, seed=31)
+    eng.reset()
+    orc.reset()
+    for t in range(steps):
+        acts = orc.scripted_actions(300 + t)
+        g_acts = eng.scripted_actions(300 + t)
+        assert np.array_equal(g_acts.cpu().numpy(), acts), f"policy differs at step {t}"
+        orc.step(acts)
+        eng.step(torch.from_numpy(acts).cuda())
+        torch.cuda.synchronize()
+        _cmp_state(eng.get_state(), orc.get_state(), n, eng.S, f"P={P} N={N} step {t}", P=P)
+        for name in ("rew", "term", "trunc", "mask"):
+            assert np.array_equal(getattr(eng, name).cpu().numpy(), getattr(orc, name)), f"{name} @ {t}"
+        _cmp_events(eng, orc, n, f"P={P} step {t}")
+        if orc.obs is not None and t % 10 == 0:
+            assert np.array_equal(eng.obs.cpu().numpy(), orc.obs), f"obs @ {t}"
