@@ -63,8 +63,10 @@ def test_struct_layout_matches_c_compiler():
 #include <stddef.h>
 #include "nmmo_hip.h"
 int main(void) {
-  printf("%zu %zu %zu %zu %zu\n", sizeof(NmmoConfig), offsetof(NmmoConfig, map_seed),
-         sizeof(NmmoLayout), offsetof(NmmoLayout, off_tile), offsetof(NmmoLayout, state_bytes_per_env));
+  printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(NmmoConfig), offsetof(NmmoConfig, map_seed),
+         sizeof(NmmoLayout), offsetof(NmmoLayout, off_tile), offsetof(NmmoLayout, state_bytes_per_env),
+         offsetof(NmmoConfig, event_cap), sizeof(NmmoTaskTerm), sizeof(NmmoTask), offsetof(NmmoTask, combine),
+         sizeof(NmmoTaskState), offsetof(NmmoTaskState, acc));
   return 0;
 }
 """
@@ -76,8 +78,24 @@ int main(void) {
         got = list(map(int, subprocess.check_output([exe]).split()))
     want = [ctypes.sizeof(abi.NmmoConfig), abi.NmmoConfig.map_seed.offset,
             ctypes.sizeof(abi.NmmoLayout), abi.NmmoLayout.off_tile.offset,
-            abi.NmmoLayout.state_bytes_per_env.offset]
+            abi.NmmoLayout.state_bytes_per_env.offset, abi.NmmoConfig.event_cap.offset,
+            ctypes.sizeof(abi.NmmoTaskTerm), ctypes.sizeof(abi.NmmoTask), abi.NmmoTask.combine.offset,
+            ctypes.sizeof(abi.NmmoTaskState), abi.NmmoTaskState.acc.offset]
     assert got == want
+    assert ctypes.sizeof(abi.NmmoTaskState) == abi.TASK_STATE_BYTES == abi.task_state_dtype().itemsize
+
+
+def test_event_and_predicate_enums_match_header():
+    text = header_text()
+    ev = re.search(r"enum NmmoEventCode \{(.*?)\};", text, re.S).group(1)
+    codes = dict((k.strip()[3:], int(v)) for k, v in (p.split("=") for p in ev.split(",")))
+    assert codes == {k: v for k, v in vars(abi.EventCode).items() if k.isupper()}
+    pr = re.search(r"enum NmmoPredicate \{(.*?)\};", text, re.S).group(1)
+    names = [p.strip().split("=")[0].strip() for p in pr.split(",")]
+    names = [n for n in names if n.startswith("PRED_")]
+    assert len(names) == len(abi.PREDICATES)
+    camel = [n[5:].replace("_", "").lower() for n in names]
+    assert camel == [p.lower() for p in abi.PREDICATES]
 
 
 def test_default_config_matches_python(native):
