@@ -316,8 +316,9 @@ __global__ void __launch_bounds__(512) policy_kernel(PolicyParams p) {
     const uint32_t c0 = (uint32_t)env[E_TICK] + 2048u * (uint32_t)env[E_EPISODE];
     const uint32_t c1 = (uint32_t)env[E_ENV_INDEX];
     const uint32_t k0 = (uint32_t)p.seed, k1 = (uint32_t)(p.seed >> 32);
+    // U(u, 1) = 0 for every u: a head with one legal index needs no Philox call (exact)
     auto draw_n = [&](int head, int n) {
-      return (int)uniform_n(philox(c0, c1, (uint32_t)a, (uint32_t)head, k0, k1).x, (uint32_t)n);
+      return n <= 1 ? 0 : (int)uniform_n(philox(c0, c1, (uint32_t)a, (uint32_t)head, k0, k1).x, (uint32_t)n);
     };
     const int r = E[F_ROW * S + a], c = E[F_COL * S + a], gold = E[F_GOLD * S + a];
     if (combat) h[0] = draw_n(0, 3);
