@@ -11,6 +11,10 @@
 namespace nmmo {
 
 constexpr int kSize = NMMO_MAP_SIZE;  // 160
+// Visibility grid: 16x16-tile cells; a 15x15 window touches at most 2x2 cells.
+constexpr int kCellShift = 4;
+constexpr int kGrid = (kSize + (1 << kCellShift) - 1) >> kCellShift;  // 10
+constexpr int kCells = kGrid * kGrid;
 constexpr int kTiles = NMMO_MAP_TILES;
 constexpr int kLo = 16, kHi = 143, kCenter = 128, kVision = 7, kNObs = 100;
 constexpr int kBitmapWords = kTiles / 32;  // 800 depleted-tile bitmap words per env

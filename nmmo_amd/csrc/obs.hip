@@ -200,22 +200,22 @@ hipError_t launch_obs(const ObsParams& p, hipStream_t stream) {
 
 // ---------------------------------------------------------------- scripted policy (SPEC §10)
 // One workgroup per env: for every head, a uniform draw over the set bits of that head's mask
-// (identical to the obs masks). Phase A (all waves, rows across lanes): for each player one
-// packed 16-bit window test per row (entity (r+7, c+7) minus player (r, c), one v_pk_sub_u16)
-// and three ballots give the visible / attackable / same-tile row bitmaps. Phase B (thread per
-// player): the first-100-visible cut, counts, draws and k-th-set-bit selections with popcounts.
+// (identical to the obs masks). Phase A: alive entities are bucketed into a uniform grid of
+// 16x16-tile cells; each player (thread) tests the entities of the <= 2x2 cells its window
+// touches and sets its visible / attackable / same-tile row bits. Phase B (thread per player):
+// the first-100-visible cut, counts, draws and k-th-set-bit selections with popcounts.
 __host__ __device__ inline int policy_threads(int S, int P) {
   const int t = ((S + 63) / 64) * 64;
   return t < P ? ((P + 63) / 64) * 64 : t;
 }
 __host__ __device__ inline size_t policy_lds_bytes(int S, int P) {
   const int NW = (S + 63) / 64;
-  return (size_t)3 * P * NW * 8 + (size_t)((P + 3) & ~3) * 4 + (size_t)NMMO_MARKET_ROWS * 12;
+  return (size_t)3 * P * NW * 8 + (size_t)((P + 3) & ~3) * 4 + (size_t)NMMO_MARKET_ROWS * 12 +
+         (size_t)(2 * kCells + 2) * 4 + (size_t)S * 4;
 }
 
 __global__ void __launch_bounds__(512) policy_kernel(PolicyParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  typedef unsigned short us2 __attribute__((ext_vector_type(2)));
   const int S = p.S, P = p.P, e = blockIdx.x, tid = threadIdx.x;
   const int NW = (S + 63) >> 6;
   uint64_t* vism = reinterpret_cast<uint64_t*>(smem);  // [P][NW] visible rows
@@ -224,6 +224,9 @@ __global__ void __launch_bounds__(512) policy_kernel(PolicyParams p) {
   uint32_t* ppos = reinterpret_cast<uint32_t*>(samm + P * NW);  // [P] r<<16 | c, or sentinel
   uint2* mitem = reinterpret_cast<uint2*>(ppos + ((P + 3) & ~3));
   int* mown = reinterpret_cast<int*>(mitem + NMMO_MARKET_ROWS);
+  int* gstart = mown + NMMO_MARKET_ROWS;  // [kCells+1] grid cell -> first glist index
+  int* gcnt = gstart + kCells + 1;        // [kCells+1]
+  uint32_t* glist = reinterpret_cast<uint32_t*>(gcnt + kCells + 1);  // [S]
   const int16_t* E = p.ent + (size_t)e * NMMO_NF * S;
   const bool combat = (p.systems & NMMO_SYS_COMBAT) != 0;
   const bool item = (p.systems & NMMO_SYS_ITEM) != 0;
@@ -237,60 +240,61 @@ __global__ void __launch_bounds__(512) policy_kernel(PolicyParams p) {
   for (int a = tid; a < ((P + 3) & ~3); a += blockDim.x)
     ppos[a] = (a < P && E[F_ALIVE * S + a]) ? ((uint32_t)E[F_ROW * S + a] << 16) | (uint32_t)E[F_COL * S + a]
                                             : 0x80008000u;
-  // the entity of datastore row (64w + lane + 1): found by the slot that owns it
-  __shared__ int rowslot[512];
-  for (int k = tid; k <= S; k += blockDim.x) rowslot[k] = -1;
-  __syncthreads();
-  for (int s = tid; s < S; s += blockDim.x)
-    if (E[F_ALIVE * S + s]) rowslot[E[F_DS_ROW * S + s]] = s;
-  __syncthreads();
   const bool tgt_any = combat || item;
   if (tgt_any) {
-    // per player: pk_sub + packed max + compare per row-lane, three ballots, writelanes.
-    // Row-constant conditions (immune target, player entity) are folded into masks once; the
-    // player's own row is cleared in phase B.
-    const int w = wave_id(), lane = lane_id(), row = (w << 6) + lane + 1;
-    if (w < NW) {
-      const int q = row <= S ? rowslot[row] : -1;
-      const uint32_t e32 = q < 0 ? 0xF000F000u
-                                 : ((uint32_t)(E[F_ROW * S + q] + 7) << 16) | (uint32_t)(E[F_COL * S + q] + 7);
-      const bool immune = q >= 0 && q < P && E[F_TIME_ALIVE * S + q] < p.spawn_immunity;
-      const uint64_t not_immune = __ballot(!immune), is_player = __ballot(q >= 0 && q < P);
-      const us2 e2 = __builtin_bit_cast(us2, e32);
-      const us2 four = {4, 4};
-      const uint4* pp4 = reinterpret_cast<const uint4*>(ppos);
-      for (int pb = 0; pb < P; pb += 64) {
-        uint32_t v_lo = 0, v_hi = 0, a_lo = 0, a_hi = 0, s_lo = 0, s_hi = 0;
-        const int pe = min(P, pb + 64);
-        for (int g = pb >> 2; g < (pe + 3) >> 2; g++) {
-          const uint4 pq = pp4[g];
-          const uint32_t pv[4] = {(uint32_t)__builtin_amdgcn_readfirstlane((int)pq.x),
-                                  (uint32_t)__builtin_amdgcn_readfirstlane((int)pq.y),
-                                  (uint32_t)__builtin_amdgcn_readfirstlane((int)pq.z),
-                                  (uint32_t)__builtin_amdgcn_readfirstlane((int)pq.w)};
+    uint32_t* m32 = reinterpret_cast<uint32_t*>(vism);  // vism | atkm | samm, contiguous
+    for (int k = tid; k < 6 * P * NW; k += blockDim.x) m32[k] = 0;
+    for (int k = tid; k < kCells; k += blockDim.x) gcnt[k] = 0;
+  }
+  __syncthreads();
+  if (tgt_any) {
+    // grid entry: (ds_row-1)<<16 | r<<8 | c, bit 30 = not spawn-immune, bit 31 = player
+    int cell = -1, gi = 0;
+    uint32_t gv = 0;
+    if (tid < S && E[F_ALIVE * S + tid]) {  // policy_threads >= S
+      const int r = E[F_ROW * S + tid], c = E[F_COL * S + tid];
+      const bool pl = tid < P, immune = pl && E[F_TIME_ALIVE * S + tid] < p.spawn_immunity;
+      cell = (r >> kCellShift) * kGrid + (c >> kCellShift);
+      gi = atomicAdd(&gcnt[cell], 1);
+      gv = ((uint32_t)(E[F_DS_ROW * S + tid] - 1) << 16) | (uint32_t)(r << 8) | (uint32_t)c |
+           (immune ? 0u : 1u << 30) | (pl ? 1u << 31 : 0u);
+    }
+    __syncthreads();
+    if (tid < 64) {  // wave 0: exclusive scan over cells, two per lane; gstart[kCells] = total
+      const int a0 = 2 * tid < kCells ? gcnt[2 * tid] : 0;
+      const int a1 = 2 * tid + 1 < kCells ? gcnt[2 * tid + 1] : 0;
+      int x = a0 + a1;
 #pragma unroll
-          for (int j = 0; j < 4; j++) {
-            const us2 t = e2 - __builtin_bit_cast(us2, pv[j]);
-            const us2 t4 = t - four;
-            const us2 mx = __builtin_elementwise_max(t, t.yx);
-            const us2 m4 = __builtin_elementwise_max(t4, t4.yx);
-            const uint64_t mv = __ballot(mx.x <= 14);
-            const uint64_t ma = __ballot(m4.x <= 6) & not_immune;
-            const uint64_t ms = __ballot(__builtin_bit_cast(uint32_t, t) == 0x00070007u) & is_player;
-            const uint32_t l = (uint32_t)((4 * g + j) & 63);
-            v_lo = writelane_u32(v_lo, (uint32_t)mv, l);
-            v_hi = writelane_u32(v_hi, (uint32_t)(mv >> 32), l);
-            a_lo = writelane_u32(a_lo, (uint32_t)ma, l);
-            a_hi = writelane_u32(a_hi, (uint32_t)(ma >> 32), l);
-            s_lo = writelane_u32(s_lo, (uint32_t)ms, l);
-            s_hi = writelane_u32(s_hi, (uint32_t)(ms >> 32), l);
-          }
-        }
-        if (pb + lane < pe) {
-          const int a = pb + lane;
-          vism[a * NW + w] = ((uint64_t)v_hi << 32) | v_lo;
-          atkm[a * NW + w] = ((uint64_t)a_hi << 32) | a_lo;
-          samm[a * NW + w] = ((uint64_t)s_hi << 32) | s_lo;
+      for (int d = 1; d < 64; d <<= 1) {
+        const int y = __shfl_up(x, d);
+        if (tid >= d) x += y;
+      }
+      const int ex = x - a0 - a1;
+      if (2 * tid <= kCells) gstart[2 * tid] = ex;
+      if (2 * tid + 1 <= kCells) gstart[2 * tid + 1] = ex + a0;
+    }
+    __syncthreads();
+    if (cell >= 0) glist[gstart[cell] + gi] = gv;
+    __syncthreads();
+    for (int a = tid; a < P; a += blockDim.x) {
+      if (ppos[a] == 0x80008000u) continue;
+      const int r = (int)(ppos[a] >> 16), c = (int)(ppos[a] & 0xFFFF);
+      const int r0 = max(r - 7, 0) >> kCellShift, r1 = min(r + 7, kSize - 1) >> kCellShift;
+      const int c0 = max(c - 7, 0) >> kCellShift, c1 = min(c + 7, kSize - 1) >> kCellShift;
+      uint32_t* mv = reinterpret_cast<uint32_t*>(vism + a * NW);
+      uint32_t* ma = reinterpret_cast<uint32_t*>(atkm + a * NW);
+      uint32_t* ms = reinterpret_cast<uint32_t*>(samm + a * NW);
+      for (int cr = r0; cr <= r1; cr++) {  // cells c0..c1 of one grid row are contiguous
+        for (int i = gstart[cr * kGrid + c0], e1 = gstart[cr * kGrid + c1 + 1]; i < e1; i++) {
+          const uint32_t v = glist[i];
+          const int dr = abs((int)((v >> 8) & 255) - r), dc = abs((int)(v & 255) - c);
+          const int d = max(dr, dc);
+          if (d > 7) continue;
+          const int wi = (v >> 21) & 15;
+          const uint32_t bit = 1u << ((v >> 16) & 31);
+          mv[wi] |= bit;
+          if (d <= 3 && (v & (1u << 30))) ma[wi] |= bit;
+          if (d == 0 && (v >> 31)) ms[wi] |= bit;
         }
       }
     }
@@ -427,7 +431,7 @@ __global__ void __launch_bounds__(512) policy_kernel(PolicyParams p) {
 }
 
 hipError_t launch_policy(const PolicyParams& p, hipStream_t stream) {
-  if (p.S > 511) return hipErrorInvalidValue;  // rowslot[512]
+  if (p.S > 511) return hipErrorInvalidValue;  // grid entries hold ds_row - 1 in 9 bits
   hipLaunchKernelGGL(policy_kernel, dim3(p.n_envs), dim3(policy_threads(p.S, p.P)),
                      policy_lds_bytes(p.S, p.P), stream, p);
   return hipGetLastError();

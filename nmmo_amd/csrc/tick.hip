@@ -29,6 +29,9 @@ namespace nmmo {
 struct Ctx {
   int16_t* T;        // [kNFLive][S]
   uint64_t* vism;    // [P][NW] visibility bitmap: bit j of word w = row 64w+j+1 visible to player
+  int* gstart;       // [kCells+1] grid cell -> first glist index (after vism, union region)
+  int* gcnt;         // [kCells] grid cell population
+  uint32_t* glist;   // [S] in-realm entities by cell: (ds_row-1)<<16 | r<<8 | c
   int* rp;           // [S+1] datastore row -> r | c<<8 | slot<<16 (-1 = no entity)
   int* sp;           // [S] slot -> r | c<<8 while in the realm with health > 0 (-1 otherwise)
   uint32_t* pp;      // [128] player -> r<<16 | c (0x80008000 when not in the realm): window tests
@@ -113,7 +116,7 @@ constexpr size_t kPlayerArrBytes = 4 * 256 + 128;  // kill, order, ev_dmg, ev_lv
 // in phase 6), the position hash (update/harvest) and the attack first-touch arrays.
 __host__ __device__ inline size_t union_lds_bytes(int S) {
   auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
-  size_t u = (size_t)128 * ((S + 63) / 64) * 8;
+  size_t u = (size_t)128 * ((S + 63) / 64) * 8 + 2 * al((kCells + 1) * 4) + al((size_t)S * 4);
   u = u > 2 * kHash * 4 ? u : 2 * kHash * 4;
   const size_t atk = al((size_t)S * 4) + al((size_t)S * 2);
   return u > atk ? u : atk;
@@ -183,6 +186,12 @@ __device__ __forceinline__ Ctx make_ctx(unsigned char* smem, const DevState& st,
   {  // the union region (see union_lds_bytes)
     unsigned char* u = smem + o;
     c.vism = reinterpret_cast<uint64_t*>(u);
+    {
+      const size_t vb = (size_t)128 * ((S + 63) / 64) * 8;
+      c.gstart = reinterpret_cast<int*>(u + vb);
+      c.gcnt = reinterpret_cast<int*>(u + vb + al((kCells + 1) * 4));
+      c.glist = reinterpret_cast<uint32_t*>(u + vb + 2 * al((kCells + 1) * 4));
+    }
     c.hkey = reinterpret_cast<int*>(u);
     c.hmin = reinterpret_cast<int*>(u + kHash * 4);
     c.ft = reinterpret_cast<int*>(u);
@@ -929,34 +938,51 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
   const int NW = (S + 63) >> 6;
   const bool combat = sys(c, NMMO_SYS_COMBAT);
   if (combat || items) {
-    // Packed 16-bit window test: entity (col+7, row+7) minus player (col, row) with one
-    // v_pk_sub_u16; both halves <= 14 <=> L-inf <= 7 (out-of-window values wrap to >= 0x8000).
-    typedef unsigned short us2 __attribute__((ext_vector_type(2)));
-    const int w = wave_id(), lane = lane_id(), row = (w << 6) + lane + 1;
-    const int v = row <= S ? c.rp[row] : -1;
-    const uint32_t e32 = v < 0 ? 0xF000F000u : ((uint32_t)((v & 255) + 7) << 16) | (uint32_t)(((v >> 8) & 255) + 7);
-    const us2 e2 = __builtin_bit_cast(us2, e32);
-    const uint4* pp4 = reinterpret_cast<const uint4*>(c.pp);
-    for (int pb = 0; pb < P; pb += 64) {
-      uint32_t mine_lo = 0, mine_hi = 0;  // lane j keeps the mask of player pb + j
-      const int pe = min(P, pb + 64);
-      for (int g = pb >> 2; g < (pe + 3) >> 2; g++) {  // 4 players per ds_read_b128 (broadcast)
-        const uint4 q = pp4[g];
-        const uint32_t pv[4] = {(uint32_t)__builtin_amdgcn_readfirstlane((int)q.x),
-                                (uint32_t)__builtin_amdgcn_readfirstlane((int)q.y),
-                                (uint32_t)__builtin_amdgcn_readfirstlane((int)q.z),
-                                (uint32_t)__builtin_amdgcn_readfirstlane((int)q.w)};
+    // Uniform grid (kCells cells of 16x16 tiles): each player tests only the entities of the
+    // <= 2x2 cells its 15x15 window touches. Bit (row-1) of the player's bitmap is set iff the
+    // entity in datastore row `row` is in the realm and within L-inf 7 -- the same set an
+    // all-pairs test gives, at ~1/16 of the pair tests on a 128-player realm.
+    uint32_t* vis32 = reinterpret_cast<uint32_t*>(c.vism);
+    for (int k = tid; k < P * NW * 2; k += nt) vis32[k] = 0;
+    for (int k = tid; k < kCells; k += nt) c.gcnt[k] = 0;
+    __syncthreads();
+    int cell = -1, gi = 0;
+    uint32_t gv = 0;
+    if (s < S && c.sp[s] >= 0) {
+      const int pos = c.sp[s], r = pos & 255, col = (pos >> 8) & 255;
+      cell = (r >> kCellShift) * kGrid + (col >> kCellShift);
+      gi = atomicAdd(&c.gcnt[cell], 1);
+      gv = ((uint32_t)(TF(F_DS_ROW, s) - 1) << 16) | (uint32_t)(r << 8) | (uint32_t)col;
+    }
+    __syncthreads();
+    if (tid < 64) {  // wave 0: exclusive scan over cells, two per lane; gstart[kCells] = total
+      const int a0 = 2 * tid < kCells ? c.gcnt[2 * tid] : 0;
+      const int a1 = 2 * tid + 1 < kCells ? c.gcnt[2 * tid + 1] : 0;
+      int x = a0 + a1;
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-          const us2 t = e2 - __builtin_bit_cast(us2, pv[j]);
-          const us2 mx = __builtin_elementwise_max(t, t.yx);
-          const uint64_t m = __ballot(mx.x <= 14);
-          const uint32_t l = (uint32_t)((4 * g + j) & 63);
-          mine_lo = writelane_u32(mine_lo, (uint32_t)m, l);
-          mine_hi = writelane_u32(mine_hi, (uint32_t)(m >> 32), l);
+      for (int d = 1; d < 64; d <<= 1) {
+        const int y = __shfl_up(x, d);
+        if (tid >= d) x += y;
+      }
+      const int ex = x - a0 - a1;
+      if (2 * tid <= kCells) c.gstart[2 * tid] = ex;
+      if (2 * tid + 1 <= kCells) c.gstart[2 * tid + 1] = ex + a0;
+    }
+    __syncthreads();
+    if (cell >= 0) c.glist[c.gstart[cell] + gi] = gv;
+    __syncthreads();
+    if (s < P && c.pres[s]) {
+      const int r = (int)(c.pp[s] >> 16), col = (int)(c.pp[s] & 0xFFFF);
+      const int r0 = max(r - 7, 0) >> kCellShift, r1 = min(r + 7, kSize - 1) >> kCellShift;
+      const int c0 = max(col - 7, 0) >> kCellShift, c1 = min(col + 7, kSize - 1) >> kCellShift;
+      uint32_t* mine = vis32 + s * NW * 2;
+      for (int cr = r0; cr <= r1; cr++) {  // cells c0..c1 of one grid row are contiguous
+        for (int i = c.gstart[cr * kGrid + c0], e = c.gstart[cr * kGrid + c1 + 1]; i < e; i++) {
+          const uint32_t v = c.glist[i];
+          const int dr = (int)((v >> 8) & 255) - r, dc = (int)(v & 255) - col;
+          if (max(abs(dr), abs(dc)) <= 7) mine[v >> 21] |= 1u << ((v >> 16) & 31);
         }
       }
-      if (pb + lane < pe) c.vism[(pb + lane) * NW + w] = ((uint64_t)mine_hi << 32) | mine_lo;
     }
   }
   __syncthreads();
