@@ -276,27 +276,24 @@ __global__ void __launch_bounds__(512) policy_kernel(PolicyParams p) {
     __syncthreads();
     if (cell >= 0) glist[gstart[cell] + gi] = gv;
     __syncthreads();
-    for (int a = tid; a < P; a += blockDim.x) {
+    // two threads per player, one grid row of its window each; no-return LDS atomics
+    for (int t = tid; t < 2 * P; t += blockDim.x) {
+      const int a = t >> 1;
       if (ppos[a] == 0x80008000u) continue;
       const int r = (int)(ppos[a] >> 16), c = (int)(ppos[a] & 0xFFFF);
-      const int r0 = max(r - 7, 0) >> kCellShift, r1 = min(r + 7, kSize - 1) >> kCellShift;
+      const int cr = (max(r - 7, 0) >> kCellShift) + (t & 1);
+      if (cr > (min(r + 7, kSize - 1) >> kCellShift)) continue;
       const int c0 = max(c - 7, 0) >> kCellShift, c1 = min(c + 7, kSize - 1) >> kCellShift;
       uint32_t* mv = reinterpret_cast<uint32_t*>(vism + a * NW);
       uint32_t* ma = reinterpret_cast<uint32_t*>(atkm + a * NW);
       uint32_t* ms = reinterpret_cast<uint32_t*>(samm + a * NW);
-      for (int cr = r0; cr <= r1; cr++) {  // cells c0..c1 of one grid row are contiguous
-        for (int i = gstart[cr * kGrid + c0], e1 = gstart[cr * kGrid + c1 + 1]; i < e1; i++) {
-          const uint32_t v = glist[i];
-          const int dr = abs((int)((v >> 8) & 255) - r), dc = abs((int)(v & 255) - c);
-          const int d = max(dr, dc);
-          if (d > 7) continue;
-          const int wi = (v >> 21) & 15;
-          const uint32_t bit = 1u << ((v >> 16) & 31);
-          mv[wi] |= bit;
-          if (d <= 3 && (v & (1u << 30))) ma[wi] |= bit;
-          if (d == 0 && (v >> 31)) ms[wi] |= bit;
-        }
-      }
+      grid_scan(glist, gstart[cr * kGrid + c0], gstart[cr * kGrid + c1 + 1], r, c, [&](uint32_t v, int d) {
+        const int wi = (v >> 21) & 15;
+        const uint32_t bit = 1u << ((v >> 16) & 31);
+        atomicOr(&mv[wi], bit);
+        if (d <= 3 && (v & (1u << 30))) atomicOr(&ma[wi], bit);
+        if (d == 0 && (v >> 31)) atomicOr(&ms[wi], bit);
+      });
     }
   }
   __syncthreads();

@@ -971,18 +971,17 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
     __syncthreads();
     if (cell >= 0) c.glist[c.gstart[cell] + gi] = gv;
     __syncthreads();
-    if (s < P && c.pres[s]) {
-      const int r = (int)(c.pp[s] >> 16), col = (int)(c.pp[s] & 0xFFFF);
-      const int r0 = max(r - 7, 0) >> kCellShift, r1 = min(r + 7, kSize - 1) >> kCellShift;
+    // two threads per player, one grid row of its window each; bits land with no-return LDS
+    // atomics (ds_or_b32), so only the candidate loads are waited on, four at a time
+    for (int t = tid; t < 2 * P; t += nt) {
+      const int p = t >> 1;
+      if (!c.pres[p]) continue;
+      const int r = (int)(c.pp[p] >> 16), col = (int)(c.pp[p] & 0xFFFF);
+      const int cr = (max(r - 7, 0) >> kCellShift) + (t & 1);
+      if (cr > (min(r + 7, kSize - 1) >> kCellShift)) continue;
       const int c0 = max(col - 7, 0) >> kCellShift, c1 = min(col + 7, kSize - 1) >> kCellShift;
-      uint32_t* mine = vis32 + s * NW * 2;
-      for (int cr = r0; cr <= r1; cr++) {  // cells c0..c1 of one grid row are contiguous
-        for (int i = c.gstart[cr * kGrid + c0], e = c.gstart[cr * kGrid + c1 + 1]; i < e; i++) {
-          const uint32_t v = c.glist[i];
-          const int dr = (int)((v >> 8) & 255) - r, dc = (int)(v & 255) - col;
-          if (max(abs(dr), abs(dc)) <= 7) mine[v >> 21] |= 1u << ((v >> 16) & 31);
-        }
-      }
+      grid_scan(c.glist, c.gstart[cr * kGrid + c0], c.gstart[cr * kGrid + c1 + 1], r, col,
+                [&](uint32_t v, int) { atomicOr(&vis32[p * NW * 2 + (v >> 21)], 1u << ((v >> 16) & 31)); });
     }
   }
   __syncthreads();
