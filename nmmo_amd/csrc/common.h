@@ -17,23 +17,23 @@ constexpr int kGrid = (kSize + (1 << kCellShift) - 1) >> kCellShift;  // 10
 constexpr int kCells = kGrid * kGrid;
 
 // Visit the grid entries glist[i0, i1) (bits 0-7 column, 8-15 row) within L-inf 7 of (r, c):
-// f(entry, L-inf distance). Loads are issued four at a time ahead of their uses.
+// f(entry, L-inf distance, index). Loads are issued four at a time ahead of their uses.
 template <class Fn>
 __device__ __forceinline__ void grid_scan(const uint32_t* __restrict__ glist, int i0, int i1, int r,
                                           int c, Fn&& f) {
-  auto one = [&](uint32_t v) {
+  auto one = [&](uint32_t v, int i) {
     const int d = max(abs((int)((v >> 8) & 255) - r), abs((int)(v & 255) - c));
-    if (d <= 7) f(v, d);
+    if (d <= 7) f(v, d, i);
   };
   int i = i0;
   for (; i + 4 <= i1; i += 4) {
     const uint32_t v0 = glist[i], v1 = glist[i + 1], v2 = glist[i + 2], v3 = glist[i + 3];
-    one(v0);
-    one(v1);
-    one(v2);
-    one(v3);
+    one(v0, i);
+    one(v1, i + 1);
+    one(v2, i + 2);
+    one(v3, i + 3);
   }
-  for (; i < i1; i++) one(glist[i]);
+  for (; i < i1; i++) one(glist[i], i);
 }
 constexpr int kTiles = NMMO_MAP_TILES;
 constexpr int kLo = 16, kHi = 143, kCenter = 128, kVision = 7, kNObs = 100;

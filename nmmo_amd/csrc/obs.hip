@@ -287,7 +287,7 @@ __global__ void __launch_bounds__(512) policy_kernel(PolicyParams p) {
       uint32_t* mv = reinterpret_cast<uint32_t*>(vism + a * NW);
       uint32_t* ma = reinterpret_cast<uint32_t*>(atkm + a * NW);
       uint32_t* ms = reinterpret_cast<uint32_t*>(samm + a * NW);
-      grid_scan(glist, gstart[cr * kGrid + c0], gstart[cr * kGrid + c1 + 1], r, c, [&](uint32_t v, int d) {
+      grid_scan(glist, gstart[cr * kGrid + c0], gstart[cr * kGrid + c1 + 1], r, c, [&](uint32_t v, int d, int) {
         const int wi = (v >> 21) & 15;
         const uint32_t bit = 1u << ((v >> 16) & 31);
         atomicOr(&mv[wi], bit);

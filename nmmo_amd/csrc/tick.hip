@@ -31,7 +31,8 @@ struct Ctx {
   uint64_t* vism;    // [P][NW] visibility bitmap: bit j of word w = row 64w+j+1 visible to player
   int* gstart;       // [kCells+1] grid cell -> first glist index (after vism, union region)
   int* gcnt;         // [kCells] grid cell population
-  uint32_t* glist;   // [S] in-realm entities by cell: (ds_row-1)<<16 | r<<8 | c
+  uint32_t* glist;   // [S] in-realm entities by cell: player<<31 | (ds_row-1)<<16 | r<<8 | c
+  int16_t* gslot;    // [S] slot of each glist entry
   int* rp;           // [S+1] datastore row -> r | c<<8 | slot<<16 (-1 = no entity)
   int* sp;           // [S] slot -> r | c<<8 while in the realm with health > 0 (-1 otherwise)
   uint32_t* pp;      // [128] player -> r<<16 | c (0x80008000 when not in the realm): window tests
@@ -116,7 +117,8 @@ constexpr size_t kPlayerArrBytes = 4 * 256 + 128;  // kill, order, ev_dmg, ev_lv
 // in phase 6), the position hash (update/harvest) and the attack first-touch arrays.
 __host__ __device__ inline size_t union_lds_bytes(int S) {
   auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
-  size_t u = (size_t)128 * ((S + 63) / 64) * 8 + 2 * al((kCells + 1) * 4) + al((size_t)S * 4);
+  size_t u = (size_t)128 * ((S + 63) / 64) * 8 + 2 * al((kCells + 1) * 4) + al((size_t)S * 4) +
+             al((size_t)S * 2);
   u = u > 2 * kHash * 4 ? u : 2 * kHash * 4;
   const size_t atk = al((size_t)S * 4) + al((size_t)S * 2);
   return u > atk ? u : atk;
@@ -191,6 +193,7 @@ __device__ __forceinline__ Ctx make_ctx(unsigned char* smem, const DevState& st,
       c.gstart = reinterpret_cast<int*>(u + vb);
       c.gcnt = reinterpret_cast<int*>(u + vb + al((kCells + 1) * 4));
       c.glist = reinterpret_cast<uint32_t*>(u + vb + 2 * al((kCells + 1) * 4));
+      c.gslot = reinterpret_cast<int16_t*>(u + vb + 2 * al((kCells + 1) * 4) + al((size_t)S * 4));
     }
     c.hkey = reinterpret_cast<int*>(u);
     c.hmin = reinterpret_cast<int*>(u + kHash * 4);
@@ -645,7 +648,9 @@ __device__ __forceinline__ bool npc_validate(Ctx& c, int n) {
 
 // closest: slot of the closest player within vision (ties to the lowest id) for a hostile NPC
 // without a target (computed block-wide by the caller), else -1
-__device__ __forceinline__ void npc_decide(Ctx& c, int n, int closest, int& move, int& tgt, int& sty) {
+// nbm: tick-start neighbourhood bits of the NPC's tile (bit d = neighbour d passable)
+__device__ __forceinline__ void npc_decide(Ctx& c, int n, int closest, uint32_t nbm, int& move, int& tgt,
+                                           int& sty) {
   const int r = TF(F_ROW, n), col = TF(F_COL, n), id = TF(F_ID, n);
   const U4 u = draw(env_seed(c), (uint32_t)c.E[E_TICK], P_NPC_MOVE, (uint32_t)(-id), 0);
   move = -1;
@@ -664,7 +669,7 @@ __device__ __forceinline__ void npc_decide(Ctx& c, int n, int closest, int& move
     int cand[4], k = 0;
 #pragma unroll
     for (int d = 0; d < 4; d++)
-      if (!impassable(c.mat[(r + dir_dr(d)) * kSize + col + dir_dc(d)])) cand[k++] = d;
+      if ((nbm >> d) & 1u) cand[k++] = d;
     if (k) move = cand[uniform_n(u.x, (uint32_t)k)];
     return;
   }
@@ -679,9 +684,8 @@ __device__ __forceinline__ void npc_decide(Ctx& c, int n, int closest, int& move
     const bool rows_first = iabs(dr) >= iabs(dc);
     const int first = rows_first ? dir_r : dir_c, second = rows_first ? dir_c : dir_r;
     const bool second_nz = rows_first ? dc != 0 : dr != 0;
-    if (!impassable(c.mat[(r + dir_dr(first)) * kSize + col + dir_dc(first)])) move = first;
-    else if (second_nz && !impassable(c.mat[(r + dir_dr(second)) * kSize + col + dir_dc(second)]))
-      move = second;
+    if ((nbm >> first) & 1u) move = first;
+    else if (second_nz && ((nbm >> second) & 1u)) move = second;
   }
   if (dist <= 3) tgt = ts;
 }
@@ -908,11 +912,25 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
     for (int k = 0; k < 2; k++) c.tdesc[s * 2 + k] = make_int4(tk.term[k].pred, tk.term[k].a, tk.term[k].b, tk.term[k].c);
   }
   __syncthreads();
+  // Materials around this slot's tile at tick start, loaded here so their latency hides behind
+  // the decode; used after it through `nbm`. Passability and Water never change within a tick
+  // (every depletion/regrowth maps passable to passable and impassable to impassable), and no
+  // entity moves before the move phase, so these stay exact for NPC steering, drinking,
+  // foilage eating (the own tile is read before any harvest) and the move check.
+  uint32_t m_own = 0, m_n0 = 0, m_n1 = 0, m_n2 = 0, m_n3 = 0;
   if (s < S) {
     const bool in = inslot && TF(F_ALIVE, s);  // in the realm => health > 0 at tick start
     const int pos = TF(F_ROW, s) | (TF(F_COL, s) << 8);
     c.sp[s] = in ? pos : -1;
-    if (in) c.rp[TF(F_DS_ROW, s)] = pos | (s << 16);
+    if (in) {
+      c.rp[TF(F_DS_ROW, s)] = pos | (s << 16);
+      const uint8_t* m = c.mat + TF(F_ROW, s) * kSize + TF(F_COL, s);
+      m_own = m[0];
+      m_n0 = m[-kSize];
+      m_n1 = m[kSize];
+      m_n2 = m[1];
+      m_n3 = m[-1];
+    }
   }
   if (tid < 128) c.pp[tid] = (tid < P && TF(F_ALIVE, tid)) ? ((uint32_t)TF(F_ROW, tid) << 16) | (uint32_t)TF(F_COL, tid)
                                                         : 0x80008000u;
@@ -937,7 +955,7 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
   // ballot per player; each player then selects its k-th set bit with popcounts.
   const int NW = (S + 63) >> 6;
   const bool combat = sys(c, NMMO_SYS_COMBAT);
-  if (combat || items) {
+  if (combat || items || sys(c, NMMO_SYS_NPC)) {
     // Uniform grid (kCells cells of 16x16 tiles): each player tests only the entities of the
     // <= 2x2 cells its 15x15 window touches. Bit (row-1) of the player's bitmap is set iff the
     // entity in datastore row `row` is in the realm and within L-inf 7 -- the same set an
@@ -952,7 +970,8 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
       const int pos = c.sp[s], r = pos & 255, col = (pos >> 8) & 255;
       cell = (r >> kCellShift) * kGrid + (col >> kCellShift);
       gi = atomicAdd(&c.gcnt[cell], 1);
-      gv = ((uint32_t)(TF(F_DS_ROW, s) - 1) << 16) | (uint32_t)(r << 8) | (uint32_t)col;
+      gv = ((uint32_t)(TF(F_DS_ROW, s) - 1) << 16) | (uint32_t)(r << 8) | (uint32_t)col |
+           (s < P ? 1u << 31 : 0u);
     }
     __syncthreads();
     if (tid < 64) {  // wave 0: exclusive scan over cells, two per lane; gstart[kCells] = total
@@ -969,7 +988,10 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
       if (2 * tid + 1 <= kCells) c.gstart[2 * tid + 1] = ex + a0;
     }
     __syncthreads();
-    if (cell >= 0) c.glist[c.gstart[cell] + gi] = gv;
+    if (cell >= 0) {
+      c.glist[c.gstart[cell] + gi] = gv;
+      c.gslot[c.gstart[cell] + gi] = (int16_t)s;
+    }
     __syncthreads();
     // two threads per player, one grid row of its window each; bits land with no-return LDS
     // atomics (ds_or_b32), so only the candidate loads are waited on, four at a time
@@ -981,11 +1003,16 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
       if (cr > (min(r + 7, kSize - 1) >> kCellShift)) continue;
       const int c0 = max(col - 7, 0) >> kCellShift, c1 = min(col + 7, kSize - 1) >> kCellShift;
       grid_scan(c.glist, c.gstart[cr * kGrid + c0], c.gstart[cr * kGrid + c1 + 1], r, col,
-                [&](uint32_t v, int) { atomicOr(&vis32[p * NW * 2 + (v >> 21)], 1u << ((v >> 16) & 31)); });
+                [&](uint32_t v, int, int) { atomicOr(&vis32[p * NW * 2 + ((v >> 21) & 15)], 1u << ((v >> 16) & 31)); });
     }
   }
   __syncthreads();
   NMMO_STAMP(13);
+  // bits 0-3: neighbour d passable; 4-7: neighbour d is Water; 8-15: own tile material
+  const uint32_t nbm = (impassable(m_n0) ? 0u : 1u) | (impassable(m_n1) ? 0u : 2u) |
+                       (impassable(m_n2) ? 0u : 4u) | (impassable(m_n3) ? 0u : 8u) |
+                       (m_n0 == M_WATER ? 16u : 0u) | (m_n1 == M_WATER ? 32u : 0u) |
+                       (m_n2 == M_WATER ? 64u : 0u) | (m_n3 == M_WATER ? 128u : 0u) | (m_own << 8);
   int my_move = -1, my_tgt = -1, my_sty = 0;
   int use_row = -1, destroy_row = -1, sell_row = -1, sell_price = 0;
   if (s < P) {
@@ -1040,34 +1067,22 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
   __syncthreads();
   NMMO_STAMP(12);
 #endif
-  // 1. npcs.actions. The closest-player search of hostile NPCs without a target is spread over
-  // the whole block: (NPC, player) pairs -> LDS atomicMin of (L-inf << 8 | player slot).
+  // 1. npcs.actions. A hostile NPC without a target takes the closest player within vision
+  // (ties to the lowest slot) from the players in the grid cells of its window.
   const bool npc_on = sys(c, NMMO_SYS_NPC);
-  const bool need = npc_on && s >= P && inslot && npc_validate(c, s);
   int closest = -1;
-  if (npc_on) {
-    int nneed;
-    const int npos = block_prefix_count(need, c.wtot, &nneed);  // its barriers end the decode
-    if (nneed > 0) {
-      int* best = c.ft;            // union region: the decode bitmap is dead past the barrier
-      int16_t* nlist = c.clist;
-      for (int j = tid; j < nneed; j += nt) best[j] = 0x7FFFFFFF;
-      if (need) nlist[npos] = (int16_t)s;
-      __syncthreads();
-      for (int i = tid; i < nneed * P; i += nt) {
-        const int j = (int)((unsigned)i / (unsigned)P), p = i - j * P;
-        const int v = c.sp[p];
-        if (v >= 0) {
-          const int n = nlist[j];
-          const int d = linf(TF(F_ROW, n), TF(F_COL, n), v & 255, (v >> 8) & 255);
-          if (d <= kVision) atomicMin(&best[j], (d << 8) | p);
-        }
-      }
-      __syncthreads();
-      if (need) closest = best[npos] == 0x7FFFFFFF ? -1 : (best[npos] & 255);
-    }
+  if (npc_on && s >= P && inslot && npc_validate(c, s)) {
+    const int r = TF(F_ROW, s), col = TF(F_COL, s);
+    const int c0 = max(col - kVision, 0) >> kCellShift, c1 = min(col + kVision, kSize - 1) >> kCellShift;
+    int best = 0x7FFFFFFF;
+    for (int cr = max(r - kVision, 0) >> kCellShift; cr <= (min(r + kVision, kSize - 1) >> kCellShift); cr++)
+      grid_scan(c.glist, c.gstart[cr * kGrid + c0], c.gstart[cr * kGrid + c1 + 1], r, col,
+                [&](uint32_t v, int d, int i) {
+                  if (v >> 31) best = min(best, (d << 8) | c.gslot[i]);
+                });
+    closest = best == 0x7FFFFFFF ? -1 : (best & 255);
   }
-  if (npc_on && s >= P && inslot) npc_decide(c, s, closest, my_move, my_tgt, my_sty);
+  if (npc_on && s >= P && inslot) npc_decide(c, s, closest, nbm, my_move, my_tgt, my_sty);
   if (s < S) {
     c.amove[s] = (int16_t)my_move;
     c.atgt[s] = (int16_t)my_tgt;
@@ -1108,12 +1123,11 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
         TF(F_HEALTH, s) = (int16_t)h;
         TF(F_HEALTH_RESTORE, s) = (int16_t)(h - org);
         TF(F_FOOD, s) = (int16_t)max(0, food - 5);
-        const bool drink = c.mat[tile - kSize] == M_WATER || c.mat[tile + kSize] == M_WATER ||
-                           c.mat[tile - 1] == M_WATER || c.mat[tile + 1] == M_WATER;
+        const bool drink = (nbm & 0xF0u) != 0;
         TF(F_WATER, s) = (int16_t)(drink ? 100 : max(0, water - 5));
         e_drink = drink;
       }
-      if ((resource && c.mat[tile] == M_FOILAGE) || c.prof) {
+      if ((resource && (nbm >> 8) == M_FOILAGE) || c.prof) {
         int hh = (int)(h32((uint32_t)tile) & (kHash - 1));
         while (true) {
           const int old = atomicCAS(&c.hkey[hh], -1, tile);
@@ -1128,7 +1142,7 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
   __syncthreads();
   NMMO_STAMP(3);
   const bool first_on_tile = hslot >= 0 && c.hmin[hslot] == s;
-  if (resource && first_on_tile && c.mat[tile] == M_FOILAGE) {
+  if (resource && first_on_tile && (nbm >> 8) == M_FOILAGE) {
     e_eat = true;
     TF(F_FOOD, s) = 100;
     c.mat[tile] = M_SCRUB;
@@ -1460,7 +1474,7 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
   if (inslot && c.amove[s] >= 0 && TF(F_ALIVE, s) && TF(F_HEALTH, s) > 0) {
     const int d = c.amove[s];
     const int nr = TF(F_ROW, s) + dir_dr(d), nc = TF(F_COL, s) + dir_dc(d);
-    if (!impassable(c.mat[nr * kSize + nc]) && TF(F_FREEZE, s) <= 0) {
+    if ((d == 4 || ((nbm >> d) & 1u)) && TF(F_FREEZE, s) <= 0) {  // d == 4: own tile
       TF(F_ROW, s) = (int16_t)nr;
       TF(F_COL, s) = (int16_t)nc;
       const int progress = 64 - linf(80, 80, nr, nc);
