@@ -11,10 +11,60 @@
 namespace nmmo {
 
 constexpr int kSize = NMMO_MAP_SIZE;  // 160
-// Visibility grid: 16x16-tile cells; a 15x15 window touches at most 2x2 cells.
+// Visibility grid: 16x16-tile cells; a 15x15 window touches at most kWinRows x kWinRows
+// cells. Players and NPCs are bucketed separately: grid cell ids [0, kCells) hold players,
+// [kCells, 2 kCells) NPCs, so the cells c0..c1 of one grid row are one contiguous range in
+// either half.
 constexpr int kCellShift = 4;
 constexpr int kGrid = (kSize + (1 << kCellShift) - 1) >> kCellShift;  // 10
 constexpr int kCells = kGrid * kGrid;
+constexpr int kGridCells = 2 * kCells;
+constexpr int kWinRows = (14 + (1 << kCellShift) - 1) / (1 << kCellShift) + 1;  // 2
+__host__ __device__ inline size_t grid_lds_bytes(int S) {  // gstart | glist
+  return (((size_t)(kGridCells + 1) * 4 + 15) & ~(size_t)15) + (((size_t)S * 4 + 15) & ~(size_t)15);
+}
+// first / last grid row and first / last grid column of the window around (r, c)
+__device__ __forceinline__ int4 grid_window(int r, int c) {
+  return make_int4(max(r - 7, 0) >> kCellShift, min(r + 7, kSize - 1) >> kCellShift,
+                   max(c - 7, 0) >> kCellShift, min(c + 7, kSize - 1) >> kCellShift);
+}
+
+// Counting sort of the block's entities into the grid. Every thread calls it (it holds
+// barriers) with its entity's grid cell id (or -1) and payload; blockDim.x >= 64. On return
+// gstart[cell] .. gstart[cell + 1] index cell's payloads in glist.
+__device__ __forceinline__ void grid_build(int* gstart, uint32_t* glist, int cell, uint32_t entry) {
+  const int tid = threadIdx.x, nt = blockDim.x;
+  for (int k = tid; k <= kGridCells; k += nt) gstart[k] = 0;
+  __syncthreads();
+  const int gi = cell >= 0 ? atomicAdd(&gstart[cell], 1) : 0;
+  __syncthreads();
+  if (tid < 64) {  // wave 0: in-place exclusive scan, kPer consecutive cells per lane
+    constexpr int kPer = (kGridCells + 63) / 64;
+    const int b = tid * kPer;
+    int loc[kPer], sum = 0;
+#pragma unroll
+    for (int j = 0; j < kPer; j++) {
+      loc[j] = b + j < kGridCells ? gstart[b + j] : 0;
+      sum += loc[j];
+    }
+    int x = sum;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int y = __shfl_up(x, d);
+      if (tid >= d) x += y;
+    }
+    int ex = x - sum;
+#pragma unroll
+    for (int j = 0; j < kPer; j++) {
+      if (b + j < kGridCells) gstart[b + j] = ex;
+      ex += loc[j];
+    }
+    if (tid == 63) gstart[kGridCells] = x;
+  }
+  __syncthreads();
+  if (cell >= 0) glist[gstart[cell] + gi] = entry;
+  __syncthreads();
+}
 
 // Visit the grid entries glist[i0, i1) (bits 0-7 column, 8-15 row) within L-inf 7 of (r, c):
 // f(entry, L-inf distance, index). Loads are issued four at a time ahead of their uses.

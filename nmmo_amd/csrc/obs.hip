@@ -210,8 +210,8 @@ __host__ __device__ inline int policy_threads(int S, int P) {
 }
 __host__ __device__ inline size_t policy_lds_bytes(int S, int P) {
   const int NW = (S + 63) / 64;
-  return (size_t)3 * P * NW * 8 + (size_t)((P + 3) & ~3) * 4 + (size_t)NMMO_MARKET_ROWS * 12 +
-         (size_t)(2 * kCells + 2) * 4 + (size_t)S * 4;
+  const size_t b = (size_t)3 * P * NW * 8 + (size_t)((P + 3) & ~3) * 4 + (size_t)NMMO_MARKET_ROWS * 12;
+  return ((b + 15) & ~(size_t)15) + grid_lds_bytes(S);
 }
 
 __global__ void __launch_bounds__(512) policy_kernel(PolicyParams p) {
@@ -224,9 +224,10 @@ __global__ void __launch_bounds__(512) policy_kernel(PolicyParams p) {
   uint32_t* ppos = reinterpret_cast<uint32_t*>(samm + P * NW);  // [P] r<<16 | c, or sentinel
   uint2* mitem = reinterpret_cast<uint2*>(ppos + ((P + 3) & ~3));
   int* mown = reinterpret_cast<int*>(mitem + NMMO_MARKET_ROWS);
-  int* gstart = mown + NMMO_MARKET_ROWS;  // [kCells+1] grid cell -> first glist index
-  int* gcnt = gstart + kCells + 1;        // [kCells+1]
-  uint32_t* glist = reinterpret_cast<uint32_t*>(gcnt + kCells + 1);  // [S]
+  // grid (common.h; grid_lds_bytes): cell -> first entry, entries
+  unsigned char* gb = smem + ((reinterpret_cast<unsigned char*>(mown + NMMO_MARKET_ROWS) - smem + 15) & ~15);
+  int* gstart = reinterpret_cast<int*>(gb);
+  uint32_t* glist = reinterpret_cast<uint32_t*>(gb + (((kGridCells + 1) * 4 + 15) & ~15));
   const int16_t* E = p.ent + (size_t)e * NMMO_NF * S;
   const bool combat = (p.systems & NMMO_SYS_COMBAT) != 0;
   const bool item = (p.systems & NMMO_SYS_ITEM) != 0;
@@ -244,56 +245,43 @@ __global__ void __launch_bounds__(512) policy_kernel(PolicyParams p) {
   if (tgt_any) {
     uint32_t* m32 = reinterpret_cast<uint32_t*>(vism);  // vism | atkm | samm, contiguous
     for (int k = tid; k < 6 * P * NW; k += blockDim.x) m32[k] = 0;
-    for (int k = tid; k < kCells; k += blockDim.x) gcnt[k] = 0;
-  }
-  __syncthreads();
-  if (tgt_any) {
-    // grid entry: (ds_row-1)<<16 | r<<8 | c, bit 30 = not spawn-immune, bit 31 = player
-    int cell = -1, gi = 0;
+    // grid entry: (ds_row-1)<<16 | r<<8 | c, bit 30 = not spawn-immune (players)
+    int cell = -1;
     uint32_t gv = 0;
     if (tid < S && E[F_ALIVE * S + tid]) {  // policy_threads >= S
       const int r = E[F_ROW * S + tid], c = E[F_COL * S + tid];
       const bool pl = tid < P, immune = pl && E[F_TIME_ALIVE * S + tid] < p.spawn_immunity;
-      cell = (r >> kCellShift) * kGrid + (c >> kCellShift);
-      gi = atomicAdd(&gcnt[cell], 1);
+      cell = (pl ? 0 : kCells) + (r >> kCellShift) * kGrid + (c >> kCellShift);
       gv = ((uint32_t)(E[F_DS_ROW * S + tid] - 1) << 16) | (uint32_t)(r << 8) | (uint32_t)c |
-           (immune ? 0u : 1u << 30) | (pl ? 1u << 31 : 0u);
+           (immune ? 0u : 1u << 30);
     }
-    __syncthreads();
-    if (tid < 64) {  // wave 0: exclusive scan over cells, two per lane; gstart[kCells] = total
-      const int a0 = 2 * tid < kCells ? gcnt[2 * tid] : 0;
-      const int a1 = 2 * tid + 1 < kCells ? gcnt[2 * tid + 1] : 0;
-      int x = a0 + a1;
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const int y = __shfl_up(x, d);
-        if (tid >= d) x += y;
-      }
-      const int ex = x - a0 - a1;
-      if (2 * tid <= kCells) gstart[2 * tid] = ex;
-      if (2 * tid + 1 <= kCells) gstart[2 * tid + 1] = ex + a0;
-    }
-    __syncthreads();
-    if (cell >= 0) glist[gstart[cell] + gi] = gv;
-    __syncthreads();
-    // two threads per player, one grid row of its window each; no-return LDS atomics
-    for (int t = tid; t < 2 * P; t += blockDim.x) {
-      const int a = t >> 1;
+    grid_build(gstart, glist, cell, gv);  // its barriers also cover ppos and m32
+    // kWinRows threads per player, one grid row of its window each; no-return LDS atomics
+    for (int t = tid; t < kWinRows * P; t += blockDim.x) {
+      const int a = t / kWinRows;
       if (ppos[a] == 0x80008000u) continue;
       const int r = (int)(ppos[a] >> 16), c = (int)(ppos[a] & 0xFFFF);
-      const int cr = (max(r - 7, 0) >> kCellShift) + (t & 1);
-      if (cr > (min(r + 7, kSize - 1) >> kCellShift)) continue;
-      const int c0 = max(c - 7, 0) >> kCellShift, c1 = min(c + 7, kSize - 1) >> kCellShift;
+      const int4 wdw = grid_window(r, c);
+      const int cr = wdw.x + (t - kWinRows * a);
+      if (cr > wdw.y) continue;
       uint32_t* mv = reinterpret_cast<uint32_t*>(vism + a * NW);
       uint32_t* ma = reinterpret_cast<uint32_t*>(atkm + a * NW);
       uint32_t* ms = reinterpret_cast<uint32_t*>(samm + a * NW);
-      grid_scan(glist, gstart[cr * kGrid + c0], gstart[cr * kGrid + c1 + 1], r, c, [&](uint32_t v, int d, int) {
-        const int wi = (v >> 21) & 15;
+      const int g = cr * kGrid;
+      grid_scan(glist, gstart[g + wdw.z], gstart[g + wdw.w + 1], r, c, [&](uint32_t v, int d, int) {
+        const int wi = (v >> 21) & 15;  // players: visible, attackable unless immune, same tile
         const uint32_t bit = 1u << ((v >> 16) & 31);
         atomicOr(&mv[wi], bit);
         if (d <= 3 && (v & (1u << 30))) atomicOr(&ma[wi], bit);
-        if (d == 0 && (v >> 31)) atomicOr(&ms[wi], bit);
+        if (d == 0) atomicOr(&ms[wi], bit);
       });
+      grid_scan(glist, gstart[kCells + g + wdw.z], gstart[kCells + g + wdw.w + 1], r, c,
+                [&](uint32_t v, int d, int) {  // NPCs: visible, attackable
+                  const int wi = (v >> 21) & 15;
+                  const uint32_t bit = 1u << ((v >> 16) & 31);
+                  atomicOr(&mv[wi], bit);
+                  if (d <= 3) atomicOr(&ma[wi], bit);
+                });
     }
   }
   __syncthreads();

@@ -29,12 +29,9 @@ namespace nmmo {
 struct Ctx {
   int16_t* T;        // [kNFLive][S]
   uint64_t* vism;    // [P][NW] visibility bitmap: bit j of word w = row 64w+j+1 visible to player
-  int* gstart;       // [kCells+1] grid cell -> first glist index (after vism, union region)
-  int* gcnt;         // [kCells] grid cell population
-  uint32_t* glist;   // [S] in-realm entities by cell: player<<31 | (ds_row-1)<<16 | r<<8 | c
-  int16_t* gslot;    // [S] slot of each glist entry
-  int* rp;           // [S+1] datastore row -> r | c<<8 | slot<<16 (-1 = no entity)
-  int* sp;           // [S] slot -> r | c<<8 while in the realm with health > 0 (-1 otherwise)
+  int* gstart;       // [kGridCells+1] grid cell -> first glist index (after vism, union region)
+  uint32_t* glist;   // [S] in-realm entities by cell: slot<<25 (players) | (ds_row-1)<<16 | r<<8 | c
+  int16_t* rslot;    // [S+1] datastore row -> slot (set for the rows of in-realm entities)
   uint32_t* pp;      // [128] player -> r<<16 | c (0x80008000 when not in the realm): window tests
   int* hkey;         // [kHash] Foilage-tile hash: tile index (-1 = empty)
   int* hmin;         // [kHash] lowest player slot standing on that tile
@@ -72,7 +69,8 @@ struct Ctx {
   // tasks (SPEC §12)
   const NmmoTask* tasks;   // global task table
   const int32_t* assign;   // global [P] task index of this env's players
-  NmmoTaskState* ts;       // LDS [P] task state of this env's players (loaded/stored with the state)
+  NmmoTaskState* ts;    // [P] task state: == tsl when staged (task events on), else in HBM
+  NmmoTaskState* tsl;   // LDS staging of ts (meaningful only when tev)
   int4* tdesc;             // LDS [128][2] (pred, a, b, c) of each player's terms (when tev)
   bool tev;
   int evcap, tick1;  // ring rows (0 = no event log); tick + 1 (the events' tick column)
@@ -115,23 +113,25 @@ __host__ __device__ inline size_t item_lds_bytes(int P) {
 constexpr size_t kPlayerArrBytes = 4 * 256 + 128;  // kill, order, ev_dmg, ev_lvl, fired
 // One LDS region, three lifetimes: the decode bitmap (phase 0; reused as the respawn group list
 // in phase 6), the position hash (update/harvest) and the attack first-touch arrays.
-__host__ __device__ inline size_t union_lds_bytes(int S) {
+__host__ __device__ inline bool uses_grid(uint32_t systems) {
+  return (systems & (NMMO_SYS_COMBAT | NMMO_SYS_ITEM | NMMO_SYS_NPC)) != 0;
+}
+__host__ __device__ inline size_t union_lds_bytes(int S, bool grid) {
   auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
-  size_t u = (size_t)128 * ((S + 63) / 64) * 8 + 2 * al((kCells + 1) * 4) + al((size_t)S * 4) +
-             al((size_t)S * 2);
+  size_t u = (size_t)128 * ((S + 63) / 64) * 8 + (grid ? grid_lds_bytes(S) : 0);
   u = u > 2 * kHash * 4 ? u : 2 * kHash * 4;
   const size_t atk = al((size_t)S * 4) + al((size_t)S * 2);
   return u > atk ? u : atk;
 }
 
-__host__ __device__ inline size_t tick_lds_bytes(int S, int P, bool items, bool tev) {
+__host__ __device__ inline size_t tick_lds_bytes(int S, int P, bool items, bool tev, bool grid) {
   auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
-  size_t b = (items ? item_lds_bytes(P) : 0) + kPlayerArrBytes + (tev ? 128 * 2 * 16 : 0) +
-             al((size_t)P * sizeof(NmmoTaskState));
+  // task state is staged in LDS only when events feed its accumulators (else read in place)
+  size_t b = (items ? item_lds_bytes(P) : 0) + kPlayerArrBytes +
+             (tev ? 128 * 2 * 16 + al((size_t)P * sizeof(NmmoTaskState)) : 0);
   b += al((size_t)kNFLive * S * 2);  // T
-  b += union_lds_bytes(S);           // vism | hkey,hmin | ft,clist
-  b += (size_t)rp_groups(S) * 16;    // rp
-  b += al((size_t)S * 4);            // sp
+  b += union_lds_bytes(S, grid);     // vism + grid | hkey,hmin | ft,clist
+  b += al((size_t)(S + 1) * 2);      // rslot
   b += 128 * 4;                      // pp
   b += 3 * al((size_t)S * 2);        // amove atgt asty
   b += al((size_t)S * 2);            // ring
@@ -173,10 +173,13 @@ __device__ __forceinline__ Ctx make_ctx(unsigned char* smem, const DevState& st,
   c.tev = st.tev != 0;
   c.tasks = st.tasks;
   c.assign = st.assign + (size_t)e * st.P;
-  c.ts = reinterpret_cast<NmmoTaskState*>(smem + o); o += al((size_t)st.P * sizeof(NmmoTaskState));
+  c.tsl = reinterpret_cast<NmmoTaskState*>(smem + o);  // an LDS address either way (copy_segs)
   if (c.tev) {
+    c.ts = c.tsl;
+    o += al((size_t)st.P * sizeof(NmmoTaskState));
     c.tdesc = reinterpret_cast<int4*>(smem + o); o += 128 * 2 * 16;
   } else {
+    c.ts = st.tstate + (size_t)e * st.P;  // HBM, touched once per player at the rewards
     c.tdesc = nullptr;
   }
   c.kill = reinterpret_cast<int16_t*>(smem + o); o += 256;
@@ -188,21 +191,18 @@ __device__ __forceinline__ Ctx make_ctx(unsigned char* smem, const DevState& st,
   {  // the union region (see union_lds_bytes)
     unsigned char* u = smem + o;
     c.vism = reinterpret_cast<uint64_t*>(u);
-    {
+    {  // grid_lds_bytes
       const size_t vb = (size_t)128 * ((S + 63) / 64) * 8;
       c.gstart = reinterpret_cast<int*>(u + vb);
-      c.gcnt = reinterpret_cast<int*>(u + vb + al((kCells + 1) * 4));
-      c.glist = reinterpret_cast<uint32_t*>(u + vb + 2 * al((kCells + 1) * 4));
-      c.gslot = reinterpret_cast<int16_t*>(u + vb + 2 * al((kCells + 1) * 4) + al((size_t)S * 4));
+      c.glist = reinterpret_cast<uint32_t*>(u + vb + al((size_t)(kGridCells + 1) * 4));
     }
     c.hkey = reinterpret_cast<int*>(u);
     c.hmin = reinterpret_cast<int*>(u + kHash * 4);
     c.ft = reinterpret_cast<int*>(u);
     c.clist = reinterpret_cast<int16_t*>(u + al((size_t)S * 4));
-    o += union_lds_bytes(S);
+    o += union_lds_bytes(S, uses_grid(sy));
   }
-  c.rp = reinterpret_cast<int*>(smem + o); o += (size_t)rp_groups(S) * 16;
-  c.sp = reinterpret_cast<int*>(smem + o); o += al((size_t)S * 4);
+  c.rslot = reinterpret_cast<int16_t*>(smem + o); o += al((size_t)(S + 1) * 2);
   c.pp = reinterpret_cast<uint32_t*>(smem + o); o += 128 * 4;
   c.amove = reinterpret_cast<int16_t*>(smem + o); o += al((size_t)S * 2);
   c.atgt = reinterpret_cast<int16_t*>(smem + o); o += al((size_t)S * 2);
@@ -290,13 +290,13 @@ __device__ __forceinline__ void load_env(Ctx& c, const DevState& st, int e) {
          c.items ? c.P * kInv / 2 : 0},
         {reinterpret_cast<uint4*>(c.iring), reinterpret_cast<const uint4*>(st.iring + (size_t)e * c.IC),
          c.items ? c.IC / 8 : 0},
-        {reinterpret_cast<uint4*>(c.ts), reinterpret_cast<const uint4*>(tsg),
-         c.P * (int)sizeof(NmmoTaskState) / 16}};
+        {reinterpret_cast<uint4*>(c.tsl), reinterpret_cast<const uint4*>(tsg),
+         c.tev ? c.P * (int)sizeof(NmmoTaskState) / 16 : 0}};
     copy_segs(sg, tid, nt);
     return;
   }
-  for (int i = tid; i < c.P * (int)sizeof(NmmoTaskState) / 4; i += nt)
-    reinterpret_cast<int*>(c.ts)[i] = reinterpret_cast<const int*>(tsg)[i];
+  for (int i = tid; i < (c.tev ? c.P * (int)sizeof(NmmoTaskState) / 4 : 0); i += nt)
+    reinterpret_cast<int*>(c.tsl)[i] = reinterpret_cast<const int*>(tsg)[i];
   for (int i = tid; i < n16; i += nt) c.T[i] = src[i];
   for (int i = tid; i < S; i += nt) c.ring[i] = st.ring[(size_t)e * S + i];
   for (int i = tid; i < kBitmapWords; i += nt) c.dep[i] = st.dep[(size_t)e * kBitmapWords + i];
@@ -328,9 +328,9 @@ __device__ __forceinline__ void store_env(const Ctx& c, const DevState& st, int 
     for (int i = tid; i < c.P * kInv / 2; i += nt) d4[i] = s4[i];
     for (int i = tid; i < c.IC; i += nt) st.iring[(size_t)e * c.IC + i] = c.iring[i];
   }
-  {  // task state (SPEC §12)
+  if (c.tev) {  // task state (SPEC §12), when staged
     int* dsti = reinterpret_cast<int*>(st.tstate + (size_t)e * c.P);
-    const int* srci = reinterpret_cast<const int*>(c.ts);
+    const int* srci = reinterpret_cast<const int*>(c.tsl);
     for (int i = tid; i < c.P * (int)sizeof(NmmoTaskState) / 4; i += nt) dsti[i] = srci[i];
   }
 }
@@ -460,7 +460,7 @@ __device__ __forceinline__ void task_accumulate(const Ctx& c, int p, int code, i
 #pragma unroll
   for (int k = 0; k < 2; k++) {
     const int4 q = c.tdesc[p * 2 + k];  // pred, a, b, c
-    int* acc = c.ts[p].acc + 2 * k;
+    int* acc = c.tsl[p].acc + 2 * k;  // called only when tev (staged)
     int add0 = 0, add1 = 0;
     switch (q.x) {
       case PRED_COUNT_EVENT: add0 = code == q.y; break;
@@ -873,7 +873,7 @@ __device__ __forceinline__ int vis_kth(const Ctx& c, int s, int NW, int k) {
     const int pc = __popcll(m);
     if (k < pc) {
       for (int i = 0; i < k; i++) m &= m - 1;  // clear the k lowest set bits
-      return (c.rp[(w << 6) + __builtin_ctzll(m) + 1] >> 16) & 511;
+      return c.rslot[(w << 6) + __builtin_ctzll(m) + 1];
     }
     k -= pc;
   }
@@ -904,7 +904,6 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
   int evn = c.E[E_EVENT_COUNT];  // block-uniform running event count (SPEC §11)
 
   if (s < P) c.pres[s] = (uint8_t)TF(F_ALIVE, s);
-  for (int k = tid; k < rp_groups(S) * 4; k += nt) c.rp[k] = -1;
   if (c.exch && tid < kLWords) c.lbits[tid] = 0;
   if (c.tev && s < P) {  // this player's task terms and event accumulators
     const NmmoTask& tk = c.tasks[c.assign[s]];
@@ -918,13 +917,12 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
   // entity moves before the move phase, so these stay exact for NPC steering, drinking,
   // foilage eating (the own tile is read before any harvest) and the move check.
   uint32_t m_own = 0, m_n0 = 0, m_n1 = 0, m_n2 = 0, m_n3 = 0;
-  if (s < S) {
-    const bool in = inslot && TF(F_ALIVE, s);  // in the realm => health > 0 at tick start
-    const int pos = TF(F_ROW, s) | (TF(F_COL, s) << 8);
-    c.sp[s] = in ? pos : -1;
-    if (in) {
-      c.rp[TF(F_DS_ROW, s)] = pos | (s << 16);
-      const uint8_t* m = c.mat + TF(F_ROW, s) * kSize + TF(F_COL, s);
+  const bool in_realm = s < S && inslot && TF(F_ALIVE, s);  // => health > 0 at tick start
+  const int pos_r = s < S ? TF(F_ROW, s) : 0, pos_c = s < S ? TF(F_COL, s) : 0;
+  {
+    if (in_realm) {
+      c.rslot[TF(F_DS_ROW, s)] = (int16_t)s;
+      const uint8_t* m = c.mat + pos_r * kSize + pos_c;
       m_own = m[0];
       m_n0 = m[-kSize];
       m_n1 = m[kSize];
@@ -955,55 +953,37 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
   // ballot per player; each player then selects its k-th set bit with popcounts.
   const int NW = (S + 63) >> 6;
   const bool combat = sys(c, NMMO_SYS_COMBAT);
-  if (combat || items || sys(c, NMMO_SYS_NPC)) {
-    // Uniform grid (kCells cells of 16x16 tiles): each player tests only the entities of the
-    // <= 2x2 cells its 15x15 window touches. Bit (row-1) of the player's bitmap is set iff the
-    // entity in datastore row `row` is in the realm and within L-inf 7 -- the same set an
-    // all-pairs test gives, at ~1/16 of the pair tests on a 128-player realm.
+  if (uses_grid(c.cfg->systems)) {
+    // Uniform grid (common.h): each player tests only the entities of the <= 3x3 cells its
+    // 15x15 window touches. Bit (row-1) of the player's bitmap is set iff the entity in
+    // datastore row `row` is in the realm and within L-inf 7 -- the same set an all-pairs test
+    // gives, at a small fraction of the pair tests.
     uint32_t* vis32 = reinterpret_cast<uint32_t*>(c.vism);
     for (int k = tid; k < P * NW * 2; k += nt) vis32[k] = 0;
-    for (int k = tid; k < kCells; k += nt) c.gcnt[k] = 0;
-    __syncthreads();
-    int cell = -1, gi = 0;
+    int cell = -1;
     uint32_t gv = 0;
-    if (s < S && c.sp[s] >= 0) {
-      const int pos = c.sp[s], r = pos & 255, col = (pos >> 8) & 255;
-      cell = (r >> kCellShift) * kGrid + (col >> kCellShift);
-      gi = atomicAdd(&c.gcnt[cell], 1);
-      gv = ((uint32_t)(TF(F_DS_ROW, s) - 1) << 16) | (uint32_t)(r << 8) | (uint32_t)col |
-           (s < P ? 1u << 31 : 0u);
+    if (in_realm) {  // players: slot in bits 25-31 (P <= 128)
+      cell = (s < P ? 0 : kCells) + (pos_r >> kCellShift) * kGrid + (pos_c >> kCellShift);
+      gv = ((uint32_t)(TF(F_DS_ROW, s) - 1) << 16) | (uint32_t)(pos_r << 8) | (uint32_t)pos_c |
+           (s < P ? (uint32_t)s << 25 : 0u);
     }
-    __syncthreads();
-    if (tid < 64) {  // wave 0: exclusive scan over cells, two per lane; gstart[kCells] = total
-      const int a0 = 2 * tid < kCells ? c.gcnt[2 * tid] : 0;
-      const int a1 = 2 * tid + 1 < kCells ? c.gcnt[2 * tid + 1] : 0;
-      int x = a0 + a1;
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const int y = __shfl_up(x, d);
-        if (tid >= d) x += y;
-      }
-      const int ex = x - a0 - a1;
-      if (2 * tid <= kCells) c.gstart[2 * tid] = ex;
-      if (2 * tid + 1 <= kCells) c.gstart[2 * tid + 1] = ex + a0;
-    }
-    __syncthreads();
-    if (cell >= 0) {
-      c.glist[c.gstart[cell] + gi] = gv;
-      c.gslot[c.gstart[cell] + gi] = (int16_t)s;
-    }
-    __syncthreads();
-    // two threads per player, one grid row of its window each; bits land with no-return LDS
-    // atomics (ds_or_b32), so only the candidate loads are waited on, four at a time
-    for (int t = tid; t < 2 * P; t += nt) {
-      const int p = t >> 1;
+    grid_build(c.gstart, c.glist, cell, gv);
+    // kWinRows threads per player, one grid row of its window each; bits land with no-return
+    // LDS atomics (ds_or_b32), so only the candidate loads are waited on, four at a time
+    for (int t = tid; t < kWinRows * P; t += nt) {
+      const int p = t / kWinRows;
       if (!c.pres[p]) continue;
       const int r = (int)(c.pp[p] >> 16), col = (int)(c.pp[p] & 0xFFFF);
-      const int cr = (max(r - 7, 0) >> kCellShift) + (t & 1);
-      if (cr > (min(r + 7, kSize - 1) >> kCellShift)) continue;
-      const int c0 = max(col - 7, 0) >> kCellShift, c1 = min(col + 7, kSize - 1) >> kCellShift;
-      grid_scan(c.glist, c.gstart[cr * kGrid + c0], c.gstart[cr * kGrid + c1 + 1], r, col,
-                [&](uint32_t v, int, int) { atomicOr(&vis32[p * NW * 2 + ((v >> 21) & 15)], 1u << ((v >> 16) & 31)); });
+      const int4 wdw = grid_window(r, col);
+      const int cr = wdw.x + (t - kWinRows * p);
+      if (cr > wdw.y) continue;
+      uint32_t* mine = vis32 + p * NW * 2;
+      auto setbit = [&](uint32_t v, int, int) {
+        atomicOr(&mine[(v >> 21) & 15], 1u << ((v >> 16) & 31));
+      };
+      const int g = cr * kGrid;
+      grid_scan(c.glist, c.gstart[g + wdw.z], c.gstart[g + wdw.w + 1], r, col, setbit);
+      grid_scan(c.glist, c.gstart[kCells + g + wdw.z], c.gstart[kCells + g + wdw.w + 1], r, col, setbit);
     }
   }
   __syncthreads();
@@ -1073,13 +1053,11 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
   int closest = -1;
   if (npc_on && s >= P && inslot && npc_validate(c, s)) {
     const int r = TF(F_ROW, s), col = TF(F_COL, s);
-    const int c0 = max(col - kVision, 0) >> kCellShift, c1 = min(col + kVision, kSize - 1) >> kCellShift;
+    const int4 wdw = grid_window(r, col);
     int best = 0x7FFFFFFF;
-    for (int cr = max(r - kVision, 0) >> kCellShift; cr <= (min(r + kVision, kSize - 1) >> kCellShift); cr++)
-      grid_scan(c.glist, c.gstart[cr * kGrid + c0], c.gstart[cr * kGrid + c1 + 1], r, col,
-                [&](uint32_t v, int d, int i) {
-                  if (v >> 31) best = min(best, (d << 8) | c.gslot[i]);
-                });
+    for (int cr = wdw.x; cr <= wdw.y; cr++)  // player cells only
+      grid_scan(c.glist, c.gstart[cr * kGrid + wdw.z], c.gstart[cr * kGrid + wdw.w + 1], r, col,
+                [&](uint32_t v, int d, int) { best = min(best, (d << 8) | (int)(v >> 25)); });
     closest = best == 0x7FFFFFFF ? -1 : (best & 255);
   }
   if (npc_on && s >= P && inslot) npc_decide(c, s, closest, nbm, my_move, my_tgt, my_sty);
@@ -1663,12 +1641,13 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
     if (c.pres[s] && c.died[s]) {
       rw = -1.f;
     } else if (c.pres[s]) {
-      NmmoTaskState& ts = c.ts[s];
+      NmmoTaskState ts = c.ts[s];  // LDS when staged, else this env's HBM copy
       const double np = task_progress(c, s, ts.acc), d = np - ts.last;
       ts.last = np;
       if (np > ts.max_progress) ts.max_progress = np;
       if (d > 0.0) ts.signals += 1;
       if (np >= 1.0 && ts.completed_tick == 0) ts.completed_tick = tick + 1;
+      c.ts[s] = ts;
       rw = (float)d;
     }
     rew[s] = rw;
@@ -1767,7 +1746,8 @@ hipError_t launch_tick(const DevState& st, const int32_t* actions, const uint64_
                        float* rew, uint8_t* term, uint8_t* trunc, uint8_t* mask, int mode,
                        hipStream_t stream) {
   const int threads = ((st.S + 63) / 64) * 64;
-  const size_t lds = tick_lds_bytes(st.S, st.P, (st.cfg.systems & NMMO_SYS_ITEM) != 0, st.tev != 0);
+  const size_t lds = tick_lds_bytes(st.S, st.P, (st.cfg.systems & NMMO_SYS_ITEM) != 0, st.tev != 0,
+                                    uses_grid(st.cfg.systems));
   hipLaunchKernelGGL(tick_kernel, dim3(st.n_envs), dim3(threads), lds, stream,
                      st, actions, env_seeds, rew, term, trunc, mask, mode);
   return hipGetLastError();
