@@ -11,80 +11,6 @@
 namespace nmmo {
 
 constexpr int kSize = NMMO_MAP_SIZE;  // 160
-// Visibility grid: 16x16-tile cells; a 15x15 window touches at most kWinRows x kWinRows
-// cells. Players and NPCs are bucketed separately: grid cell ids [0, kCells) hold players,
-// [kCells, 2 kCells) NPCs, so the cells c0..c1 of one grid row are one contiguous range in
-// either half.
-constexpr int kCellShift = 4;
-constexpr int kGrid = (kSize + (1 << kCellShift) - 1) >> kCellShift;  // 10
-constexpr int kCells = kGrid * kGrid;
-constexpr int kGridCells = 2 * kCells;
-constexpr int kWinRows = (14 + (1 << kCellShift) - 1) / (1 << kCellShift) + 1;  // 2
-__host__ __device__ inline size_t grid_lds_bytes(int S) {  // gstart | glist
-  return (((size_t)(kGridCells + 1) * 4 + 15) & ~(size_t)15) + (((size_t)S * 4 + 15) & ~(size_t)15);
-}
-// first / last grid row and first / last grid column of the window around (r, c)
-__device__ __forceinline__ int4 grid_window(int r, int c) {
-  return make_int4(max(r - 7, 0) >> kCellShift, min(r + 7, kSize - 1) >> kCellShift,
-                   max(c - 7, 0) >> kCellShift, min(c + 7, kSize - 1) >> kCellShift);
-}
-
-// Counting sort of the block's entities into the grid. Every thread calls it (it holds
-// barriers) with its entity's grid cell id (or -1) and payload; blockDim.x >= 64. On return
-// gstart[cell] .. gstart[cell + 1] index cell's payloads in glist.
-__device__ __forceinline__ void grid_build(int* gstart, uint32_t* glist, int cell, uint32_t entry) {
-  const int tid = threadIdx.x, nt = blockDim.x;
-  for (int k = tid; k <= kGridCells; k += nt) gstart[k] = 0;
-  __syncthreads();
-  const int gi = cell >= 0 ? atomicAdd(&gstart[cell], 1) : 0;
-  __syncthreads();
-  if (tid < 64) {  // wave 0: in-place exclusive scan, kPer consecutive cells per lane
-    constexpr int kPer = (kGridCells + 63) / 64;
-    const int b = tid * kPer;
-    int loc[kPer], sum = 0;
-#pragma unroll
-    for (int j = 0; j < kPer; j++) {
-      loc[j] = b + j < kGridCells ? gstart[b + j] : 0;
-      sum += loc[j];
-    }
-    int x = sum;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const int y = __shfl_up(x, d);
-      if (tid >= d) x += y;
-    }
-    int ex = x - sum;
-#pragma unroll
-    for (int j = 0; j < kPer; j++) {
-      if (b + j < kGridCells) gstart[b + j] = ex;
-      ex += loc[j];
-    }
-    if (tid == 63) gstart[kGridCells] = x;
-  }
-  __syncthreads();
-  if (cell >= 0) glist[gstart[cell] + gi] = entry;
-  __syncthreads();
-}
-
-// Visit the grid entries glist[i0, i1) (bits 0-7 column, 8-15 row) within L-inf 7 of (r, c):
-// f(entry, L-inf distance, index). Loads are issued four at a time ahead of their uses.
-template <class Fn>
-__device__ __forceinline__ void grid_scan(const uint32_t* __restrict__ glist, int i0, int i1, int r,
-                                          int c, Fn&& f) {
-  auto one = [&](uint32_t v, int i) {
-    const int d = max(abs((int)((v >> 8) & 255) - r), abs((int)(v & 255) - c));
-    if (d <= 7) f(v, d, i);
-  };
-  int i = i0;
-  for (; i + 4 <= i1; i += 4) {
-    const uint32_t v0 = glist[i], v1 = glist[i + 1], v2 = glist[i + 2], v3 = glist[i + 3];
-    one(v0, i);
-    one(v1, i + 1);
-    one(v2, i + 2);
-    one(v3, i + 3);
-  }
-  for (; i < i1; i++) one(glist[i], i);
-}
 constexpr int kTiles = NMMO_MAP_TILES;
 constexpr int kLo = 16, kHi = 143, kCenter = 128, kVision = 7, kNObs = 100;
 constexpr int kBitmapWords = kTiles / 32;  // 800 depleted-tile bitmap words per env
@@ -222,6 +148,19 @@ __device__ inline int lane_id() { return threadIdx.x & 63; }
 __device__ inline int wave_id() { return threadIdx.x >> 6; }
 __device__ inline uint64_t lanes_below() { return (1ull << lane_id()) - 1ull; }
 
+// Inclusive prefix sum over the 64 lanes of a wave in six DPP moves: row_shr 1/2/4/8 scan each
+// 16-lane row, then row_bcast:15 and row_bcast:31 carry row totals into the rows above
+// (disabled rows and out-of-row sources read the `old` operand, 0).
+__device__ __forceinline__ int wave_incl_scan(int x) {
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, false);  // row_shr:1
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xF, 0xF, false);  // row_shr:2
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, false);  // row_shr:4
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xF, false);  // row_shr:8
+  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
+  return x;
+}
+
 __device__ inline bool item_usable(const int16_t* T, int S, int p, uint2 w) {
   if (it_price(w)) return false;
   if (equip_slot(it_type(w)) >= 0 && it_equipped(w)) return true;
@@ -288,16 +227,14 @@ __device__ inline uint32_t writelane_u32(uint32_t old, uint32_t val, uint32_t la
   return lane_id() == (int)lane ? val : old;
 }
 
-// Block-wide exclusive prefix sum of an int in thread order (<= 16 waves); *total gets the sum.
+// Block-wide exclusive prefix sum of an int in thread order (<= 8 waves); *total gets the sum.
+// One barrier: `wave_tot` (>= 8 ints of LDS) must not be the buffer of the previous call (it
+// may still be read), so consecutive calls alternate two buffers. All accesses before the call
+// are ordered before all accesses after it by that barrier.
 __device__ inline int block_prefix_sum(int v, int* wave_tot, int* total) {
-  const int lane = lane_id(), w = wave_id(), nw = (blockDim.x + 63) >> 6;
-  int x = v;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const int y = __shfl_up(x, d);
-    if (lane >= d) x += y;
-  }
-  if (lane == 63) wave_tot[w] = x;
+  const int w = wave_id(), nw = (blockDim.x + 63) >> 6;
+  const int x = wave_incl_scan(v);
+  if (lane_id() == 63) wave_tot[w] = x;
   __syncthreads();
   int base = 0, sum = 0;
   for (int i = 0; i < nw; i++) {
@@ -305,13 +242,12 @@ __device__ inline int block_prefix_sum(int v, int* wave_tot, int* total) {
     base += i < w ? t : 0;
     sum += t;
   }
-  __syncthreads();
   *total = sum;
   return base + x - v;
 }
 
-// Block-wide exclusive prefix count of a 0/1 predicate in thread order (<= 16 waves).
-// `wave_tot` is LDS scratch of >= 17 ints. Returns the exclusive count; *total gets the sum.
+// Block-wide exclusive prefix count of a 0/1 predicate in thread order (<= 8 waves); same
+// buffer rule as block_prefix_sum. Returns the exclusive count; *total gets the sum.
 __device__ inline int block_prefix_count(bool pred, int* wave_tot, int* total) {
   const uint64_t b = __ballot(pred);
   const int w = wave_id(), nw = (blockDim.x + 63) >> 6;
@@ -323,9 +259,79 @@ __device__ inline int block_prefix_count(bool pred, int* wave_tot, int* total) {
     base += i < w ? v : 0;
     sum += v;
   }
-  __syncthreads();
   *total = sum;
   return base + __popcll(b & lanes_below());
+}
+
+// ---------------------------------------------------------------- visibility grid
+// Visibility grid: 16x16-tile cells; a 15x15 window touches at most kWinRows x kWinRows
+// cells. Players and NPCs are bucketed separately: grid cell ids [0, kCells) hold players,
+// [kCells, 2 kCells) NPCs, so the cells c0..c1 of one grid row are one contiguous range in
+// either half.
+constexpr int kCellShift = 4;
+constexpr int kGrid = (kSize + (1 << kCellShift) - 1) >> kCellShift;  // 10
+constexpr int kCells = kGrid * kGrid;
+constexpr int kGridCells = 2 * kCells;
+constexpr int kWinRows = (14 + (1 << kCellShift) - 1) / (1 << kCellShift) + 1;  // 2
+__host__ __device__ inline size_t grid_lds_bytes(int S) {  // gstart | glist
+  return (((size_t)(kGridCells + 1) * 4 + 15) & ~(size_t)15) + (((size_t)S * 4 + 15) & ~(size_t)15);
+}
+// first / last grid row and first / last grid column of the window around (r, c)
+__device__ __forceinline__ int4 grid_window(int r, int c) {
+  return make_int4(max(r - 7, 0) >> kCellShift, min(r + 7, kSize - 1) >> kCellShift,
+                   max(c - 7, 0) >> kCellShift, min(c + 7, kSize - 1) >> kCellShift);
+}
+
+// Counting sort of the block's entities into the grid. Every thread calls it (it holds
+// barriers) with its entity's grid cell id (or -1) and payload; blockDim.x >= 64. On return
+// gstart[cell] .. gstart[cell + 1] index cell's payloads in glist.
+__device__ __forceinline__ void grid_build(int* gstart, uint32_t* glist, int cell, uint32_t entry) {
+  const int tid = threadIdx.x, nt = blockDim.x;
+  for (int k = tid; k <= kGridCells; k += nt) gstart[k] = 0;
+  __syncthreads();
+  const int gi = cell >= 0 ? atomicAdd(&gstart[cell], 1) : 0;
+  __syncthreads();
+  if (tid < 64) {  // wave 0: in-place exclusive scan, kPer consecutive cells per lane
+    constexpr int kPer = (kGridCells + 63) / 64;
+    const int b = tid * kPer;
+    int loc[kPer], sum = 0;
+#pragma unroll
+    for (int j = 0; j < kPer; j++) {
+      loc[j] = b + j < kGridCells ? gstart[b + j] : 0;
+      sum += loc[j];
+    }
+    const int x = wave_incl_scan(sum);
+    int ex = x - sum;
+#pragma unroll
+    for (int j = 0; j < kPer; j++) {
+      if (b + j < kGridCells) gstart[b + j] = ex;
+      ex += loc[j];
+    }
+    if (tid == 63) gstart[kGridCells] = x;
+  }
+  __syncthreads();
+  if (cell >= 0) glist[gstart[cell] + gi] = entry;
+  __syncthreads();
+}
+
+// Visit the grid entries glist[i0, i1) (bits 0-7 column, 8-15 row) within L-inf 7 of (r, c):
+// f(entry, L-inf distance, index). Loads are issued four at a time ahead of their uses.
+template <class Fn>
+__device__ __forceinline__ void grid_scan(const uint32_t* __restrict__ glist, int i0, int i1, int r,
+                                          int c, Fn&& f) {
+  auto one = [&](uint32_t v, int i) {
+    const int d = max(abs((int)((v >> 8) & 255) - r), abs((int)(v & 255) - c));
+    if (d <= 7) f(v, d, i);
+  };
+  int i = i0;
+  for (; i + 4 <= i1; i += 4) {
+    const uint32_t v0 = glist[i], v1 = glist[i + 1], v2 = glist[i + 2], v3 = glist[i + 3];
+    one(v0, i);
+    one(v1, i + 1);
+    one(v2, i + 2);
+    one(v3, i + 3);
+  }
+  for (; i < i1; i++) one(glist[i], i);
 }
 
 // ---------------------------------------------------------------- packed-row scans

@@ -43,7 +43,8 @@ struct Ctx {
   int16_t* ring;     // [S]
   uint32_t* dep;     // [kBitmapWords]
   int* E;            // [NMMO_NE]
-  int* wtot;         // [32] wave totals
+  int* wtot;         // [32] wave totals: two alternating 8-wave buffers | attack-round flags
+  int wsel;          // block-uniform: offset of the wave-total buffer the last prefix used
   int* misc;         // [16]
   uint8_t* pres;     // [128] present at tick start
   uint8_t* died;     // [128]
@@ -77,6 +78,7 @@ struct Ctx {
   int S, P, N, IC;
   bool items, exch, prof, equip;
   const NmmoConfig* cfg;
+  uint32_t sysm;     // enabled systems: a compile-time constant in the specialised kernels
 };
 
 #define TF(f, s) c.T[(f) * c.S + (s)]
@@ -96,7 +98,12 @@ __device__ unsigned long long g_stamps[4096 * 16];
   } while (0)
 #endif
 
-__device__ __forceinline__ bool sys(const Ctx& c, uint32_t b) { return (c.cfg->systems & b) != 0; }
+__device__ __forceinline__ bool sys(const Ctx& c, uint32_t b) { return (c.sysm & b) != 0; }
+// the wave-total buffer for the next block prefix (alternates; see block_prefix_sum)
+__device__ __forceinline__ int* wtot_next(Ctx& c) {
+  c.wsel ^= 8;
+  return c.wtot + c.wsel;
+}
 __device__ __forceinline__ uint64_t env_seed(const Ctx& c) {
   return (uint64_t)(uint32_t)c.E[E_SEED_LO] | ((uint64_t)(uint32_t)c.E[E_SEED_HI] << 32);
 }
@@ -140,12 +147,12 @@ __host__ __device__ inline size_t tick_lds_bytes(int S, int P, bool items, bool 
   return b;
 }
 
-__device__ __forceinline__ Ctx make_ctx(unsigned char* smem, const DevState& st, int e) {
+__device__ __forceinline__ Ctx make_ctx(unsigned char* smem, const DevState& st, int e, uint32_t sy) {
   auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
   Ctx c;
   const int S = st.S;
   size_t o = 0;
-  const uint32_t sy = st.cfg.systems;
+  c.sysm = sy;
   c.items = (sy & NMMO_SYS_ITEM) != 0;
   c.exch = c.items && (sy & NMMO_SYS_EXCHANGE) != 0;
   c.prof = c.items && (sy & NMMO_SYS_PROFESSION) != 0;
@@ -211,6 +218,7 @@ __device__ __forceinline__ Ctx make_ctx(unsigned char* smem, const DevState& st,
   c.dep = reinterpret_cast<uint32_t*>(smem + o); o += (size_t)kBitmapWords * 4;
   c.E = reinterpret_cast<int*>(smem + o); o += NMMO_NE * 4;
   c.wtot = reinterpret_cast<int*>(smem + o); o += 32 * 4;
+  c.wsel = 0;
   c.misc = reinterpret_cast<int*>(smem + o); o += 16 * 4;
   c.pres = smem + o; o += 128;
   c.died = smem + o; o += 128;
@@ -413,7 +421,7 @@ __device__ __forceinline__ int inv_defense(const Ctx& c, int p) {
 // Every thread of the block must call this.
 __device__ __forceinline__ void ring_append_ordered(Ctx& c, int row) {
   int tot;
-  const int pre = block_prefix_sum(row >= 0 ? 1 : 0, c.wtot, &tot);
+  const int pre = block_prefix_sum(row >= 0 ? 1 : 0, wtot_next(c), &tot);
   if (row >= 0) c.iring[(c.E[E_ITEM_FREE_HEAD] + c.E[E_ITEM_FREE_COUNT] + pre) % c.IC] = (int16_t)row;
   __syncthreads();
   if (threadIdx.x == 0) c.E[E_ITEM_FREE_COUNT] += tot;
@@ -507,7 +515,7 @@ __device__ __forceinline__ void ev_put(const Ctx& c, int idx, int p, int code, i
 template <typename F>
 __device__ __forceinline__ void ev_append(Ctx& c, int& evn, int n, F&& emit) {
   int tot;
-  const int pre = block_prefix_sum(n, c.wtot, &tot);
+  const int pre = block_prefix_sum(n, wtot_next(c), &tot);
   if (n) emit(evn + pre);
   evn += tot;
 }
@@ -953,7 +961,7 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
   // ballot per player; each player then selects its k-th set bit with popcounts.
   const int NW = (S + 63) >> 6;
   const bool combat = sys(c, NMMO_SYS_COMBAT);
-  if (uses_grid(c.cfg->systems)) {
+  if (uses_grid(c.sysm)) {
     // Uniform grid (common.h): each player tests only the entities of the <= 3x3 cells its
     // 15x15 window touches. Bit (row-1) of the player's bitmap is set iff the entity in
     // datastore row `row` is in the realm and within L-inf 7 -- the same set an all-pairs test
@@ -1168,7 +1176,7 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
     const bool new_on = q_on >= 0 && !stack_on && n + (new_f ? 1 : 0) < kInv;
     need = (new_f ? 1 : 0) + (new_on ? 1 : 0);
     int tot;
-    const int pre = block_prefix_sum(need, c.wtot, &tot);  // rows in slot order (barriers inside)
+    const int pre = block_prefix_sum(need, wtot_next(c), &tot);  // rows in slot order (barriers inside)
     const int head = c.E[E_ITEM_FREE_HEAD];
     if (fishm) {
       const int nb[4] = {tile - kSize, tile + kSize, tile - 1, tile + 1};
@@ -1288,7 +1296,7 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
     if (c.exch) {
       const bool isb = s < P && c.a_buy[s] >= 0;
       int nbuy;
-      block_prefix_count(isb, c.wtot, &nbuy);
+      block_prefix_count(isb, wtot_next(c), &nbuy);
       if (nbuy > 0) {
         if (isb) c.ikey[s] = draw(seed, (uint32_t)tick, P_BUY_ORDER, (uint32_t)(s + 1), 0).x;
         __syncthreads();
@@ -1334,7 +1342,7 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
     {
       const bool isg = s < P && (c.a_givet[s] >= 0 || c.a_ggt[s] >= 0);
       int ng;
-      const int gpos = block_prefix_count(isg, c.wtot, &ng);
+      const int gpos = block_prefix_count(isg, wtot_next(c), &ng);
       if (isg) c.order[gpos] = (int16_t)s;
       __syncthreads();
       if (tid == 0) {
@@ -1392,9 +1400,13 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
   // round << 16 | (0xFFFF - slot), so no reset between rounds is needed.
   int* mi = c.ft;
   for (int k = tid; k < S; k += nt) mi[k] = 0;
+  if (tid < 3) c.wtot[16 + tid] = 0;  // attack-round flags
   __syncthreads();
   NMMO_STAMP(4);
-  {
+  if (combat || sys(c, NMMO_SYS_NPC)) {
+    // One barrier per round: pending attackers raise flag r % 3 before it, and thread 0 clears
+    // flag (r + 1) % 3 -- last read in round r - 2 -- for the next round.
+    int* anyf = c.wtot + 16;
     const int t = s < S ? c.atgt[s] : -1;
     bool active = inslot && t >= 0;
     const int sty = s < S ? c.asty[s] : 0;
@@ -1403,17 +1415,18 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
       if (active) {
         atomicMax(&mi[s], key);
         atomicMax(&mi[t], key);
+        anyf[round % 3] = 1;
       }
+      if (tid == 0) anyf[(round + 1) % 3] = 0;
       __syncthreads();
+      if (!anyf[round % 3]) break;
       if (active && mi[s] == key && mi[t] == key) {
         const int dmg = eval_attack(c, s, sty, t);
         if (dmg >= 0) apply_attack(c, s, sty, t, dmg, tick);
         active = false;
       }
-      if (!__syncthreads_or(active)) break;
     }
   }
-  __syncthreads();
   if (evon) {  // SCORE_HIT, LEVEL_UP, PLAYER_KILL per player attacker in slot order
     const int dm = s < P ? c.ev_dmg[s] : -1, lv = s < P ? c.ev_lvl[s] : 0, kv = s < P ? c.kill[s] : -1;
     ev_append(c, evn, (dm >= 0) + (lv > 0) + (kv >= 0), [&](int i) {
@@ -1431,7 +1444,7 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
     // every attack's validity are unaffected by them, so deferring is exact)
     const bool nd = s < P && (c.fired[s] || c.kill[s] >= 0);
     int nn;
-    const int pos = block_prefix_count(nd, c.wtot, &nn);
+    const int pos = block_prefix_count(nd, wtot_next(c), &nn);
     if (nd) c.order[pos] = (int16_t)s;
     __syncthreads();
     if (tid == 0) {
@@ -1475,7 +1488,7 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
   if (evon) {  // GO_FARTHEST (Move) events, then LIST_ITEM (Sell) events: both counts in one scan
     const int nl = it_type(sw) ? 1 : 0;
     int tot;
-    const int pre = block_prefix_sum((gf > 0 ? 1 : 0) | (nl << 16), c.wtot, &tot);
+    const int pre = block_prefix_sum((gf > 0 ? 1 : 0) | (nl << 16), wtot_next(c), &tot);
     if (gf > 0) ev_put(c, evn + (pre & 0xFFFF), s, EV_GO_FARTHEST, 0, 0, gf, 0, 0);
     if (nl)
       ev_put(c, evn + (tot & 0xFFFF) + (pre >> 16), s, EV_LIST_ITEM, it_type(sw), it_level(sw), it_qty(sw),
@@ -1488,9 +1501,9 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
   // 4. cull: rows appended to the free ring in slot order; NPC slots compacted
   const bool dead = inslot && TF(F_ALIVE, s) && TF(F_HEALTH, s) <= 0;
   int ndead;
-  const int dpos = block_prefix_count(dead, c.wtot, &ndead);
+  const int dpos = block_prefix_count(dead, wtot_next(c), &ndead);
   int npdead;
-  const int ppos = block_prefix_count(dead && s < P, c.wtot, &npdead);
+  const int ppos = block_prefix_count(dead && s < P, wtot_next(c), &npdead);
   if (s < P) c.died[s] = dead ? 1 : 0;
   if (evon) {  // AGENT_CULLED in slot order (players are slots 0..P-1: the same prefix)
     if (dead && s < P) ev_put(c, evn + ppos, s, EV_AGENT_CULLED, 0, 0, 0, 0, 0);
@@ -1505,7 +1518,7 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
     uint2* inv = c.inv + (s < P ? s : 0) * kInv;
     const int n = (dead && s < P) ? inv_count(inv) : 0;
     int tot;
-    const int pre = block_prefix_sum(n, c.wtot, &tot);
+    const int pre = block_prefix_sum(n, wtot_next(c), &tot);
     if (n) {
       const int base = c.E[E_ITEM_FREE_HEAD] + c.E[E_ITEM_FREE_COUNT] + pre;
       for (int k = 0; k < n; k++) {
@@ -1525,7 +1538,7 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
   if (sys(c, NMMO_SYS_NPC) && ndead > npdead) {  // compaction only when an NPC left the realm
     const bool keep = s >= P && inslot && TF(F_ALIVE, s);
     int nkeep;
-    const int kpos = block_prefix_count(keep, c.wtot, &nkeep);
+    const int kpos = block_prefix_count(keep, wtot_next(c), &nkeep);
     int16_t v[kNFLive];
     if (keep) {
 #pragma unroll
@@ -1560,7 +1573,7 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
       ng_mine += __popc(nz & 0x11111111u);
     }
     int ngroups;
-    const int gpos = block_prefix_sum(ng_mine, c.wtot, &ngroups);
+    const int gpos = block_prefix_sum(ng_mine, wtot_next(c), &ngroups);
     int16_t* glist = reinterpret_cast<int16_t*>(c.vism);  // dead after decode
     const int gcap = 128 * NW * 4;                         // int16 entries in vism's bytes
     const uint32_t rtick = (uint32_t)(tick + 1);
@@ -1686,13 +1699,16 @@ __device__ __forceinline__ void store_market(Ctx& c, const DevState& st, int e) 
 
 // ---------------------------------------------------------------- kernel
 // mode 0: step (auto-reset envs that are done); mode 1: reset every env.
+// kSys != 0: specialised for exactly that system set (launch_tick dispatches on
+// cfg.systems), so disabled systems compile out; kSys == 0 reads the set at run time.
+template <uint32_t kSys>
 __global__ void tick_kernel(DevState st, const int32_t* __restrict__ actions,
                             const uint64_t* __restrict__ env_seeds, float* rew, uint8_t* term,
                             uint8_t* trunc, uint8_t* mask, int mode) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int e = blockIdx.x;
   NMMO_STAMP(0);
-  Ctx c = make_ctx(smem, st, e);
+  Ctx c = make_ctx(smem, st, e, kSys ? kSys : st.cfg.systems);
   load_env(c, st, e);
   __syncthreads();
   const size_t o = (size_t)e * c.P;
@@ -1729,7 +1745,7 @@ __global__ void tick_kernel(DevState st, const int32_t* __restrict__ actions,
   if (st.counters) {  // sum(mask) of this launch (pres, or all players on a reset) + done envs
     const bool reset = mode == 1 || reset_path;
     int n;
-    block_prefix_count(threadIdx.x < c.P && (reset || c.pres[threadIdx.x]), c.wtot, &n);
+    block_prefix_count(threadIdx.x < c.P && (reset || c.pres[threadIdx.x]), wtot_next(c), &n);
     if (threadIdx.x == 0) {
       atomicAdd(&st.counters[0], (unsigned long long)n);
       if (!reset && c.E[E_DONE]) atomicAdd(&st.counters[1], 1ull);
@@ -1742,24 +1758,42 @@ __global__ void tick_kernel(DevState st, const int32_t* __restrict__ actions,
   NMMO_STAMP(11);
 }
 
+// system sets with a specialised tick kernel: BASELINE configs 2 and 3 (config 4 = all)
+constexpr uint32_t kSysC2 = NMMO_SYS_RESOURCE;
+constexpr uint32_t kSysC3 = NMMO_SYS_RESOURCE | NMMO_SYS_COMBAT | NMMO_SYS_NPC | NMMO_SYS_PROGRESSION;
+
 hipError_t launch_tick(const DevState& st, const int32_t* actions, const uint64_t* env_seeds,
                        float* rew, uint8_t* term, uint8_t* trunc, uint8_t* mask, int mode,
                        hipStream_t stream) {
   const int threads = ((st.S + 63) / 64) * 64;
   const size_t lds = tick_lds_bytes(st.S, st.P, (st.cfg.systems & NMMO_SYS_ITEM) != 0, st.tev != 0,
                                     uses_grid(st.cfg.systems));
-  hipLaunchKernelGGL(tick_kernel, dim3(st.n_envs), dim3(threads), lds, stream,
+  void (*k)(DevState, const int32_t*, const uint64_t*, float*, uint8_t*, uint8_t*, uint8_t*, int);
+  switch (st.cfg.systems) {
+    case kSysC2: k = tick_kernel<kSysC2>; break;
+    case kSysC3: k = tick_kernel<kSysC3>; break;
+    case NMMO_SYS_ALL: k = tick_kernel<NMMO_SYS_ALL>; break;
+    default: k = tick_kernel<0>; break;
+  }
+  hipLaunchKernelGGL(k, dim3(st.n_envs), dim3(threads), lds, stream,
                      st, actions, env_seeds, rew, term, trunc, mask, mode);
   return hipGetLastError();
 }
 
 hipError_t init_kernels() {
-  // dynamic LDS may use what the kernel's static LDS (e.g. __syncthreads_or) leaves of 160 KB
-  hipFuncAttributes fa;
-  hipError_t err = hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(tick_kernel));
-  if (err != hipSuccess) return err;
-  return hipFuncSetAttribute(reinterpret_cast<const void*>(tick_kernel),
-                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)(160 * 1024 - fa.sharedSizeBytes));
+  // dynamic LDS may use what the kernel's static LDS leaves of 160 KB
+  const void* ks[4] = {reinterpret_cast<const void*>(tick_kernel<kSysC2>),
+                       reinterpret_cast<const void*>(tick_kernel<kSysC3>),
+                       reinterpret_cast<const void*>(tick_kernel<NMMO_SYS_ALL>),
+                       reinterpret_cast<const void*>(tick_kernel<0>)};
+  for (const void* k : ks) {
+    hipFuncAttributes fa;
+    hipError_t err = hipFuncGetAttributes(&fa, k);
+    if (err != hipSuccess) return err;
+    err = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(160 * 1024 - fa.sharedSizeBytes));
+    if (err != hipSuccess) return err;
+  }
+  return hipSuccess;
 }
 
 // set_state support: derived state is rebuilt from the blob — the depleted-tile bitmap
