@@ -858,8 +858,7 @@ __device__ __forceinline__ double term_progress(const Ctx& c, int p, const NmmoT
 }
 
 // clipped progress of player p's task; SUM without fused multiply-adds (bit-exact with the oracle)
-__device__ __forceinline__ double task_progress(const Ctx& c, int p, const int* acc) {
-  const NmmoTask& t = c.tasks[c.assign[p]];
+__device__ __forceinline__ double task_progress(const Ctx& c, int p, const NmmoTask& t, const int* acc) {
   const double p0 = clip01(term_progress(c, p, t.term[0], acc));
   if (t.combine == NMMO_TASK_SINGLE) return p0;
   const double p1 = clip01(term_progress(c, p, t.term[1], acc + 2));
@@ -925,6 +924,7 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
   // entity moves before the move phase, so these stay exact for NPC steering, drinking,
   // foilage eating (the own tile is read before any harvest) and the move check.
   uint32_t m_own = 0, m_n0 = 0, m_n1 = 0, m_n2 = 0, m_n3 = 0;
+  const int my_task = s < P ? c.assign[s] : 0;  // HBM; first used before the respawn phase
   const bool in_realm = s < S && inslot && TF(F_ALIVE, s);  // => health > 0 at tick start
   const int pos_r = s < S ? TF(F_ROW, s) : 0, pos_c = s < S ? TF(F_COL, s) : 0;
   {
@@ -1427,7 +1427,7 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
       }
     }
   }
-  if (evon) {  // SCORE_HIT, LEVEL_UP, PLAYER_KILL per player attacker in slot order
+  if (evon && combat) {  // SCORE_HIT, LEVEL_UP, PLAYER_KILL per player attacker in slot order
     const int dm = s < P ? c.ev_dmg[s] : -1, lv = s < P ? c.ev_lvl[s] : 0, kv = s < P ? c.kill[s] : -1;
     ev_append(c, evn, (dm >= 0) + (lv > 0) + (kv >= 0), [&](int i) {
       const int sk = c.asty[s] + 1;
@@ -1558,6 +1558,13 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
   __syncthreads();
   NMMO_STAMP(7);
 
+  // this player's task state, loaded here when it lives in HBM so the rewards do not wait on it
+  NmmoTaskState tsr = {};
+  NmmoTask tk = {};  // and its task (index loaded at tick start)
+  if (s < P && c.pres[s] && !c.died[s]) {
+    if (!c.tev) tsr = c.ts[s];
+    tk = c.tasks[my_task];
+  }
   // 5-6. tick += 1; map.step respawn of depleted tiles; exchange.step listing expiry.
   // One Philox call serves a group of 4 consecutive tiles (SPEC §5.6). The groups holding a
   // depleted tile are compacted into a list (in LDS space the decode bitmap no longer needs)
@@ -1591,17 +1598,19 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
         }
       }
       __syncthreads();
+      const uint32_t* base4 = reinterpret_cast<const uint32_t*>(base);  // 4 tiles per word
       for (int i = tid; i < ngroups; i += nt) {
         const int g = glist[i], w = g >> 3, sh = (g & 7) * 4;
+        const uint32_t b4 = base4[g];  // issued ahead of the draw, whose latency covers it
         const uint32_t nib = (c.dep[w] >> sh) & 15u;
         const U4 u = draw(seed, rtick, P_RESPAWN, (uint32_t)g, 0);
         const uint32_t uu[4] = {u.x, u.y, u.z, u.w};
         uint32_t clear = 0;
 #pragma unroll
         for (int j = 0; j < 4; j++) {
-          const int tt = 4 * g + j;
-          if (((nib >> j) & 1u) && uu[j] < respawn_u32(base[tt])) {
-            c.mat[tt] = base[tt];
+          const int bm = (int)((b4 >> (8 * j)) & 255u);
+          if (((nib >> j) & 1u) && uu[j] < respawn_u32(bm)) {
+            c.mat[4 * g + j] = (uint8_t)bm;
             clear |= 1u << (sh + j);
           }
         }
@@ -1654,8 +1663,8 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
     if (c.pres[s] && c.died[s]) {
       rw = -1.f;
     } else if (c.pres[s]) {
-      NmmoTaskState ts = c.ts[s];  // LDS when staged, else this env's HBM copy
-      const double np = task_progress(c, s, ts.acc), d = np - ts.last;
+      NmmoTaskState ts = c.tev ? c.ts[s] : tsr;  // staged in LDS, or prefetched from HBM
+      const double np = task_progress(c, s, tk, ts.acc), d = np - ts.last;
       ts.last = np;
       if (np > ts.max_progress) ts.max_progress = np;
       if (d > 0.0) ts.signals += 1;
@@ -1765,7 +1774,8 @@ constexpr uint32_t kSysC3 = NMMO_SYS_RESOURCE | NMMO_SYS_COMBAT | NMMO_SYS_NPC |
 hipError_t launch_tick(const DevState& st, const int32_t* actions, const uint64_t* env_seeds,
                        float* rew, uint8_t* term, uint8_t* trunc, uint8_t* mask, int mode,
                        hipStream_t stream) {
-  const int threads = ((st.S + 63) / 64) * 64;
+  // >= 4 waves so the block-wide loops (state copies, respawn draws) use all four SIMDs
+  const int threads = max(((st.S + 63) / 64) * 64, 256);
   const size_t lds = tick_lds_bytes(st.S, st.P, (st.cfg.systems & NMMO_SYS_ITEM) != 0, st.tev != 0,
                                     uses_grid(st.cfg.systems));
   void (*k)(DevState, const int32_t*, const uint64_t*, float*, uint8_t*, uint8_t*, uint8_t*, int);

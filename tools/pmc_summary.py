@@ -25,7 +25,9 @@ def _rows(pattern):
 
 
 def _short(name):
-    name = name.split("(")[0]
+    """'void nmmo::tick_kernel<15u>(nmmo::DevState, ...)' -> 'tick_kernel' (all system-set
+    specialisations of a kernel are one entry: a bench run launches only one of them)."""
+    name = name.split("(")[0].split("<")[0]
     return name.split("::")[-1].strip()
 
 
