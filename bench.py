@@ -46,6 +46,14 @@ WORKLOADS = {
 }
 
 
+# the agent sections' reward_wrapper weights (config.yaml:103-106, 118-126, 137-140)
+WRAPPER_KW = {"neurips23_start_kit": dict(heal_bonus_weight=0.03, explore_bonus_weight=0.01),
+              "takeru": dict(explore_bonus_weight=0.01, disable_give=True),
+              "yaofeng": dict(hp_bonus_weight=0.03, exp_bonus_weight=0.002, defense_bonus_weight=0.04,
+                              attack_bonus_weight=0.0, gold_bonus_weight=0.001, custom_bonus_scale=0.1,
+                              disable_give=True, donot_attack_dangerous_npc=True)}
+
+
 def tick_bytes_per_env(S: int, P: int, items: bool) -> int:
     """Algorithmic HBM bytes of one tick of one env: the env state read and
     written once (45 int16 entity fields x slots, free-row ring, depleted-tile bitmap, env
@@ -94,6 +102,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraph replay")
     ap.add_argument("--graph-steps", type=int, default=10, help="ticks captured per hipGraph")
+    ap.add_argument("--wrapper", default="none",
+                    choices=["none", "base", "neurips23_start_kit", "takeru", "yaofeng"],
+                    help="run env_creator's RewardWrapper on the device (SPEC §13) with the "
+                         "config.yaml weights")
     return ap.parse_args()
 
 
@@ -183,6 +195,10 @@ def main():
         task = np.load(gpath)["heldout_emb"][0]  # TickGE(1024) task, SURVEY §8d
     eng = NmmoEngine(cfg, envs, seed=args.seed, device=dev, task_embedding=task,
                      env_index_base=rank * envs)
+    if args.wrapper != "none":
+        from nmmo_amd.wrappers import wrapper_config
+
+        eng.set_wrapper(wrapper_config(args.wrapper, **WRAPPER_KW.get(args.wrapper, {})))
     eng.reset()
     # device counters the tick kernel adds into: [0] = sum(mask) (agent-steps), [1] = episodes
     counters = torch.zeros(2, dtype=torch.int64, device=dev)
@@ -250,7 +266,7 @@ def main():
     eng.set_timing(True)
     for _ in range(min(args.steps, 8192)):
         one()
-    tick_ms, obs_ms, n_timed = eng.read_timing()
+    tick_ms, obs_ms, n_timed, wrap_ms = eng.read_timing()
     eng.set_timing(False)
     # practical HBM write ceiling on THIS box: the vendor fill kernel over the same obs buffer
     # (the same byte count the obs kernel writes per launch), HIP events on the current stream
@@ -319,7 +335,9 @@ def main():
             },
             "slot_steps_per_sec": round(slots_total / elapsed, 1),
             "alive_fraction": round(alive_total / slots_total, 4),
-            "kernel_ms": {"tick": round(tick_avg_ms, 5), "obs": round(obs_avg_ms, 5)},
+            "kernel_ms": {"tick": round(tick_avg_ms, 5), "obs": round(obs_avg_ms, 5),
+                          "wrapper": round(wrap_ms / max(n_timed, 1), 5)},
+            "wrapper": None if args.wrapper == "none" else args.wrapper,
             "launch": "eager" if (args.no_graph or gather) else f"hipGraph x{min(args.graph_steps, args.steps)} ticks",
             "gather": f"RCCL gather of {eng.obs.numel() * 4 + envs * cfg.PLAYER_N * 8} B/rank/step to rank 0" if gather else None,
             "roofline": {

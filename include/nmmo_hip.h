@@ -16,6 +16,8 @@
  *                                                      clean_pufferl.py:116, baseline_policy.py:28,41
  *   nmmo_get_state / nmmo_set_state  <- env.realm.{players,npcs,map,tick} reads
  *                                                      stat_wrapper.py:122-185, train_helper.py:133-166
+ *   nmmo_set_wrapper <- env_creator's RewardWrapper(BaseStatWrapper) around each env
+ *                    (reward shaping, obs edits, info) environment.py:58, stat_wrapper.py:57-185
  *   nmmo_scripted_actions  <- (bench/test helper) masked-uniform actions, the behaviour of an
  *                    untrained masked policy           agent_zoo/neurips23_start_kit/baseline_policy.py:228-264
  *
@@ -40,7 +42,7 @@ extern "C" {
 #endif
 
 #define NMMO_API __attribute__((visibility("default")))
-#define NMMO_ABI_VERSION 3
+#define NMMO_ABI_VERSION 4
 
 /* ---- error codes ---- */
 #define NMMO_OK 0
@@ -159,6 +161,61 @@ typedef struct NmmoTaskState {
   int32_t signals, completed_tick;
 } NmmoTaskState;
 
+/* ---- wrapper layer (SPEC.md §13): the reference's per-step env wrappers as a device pass
+ * after the tick — BaseStatWrapper (reinforcement_learning/stat_wrapper.py:9-185) plus the
+ * agent reward wrappers' reward shaping and ActionTargets edits. ---- */
+#define NMMO_WRAP_BASE 0       /* BaseStatWrapper only (reward_terminated_truncated_info = id) */
+#define NMMO_WRAP_START_KIT 1  /* agent_zoo/neurips23_start_kit/reward_wrapper.py */
+#define NMMO_WRAP_TAKERU 2     /* agent_zoo/takeru/reward_wrapper.py */
+#define NMMO_WRAP_YAOFENG 3    /* agent_zoo/yaofeng/reward_wrapper.py */
+typedef struct NmmoWrapperConfig {
+  int32_t kind;                       /* NMMO_WRAP_* */
+  int32_t use_custom_reward;          /* stat_wrapper.py:17,77-86 */
+  int32_t eval_mode;                  /* stat_wrapper.py:13,165-167: return = max progress */
+  int32_t clip_unique_event;          /* start kit / takeru explore-bonus clip (3) */
+  int32_t disable_give;               /* takeru / yaofeng: Give/GiveGold masks -> noop only */
+  int32_t donot_attack_dangerous_npc; /* yaofeng: Attack.Target off for npc_type > 1 rows */
+  double heal_bonus_weight, explore_bonus_weight;            /* start kit (+ takeru explore) */
+  double hp_bonus_weight, exp_bonus_weight, defense_bonus_weight, attack_bonus_weight,
+      gold_bonus_weight, custom_bonus_scale;                 /* yaofeng */
+} NmmoWrapperConfig;
+
+/* Per-agent episode record written on the step the agent is terminated or truncated (the
+ * info dict of stat_wrapper.py:118-185). `performed` bit k = info["stats"]["event/<name>"] for
+ * name in eat_food, drink_water, score_hit, player_kill, consume_item, harvest_item, list_item,
+ * buy_item, equip_armor, equip_weapon, equip_tool, equip_ammo, harvest_weapon. */
+typedef struct NmmoAgentInfo {
+  int32_t done;                /* 1 on the agent's final step (term or trunc), else 0 */
+  int32_t length;              /* info["length"] = realm.tick */
+  double ret;                  /* info["return"] (eval_mode: the task's max progress) */
+  double max_progress;         /* task._max_progress (info["curriculum"]) */
+  int32_t reward_signal_count; /* task.reward_signal_count */
+  int32_t task_completed;
+  int32_t cod_attacked, cod_starved, cod_dehydrated;
+  int32_t max_combat_level, max_harvest_skill_ammo, max_harvest_skill_consum;
+  uint32_t performed;
+  int32_t max_progress_to_center, earned_gold, max_damage;
+  int32_t max_item_level[5];   /* armor, weapon, tool, ammo, consumable; -1 = key absent */
+  int32_t agent_kill_count, npc_kill_count, unique_events;
+} NmmoAgentInfo;
+
+/* Per-agent wrapper state (nmmo_get_wrapper_state, parity tests). */
+typedef struct NmmoWrapState {
+  double cum_reward;           /* BaseStatWrapper.cum_rewards */
+  int32_t prev_count, curr_count; /* _unique_events prev/curr */
+  int32_t prev_price;          /* start kit _history.prev_price */
+  int32_t hp, exp, gold, dmg_inflicted_prev; /* yaofeng _data */
+  int32_t dmg_inflicted;       /* history.damage_inflicted */
+  uint32_t performed;          /* event-log accumulators of the episode (NmmoAgentInfo) */
+  int32_t max_dist, earned_gold, max_damage;
+  int32_t max_item_level[5];
+  int32_t agent_kills, npc_kills;
+  int32_t reserved;
+} NmmoWrapState;
+/* unique (event, type, level) tuples an agent has experienced: a bitset of
+ * 17 codes x 18 types x 16 levels */
+#define NMMO_UNIQ_WORDS 153
+
 typedef struct NmmoConfig {
   int32_t abi_version;        /* must be NMMO_ABI_VERSION */
   int32_t player_n;           /* PLAYER_N 128 (environment.py:35, config.yaml:76); <= 128 */
@@ -225,6 +282,16 @@ NMMO_API int nmmo_step(NmmoHandle* h, const int32_t* actions, void* obs, float* 
 NMMO_API int nmmo_set_tasks(NmmoHandle* h, const NmmoTask* tasks, int32_t n_tasks,
                             const uint16_t* embeddings, const int32_t* assign);
 
+/* Wrapper layer (SPEC.md §13; replaces the RewardWrapper(BaseStatWrapper) that env_creator
+ * puts around every nmmo.Env, environment.py:58): wc = NULL turns it off. While on, every
+ * nmmo_step / nmmo_reset runs it after the tick: rewards are shaped in place, the obs
+ * ActionTargets edits are applied, and dev_info (device NmmoAgentInfo [n_envs][player_n],
+ * caller-owned) receives each agent's episode record on its final step (done = 0 elsewhere).
+ * Needs the event log (event_cap > 0). Resets every env's wrapper state; synchronous. */
+NMMO_API int nmmo_set_wrapper(NmmoHandle* h, const NmmoWrapperConfig* wc, NmmoAgentInfo* dev_info);
+/* host NmmoWrapState [n_envs][player_n] + u32 [n_envs][player_n][NMMO_UNIQ_WORDS]. Synchronous. */
+NMMO_API int nmmo_get_wrapper_state(NmmoHandle* h, NmmoWrapState* host_state, uint32_t* host_uniq);
+
 /* Masked-uniform scripted actions from the current state (bench / tests). */
 NMMO_API int nmmo_scripted_actions(NmmoHandle* h, uint64_t policy_seed, int32_t* actions, void* stream);
 
@@ -239,15 +306,16 @@ NMMO_API int nmmo_get_map_bank(NmmoHandle* h, uint8_t* host_buf, size_t nbytes);
 
 /* Kernel timing with HIP events recorded on the launch stream around each kernel of
  * nmmo_step (bench/profiling; off by default, up to 8192 steps buffered).
- * nmmo_read_timing synchronises, returns the summed milliseconds of the tick and obs kernels
- * over the buffered steps in ms[0], ms[1], their count in *n, and clears the buffer. */
+ * nmmo_read_timing synchronises, returns the summed milliseconds of the tick, obs and wrapper
+ * kernels over the buffered steps in ms[0], ms[1], ms[2], their count in *n, and clears the
+ * buffer. */
 NMMO_API int nmmo_set_timing(NmmoHandle* h, int32_t enable);
 /* Device-side rollout counters (the trainer's agent_SPS numerator, clean_pufferl.py:306):
  * when set, every nmmo_step / nmmo_reset adds into dev_counters (device u64 [2]):
  * [0] += sum of the mask it writes (agent-steps), [1] += envs whose episode ended.
  * NULL disables. The caller owns and zeroes the buffer; capture-safe. */
 NMMO_API int nmmo_set_counters(NmmoHandle* h, uint64_t* dev_counters);
-NMMO_API int nmmo_read_timing(NmmoHandle* h, double* ms /* [2] */, int32_t* n);
+NMMO_API int nmmo_read_timing(NmmoHandle* h, double* ms /* [3] */, int32_t* n);
 
 /* The event log of env `env` (realm.event_log.get_data): copies the most recent
  * min(retained, max_rows) rows, oldest first, into host_rows [max_rows][NMMO_EVENT_COLS] and

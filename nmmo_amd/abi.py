@@ -6,7 +6,7 @@ struct sizes against the compiled library and the enum values against the header
 
 import ctypes
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 NMMO_OK = 0
 NMMO_E_INVALID = -1
@@ -171,3 +171,47 @@ TASK_STATE_BYTES = 40
 def state_bytes_per_env(slots: int, players: int = 128) -> int:
     return NE * 4 + NF * slots * 2 + slots * 2 + MAP_TILES + players * INV_SLOTS * 8 \
         + INV_SLOTS * players * 2 + players * 4 + players * TASK_STATE_BYTES
+
+
+# Wrapper layer (SPEC.md §13; nmmo_set_wrapper)
+WRAP_BASE, WRAP_START_KIT, WRAP_TAKERU, WRAP_YAOFENG = 0, 1, 2, 3
+UNIQ_WORDS = 153
+# NmmoAgentInfo.performed bit order (stat_wrapper.py:196-205 KEY_EVENT, then :207-236)
+PERFORMED_KEYS = ["eat_food", "drink_water", "score_hit", "player_kill", "consume_item",
+                  "harvest_item", "list_item", "buy_item", "equip_armor", "equip_weapon",
+                  "equip_tool", "equip_ammo", "harvest_weapon"]
+ITEM_CATEGORIES = ["armor", "weapon", "tool", "ammo", "consumable"]
+
+
+class NmmoWrapperConfig(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int32), ("use_custom_reward", ctypes.c_int32),
+                ("eval_mode", ctypes.c_int32), ("clip_unique_event", ctypes.c_int32),
+                ("disable_give", ctypes.c_int32), ("donot_attack_dangerous_npc", ctypes.c_int32),
+                ("heal_bonus_weight", ctypes.c_double), ("explore_bonus_weight", ctypes.c_double),
+                ("hp_bonus_weight", ctypes.c_double), ("exp_bonus_weight", ctypes.c_double),
+                ("defense_bonus_weight", ctypes.c_double), ("attack_bonus_weight", ctypes.c_double),
+                ("gold_bonus_weight", ctypes.c_double), ("custom_bonus_scale", ctypes.c_double)]
+
+
+def agent_info_dtype():
+    import numpy as np
+
+    return np.dtype([("done", "<i4"), ("length", "<i4"), ("ret", "<f8"), ("max_progress", "<f8"),
+                     ("reward_signal_count", "<i4"), ("task_completed", "<i4"),
+                     ("cod_attacked", "<i4"), ("cod_starved", "<i4"), ("cod_dehydrated", "<i4"),
+                     ("max_combat_level", "<i4"), ("max_harvest_skill_ammo", "<i4"),
+                     ("max_harvest_skill_consum", "<i4"), ("performed", "<u4"),
+                     ("max_progress_to_center", "<i4"), ("earned_gold", "<i4"), ("max_damage", "<i4"),
+                     ("max_item_level", "<i4", (5,)), ("agent_kill_count", "<i4"),
+                     ("npc_kill_count", "<i4"), ("unique_events", "<i4")])
+
+
+def wrap_state_dtype():
+    import numpy as np
+
+    return np.dtype([("cum_reward", "<f8"), ("prev_count", "<i4"), ("curr_count", "<i4"),
+                     ("prev_price", "<i4"), ("hp", "<i4"), ("exp", "<i4"), ("gold", "<i4"),
+                     ("dmg_inflicted_prev", "<i4"), ("dmg_inflicted", "<i4"), ("performed", "<u4"),
+                     ("max_dist", "<i4"), ("earned_gold", "<i4"), ("max_damage", "<i4"),
+                     ("max_item_level", "<i4", (5,)), ("agent_kills", "<i4"), ("npc_kills", "<i4"),
+                     ("reserved", "<i4")])

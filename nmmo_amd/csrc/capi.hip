@@ -53,10 +53,17 @@ struct NmmoHandle {
   NmmoTask* d_tasks = nullptr;
   int32_t* d_assign = nullptr;
   NmmoTaskState* d_tstate = nullptr;
+  // wrapper layer (nmmo_set_wrapper, SPEC §13)
+  bool wrap_on = false;
+  NmmoWrapperConfig wc{};
+  NmmoWrapState* d_ws = nullptr;
+  uint32_t* d_uniq = nullptr;
+  int32_t* d_wenv = nullptr;
+  NmmoAgentInfo* d_info = nullptr;  // caller-owned
   // bench timing (nmmo_set_timing): event pairs around the tick and obs kernels
   bool timing = false;
   int t_count = 0;
-  std::vector<hipEvent_t> ev;  // [kTimingCap][4]: tick begin/end, obs begin/end
+  std::vector<hipEvent_t> ev;  // [kTimingCap][4]: tick begin, tick end, wrapper end, obs end
 };
 static constexpr int kTimingCap = 8192;
 
@@ -152,7 +159,7 @@ void nmmo_destroy(NmmoHandle* h) {
   for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
   void* bufs[] = {h->d_env,  h->d_ent,   h->d_ring,  h->d_mat,   h->d_dep,   h->d_bank,
                   h->d_task, h->d_seeds, h->d_items, h->d_iring, h->d_mlist, h->d_mcount,
-                  h->d_events, h->d_tasks, h->d_assign, h->d_tstate};
+                  h->d_events, h->d_tasks, h->d_assign, h->d_tstate, h->d_ws, h->d_uniq, h->d_wenv};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   delete h;
@@ -245,6 +252,24 @@ static ObsParams obs_params(NmmoHandle* h, float* obs) {
   p.o_agent_id = L.off_agent_id; p.o_tick = L.off_current_tick; p.o_entity = L.off_entity;
   p.o_inventory = L.off_inventory; p.o_market = L.off_market; p.o_task = L.off_task;
   p.o_tile = L.off_tile;
+  p.ws = h->wrap_on ? h->d_ws : nullptr;
+  p.wflags = 0;
+  if (h->wrap_on) {
+    if (h->wc.kind == NMMO_WRAP_START_KIT) p.wflags |= kWrapObsPrice;
+    if (h->wc.disable_give) p.wflags |= kWrapObsNoGive;
+    if (h->wc.donot_attack_dangerous_npc) p.wflags |= kWrapObsNoDangerous;
+  }
+  return p;
+}
+
+static WrapParams wrap_params(NmmoHandle* h, const int32_t* actions, float* rew, const uint8_t* term,
+                              const uint8_t* trunc, const uint8_t* mask) {
+  WrapParams p;
+  p.env = h->d_env; p.ent = h->d_ent; p.items = h->d_items; p.events = h->d_events;
+  p.tstate = h->d_tstate; p.actions = actions; p.rew = rew; p.term = term; p.trunc = trunc;
+  p.mask = mask; p.ws = h->d_ws; p.uniq = h->d_uniq; p.wenv = h->d_wenv; p.info = h->d_info;
+  p.wc = h->wc; p.n_envs = h->st.n_envs; p.P = h->st.P; p.S = h->st.S; p.evcap = h->cfg.event_cap;
+  p.items_on = (h->cfg.systems & NMMO_SYS_ITEM) != 0;
   return p;
 }
 
@@ -258,6 +283,7 @@ int nmmo_reset(NmmoHandle* h, const uint64_t* env_seeds, void* obs, uint8_t* mas
   }
   HIP_TRY(launch_tick(h->st, nullptr, env_seeds ? h->d_seeds : nullptr, nullptr, nullptr, nullptr,
                       mask, 1, s));
+  if (h->wrap_on) HIP_TRY(launch_wrap(wrap_params(h, nullptr, nullptr, nullptr, nullptr, nullptr), 0, s));
   if (obs && h->cfg.obs_layout == NMMO_OBS_FLAT) HIP_TRY(launch_obs(obs_params(h, (float*)obs), s));
   return NMMO_OK;
 }
@@ -273,10 +299,12 @@ int nmmo_step(NmmoHandle* h, const int32_t* actions, void* obs, float* rew, uint
   if (rec) HIP_TRY(hipEventRecord(ev[0], s));
   HIP_TRY(launch_tick(h->st, actions, nullptr, rew, term, trunc, mask, 0, s));
   if (rec) HIP_TRY(hipEventRecord(ev[1], s));
+  if (h->wrap_on) HIP_TRY(launch_wrap(wrap_params(h, actions, rew, term, trunc, mask), 0, s));
+  if (rec) HIP_TRY(hipEventRecord(ev[2], s));  // wrapper span = ev[1]..ev[2] (empty when off)
   const bool do_obs = obs && h->cfg.obs_layout == NMMO_OBS_FLAT;
   if (do_obs) HIP_TRY(launch_obs(obs_params(h, (float*)obs), s));
   if (rec) {
-    HIP_TRY(hipEventRecord(ev[2], s));  // obs span = ev[1]..ev[2] (empty when no obs)
+    HIP_TRY(hipEventRecord(ev[3], s));  // obs span = ev[2]..ev[3] (empty when no obs)
     h->t_count++;
   }
   return NMMO_OK;
@@ -302,16 +330,18 @@ int nmmo_set_counters(NmmoHandle* h, uint64_t* dev_counters) {
 
 int nmmo_read_timing(NmmoHandle* h, double* ms, int32_t* n) {
   if (!h || !ms || !n) return fail(NMMO_E_INVALID, "null argument");
-  ms[0] = ms[1] = 0.0;
+  ms[0] = ms[1] = ms[2] = 0.0;
   *n = h->t_count;
   for (int i = 0; i < h->t_count; i++) {
     hipEvent_t* ev = &h->ev[(size_t)i * 4];
-    float a = 0.f, b = 0.f;
-    HIP_TRY(hipEventSynchronize(ev[2]));
+    float a = 0.f, b = 0.f, c = 0.f;
+    HIP_TRY(hipEventSynchronize(ev[3]));
     HIP_TRY(hipEventElapsedTime(&a, ev[0], ev[1]));
-    HIP_TRY(hipEventElapsedTime(&b, ev[1], ev[2]));
+    HIP_TRY(hipEventElapsedTime(&b, ev[2], ev[3]));
+    HIP_TRY(hipEventElapsedTime(&c, ev[1], ev[2]));
     ms[0] += a;
     ms[1] += b;
+    ms[2] += c;
   }
   h->t_count = 0;
   return NMMO_OK;
@@ -451,6 +481,44 @@ int nmmo_set_tasks(NmmoHandle* h, const NmmoTask* tasks, int32_t n_tasks, const 
   h->st.tasks = d_tasks;
   h->st.n_tasks = n_tasks;
   h->st.tev = tev;
+  return NMMO_OK;
+}
+
+int nmmo_set_wrapper(NmmoHandle* h, const NmmoWrapperConfig* wc, NmmoAgentInfo* dev_info) {
+  if (!h) return fail(NMMO_E_INVALID, "null handle");
+  HIP_TRY(hipSetDevice(h->device));
+  HIP_TRY(hipDeviceSynchronize());
+  if (!wc) {
+    h->wrap_on = false;
+    h->d_info = nullptr;
+    return NMMO_OK;
+  }
+  if (h->cfg.event_cap <= 0) return fail(NMMO_E_INVALID, "the wrapper layer needs the event log (event_cap > 0)");
+  if (wc->kind < NMMO_WRAP_BASE || wc->kind > NMMO_WRAP_YAOFENG) return fail(NMMO_E_INVALID, "wrapper kind %d", wc->kind);
+  if (wc->clip_unique_event < 0) return fail(NMMO_E_INVALID, "clip_unique_event < 0");
+  const size_t nP = (size_t)h->st.n_envs * h->st.P;
+  if (!h->d_ws) {
+    if (hipMalloc((void**)&h->d_ws, nP * sizeof(NmmoWrapState)) != hipSuccess ||
+        hipMalloc((void**)&h->d_uniq, nP * NMMO_UNIQ_WORDS * 4) != hipSuccess ||
+        hipMalloc((void**)&h->d_wenv, (size_t)h->st.n_envs * 4) != hipSuccess)
+      return fail(NMMO_E_NOMEM, "wrapper state allocation");
+  }
+  h->wc = *wc;
+  h->d_info = dev_info;
+  h->wrap_on = true;
+  HIP_TRY(launch_wrap(wrap_params(h, nullptr, nullptr, nullptr, nullptr, nullptr), 1, nullptr));
+  HIP_TRY(hipDeviceSynchronize());
+  return NMMO_OK;
+}
+
+int nmmo_get_wrapper_state(NmmoHandle* h, NmmoWrapState* host_state, uint32_t* host_uniq) {
+  if (!h || !host_state) return fail(NMMO_E_INVALID, "null argument");
+  if (!h->d_ws) return fail(NMMO_E_INVALID, "the wrapper layer was never enabled");
+  const size_t nP = (size_t)h->st.n_envs * h->st.P;
+  HIP_TRY(hipSetDevice(h->device));
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(host_state, h->d_ws, nP * sizeof(NmmoWrapState), hipMemcpyDeviceToHost));
+  if (host_uniq) HIP_TRY(hipMemcpy(host_uniq, h->d_uniq, nP * NMMO_UNIQ_WORDS * 4, hipMemcpyDeviceToHost));
   return NMMO_OK;
 }
 

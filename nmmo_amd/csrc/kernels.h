@@ -44,6 +44,29 @@ struct ObsParams {
   int o_style, o_target, o_buy, o_destroy, o_give_item, o_give_target, o_gg_price, o_gg_target,
       o_move, o_sell_item, o_sell_price, o_use, o_agent_id, o_tick, o_entity, o_inventory,
       o_market, o_task, o_tile;
+  // wrapper observation edits (SPEC §13): kWrapObs* bits, prev_price from the wrapper state
+  const NmmoWrapState* ws;  // [n][P] or NULL
+  int wflags;
+};
+constexpr int kWrapObsPrice = 1, kWrapObsNoGive = 2, kWrapObsNoDangerous = 4;
+
+struct WrapParams {
+  const int32_t* env;        // [n][NE]
+  const int16_t* ent;        // [n][NF][S]
+  const uint2* items;        // [n][P][kInv]
+  const int32_t* events;     // [n][evcap][NMMO_EVENT_COLS]
+  const NmmoTaskState* tstate;  // [n][P]
+  const int32_t* actions;    // [n][P][12] of this step, NULL on reset
+  float* rew;                // [n][P] shaped in place
+  const uint8_t* term;
+  const uint8_t* trunc;
+  const uint8_t* mask;
+  NmmoWrapState* ws;         // [n][P]
+  uint32_t* uniq;            // [n][P][NMMO_UNIQ_WORDS]
+  int32_t* wenv;             // [n] event rows already processed
+  NmmoAgentInfo* info;       // [n][P] caller-owned, may be NULL
+  NmmoWrapperConfig wc;
+  int n_envs, P, S, evcap, items_on;
 };
 
 struct PolicyParams {
@@ -68,5 +91,6 @@ hipError_t launch_tick(const DevState& st, const int32_t* actions, const uint64_
 hipError_t launch_rebuild_dep(const DevState& st, hipStream_t stream);
 hipError_t launch_obs(const ObsParams& p, hipStream_t stream);
 hipError_t launch_policy(const PolicyParams& p, hipStream_t stream);
+hipError_t launch_wrap(const WrapParams& p, int mode, hipStream_t stream);
 
 }  // namespace nmmo

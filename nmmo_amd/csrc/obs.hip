@@ -120,6 +120,7 @@ __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
 
     const int ninv = inv_count(inv);
+    const int prev_price = p.ws ? p.ws[(size_t)e * p.P + a].prev_price : -1;
     const int aid = T[F_ID * S + a];
     // ActionTargets [0, o_agent_id) (SPEC §8, §9)
     auto mask_val = [&](int j) -> bool {
@@ -161,6 +162,19 @@ __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
       } else {
         const int k = j - p.o_use;
         v = k == kInv || (item && k < ninv && item_usable(T, S, a, inv[k]));
+      }
+      if (p.wflags) {  // wrapper observation() edits (SPEC §13)
+        if ((p.wflags & kWrapObsPrice) && j >= p.o_sell_price && j < p.o_use && j - p.o_sell_price == prev_price)
+          v = false;
+        if ((p.wflags & kWrapObsNoGive) && j >= p.o_give_item && j < p.o_move) {
+          const bool keep = j == p.o_give_target - 1 || j == p.o_gg_price - 1 || j == p.o_gg_price ||
+                            j == p.o_move - 1;  // Give.InventoryItem/Target noop, Price 0, GiveGold noop
+          if (!keep) v = false;
+        }
+        if ((p.wflags & kWrapObsNoDangerous) && j >= p.o_target && j < p.o_buy) {
+          const int k = j - p.o_target;
+          if (k < nv && T[F_NPC_TYPE * S + vis[k]] > 1) v = false;
+        }
       }
       return v;
     };

@@ -53,6 +53,7 @@ class NmmoEngine:
         self.term = torch.zeros((n, P), dtype=torch.uint8, device=d)
         self.trunc = torch.zeros((n, P), dtype=torch.uint8, device=d)
         self.mask = torch.zeros((n, P), dtype=torch.uint8, device=d)
+        self.info = None
 
     def close(self):
         if getattr(self, "h", None) is not None and self.h.value:
@@ -107,6 +108,32 @@ class NmmoEngine:
                                               self._stream()), "nmmo_scripted_actions")
         return out
 
+    def set_wrapper(self, wc):
+        """Turn the device wrapper layer on (abi.NmmoWrapperConfig, e.g. from
+        nmmo_amd.wrappers.wrapper_config) or off (None). While on, rewards are shaped in place,
+        obs masks edited, and `self.info` (agent_info_dtype records [n_envs, P] as raw bytes on
+        the device) holds each agent's episode record on its final step (SPEC §13)."""
+        if wc is None:
+            check(lib().nmmo_set_wrapper(self.h, None, None), "nmmo_set_wrapper")
+            self.info = None
+            return
+        rec = abi.agent_info_dtype().itemsize
+        self.info = torch.zeros((self.n_envs, self.P, rec), dtype=torch.uint8, device=self.device)
+        self.wrapper = wc
+        check(lib().nmmo_set_wrapper(self.h, ctypes.byref(wc), self._ptr(self.info)), "nmmo_set_wrapper")
+
+    def info_records(self) -> np.ndarray:
+        """The device episode records as numpy agent_info_dtype [n_envs, P] (synchronous)."""
+        return self.info.cpu().numpy().view(abi.agent_info_dtype()).reshape(self.n_envs, self.P)
+
+    def wrapper_state(self):
+        """(NmmoWrapState records [n_envs, P], experienced bitsets u32 [n_envs, P, 153])."""
+        st = np.zeros((self.n_envs, self.P), abi.wrap_state_dtype())
+        uq = np.zeros((self.n_envs, self.P, abi.UNIQ_WORDS), np.uint32)
+        check(lib().nmmo_get_wrapper_state(self.h, st.ctypes.data_as(ctypes.c_void_p),
+                                           uq.ctypes.data_as(ctypes.c_void_p)), "nmmo_get_wrapper_state")
+        return st, uq
+
     def set_timing(self, enable: bool):
         check(lib().nmmo_set_timing(self.h, 1 if enable else 0), "nmmo_set_timing")
 
@@ -118,11 +145,11 @@ class NmmoEngine:
         check(lib().nmmo_set_counters(self.h, ptr), "nmmo_set_counters")
 
     def read_timing(self):
-        """(tick_ms_sum, obs_ms_sum, n_steps) from HIP events on the launch stream."""
-        ms = (ctypes.c_double * 2)()
+        """(tick_ms_sum, obs_ms_sum, n_steps, wrapper_ms_sum) from HIP events on the launch stream."""
+        ms = (ctypes.c_double * 3)()
         n = ctypes.c_int32()
         check(lib().nmmo_read_timing(self.h, ms, ctypes.byref(n)), "nmmo_read_timing")
-        return ms[0], ms[1], n.value
+        return ms[0], ms[1], n.value, ms[2]
 
     def get_state(self) -> np.ndarray:
         n = self.layout.state_bytes_per_env * self.n_envs

@@ -83,7 +83,7 @@ class GpuVecEnv:
 
     def __init__(self, env_creator=None, env_kwargs=None, num_envs=1, envs_per_worker=1,
                  envs_per_batch=None, env_pool=False, mask_agents=True, *, config=None,
-                 device=None, seed=0, task_embedding=None, env_index_base=0):
+                 device=None, seed=0, task_embedding=None, env_index_base=0, agent=None):
         del env_creator, envs_per_worker, env_pool  # the engine replaces workers and creators
         self.config = config or _config_from_kwargs(env_kwargs)
         if self.config.obs_layout != abi.OBS_FLAT:
@@ -97,6 +97,14 @@ class GpuVecEnv:
         self.mask_agents = mask_agents
         self.engine = NmmoEngine(self.config, self.num_envs, seed=seed, device=device,
                                  task_embedding=task_embedding, env_index_base=env_index_base)
+        # env_creator's RewardWrapper (environment.py:58) with the YAML reward_wrapper kwargs,
+        # run on the device (SPEC §13); agent=None keeps the bare env
+        rw = dict((env_kwargs or {}).get("reward_wrapper", {})) if isinstance(env_kwargs, dict) else {}
+        self.stat_prefix = rw.get("stat_prefix")
+        if agent is not None:
+            from .wrappers import wrapper_config
+
+            self.engine.set_wrapper(wrapper_config(agent, **rw))
         self.agents_per_env = self.config.PLAYER_N
         self.driver_env = DriverEnv(self.config, self.engine.obs_elems)
         self.single_observation_space = self.driver_env.single_observation_space
@@ -126,7 +134,24 @@ class GpuVecEnv:
         t = e.trunc.view(N)
         mask = e.mask.view(N).to(torch.bool).cpu().numpy()
         self._ready = False
-        return o, r, d, t, [], self.env_id, mask
+        return o, r, d, t, self._infos(), self.env_id, mask
+
+    def _infos(self):
+        """Per env {agent_id: info} of the agents whose episode ended this step (BaseStatWrapper's
+        info dicts, stat_wrapper.py:128-185); empty dicts without the wrapper layer. Only the
+        records of finished agents cross to the host."""
+        e = self.engine
+        if e.info is None:
+            return [{} for _ in range(self.num_envs)]
+        from .wrappers import infos_from_records
+
+        done = (e.term | e.trunc).view(-1).nonzero().view(-1)
+        recs = np.zeros((self.num_envs, self.agents_per_env), abi.agent_info_dtype())
+        if done.numel():
+            rows = e.info.view(-1, e.info.shape[-1]).index_select(0, done).cpu().numpy()
+            idx = done.cpu().numpy()
+            recs.reshape(-1)[idx] = rows.view(abi.agent_info_dtype()).reshape(-1)
+        return infos_from_records(recs, stat_prefix=self.stat_prefix)
 
     def send(self, actions):
         a = torch.as_tensor(actions)

@@ -127,3 +127,36 @@ def test_state_blob_size(native):
         lay = _native.layout(Config.preset(preset).to_c())
         assert lay.slots == slots
         assert lay.state_bytes_per_env == abi.state_bytes_per_env(slots)
+
+
+def test_wrapper_structs_match_c_compiler():
+    src = r"""
+#include <stdio.h>
+#include <stddef.h>
+#include "nmmo_hip.h"
+int main(void) {
+  printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(NmmoWrapperConfig),
+         offsetof(NmmoWrapperConfig, heal_bonus_weight), offsetof(NmmoWrapperConfig, custom_bonus_scale),
+         sizeof(NmmoAgentInfo), offsetof(NmmoAgentInfo, performed), offsetof(NmmoAgentInfo, unique_events),
+         sizeof(NmmoWrapState), offsetof(NmmoWrapState, max_item_level), (size_t)NMMO_UNIQ_WORDS);
+  return 0;
+}
+"""
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "t.c")
+        open(c, "w").write(src)
+        exe = os.path.join(d, "t")
+        subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), c, "-o", exe])
+        got = list(map(int, subprocess.check_output([exe]).split()))
+    info, ws = abi.agent_info_dtype(), abi.wrap_state_dtype()
+    want = [ctypes.sizeof(abi.NmmoWrapperConfig), abi.NmmoWrapperConfig.heal_bonus_weight.offset,
+            abi.NmmoWrapperConfig.custom_bonus_scale.offset, info.itemsize, info.fields["performed"][1],
+            info.fields["unique_events"][1], ws.itemsize, ws.fields["max_item_level"][1], abi.UNIQ_WORDS]
+    assert got == want
+    # 17 event codes x 18 item/skill types x 16 levels fit the experienced bitset
+    assert abi.UNIQ_WORDS * 32 >= 17 * 18 * 16
+
+
+def test_set_wrapper_rejects_bad_handles(native):
+    assert native.nmmo_set_wrapper(None, None, None) == abi.NMMO_E_INVALID
+    assert native.nmmo_get_wrapper_state(None, None, None) == abi.NMMO_E_INVALID
