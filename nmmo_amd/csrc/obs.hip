@@ -46,6 +46,9 @@ __device__ inline void wave_zero(float* row, int lo, int hi) {
   if (tail0 + lane < hi) obs_st(&row[tail0 + lane], 0.f);
 }
 
+// kWrap: the wrapper's observation() edits are compiled in (SPEC §13). Both variants stay at
+// 79 VGPRs = 6 waves/SIMD (a run-time flag check in the shared body cost 2 VGPRs and a wave).
+template <bool kWrap>
 __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int S = p.S;
@@ -120,7 +123,7 @@ __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
 
     const int ninv = inv_count(inv);
-    const int prev_price = p.ws ? p.ws[(size_t)e * p.P + a].prev_price : -1;
+    const int prev_price = kWrap && p.ws ? __builtin_amdgcn_readfirstlane(p.ws[(size_t)e * p.P + a].prev_price) : -1;
     const int aid = T[F_ID * S + a];
     // ActionTargets [0, o_agent_id) (SPEC §8, §9)
     auto mask_val = [&](int j) -> bool {
@@ -163,7 +166,7 @@ __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
         const int k = j - p.o_use;
         v = k == kInv || (item && k < ninv && item_usable(T, S, a, inv[k]));
       }
-      if (p.wflags) {  // wrapper observation() edits (SPEC §13)
+      if constexpr (kWrap) {  // wrapper observation() edits (SPEC §13)
         if ((p.wflags & kWrapObsPrice) && j >= p.o_sell_price && j < p.o_use && j - p.o_sell_price == prev_price)
           v = false;
         if ((p.wflags & kWrapObsNoGive) && j >= p.o_give_item && j < p.o_move) {
@@ -208,7 +211,10 @@ __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
 
 hipError_t launch_obs(const ObsParams& p, hipStream_t stream) {
   dim3 grid(p.n_envs, (p.P + kObsAgentsPerBlock - 1) / kObsAgentsPerBlock);
-  hipLaunchKernelGGL(obs_kernel, grid, dim3(64 * kObsWaves), obs_lds_bytes(p.S), stream, p);
+  if (p.wflags)
+    hipLaunchKernelGGL(obs_kernel<true>, grid, dim3(64 * kObsWaves), obs_lds_bytes(p.S), stream, p);
+  else
+    hipLaunchKernelGGL(obs_kernel<false>, grid, dim3(64 * kObsWaves), obs_lds_bytes(p.S), stream, p);
   return hipGetLastError();
 }
 

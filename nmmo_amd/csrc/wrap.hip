@@ -51,6 +51,18 @@ __host__ __device__ inline int key_event_bit(int code) {
   }
 }
 
+// entity fields phase 2 reads (skill levels/exps in nmmo skill order melee..alchemy)
+enum : int {
+  WF_ALIVE, WF_HEALTH_RESTORE, WF_HEALTH, WF_GOLD, WF_DAMAGE, WF_FOOD, WF_WATER, WF_LVL0,
+  WF_EXP0 = WF_LVL0 + 8, kWrapFields = WF_EXP0 + 8
+};
+__constant__ const int kWrapField[kWrapFields] = {
+    F_ALIVE, F_HEALTH_RESTORE, F_HEALTH, F_GOLD, F_DAMAGE, F_FOOD, F_WATER,
+    F_MELEE_LEVEL, F_RANGE_LEVEL, F_MAGE_LEVEL, F_FISHING_LEVEL, F_HERBALISM_LEVEL,
+    F_PROSPECTING_LEVEL, F_CARVING_LEVEL, F_ALCHEMY_LEVEL,
+    F_MELEE_EXP, F_RANGE_EXP, F_MAGE_EXP, F_FISHING_EXP, F_HERBALISM_EXP,
+    F_PROSPECTING_EXP, F_CARVING_EXP, F_ALCHEMY_EXP};
+
 __device__ inline void ws_init(NmmoWrapState& w) {
   w.cum_reward = 0.0;
   w.prev_count = w.curr_count = 0;
@@ -95,10 +107,33 @@ __global__ void __launch_bounds__(kWrapThreads) wrap_kernel(WrapParams p, int mo
     if (tid == 0) p.wenv[e] = mode == 1 ? evc : 0;  // rows logged before this point are not ours
     return;
   }
-  for (int a = tid; a < 128; a += blockDim.x) {
-    cnt[a] = dmg[a] = maxdist[a] = earned[a] = maxdmg[a] = ak[a] = nk[a] = 0;
-    perf[a] = 0u;
-    for (int k = 0; k < 5; k++) lvl[k][a] = -1;
+  // the agent's inputs are loaded before the event walk so their latency overlaps it
+  // (blockDim = 128 >= P: thread a owns agent a)
+  const int a = tid;
+  const bool mine = a < P;
+  const size_t o = (size_t)e * P + (mine ? a : 0);
+  const int16_t* T = p.ent + (size_t)e * NMMO_NF * S;
+  NmmoWrapState w;
+  NmmoTaskState ts;
+  int f[kWrapFields];
+  uint8_t present = 0, term8 = 0, trunc8 = 0;
+  float raw = 0.f;
+  int price = 0;
+  if (mine) {
+    w = ws[a];
+    present = p.mask[o];
+    term8 = p.term[o];
+    trunc8 = p.trunc[o];
+    raw = p.rew[o];
+    ts = p.tstate[o];
+    if (p.actions) price = p.actions[o * kHeads + 10];
+#pragma unroll
+    for (int k = 0; k < kWrapFields; k++) f[k] = T[kWrapField[k] * S + a];
+  }
+  for (int i = tid; i < 128; i += blockDim.x) {
+    cnt[i] = dmg[i] = maxdist[i] = earned[i] = maxdmg[i] = ak[i] = nk[i] = 0;
+    perf[i] = 0u;
+    for (int k = 0; k < 5; k++) lvl[k][i] = -1;
   }
   __syncthreads();
   // phase 1: this tick's rows (env ring, SPEC §11) -> per-agent terms
@@ -108,46 +143,43 @@ __global__ void __launch_bounds__(kWrapThreads) wrap_kernel(WrapParams p, int mo
   const int32_t* ring = p.events + (size_t)e * cap * NMMO_EVENT_COLS;
   for (int i = lo + tid; i < evc; i += blockDim.x) {
     const int32_t* r = ring + (size_t)(i % cap) * NMMO_EVENT_COLS;
-    const int a = r[1] - 1, code = r[3], type = r[4], level = r[5], num = r[6], gold = r[7], tgt = r[8];
-    if (a < 0 || a >= P) continue;
+    const int ag = r[1] - 1, code = r[3], type = r[4], level = r[5], num = r[6], gold = r[7], tgt = r[8];
+    if (ag < 0 || ag >= P) continue;
     const int ci = ev_index(code);
     bool fresh = false;
     if (ci >= 0 && type >= 0 && type < 18 && level >= 0 && level < 16) {
       const int b = (ci * 18 + type) * 16 + level;
       const uint32_t bit = 1u << (b & 31);
-      fresh = (atomicOr(&uq[a * NMMO_UNIQ_WORDS + (b >> 5)], bit) & bit) == 0u;
+      fresh = (atomicOr(&uq[ag * NMMO_UNIQ_WORDS + (b >> 5)], bit) & bit) == 0u;
     }
-    if (fresh || code == EV_PLAYER_KILL || code == EV_EARN_GOLD) atomicAdd(&cnt[a], 1);
+    if (fresh || code == EV_PLAYER_KILL || code == EV_EARN_GOLD) atomicAdd(&cnt[ag], 1);
     unsigned int pb = 0u;
     const int kb = key_event_bit(code);
     if (kb >= 0) pb |= 1u << kb;
     const int cat = item_category(type);
     if (code == EV_EQUIP_ITEM && cat >= 0 && cat < 4) pb |= 1u << (8 + cat);
     if (code == EV_HARVEST_ITEM && cat == 1) pb |= 1u << 12;
-    if (pb) atomicOr(&perf[a], pb);
+    if (pb) atomicOr(&perf[ag], pb);
     switch (code) {
-      case EV_GO_FARTHEST: atomicMax(&maxdist[a], num); break;
-      case EV_EARN_GOLD: atomicAdd(&earned[a], gold); break;
+      case EV_GO_FARTHEST: atomicMax(&maxdist[ag], num); break;
+      case EV_EARN_GOLD: atomicAdd(&earned[ag], gold); break;
       case EV_SCORE_HIT:
-        atomicMax(&maxdmg[a], num);
-        atomicAdd(&dmg[a], num);
+        atomicMax(&maxdmg[ag], num);
+        atomicAdd(&dmg[ag], num);
         break;
       case EV_PLAYER_KILL:
-        if (tgt > 0) atomicAdd(&ak[a], 1);
-        if (tgt < 0) atomicAdd(&nk[a], 1);
+        if (tgt > 0) atomicAdd(&ak[ag], 1);
+        if (tgt < 0) atomicAdd(&nk[ag], 1);
         break;
       default: break;
     }
     if ((code == EV_HARVEST_ITEM || code == EV_LOOT_ITEM || code == EV_BUY_ITEM) && cat >= 0)
-      atomicMax(&lvl[cat][a], level);
+      atomicMax(&lvl[cat][ag], level);
   }
   __syncthreads();
   // phase 2: thread per agent
   const NmmoWrapperConfig& wc = p.wc;
-  const int16_t* T = p.ent + (size_t)e * NMMO_NF * S;
-  for (int a = tid; a < P; a += blockDim.x) {
-    const size_t o = (size_t)e * P + a;
-    NmmoWrapState w = ws[a];
+  if (mine) {
     // event accumulators: every row of this tick belongs to an agent present at tick start
     w.performed |= perf[a];
     w.max_dist = max(w.max_dist, maxdist[a]);
@@ -157,23 +189,22 @@ __global__ void __launch_bounds__(kWrapThreads) wrap_kernel(WrapParams p, int mo
     w.agent_kills += ak[a];
     w.npc_kills += nk[a];
     w.dmg_inflicted += dmg[a];
-    if (!p.mask[o]) {
-      ws[a] = w;
-      if (info) info[a].done = 0;
-      continue;
-    }
+  }
+  if (mine && !present) {
+    ws[a] = w;
+    if (info) info[a].done = 0;
+  } else if (mine) {
     w.prev_count = w.curr_count;
     w.curr_count += cnt[a];
-    const bool term = p.term[o] != 0, trunc = p.trunc[o] != 0, done = term || trunc;
-    const float raw = p.rew[o];
+    const bool term = term8 != 0, trunc = trunc8 != 0, done = term || trunc;
     if (!done) w.cum_reward = __dadd_rn(w.cum_reward, (double)raw);
-    const bool in_realm = T[F_ALIVE * S + a] != 0;
+    const bool in_realm = f[WF_ALIVE] != 0;
     double rd = (double)raw;
     if (!wc.use_custom_reward) {
       rd = term ? 0.0 : rd;
     } else if (wc.kind == NMMO_WRAP_START_KIT) {
       double heal = 0.0, explore = 0.0;
-      if (wc.heal_bonus_weight > 0.0 && in_realm && T[F_HEALTH_RESTORE * S + a] > 0) heal = wc.heal_bonus_weight;
+      if (wc.heal_bonus_weight > 0.0 && in_realm && f[WF_HEALTH_RESTORE] > 0) heal = wc.heal_bonus_weight;
       if (wc.explore_bonus_weight > 0.0 && w.curr_count > w.prev_count)
         explore = __dmul_rn((double)min(wc.clip_unique_event, w.curr_count - w.prev_count), wc.explore_bonus_weight);
       rd = __dadd_rn(rd, __dadd_rn(heal, explore));
@@ -183,11 +214,11 @@ __global__ void __launch_bounds__(kWrapThreads) wrap_kernel(WrapParams p, int mo
                                      wc.explore_bonus_weight));
     } else if (wc.kind == NMMO_WRAP_YAOFENG) {
       if (!done) {
-        const int hp = T[F_HEALTH * S + a];
+        const int hp = f[WF_HEALTH];
         const double hp_b = __dmul_rn((double)(hp - w.hp), wc.hp_bonus_weight);
         w.hp = hp;
-        int xp = T[F_MELEE_EXP * S + a];
-        for (int k = 1; k < 8; k++) xp = max(xp, (int)T[(F_MELEE_EXP + 2 * k) * S + a]);
+        int xp = f[WF_EXP0];
+        for (int k = 1; k < 8; k++) xp = max(xp, f[WF_EXP0 + k]);
         const double exp_b = __dmul_rn((double)(xp - w.exp), wc.exp_bonus_weight);
         w.exp = xp;
         int D = 0;
@@ -201,7 +232,7 @@ __global__ void __launch_bounds__(kWrapThreads) wrap_kernel(WrapParams p, int mo
         const double def_b = __dmul_rn(wc.defense_bonus_weight, __ddiv_rn((double)(3 * D), 45.0));
         const double atk_b = __dmul_rn((double)(w.dmg_inflicted - w.dmg_inflicted_prev), wc.attack_bonus_weight);
         w.dmg_inflicted_prev = w.dmg_inflicted;
-        const int gold = T[F_GOLD * S + a];
+        const int gold = f[WF_GOLD];
         const double gold_b = __dmul_rn((double)(gold - w.gold), wc.gold_bonus_weight);
         w.gold = gold;
         const double sum = __dadd_rn(__dadd_rn(__dadd_rn(__dadd_rn(hp_b, exp_b), def_b), atk_b), gold_b);
@@ -209,27 +240,22 @@ __global__ void __launch_bounds__(kWrapThreads) wrap_kernel(WrapParams p, int mo
       }
     }
     p.rew[o] = (float)rd;
-    if (p.actions) {  // start kit action(): the Sell.Price index of this step
-      const int pr = p.actions[o * kHeads + 10];
-      w.prev_price = pr;
-    }
+    if (p.actions) w.prev_price = price;  // start kit action(): the Sell.Price index of this step
     if (info) {
       if (done) {
         NmmoAgentInfo r;
-        const NmmoTaskState ts = p.tstate[o];
         r.done = 1;
         r.length = tick;
         r.ret = wc.eval_mode ? ts.max_progress : w.cum_reward;
         r.max_progress = ts.max_progress;
         r.reward_signal_count = ts.signals;
         r.task_completed = ts.completed_tick != 0;
-        r.cod_attacked = term && T[F_DAMAGE * S + a] > 0;
-        r.cod_starved = term && T[F_FOOD * S + a] == 0;
-        r.cod_dehydrated = term && T[F_WATER * S + a] == 0;
-        r.max_combat_level = max((int)T[F_MELEE_LEVEL * S + a], max((int)T[F_RANGE_LEVEL * S + a], (int)T[F_MAGE_LEVEL * S + a]));
-        r.max_harvest_skill_ammo = max((int)T[F_PROSPECTING_LEVEL * S + a],
-                                       max((int)T[F_CARVING_LEVEL * S + a], (int)T[F_ALCHEMY_LEVEL * S + a]));
-        r.max_harvest_skill_consum = max((int)T[F_FISHING_LEVEL * S + a], (int)T[F_HERBALISM_LEVEL * S + a]);
+        r.cod_attacked = term && f[WF_DAMAGE] > 0;
+        r.cod_starved = term && f[WF_FOOD] == 0;
+        r.cod_dehydrated = term && f[WF_WATER] == 0;
+        r.max_combat_level = max(f[WF_LVL0], max(f[WF_LVL0 + 1], f[WF_LVL0 + 2]));
+        r.max_harvest_skill_ammo = max(f[WF_LVL0 + 5], max(f[WF_LVL0 + 6], f[WF_LVL0 + 7]));
+        r.max_harvest_skill_consum = max(f[WF_LVL0 + 3], f[WF_LVL0 + 4]);
         r.performed = w.performed;
         r.max_progress_to_center = w.max_dist;
         r.earned_gold = w.earned_gold;
