@@ -65,6 +65,11 @@ extern "C" {
 /* ---- observation layouts ---- */
 #define NMMO_OBS_NONE 0   /* C2/C3 benchmark configs: state only */
 #define NMMO_OBS_FLAT 1   /* pufferlib-0.7.3 flat float32 vector, 23,987 / agent */
+#define NMMO_OBS_NATIVE 2 /* nmmo space dtypes, Market once per env (SPEC.md §8b) */
+#define NMMO_NATIVE_MASK_BYTES 1600   /* u8 ActionTargets (1,586) + pad */
+#define NMMO_NATIVE_I16 3976          /* int16 part of an agent row */
+#define NMMO_NATIVE_ROW_BYTES (NMMO_NATIVE_MASK_BYTES + 2 * NMMO_NATIVE_I16)  /* 9,552 */
+#define NMMO_NATIVE_MARKET_BYTES (NMMO_MARKET_ROWS * 16 * 2)               /* 32,768 per env */
 
 /* ---- items (SPEC.md §9): per player NMMO_INV_SLOTS inventory slots in ascending item-row
  * order, each item two u32 words: w0 = type | level<<5 | equipped<<9 | listed_price<<10 |
@@ -268,7 +273,9 @@ NMMO_API int nmmo_reset(NmmoHandle* h, const uint64_t* env_seeds, void* obs, uin
 
 /* One tick of every env. actions: device int32 [n_envs][player_n][12]. Envs whose previous
  * step ended the episode are reset instead (pufferlib auto-reset), with rewards/flags 0.
- * obs: device float32 [n_envs][player_n][obs_elems] (NMMO_OBS_FLAT) or NULL (NMMO_OBS_NONE).
+ * obs: device float32 [n_envs][player_n][obs_elems] (NMMO_OBS_FLAT), the native layout
+ * [n_envs] x (player_n x NMMO_NATIVE_ROW_BYTES + NMMO_NATIVE_MARKET_BYTES) (NMMO_OBS_NATIVE),
+ * or NULL (NMMO_OBS_NONE).
  * rew f32, term/trunc/mask u8: device [n_envs][player_n]. */
 NMMO_API int nmmo_step(NmmoHandle* h, const int32_t* actions, void* obs, float* rew, uint8_t* term,
               uint8_t* trunc, uint8_t* mask, void* stream);
@@ -291,6 +298,12 @@ NMMO_API int nmmo_set_tasks(NmmoHandle* h, const NmmoTask* tasks, int32_t n_task
 NMMO_API int nmmo_set_wrapper(NmmoHandle* h, const NmmoWrapperConfig* wc, NmmoAgentInfo* dev_info);
 /* host NmmoWrapState [n_envs][player_n] + u32 [n_envs][player_n][NMMO_UNIQ_WORDS]. Synchronous. */
 NMMO_API int nmmo_get_wrapper_state(NmmoHandle* h, NmmoWrapState* host_state, uint32_t* host_uniq);
+
+/* Native -> flat obs (SPEC.md §8b): native device [n_envs] x (player_n rows + market) as
+ * written by nmmo_step under NMMO_OBS_NATIVE, flat device float32 [n_envs][player_n][obs_elems]
+ * (the pufferlib layout, bit-identical to what NMMO_OBS_FLAT writes). n_envs may be any count
+ * of consecutive envs (e.g. a learner expanding gathered shards). Enqueued on `stream`. */
+NMMO_API int nmmo_expand_obs(NmmoHandle* h, const void* native, float* flat, int32_t n_envs, void* stream);
 
 /* Masked-uniform scripted actions from the current state (bench / tests). */
 NMMO_API int nmmo_scripted_actions(NmmoHandle* h, uint64_t policy_seed, int32_t* actions, void* stream);

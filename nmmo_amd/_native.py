@@ -20,7 +20,7 @@ SYMBOLS = [
     "nmmo_default_config", "nmmo_layout", "nmmo_create", "nmmo_destroy", "nmmo_reset",
     "nmmo_step", "nmmo_scripted_actions", "nmmo_get_state", "nmmo_set_state",
     "nmmo_get_map_bank", "nmmo_set_timing", "nmmo_read_timing", "nmmo_set_counters", "nmmo_get_events", "nmmo_set_tasks",
-    "nmmo_set_wrapper", "nmmo_get_wrapper_state", "nmmo_n_envs",
+    "nmmo_set_wrapper", "nmmo_get_wrapper_state", "nmmo_expand_obs", "nmmo_n_envs",
     "nmmo_last_error", "nmmo_abi_version",
 ]
 
@@ -61,6 +61,7 @@ def lib():
     L.nmmo_set_tasks.argtypes = [vp, vp, i32, vp, vp]
     L.nmmo_set_wrapper.argtypes = [vp, ctypes.POINTER(abi.NmmoWrapperConfig), vp]
     L.nmmo_get_wrapper_state.argtypes = [vp, vp, vp]
+    L.nmmo_expand_obs.argtypes = [vp, vp, vp, i32, vp]
     L.nmmo_n_envs.argtypes = [vp]
     L.nmmo_last_error.restype = ctypes.c_char_p
     L.nmmo_abi_version.restype = i32

@@ -26,6 +26,16 @@ SYS_ALL = 0xFF
 
 OBS_NONE = 0
 OBS_FLAT = 1
+OBS_NATIVE = 2
+# native layout (SPEC.md §8b)
+NATIVE_MASK_BYTES = 1600
+NATIVE_I16 = 3976
+NATIVE_ROW_BYTES = NATIVE_MASK_BYTES + 2 * NATIVE_I16
+NATIVE_MARKET_BYTES = 1024 * 16 * 2
+
+
+def native_env_bytes(players: int = 128) -> int:
+    return players * NATIVE_ROW_BYTES + NATIVE_MARKET_BYTES
 
 MAP_SIZE = 160
 MAP_TILES = MAP_SIZE * MAP_SIZE

@@ -178,7 +178,7 @@ int nmmo_create(const NmmoConfig* cfg, int32_t n_envs, uint64_t seed, int32_t de
   if (cfg->horizon <= 0 || cfg->task_num_tick <= 0) return fail(NMMO_E_INVALID, "horizon/task_num_tick");
   if (cfg->task_embed_dim < 0 || cfg->task_embed_dim > 65536) return fail(NMMO_E_INVALID, "task_embed_dim");
   if (cfg->event_cap < 0 || cfg->event_cap > (1 << 24)) return fail(NMMO_E_INVALID, "event_cap in 0..2^24");
-  if (cfg->obs_layout != NMMO_OBS_NONE && cfg->obs_layout != NMMO_OBS_FLAT)
+  if (cfg->obs_layout != NMMO_OBS_NONE && cfg->obs_layout != NMMO_OBS_FLAT && cfg->obs_layout != NMMO_OBS_NATIVE)
     return fail(NMMO_E_INVALID, "obs_layout %d", cfg->obs_layout);
   NmmoHandle* h = new NmmoHandle();
   h->cfg = *cfg;
@@ -235,10 +235,13 @@ int nmmo_create(const NmmoConfig* cfg, int32_t n_envs, uint64_t seed, int32_t de
   return NMMO_OK;
 }
 
-static ObsParams obs_params(NmmoHandle* h, float* obs) {
+static ObsParams obs_params(NmmoHandle* h, void* obs) {
   const NmmoLayout& L = h->layout;
   ObsParams p;
-  p.env = h->d_env; p.ent = h->d_ent; p.mat = h->d_mat; p.task = h->d_task; p.obs = obs;
+  const bool native = h->cfg.obs_layout == NMMO_OBS_NATIVE;
+  p.env = h->d_env; p.ent = h->d_ent; p.mat = h->d_mat; p.task = h->d_task;
+  p.obs = native ? nullptr : (float*)obs;
+  p.nat = native ? (uint8_t*)obs : nullptr;
   p.items = h->d_items; p.mlist = h->d_mlist; p.mcount = h->d_mcount; p.assign = h->d_assign;
   p.n_envs = h->st.n_envs; p.P = h->st.P; p.S = h->st.S; p.elems = L.obs_elems;
   p.task_dim = h->cfg.task_embed_dim; p.systems = h->cfg.systems;
@@ -284,7 +287,7 @@ int nmmo_reset(NmmoHandle* h, const uint64_t* env_seeds, void* obs, uint8_t* mas
   HIP_TRY(launch_tick(h->st, nullptr, env_seeds ? h->d_seeds : nullptr, nullptr, nullptr, nullptr,
                       mask, 1, s));
   if (h->wrap_on) HIP_TRY(launch_wrap(wrap_params(h, nullptr, nullptr, nullptr, nullptr, nullptr), 0, s));
-  if (obs && h->cfg.obs_layout == NMMO_OBS_FLAT) HIP_TRY(launch_obs(obs_params(h, (float*)obs), s));
+  if (obs && h->cfg.obs_layout != NMMO_OBS_NONE) HIP_TRY(launch_obs(obs_params(h, obs), s));
   return NMMO_OK;
 }
 
@@ -301,12 +304,23 @@ int nmmo_step(NmmoHandle* h, const int32_t* actions, void* obs, float* rew, uint
   if (rec) HIP_TRY(hipEventRecord(ev[1], s));
   if (h->wrap_on) HIP_TRY(launch_wrap(wrap_params(h, actions, rew, term, trunc, mask), 0, s));
   if (rec) HIP_TRY(hipEventRecord(ev[2], s));  // wrapper span = ev[1]..ev[2] (empty when off)
-  const bool do_obs = obs && h->cfg.obs_layout == NMMO_OBS_FLAT;
-  if (do_obs) HIP_TRY(launch_obs(obs_params(h, (float*)obs), s));
+  const bool do_obs = obs && h->cfg.obs_layout != NMMO_OBS_NONE;
+  if (do_obs) HIP_TRY(launch_obs(obs_params(h, obs), s));
   if (rec) {
     HIP_TRY(hipEventRecord(ev[3], s));  // obs span = ev[2]..ev[3] (empty when no obs)
     h->t_count++;
   }
+  return NMMO_OK;
+}
+
+int nmmo_expand_obs(NmmoHandle* h, const void* native, float* flat, int32_t n_envs, void* stream) {
+  if (!h || !native || !flat) return fail(NMMO_E_INVALID, "null argument");
+  if (n_envs <= 0) return fail(NMMO_E_INVALID, "n_envs must be > 0");
+  ObsParams p = obs_params(h, nullptr);
+  p.nat = (uint8_t*)native;
+  p.obs = flat;
+  p.n_envs = n_envs;
+  HIP_TRY(launch_expand(p, (hipStream_t)stream));
   return NMMO_OK;
 }
 

@@ -36,7 +36,8 @@ struct ObsParams {
   const int* mcount;    // [n]
   const float* task;    // [n_tasks][task_dim] Task obs per task
   const int32_t* assign; // [n][P]
-  float* obs;           // [n][P][elems]
+  float* obs;           // [n][P][elems] (flat layout)
+  uint8_t* nat;         // native layout (SPEC §8b) instead of obs when non-NULL
   int n_envs, P, S, elems, task_dim;
   uint32_t systems;
   int spawn_immunity;
@@ -90,6 +91,7 @@ hipError_t launch_tick(const DevState& st, const int32_t* actions, const uint64_
                        hipStream_t stream);
 hipError_t launch_rebuild_dep(const DevState& st, hipStream_t stream);
 hipError_t launch_obs(const ObsParams& p, hipStream_t stream);
+hipError_t launch_expand(const ObsParams& p, hipStream_t stream);  // native -> flat (SPEC §8b)
 hipError_t launch_policy(const PolicyParams& p, hipStream_t stream);
 hipError_t launch_wrap(const WrapParams& p, int mode, hipStream_t stream);
 

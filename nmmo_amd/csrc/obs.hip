@@ -46,9 +46,22 @@ __device__ inline void wave_zero(float* row, int lo, int hi) {
   if (tail0 + lane < hi) obs_st(&row[tail0 + lane], 0.f);
 }
 
+// native layout (SPEC §8b): int16 part offsets, env stride, two int16 per dword store
+constexpr int kNatEntity = 2, kNatInv = kNatEntity + kNObs * NMMO_N_ENTITY_COLS,
+              kNatTile = kNatInv + kInv * 16, kNatTask = kNatTile + 225 * 3;
+static_assert(kNatTask < NMMO_NATIVE_I16, "native int16 part overflows its row");
+__host__ __device__ inline size_t native_env_bytes(int P) {
+  return (size_t)P * NMMO_NATIVE_ROW_BYTES + NMMO_NATIVE_MARKET_BYTES;
+}
+__device__ __forceinline__ uint32_t i16pack(int lo, int hi) {
+  return (uint32_t)(uint16_t)(int16_t)lo | ((uint32_t)(uint16_t)(int16_t)hi << 16);
+}
+
 // kWrap: the wrapper's observation() edits are compiled in (SPEC §13). Both variants stay at
 // 79 VGPRs = 6 waves/SIMD (a run-time flag check in the shared body cost 2 VGPRs and a wave).
-template <bool kWrap>
+// kNative: the nmmo-dtype layout of SPEC §8b (u8 masks, int16 fields, Market once per env,
+// task index) instead of pufferlib's float32 row: ~10x fewer bytes per agent.
+template <bool kWrap, bool kNative>
 __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int S = p.S;
@@ -84,6 +97,18 @@ __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
     if (T[F_ALIVE * S + s]) rowslot[T[F_DS_ROW * S + s]] = (int16_t)s;
   __syncthreads();
 
+  if constexpr (kNative) {  // the env's Market, once per env (the y == 0 workgroup)
+    if (g == 0) {
+      uint32_t* mk = reinterpret_cast<uint32_t*>(p.nat + (size_t)e * native_env_bytes(p.P) +
+                                                 (size_t)p.P * NMMO_NATIVE_ROW_BYTES);
+      for (int j2 = tid; j2 < NMMO_MARKET_ROWS * 8; j2 += blockDim.x) {
+        const int j = 2 * j2, k = j >> 4;
+        uint32_t v = 0u;
+        if (k < nm) v = i16pack((int)item_col(mitem[k], mown[k] + 1, j & 15), (int)item_col(mitem[k], mown[k] + 1, (j + 1) & 15));
+        mk[j2] = v;
+      }
+    }
+  }
   const int lane = lane_id(), w = wave_id();
   int16_t* vis = vis_all + w * 128;
   const uint8_t* mat = p.mat + (size_t)e * kTiles;
@@ -95,9 +120,15 @@ __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
   for (int i = w; i < kObsAgentsPerBlock; i += kObsWaves) {
     const int a = g * kObsAgentsPerBlock + i;
     if (a >= p.P) break;
-    float* row = p.obs + ((size_t)e * p.P + a) * p.elems;
+    float* row = kNative ? nullptr : p.obs + ((size_t)e * p.P + a) * p.elems;
+    uint8_t* nrow = kNative ? p.nat + (size_t)e * native_env_bytes(p.P) + (size_t)a * NMMO_NATIVE_ROW_BYTES : nullptr;
     if (!T[F_ALIVE * S + a]) {
-      wave_zero(row, 0, p.elems);
+      if constexpr (kNative) {
+        uint4* z = reinterpret_cast<uint4*>(nrow);
+        for (int j = lane; j < NMMO_NATIVE_ROW_BYTES / 16; j += 64) z[j] = make_uint4(0u, 0u, 0u, 0u);
+      } else {
+        wave_zero(row, 0, p.elems);
+      }
       continue;
     }
     const int r = T[F_ROW * S + a], c = T[F_COL * S + a];
@@ -181,6 +212,43 @@ __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
       }
       return v;
     };
+    if constexpr (kNative) {
+      // masks: 4 bytes per lane per store
+      uint32_t* m32 = reinterpret_cast<uint32_t*>(nrow);
+      for (int j4 = lane; j4 < NMMO_NATIVE_MASK_BYTES / 4; j4 += 64) {
+        uint32_t v = 0u;
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+          const int j = 4 * j4 + b;
+          if (j < p.o_agent_id && mask_val(j)) v |= 1u << (8 * b);
+        }
+        m32[j4] = v;
+      }
+      // int16 part: AgentId, CurrentTick, Entity, Inventory, Tile, task index, pads (SPEC §8b)
+      const int task_idx = p.assign[(size_t)e * p.P + a];
+      auto i16v = [&](int i) -> int {
+        if (i == 0) return aid;
+        if (i == 1) return tick;
+        if (i < kNatInv) {
+          const int jj = i - kNatEntity, k = jj / NMMO_N_ENTITY_COLS, f = jj - k * NMMO_N_ENTITY_COLS;
+          return k < nv ? (int)T[f * S + vis[k]] : 0;
+        }
+        if (i < kNatTile) {
+          const int jj = i - kNatInv, k = jj >> 4;
+          return k < ninv ? (int)item_col(inv[k], aid, jj & 15) : 0;
+        }
+        if (i < kNatTask) {
+          const int jj = i - kNatTile, t = jj / 3, comp = jj - 3 * t;
+          const int tr = r + t / 15 - kVision, tc = c + t % 15 - kVision;
+          return comp == 0 ? tr : comp == 1 ? tc : (int)mat[tr * kSize + tc];
+        }
+        return i == kNatTask ? task_idx : 0;
+      };
+      uint32_t* d32 = reinterpret_cast<uint32_t*>(nrow + NMMO_NATIVE_MASK_BYTES);
+      for (int j2 = lane; j2 < NMMO_NATIVE_I16 / 2; j2 += 64) d32[j2] = i16pack(i16v(2 * j2), i16v(2 * j2 + 1));
+      __builtin_amdgcn_wave_barrier();
+      continue;
+    }
     for (int j = lane; j < p.o_agent_id; j += 64) obs_st(&row[j], mask_val(j) ? 1.f : 0.f);
     if (lane == 0) obs_st(&row[p.o_agent_id], (float)aid);
     if (lane == 1) obs_st(&row[p.o_tick], (float)tick);
@@ -211,10 +279,62 @@ __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
 
 hipError_t launch_obs(const ObsParams& p, hipStream_t stream) {
   dim3 grid(p.n_envs, (p.P + kObsAgentsPerBlock - 1) / kObsAgentsPerBlock);
-  if (p.wflags)
-    hipLaunchKernelGGL(obs_kernel<true>, grid, dim3(64 * kObsWaves), obs_lds_bytes(p.S), stream, p);
-  else
-    hipLaunchKernelGGL(obs_kernel<false>, grid, dim3(64 * kObsWaves), obs_lds_bytes(p.S), stream, p);
+  const dim3 block(64 * kObsWaves);
+  const size_t lds = obs_lds_bytes(p.S);
+  if (p.nat) {
+    if (p.wflags) hipLaunchKernelGGL((obs_kernel<true, true>), grid, block, lds, stream, p);
+    else hipLaunchKernelGGL((obs_kernel<false, true>), grid, block, lds, stream, p);
+  } else {
+    if (p.wflags) hipLaunchKernelGGL((obs_kernel<true, false>), grid, block, lds, stream, p);
+    else hipLaunchKernelGGL((obs_kernel<false, false>), grid, block, lds, stream, p);
+  }
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- native -> flat (SPEC §8b)
+// For learners that want pufferlib's float32 row from the native layout (e.g. after gathering
+// native shards over xGMI). Grid (env, 16-agent group), 4 waves; the env's Market (32 KB) is
+// staged in LDS once per workgroup; one wave expands one agent row. HBM-write-bound like
+// obs_kernel: 95,948 B written per agent for 9,552 B (+ 1/16 of the Market) read.
+__global__ void __launch_bounds__(256) expand_kernel(ObsParams p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  int16_t* mk = reinterpret_cast<int16_t*>(smem);
+  const int e = blockIdx.x, g = blockIdx.y, tid = threadIdx.x;
+  const uint8_t* base = p.nat + (size_t)e * native_env_bytes(p.P);
+  {
+    const uint4* src = reinterpret_cast<const uint4*>(base + (size_t)p.P * NMMO_NATIVE_ROW_BYTES);
+    uint4* dst = reinterpret_cast<uint4*>(mk);
+    for (int i = tid; i < NMMO_NATIVE_MARKET_BYTES / 16; i += blockDim.x) dst[i] = src[i];
+  }
+  __syncthreads();
+  const int lane = lane_id(), w = wave_id();
+  for (int i = w; i < kObsAgentsPerBlock; i += kObsWaves) {
+    const int a = g * kObsAgentsPerBlock + i;
+    if (a >= p.P) break;
+    const uint8_t* nrow = base + (size_t)a * NMMO_NATIVE_ROW_BYTES;
+    const int16_t* q = reinterpret_cast<const int16_t*>(nrow + NMMO_NATIVE_MASK_BYTES);
+    float* row = p.obs + ((size_t)e * p.P + a) * p.elems;
+    const int aid = __builtin_amdgcn_readfirstlane(q[0]);
+    if (aid == 0) {  // not in the realm: all-zero row
+      wave_zero(row, 0, p.elems);
+      continue;
+    }
+    for (int j = lane; j < p.o_agent_id; j += 64) obs_st(&row[j], (float)nrow[j]);
+    if (lane == 0) obs_st(&row[p.o_agent_id], (float)aid);
+    if (lane == 1) obs_st(&row[p.o_tick], (float)q[1]);
+    for (int j = lane; j < kNObs * NMMO_N_ENTITY_COLS; j += 64) obs_st(&row[p.o_entity + j], (float)q[kNatEntity + j]);
+    for (int j = lane; j < kInv * 16; j += 64) obs_st(&row[p.o_inventory + j], (float)q[kNatInv + j]);
+    for (int j = lane; j < NMMO_MARKET_ROWS * 16; j += 64) obs_st(&row[p.o_market + j], (float)mk[j]);
+    const float* temb = p.task + (size_t)q[kNatTask] * p.task_dim;
+    for (int j = lane; j < p.task_dim; j += 64) obs_st(&row[p.o_task + j], temb[j]);
+    for (int j = lane; j < 225 * 3; j += 64) obs_st(&row[p.o_tile + j], (float)q[kNatTile + j]);
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+hipError_t launch_expand(const ObsParams& p, hipStream_t stream) {
+  dim3 grid(p.n_envs, (p.P + kObsAgentsPerBlock - 1) / kObsAgentsPerBlock);
+  hipLaunchKernelGGL(expand_kernel, grid, dim3(64 * kObsWaves), NMMO_NATIVE_MARKET_BYTES, stream, p);
   return hipGetLastError();
 }
 

@@ -47,8 +47,15 @@ class NmmoEngine:
         d = self.device
         n, P = self.n_envs, self.P
         self.actions = torch.zeros((n, P, abi.N_ACTION_HEADS), dtype=torch.int32, device=d)
-        self.obs = (torch.empty((n, P, self.obs_elems), dtype=torch.float32, device=d)
-                    if config.obs_layout == abi.OBS_FLAT else None)
+        if config.obs_layout == abi.OBS_FLAT:
+            self.obs = torch.empty((n, P, self.obs_elems), dtype=torch.float32, device=d)
+        elif config.obs_layout == abi.OBS_NATIVE:  # SPEC §8b: per env, P rows + the Market
+            self.obs = torch.empty((n, abi.native_env_bytes(P)), dtype=torch.uint8, device=d)
+        else:
+            self.obs = None
+        emb = np.zeros((1, config.TASK_EMBED_DIM), np.float32) if task is None else \
+            task.view(np.float16).astype(np.float32).reshape(1, -1)
+        self.task_table = emb  # Task obs per task index (native-layout decoding)
         self.rew = torch.zeros((n, P), dtype=torch.float32, device=d)
         self.term = torch.zeros((n, P), dtype=torch.uint8, device=d)
         self.trunc = torch.zeros((n, P), dtype=torch.uint8, device=d)
@@ -100,6 +107,18 @@ class NmmoEngine:
                                   self._ptr(self.term), self._ptr(self.trunc), self._ptr(self.mask),
                                   self._stream()), "nmmo_step")
         return self.obs, self.rew, self.term, self.trunc, self.mask
+
+    def expand_obs(self, native=None, out=None):
+        """Native obs (SPEC §8b; default: this engine's) -> pufferlib flat float32
+        [n, P, obs_elems] on the device, bit-identical to the flat layout (nmmo_expand_obs)."""
+        native = self.obs if native is None else native
+        n = native.shape[0]
+        out = torch.empty((n, self.P, self.obs_elems), dtype=torch.float32, device=self.device) \
+            if out is None else out
+        with torch.cuda.device(self.device):
+            check(lib().nmmo_expand_obs(self.h, self._ptr(native), self._ptr(out), n, self._stream()),
+                  "nmmo_expand_obs")
+        return out
 
     def scripted_actions(self, policy_seed: int, out=None):
         out = self.actions if out is None else out
@@ -168,6 +187,8 @@ class NmmoEngine:
         (None = task 0 for everyone). SPEC §12; call before reset() for whole episodes."""
         arr = (abi.NmmoTask * len(tasks))(*tasks)
         emb = None if embeddings is None else np.ascontiguousarray(embeddings, np.float16)
+        self.task_table = (np.repeat(self.task_table[:1], len(tasks), axis=0) if emb is None
+                           else emb.astype(np.float32).reshape(len(tasks), -1))
         asg = None if assign is None else np.ascontiguousarray(assign, np.int32)
         check(lib().nmmo_set_tasks(self.h, ctypes.cast(arr, ctypes.c_void_p), len(tasks),
                                    None if emb is None else emb.ctypes.data_as(ctypes.c_void_p),

@@ -94,3 +94,68 @@ def unflatten(flat, task_dim: int = 2048) -> dict:
         else:
             out[key] = view
     return out
+
+
+# ---------------------------------------------------------------- native layout (SPEC.md §8b)
+NATIVE_I16_FIELDS = [("AgentId", (1,)), ("CurrentTick", (1,)), ("Entity", (PLAYER_N_OBS, ENTITY_COLS)),
+                     ("Inventory", (INVENTORY_N_OBS, ITEM_COLS)), ("Tile", (TILE_ROWS, TILE_COLS)),
+                     ("TaskIndex", (1,))]
+
+
+def native_offsets() -> dict:
+    """int16 offsets of the agent row's fields (after the 1,600 mask bytes)."""
+    out, off = {}, 0
+    for name, shape in NATIVE_I16_FIELDS:
+        out[name] = (off, shape)
+        off += int(np.prod(shape))
+    return out
+
+
+def unflatten_native(native, players: int, task_table, task_dim: int = 2048) -> dict:
+    """The native obs of n envs (uint8 [n, native_env_bytes], numpy or torch) decoded into the same
+    nested dict `unflatten(flat)` returns for [n*players, obs_elems] — float32 values equal to the
+    flat layout's, Market broadcast to the env's agents and Task looked up in `task_table`
+    (float32 [n_tasks, task_dim]). The learner-side replacement for unpack_batched_obs
+    (baseline_policy.py:41) when the env ships the native layout."""
+    from . import abi
+
+    torch_in = not isinstance(native, np.ndarray)
+    xp_float = (lambda x: x.float()) if torch_in else (lambda x: x.astype(np.float32))
+    n = native.shape[0]
+    rows = native[:, :players * abi.NATIVE_ROW_BYTES].reshape(n * players, abi.NATIVE_ROW_BYTES)
+    masks = rows[:, :abi.NATIVE_MASK_BYTES]
+    if torch_in:
+        import torch
+
+        i16 = rows[:, abi.NATIVE_MASK_BYTES:].contiguous().view(dtype=torch.int16)
+        mk = native[:, players * abi.NATIVE_ROW_BYTES:].contiguous().view(dtype=torch.int16)
+    else:
+        i16 = np.ascontiguousarray(rows[:, abi.NATIVE_MASK_BYTES:]).view(np.int16)
+        mk = np.ascontiguousarray(native[:, players * abi.NATIVE_ROW_BYTES:]).view(np.int16)
+    alive = i16[:, 0] != 0
+    out: dict = {"ActionTargets": {}}
+    off = 0
+    for (a, b), size in MASK_SEGMENTS:
+        out["ActionTargets"].setdefault(a, {})[b] = xp_float(masks[:, off:off + size])
+        off += size
+    for name, (o, shape) in native_offsets().items():
+        if name == "TaskIndex":
+            continue
+        k = int(np.prod(shape))
+        out[name] = xp_float(i16[:, o:o + k]).reshape(n * players, *shape)
+    market = xp_float(mk).reshape(n, 1, MARKET_N_OBS, ITEM_COLS)
+    if torch_in:
+        market = market.expand(n, players, MARKET_N_OBS, ITEM_COLS).reshape(n * players, MARKET_N_OBS, ITEM_COLS)
+        market = market * alive.view(-1, 1, 1)
+        tidx = i16[:, native_offsets()["TaskIndex"][0]].long()
+        import torch
+
+        task = torch.as_tensor(task_table, dtype=torch.float32, device=market.device)[tidx] * alive.view(-1, 1)
+    else:
+        market = np.broadcast_to(market, (n, players, MARKET_N_OBS, ITEM_COLS)).reshape(n * players, MARKET_N_OBS, ITEM_COLS)
+        market = market * alive.reshape(-1, 1, 1)
+        tidx = i16[:, native_offsets()["TaskIndex"][0]].astype(np.int64)
+        task = np.asarray(task_table, np.float32)[tidx] * alive.reshape(-1, 1)
+    out["Market"] = market
+    out["Task"] = task
+    return out
