@@ -40,8 +40,8 @@ WORKLOADS = {
     "C4": dict(envs=1024, preset="C4", obs=True,
                desc="C4: 1024 envs x 128 agents, all systems + per-agent flat obs gather"),
     # BASELINE.json configs[4]: C4 per GPU (8192 envs on 8) + the learner gather every step
-    "C5": dict(envs=1024, preset="C4", obs=True, gather=True,
-               desc="C5: 1024 envs x 128 agents per GPU, all systems + flat obs, RCCL gather of "
+    "C5": dict(envs=1024, preset="C4", obs=True, gather=True, layout="native",
+               desc="C5: 1024 envs x 128 agents per GPU, all systems + obs, RCCL gather of "
                     "obs/reward/dones/mask to the learner (rank 0) every step"),
 }
 
@@ -84,10 +84,14 @@ def pmc_traffic(cfg_name: str, kernel: str, envs: int):
     return None, None
 
 
-def obs_bytes_per_env(S: int, P: int, elems: int) -> int:
-    """Flat fp32 obs rows written + the entity columns staged once per 16-agent workgroup +
+def obs_bytes_per_env(S: int, P: int, elems: int, native: bool = False) -> int:
+    """Obs rows written (flat fp32: 23,987 x 4 B per agent; native, SPEC §8b: 9,552 B per agent
+    + the env's 32 KB Market once) + the entity columns staged once per 16-agent workgroup +
     the 15x15 tile window read per agent."""
-    return P * elems * 4 + (P // 16) * (33 * S * 2) + P * 225
+    from nmmo_amd import abi
+
+    rows = abi.native_env_bytes(P) if native else P * elems * 4
+    return rows + (P // 16) * (33 * S * 2) + P * 225
 
 
 def parse():
@@ -102,6 +106,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraph replay")
     ap.add_argument("--graph-steps", type=int, default=10, help="ticks captured per hipGraph")
+    ap.add_argument("--obs", default=None, choices=["flat", "native"],
+                    help="obs layout for the obs configs (default: flat for C4 = the pufferlib row "
+                         "the reference's learner reads, native for C5 = SURVEY §8e's gather layout)")
     ap.add_argument("--wrapper", default="none",
                     choices=["none", "base", "neurips23_start_kit", "takeru", "yaofeng"],
                     help="run env_creator's RewardWrapper on the device (SPEC §13) with the "
@@ -185,8 +192,9 @@ def main():
 
     wl = WORKLOADS[args.config]
     envs = args.envs or wl["envs"]
-    cfg = Config.preset(wl["preset"], early_stop_agent_num=8,
-                        obs_layout=abi.OBS_FLAT if wl["obs"] else abi.OBS_NONE)
+    native = wl["obs"] and (args.obs or wl.get("layout", "flat")) == "native"
+    obs_layout = (abi.OBS_NATIVE if native else abi.OBS_FLAT) if wl["obs"] else abi.OBS_NONE
+    cfg = Config.preset(wl["preset"], early_stop_agent_num=8, obs_layout=obs_layout)
     import numpy as np
 
     task = None
@@ -279,7 +287,7 @@ def main():
             eng.obs.zero_()
         s1.record()
         torch.cuda.synchronize(dev)
-        fill_gbs = eng.obs.numel() * 4 / (s0.elapsed_time(s1) / 10 * 1e-3) / 1e9
+        fill_gbs = eng.obs.numel() * eng.obs.element_size() / (s0.elapsed_time(s1) / 10 * 1e-3) / 1e9
 
     vals = torch.tensor([elapsed, float(alive.item()), float(envs * cfg.PLAYER_N * args.steps)],
                         dtype=torch.float64, device=dev)
@@ -298,15 +306,18 @@ def main():
         tick_avg_ms = tick_ms / max(n_timed, 1)
         obs_avg_ms = obs_ms / max(n_timed, 1)
         tick_b = tick_bytes_per_env(S, P, "Item" in cfg.systems) * envs
-        obs_b = obs_bytes_per_env(S, P, eng.obs_elems) * envs if wl["obs"] else 0
+        obs_b = obs_bytes_per_env(S, P, eng.obs_elems, native) * envs if wl["obs"] else 0
         if wl["obs"] and obs_avg_ms > tick_avg_ms:
             kern, byts, ms = "obs_kernel", obs_b, obs_avg_ms
         else:
             kern, byts, ms = "tick_kernel", tick_b, tick_avg_ms
         achieved = byts / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
-        traffic, traffic_src = pmc_traffic(args.config, kern, envs)
+        traffic, traffic_src = pmc_traffic(args.config + ("-native" if native and args.config != "C5" else ""),
+                                           kern, envs)
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
+            # the CPU leg always builds the flat pufferlib row when the workload has obs (the
+            # reference's CPU path; the oracle has no native writer)
             cpu = cpu_baseline(Config.preset(wl["preset"], early_stop_agent_num=8,
                                              obs_layout=abi.OBS_FLAT if wl["obs"] else abi.OBS_NONE),
                                args.cpu_seconds)
@@ -329,17 +340,20 @@ def main():
                 "agents_per_env": P,
                 "npcs_per_env": S - P,
                 "systems": list(cfg.systems),
-                "obs": "pufferlib-flat fp32 (23,987/agent)" if wl["obs"] else "none",
+                "obs": ("native nmmo dtypes (SPEC §8b, 9,552 B/agent + 32 KB Market/env)" if native else
+                        "pufferlib-flat fp32 (23,987/agent)") if wl["obs"] else "none",
                 "early_stop_agent_num": 8,
                 "parallelism": f"env-shard x{world}",
             },
             "slot_steps_per_sec": round(slots_total / elapsed, 1),
             "alive_fraction": round(alive_total / slots_total, 4),
-            "kernel_ms": {"tick": round(tick_avg_ms, 5), "obs": round(obs_avg_ms, 5),
-                          "wrapper": round(wrap_ms / max(n_timed, 1), 5)},
+            "kernel_ms": {"tick": round(tick_avg_ms, 5),
+                          "obs": round(obs_avg_ms, 5) if wl["obs"] else None,
+                          "wrapper": round(wrap_ms / max(n_timed, 1), 5) if args.wrapper != "none" else None},
             "wrapper": None if args.wrapper == "none" else args.wrapper,
             "launch": "eager" if (args.no_graph or gather) else f"hipGraph x{min(args.graph_steps, args.steps)} ticks",
-            "gather": f"RCCL gather of {eng.obs.numel() * 4 + envs * cfg.PLAYER_N * 8} B/rank/step to rank 0" if gather else None,
+            "gather": f"RCCL gather of {eng.obs.numel() * eng.obs.element_size() + envs * cfg.PLAYER_N * 8} "
+                      f"B/rank/step to rank 0" if gather else None,
             "roofline": {
                 "kernel": kern,
                 "bound": "hbm",

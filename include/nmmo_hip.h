@@ -42,7 +42,7 @@ extern "C" {
 #endif
 
 #define NMMO_API __attribute__((visibility("default")))
-#define NMMO_ABI_VERSION 4
+#define NMMO_ABI_VERSION 5
 
 /* ---- error codes ---- */
 #define NMMO_OK 0
@@ -335,6 +335,67 @@ NMMO_API int nmmo_read_timing(NmmoHandle* h, double* ms /* [3] */, int32_t* n);
  * their count into *n_rows (retained = min(E_EVENT_COUNT, event_cap)). Synchronous. */
 NMMO_API int nmmo_get_events(NmmoHandle* h, int32_t env, int32_t* host_rows, int32_t max_rows,
                              int32_t* n_rows);
+
+/* ---- GPU-resident experience storage ----
+ * The trainer-side buffers of the reference's clean_pufferl kept in HBM (the reference keeps
+ * them as host numpy arrays and copies every step across PCIe):
+ *   nmmo_exp_store   <- evaluate(): learner_mask / torch.where(...)[: batch_size - ptr + 1] and the
+ *                       obs/values/actions/logprobs/rewards/dones stores + sort_keys
+ *                                                  reinforcement_learning/clean_pufferl.py:331-346
+ *                       (storage allocated at :182-197)
+ *   nmmo_exp_sort    <- sorted(range(len(sort_keys)), key=sort_keys.__getitem__)  :414
+ *   nmmo_exp_gae     <- the reversed advantage loop                              :424-436
+ *   nmmo_gather_rows <- b_obs = obs_ary[b_idxs], b_actions/... and mb copies     :439-458
+ * Every buffer is caller-owned device memory; rows are `capacity` = batch_size + 1 (:182). */
+typedef struct NmmoExperience {
+  int32_t capacity;     /* rows (batch_size + 1) */
+  int32_t obs_elems;    /* flat obs row length (NmmoLayout.obs_elems) */
+  int32_t n_slots;      /* env_id range: num_envs * player_n agent slots (:119) */
+  float* obs;           /* [capacity][obs_elems] */
+  int64_t* actions;     /* [capacity][12] (torch int64, :183) */
+  float* logprobs;      /* [capacity] */
+  float* rewards;       /* [capacity] */
+  float* dones;         /* [capacity] */
+  float* truncateds;    /* [capacity] (allocated by the reference, never written by evaluate) */
+  float* values;        /* [capacity] */
+  int32_t* env_id;      /* [capacity] sort key 1 */
+  int32_t* step;        /* [capacity] sort key 2 (evaluate's step counter) */
+  int32_t* seq;         /* [capacity] rank of the row among its env_id's rows */
+  int32_t* slot_count;  /* [n_slots] rows stored per env_id; zero it with ptr to start a batch */
+  int32_t* ptr;         /* [1] rows stored (clean_pufferl.py:200 ptr) */
+} NmmoExperience;
+
+typedef struct NmmoStoreInput {
+  int32_t n_rows;         /* agent rows of this recv (num_envs * player_n) */
+  int32_t step;           /* evaluate's step counter; must increase between stores */
+  const float* obs;       /* flat [n_rows][obs_elems], or NULL with native */
+  const void* native;     /* NMMO_OBS_NATIVE buffer of n_rows / player_n envs (needs the handle) */
+  const float* rewards;   /* [n_rows] */
+  const uint8_t* dones;   /* [n_rows] (recv's d) */
+  const uint8_t* mask;    /* [n_rows] learner mask (recv mask x policy-pool mask) */
+  const int32_t* env_id;  /* [n_rows], distinct ids in [0, n_slots); NULL = env_id_base + row */
+  int32_t env_id_base;
+  const int32_t* actions; /* [n_rows][12] */
+  const float* logprobs;  /* [n_rows] */
+  const float* values;    /* [n_rows] */
+} NmmoStoreInput;
+
+/* int32 scratch the storage calls need: max(n_rows + n_rows/512 + 2, n_slots). */
+NMMO_API int64_t nmmo_exp_scratch_ints(int32_t max_rows, int32_t n_slots);
+/* Appends the mask-selected rows of one recv (in row order, cut at the capacity) and advances
+ * *ptr on the device; native obs are expanded straight into the flat experience rows (h = the
+ * handle whose layout/task table produced them; NULL for flat obs). Enqueued on `stream`. */
+NMMO_API int nmmo_exp_store(NmmoHandle* h, const NmmoExperience* x, const NmmoStoreInput* in,
+                            int32_t* scratch, void* stream);
+/* idxs (device int32 [*ptr]) = the row order sorted by (env_id, step). Enqueued. */
+NMMO_API int nmmo_exp_sort(const NmmoExperience* x, int32_t* idxs, int32_t* scratch, void* stream);
+/* advantages (device f32 [batch_size]) over idxs[0..batch_size], float32, the reference's op
+ * order (bit-identical). Enqueued. */
+NMMO_API int nmmo_exp_gae(const NmmoExperience* x, const int32_t* idxs, int32_t batch_size, double gamma,
+                          double gae_lambda, float* advantages, void* stream);
+/* out[k] = src[idx[k]] for n rows of row_bytes (a multiple of 4). Enqueued. */
+NMMO_API int nmmo_gather_rows(const void* src, int64_t row_bytes, const int32_t* idx, int32_t n, void* out,
+                              void* stream);
 
 NMMO_API int32_t nmmo_n_envs(const NmmoHandle* h);
 NMMO_API const char* nmmo_last_error(void);

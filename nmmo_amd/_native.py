@@ -20,7 +20,8 @@ SYMBOLS = [
     "nmmo_default_config", "nmmo_layout", "nmmo_create", "nmmo_destroy", "nmmo_reset",
     "nmmo_step", "nmmo_scripted_actions", "nmmo_get_state", "nmmo_set_state",
     "nmmo_get_map_bank", "nmmo_set_timing", "nmmo_read_timing", "nmmo_set_counters", "nmmo_get_events", "nmmo_set_tasks",
-    "nmmo_set_wrapper", "nmmo_get_wrapper_state", "nmmo_expand_obs", "nmmo_n_envs",
+    "nmmo_set_wrapper", "nmmo_get_wrapper_state", "nmmo_expand_obs", "nmmo_exp_scratch_ints",
+    "nmmo_exp_store", "nmmo_exp_sort", "nmmo_exp_gae", "nmmo_gather_rows", "nmmo_n_envs",
     "nmmo_last_error", "nmmo_abi_version",
 ]
 
@@ -62,6 +63,13 @@ def lib():
     L.nmmo_set_wrapper.argtypes = [vp, ctypes.POINTER(abi.NmmoWrapperConfig), vp]
     L.nmmo_get_wrapper_state.argtypes = [vp, vp, vp]
     L.nmmo_expand_obs.argtypes = [vp, vp, vp, i32, vp]
+    xp = ctypes.POINTER(abi.NmmoExperience)
+    L.nmmo_exp_scratch_ints.argtypes = [i32, i32]
+    L.nmmo_exp_scratch_ints.restype = ctypes.c_int64
+    L.nmmo_exp_store.argtypes = [vp, xp, ctypes.POINTER(abi.NmmoStoreInput), vp, vp]
+    L.nmmo_exp_sort.argtypes = [xp, vp, vp, vp]
+    L.nmmo_exp_gae.argtypes = [xp, vp, i32, ctypes.c_double, ctypes.c_double, vp, vp]
+    L.nmmo_gather_rows.argtypes = [vp, ctypes.c_int64, vp, i32, vp, vp]
     L.nmmo_n_envs.argtypes = [vp]
     L.nmmo_last_error.restype = ctypes.c_char_p
     L.nmmo_abi_version.restype = i32

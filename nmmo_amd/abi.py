@@ -6,7 +6,7 @@ struct sizes against the compiled library and the enum values against the header
 
 import ctypes
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 NMMO_OK = 0
 NMMO_E_INVALID = -1
@@ -225,3 +225,17 @@ def wrap_state_dtype():
                      ("max_dist", "<i4"), ("earned_gold", "<i4"), ("max_damage", "<i4"),
                      ("max_item_level", "<i4", (5,)), ("agent_kills", "<i4"), ("npc_kills", "<i4"),
                      ("reserved", "<i4")])
+
+
+# ---------------------------------------------------------------- experience storage
+class NmmoExperience(ctypes.Structure):
+    _fields_ = [("capacity", ctypes.c_int32), ("obs_elems", ctypes.c_int32), ("n_slots", ctypes.c_int32)] + [
+        (n, ctypes.c_void_p) for n in ("obs", "actions", "logprobs", "rewards", "dones", "truncateds", "values",
+                                       "env_id", "step", "seq", "slot_count", "ptr")]
+
+
+class NmmoStoreInput(ctypes.Structure):
+    _fields_ = [("n_rows", ctypes.c_int32), ("step", ctypes.c_int32), ("obs", ctypes.c_void_p),
+                ("native", ctypes.c_void_p), ("rewards", ctypes.c_void_p), ("dones", ctypes.c_void_p),
+                ("mask", ctypes.c_void_p), ("env_id", ctypes.c_void_p), ("env_id_base", ctypes.c_int32),
+                ("actions", ctypes.c_void_p), ("logprobs", ctypes.c_void_p), ("values", ctypes.c_void_p)]

@@ -12,7 +12,7 @@ CSRC = os.path.join(HERE, "csrc")
 LIB_DIR = os.path.join(HERE, "lib")
 LIB_PATH = os.path.join(LIB_DIR, "libnmmo_hip.so")
 STAMPS_PATH = os.path.join(LIB_DIR, "libnmmo_hip_stamps.so")
-SOURCES = ["mapgen.hip", "tick.hip", "obs.hip", "wrap.hip", "capi.hip"]
+SOURCES = ["mapgen.hip", "tick.hip", "obs.hip", "wrap.hip", "storage.hip", "capi.hip"]
 HEADERS = ["common.h", "kernels.h"]
 ARCH = os.environ.get("NMMO_OFFLOAD_ARCH", "gfx950")
 
@@ -43,7 +43,10 @@ def build(force: bool = False, verbose: bool = False, stamps: bool = False) -> s
     tmp = out + ".tmp"
     cmd = [
         _hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-        "-fvisibility=hidden", "-Wall", "-Werror", *(["-DNMMO_STAMPS"] if stamps else []),
+        "-fvisibility=hidden", "-Wall", "-Werror",
+        # no FMA contraction: hipcc contracts even __dadd_rn(__dmul_rn(..)) pairs, and the float /
+        # double reward, wrapper and advantage arithmetic must round op by op like the oracle
+        "-ffp-contract=off", *(["-DNMMO_STAMPS"] if stamps else []),
         *[os.path.join(CSRC, f) for f in SOURCES], "-o", tmp,
     ]
     if verbose:

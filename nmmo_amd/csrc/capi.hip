@@ -255,6 +255,7 @@ static ObsParams obs_params(NmmoHandle* h, void* obs) {
   p.o_agent_id = L.off_agent_id; p.o_tick = L.off_current_tick; p.o_entity = L.off_entity;
   p.o_inventory = L.off_inventory; p.o_market = L.off_market; p.o_task = L.off_task;
   p.o_tile = L.off_tile;
+  p.row_map = nullptr;
   p.ws = h->wrap_on ? h->d_ws : nullptr;
   p.wflags = 0;
   if (h->wrap_on) {
@@ -321,6 +322,75 @@ int nmmo_expand_obs(NmmoHandle* h, const void* native, float* flat, int32_t n_en
   p.obs = flat;
   p.n_envs = n_envs;
   HIP_TRY(launch_expand(p, (hipStream_t)stream));
+  return NMMO_OK;
+}
+
+// ---------------------------------------------------------------- experience storage (§8f row 3)
+int64_t nmmo_exp_scratch_ints(int32_t max_rows, int32_t n_slots) {
+  const int64_t a = (int64_t)max_rows + store_blocks(max_rows) + 2;
+  return a > n_slots ? a : (int64_t)n_slots;
+}
+
+static int check_exp(const NmmoExperience* x) {
+  if (!x) return fail(NMMO_E_INVALID, "null experience");
+  if (x->capacity <= 0 || x->obs_elems <= 0 || x->n_slots <= 0)
+    return fail(NMMO_E_INVALID, "capacity/obs_elems/n_slots must be > 0");
+  if (!x->obs || !x->actions || !x->logprobs || !x->rewards || !x->dones || !x->values || !x->env_id ||
+      !x->step || !x->seq || !x->slot_count || !x->ptr)
+    return fail(NMMO_E_INVALID, "experience buffers must be device pointers");
+  return NMMO_OK;
+}
+
+int nmmo_exp_store(NmmoHandle* h, const NmmoExperience* x, const NmmoStoreInput* in, int32_t* scratch,
+                   void* stream) {
+  if (int rc = check_exp(x)) return rc;
+  if (!in || !scratch) return fail(NMMO_E_INVALID, "null input/scratch");
+  if (in->n_rows <= 0) return fail(NMMO_E_INVALID, "n_rows must be > 0");
+  if (!in->rewards || !in->dones || !in->mask || !in->actions || !in->logprobs || !in->values)
+    return fail(NMMO_E_INVALID, "store inputs must be device pointers");
+  if (!in->env_id && (in->env_id_base < 0 || (int64_t)in->env_id_base + in->n_rows > x->n_slots))
+    return fail(NMMO_E_INVALID, "env_id_base + n_rows exceeds n_slots");
+  if (!in->obs == !in->native) return fail(NMMO_E_INVALID, "exactly one of obs / native");
+  if (in->native) {
+    if (!h) return fail(NMMO_E_INVALID, "native obs need the handle that wrote them");
+    if (h->cfg.obs_layout != NMMO_OBS_NATIVE) return fail(NMMO_E_INVALID, "handle is not NMMO_OBS_NATIVE");
+    if (in->n_rows % h->st.P) return fail(NMMO_E_SIZE, "n_rows must be whole envs of player_n rows");
+    if (x->obs_elems != h->layout.obs_elems) return fail(NMMO_E_SIZE, "obs_elems != the handle's layout");
+    ObsParams p = obs_params(h, nullptr);
+    p.nat = (uint8_t*)in->native;
+    p.n_envs = in->n_rows / h->st.P;
+    HIP_TRY(launch_store(*x, *in, &p, scratch, (hipStream_t)stream));
+  } else {
+    HIP_TRY(launch_store(*x, *in, nullptr, scratch, (hipStream_t)stream));
+  }
+  return NMMO_OK;
+}
+
+int nmmo_exp_sort(const NmmoExperience* x, int32_t* idxs, int32_t* scratch, void* stream) {
+  if (int rc = check_exp(x)) return rc;
+  if (!idxs || !scratch) return fail(NMMO_E_INVALID, "null idxs/scratch");
+  HIP_TRY(launch_sort(*x, idxs, scratch, (hipStream_t)stream));
+  return NMMO_OK;
+}
+
+int nmmo_exp_gae(const NmmoExperience* x, const int32_t* idxs, int32_t batch_size, double gamma, double gae_lambda,
+                 float* advantages, void* stream) {
+  if (int rc = check_exp(x)) return rc;
+  if (!idxs || !advantages) return fail(NMMO_E_INVALID, "null idxs/advantages");
+  if (batch_size <= 0 || batch_size >= x->capacity)
+    return fail(NMMO_E_SIZE, "batch_size must be in [1, capacity - 1]");
+  // the reference multiplies float32 tensors by the Python floats gamma and gamma*gae_lambda
+  // (a double product), each cast to float32 by the op (clean_pufferl.py:431-435)
+  HIP_TRY(launch_gae(*x, idxs, batch_size, (float)gamma, (float)(gamma * gae_lambda), advantages,
+                     (hipStream_t)stream));
+  return NMMO_OK;
+}
+
+int nmmo_gather_rows(const void* src, int64_t row_bytes, const int32_t* idx, int32_t n, void* out, void* stream) {
+  if (!src || !idx || !out) return fail(NMMO_E_INVALID, "null argument");
+  if (row_bytes <= 0 || row_bytes % 4) return fail(NMMO_E_INVALID, "row_bytes must be a positive multiple of 4");
+  if (n < 0) return fail(NMMO_E_INVALID, "n must be >= 0");
+  if (n) HIP_TRY(launch_gather_rows(src, row_bytes / 4, idx, n, out, (hipStream_t)stream));
   return NMMO_OK;
 }
 

@@ -38,6 +38,7 @@ struct ObsParams {
   const int32_t* assign; // [n][P]
   float* obs;           // [n][P][elems] (flat layout)
   uint8_t* nat;         // native layout (SPEC §8b) instead of obs when non-NULL
+  const int* row_map;   // expand only: flat row of agent row e*P+a (< 0 = skip); NULL = identity
   int n_envs, P, S, elems, task_dim;
   uint32_t systems;
   int spawn_immunity;
@@ -92,6 +93,14 @@ hipError_t launch_tick(const DevState& st, const int32_t* actions, const uint64_
 hipError_t launch_rebuild_dep(const DevState& st, hipStream_t stream);
 hipError_t launch_obs(const ObsParams& p, hipStream_t stream);
 hipError_t launch_expand(const ObsParams& p, hipStream_t stream);  // native -> flat (SPEC §8b)
+hipError_t launch_store(const NmmoExperience& x, const NmmoStoreInput& in, const ObsParams* native,
+                        int* scratch, hipStream_t stream);  // storage.hip
+int store_blocks(int n_rows);
+hipError_t launch_sort(const NmmoExperience& x, int32_t* idxs, int* scratch, hipStream_t stream);
+hipError_t launch_gae(const NmmoExperience& x, const int32_t* idxs, int B, float g, float gl, float* adv,
+                      hipStream_t stream);
+hipError_t launch_gather_rows(const void* src, int64_t row_words, const int32_t* idx, int n, void* out,
+                              hipStream_t stream);
 hipError_t launch_policy(const PolicyParams& p, hipStream_t stream);
 hipError_t launch_wrap(const WrapParams& p, int mode, hipStream_t stream);
 

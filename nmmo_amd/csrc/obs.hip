@@ -313,7 +313,9 @@ __global__ void __launch_bounds__(256) expand_kernel(ObsParams p) {
     if (a >= p.P) break;
     const uint8_t* nrow = base + (size_t)a * NMMO_NATIVE_ROW_BYTES;
     const int16_t* q = reinterpret_cast<const int16_t*>(nrow + NMMO_NATIVE_MASK_BYTES);
-    float* row = p.obs + ((size_t)e * p.P + a) * p.elems;
+    const int frow = p.row_map ? p.row_map[(size_t)e * p.P + a] : e * p.P + a;
+    if (frow < 0) continue;  // storage: row not kept (wave-uniform)
+    float* row = p.obs + (size_t)frow * p.elems;
     const int aid = __builtin_amdgcn_readfirstlane(q[0]);
     if (aid == 0) {  // not in the realm: all-zero row
       wave_zero(row, 0, p.elems);

@@ -1,0 +1,221 @@
+// storage.hip — GPU-resident experience storage: the trainer-side
+// buffers of the reference's clean_pufferl kept in HBM, so the rollout never leaves the device.
+//
+//   store_count / store_place / store_rows  <- evaluate(): learner_mask, the alive-row indices
+//       truncated to the room left, the obs/values/actions/logprobs/rewards/dones row stores
+//       and the (env_id, step) sort keys      reinforcement_learning/clean_pufferl.py:331-346
+//   sort_scan / sort_scatter  <- sorted(range(len(sort_keys)), key=sort_keys.__getitem__)  :414
+//   gae_kernel                <- the reversed advantage loop (float32, serial order)   :424-436
+//   gather_rows_kernel        <- b_obs = obs_ary[b_idxs] and the per-minibatch copies  :439-458
+//
+// Byte work, HBM-bound: a stored row moves 95,948 B of obs (flat) or is expanded straight from
+// the native layout (SPEC §8b: 9,552 B read per row) into its experience slot; every other
+// field is a few bytes per row.
+#include "kernels.h"
+
+namespace nmmo {
+
+constexpr int kStoreBlock = 512;  // rows per workgroup in the count/place passes (8 waves)
+
+// Pass 1: alive rows per block of kStoreBlock rows.
+__global__ void __launch_bounds__(kStoreBlock) store_count_kernel(const uint8_t* mask, int n, int* blk_cnt) {
+  __shared__ int wt[8];
+  const int r = blockIdx.x * kStoreBlock + threadIdx.x;
+  const uint64_t b = __ballot(r < n && mask[r] != 0);
+  if (lane_id() == 0) wt[wave_id()] = __popcll(b);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int s = 0;
+    for (int i = 0; i < kStoreBlock / 64; i++) s += wt[i];
+    blk_cnt[blockIdx.x] = s;
+  }
+}
+
+// Pass 2: each alive row's rank in row order (clean_pufferl.py:333 torch.where(learner_mask)),
+// its experience slot ptr + rank if that is below the capacity (the [: batch_size - ptr + 1]
+// cut, :333), and the small per-row fields. dst[r] = slot or -1 (read by store_rows).
+__global__ void __launch_bounds__(kStoreBlock) store_place_kernel(NmmoExperience x, NmmoStoreInput in,
+                                                                  const int* blk_cnt, int* dst, int* total) {
+  __shared__ int wt[2][8];
+  const int b = blockIdx.x, tid = threadIdx.x, r = b * kStoreBlock + tid;
+  int part = 0;  // rows of the blocks before this one
+  for (int i = tid; i < b; i += kStoreBlock) part += blk_cnt[i];
+  int base_total;
+  (void)block_prefix_sum(part, wt[0], &base_total);
+  const bool alive = r < in.n_rows && in.mask[r] != 0;
+  int blk_total;
+  const int rank = base_total + block_prefix_count(alive, wt[1], &blk_total);
+  const int ptr0 = *x.ptr;
+  const int room = x.capacity - ptr0;
+  if (r < in.n_rows) dst[r] = (alive && rank < room) ? ptr0 + rank : -1;
+  if (alive && rank < room) {
+    const int s = ptr0 + rank;
+    const int eid = in.env_id ? in.env_id[r] : in.env_id_base + r;
+    x.rewards[s] = in.rewards[r];
+    x.dones[s] = (float)in.dones[r];
+    x.logprobs[s] = in.logprobs[r];
+    x.values[s] = in.values[r];
+    const int32_t* a = in.actions + (size_t)r * kHeads;
+    long long* o = reinterpret_cast<long long*>(x.actions) + (size_t)s * kHeads;
+#pragma unroll
+    for (int h = 0; h < kHeads; h++) o[h] = a[h];
+    x.env_id[s] = eid;
+    x.step[s] = in.step;
+    // rank of this row among its env_id's rows: env ids are distinct within one store, so the
+    // slot counter has exactly one writer here, and stores arrive in step order
+    x.seq[s] = x.slot_count[eid]++;
+  }
+  if (b == gridDim.x - 1 && tid == 0) *total = base_total + blk_total;
+}
+
+// Pass 3 (flat obs): one wave copies one 95,948-B row (4-B aligned rows, so dword accesses;
+// eight loads in flight per lane).
+__global__ void __launch_bounds__(256) store_rows_kernel(const float* __restrict__ src, int n, int elems,
+                                                        const int* __restrict__ dst, float* __restrict__ out) {
+  const int r = blockIdx.x * 4 + wave_id();
+  if (r >= n) return;
+  const int s = dst[r];
+  if (s < 0) return;
+  const float* a = src + (size_t)r * elems;
+  float* o = out + (size_t)s * elems;
+  const int lane = lane_id();
+  int j = lane;
+  for (; j + 7 * 64 < elems; j += 8 * 64) {
+    float v[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) v[k] = a[j + k * 64];
+#pragma unroll
+    for (int k = 0; k < 8; k++) o[j + k * 64] = v[k];
+  }
+  for (; j < elems; j += 64) o[j] = a[j];
+}
+
+__global__ void store_commit_kernel(int* ptr, const int* total, int capacity) {
+  const int p = *ptr + *total;
+  *ptr = p < capacity ? p : capacity;
+}
+
+// ---------------------------------------------------------------- sort by (env_id, step)
+// Rows of one env_id arrive in step order, so the stable order of clean_pufferl.py:414 is
+// position = (rows of all smaller env ids) + the row's rank among its env id's rows: an
+// exclusive scan of the per-env-id counts (one workgroup) and a scatter. No comparison sort.
+__global__ void __launch_bounds__(512) sort_scan_kernel(const int* slot_count, int n_slots, int* offset) {
+  __shared__ int wt[2][8];
+  int carry = 0;
+  for (int base = 0, k = 0; base < n_slots; base += 512, k ^= 1) {
+    const int i = base + threadIdx.x;
+    const int v = i < n_slots ? slot_count[i] : 0;
+    int t;
+    const int ex = block_prefix_sum(v, wt[k], &t);
+    if (i < n_slots) offset[i] = carry + ex;
+    carry += t;
+  }
+}
+
+__global__ void __launch_bounds__(256) sort_scatter_kernel(NmmoExperience x, const int* offset, int32_t* idxs) {
+  const int r = blockIdx.x * 256 + threadIdx.x;
+  if (r >= *x.ptr) return;
+  idxs[offset[x.env_id[r]] + x.seq[r]] = r;
+}
+
+// ---------------------------------------------------------------- advantages (:424-436)
+// for t = B-1 .. 0 with i = idxs[t], j = idxs[t+1]:
+//   nnt = 1 - dones[j]; delta = rewards[j] + g*values[j]*nnt - values[i]
+//   adv[t] = last = delta + gl*nnt*last           (g = gamma, gl = gamma*gae_lambda, float32)
+// The reference evaluates this on float32 CPU tensors one op at a time (left to right, each op
+// rounded); delta and gl*nnt do not depend on `last`, so all 64 lanes form them for a chunk of
+// 64 t's in parallel and only the two-op recurrence walks the chunk serially (operands read
+// with v_readlane). FP contraction is off here: no FMA, bit-identical to the reference.
+__global__ void __launch_bounds__(64) gae_kernel(NmmoExperience x, const int32_t* idxs, int B, float g, float gl,
+                                                 float* adv) {
+#pragma clang fp contract(off)
+  const int lane = lane_id();
+  float last = 0.f;
+  for (int hi = B - 1; hi >= 0; hi -= 64) {
+    const int t = hi - lane;  // lane 0 walks first (largest t)
+    float delta = 0.f, k = 0.f;
+    if (t >= 0) {
+      const int i = idxs[t], j = idxs[t + 1];
+      const float nnt = 1.0f - x.dones[j];
+      delta = x.rewards[j] + g * x.values[j] * nnt - x.values[i];
+      k = gl * nnt;
+    }
+    float mine = 0.f;
+    // lanes past t = 0 in the last chunk carry delta = k = 0: they only overwrite `last` after
+    // the final stored element
+#pragma unroll
+    for (int l = 0; l < 64; l++) {
+      const float d = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, delta), l));
+      const float kk = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, k), l));
+      last = d + kk * last;
+      mine = lane == l ? last : mine;
+    }
+    if (t >= 0) adv[t] = mine;
+  }
+}
+
+// ---------------------------------------------------------------- row gather (:439-458)
+// out[k] = src[idx[k]] for rows of `words` dwords; one wave per row, eight loads in flight.
+__global__ void __launch_bounds__(256) gather_rows_kernel(const uint32_t* __restrict__ src, int64_t words,
+                                                         const int32_t* __restrict__ idx, int n,
+                                                         uint32_t* __restrict__ out) {
+  const int k = blockIdx.x * 4 + wave_id();
+  if (k >= n) return;
+  const uint32_t* a = src + (size_t)idx[k] * words;
+  uint32_t* o = out + (size_t)k * words;
+  int64_t j = lane_id();
+  for (; j + 7 * 64 < words; j += 8 * 64) {
+    uint32_t v[8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) v[q] = a[j + q * 64];
+#pragma unroll
+    for (int q = 0; q < 8; q++) o[j + q * 64] = v[q];
+  }
+  for (; j < words; j += 64) o[j] = a[j];
+}
+
+// ---------------------------------------------------------------- launches
+int store_blocks(int n_rows) { return (n_rows + kStoreBlock - 1) / kStoreBlock; }
+
+hipError_t launch_store(const NmmoExperience& x, const NmmoStoreInput& in, const ObsParams* native,
+                        int* scratch, hipStream_t stream) {
+  const int nb = store_blocks(in.n_rows);
+  int* dst = scratch;                // [n_rows]
+  int* blk = scratch + in.n_rows;    // [nb]
+  int* total = blk + nb;             // [1]
+  hipLaunchKernelGGL(store_count_kernel, dim3(nb), dim3(kStoreBlock), 0, stream, in.mask, in.n_rows, blk);
+  hipLaunchKernelGGL(store_place_kernel, dim3(nb), dim3(kStoreBlock), 0, stream, x, in, blk, dst, total);
+  if (native) {
+    ObsParams p = *native;
+    p.obs = x.obs;
+    p.row_map = dst;
+    hipError_t e = launch_expand(p, stream);
+    if (e != hipSuccess) return e;
+  } else {
+    hipLaunchKernelGGL(store_rows_kernel, dim3((in.n_rows + 3) / 4), dim3(256), 0, stream, in.obs, in.n_rows,
+                       x.obs_elems, dst, x.obs);
+  }
+  hipLaunchKernelGGL(store_commit_kernel, dim3(1), dim3(1), 0, stream, x.ptr, total, x.capacity);
+  return hipGetLastError();
+}
+
+hipError_t launch_sort(const NmmoExperience& x, int32_t* idxs, int* scratch, hipStream_t stream) {
+  hipLaunchKernelGGL(sort_scan_kernel, dim3(1), dim3(512), 0, stream, x.slot_count, x.n_slots, scratch);
+  hipLaunchKernelGGL(sort_scatter_kernel, dim3((x.capacity + 255) / 256), dim3(256), 0, stream, x, scratch, idxs);
+  return hipGetLastError();
+}
+
+hipError_t launch_gae(const NmmoExperience& x, const int32_t* idxs, int B, float g, float gl, float* adv,
+                      hipStream_t stream) {
+  hipLaunchKernelGGL(gae_kernel, dim3(1), dim3(64), 0, stream, x, idxs, B, g, gl, adv);
+  return hipGetLastError();
+}
+
+hipError_t launch_gather_rows(const void* src, int64_t row_words, const int32_t* idx, int n, void* out,
+                              hipStream_t stream) {
+  hipLaunchKernelGGL(gather_rows_kernel, dim3((n + 3) / 4), dim3(256), 0, stream, (const uint32_t*)src,
+                     row_words, idx, n, (uint32_t*)out);
+  return hipGetLastError();
+}
+
+}  // namespace nmmo

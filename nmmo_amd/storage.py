@@ -1,0 +1,178 @@
+"""DeviceExperience — the reference trainer's rollout storage kept in HBM.
+
+The reference's `clean_pufferl` allocates its experience buffers as host tensors viewed as numpy
+arrays (`reinforcement_learning/clean_pufferl.py:182-197`), copies every recv's observations,
+values, actions, logprobs, rewards and dones into them through the host (`:318,:329-346`), sorts
+the `(env_id, step)` keys on the host (`:414`), walks the advantage recurrence in a Python loop
+(`:424-436`) and gathers the minibatch rows with numpy fancy indexing before the H2D copies
+(`:439-458`). Here every one of those steps is a HIP kernel on device buffers
+(`nmmo_amd/csrc/storage.hip`), reached through the C-ABI (`include/nmmo_hip.h`,
+`nmmo_exp_*`); the observation rows go straight from the env's obs buffer (flat) or its native
+layout (SPEC §8b, expanded on store) into their experience slot.
+
+Names follow the reference: obs / actions / logprobs / rewards / dones / truncateds / values,
+`ptr`, `batch_size`, `batch_rows`, `bptt_horizon`, b_idxs, advantages, returns.
+"""
+
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import abi
+from ._native import check, lib
+
+
+def _p(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+class DeviceExperience:
+    def __init__(self, batch_size: int, obs_elems: int, n_slots: int, device=None):
+        """batch_size: rows trained on per update (the buffers hold batch_size + 1, :182);
+        n_slots: the env_id range = num_envs x agents_per_env (:119)."""
+        self.device = torch.device("cuda", torch.cuda.current_device()) if device is None \
+            else torch.device(device)
+        self.batch_size = int(batch_size)
+        self.capacity = cap = self.batch_size + 1
+        self.obs_elems = int(obs_elems)
+        self.n_slots = int(n_slots)
+        d = self.device
+        f32 = dict(dtype=torch.float32, device=d)
+        i32 = dict(dtype=torch.int32, device=d)
+        self.obs = torch.zeros((cap, self.obs_elems), **f32)
+        self.actions = torch.zeros((cap, abi.N_ACTION_HEADS), dtype=torch.int64, device=d)
+        self.logprobs = torch.zeros(cap, **f32)
+        self.rewards = torch.zeros(cap, **f32)
+        self.dones = torch.zeros(cap, **f32)
+        self.truncateds = torch.zeros(cap, **f32)
+        self.values = torch.zeros(cap, **f32)
+        self.env_id = torch.zeros(cap, **i32)
+        self.step = torch.zeros(cap, **i32)
+        self.seq = torch.zeros(cap, **i32)
+        self.slot_count = torch.zeros(self.n_slots, **i32)
+        self.ptr_dev = torch.zeros(1, **i32)
+        self._scratch_rows = 0
+        self.scratch = torch.zeros(0, **i32)
+        self.x = abi.NmmoExperience(cap, self.obs_elems, self.n_slots, *[
+            t.data_ptr() for t in (self.obs, self.actions, self.logprobs, self.rewards, self.dones,
+                                   self.truncateds, self.values, self.env_id, self.step, self.seq,
+                                   self.slot_count, self.ptr_dev)])
+
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def _ensure_scratch(self, n_rows: int):
+        need = int(lib().nmmo_exp_scratch_ints(max(n_rows, 1), self.n_slots))
+        if self.scratch.numel() < need:
+            self.scratch = torch.zeros(need, dtype=torch.int32, device=self.device)
+
+    # -- evaluate side (clean_pufferl.py:200-346)
+    def reset(self):
+        """Start a new batch: ptr = 0 (:200) and empty sort keys (:415)."""
+        self.ptr_dev.zero_()
+        self.slot_count.zero_()
+
+    @property
+    def ptr(self) -> int:
+        return int(self.ptr_dev.item())
+
+    def full(self) -> bool:
+        """The evaluate loop's exit test `ptr == batch_size + 1` (:290)."""
+        return self.ptr == self.capacity
+
+    def store(self, o, r, d, mask, actions, logprob, value, step: int, env_id=None, env_id_base: int = 0,
+              engine=None):
+        """Append the learner-mask rows of one recv in row order, cut at the room left (:331-346).
+        o: flat float32 [N, obs_elems] (or [n_envs, P, obs_elems]), or the native uint8
+        [n_envs, env_bytes] buffer of `engine` (an NmmoEngine with obs_layout NATIVE), expanded
+        on store; r float32 [N]; d / mask uint8 or bool [N]; actions int [N, 12]; logprob /
+        value float32 [N]; env_id int [N] distinct agent-slot ids (None = env_id_base + row)."""
+        dev = self.device
+
+        def cvt(t, dtype):
+            t = torch.as_tensor(t)
+            if t.dtype == torch.bool:
+                t = t.to(torch.uint8)
+            return t.to(device=dev, dtype=dtype).contiguous().view(-1)
+
+        r_, d_, m_ = cvt(r, torch.float32), cvt(d, torch.uint8), cvt(mask, torch.uint8)
+        lp, v = cvt(logprob, torch.float32), cvt(value, torch.float32)
+        n = r_.numel()
+        a = torch.as_tensor(actions).to(device=dev, dtype=torch.int32).contiguous().view(n, abi.N_ACTION_HEADS)
+        eid = None if env_id is None else cvt(env_id, torch.int32)
+        native = engine is not None and engine.config.obs_layout == abi.OBS_NATIVE
+        if native:
+            if o.dtype != torch.uint8 or o.shape[0] * engine.P != n:
+                raise ValueError("native obs must be the engine's uint8 [n_envs, env_bytes] buffer")
+            obs_flat, obs_nat = None, o.contiguous()
+        else:
+            obs_flat, obs_nat = o.contiguous().view(n, self.obs_elems), None
+            if obs_flat.dtype != torch.float32:
+                raise ValueError("flat obs must be float32")
+        for t in (m_, d_, lp, v):
+            if t.numel() != n:
+                raise ValueError("per-row inputs must all have N rows")
+        self._ensure_scratch(n)
+        inp = abi.NmmoStoreInput(n, int(step), obs_flat.data_ptr() if obs_flat is not None else None,
+                                 obs_nat.data_ptr() if obs_nat is not None else None, r_.data_ptr(),
+                                 d_.data_ptr(), m_.data_ptr(), eid.data_ptr() if eid is not None else None,
+                                 int(env_id_base), a.data_ptr(), lp.data_ptr(), v.data_ptr())
+        with torch.cuda.device(dev):
+            check(lib().nmmo_exp_store(engine.h if native else None, ctypes.byref(self.x), ctypes.byref(inp),
+                                       _p(self.scratch), self._stream()), "nmmo_exp_store")
+        # keep the inputs alive until the kernels that read them have been enqueued
+        self._inflight = (r_, d_, m_, lp, v, a, eid, obs_flat, obs_nat)
+
+    # -- train side (clean_pufferl.py:413-458)
+    def sort(self) -> torch.Tensor:
+        """idxs: the stored rows sorted by (env_id, step) (:414), device int32 [ptr]."""
+        n = self.ptr
+        idxs = torch.empty(n, dtype=torch.int32, device=self.device)
+        self._ensure_scratch(1)
+        with torch.cuda.device(self.device):
+            check(lib().nmmo_exp_sort(ctypes.byref(self.x), _p(idxs), _p(self.scratch), self._stream()),
+                  "nmmo_exp_sort")
+        self.slot_count.zero_()  # data.sort_keys = [] (:415)
+        return idxs
+
+    def advantages(self, idxs: torch.Tensor, gamma: float, gae_lambda: float) -> torch.Tensor:
+        """The reversed GAE loop over idxs (:424-436), float32, bit-identical to the reference."""
+        if idxs.numel() != self.capacity:
+            raise ValueError("advantages need a full batch (ptr == batch_size + 1)")
+        adv = torch.zeros(self.batch_size, dtype=torch.float32, device=self.device)
+        with torch.cuda.device(self.device):
+            check(lib().nmmo_exp_gae(ctypes.byref(self.x), _p(idxs), self.batch_size, float(gamma),
+                                     float(gae_lambda), _p(adv), self._stream()), "nmmo_exp_gae")
+        return adv
+
+    def batch(self, idxs: torch.Tensor, advantages: torch.Tensor, batch_rows: int, bptt_horizon: int) -> dict:
+        """The flattened batch of :417-450: b_idxs [num_minibatches, batch_rows, bptt_horizon],
+        b_advantages, b_values, b_returns in the same shapes (values/advantages gathered on
+        the device; obs stay in place and are gathered per minibatch)."""
+        num_mb = self.batch_size // bptt_horizon // batch_rows
+        b_idxs = idxs[:-1].reshape(batch_rows, num_mb, bptt_horizon).transpose(0, 1)
+        b_values = self.gather(self.values, b_idxs)
+        b_adv = advantages.reshape(batch_rows, num_mb, bptt_horizon).transpose(0, 1)
+        return {"b_idxs": b_idxs, "b_values": b_values, "b_advantages": b_adv, "b_returns": b_adv + b_values,
+                "num_minibatches": num_mb}
+
+    def minibatch(self, b_idxs: torch.Tensor, mb: int) -> dict:
+        """Minibatch `mb` of the flattened batch (:456-462): obs [batch_rows, bptt, obs_elems],
+        actions, logprobs, dones, values gathered straight from the experience rows."""
+        idx = b_idxs[mb]
+        return {"obs": self.gather(self.obs, idx), "actions": self.gather(self.actions, idx),
+                "logprobs": self.gather(self.logprobs, idx), "dones": self.gather(self.dones, idx),
+                "values": self.gather(self.values, idx)}
+
+    def gather(self, src: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
+        """src[idx] on the device through nmmo_gather_rows (rows of src's trailing dims)."""
+        flat_idx = idx.reshape(-1).to(torch.int32).contiguous()
+        row_shape = tuple(src.shape[1:])
+        out = torch.empty((flat_idx.numel(),) + row_shape, dtype=src.dtype, device=src.device)
+        row_bytes = src[0].numel() * src.element_size()
+        with torch.cuda.device(self.device):
+            check(lib().nmmo_gather_rows(_p(src), row_bytes, _p(flat_idx), flat_idx.numel(), _p(out),
+                                         self._stream()), "nmmo_gather_rows")
+        return out.view(tuple(idx.shape) + row_shape)
