@@ -316,6 +316,11 @@ NMMO_API int nmmo_get_state(NmmoHandle* h, void* host_buf, size_t nbytes);
 NMMO_API int nmmo_set_state(NmmoHandle* h, const void* host_buf, size_t nbytes);
 /* The generated map bank: host u8 [map_n][MAP_TILES]. Synchronous. */
 NMMO_API int nmmo_get_map_bank(NmmoHandle* h, uint8_t* host_buf, size_t nbytes);
+/* Replaces the map bank (maps loaded from PATH_MAPS/map{i}/map.npy, environment.py:33,41;
+ * SURVEY.md §8f row 4): host u8 [map_n][MAP_TILES], every value a material id < 16. Envs pick
+ * up their map at the next reset; the depleted-tile bitmap of the current state is re-derived
+ * against the new bank. Synchronous. */
+NMMO_API int nmmo_set_map_bank(NmmoHandle* h, const uint8_t* host_buf, size_t nbytes);
 
 /* Kernel timing with HIP events recorded on the launch stream around each kernel of
  * nmmo_step (bench/profiling; off by default, up to 8192 steps buffered).

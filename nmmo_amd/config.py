@@ -53,6 +53,8 @@ class Config:
     event_cap: int = 4096                # event-log ring rows per env (SPEC §11), 0 = off
     obs_layout: int = abi.OBS_FLAT
     map_seed: int = 0
+    PATH_MAPS: str | None = None         # f"{maps_path}/{map_size}/" (environment.py:41); None = in memory
+    MAP_FORCE_GENERATION: bool = False   # env_args.map_force_generation (environment.py:33)
 
     def __init__(self, env_args: Namespace | None = None, **overrides):
         for f in dataclasses.fields(self):
@@ -69,6 +71,10 @@ class Config:
             for k, v in vars(env_args).items():
                 if k in mapping:
                     setattr(self, mapping[k], v)
+            if getattr(env_args, "maps_path", None):
+                self.PATH_MAPS = f"{env_args.maps_path}/{getattr(env_args, 'map_size', self.MAP_CENTER)}/"
+            if hasattr(env_args, "map_force_generation"):
+                self.MAP_FORCE_GENERATION = bool(env_args.map_force_generation)
         for k, v in overrides.items():
             if not hasattr(self, k):
                 raise AttributeError(f"unknown config key {k}")

@@ -630,6 +630,21 @@ int nmmo_get_events(NmmoHandle* h, int32_t env, int32_t* host_rows, int32_t max_
   return NMMO_OK;
 }
 
+int nmmo_set_map_bank(NmmoHandle* h, const uint8_t* host_buf, size_t nbytes) {
+  if (!h || !host_buf) return fail(NMMO_E_INVALID, "null argument");
+  const size_t need = (size_t)h->cfg.map_n * NMMO_MAP_TILES;
+  if (nbytes != need) return fail(NMMO_E_SIZE, "map bank buffer %zu != %zu", nbytes, need);
+  for (size_t i = 0; i < need; i++)
+    if (host_buf[i] >= 16) return fail(NMMO_E_INVALID, "map %zu tile %zu: material %d >= 16", i / NMMO_MAP_TILES,
+                                       i % NMMO_MAP_TILES, (int)host_buf[i]);
+  HIP_TRY(hipSetDevice(h->device));
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(h->d_bank, host_buf, need, hipMemcpyHostToDevice));
+  HIP_TRY(launch_rebuild_dep(h->st, nullptr));
+  HIP_TRY(hipDeviceSynchronize());
+  return NMMO_OK;
+}
+
 int nmmo_get_map_bank(NmmoHandle* h, uint8_t* host_buf, size_t nbytes) {
   if (!h || !host_buf) return fail(NMMO_E_INVALID, "null argument");
   const size_t need = (size_t)h->cfg.map_n * NMMO_MAP_TILES;

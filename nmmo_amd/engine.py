@@ -61,6 +61,9 @@ class NmmoEngine:
         self.trunc = torch.zeros((n, P), dtype=torch.uint8, device=d)
         self.mask = torch.zeros((n, P), dtype=torch.uint8, device=d)
         self.info = None
+        from . import maps
+
+        self.maps_source = maps.prepare(self)  # PATH_MAPS / MAP_FORCE_GENERATION (environment.py:33,41)
 
     def close(self):
         if getattr(self, "h", None) is not None and self.h.value:
@@ -211,3 +214,12 @@ class NmmoEngine:
         check(lib().nmmo_get_map_bank(self.h, buf.ctypes.data_as(ctypes.c_void_p), buf.nbytes),
               "nmmo_get_map_bank")
         return buf
+
+    def set_map_bank(self, bank: np.ndarray):
+        """Replace the generated bank (e.g. maps loaded from PATH_MAPS, nmmo_amd/maps.py); envs
+        use it from their next reset."""
+        buf = np.ascontiguousarray(bank, dtype=np.uint8)
+        if buf.shape != (self.config.MAP_N, abi.MAP_SIZE, abi.MAP_SIZE):
+            raise ValueError(f"map bank must be uint8 [{self.config.MAP_N}, {abi.MAP_SIZE}, {abi.MAP_SIZE}]")
+        check(lib().nmmo_set_map_bank(self.h, buf.ctypes.data_as(ctypes.c_void_p), buf.nbytes),
+              "nmmo_set_map_bank")

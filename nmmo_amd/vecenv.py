@@ -224,13 +224,15 @@ class NmmoEnv:
         terms = {a: bool(term[a - 1]) for a in present}
         truncs = {a: bool(trunc[a - 1]) for a in present}
         self.agents = [a for a in present if not (terms[a] or truncs[a])]
+        if getattr(self, "_replay", None) is not None:
+            self._replay.update()
         return obs, rewards, terms, truncs, {a: {} for a in present}
 
     @property
     def realm(self):
         """Partial realm facade: `realm.tick`, `realm.players[id]` with the entity columns as
         attributes and `realm.event_log` (the reads of stat_wrapper.py:122-185, 216-285)."""
-        return _Realm(self.state(), self.engine.events(0))
+        return _Realm(self.state(), self.engine.events(0), env=self)
 
     def state(self) -> dict:
         st = self.engine.get_state()
@@ -238,9 +240,18 @@ class NmmoEnv:
         per = abi.state_bytes_per_env(S, self.config.PLAYER_N)
         b = st[:per]
         env = b[:abi.NE * 4].view(np.int32)
-        ent = b[abi.NE * 4:abi.NE * 4 + abi.NF * S * 2].view(np.int16).reshape(abi.NF, S)
-        return {"tick": int(env[abi.E["tick"]]),
+        o = abi.NE * 4
+        ent = b[o:o + abi.NF * S * 2].view(np.int16).reshape(abi.NF, S)
+        o += abi.NF * S * 2 + S * 2  # entity table, free-row ring
+        mat = b[o:o + abi.MAP_TILES].reshape(abi.MAP_SIZE, abi.MAP_SIZE)
+        return {"tick": int(env[abi.E["tick"]]), "material": mat.copy(),
                 "entities": {n: ent[i].copy() for i, n in enumerate(abi.ENTITY_FIELDS)}}
+
+    def record_replay(self, helper):
+        """realm.record_replay(replay_helper) (train_helper.py:134): the helper is updated after
+        every step (nmmo_amd/replay.py)."""
+        helper.set_env(self)
+        self._replay = helper
 
     def close(self):
         self.engine.close()
@@ -286,7 +297,8 @@ class EventLog:
 
 
 class _Realm:
-    def __init__(self, st: dict, events: np.ndarray | None = None):
+    def __init__(self, st: dict, events: np.ndarray | None = None, env=None):
+        self._env = env
         self.tick = st["tick"]
         self.event_log = EventLog(np.zeros((0, abi.EVENT_COLS), np.int32) if events is None else events,
                                   self.tick)
@@ -295,6 +307,9 @@ class _Realm:
                         if ent["id"][s] > 0 and ent["alive"][s]}
         self.npcs = {int(ent["id"][s]): _Entity(ent, s) for s in range(len(ent["id"]))
                      if ent["id"][s] < 0 and ent["alive"][s]}
+
+    def record_replay(self, helper):
+        self._env.record_replay(helper)
 
 
 def _index(d, i):

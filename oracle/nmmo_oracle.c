@@ -1469,6 +1469,15 @@ EXPORT int oracle_get_events(void* h, int env, int32_t* rows, int max_rows, int*
   return 0;
 }
 
+EXPORT int oracle_set_map_bank(void* h, const uint8_t* buf, size_t nbytes) {
+  Oracle* o = (Oracle*)h;
+  if (nbytes != (size_t)o->cfg.map_n * NMMO_MAP_TILES) return NMMO_E_SIZE;
+  for (size_t i = 0; i < nbytes; i++)
+    if (buf[i] >= 16) return NMMO_E_INVALID;
+  memcpy(o->bank, buf, nbytes);
+  return 0;
+}
+
 EXPORT int oracle_get_map_bank(void* h, uint8_t* buf, size_t nbytes) {
   Oracle* o = (Oracle*)h;
   if (nbytes != (size_t)o->cfg.map_n * NMMO_MAP_TILES) return NMMO_E_SIZE;

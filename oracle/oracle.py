@@ -43,6 +43,7 @@ def lib():
         L.oracle_get_state.argtypes = [vp, vp, sz]
         L.oracle_set_state.argtypes = [vp, vp, sz]
         L.oracle_get_map_bank.argtypes = [vp, vp, sz]
+        L.oracle_set_map_bank.argtypes = [vp, vp, sz]
         L.oracle_get_events.argtypes = [vp, i32, vp, i32, ctypes.POINTER(i32)]
         L.oracle_set_tasks.argtypes = [vp, vp, i32, vp, vp]
         L.oracle_obs_elems.argtypes = [i32]
@@ -140,6 +141,12 @@ class OracleEnvs:
         rc = lib().oracle_get_map_bank(self.h, _p(buf), buf.nbytes)
         assert rc == 0, rc
         return buf
+
+    def set_map_bank(self, bank: np.ndarray):
+        buf = np.ascontiguousarray(bank, dtype=np.uint8)
+        rc = lib().oracle_set_map_bank(self.h, _p(buf), buf.nbytes)
+        if rc != 0:
+            raise ValueError(f"oracle_set_map_bank failed ({rc})")
 
 
 def split_state(buf: np.ndarray, n_envs: int, slots: int, players: int = 128) -> dict:
