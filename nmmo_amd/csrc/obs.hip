@@ -22,7 +22,8 @@ constexpr int kObsFields = F_DS_ROW + 1;  // 0..30 obs columns, alive, ds_row
 // LDS: entity fields | row->slot | per-wave visible list | per-wave inventory | market listings
 __host__ __device__ inline size_t obs_lds_bytes(int S) {
   return (((size_t)kObsFields * S * 2 + 15) & ~(size_t)15) + (((size_t)(S + 1) * 2 + 15) & ~(size_t)15) +
-         (size_t)kObsWaves * 128 * 2 + (size_t)kObsWaves * kInv * 8 + (size_t)NMMO_MARKET_ROWS * 12;
+         (size_t)kObsWaves * 128 * 2 + (size_t)kObsWaves * kInv * 8 + (size_t)NMMO_MARKET_ROWS * 12 +
+         (size_t)kObsWaves * 256;  // per-wave 15x15 window materials (native layout)
 }
 
 // Plain (temporal) stores. Measured on MI355X (same-box A/B): __builtin_nontemporal_store
@@ -71,6 +72,7 @@ __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
   uint2* inv_all = reinterpret_cast<uint2*>(vis_all + kObsWaves * 128);
   uint2* mitem = inv_all + kObsWaves * kInv;                       // listed item words
   int* mown = reinterpret_cast<int*>(mitem + NMMO_MARKET_ROWS);    // listing owner slot
+  uint8_t* wmat_all = reinterpret_cast<uint8_t*>(mown + NMMO_MARKET_ROWS);
   const int e = blockIdx.x, g = blockIdx.y;
   const int tid = threadIdx.x;
   const int nm = p.mcount[e];
@@ -111,6 +113,7 @@ __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
   }
   const int lane = lane_id(), w = wave_id();
   int16_t* vis = vis_all + w * 128;
+  uint8_t* wmat = wmat_all + w * 256;
   const uint8_t* mat = p.mat + (size_t)e * kTiles;
   const int tick = p.env[(size_t)e * NMMO_NE + E_TICK];
   const bool combat = (p.systems & NMMO_SYS_COMBAT) != 0;
@@ -134,6 +137,14 @@ __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
     const int r = T[F_ROW * S + a], c = T[F_COL * S + a];
     const int gold = T[F_GOLD * S + a];
     if (lane < kInv) inv[lane] = p.items[((size_t)e * p.P + a) * kInv + lane];
+    uint32_t wm[4] = {0u, 0u, 0u, 0u};  // native: the 15x15 window materials, tile lane + 64 i
+    if constexpr (kNative) {
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const int t = lane + 64 * i;
+        if (t < 225) wm[i] = mat[(r + t / 15 - kVision) * kSize + c + t % 15 - kVision];
+      }
+    }
     // Entity.Query.window: ascending datastore rows within L-inf <= 7, first 100
     int nv = 0;
     for (int base = 1; base <= S; base += 64) {
@@ -150,6 +161,11 @@ __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
       nv += __popcll(b);
     }
     nv = min(nv, kNObs);
+    if constexpr (kNative) {
+#pragma unroll
+      for (int i = 0; i < 4; i++)
+        if (lane + 64 * i < 225) wmat[lane + 64 * i] = (uint8_t)wm[i];
+    }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
 
@@ -213,39 +229,108 @@ __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
       return v;
     };
     if constexpr (kNative) {
-      // masks: 4 bytes per lane per store
-      uint32_t* m32 = reinterpret_cast<uint32_t*>(nrow);
-      for (int j4 = lane; j4 < NMMO_NATIVE_MASK_BYTES / 4; j4 += 64) {
-        uint32_t v = 0u;
-#pragma unroll
-        for (int b = 0; b < 4; b++) {
-          const int j = 4 * j4 + b;
-          if (j < p.o_agent_id && mask_val(j)) v |= 1u << (8 * b);
-        }
-        m32[j4] = v;
-      }
-      // int16 part: AgentId, CurrentTick, Entity, Inventory, Tile, task index, pads (SPEC §8b)
-      const int task_idx = p.assign[(size_t)e * p.P + a];
-      auto i16v = [&](int i) -> int {
-        if (i == 0) return aid;
-        if (i == 1) return tick;
-        if (i < kNatInv) {
-          const int jj = i - kNatEntity, k = jj / NMMO_N_ENTITY_COLS, f = jj - k * NMMO_N_ENTITY_COLS;
-          return k < nv ? (int)T[f * S + vis[k]] : 0;
-        }
-        if (i < kNatTile) {
-          const int jj = i - kNatInv, k = jj >> 4;
-          return k < ninv ? (int)item_col(inv[k], aid, jj & 15) : 0;
-        }
-        if (i < kNatTask) {
-          const int jj = i - kNatTile, t = jj / 3, comp = jj - 3 * t;
-          const int tr = r + t / 15 - kVision, tc = c + t % 15 - kVision;
-          return comp == 0 ? tr : comp == 1 ? tc : (int)mat[tr * kSize + tc];
-        }
-        return i == kNatTask ? task_idx : 0;
+      // Section by section (no per-element section dispatch): every lane of a store works on the
+      // same section, the window materials were prefetched into registers ahead of the
+      // visibility compaction, and nothing below waits on global memory.
+      uint8_t* mb = nrow;  // u8 ActionTargets in flat order, then pad to NMMO_NATIVE_MASK_BYTES
+      const bool no_give = kWrap && (p.wflags & kWrapObsNoGive);
+      auto free_item = [&](int k) { return k < ninv && !it_equipped(inv[k]) && !it_price(inv[k]); };
+      auto same_tile = [&](int k) {
+        const int q = vis[k];
+        return q < p.P && q != a && T[F_ROW * S + q] == r && T[F_COL * S + q] == c;
       };
-      uint32_t* d32 = reinterpret_cast<uint32_t*>(nrow + NMMO_NATIVE_MASK_BYTES);
-      for (int j2 = lane; j2 < NMMO_NATIVE_I16 / 2; j2 += 64) d32[j2] = i16pack(i16v(2 * j2), i16v(2 * j2 + 1));
+      // one uniform loop over (section, 64-entry chunk): the section is a scalar, so its case runs
+      // without divergence and only its own operands are live
+      int sec = 0, k0 = 0;
+#pragma unroll 1
+      while (sec < 12) {
+        int lo, n;
+        switch (sec) {
+          case 0: lo = p.o_style; n = p.o_target - p.o_style; break;
+          case 1: lo = p.o_target; n = kNObs + 1; break;
+          case 2: lo = p.o_buy; n = NMMO_MARKET_ROWS + 1; break;
+          case 3: lo = p.o_destroy; n = kInv + 1; break;
+          case 4: lo = p.o_give_item; n = kInv + 1; break;
+          case 5: lo = p.o_give_target; n = kNObs + 1; break;
+          case 6: lo = p.o_gg_price; n = p.o_gg_target - p.o_gg_price; break;
+          case 7: lo = p.o_gg_target; n = kNObs + 1; break;
+          case 8: lo = p.o_move; n = p.o_sell_item - p.o_move; break;
+          case 9: lo = p.o_sell_item; n = kInv + 1; break;
+          case 10: lo = p.o_sell_price; n = p.o_use - p.o_sell_price; break;
+          default: lo = p.o_use; n = p.o_agent_id - p.o_use; break;
+        }
+        const int k = k0 + lane;
+        if (k < n) {
+          bool v;
+          switch (sec) {
+            case 0: v = combat; break;
+            case 1:
+              if (k == kNObs) {
+                v = true;
+              } else if (!combat || k >= nv) {
+                v = false;
+              } else {
+                const int q = vis[k];
+                v = q != a && linf(r, c, T[F_ROW * S + q], T[F_COL * S + q]) <= 3 &&
+                    !(q < p.P && T[F_TIME_ALIVE * S + q] < p.spawn_immunity);
+                if constexpr (kWrap)
+                  if ((p.wflags & kWrapObsNoDangerous) && T[F_NPC_TYPE * S + q] > 1) v = false;
+              }
+              break;
+            case 2: v = k == NMMO_MARKET_ROWS || (exch && k < nm && it_price(mitem[k]) <= gold && mown[k] != a); break;
+            case 3: v = k == kInv || (item && free_item(k)); break;
+            case 4: v = k == kInv || (!no_give && item && free_item(k)); break;
+            case 5: v = k == kNObs || (!no_give && item && k < nv && same_tile(k)); break;
+            case 6: v = exch && k < gold && (!no_give || k == 0); break;
+            case 7: v = k == kNObs || (!no_give && exch && k < nv && same_tile(k)); break;
+            case 8: v = !impassable(wmat[(kVision + dir_dr(k)) * 15 + kVision + dir_dc(k)]); break;
+            case 9: v = k == kInv || (exch && k < ninv && !it_equipped(inv[k])); break;
+            case 10:
+              v = exch;
+              if constexpr (kWrap)
+                if ((p.wflags & kWrapObsPrice) && k == prev_price) v = false;
+              break;
+            default: v = k == kInv || (item && k < ninv && item_usable(T, S, a, inv[k])); break;
+          }
+          mb[lo + k] = v ? 1 : 0;
+        }
+        k0 += 64;
+        if (k0 >= n) {
+          sec++;
+          k0 = 0;
+        }
+      }
+      if (lane < NMMO_NATIVE_MASK_BYTES - p.o_agent_id) mb[p.o_agent_id + lane] = 0;
+      // int16 part: AgentId, CurrentTick, Entity 100x31, Inventory 12x16, Tile 225x3, task index,
+      // zero pads (SPEC §8b)
+      int16_t* d16 = reinterpret_cast<int16_t*>(nrow + NMMO_NATIVE_MASK_BYTES);
+      if (lane == 0) d16[0] = (int16_t)aid;
+      if (lane == 1) d16[1] = (int16_t)tick;
+      {  // two entity rows per pass: lanes 0-30 row k, lanes 32-62 row k + 1, one column each
+        const int f = lane & 31, half = lane >> 5;
+#pragma unroll 1
+        for (int k0 = 0; k0 < kNObs; k0 += 2) {
+          const int k = k0 + half;
+          if (f < NMMO_N_ENTITY_COLS)
+            d16[kNatEntity + k * NMMO_N_ENTITY_COLS + f] = k < nv ? T[f * S + vis[k]] : (int16_t)0;
+        }
+      }
+      for (int j = lane; j < kInv * 16; j += 64) {
+        const int k = j >> 4;
+        d16[kNatInv + j] = k < ninv ? (int16_t)(int)item_col(inv[k], aid, j & 15) : (int16_t)0;
+      }
+#pragma unroll 1
+      for (int i = 0; i < 4; i++) {
+        const int t = lane + 64 * i;
+        if (t < 225) {
+          const int tr = r + t / 15 - kVision, tc = c + t % 15 - kVision;
+          d16[kNatTile + 3 * t] = (int16_t)tr;
+          d16[kNatTile + 3 * t + 1] = (int16_t)tc;
+          d16[kNatTile + 3 * t + 2] = (int16_t)wm[i];
+        }
+      }
+      if (lane == 0) d16[kNatTask] = (int16_t)p.assign[(size_t)e * p.P + a];
+      else if (lane < NMMO_NATIVE_I16 - kNatTask) d16[kNatTask + lane] = 0;
       __builtin_amdgcn_wave_barrier();
       continue;
     }

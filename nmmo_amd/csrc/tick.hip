@@ -86,11 +86,11 @@ struct Ctx {
 // Diagnostic build only (-DNMMO_STAMPS, tools/stamps.py): thread 0 stamps the shader clock right
 // after phase barriers; never compiled into the product library.
 #ifdef NMMO_STAMPS
-__device__ unsigned long long g_stamps[4096 * 16];
+__device__ unsigned long long g_stamps[4096 * 32];
 #define NMMO_STAMP(k)                                                        \
   do {                                                                       \
     if (threadIdx.x == 0 && blockIdx.x < 4096)                               \
-      g_stamps[blockIdx.x * 16 + (k)] = __builtin_amdgcn_s_memtime();        \
+      g_stamps[blockIdx.x * 32 + (k)] = __builtin_amdgcn_s_memtime();        \
   } while (0)
 #else
 #define NMMO_STAMP(k) \
@@ -1580,7 +1580,9 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
       ng_mine += __popc(nz & 0x11111111u);
     }
     int ngroups;
+    NMMO_STAMP(16);
     const int gpos = block_prefix_sum(ng_mine, wtot_next(c), &ngroups);
+    NMMO_STAMP(17);
     int16_t* glist = reinterpret_cast<int16_t*>(c.vism);  // dead after decode
     const int gcap = 128 * NW * 4;                         // int16 entries in vism's bytes
     const uint32_t rtick = (uint32_t)(tick + 1);
@@ -1598,6 +1600,7 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
         }
       }
       __syncthreads();
+      NMMO_STAMP(18);
       const uint32_t* base4 = reinterpret_cast<const uint32_t*>(base);  // 4 tiles per word
       for (int i = tid; i < ngroups; i += nt) {
         const int g = glist[i], w = g >> 3, sh = (g & 7) * 4;
@@ -1642,6 +1645,7 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
       if (it_price(inv[k]) && tick + 1 - it_ltick(inv[k]) > 5) inv[k].x &= 0x3FFu;
     }
   }
+  NMMO_STAMP(19);
   __syncthreads();
   if (tid == 0) c.E[E_TICK] = tick + 1;
   __syncthreads();
@@ -1720,6 +1724,7 @@ __global__ void tick_kernel(DevState st, const int32_t* __restrict__ actions,
   Ctx c = make_ctx(smem, st, e, kSys ? kSys : st.cfg.systems);
   load_env(c, st, e);
   __syncthreads();
+  NMMO_STAMP(20);
   const size_t o = (size_t)e * c.P;
   const bool reset_path = mode == 1 || c.E[E_DONE];
   if (reset_path) {

@@ -7,19 +7,34 @@
 # Usage: bash profiles/run_rocprof.sh <round-tag> [configs...]
 set -e -o pipefail
 TAG=${1:-r01}; shift || true
-CONFIGS=${@:-C2 C3 C4}
+CONFIGS=${@:-C2 C3 C4 C4-native storage}
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 for c in $CONFIGS; do
   mkdir -p $OUT/$c
+  case $c in
+    *-native) ARGS="--config ${c%-native} --obs native" ;;
+    *) ARGS="--config $c" ;;
+  esac
+  if [ "$c" = storage ]; then  # experience-storage kernels (tools/bench_storage.py)
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/$c/trace -o run -- \
+      python3 tools/bench_storage.py > $OUT/$c/bench_storage.json
+    timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/$c/fetch -o run -- \
+      python3 tools/bench_storage.py > /dev/null
+    timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/$c/write -o run -- \
+      python3 tools/bench_storage.py > /dev/null
+    python3 tools/pmc_summary.py $OUT/$c > $OUT/$c/pmc.json
+    echo "profiled $c"
+    continue
+  fi
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/$c/trace -o run -- \
-    python3 bench.py --config $c --steps 100 --warmup 20 --no-cpu-baseline > $OUT/$c/bench.json
-  timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/$c/fetch -o run -- \
-    python3 bench.py --config $c --steps 30 --warmup 5 --no-cpu-baseline > /dev/null
-  timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/$c/write -o run -- \
-    python3 bench.py --config $c --steps 30 --warmup 5 --no-cpu-baseline > /dev/null
+    python3 bench.py $ARGS --steps 100 --warmup 20 --no-cpu-baseline > $OUT/$c/bench.json
+  timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/$c/fetch -o run -- \
+    python3 bench.py $ARGS --steps 30 --warmup 5 --no-cpu-baseline > /dev/null
+  timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/$c/write -o run -- \
+    python3 bench.py $ARGS --steps 30 --warmup 5 --no-cpu-baseline > /dev/null
   python3 tools/pmc_summary.py $OUT/$c > $OUT/$c/pmc.json
   echo "profiled $c"
 done

@@ -40,16 +40,19 @@ def main():
         eng.step()
         torch.cuda.synchronize()
         if t >= warm:
-            buf = np.zeros(4096 * 16, np.uint64)
+            buf = np.zeros(4096 * 32, np.uint64)
             assert L.nmmo_debug_read_stamps(buf.ctypes.data_as(ctypes.c_void_p), buf.size) == 0
-            st = buf.reshape(4096, 16)[:min(envs, 4096), :12].astype(np.int64)
+            st = buf.reshape(4096, 32)[:min(envs, 4096), :12].astype(np.int64)
             ok = (st[:, 2] > 0) & (st[:, 11] > st[:, 0])  # stepped (not reset) envs
             d = np.diff(st[ok], axis=1)
             rows.append(d)
-            full = buf.reshape(4096, 16)[:min(envs, 4096)].astype(np.int64)[ok]
+            full = buf.reshape(4096, 32)[:min(envs, 4096)].astype(np.int64)[ok]
             subs.append(np.stack([full[:, 12] - full[:, 1], full[:, 2] - full[:, 12],
                                   full[:, 13] - full[:, 1], full[:, 15] - full[:, 3],
-                                  full[:, 14] - full[:, 15], full[:, 4] - full[:, 14]], 1))
+                                  full[:, 14] - full[:, 15], full[:, 4] - full[:, 14],
+                                  full[:, 16] - full[:, 7], full[:, 17] - full[:, 16], full[:, 18] - full[:, 17],
+                                  full[:, 19] - full[:, 18], full[:, 8] - full[:, 19],
+                                  full[:, 20] - full[:, 0]], 1))
     d = np.concatenate(rows)
     tot = np.median(d.sum(1))
     print(f"{preset} envs={envs}: median total {tot:.0f} cycles over {len(d)} env-ticks")
@@ -62,6 +65,10 @@ def main():
     print(f"  update+harvest = resource {np.median(d[:, 2]):9.0f} + professions "
           f"{np.median(sub[:, 3]):9.0f}; item actions (Use..Destroy) {np.median(sub[:, 4]):9.0f}; "
           f"attack init {np.median(sub[:, 5]):9.0f}")
+    print(f"  respawn = count {np.median(sub[:, 6]):9.0f} + prefix {np.median(sub[:, 7]):9.0f} + list "
+          f"{np.median(sub[:, 8]):9.0f} + draws {np.median(sub[:, 9]):9.0f} + expiry/tick {np.median(sub[:, 10]):9.0f}; "
+          f"groups n/a")
+    print(f"  rowslot phase: state load {np.median(sub[:, 11]):9.0f}")
 
 
 if __name__ == "__main__":
