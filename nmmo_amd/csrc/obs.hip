@@ -20,10 +20,12 @@ constexpr int kObsWaves = 4;
 constexpr int kObsFields = F_DS_ROW + 1;  // 0..30 obs columns, alive, ds_row
 
 // LDS: entity fields | row->slot | per-wave visible list | per-wave inventory | market listings
-__host__ __device__ inline size_t obs_lds_bytes(int S) {
+// (flat: listed item words + owners, 12 B per listing; native: price | owner << 8, 2 B per listing,
+// and per-wave 15x15 window materials)
+__host__ __device__ inline size_t obs_lds_bytes(int S, bool native) {
   return (((size_t)kObsFields * S * 2 + 15) & ~(size_t)15) + (((size_t)(S + 1) * 2 + 15) & ~(size_t)15) +
-         (size_t)kObsWaves * 128 * 2 + (size_t)kObsWaves * kInv * 8 + (size_t)NMMO_MARKET_ROWS * 12 +
-         (size_t)kObsWaves * 256;  // per-wave 15x15 window materials (native layout)
+         (size_t)kObsWaves * 128 * 2 + (size_t)kObsWaves * kInv * 8 +
+         (native ? (size_t)NMMO_MARKET_ROWS * 2 + (size_t)kObsWaves * 256 : (size_t)NMMO_MARKET_ROWS * 12);
 }
 
 // Plain (temporal) stores. Measured on MI355X (same-box A/B): __builtin_nontemporal_store
@@ -70,17 +72,23 @@ __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
   int16_t* rowslot = reinterpret_cast<int16_t*>(smem + (((size_t)kObsFields * S * 2 + 15) & ~(size_t)15));
   int16_t* vis_all = rowslot + ((((size_t)(S + 1) * 2 + 15) & ~(size_t)15) / 2);
   uint2* inv_all = reinterpret_cast<uint2*>(vis_all + kObsWaves * 128);
-  uint2* mitem = inv_all + kObsWaves * kInv;                       // listed item words
-  int* mown = reinterpret_cast<int*>(mitem + NMMO_MARKET_ROWS);    // listing owner slot
-  uint8_t* wmat_all = reinterpret_cast<uint8_t*>(mown + NMMO_MARKET_ROWS);
+  uint2* mitem = inv_all + kObsWaves * kInv;                       // flat: listed item words
+  int* mown = reinterpret_cast<int*>(mitem + NMMO_MARKET_ROWS);    // flat: listing owner slot
+  uint16_t* mpo = reinterpret_cast<uint16_t*>(inv_all + kObsWaves * kInv);  // native: price | owner << 8
+  uint8_t* wmat_all = reinterpret_cast<uint8_t*>(mpo + NMMO_MARKET_ROWS);   // native only
   const int e = blockIdx.x, g = blockIdx.y;
   const int tid = threadIdx.x;
   const int nm = p.mcount[e];
   for (int j = tid; j < nm; j += blockDim.x) {  // end-of-tick listings, ascending row
     const int v = p.mlist[(size_t)e * NMMO_MARKET_ROWS + j];
     const int own = (v >> 16) & 255, slot = (v >> 24) & 15;
-    mown[j] = own;
-    mitem[j] = p.items[((size_t)e * p.P + own) * kInv + slot];
+    const uint2 wd = p.items[((size_t)e * p.P + own) * kInv + slot];
+    if constexpr (kNative) {
+      mpo[j] = (uint16_t)(it_price(wd) | own << 8);
+    } else {
+      mown[j] = own;
+      mitem[j] = wd;
+    }
   }
   {
     const int16_t* src = p.ent + (size_t)e * NMMO_NF * S;
@@ -100,14 +108,21 @@ __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
   __syncthreads();
 
   if constexpr (kNative) {  // the env's Market, once per env (the y == 0 workgroup)
-    if (g == 0) {
-      uint32_t* mk = reinterpret_cast<uint32_t*>(p.nat + (size_t)e * native_env_bytes(p.P) +
-                                                 (size_t)p.P * NMMO_NATIVE_ROW_BYTES);
-      for (int j2 = tid; j2 < NMMO_MARKET_ROWS * 8; j2 += blockDim.x) {
-        const int j = 2 * j2, k = j >> 4;
-        uint32_t v = 0u;
-        if (k < nm) v = i16pack((int)item_col(mitem[k], mown[k] + 1, j & 15), (int)item_col(mitem[k], mown[k] + 1, (j + 1) & 15));
-        mk[j2] = v;
+    if (g == 0) {  // one listing row (16 int16 = two 16-B stores) per thread
+      uint4* mk = reinterpret_cast<uint4*>(p.nat + (size_t)e * native_env_bytes(p.P) +
+                                           (size_t)p.P * NMMO_NATIVE_ROW_BYTES);
+      for (int k = tid; k < NMMO_MARKET_ROWS; k += blockDim.x) {
+        uint32_t q[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+        if (k < nm) {
+          const int v = p.mlist[(size_t)e * NMMO_MARKET_ROWS + k];
+          const int own = (v >> 16) & 255, slot = (v >> 24) & 15;
+          const uint2 wd = p.items[((size_t)e * p.P + own) * kInv + slot];
+#pragma unroll
+          for (int i = 0; i < 8; i++)
+            q[i] = i16pack((int)item_col(wd, own + 1, 2 * i), (int)item_col(wd, own + 1, 2 * i + 1));
+        }
+        mk[2 * k] = make_uint4(q[0], q[1], q[2], q[3]);
+        mk[2 * k + 1] = make_uint4(q[4], q[5], q[6], q[7]);
       }
     }
   }
@@ -239,6 +254,26 @@ __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
         const int q = vis[k];
         return q < p.P && q != a && T[F_ROW * S + q] == r && T[F_COL * S + q] == c;
       };
+      // Buy.MarketItem (1,025 entries, the longest section): four entries per lane per dword store
+      // from one 8-B LDS read of the packed listings (the section starts dword-aligned in the
+      // SPEC §8b layout; the per-byte case below covers any other offset)
+      const bool buy4 = (p.o_buy & 3) == 0;
+      if (buy4) {
+        uint32_t* b32 = reinterpret_cast<uint32_t*>(mb + p.o_buy);
+        for (int j4 = lane; j4 < NMMO_MARKET_ROWS / 4; j4 += 64) {
+          uint32_t v = 0u;
+          if (exch && 4 * j4 < nm) {
+            const uint2 q = *reinterpret_cast<const uint2*>(mpo + 4 * j4);
+#pragma unroll
+            for (int b = 0; b < 4; b++) {
+              const uint32_t pw = ((b < 2 ? q.x : q.y) >> (16 * (b & 1))) & 0xFFFFu;
+              if (4 * j4 + b < nm && (int)(pw & 255u) <= gold && (int)(pw >> 8) != a) v |= 1u << (8 * b);
+            }
+          }
+          b32[j4] = v;
+        }
+        if (lane == 0) mb[p.o_buy + NMMO_MARKET_ROWS] = 1;
+      }
       // one uniform loop over (section, 64-entry chunk): the section is a scalar, so its case runs
       // without divergence and only its own operands are live
       int sec = 0, k0 = 0;
@@ -248,7 +283,7 @@ __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
         switch (sec) {
           case 0: lo = p.o_style; n = p.o_target - p.o_style; break;
           case 1: lo = p.o_target; n = kNObs + 1; break;
-          case 2: lo = p.o_buy; n = NMMO_MARKET_ROWS + 1; break;
+          case 2: lo = p.o_buy; n = buy4 ? 0 : NMMO_MARKET_ROWS + 1; break;
           case 3: lo = p.o_destroy; n = kInv + 1; break;
           case 4: lo = p.o_give_item; n = kInv + 1; break;
           case 5: lo = p.o_give_target; n = kNObs + 1; break;
@@ -277,7 +312,9 @@ __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
                   if ((p.wflags & kWrapObsNoDangerous) && T[F_NPC_TYPE * S + q] > 1) v = false;
               }
               break;
-            case 2: v = k == NMMO_MARKET_ROWS || (exch && k < nm && it_price(mitem[k]) <= gold && mown[k] != a); break;
+            case 2:
+              v = k == NMMO_MARKET_ROWS || (exch && k < nm && (int)(mpo[k] & 255u) <= gold && (int)(mpo[k] >> 8) != a);
+              break;
             case 3: v = k == kInv || (item && free_item(k)); break;
             case 4: v = k == kInv || (!no_give && item && free_item(k)); break;
             case 5: v = k == kNObs || (!no_give && item && k < nv && same_tile(k)); break;
@@ -365,7 +402,7 @@ __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
 hipError_t launch_obs(const ObsParams& p, hipStream_t stream) {
   dim3 grid(p.n_envs, (p.P + kObsAgentsPerBlock - 1) / kObsAgentsPerBlock);
   const dim3 block(64 * kObsWaves);
-  const size_t lds = obs_lds_bytes(p.S);
+  const size_t lds = obs_lds_bytes(p.S, p.nat != nullptr);
   if (p.nat) {
     if (p.wflags) hipLaunchKernelGGL((obs_kernel<true, true>), grid, block, lds, stream, p);
     else hipLaunchKernelGGL((obs_kernel<false, true>), grid, block, lds, stream, p);
