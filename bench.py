@@ -276,6 +276,24 @@ def main():
         one()
     tick_ms, obs_ms, n_timed, wrap_ms = eng.read_timing()
     eng.set_timing(False)
+    # The roofline's tick duration without per-kernel event overhead (which inflates a ~15 us
+    # launch by ~20%): the timed step (policy + nmmo_step, graph-replayed) minus a hipGraph of
+    # `batch` policy-only launches timed with HIP events on the same stream. Timing nmmo_step
+    # alone would need stale actions, which change the tick's work (attack rounds) at C3/C4.
+    batch = 20
+    pol_graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(pol_graph):
+        for _ in range(batch):
+            eng.scripted_actions(pseed)
+    b0, b1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    pol_graph.replay()
+    b0.record()
+    reps = 10
+    for _ in range(reps):
+        pol_graph.replay()
+    b1.record()
+    torch.cuda.synchronize(dev)
+    policy_avg_ms = b0.elapsed_time(b1) / (reps * batch)
     # practical HBM write ceiling on THIS box: the vendor fill kernel over the same obs buffer
     # (the same byte count the obs kernel writes per launch), HIP events on the current stream
     fill_gbs = None
@@ -309,8 +327,15 @@ def main():
         obs_b = obs_bytes_per_env(S, P, eng.obs_elems, native) * envs if wl["obs"] else 0
         if wl["obs"] and obs_avg_ms > tick_avg_ms:
             kern, byts, ms = "obs_kernel", obs_b, obs_avg_ms
+            timing = "HIP events around each obs_kernel launch on the launch stream"
         else:
             kern, byts, ms = "tick_kernel", tick_b, tick_avg_ms
+            timing = "HIP events around each tick_kernel launch on the launch stream"
+            if not wl["obs"] and args.wrapper == "none" and plan and not gather:
+                # nmmo_step = the tick kernel alone: timed step minus the policy launch
+                ms = elapsed * 1e3 / args.steps - policy_avg_ms
+                timing = (f"timed step (hipGraph: policy + tick) minus a {batch}-launch policy-only "
+                          f"hipGraph, HIP events on the launch stream")
         achieved = byts / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
         traffic, traffic_src = pmc_traffic(args.config + ("-native" if native and args.config != "C5" else ""),
                                            kern, envs)
@@ -347,7 +372,7 @@ def main():
             },
             "slot_steps_per_sec": round(slots_total / elapsed, 1),
             "alive_fraction": round(alive_total / slots_total, 4),
-            "kernel_ms": {"tick": round(tick_avg_ms, 5),
+            "kernel_ms": {"policy": round(policy_avg_ms, 5), "tick": round(tick_avg_ms, 5),
                           "obs": round(obs_avg_ms, 5) if wl["obs"] else None,
                           "wrapper": round(wrap_ms / max(n_timed, 1), 5) if args.wrapper != "none" else None},
             "wrapper": None if args.wrapper == "none" else args.wrapper,
@@ -364,6 +389,8 @@ def main():
                 "traffic": traffic,
                 "traffic_source": traffic_src,
                 "bytes_per_launch": byts,
+                "avg_launch_ms": round(ms, 5),
+                "timing": timing,
                 "write_ceiling_gbs": None if fill_gbs is None else round(fill_gbs, 1),
                 "frac_of_write_ceiling": None if not fill_gbs or kern != "obs_kernel" else round(achieved / fill_gbs, 4),
             },
