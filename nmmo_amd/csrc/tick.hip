@@ -263,21 +263,28 @@ __device__ __forceinline__ void copy_segs(const Seg16 (&sg)[6], int tid, int nt)
            : i < e4 ? sg[4].d + (i - e3)
                     : sg[5].d + (i - e4);
   };
+  // Full batches of U words per thread issue all U loads before the first LDS store. The
+  // remainder (the whole copy at C2/C3: 3.7 and 6.3 words per thread) goes in batches of 4 whose
+  // loads read a clamped index instead of branching around them, so 4 loads are in flight at once
+  // at a quarter of the full batch's registers.
   constexpr int U = 8;
   int b = tid;
-  for (; b + (U - 1) * nt < total; b += U * nt) {  // full batches: U loads in flight
-    uint4 r0 = *src(b), r1 = *src(b + nt), r2 = *src(b + 2 * nt), r3 = *src(b + 3 * nt);
-    uint4 r4 = *src(b + 4 * nt), r5 = *src(b + 5 * nt), r6 = *src(b + 6 * nt), r7 = *src(b + 7 * nt);
-    *dst(b) = r0;
-    *dst(b + nt) = r1;
-    *dst(b + 2 * nt) = r2;
-    *dst(b + 3 * nt) = r3;
-    *dst(b + 4 * nt) = r4;
-    *dst(b + 5 * nt) = r5;
-    *dst(b + 6 * nt) = r6;
-    *dst(b + 7 * nt) = r7;
+  for (; b + (U - 1) * nt < total; b += U * nt) {
+    uint4 r[U];
+#pragma unroll
+    for (int k = 0; k < U; k++) r[k] = *src(b + k * nt);
+#pragma unroll
+    for (int k = 0; k < U; k++) *dst(b + k * nt) = r[k];
   }
-  for (; b < total; b += nt) *dst(b) = *src(b);
+  constexpr int T = 4;
+  for (; b < total; b += T * nt) {
+    uint4 r[T];
+#pragma unroll
+    for (int k = 0; k < T; k++) r[k] = *src(min(b + k * nt, total - 1));
+#pragma unroll
+    for (int k = 0; k < T; k++)
+      if (b + k * nt < total) *dst(b + k * nt) = r[k];
+  }
 }
 
 __device__ __forceinline__ void load_env(Ctx& c, const DevState& st, int e) {
