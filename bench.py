@@ -2,18 +2,33 @@
 """bench.py — agent-steps/sec of the MI355X Neural MMO stepper (BASELINE.json metric).
 
 One "step" = one tick of every env on this GPU: the scripted masked-uniform policy kernel
-(SPEC.md §10, the synthetic action input) + nmmo_step (tick kernel [+ obs kernel]).
-Inputs/state are resident in HBM before the timed region. Envs shard across ranks with no
-data-path collective (weak scaling: envs per GPU fixed); each rank times K steps between a
-barrier + device sync, rank 0 reports the max over ranks.
+(SPEC.md §10, the synthetic action input) + nmmo_step (tick kernel + obs kernel). Inputs and
+state are resident in HBM before the timed region. Envs shard across ranks with no data-path
+collective (weak scaling: envs per GPU fixed); each rank times K steps between a barrier +
+device sync, rank 0 reports the max over ranks.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2|C3|C4] [--envs E]
-  torchrun --nproc-per-node N bench.py --gpus N ...
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config C4|C2|C3|C5] [--obs flat|native]
+
+`--gpus N` with N > 1 and no WORLD_SIZE in the environment starts N ranks itself (a child
+`torch.distributed.run --nproc-per-node N`, before anything touches the GPU) and exits with its
+status; under torchrun WORLD_SIZE must equal N.
+
+Headline workload (default): BASELINE.json configs[3] = C4, 1024 envs x 128 agents per GPU,
+all ten systems, the pufferlib-flat float32 obs row the reference learner reads. At N = 1 the
+line also carries `extra_configs` (C2, C3, C4 with the native obs layout) measured the same way.
+
+Steady state: envs start with staggered episode phases (`--stagger L`: during an untimed
+pre-roll of L ticks, the envs e = k mod L end their episode at pre-roll tick k, via
+nmmo_end_episodes, the per-env reset of an async pool), so every timed window holds deaths,
+culls and in-kernel auto-resets in the proportions of a long run, as in the reference's async
+worker pool (config.yaml env_pool: True) where envs never run in lockstep.
 
 value = alive agent-steps/s over the whole job (the reference's agent_SPS = sum(mask)/time,
-reinforcement_learning/clean_pufferl.py:306,365); slot-steps/s (envs x 128 x ticks / s, the
-padded count, :307,364) is reported beside it. cpu_baseline = the CPU oracle (a port of the
-same semantics, not nmmo 2.1, which is absent) on the host's cores, rank 0 at N=1 only.
+reinforcement_learning/clean_pufferl.py:306,365), counted on the device; slot-steps/s (envs x
+128 x ticks / s, the padded count, :307,364) is reported beside it. cpu_baseline = the CPU
+oracle (a port of the same semantics, not nmmo 2.1, which is absent) on the host cores,
+rank 0 at N = 1 only: one thread per usable core, plus the single-thread 1 env x 128 agents
+C1 leg (BASELINE.json configs[0]).
 """
 
 from __future__ import annotations
@@ -21,6 +36,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import threading
 import time
@@ -32,19 +49,19 @@ METRIC = "agent-steps/sec (whole node), 128-agent envs at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 WORKLOADS = {
-    # BASELINE.json configs[1..3]; early stop 8 = config.yaml reward_wrapper.early_stop_agent_num
+    # BASELINE.json configs[1..4]
     "C2": dict(envs=256, preset="C2", obs=False,
                desc="C2: 256 envs x 128 agents, movement + food/water (Resource)"),
     "C3": dict(envs=1024, preset="C3", obs=False,
                desc="C3: 1024 envs x 128 agents, + melee/range/mage combat, NPC spawn/AI, progression"),
-    "C4": dict(envs=1024, preset="C4", obs=True,
-               desc="C4: 1024 envs x 128 agents, all systems + per-agent flat obs gather"),
-    # BASELINE.json configs[4]: C4 per GPU (8192 envs on 8) + the learner gather every step
+    "C4": dict(envs=1024, preset="C4", obs=True, layout="flat",
+               desc="C4: 1024 envs x 128 agents, all systems + per-agent obs gather"),
+    # C4 per GPU (8192 envs on 8) + the learner gather of every rank's obs/outputs each step
     "C5": dict(envs=1024, preset="C4", obs=True, gather=True, layout="native",
-               desc="C5: 1024 envs x 128 agents per GPU, all systems + obs, RCCL gather of "
-                    "obs/reward/dones/mask to the learner (rank 0) every step"),
+               desc="C5: 1024 envs x 128 agents per GPU, all systems + obs, RCCL point-to-point "
+                    "gather of obs/reward/dones/mask to the learner (rank 0) every step"),
 }
-
+EXTRAS = [("C2", None), ("C3", None), ("C4", "native")]
 
 # the agent sections' reward_wrapper weights (config.yaml:103-106, 118-126, 137-140)
 WRAPPER_KW = {"neurips23_start_kit": dict(heal_bonus_weight=0.03, explore_bonus_weight=0.01),
@@ -52,23 +69,35 @@ WRAPPER_KW = {"neurips23_start_kit": dict(heal_bonus_weight=0.03, explore_bonus_
               "yaofeng": dict(hp_bonus_weight=0.03, exp_bonus_weight=0.002, defense_bonus_weight=0.04,
                               attack_bonus_weight=0.0, gold_bonus_weight=0.001, custom_bonus_scale=0.1,
                               disable_give=True, donot_attack_dangerous_npc=True)}
+EVENT_ROW_BYTES = 9 * 4
 
 
-def tick_bytes_per_env(S: int, P: int, items: bool) -> int:
+def tick_bytes_per_env(S: int, P: int, items: bool, events_per_env: float = 0.0) -> int:
     """Algorithmic HBM bytes of one tick of one env: the env state read and
     written once (45 int16 entity fields x slots, free-row ring, depleted-tile bitmap, env
     scalars; with the Item system the 12-slot inventories and the item-row ring), the actions
-    read, the outputs written and the map tiles a player touches (own tile + 4 neighbours for
-    harvest/drink, 1 move target)."""
+    read, the outputs written, the map tiles a player touches (own tile + 4 neighbours for
+    harvest/drink, 1 move target) and the event-log rows appended (36 B each; measured mean
+    per env-tick)."""
     state = 45 * S * 2 + S * 2 + 800 * 4 + 16 * 4
     if items:
         state += P * 12 * 8 + 12 * P * 2
-    return 2 * state + P * 12 * 4 + P * (4 + 1 + 1 + 1) + P * 6
+    return int(2 * state + P * 12 * 4 + P * (4 + 1 + 1 + 1) + P * 6 + events_per_env * EVENT_ROW_BYTES)
+
+
+def obs_bytes_per_env(S: int, P: int, elems: int, native: bool = False) -> int:
+    """Obs rows written (flat fp32: 23,987 x 4 B per agent; native, SPEC §8b: 9,552 B per agent
+    + the env's 32 KB Market once) + the entity columns staged once per 16-agent workgroup +
+    the 15x15 tile window read per agent."""
+    from nmmo_amd import abi
+
+    rows = abi.native_env_bytes(P) if native else P * elems * 4
+    return rows + (P // 16) * (33 * S * 2) + P * 225
 
 
 def pmc_traffic(cfg_name: str, kernel: str, envs: int):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of the same
-    bench command (profiles/<round>/<cfg>/pmc.json, tools/pmc_summary.py): 2 x FETCH_SIZE +
+    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary of the
+    same workload (profiles/<round>/<cfg>/pmc.json, tools/pmc_summary.py): 2 x FETCH_SIZE +
     WRITE_SIZE, gfx950-corrected. None when no summary matches this workload."""
     import glob
 
@@ -84,26 +113,19 @@ def pmc_traffic(cfg_name: str, kernel: str, envs: int):
     return None, None
 
 
-def obs_bytes_per_env(S: int, P: int, elems: int, native: bool = False) -> int:
-    """Obs rows written (flat fp32: 23,987 x 4 B per agent; native, SPEC §8b: 9,552 B per agent
-    + the env's 32 KB Market once) + the entity columns staged once per 16-agent workgroup +
-    the 15x15 tile window read per agent."""
-    from nmmo_amd import abi
-
-    rows = abi.native_env_bytes(P) if native else P * elems * 4
-    return rows + (P // 16) * (33 * S * 2) + P * 225
-
-
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=300)
     ap.add_argument("--warmup", type=int, default=50)
-    ap.add_argument("--config", default="C2", choices=sorted(WORKLOADS))
+    ap.add_argument("--config", default="C4", choices=sorted(WORKLOADS))
     ap.add_argument("--envs", type=int, default=None, help="envs per GPU (default: config's)")
     ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--stagger", type=int, default=64,
+                    help="pre-roll ticks over which env episode phases are staggered (0 = lockstep)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true", help="skip the extra_configs at N = 1")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraph replay")
     ap.add_argument("--graph-steps", type=int, default=10, help="ticks captured per hipGraph")
     ap.add_argument("--obs", default=None, choices=["flat", "native"],
@@ -113,27 +135,70 @@ def parse():
                     choices=["none", "base", "neurips23_start_kit", "takeru", "yaofeng"],
                     help="run env_creator's RewardWrapper on the device (SPEC §13) with the "
                          "config.yaml weights")
-    return ap.parse_args()
+    ap.add_argument("--dry-launch", action="store_true",
+                    help="launcher check: each rank prints its RANK/WORLD_SIZE and exits (no GPU)")
+    return ap.parse_args(argv)
 
 
-def cpu_baseline(cfg, seconds: float):
-    """The CPU oracle (oracle/, a port of SPEC.md) on the host cores: one Python thread per core,
-    each stepping its own env range through ctypes (the GIL is released inside the C calls)."""
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args) -> int:
+    """Start args.gpus ranks of this script under torch.distributed.run (one process per GPU,
+    127.0.0.1 rendezvous) as a child process; returns its exit status. Runs before any GPU
+    call in this process (the parent never initialises HIP)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()), os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.call(cmd, env=env)
+
+
+# ------------------------------------------------------------------------------- CPU baseline
+def cpu_info() -> dict:
+    """The host cores this process may use: the affinity mask, capped by a cgroup CPU quota
+    when one is set (the GPU box gives each one-GPU job a share of a larger machine), and the
+    CPU model."""
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = os.cpu_count() or 1
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(period)))
+    except (OSError, ValueError):
+        pass
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    usable = min(affinity, quota) if quota else affinity
+    return {"affinity": affinity, "cgroup_quota_cpus": quota, "usable": usable, "model": model}
+
+
+def _cpu_rate(cfg, n_envs: int, threads: int, seconds: float, seed: int):
+    """agent-steps/s of the CPU oracle stepping n_envs envs on `threads` Python threads (each owns
+    an env range; the GIL is released inside the C calls), scripted actions included."""
     import numpy as np
 
     from oracle.oracle import OracleEnvs
-
-    try:
-        cores = len(os.sched_getaffinity(0))
-    except AttributeError:
-        cores = os.cpu_count() or 1
-    threads = max(1, min(cores, 16))
-    per = 4
-    n = threads * per
-    o = OracleEnvs(cfg, n, seed=7)
-    o.reset()
-    acts = np.zeros((n, cfg.PLAYER_N, 12), np.int32)
     from oracle.oracle import lib as olib
+
+    o = OracleEnvs(cfg, n_envs, seed=seed)
+    o.reset()
+    acts = np.zeros((n_envs, cfg.PLAYER_N, 12), np.int32)
+    per = n_envs // threads
 
     def worker(k, counter, stop_at):
         lo, hi = k * per, (k + 1) * per
@@ -144,59 +209,58 @@ def cpu_baseline(cfg, seconds: float):
             counter[k] += int(o.mask[lo:hi].sum())
             t += 1
 
+    def run(secs, counter):
+        stop_at = time.perf_counter() + secs
+        ths = [threading.Thread(target=worker, args=(k, counter, stop_at)) for k in range(threads)]
+        [t.start() for t in ths]
+        [t.join() for t in ths]
+
+    run(min(1.0, seconds / 4), [0] * threads)  # warm-up (page in the obs buffer)
     counter = [0] * threads
-    stop_at = time.perf_counter() + 1.0  # warmup
-    ths = [threading.Thread(target=worker, args=(k, [0] * threads, stop_at)) for k in range(threads)]
-    [t.start() for t in ths]
-    [t.join() for t in ths]
     t0 = time.perf_counter()
-    stop_at = t0 + seconds
-    ths = [threading.Thread(target=worker, args=(k, counter, stop_at)) for k in range(threads)]
-    [t.start() for t in ths]
-    [t.join() for t in ths]
+    run(seconds, counter)
     dt = time.perf_counter() - t0
+    del o
+    return sum(counter) / dt, dt
+
+
+def cpu_baseline(cfg, seconds: float):
+    """BASELINE.md's two CPU legs on the GPU box's host: (i) one thread per usable core over
+    2 envs per thread, (ii) the single-thread 1 env x 128 agents C1 analogue."""
+    info = cpu_info()
+    threads = info["usable"]
+    rate, dt = _cpu_rate(cfg, 2 * threads, threads, seconds, seed=7)
+    c1, dt1 = _cpu_rate(cfg, 1, 1, max(2.0, seconds / 3), seed=7)
     return {
-        "value": round(sum(counter) / dt, 1),
+        "value": round(rate, 1),
         "unit": "agent-steps/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"CPU oracle (SPEC.md port, not nmmo 2.1) on {threads} host threads x {per} envs "
-                  f"= {n} envs x {cfg.PLAYER_N} agents, same systems/obs as the GPU workload, "
-                  f"{dt:.1f} s wall incl. the scripted policy",
+        "cpu_model": info["model"],
+        "affinity_cpus": info["affinity"],
+        "cgroup_quota_cpus": info["cgroup_quota_cpus"],
+        "c1_single_thread": round(c1, 1),
+        "sample": f"CPU oracle (SPEC.md port, not nmmo 2.1) on {threads} host threads (one per usable "
+                  f"core) x 2 envs x {cfg.PLAYER_N} agents, same systems/obs as the GPU workload, "
+                  f"{dt:.1f} s wall incl. the scripted policy; c1_single_thread = 1 thread x 1 env x "
+                  f"{cfg.PLAYER_N} agents ({dt1:.1f} s)",
     }
 
 
-def main():
-    args = parse()
-    # The JSON line is the only thing on stdout: native libraries (RCCL prints a version banner
-    # on stdout when a communicator is created) are sent to stderr by pointing fd 1 at fd 2.
-    json_out = os.fdopen(os.dup(1), "w")
-    sys.stdout.flush()
-    os.dup2(2, 1)
+# ------------------------------------------------------------------------------- GPU workload
+def measure(args, name, layout_name, envs, rank, world, dev, steps, warmup, dist=None):
+    """Build, stagger, warm up and time one workload on this rank; returns a result dict."""
+    import numpy as np
     import torch
-    import torch.distributed as dist
 
     from nmmo_amd import abi
     from nmmo_amd.config import Config
     from nmmo_amd.engine import NmmoEngine
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(0)
-    dev = torch.device("cuda", torch.cuda.current_device())
-
-    wl = WORKLOADS[args.config]
-    envs = args.envs or wl["envs"]
-    native = wl["obs"] and (args.obs or wl.get("layout", "flat")) == "native"
+    wl = WORKLOADS[name]
+    native = wl["obs"] and (layout_name or wl.get("layout", "flat")) == "native"
     obs_layout = (abi.OBS_NATIVE if native else abi.OBS_FLAT) if wl["obs"] else abi.OBS_NONE
     cfg = Config.preset(wl["preset"], early_stop_agent_num=8, obs_layout=obs_layout)
-    import numpy as np
-
     task = None
     gpath = os.path.join(ROOT, "tests", "golden", "task_embeddings.npz")
     if os.path.exists(gpath):
@@ -208,40 +272,35 @@ def main():
 
         eng.set_wrapper(wrapper_config(args.wrapper, **WRAPPER_KW.get(args.wrapper, {})))
     eng.reset()
-    # device counters the tick kernel adds into: [0] = sum(mask) (agent-steps), [1] = episodes
-    counters = torch.zeros(2, dtype=torch.int64, device=dev)
-    eng.set_counters(counters)
     pseed = args.seed * 1_000_003  # the policy's Philox counter already walks (tick, episode)
+    # staggered episode phases (module docstring): untimed, obs not gathered during the pre-roll
+    L = max(0, args.stagger)
+    ids = np.arange(envs) + rank * envs
+    for k in range(L):
+        eng.end_episodes(ids % L == k)
+        eng.scripted_actions(pseed)
+        eng.step(write_obs=False)
+    # device counters the tick kernel adds into: [0] = sum(mask) (agent-steps), [1] = episodes,
+    # [2] = event-log rows appended
+    counters = torch.zeros(3, dtype=torch.int64, device=dev)
+    eng.set_counters(counters)
 
     gather = wl.get("gather", False)
+    one, step_events = None, None
     if gather:
-        # learner-side receive buffers on rank 0 (one gather per tick over xGMI);
-        # the four small outputs travel packed in one buffer with the obs in another
-        small = torch.empty((envs, cfg.PLAYER_N, 8), dtype=torch.uint8, device=dev)
-        recv_obs = [torch.empty_like(eng.obs) for _ in range(world)] if rank == 0 else None
-        recv_small = [torch.empty_like(small) for _ in range(world)] if rank == 0 else None
-        if world == 1:  # a one-rank RCCL group: the gather degenerates to the root's own copy
-            dist.init_process_group("nccl", init_method="tcp://127.0.0.1:29533", rank=0, world_size=1,
-                                    device_id=dev)
+        one = _gather_stepper(eng, cfg, envs, rank, world, dev, pseed, dist)
+    else:
+        def one():
+            eng.scripted_actions(pseed)
+            eng.step()
 
-    def one():
-        eng.scripted_actions(pseed)
-        eng.step()
-        if gather:
-            small[..., 0:4] = eng.rew.view(torch.uint8).view(envs, cfg.PLAYER_N, 4)
-            small[..., 4] = eng.term
-            small[..., 5] = eng.trunc
-            small[..., 6] = eng.mask
-            dist.gather(eng.obs, recv_obs, dst=0)
-            dist.gather(small, recv_small, dst=0)
-
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         one()
     torch.cuda.synchronize(dev)
     graphs = []
     if not args.no_graph and not gather:  # the step is capture-safe: no sync / alloc inside nmmo_step
-        g_n = max(1, min(args.graph_steps, args.steps))
-        for n in sorted({g_n, args.steps % g_n} - {0}):
+        g_n = max(1, min(args.graph_steps, steps))
+        for n in sorted({g_n, steps % g_n} - {0}):
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 for _ in range(n):
@@ -250,8 +309,8 @@ def main():
         torch.cuda.synchronize(dev)
     plan = []
     if graphs:
-        big = graphs[-1] if graphs[-1][0] == max(n for n, _ in graphs) else graphs[0]
-        q, r = divmod(args.steps, big[0])
+        big = max(graphs, key=lambda x: x[0])
+        q, r = divmod(steps, big[0])
         plan = [big[1]] * q + [g for n, g in graphs if n == r and r]
     counters.zero_()
     if world > 1:
@@ -262,25 +321,30 @@ def main():
         for g in plan:
             g.replay()
     else:
-        for _ in range(args.steps):
+        for _ in range(steps):
             one()
+    if gather:
+        one.drain()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    alive = counters[0].clone()
+    alive = float(counters[0].item())
+    episodes = int(counters[1].item())
+    events_per_env_tick = float(counters[2].item()) / (envs * steps) if cfg.event_cap > 0 else None
     # per-kernel durations: HIP events on the launch stream around each kernel of nmmo_step,
     # over an equal number of eager steps right after the timed region (same state stream)
     eng.set_timing(True)
-    for _ in range(min(args.steps, 8192)):
-        one()
+    for _ in range(min(steps, 8192)):
+        eng.scripted_actions(pseed)
+        eng.step()
     tick_ms, obs_ms, n_timed, wrap_ms = eng.read_timing()
     eng.set_timing(False)
     # The roofline's tick duration without per-kernel event overhead (which inflates a ~15 us
     # launch by ~20%): the timed step (policy + nmmo_step, graph-replayed) minus a hipGraph of
     # `batch` policy-only launches timed with HIP events on the same stream. Timing nmmo_step
-    # alone would need stale actions, which change the tick's work (attack rounds) at C3/C4.
-    batch = 20
+    # alone would need stale actions, which change the tick's work (attack rounds).
+    batch, reps = 20, 10
     pol_graph = torch.cuda.CUDAGraph()
     with torch.cuda.graph(pol_graph):
         for _ in range(batch):
@@ -288,14 +352,12 @@ def main():
     b0, b1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     pol_graph.replay()
     b0.record()
-    reps = 10
     for _ in range(reps):
         pol_graph.replay()
     b1.record()
     torch.cuda.synchronize(dev)
     policy_avg_ms = b0.elapsed_time(b1) / (reps * batch)
     # practical HBM write ceiling on THIS box: the vendor fill kernel over the same obs buffer
-    # (the same byte count the obs kernel writes per launch), HIP events on the current stream
     fill_gbs = None
     if wl["obs"]:
         s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -307,100 +369,233 @@ def main():
         torch.cuda.synchronize(dev)
         fill_gbs = eng.obs.numel() * eng.obs.element_size() / (s0.elapsed_time(s1) / 10 * 1e-3) / 1e9
 
-    vals = torch.tensor([elapsed, float(alive.item()), float(envs * cfg.PLAYER_N * args.steps)],
-                        dtype=torch.float64, device=dev)
+    S, P = eng.S, cfg.PLAYER_N
+    tick_avg_ms = tick_ms / max(n_timed, 1)
+    obs_avg_ms = obs_ms / max(n_timed, 1)
+    tick_b = tick_bytes_per_env(S, P, "Item" in cfg.systems, events_per_env_tick or 0.0) * envs
+    obs_b = obs_bytes_per_env(S, P, eng.obs_elems, native) * envs if wl["obs"] else 0
+    if wl["obs"] and obs_avg_ms > tick_avg_ms:
+        kern, byts, ms = "obs_kernel", obs_b, obs_avg_ms
+        timing = "HIP events around each obs_kernel launch on the launch stream"
+    else:
+        kern, byts, ms = "tick_kernel", tick_b, tick_avg_ms
+        timing = "HIP events around each tick_kernel launch on the launch stream"
+        if not wl["obs"] and args.wrapper == "none" and plan:
+            ms = elapsed * 1e3 / steps - policy_avg_ms  # nmmo_step = the tick kernel alone
+            timing = (f"timed step (hipGraph: policy + tick) minus a {batch}-launch policy-only "
+                      f"hipGraph, HIP events on the launch stream")
+    achieved = byts / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
+    prof_name = name + ("-native" if native and name != "C5" else "")
+    traffic, traffic_src = pmc_traffic(prof_name, kern, envs)
+    res = {
+        "name": prof_name, "envs": envs, "cfg": cfg, "native": native, "S": S, "P": P,
+        "elapsed": elapsed, "alive": alive, "slots": float(envs * P * steps), "episodes": episodes,
+        "events_per_env_tick": events_per_env_tick, "gather": gather,
+        "launch": "eager" if (args.no_graph or gather) else f"hipGraph x{min(args.graph_steps, steps)} ticks",
+        "kernel_ms": {"policy": round(policy_avg_ms, 5), "tick": round(tick_avg_ms, 5),
+                      "obs": round(obs_avg_ms, 5) if wl["obs"] else None,
+                      "wrapper": round(wrap_ms / max(n_timed, 1), 5) if args.wrapper != "none" else None},
+        "roofline": {
+            "kernel": kern, "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+            "traffic_source": traffic_src, "bytes_per_launch": byts, "avg_launch_ms": round(ms, 5),
+            "timing": timing,
+            "write_ceiling_gbs": None if fill_gbs is None else round(fill_gbs, 1),
+            "frac_of_write_ceiling": None if not fill_gbs or kern != "obs_kernel" else round(achieved / fill_gbs, 4),
+        },
+        "gather_bytes": getattr(one, "bytes_per_step", None),
+    }
+    if gather:
+        one.close()
+    eng.close()
+    del eng
+    torch.cuda.empty_cache()
+    return res
+
+
+def _gather_stepper(eng, cfg, envs, rank, world, dev, pseed, dist):
+    """C5's step: tick + obs into one of two obs buffers, then the learner gather of that
+    buffer on a side stream (point-to-point sends into rank 0 over xGMI, overlapped with the
+    next tick); the root uses its own shard in place (no self-copy). The obs and the packed
+    reward/term/trunc/mask of step t travel while step t+1 computes into the other buffer."""
+    import torch
+
+    bufs = [eng.obs, torch.empty_like(eng.obs)]
+    smalls = [torch.empty((envs, cfg.PLAYER_N, 8), dtype=torch.uint8, device=dev) for _ in range(2)]
+    comm = torch.cuda.Stream(device=dev)
+    done_ev = [None, None]  # event on the compute stream after the buffer's sends finished
+    recv = None
+    if rank == 0 and world > 1:
+        recv = [[torch.empty_like(bufs[0]), torch.empty_like(smalls[0])] for _ in range(world - 1)]
+
+    class Stepper:
+        t = 0
+        bytes_per_step = (bufs[0].numel() * bufs[0].element_size() + smalls[0].numel()) * max(world - 1, 0)
+
+        def __call__(self):
+            i = self.t % 2
+            cur = torch.cuda.current_stream(dev)
+            if done_ev[i] is not None:
+                cur.wait_event(done_ev[i])  # the sends of step t-2 have read this buffer
+            eng.obs = bufs[i]
+            eng.scripted_actions(pseed)
+            eng.step()
+            sm = smalls[i]
+            sm[..., 0:4] = eng.rew.view(torch.uint8).view(envs, cfg.PLAYER_N, 4)
+            sm[..., 4] = eng.term
+            sm[..., 5] = eng.trunc
+            sm[..., 6] = eng.mask
+            if world > 1:
+                ready = torch.cuda.Event()
+                ready.record(cur)
+                with torch.cuda.stream(comm):
+                    comm.wait_event(ready)
+                    if rank == 0:
+                        ops = [dist.P2POp(dist.irecv, recv[r - 1][0], r) for r in range(1, world)]
+                        ops += [dist.P2POp(dist.irecv, recv[r - 1][1], r) for r in range(1, world)]
+                    else:
+                        ops = [dist.P2POp(dist.isend, bufs[i], 0), dist.P2POp(dist.isend, sm, 0)]
+                    for w in dist.batch_isend_irecv(ops):
+                        w.wait()
+                    ev = torch.cuda.Event()
+                    ev.record(comm)
+                done_ev[i] = ev
+            self.t += 1
+
+        def drain(self):
+            torch.cuda.current_stream(dev).wait_stream(comm)
+
+        def close(self):
+            torch.cuda.synchronize(dev)
+            eng.obs = bufs[0]
+
+    return Stepper()
+
+
+def result_line(res, args, world, steps, alive_total, slots_total, elapsed, warmup):
+    cfg = res["cfg"]
+    wl_desc = next(w["desc"] for k, w in WORKLOADS.items() if res["name"].split("-")[0] == k)
+    return {
+        "value": round(alive_total / elapsed, 1),
+        "ms_per_step": round(elapsed * 1e3 / steps, 4),
+        "config": {
+            "workload": wl_desc,
+            "envs_per_gpu": res["envs"],
+            "agents_per_env": res["P"],
+            "npcs_per_env": res["S"] - res["P"],
+            "systems": list(cfg.systems),
+            "obs": ("native nmmo dtypes (SPEC §8b, 9,552 B/agent + 32 KB Market/env)" if res["native"] else
+                    "pufferlib-flat fp32 (23,987/agent)") if WORKLOADS[res["name"].split("-")[0]]["obs"] else "none",
+            "early_stop_agent_num": 8,
+            "stagger_ticks": args.stagger,
+            "parallelism": f"env-shard x{world}",
+        },
+        "slot_steps_per_sec": round(slots_total / elapsed, 1),
+        "alive_fraction": round(alive_total / slots_total, 4),
+        "episodes_ended": res["episodes"],
+        "events_per_env_tick": None if res["events_per_env_tick"] is None else round(res["events_per_env_tick"], 3),
+        "kernel_ms": res["kernel_ms"],
+        "launch": res["launch"],
+        "roofline": res["roofline"],
+    }
+
+
+def main():
+    args = parse()
+    world_env = os.environ.get("WORLD_SIZE")
+    if args.dry_launch and world_env is not None:
+        print(json.dumps({"rank": int(os.environ["RANK"]), "world_size": int(world_env),
+                          "local_rank": int(os.environ.get("LOCAL_RANK", "0"))}), flush=True)
+        return 0
+    if world_env is None and args.gpus > 1:
+        return launch_ranks(args)
+    world = int(world_env or "1")
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        return 2
+    if args.dry_launch:
+        print(json.dumps({"rank": 0, "world_size": 1, "local_rank": 0}), flush=True)
+        return 0
+    # The JSON line is the only thing on stdout: native libraries (RCCL prints a version banner
+    # on stdout when a communicator is created) are sent to stderr by pointing fd 1 at fd 2.
+    json_out = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
+    import torch
+    import torch.distributed as dist
+
+    from nmmo_amd import _native
+
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local if world > 1 else 0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    wl = WORKLOADS[args.config]
+    envs = args.envs or wl["envs"]
+    res = measure(args, args.config, args.obs, envs, rank, world, dev, args.steps, args.warmup, dist)
+    vals = torch.tensor([res["elapsed"], res["alive"], res["slots"]], dtype=torch.float64, device=dev)
     if world > 1:
         t_max = vals[0:1].clone()
         dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
         sums = vals[1:3].clone()
         dist.all_reduce(sums, op=dist.ReduceOp.SUM)
-        elapsed = float(t_max.item())
-        alive_total, slots_total = float(sums[0].item()), float(sums[1].item())
+        elapsed, alive_total, slots_total = float(t_max.item()), float(sums[0].item()), float(sums[1].item())
     else:
-        alive_total, slots_total = float(vals[1].item()), float(vals[2].item())
+        elapsed, alive_total, slots_total = res["elapsed"], res["alive"], res["slots"]
+
+    extras = {}
+    if world == 1 and not args.no_extras and args.config == "C4" and not args.envs:
+        ex_steps, ex_warm = max(args.steps, 100), max(args.warmup, 20)
+        for name, lay in EXTRAS:
+            if name == args.config and (lay or "flat") == (args.obs or "flat"):
+                continue
+            r = measure(args, name, lay, WORKLOADS[name]["envs"], 0, 1, dev, ex_steps, ex_warm)
+            line = result_line(r, args, 1, ex_steps, r["alive"], r["slots"], r["elapsed"], ex_warm)
+            line["steps"], line["warmup"] = ex_steps, ex_warm
+            extras[r["name"]] = line
 
     if rank == 0:
-        S, P = eng.S, cfg.PLAYER_N
-        tick_avg_ms = tick_ms / max(n_timed, 1)
-        obs_avg_ms = obs_ms / max(n_timed, 1)
-        tick_b = tick_bytes_per_env(S, P, "Item" in cfg.systems) * envs
-        obs_b = obs_bytes_per_env(S, P, eng.obs_elems, native) * envs if wl["obs"] else 0
-        if wl["obs"] and obs_avg_ms > tick_avg_ms:
-            kern, byts, ms = "obs_kernel", obs_b, obs_avg_ms
-            timing = "HIP events around each obs_kernel launch on the launch stream"
-        else:
-            kern, byts, ms = "tick_kernel", tick_b, tick_avg_ms
-            timing = "HIP events around each tick_kernel launch on the launch stream"
-            if not wl["obs"] and args.wrapper == "none" and plan and not gather:
-                # nmmo_step = the tick kernel alone: timed step minus the policy launch
-                ms = elapsed * 1e3 / args.steps - policy_avg_ms
-                timing = (f"timed step (hipGraph: policy + tick) minus a {batch}-launch policy-only "
-                          f"hipGraph, HIP events on the launch stream")
-        achieved = byts / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
-        traffic, traffic_src = pmc_traffic(args.config + ("-native" if native and args.config != "C5" else ""),
-                                           kern, envs)
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            # the CPU leg always builds the flat pufferlib row when the workload has obs (the
+            from nmmo_amd import abi
+            from nmmo_amd.config import Config
+
+            # the CPU leg builds the flat pufferlib row when the workload has obs (the
             # reference's CPU path; the oracle has no native writer)
             cpu = cpu_baseline(Config.preset(wl["preset"], early_stop_agent_num=8,
                                              obs_layout=abi.OBS_FLAT if wl["obs"] else abi.OBS_NONE),
                                args.cpu_seconds)
+        body = result_line(res, args, world, args.steps, alive_total, slots_total, elapsed, args.warmup)
         line = {
             "metric": METRIC,
-            "value": round(alive_total / elapsed, 1),
+            "value": body.pop("value"),
             "unit": "agent-steps/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
+            "ms_per_step": body.pop("ms_per_step"),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "int16",
-            "data": "synthetic: generated map bank (SPEC §3), masked-uniform scripted actions (SPEC §10)",
-            "config": {
-                "workload": wl["desc"],
-                "envs_per_gpu": envs,
-                "agents_per_env": P,
-                "npcs_per_env": S - P,
-                "systems": list(cfg.systems),
-                "obs": ("native nmmo dtypes (SPEC §8b, 9,552 B/agent + 32 KB Market/env)" if native else
-                        "pufferlib-flat fp32 (23,987/agent)") if wl["obs"] else "none",
-                "early_stop_agent_num": 8,
-                "parallelism": f"env-shard x{world}",
-            },
-            "slot_steps_per_sec": round(slots_total / elapsed, 1),
-            "alive_fraction": round(alive_total / slots_total, 4),
-            "kernel_ms": {"policy": round(policy_avg_ms, 5), "tick": round(tick_avg_ms, 5),
-                          "obs": round(obs_avg_ms, 5) if wl["obs"] else None,
-                          "wrapper": round(wrap_ms / max(n_timed, 1), 5) if args.wrapper != "none" else None},
-            "wrapper": None if args.wrapper == "none" else args.wrapper,
-            "launch": "eager" if (args.no_graph or gather) else f"hipGraph x{min(args.graph_steps, args.steps)} ticks",
-            "gather": f"RCCL gather of {eng.obs.numel() * eng.obs.element_size() + envs * cfg.PLAYER_N * 8} "
-                      f"B/rank/step to rank 0" if gather else None,
-            "roofline": {
-                "kernel": kern,
-                "bound": "hbm",
-                "achieved": round(achieved, 2),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 5),
-                "traffic": traffic,
-                "traffic_source": traffic_src,
-                "bytes_per_launch": byts,
-                "avg_launch_ms": round(ms, 5),
-                "timing": timing,
-                "write_ceiling_gbs": None if fill_gbs is None else round(fill_gbs, 1),
-                "frac_of_write_ceiling": None if not fill_gbs or kern != "obs_kernel" else round(achieved / fill_gbs, 4),
-            },
-            "cpu_baseline": cpu,
+            "data": "synthetic: generated map bank (SPEC §3), masked-uniform scripted actions "
+                    f"(SPEC §10), episode phases staggered over {args.stagger} pre-roll ticks",
         }
+        line.update(body)
+        line["wrapper"] = None if args.wrapper == "none" else args.wrapper
+        line["gather"] = (f"RCCL point-to-point sends of {res['gather_bytes']} B/step into rank 0, "
+                          "double-buffered on a side stream" if res["gather"] else None)
+        line["cpu_baseline"] = cpu
+        line["extra_configs"] = extras or None
+        line["build"] = _native.build_info()
         print(json.dumps(line), file=json_out, flush=True)
-    eng.close()
-    if world > 1 or gather:
+    if world > 1:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

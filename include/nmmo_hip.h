@@ -42,7 +42,7 @@ extern "C" {
 #endif
 
 #define NMMO_API __attribute__((visibility("default")))
-#define NMMO_ABI_VERSION 5
+#define NMMO_ABI_VERSION 6
 
 /* ---- error codes ---- */
 #define NMMO_OK 0
@@ -271,6 +271,14 @@ NMMO_API void nmmo_destroy(NmmoHandle* h);
 /* Reset every env (env_seeds: host uint64[n_envs] or NULL = derive from the create seed). */
 NMMO_API int nmmo_reset(NmmoHandle* h, const uint64_t* env_seeds, void* obs, uint8_t* mask, void* stream);
 
+/* Ends the current episode of every env whose host_env_mask[e] != 0 (host u8 [n_envs]): the
+ * env's next nmmo_step resets it instead of stepping (the auto-reset path, rewards/flags 0),
+ * exactly as if its previous step had ended the episode; the ended episode's agents are not
+ * reported as truncated. This is the per-env `env.reset()` the reference's async worker pool
+ * issues independently for each env (pufferlib vectorization, clean_pufferl.py:106-114,175);
+ * bench.py uses it to stagger episode phases across envs. Synchronous. */
+NMMO_API int nmmo_end_episodes(NmmoHandle* h, const uint8_t* host_env_mask);
+
 /* One tick of every env. actions: device int32 [n_envs][player_n][12]. Envs whose previous
  * step ended the episode are reset instead (pufferlib auto-reset), with rewards/flags 0.
  * obs: device float32 [n_envs][player_n][obs_elems] (NMMO_OBS_FLAT), the native layout
@@ -329,8 +337,9 @@ NMMO_API int nmmo_set_map_bank(NmmoHandle* h, const uint8_t* host_buf, size_t nb
  * buffer. */
 NMMO_API int nmmo_set_timing(NmmoHandle* h, int32_t enable);
 /* Device-side rollout counters (the trainer's agent_SPS numerator, clean_pufferl.py:306):
- * when set, every nmmo_step / nmmo_reset adds into dev_counters (device u64 [2]):
- * [0] += sum of the mask it writes (agent-steps), [1] += envs whose episode ended.
+ * when set, every nmmo_step / nmmo_reset adds into dev_counters (device u64 [3]):
+ * [0] += sum of the mask it writes (agent-steps), [1] += envs whose episode ended,
+ * [2] += event-log rows appended by stepped (not reset) envs.
  * NULL disables. The caller owns and zeroes the buffer; capture-safe. */
 NMMO_API int nmmo_set_counters(NmmoHandle* h, uint64_t* dev_counters);
 NMMO_API int nmmo_read_timing(NmmoHandle* h, double* ms /* [3] */, int32_t* n);
@@ -405,6 +414,9 @@ NMMO_API int nmmo_gather_rows(const void* src, int64_t row_bytes, const int32_t*
 NMMO_API int32_t nmmo_n_envs(const NmmoHandle* h);
 NMMO_API const char* nmmo_last_error(void);
 NMMO_API int32_t nmmo_abi_version(void);
+/* "src=<sha256 of the HIP sources + headers this library was compiled from> arch=gfx950 ...";
+ * nmmo_amd/_native.py refuses a library whose source hash differs from the tree it ships in. */
+NMMO_API const char* nmmo_build_info(void);
 
 #ifdef __cplusplus
 }

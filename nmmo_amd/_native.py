@@ -12,6 +12,7 @@ import os
 
 from . import abi
 
+_PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get(
     "NMMO_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libnmmo_hip.so"))
 _lib = None
@@ -22,7 +23,7 @@ SYMBOLS = [
     "nmmo_get_map_bank", "nmmo_set_map_bank", "nmmo_set_timing", "nmmo_read_timing", "nmmo_set_counters", "nmmo_get_events", "nmmo_set_tasks",
     "nmmo_set_wrapper", "nmmo_get_wrapper_state", "nmmo_expand_obs", "nmmo_exp_scratch_ints",
     "nmmo_exp_store", "nmmo_exp_sort", "nmmo_exp_gae", "nmmo_gather_rows", "nmmo_n_envs",
-    "nmmo_last_error", "nmmo_abi_version",
+    "nmmo_last_error", "nmmo_abi_version", "nmmo_end_episodes", "nmmo_build_info",
 ]
 
 
@@ -74,10 +75,27 @@ def lib():
     L.nmmo_n_envs.argtypes = [vp]
     L.nmmo_last_error.restype = ctypes.c_char_p
     L.nmmo_abi_version.restype = i32
+    L.nmmo_end_episodes.argtypes = [vp, vp]
+    L.nmmo_build_info.restype = ctypes.c_char_p
     if L.nmmo_abi_version() != abi.ABI_VERSION:
         raise NativeError(f"ABI mismatch: lib {L.nmmo_abi_version()} != python {abi.ABI_VERSION}")
+    info = build_info(L)
+    if os.environ.get("NMMO_ALLOW_STALE") != "1" and os.path.isdir(os.path.join(_PKG, "csrc")):
+        from .build import source_hash
+
+        want = source_hash()
+        if info.get("src") != want:
+            raise NativeError(
+                f"{LIB_PATH} was built from other sources (src={info.get('src')}, tree={want}): "
+                "rebuild it (`python -m nmmo_amd.build --force`)")
     _lib = L
     return L
+
+
+def build_info(L=None) -> dict:
+    """nmmo_build_info() as a dict (src = source hash the library was compiled from)."""
+    L = lib() if L is None else L
+    return dict(kv.split("=", 1) for kv in L.nmmo_build_info().decode().split() if "=" in kv)
 
 
 def check(rc: int, what: str):

@@ -3,6 +3,7 @@ snapshot to the GPU box)."""
 
 from __future__ import annotations
 
+import hashlib
 import os
 import subprocess
 import sys
@@ -24,13 +25,24 @@ def _hipcc() -> str:
     raise RuntimeError("hipcc not found")
 
 
+def source_hash() -> str:
+    """sha256 (first 16 hex) over the HIP sources and headers the library is compiled from; the
+    library embeds it (nmmo_build_info) and _native.lib() refuses a library built from other
+    sources, so a run always reflects the tree it ships with."""
+    h = hashlib.sha256()
+    for f in [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [
+            os.path.join(HERE, "..", "include", "nmmo_hip.h")]:
+        with open(f, "rb") as fh:
+            h.update(os.path.basename(f).encode() + b"\0" + fh.read())
+    return h.hexdigest()[:16]
+
+
 def stale() -> bool:
+    """True unless the library exists and embeds the current source hash."""
     if not os.path.exists(LIB_PATH):
         return True
-    t = os.path.getmtime(LIB_PATH)
-    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS]
-    deps.append(os.path.join(HERE, "..", "include", "nmmo_hip.h"))
-    return any(os.path.getmtime(d) > t for d in deps)
+    with open(LIB_PATH, "rb") as fh:
+        return ("src=" + source_hash()).encode() not in fh.read()
 
 
 def build(force: bool = False, verbose: bool = False, stamps: bool = False) -> str:
@@ -47,6 +59,7 @@ def build(force: bool = False, verbose: bool = False, stamps: bool = False) -> s
         # no FMA contraction: hipcc contracts even __dadd_rn(__dmul_rn(..)) pairs, and the float /
         # double reward, wrapper and advantage arithmetic must round op by op like the oracle
         "-ffp-contract=off", *(["-DNMMO_STAMPS"] if stamps else []),
+        f'-DNMMO_SRC_HASH="{source_hash()}"',
         *[os.path.join(CSRC, f) for f in SOURCES], "-o", tmp,
     ]
     if verbose:

@@ -91,6 +91,16 @@ static float half_to_float(uint16_t h) {
 extern "C" {
 
 int32_t nmmo_abi_version(void) { return NMMO_ABI_VERSION; }
+#ifndef NMMO_SRC_HASH
+#define NMMO_SRC_HASH "unknown"
+#endif
+const char* nmmo_build_info(void) {
+  return "src=" NMMO_SRC_HASH " arch=gfx950 fp_contract=off"
+#ifdef NMMO_STAMPS
+         " stamps=1"
+#endif
+      ;
+}
 const char* nmmo_last_error(void) { return g_err.c_str(); }
 
 void nmmo_default_config(NmmoConfig* c) {
@@ -289,6 +299,24 @@ int nmmo_reset(NmmoHandle* h, const uint64_t* env_seeds, void* obs, uint8_t* mas
                       mask, 1, s));
   if (h->wrap_on) HIP_TRY(launch_wrap(wrap_params(h, nullptr, nullptr, nullptr, nullptr, nullptr), 0, s));
   if (obs && h->cfg.obs_layout != NMMO_OBS_NONE) HIP_TRY(launch_obs(obs_params(h, obs), s));
+  return NMMO_OK;
+}
+
+__global__ void end_episodes_kernel(int32_t* env, const uint8_t* m, int n) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < n && m[e]) env[(size_t)e * NMMO_NE + E_DONE] = 1;
+}
+
+int nmmo_end_episodes(NmmoHandle* h, const uint8_t* host_env_mask) {
+  if (!h || !host_env_mask) return fail(NMMO_E_INVALID, "null argument");
+  const int n = h->st.n_envs;
+  HIP_TRY(hipSetDevice(h->device));
+  HIP_TRY(hipDeviceSynchronize());
+  // d_seeds (n x 8 B) is reset-time scratch: n mask bytes fit in it
+  HIP_TRY(hipMemcpy(h->d_seeds, host_env_mask, (size_t)n, hipMemcpyHostToDevice));
+  end_episodes_kernel<<<(n + 255) / 256, 256>>>(h->d_env, reinterpret_cast<const uint8_t*>(h->d_seeds), n);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipDeviceSynchronize());
   return NMMO_OK;
 }
 

@@ -23,7 +23,7 @@ struct DevState {
   int n_tasks, tev;      // tev: some task term counts events
   int n_envs, P, N, S;   // N = NPC capacity (0 when the NPC system is off), S = P + N
   uint64_t seed;         // create seed (first-episode seeds)
-  unsigned long long* counters;  // optional device u64 [2]: agent-steps, finished episodes
+  unsigned long long* counters;  // optional device u64 [3]: agent-steps, finished episodes, event rows
   NmmoConfig cfg;
 };
 

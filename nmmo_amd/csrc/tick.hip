@@ -1734,6 +1734,7 @@ __global__ void tick_kernel(DevState st, const int32_t* __restrict__ actions,
   NMMO_STAMP(20);
   const size_t o = (size_t)e * c.P;
   const bool reset_path = mode == 1 || c.E[E_DONE];
+  const int ev_start = c.E[E_EVENT_COUNT];  // event rows this tick appends (counters[2])
   if (reset_path) {
     const int env_global = (int)(st.cfg.env_index_base + (uint64_t)e);
     uint64_t seed;
@@ -1770,6 +1771,7 @@ __global__ void tick_kernel(DevState st, const int32_t* __restrict__ actions,
     if (threadIdx.x == 0) {
       atomicAdd(&st.counters[0], (unsigned long long)n);
       if (!reset && c.E[E_DONE]) atomicAdd(&st.counters[1], 1ull);
+      if (!reset && c.evcap) atomicAdd(&st.counters[2], (unsigned long long)(c.E[E_EVENT_COUNT] - ev_start));
     }
   }
   NMMO_STAMP(10);

@@ -98,15 +98,25 @@ class NmmoEngine:
         self.trunc.zero_()
         return self.obs, self.mask
 
-    def step(self, actions=None):
+    def end_episodes(self, env_mask):
+        """End the current episode of the envs where env_mask (host bool/u8 [n_envs]) is set: their
+        next step resets them (nmmo_end_episodes; per-env reset of an async pool)."""
+        m = np.ascontiguousarray(np.asarray(env_mask, dtype=np.uint8))
+        assert m.shape == (self.n_envs,)
+        with torch.cuda.device(self.device):
+            check(lib().nmmo_end_episodes(self.h, m.ctypes.data_as(ctypes.c_void_p)), "nmmo_end_episodes")
+
+    def step(self, actions=None, write_obs: bool = True):
         """One tick of every env; `actions` int32 [n_envs, P, 12] on the device (default: the
-        engine's own action buffer). Outputs are the engine's tensors (overwritten in place)."""
+        engine's own action buffer). Outputs are the engine's tensors (overwritten in place);
+        write_obs=False skips the obs gather for this tick (obs keeps its previous contents)."""
         a = self.actions if actions is None else actions
         if a.dtype != torch.int32 or not a.is_contiguous() or a.device != self.device:
             a = a.to(device=self.device, dtype=torch.int32).contiguous()
         assert tuple(a.shape) == (self.n_envs, self.P, abi.N_ACTION_HEADS)
         with torch.cuda.device(self.device):
-            check(lib().nmmo_step(self.h, self._ptr(a), self._ptr(self.obs), self._ptr(self.rew),
+            check(lib().nmmo_step(self.h, self._ptr(a), self._ptr(self.obs if write_obs else None),
+                                  self._ptr(self.rew),
                                   self._ptr(self.term), self._ptr(self.trunc), self._ptr(self.mask),
                                   self._stream()), "nmmo_step")
         return self.obs, self.rew, self.term, self.trunc, self.mask
@@ -160,8 +170,11 @@ class NmmoEngine:
         check(lib().nmmo_set_timing(self.h, 1 if enable else 0), "nmmo_set_timing")
 
     def set_counters(self, counters):
-        """Device u64 [2] (torch int64 tensor on this device) the kernels add into: agent-steps
-        (sum of mask) and finished episodes; None disables."""
+        """Device u64 [3] (torch int64 tensor on this device) the kernels add into: agent-steps
+        (sum of mask), finished episodes and event-log rows appended; None disables."""
+        if counters is not None and (counters.numel() < 3 or counters.dtype != torch.int64
+                                     or counters.device != self.device):
+            raise ValueError("counters must be an int64 tensor of >= 3 elements on the engine's device")
         ptr = None if counters is None else ctypes.c_void_p(counters.data_ptr())
         self._counters = counters
         check(lib().nmmo_set_counters(self.h, ptr), "nmmo_set_counters")

@@ -1366,6 +1366,21 @@ EXPORT int oracle_reset(void* h, const uint64_t* env_seeds, float* obs, uint8_t*
   return 0;
 }
 
+/* as nmmo_end_episodes: the next step of each masked env resets it (auto-reset path) */
+EXPORT int oracle_end_episodes(void* h, const uint8_t* env_mask) {
+  Oracle* o = (Oracle*)h;
+  for (int e = 0; e < o->n_envs; e++)
+    if (env_mask[e]) ENV(o, e)[E_DONE] = 1;
+  return 0;
+}
+/* one env's flat obs (P x obs_elems floats) from its current state, as the step/reset writes it */
+EXPORT int oracle_write_obs(void* h, int env, float* obs_env) {
+  Oracle* o = (Oracle*)h;
+  if (env < 0 || env >= o->n_envs || !obs_env) return NMMO_E_INVALID;
+  write_obs(o, env, obs_env);
+  return 0;
+}
+
 /* Envs are independent; `env_lo..env_hi` lets the CPU baseline run one thread per env range. */
 EXPORT int oracle_step_range(void* h, int env_lo, int env_hi, const int32_t* actions, float* obs,
                              float* rew, uint8_t* term, uint8_t* trunc, uint8_t* mask) {

@@ -44,6 +44,8 @@ def lib():
         L.oracle_set_state.argtypes = [vp, vp, sz]
         L.oracle_get_map_bank.argtypes = [vp, vp, sz]
         L.oracle_set_map_bank.argtypes = [vp, vp, sz]
+        L.oracle_end_episodes.argtypes = [vp, vp]
+        L.oracle_write_obs.argtypes = [vp, i32, vp]
         L.oracle_get_events.argtypes = [vp, i32, vp, i32, ctypes.POINTER(i32)]
         L.oracle_set_tasks.argtypes = [vp, vp, i32, vp, vp]
         L.oracle_obs_elems.argtypes = [i32]
@@ -95,6 +97,18 @@ class OracleEnvs:
         assert actions.shape == (self.n_envs, self.P, abi.N_ACTION_HEADS)
         lib().oracle_step(self.h, _p(actions), _p(self.obs), _p(self.rew), _p(self.term),
                           _p(self.trunc), _p(self.mask))
+
+    def end_episodes(self, env_mask):
+        m = np.ascontiguousarray(env_mask, dtype=np.uint8)
+        assert m.shape == (self.n_envs,)
+        lib().oracle_end_episodes(self.h, _p(m))
+
+    def flat_obs(self, env: int) -> np.ndarray:
+        """Flat obs [P, obs_elems] of one env from its current state (any obs layout config)."""
+        out = np.zeros((self.P, self.obs_elems), np.float32)
+        rc = lib().oracle_write_obs(self.h, env, _p(out))
+        assert rc == 0, rc
+        return out
 
     def step_range(self, lo, hi, actions):
         lib().oracle_step_range(self.h, lo, hi, _p(actions), _p(self.obs), _p(self.rew),
