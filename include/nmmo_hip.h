@@ -377,6 +377,9 @@ typedef struct NmmoExperience {
   int32_t* seq;         /* [capacity] rank of the row among its env_id's rows */
   int32_t* slot_count;  /* [n_slots] rows stored per env_id; zero it with ptr to start a batch */
   int32_t* ptr;         /* [1] rows stored (clean_pufferl.py:200 ptr) */
+  int32_t* status;      /* [1] or NULL: bit 0 set when a store met a selected row whose env_id is
+                           outside [0, n_slots) (the row is dropped, nothing out of range is
+                           written). Env ids must be distinct within one store (precondition). */
 } NmmoExperience;
 
 typedef struct NmmoStoreInput {

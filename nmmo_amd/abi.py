@@ -231,7 +231,7 @@ def wrap_state_dtype():
 class NmmoExperience(ctypes.Structure):
     _fields_ = [("capacity", ctypes.c_int32), ("obs_elems", ctypes.c_int32), ("n_slots", ctypes.c_int32)] + [
         (n, ctypes.c_void_p) for n in ("obs", "actions", "logprobs", "rewards", "dones", "truncateds", "values",
-                                       "env_id", "step", "seq", "slot_count", "ptr")]
+                                       "env_id", "step", "seq", "slot_count", "ptr", "status")]
 
 
 class NmmoStoreInput(ctypes.Structure):

@@ -17,11 +17,22 @@ namespace nmmo {
 
 constexpr int kStoreBlock = 512;  // rows per workgroup in the count/place passes (8 waves)
 
-// Pass 1: alive rows per block of kStoreBlock rows.
-__global__ void __launch_bounds__(kStoreBlock) store_count_kernel(const uint8_t* mask, int n, int* blk_cnt) {
+// A row is stored iff the learner mask selects it and its env id is a valid slot; a selected
+// row with an env id outside [0, n_slots) is dropped (never indexes slot_count / offset) and
+// raises bit 0 of x.status.
+__device__ __forceinline__ bool row_selected(const NmmoExperience& x, const NmmoStoreInput& in, int r) {
+  if (r >= in.n_rows || in.mask[r] == 0) return false;
+  const int eid = in.env_id ? in.env_id[r] : in.env_id_base + r;
+  if (eid >= 0 && eid < x.n_slots) return true;
+  if (x.status) atomicOr(x.status, 1);
+  return false;
+}
+
+// Pass 1: selected rows per block of kStoreBlock rows.
+__global__ void __launch_bounds__(kStoreBlock) store_count_kernel(NmmoExperience x, NmmoStoreInput in, int* blk_cnt) {
   __shared__ int wt[8];
   const int r = blockIdx.x * kStoreBlock + threadIdx.x;
-  const uint64_t b = __ballot(r < n && mask[r] != 0);
+  const uint64_t b = __ballot(row_selected(x, in, r));
   if (lane_id() == 0) wt[wave_id()] = __popcll(b);
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -42,7 +53,7 @@ __global__ void __launch_bounds__(kStoreBlock) store_place_kernel(NmmoExperience
   for (int i = tid; i < b; i += kStoreBlock) part += blk_cnt[i];
   int base_total;
   (void)block_prefix_sum(part, wt[0], &base_total);
-  const bool alive = r < in.n_rows && in.mask[r] != 0;
+  const bool alive = row_selected(x, in, r);
   int blk_total;
   const int rank = base_total + block_prefix_count(alive, wt[1], &blk_total);
   const int ptr0 = *x.ptr;
@@ -61,9 +72,10 @@ __global__ void __launch_bounds__(kStoreBlock) store_place_kernel(NmmoExperience
     for (int h = 0; h < kHeads; h++) o[h] = a[h];
     x.env_id[s] = eid;
     x.step[s] = in.step;
-    // rank of this row among its env_id's rows: env ids are distinct within one store, so the
-    // slot counter has exactly one writer here, and stores arrive in step order
-    x.seq[s] = x.slot_count[eid]++;
+    // rank of this row among its env_id's rows (stores arrive in step order). Env ids are
+    // distinct within one store (ABI precondition), so the counter has one writer; the atomic
+    // keeps a violating caller's rows at distinct sorted positions instead of corrupting them.
+    x.seq[s] = atomicAdd(&x.slot_count[eid], 1);
   }
   if (b == gridDim.x - 1 && tid == 0) *total = base_total + blk_total;
 }
@@ -183,7 +195,7 @@ hipError_t launch_store(const NmmoExperience& x, const NmmoStoreInput& in, const
   int* dst = scratch;                // [n_rows]
   int* blk = scratch + in.n_rows;    // [nb]
   int* total = blk + nb;             // [1]
-  hipLaunchKernelGGL(store_count_kernel, dim3(nb), dim3(kStoreBlock), 0, stream, in.mask, in.n_rows, blk);
+  hipLaunchKernelGGL(store_count_kernel, dim3(nb), dim3(kStoreBlock), 0, stream, x, in, blk);
   hipLaunchKernelGGL(store_place_kernel, dim3(nb), dim3(kStoreBlock), 0, stream, x, in, blk, dst, total);
   if (native) {
     ObsParams p = *native;

@@ -53,12 +53,13 @@ class DeviceExperience:
         self.seq = torch.zeros(cap, **i32)
         self.slot_count = torch.zeros(self.n_slots, **i32)
         self.ptr_dev = torch.zeros(1, **i32)
+        self.status_dev = torch.zeros(1, **i32)  # bit 0: a row with an out-of-range env_id was dropped
         self._scratch_rows = 0
         self.scratch = torch.zeros(0, **i32)
         self.x = abi.NmmoExperience(cap, self.obs_elems, self.n_slots, *[
             t.data_ptr() for t in (self.obs, self.actions, self.logprobs, self.rewards, self.dones,
                                    self.truncateds, self.values, self.env_id, self.step, self.seq,
-                                   self.slot_count, self.ptr_dev)])
+                                   self.slot_count, self.ptr_dev, self.status_dev)])
 
     def _stream(self):
         return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
@@ -75,6 +76,11 @@ class DeviceExperience:
         self.slot_count.zero_()
 
     @property
+    def status(self) -> int:
+        """Device status word (nmmo_hip.h NmmoExperience.status); 0 = every selected row stored."""
+        return int(self.status_dev.item())
+
+    @property
     def ptr(self) -> int:
         return int(self.ptr_dev.item())
 
@@ -83,7 +89,7 @@ class DeviceExperience:
         return self.ptr == self.capacity
 
     def store(self, o, r, d, mask, actions, logprob, value, step: int, env_id=None, env_id_base: int = 0,
-              engine=None):
+              engine=None, validate: bool = False):
         """Append the learner-mask rows of one recv in row order, cut at the room left (:331-346).
         o: flat float32 [N, obs_elems] (or [n_envs, P, obs_elems]), or the native uint8
         [n_envs, env_bytes] buffer of `engine` (an NmmoEngine with obs_layout NATIVE), expanded
@@ -102,6 +108,12 @@ class DeviceExperience:
         n = r_.numel()
         a = torch.as_tensor(actions).to(device=dev, dtype=torch.int32).contiguous().view(n, abi.N_ACTION_HEADS)
         eid = None if env_id is None else cvt(env_id, torch.int32)
+        if validate and eid is not None:  # the ABI precondition (synchronising check)
+            sel = eid[cvt(mask, torch.uint8) != 0]
+            if sel.numel() and (int(sel.min()) < 0 or int(sel.max()) >= self.n_slots):
+                raise ValueError("env_id outside [0, n_slots)")
+            if torch.unique(sel).numel() != sel.numel():
+                raise ValueError("env_id must be distinct within one store")
         native = engine is not None and engine.config.obs_layout == abi.OBS_NATIVE
         if native:
             if o.dtype != torch.uint8 or o.shape[0] * engine.P != n:

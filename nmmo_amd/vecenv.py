@@ -70,6 +70,13 @@ class DriverEnv:
         return layout.unflatten(flat, self.config.TASK_EMBED_DIM)
 
 
+def reset_seeds(seed: int, env_index_base: int, n: int) -> np.ndarray:
+    """Per-env reset seeds of pool.async_reset(seed) (clean_pufferl.py:175): env i of a shard
+    whose first global env index is env_index_base gets seed + env_index_base + i, so the
+    shards of a multi-GPU pool reset exactly the envs one pool of all envs would."""
+    return (np.uint64(seed) + np.uint64(env_index_base) + np.arange(n, dtype=np.uint64)).astype(np.uint64)
+
+
 def _config_from_kwargs(env_kwargs) -> Config:
     if isinstance(env_kwargs, Config):
         return env_kwargs
@@ -111,14 +118,13 @@ class GpuVecEnv:
         self.single_action_space = self.driver_env.single_action_space
         self.env_id = np.arange(self.num_envs * self.agents_per_env)
         self._seed = seed
+        self.env_index_base = int(env_index_base)
         self._ready = False
 
     # -- protocol
     def async_reset(self, seed=None):
         if seed is not None:
-            base = np.uint64(seed)
-            seeds = np.array([base + np.uint64(i) for i in range(self.num_envs)], dtype=np.uint64)
-            self.engine.reset(seeds)
+            self.engine.reset(reset_seeds(seed, self.env_index_base, self.num_envs))
         else:
             self.engine.reset()
         self._ready = True

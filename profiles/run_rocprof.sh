@@ -30,11 +30,11 @@ for c in $CONFIGS; do
     continue
   fi
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/$c/trace -o run -- \
-    python3 bench.py $ARGS --steps 100 --warmup 20 --no-cpu-baseline > $OUT/$c/bench.json
+    python3 bench.py $ARGS --steps 100 --warmup 20 --no-cpu-baseline --no-extras > $OUT/$c/bench.json
   timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/$c/fetch -o run -- \
-    python3 bench.py $ARGS --steps 30 --warmup 5 --no-cpu-baseline > /dev/null
+    python3 bench.py $ARGS --steps 30 --warmup 5 --no-cpu-baseline --no-extras > /dev/null
   timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/$c/write -o run -- \
-    python3 bench.py $ARGS --steps 30 --warmup 5 --no-cpu-baseline > /dev/null
+    python3 bench.py $ARGS --steps 30 --warmup 5 --no-cpu-baseline --no-extras > /dev/null
   python3 tools/pmc_summary.py $OUT/$c > $OUT/$c/pmc.json
   echo "profiled $c"
 done

@@ -7,6 +7,7 @@ import os
 import socket
 
 import numpy as np
+import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
@@ -29,19 +30,22 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, reset_seed=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from oracle.oracle import OracleEnvs
 
     base, n = nd.shard(TOTAL, world, rank)
+    from nmmo_amd.vecenv import reset_seeds
+
     o = OracleEnvs(_cfg(), n, seed=31, env_index_base=base)
-    o.reset()
+    # GpuVecEnv.async_reset(seed)'s per-env seeds for this shard (clean_pufferl.py:175)
+    o.reset(None if reset_seed is None else reset_seeds(reset_seed, base, n))
     results = []
     full_ref = None
     if rank == 0:
         full_ref = OracleEnvs(_cfg(), TOTAL, seed=31)
-        full_ref.reset()
+        full_ref.reset(None if reset_seed is None else reset_seeds(reset_seed, 0, TOTAL))
     for t in range(STEPS):
         full_a = torch.from_numpy(full_ref.scripted_actions(100 + t)) if rank == 0 else None
         local_a = nd.scatter_from_learner(full_a, torch.zeros((n, o.P, 12), dtype=torch.int32))
@@ -60,11 +64,12 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_sharded_equals_single_process():
+@pytest.mark.parametrize("reset_seed", [None, 42])
+def test_sharded_equals_single_process(reset_seed):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, reset_seed)) for r in range(2)]
     for p in procs:
         p.start()
     res = q.get(timeout=240)
@@ -72,6 +77,14 @@ def test_sharded_equals_single_process():
         p.join(timeout=60)
         assert p.exitcode == 0
     assert len(res) == STEPS and all(res)
+
+
+def test_reset_seeds_distinct_across_shards():
+    from nmmo_amd.vecenv import reset_seeds
+
+    a = np.concatenate([reset_seeds(7, r * 4, 4) for r in range(2)])
+    assert np.array_equal(a, reset_seeds(7, 0, 8))
+    assert len(set(a.tolist())) == 8
 
 
 def test_shard_bounds():

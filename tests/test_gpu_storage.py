@@ -108,3 +108,29 @@ def test_store_respects_capacity_in_one_recv():
     assert torch.equal(x.env_id.cpu().long(), keep)
     x.store(o, z, z.to(torch.uint8), mask, torch.zeros(n, 12, dtype=torch.int32), z, z, 2)
     assert x.ptr == 100  # full: nothing more is stored
+
+
+def test_store_drops_out_of_range_env_ids():
+    """A selected row whose env_id is outside [0, n_slots) is dropped without writing out of range
+    and raises status bit 0 (nmmo_hip.h NmmoExperience.status); the other rows store normally."""
+    import torch
+
+    from nmmo_amd.storage import DeviceExperience
+
+    n, elems, slots = 64, 5, 64
+    x = DeviceExperience(200, elems, slots)
+    o = torch.arange(n * elems, dtype=torch.float32).view(n, elems).cuda()
+    mask = torch.ones(n, dtype=torch.uint8).cuda()
+    eid = torch.arange(n, dtype=torch.int32)
+    eid[5], eid[9] = slots + 1000, -3
+    z = torch.zeros(n, device="cuda")
+    x.store(o, z, z.to(torch.uint8), mask, torch.zeros(n, 12, dtype=torch.int32), z, z, 1, env_id=eid)
+    assert x.status == 1
+    assert x.ptr == n - 2
+    keep = [r for r in range(n) if r not in (5, 9)]
+    assert torch.equal(x.obs[:n - 2].cpu(), o.cpu()[keep])
+    assert torch.equal(x.slot_count.cpu(), torch.tensor([0 if r in (5, 9) else 1 for r in range(slots)],
+                                                         dtype=torch.int32))
+    with pytest.raises(ValueError):
+        x.store(o, z, z.to(torch.uint8), mask, torch.zeros(n, 12, dtype=torch.int32), z, z, 2, env_id=eid,
+                validate=True)
