@@ -306,6 +306,11 @@ NMMO_API int nmmo_set_tasks(NmmoHandle* h, const NmmoTask* tasks, int32_t n_task
 NMMO_API int nmmo_set_wrapper(NmmoHandle* h, const NmmoWrapperConfig* wc, NmmoAgentInfo* dev_info);
 /* host NmmoWrapState [n_envs][player_n] + u32 [n_envs][player_n][NMMO_UNIQ_WORDS]. Synchronous. */
 NMMO_API int nmmo_get_wrapper_state(NmmoHandle* h, NmmoWrapState* host_state, uint32_t* host_uniq);
+/* Event rows the wrapper never saw since nmmo_set_wrapper because a tick logged more than
+ * event_cap rows and the ring overwrote them (summed over envs). Non-zero means the unique-event
+ * counts and episode stats diverge from the reference's BaseStatWrapper: raise event_cap.
+ * Synchronous. */
+NMMO_API int nmmo_get_wrapper_dropped(NmmoHandle* h, int64_t* total);
 
 /* Native -> flat obs (SPEC.md §8b): native device [n_envs] x (player_n rows + market) as
  * written by nmmo_step under NMMO_OBS_NATIVE, flat device float32 [n_envs][player_n][obs_elems]

@@ -24,6 +24,7 @@ SYMBOLS = [
     "nmmo_set_wrapper", "nmmo_get_wrapper_state", "nmmo_expand_obs", "nmmo_exp_scratch_ints",
     "nmmo_exp_store", "nmmo_exp_sort", "nmmo_exp_gae", "nmmo_gather_rows", "nmmo_n_envs",
     "nmmo_last_error", "nmmo_abi_version", "nmmo_end_episodes", "nmmo_build_info",
+    "nmmo_get_wrapper_dropped",
 ]
 
 
@@ -76,6 +77,7 @@ def lib():
     L.nmmo_last_error.restype = ctypes.c_char_p
     L.nmmo_abi_version.restype = i32
     L.nmmo_end_episodes.argtypes = [vp, vp]
+    L.nmmo_get_wrapper_dropped.argtypes = [vp, ctypes.POINTER(ctypes.c_int64)]
     L.nmmo_build_info.restype = ctypes.c_char_p
     if L.nmmo_abi_version() != abi.ABI_VERSION:
         raise NativeError(f"ABI mismatch: lib {L.nmmo_abi_version()} != python {abi.ABI_VERSION}")

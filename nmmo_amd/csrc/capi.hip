@@ -59,6 +59,7 @@ struct NmmoHandle {
   NmmoWrapState* d_ws = nullptr;
   uint32_t* d_uniq = nullptr;
   int32_t* d_wenv = nullptr;
+  unsigned long long* d_wdrop = nullptr;
   NmmoAgentInfo* d_info = nullptr;  // caller-owned
   // bench timing (nmmo_set_timing): event pairs around the tick and obs kernels
   bool timing = false;
@@ -169,7 +170,7 @@ void nmmo_destroy(NmmoHandle* h) {
   for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
   void* bufs[] = {h->d_env,  h->d_ent,   h->d_ring,  h->d_mat,   h->d_dep,   h->d_bank,
                   h->d_task, h->d_seeds, h->d_items, h->d_iring, h->d_mlist, h->d_mcount,
-                  h->d_events, h->d_tasks, h->d_assign, h->d_tstate, h->d_ws, h->d_uniq, h->d_wenv};
+                  h->d_events, h->d_tasks, h->d_assign, h->d_tstate, h->d_ws, h->d_uniq, h->d_wenv, h->d_wdrop};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   delete h;
@@ -281,7 +282,7 @@ static WrapParams wrap_params(NmmoHandle* h, const int32_t* actions, float* rew,
   WrapParams p;
   p.env = h->d_env; p.ent = h->d_ent; p.items = h->d_items; p.events = h->d_events;
   p.tstate = h->d_tstate; p.actions = actions; p.rew = rew; p.term = term; p.trunc = trunc;
-  p.mask = mask; p.ws = h->d_ws; p.uniq = h->d_uniq; p.wenv = h->d_wenv; p.info = h->d_info;
+  p.mask = mask; p.ws = h->d_ws; p.uniq = h->d_uniq; p.wenv = h->d_wenv; p.wdrop = h->d_wdrop; p.info = h->d_info;
   p.wc = h->wc; p.n_envs = h->st.n_envs; p.P = h->st.P; p.S = h->st.S; p.evcap = h->cfg.event_cap;
   p.items_on = (h->cfg.systems & NMMO_SYS_ITEM) != 0;
   return p;
@@ -612,9 +613,11 @@ int nmmo_set_wrapper(NmmoHandle* h, const NmmoWrapperConfig* wc, NmmoAgentInfo* 
   if (!h->d_ws) {
     if (hipMalloc((void**)&h->d_ws, nP * sizeof(NmmoWrapState)) != hipSuccess ||
         hipMalloc((void**)&h->d_uniq, nP * NMMO_UNIQ_WORDS * 4) != hipSuccess ||
-        hipMalloc((void**)&h->d_wenv, (size_t)h->st.n_envs * 4) != hipSuccess)
+        hipMalloc((void**)&h->d_wenv, (size_t)h->st.n_envs * 4) != hipSuccess ||
+        hipMalloc((void**)&h->d_wdrop, sizeof(unsigned long long)) != hipSuccess)
       return fail(NMMO_E_NOMEM, "wrapper state allocation");
   }
+  HIP_TRY(hipMemset(h->d_wdrop, 0, sizeof(unsigned long long)));
   h->wc = *wc;
   h->d_info = dev_info;
   h->wrap_on = true;
@@ -631,6 +634,17 @@ int nmmo_get_wrapper_state(NmmoHandle* h, NmmoWrapState* host_state, uint32_t* h
   HIP_TRY(hipDeviceSynchronize());
   HIP_TRY(hipMemcpy(host_state, h->d_ws, nP * sizeof(NmmoWrapState), hipMemcpyDeviceToHost));
   if (host_uniq) HIP_TRY(hipMemcpy(host_uniq, h->d_uniq, nP * NMMO_UNIQ_WORDS * 4, hipMemcpyDeviceToHost));
+  return NMMO_OK;
+}
+
+int nmmo_get_wrapper_dropped(NmmoHandle* h, int64_t* total) {
+  if (!h || !total) return fail(NMMO_E_INVALID, "null argument");
+  if (!h->d_wdrop) return fail(NMMO_E_INVALID, "the wrapper layer was never enabled");
+  HIP_TRY(hipSetDevice(h->device));
+  HIP_TRY(hipDeviceSynchronize());
+  unsigned long long v = 0;
+  HIP_TRY(hipMemcpy(&v, h->d_wdrop, sizeof(v), hipMemcpyDeviceToHost));
+  *total = (int64_t)v;
   return NMMO_OK;
 }
 

@@ -66,6 +66,7 @@ struct WrapParams {
   NmmoWrapState* ws;         // [n][P]
   uint32_t* uniq;            // [n][P][NMMO_UNIQ_WORDS]
   int32_t* wenv;             // [n] event rows already processed
+  unsigned long long* wdrop; // [1] event rows overwritten before the wrapper read them
   NmmoAgentInfo* info;       // [n][P] caller-owned, may be NULL
   NmmoWrapperConfig wc;
   int n_envs, P, S, evcap, items_on;

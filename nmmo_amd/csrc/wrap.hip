@@ -139,7 +139,10 @@ __global__ void __launch_bounds__(kWrapThreads) wrap_kernel(WrapParams p, int mo
   // phase 1: this tick's rows (env ring, SPEC §11) -> per-agent terms
   const int cap = p.evcap;
   int lo = p.wenv[e];
-  if (evc - lo > cap) lo = evc - cap;  // rows the ring already overwrote are lost (event_cap too small)
+  if (evc - lo > cap) {  // rows the ring already overwrote are lost (event_cap too small): counted
+    if (tid == 0) atomicAdd(p.wdrop, (unsigned long long)(evc - lo - cap));
+    lo = evc - cap;
+  }
   const int32_t* ring = p.events + (size_t)e * cap * NMMO_EVENT_COLS;
   for (int i = lo + tid; i < evc; i += blockDim.x) {
     const int32_t* r = ring + (size_t)(i % cap) * NMMO_EVENT_COLS;

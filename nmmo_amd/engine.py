@@ -154,6 +154,13 @@ class NmmoEngine:
         self.wrapper = wc
         check(lib().nmmo_set_wrapper(self.h, ctypes.byref(wc), self._ptr(self.info)), "nmmo_set_wrapper")
 
+    def wrapper_dropped_events(self) -> int:
+        """Event rows the wrapper missed (ring overwritten within one tick; nonzero = raise
+        event_cap, the episode stats diverge from the reference's BaseStatWrapper)."""
+        v = ctypes.c_int64()
+        check(lib().nmmo_get_wrapper_dropped(self.h, ctypes.byref(v)), "nmmo_get_wrapper_dropped")
+        return v.value
+
     def info_records(self) -> np.ndarray:
         """The device episode records as numpy agent_info_dtype [n_envs, P] (synchronous)."""
         return self.info.cpu().numpy().view(abi.agent_info_dtype()).reshape(self.n_envs, self.P)

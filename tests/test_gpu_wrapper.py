@@ -84,6 +84,19 @@ def test_wrapper_parity(agent, preset, kw):
                 bad = np.argwhere(go != orc.obs)[:5]
                 raise AssertionError(f"obs differs at step {t}: {bad.tolist()}")
     assert n_done > 0, "no agent finished an episode: the info path was not exercised"
+    assert eng.wrapper_dropped_events() == 0
+
+
+def test_wrapper_reports_dropped_events():
+    """A ring smaller than one tick's events: the overwritten rows are counted, not silently lost."""
+    from nmmo_amd.engine import NmmoEngine
+
+    eng = NmmoEngine(Config.preset("C2", MAP_N=2, event_cap=8), 2, seed=4)
+    eng.set_wrapper(wrapper_config("base"))
+    eng.reset()
+    for t in range(6):
+        eng.step(eng.scripted_actions(t))
+    assert eng.wrapper_dropped_events() > 0
 
 
 def test_wrapper_off_restores_raw_rewards():
