@@ -141,7 +141,9 @@ enum NmmoPredicate {
   PRED_CONSUME_ITEM, PRED_LIST_ITEM, PRED_BUY_ITEM, PRED_EARN_GOLD, PRED_SPEND_GOLD,
   PRED_MAKE_PROFIT, PRED_DEFEAT_ENTITY, PRED_HOARD_GOLD, PRED_ATTAIN_SKILL, PRED_GAIN_EXPERIENCE,
   PRED_EQUIP_ITEM, PRED_OWN_ITEM, PRED_INVENTORY_SPACE_GE, PRED_OCCUPY_TILE, PRED_CAN_SEE_TILE,
-  PRED_FULLY_ARMED, NMMO_N_PREDICATES
+  PRED_FULLY_ARMED,
+  PRED_PRACTICE_EATING, /* curriculum_generation/curriculum_tutorial.py:45-57 (EAT_FOOD count) */
+  NMMO_N_PREDICATES
 };
 #define NMMO_TASK_SINGLE 0
 #define NMMO_TASK_SUM 1
@@ -296,6 +298,15 @@ NMMO_API int nmmo_step(NmmoHandle* h, const int32_t* actions, void* obs, float* 
  * Synchronous. Default after create: one task TickGE(task_num_tick). */
 NMMO_API int nmmo_set_tasks(NmmoHandle* h, const NmmoTask* tasks, int32_t n_tasks,
                             const uint16_t* embeddings, const int32_t* assign);
+/* Task sampling at reset (nmmo.Env's curriculum sampling by TaskSpec.sampling_weight,
+ * environment.py:48-49 CURRICULUM_FILE_PATH, curriculum_generation/manual_curriculum.py):
+ * weights: host double [n_tasks] (>= 0, finite, positive sum; n_tasks = the current table's),
+ * or NULL to keep fixed assignments. While set, every env reset (nmmo_reset and the in-step
+ * auto-reset) draws each player's task index independently with probability w_i / sum(w):
+ * u = Philox draw (SPEC §2, purpose 8, index = player) compared against the thresholds
+ * floor(2^32 * (w_0 + .. + w_i) / sum(w)) (SPEC §12). The drawn index is the player's
+ * assignment (nmmo_get_state). nmmo_set_tasks clears the weights. Synchronous. */
+NMMO_API int nmmo_set_task_weights(NmmoHandle* h, const double* weights, int32_t n_tasks);
 
 /* Wrapper layer (SPEC.md §13; replaces the RewardWrapper(BaseStatWrapper) that env_creator
  * puts around every nmmo.Env, environment.py:58): wc = NULL turns it off. While on, every

@@ -24,7 +24,7 @@ SYMBOLS = [
     "nmmo_set_wrapper", "nmmo_get_wrapper_state", "nmmo_expand_obs", "nmmo_exp_scratch_ints",
     "nmmo_exp_store", "nmmo_exp_sort", "nmmo_exp_gae", "nmmo_gather_rows", "nmmo_n_envs",
     "nmmo_last_error", "nmmo_abi_version", "nmmo_end_episodes", "nmmo_build_info",
-    "nmmo_get_wrapper_dropped",
+    "nmmo_get_wrapper_dropped", "nmmo_set_task_weights",
 ]
 
 
@@ -63,6 +63,7 @@ def lib():
     L.nmmo_set_counters.argtypes = [vp, vp]
     L.nmmo_get_events.argtypes = [vp, i32, vp, i32, ctypes.POINTER(i32)]
     L.nmmo_set_tasks.argtypes = [vp, vp, i32, vp, vp]
+    L.nmmo_set_task_weights.argtypes = [vp, vp, i32]
     L.nmmo_set_wrapper.argtypes = [vp, ctypes.POINTER(abi.NmmoWrapperConfig), vp]
     L.nmmo_get_wrapper_state.argtypes = [vp, vp, vp]
     L.nmmo_expand_obs.argtypes = [vp, vp, vp, i32, vp]

@@ -1,6 +1,7 @@
 // capi.hip — the C-ABI of libnmmo_hip.so (include/nmmo_hip.h). Host side only: owns the
 // device state (SoA over env x slot in HBM), enqueues the gfx950 kernels on the caller's
 // stream, never synchronises inside nmmo_step (graph-capturable, no allocation).
+#include <math.h>
 #include <stdarg.h>
 #include <stdio.h>
 #include <string.h>
@@ -59,6 +60,7 @@ struct NmmoHandle {
   NmmoWrapState* d_ws = nullptr;
   uint32_t* d_uniq = nullptr;
   int32_t* d_wenv = nullptr;
+  uint64_t* d_task_cum = nullptr;
   unsigned long long* d_wdrop = nullptr;
   NmmoAgentInfo* d_info = nullptr;  // caller-owned
   // bench timing (nmmo_set_timing): event pairs around the tick and obs kernels
@@ -170,7 +172,7 @@ void nmmo_destroy(NmmoHandle* h) {
   for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
   void* bufs[] = {h->d_env,  h->d_ent,   h->d_ring,  h->d_mat,   h->d_dep,   h->d_bank,
                   h->d_task, h->d_seeds, h->d_items, h->d_iring, h->d_mlist, h->d_mcount,
-                  h->d_events, h->d_tasks, h->d_assign, h->d_tstate, h->d_ws, h->d_uniq, h->d_wenv, h->d_wdrop};
+                  h->d_events, h->d_tasks, h->d_assign, h->d_tstate, h->d_ws, h->d_uniq, h->d_wenv, h->d_wdrop, h->d_task_cum};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   delete h;
@@ -229,7 +231,7 @@ int nmmo_create(const NmmoConfig* cfg, int32_t n_envs, uint64_t seed, int32_t de
   }
   h->st = DevState{h->d_env,   h->d_ent,   h->d_ring,  h->d_mat,    h->d_dep, h->d_bank,
                    h->d_items, h->d_iring, h->d_mlist, h->d_mcount, h->d_events,
-                   h->d_tasks, h->d_assign, h->d_tstate, 1,            0,           n_envs, P,
+                   h->d_tasks, h->d_assign, nullptr, h->d_tstate, 1,            0,           n_envs, P,
                    N,          S,          seed,       nullptr,     *cfg};
   {  // default task table: everyone runs TickGE(task_num_tick) (SPEC §12)
     NmmoTask t;
@@ -560,7 +562,7 @@ int nmmo_set_tasks(NmmoHandle* h, const NmmoTask* tasks, int32_t n_tasks, const 
     for (int k = 0; k < 2; k++) {
       const int pr = tasks[i].term[k].pred;
       if (pr < 0 || pr >= NMMO_N_PREDICATES) return fail(NMMO_E_INVALID, "task %d term %d: predicate %d", i, k, pr);
-      tev |= pr >= PRED_COUNT_EVENT && pr <= PRED_DEFEAT_ENTITY;
+      tev |= (pr >= PRED_COUNT_EVENT && pr <= PRED_DEFEAT_ENTITY) || pr == PRED_PRACTICE_EATING;
     }
   const size_t nP = (size_t)h->st.n_envs * h->st.P;
   if (assign)
@@ -594,6 +596,47 @@ int nmmo_set_tasks(NmmoHandle* h, const NmmoTask* tasks, int32_t n_tasks, const 
   h->st.tasks = d_tasks;
   h->st.n_tasks = n_tasks;
   h->st.tev = tev;
+  h->st.task_cum = nullptr;  // weights belong to the previous table
+  return NMMO_OK;
+}
+
+// SPEC §12 sampling thresholds: cum[i] = floor(2^32 * (w_0 + .. + w_i) / sum(w)), summed in
+// order in double; the last is exactly 2^32 so every draw u < 2^32 selects a task.
+static void task_thresholds(const double* w, int n, uint64_t* cum) {
+  double sum = 0.0;
+  for (int i = 0; i < n; i++) sum += w[i];
+  double acc = 0.0;
+  for (int i = 0; i < n; i++) {
+    acc += w[i];
+    const double f = floor(acc / sum * 4294967296.0);
+    cum[i] = f >= 4294967296.0 ? (1ull << 32) : (uint64_t)f;
+  }
+  cum[n - 1] = 1ull << 32;
+}
+
+int nmmo_set_task_weights(NmmoHandle* h, const double* weights, int32_t n_tasks) {
+  if (!h) return fail(NMMO_E_INVALID, "null handle");
+  HIP_TRY(hipSetDevice(h->device));
+  HIP_TRY(hipDeviceSynchronize());
+  if (!weights) {
+    h->st.task_cum = nullptr;
+    return NMMO_OK;
+  }
+  if (n_tasks != h->st.n_tasks) return fail(NMMO_E_SIZE, "n_tasks %d != the task table's %d", n_tasks, h->st.n_tasks);
+  double sum = 0.0;
+  for (int i = 0; i < n_tasks; i++) {
+    if (!(weights[i] >= 0.0) || weights[i] > 1e300) return fail(NMMO_E_INVALID, "weight %d = %g", i, weights[i]);
+    sum += weights[i];
+  }
+  if (!(sum > 0.0)) return fail(NMMO_E_INVALID, "weights must have a positive sum");
+  std::vector<uint64_t> cum((size_t)n_tasks);
+  task_thresholds(weights, n_tasks, cum.data());
+  if (!h->d_task_cum) {
+    if (hipMalloc((void**)&h->d_task_cum, (size_t)NMMO_MAX_TASKS * 8) != hipSuccess)
+      return fail(NMMO_E_NOMEM, "task weight allocation");
+  }
+  HIP_TRY(hipMemcpy(h->d_task_cum, cum.data(), cum.size() * 8, hipMemcpyHostToDevice));
+  h->st.task_cum = h->d_task_cum;
   return NMMO_OK;
 }
 

@@ -24,7 +24,7 @@ enum Material : int {
 };
 enum Purpose : uint32_t {
   P_MAPSEL = 1, P_SPAWN_OFFSET = 2, P_RESILIENT = 3, P_NPC_SPAWN = 4, P_NPC_MOVE = 5,
-  P_RESPAWN = 6, P_BUY_ORDER = 7
+  P_RESPAWN = 6, P_BUY_ORDER = 7, P_TASK = 8
 };
 
 // ---------------------------------------------------------------- items (SPEC §9)

@@ -19,6 +19,7 @@ struct DevState {
   int32_t* events;       // [n][cfg.event_cap][NMMO_EVENT_COLS] event-log rings (SPEC §11)
   const NmmoTask* tasks; // [n_tasks] task programs (SPEC §12)
   int32_t* assign;       // [n][P] task index of each player
+  const uint64_t* task_cum;  // [n_tasks] sampling thresholds (nmmo_set_task_weights) or NULL
   NmmoTaskState* tstate; // [n][P] progress / event accumulators
   int n_tasks, tev;      // tev: some task term counts events
   int n_envs, P, N, S;   // N = NPC capacity (0 when the NPC system is off), S = P + N

@@ -69,7 +69,9 @@ struct Ctx {
   int32_t* evg;      // this env's event ring (global), evcap rows (SPEC §11)
   // tasks (SPEC §12)
   const NmmoTask* tasks;   // global task table
-  const int32_t* assign;   // global [P] task index of this env's players
+  int32_t* assign;         // global [P] task index of this env's players (written at reset when sampling)
+  const uint64_t* task_cum;  // global [n_tasks] sampling thresholds, or NULL (fixed assignment)
+  int n_tasks;
   NmmoTaskState* ts;    // [P] task state: == tsl when staged (task events on), else in HBM
   NmmoTaskState* tsl;   // LDS staging of ts (meaningful only when tev)
   int4* tdesc;             // LDS [128][2] (pred, a, b, c) of each player's terms (when tev)
@@ -180,6 +182,8 @@ __device__ __forceinline__ Ctx make_ctx(unsigned char* smem, const DevState& st,
   c.tev = st.tev != 0;
   c.tasks = st.tasks;
   c.assign = st.assign + (size_t)e * st.P;
+  c.task_cum = st.task_cum;
+  c.n_tasks = st.n_tasks;
   c.tsl = reinterpret_cast<NmmoTaskState*>(smem + o);  // an LDS address either way (copy_segs)
   if (c.tev) {
     c.ts = c.tsl;
@@ -479,6 +483,7 @@ __device__ __forceinline__ void task_accumulate(const Ctx& c, int p, int code, i
     int add0 = 0, add1 = 0;
     switch (q.x) {
       case PRED_COUNT_EVENT: add0 = code == q.y; break;
+      case PRED_PRACTICE_EATING: add0 = code == EV_EAT_FOOD; break;
       case PRED_SCORE_HIT: add0 = code == EV_SCORE_HIT && type == q.y; break;
       case PRED_HARVEST_ITEM: add0 = code == EV_HARVEST_ITEM && type == q.y && level >= q.z ? number : 0; break;
       case PRED_CONSUME_ITEM: add0 = code == EV_CONSUME_ITEM && type == q.y && level >= q.z ? number : 0; break;
@@ -640,6 +645,15 @@ __device__ __forceinline__ void reset_env(Ctx& c, uint64_t seed, int episode, in
     TF(F_ALIVE, tid) = 1;
     TF(F_DS_ROW, tid) = (int16_t)(tid + 1);
     TF(F_RESILIENT, tid) = u < c.cfg->resilient_u32 ? 1 : 0;
+    if (c.task_cum) {  // curriculum sampling (SPEC §12): first i with u < cum[i], cum[n-1] = 2^32
+      const uint64_t ut = draw(seed, 0, P_TASK, (uint32_t)tid, 0).x;
+      int lo = 0, hi = c.n_tasks - 1;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (ut < c.task_cum[mid]) hi = mid; else lo = mid + 1;
+      }
+      c.assign[tid] = lo;
+    }
   }
   __syncthreads();
   if (sys(c, NMMO_SYS_NPC)) npc_spawn(c, 0);
@@ -822,6 +836,12 @@ __device__ __forceinline__ double term_progress(const Ctx& c, int p, const NmmoT
   const uint2* inv = c.items ? c.inv + p * kInv : nullptr;
   switch (q.pred) {
     case PRED_TICK_GE: return per_d(c.tick1, q.a);
+    case PRED_PRACTICE_EATING: {  // curriculum_tutorial.py:45-57, Python float arithmetic
+      double pr = __dmul_rn((double)acc[0], 0.06);
+      if (acc[0] >= 1) pr = __dadd_rn(pr, 0.1);
+      if (acc[0] >= 3) pr = __dadd_rn(pr, 0.3);
+      return pr;
+    }
     case PRED_COUNT_EVENT: case PRED_SCORE_HIT: return per_d(acc[0], q.b);
     case PRED_HARVEST_ITEM: case PRED_CONSUME_ITEM: case PRED_LIST_ITEM: case PRED_BUY_ITEM:
     case PRED_DEFEAT_ENTITY: return per_d(acc[0], q.c);

@@ -213,10 +213,32 @@ class NmmoEngine:
         self.task_table = (np.repeat(self.task_table[:1], len(tasks), axis=0) if emb is None
                            else emb.astype(np.float32).reshape(len(tasks), -1))
         asg = None if assign is None else np.ascontiguousarray(assign, np.int32)
+        self.task_names = None
         check(lib().nmmo_set_tasks(self.h, ctypes.cast(arr, ctypes.c_void_p), len(tasks),
                                    None if emb is None else emb.ctypes.data_as(ctypes.c_void_p),
                                    None if asg is None else asg.ctypes.data_as(ctypes.c_void_p)),
               "nmmo_set_tasks")
+
+    def set_task_weights(self, weights):
+        """Sample every player's task at each env reset with probability weight / sum (SPEC §12,
+        nmmo_set_task_weights); None = keep the fixed assignment."""
+        w = None if weights is None else np.ascontiguousarray(weights, np.float64)
+        check(lib().nmmo_set_task_weights(self.h, None if w is None else w.ctypes.data_as(ctypes.c_void_p),
+                                          0 if w is None else len(w)), "nmmo_set_task_weights")
+
+    def set_curriculum(self, specs, sample: bool = True, assign=None):
+        """The curriculum the reference's env samples from (nmmo.Env with CURRICULUM_FILE_PATH,
+        environment.py:48-49): a list of nmmo_amd.tasks.TaskSpec. Their programs become the task
+        table, their embeddings (when every spec has one) the Task obs, their names the
+        facade's spec_name; with sample=True each reset draws every player's task by
+        sampling_weight (call before reset())."""
+        emb = None
+        if all(s.embedding is not None for s in specs):
+            emb = np.stack([np.asarray(s.embedding, np.float16) for s in specs])
+        self.set_tasks([s.program() for s in specs], emb, assign)
+        self.task_names = [s.name for s in specs]
+        if sample:
+            self.set_task_weights([float(s.sampling_weight) for s in specs])
 
     def events(self, env: int, max_rows: int | None = None) -> np.ndarray:
         """Retained event-log rows of `env`, oldest first: int32 [n, 9] (SPEC §11 columns

@@ -236,22 +236,29 @@ class NmmoEnv:
 
     @property
     def realm(self):
-        """Partial realm facade: `realm.tick`, `realm.players[id]` with the entity columns as
-        attributes and `realm.event_log` (the reads of stat_wrapper.py:122-185, 216-285)."""
+        """Realm facade: `realm.tick`, `realm.players` (id -> entity, with `dead_this_tick`),
+        `realm.npcs` and `realm.event_log` — the reads of stat_wrapper.py:122-185, 216-285 and
+        train_helper.py:133-166."""
         return _Realm(self.state(), self.engine.events(0), env=self)
+
+    @property
+    def max_num_agents(self) -> int:
+        return self.config.PLAYER_N
+
+    @property
+    def tasks(self) -> list:
+        """One Task per agent in possible_agents order (nmmo.Env.tasks)."""
+        names = getattr(self.engine, "task_names", None) or [default_spec_name(self.config)]
+        return tasks_from_state(self.state(), self.possible_agents, names, self.engine.task_table)
+
+    @property
+    def agent_task_map(self) -> dict:
+        """agent id -> [Task] (nmmo.Env.agent_task_map, read at stat_wrapper.py:155)."""
+        return {t.assignee[0]: [t] for t in self.tasks}
 
     def state(self) -> dict:
         st = self.engine.get_state()
-        S = self.engine.S
-        per = abi.state_bytes_per_env(S, self.config.PLAYER_N)
-        b = st[:per]
-        env = b[:abi.NE * 4].view(np.int32)
-        o = abi.NE * 4
-        ent = b[o:o + abi.NF * S * 2].view(np.int16).reshape(abi.NF, S)
-        o += abi.NF * S * 2 + S * 2  # entity table, free-row ring
-        mat = b[o:o + abi.MAP_TILES].reshape(abi.MAP_SIZE, abi.MAP_SIZE)
-        return {"tick": int(env[abi.E["tick"]]), "material": mat.copy(),
-                "entities": {n: ent[i].copy() for i, n in enumerate(abi.ENTITY_FIELDS)}}
+        return parse_env_state(st, self.engine.S, self.config.PLAYER_N)
 
     def record_replay(self, helper):
         """realm.record_replay(replay_helper) (train_helper.py:134): the helper is updated after
@@ -273,12 +280,91 @@ def flatten_action(act: dict) -> np.ndarray:
     return out
 
 
+def parse_env_state(blob: np.ndarray, S: int, P: int, env: int = 0) -> dict:
+    """One env of an nmmo_get_state blob (include/nmmo_hip.h) as named arrays."""
+    per = abi.state_bytes_per_env(S, P)
+    b = blob[env * per:(env + 1) * per]
+    o = 0
+    E = b[o:o + abi.NE * 4].copy().view(np.int32); o += abi.NE * 4
+    ent = b[o:o + abi.NF * S * 2].copy().view(np.int16).reshape(abi.NF, S); o += abi.NF * S * 2
+    o += S * 2  # free datastore-row ring
+    mat = b[o:o + abi.MAP_TILES].reshape(abi.MAP_SIZE, abi.MAP_SIZE).copy(); o += abi.MAP_TILES
+    ni = P * abi.INV_SLOTS
+    items = b[o:o + ni * 8].copy().view(np.uint32).reshape(P, abi.INV_SLOTS, 2); o += ni * 8
+    o += ni * 2  # item-row ring
+    assign = b[o:o + P * 4].copy().view(np.int32); o += P * 4
+    tstate = b[o:o + P * abi.TASK_STATE_BYTES].copy().view(abi.task_state_dtype())
+    return {"tick": int(E[abi.E["tick"]]), "env": E, "material": mat, "items": items,
+            "assign": assign, "tstate": tstate,
+            "entities": {n: ent[i].copy() for i, n in enumerate(abi.ENTITY_FIELDS)}}
+
+
+def default_spec_name(config) -> str:
+    from .tasks import spec_name
+
+    return spec_name("TickGE", num_tick=config.task_num_tick)
+
+
+def tasks_from_state(st: dict, possible_agents, names, embeddings=None) -> list:
+    """Task facades of one env (parse_env_state) in possible_agents order."""
+    out = []
+    for i, a in enumerate(possible_agents):
+        k = int(st["assign"][i])
+        out.append(Task((a,), names[k] if k < len(names) else names[0], st["tstate"][i],
+                        None if embeddings is None else embeddings[min(k, len(embeddings) - 1)]))
+    return out
+
+
+class Val(int):
+    """An int entity attribute that also answers `.val` (nmmo's datastore-backed attributes are
+    read as `agent.food.val` at stat_wrapper.py:146-175)."""
+
+    @property
+    def val(self) -> int:
+        return int(self)
+
+
 class _Entity:
-    """One entity row; every entity-table field is an int attribute (alive, health, food, ...)."""
+    """One entity row: every entity-table field is a Val attribute (alive, health, food, ...),
+    plus nmmo's derived `attack_level` (max melee/range/mage level, stat_wrapper.py:170) and a
+    settable `name` (train_helper.py:147)."""
 
     def __init__(self, cols: dict, slot: int):
         for k, v in cols.items():
-            setattr(self, k, int(v[slot]))
+            setattr(self, k, Val(int(v[slot])))
+        self.ent_id = int(self.id)
+        self.name = f"{'Player' if self.ent_id > 0 else 'NPC'}_{self.ent_id}"
+
+    @property
+    def attack_level(self) -> int:
+        return int(max(self.melee_level, self.range_level, self.mage_level))
+
+
+class _Players(dict):
+    """realm.players: id -> entity of live players, plus `dead_this_tick` (id -> entity of the
+    players culled by the last tick, still readable: stat_wrapper.py:136)."""
+
+    def __init__(self, live: dict, dead_this_tick: dict):
+        super().__init__(live)
+        self.dead_this_tick = dead_this_tick
+
+
+class Task:
+    """nmmo.task.task_api.Task facade over the engine's per-agent task state (SPEC §12): the
+    fields stat_wrapper.py:155-163 and train_helper.py:201-225 read."""
+
+    def __init__(self, assignee, spec_name: str, ts, embedding=None):
+        self.assignee = tuple(assignee)
+        self.spec_name = spec_name
+        self._max_progress = float(ts["max_progress"])
+        self.reward_signal_count = int(ts["signals"])
+        self.completed = bool(ts["completed_tick"] > 0)
+        self.embedding = embedding
+        self.progress_info = {"max_progress": self._max_progress,
+                              "completed_tick": int(ts["completed_tick"])}
+
+    def __repr__(self):
+        return f"Task({self.spec_name}, assignee={self.assignee}, max_progress={self._max_progress})"
 
 
 class EventLog:
@@ -309,8 +395,11 @@ class _Realm:
         self.event_log = EventLog(np.zeros((0, abi.EVENT_COLS), np.int32) if events is None else events,
                                   self.tick)
         ent = st["entities"]
-        self.players = {int(ent["id"][s]): _Entity(ent, s) for s in range(len(ent["id"]))
-                        if ent["id"][s] > 0 and ent["alive"][s]}
+        ids, alive, died = ent["id"], ent["alive"], ent["died_tick"]
+        live = {int(ids[s]): _Entity(ent, s) for s in range(len(ids)) if ids[s] > 0 and alive[s]}
+        dead = {int(ids[s]): _Entity(ent, s) for s in range(len(ids))
+                if ids[s] > 0 and not alive[s] and self.tick > 0 and died[s] == self.tick}
+        self.players = _Players(live, dead)
         self.npcs = {int(ent["id"][s]): _Entity(ent, s) for s in range(len(ent["id"]))
                      if ent["id"][s] < 0 and ent["alive"][s]}
 

@@ -16,6 +16,7 @@
  * sites of the path: env.step  reinforcement_learning/stat_wrapper.py:64, env.reset :51,
  * realm reads :122-185; obs consumers agent_zoo/neurips23_start_kit/baseline_policy.py:41-264.
  */
+#include <math.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -192,6 +193,7 @@ typedef struct {
   float* task_emb;     /* [n_tasks][task_embed_dim] Task obs per task */
   int32_t* assign;     /* [n_envs][P] task index of each player */
   NmmoTaskState* tstate; /* [n_envs][P] */
+  uint64_t* task_cum;  /* [n_tasks] sampling thresholds (oracle_set_task_weights) or NULL */
 } Oracle;
 
 #define ENV(o, e) ((o)->env + (size_t)(e) * NMMO_NE)
@@ -233,7 +235,7 @@ static float half_to_float(uint16_t h) {
 /* ------------------------------------------------------------------ items (SPEC §9) */
 enum { T_HAT = 2, T_TOP, T_BOTTOM, T_SPEAR, T_BOW, T_WAND, T_ROD, T_GLOVES, T_PICKAXE, T_AXE,
        T_CHISEL, T_WHETSTONE, T_ARROW, T_RUNES, T_RATION, T_POTION };
-enum { P_BUY_ORDER = 7 };
+enum { P_BUY_ORDER = 7, P_TASK = 8 };
 #define IT_TYPE(w) ((int)((w)[0] & 31))
 #define IT_LEVEL(w) ((int)(((w)[0] >> 5) & 15))
 #define IT_EQUIPPED(w) ((int)(((w)[0] >> 9) & 1))
@@ -372,7 +374,9 @@ static int add_skill_exp(int16_t* T, int S, int p, int f_exp, int xp) {
 /* ------------------------------------------------------------------ event log (SPEC §11) */
 /* EventLogger.record: players only; row k of the episode at ring index (k-1) mod event_cap */
 /* ------------------------------------------------------------------ tasks (SPEC §12) */
-static int pred_counts_events(int pred) { return pred >= PRED_COUNT_EVENT && pred <= PRED_DEFEAT_ENTITY; }
+static int pred_counts_events(int pred) {
+  return (pred >= PRED_COUNT_EVENT && pred <= PRED_DEFEAT_ENTITY) || pred == PRED_PRACTICE_EATING;
+}
 
 /* an event of player p feeds the event accumulators of p's task terms */
 static void task_accumulate(Oracle* o, int e, int p, int code, int type, int level, int number,
@@ -384,6 +388,7 @@ static void task_accumulate(Oracle* o, int e, int p, int code, int type, int lev
     int32_t* acc = ts->acc + 2 * k;
     switch (q->pred) {
       case PRED_COUNT_EVENT: if (code == q->a) acc[0] += 1; break;
+      case PRED_PRACTICE_EATING: if (code == EV_EAT_FOOD) acc[0] += 1; break;
       case PRED_SCORE_HIT: if (code == EV_SCORE_HIT && type == q->a) acc[0] += 1; break;
       case PRED_HARVEST_ITEM: if (code == EV_HARVEST_ITEM && type == q->a && level >= q->b) acc[0] += number; break;
       case PRED_CONSUME_ITEM: if (code == EV_CONSUME_ITEM && type == q->a && level >= q->b) acc[0] += number; break;
@@ -485,6 +490,13 @@ static void reset_env(Oracle* o, int e, uint64_t seed, int episode) {
   E[E_ITEM_FREE_HEAD] = 0;
   E[E_ITEM_FREE_COUNT] = INV * P;
   memset(&o->tstate[(size_t)e * P], 0, (size_t)P * sizeof(NmmoTaskState));
+  if (o->task_cum) /* curriculum sampling (SPEC §12): each player draws its task independently */
+    for (int i = 0; i < P; i++) {
+      draw(seed, 0, P_TASK, (uint32_t)i, 0, u);
+      int k = 0;
+      while ((uint64_t)u[0] >= o->task_cum[k]) k++; /* task_cum[n_tasks - 1] = 2^32 */
+      o->assign[(size_t)e * P + i] = k;
+    }
   if (sys_on(o, NMMO_SYS_NPC)) npc_spawn(o, e, 0);
 }
 
@@ -882,6 +894,13 @@ static double term_progress(Oracle* o, int e, int p, const NmmoTaskTerm* q, cons
   const int sk = q->a >= 1 && q->a <= 8 ? q->a - 1 : -1; /* skill id -> 0..7 */
   switch (q->pred) {
     case PRED_TICK_GE: return per(E[E_TICK], q->a);
+    case PRED_PRACTICE_EATING: { /* curriculum_tutorial.py:45-57: num_eat * 0.06 (+0.1 at >= 1,
+                                    +0.3 at >= 3), Python float arithmetic; norm() is the clip */
+      double pr = (double)acc[0] * 0.06;
+      if (acc[0] >= 1) pr += 0.1;
+      if (acc[0] >= 3) pr += 0.3;
+      return pr;
+    }
     case PRED_COUNT_EVENT: case PRED_SCORE_HIT: return per(acc[0], q->b);
     case PRED_HARVEST_ITEM: case PRED_CONSUME_ITEM: case PRED_LIST_ITEM: case PRED_BUY_ITEM:
     case PRED_DEFEAT_ENTITY: return per(acc[0], q->c);
@@ -1351,7 +1370,7 @@ EXPORT void oracle_destroy(void* h) {
   if (!o) return;
   free(o->env); free(o->ent); free(o->ring); free(o->mat); free(o->bank);
   free(o->items); free(o->iring); free(o->events);
-  free(o->tasks); free(o->task_emb); free(o->assign); free(o->tstate); free(o);
+  free(o->tasks); free(o->task_emb); free(o->assign); free(o->tstate); free(o->task_cum); free(o);
 }
 
 EXPORT int oracle_reset(void* h, const uint64_t* env_seeds, float* obs, uint8_t* mask) {
@@ -1461,10 +1480,36 @@ EXPORT int oracle_set_tasks(void* h, const NmmoTask* tasks, int n_tasks, const u
   o->tasks = (NmmoTask*)malloc((size_t)n_tasks * sizeof(NmmoTask));
   memcpy(o->tasks, tasks, (size_t)n_tasks * sizeof(NmmoTask));
   o->n_tasks = n_tasks;
+  free(o->task_cum); /* weights belong to the previous table */
+  o->task_cum = NULL;
   o->tev = 0;
   for (int i = 0; i < n_tasks; i++)
     for (int k = 0; k < 2; k++) o->tev |= pred_counts_events(tasks[i].term[k].pred);
   for (size_t i = 0; i < (size_t)o->n_envs * o->P; i++) o->assign[i] = assign ? assign[i] : 0;
+  return 0;
+}
+
+/* as nmmo_set_task_weights (SPEC §12): thresholds floor(2^32 * prefix / sum), last = 2^32 */
+EXPORT int oracle_set_task_weights(void* h, const double* w, int n_tasks) {
+  Oracle* o = (Oracle*)h;
+  if (!w) { free(o->task_cum); o->task_cum = NULL; return 0; }
+  if (n_tasks != o->n_tasks) return NMMO_E_SIZE;
+  double sum = 0.0;
+  for (int i = 0; i < n_tasks; i++) {
+    if (!(w[i] >= 0.0) || w[i] > 1e300) return NMMO_E_INVALID;
+    sum += w[i];
+  }
+  if (!(sum > 0.0)) return NMMO_E_INVALID;
+  uint64_t* cum = (uint64_t*)malloc((size_t)n_tasks * 8);
+  double acc = 0.0;
+  for (int i = 0; i < n_tasks; i++) {
+    acc += w[i];
+    double f = floor(acc / sum * 4294967296.0);
+    cum[i] = f >= 4294967296.0 ? (1ull << 32) : (uint64_t)f;
+  }
+  cum[n_tasks - 1] = 1ull << 32;
+  free(o->task_cum);
+  o->task_cum = cum;
   return 0;
 }
 

@@ -45,6 +45,7 @@ def lib():
         L.oracle_get_map_bank.argtypes = [vp, vp, sz]
         L.oracle_set_map_bank.argtypes = [vp, vp, sz]
         L.oracle_end_episodes.argtypes = [vp, vp]
+        L.oracle_set_task_weights.argtypes = [vp, vp, i32]
         L.oracle_write_obs.argtypes = [vp, i32, vp]
         L.oracle_get_events.argtypes = [vp, i32, vp, i32, ctypes.POINTER(i32)]
         L.oracle_set_tasks.argtypes = [vp, vp, i32, vp, vp]
@@ -140,6 +141,22 @@ class OracleEnvs:
         rc = lib().oracle_set_tasks(self.h, ctypes.cast(arr, ctypes.c_void_p), len(tasks),
                                     None if emb is None else emb.ctypes.data_as(ctypes.c_void_p), _p(asg))
         assert rc == 0, rc
+
+    def set_task_weights(self, weights):
+        """as nmmo_set_task_weights (SPEC §12); None = fixed assignment."""
+        w = None if weights is None else np.ascontiguousarray(weights, np.float64)
+        rc = lib().oracle_set_task_weights(self.h, _p(w), 0 if w is None else len(w))
+        if rc != 0:
+            raise ValueError(f"oracle_set_task_weights failed ({rc})")
+
+    def set_curriculum(self, specs, sample=True, assign=None):
+        """A list of nmmo_amd.tasks.TaskSpec, as NmmoEngine.set_curriculum."""
+        emb = None
+        if all(s.embedding is not None for s in specs):
+            emb = np.stack([np.asarray(s.embedding, np.float16) for s in specs])
+        self.set_tasks([s.program() for s in specs], emb, assign)
+        if sample:
+            self.set_task_weights([float(s.sampling_weight) for s in specs])
 
     def events(self, env: int, max_rows: int = 1 << 20) -> np.ndarray:
         """Retained event-log rows of `env`, oldest first: int32 [n, 9] (SPEC §11)."""

@@ -278,6 +278,44 @@ def test_task_parity_all_predicates():
     assert (st["signals"] > 0).mean() > 0.15 and (st["completed_tick"] > 0).any()
 
 
+def test_curriculum_sampling_parity():
+    """The reference's training curriculum (manual_curriculum.py + curriculum_tutorial.py, with
+    PracticeEating), sampled per player by sampling_weight at every reset and auto-reset
+    (nmmo_set_task_weights, SPEC §12): assignments, task state, rewards and Task obs bit-exact."""
+    import torch
+
+    from nmmo_amd import tasks
+
+    n, steps = 6, 150
+    cfg = Config.preset("C4", MAP_N=8, early_stop_agent_num=8)
+    specs = tasks.manual_curriculum() + tasks.tutorial_curriculum()
+    rng = np.random.default_rng(4)
+    for s in specs:
+        s.embedding = rng.standard_normal(cfg.TASK_EMBED_DIM).astype(np.float16)
+    eng = _engine(cfg, n, seed=13)
+    orc = OracleEnvs(cfg, n, seed=13)
+    eng.set_curriculum(specs)
+    orc.set_curriculum(specs)
+    eng.reset()
+    orc.reset()
+    seen = set()
+    for t in range(steps):
+        acts = orc.scripted_actions(700 + t)
+        orc.step(acts)
+        eng.step(torch.from_numpy(acts).cuda())
+        torch.cuda.synchronize()
+        g = split_state(eng.get_state(), n, eng.S, eng.P)
+        o = split_state(orc.get_state(), n, orc.S, orc.P)
+        assert np.array_equal(g["tasks"], o["tasks"]), f"sampled assignment @ {t}"
+        seen.update(np.unique(o["tasks"]).tolist())
+        _cmp_state(eng.get_state(), orc.get_state(), n, eng.S, f"curriculum step {t}")
+        assert np.array_equal(eng.rew.cpu().numpy(), orc.rew), f"rewards @ {t}"
+        if t % 25 == 0:
+            assert np.array_equal(eng.obs.cpu().numpy(), orc.obs), f"obs @ {t}"
+    assert len(seen) > 200  # many distinct tasks drawn over the resets
+    assert int(split_state(orc.get_state(), n, orc.S, orc.P)["env"][:, abi.E["episode"]].min()) >= 1
+
+
 @pytest.mark.parametrize("P,N,preset", [(100, 50, "C4"), (13, 0, "C3"), (64, 256, "C4"), (1, 7, "C4")])
 def test_rollout_parity_odd_sizes(P, N, preset):
     """Player/NPC counts that are not multiples of 8/16/64: scalar state-copy fallbacks, partial

@@ -104,3 +104,40 @@ def test_pool_with_reward_wrapper_returns_stat_infos():
         ow.after_step(acts)
     assert finished > 0
     pool.close()
+
+
+def test_facade_serves_stat_wrapper_reads():
+    """NmmoEnv over the HIP engine answers every read of stat_wrapper.py:122-185 (dead_this_tick,
+    .val attributes, attack_level, agent_task_map task fields) with the values the oracle's state
+    gives, on a sampled heldout curriculum."""
+    from nmmo_amd import tasks
+    from nmmo_amd.vecenv import NmmoEnv, _Realm, parse_env_state, tasks_from_state
+    from oracle.oracle import OracleEnvs
+    from tests.test_facade import walk_stat_wrapper_reads
+
+    cfg = Config.preset("C4", MAP_N=2, early_stop_agent_num=0)
+    env = NmmoEnv(cfg, seed=17)
+    ref = OracleEnvs(cfg, 1, seed=17)
+    specs = tasks.heldout_curriculum()
+    env.engine.set_curriculum(specs)
+    ref.set_curriculum(specs)
+    env.reset()
+    ref.reset()
+    names = [s.name for s in specs]
+    walked = 0
+    for t in range(90):
+        a = ref.scripted_actions(40 + t)
+        ref.step(a)
+        _, rew, term, trunc, _ = env.step({p: a[0, p - 1] for p in env.possible_agents})
+        realm, tmap = env.realm, env.agent_task_map
+        st = parse_env_state(ref.get_state(), ref.S, ref.P)
+        oreal = _Realm(st, ref.events(0))
+        otmap = {tk.assignee[0]: [tk] for tk in tasks_from_state(st, env.possible_agents, names)}
+        assert realm.tick == oreal.tick
+        assert sorted(realm.players.dead_this_tick) == sorted(oreal.players.dead_this_tick)
+        for p, dead in term.items():
+            if dead or trunc[p]:
+                assert walk_stat_wrapper_reads(realm, tmap, p, dead) == walk_stat_wrapper_reads(oreal, otmap, p, dead)
+                walked += 1
+    assert walked > 0
+    env.close()
