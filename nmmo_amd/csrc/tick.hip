@@ -675,6 +675,58 @@ __device__ __forceinline__ bool npc_validate(Ctx& c, int n) {
   return TF(F_NPC_TYPE, n) == 3 && !TF(F_TARGET_ID, n);
 }
 
+// SPEC §6 v2 pathing, bit-parallel: the 15x15 window around the NPC as 15 row masks (bit j =
+// window column j passable), a breadth-first wave grown from the target tile one 4-neighbour
+// step per iteration with shifts and ORs, until it covers the NPC's tile (window centre) or
+// stops growing. The NPC steps to the first of N, S, E, W that the previous wave covered, i.e.
+// a neighbour one step closer to the target. -1 = unreachable inside the window. The window
+// (rows r-7..r+7, cols c-7..c+7) lies inside the map: NPCs stay in the playable area 16..143.
+__device__ __forceinline__ int window_bfs_step(const uint8_t* __restrict__ mat, int r, int col,
+                                                          int tr, int tc) {
+  constexpr int W = 2 * kVision + 1;
+  constexpr uint32_t kImp = (1u << M_VOID) | (1u << M_WATER) | (1u << M_STONE) | (1u << M_OCEAN) | (1u << M_FISH);
+  uint32_t pass[W], R[W];
+#pragma unroll
+  for (int i = 0; i < W; i++) {
+    const int base = (r - kVision + i) * kSize + col - kVision;  // 15 bytes from here
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(mat + (base & ~3));
+    const int sh = base & 3;
+    const uint32_t d0 = w[0], d1 = w[1], d2 = w[2], d3 = w[3], d4 = w[4];
+    uint32_t m = 0;
+#pragma unroll
+    for (int j = 0; j < W; j++) {
+      const int k = sh + j;  // byte k of the 20 loaded
+      const uint32_t dw = (k >> 2) == 0 ? d0 : (k >> 2) == 1 ? d1 : (k >> 2) == 2 ? d2 : (k >> 2) == 3 ? d3 : d4;
+      const uint32_t mt = (dw >> ((k & 3) * 8)) & 15u;
+      m |= ((kImp >> mt) & 1u) ? 0u : (1u << j);
+    }
+    pass[i] = m;
+  }
+  const int si = tr - r + kVision, sj = tc - col + kVision;
+#pragma unroll
+  for (int i = 0; i < W; i++) R[i] = i == si ? (1u << sj) : 0u;
+  constexpr uint32_t kMid = 1u << kVision;
+  for (int it = 0; it < W * W; it++) {
+    uint32_t N[W], grew = 0;
+#pragma unroll
+    for (int i = 0; i < W; i++) {
+      const uint32_t up = i > 0 ? R[i - 1] : 0u, dn = i < W - 1 ? R[i + 1] : 0u;
+      N[i] = (R[i] | (R[i] << 1) | (R[i] >> 1) | up | dn) & pass[i];
+      grew |= N[i] ^ R[i];
+    }
+    if (N[kVision] & kMid) {  // the NPC's tile is reached at distance it+1: R = distance <= it
+      if ((R[kVision - 1] & kMid) != 0u) return 0;   // N
+      if ((R[kVision + 1] & kMid) != 0u) return 1;   // S
+      if ((R[kVision] & (kMid << 1)) != 0u) return 2;  // E (col + 1)
+      return 3;                                       // W (col - 1)
+    }
+    if (!grew) return -1;
+#pragma unroll
+    for (int i = 0; i < W; i++) R[i] = N[i];
+  }
+  return -1;
+}
+
 // closest: slot of the closest player within vision (ties to the lowest id) for a hostile NPC
 // without a target (computed block-wide by the caller), else -1
 // nbm: tick-start neighbourhood bits of the NPC's tile (bit d = neighbour d passable)
@@ -707,7 +759,9 @@ __device__ __forceinline__ void npc_decide(Ctx& c, int n, int closest, uint32_t 
   const int dist = linf(r, col, tr, tc);
   if (dist == 0) {
     move = (int)uniform_n(u.y, 4);
-  } else if (dist > 1) {
+  } else if (dist > 1 && (move = window_bfs_step(c.mat, r, col, tr, tc)) >= 0) {
+    // move.pathfind: first step of a shortest path inside the 15x15 window (SPEC §6 v2)
+  } else if (dist > 1) {  // target unreachable inside the window: greedy step (SPEC §6 v1 rule)
     const int dr = tr - r, dc = tc - col;
     const int dir_r = dr > 0 ? 1 : 0, dir_c = dc > 0 ? 2 : 3;
     const bool rows_first = iabs(dr) >= iabs(dc);

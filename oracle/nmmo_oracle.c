@@ -581,6 +581,37 @@ static int player_slot_valid(const Oracle* o, const int16_t* T, int id, int r, i
          linf(r, c, FLD(T, F_ROW, s), FLD(T, F_COL, s)) <= VISION;
 }
 
+/* SPEC §6 v2 pathing: breadth-first search from the target tile (tr, tc) over the passable tiles
+ * of the 15x15 window centred on the NPC at (r, c), 4-neighbour moves. Returns the first of
+ * N, S, E, W whose neighbour of the NPC lies one step closer to the target, or -1 when the
+ * target cannot be reached inside the window. */
+static int window_bfs_step(const uint8_t* mat, int r, int c, int tr, int tc) {
+  enum { W = 2 * VISION + 1 };
+  int dist[W][W], qr[W * W], qc[W * W], head = 0, tail = 0;
+  for (int i = 0; i < W; i++)
+    for (int j = 0; j < W; j++) dist[i][j] = -1;
+  const int si = tr - r + VISION, sj = tc - c + VISION;
+  dist[si][sj] = 0;
+  qr[tail] = si; qc[tail++] = sj;
+  while (head < tail) {
+    const int i = qr[head], j = qc[head++];
+    for (int d = 0; d < 4; d++) {
+      const int ni = i + DR[d], nj = j + DC[d];
+      if (ni < 0 || ni >= W || nj < 0 || nj >= W || dist[ni][nj] >= 0) continue;
+      if (impassable(mat[(r - VISION + ni) * SIZE + (c - VISION + nj)])) continue;
+      dist[ni][nj] = dist[i][j] + 1;
+      qr[tail] = ni; qc[tail++] = nj;
+    }
+  }
+  const int here = dist[VISION][VISION];
+  if (here < 0) return -1;
+  for (int d = 0; d < 4; d++) {
+    const int ni = VISION + DR[d], nj = VISION + DC[d];
+    if (dist[ni][nj] == here - 1) return d;
+  }
+  return -1; /* unreachable: a neighbour one step closer always exists */
+}
+
 static void npc_decide(Oracle* o, int e, int n, int* move_dir, int* atk_target, int* atk_style) {
   const int S = o->S;
   int16_t* T = ENT(o, e);
@@ -623,7 +654,10 @@ static void npc_decide(Oracle* o, int e, int n, int* move_dir, int* atk_target, 
   int dist = linf(r, c, tr, tc);
   if (dist == 0) {
     *move_dir = (int)U(u[1], 4);
-  } else if (dist > 1) { /* move.pathfind: greedy step (SPEC §6 decision) */
+  } else if (dist > 1 && (*move_dir = window_bfs_step(mat, r, c, tr, tc)) >= 0) {
+    /* move.pathfind: first step of a shortest 4-neighbour path inside the NPC's 15x15 window
+       (SPEC §6 v2, a bounded stand-in for nmmo's A*) */
+  } else if (dist > 1) { /* target unreachable inside the window: greedy step (SPEC §6 v1 rule) */
     int dr = tr - r, dc = tc - c;
     int dir_r = dr > 0 ? 1 : 0, dir_c = dc > 0 ? 2 : 3;
     int first = abs(dr) >= abs(dc) ? dir_r : dir_c, second = abs(dr) >= abs(dc) ? dir_c : dir_r;

@@ -278,6 +278,71 @@ def test_task_parity_all_predicates():
     assert (st["signals"] > 0).mean() > 0.15 and (st["completed_tick"] > 0).any()
 
 
+def pathing_scenario(n=4):
+    """SPEC §6 v2 window BFS under stress: in every env, hostile NPCs are put 2-7 tiles from live
+    players and stone walls are scattered around them, so most hunts path around obstacles (and
+    some targets are unreachable inside the window: greedy fallback). HIP vs oracle, bit-exact."""
+    from oracle.oracle import join_state
+
+    cfg = Config.preset("C3", MAP_N=4, early_stop_agent_num=0)
+    orc = OracleEnvs(cfg, n, seed=41)
+    orc.reset()
+    for t in range(3):
+        orc.step(orc.scripted_actions(t))
+    d = split_state(orc.get_state(), n, orc.S, orc.P)
+    rng = np.random.default_rng(12)
+    F = abi.F
+    for e in range(n):
+        ent, mat = d["ent"][e], d["mat"][e]
+        occupied = {(int(ent[F["row"], s]), int(ent[F["col"], s])) for s in range(orc.S) if ent[F["alive"], s]}
+        players = [s for s in range(orc.P) if ent[F["alive"], s]]
+        npcs = [s for s in range(orc.P, orc.S) if ent[F["alive"], s]][:60]
+        for k, s in enumerate(npcs):
+            p = players[k % len(players)]
+            pr, pc = int(ent[F["row"], p]), int(ent[F["col"], p])
+            for _ in range(50):
+                r = int(np.clip(pr + rng.integers(-7, 8), 17, 142))
+                c = int(np.clip(pc + rng.integers(-7, 8), 17, 142))
+                if max(abs(r - pr), abs(c - pc)) >= 2 and (r, c) not in occupied and mat[r, c] not in (0, 1, 5, 14, 15):
+                    break
+            occupied.discard((int(ent[F["row"], s]), int(ent[F["col"], s])))
+            occupied.add((r, c))
+            ent[F["row"], s], ent[F["col"], s] = r, c
+            ent[F["npc_type"], s] = 3
+            ent[F["target_id"], s] = 0
+        for p in players:  # scattered walls around each player, never under an entity
+            pr, pc = int(ent[F["row"], p]), int(ent[F["col"], p])
+            for _ in range(20):
+                r, c = pr + int(rng.integers(-6, 7)), pc + int(rng.integers(-6, 7))
+                if 16 <= r <= 143 and 16 <= c <= 143 and (r, c) not in occupied:
+                    mat[r, c] = 5  # Stone
+    orc.set_state(join_state(d))
+    return orc
+
+
+def test_npc_pathing_parity():
+    """SPEC §6 v2 window BFS under stress (pathing_scenario): HIP vs oracle, bit-exact."""
+    import torch
+
+    n, steps = 4, 40
+    F = abi.F
+    orc = pathing_scenario(n)
+    cfg = orc.config
+    eng = _engine(cfg, n, seed=0)
+    eng.set_state(orc.get_state())
+    for t in range(steps):
+        acts = orc.scripted_actions(300 + t)
+        orc.step(acts)
+        eng.step(torch.from_numpy(acts).cuda())
+        torch.cuda.synchronize()
+        _cmp_state(eng.get_state(), orc.get_state(), n, eng.S, f"pathing step {t}")
+        assert np.array_equal(eng.rew.cpu().numpy(), orc.rew), f"rewards @ {t}"
+        if t == 0:
+            hunting = int((split_state(orc.get_state(), n, orc.S, orc.P)["ent"][:, F["target_id"]] > 0).sum())
+            assert hunting > 100, hunting
+    _cmp_events(eng, orc, n, "pathing end")
+
+
 def test_curriculum_sampling_parity():
     """The reference's training curriculum (manual_curriculum.py + curriculum_tutorial.py, with
     PracticeEating), sampled per player by sampling_weight at every reset and auto-reset

@@ -452,3 +452,52 @@ def test_event_log_harvest_item():
     ev = o.events(0)
     h = ev[(ev[:, C["event"]] == EV.HARVEST_ITEM) & (ev[:, C["ent_id"]] == 1)]
     assert h.shape[0] == 1 and (h[0, C["item_type"]], h[0, C["level"]], h[0, C["quantity"]]) == (13, 1, 1)
+
+
+def _npc_scenario(wall):
+    """A hostile NPC 3 tiles west of player 1 on open grass; `wall` = list of (dr, dc) offsets
+    from the NPC that are turned to Stone. Returns (o, npc_slot, (r, c))."""
+    o, d = make(("Resource", "Combat", "NPC"), P=4)
+    mat = d["mat"][0]
+    r, c = 60, 60
+    mat[r - 8:r + 9, c - 8:c + 12] = GRASS  # an open field (tiles off the bank material never respawn: grass)
+    park_others(d, {0}, mat)
+    place(d, 0, r, c + 3)
+    ent = d["ent"][0]
+    n = o.P  # first NPC slot; move every other NPC far away
+    for s in range(o.P + 1, o.S):
+        if ent[F["alive"], s]:
+            place(d, s, 30 + (s % 50), 30 + (s // 50))
+    place(d, n, r, c, npc_type=3, target_id=1, attacker_id=0, health=100)
+    for dr, dc in wall:
+        mat[r + dr, c + dc] = STONE
+    put(o, d)
+    return o, n, (r, c)
+
+
+def test_npc_hunt_takes_shortest_path_around_a_wall():
+    """SPEC §6 v2: BFS inside the 15x15 window. A wall at column +1 (rows -2..+2) between the NPC
+    and its target: both N and S start a shortest path around it; N comes first. (The v1 greedy
+    rule would try E, find Stone, and stay because the row offset is 0.)"""
+    o, n, (r, c) = _npc_scenario([(i, 1) for i in range(-2, 3)])
+    o.step(noop_actions(o))
+    ent = split_state(o.get_state(), 1, o.S, o.P)["ent"][0]
+    assert (ent[F["row"], n], ent[F["col"], n]) == (r - 1, c)
+
+
+def test_npc_hunt_prefers_first_direction_on_open_ground():
+    """No obstacle: N/S/E/W order among the shortest-path first steps; target due east -> E."""
+    o, n, (r, c) = _npc_scenario([])
+    o.step(noop_actions(o))
+    ent = split_state(o.get_state(), 1, o.S, o.P)["ent"][0]
+    assert (ent[F["row"], n], ent[F["col"], n]) == (r, c + 1)
+
+
+def test_npc_hunt_unreachable_falls_back_to_greedy():
+    """Target walled in on all sides inside the window: the v1 greedy step (E is Stone, row offset
+    0) -> stay."""
+    ring = [(i, j) for i in range(-1, 2) for j in range(2, 5) if (i, j) != (0, 3)]
+    o, n, (r, c) = _npc_scenario(ring)
+    o.step(noop_actions(o))
+    ent = split_state(o.get_state(), 1, o.S, o.P)["ent"][0]
+    assert (ent[F["row"], n], ent[F["col"], n]) == (r, c + 1)  # E is open here: greedy steps E
