@@ -7,10 +7,12 @@
 //
 // Roofline: this kernel is HBM-write-bound — 95,948 B written per agent row against ~0.3 KB of
 // reads (the env's entity columns are staged once per workgroup in LDS and shared by its 16
-// agents; the 225 map bytes per agent come from L2). One wave owns one agent row at a time:
-// it compacts the agent's visible entities with a ballot/prefix-popcount over datastore rows
-// (the nmmo window order) into LDS, then streams the row with coalesced stores — 16-byte
-// stores for the long constant runs (Inventory+Market), dword stores elsewhere.
+// agents; the 225 map bytes and the 8-KB Task embedding per agent come from L2). One wave owns
+// one agent row at a time: it compacts the agent's visible entities with a ballot/prefix-popcount
+// over datastore rows (the nmmo window order) into LDS, then streams the row with coalesced
+// stores — 16-byte stores for the zero runs (unseen Entity rows, Market), dword stores elsewhere.
+// Every global load of the next agent is issued ahead of the current row's bulk stores, so the
+// store stream never waits on a load (vmcnt retires in issue order).
 #include "kernels.h"
 
 namespace nmmo {
@@ -19,13 +21,13 @@ constexpr int kObsAgentsPerBlock = 16;
 constexpr int kObsWaves = 4;
 constexpr int kObsFields = F_DS_ROW + 1;  // 0..30 obs columns, alive, ds_row
 
-// LDS: entity fields | row->slot | per-wave visible list | per-wave inventory | market listings
-// (flat: listed item words + owners, 12 B per listing; native: price | owner << 8, 2 B per listing,
-// and per-wave 15x15 window materials)
+// LDS: entity fields | row->slot | per-wave visible list | per-wave inventory | per-wave 15x15
+// window materials | market listings (price | owner << 8, 2 B per listing; flat rows also the
+// listed item words, 8 B). 38.8 KB at S = 384: 4 workgroups (16 waves) per CU.
 __host__ __device__ inline size_t obs_lds_bytes(int S, bool native) {
   return (((size_t)kObsFields * S * 2 + 15) & ~(size_t)15) + (((size_t)(S + 1) * 2 + 15) & ~(size_t)15) +
          (size_t)kObsWaves * 128 * 2 + (size_t)kObsWaves * kInv * 8 +
-         (native ? (size_t)NMMO_MARKET_ROWS * 2 + (size_t)kObsWaves * 256 : (size_t)NMMO_MARKET_ROWS * 12);
+         (size_t)kObsWaves * 256 + (native ? (size_t)NMMO_MARKET_ROWS * 2 : (size_t)NMMO_MARKET_ROWS * 10);
 }
 
 // Plain (temporal) stores. Measured on MI355X (same-box A/B): __builtin_nontemporal_store
@@ -60,8 +62,99 @@ __device__ __forceinline__ uint32_t i16pack(int lo, int hi) {
   return (uint32_t)(uint16_t)(int16_t)lo | ((uint32_t)(uint16_t)(int16_t)hi << 16);
 }
 
-// kWrap: the wrapper's observation() edits are compiled in (SPEC §13). Both variants stay at
-// 79 VGPRs = 6 waves/SIMD (a run-time flag check in the shared body cost 2 VGPRs and a wave).
+// One agent's view for the ActionTargets sections (SPEC §8, §9, §13 edits).
+struct MaskCtx {
+  int a, r, c, nv, gold, ninv, prev_price;
+  uint32_t movebits;  // bit d: the tile in direction d is passable
+  bool combat, item, exch, no_give;
+};
+
+// The 12 ActionTargets sections in flat order: [lo, lo + n) of the mask part of the row.
+__device__ __forceinline__ void mask_section(const ObsParams& p, int sec, int& lo, int& n) {
+  switch (sec) {
+    case 0: lo = p.o_style; n = p.o_target - p.o_style; break;
+    case 1: lo = p.o_target; n = kNObs + 1; break;
+    case 2: lo = p.o_buy; n = NMMO_MARKET_ROWS + 1; break;
+    case 3: lo = p.o_destroy; n = kInv + 1; break;
+    case 4: lo = p.o_give_item; n = kInv + 1; break;
+    case 5: lo = p.o_give_target; n = kNObs + 1; break;
+    case 6: lo = p.o_gg_price; n = p.o_gg_target - p.o_gg_price; break;
+    case 7: lo = p.o_gg_target; n = kNObs + 1; break;
+    case 8: lo = p.o_move; n = p.o_sell_item - p.o_move; break;
+    case 9: lo = p.o_sell_item; n = kInv + 1; break;
+    case 10: lo = p.o_sell_price; n = p.o_use - p.o_sell_price; break;
+    default: lo = p.o_use; n = p.o_agent_id - p.o_use; break;
+  }
+}
+
+// Entry k of section sec (the section id is wave-uniform: no lane evaluates another section's
+// predicate). Buy.MarketItem reads the packed listings (price | owner << 8) in either layout.
+template <bool kWrap>
+__device__ __forceinline__ bool mask_value(const ObsParams& p, const int16_t* T, int S,
+                                           const int16_t* vis, const uint2* inv, const uint16_t* mpo,
+                                           int nm, const MaskCtx& m, int sec, int k) {
+  auto free_item = [&](int q) { return q < m.ninv && !it_equipped(inv[q]) && !it_price(inv[q]); };
+  auto same_tile = [&](int q) {
+    const int s = vis[q];
+    return s < p.P && s != m.a && T[F_ROW * S + s] == m.r && T[F_COL * S + s] == m.c;
+  };
+  bool v;
+  switch (sec) {
+    case 0: v = m.combat; break;
+    case 1:
+      if (k == kNObs) {
+        v = true;
+      } else if (!m.combat || k >= m.nv) {
+        v = false;
+      } else {
+        const int q = vis[k];
+        v = q != m.a && linf(m.r, m.c, T[F_ROW * S + q], T[F_COL * S + q]) <= 3 &&
+            !(q < p.P && T[F_TIME_ALIVE * S + q] < p.spawn_immunity);
+        if constexpr (kWrap)
+          if ((p.wflags & kWrapObsNoDangerous) && T[F_NPC_TYPE * S + q] > 1) v = false;
+      }
+      break;
+    case 2:
+      v = k == NMMO_MARKET_ROWS ||
+          (m.exch && k < nm && (int)(mpo[k] & 255u) <= m.gold && (int)(mpo[k] >> 8) != m.a);
+      break;
+    case 3: v = k == kInv || (m.item && free_item(k)); break;
+    case 4: v = k == kInv || (!m.no_give && m.item && free_item(k)); break;
+    case 5: v = k == kNObs || (!m.no_give && m.item && k < m.nv && same_tile(k)); break;
+    case 6: v = m.exch && k < m.gold && (!m.no_give || k == 0); break;
+    case 7: v = k == kNObs || (!m.no_give && m.exch && k < m.nv && same_tile(k)); break;
+    case 8: v = (m.movebits >> k) & 1u; break;
+    case 9: v = k == kInv || (m.exch && k < m.ninv && !it_equipped(inv[k])); break;
+    case 10:
+      v = m.exch;
+      if constexpr (kWrap)
+        if ((p.wflags & kWrapObsPrice) && k == m.prev_price) v = false;
+      break;
+    default: v = k == kInv || (m.item && k < m.ninv && item_usable(T, S, m.a, inv[k])); break;
+  }
+  return v;
+}
+
+// Passability of the 5 move targets from the prefetched window materials: tile t of the 15x15
+// window sits in lane t & 63 of register t >> 6; the centre's 4 neighbours (t = 97, 111, 112,
+// 113, 127) are all in register 1.
+__device__ __forceinline__ uint32_t move_bits(uint32_t wm1) {
+  uint32_t b = 0u;
+#pragma unroll
+  for (int d = 0; d < 5; d++) {
+    const int t = (kVision + dir_dr(d)) * 15 + kVision + dir_dc(d);
+    if (!impassable((int)__builtin_amdgcn_readlane((int)wm1, t - 64))) b |= 1u << d;
+  }
+  return b;
+}
+
+// Flat rows: each agent's global loads (its 12 item words, 15x15 window materials, Task
+// embedding) are issued before the previous agent's remaining ~130 stores (vmcnt retires in
+// issue order, so a load issued after a store stream waits for all of it; issued ahead of >= 63
+// younger stores it costs no wait at all).
+constexpr int kTaskRegs = 32;  // Task embedding dwords per lane held in registers (2,048 per row)
+
+// kWrap: the wrapper's observation() edits are compiled in (SPEC §13).
 // kNative: the nmmo-dtype layout of SPEC §8b (u8 masks, int16 fields, Market once per env,
 // task index) instead of pufferlib's float32 row: ~10x fewer bytes per agent.
 template <bool kWrap, bool kNative>
@@ -72,10 +165,9 @@ __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
   int16_t* rowslot = reinterpret_cast<int16_t*>(smem + (((size_t)kObsFields * S * 2 + 15) & ~(size_t)15));
   int16_t* vis_all = rowslot + ((((size_t)(S + 1) * 2 + 15) & ~(size_t)15) / 2);
   uint2* inv_all = reinterpret_cast<uint2*>(vis_all + kObsWaves * 128);
-  uint2* mitem = inv_all + kObsWaves * kInv;                       // flat: listed item words
-  int* mown = reinterpret_cast<int*>(mitem + NMMO_MARKET_ROWS);    // flat: listing owner slot
-  uint16_t* mpo = reinterpret_cast<uint16_t*>(inv_all + kObsWaves * kInv);  // native: price | owner << 8
-  uint8_t* wmat_all = reinterpret_cast<uint8_t*>(mpo + NMMO_MARKET_ROWS);   // native only
+  uint2* mitem = inv_all + kObsWaves * kInv;  // flat only: listed item words
+  uint16_t* mpo = reinterpret_cast<uint16_t*>(kNative ? mitem : mitem + NMMO_MARKET_ROWS);  // price | owner << 8
+  uint8_t* wmat_all = reinterpret_cast<uint8_t*>(mpo + NMMO_MARKET_ROWS);  // per-wave 15x15 materials
   const int e = blockIdx.x, g = blockIdx.y;
   const int tid = threadIdx.x;
   const int nm = p.mcount[e];
@@ -83,12 +175,8 @@ __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
     const int v = p.mlist[(size_t)e * NMMO_MARKET_ROWS + j];
     const int own = (v >> 16) & 255, slot = (v >> 24) & 15;
     const uint2 wd = p.items[((size_t)e * p.P + own) * kInv + slot];
-    if constexpr (kNative) {
-      mpo[j] = (uint16_t)(it_price(wd) | own << 8);
-    } else {
-      mown[j] = own;
-      mitem[j] = wd;
-    }
+    mpo[j] = (uint16_t)(it_price(wd) | own << 8);
+    if constexpr (!kNative) mitem[j] = wd;
   }
   {
     const int16_t* src = p.ent + (size_t)e * NMMO_NF * S;
@@ -128,39 +216,27 @@ __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
   }
   const int lane = lane_id(), w = wave_id();
   int16_t* vis = vis_all + w * 128;
-  uint8_t* wmat = wmat_all + w * 256;
+  uint2* inv = inv_all + w * kInv;
   const uint8_t* mat = p.mat + (size_t)e * kTiles;
   const int tick = p.env[(size_t)e * NMMO_NE + E_TICK];
-  const bool combat = (p.systems & NMMO_SYS_COMBAT) != 0;
-  const bool item = (p.systems & NMMO_SYS_ITEM) != 0;
-  const bool exch = item && (p.systems & NMMO_SYS_EXCHANGE) != 0;
-  uint2* inv = inv_all + w * kInv;
-  for (int i = w; i < kObsAgentsPerBlock; i += kObsWaves) {
-    const int a = g * kObsAgentsPerBlock + i;
-    if (a >= p.P) break;
-    float* row = kNative ? nullptr : p.obs + ((size_t)e * p.P + a) * p.elems;
-    uint8_t* nrow = kNative ? p.nat + (size_t)e * native_env_bytes(p.P) + (size_t)a * NMMO_NATIVE_ROW_BYTES : nullptr;
-    if (!T[F_ALIVE * S + a]) {
-      if constexpr (kNative) {
-        uint4* z = reinterpret_cast<uint4*>(nrow);
-        for (int j = lane; j < NMMO_NATIVE_ROW_BYTES / 16; j += 64) z[j] = make_uint4(0u, 0u, 0u, 0u);
-      } else {
-        wave_zero(row, 0, p.elems);
-      }
-      continue;
-    }
-    const int r = T[F_ROW * S + a], c = T[F_COL * S + a];
-    const int gold = T[F_GOLD * S + a];
-    if (lane < kInv) inv[lane] = p.items[((size_t)e * p.P + a) * kInv + lane];
-    uint32_t wm[4] = {0u, 0u, 0u, 0u};  // native: the 15x15 window materials, tile lane + 64 i
-    if constexpr (kNative) {
-#pragma unroll
-      for (int i = 0; i < 4; i++) {
-        const int t = lane + 64 * i;
-        if (t < 225) wm[i] = mat[(r + t / 15 - kVision) * kSize + c + t % 15 - kVision];
-      }
-    }
-    // Entity.Query.window: ascending datastore rows within L-inf <= 7, first 100
+  MaskCtx m;
+  m.combat = (p.systems & NMMO_SYS_COMBAT) != 0;
+  m.item = (p.systems & NMMO_SYS_ITEM) != 0;
+  m.exch = m.item && (p.systems & NMMO_SYS_EXCHANGE) != 0;
+  m.no_give = kWrap && (p.wflags & kWrapObsNoGive);
+  // this wave's agents: a_j = g * 16 + w + 4 j; lane j holds a_j's task index and (wrapper) last
+  // Sell price, loaded before any store
+  constexpr int kPerWave = kObsAgentsPerBlock / kObsWaves;
+  const int abase = g * kObsAgentsPerBlock + w;
+  int my_task = 0, my_prev = -1;
+  if (lane < kPerWave && abase + kObsWaves * lane < p.P) {
+    const size_t ai = (size_t)e * p.P + abase + kObsWaves * lane;
+    my_task = p.assign[ai];
+    if constexpr (kWrap)
+      if (p.ws) my_prev = p.ws[ai].prev_price;
+  }
+  // Entity.Query.window: ascending datastore rows within L-inf <= 7, first 100 -> vis, returns nv
+  auto compact = [&](int r, int c) {
     int nv = 0;
     for (int base = 1; base <= S; base += 64) {
       const int k = base + lane;
@@ -175,226 +251,221 @@ __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
       if (v && pos < kNObs) vis[pos] = (int16_t)q;
       nv += __popcll(b);
     }
-    nv = min(nv, kNObs);
-    if constexpr (kNative) {
+    return min(nv, kNObs);
+  };
+  // the agent's global loads: 12 item words (lanes 0..11), the 15x15 window materials (tile
+  // lane + 64 i in wm[i]) and, for flat rows, the first kTaskRegs * 64 Task embedding floats
+  uint2 iv;
+  uint32_t wm[4];
+  float tv[kTaskRegs];
+  const bool treg = p.task_dim >= kTaskRegs * 64;  // the first kTaskRegs * 64 Task floats prefetched
+  uint8_t* wmat = wmat_all + w * 256;
+  auto prefetch = [&](int a, int j) {
+    const int r = T[F_ROW * S + a], c = T[F_COL * S + a];
+    iv = lane < kInv ? p.items[((size_t)e * p.P + a) * kInv + lane] : make_uint2(0u, 0u);
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const int t = lane + 64 * i;
+      wm[i] = t < 225 ? mat[(r + t / 15 - kVision) * kSize + c + t % 15 - kVision] : 0u;
+    }
+    if constexpr (!kNative) {
+      if (treg) {
+        const float* temb = p.task + (size_t)__builtin_amdgcn_readlane(my_task, j) * p.task_dim + lane;
+#pragma unroll
+        for (int i = 0; i < kTaskRegs; i++) tv[i] = temb[64 * i];
+      }
+    }
+  };
+  auto alive = [&](int j) {
+    const int a = abase + kObsWaves * j;
+    return j < kPerWave && a < p.P && T[F_ALIVE * S + a] != 0;
+  };
+  if (alive(0)) prefetch(abase, 0);
+
+  if constexpr (!kNative) {
+    for (int j = 0; j < kPerWave; j++) {
+      const int a = abase + kObsWaves * j;
+      if (a >= p.P) break;
+      float* row = p.obs + ((size_t)e * p.P + a) * p.elems;
+      if (!T[F_ALIVE * S + a]) {
+        if (alive(j + 1)) prefetch(a + kObsWaves, j + 1);  // ahead of this row's stores
+        wave_zero(row, 0, p.elems);
+        continue;
+      }
+      m.a = a;
+      m.r = T[F_ROW * S + a];
+      m.c = T[F_COL * S + a];
+      m.gold = T[F_GOLD * S + a];
+      m.nv = compact(m.r, m.c);
+      if (lane < kInv) inv[lane] = iv;
 #pragma unroll
       for (int i = 0; i < 4; i++)
         if (lane + 64 * i < 225) wmat[lane + 64 * i] = (uint8_t)wm[i];
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      m.ninv = inv_count(inv);
+      m.prev_price = kWrap ? __builtin_amdgcn_readlane(my_prev, j) : -1;
+      m.movebits = move_bits(wm[1]);
+      const int aid = T[F_ID * S + a];
+      // Task (from registers; a task_dim beyond kTaskRegs * 64 reads the rest directly)
+      {
+        const int k0 = treg ? kTaskRegs * 64 : 0;  // a shorter embedding is read in place
+        if (treg) {
+          float* dst = row + p.o_task + lane;
+#pragma unroll
+          for (int i = 0; i < kTaskRegs; i++) obs_st(&dst[64 * i], tv[i]);
+        }
+        const float* temb = p.task + (size_t)__builtin_amdgcn_readlane(my_task, j) * p.task_dim;
+        for (int k = k0 + lane; k < p.task_dim; k += 64) obs_st(&row[p.o_task + k], temb[k]);
+      }
+      // Tile (the window materials went to LDS with the inventory)
+      for (int k = lane; k < 225 * 3; k += 64) {
+        const int t = k / 3, comp = k - 3 * t;
+        const int tr = m.r + t / 15 - kVision, tc = m.c + t % 15 - kVision;
+        obs_st(&row[p.o_tile + k], comp == 0 ? (float)tr : comp == 1 ? (float)tc : (float)wmat[t]);
+      }
+      // the next agent's loads go out now, ahead of this row's remaining stores
+      if (alive(j + 1)) prefetch(a + kObsWaves, j + 1);
+      // ActionTargets: one uniform loop over (section, 64-entry chunk)
+      {
+        int sec = 0, k0 = 0;
+#pragma unroll 1
+        while (sec < 12) {
+          int lo, n;
+          mask_section(p, sec, lo, n);
+          const int k = k0 + lane;
+          if (k < n)
+            obs_st(&row[lo + k], mask_value<kWrap>(p, T, S, vis, inv, mpo, nm, m, sec, k) ? 1.f : 0.f);
+          k0 += 64;
+          if (k0 >= n) {
+            sec++;
+            k0 = 0;
+          }
+        }
+      }
+      if (lane == 0) obs_st(&row[p.o_agent_id], (float)aid);
+      if (lane == 1) obs_st(&row[p.o_tick], (float)tick);
+      // Entity rows: two per pass (lanes 0-30 row k, lanes 32-62 row k + 1: 62 contiguous floats),
+      // the rows past the visible ones as one zero run
+      {
+        const int f = lane & 31, half = lane >> 5;
+        const int nv2 = (m.nv + 1) & ~1;
+#pragma unroll 1
+        for (int k0 = 0; k0 < nv2; k0 += 2) {
+          const int k = k0 + half;
+          if (f < NMMO_N_ENTITY_COLS)
+            obs_st(&row[p.o_entity + k * NMMO_N_ENTITY_COLS + f], k < m.nv ? (float)T[f * S + vis[k]] : 0.f);
+        }
+        wave_zero(row, p.o_entity + nv2 * NMMO_N_ENTITY_COLS, p.o_entity + kNObs * NMMO_N_ENTITY_COLS);
+      }
+      // Inventory (own items, owner = self) and Market (env listings, ascending row)
+      for (int k = lane; k < kInv * 16; k += 64) {
+        const int q = k >> 4;
+        obs_st(&row[p.o_inventory + k], q < m.ninv ? item_col(inv[q], aid, k & 15) : 0.f);
+      }
+      for (int k = lane; k < nm * 16; k += 64)
+        obs_st(&row[p.o_market + k], item_col(mitem[k >> 4], (mpo[k >> 4] >> 8) + 1, k & 15));
+      wave_zero(row, p.o_market + nm * 16, p.o_task);
+      __builtin_amdgcn_wave_barrier();
     }
+    return;
+  }
+
+  for (int j = 0; j < kPerWave; j++) {
+    const int a = abase + kObsWaves * j;
+    if (a >= p.P) break;
+    uint8_t* nrow = p.nat + (size_t)e * native_env_bytes(p.P) + (size_t)a * NMMO_NATIVE_ROW_BYTES;
+    if (!T[F_ALIVE * S + a]) {
+      if (alive(j + 1)) prefetch(a + kObsWaves, j + 1);
+      uint4* z = reinterpret_cast<uint4*>(nrow);
+      for (int i = lane; i < NMMO_NATIVE_ROW_BYTES / 16; i += 64) z[i] = make_uint4(0u, 0u, 0u, 0u);
+      continue;
+    }
+    m.a = a;
+    m.r = T[F_ROW * S + a];
+    m.c = T[F_COL * S + a];
+    m.gold = T[F_GOLD * S + a];
+    m.nv = compact(m.r, m.c);
+    if (lane < kInv) inv[lane] = iv;
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+      if (lane + 64 * i < 225) wmat[lane + 64 * i] = (uint8_t)wm[i];
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-
-    const int ninv = inv_count(inv);
-    const int prev_price = kWrap && p.ws ? __builtin_amdgcn_readfirstlane(p.ws[(size_t)e * p.P + a].prev_price) : -1;
+    m.ninv = inv_count(inv);
+    m.prev_price = kWrap ? __builtin_amdgcn_readlane(my_prev, j) : -1;
+    m.movebits = move_bits(wm[1]);
     const int aid = T[F_ID * S + a];
-    // ActionTargets [0, o_agent_id) (SPEC §8, §9)
-    auto mask_val = [&](int j) -> bool {
-      bool v = false;
-      if (j < p.o_target) {
-        v = combat;
-      } else if (j < p.o_buy) {
-        const int k = j - p.o_target;
-        if (k == kNObs) v = true;
-        else if (combat && k < nv) {
-          const int q = vis[k];
-          v = q != a && linf(r, c, T[F_ROW * S + q], T[F_COL * S + q]) <= 3 &&
-              !(q < p.P && T[F_TIME_ALIVE * S + q] < p.spawn_immunity);
-        }
-      } else if (j < p.o_destroy) {
-        const int k = j - p.o_buy;
-        v = k == NMMO_MARKET_ROWS || (exch && k < nm && it_price(mitem[k]) <= gold && mown[k] != a);
-      } else if (j < p.o_give_target) {  // Destroy.InventoryItem, Give.InventoryItem
-        const int k = j < p.o_give_item ? j - p.o_destroy : j - p.o_give_item;
-        v = k == kInv || (item && k < ninv && !it_equipped(inv[k]) && !it_price(inv[k]));
-      } else if (j < p.o_gg_price || (j >= p.o_gg_target && j < p.o_move)) {  // Give/GiveGold.Target
-        const bool on = j < p.o_gg_price ? item : exch;
-        const int k = j < p.o_gg_price ? j - p.o_give_target : j - p.o_gg_target;
-        if (k == kNObs) v = true;
-        else if (on && k < nv) {
-          const int q = vis[k];
-          v = q < p.P && q != a && T[F_ROW * S + q] == r && T[F_COL * S + q] == c;
-        }
-      } else if (j < p.o_gg_target) {
-        v = exch && j - p.o_gg_price < gold;
-      } else if (j < p.o_sell_item) {
-        const int d = j - p.o_move;
-        v = !impassable(mat[(r + dir_dr(d)) * kSize + c + dir_dc(d)]);
-      } else if (j < p.o_sell_price) {
-        const int k = j - p.o_sell_item;
-        v = k == kInv || (exch && k < ninv && !it_equipped(inv[k]));
-      } else if (j < p.o_use) {
-        v = exch;
-      } else {
-        const int k = j - p.o_use;
-        v = k == kInv || (item && k < ninv && item_usable(T, S, a, inv[k]));
-      }
-      if constexpr (kWrap) {  // wrapper observation() edits (SPEC §13)
-        if ((p.wflags & kWrapObsPrice) && j >= p.o_sell_price && j < p.o_use && j - p.o_sell_price == prev_price)
-          v = false;
-        if ((p.wflags & kWrapObsNoGive) && j >= p.o_give_item && j < p.o_move) {
-          const bool keep = j == p.o_give_target - 1 || j == p.o_gg_price - 1 || j == p.o_gg_price ||
-                            j == p.o_move - 1;  // Give.InventoryItem/Target noop, Price 0, GiveGold noop
-          if (!keep) v = false;
-        }
-        if ((p.wflags & kWrapObsNoDangerous) && j >= p.o_target && j < p.o_buy) {
-          const int k = j - p.o_target;
-          if (k < nv && T[F_NPC_TYPE * S + vis[k]] > 1) v = false;
-        }
-      }
-      return v;
-    };
-    if constexpr (kNative) {
-      // Section by section (no per-element section dispatch): every lane of a store works on the
-      // same section, the window materials were prefetched into registers ahead of the
-      // visibility compaction, and nothing below waits on global memory.
-      uint8_t* mb = nrow;  // u8 ActionTargets in flat order, then pad to NMMO_NATIVE_MASK_BYTES
-      const bool no_give = kWrap && (p.wflags & kWrapObsNoGive);
-      auto free_item = [&](int k) { return k < ninv && !it_equipped(inv[k]) && !it_price(inv[k]); };
-      auto same_tile = [&](int k) {
-        const int q = vis[k];
-        return q < p.P && q != a && T[F_ROW * S + q] == r && T[F_COL * S + q] == c;
-      };
-      // Buy.MarketItem (1,025 entries, the longest section): four entries per lane per dword store
-      // from one 8-B LDS read of the packed listings (the section starts dword-aligned in the
-      // SPEC §8b layout; the per-byte case below covers any other offset)
-      const bool buy4 = (p.o_buy & 3) == 0;
-      if (buy4) {
-        uint32_t* b32 = reinterpret_cast<uint32_t*>(mb + p.o_buy);
-        for (int j4 = lane; j4 < NMMO_MARKET_ROWS / 4; j4 += 64) {
-          uint32_t v = 0u;
-          if (exch && 4 * j4 < nm) {
-            const uint2 q = *reinterpret_cast<const uint2*>(mpo + 4 * j4);
+    if (alive(j + 1)) prefetch(a + kObsWaves, j + 1);  // wm is in LDS now; next agent's loads
+    // u8 ActionTargets in flat order, then pad to NMMO_NATIVE_MASK_BYTES. Buy.MarketItem (1,025
+    // entries, the longest section): four entries per lane per dword store from one 8-B LDS read
+    // of the packed listings (the section starts dword-aligned in the SPEC §8b layout; the
+    // per-byte case of mask_value covers any other offset)
+    uint8_t* mb = nrow;
+    const bool buy4 = (p.o_buy & 3) == 0;
+    if (buy4) {
+      uint32_t* b32 = reinterpret_cast<uint32_t*>(mb + p.o_buy);
+      for (int j4 = lane; j4 < NMMO_MARKET_ROWS / 4; j4 += 64) {
+        uint32_t v = 0u;
+        if (m.exch && 4 * j4 < nm) {
+          const uint2 q = *reinterpret_cast<const uint2*>(mpo + 4 * j4);
 #pragma unroll
-            for (int b = 0; b < 4; b++) {
-              const uint32_t pw = ((b < 2 ? q.x : q.y) >> (16 * (b & 1))) & 0xFFFFu;
-              if (4 * j4 + b < nm && (int)(pw & 255u) <= gold && (int)(pw >> 8) != a) v |= 1u << (8 * b);
-            }
+          for (int b = 0; b < 4; b++) {
+            const uint32_t pw = ((b < 2 ? q.x : q.y) >> (16 * (b & 1))) & 0xFFFFu;
+            if (4 * j4 + b < nm && (int)(pw & 255u) <= m.gold && (int)(pw >> 8) != a) v |= 1u << (8 * b);
           }
-          b32[j4] = v;
         }
-        if (lane == 0) mb[p.o_buy + NMMO_MARKET_ROWS] = 1;
+        b32[j4] = v;
       }
-      // one uniform loop over (section, 64-entry chunk): the section is a scalar, so its case runs
-      // without divergence and only its own operands are live
+      if (lane == 0) mb[p.o_buy + NMMO_MARKET_ROWS] = 1;
+    }
+    {
       int sec = 0, k0 = 0;
 #pragma unroll 1
       while (sec < 12) {
         int lo, n;
-        switch (sec) {
-          case 0: lo = p.o_style; n = p.o_target - p.o_style; break;
-          case 1: lo = p.o_target; n = kNObs + 1; break;
-          case 2: lo = p.o_buy; n = buy4 ? 0 : NMMO_MARKET_ROWS + 1; break;
-          case 3: lo = p.o_destroy; n = kInv + 1; break;
-          case 4: lo = p.o_give_item; n = kInv + 1; break;
-          case 5: lo = p.o_give_target; n = kNObs + 1; break;
-          case 6: lo = p.o_gg_price; n = p.o_gg_target - p.o_gg_price; break;
-          case 7: lo = p.o_gg_target; n = kNObs + 1; break;
-          case 8: lo = p.o_move; n = p.o_sell_item - p.o_move; break;
-          case 9: lo = p.o_sell_item; n = kInv + 1; break;
-          case 10: lo = p.o_sell_price; n = p.o_use - p.o_sell_price; break;
-          default: lo = p.o_use; n = p.o_agent_id - p.o_use; break;
-        }
+        mask_section(p, sec, lo, n);
+        if (sec == 2 && buy4) n = 0;
         const int k = k0 + lane;
-        if (k < n) {
-          bool v;
-          switch (sec) {
-            case 0: v = combat; break;
-            case 1:
-              if (k == kNObs) {
-                v = true;
-              } else if (!combat || k >= nv) {
-                v = false;
-              } else {
-                const int q = vis[k];
-                v = q != a && linf(r, c, T[F_ROW * S + q], T[F_COL * S + q]) <= 3 &&
-                    !(q < p.P && T[F_TIME_ALIVE * S + q] < p.spawn_immunity);
-                if constexpr (kWrap)
-                  if ((p.wflags & kWrapObsNoDangerous) && T[F_NPC_TYPE * S + q] > 1) v = false;
-              }
-              break;
-            case 2:
-              v = k == NMMO_MARKET_ROWS || (exch && k < nm && (int)(mpo[k] & 255u) <= gold && (int)(mpo[k] >> 8) != a);
-              break;
-            case 3: v = k == kInv || (item && free_item(k)); break;
-            case 4: v = k == kInv || (!no_give && item && free_item(k)); break;
-            case 5: v = k == kNObs || (!no_give && item && k < nv && same_tile(k)); break;
-            case 6: v = exch && k < gold && (!no_give || k == 0); break;
-            case 7: v = k == kNObs || (!no_give && exch && k < nv && same_tile(k)); break;
-            case 8: v = !impassable(wmat[(kVision + dir_dr(k)) * 15 + kVision + dir_dc(k)]); break;
-            case 9: v = k == kInv || (exch && k < ninv && !it_equipped(inv[k])); break;
-            case 10:
-              v = exch;
-              if constexpr (kWrap)
-                if ((p.wflags & kWrapObsPrice) && k == prev_price) v = false;
-              break;
-            default: v = k == kInv || (item && k < ninv && item_usable(T, S, a, inv[k])); break;
-          }
-          mb[lo + k] = v ? 1 : 0;
-        }
+        if (k < n) mb[lo + k] = mask_value<kWrap>(p, T, S, vis, inv, mpo, nm, m, sec, k) ? 1 : 0;
         k0 += 64;
         if (k0 >= n) {
           sec++;
           k0 = 0;
         }
       }
-      if (lane < NMMO_NATIVE_MASK_BYTES - p.o_agent_id) mb[p.o_agent_id + lane] = 0;
-      // int16 part: AgentId, CurrentTick, Entity 100x31, Inventory 12x16, Tile 225x3, task index,
-      // zero pads (SPEC §8b)
-      int16_t* d16 = reinterpret_cast<int16_t*>(nrow + NMMO_NATIVE_MASK_BYTES);
-      if (lane == 0) d16[0] = (int16_t)aid;
-      if (lane == 1) d16[1] = (int16_t)tick;
-      {  // two entity rows per pass: lanes 0-30 row k, lanes 32-62 row k + 1, one column each
-        const int f = lane & 31, half = lane >> 5;
+    }
+    if (lane < NMMO_NATIVE_MASK_BYTES - p.o_agent_id) mb[p.o_agent_id + lane] = 0;
+    // int16 part: AgentId, CurrentTick, Entity 100x31, Inventory 12x16, Tile 225x3, task index,
+    // zero pads (SPEC §8b)
+    int16_t* d16 = reinterpret_cast<int16_t*>(nrow + NMMO_NATIVE_MASK_BYTES);
+    if (lane == 0) d16[0] = (int16_t)aid;
+    if (lane == 1) d16[1] = (int16_t)tick;
+    {  // two entity rows per pass: lanes 0-30 row k, lanes 32-62 row k + 1, one column each
+      const int f = lane & 31, half = lane >> 5;
 #pragma unroll 1
-        for (int k0 = 0; k0 < kNObs; k0 += 2) {
-          const int k = k0 + half;
-          if (f < NMMO_N_ENTITY_COLS)
-            d16[kNatEntity + k * NMMO_N_ENTITY_COLS + f] = k < nv ? T[f * S + vis[k]] : (int16_t)0;
-        }
+      for (int k0 = 0; k0 < kNObs; k0 += 2) {
+        const int k = k0 + half;
+        if (f < NMMO_N_ENTITY_COLS)
+          d16[kNatEntity + k * NMMO_N_ENTITY_COLS + f] = k < m.nv ? T[f * S + vis[k]] : (int16_t)0;
       }
-      for (int j = lane; j < kInv * 16; j += 64) {
-        const int k = j >> 4;
-        d16[kNatInv + j] = k < ninv ? (int16_t)(int)item_col(inv[k], aid, j & 15) : (int16_t)0;
-      }
+    }
+    for (int k = lane; k < kInv * 16; k += 64) {
+      const int q = k >> 4;
+      d16[kNatInv + k] = q < m.ninv ? (int16_t)(int)item_col(inv[q], aid, k & 15) : (int16_t)0;
+    }
 #pragma unroll 1
-      for (int i = 0; i < 4; i++) {
-        const int t = lane + 64 * i;
-        if (t < 225) {
-          const int tr = r + t / 15 - kVision, tc = c + t % 15 - kVision;
-          d16[kNatTile + 3 * t] = (int16_t)tr;
-          d16[kNatTile + 3 * t + 1] = (int16_t)tc;
-          d16[kNatTile + 3 * t + 2] = (int16_t)wm[i];
-        }
+    for (int i = 0; i < 4; i++) {
+      const int t = lane + 64 * i;
+      if (t < 225) {
+        const int tr = m.r + t / 15 - kVision, tc = m.c + t % 15 - kVision;
+        d16[kNatTile + 3 * t] = (int16_t)tr;
+        d16[kNatTile + 3 * t + 1] = (int16_t)tc;
+        d16[kNatTile + 3 * t + 2] = (int16_t)wmat[t];
       }
-      if (lane == 0) d16[kNatTask] = (int16_t)p.assign[(size_t)e * p.P + a];
-      else if (lane < NMMO_NATIVE_I16 - kNatTask) d16[kNatTask + lane] = 0;
-      __builtin_amdgcn_wave_barrier();
-      continue;
     }
-    for (int j = lane; j < p.o_agent_id; j += 64) obs_st(&row[j], mask_val(j) ? 1.f : 0.f);
-    if (lane == 0) obs_st(&row[p.o_agent_id], (float)aid);
-    if (lane == 1) obs_st(&row[p.o_tick], (float)tick);
-    // Entity rows (31 columns each)
-    const int ne = kNObs * NMMO_N_ENTITY_COLS;
-    for (int j = lane; j < ne; j += 64) {
-      const int k = j / NMMO_N_ENTITY_COLS, f = j - k * NMMO_N_ENTITY_COLS;
-      obs_st(&row[p.o_entity + j], k < nv ? (float)T[f * S + vis[k]] : 0.f);
-    }
-    // Inventory (own items, owner = self) and Market (env listings, ascending row)
-    for (int j = lane; j < kInv * 16; j += 64) {
-      const int k = j >> 4;
-      obs_st(&row[p.o_inventory + j], k < ninv ? item_col(inv[k], aid, j & 15) : 0.f);
-    }
-    for (int j = lane; j < nm * 16; j += 64)
-      obs_st(&row[p.o_market + j], item_col(mitem[j >> 4], mown[j >> 4] + 1, j & 15));
-    wave_zero(row, p.o_market + nm * 16, p.o_task);
-    const float* temb = p.task + (size_t)p.assign[(size_t)e * p.P + a] * p.task_dim;  // this player's task
-    for (int j = lane; j < p.task_dim; j += 64) obs_st(&row[p.o_task + j], temb[j]);
-    for (int j = lane; j < 225 * 3; j += 64) {
-      const int t = j / 3, comp = j - 3 * t;
-      const int tr = r + t / 15 - kVision, tc = c + t % 15 - kVision;
-      obs_st(&row[p.o_tile + j], comp == 0 ? (float)tr : comp == 1 ? (float)tc : (float)mat[tr * kSize + tc]);
-    }
+    if (lane == 0) d16[kNatTask] = (int16_t)__builtin_amdgcn_readlane(my_task, j);
+    else if (lane < NMMO_NATIVE_I16 - kNatTask) d16[kNatTask + lane] = 0;
     __builtin_amdgcn_wave_barrier();
   }
 }

@@ -1,0 +1,113 @@
+// Diagnostic: HBM write rate of the store patterns an obs launch can use, over the C4 obs
+// buffer (1024 envs x 128 agents x 23,987 floats = 12.8 GB). Build + run on the GPU box:
+//   hipcc --offload-arch=gfx950 -O3 tools/fill_patterns.hip -o /tmp/fill && /tmp/fill
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdint>
+
+constexpr int kElems = 23987, kEnvs = 1024, kP = 128;
+
+__device__ inline void row_zero(float* row, int lo, int hi, int lane, int nl) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(row + lo);
+  int head = (int)(((16 - (a & 15)) & 15) >> 2);
+  if (head > hi - lo) head = hi - lo;
+  if (lane < head) row[lo + lane] = 0.f;
+  const int body = (hi - lo - head) >> 2;
+  float4* p4 = reinterpret_cast<float4*>(row + lo + head);
+  for (int i = lane; i < body; i += nl) p4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  const int tail0 = lo + head + body * 4;
+  if (tail0 + lane < hi) row[tail0 + lane] = 0.f;
+}
+
+// (a) grid-stride float4 fill of the whole buffer
+__global__ void fill_stride(float4* p, size_t n4) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x)
+    p[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+}
+// (b) the obs grid: (env, 16-agent group), 4 waves, one wave per row, rows w, w+4, w+8, w+12
+__global__ void __launch_bounds__(256) fill_row_per_wave(float* obs) {
+  const int e = blockIdx.x, g = blockIdx.y, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int i = w; i < 16; i += 4) row_zero(obs + ((size_t)e * kP + g * 16 + i) * kElems, 0, kElems, lane, 64);
+}
+// (c) same grid, the whole workgroup writes one row at a time
+__global__ void __launch_bounds__(256) fill_row_per_block(float* obs) {
+  const int e = blockIdx.x, g = blockIdx.y;
+  for (int i = 0; i < 16; i++) row_zero(obs + ((size_t)e * kP + g * 16 + i) * kElems, 0, kElems, threadIdx.x, 256);
+}
+// (d) one wave per row, rows w, w+4, ... but rows of a wave interleaved in 4-KB pieces: the
+// 4 waves of a block sweep the block's 16 rows piece by piece together
+__global__ void __launch_bounds__(256) fill_row_per_wave_dword(float* obs) {
+  const int e = blockIdx.x, g = blockIdx.y, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int i = w; i < 16; i += 4) {
+    float* row = obs + ((size_t)e * kP + g * 16 + i) * kElems;
+    for (int j = lane; j < kElems; j += 64) row[j] = 0.f;
+  }
+}
+// (e) one wave per row with 8 waves per block (2 rows each)
+__global__ void __launch_bounds__(512) fill_row_per_wave8(float* obs) {
+  const int e = blockIdx.x, g = blockIdx.y, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int i = w; i < 16; i += 8) row_zero(obs + ((size_t)e * kP + g * 16 + i) * kElems, 0, kElems, lane, 64);
+}
+
+// (f) one-shot blocks: 256 threads write 16 KB (4 float4 each, 4 KB per wave-instruction group) and exit
+__global__ void __launch_bounds__(256) fill_oneshot(float4* p, size_t n4) {
+  const size_t base = (size_t)blockIdx.x * 1024 + threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 4; i++)
+    if (base + 256 * i < n4) p[base + 256 * i] = make_float4(0.f, 0.f, 0.f, 0.f);
+}
+// (b') the obs rows with the group index fastest in dispatch order (blockIdx.x = group): resident
+// workgroups write adjacent 1.5-MB spans
+__global__ void __launch_bounds__(256) fill_row_per_wave_gmajor(float* obs) {
+  const int g = blockIdx.x, e = blockIdx.y, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int i = w; i < 16; i += 4) row_zero(obs + ((size_t)e * kP + g * 16 + i) * kElems, 0, kElems, lane, 64);
+}
+// (b'') as (b') with a 1-D grid walked in row order and 8 agents per workgroup (2 per wave)
+__global__ void __launch_bounds__(256) fill_row_per_wave_8(float* obs) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const size_t r0 = (size_t)blockIdx.x * 8;
+  for (int i = w; i < 8; i += 4) row_zero(obs + (r0 + i) * kElems, 0, kElems, lane, 64);
+}
+int main() {
+  const size_t n = (size_t)kEnvs * kP * kElems;
+  hipEvent_t t0, t1;
+  hipEventCreate(&t0);
+  hipEventCreate(&t1);
+  const dim3 grid(kEnvs, kP / 16);
+  auto timeit = [&](const char* name, auto launch) {
+    for (int i = 0; i < 3; i++) launch();
+    hipEventRecord(t0);
+    const int k = 10;
+    for (int i = 0; i < k; i++) launch();
+    hipEventRecord(t1);
+    hipEventSynchronize(t1);
+    float ms;
+    hipEventElapsedTime(&ms, t0, t1);
+    ms /= k;
+    printf("%-40s %.3f ms  %.2f TB/s\n", name, ms, n * 4 / (ms * 1e-3) / 1e12);
+  };
+  auto suite = [&](float* obs, const char* tag) {
+    printf("-- %s\n", tag);
+    timeit("stride float4 (8192x256)", [&] { fill_stride<<<8192, 256>>>((float4*)obs, n / 4); });
+    timeit("row per wave (4 waves)", [&] { fill_row_per_wave<<<grid, 256, 38800>>>(obs); });
+    timeit("row per wave, dword stores", [&] { fill_row_per_wave_dword<<<grid, 256, 38800>>>(obs); });
+    timeit("row per block", [&] { fill_row_per_block<<<grid, 256>>>(obs); });
+  };
+  float* bufs[12];
+  int nb = 0;
+  auto probe = [&](size_t bytes, const char* tag) {
+    float* q;
+    if (hipMalloc(&q, bytes) != hipSuccess) { printf("alloc failed\n"); return; }
+    bufs[nb++] = q;
+    printf("%s\n", tag);
+    timeit("  stride float4 (8192x256)", [&] { fill_stride<<<8192, 256>>>((float4*)q, n / 4); });
+    timeit("  one-shot 16-KB blocks", [&] { fill_oneshot<<<(unsigned)((n / 4 + 1023) / 1024), 256>>>((float4*)q, n / 4); });
+    timeit("  rows, grid (env, group)", [&] { fill_row_per_wave<<<grid, 256, 38800>>>(q); });
+    timeit("  rows, grid (group, env)", [&] { fill_row_per_wave_gmajor<<<dim3(kP / 16, kEnvs), 256, 38800>>>(q); });
+    timeit("  rows, 1-D, 8 per block", [&] { fill_row_per_wave_8<<<kEnvs * kP / 8, 256, 19400>>>(q); });
+  };
+  for (int i = 0; i < 4; i++) probe(n * 4, "allocation");
+  for (int i = 0; i < nb; i++) hipFree(bufs[i]);
+  return 0;
+}
