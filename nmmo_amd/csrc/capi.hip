@@ -538,6 +538,16 @@ int nmmo_set_state(NmmoHandle* h, const void* host_buf, size_t nbytes) {
   }
   for (int32_t a : assign)
     if (a < 0 || a >= h->st.n_tasks) return fail(NMMO_E_INVALID, "state blob: task index %d outside the task table", a);
+  if (slim_systems(h->st.cfg.systems)) {  // the tick keeps these fields in HBM as reset wrote them
+    for (size_t e = 0; e < n; e++)
+      for (int f = 0; f < NMMO_NF_USED; f++)
+        for (size_t sl = 0; !slim_staged(f) && sl < S; sl++)
+          if (ent[(e * NMMO_NF + f) * S + sl] != slim_const(f, sl < P))
+            return fail(NMMO_E_INVALID,
+                        "state blob: env %zu slot %zu field %d = %d, but without the Item/Equipment/Profession/"
+                        "Exchange systems it must hold its reset value %d", e, sl, f,
+                        (int)ent[(e * NMMO_NF + f) * S + sl], slim_const(f, sl < P));
+  }
   HIP_TRY(hipSetDevice(h->device));
   HIP_TRY(hipDeviceSynchronize());
   HIP_TRY(hipMemcpy(h->d_env, env.data(), env.size() * 4, hipMemcpyHostToDevice));

@@ -5,6 +5,20 @@
 
 namespace nmmo {
 
+// Slim entity table (tick.hip): system sets whose tick never changes 15 of the entity fields
+constexpr int kSlimNF = 30;
+__host__ __device__ constexpr bool slim_systems(uint32_t sy) {
+  return (sy & (NMMO_SYS_ITEM | NMMO_SYS_EQUIPMENT | NMMO_SYS_PROFESSION | NMMO_SYS_EXCHANGE)) == 0;
+}
+__host__ __device__ constexpr bool slim_staged(int f) {
+  return f != F_ITEM_LEVEL && f != F_MESSAGE && f != F_GOLD && !(f >= F_FISHING_LEVEL && f <= F_ALCHEMY_EXP) &&
+         f != F_EQUIP_OFFENSE && f != F_EQUIP_DEFENSE;
+}
+// value of an unstaged field (slim only): profession levels are 1 for players, all else 0
+__host__ __device__ constexpr int slim_const(int f, bool player) {
+  return player && f >= F_FISHING_LEVEL && f <= F_ALCHEMY_EXP && ((f - F_FISHING_LEVEL) & 1) == 0 ? 1 : 0;
+}
+
 struct DevState {
   int32_t* env;          // [n][NMMO_NE]
   int16_t* ent;          // [n][NMMO_NF][S]

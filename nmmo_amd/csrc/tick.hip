@@ -27,7 +27,8 @@
 namespace nmmo {
 
 struct Ctx {
-  int16_t* T;        // [kNFLive][S]
+  int16_t* T;        // [nf][S] staged entity fields (all kNFLive, or the slim set: ent_row)
+  int16_t* ent_g;    // global, this env's [NMMO_NF][S] entity table (slim reset writes)
   uint64_t* vism;    // [P][NW] visibility bitmap: bit j of word w = row 64w+j+1 visible to player
   int* gstart;       // [kGridCells+1] grid cell -> first glist index (after vism, union region)
   uint32_t* glist;   // [S] in-realm entities by cell: slot<<25 (players) | (ds_row-1)<<16 | r<<8 | c
@@ -79,11 +80,26 @@ struct Ctx {
   int evcap, tick1;  // ring rows (0 = no event log); tick + 1 (the events' tick column)
   int S, P, N, IC;
   bool items, exch, prof, equip;
+  bool slim;         // no Item/Equipment/Profession/Exchange: the fields only they change stay in HBM
+  int nf;            // staged entity fields (LDS rows of T)
   const NmmoConfig* cfg;
   uint32_t sysm;     // enabled systems: a compile-time constant in the specialised kernels
 };
 
-#define TF(f, s) c.T[(f) * c.S + (s)]
+// Slim entity table (system sets without Item, Equipment, Profession and Exchange, e.g. BASELINE
+// config 3): the 15 fields only those systems change -- ITEM_LEVEL, MESSAGE, GOLD, the 10
+// profession levels/exps and the NPC equipment pair -- hold per-kind constants for the whole
+// episode (players: profession levels 1, the rest 0; NPCs: 0), written to HBM at reset and never
+// staged. The other 30 fields keep their order in 30 LDS rows: 45 -> 30 x S x 2 B of LDS
+// (C3: 34.6 -> 23.0 KB, so 4 workgroups fit a CU instead of 3).
+// LDS row of a staged field: its index minus the unstaged fields below it
+__host__ __device__ constexpr int slim_row(int f) {
+  return f - (f > F_ITEM_LEVEL) - (f > F_MESSAGE) - (f > F_GOLD) - (f > F_ALCHEMY_EXP ? 10 : 0) -
+         (f > F_EQUIP_DEFENSE ? 2 : 0);
+}
+static_assert(slim_row(F_DROP_TOOL) == kSlimNF - 1, "slim rows");
+__device__ __forceinline__ int ent_row(bool slim, int f) { return slim ? slim_row(f) : f; }
+#define TF(f, s) c.T[ent_row(c.slim, (f)) * c.S + (s)]
 
 // Diagnostic build only (-DNMMO_STAMPS, tools/stamps.py): thread 0 stamps the shader clock right
 // after phase barriers; never compiled into the product library.
@@ -101,6 +117,14 @@ __device__ unsigned long long g_stamps[4096 * 32];
 #endif
 
 __device__ __forceinline__ bool sys(const Ctx& c, uint32_t b) { return (c.sysm & b) != 0; }
+// field of LDS row `row` of T (the inverse of ent_row)
+__device__ __forceinline__ int row_field(bool slim, int row) {
+  return slim ? row + (row >= 7) + 2 * (row >= 9) + 10 * (row >= 18) + 2 * (row >= 25) : row;
+}
+// read of any field, staged or not (the slim constants for the unstaged ones)
+__device__ __forceinline__ int ent_get(const Ctx& c, int f, int s) {
+  return c.slim && !slim_staged(f) ? slim_const(f, s < c.P) : (int)TF(f, s);
+}
 // the wave-total buffer for the next block prefix (alternates; see block_prefix_sum)
 __device__ __forceinline__ int* wtot_next(Ctx& c) {
   c.wsel ^= 8;
@@ -133,12 +157,12 @@ __host__ __device__ inline size_t union_lds_bytes(int S, bool grid) {
   return u > atk ? u : atk;
 }
 
-__host__ __device__ inline size_t tick_lds_bytes(int S, int P, bool items, bool tev, bool grid) {
+__host__ __device__ inline size_t tick_lds_bytes(int S, int P, bool items, bool tev, bool grid, bool slim) {
   auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
   // task state is staged in LDS only when events feed its accumulators (else read in place)
   size_t b = (items ? item_lds_bytes(P) : 0) + kPlayerArrBytes +
              (tev ? 128 * 2 * 16 + al((size_t)P * sizeof(NmmoTaskState)) : 0);
-  b += al((size_t)kNFLive * S * 2);  // T
+  b += al((size_t)(slim ? kSlimNF : kNFLive) * S * 2);  // T
   b += union_lds_bytes(S, grid);     // vism + grid | hkey,hmin | ft,clist
   b += al((size_t)(S + 1) * 2);      // rslot
   b += 128 * 4;                      // pp
@@ -198,7 +222,10 @@ __device__ __forceinline__ Ctx make_ctx(unsigned char* smem, const DevState& st,
   c.ev_dmg = reinterpret_cast<int16_t*>(smem + o); o += 256;
   c.ev_lvl = reinterpret_cast<int16_t*>(smem + o); o += 256;
   c.fired = smem + o; o += 128;
-  c.T = reinterpret_cast<int16_t*>(smem + o); o += al((size_t)kNFLive * S * 2);
+  c.slim = slim_systems(sy);
+  c.nf = c.slim ? kSlimNF : kNFLive;
+  c.T = reinterpret_cast<int16_t*>(smem + o); o += al((size_t)c.nf * S * 2);
+  c.ent_g = st.ent + (size_t)e * NMMO_NF * S;
   {  // the union region (see union_lds_bytes)
     unsigned char* u = smem + o;
     c.vism = reinterpret_cast<uint64_t*>(u);
@@ -239,20 +266,27 @@ __device__ __forceinline__ Ctx make_ctx(unsigned char* smem, const DevState& st,
 }
 
 // ---------------------------------------------------------------- load / store
-// HBM -> LDS copy of up to 5 segments of 16-byte words as one flat index space, 8 loads in
+// HBM -> LDS copy of up to 6 segments of 16-byte words as one flat index space, 8 loads in
 // flight per thread before their LDS stores (a plain strided copy loop keeps one dependent
-// load in flight per iteration: the state load was a quarter of a C2 tick).
+// load in flight per iteration: the state load was a quarter of a C2 tick). Segment 0 is the
+// entity table; with `slim` its LDS rows are gathered from the staged fields' HBM rows
+// (w = 16-B words per field row).
 struct Seg16 {
   uint4* d;
   const uint4* s;
   int n;
 };
-__device__ __forceinline__ void copy_segs(const Seg16 (&sg)[6], int tid, int nt) {
+__device__ __forceinline__ void copy_segs(const Seg16 (&sg)[6], int tid, int nt, bool slim, int w) {
   // segment lookup by selects (a runtime index into sg[] would put the array in scratch)
   const int e0 = sg[0].n, e1 = e0 + sg[1].n, e2 = e1 + sg[2].n, e3 = e2 + sg[3].n, e4 = e3 + sg[4].n,
             total = e4 + sg[5].n;
+  auto src0 = [&](int i) -> const uint4* {
+    if (!slim) return sg[0].s + i;
+    const int row = i / w;
+    return sg[0].s + row_field(true, row) * w + (i - row * w);
+  };
   auto src = [&](int i) -> const uint4* {
-    return i < e0 ? sg[0].s + i
+    return i < e0 ? src0(i)
            : i < e1 ? sg[1].s + (i - e0)
            : i < e2 ? sg[2].s + (i - e1)
            : i < e3 ? sg[3].s + (i - e2)
@@ -295,28 +329,31 @@ __device__ __forceinline__ void load_env(Ctx& c, const DevState& st, int e) {
   const int tid = threadIdx.x, nt = blockDim.x, S = c.S;
   if (tid < NMMO_NE) c.E[tid] = st.env[(size_t)e * NMMO_NE + tid];
   const int16_t* src = st.ent + (size_t)e * NMMO_NF * S;
-  const int n16 = kNFLive * S;
   // every segment a whole number of 16-B words (task state: 40 B per player)
   const bool v16 = (S & 7) == 0 && (c.IC & 7) == 0 && (c.P & 1) == 0;
   NmmoTaskState* tsg = st.tstate + (size_t)e * c.P;
+  const uint4* ring4 = reinterpret_cast<const uint4*>(st.ring + (size_t)e * S);
+  const uint4* dep4 = reinterpret_cast<const uint4*>(st.dep + (size_t)e * kBitmapWords);
+  const int ntask = c.tev ? c.P * (int)sizeof(NmmoTaskState) / 16 : 0;
   if (v16) {
     Seg16 sg[6] = {
-        {reinterpret_cast<uint4*>(c.T), reinterpret_cast<const uint4*>(src), n16 / 8},
-        {reinterpret_cast<uint4*>(c.ring), reinterpret_cast<const uint4*>(st.ring + (size_t)e * S), S / 8},
-        {reinterpret_cast<uint4*>(c.dep), reinterpret_cast<const uint4*>(st.dep + (size_t)e * kBitmapWords),
-         kBitmapWords / 4},
+        {reinterpret_cast<uint4*>(c.T), reinterpret_cast<const uint4*>(src), c.nf * S / 8},
+        {reinterpret_cast<uint4*>(c.ring), ring4, S / 8},
+        {reinterpret_cast<uint4*>(c.dep), dep4, kBitmapWords / 4},
         {reinterpret_cast<uint4*>(c.inv), reinterpret_cast<const uint4*>(st.items + (size_t)e * c.P * kInv),
          c.items ? c.P * kInv / 2 : 0},
         {reinterpret_cast<uint4*>(c.iring), reinterpret_cast<const uint4*>(st.iring + (size_t)e * c.IC),
          c.items ? c.IC / 8 : 0},
-        {reinterpret_cast<uint4*>(c.tsl), reinterpret_cast<const uint4*>(tsg),
-         c.tev ? c.P * (int)sizeof(NmmoTaskState) / 16 : 0}};
-    copy_segs(sg, tid, nt);
+        {reinterpret_cast<uint4*>(c.tsl), reinterpret_cast<const uint4*>(tsg), ntask}};
+    copy_segs(sg, tid, nt, c.slim, S / 8);
     return;
   }
   for (int i = tid; i < (c.tev ? c.P * (int)sizeof(NmmoTaskState) / 4 : 0); i += nt)
     reinterpret_cast<int*>(c.tsl)[i] = reinterpret_cast<const int*>(tsg)[i];
-  for (int i = tid; i < n16; i += nt) c.T[i] = src[i];
+  for (int i = tid; i < c.nf * S; i += nt) {  // field by field (slim: staged fields only)
+    const int row = i / S;
+    c.T[i] = src[row_field(c.slim, row) * S + i - row * S];
+  }
   for (int i = tid; i < S; i += nt) c.ring[i] = st.ring[(size_t)e * S + i];
   for (int i = tid; i < kBitmapWords; i += nt) c.dep[i] = st.dep[(size_t)e * kBitmapWords + i];
   if (c.items) {
@@ -331,13 +368,19 @@ __device__ __forceinline__ void store_env(const Ctx& c, const DevState& st, int 
   const int tid = threadIdx.x, nt = blockDim.x, S = c.S;
   if (tid < NMMO_NE) st.env[(size_t)e * NMMO_NE + tid] = c.E[tid];
   int16_t* dst = st.ent + (size_t)e * NMMO_NF * S;
-  const int n16 = kNFLive * S;
-  if ((S & 7) == 0) {
-    const uint4* s4 = reinterpret_cast<const uint4*>(c.T);
+  if ((S & 7) == 0) {  // 16-B words, field runs contiguous in both layouts
+    const int w = S / 8;
     uint4* d4 = reinterpret_cast<uint4*>(dst);
-    for (int i = tid; i < n16 / 8; i += nt) d4[i] = s4[i];
+    const uint4* s4 = reinterpret_cast<const uint4*>(c.T);
+    for (int i = tid; i < c.nf * w; i += nt) {
+      const int row = i / w;
+      d4[row_field(c.slim, row) * w + i - row * w] = s4[i];
+    }
   } else {
-    for (int i = tid; i < n16; i += nt) dst[i] = c.T[i];
+    for (int i = tid; i < c.nf * S; i += nt) {
+      const int row = i / S;
+      dst[row_field(c.slim, row) * S + i - row * S] = c.T[i];
+    }
   }
   for (int i = tid; i < S; i += nt) st.ring[(size_t)e * S + i] = c.ring[i];
   for (int i = tid; i < kBitmapWords; i += nt) st.dep[(size_t)e * kBitmapWords + i] = c.dep[i];
@@ -561,7 +604,7 @@ __device__ __forceinline__ void npc_spawn(Ctx& c, uint32_t tick) {
     const int nacc = min(__popcll(b), room);
     if (valid && rank < room) {
       const int s = c.P + cnt + rank;
-      for (int f = 0; f < kNFLive; f++) TF(f, s) = 0;
+      for (int row = 0; row < c.nf; row++) c.T[row * c.S + s] = 0;
       TF(F_ID, s) = (int16_t)(c.E[E_NPC_NEXT_ID] - rank);
       TF(F_NPC_TYPE, s) = (int16_t)type;
       TF(F_ROW, s) = (int16_t)r;
@@ -602,7 +645,15 @@ __device__ __forceinline__ void npc_spawn(Ctx& c, uint32_t tick) {
 // ---------------------------------------------------------------- reset (SPEC §4)
 __device__ __forceinline__ void reset_env(Ctx& c, uint64_t seed, int episode, int env_global) {
   const int tid = threadIdx.x, nt = blockDim.x, S = c.S, P = c.P;
-  for (int i = tid; i < kNFLive * S; i += nt) c.T[i] = 0;
+  for (int i = tid; i < c.nf * S; i += nt) c.T[i] = 0;
+  if (c.slim) {  // the unstaged fields' per-kind constants, straight to HBM (never change after)
+    for (int i = tid; i < (NMMO_NF_USED - kSlimNF) * S; i += nt) {
+      const int k = i / S, slot = i - k * S;
+      const int f = k == 0 ? F_ITEM_LEVEL : k == 1 ? F_MESSAGE : k == 2 ? F_GOLD
+                  : k < 13 ? F_FISHING_LEVEL + (k - 3) : F_EQUIP_OFFENSE + (k - 13);
+      c.ent_g[f * S + slot] = (int16_t)slim_const(f, slot < P);
+    }
+  }
   for (int i = tid; i < kBitmapWords; i += nt) c.dep[i] = 0;
   for (int i = tid; i < S; i += nt) c.ring[i] = i < c.N ? (int16_t)(P + 1 + i) : (int16_t)0;
   if (tid < NMMO_NE) c.E[tid] = 0;
@@ -641,7 +692,7 @@ __device__ __forceinline__ void reset_env(Ctx& c, uint64_t seed, int episode, in
     TF(F_FOOD, tid) = 100;
     TF(F_WATER, tid) = 100;
 #pragma unroll
-    for (int sk = 0; sk < 8; sk++) TF(F_MELEE_LEVEL + 2 * sk, tid) = 1;
+    for (int sk = 0; sk < (c.slim ? 3 : 8); sk++) TF(F_MELEE_LEVEL + 2 * sk, tid) = 1;
     TF(F_ALIVE, tid) = 1;
     TF(F_DS_ROW, tid) = (int16_t)(tid + 1);
     TF(F_RESILIENT, tid) = u < c.cfg->resilient_u32 ? 1 : 0;
@@ -775,7 +826,7 @@ __device__ __forceinline__ void npc_decide(Ctx& c, int n, int closest, uint32_t 
 
 // ---------------------------------------------------------------- combat (SPEC §5.3)
 __device__ __forceinline__ int combat_level(const Ctx& c, int s) {
-  const int nsk = s < c.P ? 8 : 3;
+  const int nsk = s < c.P && !c.slim ? 8 : 3;  // slim: profession levels are 1 <= melee level
   int l = 0;
   for (int k = 0; k < nsk; k++) l = max(l, (int)TF(F_MELEE_LEVEL + 2 * k, s));
   return l;
@@ -901,9 +952,9 @@ __device__ __forceinline__ double term_progress(const Ctx& c, int p, const NmmoT
     case PRED_DEFEAT_ENTITY: return per_d(acc[0], q.c);
     case PRED_EARN_GOLD: case PRED_SPEND_GOLD: return per_d(acc[0], q.a);
     case PRED_MAKE_PROFIT: return per_d(acc[0] - acc[1], q.a);
-    case PRED_HOARD_GOLD: return per_d(TF(F_GOLD, p), q.a);
-    case PRED_ATTAIN_SKILL: return sk >= 0 && TF(F_MELEE_LEVEL + 2 * sk, p) >= q.b ? 1.0 : 0.0;
-    case PRED_GAIN_EXPERIENCE: return sk >= 0 ? per_d(TF(F_MELEE_EXP + 2 * sk, p), q.b) : 0.0;
+    case PRED_HOARD_GOLD: return per_d(ent_get(c, F_GOLD, p), q.a);
+    case PRED_ATTAIN_SKILL: return sk >= 0 && ent_get(c, F_MELEE_LEVEL + 2 * sk, p) >= q.b ? 1.0 : 0.0;
+    case PRED_GAIN_EXPERIENCE: return sk >= 0 ? per_d(ent_get(c, F_MELEE_EXP + 2 * sk, p), q.b) : 0.0;
     case PRED_EQUIP_ITEM:
       for (int k = 0; inv && k < kInv && it_type(inv[k]); k++)
         if (it_equipped(inv[k]) && it_type(inv[k]) == q.a && it_level(inv[k]) >= q.b) return 1.0;
@@ -1623,16 +1674,19 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
     int16_t v[kNFLive];
     if (keep) {
 #pragma unroll
-      for (int f = 0; f < kNFLive; f++) v[f] = TF(f, s);
+      for (int row = 0; row < kNFLive; row++)
+        if (row < c.nf) v[row] = c.T[row * S + s];
     }
     __syncthreads();
     if (keep) {
 #pragma unroll
-      for (int f = 0; f < kNFLive; f++) TF(f, P + kpos) = v[f];
+      for (int row = 0; row < kNFLive; row++)
+        if (row < c.nf) c.T[row * S + P + kpos] = v[row];
     }
     if (s >= P + nkeep && inslot) {
 #pragma unroll
-      for (int f = 0; f < kNFLive; f++) TF(f, s) = 0;
+      for (int row = 0; row < kNFLive; row++)
+        if (row < c.nf) c.T[row * S + s] = 0;
     }
     if (tid == 0) c.E[E_NPC_COUNT] = nkeep;
   }
@@ -1796,9 +1850,9 @@ __device__ __forceinline__ void store_market(Ctx& c, const DevState& st, int e) 
 // kSys != 0: specialised for exactly that system set (launch_tick dispatches on
 // cfg.systems), so disabled systems compile out; kSys == 0 reads the set at run time.
 template <uint32_t kSys>
-__global__ void tick_kernel(DevState st, const int32_t* __restrict__ actions,
-                            const uint64_t* __restrict__ env_seeds, float* rew, uint8_t* term,
-                            uint8_t* trunc, uint8_t* mask, int mode) {
+__device__ __forceinline__ void tick_body(const DevState& st, const int32_t* __restrict__ actions,
+                                          const uint64_t* __restrict__ env_seeds, float* rew, uint8_t* term,
+                                          uint8_t* trunc, uint8_t* mask, int mode) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int e = blockIdx.x;
   NMMO_STAMP(0);
@@ -1855,6 +1909,21 @@ __global__ void tick_kernel(DevState st, const int32_t* __restrict__ actions,
   NMMO_STAMP(11);
 }
 
+template <uint32_t kSys>
+__global__ void tick_kernel(DevState st, const int32_t* __restrict__ actions,
+                            const uint64_t* __restrict__ env_seeds, float* rew, uint8_t* term,
+                            uint8_t* trunc, uint8_t* mask, int mode) {
+  tick_body<kSys>(st, actions, env_seeds, rew, term, trunc, mask, mode);
+}
+// The C3 specialisation at <= 64 VGPRs: a 6-wave workgroup puts 2 waves on two SIMDs, so 4
+// workgroups per CU (the 1,024 envs of C3 in one round on 256 CUs) need 8 wave slots there.
+template <uint32_t kSys>
+__global__ void __attribute__((amdgpu_waves_per_eu(8, 8)))
+tick_kernel_w8(DevState st, const int32_t* __restrict__ actions, const uint64_t* __restrict__ env_seeds,
+               float* rew, uint8_t* term, uint8_t* trunc, uint8_t* mask, int mode) {
+  tick_body<kSys>(st, actions, env_seeds, rew, term, trunc, mask, mode);
+}
+
 // system sets with a specialised tick kernel: BASELINE configs 2 and 3 (config 4 = all)
 constexpr uint32_t kSysC2 = NMMO_SYS_RESOURCE;
 constexpr uint32_t kSysC3 = NMMO_SYS_RESOURCE | NMMO_SYS_COMBAT | NMMO_SYS_NPC | NMMO_SYS_PROGRESSION;
@@ -1865,11 +1934,11 @@ hipError_t launch_tick(const DevState& st, const int32_t* actions, const uint64_
   // >= 4 waves so the block-wide loops (state copies, respawn draws) use all four SIMDs
   const int threads = max(((st.S + 63) / 64) * 64, 256);
   const size_t lds = tick_lds_bytes(st.S, st.P, (st.cfg.systems & NMMO_SYS_ITEM) != 0, st.tev != 0,
-                                    uses_grid(st.cfg.systems));
+                                    uses_grid(st.cfg.systems), slim_systems(st.cfg.systems));
   void (*k)(DevState, const int32_t*, const uint64_t*, float*, uint8_t*, uint8_t*, uint8_t*, int);
   switch (st.cfg.systems) {
     case kSysC2: k = tick_kernel<kSysC2>; break;
-    case kSysC3: k = tick_kernel<kSysC3>; break;
+    case kSysC3: k = tick_kernel_w8<kSysC3>; break;
     case NMMO_SYS_ALL: k = tick_kernel<NMMO_SYS_ALL>; break;
     default: k = tick_kernel<0>; break;
   }
@@ -1881,7 +1950,7 @@ hipError_t launch_tick(const DevState& st, const int32_t* actions, const uint64_
 hipError_t init_kernels() {
   // dynamic LDS may use what the kernel's static LDS leaves of 160 KB
   const void* ks[4] = {reinterpret_cast<const void*>(tick_kernel<kSysC2>),
-                       reinterpret_cast<const void*>(tick_kernel<kSysC3>),
+                       reinterpret_cast<const void*>(tick_kernel_w8<kSysC3>),
                        reinterpret_cast<const void*>(tick_kernel<NMMO_SYS_ALL>),
                        reinterpret_cast<const void*>(tick_kernel<0>)};
   for (const void* k : ks) {
