@@ -106,6 +106,27 @@ def test_set_state_roundtrip():
     _cmp_state(eng.get_state(), orc.get_state(), 3, eng.S, "after set_state")
 
 
+def test_set_state_rejects_changed_slim_fields():
+    """Without Item/Equipment/Profession/Exchange (C3) the tick keeps 15 entity fields in HBM as
+    reset wrote them (tick.hip slim table); a blob that changes one of them is refused."""
+    from nmmo_amd._native import NativeError
+
+    cfg = Config.preset("C3", MAP_N=4)
+    eng = _engine(cfg, 2, seed=3)
+    eng.reset()
+    blob = eng.get_state()
+    eng.set_state(blob)  # a state the engine produced is accepted
+    st = split_state(blob.copy(), 2, eng.S, 128)
+    per = blob.nbytes // 2
+    off = 16 * 4 + (abi.ENTITY_FIELDS.index("gold") * eng.S + 5) * 2  # env 0, player slot 5, gold
+    bad = blob.copy()
+    bad[off:off + 2] = np.array([7], np.int16).view(np.uint8)
+    assert split_state(bad, 2, eng.S, 128)["ent"][0, abi.ENTITY_FIELDS.index("gold"), 5] == 7
+    assert st["ent"].shape[1] >= 45 and per > off
+    with pytest.raises(NativeError):
+        eng.set_state(bad)
+
+
 class _EngineStepper:
     """HIP engine behind the golden-rollout driver (numpy in/out)."""
 

@@ -28,7 +28,8 @@ def _short(name):
     """'void nmmo::tick_kernel<15u>(nmmo::DevState, ...)' -> 'tick_kernel' (all system-set
     specialisations of a kernel are one entry: a bench run launches only one of them)."""
     name = name.split("(")[0].split("<")[0]
-    return name.split("::")[-1].strip()
+    name = name.split("::")[-1].strip()
+    return name[:-3] if name.endswith("_w8") else name  # occupancy variant of the same kernel
 
 
 def summarise(d):
