@@ -72,14 +72,15 @@ WRAPPER_KW = {"neurips23_start_kit": dict(heal_bonus_weight=0.03, explore_bonus_
 EVENT_ROW_BYTES = 9 * 4
 
 
-def tick_bytes_per_env(S: int, P: int, items: bool, events_per_env: float = 0.0) -> int:
+def tick_bytes_per_env(S: int, P: int, items: bool, events_per_env: float = 0.0, slim: bool = False) -> int:
     """Algorithmic HBM bytes of one tick of one env: the env state read and
-    written once (45 int16 entity fields x slots, free-row ring, depleted-tile bitmap, env
+    written once (the staged int16 entity fields x slots -- 45, or 30 for the slim system sets
+    without Item/Equipment/Profession/Exchange -- free-row ring, depleted-tile bitmap, env
     scalars; with the Item system the 12-slot inventories and the item-row ring), the actions
     read, the outputs written, the map tiles a player touches (own tile + 4 neighbours for
     harvest/drink, 1 move target) and the event-log rows appended (36 B each; measured mean
     per env-tick)."""
-    state = 45 * S * 2 + S * 2 + 800 * 4 + 16 * 4
+    state = (30 if slim else 45) * S * 2 + S * 2 + 800 * 4 + 16 * 4
     if items:
         state += P * 12 * 8 + 12 * P * 2
     return int(2 * state + P * 12 * 4 + P * (4 + 1 + 1 + 1) + P * 6 + events_per_env * EVENT_ROW_BYTES)
@@ -372,7 +373,8 @@ def measure(args, name, layout_name, envs, rank, world, dev, steps, warmup, dist
     S, P = eng.S, cfg.PLAYER_N
     tick_avg_ms = tick_ms / max(n_timed, 1)
     obs_avg_ms = obs_ms / max(n_timed, 1)
-    tick_b = tick_bytes_per_env(S, P, "Item" in cfg.systems, events_per_env_tick or 0.0) * envs
+    slim = not any(x in cfg.systems for x in ("Item", "Equipment", "Profession", "Exchange"))
+    tick_b = tick_bytes_per_env(S, P, "Item" in cfg.systems, events_per_env_tick or 0.0, slim) * envs
     obs_b = obs_bytes_per_env(S, P, eng.obs_elems, native) * envs if wl["obs"] else 0
     if wl["obs"] and obs_avg_ms > tick_avg_ms:
         kern, byts, ms = "obs_kernel", obs_b, obs_avg_ms
@@ -414,29 +416,70 @@ def measure(args, name, layout_name, envs, rank, world, dev, steps, warmup, dist
 
 
 def _gather_stepper(eng, cfg, envs, rank, world, dev, pseed, dist):
-    """C5's step: tick + obs into one of two obs buffers, then the learner gather of that
-    buffer on a side stream (point-to-point sends into rank 0 over xGMI, overlapped with the
-    next tick); the root uses its own shard in place (no self-copy). The obs and the packed
-    reward/term/trunc/mask of step t travel while step t+1 computes into the other buffer."""
+    """C5's step: tick + obs into one of two obs buffers, then the learner gather of that step's
+    observations and packed reward/term/trunc/mask into rank 0 (point-to-point sends over xGMI
+    on a side stream, one step behind the compute stream so they overlap the next tick). The
+    root uses its own shard in place (no self-copy). Native obs travel wire-encoded (SPEC §8c,
+    nmmo_wire_pack: ~1.3 KB per agent instead of 9,552 B) and the root decodes every peer's
+    buffer back into its native receive buffer (the learner's tensor); flat obs (`--obs flat`)
+    travel as they are."""
     import torch
 
+    from nmmo_amd import abi, wire
+    from nmmo_amd import distributed as nd
+
+    native = eng.config.obs_layout == abi.OBS_NATIVE
     bufs = [eng.obs, torch.empty_like(eng.obs)]
     smalls = [torch.empty((envs, cfg.PLAYER_N, 8), dtype=torch.uint8, device=dev) for _ in range(2)]
+    wires = [torch.empty(wire.max_bytes(envs, cfg.PLAYER_N), dtype=torch.uint8, device=dev)
+             for _ in range(2)] if native and world > 1 else None
+    hdr = wire.header_bytes(envs, cfg.PLAYER_N) if native else 0
     comm = torch.cuda.Stream(device=dev)
-    done_ev = [None, None]  # event on the compute stream after the buffer's sends finished
+    done_ev = [None, None]  # compute-stream wait: the exchange of the step that used this buffer
     recv = None
     if rank == 0 and world > 1:
-        recv = [[torch.empty_like(bufs[0]), torch.empty_like(smalls[0])] for _ in range(world - 1)]
+        recv = {r: {"obs": torch.empty_like(bufs[0]), "small": torch.empty_like(smalls[0]),
+                    "wire": torch.empty_like(wires[0]) if native else None} for r in range(1, world)}
 
     class Stepper:
         t = 0
-        bytes_per_step = (bufs[0].numel() * bufs[0].element_size() + smalls[0].numel()) * max(world - 1, 0)
+        pending = None  # (buffer index, ready event) of the step whose exchange is still to run
+        sent_bytes = 0
+        bytes_per_step = None
+
+        def _exchange(self, i, ready):
+            with torch.cuda.stream(comm):
+                comm.wait_event(ready)
+                if rank == 0:
+                    ops = [dist.P2POp(dist.irecv, recv[r]["small"], r) for r in recv]
+                    if native:
+                        got = nd.gather_wire_to_learner(wires[i], hdr,
+                                                        recv_bufs=[None] + [recv[r]["wire"] for r in recv])
+                        for r in recv:  # decode each peer's wire buffer into its native obs
+                            wire.unpack(got[r], envs, cfg.PLAYER_N, out=recv[r]["obs"])
+                            self.sent_bytes += got[r].numel()
+                    else:
+                        ops += [dist.P2POp(dist.irecv, recv[r]["obs"], r) for r in recv]
+                        self.sent_bytes += (world - 1) * bufs[i].numel() * bufs[i].element_size()
+                    for w in dist.batch_isend_irecv(ops):
+                        w.wait()
+                else:
+                    ops = [dist.P2POp(dist.isend, smalls[i], 0)]
+                    if native:
+                        nd.gather_wire_to_learner(wires[i], hdr)
+                    else:
+                        ops.append(dist.P2POp(dist.isend, bufs[i], 0))
+                    for w in dist.batch_isend_irecv(ops):
+                        w.wait()
+                ev = torch.cuda.Event()
+                ev.record(comm)
+            done_ev[i] = ev
 
         def __call__(self):
             i = self.t % 2
             cur = torch.cuda.current_stream(dev)
             if done_ev[i] is not None:
-                cur.wait_event(done_ev[i])  # the sends of step t-2 have read this buffer
+                cur.wait_event(done_ev[i])  # the exchange of step t-2 has read this buffer
             eng.obs = bufs[i]
             eng.scripted_actions(pseed)
             eng.step()
@@ -446,24 +489,22 @@ def _gather_stepper(eng, cfg, envs, rank, world, dev, pseed, dist):
             sm[..., 5] = eng.trunc
             sm[..., 6] = eng.mask
             if world > 1:
+                if native:
+                    wire.pack(eng, bufs[i], out=wires[i])
                 ready = torch.cuda.Event()
                 ready.record(cur)
-                with torch.cuda.stream(comm):
-                    comm.wait_event(ready)
-                    if rank == 0:
-                        ops = [dist.P2POp(dist.irecv, recv[r - 1][0], r) for r in range(1, world)]
-                        ops += [dist.P2POp(dist.irecv, recv[r - 1][1], r) for r in range(1, world)]
-                    else:
-                        ops = [dist.P2POp(dist.isend, bufs[i], 0), dist.P2POp(dist.isend, sm, 0)]
-                    for w in dist.batch_isend_irecv(ops):
-                        w.wait()
-                    ev = torch.cuda.Event()
-                    ev.record(comm)
-                done_ev[i] = ev
+                if self.pending is not None:  # step t-1's exchange, now that step t is queued
+                    self._exchange(*self.pending)
+                self.pending = (i, ready)
             self.t += 1
 
         def drain(self):
+            if self.pending is not None:
+                self._exchange(*self.pending)
+                self.pending = None
             torch.cuda.current_stream(dev).wait_stream(comm)
+            if world > 1 and self.t:
+                self.bytes_per_step = self.sent_bytes / self.t + (world - 1) * smalls[0].numel()
 
         def close(self):
             torch.cuda.synchronize(dev)
@@ -586,8 +627,14 @@ def main():
         }
         line.update(body)
         line["wrapper"] = None if args.wrapper == "none" else args.wrapper
-        line["gather"] = (f"RCCL point-to-point sends of {res['gather_bytes']} B/step into rank 0, "
-                          "double-buffered on a side stream" if res["gather"] else None)
+        if res["gather"]:
+            how = ("wire-encoded native obs (SPEC §8c), decoded on rank 0 into its native buffers"
+                   if res["native"] else "flat obs")
+            line["gather"] = (f"RCCL point-to-point sends into rank 0 of {res['gather_bytes']} B/step "
+                              f"({how}) + reward/dones/mask, one step behind on a side stream"
+                              if res["gather_bytes"] else "N = 1: rank 0's own shard in place, nothing sent")
+        else:
+            line["gather"] = None
         line["cpu_baseline"] = cpu
         line["extra_configs"] = extras or None
         line["build"] = _native.build_info()

@@ -329,6 +329,30 @@ NMMO_API int nmmo_get_wrapper_dropped(NmmoHandle* h, int64_t* total);
  * of consecutive envs (e.g. a learner expanding gathered shards). Enqueued on `stream`. */
 NMMO_API int nmmo_expand_obs(NmmoHandle* h, const void* native, float* flat, int32_t n_envs, void* stream);
 
+/* ---- Wire encoding of native observations (SPEC.md §8c) ----
+ * For moving observations between GPUs (the learner gather of BASELINE config 5): the native
+ * layout without its padding. A wire buffer of n_envs x player_n agents is
+ *   header: int64 total bytes | int64 env payload offset [n_envs] | u16 agent count word
+ *           [n_envs][player_n] (bit 15 in the realm, bits 0-6 visible entities, 7-10 items) |
+ *           u16 market listings [n_envs], padded to 16 B (nmmo_wire_header_bytes);
+ *   payload: per env, one record per agent in the realm (slot order) then its listings (32 B
+ *           each); a record is a 16-B head (int16 AgentId, CurrentTick, task index, tile row 0,
+ *           tile col 0, nv, ninv, 0), the 1,586 ActionTargets bits in 208 B, nv Entity rows
+ *           (31 int16), ninv Inventory rows (16 int16), the 225 window materials, zero pad to 16 B.
+ * A sender transfers the header (fixed size) and then total - header bytes; the receiver reads
+ * `total` from the header. */
+NMMO_API int64_t nmmo_wire_header_bytes(int32_t n_envs, int32_t player_n);
+/* Upper bound of a wire buffer (every agent in the realm with 100 visible entities, 12 items). */
+NMMO_API int64_t nmmo_wire_max_bytes(int32_t n_envs, int32_t player_n);
+/* Encodes `native` (the NMMO_OBS_NATIVE buffer of h's most recent nmmo_step / nmmo_reset; the
+ * per-agent counts come from that launch) into `wire` (device, nmmo_wire_max_bytes). Enqueued;
+ * the buffer's total size is its first int64 once the stream reaches it. */
+NMMO_API int nmmo_wire_pack(NmmoHandle* h, const void* native, void* wire, void* stream);
+/* Decodes a wire buffer of n_envs x player_n agents into the native layout (every byte of the
+ * n_envs x (player_n x NMMO_NATIVE_ROW_BYTES + NMMO_NATIVE_MARKET_BYTES) buffer is written;
+ * bit-identical to what the sender's nmmo_step wrote). Enqueued; needs no handle. */
+NMMO_API int nmmo_wire_unpack(int32_t n_envs, int32_t player_n, const void* wire, void* native, void* stream);
+
 /* Masked-uniform scripted actions from the current state (bench / tests). */
 NMMO_API int nmmo_scripted_actions(NmmoHandle* h, uint64_t policy_seed, int32_t* actions, void* stream);
 

@@ -24,7 +24,8 @@ SYMBOLS = [
     "nmmo_set_wrapper", "nmmo_get_wrapper_state", "nmmo_expand_obs", "nmmo_exp_scratch_ints",
     "nmmo_exp_store", "nmmo_exp_sort", "nmmo_exp_gae", "nmmo_gather_rows", "nmmo_n_envs",
     "nmmo_last_error", "nmmo_abi_version", "nmmo_end_episodes", "nmmo_build_info",
-    "nmmo_get_wrapper_dropped", "nmmo_set_task_weights",
+    "nmmo_get_wrapper_dropped", "nmmo_set_task_weights", "nmmo_wire_header_bytes", "nmmo_wire_max_bytes",
+    "nmmo_wire_pack", "nmmo_wire_unpack",
 ]
 
 
@@ -79,6 +80,12 @@ def lib():
     L.nmmo_abi_version.restype = i32
     L.nmmo_end_episodes.argtypes = [vp, vp]
     L.nmmo_get_wrapper_dropped.argtypes = [vp, ctypes.POINTER(ctypes.c_int64)]
+    L.nmmo_wire_header_bytes.argtypes = [i32, i32]
+    L.nmmo_wire_header_bytes.restype = ctypes.c_int64
+    L.nmmo_wire_max_bytes.argtypes = [i32, i32]
+    L.nmmo_wire_max_bytes.restype = ctypes.c_int64
+    L.nmmo_wire_pack.argtypes = [vp, vp, vp, vp]
+    L.nmmo_wire_unpack.argtypes = [i32, i32, vp, vp, vp]
     L.nmmo_build_info.restype = ctypes.c_char_p
     if L.nmmo_abi_version() != abi.ABI_VERSION:
         raise NativeError(f"ABI mismatch: lib {L.nmmo_abi_version()} != python {abi.ABI_VERSION}")

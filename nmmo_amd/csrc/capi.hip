@@ -54,6 +54,7 @@ struct NmmoHandle {
   NmmoTask* d_tasks = nullptr;
   int32_t* d_assign = nullptr;
   NmmoTaskState* d_tstate = nullptr;
+  uint16_t* d_wcount = nullptr;  // native obs: per-agent wire count words of the last obs (wire.hip)
   // wrapper layer (nmmo_set_wrapper, SPEC §13)
   bool wrap_on = false;
   NmmoWrapperConfig wc{};
@@ -172,7 +173,8 @@ void nmmo_destroy(NmmoHandle* h) {
   for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
   void* bufs[] = {h->d_env,  h->d_ent,   h->d_ring,  h->d_mat,   h->d_dep,   h->d_bank,
                   h->d_task, h->d_seeds, h->d_items, h->d_iring, h->d_mlist, h->d_mcount,
-                  h->d_events, h->d_tasks, h->d_assign, h->d_tstate, h->d_ws, h->d_uniq, h->d_wenv, h->d_wdrop, h->d_task_cum};
+                  h->d_events, h->d_tasks, h->d_assign, h->d_tstate, h->d_ws, h->d_uniq, h->d_wenv, h->d_wdrop, h->d_task_cum,
+                  h->d_wcount};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   delete h;
@@ -221,6 +223,9 @@ int nmmo_create(const NmmoConfig* cfg, int32_t n_envs, uint64_t seed, int32_t de
   ALLOC(h->d_tasks, sizeof(NmmoTask));
   ALLOC(h->d_assign, n * P * 4);
   ALLOC(h->d_tstate, n * P * sizeof(NmmoTaskState));
+  if (cfg->obs_layout == NMMO_OBS_NATIVE) {
+    ALLOC(h->d_wcount, n * P * 2);
+  }
 #undef ALLOC
   if (init_kernels() != hipSuccess) return cleanup_fail(fail(NMMO_E_HIP, "kernel attributes"));
   if (task_embedding && cfg->task_embed_dim > 0) {
@@ -269,6 +274,7 @@ static ObsParams obs_params(NmmoHandle* h, void* obs) {
   p.o_inventory = L.off_inventory; p.o_market = L.off_market; p.o_task = L.off_task;
   p.o_tile = L.off_tile;
   p.row_map = nullptr;
+  p.wcount = native ? h->d_wcount : nullptr;
   p.ws = h->wrap_on ? h->d_ws : nullptr;
   p.wflags = 0;
   if (h->wrap_on) {
@@ -353,6 +359,35 @@ int nmmo_expand_obs(NmmoHandle* h, const void* native, float* flat, int32_t n_en
   p.obs = flat;
   p.n_envs = n_envs;
   HIP_TRY(launch_expand(p, (hipStream_t)stream));
+  return NMMO_OK;
+}
+
+// ---------------------------------------------------------------- wire codec (SPEC §8c)
+int64_t nmmo_wire_header_bytes(int32_t n_envs, int32_t player_n) {
+  if (n_envs <= 0 || player_n <= 0 || player_n > 128) return fail(NMMO_E_INVALID, "n_envs > 0, player_n in 1..128");
+  return ((8 + 8 * (int64_t)n_envs + 2 * (int64_t)n_envs * player_n + 2 * (int64_t)n_envs) + 15) & ~(int64_t)15;
+}
+
+int64_t nmmo_wire_max_bytes(int32_t n_envs, int32_t player_n) {
+  const int64_t hdr = nmmo_wire_header_bytes(n_envs, player_n);
+  if (hdr < 0) return hdr;
+  const int64_t rec = (16 + 208 + 62 * 100 + 32 * 12 + 225 + 15) & ~15;  // every agent in the realm, full windows
+  return hdr + (int64_t)n_envs * ((int64_t)player_n * rec + NMMO_NATIVE_MARKET_BYTES);
+}
+
+int nmmo_wire_pack(NmmoHandle* h, const void* native, void* wire, void* stream) {
+  if (!h || !native || !wire) return fail(NMMO_E_INVALID, "null argument");
+  if (h->cfg.obs_layout != NMMO_OBS_NATIVE || !h->d_wcount)
+    return fail(NMMO_E_INVALID, "nmmo_wire_pack needs a handle created with NMMO_OBS_NATIVE");
+  HIP_TRY(launch_wire_pack(h->d_wcount, h->d_mcount, (const uint8_t*)native, (uint8_t*)wire, h->st.n_envs, h->st.P,
+                           (hipStream_t)stream));
+  return NMMO_OK;
+}
+
+int nmmo_wire_unpack(int32_t n_envs, int32_t player_n, const void* wire, void* native, void* stream) {
+  if (!wire || !native) return fail(NMMO_E_INVALID, "null argument");
+  if (n_envs <= 0 || player_n <= 0 || player_n > 128) return fail(NMMO_E_INVALID, "n_envs > 0, player_n in 1..128");
+  HIP_TRY(launch_wire_unpack((const uint8_t*)wire, (uint8_t*)native, n_envs, player_n, (hipStream_t)stream));
   return NMMO_OK;
 }
 

@@ -64,6 +64,7 @@ struct ObsParams {
   // wrapper observation edits (SPEC §13): kWrapObs* bits, prev_price from the wrapper state
   const NmmoWrapState* ws;  // [n][P] or NULL
   int wflags;
+  uint16_t* wcount;     // native only, or NULL: per agent 0x8000 | nv | ninv << 7 (0 = not in the realm), wire.hip
 };
 constexpr int kWrapObsPrice = 1, kWrapObsNoGive = 2, kWrapObsNoDangerous = 4;
 
@@ -109,6 +110,10 @@ hipError_t launch_tick(const DevState& st, const int32_t* actions, const uint64_
 hipError_t launch_rebuild_dep(const DevState& st, hipStream_t stream);
 hipError_t launch_obs(const ObsParams& p, hipStream_t stream);
 hipError_t launch_expand(const ObsParams& p, hipStream_t stream);  // native -> flat (SPEC §8b)
+// wire codec (wire.hip, SPEC §8c): native <-> compact transport records
+hipError_t launch_wire_pack(const uint16_t* counts, const int* mcount, const uint8_t* native, uint8_t* wire, int n,
+                            int P, hipStream_t s);
+hipError_t launch_wire_unpack(const uint8_t* wire, uint8_t* native, int n, int P, hipStream_t s);
 hipError_t launch_store(const NmmoExperience& x, const NmmoStoreInput& in, const ObsParams* native,
                         int* scratch, hipStream_t stream);  // storage.hip
 int store_blocks(int n_rows);

@@ -377,6 +377,7 @@ __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
     uint8_t* nrow = p.nat + (size_t)e * native_env_bytes(p.P) + (size_t)a * NMMO_NATIVE_ROW_BYTES;
     if (!T[F_ALIVE * S + a]) {
       if (alive(j + 1)) prefetch(a + kObsWaves, j + 1);
+      if (p.wcount && lane == 0) p.wcount[(size_t)e * p.P + a] = 0;
       uint4* z = reinterpret_cast<uint4*>(nrow);
       for (int i = lane; i < NMMO_NATIVE_ROW_BYTES / 16; i += 64) z[i] = make_uint4(0u, 0u, 0u, 0u);
       continue;
@@ -396,6 +397,7 @@ __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
     m.prev_price = kWrap ? __builtin_amdgcn_readlane(my_prev, j) : -1;
     m.movebits = move_bits(wm[1]);
     const int aid = T[F_ID * S + a];
+    if (p.wcount && lane == 0) p.wcount[(size_t)e * p.P + a] = (uint16_t)(0x8000 | m.nv | m.ninv << 7);
     if (alive(j + 1)) prefetch(a + kObsWaves, j + 1);  // wm is in LDS now; next agent's loads
     // u8 ActionTargets in flat order, then pad to NMMO_NATIVE_MASK_BYTES. Buy.MarketItem (1,025
     // entries, the longest section): four entries per lane per dword store from one 8-B LDS read
@@ -549,7 +551,7 @@ __host__ __device__ inline size_t policy_lds_bytes(int S, int P) {
   return ((b + 15) & ~(size_t)15) + grid_lds_bytes(S);
 }
 
-__global__ void __launch_bounds__(512) policy_kernel(PolicyParams p) {
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8, 8))) policy_kernel(PolicyParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int S = p.S, P = p.P, e = blockIdx.x, tid = threadIdx.x;
   const int NW = (S + 63) >> 6;

@@ -51,3 +51,40 @@ def scatter_from_learner(full, like: torch.Tensor, src: int = 0) -> torch.Tensor
     else:
         dist.scatter(out, src=src)
     return out
+
+
+def gather_wire_to_learner(wire: torch.Tensor, header_bytes: int, dst: int = 0, recv_bufs=None):
+    """The learner gather of wire-encoded observations (SPEC §8c, nmmo_amd.wire): every rank's
+    packed buffer reaches rank `dst`, each peer -> root transfer carrying exactly the bytes its
+    header announces (a fixed-size header first, then the payload). Returns, on `dst`, the
+    buffers in rank order (dst's own `wire` in place, no self-copy); None elsewhere.
+    `recv_bufs[r]` (dst only) holds rank r's buffer (nmmo_wire_max_bytes of its shard); they are
+    allocated when missing. The sender reads its total size on the host (one 8-byte copy)."""
+    world, rank = dist.get_world_size(), dist.get_rank()
+    if world == 1:
+        return [wire]
+
+    def total_of(buf):
+        return int(buf[:8].view(torch.int64).item())
+
+    if rank != dst:
+        total = total_of(wire)
+        reqs = [dist.isend(wire[:header_bytes], dst)]
+        if total > header_bytes:
+            reqs.append(dist.isend(wire[header_bytes:total], dst))
+        for q in reqs:
+            q.wait()
+        return None
+    bufs = list(recv_bufs) if recv_bufs is not None else [None] * world
+    peers = [r for r in range(world) if r != dst]
+    for r in peers:
+        if bufs[r] is None:
+            bufs[r] = torch.empty_like(wire)
+    for q in [dist.irecv(bufs[r][:header_bytes], src=r) for r in peers]:
+        q.wait()
+    totals = {r: total_of(bufs[r]) for r in peers}
+    reqs = [dist.irecv(bufs[r][header_bytes:totals[r]], src=r) for r in peers if totals[r] > header_bytes]
+    for q in reqs:
+        q.wait()
+    bufs[dst] = wire
+    return [bufs[r][:totals[r]] if r != dst else wire for r in range(world)]

@@ -1,0 +1,61 @@
+"""Wire encoding of native observations (SPEC.md §8c): the transport form of the learner gather.
+
+BASELINE config 5 returns every rank's observations to one learner GPU over xGMI. The native
+layout (9,552 B per agent + 32 KB Market per env) is mostly padding on the wire; a wire buffer
+(`nmmo_wire_pack`, csrc/wire.hip) keeps the 16-B record head, the ActionTargets as bits, only
+the visible Entity rows and held items, the 225 window materials and only the listed Market
+rows: ~1.3 KB per agent in C4 steady state. The receiver decodes it back to the native layout
+bit-identically (`nmmo_wire_unpack`). The transfer protocol — the fixed-size header first, then
+exactly the payload the header announces — is `nmmo_amd.distributed.gather_wire_to_learner`.
+"""
+
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from ._native import check, lib
+
+
+def header_bytes(n_envs: int, players: int) -> int:
+    return int(lib().nmmo_wire_header_bytes(n_envs, players))
+
+
+def max_bytes(n_envs: int, players: int) -> int:
+    return int(lib().nmmo_wire_max_bytes(n_envs, players))
+
+
+def total_bytes(wire: torch.Tensor) -> int:
+    """The size a packed buffer announces (its first int64). Synchronises with wire's stream."""
+    return int(wire[:8].view(torch.int64).item())
+
+
+def _stream(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def pack(engine, native: torch.Tensor | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
+    """Encode the engine's most recent native obs (default: engine.obs) into a device uint8
+    buffer of nmmo_wire_max_bytes (enqueued on the current stream)."""
+    native = engine.obs if native is None else native
+    cap = max_bytes(engine.n_envs, engine.P)
+    out = torch.empty(cap, dtype=torch.uint8, device=engine.device) if out is None else out
+    if out.numel() < cap:
+        raise ValueError(f"wire buffer holds {out.numel()} B < {cap} B")
+    with torch.cuda.device(engine.device):
+        check(lib().nmmo_wire_pack(engine.h, ctypes.c_void_p(native.data_ptr()), ctypes.c_void_p(out.data_ptr()),
+                                   _stream(engine.device)), "nmmo_wire_pack")
+    return out
+
+
+def unpack(wire: torch.Tensor, n_envs: int, players: int, out: torch.Tensor | None = None) -> torch.Tensor:
+    """Decode a wire buffer into the native layout [n_envs, env_bytes] (enqueued)."""
+    from . import abi
+
+    if out is None:
+        out = torch.empty((n_envs, abi.native_env_bytes(players)), dtype=torch.uint8, device=wire.device)
+    with torch.cuda.device(wire.device):
+        check(lib().nmmo_wire_unpack(n_envs, players, ctypes.c_void_p(wire.data_ptr()),
+                                     ctypes.c_void_p(out.data_ptr()), _stream(wire.device)), "nmmo_wire_unpack")
+    return out
