@@ -551,7 +551,7 @@ __host__ __device__ inline size_t policy_lds_bytes(int S, int P) {
   return ((b + 15) & ~(size_t)15) + grid_lds_bytes(S);
 }
 
-__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8, 8))) policy_kernel(PolicyParams p) {
+__device__ __forceinline__ void policy_body(const PolicyParams& p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int S = p.S, P = p.P, e = blockIdx.x, tid = threadIdx.x;
   const int NW = (S + 63) >> 6;
@@ -752,9 +752,17 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8, 8))
   }
 }
 
+__global__ void __launch_bounds__(512) policy_kernel(PolicyParams p) { policy_body(p); }
+// <= 64 VGPRs / 96 SGPRs: a 6-wave workgroup (S = 384) puts two waves on two SIMDs, so 4 per CU
+// need 8 wave slots there (C3/C4: 21 -> 17 us per launch; the 2-wave C2 launch is faster without)
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8, 8))) policy_kernel_w8(PolicyParams p) {
+  policy_body(p);
+}
+
 hipError_t launch_policy(const PolicyParams& p, hipStream_t stream) {
   if (p.S > 511) return hipErrorInvalidValue;  // grid entries hold ds_row - 1 in 9 bits
-  hipLaunchKernelGGL(policy_kernel, dim3(p.n_envs), dim3(policy_threads(p.S, p.P)),
+  const int threads = policy_threads(p.S, p.P);
+  hipLaunchKernelGGL(threads > 256 ? policy_kernel_w8 : policy_kernel, dim3(p.n_envs), dim3(threads),
                      policy_lds_bytes(p.S, p.P), stream, p);
   return hipGetLastError();
 }

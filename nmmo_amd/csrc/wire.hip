@@ -182,10 +182,16 @@ __global__ void __launch_bounds__(256) wire_pack_kernel(const uint8_t* native, u
   }
 }
 
-// wire -> native: every byte of the native buffer is written
+// wire -> native: every byte of the native buffer is written. Each wave first copies its
+// agent's record into LDS (every load issued before the first store: vmcnt retires in issue
+// order, so loads between stores would wait for them), then writes the 9,552-B row with 16-B
+// stores computed from LDS.
+constexpr int kRecMaxU4 = (kWireHead + kWireMask + 62 * kNObs + 32 * kInv + kWireTiles + 15) / 16;  // 440
+
 __global__ void __launch_bounds__(256) wire_unpack_kernel(const uint8_t* wire, uint8_t* native, int n, int P) {
   WireView v = wire_view(const_cast<uint8_t*>(wire), n, P);
   __shared__ int off[129];
+  __shared__ uint4 recbuf[4][kRecMaxU4];
   const int e = blockIdx.x, g = blockIdx.y, lane = lane_id(), w = wave_id();
   const uint16_t* cnt = v.cnt + (size_t)e * P;
   record_offsets(cnt, P, off);
@@ -198,52 +204,70 @@ __global__ void __launch_bounds__(256) wire_unpack_kernel(const uint8_t* wire, u
     for (int k = threadIdx.x; k < NMMO_NATIVE_MARKET_BYTES / 16; k += blockDim.x)
       dst[k] = k < 2 * nm ? src[k] : make_uint4(0u, 0u, 0u, 0u);
   }
+  uint4* lrec = recbuf[w];
+  const uint8_t* lb = reinterpret_cast<const uint8_t*>(lrec);
   for (int i = w; i < kWireAgentsPerBlock; i += 4) {
     const int a = g * kWireAgentsPerBlock + i;
     if (a >= P) break;
     const uint32_t c = cnt[a];
-    uint8_t* row = nenv + (size_t)a * NMMO_NATIVE_ROW_BYTES;
+    uint4* row4 = reinterpret_cast<uint4*>(nenv + (size_t)a * NMMO_NATIVE_ROW_BYTES);
     if (!(c & 0x8000u)) {
-      uint4* z = reinterpret_cast<uint4*>(row);
-      for (int k = lane; k < NMMO_NATIVE_ROW_BYTES / 16; k += 64) z[k] = make_uint4(0u, 0u, 0u, 0u);
+      for (int k = lane; k < NMMO_NATIVE_ROW_BYTES / 16; k += 64) row4[k] = make_uint4(0u, 0u, 0u, 0u);
       continue;
     }
-    const int nv = c & 127, ninv = (c >> 7) & 15;
-    const uint8_t* rec = penv + off[a];
-    const int16_t* h16 = reinterpret_cast<const int16_t*>(rec);
-    // mask bytes, 16 per lane (lanes 0..99: 1,600 bytes)
+    const int nv = c & 127, ninv = (c >> 7) & 15, nq = wire_record_bytes(c) / 16;
+    {
+      const uint4* src4 = reinterpret_cast<const uint4*>(penv + off[a]);
+      constexpr int kPer = (kRecMaxU4 + 63) / 64;
+      uint4 r[kPer];
+#pragma unroll
+      for (int k = 0; k < kPer; k++) r[k] = lane + 64 * k < nq ? src4[lane + 64 * k] : make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+      for (int k = 0; k < kPer; k++)
+        if (lane + 64 * k < nq) lrec[lane + 64 * k] = r[k];
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    const int16_t* h16 = reinterpret_cast<const int16_t*>(lb);
+    const int16_t* s16 = reinterpret_cast<const int16_t*>(lb + kWireHead + kWireMask);
+    const uint8_t* mat = lb + kWireHead + kWireMask + 62 * nv + 32 * ninv;
+    const int r0 = h16[3], c0 = h16[4], task = h16[2];
+    // mask bytes, 16 per lane (1,600 bytes = 100 stores)
     for (int k = lane; k < NMMO_NATIVE_MASK_BYTES / 16; k += 64) {
-      const uint32_t bits = (reinterpret_cast<const uint32_t*>(rec + kWireHead)[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
+      const uint32_t bits = (reinterpret_cast<const uint32_t*>(lb + kWireHead)[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
       uint32_t q[4];
 #pragma unroll
       for (int j = 0; j < 4; j++)
         q[j] = ((bits >> (4 * j)) & 1u) | ((bits >> (4 * j + 1)) & 1u) << 8 | ((bits >> (4 * j + 2)) & 1u) << 16 |
                ((bits >> (4 * j + 3)) & 1u) << 24;
-      reinterpret_cast<uint4*>(row)[k] = make_uint4(q[0], q[1], q[2], q[3]);
+      row4[k] = make_uint4(q[0], q[1], q[2], q[3]);
     }
-    const int16_t* s16 = reinterpret_cast<const int16_t*>(rec + kWireHead + kWireMask);
-    const uint8_t* mat = rec + kWireHead + kWireMask + 62 * nv + 32 * ninv;
-    const int r0 = h16[3], c0 = h16[4], task = h16[2];
-    // the int16 part, two entries per lane per pass (dword stores)
-    uint32_t* d32 = reinterpret_cast<uint32_t*>(row + NMMO_NATIVE_MASK_BYTES);
-    auto val = [&](int k) -> int {
-      if (k < kNatI16Entity) return h16[k];
-      if (k < kNatI16Inv) {
+    auto val = [&](int k) -> uint32_t {
+      int x;
+      if (k < kNatI16Entity) {
+        x = h16[k];
+      } else if (k < kNatI16Inv) {
         const int j = k - kNatI16Entity;
-        return j < nv * NMMO_N_ENTITY_COLS ? s16[j] : 0;
-      }
-      if (k < kNatI16Tile) {
+        x = j < nv * NMMO_N_ENTITY_COLS ? s16[j] : 0;
+      } else if (k < kNatI16Tile) {
         const int j = k - kNatI16Inv;
-        return j < ninv * 16 ? s16[nv * NMMO_N_ENTITY_COLS + j] : 0;
-      }
-      if (k < kNatI16Task) {
+        x = j < ninv * 16 ? s16[nv * NMMO_N_ENTITY_COLS + j] : 0;
+      } else if (k < kNatI16Task) {
         const int j = k - kNatI16Tile, t = j / 3, comp = j - 3 * t;
-        return comp == 0 ? r0 + t / 15 : comp == 1 ? c0 + t % 15 : (int)mat[t];
+        x = comp == 0 ? r0 + t / 15 : comp == 1 ? c0 + t % 15 : (int)mat[t];
+      } else {
+        x = k == kNatI16Task ? task : 0;
       }
-      return k == kNatI16Task ? task : 0;
+      return (uint32_t)(uint16_t)x;
     };
-    for (int k2 = lane; k2 < NMMO_NATIVE_I16 / 2; k2 += 64)
-      d32[k2] = (uint32_t)(uint16_t)val(2 * k2) | (uint32_t)(uint16_t)val(2 * k2 + 1) << 16;
+    // the int16 part, 8 entries per lane per pass (16-B stores)
+    uint4* d4 = reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(row4) + NMMO_NATIVE_MASK_BYTES);
+    for (int q = lane; q < NMMO_NATIVE_I16 / 8; q += 64) {
+      const int k = 8 * q;
+      d4[q] = make_uint4(val(k) | val(k + 1) << 16, val(k + 2) | val(k + 3) << 16, val(k + 4) | val(k + 5) << 16,
+                         val(k + 6) | val(k + 7) << 16);
+    }
+    __builtin_amdgcn_wave_barrier();  // the next agent's record overwrites this one
   }
 }
 
