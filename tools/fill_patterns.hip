@@ -69,6 +69,36 @@ __global__ void __launch_bounds__(256) fill_row_per_wave_8(float* obs) {
   const size_t r0 = (size_t)blockIdx.x * 8;
   for (int i = w; i < 8; i += 4) row_zero(obs + (r0 + i) * kElems, 0, kElems, lane, 64);
 }
+// (g) the obs grid restricted to envs [e0, e0 + ne): a launch per chunk of envs
+__global__ void __launch_bounds__(256) fill_row_per_wave_chunk(float* obs, int e0) {
+  const int e = e0 + blockIdx.x, g = blockIdx.y, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int i = w; i < 16; i += 4) row_zero(obs + ((size_t)e * kP + g * 16 + i) * kElems, 0, kElems, lane, 64);
+}
+// (h) torch-like one-shot blocks: T threads, V float4 per thread, block chunk = T*V*16 B, lane-linear
+template <int T, int V>
+__global__ void __launch_bounds__(T) fill_oneshot_tv(float4* p, size_t n4) {
+  const size_t base = (size_t)blockIdx.x * (T * V) + threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < V; i++)
+    if (base + (size_t)T * i < n4) p[base + (size_t)T * i] = make_float4(0.f, 0.f, 0.f, 0.f);
+}
+// (P4) one workgroup per row (4 waves interleaved 1 KB each, 4 KB steps), workgroups in row order
+__global__ void __launch_bounds__(256) fill_wg_per_row(float* obs) {
+  row_zero(obs + (size_t)blockIdx.x * kElems, 0, kElems, threadIdx.x, 256);
+}
+// (P5) one single-wave workgroup per row, in row order
+__global__ void __launch_bounds__(64) fill_wave_per_row(float* obs) {
+  row_zero(obs + (size_t)blockIdx.x * kElems, 0, kElems, threadIdx.x, 64);
+}
+// (P6) 4-wave workgroups, wave w writes row 4 * blockIdx.x + w, in row order
+__global__ void __launch_bounds__(256) fill_4rows_per_wg(float* obs) {
+  row_zero(obs + ((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * kElems, 0, kElems, threadIdx.x & 63, 64);
+}
+// (P7) as P6 with 16 rows per workgroup (the obs kernel's) but row-ordered grid
+__global__ void __launch_bounds__(256) fill_16rows_rowordered(float* obs) {
+  const int w = threadIdx.x >> 6;
+  for (int i = w; i < 16; i += 4) row_zero(obs + ((size_t)blockIdx.x * 16 + i) * kElems, 0, kElems, threadIdx.x & 63, 64);
+}
 int main() {
   const size_t n = (size_t)kEnvs * kP * kElems;
   hipEvent_t t0, t1;
@@ -101,13 +131,16 @@ int main() {
     if (hipMalloc(&q, bytes) != hipSuccess) { printf("alloc failed\n"); return; }
     bufs[nb++] = q;
     printf("%s\n", tag);
-    timeit("  stride float4 (8192x256)", [&] { fill_stride<<<8192, 256>>>((float4*)q, n / 4); });
-    timeit("  one-shot 16-KB blocks", [&] { fill_oneshot<<<(unsigned)((n / 4 + 1023) / 1024), 256>>>((float4*)q, n / 4); });
-    timeit("  rows, grid (env, group)", [&] { fill_row_per_wave<<<grid, 256, 38800>>>(q); });
-    timeit("  rows, grid (group, env)", [&] { fill_row_per_wave_gmajor<<<dim3(kP / 16, kEnvs), 256, 38800>>>(q); });
-    timeit("  rows, 1-D, 8 per block", [&] { fill_row_per_wave_8<<<kEnvs * kP / 8, 256, 19400>>>(q); });
+    const size_t n4 = n / 4;
+    const int rows = kEnvs * kP;
+    timeit("  rows, one launch (obs shape)", [&] { fill_row_per_wave<<<grid, 256, 38800>>>(q); });
+    timeit("  one-shot 256 thr x 1 f4 (4 KB)", [&] { fill_oneshot_tv<256, 1><<<(unsigned)((n4 + 255) / 256), 256>>>((float4*)q, n4); });
+    timeit("  P4 wg per row (row order)", [&] { fill_wg_per_row<<<rows, 256>>>(q); });
+    timeit("  P5 wave per row (row order)", [&] { fill_wave_per_row<<<rows, 64>>>(q); });
+    timeit("  P6 4 rows per wg (row order)", [&] { fill_4rows_per_wg<<<rows / 4, 256>>>(q); });
+    timeit("  P7 16 rows per wg (row order)", [&] { fill_16rows_rowordered<<<rows / 16, 256, 38800>>>(q); });
   };
-  for (int i = 0; i < 4; i++) probe(n * 4, "allocation");
+  for (int i = 0; i < 3; i++) probe(n * 4, "allocation");
   for (int i = 0; i < nb; i++) hipFree(bufs[i]);
   return 0;
 }
