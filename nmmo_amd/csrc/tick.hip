@@ -732,55 +732,94 @@ __device__ __forceinline__ bool npc_validate(Ctx& c, int n) {
 // stops growing. The NPC steps to the first of N, S, E, W that the previous wave covered, i.e.
 // a neighbour one step closer to the target. -1 = unreachable inside the window. The window
 // (rows r-7..r+7, cols c-7..c+7) lies inside the map: NPCs stay in the playable area 16..143.
-__device__ __forceinline__ int window_bfs_step(const uint8_t* __restrict__ mat, int r, int col,
-                                                          int tr, int tc) {
+// NPC hunt pathing (SPEC §6 v2): the first step of a shortest path from the NPC to its target
+// inside the NPC's 15x15 window, by a breadth-first wave from the target over the window's
+// passable tiles, stopping when it reaches the NPC's tile (then N, S, E, W: the first neighbour
+// at distance - 1). Wave-cooperative: 16 lanes per request (lane i holds window row i as a 15-bit
+// row of reached / passable tiles; rows i - 1 and i + 1 come from the neighbouring lanes by DPP),
+// 4 requests per wave at once; the requests are the hunting NPCs farther than one tile from
+// their target (a 256-bit slot mask in c.misc). Result per NPC slot in c.amove (direction, or -1
+// = unreachable in the window, so the greedy step applies). Same iteration as the serial
+// restatement in the oracle, so the same step.
+constexpr int kBfsPending = -2;
+__device__ __forceinline__ uint32_t dpp_row_up(uint32_t x) {    // lane i <- lane i - 1 in its 16-lane row (0 at row start)
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true);
+}
+__device__ __forceinline__ uint32_t dpp_row_down(uint32_t x) {  // lane i <- lane i + 1 in its row (0 at row end)
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x101, 0xF, 0xF, true);
+}
+__device__ __forceinline__ void npc_bfs_phase(Ctx& c) {
   constexpr int W = 2 * kVision + 1;
   constexpr uint32_t kImp = (1u << M_VOID) | (1u << M_WATER) | (1u << M_STONE) | (1u << M_OCEAN) | (1u << M_FISH);
-  uint32_t pass[W], R[W];
-#pragma unroll
-  for (int i = 0; i < W; i++) {
-    const int base = (r - kVision + i) * kSize + col - kVision;  // 15 bytes from here
-    const uint32_t* w = reinterpret_cast<const uint32_t*>(mat + (base & ~3));
-    const int sh = base & 3;
-    const uint32_t d0 = w[0], d1 = w[1], d2 = w[2], d3 = w[3], d4 = w[4];
-    uint32_t m = 0;
-#pragma unroll
-    for (int j = 0; j < W; j++) {
-      const int k = sh + j;  // byte k of the 20 loaded
-      const uint32_t dw = (k >> 2) == 0 ? d0 : (k >> 2) == 1 ? d1 : (k >> 2) == 2 ? d2 : (k >> 2) == 3 ? d3 : d4;
-      const uint32_t mt = (dw >> ((k & 3) * 8)) & 15u;
-      m |= ((kImp >> mt) & 1u) ? 0u : (1u << j);
-    }
-    pass[i] = m;
-  }
-  const int si = tr - r + kVision, sj = tc - col + kVision;
-#pragma unroll
-  for (int i = 0; i < W; i++) R[i] = i == si ? (1u << sj) : 0u;
   constexpr uint32_t kMid = 1u << kVision;
-  for (int it = 0; it < W * W; it++) {
-    uint32_t N[W], grew = 0;
+  const uint32_t* req = reinterpret_cast<const uint32_t*>(c.misc);
+  int nreq = 0;
 #pragma unroll
-    for (int i = 0; i < W; i++) {
-      const uint32_t up = i > 0 ? R[i - 1] : 0u, dn = i < W - 1 ? R[i + 1] : 0u;
-      N[i] = (R[i] | (R[i] << 1) | (R[i] >> 1) | up | dn) & pass[i];
-      grew |= N[i] ^ R[i];
+  for (int k = 0; k < 8; k++) nreq += __popc(req[k]);
+  const int lane = lane_id(), grp = lane >> 4, row = lane & 15;
+  const int nw = blockDim.x >> 6;
+  const uint64_t gmask = 0xFFFFull << (16 * grp);
+  for (int q0 = wave_id() * 4; q0 < nreq; q0 += nw * 4) {  // wave-uniform loop
+    const int q = q0 + grp;
+    const bool on = q < nreq;
+    int n = -1;
+    if (on) {  // the q-th requested NPC slot
+      int k = q, wd = 0;
+      while (k >= __popc(req[wd])) k -= __popc(req[wd++]);
+      uint32_t m = req[wd];
+      for (int i = 0; i < k; i++) m &= m - 1;
+      n = c.P + 32 * wd + __builtin_ctz(m);
     }
-    if (N[kVision] & kMid) {  // the NPC's tile is reached at distance it+1: R = distance <= it
-      if ((R[kVision - 1] & kMid) != 0u) return 0;   // N
-      if ((R[kVision + 1] & kMid) != 0u) return 1;   // S
-      if ((R[kVision] & (kMid << 1)) != 0u) return 2;  // E (col + 1)
-      return 3;                                       // W (col - 1)
-    }
-    if (!grew) return -1;
+    uint32_t pass = 0u, R = 0u;
+    if (on && row < W) {
+      const int r = TF(F_ROW, n), col = TF(F_COL, n), ts = TF(F_TARGET_ID, n) - 1;
+      const int base = (r - kVision + row) * kSize + col - kVision;  // 15 bytes of this window row
+      const uint32_t* wp = reinterpret_cast<const uint32_t*>(c.mat + (base & ~3));
+      const int sh = base & 3;
+      const uint32_t d[5] = {wp[0], wp[1], wp[2], wp[3], wp[4]};
 #pragma unroll
-    for (int i = 0; i < W; i++) R[i] = N[i];
+      for (int j = 0; j < W; j++) {
+        const int k = sh + j;
+        const uint32_t mt = (d[k >> 2] >> ((k & 3) * 8)) & 15u;
+        pass |= ((kImp >> mt) & 1u) ? 0u : (1u << j);
+      }
+      const int si = TF(F_ROW, ts) - r + kVision, sj = TF(F_COL, ts) - col + kVision;
+      R = row == si ? (1u << sj) : 0u;
+    }
+    int result = -1;
+    bool done = !on;
+    for (int it = 0; it < W * W; it++) {
+      const uint32_t up = dpp_row_up(R), dn = dpp_row_down(R);
+      const uint32_t N = (R | (R << 1) | (R >> 1) | up | dn) & pass;
+      const uint64_t grew = __ballot(N != R) & gmask;
+      const uint64_t hit = __ballot(row == kVision && (N & kMid)) & gmask;
+      const uint64_t rn = __ballot(row == kVision - 1 && (R & kMid)) & gmask;
+      const uint64_t rs = __ballot(row == kVision + 1 && (R & kMid)) & gmask;
+      const uint64_t re = __ballot(row == kVision && (R & (kMid << 1))) & gmask;
+      if (!done) {
+        if (hit) {  // the NPC's tile is reached at distance it + 1: R = distance <= it
+          result = rn ? 0 : rs ? 1 : re ? 2 : 3;
+          done = true;
+        } else if (!grew) {
+          done = true;
+        }
+      }
+      if (__ballot(!done) == 0) break;
+      R = N;
+    }
+    if (on && row == 0) c.amove[n] = (int16_t)result;
   }
+}
+// greedy step toward (dr, dc) over the passable neighbours in nbm (SPEC §6 v1 rule)
+__device__ __forceinline__ int greedy_step(int dr, int dc, uint32_t nbm) {
+  const int dir_r = dr > 0 ? 1 : 0, dir_c = dc > 0 ? 2 : 3;
+  const bool rows_first = iabs(dr) >= iabs(dc);
+  const int first = rows_first ? dir_r : dir_c, second = rows_first ? dir_c : dir_r;
+  const bool second_nz = rows_first ? dc != 0 : dr != 0;
+  if ((nbm >> first) & 1u) return first;
+  if (second_nz && ((nbm >> second) & 1u)) return second;
   return -1;
 }
-
-// closest: slot of the closest player within vision (ties to the lowest id) for a hostile NPC
-// without a target (computed block-wide by the caller), else -1
-// nbm: tick-start neighbourhood bits of the NPC's tile (bit d = neighbour d passable)
 __device__ __forceinline__ void npc_decide(Ctx& c, int n, int closest, uint32_t nbm, int& move, int& tgt,
                                            int& sty) {
   const int r = TF(F_ROW, n), col = TF(F_COL, n), id = TF(F_ID, n);
@@ -810,16 +849,9 @@ __device__ __forceinline__ void npc_decide(Ctx& c, int n, int closest, uint32_t 
   const int dist = linf(r, col, tr, tc);
   if (dist == 0) {
     move = (int)uniform_n(u.y, 4);
-  } else if (dist > 1 && (move = window_bfs_step(c.mat, r, col, tr, tc)) >= 0) {
-    // move.pathfind: first step of a shortest path inside the 15x15 window (SPEC §6 v2)
-  } else if (dist > 1) {  // target unreachable inside the window: greedy step (SPEC §6 v1 rule)
-    const int dr = tr - r, dc = tc - col;
-    const int dir_r = dr > 0 ? 1 : 0, dir_c = dc > 0 ? 2 : 3;
-    const bool rows_first = iabs(dr) >= iabs(dc);
-    const int first = rows_first ? dir_r : dir_c, second = rows_first ? dir_c : dir_r;
-    const bool second_nz = rows_first ? dc != 0 : dr != 0;
-    if ((nbm >> first) & 1u) move = first;
-    else if (second_nz && ((nbm >> second) & 1u)) move = second;
+  } else if (dist > 1) {  // move.pathfind: npc_bfs_phase, then greedy if unreachable in the window
+    move = kBfsPending;
+    atomicOr(reinterpret_cast<uint32_t*>(c.misc) + ((n - c.P) >> 5), 1u << ((n - c.P) & 31));
   }
   if (dist <= 3) tgt = ts;
 }
@@ -1043,6 +1075,7 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
   int evn = c.E[E_EVENT_COUNT];  // block-uniform running event count (SPEC §11)
 
   if (s < P) c.pres[s] = (uint8_t)TF(F_ALIVE, s);
+  if (tid < 8) c.misc[tid] = 0;  // hunt-pathing request mask (npc_bfs_phase)
   if (c.exch && tid < kLWords) c.lbits[tid] = 0;
   if (c.tev && s < P) {  // this player's task terms and event accumulators
     const NmmoTask& tk = c.tasks[c.assign[s]];
@@ -1201,6 +1234,16 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
     closest = best == 0x7FFFFFFF ? -1 : (best & 255);
   }
   if (npc_on && s >= P && inslot) npc_decide(c, s, closest, nbm, my_move, my_tgt, my_sty);
+  if (npc_on) {  // hunt pathing for the NPCs that asked (block-uniform)
+    __syncthreads();
+    npc_bfs_phase(c);
+    __syncthreads();
+    if (my_move == kBfsPending) {
+      const int r = c.amove[s];
+      const int ts = TF(F_TARGET_ID, s) - 1;
+      my_move = r >= 0 ? r : greedy_step(TF(F_ROW, ts) - TF(F_ROW, s), TF(F_COL, ts) - TF(F_COL, s), nbm);
+    }
+  }
   if (s < S) {
     c.amove[s] = (int16_t)my_move;
     c.atgt[s] = (int16_t)my_tgt;
