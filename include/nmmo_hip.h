@@ -329,6 +329,14 @@ NMMO_API int nmmo_get_wrapper_dropped(NmmoHandle* h, int64_t* total);
  * of consecutive envs (e.g. a learner expanding gathered shards). Enqueued on `stream`. */
 NMMO_API int nmmo_expand_obs(NmmoHandle* h, const void* native, float* flat, int32_t n_envs, void* stream);
 
+/* Device buffer for the observation tensor: `bytes` of device memory mapped from 64-MB physical
+ * chunks into one contiguous virtual range (hipMemCreate / hipMemMap). Large hipMalloc
+ * allocations landed on physical placements whose write rate varied 5.4-6.5 TB/s under the obs
+ * kernel's store pattern; chunk-mapped ones wrote at 6.5-6.6 TB/s every time. Synchronous;
+ * nmmo_dev_free synchronises the device first. */
+NMMO_API int nmmo_dev_alloc(int32_t device, uint64_t bytes, void** out);
+NMMO_API int nmmo_dev_free(void* ptr);
+
 /* ---- Wire encoding of native observations (SPEC.md §8c) ----
  * For moving observations between GPUs (the learner gather of BASELINE config 5): the native
  * layout without its padding. A wire buffer of n_envs x player_n agents is

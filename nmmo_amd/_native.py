@@ -25,7 +25,7 @@ SYMBOLS = [
     "nmmo_exp_store", "nmmo_exp_sort", "nmmo_exp_gae", "nmmo_gather_rows", "nmmo_n_envs",
     "nmmo_last_error", "nmmo_abi_version", "nmmo_end_episodes", "nmmo_build_info",
     "nmmo_get_wrapper_dropped", "nmmo_set_task_weights", "nmmo_wire_header_bytes", "nmmo_wire_max_bytes",
-    "nmmo_wire_pack", "nmmo_wire_unpack",
+    "nmmo_wire_pack", "nmmo_wire_unpack", "nmmo_dev_alloc", "nmmo_dev_free",
 ]
 
 
@@ -86,6 +86,8 @@ def lib():
     L.nmmo_wire_max_bytes.restype = ctypes.c_int64
     L.nmmo_wire_pack.argtypes = [vp, vp, vp, vp]
     L.nmmo_wire_unpack.argtypes = [i32, i32, vp, vp, vp]
+    L.nmmo_dev_alloc.argtypes = [i32, u64, ctypes.POINTER(vp)]
+    L.nmmo_dev_free.argtypes = [vp]
     L.nmmo_build_info.restype = ctypes.c_char_p
     if L.nmmo_abi_version() != abi.ABI_VERSION:
         raise NativeError(f"ABI mismatch: lib {L.nmmo_abi_version()} != python {abi.ABI_VERSION}")

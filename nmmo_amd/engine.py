@@ -47,8 +47,10 @@ class NmmoEngine:
         d = self.device
         n, P = self.n_envs, self.P
         self.actions = torch.zeros((n, P, abi.N_ACTION_HEADS), dtype=torch.int32, device=d)
-        if config.obs_layout == abi.OBS_FLAT:
-            self.obs = torch.empty((n, P, self.obs_elems), dtype=torch.float32, device=d)
+        if config.obs_layout == abi.OBS_FLAT:  # 12.6 GB at 1,024 envs: chunk-mapped (devmem)
+            from . import devmem
+
+            self.obs = devmem.empty((n, P, self.obs_elems), torch.float32, d)
         elif config.obs_layout == abi.OBS_NATIVE:  # SPEC §8b: per env, P rows + the Market
             self.obs = torch.empty((n, abi.native_env_bytes(P)), dtype=torch.uint8, device=d)
         else:

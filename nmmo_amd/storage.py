@@ -41,7 +41,10 @@ class DeviceExperience:
         d = self.device
         f32 = dict(dtype=torch.float32, device=d)
         i32 = dict(dtype=torch.int32, device=d)
-        self.obs = torch.zeros((cap, self.obs_elems), **f32)
+        from . import devmem
+
+        self.obs = devmem.empty((cap, self.obs_elems), torch.float32, d)  # chunk-mapped when large
+        self.obs.zero_()
         self.actions = torch.zeros((cap, abi.N_ACTION_HEADS), dtype=torch.int64, device=d)
         self.logprobs = torch.zeros(cap, **f32)
         self.rewards = torch.zeros(cap, **f32)

@@ -5,6 +5,7 @@
 
 #include <cstdio>
 #include <cstdint>
+#include <vector>
 
 constexpr int kElems = 23987, kEnvs = 1024, kP = 128;
 
@@ -100,6 +101,7 @@ __global__ void __launch_bounds__(256) fill_16rows_rowordered(float* obs) {
   for (int i = w; i < 16; i += 4) row_zero(obs + ((size_t)blockIdx.x * 16 + i) * kElems, 0, kElems, threadIdx.x & 63, 64);
 }
 int main() {
+  setvbuf(stdout, nullptr, _IONBF, 0);
   const size_t n = (size_t)kEnvs * kP * kElems;
   hipEvent_t t0, t1;
   hipEventCreate(&t0);
@@ -124,23 +126,51 @@ int main() {
     timeit("row per wave, dword stores", [&] { fill_row_per_wave_dword<<<grid, 256, 38800>>>(obs); });
     timeit("row per block", [&] { fill_row_per_block<<<grid, 256>>>(obs); });
   };
-  float* bufs[12];
-  int nb = 0;
-  auto probe = [&](size_t bytes, const char* tag) {
-    float* q;
-    if (hipMalloc(&q, bytes) != hipSuccess) { printf("alloc failed\n"); return; }
-    bufs[nb++] = q;
+  // hipMalloc vs virtual-memory allocations (hipMemCreate chunks mapped into one VA range)
+  auto timepat = [&](float* q, const char* tag) {
     printf("%s\n", tag);
     const size_t n4 = n / 4;
-    const int rows = kEnvs * kP;
     timeit("  rows, one launch (obs shape)", [&] { fill_row_per_wave<<<grid, 256, 38800>>>(q); });
     timeit("  one-shot 256 thr x 1 f4 (4 KB)", [&] { fill_oneshot_tv<256, 1><<<(unsigned)((n4 + 255) / 256), 256>>>((float4*)q, n4); });
-    timeit("  P4 wg per row (row order)", [&] { fill_wg_per_row<<<rows, 256>>>(q); });
-    timeit("  P5 wave per row (row order)", [&] { fill_wave_per_row<<<rows, 64>>>(q); });
-    timeit("  P6 4 rows per wg (row order)", [&] { fill_4rows_per_wg<<<rows / 4, 256>>>(q); });
-    timeit("  P7 16 rows per wg (row order)", [&] { fill_16rows_rowordered<<<rows / 16, 256, 38800>>>(q); });
   };
-  for (int i = 0; i < 3; i++) probe(n * 4, "allocation");
-  for (int i = 0; i < nb; i++) hipFree(bufs[i]);
+  float* bufs[4];
+  for (int i = 0; i < 2; i++) {
+    if (hipMalloc(&bufs[i], n * 4) != hipSuccess) return 1;
+    timepat(bufs[i], "hipMalloc");
+  }
+  for (int i = 0; i < 2; i++) hipFree(bufs[i]);
+  hipMemAllocationProp prop = {};
+  prop.type = hipMemAllocationTypePinned;
+  prop.location.type = hipMemLocationTypeDevice;
+  prop.location.id = 0;
+  size_t gran = 0;
+  hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityRecommended);
+  printf("recommended granularity %zu\n", gran);
+  for (size_t chunk : {(size_t)2 << 20, (size_t)16 << 20, (size_t)64 << 20, (size_t)256 << 20}) {
+    for (int rep = 0; rep < 2; rep++) {
+      printf("mapping %zu MB chunks\n", chunk >> 20);
+      const size_t total = ((n * 4 + chunk - 1) / chunk) * chunk;
+      void* va = nullptr;
+      if (hipMemAddressReserve(&va, total, chunk, nullptr, 0) != hipSuccess) { printf("reserve failed\n"); break; }
+      std::vector<hipMemGenericAllocationHandle_t> hs;
+      bool ok = true;
+      for (size_t off = 0; off < total && ok; off += chunk) {
+        hipMemGenericAllocationHandle_t h;
+        ok = hipMemCreate(&h, chunk, &prop, 0) == hipSuccess &&
+             hipMemMap((char*)va + off, chunk, 0, h, 0) == hipSuccess;
+        hs.push_back(h);
+      }
+      hipMemAccessDesc acc = {};
+      acc.location = prop.location;
+      acc.flags = hipMemAccessFlagsProtReadWrite;
+      ok = ok && hipMemSetAccess(va, total, &acc, 1) == hipSuccess;
+      char tag[96];
+      snprintf(tag, sizeof tag, "VMM chunks of %zu MB (%s)", chunk >> 20, ok ? "ok" : "FAILED");
+      if (ok) timepat((float*)va, tag); else printf("%s\n", tag);
+      hipMemUnmap(va, total);
+      for (auto h : hs) hipMemRelease(h);
+      hipMemAddressFree(va, total);
+    }
+  }
   return 0;
 }
