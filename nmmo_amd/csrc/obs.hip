@@ -51,6 +51,20 @@ __device__ inline void wave_zero(float* row, int lo, int hi) {
   if (tail0 + lane < hi) obs_st(&row[tail0 + lane], 0.f);
 }
 
+// zero bytes [lo, hi) of a row (lo, hi even): int16 stores up to 16-B alignment, then 16-B stores
+__device__ inline void wave_zero_bytes(uint8_t* row, int lo, int hi) {
+  const int lane = lane_id();
+  const uintptr_t a = reinterpret_cast<uintptr_t>(row + lo);
+  int head = (int)((16 - (a & 15)) & 15);
+  if (head > hi - lo) head = hi - lo;
+  if (2 * lane < head) reinterpret_cast<int16_t*>(row + lo)[lane] = 0;
+  const int body = (hi - lo - head) >> 4;
+  uint4* p4 = reinterpret_cast<uint4*>(row + lo + head);
+  for (int i = lane; i < body; i += 64) p4[i] = make_uint4(0u, 0u, 0u, 0u);
+  const int t0 = lo + head + body * 16;
+  if (t0 + 2 * lane < hi) reinterpret_cast<int16_t*>(row + t0)[lane] = 0;
+}
+
 // native layout (SPEC §8b): int16 part offsets, env stride, two int16 per dword store
 constexpr int kNatEntity = 2, kNatInv = kNatEntity + kNObs * NMMO_N_ENTITY_COLS,
               kNatTile = kNatInv + kInv * 16, kNatTask = kNatTile + 225 * 3;
@@ -443,14 +457,18 @@ __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
     int16_t* d16 = reinterpret_cast<int16_t*>(nrow + NMMO_NATIVE_MASK_BYTES);
     if (lane == 0) d16[0] = (int16_t)aid;
     if (lane == 1) d16[1] = (int16_t)tick;
-    {  // two entity rows per pass: lanes 0-30 row k, lanes 32-62 row k + 1, one column each
+    {  // two entity rows per pass: lanes 0-30 row k, lanes 32-62 row k + 1, one column each;
+       // the rows past the visible ones as one zero run
       const int f = lane & 31, half = lane >> 5;
+      const int nv2 = (m.nv + 1) & ~1;
 #pragma unroll 1
-      for (int k0 = 0; k0 < kNObs; k0 += 2) {
+      for (int k0 = 0; k0 < nv2; k0 += 2) {
         const int k = k0 + half;
         if (f < NMMO_N_ENTITY_COLS)
           d16[kNatEntity + k * NMMO_N_ENTITY_COLS + f] = k < m.nv ? T[f * S + vis[k]] : (int16_t)0;
       }
+      wave_zero_bytes(nrow, NMMO_NATIVE_MASK_BYTES + 2 * (kNatEntity + nv2 * NMMO_N_ENTITY_COLS),
+                      NMMO_NATIVE_MASK_BYTES + 2 * kNatInv);
     }
     for (int k = lane; k < kInv * 16; k += 64) {
       const int q = k >> 4;

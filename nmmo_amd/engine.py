@@ -52,7 +52,9 @@ class NmmoEngine:
 
             self.obs = devmem.empty((n, P, self.obs_elems), torch.float32, d)
         elif config.obs_layout == abi.OBS_NATIVE:  # SPEC §8b: per env, P rows + the Market
-            self.obs = torch.empty((n, abi.native_env_bytes(P)), dtype=torch.uint8, device=d)
+            from . import devmem
+
+            self.obs = devmem.empty((n, abi.native_env_bytes(P)), torch.uint8, d)
         else:
             self.obs = None
         emb = np.zeros((1, config.TASK_EMBED_DIM), np.float32) if task is None else \
