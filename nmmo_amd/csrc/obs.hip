@@ -27,7 +27,9 @@ constexpr int kObsFields = F_DS_ROW + 1;  // 0..30 obs columns, alive, ds_row
 __host__ __device__ inline size_t obs_lds_bytes(int S, bool native) {
   return (((size_t)kObsFields * S * 2 + 15) & ~(size_t)15) + (((size_t)(S + 1) * 2 + 15) & ~(size_t)15) +
          (size_t)kObsWaves * 128 * 2 + (size_t)kObsWaves * kInv * 8 +
-         (size_t)kObsWaves * 256 + (native ? (size_t)NMMO_MARKET_ROWS * 2 : (size_t)NMMO_MARKET_ROWS * 10);
+         (size_t)kObsWaves * 256 +
+         (native ? (size_t)NMMO_MARKET_ROWS * 2 + (size_t)kObsWaves * NMMO_NATIVE_MASK_BYTES
+                 : (size_t)NMMO_MARKET_ROWS * 10);
 }
 
 // Plain (temporal) stores. Measured on MI355X (same-box A/B): __builtin_nontemporal_store
@@ -182,6 +184,7 @@ __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
   uint2* mitem = inv_all + kObsWaves * kInv;  // flat only: listed item words
   uint16_t* mpo = reinterpret_cast<uint16_t*>(kNative ? mitem : mitem + NMMO_MARKET_ROWS);  // price | owner << 8
   uint8_t* wmat_all = reinterpret_cast<uint8_t*>(mpo + NMMO_MARKET_ROWS);  // per-wave 15x15 materials
+  uint8_t* mask_all = wmat_all + kObsWaves * 256;  // native: per-wave ActionTargets bytes (16-B aligned)
   const int e = blockIdx.x, g = blockIdx.y;
   const int tid = threadIdx.x;
   const int nm = p.mcount[e];
@@ -417,7 +420,9 @@ __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
     // entries, the longest section): four entries per lane per dword store from one 8-B LDS read
     // of the packed listings (the section starts dword-aligned in the SPEC §8b layout; the
     // per-byte case of mask_value covers any other offset)
-    uint8_t* mb = nrow;
+    // (built in this wave's LDS, then written out with 16-B stores: 100 instead of ~40 byte-store
+    // instructions per row)
+    uint8_t* mb = mask_all + w * NMMO_NATIVE_MASK_BYTES;
     const bool buy4 = (p.o_buy & 3) == 0;
     if (buy4) {
       uint32_t* b32 = reinterpret_cast<uint32_t*>(mb + p.o_buy);
@@ -452,6 +457,10 @@ __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
       }
     }
     if (lane < NMMO_NATIVE_MASK_BYTES - p.o_agent_id) mb[p.o_agent_id + lane] = 0;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    for (int k = lane; k < NMMO_NATIVE_MASK_BYTES / 16; k += 64)
+      reinterpret_cast<uint4*>(nrow)[k] = reinterpret_cast<const uint4*>(mb)[k];
     // int16 part: AgentId, CurrentTick, Entity 100x31, Inventory 12x16, Tile 225x3, task index,
     // zero pads (SPEC §8b)
     int16_t* d16 = reinterpret_cast<int16_t*>(nrow + NMMO_NATIVE_MASK_BYTES);
