@@ -34,6 +34,7 @@ C1 leg (BASELINE.json configs[0]).
 from __future__ import annotations
 
 import argparse
+import contextlib
 import json
 import os
 import socket
@@ -99,16 +100,20 @@ def obs_bytes_per_env(S: int, P: int, elems: int, native: bool = False) -> int:
 def pmc_traffic(cfg_name: str, kernel: str, envs: int):
     """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary of the
     same workload (profiles/<round>/<cfg>/pmc.json, tools/pmc_summary.py): 2 x FETCH_SIZE +
-    WRITE_SIZE, gfx950-corrected. None when no summary matches this workload."""
+    WRITE_SIZE, gfx950-corrected, scaled per env to a launch of `envs` envs (the summary's
+    launches covered its roofline.envs_per_launch, or its envs_per_gpu). None when no summary
+    matches this workload."""
     import glob
 
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", cfg_name, "pmc.json")), reverse=True):
         try:
             d = json.load(open(path))
             k = d["kernels"][kernel]
-            if d.get("bench", {}).get("config", {}).get("envs_per_gpu") != envs:
+            b = d.get("bench", {})
+            pe = b.get("roofline", {}).get("envs_per_launch") or b.get("config", {}).get("envs_per_gpu")
+            if not pe:
                 continue
-            return k["hbm_bytes_per_dispatch"], os.path.relpath(path, ROOT)
+            return round(k["hbm_bytes_per_dispatch"] * envs / pe), os.path.relpath(path, ROOT)
         except (KeyError, ValueError, OSError):
             continue
     return None, None
@@ -129,6 +134,11 @@ def parse(argv=None):
     ap.add_argument("--no-extras", action="store_true", help="skip the extra_configs at N = 1")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraph replay")
     ap.add_argument("--graph-steps", type=int, default=10, help="ticks captured per hipGraph")
+    ap.add_argument("--batches", type=int, default=2,
+                    help="obs workloads: env batches per GPU, each on its own stream (1 = lockstep)")
+    ap.add_argument("--overlap", choices=("free", "chained"), default="free",
+                    help="--batches > 1: per-stream hipGraphs the hardware interleaves (free), or "
+                         "eager steps whose obs gathers wait for each other (chained)")
     ap.add_argument("--obs", default=None, choices=["flat", "native"],
                     help="obs layout for the obs configs (default: flat for C4 = the pufferlib row "
                          "the reference's learner reads, native for C5 = SURVEY §8e's gather layout)")
@@ -250,7 +260,13 @@ def cpu_baseline(cfg, seconds: float):
 
 # ------------------------------------------------------------------------------- GPU workload
 def measure(args, name, layout_name, envs, rank, world, dev, steps, warmup, dist=None):
-    """Build, stagger, warm up and time one workload on this rank; returns a result dict."""
+    """Build, stagger, warm up and time one workload on this rank; returns a result dict.
+
+    With obs (and no learner gather) the rank's envs run as `--batches` batches (one handle each,
+    consecutive global env indices, so the rollout is the same as one handle's) on their own
+    streams (issue()): a batch's policy and tick run under another batch's HBM-bound obs writes,
+    as the reference's async pool (config.yaml env_pool: True) overlaps env batches. Every env
+    still ticks and writes its obs once per step."""
     import numpy as np
     import torch
 
@@ -266,75 +282,117 @@ def measure(args, name, layout_name, envs, rank, world, dev, steps, warmup, dist
     gpath = os.path.join(ROOT, "tests", "golden", "task_embeddings.npz")
     if os.path.exists(gpath):
         task = np.load(gpath)["heldout_emb"][0]  # TickGE(1024) task, SURVEY §8d
-    eng = NmmoEngine(cfg, envs, seed=args.seed, device=dev, task_embedding=task,
-                     env_index_base=rank * envs)
-    if args.wrapper != "none":
-        from nmmo_amd.wrappers import wrapper_config
+    gather = wl.get("gather", False)
+    nb = max(1, args.batches) if (wl["obs"] and not gather) else 1
+    if envs % nb:
+        raise SystemExit(f"--batches {nb} must divide the {envs} envs per GPU")
+    per = envs // nb
+    engs = [NmmoEngine(cfg, per, seed=args.seed, device=dev, task_embedding=task,
+                       env_index_base=rank * envs + i * per) for i in range(nb)]
+    eng = engs[0]
+    for e in engs:
+        if args.wrapper != "none":
+            from nmmo_amd.wrappers import wrapper_config
 
-        eng.set_wrapper(wrapper_config(args.wrapper, **WRAPPER_KW.get(args.wrapper, {})))
-    eng.reset()
+            e.set_wrapper(wrapper_config(args.wrapper, **WRAPPER_KW.get(args.wrapper, {})))
+        e.reset()
     pseed = args.seed * 1_000_003  # the policy's Philox counter already walks (tick, episode)
     # staggered episode phases (module docstring): untimed, obs not gathered during the pre-roll
     L = max(0, args.stagger)
-    ids = np.arange(envs) + rank * envs
     for k in range(L):
-        eng.end_episodes(ids % L == k)
-        eng.scripted_actions(pseed)
-        eng.step(write_obs=False)
+        for i, e in enumerate(engs):
+            ids = np.arange(per) + rank * envs + i * per
+            e.end_episodes(ids % L == k)
+            e.scripted_actions(pseed)
+            e.step(write_obs=False)
     # device counters the tick kernel adds into: [0] = sum(mask) (agent-steps), [1] = episodes,
     # [2] = event-log rows appended
-    counters = torch.zeros(3, dtype=torch.int64, device=dev)
-    eng.set_counters(counters)
+    counters = [torch.zeros(3, dtype=torch.int64, device=dev) for _ in engs]
+    for e, c in zip(engs, counters):
+        e.set_counters(c)
+    # nb > 1: all side streams (a capture cannot run on the legacy default stream)
+    streams = [torch.cuda.current_stream(dev)] if nb == 1 else [torch.cuda.Stream(device=dev) for _ in engs]
 
-    gather = wl.get("gather", False)
-    one, step_events = None, None
+    one = None
     if gather:
         one = _gather_stepper(eng, cfg, envs, rank, world, dev, pseed, dist)
-    else:
-        def one():
-            eng.scripted_actions(pseed)
-            eng.step()
 
-    for _ in range(warmup):
-        one()
+    chained = nb > 1 and args.overlap == "chained"
+
+    def issue(k, batches=None):
+        """k steps of the given batches (default: all), each on its own stream (nb == 1: the
+        current one). "free": batch j's steps (policy + nmmo_step with obs) queue on stream j
+        and the hardware interleaves the streams. "chained" (eager only): batch j's obs gather
+        (nmmo_observe after nmmo_step without obs) waits for batch j-1's gather of the same step,
+        so the HBM-bound gathers run one at a time and each batch's policy + tick overlap
+        another's gather."""
+        if gather:
+            for _ in range(k):
+                one()
+            return
+        idx = range(nb) if batches is None else batches
+        if not chained:
+            for j in idx:
+                with torch.cuda.stream(streams[j]) if nb > 1 else contextlib.nullcontext():  # nb == 1: the
+                    # current stream, which is torch's capture stream inside torch.cuda.graph
+                    for _ in range(k):
+                        engs[j].scripted_actions(pseed)
+                        engs[j].step()
+            return
+        prev = None
+        for _ in range(k):
+            for j in idx:
+                with torch.cuda.stream(streams[j]):
+                    engs[j].scripted_actions(pseed)
+                    engs[j].step(write_obs=False)
+                    if prev is not None:
+                        streams[j].wait_event(prev)
+                    engs[j].observe()
+                    prev = torch.cuda.Event()
+                    prev.record(streams[j])
+
+    torch.cuda.synchronize(dev)  # the pre-roll ran on the default stream
+    issue(warmup)
     torch.cuda.synchronize(dev)
-    graphs = []
-    if not args.no_graph and not gather:  # the step is capture-safe: no sync / alloc inside nmmo_step
+    plans = []  # per batch: the hipGraphs its stream replays
+    if not args.no_graph and not gather and not chained:  # capture-safe: no sync / alloc in nmmo_step
         g_n = max(1, min(args.graph_steps, steps))
-        for n in sorted({g_n, steps % g_n} - {0}):
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                for _ in range(n):
-                    one()
-            graphs.append((n, g))
+        q, r = divmod(steps, g_n)
+        for j in range(nb):
+            graphs = {}
+            for n in sorted({g_n, r} - {0}):
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=streams[j] if nb > 1 else None):
+                    issue(n, [j])
+                graphs[n] = g
+            plans.append([graphs[g_n]] * q + ([graphs[r]] if r else []))
         torch.cuda.synchronize(dev)
-    plan = []
-    if graphs:
-        big = max(graphs, key=lambda x: x[0])
-        q, r = divmod(steps, big[0])
-        plan = [big[1]] * q + [g for n, g in graphs if n == r and r]
-    counters.zero_()
+    for c in counters:
+        c.zero_()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    if plan:
-        for g in plan:
-            g.replay()
+    if plans:
+        for k in range(len(plans[0])):
+            for j in range(nb):
+                with torch.cuda.stream(streams[j]) if nb > 1 else contextlib.nullcontext():
+                    plans[j][k].replay()
     else:
-        for _ in range(steps):
-            one()
+        issue(steps)
     if gather:
         one.drain()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    alive = float(counters[0].item())
-    episodes = int(counters[1].item())
-    events_per_env_tick = float(counters[2].item()) / (envs * steps) if cfg.event_cap > 0 else None
+    tot = torch.stack(counters).sum(0)
+    alive = float(tot[0].item())
+    episodes = int(tot[1].item())
+    events_per_env_tick = float(tot[2].item()) / (envs * steps) if cfg.event_cap > 0 else None
     # per-kernel durations: HIP events on the launch stream around each kernel of nmmo_step,
-    # over an equal number of eager steps right after the timed region (same state stream)
+    # over an equal number of eager steps right after the timed region (same state stream), one
+    # batch alone (no overlap): a launch covers `per` envs
     eng.set_timing(True)
     for _ in range(min(steps, 8192)):
         eng.scripted_actions(pseed)
@@ -374,43 +432,47 @@ def measure(args, name, layout_name, envs, rank, world, dev, steps, warmup, dist
     tick_avg_ms = tick_ms / max(n_timed, 1)
     obs_avg_ms = obs_ms / max(n_timed, 1)
     slim = not any(x in cfg.systems for x in ("Item", "Equipment", "Profession", "Exchange"))
-    tick_b = tick_bytes_per_env(S, P, "Item" in cfg.systems, events_per_env_tick or 0.0, slim) * envs
-    obs_b = obs_bytes_per_env(S, P, eng.obs_elems, native) * envs if wl["obs"] else 0
+    tick_b = tick_bytes_per_env(S, P, "Item" in cfg.systems, events_per_env_tick or 0.0, slim) * per
+    obs_b = obs_bytes_per_env(S, P, eng.obs_elems, native) * per if wl["obs"] else 0
     if wl["obs"] and obs_avg_ms > tick_avg_ms:
         kern, byts, ms = "obs_kernel", obs_b, obs_avg_ms
         timing = "HIP events around each obs_kernel launch on the launch stream"
     else:
         kern, byts, ms = "tick_kernel", tick_b, tick_avg_ms
         timing = "HIP events around each tick_kernel launch on the launch stream"
-        if not wl["obs"] and args.wrapper == "none" and plan:
+        if not wl["obs"] and args.wrapper == "none" and plans:
             ms = elapsed * 1e3 / steps - policy_avg_ms  # nmmo_step = the tick kernel alone
             timing = (f"timed step (hipGraph: policy + tick) minus a {batch}-launch policy-only "
                       f"hipGraph, HIP events on the launch stream")
     achieved = byts / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
     prof_name = name + ("-native" if native and name != "C5" else "")
-    traffic, traffic_src = pmc_traffic(prof_name, kern, envs)
+    traffic, traffic_src = pmc_traffic(prof_name, kern, per)
+    launch = "eager" if not plans else f"hipGraph x{min(args.graph_steps, steps)} ticks"
+    if nb > 1:
+        launch += f", {nb} batches of {per} envs on {nb} streams ({args.overlap})"
     res = {
         "name": prof_name, "envs": envs, "cfg": cfg, "native": native, "S": S, "P": P,
         "elapsed": elapsed, "alive": alive, "slots": float(envs * P * steps), "episodes": episodes,
-        "events_per_env_tick": events_per_env_tick, "gather": gather,
-        "launch": "eager" if (args.no_graph or gather) else f"hipGraph x{min(args.graph_steps, steps)} ticks",
+        "events_per_env_tick": events_per_env_tick, "gather": gather, "launch": launch,
         "kernel_ms": {"policy": round(policy_avg_ms, 5), "tick": round(tick_avg_ms, 5),
                       "obs": round(obs_avg_ms, 5) if wl["obs"] else None,
                       "wrapper": round(wrap_ms / max(n_timed, 1), 5) if args.wrapper != "none" else None},
         "roofline": {
             "kernel": kern, "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-            "traffic_source": traffic_src, "bytes_per_launch": byts, "avg_launch_ms": round(ms, 5),
-            "timing": timing,
+            "traffic_source": traffic_src, "bytes_per_launch": byts, "envs_per_launch": per,
+            "avg_launch_ms": round(ms, 5), "timing": timing,
             "write_ceiling_gbs": None if fill_gbs is None else round(fill_gbs, 1),
             "frac_of_write_ceiling": None if not fill_gbs or kern != "obs_kernel" else round(achieved / fill_gbs, 4),
         },
         "gather_bytes": getattr(one, "bytes_per_step", None),
+        "batches": nb,
     }
     if gather:
         one.close()
-    eng.close()
-    del eng
+    for e in engs:
+        e.close()
+    del eng, engs
     torch.cuda.empty_cache()
     return res
 
@@ -529,6 +591,7 @@ def result_line(res, args, world, steps, alive_total, slots_total, elapsed, warm
                     "pufferlib-flat fp32 (23,987/agent)") if WORKLOADS[res["name"].split("-")[0]]["obs"] else "none",
             "early_stop_agent_num": 8,
             "stagger_ticks": args.stagger,
+            "env_batches": res["batches"],
             "parallelism": f"env-shard x{world}",
         },
         "slot_steps_per_sec": round(slots_total / elapsed, 1),
@@ -545,8 +608,11 @@ def main():
     args = parse()
     world_env = os.environ.get("WORLD_SIZE")
     if args.dry_launch and world_env is not None:
-        print(json.dumps({"rank": int(os.environ["RANK"]), "world_size": int(world_env),
-                          "local_rank": int(os.environ.get("LOCAL_RANK", "0"))}), flush=True)
+        # one write() per line: the ranks share the launcher's stdout pipe, and print() issues the
+        # text and its newline as two writes that another rank's line can land between
+        sys.stdout.write(json.dumps({"rank": int(os.environ["RANK"]), "world_size": int(world_env),
+                                     "local_rank": int(os.environ.get("LOCAL_RANK", "0"))}) + "\n")
+        sys.stdout.flush()
         return 0
     if world_env is None and args.gpus > 1:
         return launch_ranks(args)

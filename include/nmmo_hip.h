@@ -290,6 +290,13 @@ NMMO_API int nmmo_end_episodes(NmmoHandle* h, const uint8_t* host_env_mask);
 NMMO_API int nmmo_step(NmmoHandle* h, const int32_t* actions, void* obs, float* rew, uint8_t* term,
               uint8_t* trunc, uint8_t* mask, void* stream);
 
+/* The observation gather alone, over the envs' current state (what nmmo_step's obs argument
+ * writes after the tick): nmmo_step(obs = NULL) followed by nmmo_observe(obs) on the same stream
+ * gives the same bytes as nmmo_step(obs). Replaces nmmo.Env._compute_observations, the second
+ * half of nmmo.Env.step; lets a caller with several handles order their
+ * HBM-bound gathers apart from their ticks (bench.py --batches). Graph-capturable. */
+NMMO_API int nmmo_observe(NmmoHandle* h, void* obs, void* stream);
+
 /* Task table and per-player assignment (SPEC.md §12; nmmo.Env.reset(make_task_fn) /
  * agent_task_map). tasks: host [n_tasks] (1..NMMO_MAX_TASKS); embeddings: host fp16
  * [n_tasks][task_embed_dim] used as each player's Task obs (NULL = keep the create-time

@@ -25,7 +25,7 @@ SYMBOLS = [
     "nmmo_exp_store", "nmmo_exp_sort", "nmmo_exp_gae", "nmmo_gather_rows", "nmmo_n_envs",
     "nmmo_last_error", "nmmo_abi_version", "nmmo_end_episodes", "nmmo_build_info",
     "nmmo_get_wrapper_dropped", "nmmo_set_task_weights", "nmmo_wire_header_bytes", "nmmo_wire_max_bytes",
-    "nmmo_wire_pack", "nmmo_wire_unpack", "nmmo_dev_alloc", "nmmo_dev_free",
+    "nmmo_wire_pack", "nmmo_wire_unpack", "nmmo_dev_alloc", "nmmo_dev_free", "nmmo_observe",
 ]
 
 
@@ -68,6 +68,7 @@ def lib():
     L.nmmo_set_wrapper.argtypes = [vp, ctypes.POINTER(abi.NmmoWrapperConfig), vp]
     L.nmmo_get_wrapper_state.argtypes = [vp, vp, vp]
     L.nmmo_expand_obs.argtypes = [vp, vp, vp, i32, vp]
+    L.nmmo_observe.argtypes = [vp, vp, vp]
     xp = ctypes.POINTER(abi.NmmoExperience)
     L.nmmo_exp_scratch_ints.argtypes = [i32, i32]
     L.nmmo_exp_scratch_ints.restype = ctypes.c_int64

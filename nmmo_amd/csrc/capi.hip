@@ -353,6 +353,13 @@ int nmmo_step(NmmoHandle* h, const int32_t* actions, void* obs, float* rew, uint
   return NMMO_OK;
 }
 
+int nmmo_observe(NmmoHandle* h, void* obs, void* stream) {
+  if (!h || !obs) return fail(NMMO_E_INVALID, "null argument");
+  if (h->cfg.obs_layout == NMMO_OBS_NONE) return fail(NMMO_E_INVALID, "handle built with NMMO_OBS_NONE");
+  HIP_TRY(launch_obs(obs_params(h, obs), (hipStream_t)stream));
+  return NMMO_OK;
+}
+
 int nmmo_expand_obs(NmmoHandle* h, const void* native, float* flat, int32_t n_envs, void* stream) {
   if (!h || !native || !flat) return fail(NMMO_E_INVALID, "null argument");
   if (n_envs <= 0) return fail(NMMO_E_INVALID, "n_envs must be > 0");

@@ -125,6 +125,14 @@ class NmmoEngine:
                                   self._stream()), "nmmo_step")
         return self.obs, self.rew, self.term, self.trunc, self.mask
 
+    def observe(self, out=None):
+        """The obs gather alone over the current state into `out` (default: the engine's obs
+        buffer): step(write_obs=False) + observe() == step() (nmmo_observe)."""
+        out = self.obs if out is None else out
+        with torch.cuda.device(self.device):
+            check(lib().nmmo_observe(self.h, self._ptr(out), self._stream()), "nmmo_observe")
+        return out
+
     def expand_obs(self, native=None, out=None):
         """Native obs (SPEC §8b; default: this engine's) -> pufferlib flat float32
         [n, P, obs_elems] on the device, bit-identical to the flat layout (nmmo_expand_obs)."""
