@@ -136,9 +136,6 @@ def parse(argv=None):
     ap.add_argument("--graph-steps", type=int, default=10, help="ticks captured per hipGraph")
     ap.add_argument("--batches", type=int, default=2,
                     help="obs workloads: env batches per GPU, each on its own stream (1 = lockstep)")
-    ap.add_argument("--overlap", choices=("free", "chained"), default="free",
-                    help="--batches > 1: per-stream hipGraphs the hardware interleaves (free), or "
-                         "eager steps whose obs gathers wait for each other (chained)")
     ap.add_argument("--obs", default=None, choices=["flat", "native"],
                     help="obs layout for the obs configs (default: flat for C4 = the pufferlib row "
                          "the reference's learner reads, native for C5 = SURVEY §8e's gather layout)")
@@ -317,45 +314,25 @@ def measure(args, name, layout_name, envs, rank, world, dev, steps, warmup, dist
     if gather:
         one = _gather_stepper(eng, cfg, envs, rank, world, dev, pseed, dist)
 
-    chained = nb > 1 and args.overlap == "chained"
-
     def issue(k, batches=None):
-        """k steps of the given batches (default: all), each on its own stream (nb == 1: the
-        current one). "free": batch j's steps (policy + nmmo_step with obs) queue on stream j
-        and the hardware interleaves the streams. "chained" (eager only): batch j's obs gather
-        (nmmo_observe after nmmo_step without obs) waits for batch j-1's gather of the same step,
-        so the HBM-bound gathers run one at a time and each batch's policy + tick overlap
-        another's gather."""
+        """k steps of the given batches (default: all): batch j's steps (policy + nmmo_step) queue
+        on stream j (nb == 1: the current stream, torch's capture stream inside
+        torch.cuda.graph), and the hardware interleaves the streams."""
         if gather:
             for _ in range(k):
                 one()
             return
-        idx = range(nb) if batches is None else batches
-        if not chained:
-            for j in idx:
-                with torch.cuda.stream(streams[j]) if nb > 1 else contextlib.nullcontext():  # nb == 1: the
-                    # current stream, which is torch's capture stream inside torch.cuda.graph
-                    for _ in range(k):
-                        engs[j].scripted_actions(pseed)
-                        engs[j].step()
-            return
-        prev = None
-        for _ in range(k):
-            for j in idx:
-                with torch.cuda.stream(streams[j]):
+        for j in (range(nb) if batches is None else batches):
+            with torch.cuda.stream(streams[j]) if nb > 1 else contextlib.nullcontext():
+                for _ in range(k):
                     engs[j].scripted_actions(pseed)
-                    engs[j].step(write_obs=False)
-                    if prev is not None:
-                        streams[j].wait_event(prev)
-                    engs[j].observe()
-                    prev = torch.cuda.Event()
-                    prev.record(streams[j])
+                    engs[j].step()
 
     torch.cuda.synchronize(dev)  # the pre-roll ran on the default stream
     issue(warmup)
     torch.cuda.synchronize(dev)
     plans = []  # per batch: the hipGraphs its stream replays
-    if not args.no_graph and not gather and not chained:  # capture-safe: no sync / alloc in nmmo_step
+    if not args.no_graph and not gather:  # capture-safe: no sync / alloc inside nmmo_step
         g_n = max(1, min(args.graph_steps, steps))
         q, r = divmod(steps, g_n)
         for j in range(nb):
@@ -392,7 +369,9 @@ def measure(args, name, layout_name, envs, rank, world, dev, steps, warmup, dist
     events_per_env_tick = float(tot[2].item()) / (envs * steps) if cfg.event_cap > 0 else None
     # per-kernel durations: HIP events on the launch stream around each kernel of nmmo_step,
     # over an equal number of eager steps right after the timed region (same state stream), one
-    # batch alone (no overlap): a launch covers `per` envs
+    # batch alone (no overlap): a launch covers `per` envs. rocprofv3's kernel trace of the same
+    # command splits these solo dispatches from the overlapped ones of the timed region
+    # (tools/pmc_summary.py solo_avg_ns / overlapped_avg_ns).
     eng.set_timing(True)
     for _ in range(min(steps, 8192)):
         eng.scripted_actions(pseed)
@@ -449,7 +428,7 @@ def measure(args, name, layout_name, envs, rank, world, dev, steps, warmup, dist
     traffic, traffic_src = pmc_traffic(prof_name, kern, per)
     launch = "eager" if not plans else f"hipGraph x{min(args.graph_steps, steps)} ticks"
     if nb > 1:
-        launch += f", {nb} batches of {per} envs on {nb} streams ({args.overlap})"
+        launch += f", {nb} batches of {per} envs on {nb} streams"
     res = {
         "name": prof_name, "envs": envs, "cfg": cfg, "native": native, "S": S, "P": P,
         "elapsed": elapsed, "alive": alive, "slots": float(envs * P * steps), "episodes": episodes,
@@ -462,6 +441,10 @@ def measure(args, name, layout_name, envs, rank, world, dev, steps, warmup, dist
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
             "traffic_source": traffic_src, "bytes_per_launch": byts, "envs_per_launch": per,
             "avg_launch_ms": round(ms, 5), "timing": timing,
+            # the dominant kernel's bytes of a whole step over the timed step time: a floor on
+            # its in-run rate (policy and tick share the step; --batches overlaps them)
+            "timed_step_gbs": round(byts * nb / (elapsed / steps) / 1e9, 1),
+            "concurrent_batches": nb,
             "write_ceiling_gbs": None if fill_gbs is None else round(fill_gbs, 1),
             "frac_of_write_ceiling": None if not fill_gbs or kern != "obs_kernel" else round(achieved / fill_gbs, 4),
         },

@@ -5,5 +5,3 @@ for b in 2 1 2; do
   timeout -k 10 300 python bench.py --no-extras --no-cpu-baseline --batches $b "$@" > gpurun_out/bb$b.json 2> gpurun_out/bb$b.err || exit 1
   python -c "import json;d=json.loads(open('gpurun_out/bb$b.json').read().strip().splitlines()[-1]);print('batches',$b,round(d['value']/1e6,2),d['ms_per_step'],d['kernel_ms'],d['roofline']['frac'],d['launch'])"
 done
-timeout -k 10 300 python bench.py --no-extras --no-cpu-baseline --batches 2 --overlap chained "$@" > gpurun_out/bbc.json 2> gpurun_out/bbc.err || exit 1
-python -c "import json;d=json.loads(open('gpurun_out/bbc.json').read().strip().splitlines()[-1]);print('chained',round(d['value']/1e6,2),d['ms_per_step'],d['kernel_ms'],d['roofline']['frac'],d['launch'])"

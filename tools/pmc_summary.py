@@ -38,6 +38,21 @@ def summarise(d):
         k = _short(r["Name"])
         out[k]["dispatches"] = int(r["Calls"])
         out[k]["avg_ns"] = float(r["AverageNs"])
+    # dispatches that ran alone vs while another dispatch of the same kernel ran (bench.py
+    # --batches > 1 overlaps the batches' streams; its roofline times launches alone)
+    spans = defaultdict(list)
+    for r in _rows(os.path.join(d, "trace", "**", "*kernel_trace.csv")):
+        spans[_short(r["Kernel_Name"])].append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
+    for k, sp in spans.items():
+        sp.sort()
+        solo, over = [], []
+        for i, (a, b) in enumerate(sp):
+            hit = (i > 0 and max(e for _, e in sp[max(0, i - 8):i]) > a) or (i + 1 < len(sp) and sp[i + 1][0] < b)
+            (over if hit else solo).append(b - a)
+        out[k]["solo_dispatches"] = len(solo)
+        out[k]["solo_avg_ns"] = round(sum(solo) / len(solo), 1) if solo else None
+        out[k]["overlapped_dispatches"] = len(over)
+        out[k]["overlapped_avg_ns"] = round(sum(over) / len(over), 1) if over else None
     for sub, ctr in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
         acc = defaultdict(list)
         for r in _rows(os.path.join(d, sub, "**", "*counter_collection.csv")):
