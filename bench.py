@@ -135,7 +135,7 @@ def parse(argv=None):
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraph replay")
     ap.add_argument("--graph-steps", type=int, default=10, help="ticks captured per hipGraph")
     ap.add_argument("--batches", type=int, default=2,
-                    help="obs workloads: env batches per GPU, each on its own stream (1 = lockstep)")
+                    help="env batches per GPU, each on its own stream (1 = one handle in lockstep)")
     ap.add_argument("--obs", default=None, choices=["flat", "native"],
                     help="obs layout for the obs configs (default: flat for C4 = the pufferlib row "
                          "the reference's learner reads, native for C5 = SURVEY §8e's gather layout)")
@@ -259,11 +259,12 @@ def cpu_baseline(cfg, seconds: float):
 def measure(args, name, layout_name, envs, rank, world, dev, steps, warmup, dist=None):
     """Build, stagger, warm up and time one workload on this rank; returns a result dict.
 
-    With obs (and no learner gather) the rank's envs run as `--batches` batches (one handle each,
+    Without the learner gather the rank's envs run as `--batches` batches (one handle each,
     consecutive global env indices, so the rollout is the same as one handle's) on their own
-    streams (issue()): a batch's policy and tick run under another batch's HBM-bound obs writes,
-    as the reference's async pool (config.yaml env_pool: True) overlaps env batches. Every env
-    still ticks and writes its obs once per step."""
+    streams (issue()), as the reference's async pool (config.yaml env_pool: True) overlaps env
+    batches: with obs, a batch's policy and tick run under another batch's HBM-bound obs writes;
+    without, one batch's bandwidth-bound state load overlaps the other's issue-bound phases.
+    Every env still ticks (and writes its obs) once per step."""
     import numpy as np
     import torch
 
@@ -280,7 +281,7 @@ def measure(args, name, layout_name, envs, rank, world, dev, steps, warmup, dist
     if os.path.exists(gpath):
         task = np.load(gpath)["heldout_emb"][0]  # TickGE(1024) task, SURVEY §8d
     gather = wl.get("gather", False)
-    nb = max(1, args.batches) if (wl["obs"] and not gather) else 1
+    nb = 1 if gather else max(1, args.batches)
     if envs % nb:
         raise SystemExit(f"--batches {nb} must divide the {envs} envs per GPU")
     per = envs // nb
@@ -395,6 +396,21 @@ def measure(args, name, layout_name, envs, rank, world, dev, steps, warmup, dist
     b1.record()
     torch.cuda.synchronize(dev)
     policy_avg_ms = b0.elapsed_time(b1) / (reps * batch)
+    solo_step_ms = None
+    if not wl["obs"] and args.wrapper == "none" and plans and nb > 1:
+        # one batch alone (the timed region overlaps the batches): a hipGraph of `batch` steps
+        step_graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(step_graph):
+            for _ in range(batch):
+                eng.scripted_actions(pseed)
+                eng.step()
+        step_graph.replay()
+        b0.record()
+        for _ in range(reps):
+            step_graph.replay()
+        b1.record()
+        torch.cuda.synchronize(dev)
+        solo_step_ms = b0.elapsed_time(b1) / (reps * batch)
     # practical HBM write ceiling on THIS box: the vendor fill kernel over the same obs buffer
     fill_gbs = None
     if wl["obs"]:
@@ -420,9 +436,15 @@ def measure(args, name, layout_name, envs, rank, world, dev, steps, warmup, dist
         kern, byts, ms = "tick_kernel", tick_b, tick_avg_ms
         timing = "HIP events around each tick_kernel launch on the launch stream"
         if not wl["obs"] and args.wrapper == "none" and plans:
-            ms = elapsed * 1e3 / steps - policy_avg_ms  # nmmo_step = the tick kernel alone
-            timing = (f"timed step (hipGraph: policy + tick) minus a {batch}-launch policy-only "
-                      f"hipGraph, HIP events on the launch stream")
+            if nb == 1:
+                ms = elapsed * 1e3 / steps - policy_avg_ms  # nmmo_step = the tick kernel alone
+                timing = (f"timed step (hipGraph: policy + tick) minus a {batch}-launch policy-only "
+                          f"hipGraph, HIP events on the launch stream")
+            else:
+                ms = solo_step_ms - policy_avg_ms
+                timing = (f"one batch alone after the timed region: a {batch}-step hipGraph (policy + "
+                          f"tick) minus a {batch}-launch policy-only hipGraph, HIP events on the "
+                          f"launch stream")
     achieved = byts / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
     prof_name = name + ("-native" if native and name != "C5" else "")
     traffic, traffic_src = pmc_traffic(prof_name, kern, per)

@@ -75,6 +75,9 @@ struct Ctx {
   int n_tasks;
   NmmoTaskState* ts;    // [P] task state: == tsl when staged (task events on), else in HBM
   NmmoTaskState* tsl;   // LDS staging of ts (meaningful only when tev)
+  NmmoTaskState* tsg;   // this env's task state in HBM. Accessed through tsl/tsg, never ts, on the
+                        // hot path: ts may point to either, so its accesses are flat, and a flat
+                        // load makes the next LDS wait (lgkmcnt) wait for HBM too
   int4* tdesc;             // LDS [128][2] (pred, a, b, c) of each player's terms (when tev)
   bool tev;
   int evcap, tick1;  // ring rows (0 = no event log); tick + 1 (the events' tick column)
@@ -209,6 +212,7 @@ __device__ __forceinline__ Ctx make_ctx(unsigned char* smem, const DevState& st,
   c.task_cum = st.task_cum;
   c.n_tasks = st.n_tasks;
   c.tsl = reinterpret_cast<NmmoTaskState*>(smem + o);  // an LDS address either way (copy_segs)
+  c.tsg = st.tstate + (size_t)e * st.P;
   if (c.tev) {
     c.ts = c.tsl;
     o += al((size_t)st.P * sizeof(NmmoTaskState));
@@ -1740,7 +1744,7 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
   NmmoTaskState tsr = {};
   NmmoTask tk = {};  // and its task (index loaded at tick start)
   if (s < P && c.pres[s] && !c.died[s]) {
-    if (!c.tev) tsr = c.ts[s];
+    if (!c.tev) tsr = c.tsg[s];
     tk = c.tasks[my_task];
   }
   // 5-6. tick += 1; map.step respawn of depleted tiles; exchange.step listing expiry.
@@ -1845,13 +1849,16 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
     if (c.pres[s] && c.died[s]) {
       rw = -1.f;
     } else if (c.pres[s]) {
-      NmmoTaskState ts = c.tev ? c.ts[s] : tsr;  // staged in LDS, or prefetched from HBM
+      NmmoTaskState ts = c.tev ? c.tsl[s] : tsr;  // staged in LDS, or prefetched from HBM
       const double np = task_progress(c, s, tk, ts.acc), d = np - ts.last;
       ts.last = np;
       if (np > ts.max_progress) ts.max_progress = np;
       if (d > 0.0) ts.signals += 1;
       if (np >= 1.0 && ts.completed_tick == 0) ts.completed_tick = tick + 1;
-      c.ts[s] = ts;
+      if (c.tev)
+        c.tsl[s] = ts;
+      else
+        c.tsg[s] = ts;
       rw = (float)d;
     }
     rew[s] = rw;
@@ -1919,8 +1926,12 @@ __device__ __forceinline__ void tick_body(const DevState& st, const int32_t* __r
     }
     __syncthreads();
     reset_env(c, seed, episode, env_global);
-    for (int i = threadIdx.x; i < c.P * (int)sizeof(NmmoTaskState) / 4; i += blockDim.x)
-      reinterpret_cast<int*>(c.ts)[i] = 0;  // task progress restarts with the episode
+    for (int i = threadIdx.x; i < c.P * (int)sizeof(NmmoTaskState) / 4; i += blockDim.x) {
+      if (c.tev)  // task progress restarts with the episode
+        reinterpret_cast<int*>(c.tsl)[i] = 0;
+      else
+        reinterpret_cast<int*>(c.tsg)[i] = 0;
+    }
     if (!c.items) {  // item state is not staged in LDS without the Item system; reset it in HBM
       for (int i = threadIdx.x; i < c.P * kInv; i += blockDim.x) st.items[(size_t)e * c.P * kInv + i] = make_uint2(0u, 0u);
       for (int i = threadIdx.x; i < c.IC; i += blockDim.x) st.iring[(size_t)e * c.IC + i] = (int16_t)(i + 1);

@@ -32,6 +32,12 @@ def main():
                         obs_layout=abi.OBS_FLAT if preset == "C4" else abi.OBS_NONE)
     eng = NmmoEngine(cfg, envs, seed=1)
     eng.reset()
+    stagger = int(os.environ.get("STAMPS_STAGGER", "0"))  # bench.py's staggered pre-roll
+    for k in range(stagger):
+        eng.end_episodes(np.arange(envs) % stagger == k)
+        eng.scripted_actions(1_000_003)
+        eng.step(write_obs=False)
+    totals = []
     L = _native.lib()
     L.nmmo_debug_read_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
     rows, subs = [], []
@@ -43,6 +49,8 @@ def main():
             buf = np.zeros(4096 * 32, np.uint64)
             assert L.nmmo_debug_read_stamps(buf.ctypes.data_as(ctypes.c_void_p), buf.size) == 0
             st = buf.reshape(4096, 32)[:min(envs, 4096), :12].astype(np.int64)
+            fin = st[:, 11] > st[:, 0]
+            totals.append(np.stack([st[fin, 11] - st[fin, 0], (st[fin, 2] > 0).astype(np.int64)], 1))
             ok = (st[:, 2] > 0) & (st[:, 11] > st[:, 0])  # stepped (not reset) envs
             d = np.diff(st[ok], axis=1)
             rows.append(d)
@@ -69,6 +77,12 @@ def main():
           f"{np.median(sub[:, 8]):9.0f} + draws {np.median(sub[:, 9]):9.0f} + expiry/tick {np.median(sub[:, 10]):9.0f}; "
           f"groups n/a")
     print(f"  rowslot phase: state load {np.median(sub[:, 11]):9.0f}")
+    tt = np.concatenate(totals)
+    for name, sel in (("stepped", tt[:, 1] == 1), ("reset", tt[:, 1] == 0)):
+        x = tt[sel, 0]
+        if len(x):
+            print(f"  {name:8s} env-ticks {len(x):6d}: total median {np.median(x):9.0f} p99 "
+                  f"{np.percentile(x, 99):9.0f} max {x.max():9.0f}")
 
 
 if __name__ == "__main__":
