@@ -492,11 +492,14 @@ def _gather_stepper(eng, cfg, envs, rank, world, dev, pseed, dist):
     travel as they are."""
     import torch
 
-    from nmmo_amd import abi, wire
+    from nmmo_amd import abi, devmem, wire
     from nmmo_amd import distributed as nd
 
+    def like(t):  # large obs buffers chunk-mapped like the engine's own (DESIGN §3.2)
+        return devmem.empty(tuple(t.shape), t.dtype, dev)
+
     native = eng.config.obs_layout == abi.OBS_NATIVE
-    bufs = [eng.obs, torch.empty_like(eng.obs)]
+    bufs = [eng.obs, like(eng.obs)]
     smalls = [torch.empty((envs, cfg.PLAYER_N, 8), dtype=torch.uint8, device=dev) for _ in range(2)]
     wires = [torch.empty(wire.max_bytes(envs, cfg.PLAYER_N), dtype=torch.uint8, device=dev)
              for _ in range(2)] if native and world > 1 else None
@@ -505,7 +508,7 @@ def _gather_stepper(eng, cfg, envs, rank, world, dev, pseed, dist):
     done_ev = [None, None]  # compute-stream wait: the exchange of the step that used this buffer
     recv = None
     if rank == 0 and world > 1:
-        recv = {r: {"obs": torch.empty_like(bufs[0]), "small": torch.empty_like(smalls[0]),
+        recv = {r: {"obs": like(bufs[0]), "small": torch.empty_like(smalls[0]),
                     "wire": torch.empty_like(wires[0]) if native else None} for r in range(1, world)}
 
     class Stepper:

@@ -51,10 +51,10 @@ def pack(engine, native: torch.Tensor | None = None, out: torch.Tensor | None = 
 
 def unpack(wire: torch.Tensor, n_envs: int, players: int, out: torch.Tensor | None = None) -> torch.Tensor:
     """Decode a wire buffer into the native layout [n_envs, env_bytes] (enqueued)."""
-    from . import abi
+    from . import abi, devmem
 
-    if out is None:
-        out = torch.empty((n_envs, abi.native_env_bytes(players)), dtype=torch.uint8, device=wire.device)
+    if out is None:  # the learner's native obs: chunk-mapped like the engine's (DESIGN §3.2)
+        out = devmem.empty((n_envs, abi.native_env_bytes(players)), torch.uint8, wire.device)
     with torch.cuda.device(wire.device):
         check(lib().nmmo_wire_unpack(n_envs, players, ctypes.c_void_p(wire.data_ptr()),
                                      ctypes.c_void_p(out.data_ptr()), _stream(wire.device)), "nmmo_wire_unpack")
