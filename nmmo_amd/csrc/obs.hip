@@ -151,6 +151,29 @@ __device__ __forceinline__ bool mask_value(const ObsParams& p, const int16_t* T,
   return v;
 }
 
+// Section kSec of the ActionTargets as u8 into a wave's LDS mask image: the section is a
+// template constant, so mask_section / mask_value fold to straight-line code (the generic
+// (section, chunk) loop spent ~1.3k scalar and branch instructions per agent on the dispatch).
+template <int kSec, bool kWrap>
+__device__ __forceinline__ void mask_sec_u8(const ObsParams& p, const int16_t* T, int S, const int16_t* vis,
+                                            const uint2* inv, const uint16_t* mpo, int nm, const MaskCtx& m,
+                                            uint8_t* mb) {
+  int lo, n;
+  mask_section(p, kSec, lo, n);
+  for (int k = lane_id(); k < n; k += 64) mb[lo + k] = mask_value<kWrap>(p, T, S, vis, inv, mpo, nm, m, kSec, k) ? 1 : 0;
+}
+
+// The same for a flat row: section kSec as float32 0/1 straight into the row.
+template <int kSec, bool kWrap>
+__device__ __forceinline__ void mask_sec_f32(const ObsParams& p, const int16_t* T, int S, const int16_t* vis,
+                                             const uint2* inv, const uint16_t* mpo, int nm, const MaskCtx& m,
+                                             float* row) {
+  int lo, n;
+  mask_section(p, kSec, lo, n);
+  for (int k = lane_id(); k < n; k += 64)
+    obs_st(&row[lo + k], mask_value<kWrap>(p, T, S, vis, inv, mpo, nm, m, kSec, k) ? 1.f : 0.f);
+}
+
 // Passability of the 5 move targets from the prefetched window materials: tile t of the 15x15
 // window sits in lane t & 63 of register t >> 6; the centre's 4 neighbours (t = 97, 111, 112,
 // 113, 127) are all in register 1.
@@ -343,23 +366,19 @@ __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
       }
       // the next agent's loads go out now, ahead of this row's remaining stores
       if (alive(j + 1)) prefetch(a + kObsWaves, j + 1);
-      // ActionTargets: one uniform loop over (section, 64-entry chunk)
-      {
-        int sec = 0, k0 = 0;
-#pragma unroll 1
-        while (sec < 12) {
-          int lo, n;
-          mask_section(p, sec, lo, n);
-          const int k = k0 + lane;
-          if (k < n)
-            obs_st(&row[lo + k], mask_value<kWrap>(p, T, S, vis, inv, mpo, nm, m, sec, k) ? 1.f : 0.f);
-          k0 += 64;
-          if (k0 >= n) {
-            sec++;
-            k0 = 0;
-          }
-        }
-      }
+      // ActionTargets, section by section
+      mask_sec_f32<0, kWrap>(p, T, S, vis, inv, mpo, nm, m, row);
+      mask_sec_f32<1, kWrap>(p, T, S, vis, inv, mpo, nm, m, row);
+      mask_sec_f32<2, kWrap>(p, T, S, vis, inv, mpo, nm, m, row);
+      mask_sec_f32<3, kWrap>(p, T, S, vis, inv, mpo, nm, m, row);
+      mask_sec_f32<4, kWrap>(p, T, S, vis, inv, mpo, nm, m, row);
+      mask_sec_f32<5, kWrap>(p, T, S, vis, inv, mpo, nm, m, row);
+      mask_sec_f32<6, kWrap>(p, T, S, vis, inv, mpo, nm, m, row);
+      mask_sec_f32<7, kWrap>(p, T, S, vis, inv, mpo, nm, m, row);
+      mask_sec_f32<8, kWrap>(p, T, S, vis, inv, mpo, nm, m, row);
+      mask_sec_f32<9, kWrap>(p, T, S, vis, inv, mpo, nm, m, row);
+      mask_sec_f32<10, kWrap>(p, T, S, vis, inv, mpo, nm, m, row);
+      mask_sec_f32<11, kWrap>(p, T, S, vis, inv, mpo, nm, m, row);
       if (lane == 0) obs_st(&row[p.o_agent_id], (float)aid);
       if (lane == 1) obs_st(&row[p.o_tick], (float)tick);
       // Entity rows: two per pass (lanes 0-30 row k, lanes 32-62 row k + 1: 62 contiguous floats),
@@ -440,22 +459,18 @@ __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
       }
       if (lane == 0) mb[p.o_buy + NMMO_MARKET_ROWS] = 1;
     }
-    {
-      int sec = 0, k0 = 0;
-#pragma unroll 1
-      while (sec < 12) {
-        int lo, n;
-        mask_section(p, sec, lo, n);
-        if (sec == 2 && buy4) n = 0;
-        const int k = k0 + lane;
-        if (k < n) mb[lo + k] = mask_value<kWrap>(p, T, S, vis, inv, mpo, nm, m, sec, k) ? 1 : 0;
-        k0 += 64;
-        if (k0 >= n) {
-          sec++;
-          k0 = 0;
-        }
-      }
-    }
+    mask_sec_u8<0, kWrap>(p, T, S, vis, inv, mpo, nm, m, mb);
+    mask_sec_u8<1, kWrap>(p, T, S, vis, inv, mpo, nm, m, mb);
+    if (!buy4) mask_sec_u8<2, kWrap>(p, T, S, vis, inv, mpo, nm, m, mb);
+    mask_sec_u8<3, kWrap>(p, T, S, vis, inv, mpo, nm, m, mb);
+    mask_sec_u8<4, kWrap>(p, T, S, vis, inv, mpo, nm, m, mb);
+    mask_sec_u8<5, kWrap>(p, T, S, vis, inv, mpo, nm, m, mb);
+    mask_sec_u8<6, kWrap>(p, T, S, vis, inv, mpo, nm, m, mb);
+    mask_sec_u8<7, kWrap>(p, T, S, vis, inv, mpo, nm, m, mb);
+    mask_sec_u8<8, kWrap>(p, T, S, vis, inv, mpo, nm, m, mb);
+    mask_sec_u8<9, kWrap>(p, T, S, vis, inv, mpo, nm, m, mb);
+    mask_sec_u8<10, kWrap>(p, T, S, vis, inv, mpo, nm, m, mb);
+    mask_sec_u8<11, kWrap>(p, T, S, vis, inv, mpo, nm, m, mb);
     if (lane < NMMO_NATIVE_MASK_BYTES - p.o_agent_id) mb[p.o_agent_id + lane] = 0;
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -466,17 +481,26 @@ __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
     int16_t* d16 = reinterpret_cast<int16_t*>(nrow + NMMO_NATIVE_MASK_BYTES);
     if (lane == 0) d16[0] = (int16_t)aid;
     if (lane == 1) d16[1] = (int16_t)tick;
-    {  // two entity rows per pass: lanes 0-30 row k, lanes 32-62 row k + 1, one column each;
-       // the rows past the visible ones as one zero run
-      const int f = lane & 31, half = lane >> 5;
-      const int nv2 = (m.nv + 1) & ~1;
+    {  // four entity rows per pass as dwords: a row pair is 62 int16 = 31 dwords (dword-aligned:
+       // it starts 4 + 124 j bytes into the int16 part), lanes 0-30 the pair (k, k + 1), lanes
+       // 32-62 the pair (k + 2, k + 3); lane i packs int16 2i, 2i + 1 of its pair. The rows past
+       // the visible ones (rounded up to the pass) are one zero run.
+      const int i = lane & 31, pr = lane >> 5;
+      const int nv4 = (m.nv + 3) & ~3;
+      const int c0 = 2 * i, c1 = 2 * i + 1;  // pair positions: 0-30 the first row, 31-61 the second
+      const int r0 = c0 >= NMMO_N_ENTITY_COLS, r1 = c1 >= NMMO_N_ENTITY_COLS;
+      const int f0 = c0 - r0 * NMMO_N_ENTITY_COLS, f1 = c1 - r1 * NMMO_N_ENTITY_COLS;
+      uint32_t* d32 = reinterpret_cast<uint32_t*>(d16 + kNatEntity);
 #pragma unroll 1
-      for (int k0 = 0; k0 < nv2; k0 += 2) {
-        const int k = k0 + half;
-        if (f < NMMO_N_ENTITY_COLS)
-          d16[kNatEntity + k * NMMO_N_ENTITY_COLS + f] = k < m.nv ? T[f * S + vis[k]] : (int16_t)0;
+      for (int k0 = 0; k0 < nv4; k0 += 4) {
+        const int k = k0 + 2 * pr;
+        if (i < NMMO_N_ENTITY_COLS) {
+          const int ka = k + r0, kb = k + r1;
+          const int lo = ka < m.nv ? T[f0 * S + vis[ka]] : 0, hi = kb < m.nv ? T[f1 * S + vis[kb]] : 0;
+          d32[(k >> 1) * NMMO_N_ENTITY_COLS + i] = i16pack(lo, hi);
+        }
       }
-      wave_zero_bytes(nrow, NMMO_NATIVE_MASK_BYTES + 2 * (kNatEntity + nv2 * NMMO_N_ENTITY_COLS),
+      wave_zero_bytes(nrow, NMMO_NATIVE_MASK_BYTES + 2 * (kNatEntity + nv4 * NMMO_N_ENTITY_COLS),
                       NMMO_NATIVE_MASK_BYTES + 2 * kNatInv);
     }
     for (int k = lane; k < kInv * 16; k += 64) {
