@@ -643,10 +643,18 @@ def main():
 
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local if world > 1 else 0)
+    # NMMO_BENCH_BACKEND=gloo rehearses the multi-rank path on fewer GPUs than ranks (ranks share
+    # devices round-robin; gloo reduces the CUDA timing tensors through the host). The bench
+    # proper is one rank per GPU over RCCL ("nccl").
+    backend = os.environ.get("NMMO_BENCH_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    torch.cuda.set_device((local % ndev if backend == "gloo" else local) if world > 1 else 0)
     dev = torch.device("cuda", torch.cuda.current_device())
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "gloo":
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     wl = WORKLOADS[args.config]
     envs = args.envs or wl["envs"]
@@ -704,7 +712,8 @@ def main():
         if res["gather"]:
             how = ("wire-encoded native obs (SPEC §8c), decoded on rank 0 into its native buffers"
                    if res["native"] else "flat obs")
-            line["gather"] = (f"RCCL point-to-point sends into rank 0 of {res['gather_bytes']} B/step "
+            via = "RCCL" if backend == "nccl" else "gloo (rehearsal)"
+            line["gather"] = (f"{via} point-to-point sends into rank 0 of {res['gather_bytes']} B/step "
                               f"({how}) + reward/dones/mask, one step behind on a side stream"
                               if res["gather_bytes"] else "N = 1: rank 0's own shard in place, nothing sent")
         else:
