@@ -117,6 +117,7 @@ def test_invalid_arguments_report_errors(native):
     bad.abi_version = 99
     assert native.nmmo_create(ctypes.byref(bad), 4, 0, 0, None, ctypes.byref(h)) == abi.NMMO_E_INVALID
     assert native.nmmo_step(None, None, None, None, None, None, None, None) == abi.NMMO_E_INVALID
+    assert native.nmmo_observe(None, None, None) == abi.NMMO_E_INVALID
     assert native.nmmo_get_state(None, None, 0) == abi.NMMO_E_INVALID
 
 
