@@ -160,6 +160,8 @@ __device__ __forceinline__ int wave_incl_scan(int x) {
   x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
   return x;
 }
+// Sum over the 64 lanes of a wave (all lanes active), wave-uniform.
+__device__ __forceinline__ int wave_sum(int x) { return __builtin_amdgcn_readlane(wave_incl_scan(x), 63); }
 
 __device__ inline bool item_usable(const int16_t* T, int S, int p, uint2 w) {
   if (it_price(w)) return false;

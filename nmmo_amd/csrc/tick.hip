@@ -1748,44 +1748,48 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
     tk = c.tasks[my_task];
   }
   // 5-6. tick += 1; map.step respawn of depleted tiles; exchange.step listing expiry.
-  // One Philox call serves a group of 4 consecutive tiles (SPEC §5.6). The groups holding a
-  // depleted tile are compacted into a list (in LDS space the decode bitmap no longer needs)
-  // and drawn one group per lane, so the phase costs ~one Philox per lane instead of the
-  // busiest lane's tile count; beyond the list's capacity the per-word loop is used.
+  // One Philox call serves a group of 4 consecutive tiles (SPEC §5.6). Each wave takes every
+  // nwv-th chunk of 64 bitmap words, compacts the groups holding a depleted tile into its own
+  // list (wave scan; in LDS space the decode bitmap no longer needs) and draws them one group
+  // per lane: ~one Philox per lane instead of the busiest lane's tile count, and no block-wide
+  // prefix sum or barrier. A wave whose groups overflow its list share uses the per-word loop.
   {
     const uint8_t* base = c.bank + (size_t)c.E[E_MAP_ID] * kTiles;
-    int ng_mine = 0;
-    for (int w = tid; w < kBitmapWords; w += nt) {
-      uint32_t nz = c.dep[w];
+    const uint32_t* base4 = reinterpret_cast<const uint32_t*>(base);  // 4 tiles per word
+    const int lane = lane_id(), wv = tid >> 6, nwv = nt >> 6;
+    const int wcap = (128 * NW * 4) / nwv;                              // int16 entries per wave
+    int16_t* wlist = reinterpret_cast<int16_t*>(c.vism) + wv * wcap;  // vism: dead after decode
+    const uint32_t rtick = (uint32_t)(tick + 1);
+    auto groups_of = [&](int w) {  // bit 4q of the result: group q of word w holds a depleted tile
+      uint32_t nz = w < kBitmapWords ? c.dep[w] : 0u;
       nz |= nz >> 1;
       nz |= nz >> 2;
-      ng_mine += __popc(nz & 0x11111111u);
-    }
-    int ngroups;
+      return nz & 0x11111111u;
+    };
+    int ng = 0;  // this wave's groups (wave-uniform)
+    for (int ch = wv * 64; ch < kBitmapWords; ch += nwv * 64) ng += wave_sum(__popc(groups_of(ch + lane)));
     NMMO_STAMP(16);
-    const int gpos = block_prefix_sum(ng_mine, wtot_next(c), &ngroups);
-    NMMO_STAMP(17);
-    int16_t* glist = reinterpret_cast<int16_t*>(c.vism);  // dead after decode
-    const int gcap = 128 * NW * 4;                         // int16 entries in vism's bytes
-    const uint32_t rtick = (uint32_t)(tick + 1);
-    if (ngroups <= gcap) {
-      int k = gpos;
-      for (int w = tid; w < kBitmapWords; w += nt) {
-        uint32_t nz = c.dep[w];
-        nz |= nz >> 1;
-        nz |= nz >> 2;
-        nz &= 0x11111111u;
+    if (ng <= wcap) {
+      int k0 = 0;
+      for (int ch = wv * 64; ch < kBitmapWords; ch += nwv * 64) {
+        const int w = ch + lane;
+        uint32_t nz = groups_of(w);
+        const int n = __popc(nz);
+        const int inc = wave_incl_scan(n);
+        int k = k0 + inc - n;
+        k0 += __shfl(inc, 63);
         while (nz) {
           const int b = __builtin_ctz(nz);
           nz &= nz - 1;
-          glist[k++] = (int16_t)(w * 8 + (b >> 2));
+          wlist[k++] = (int16_t)(w * 8 + (b >> 2));
         }
       }
-      __syncthreads();
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       NMMO_STAMP(18);
-      const uint32_t* base4 = reinterpret_cast<const uint32_t*>(base);  // 4 tiles per word
-      for (int i = tid; i < ngroups; i += nt) {
-        const int g = glist[i], w = g >> 3, sh = (g & 7) * 4;
+      for (int i = lane; i < ng; i += 64) {
+        const int g = wlist[i], w = g >> 3, sh = (g & 7) * 4;
         const uint32_t b4 = base4[g];  // issued ahead of the draw, whose latency covers it
         const uint32_t nib = (c.dep[w] >> sh) & 15u;
         const U4 u = draw(seed, rtick, P_RESPAWN, (uint32_t)g, 0);
@@ -1799,10 +1803,12 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
             clear |= 1u << (sh + j);
           }
         }
-        if (clear) atomicAnd(&c.dep[w], ~clear);
+        if (clear) atomicAnd(&c.dep[w], ~clear);  // lanes may share a word
       }
     } else {
-      for (int w = tid; w < kBitmapWords; w += nt) {
+      for (int ch = wv * 64; ch < kBitmapWords; ch += nwv * 64) {
+        const int w = ch + lane;
+        if (w >= kBitmapWords) continue;
         uint32_t bits = c.dep[w], keepb = bits;
         while (bits) {
           const int b = __builtin_ctz(bits);
