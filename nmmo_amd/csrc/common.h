@@ -162,7 +162,6 @@ __device__ __forceinline__ int wave_incl_scan(int x) {
 }
 // Sum over the 64 lanes of a wave (all lanes active), wave-uniform.
 __device__ __forceinline__ int wave_sum(int x) { return __builtin_amdgcn_readlane(wave_incl_scan(x), 63); }
-
 __device__ inline bool item_usable(const int16_t* T, int S, int p, uint2 w) {
   if (it_price(w)) return false;
   if (equip_slot(it_type(w)) >= 0 && it_equipped(w)) return true;

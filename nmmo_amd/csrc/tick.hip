@@ -329,9 +329,19 @@ __device__ __forceinline__ void copy_segs(const Seg16 (&sg)[6], int tid, int nt,
   }
 }
 
+__device__ __forceinline__ void load_env_arrays(Ctx& c, const DevState& st, int e);
 __device__ __forceinline__ void load_env(Ctx& c, const DevState& st, int e) {
+  const int tid = threadIdx.x;
+  // env scalars: loaded first, written to LDS after the copy has issued its loads (stored right
+  // away, their wait put a whole HBM round trip ahead of the state copy)
+  int ev = st.env[(size_t)e * NMMO_NE + min(tid, NMMO_NE - 1)];  // every thread: no branch join
+  load_env_arrays(c, st, e);
+  asm volatile("" : "+v"(ev));
+  if (tid < NMMO_NE) c.E[tid] = ev;
+}
+
+__device__ __forceinline__ void load_env_arrays(Ctx& c, const DevState& st, int e) {
   const int tid = threadIdx.x, nt = blockDim.x, S = c.S;
-  if (tid < NMMO_NE) c.E[tid] = st.env[(size_t)e * NMMO_NE + tid];
   const int16_t* src = st.ent + (size_t)e * NMMO_NF * S;
   // every segment a whole number of 16-B words (task state: 40 B per player)
   const bool v16 = (S & 7) == 0 && (c.IC & 7) == 0 && (c.P & 1) == 0;
@@ -1065,7 +1075,26 @@ __device__ __forceinline__ int hash_min(const Ctx& c, int tile) {
   }
 }
 
-__device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act, float* rew, uint8_t* term,
+// system sets with a specialised tick kernel: BASELINE configs 2 and 3 (config 4 = all)
+constexpr uint32_t kSysC2 = NMMO_SYS_RESOURCE;
+constexpr uint32_t kSysC3 = NMMO_SYS_RESOURCE | NMMO_SYS_COMBAT | NMMO_SYS_NPC | NMMO_SYS_PROGRESSION;
+
+// Make a prefetched task / task state opaque at this point, field by field (an address-taken
+// copy would go to scratch): nothing computed from them can be scheduled above the call, so the
+// loads issued before the respawn are waited on at the rewards, not next to their issue.
+__device__ __forceinline__ void launder(NmmoTask& t) {
+#pragma unroll
+  for (int k = 0; k < 2; k++)
+    asm volatile("" : "+v"(t.term[k].pred), "+v"(t.term[k].a), "+v"(t.term[k].b), "+v"(t.term[k].c),
+                 "+v"(t.term[k].weight));
+  asm volatile("" : "+v"(t.combine));
+}
+__device__ __forceinline__ void launder(NmmoTaskState& t) {
+  asm volatile("" : "+v"(t.last), "+v"(t.max_progress), "+v"(t.signals), "+v"(t.completed_tick));
+  asm volatile("" : "+v"(t.acc[0]), "+v"(t.acc[1]), "+v"(t.acc[2]), "+v"(t.acc[3]));
+}
+
+__device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act, int3 a_pre, float* rew, uint8_t* term,
                          uint8_t* trunc, uint8_t* mask) {
   const int tid = threadIdx.x, nt = blockDim.x, S = c.S, P = c.P;
   const int s = tid;
@@ -1092,21 +1121,19 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
   // (every depletion/regrowth maps passable to passable and impassable to impassable), and no
   // entity moves before the move phase, so these stay exact for NPC steering, drinking,
   // foilage eating (the own tile is read before any harvest) and the move check.
-  uint32_t m_own = 0, m_n0 = 0, m_n1 = 0, m_n2 = 0, m_n3 = 0;
   const int my_task = s < P ? c.assign[s] : 0;  // HBM; first used before the respawn phase
   const bool in_realm = s < S && inslot && TF(F_ALIVE, s);  // => health > 0 at tick start
   const int pos_r = s < S ? TF(F_ROW, s) : 0, pos_c = s < S ? TF(F_COL, s) : 0;
-  {
-    if (in_realm) {
-      c.rslot[TF(F_DS_ROW, s)] = (int16_t)s;
-      const uint8_t* m = c.mat + pos_r * kSize + pos_c;
-      m_own = m[0];
-      m_n0 = m[-kSize];
-      m_n1 = m[kSize];
-      m_n2 = m[1];
-      m_n3 = m[-1];
-    }
-  }
+  if (in_realm) c.rslot[TF(F_DS_ROW, s)] = (int16_t)s;
+  // Loaded as whole dwords by every thread (the map centre for slots not in the realm): row r's
+  // 8 aligned bytes holding columns c-1..c+1, and the dwords holding column c in rows r-1 and
+  // r+1. They stay opaque until the decode is done: byte loads let the compiler merge two of
+  // them and split the result right after the load, which waited on HBM here.
+  const int qr = in_realm ? pos_r : kSize / 2, qc = in_realm ? pos_c : kSize / 2;
+  const uint32_t* mrow = reinterpret_cast<const uint32_t*>(c.mat + qr * kSize);
+  const int mcw = (qc - 1) >> 2;
+  uint32_t mw0 = mrow[mcw], mw1 = mrow[mcw + 1], mup = mrow[(qc >> 2) - kSize / 4],
+           mdn = mrow[(qc >> 2) + kSize / 4];
   if (tid < 128) c.pp[tid] = (tid < P && TF(F_ALIVE, tid)) ? ((uint32_t)TF(F_ROW, tid) << 16) | (uint32_t)TF(F_COL, tid)
                                                         : 0x80008000u;
   if (c.exch && s < P) {  // listings of the previous observation (Buy.MarketItem index space)
@@ -1166,6 +1193,14 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
   __syncthreads();
   NMMO_STAMP(13);
   // bits 0-3: neighbour d passable; 4-7: neighbour d is Water; 8-15: own tile material
+  asm volatile("" : "+v"(mw0), "+v"(mw1), "+v"(mup), "+v"(mdn));
+  const uint64_t mrow8 = (uint64_t)mw0 | ((uint64_t)mw1 << 32);
+  const int msh = 8 * ((qc - 1) & 3), mcol = 8 * (qc & 3);
+  const uint32_t m_n3 = in_realm ? (uint32_t)(mrow8 >> msh) & 255u : 0u;  // column c-1
+  const uint32_t m_own = in_realm ? (uint32_t)(mrow8 >> (msh + 8)) & 255u : 0u;
+  const uint32_t m_n2 = in_realm ? (uint32_t)(mrow8 >> (msh + 16)) & 255u : 0u;  // column c+1
+  const uint32_t m_n0 = in_realm ? (mup >> mcol) & 255u : 0u;                    // row r-1
+  const uint32_t m_n1 = in_realm ? (mdn >> mcol) & 255u : 0u;                    // row r+1
   const uint32_t nbm = (impassable(m_n0) ? 0u : 1u) | (impassable(m_n1) ? 0u : 2u) |
                        (impassable(m_n2) ? 0u : 4u) | (impassable(m_n3) ? 0u : 8u) |
                        (m_n0 == M_WATER ? 16u : 0u) | (m_n1 == M_WATER ? 32u : 0u) |
@@ -1184,7 +1219,8 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
   }
   if (s < P && c.pres[s]) {
     const int32_t* a = act + (size_t)s * kHeads;
-    const int dmove = a[8], dsty = a[0], dk = a[1];
+    asm volatile("" : "+v"(a_pre.x), "+v"(a_pre.y), "+v"(a_pre.z));  // loaded before the state
+    const int dmove = a_pre.x, dsty = a_pre.y, dk = a_pre.z;
     if (dmove >= 0 && dmove < 5) my_move = dmove;
     if (combat && dsty >= 0 && dsty < 3 && dk >= 0 && dk < kNObs) {
       my_tgt = vis_kth(c, s, NW, dk);
@@ -1255,6 +1291,19 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
   }
   __syncthreads();
   NMMO_STAMP(2);
+  // This player's task state (when it lives in HBM) and task, for the rewards. Loaded by every
+  // thread from valid addresses (a conditional load leaves a register merge at the branch join
+  // that waits on it); used only for present, surviving players. Issued here, a whole tick ahead
+  // of the rewards, except in the <= 64-VGPR C3 variant, which cannot hold 24 more registers
+  // through the middle phases and issues them after the respawn draws instead (issued before
+  // them, the draw loop's head waits on them).
+  const bool task_early = c.sysm != kSysC3;
+  NmmoTaskState tsr = {};
+  NmmoTask tk = {};
+  if (task_early) {
+    tsr = c.tsg[s < P ? s : 0];
+    tk = c.tasks[my_task];
+  }
   for (int k = tid; k < kHash; k += nt) {  // position hash (its LDS held the decode bitmap)
     c.hkey[k] = -1;
     c.hmin[k] = 0x7FFF;
@@ -1740,13 +1789,6 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
   __syncthreads();
   NMMO_STAMP(7);
 
-  // this player's task state, loaded here when it lives in HBM so the rewards do not wait on it
-  NmmoTaskState tsr = {};
-  NmmoTask tk = {};  // and its task (index loaded at tick start)
-  if (s < P && c.pres[s] && !c.died[s]) {
-    if (!c.tev) tsr = c.tsg[s];
-    tk = c.tasks[my_task];
-  }
   // 5-6. tick += 1; map.step respawn of depleted tiles; exchange.step listing expiry.
   // One Philox call serves a group of 4 consecutive tiles (SPEC §5.6). Each wave takes every
   // nwv-th chunk of 64 bitmap words, compacts the groups holding a depleted tile into its own
@@ -1766,44 +1808,57 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
       nz |= nz >> 2;
       return nz & 0x11111111u;
     };
+    // one pass counts and lists (entries past wcap are dropped; the per-word loop then runs)
     int ng = 0;  // this wave's groups (wave-uniform)
-    for (int ch = wv * 64; ch < kBitmapWords; ch += nwv * 64) ng += wave_sum(__popc(groups_of(ch + lane)));
+    for (int ch = wv * 64; ch < kBitmapWords; ch += nwv * 64) {
+      const int w = ch + lane;
+      uint32_t nz = groups_of(w);
+      const int n = __popc(nz);
+      const int inc = wave_incl_scan(n);
+      int k = ng + inc - n;
+      ng += __builtin_amdgcn_readlane(inc, 63);
+      while (nz) {
+        const int b = __builtin_ctz(nz);
+        nz &= nz - 1;
+        if (k < wcap) wlist[k] = (int16_t)(w * 8 + (b >> 2));
+        k++;
+      }
+    }
     NMMO_STAMP(16);
     if (ng <= wcap) {
-      int k0 = 0;
-      for (int ch = wv * 64; ch < kBitmapWords; ch += nwv * 64) {
-        const int w = ch + lane;
-        uint32_t nz = groups_of(w);
-        const int n = __popc(nz);
-        const int inc = wave_incl_scan(n);
-        int k = k0 + inc - n;
-        k0 += __shfl(inc, 63);
-        while (nz) {
-          const int b = __builtin_ctz(nz);
-          nz &= nz - 1;
-          wlist[k++] = (int16_t)(w * 8 + (b >> 2));
-        }
-      }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       NMMO_STAMP(18);
-      for (int i = lane; i < ng; i += 64) {
-        const int g = wlist[i], w = g >> 3, sh = (g & 7) * 4;
-        const uint32_t b4 = base4[g];  // issued ahead of the draw, whose latency covers it
-        const uint32_t nib = (c.dep[w] >> sh) & 15u;
-        const U4 u = draw(seed, rtick, P_RESPAWN, (uint32_t)g, 0);
-        const uint32_t uu[4] = {u.x, u.y, u.z, u.w};
-        uint32_t clear = 0;
+      // a lane's groups in batches of 4: the 4 bank words are loaded (clamped index, no branch)
+      // before the first draw, so one HBM round trip serves 4 draws
+      constexpr int kB = 4;
+      for (int i0 = lane; i0 < ng; i0 += kB * 64) {
+        int gb[kB];
+        uint32_t b4[kB];
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-          const int bm = (int)((b4 >> (8 * j)) & 255u);
-          if (((nib >> j) & 1u) && uu[j] < respawn_u32(bm)) {
-            c.mat[4 * g + j] = (uint8_t)bm;
-            clear |= 1u << (sh + j);
-          }
+        for (int q = 0; q < kB; q++) {
+          gb[q] = wlist[min(i0 + 64 * q, ng - 1)];
+          b4[q] = base4[gb[q]];
         }
-        if (clear) atomicAnd(&c.dep[w], ~clear);  // lanes may share a word
+#pragma unroll
+        for (int q = 0; q < kB; q++) {
+          if (i0 + 64 * q >= ng) break;
+          const int g = gb[q], w = g >> 3, sh = (g & 7) * 4;
+          const uint32_t nib = (c.dep[w] >> sh) & 15u;
+          const U4 u = draw(seed, rtick, P_RESPAWN, (uint32_t)g, 0);
+          const uint32_t uu[4] = {u.x, u.y, u.z, u.w};
+          uint32_t clear = 0;
+#pragma unroll
+          for (int j = 0; j < 4; j++) {
+            const int bm = (int)((b4[q] >> (8 * j)) & 255u);
+            if (((nib >> j) & 1u) && uu[j] < respawn_u32(bm)) {
+              c.mat[4 * g + j] = (uint8_t)bm;
+              clear |= 1u << (sh + j);
+            }
+          }
+          if (clear) atomicAnd(&c.dep[w], ~clear);  // lanes may share a word
+        }
       }
     } else {
       for (int ch = wv * 64; ch < kBitmapWords; ch += nwv * 64) {
@@ -1825,6 +1880,10 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
         c.dep[w] = keepb;
       }
     }
+  }
+  if (!task_early) {
+    tsr = c.tsg[s < P ? s : 0];
+    tk = c.tasks[my_task];
   }
   if (c.exch && s < P) {
     uint2* inv = c.inv + s * kInv;
@@ -1852,6 +1911,10 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
   __syncthreads();
   if (s < P) {  // Task.compute_rewards: progress delta, death penalty (SPEC §12)
     float rw = 0.f;
+    // the prefetched task words stay opaque until here, or the compiler hoists their conversions
+    // (float weight -> double) up to the loads and waits on HBM before the respawn
+    launder(tk);
+    if (!c.tev) launder(tsr);
     if (c.pres[s] && c.died[s]) {
       rw = -1.f;
     } else if (c.pres[s]) {
@@ -1913,6 +1976,13 @@ __device__ __forceinline__ void tick_body(const DevState& st, const int32_t* __r
   const int e = blockIdx.x;
   NMMO_STAMP(0);
   Ctx c = make_ctx(smem, st, e, kSys ? kSys : st.cfg.systems);
+  // a step's Move / AttackStyle / AttackTarget heads of this thread's player (a valid row for
+  // every thread), loaded ahead of the state so their latency hides under its load
+  int3 a_pre = make_int3(0, 0, 0);
+  if (mode == 0) {
+    const int32_t* a = actions + ((size_t)e * st.P + min((int)threadIdx.x, st.P - 1)) * kHeads;
+    a_pre = make_int3(a[8], a[0], a[1]);
+  }
   load_env(c, st, e);
   __syncthreads();
   NMMO_STAMP(20);
@@ -1949,7 +2019,7 @@ __device__ __forceinline__ void tick_body(const DevState& st, const int32_t* __r
       if (mask) mask[o + p] = 1;
     }
   } else {
-    tick_env(c, actions + o * kHeads, rew + o, term + o, trunc + o, mask + o);
+    tick_env(c, actions + o * kHeads, a_pre, rew + o, term + o, trunc + o, mask + o);
   }
   __syncthreads();
   if (st.counters) {  // sum(mask) of this launch (pres, or all players on a reset) + done envs
@@ -1984,9 +2054,6 @@ tick_kernel_w8(DevState st, const int32_t* __restrict__ actions, const uint64_t*
   tick_body<kSys>(st, actions, env_seeds, rew, term, trunc, mask, mode);
 }
 
-// system sets with a specialised tick kernel: BASELINE configs 2 and 3 (config 4 = all)
-constexpr uint32_t kSysC2 = NMMO_SYS_RESOURCE;
-constexpr uint32_t kSysC3 = NMMO_SYS_RESOURCE | NMMO_SYS_COMBAT | NMMO_SYS_NPC | NMMO_SYS_PROGRESSION;
 
 hipError_t launch_tick(const DevState& st, const int32_t* actions, const uint64_t* env_seeds,
                        float* rew, uint8_t* term, uint8_t* trunc, uint8_t* mask, int mode,
