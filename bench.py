@@ -71,6 +71,7 @@ WRAPPER_KW = {"neurips23_start_kit": dict(heal_bonus_weight=0.03, explore_bonus_
                               attack_bonus_weight=0.0, gold_bonus_weight=0.001, custom_bonus_scale=0.1,
                               disable_give=True, donot_attack_dangerous_npc=True)}
 EVENT_ROW_BYTES = 9 * 4
+TASK_STATE_BYTES = 40  # NmmoTaskState (include/nmmo_hip.h), abi.TASK_STATE_BYTES
 
 
 def tick_bytes_per_env(S: int, P: int, items: bool, events_per_env: float = 0.0, slim: bool = False) -> int:
@@ -79,12 +80,13 @@ def tick_bytes_per_env(S: int, P: int, items: bool, events_per_env: float = 0.0,
     without Item/Equipment/Profession/Exchange -- free-row ring, depleted-tile bitmap, env
     scalars; with the Item system the 12-slot inventories and the item-row ring), the actions
     read, the outputs written, the map tiles a player touches (own tile + 4 neighbours for
-    harvest/drink, 1 move target) and the event-log rows appended (36 B each; measured mean
-    per env-tick)."""
-    state = (30 if slim else 45) * S * 2 + S * 2 + 800 * 4 + 16 * 4
+    harvest/drink, 1 move target), each player's task assignment read and its 40-B task state
+    read and written (the reward's progress, SPEC §12) and the event-log rows appended (36 B
+    each; measured mean per env-tick)."""
+    state = (30 if slim else 45) * S * 2 + S * 2 + 800 * 4 + 16 * 4 + P * TASK_STATE_BYTES
     if items:
         state += P * 12 * 8 + 12 * P * 2
-    return int(2 * state + P * 12 * 4 + P * (4 + 1 + 1 + 1) + P * 6 + events_per_env * EVENT_ROW_BYTES)
+    return int(2 * state + P * 4 + P * 12 * 4 + P * (4 + 1 + 1 + 1) + P * 6 + events_per_env * EVENT_ROW_BYTES)
 
 
 def obs_bytes_per_env(S: int, P: int, elems: int, native: bool = False) -> int:
