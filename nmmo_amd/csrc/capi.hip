@@ -45,6 +45,7 @@ struct NmmoHandle {
   int16_t* d_ring = nullptr;
   uint8_t* d_mat = nullptr;
   uint32_t* d_dep = nullptr;
+  int32_t* d_foreign = nullptr;  // DevState::foreign
   uint8_t* d_bank = nullptr;
   float* d_task = nullptr;
   uint64_t* d_seeds = nullptr;
@@ -176,7 +177,7 @@ void nmmo_destroy(NmmoHandle* h) {
   void* bufs[] = {h->d_env,  h->d_ent,   h->d_ring,  h->d_mat,   h->d_dep,   h->d_bank,
                   h->d_task, h->d_seeds, h->d_items, h->d_iring, h->d_mlist, h->d_mcount,
                   h->d_events, h->d_tasks, h->d_assign, h->d_tstate, h->d_ws, h->d_uniq, h->d_wenv, h->d_wdrop, h->d_task_cum,
-                  h->d_wcount};
+                  h->d_wcount, h->d_foreign};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   delete h;
@@ -214,6 +215,7 @@ int nmmo_create(const NmmoConfig* cfg, int32_t n_envs, uint64_t seed, int32_t de
   ALLOC(h->d_ring, n * S * 2);
   ALLOC(h->d_mat, n * NMMO_MAP_TILES);
   ALLOC(h->d_dep, n * kBitmapWords * 4);
+  ALLOC(h->d_foreign, 4);
   ALLOC(h->d_bank, (size_t)cfg->map_n * NMMO_MAP_TILES);
   ALLOC(h->d_task, (size_t)(cfg->task_embed_dim > 0 ? cfg->task_embed_dim : 1) * 4);
   ALLOC(h->d_seeds, n * 8);
@@ -239,7 +241,7 @@ int nmmo_create(const NmmoConfig* cfg, int32_t n_envs, uint64_t seed, int32_t de
   h->st = DevState{h->d_env,   h->d_ent,   h->d_ring,  h->d_mat,    h->d_dep, h->d_bank,
                    h->d_items, h->d_iring, h->d_mlist, h->d_mcount, h->d_events,
                    h->d_tasks, h->d_assign, nullptr, h->d_tstate, 1,            0,           n_envs, P,
-                   N,          S,          seed,       nullptr,     *cfg};
+                   N,          S,          seed,       nullptr,     *cfg,      h->d_foreign};
   {  // default task table: everyone runs TickGE(task_num_tick) (SPEC §12)
     NmmoTask t;
     memset(&t, 0, sizeof(t));
@@ -308,6 +310,7 @@ int nmmo_reset(NmmoHandle* h, const uint64_t* env_seeds, void* obs, uint8_t* mas
   }
   HIP_TRY(launch_tick(h->st, nullptr, env_seeds ? h->d_seeds : nullptr, nullptr, nullptr, nullptr,
                       mask, 1, s));
+  HIP_TRY(hipMemsetAsync(h->d_foreign, 0, 4, s));  // every env's tiles now match its bank
   if (h->wrap_on) HIP_TRY(launch_wrap(wrap_params(h, nullptr, nullptr, nullptr, nullptr, nullptr), 0, s));
   if (obs && h->cfg.obs_layout != NMMO_OBS_NONE) HIP_TRY(launch_obs(obs_params(h, obs), s));
   return NMMO_OK;

@@ -228,40 +228,42 @@ __device__ inline uint32_t writelane_u32(uint32_t old, uint32_t val, uint32_t la
   return lane_id() == (int)lane ? val : old;
 }
 
+// The wave totals below wave w and of all nw waves, read from an 8-entry buffer in one fixed
+// pass (all 8 entries are read, those of waves >= nw masked): a loop to the runtime wave count
+// compiles to a general unrolled loop with remainder handling, ~100 instructions per prefix.
+__device__ __forceinline__ int wave_tot_below(const int* wave_tot, int w, int nw, int* total) {
+  int base = 0, sum = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const int ti = wave_tot[i];
+    const int t = i < nw ? ti : 0;
+    base += i < w ? t : 0;
+    sum += t;
+  }
+  *total = sum;
+  return base;
+}
+
 // Block-wide exclusive prefix sum of an int in thread order (<= 8 waves); *total gets the sum.
 // One barrier: `wave_tot` (>= 8 ints of LDS) must not be the buffer of the previous call (it
 // may still be read), so consecutive calls alternate two buffers. All accesses before the call
 // are ordered before all accesses after it by that barrier.
 __device__ inline int block_prefix_sum(int v, int* wave_tot, int* total) {
-  const int w = wave_id(), nw = (blockDim.x + 63) >> 6;
+  const int w = __builtin_amdgcn_readfirstlane(wave_id()), nw = (blockDim.x + 63) >> 6;
   const int x = wave_incl_scan(v);
   if (lane_id() == 63) wave_tot[w] = x;
   __syncthreads();
-  int base = 0, sum = 0;
-  for (int i = 0; i < nw; i++) {
-    const int t = wave_tot[i];
-    base += i < w ? t : 0;
-    sum += t;
-  }
-  *total = sum;
-  return base + x - v;
+  return wave_tot_below(wave_tot, w, nw, total) + x - v;
 }
 
 // Block-wide exclusive prefix count of a 0/1 predicate in thread order (<= 8 waves); same
 // buffer rule as block_prefix_sum. Returns the exclusive count; *total gets the sum.
 __device__ inline int block_prefix_count(bool pred, int* wave_tot, int* total) {
   const uint64_t b = __ballot(pred);
-  const int w = wave_id(), nw = (blockDim.x + 63) >> 6;
+  const int w = __builtin_amdgcn_readfirstlane(wave_id()), nw = (blockDim.x + 63) >> 6;
   if (lane_id() == 0) wave_tot[w] = __popcll(b);
   __syncthreads();
-  int base = 0, sum = 0;
-  for (int i = 0; i < nw; i++) {
-    int v = wave_tot[i];
-    base += i < w ? v : 0;
-    sum += v;
-  }
-  *total = sum;
-  return base + __popcll(b & lanes_below());
+  return wave_tot_below(wave_tot, w, nw, total) + __popcll(b & lanes_below());
 }
 
 // ---------------------------------------------------------------- visibility grid

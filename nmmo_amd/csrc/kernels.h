@@ -40,6 +40,11 @@ struct DevState {
   uint64_t seed;         // create seed (first-episode seeds)
   unsigned long long* counters;  // optional device u64 [3]: agent-steps, finished episodes, event rows
   NmmoConfig cfg;
+  // device int: 1 when some env may hold a depleted tile whose map-bank material is not Foilage
+  // (only nmmo_set_state / nmmo_set_map_bank can make one without the Profession system; a full
+  // nmmo_reset clears it). While 0, the tick's respawn of a system set without professions needs
+  // no map-bank read: its only depletion is Foilage eaten to Scrub.
+  int32_t* foreign;
 };
 
 struct ObsParams {

@@ -83,6 +83,7 @@ struct Ctx {
   int evcap, tick1;  // ring rows (0 = no event log); tick + 1 (the events' tick column)
   int S, P, N, IC;
   bool items, exch, prof, equip;
+  bool foreign;      // !prof and DevState::foreign is set: respawn reads the map bank
   bool slim;         // no Item/Equipment/Profession/Exchange: the fields only they change stay in HBM
   int nf;            // staged entity fields (LDS rows of T)
   const NmmoConfig* cfg;
@@ -186,6 +187,7 @@ __device__ __forceinline__ Ctx make_ctx(unsigned char* smem, const DevState& st,
   c.exch = c.items && (sy & NMMO_SYS_EXCHANGE) != 0;
   c.prof = c.items && (sy & NMMO_SYS_PROFESSION) != 0;
   c.equip = c.items && (sy & NMMO_SYS_EQUIPMENT) != 0;
+  c.foreign = !c.prof && *st.foreign != 0;  // uniform, read before any store (a scalar load)
   c.IC = kInv * st.P;
   if (c.items) {  // 16-B aligned block first (inventories are copied with 16-B accesses)
     c.inv = reinterpret_cast<uint2*>(smem + o); o += (size_t)st.P * kInv * 8;
@@ -1798,6 +1800,11 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
   {
     const uint8_t* base = c.bank + (size_t)c.E[E_MAP_ID] * kTiles;
     const uint32_t* base4 = reinterpret_cast<const uint32_t*>(base);  // 4 tiles per word
+    // Without professions the only depletion is Foilage eaten to Scrub, so every depleted tile's
+    // bank material is Foilage unless a set_state / set_map_bank installed another (c.foreign,
+    // loaded at kernel start): no bank read, so the draws do not wait on HBM -- with stores in
+    // flight a load's wait is a store round trip as well (gfx9 counts both in vmcnt).
+    const bool foilage_only = !c.prof && !c.foreign;
     const int lane = lane_id(), wv = tid >> 6, nwv = nt >> 6;
     const int wcap = (128 * NW * 4) / nwv;                              // int16 entries per wave
     int16_t* wlist = reinterpret_cast<int16_t*>(c.vism) + wv * wcap;  // vism: dead after decode
@@ -1839,7 +1846,7 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
 #pragma unroll
         for (int q = 0; q < kB; q++) {
           gb[q] = wlist[min(i0 + 64 * q, ng - 1)];
-          b4[q] = base4[gb[q]];
+          b4[q] = foilage_only ? (uint32_t)M_FOILAGE * 0x01010101u : base4[gb[q]];
         }
 #pragma unroll
         for (int q = 0; q < kB; q++) {
@@ -1869,7 +1876,7 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
           const int b = __builtin_ctz(bits);
           bits &= bits - 1;
           const int tt = w * 32 + b;
-          const int bm = base[tt];
+          const int bm = foilage_only ? (int)M_FOILAGE : base[tt];
           const U4 u = draw(seed, rtick, P_RESPAWN, (uint32_t)(tt >> 2), 0);
           const uint32_t ut = (tt & 3) == 0 ? u.x : (tt & 3) == 1 ? u.y : (tt & 3) == 2 ? u.z : u.w;
           if (ut < respawn_u32(bm)) {
@@ -2099,11 +2106,17 @@ __global__ void rebuild_dep_kernel(DevState st) {
   const int32_t* E = st.env + (size_t)e * NMMO_NE;
   const uint8_t* mat = st.mat + (size_t)e * kTiles;
   const uint8_t* base = st.bank + (size_t)E[E_MAP_ID] * kTiles;
+  bool foreign = false;  // a depleted tile whose bank material is not Foilage (DevState::foreign)
   for (int w = tid; w < kBitmapWords; w += blockDim.x) {
     uint32_t bits = 0;
-    for (int b = 0; b < 32; b++) bits |= (mat[w * 32 + b] != base[w * 32 + b] ? 1u : 0u) << b;
+    for (int b = 0; b < 32; b++) {
+      const bool d = mat[w * 32 + b] != base[w * 32 + b];
+      bits |= (d ? 1u : 0u) << b;
+      foreign = foreign || (d && base[w * 32 + b] != M_FOILAGE);
+    }
     st.dep[(size_t)e * kBitmapWords + w] = bits;
   }
+  if (__ballot(foreign) && lane_id() == 0) atomicOr(st.foreign, 1);
   if (tid < kLWords) lbits[tid] = 0;
   __syncthreads();
   const bool exch = (st.cfg.systems & NMMO_SYS_ITEM) && (st.cfg.systems & NMMO_SYS_EXCHANGE);
@@ -2130,6 +2143,8 @@ __global__ void rebuild_dep_kernel(DevState st) {
 }
 
 hipError_t launch_rebuild_dep(const DevState& st, hipStream_t stream) {
+  const hipError_t err = hipMemsetAsync(st.foreign, 0, 4, stream);
+  if (err != hipSuccess) return err;
   hipLaunchKernelGGL(rebuild_dep_kernel, dim3(st.n_envs), dim3(256), 0, stream, st);
   return hipGetLastError();
 }

@@ -6,7 +6,7 @@ import pytest
 
 from nmmo_amd import abi
 from nmmo_amd.config import Config
-from oracle.oracle import OracleEnvs, split_state
+from oracle.oracle import OracleEnvs, join_state, split_state
 
 pytestmark = pytest.mark.gpu
 
@@ -104,6 +104,44 @@ def test_set_state_roundtrip():
         eng.step(torch.from_numpy(a).cuda())
     torch.cuda.synchronize()
     _cmp_state(eng.get_state(), orc.get_state(), 3, eng.S, "after set_state")
+
+
+def test_foreign_depletion_parity():
+    """Without professions the tick's respawn assumes every depleted tile is eaten Foilage and
+    skips the map-bank read (tick.hip, DevState::foreign). A set_state that depletes Tree and Ore
+    tiles instead must switch it back to the bank: the restored materials and their respawn
+    probabilities then differ from Foilage's, so any shortcut shows up in `mat`."""
+    import torch
+
+    cfg = Config.preset("C2", MAP_N=4)
+    n = 3
+    orc = OracleEnvs(cfg, n, seed=21)
+    orc.reset()
+    for t in range(5):
+        orc.step(orc.scripted_actions(t))
+    d = split_state(orc.get_state(), n, orc.S, 128)
+    bank = orc.map_bank().reshape(-1, abi.MAP_SIZE, abi.MAP_SIZE)
+    M = {"stump": 8, "tree": 9, "slag": 6, "ore": 7}  # common.h material enum
+    changed = 0
+    for e in range(n):
+        b = bank[d["env"][e, abi.E["map_id"]]]
+        for src, dst in (("tree", "stump"), ("ore", "slag")):
+            rr, cc = np.nonzero((b == M[src]) & (d["mat"][e] == M[src]))
+            d["mat"][e, rr[:40], cc[:40]] = M[dst]
+            changed += min(40, rr.size)
+    assert changed > 40
+    orc.set_state(join_state(d))
+    eng = _engine(cfg, n, seed=21)
+    eng.set_state(orc.get_state())
+    for t in range(5, 45):
+        a = orc.scripted_actions(t)
+        orc.step(a)
+        eng.step(torch.from_numpy(a).cuda())
+        torch.cuda.synchronize()
+        _cmp_state(eng.get_state(), orc.get_state(), n, eng.S, f"step {t}")
+        if t == 25:  # most of the stumps have grown back into trees (p = 0.1 per tick)
+            m = split_state(orc.get_state(), n, orc.S, 128)["mat"]
+            assert sum(int(((m[e] == M["tree"]) & (d["mat"][e] == M["stump"])).sum()) for e in range(n)) > 60
 
 
 def test_set_state_rejects_changed_slim_fields():
