@@ -8,7 +8,10 @@ loads, but HBM is read in 128-B lines (on MI355X 90+% of the tick's TCC_EA0 read
 lines touched per env, not the bytes used. This replays the bench's C2/C3 scenario on the oracle
 (staggered episode phases, masked-uniform scripted actions) and counts them.
 
-  python tools/tick_lines.py [C2|C3] [envs] [stagger] [ticks]
+  python tools/tick_lines.py [C2|C3|C4] [envs] [stagger] [ticks] [--bank]
+
+(--bank: count the bank lines without professions too, as the tick read them before round 2
+skipped that read.)
 """
 
 import os
@@ -55,12 +58,13 @@ def main():
     for t in range(ticks):
         st = split_state(o.get_state(), envs, slots)
         n += [lines_touched(st["ent"][e], slots) for e in range(envs)]
-        # respawn: one bank dword per 4-tile group holding a depleted tile (mat != bank)
-        for e in range(envs):
+        # respawn: one bank dword per 4-tile group holding a depleted tile (mat != bank); without
+        # professions the tick no longer reads the bank (every depletion is eaten Foilage)
+        for e in range(envs if "Profession" in cfg.systems or "--bank" in sys.argv else 0):
             dep = np.flatnonzero(st["mat"][e].reshape(-1) != bank[st["env"][e, abi.E["map_id"]]])
             nb.append(np.unique(dep // LINE).size)
         o.step(o.scripted_actions(1000 + t))
-    n, nb = np.asarray(n), np.asarray(nb)
+    n, nb = np.asarray(n), np.asarray(nb if nb else [0])
     print(f"{preset}: {envs} envs x {ticks} ticks, per env-tick: material-map lines read by the "
           f"neighbourhood loads mean {n.mean():.1f} ({n.mean() * LINE / 1024:.1f} KiB of the "
           f"{K * K / 1024:.1f} KiB map; min {n.min()} max {n.max()}); map-bank lines read by the "
