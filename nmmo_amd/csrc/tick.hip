@@ -570,7 +570,10 @@ __device__ __forceinline__ void ev_put(const Ctx& c, int idx, int p, int code, i
                                        int number, int gold, int target) {
   if (c.tev) task_accumulate(c, p, code, type, level, number, gold, target);
   if (!c.evcap) return;
-  int32_t* r = c.evg + (size_t)(idx % c.evcap) * NMMO_EVENT_COLS;
+  // ring row: a mask for power-of-two rings (the default 4,096; a uniform branch), else a
+  // division, ~20 dependent instructions per event on this latency-bound path
+  const int row = (c.evcap & (c.evcap - 1)) == 0 ? (idx & (c.evcap - 1)) : idx % c.evcap;
+  int32_t* r = c.evg + (size_t)row * NMMO_EVENT_COLS;
   r[0] = idx + 1;
   r[1] = p + 1;
   r[2] = c.tick1;
