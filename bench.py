@@ -7,15 +7,22 @@ state are resident in HBM before the timed region. Envs shard across ranks with 
 collective (weak scaling: envs per GPU fixed); each rank times K steps between a barrier +
 device sync, rank 0 reports the max over ranks.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config C4|C2|C3|C5] [--obs flat|native]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2|C3|C4|C5] [--obs flat|native]
 
 `--gpus N` with N > 1 and no WORLD_SIZE in the environment starts N ranks itself (a child
 `torch.distributed.run --nproc-per-node N`, before anything touches the GPU) and exits with its
 status; under torchrun WORLD_SIZE must equal N.
 
-Headline workload (default): BASELINE.json configs[3] = C4, 1024 envs x 128 agents per GPU,
-all ten systems, the pufferlib-flat float32 obs row the reference learner reads. At N = 1 the
-line also carries `extra_configs` (C2, C3, C4 with the native obs layout) measured the same way.
+Headline workload: at N = 1, BASELINE.json configs[3] = C4, 1024 envs x 128 agents per GPU,
+all ten systems, the pufferlib-flat float32 obs row the reference learner reads; the line also
+carries `extra_configs` (C2, C3, C4 with the native obs layout, C5 at one GPU, C4 under the
+start-kit RewardWrapper env_creator always applies) measured the same way. At N > 1 the
+headline is configs[4] = C5: 1024 envs per GPU (8192 on 8), every rank's observations + packed
+reward / dones / mask gathered into rank 0 every step (RCCL point-to-point over xGMI, wire
+records, nmmo_amd.distributed.WireGather), with gather-free C4 as the extra. C5 reports
+"delivered" (value: every agent's observation landed and validated in rank 0's HBM in the form
+the experience store decodes its kept rows from) and "decoded" (rank 0 also decodes every
+rank's buffers into the native layout each step).
 
 Steady state: envs start with staggered episode phases (`--stagger L`: during an untimed
 pre-roll of L ticks, the envs e = k mod L end their episode at pre-roll tick k, via
@@ -58,11 +65,15 @@ WORKLOADS = {
     "C4": dict(envs=1024, preset="C4", obs=True, layout="flat",
                desc="C4: 1024 envs x 128 agents, all systems + per-agent obs gather"),
     # C4 per GPU (8192 envs on 8) + the learner gather of every rank's obs/outputs each step
-    "C5": dict(envs=1024, preset="C4", obs=True, gather=True, layout="native",
-               desc="C5: 1024 envs x 128 agents per GPU, all systems + obs, RCCL point-to-point "
-                    "gather of obs/reward/dones/mask to the learner (rank 0) every step"),
+    "C5": dict(envs=1024, preset="C4", obs=True, gather=True, layout="wire",
+               desc="C5: 1024 envs x 128 agents per GPU (8192 on 8), all systems + obs, RCCL "
+                    "point-to-point gather of every rank's obs/reward/dones/mask to the learner "
+                    "(rank 0) every step"),
 }
-EXTRAS = [("C2", None), ("C3", None), ("C4", "native")]
+# (config, obs layout, wrapper) measured beside the headline
+EXTRAS = [("C2", None, None), ("C3", None, None), ("C4", "native", None), ("C5", None, None),
+          ("C4", None, "neurips23_start_kit")]
+EXTRAS_MULTI = [("C4", None, None)]
 
 # the agent sections' reward_wrapper weights (config.yaml:103-106, 118-126, 137-140)
 WRAPPER_KW = {"neurips23_start_kit": dict(heal_bonus_weight=0.03, explore_bonus_weight=0.01),
@@ -89,14 +100,19 @@ def tick_bytes_per_env(S: int, P: int, items: bool, events_per_env: float = 0.0,
     return int(2 * state + P * 4 + P * 12 * 4 + P * (4 + 1 + 1 + 1) + P * 6 + events_per_env * EVENT_ROW_BYTES)
 
 
-def obs_bytes_per_env(S: int, P: int, elems: int, native: bool = False) -> int:
-    """Obs rows written (flat fp32: 23,987 x 4 B per agent; native, SPEC §8b: 9,552 B per agent
-    + the env's 32 KB Market once) + the entity columns staged once per 16-agent workgroup +
-    the 15x15 tile window read per agent."""
+def obs_bytes_per_env(S: int, P: int, elems: int, native: bool = False, wire_bytes: float | None = None) -> float:
+    """Algorithmic bytes of one env's obs gather, each byte counted once:
+    the rows written (flat fp32: 23,987 x 4 B per agent; native, SPEC §8b: 9,552 B per agent +
+    the env's 32 KB Market once; wire, SPEC §8c: the measured record + header bytes per env)
+    + the env's 33 obs-relevant int16 entity columns read once + each agent's 15x15 window
+    materials and 12 item words read."""
     from nmmo_amd import abi
 
-    rows = abi.native_env_bytes(P) if native else P * elems * 4
-    return rows + (P // 16) * (33 * S * 2) + P * 225
+    if wire_bytes is not None:
+        rows = wire_bytes
+    else:
+        rows = abi.native_env_bytes(P) if native else P * elems * 4
+    return rows + 33 * S * 2 + P * (225 + 12 * 8)
 
 
 def pmc_traffic(cfg_name: str, kernel: str, envs: int):
@@ -126,7 +142,8 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=300)
     ap.add_argument("--warmup", type=int, default=50)
-    ap.add_argument("--config", default="C4", choices=sorted(WORKLOADS))
+    ap.add_argument("--config", default=None, choices=sorted(WORKLOADS),
+                    help="default: C4 at --gpus 1, C5 (the learner gather) at --gpus > 1")
     ap.add_argument("--envs", type=int, default=None, help="envs per GPU (default: config's)")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--stagger", type=int, default=64,
@@ -145,6 +162,7 @@ def parse(argv=None):
                     choices=["none", "base", "neurips23_start_kit", "takeru", "yaofeng"],
                     help="run env_creator's RewardWrapper on the device (SPEC §13) with the "
                          "config.yaml weights")
+    ap.add_argument("--no-decode", action="store_true", help="C5: skip the decoded pass")
     ap.add_argument("--dry-launch", action="store_true",
                     help="launcher check: each rank prints its RANK/WORLD_SIZE and exits (no GPU)")
     return ap.parse_args(argv)
@@ -258,32 +276,80 @@ def cpu_baseline(cfg, seconds: float):
 
 
 # ------------------------------------------------------------------------------- GPU workload
-def measure(args, name, layout_name, envs, rank, world, dev, steps, warmup, dist=None):
-    """Build, stagger, warm up and time one workload on this rank; returns a result dict.
-
-    Without the learner gather the rank's envs run as `--batches` batches (one handle each,
-    consecutive global env indices, so the rollout is the same as one handle's) on their own
-    streams (issue()), as the reference's async pool (config.yaml env_pool: True) overlaps env
-    batches: with obs, a batch's policy and tick run under another batch's HBM-bound obs writes;
-    without, one batch's bandwidth-bound state load overlaps the other's issue-bound phases.
-    Every env still ticks (and writes its obs) once per step."""
+def _task_embedding():
     import numpy as np
+
+    gpath = os.path.join(ROOT, "tests", "golden", "task_embeddings.npz")
+    if os.path.exists(gpath):
+        return np.load(gpath)["heldout_emb"][0]  # TickGE(1024) task, SURVEY §8d
+    return None
+
+
+def _stagger(engs, L: int, per: int, base: int, pseed: int):
+    """Staggered episode phases (module docstring): during an untimed pre-roll of L ticks, the
+    envs e = k mod L (global index) end their episode at pre-roll tick k; no obs gathered."""
+    import numpy as np
+
+    for k in range(max(0, L)):
+        for i, e in enumerate(engs):
+            ids = np.arange(per) + base + i * per
+            e.end_episodes(ids % L == k)
+            e.scripted_actions(pseed)
+            e.step(write_obs=False)
+
+
+def _kernel_timing(eng, pseed: int, steps: int):
+    """Per-kernel durations: HIP events on the launch stream around each kernel of nmmo_step,
+    over eager steps after the timed region (same state stream), one batch alone (no overlap).
+    rocprofv3's kernel trace of the same command splits these solo dispatches from the
+    overlapped ones of the timed region (tools/pmc_summary.py solo_avg_ns / overlapped_avg_ns)."""
+    eng.set_timing(True)
+    for _ in range(min(steps, 8192)):
+        eng.scripted_actions(pseed)
+        eng.step()
+    tick_ms, obs_ms, n_timed, wrap_ms = eng.read_timing()
+    eng.set_timing(False)
+    n = max(n_timed, 1)
+    return tick_ms / n, obs_ms / n, wrap_ms / n
+
+
+def _write_ceiling(t, dev):
+    """Practical HBM write ceiling on THIS box: the vendor fill kernel over the same buffer."""
+    import torch
+
+    s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t.zero_()
+    s0.record()
+    for _ in range(10):
+        t.zero_()
+    s1.record()
+    torch.cuda.synchronize(dev)
+    return t.numel() * t.element_size() / (s0.elapsed_time(s1) / 10 * 1e-3) / 1e9
+
+
+def measure(args, name, layout_name, envs, rank, world, dev, steps, warmup, dist=None, wrapper=None):
+    """Build, stagger, warm up and time one gather-free workload on this rank; returns a result
+    dict.
+
+    The rank's envs run as `--batches` batches (one handle each, consecutive global env indices,
+    so the rollout is the same as one handle's) on their own streams (issue()), as the
+    reference's async pool (config.yaml env_pool: True) overlaps env batches: with obs, a
+    batch's policy and tick run under another batch's HBM-bound obs writes; without, one batch's
+    bandwidth-bound state load overlaps the other's issue-bound phases. Every env still ticks
+    (and writes its obs) once per step."""
     import torch
 
     from nmmo_amd import abi
     from nmmo_amd.config import Config
     from nmmo_amd.engine import NmmoEngine
 
+    wrapper = wrapper or args.wrapper
     wl = WORKLOADS[name]
     native = wl["obs"] and (layout_name or wl.get("layout", "flat")) == "native"
     obs_layout = (abi.OBS_NATIVE if native else abi.OBS_FLAT) if wl["obs"] else abi.OBS_NONE
     cfg = Config.preset(wl["preset"], early_stop_agent_num=8, obs_layout=obs_layout)
-    task = None
-    gpath = os.path.join(ROOT, "tests", "golden", "task_embeddings.npz")
-    if os.path.exists(gpath):
-        task = np.load(gpath)["heldout_emb"][0]  # TickGE(1024) task, SURVEY §8d
-    gather = wl.get("gather", False)
-    nb = 1 if gather else max(1, args.batches)
+    task = _task_embedding()
+    nb = max(1, args.batches)
     if envs % nb:
         raise SystemExit(f"--batches {nb} must divide the {envs} envs per GPU")
     per = envs // nb
@@ -291,20 +357,13 @@ def measure(args, name, layout_name, envs, rank, world, dev, steps, warmup, dist
                        env_index_base=rank * envs + i * per) for i in range(nb)]
     eng = engs[0]
     for e in engs:
-        if args.wrapper != "none":
+        if wrapper != "none":
             from nmmo_amd.wrappers import wrapper_config
 
-            e.set_wrapper(wrapper_config(args.wrapper, **WRAPPER_KW.get(args.wrapper, {})))
+            e.set_wrapper(wrapper_config(wrapper, **WRAPPER_KW.get(wrapper, {})))
         e.reset()
     pseed = args.seed * 1_000_003  # the policy's Philox counter already walks (tick, episode)
-    # staggered episode phases (module docstring): untimed, obs not gathered during the pre-roll
-    L = max(0, args.stagger)
-    for k in range(L):
-        for i, e in enumerate(engs):
-            ids = np.arange(per) + rank * envs + i * per
-            e.end_episodes(ids % L == k)
-            e.scripted_actions(pseed)
-            e.step(write_obs=False)
+    _stagger(engs, args.stagger, per, rank * envs, pseed)
     # device counters the tick kernel adds into: [0] = sum(mask) (agent-steps), [1] = episodes,
     # [2] = event-log rows appended
     counters = [torch.zeros(3, dtype=torch.int64, device=dev) for _ in engs]
@@ -313,18 +372,10 @@ def measure(args, name, layout_name, envs, rank, world, dev, steps, warmup, dist
     # nb > 1: all side streams (a capture cannot run on the legacy default stream)
     streams = [torch.cuda.current_stream(dev)] if nb == 1 else [torch.cuda.Stream(device=dev) for _ in engs]
 
-    one = None
-    if gather:
-        one = _gather_stepper(eng, cfg, envs, rank, world, dev, pseed, dist)
-
     def issue(k, batches=None):
         """k steps of the given batches (default: all): batch j's steps (policy + nmmo_step) queue
         on stream j (nb == 1: the current stream, torch's capture stream inside
         torch.cuda.graph), and the hardware interleaves the streams."""
-        if gather:
-            for _ in range(k):
-                one()
-            return
         for j in (range(nb) if batches is None else batches):
             with torch.cuda.stream(streams[j]) if nb > 1 else contextlib.nullcontext():
                 for _ in range(k):
@@ -335,7 +386,7 @@ def measure(args, name, layout_name, envs, rank, world, dev, steps, warmup, dist
     issue(warmup)
     torch.cuda.synchronize(dev)
     plans = []  # per batch: the hipGraphs its stream replays
-    if not args.no_graph and not gather:  # capture-safe: no sync / alloc inside nmmo_step
+    if not args.no_graph:  # capture-safe: no sync / alloc inside nmmo_step
         g_n = max(1, min(args.graph_steps, steps))
         q, r = divmod(steps, g_n)
         for j in range(nb):
@@ -360,8 +411,6 @@ def measure(args, name, layout_name, envs, rank, world, dev, steps, warmup, dist
                     plans[j][k].replay()
     else:
         issue(steps)
-    if gather:
-        one.drain()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -370,17 +419,7 @@ def measure(args, name, layout_name, envs, rank, world, dev, steps, warmup, dist
     alive = float(tot[0].item())
     episodes = int(tot[1].item())
     events_per_env_tick = float(tot[2].item()) / (envs * steps) if cfg.event_cap > 0 else None
-    # per-kernel durations: HIP events on the launch stream around each kernel of nmmo_step,
-    # over an equal number of eager steps right after the timed region (same state stream), one
-    # batch alone (no overlap): a launch covers `per` envs. rocprofv3's kernel trace of the same
-    # command splits these solo dispatches from the overlapped ones of the timed region
-    # (tools/pmc_summary.py solo_avg_ns / overlapped_avg_ns).
-    eng.set_timing(True)
-    for _ in range(min(steps, 8192)):
-        eng.scripted_actions(pseed)
-        eng.step()
-    tick_ms, obs_ms, n_timed, wrap_ms = eng.read_timing()
-    eng.set_timing(False)
+    tick_avg_ms, obs_avg_ms, wrap_avg_ms = _kernel_timing(eng, pseed, steps)
     # The roofline's tick duration without per-kernel event overhead (which inflates a ~15 us
     # launch by ~20%): the timed step (policy + nmmo_step, graph-replayed) minus a hipGraph of
     # `batch` policy-only launches timed with HIP events on the same stream. Timing nmmo_step
@@ -399,7 +438,7 @@ def measure(args, name, layout_name, envs, rank, world, dev, steps, warmup, dist
     torch.cuda.synchronize(dev)
     policy_avg_ms = b0.elapsed_time(b1) / (reps * batch)
     solo_step_ms = None
-    if not wl["obs"] and args.wrapper == "none" and plans and nb > 1:
+    if not wl["obs"] and wrapper == "none" and plans and nb > 1:
         # one batch alone (the timed region overlaps the batches): a hipGraph of `batch` steps
         step_graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(step_graph):
@@ -413,21 +452,9 @@ def measure(args, name, layout_name, envs, rank, world, dev, steps, warmup, dist
         b1.record()
         torch.cuda.synchronize(dev)
         solo_step_ms = b0.elapsed_time(b1) / (reps * batch)
-    # practical HBM write ceiling on THIS box: the vendor fill kernel over the same obs buffer
-    fill_gbs = None
-    if wl["obs"]:
-        s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        eng.obs.zero_()
-        s0.record()
-        for _ in range(10):
-            eng.obs.zero_()
-        s1.record()
-        torch.cuda.synchronize(dev)
-        fill_gbs = eng.obs.numel() * eng.obs.element_size() / (s0.elapsed_time(s1) / 10 * 1e-3) / 1e9
+    fill_gbs = _write_ceiling(eng.obs, dev) if wl["obs"] else None
 
     S, P = eng.S, cfg.PLAYER_N
-    tick_avg_ms = tick_ms / max(n_timed, 1)
-    obs_avg_ms = obs_ms / max(n_timed, 1)
     slim = not any(x in cfg.systems for x in ("Item", "Equipment", "Profession", "Exchange"))
     tick_b = tick_bytes_per_env(S, P, "Item" in cfg.systems, events_per_env_tick or 0.0, slim) * per
     obs_b = obs_bytes_per_env(S, P, eng.obs_elems, native) * per if wl["obs"] else 0
@@ -437,7 +464,7 @@ def measure(args, name, layout_name, envs, rank, world, dev, steps, warmup, dist
     else:
         kern, byts, ms = "tick_kernel", tick_b, tick_avg_ms
         timing = "HIP events around each tick_kernel launch on the launch stream"
-        if not wl["obs"] and args.wrapper == "none" and plans:
+        if not wl["obs"] and wrapper == "none" and plans:
             if nb == 1:
                 ms = elapsed * 1e3 / steps - policy_avg_ms  # nmmo_step = the tick kernel alone
                 timing = (f"timed step (hipGraph: policy + tick) minus a {batch}-launch policy-only "
@@ -447,36 +474,20 @@ def measure(args, name, layout_name, envs, rank, world, dev, steps, warmup, dist
                 timing = (f"one batch alone after the timed region: a {batch}-step hipGraph (policy + "
                           f"tick) minus a {batch}-launch policy-only hipGraph, HIP events on the "
                           f"launch stream")
-    achieved = byts / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
-    prof_name = name + ("-native" if native and name != "C5" else "")
-    traffic, traffic_src = pmc_traffic(prof_name, kern, per)
+    prof_name = name + ("-native" if native else "") + ("" if wrapper == "none" else "+" + wrapper)
     launch = "eager" if not plans else f"hipGraph x{min(args.graph_steps, steps)} ticks"
     if nb > 1:
         launch += f", {nb} batches of {per} envs on {nb} streams"
     res = {
-        "name": prof_name, "envs": envs, "cfg": cfg, "native": native, "S": S, "P": P,
+        "name": prof_name, "envs": envs, "cfg": cfg, "layout": "native" if native else "flat", "S": S, "P": P,
         "elapsed": elapsed, "alive": alive, "slots": float(envs * P * steps), "episodes": episodes,
-        "events_per_env_tick": events_per_env_tick, "gather": gather, "launch": launch,
+        "events_per_env_tick": events_per_env_tick, "gather": False, "launch": launch, "wrapper": wrapper,
         "kernel_ms": {"policy": round(policy_avg_ms, 5), "tick": round(tick_avg_ms, 5),
                       "obs": round(obs_avg_ms, 5) if wl["obs"] else None,
-                      "wrapper": round(wrap_ms / max(n_timed, 1), 5) if args.wrapper != "none" else None},
-        "roofline": {
-            "kernel": kern, "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-            "traffic_source": traffic_src, "bytes_per_launch": byts, "envs_per_launch": per,
-            "avg_launch_ms": round(ms, 5), "timing": timing,
-            # the dominant kernel's bytes of a whole step over the timed step time: a floor on
-            # its in-run rate (policy and tick share the step; --batches overlaps them)
-            "timed_step_gbs": round(byts * nb / (elapsed / steps) / 1e9, 1),
-            "concurrent_batches": nb,
-            "write_ceiling_gbs": None if fill_gbs is None else round(fill_gbs, 1),
-            "frac_of_write_ceiling": None if not fill_gbs or kern != "obs_kernel" else round(achieved / fill_gbs, 4),
-        },
-        "gather_bytes": getattr(one, "bytes_per_step", None),
+                      "wrapper": round(wrap_avg_ms, 5) if wrapper != "none" else None},
+        "roofline": _roofline(prof_name, kern, byts, ms, per, timing, nb, elapsed / steps, fill_gbs),
         "batches": nb,
     }
-    if gather:
-        one.close()
     for e in engs:
         e.close()
     del eng, engs
@@ -484,111 +495,126 @@ def measure(args, name, layout_name, envs, rank, world, dev, steps, warmup, dist
     return res
 
 
-def _gather_stepper(eng, cfg, envs, rank, world, dev, pseed, dist):
-    """C5's step: tick + obs into one of two obs buffers, then the learner gather of that step's
-    observations and packed reward/term/trunc/mask into rank 0 (point-to-point sends over xGMI
-    on a side stream, one step behind the compute stream so they overlap the next tick). The
-    root uses its own shard in place (no self-copy). Native obs travel wire-encoded (SPEC §8c,
-    nmmo_wire_pack: ~1.3 KB per agent instead of 9,552 B) and the root decodes every peer's
-    buffer back into its native receive buffer (the learner's tensor); flat obs (`--obs flat`)
-    travel as they are."""
+def _roofline(prof_name, kern, byts, ms, per, timing, nb, step_s, fill_gbs):
+    achieved = byts / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
+    traffic, traffic_src = pmc_traffic(prof_name, kern, per)
+    return {
+        "kernel": kern, "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+        "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+        "traffic_source": traffic_src, "bytes_per_launch": round(byts), "envs_per_launch": per,
+        "avg_launch_ms": round(ms, 5), "timing": timing,
+        # the dominant kernel's bytes of a whole step over the timed step time: a floor on its
+        # in-run rate (policy and tick share the step; --batches overlaps them)
+        "timed_step_gbs": round(byts * nb / step_s / 1e9, 1),
+        "concurrent_batches": nb,
+        "write_ceiling_gbs": None if fill_gbs is None else round(fill_gbs, 1),
+        "frac_of_write_ceiling": None if not fill_gbs or kern != "obs_kernel" else round(achieved / fill_gbs, 4),
+    }
+
+
+def measure_gather(args, name, envs, rank, world, dev, steps, warmup, dist=None, backend="nccl"):
+    """C5: the rank's envs as `--batches` wire-obs handles stepped by WireGather (policy +
+    nmmo_step into a ring of wire buffers, hipGraph-captured, one stream per batch; the learner
+    gather into rank 0 one step behind on a comm stream). Two timed passes over the same
+    engines: "delivered" (rank 0 validates every received buffer on the device) and "decoded"
+    (rank 0 also decodes every rank's buffers into the native layout each step)."""
     import torch
 
-    from nmmo_amd import abi, devmem, wire
-    from nmmo_amd import distributed as nd
+    from nmmo_amd import abi
+    from nmmo_amd import wire as nw
+    from nmmo_amd.config import Config
+    from nmmo_amd.distributed import WireGather
+    from nmmo_amd.engine import NmmoEngine
 
-    def like(t):  # large obs buffers chunk-mapped like the engine's own (DESIGN §3.2)
-        return devmem.empty(tuple(t.shape), t.dtype, dev)
-
-    native = eng.config.obs_layout == abi.OBS_NATIVE
-    bufs = [eng.obs, like(eng.obs)]
-    smalls = [torch.empty((envs, cfg.PLAYER_N, 8), dtype=torch.uint8, device=dev) for _ in range(2)]
-    wires = [torch.empty(wire.max_bytes(envs, cfg.PLAYER_N), dtype=torch.uint8, device=dev)
-             for _ in range(2)] if native and world > 1 else None
-    hdr = wire.header_bytes(envs, cfg.PLAYER_N) if native else 0
-    comm = torch.cuda.Stream(device=dev)
-    done_ev = [None, None]  # compute-stream wait: the exchange of the step that used this buffer
-    recv = None
-    if rank == 0 and world > 1:
-        recv = {r: {"obs": like(bufs[0]), "small": torch.empty_like(smalls[0]),
-                    "wire": torch.empty_like(wires[0]) if native else None} for r in range(1, world)}
-
-    class Stepper:
-        t = 0
-        pending = None  # (buffer index, ready event) of the step whose exchange is still to run
-        sent_bytes = 0
-        bytes_per_step = None
-
-        def _exchange(self, i, ready):
-            with torch.cuda.stream(comm):
-                comm.wait_event(ready)
-                if rank == 0:
-                    ops = [dist.P2POp(dist.irecv, recv[r]["small"], r) for r in recv]
-                    if native:
-                        got = nd.gather_wire_to_learner(wires[i], hdr,
-                                                        recv_bufs=[None] + [recv[r]["wire"] for r in recv])
-                        for r in recv:  # decode each peer's wire buffer into its native obs
-                            wire.unpack(got[r], envs, cfg.PLAYER_N, out=recv[r]["obs"])
-                            self.sent_bytes += got[r].numel()
-                    else:
-                        ops += [dist.P2POp(dist.irecv, recv[r]["obs"], r) for r in recv]
-                        self.sent_bytes += (world - 1) * bufs[i].numel() * bufs[i].element_size()
-                    for w in dist.batch_isend_irecv(ops):
-                        w.wait()
-                else:
-                    ops = [dist.P2POp(dist.isend, smalls[i], 0)]
-                    if native:
-                        nd.gather_wire_to_learner(wires[i], hdr)
-                    else:
-                        ops.append(dist.P2POp(dist.isend, bufs[i], 0))
-                    for w in dist.batch_isend_irecv(ops):
-                        w.wait()
-                ev = torch.cuda.Event()
-                ev.record(comm)
-            done_ev[i] = ev
-
-        def __call__(self):
-            i = self.t % 2
-            cur = torch.cuda.current_stream(dev)
-            if done_ev[i] is not None:
-                cur.wait_event(done_ev[i])  # the exchange of step t-2 has read this buffer
-            eng.obs = bufs[i]
-            eng.scripted_actions(pseed)
-            eng.step()
-            sm = smalls[i]
-            sm[..., 0:4] = eng.rew.view(torch.uint8).view(envs, cfg.PLAYER_N, 4)
-            sm[..., 4] = eng.term
-            sm[..., 5] = eng.trunc
-            sm[..., 6] = eng.mask
-            if world > 1:
-                if native:
-                    wire.pack(eng, bufs[i], out=wires[i])
-                ready = torch.cuda.Event()
-                ready.record(cur)
-                if self.pending is not None:  # step t-1's exchange, now that step t is queued
-                    self._exchange(*self.pending)
-                self.pending = (i, ready)
-            self.t += 1
-
-        def drain(self):
-            if self.pending is not None:
-                self._exchange(*self.pending)
-                self.pending = None
-            torch.cuda.current_stream(dev).wait_stream(comm)
-            if world > 1 and self.t:
-                self.bytes_per_step = self.sent_bytes / self.t + (world - 1) * smalls[0].numel()
-
-        def close(self):
-            torch.cuda.synchronize(dev)
-            eng.obs = bufs[0]
-
-    return Stepper()
+    wl = WORKLOADS[name]
+    cfg = Config.preset(wl["preset"], early_stop_agent_num=8, obs_layout=abi.OBS_WIRE)
+    nb = max(1, args.batches)
+    if envs % nb:
+        raise SystemExit(f"--batches {nb} must divide the {envs} envs per GPU")
+    per = envs // nb
+    task = _task_embedding()
+    engs = [NmmoEngine(cfg, per, seed=args.seed, device=dev, task_embedding=task,
+                       env_index_base=rank * envs + i * per) for i in range(nb)]
+    for e in engs:
+        e.reset()
+    pseed = args.seed * 1_000_003
+    _stagger(engs, args.stagger, per, rank * envs, pseed)
+    counters = [torch.zeros(3, dtype=torch.int64, device=dev) for _ in engs]
+    for e, c in zip(engs, counters):
+        e.set_counters(c)
+    torch.cuda.synchronize(dev)
+    passes = {}
+    for decode in ((False,) if args.no_decode else (False, True)):
+        g = WireGather(engs, pseed, rank, world, decode=decode, graphs=not args.no_graph, backend=backend)
+        for _ in range(warmup):
+            g.step()
+        g.drain()
+        torch.cuda.synchronize(dev)
+        for c in counters:
+            c.zero_()
+        b0 = g.x.payload_bytes
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            g.step()
+        g.drain()
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        tot = torch.stack(counters).sum(0)
+        status = g.check_status()
+        if status:
+            raise RuntimeError(f"nmmo_wire_check flagged received wire buffers (status {status})")
+        passes[decode] = {"elapsed": elapsed, "alive": float(tot[0].item()), "episodes": int(tot[1].item()),
+                          "events": float(tot[2].item()),
+                          "payload_bytes_per_step": (g.x.payload_bytes - b0) / steps}
+        g.close()
+    eng = engs[0]
+    tick_avg_ms, obs_avg_ms, _ = _kernel_timing(eng, pseed, steps)
+    wire_env_bytes = nw.total_bytes(eng.obs) / per  # this batch's last step: header + records
+    S, P = eng.S, cfg.PLAYER_N
+    d = passes[False]
+    events_per_env_tick = d["events"] / (envs * steps)
+    tick_b = tick_bytes_per_env(S, P, True, events_per_env_tick) * per
+    obs_b = obs_bytes_per_env(S, P, eng.obs_elems, wire_bytes=wire_env_bytes) * per
+    if obs_avg_ms > tick_avg_ms:
+        kern, byts, ms = "obs_kernel", obs_b, obs_avg_ms
+        timing = ("HIP events around each wire obs gather (wire_count + wire_scan + obs_kernel) on the launch "
+                  "stream")
+    else:
+        kern, byts, ms = "tick_kernel", tick_b, tick_avg_ms
+        timing = "HIP events around each tick_kernel launch on the launch stream"
+    res = {
+        "name": name, "envs": envs, "cfg": cfg, "layout": "wire", "S": S, "P": P,
+        "elapsed": d["elapsed"], "alive": d["alive"], "slots": float(envs * P * steps), "episodes": d["episodes"],
+        "events_per_env_tick": events_per_env_tick, "gather": True, "wrapper": "none",
+        "launch": f"hipGraph per step and ring slot, {nb} batches of {per} envs on {nb} streams, gather on a "
+                  f"comm stream one step behind",
+        "kernel_ms": {"policy": None, "tick": round(tick_avg_ms, 5), "obs": round(obs_avg_ms, 5), "wrapper": None},
+        "roofline": _roofline(name, kern, byts, ms, per, timing, nb, d["elapsed"] / steps, None),
+        "batches": nb,
+        "gather_bytes": d["payload_bytes_per_step"] if world > 1 else 0,
+        "wire_bytes_per_agent_in_realm": round(wire_env_bytes * per * nb * steps / max(d["alive"], 1.0), 1),
+        "decoded": passes.get(True),
+    }
+    for e in engs:
+        e.close()
+    del eng, engs
+    torch.cuda.empty_cache()
+    return res
 
 
 def result_line(res, args, world, steps, alive_total, slots_total, elapsed, warmup):
     cfg = res["cfg"]
-    wl_desc = next(w["desc"] for k, w in WORKLOADS.items() if res["name"].split("-")[0] == k)
-    return {
+    wl_desc = WORKLOADS[res["name"].split("-")[0].split("+")[0]]["desc"]
+    obs = {"flat": "pufferlib-flat fp32 (23,987/agent)",
+           "native": "native nmmo dtypes (SPEC §8b, 9,552 B/agent + 32 KB Market/env)",
+           "wire": "wire records (SPEC §8c) written straight from the state"}[res["layout"]] \
+        if WORKLOADS[res["name"].split("-")[0].split("+")[0]]["obs"] else "none"
+    line = {
         "value": round(alive_total / elapsed, 1),
         "ms_per_step": round(elapsed * 1e3 / steps, 4),
         "config": {
@@ -597,12 +623,12 @@ def result_line(res, args, world, steps, alive_total, slots_total, elapsed, warm
             "agents_per_env": res["P"],
             "npcs_per_env": res["S"] - res["P"],
             "systems": list(cfg.systems),
-            "obs": ("native nmmo dtypes (SPEC §8b, 9,552 B/agent + 32 KB Market/env)" if res["native"] else
-                    "pufferlib-flat fp32 (23,987/agent)") if WORKLOADS[res["name"].split("-")[0]]["obs"] else "none",
+            "obs": obs,
+            "wrapper": None if res.get("wrapper", "none") == "none" else res["wrapper"],
             "early_stop_agent_num": 8,
             "stagger_ticks": args.stagger,
             "env_batches": res["batches"],
-            "parallelism": f"env-shard x{world}",
+            "parallelism": f"env-shard x{world}" + (", learner gather to rank 0" if res["gather"] else ""),
         },
         "slot_steps_per_sec": round(slots_total / elapsed, 1),
         "alive_fraction": round(alive_total / slots_total, 4),
@@ -612,6 +638,20 @@ def result_line(res, args, world, steps, alive_total, slots_total, elapsed, warm
         "launch": res["launch"],
         "roofline": res["roofline"],
     }
+    if res["gather"]:
+        line["wire_bytes_per_agent_in_realm"] = res["wire_bytes_per_agent_in_realm"]
+    return line
+
+
+def _gather_fields(res, world, backend, steps):
+    """The C5 line's gather description and its decoded pass (whole job, max over ranks)."""
+    via = "RCCL" if backend == "nccl" else "gloo (rehearsal)"
+    out = {"gather": (f"{via} point-to-point sends into rank 0 of {round(res['gather_bytes'])} B/step of wire "
+                      f"records (+ reward/dones/mask), one step behind the compute on a comm stream; rank 0 "
+                      f"validates every received buffer (nmmo_wire_check) and keeps its own in place"
+                      if world > 1 else "N = 1: rank 0's own wire buffers in place, nothing sent"),
+           "gather_bytes_per_step": round(res["gather_bytes"]) if world > 1 else 0}
+    return out
 
 
 def main():
@@ -658,28 +698,49 @@ def main():
         else:
             dist.init_process_group("nccl", device_id=dev)
 
-    wl = WORKLOADS[args.config]
+    name = args.config or ("C4" if world == 1 else "C5")
+    wl = WORKLOADS[name]
     envs = args.envs or wl["envs"]
-    res = measure(args, args.config, args.obs, envs, rank, world, dev, args.steps, args.warmup, dist)
-    vals = torch.tensor([res["elapsed"], res["alive"], res["slots"]], dtype=torch.float64, device=dev)
-    if world > 1:
-        t_max = vals[0:1].clone()
-        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
-        sums = vals[1:3].clone()
-        dist.all_reduce(sums, op=dist.ReduceOp.SUM)
-        elapsed, alive_total, slots_total = float(t_max.item()), float(sums[0].item()), float(sums[1].item())
-    else:
-        elapsed, alive_total, slots_total = res["elapsed"], res["alive"], res["slots"]
+
+    def run(nm, lay, wrapper, n_envs, steps, warmup):
+        if WORKLOADS[nm].get("gather"):
+            return measure_gather(args, nm, n_envs, rank, world, dev, steps, warmup, dist, backend)
+        return measure(args, nm, lay, n_envs, rank, world, dev, steps, warmup, dist, wrapper)
+
+    def reduce(res, key="elapsed", alive="alive"):
+        vals = torch.tensor([res[key], res[alive], res["slots"]], dtype=torch.float64, device=dev)
+        if world > 1:
+            t_max = vals[0:1].clone()
+            dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+            sums = vals[1:3].clone()
+            dist.all_reduce(sums, op=dist.ReduceOp.SUM)
+            return float(t_max.item()), float(sums[0].item()), float(sums[1].item())
+        return res[key], res[alive], res["slots"]
+
+    res = run(name, args.obs, None, envs, args.steps, args.warmup)
+    elapsed, alive_total, slots_total = reduce(res)
+    decoded = None
+    if res.get("decoded"):
+        dres = dict(res, elapsed=res["decoded"]["elapsed"], alive=res["decoded"]["alive"])
+        d_el, d_alive, d_slots = reduce(dres)
+        decoded = {"value": round(d_alive / d_el, 1), "ms_per_step": round(d_el * 1e3 / args.steps, 4),
+                   "what": "rank 0 also decodes every rank's wire buffers into the native layout "
+                           "(nmmo_wire_unpack) each step: the full learner-ready obs tensor"}
 
     extras = {}
-    if world == 1 and not args.no_extras and args.config == "C4" and not args.envs:
+    if not args.no_extras and not args.envs and args.config is None:
         ex_steps, ex_warm = max(args.steps, 100), max(args.warmup, 20)
-        for name, lay in EXTRAS:
-            if name == args.config and (lay or "flat") == (args.obs or "flat"):
-                continue
-            r = measure(args, name, lay, WORKLOADS[name]["envs"], 0, 1, dev, ex_steps, ex_warm)
-            line = result_line(r, args, 1, ex_steps, r["alive"], r["slots"], r["elapsed"], ex_warm)
+        for nm, lay, wrapper in (EXTRAS if world == 1 else EXTRAS_MULTI):
+            r = run(nm, lay, wrapper, WORKLOADS[nm]["envs"], ex_steps, ex_warm)
+            el, al, sl = reduce(r)
+            line = result_line(r, args, world, ex_steps, al, sl, el, ex_warm)
             line["steps"], line["warmup"] = ex_steps, ex_warm
+            if r.get("gather"):
+                line.update(_gather_fields(r, world, backend, ex_steps))
+                if r.get("decoded"):
+                    dres = dict(r, elapsed=r["decoded"]["elapsed"], alive=r["decoded"]["alive"])
+                    d_el, d_al, _ = reduce(dres)
+                    line["decoded"] = {"value": round(d_al / d_el, 1), "ms_per_step": round(d_el * 1e3 / ex_steps, 4)}
             extras[r["name"]] = line
 
     if rank == 0:
@@ -712,12 +773,9 @@ def main():
         line.update(body)
         line["wrapper"] = None if args.wrapper == "none" else args.wrapper
         if res["gather"]:
-            how = ("wire-encoded native obs (SPEC §8c), decoded on rank 0 into its native buffers"
-                   if res["native"] else "flat obs")
-            via = "RCCL" if backend == "nccl" else "gloo (rehearsal)"
-            line["gather"] = (f"{via} point-to-point sends into rank 0 of {res['gather_bytes']} B/step "
-                              f"({how}) + reward/dones/mask, one step behind on a side stream"
-                              if res["gather_bytes"] else "N = 1: rank 0's own shard in place, nothing sent")
+            line.update(_gather_fields(res, world, backend, args.steps))
+            line["value_kind"] = "delivered"
+            line["decoded"] = decoded
         else:
             line["gather"] = None
         line["cpu_baseline"] = cpu

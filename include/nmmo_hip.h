@@ -42,7 +42,7 @@ extern "C" {
 #endif
 
 #define NMMO_API __attribute__((visibility("default")))
-#define NMMO_ABI_VERSION 6
+#define NMMO_ABI_VERSION 7
 
 /* ---- error codes ---- */
 #define NMMO_OK 0
@@ -66,6 +66,9 @@ extern "C" {
 #define NMMO_OBS_NONE 0   /* C2/C3 benchmark configs: state only */
 #define NMMO_OBS_FLAT 1   /* pufferlib-0.7.3 flat float32 vector, 23,987 / agent */
 #define NMMO_OBS_NATIVE 2 /* nmmo space dtypes, Market once per env (SPEC.md §8b) */
+#define NMMO_OBS_WIRE 3   /* the wire records of SPEC.md §8c written straight from the state
+                             (the learner-gather transport; nmmo_wire_unpack gives the native
+                             layout, nmmo_exp_store decodes kept rows to flat rows) */
 #define NMMO_NATIVE_MASK_BYTES 1600   /* u8 ActionTargets (1,586) + pad */
 #define NMMO_NATIVE_I16 3976          /* int16 part of an agent row */
 #define NMMO_NATIVE_ROW_BYTES (NMMO_NATIVE_MASK_BYTES + 2 * NMMO_NATIVE_I16)  /* 9,552 */
@@ -273,19 +276,21 @@ NMMO_API void nmmo_destroy(NmmoHandle* h);
 /* Reset every env (env_seeds: host uint64[n_envs] or NULL = derive from the create seed). */
 NMMO_API int nmmo_reset(NmmoHandle* h, const uint64_t* env_seeds, void* obs, uint8_t* mask, void* stream);
 
-/* Ends the current episode of every env whose host_env_mask[e] != 0 (host u8 [n_envs]): the
+/* Ends the current episode of every env whose dev_env_mask[e] != 0 (device u8 [n_envs]): the
  * env's next nmmo_step resets it instead of stepping (the auto-reset path, rewards/flags 0),
  * exactly as if its previous step had ended the episode; the ended episode's agents are not
  * reported as truncated. This is the per-env `env.reset()` the reference's async worker pool
  * issues independently for each env (pufferlib vectorization, clean_pufferl.py:106-114,175);
- * bench.py uses it to stagger episode phases across envs. Synchronous. */
-NMMO_API int nmmo_end_episodes(NmmoHandle* h, const uint8_t* host_env_mask);
+ * bench.py uses it to stagger episode phases across envs. Enqueued on `stream` (no device
+ * synchronisation; graph-capturable). */
+NMMO_API int nmmo_end_episodes(NmmoHandle* h, const uint8_t* dev_env_mask, void* stream);
 
 /* One tick of every env. actions: device int32 [n_envs][player_n][12]. Envs whose previous
  * step ended the episode are reset instead (pufferlib auto-reset), with rewards/flags 0.
  * obs: device float32 [n_envs][player_n][obs_elems] (NMMO_OBS_FLAT), the native layout
  * [n_envs] x (player_n x NMMO_NATIVE_ROW_BYTES + NMMO_NATIVE_MARKET_BYTES) (NMMO_OBS_NATIVE),
- * or NULL (NMMO_OBS_NONE).
+ * a wire buffer of nmmo_wire_max_bytes (NMMO_OBS_WIRE: header + records, SPEC.md §8c; its
+ * bytes equal nmmo_wire_pack of the native obs of the same state), or NULL (no obs gather).
  * rew f32, term/trunc/mask u8: device [n_envs][player_n]. */
 NMMO_API int nmmo_step(NmmoHandle* h, const int32_t* actions, void* obs, float* rew, uint8_t* term,
               uint8_t* trunc, uint8_t* mask, void* stream);
@@ -340,7 +345,9 @@ NMMO_API int nmmo_expand_obs(NmmoHandle* h, const void* native, float* flat, int
  * chunks into one contiguous virtual range (hipMemCreate / hipMemMap). Large hipMalloc
  * allocations landed on physical placements whose write rate varied 5.4-6.5 TB/s under the obs
  * kernel's store pattern; chunk-mapped ones wrote at 6.5-6.6 TB/s every time. Synchronous;
- * nmmo_dev_free synchronises the device first. */
+ * NMMO_E_INVALID on a device without virtual memory management (the caller falls back to a
+ * plain allocation). nmmo_dev_free synchronises the device first: call it at a sync point
+ * (nmmo_amd/devmem.py defers it to one), never while a stream is capturing a graph. */
 NMMO_API int nmmo_dev_alloc(int32_t device, uint64_t bytes, void** out);
 NMMO_API int nmmo_dev_free(void* ptr);
 
@@ -359,10 +366,20 @@ NMMO_API int nmmo_dev_free(void* ptr);
 NMMO_API int64_t nmmo_wire_header_bytes(int32_t n_envs, int32_t player_n);
 /* Upper bound of a wire buffer (every agent in the realm with 100 visible entities, 12 items). */
 NMMO_API int64_t nmmo_wire_max_bytes(int32_t n_envs, int32_t player_n);
-/* Encodes `native` (the NMMO_OBS_NATIVE buffer of h's most recent nmmo_step / nmmo_reset; the
- * per-agent counts come from that launch) into `wire` (device, nmmo_wire_max_bytes). Enqueued;
- * the buffer's total size is its first int64 once the stream reaches it. */
+/* Encodes `native` (the NMMO_OBS_NATIVE buffer of h's most recent obs gather; the per-agent
+ * counts and the listing count come from that launch) into `wire` (device,
+ * nmmo_wire_max_bytes). NMMO_E_INVALID when `native` is not the buffer the last obs gather
+ * wrote, or a tick ran after it without an obs gather (the buffer no longer describes the
+ * state the counts were taken from). Enqueued; the buffer's total size is its first int64
+ * once the stream reaches it. */
 NMMO_API int nmmo_wire_pack(NmmoHandle* h, const void* native, void* wire, void* stream);
+/* Consistency check of a (received) wire buffer of n_envs x player_n agents: its announced
+ * total against *dev_expect_total (device int64, or NULL to skip), the env payload offsets
+ * against the count words and listing counts, the count ranges, and every record head's
+ * AgentId / nv / ninv against its count word. ORs error bits into *dev_status (device int32:
+ * 1 total, 2 offsets, 4 count ranges, 8 record heads; 0 = valid). Enqueued; needs no handle. */
+NMMO_API int nmmo_wire_check(const void* wire, int32_t n_envs, int32_t player_n, const int64_t* dev_expect_total,
+                             int32_t* dev_status, void* stream);
 /* Decodes a wire buffer of n_envs x player_n agents into the native layout (every byte of the
  * n_envs x (player_n x NMMO_NATIVE_ROW_BYTES + NMMO_NATIVE_MARKET_BYTES) buffer is written;
  * bit-identical to what the sender's nmmo_step wrote). Enqueued; needs no handle. */
@@ -450,13 +467,16 @@ typedef struct NmmoStoreInput {
   const int32_t* actions; /* [n_rows][12] */
   const float* logprobs;  /* [n_rows] */
   const float* values;    /* [n_rows] */
+  const void* wire;       /* NMMO_OBS_WIRE / nmmo_wire_pack buffer of n_rows / player_n envs (needs a
+                             handle for the layout and task table), or NULL */
 } NmmoStoreInput;
 
 /* int32 scratch the storage calls need: max(n_rows + n_rows/512 + 2, n_slots). */
 NMMO_API int64_t nmmo_exp_scratch_ints(int32_t max_rows, int32_t n_slots);
 /* Appends the mask-selected rows of one recv (in row order, cut at the capacity) and advances
- * *ptr on the device; native obs are expanded straight into the flat experience rows (h = the
- * handle whose layout/task table produced them; NULL for flat obs). Enqueued on `stream`. */
+ * *ptr on the device; exactly one of obs / native / wire: native obs are expanded, and wire
+ * records decoded, straight into the flat experience rows of the kept rows only (h = a handle
+ * whose layout and task table produced them; NULL for flat obs). Enqueued on `stream`. */
 NMMO_API int nmmo_exp_store(NmmoHandle* h, const NmmoExperience* x, const NmmoStoreInput* in,
                             int32_t* scratch, void* stream);
 /* idxs (device int32 [*ptr]) = the row order sorted by (env_id, step). Enqueued. */

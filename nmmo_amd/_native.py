@@ -25,7 +25,7 @@ SYMBOLS = [
     "nmmo_exp_store", "nmmo_exp_sort", "nmmo_exp_gae", "nmmo_gather_rows", "nmmo_n_envs",
     "nmmo_last_error", "nmmo_abi_version", "nmmo_end_episodes", "nmmo_build_info",
     "nmmo_get_wrapper_dropped", "nmmo_set_task_weights", "nmmo_wire_header_bytes", "nmmo_wire_max_bytes",
-    "nmmo_wire_pack", "nmmo_wire_unpack", "nmmo_dev_alloc", "nmmo_dev_free", "nmmo_observe",
+    "nmmo_wire_pack", "nmmo_wire_unpack", "nmmo_wire_check", "nmmo_dev_alloc", "nmmo_dev_free", "nmmo_observe",
 ]
 
 
@@ -79,7 +79,7 @@ def lib():
     L.nmmo_n_envs.argtypes = [vp]
     L.nmmo_last_error.restype = ctypes.c_char_p
     L.nmmo_abi_version.restype = i32
-    L.nmmo_end_episodes.argtypes = [vp, vp]
+    L.nmmo_end_episodes.argtypes = [vp, vp, vp]
     L.nmmo_get_wrapper_dropped.argtypes = [vp, ctypes.POINTER(ctypes.c_int64)]
     L.nmmo_wire_header_bytes.argtypes = [i32, i32]
     L.nmmo_wire_header_bytes.restype = ctypes.c_int64
@@ -87,6 +87,7 @@ def lib():
     L.nmmo_wire_max_bytes.restype = ctypes.c_int64
     L.nmmo_wire_pack.argtypes = [vp, vp, vp, vp]
     L.nmmo_wire_unpack.argtypes = [i32, i32, vp, vp, vp]
+    L.nmmo_wire_check.argtypes = [vp, i32, i32, vp, vp, vp]
     L.nmmo_dev_alloc.argtypes = [i32, u64, ctypes.POINTER(vp)]
     L.nmmo_dev_free.argtypes = [vp]
     L.nmmo_build_info.restype = ctypes.c_char_p

@@ -6,7 +6,7 @@ struct sizes against the compiled library and the enum values against the header
 
 import ctypes
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 NMMO_OK = 0
 NMMO_E_INVALID = -1
@@ -27,6 +27,7 @@ SYS_ALL = 0xFF
 OBS_NONE = 0
 OBS_FLAT = 1
 OBS_NATIVE = 2
+OBS_WIRE = 3  # SPEC.md §8c wire records straight from the state (the learner-gather transport)
 # native layout (SPEC.md §8b)
 NATIVE_MASK_BYTES = 1600
 NATIVE_I16 = 3976
@@ -238,4 +239,5 @@ class NmmoStoreInput(ctypes.Structure):
     _fields_ = [("n_rows", ctypes.c_int32), ("step", ctypes.c_int32), ("obs", ctypes.c_void_p),
                 ("native", ctypes.c_void_p), ("rewards", ctypes.c_void_p), ("dones", ctypes.c_void_p),
                 ("mask", ctypes.c_void_p), ("env_id", ctypes.c_void_p), ("env_id_base", ctypes.c_int32),
-                ("actions", ctypes.c_void_p), ("logprobs", ctypes.c_void_p), ("values", ctypes.c_void_p)]
+                ("actions", ctypes.c_void_p), ("logprobs", ctypes.c_void_p), ("values", ctypes.c_void_p),
+                ("wire", ctypes.c_void_p)]

@@ -58,6 +58,10 @@ struct NmmoHandle {
   int32_t* d_assign = nullptr;
   NmmoTaskState* d_tstate = nullptr;
   uint16_t* d_wcount = nullptr;  // native obs: per-agent wire count words of the last obs (wire.hip)
+  int32_t* d_wmcount = nullptr;  // native obs: per-env listing count of the last obs
+  // the native buffer the last obs gather wrote, and whether no tick ran since (nmmo_wire_pack)
+  const void* last_native = nullptr;
+  bool native_fresh = false;
   // wrapper layer (nmmo_set_wrapper, SPEC §13)
   bool wrap_on = false;
   NmmoWrapperConfig wc{};
@@ -177,7 +181,7 @@ void nmmo_destroy(NmmoHandle* h) {
   void* bufs[] = {h->d_env,  h->d_ent,   h->d_ring,  h->d_mat,   h->d_dep,   h->d_bank,
                   h->d_task, h->d_seeds, h->d_items, h->d_iring, h->d_mlist, h->d_mcount,
                   h->d_events, h->d_tasks, h->d_assign, h->d_tstate, h->d_ws, h->d_uniq, h->d_wenv, h->d_wdrop, h->d_task_cum,
-                  h->d_wcount, h->d_foreign};
+                  h->d_wcount, h->d_wmcount, h->d_foreign};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   delete h;
@@ -196,7 +200,8 @@ int nmmo_create(const NmmoConfig* cfg, int32_t n_envs, uint64_t seed, int32_t de
   if (cfg->horizon <= 0 || cfg->task_num_tick <= 0) return fail(NMMO_E_INVALID, "horizon/task_num_tick");
   if (cfg->task_embed_dim < 0 || cfg->task_embed_dim > 65536) return fail(NMMO_E_INVALID, "task_embed_dim");
   if (cfg->event_cap < 0 || cfg->event_cap > (1 << 24)) return fail(NMMO_E_INVALID, "event_cap in 0..2^24");
-  if (cfg->obs_layout != NMMO_OBS_NONE && cfg->obs_layout != NMMO_OBS_FLAT && cfg->obs_layout != NMMO_OBS_NATIVE)
+  if (cfg->obs_layout != NMMO_OBS_NONE && cfg->obs_layout != NMMO_OBS_FLAT && cfg->obs_layout != NMMO_OBS_NATIVE &&
+      cfg->obs_layout != NMMO_OBS_WIRE)
     return fail(NMMO_E_INVALID, "obs_layout %d", cfg->obs_layout);
   NmmoHandle* h = new NmmoHandle();
   h->cfg = *cfg;
@@ -229,6 +234,7 @@ int nmmo_create(const NmmoConfig* cfg, int32_t n_envs, uint64_t seed, int32_t de
   ALLOC(h->d_tstate, n * P * sizeof(NmmoTaskState));
   if (cfg->obs_layout == NMMO_OBS_NATIVE) {
     ALLOC(h->d_wcount, n * P * 2);
+    ALLOC(h->d_wmcount, n * 4);
   }
 #undef ALLOC
   if (init_kernels() != hipSuccess) return cleanup_fail(fail(NMMO_E_HIP, "kernel attributes"));
@@ -260,10 +266,11 @@ int nmmo_create(const NmmoConfig* cfg, int32_t n_envs, uint64_t seed, int32_t de
 static ObsParams obs_params(NmmoHandle* h, void* obs) {
   const NmmoLayout& L = h->layout;
   ObsParams p;
-  const bool native = h->cfg.obs_layout == NMMO_OBS_NATIVE;
+  const bool native = h->cfg.obs_layout == NMMO_OBS_NATIVE, wire = h->cfg.obs_layout == NMMO_OBS_WIRE;
   p.env = h->d_env; p.ent = h->d_ent; p.mat = h->d_mat; p.task = h->d_task;
-  p.obs = native ? nullptr : (float*)obs;
+  p.obs = native || wire ? nullptr : (float*)obs;
   p.nat = native ? (uint8_t*)obs : nullptr;
+  p.wire = wire ? (uint8_t*)obs : nullptr;
   p.items = h->d_items; p.mlist = h->d_mlist; p.mcount = h->d_mcount; p.assign = h->d_assign;
   p.n_envs = h->st.n_envs; p.P = h->st.P; p.S = h->st.S; p.elems = L.obs_elems;
   p.task_dim = h->cfg.task_embed_dim; p.systems = h->cfg.systems;
@@ -279,6 +286,7 @@ static ObsParams obs_params(NmmoHandle* h, void* obs) {
   p.o_tile = L.off_tile;
   p.row_map = nullptr;
   p.wcount = native ? h->d_wcount : nullptr;
+  p.wmcount = native ? h->d_wmcount : nullptr;
   p.ws = h->wrap_on ? h->d_ws : nullptr;
   p.wflags = 0;
   if (h->wrap_on) {
@@ -312,7 +320,10 @@ int nmmo_reset(NmmoHandle* h, const uint64_t* env_seeds, void* obs, uint8_t* mas
                       mask, 1, s));
   HIP_TRY(hipMemsetAsync(h->d_foreign, 0, 4, s));  // every env's tiles now match its bank
   if (h->wrap_on) HIP_TRY(launch_wrap(wrap_params(h, nullptr, nullptr, nullptr, nullptr, nullptr), 0, s));
-  if (obs && h->cfg.obs_layout != NMMO_OBS_NONE) HIP_TRY(launch_obs(obs_params(h, obs), s));
+  const bool do_obs = obs && h->cfg.obs_layout != NMMO_OBS_NONE;
+  if (do_obs) HIP_TRY(launch_obs(obs_params(h, obs), s));
+  h->last_native = do_obs ? obs : nullptr;
+  h->native_fresh = do_obs;
   return NMMO_OK;
 }
 
@@ -321,16 +332,13 @@ __global__ void end_episodes_kernel(int32_t* env, const uint8_t* m, int n) {
   if (e < n && m[e]) env[(size_t)e * NMMO_NE + E_DONE] = 1;
 }
 
-int nmmo_end_episodes(NmmoHandle* h, const uint8_t* host_env_mask) {
-  if (!h || !host_env_mask) return fail(NMMO_E_INVALID, "null argument");
+int nmmo_end_episodes(NmmoHandle* h, const uint8_t* dev_env_mask, void* stream) {
+  if (!h || !dev_env_mask) return fail(NMMO_E_INVALID, "null argument");
   const int n = h->st.n_envs;
   HIP_TRY(hipSetDevice(h->device));
-  HIP_TRY(hipDeviceSynchronize());
-  // d_seeds (n x 8 B) is reset-time scratch: n mask bytes fit in it
-  HIP_TRY(hipMemcpy(h->d_seeds, host_env_mask, (size_t)n, hipMemcpyHostToDevice));
-  end_episodes_kernel<<<(n + 255) / 256, 256>>>(h->d_env, reinterpret_cast<const uint8_t*>(h->d_seeds), n);
+  hipLaunchKernelGGL(end_episodes_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, h->d_env,
+                     dev_env_mask, n);
   HIP_TRY(hipGetLastError());
-  HIP_TRY(hipDeviceSynchronize());
   return NMMO_OK;
 }
 
@@ -339,6 +347,7 @@ int nmmo_step(NmmoHandle* h, const int32_t* actions, void* obs, float* rew, uint
   if (!h) return fail(NMMO_E_INVALID, "null handle");
   if (!actions || !rew || !term || !trunc || !mask)
     return fail(NMMO_E_INVALID, "actions/rew/term/trunc/mask must be device pointers");
+  HIP_TRY(hipSetDevice(h->device));
   hipStream_t s = (hipStream_t)stream;
   const bool rec = h->timing && h->t_count < kTimingCap;
   hipEvent_t* ev = rec ? &h->ev[(size_t)h->t_count * 4] : nullptr;
@@ -349,6 +358,8 @@ int nmmo_step(NmmoHandle* h, const int32_t* actions, void* obs, float* rew, uint
   if (rec) HIP_TRY(hipEventRecord(ev[2], s));  // wrapper span = ev[1]..ev[2] (empty when off)
   const bool do_obs = obs && h->cfg.obs_layout != NMMO_OBS_NONE;
   if (do_obs) HIP_TRY(launch_obs(obs_params(h, obs), s));
+  h->last_native = do_obs ? obs : nullptr;
+  h->native_fresh = do_obs;
   if (rec) {
     HIP_TRY(hipEventRecord(ev[3], s));  // obs span = ev[2]..ev[3] (empty when no obs)
     h->t_count++;
@@ -359,7 +370,10 @@ int nmmo_step(NmmoHandle* h, const int32_t* actions, void* obs, float* rew, uint
 int nmmo_observe(NmmoHandle* h, void* obs, void* stream) {
   if (!h || !obs) return fail(NMMO_E_INVALID, "null argument");
   if (h->cfg.obs_layout == NMMO_OBS_NONE) return fail(NMMO_E_INVALID, "handle built with NMMO_OBS_NONE");
+  HIP_TRY(hipSetDevice(h->device));
   HIP_TRY(launch_obs(obs_params(h, obs), (hipStream_t)stream));
+  h->last_native = obs;
+  h->native_fresh = true;
   return NMMO_OK;
 }
 
@@ -393,6 +407,9 @@ int nmmo_dev_alloc(int32_t device, uint64_t bytes, void** out) {
   if (!out || bytes == 0) return fail(NMMO_E_INVALID, "null out / zero bytes");
   *out = nullptr;
   HIP_TRY(hipSetDevice(device));
+  int vmm = 0;
+  HIP_TRY(hipDeviceGetAttribute(&vmm, hipDeviceAttributeVirtualMemoryManagementSupported, device));
+  if (!vmm) return fail(NMMO_E_INVALID, "device %d has no virtual memory management (hipMemCreate / hipMemMap)", device);
   hipMemAllocationProp prop = {};
   prop.type = hipMemAllocationTypePinned;
   prop.location.type = hipMemLocationTypeDevice;
@@ -468,8 +485,21 @@ int nmmo_wire_pack(NmmoHandle* h, const void* native, void* wire, void* stream) 
   if (!h || !native || !wire) return fail(NMMO_E_INVALID, "null argument");
   if (h->cfg.obs_layout != NMMO_OBS_NATIVE || !h->d_wcount)
     return fail(NMMO_E_INVALID, "nmmo_wire_pack needs a handle created with NMMO_OBS_NATIVE");
-  HIP_TRY(launch_wire_pack(h->d_wcount, h->d_mcount, (const uint8_t*)native, (uint8_t*)wire, h->st.n_envs, h->st.P,
+  if (native != h->last_native)
+    return fail(NMMO_E_INVALID, "nmmo_wire_pack: `native` is not the buffer the handle's last obs gather wrote");
+  if (!h->native_fresh)
+    return fail(NMMO_E_INVALID, "nmmo_wire_pack: a tick ran after the last obs gather without one (stale native obs)");
+  HIP_TRY(hipSetDevice(h->device));
+  HIP_TRY(launch_wire_pack(h->d_wcount, h->d_wmcount, (const uint8_t*)native, (uint8_t*)wire, h->st.n_envs, h->st.P,
                            (hipStream_t)stream));
+  return NMMO_OK;
+}
+
+int nmmo_wire_check(const void* wire, int32_t n_envs, int32_t player_n, const int64_t* dev_expect_total,
+                    int32_t* dev_status, void* stream) {
+  if (!wire || !dev_status) return fail(NMMO_E_INVALID, "null argument");
+  if (n_envs <= 0 || player_n <= 0 || player_n > 128) return fail(NMMO_E_INVALID, "n_envs > 0, player_n in 1..128");
+  HIP_TRY(launch_wire_check((const uint8_t*)wire, n_envs, player_n, dev_expect_total, dev_status, (hipStream_t)stream));
   return NMMO_OK;
 }
 
@@ -505,14 +535,17 @@ int nmmo_exp_store(NmmoHandle* h, const NmmoExperience* x, const NmmoStoreInput*
     return fail(NMMO_E_INVALID, "store inputs must be device pointers");
   if (!in->env_id && (in->env_id_base < 0 || (int64_t)in->env_id_base + in->n_rows > x->n_slots))
     return fail(NMMO_E_INVALID, "env_id_base + n_rows exceeds n_slots");
-  if (!in->obs == !in->native) return fail(NMMO_E_INVALID, "exactly one of obs / native");
-  if (in->native) {
-    if (!h) return fail(NMMO_E_INVALID, "native obs need the handle that wrote them");
-    if (h->cfg.obs_layout != NMMO_OBS_NATIVE) return fail(NMMO_E_INVALID, "handle is not NMMO_OBS_NATIVE");
+  if ((in->obs != nullptr) + (in->native != nullptr) + (in->wire != nullptr) != 1)
+    return fail(NMMO_E_INVALID, "exactly one of obs / native / wire");
+  if (in->native || in->wire) {
+    if (!h) return fail(NMMO_E_INVALID, "native / wire obs need a handle with their layout and task table");
+    if (in->native && h->cfg.obs_layout != NMMO_OBS_NATIVE) return fail(NMMO_E_INVALID, "handle is not NMMO_OBS_NATIVE");
     if (in->n_rows % h->st.P) return fail(NMMO_E_SIZE, "n_rows must be whole envs of player_n rows");
     if (x->obs_elems != h->layout.obs_elems) return fail(NMMO_E_SIZE, "obs_elems != the handle's layout");
+    HIP_TRY(hipSetDevice(h->device));
     ObsParams p = obs_params(h, nullptr);
     p.nat = (uint8_t*)in->native;
+    p.wire = (uint8_t*)in->wire;
     p.n_envs = in->n_rows / h->st.P;
     HIP_TRY(launch_store(*x, *in, &p, scratch, (hipStream_t)stream));
   } else {

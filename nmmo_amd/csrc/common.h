@@ -162,6 +162,20 @@ __device__ __forceinline__ int wave_incl_scan(int x) {
 }
 // Sum over the 64 lanes of a wave (all lanes active), wave-uniform.
 __device__ __forceinline__ int wave_sum(int x) { return __builtin_amdgcn_readlane(wave_incl_scan(x), 63); }
+
+// zero [lo, hi) of a float row with 16-byte stores on the aligned body (wave-cooperative)
+__device__ inline void wave_zero(float* row, int lo, int hi) {
+  const int lane = lane_id();
+  const uintptr_t a = reinterpret_cast<uintptr_t>(row + lo);
+  int head = (int)(((16 - (a & 15)) & 15) >> 2);
+  if (head > hi - lo) head = hi - lo;
+  if (lane < head) row[lo + lane] = 0.f;
+  const int body = (hi - lo - head) >> 2;
+  float4* p4 = reinterpret_cast<float4*>(row + lo + head);
+  for (int i = lane; i < body; i += 64) p4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  const int tail0 = lo + head + body * 4;
+  if (tail0 + lane < hi) row[tail0 + lane] = 0.f;
+}
 __device__ inline bool item_usable(const int16_t* T, int S, int p, uint2 w) {
   if (it_price(w)) return false;
   if (equip_slot(it_type(w)) >= 0 && it_equipped(w)) return true;

@@ -58,6 +58,8 @@ struct ObsParams {
   const int32_t* assign; // [n][P]
   float* obs;           // [n][P][elems] (flat layout)
   uint8_t* nat;         // native layout (SPEC §8b) instead of obs when non-NULL
+  uint8_t* wire;        // wire layout (SPEC §8c, NMMO_OBS_WIRE) instead of obs / nat when non-NULL;
+                        // expand: the wire buffer the flat rows are decoded from
   const int* row_map;   // expand only: flat row of agent row e*P+a (< 0 = skip); NULL = identity
   int n_envs, P, S, elems, task_dim;
   uint32_t systems;
@@ -70,6 +72,7 @@ struct ObsParams {
   const NmmoWrapState* ws;  // [n][P] or NULL
   int wflags;
   uint16_t* wcount;     // native only, or NULL: per agent 0x8000 | nv | ninv << 7 (0 = not in the realm), wire.hip
+  int* wmcount;         // native only, or NULL: [n] the listing count of this obs launch (nmmo_wire_pack)
 };
 constexpr int kWrapObsPrice = 1, kWrapObsNoGive = 2, kWrapObsNoDangerous = 4;
 
@@ -119,6 +122,14 @@ hipError_t launch_expand(const ObsParams& p, hipStream_t stream);  // native -> 
 hipError_t launch_wire_pack(const uint16_t* counts, const int* mcount, const uint8_t* native, uint8_t* wire, int n,
                             int P, hipStream_t s);
 hipError_t launch_wire_unpack(const uint8_t* wire, uint8_t* native, int n, int P, hipStream_t s);
+// NMMO_OBS_WIRE: per-agent count words + per-env payload sizes (wire_count_kernel) and their
+// scan, ahead of obs_kernel's record writes (obs.hip launch_obs)
+hipError_t launch_wire_header(const ObsParams& p, hipStream_t s);
+// header + record-head consistency of a wire buffer; bits into *status (0 = valid)
+hipError_t launch_wire_check(const uint8_t* wire, int n, int P, const int64_t* expect_total, int* status,
+                             hipStream_t s);
+// wire records -> flat float32 rows (p.wire, p.obs, p.row_map as in launch_expand)
+hipError_t launch_wire_expand(const ObsParams& p, hipStream_t s);
 hipError_t launch_store(const NmmoExperience& x, const NmmoStoreInput& in, const ObsParams* native,
                         int* scratch, hipStream_t stream);  // storage.hip
 int store_blocks(int n_rows);

@@ -14,22 +14,26 @@
 // Every global load of the next agent is issued ahead of the current row's bulk stores, so the
 // store stream never waits on a load (vmcnt retires in issue order).
 #include "kernels.h"
+#include "wire.h"
 
 namespace nmmo {
 
 constexpr int kObsAgentsPerBlock = 16;
 constexpr int kObsWaves = 4;
 constexpr int kObsFields = F_DS_ROW + 1;  // 0..30 obs columns, alive, ds_row
+// output layouts of obs_kernel
+constexpr int kModeFlat = 0, kModeNative = 1, kModeWire = 2;
 
 // LDS: entity fields | row->slot | per-wave visible list | per-wave inventory | per-wave 15x15
 // window materials | market listings (price | owner << 8, 2 B per listing; flat rows also the
-// listed item words, 8 B). 38.8 KB at S = 384: 4 workgroups (16 waves) per CU.
-__host__ __device__ inline size_t obs_lds_bytes(int S, bool native) {
-  return (((size_t)kObsFields * S * 2 + 15) & ~(size_t)15) + (((size_t)(S + 1) * 2 + 15) & ~(size_t)15) +
-         (size_t)kObsWaves * 128 * 2 + (size_t)kObsWaves * kInv * 8 +
-         (size_t)kObsWaves * 256 +
-         (native ? (size_t)NMMO_MARKET_ROWS * 2 + (size_t)kObsWaves * NMMO_NATIVE_MASK_BYTES
-                 : (size_t)NMMO_MARKET_ROWS * 10);
+// listed item words, 8 B) | native: per-wave ActionTargets bytes; wire: per-wave ActionTargets
+// bits + the env's record offsets. 38.8 KB (native) at S = 384: 4 workgroups (16 waves) per CU.
+__host__ __device__ inline size_t obs_lds_bytes(int S, int mode) {
+  const size_t base = (((size_t)kObsFields * S * 2 + 15) & ~(size_t)15) + (((size_t)(S + 1) * 2 + 15) & ~(size_t)15) +
+                      (size_t)kObsWaves * 128 * 2 + (size_t)kObsWaves * kInv * 8 + (size_t)kObsWaves * 256;
+  if (mode == kModeFlat) return base + (size_t)NMMO_MARKET_ROWS * 10;
+  if (mode == kModeNative) return base + (size_t)NMMO_MARKET_ROWS * 2 + (size_t)kObsWaves * NMMO_NATIVE_MASK_BYTES;
+  return base + (size_t)NMMO_MARKET_ROWS * 2 + (size_t)kObsWaves * kWireMask + 132 * 4;
 }
 
 // Plain (temporal) stores. Measured on MI355X (same-box A/B): __builtin_nontemporal_store
@@ -38,20 +42,6 @@ __host__ __device__ inline size_t obs_lds_bytes(int S, bool native) {
 // per-element section dispatch doubled the VGPRs and halved occupancy).
 __device__ __forceinline__ void obs_st(float* p, float v) { *p = v; }
 __device__ __forceinline__ void obs_st4(float4* p, float4 v) { *p = v; }
-
-// zero [lo, hi) of a row with 16-byte stores on the aligned body (wave-cooperative)
-__device__ inline void wave_zero(float* row, int lo, int hi) {
-  const int lane = lane_id();
-  const uintptr_t a = reinterpret_cast<uintptr_t>(row + lo);
-  int head = (int)(((16 - (a & 15)) & 15) >> 2);
-  if (head > hi - lo) head = hi - lo;
-  if (lane < head) obs_st(&row[lo + lane], 0.f);
-  const int body = (hi - lo - head) >> 2;
-  float4* p4 = reinterpret_cast<float4*>(row + lo + head);
-  for (int i = lane; i < body; i += 64) obs_st4(&p4[i], make_float4(0.f, 0.f, 0.f, 0.f));
-  const int tail0 = lo + head + body * 4;
-  if (tail0 + lane < hi) obs_st(&row[tail0 + lane], 0.f);
-}
 
 // zero bytes [lo, hi) of a row (lo, hi even): int16 stores up to 16-B alignment, then 16-B stores
 __device__ inline void wave_zero_bytes(uint8_t* row, int lo, int hi) {
@@ -174,6 +164,28 @@ __device__ __forceinline__ void mask_sec_f32(const ObsParams& p, const int16_t* 
     obs_st(&row[lo + k], mask_value<kWrap>(p, T, S, vis, inv, mpo, nm, m, kSec, k) ? 1.f : 0.f);
 }
 
+// The same for a wire record (SPEC §8c): section kSec as bits of the wave's LDS bit image
+// (zeroed beforehand), one ballot per 64 entries OR-ed in at the section's bit offset (a
+// 64-bit ballot shifted by 0..31 spans 3 words: lanes 0-2 take one each).
+template <int kSec, bool kWrap>
+__device__ __forceinline__ void mask_sec_bits(const ObsParams& p, const int16_t* T, int S, const int16_t* vis,
+                                              const uint2* inv, const uint16_t* mpo, int nm, const MaskCtx& m,
+                                              uint32_t* bw) {
+  int lo, n;
+  mask_section(p, kSec, lo, n);
+  const int lane = lane_id();
+  for (int k0 = 0; k0 < n; k0 += 64) {
+    const int k = k0 + lane;
+    const uint64_t b = __ballot(k < n && mask_value<kWrap>(p, T, S, vis, inv, mpo, nm, m, kSec, k));
+    if (b == 0ull) continue;
+    const int bit = lo + k0, sh = bit & 31;
+    const uint64_t lo64 = b << sh;
+    const uint32_t part = lane == 0 ? (uint32_t)lo64 : lane == 1 ? (uint32_t)(lo64 >> 32)
+                                                                 : (sh ? (uint32_t)(b >> (64 - sh)) : 0u);
+    if (lane < 3 && part) atomicOr(&bw[(bit >> 5) + lane], part);
+  }
+}
+
 // Passability of the 5 move targets from the prefetched window materials: tile t of the 15x15
 // window sits in lane t & 63 of register t >> 6; the centre's 4 neighbours (t = 97, 111, 112,
 // 113, 127) are all in register 1.
@@ -194,10 +206,13 @@ __device__ __forceinline__ uint32_t move_bits(uint32_t wm1) {
 constexpr int kTaskRegs = 32;  // Task embedding dwords per lane held in registers (2,048 per row)
 
 // kWrap: the wrapper's observation() edits are compiled in (SPEC §13).
-// kNative: the nmmo-dtype layout of SPEC §8b (u8 masks, int16 fields, Market once per env,
-// task index) instead of pufferlib's float32 row: ~10x fewer bytes per agent.
-template <bool kWrap, bool kNative>
+// kMode: kModeFlat = pufferlib's float32 row; kModeNative = the nmmo-dtype layout of SPEC §8b
+// (u8 masks, int16 fields, Market once per env, task index): ~10x fewer bytes per agent;
+// kModeWire = the wire records of SPEC §8c straight from the state (~1.3 KB per agent; the
+// header's count words and offsets come from wire_count_kernel + wire_scan_kernel).
+template <bool kWrap, int kMode>
 __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
+  constexpr bool kNative = kMode != kModeFlat;  // native and wire share the market staging
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int S = p.S;
   int16_t* T = reinterpret_cast<int16_t*>(smem);
@@ -208,9 +223,14 @@ __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
   uint16_t* mpo = reinterpret_cast<uint16_t*>(kNative ? mitem : mitem + NMMO_MARKET_ROWS);  // price | owner << 8
   uint8_t* wmat_all = reinterpret_cast<uint8_t*>(mpo + NMMO_MARKET_ROWS);  // per-wave 15x15 materials
   uint8_t* mask_all = wmat_all + kObsWaves * 256;  // native: per-wave ActionTargets bytes (16-B aligned)
+  int* woff = reinterpret_cast<int*>(mask_all + kObsWaves * kWireMask);  // wire: the env's record offsets
   const int e = blockIdx.x, g = blockIdx.y;
   const int tid = threadIdx.x;
   const int nm = p.mcount[e];
+  if constexpr (kMode == kModeWire)
+    record_offsets_wave0(wire_view(p.wire, p.n_envs, p.P).cnt + (size_t)e * p.P, p.P, woff);
+  if constexpr (kMode == kModeNative)
+    if (p.wmcount && g == 0 && tid == 0) p.wmcount[e] = nm;  // nmmo_wire_pack reads this launch's count
   for (int j = tid; j < nm; j += blockDim.x) {  // end-of-tick listings, ascending row
     const int v = p.mlist[(size_t)e * NMMO_MARKET_ROWS + j];
     const int own = (v >> 16) & 255, slot = (v >> 24) & 15;
@@ -235,11 +255,14 @@ __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
     if (T[F_ALIVE * S + s]) rowslot[T[F_DS_ROW * S + s]] = (int16_t)s;
   __syncthreads();
 
+  uint8_t* wenv = nullptr;  // wire: this env's payload
+  if constexpr (kMode == kModeWire) wenv = p.wire + wire_view(p.wire, p.n_envs, p.P).env_off[e];
   if constexpr (kNative) {  // the env's Market, once per env (the y == 0 workgroup)
     if (g == 0) {  // one listing row (16 int16 = two 16-B stores) per thread
-      uint4* mk = reinterpret_cast<uint4*>(p.nat + (size_t)e * native_env_bytes(p.P) +
-                                           (size_t)p.P * NMMO_NATIVE_ROW_BYTES);
-      for (int k = tid; k < NMMO_MARKET_ROWS; k += blockDim.x) {
+      uint4* mk = kMode == kModeWire ? reinterpret_cast<uint4*>(wenv + woff[p.P])
+                                     : reinterpret_cast<uint4*>(p.nat + (size_t)e * native_env_bytes(p.P) +
+                                                                (size_t)p.P * NMMO_NATIVE_ROW_BYTES);
+      for (int k = tid; k < (kMode == kModeWire ? min(nm, NMMO_MARKET_ROWS) : NMMO_MARKET_ROWS); k += blockDim.x) {
         uint32_t q[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
         if (k < nm) {
           const int v = p.mlist[(size_t)e * NMMO_MARKET_ROWS + k];
@@ -407,6 +430,93 @@ __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
     return;
   }
 
+  if constexpr (kMode == kModeWire) {
+    const uint16_t* cnt = wire_view(p.wire, p.n_envs, p.P).cnt + (size_t)e * p.P;
+    uint32_t* bw = reinterpret_cast<uint32_t*>(mask_all + w * kWireMask);
+    for (int j = 0; j < kPerWave; j++) {
+      const int a = abase + kObsWaves * j;
+      if (a >= p.P) break;
+      if (!T[F_ALIVE * S + a]) {  // no record
+        if (alive(j + 1)) prefetch(a + kObsWaves, j + 1);
+        continue;
+      }
+      m.a = a;
+      m.r = T[F_ROW * S + a];
+      m.c = T[F_COL * S + a];
+      m.gold = T[F_GOLD * S + a];
+      m.nv = compact(m.r, m.c);
+      if (lane < kInv) inv[lane] = iv;
+#pragma unroll
+      for (int i = 0; i < 4; i++)
+        if (lane + 64 * i < 225) wmat[lane + 64 * i] = (uint8_t)wm[i];
+      if (lane < kWireMask / 4) bw[lane] = 0u;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      m.ninv = inv_count(inv);
+      m.prev_price = kWrap ? __builtin_amdgcn_readlane(my_prev, j) : -1;
+      m.movebits = move_bits(wm[1]);
+      const int aid = T[F_ID * S + a];
+      if (alive(j + 1)) prefetch(a + kObsWaves, j + 1);  // wm is in LDS now; next agent's loads
+      mask_sec_bits<0, kWrap>(p, T, S, vis, inv, mpo, nm, m, bw);
+      mask_sec_bits<1, kWrap>(p, T, S, vis, inv, mpo, nm, m, bw);
+      mask_sec_bits<2, kWrap>(p, T, S, vis, inv, mpo, nm, m, bw);
+      mask_sec_bits<3, kWrap>(p, T, S, vis, inv, mpo, nm, m, bw);
+      mask_sec_bits<4, kWrap>(p, T, S, vis, inv, mpo, nm, m, bw);
+      mask_sec_bits<5, kWrap>(p, T, S, vis, inv, mpo, nm, m, bw);
+      mask_sec_bits<6, kWrap>(p, T, S, vis, inv, mpo, nm, m, bw);
+      mask_sec_bits<7, kWrap>(p, T, S, vis, inv, mpo, nm, m, bw);
+      mask_sec_bits<8, kWrap>(p, T, S, vis, inv, mpo, nm, m, bw);
+      mask_sec_bits<9, kWrap>(p, T, S, vis, inv, mpo, nm, m, bw);
+      mask_sec_bits<10, kWrap>(p, T, S, vis, inv, mpo, nm, m, bw);
+      mask_sec_bits<11, kWrap>(p, T, S, vis, inv, mpo, nm, m, bw);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      // the record's sizes come from its header count word (wire_count_kernel computes the same
+      // nv / ninv from the same state), so the records never overlap whatever the state holds
+      const uint32_t cw = cnt[a];
+      const int nv = cw & 127, ninv = (cw >> 7) & 15;
+      uint8_t* rec = wenv + woff[a];
+      if (lane < kWireMask / 16) {
+        reinterpret_cast<uint4*>(rec + kWireHead)[lane] = reinterpret_cast<const uint4*>(bw)[lane];
+      } else if (lane == kWireMask / 16) {
+        *reinterpret_cast<uint4*>(rec) =
+            make_uint4(i16pack(aid, tick), i16pack(__builtin_amdgcn_readlane(my_task, j), m.r - kVision),
+                       i16pack(m.c - kVision, nv), (uint32_t)ninv);
+      }
+      // body: nv Entity rows | ninv Inventory rows | 225 materials | pad, as int16 half-words
+      // (a material half-word holds two of them), 8 per lane per 16-B store
+      const int eb = 62 * nv, ib = eb + 32 * ninv;
+      const int nq = (wire_record_bytes(cw) - kWireBody) >> 4;
+      uint4* body = reinterpret_cast<uint4*>(rec + kWireBody);
+      auto half = [&](int h) -> uint32_t {
+        const int o = 2 * h;
+        int x;
+        if (o < eb) {
+          const int k = h / NMMO_N_ENTITY_COLS, f = h - k * NMMO_N_ENTITY_COLS;
+          x = T[f * S + vis[k]];
+        } else if (o < ib) {
+          const int i = (o - eb) >> 1;
+          x = (int)item_col(inv[i >> 4], aid, i & 15);
+        } else {
+          const int t = o - ib;
+          x = (t < kWireTiles ? (int)wmat[t] : 0) | (t + 1 < kWireTiles ? (int)wmat[t + 1] << 8 : 0);
+        }
+        return (uint32_t)(uint16_t)x;
+      };
+      for (int q = lane; q < nq; q += 64) {
+        const int h = 8 * q;
+        body[q] = make_uint4(half(h) | half(h + 1) << 16, half(h + 2) | half(h + 3) << 16,
+                             half(h + 4) | half(h + 5) << 16, half(h + 6) | half(h + 7) << 16);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the next agent reuses vis / inv / wmat / bw
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    return;
+  }
+
   for (int j = 0; j < kPerWave; j++) {
     const int a = abase + kObsWaves * j;
     if (a >= p.P) break;
@@ -526,13 +636,19 @@ __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
 hipError_t launch_obs(const ObsParams& p, hipStream_t stream) {
   dim3 grid(p.n_envs, (p.P + kObsAgentsPerBlock - 1) / kObsAgentsPerBlock);
   const dim3 block(64 * kObsWaves);
-  const size_t lds = obs_lds_bytes(p.S, p.nat != nullptr);
-  if (p.nat) {
-    if (p.wflags) hipLaunchKernelGGL((obs_kernel<true, true>), grid, block, lds, stream, p);
-    else hipLaunchKernelGGL((obs_kernel<false, true>), grid, block, lds, stream, p);
+  const int mode = p.wire ? kModeWire : p.nat ? kModeNative : kModeFlat;
+  const size_t lds = obs_lds_bytes(p.S, mode);
+  if (mode == kModeWire) {
+    const hipError_t err = launch_wire_header(p, stream);  // count words, sizes, offsets
+    if (err != hipSuccess) return err;
+    if (p.wflags) hipLaunchKernelGGL((obs_kernel<true, kModeWire>), grid, block, lds, stream, p);
+    else hipLaunchKernelGGL((obs_kernel<false, kModeWire>), grid, block, lds, stream, p);
+  } else if (mode == kModeNative) {
+    if (p.wflags) hipLaunchKernelGGL((obs_kernel<true, kModeNative>), grid, block, lds, stream, p);
+    else hipLaunchKernelGGL((obs_kernel<false, kModeNative>), grid, block, lds, stream, p);
   } else {
-    if (p.wflags) hipLaunchKernelGGL((obs_kernel<true, false>), grid, block, lds, stream, p);
-    else hipLaunchKernelGGL((obs_kernel<false, false>), grid, block, lds, stream, p);
+    if (p.wflags) hipLaunchKernelGGL((obs_kernel<true, kModeFlat>), grid, block, lds, stream, p);
+    else hipLaunchKernelGGL((obs_kernel<false, kModeFlat>), grid, block, lds, stream, p);
   }
   return hipGetLastError();
 }

@@ -9,7 +9,8 @@
 //   gather_rows_kernel        <- b_obs = obs_ary[b_idxs] and the per-minibatch copies  :439-458
 //
 // Byte work, HBM-bound: a stored row moves 95,948 B of obs (flat) or is expanded straight from
-// the native layout (SPEC §8b: 9,552 B read per row) into its experience slot; every other
+// the native layout (SPEC §8b: 9,552 B read per row) or decoded from its wire record (SPEC §8c,
+// ~1.3 KB read per row; wire.hip wire_expand_kernel) into its experience slot; every other
 // field is a few bytes per row.
 #include "kernels.h"
 
@@ -201,7 +202,7 @@ hipError_t launch_store(const NmmoExperience& x, const NmmoStoreInput& in, const
     ObsParams p = *native;
     p.obs = x.obs;
     p.row_map = dst;
-    hipError_t e = launch_expand(p, stream);
+    hipError_t e = p.wire ? launch_wire_expand(p, stream) : launch_expand(p, stream);
     if (e != hipSuccess) return e;
   } else {
     hipLaunchKernelGGL(store_rows_kernel, dim3((in.n_rows + 3) / 4), dim3(256), 0, stream, in.obs, in.n_rows,

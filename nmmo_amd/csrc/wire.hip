@@ -1,59 +1,27 @@
 // wire.hip — compact transport encoding of native observations (SPEC.md §8c) for the learner
-// gather of BASELINE config 5 (every rank's observations into one GPU over xGMI).
+// gather of BASELINE config 5 (every rank's observations into one GPU over xGMI). Format:
+// wire.h.
 //
 // The native layout (SPEC §8b: 9,552 B per agent + 32 KB per env) is what the learner reads, but
 // most of its bytes are padding a transfer can drop: Entity rows past the visible ones, empty
 // inventory slots, Market rows past the listings, one byte per ActionTargets bit, and the Tile
-// rows/columns that follow from the window's corner. A wire buffer keeps only what varies:
+// rows/columns that follow from the window's corner. ~1.3 KB per agent in C4 steady state
+// instead of 9,552 B.
 //
-//   header  int64 total bytes | int64 env payload offset [n_envs] | u16 agent count word
-//           [n_envs][P] (bit 15 in the realm, bits 0-6 visible entities nv, 7-10 items ninv) |
-//           u16 market listings [n_envs]; 16-B aligned
-//   payload per env: one record per agent in the realm (slot order), then its listings
-//   record  16-B head (int16 AgentId, CurrentTick, task index, tile row 0, tile col 0, nv, ninv,
-//           0) | 1,586 ActionTargets bits in 208 B | nv Entity rows (31 x int16) | ninv Inventory
-//           rows (16 x int16) | 225 window materials (u8) | zero pad to 16 B
-//   listing 16 x int16 (the native Market row)
-//
-// ~1.3 KB per agent in C4 steady state instead of 9,552 B. HBM-bound: pack reads the ~2.5 KB of
-// the native row the record needs and writes the record; unpack reads the record and writes the
-// whole 9,552-B native row. The counts come from the native obs kernel (no scan of the rows).
+// Kernels:
+//   wire_size / wire_scan / wire_pack   native -> wire (nmmo_wire_pack; counts from the native
+//                                       obs launch, no scan of the rows)
+//   wire_count (+ wire_scan)            the header of a wire buffer written straight from the
+//                                       env state (NMMO_OBS_WIRE; obs_kernel writes the records)
+//   wire_unpack                         wire -> native (every byte of the native buffer)
+//   wire_check                          header and record-head consistency of a received buffer
+//   wire_expand                         wire records -> flat float32 rows (the experience store
+//                                       decoding only the rows it keeps, clean_pufferl.py:333-346)
+// All HBM-bound byte work.
 #include "kernels.h"
+#include "wire.h"
 
 namespace nmmo {
-
-constexpr int kWireHead = 16, kWireMask = 208, kWireTiles = 225;
-constexpr int kNatI16Entity = 2, kNatI16Inv = kNatI16Entity + kNObs * NMMO_N_ENTITY_COLS,
-              kNatI16Tile = kNatI16Inv + kInv * 16, kNatI16Task = kNatI16Tile + 225 * 3;
-
-__host__ __device__ inline int64_t wire_header_bytes(int n, int P) {
-  return ((8 + 8 * (int64_t)n + 2 * (int64_t)n * P + 2 * (int64_t)n) + 15) & ~(int64_t)15;
-}
-__host__ __device__ inline int wire_record_bytes(uint32_t cnt) {
-  if (!(cnt & 0x8000u)) return 0;
-  const int nv = cnt & 127, ninv = (cnt >> 7) & 15;
-  return (kWireHead + kWireMask + 62 * nv + 32 * ninv + kWireTiles + 15) & ~15;
-}
-__host__ __device__ inline size_t wire_native_env_bytes(int P) {
-  return (size_t)P * NMMO_NATIVE_ROW_BYTES + NMMO_NATIVE_MARKET_BYTES;
-}
-
-struct WireView {  // the header fields of a wire buffer of n envs x P agents
-  int64_t* total;
-  int64_t* env_off;  // [n] payload offsets (relative to the buffer start)
-  uint16_t* cnt;     // [n][P]
-  uint16_t* mcount;  // [n]
-  uint8_t* base;
-};
-__device__ inline WireView wire_view(uint8_t* w, int n, int P) {
-  WireView v;
-  v.base = w;
-  v.total = reinterpret_cast<int64_t*>(w);
-  v.env_off = v.total + 1;
-  v.cnt = reinterpret_cast<uint16_t*>(v.env_off + n);
-  v.mcount = v.cnt + (size_t)n * P;
-  return v;
-}
 
 // per env: its count words and listings into the header, its payload bytes into env_off[e]
 __global__ void __launch_bounds__(128) wire_size_kernel(const uint16_t* counts, const int* mcount, uint8_t* wire,
@@ -74,6 +42,55 @@ __global__ void __launch_bounds__(128) wire_size_kernel(const uint16_t* counts, 
     const int nm = min(max(mcount[e], 0), NMMO_MARKET_ROWS);
     v.mcount[e] = (uint16_t)nm;
     v.env_off[e] = part[0] + (blockDim.x > 64 ? part[1] : 0) + 32 * nm;
+  }
+}
+
+// NMMO_OBS_WIRE header from the env state: per agent in the realm nv = entities within the
+// L-inf <= 7 window (itself included; capped at 100, as obs_kernel's compaction), ninv = its
+// occupied inventory prefix; per env the payload bytes into env_off[e] (then wire_scan_kernel).
+__global__ void __launch_bounds__(256) wire_count_kernel(ObsParams p) {
+  __shared__ uint32_t pos[kMaxSlots];  // r << 16 | c of entities in the realm, else kOut
+  __shared__ int bytes;
+  constexpr uint32_t kOut = 0x80008000u;
+  WireView v = wire_view(p.wire, p.n_envs, p.P);
+  const int e = blockIdx.x, tid = threadIdx.x, lane = lane_id(), w = wave_id(), S = p.S;
+  const int16_t* E = p.ent + (size_t)e * NMMO_NF * S;
+  for (int s = tid; s < S; s += blockDim.x)
+    pos[s] = E[F_ALIVE * S + s] ? ((uint32_t)(uint16_t)E[F_ROW * S + s] << 16) | (uint32_t)(uint16_t)E[F_COL * S + s]
+                                : kOut;
+  if (tid == 0) bytes = 0;
+  __syncthreads();
+  int mine = 0;
+  for (int a = w; a < p.P; a += blockDim.x >> 6) {
+    const uint32_t pa = pos[a];
+    uint32_t word = 0u;
+    if (pa != kOut) {  // wave-uniform
+      const int r = (int)(pa >> 16), c = (int)(pa & 0xFFFFu);
+      int nv = 0;
+      for (int s0 = 0; s0 < S; s0 += 64) {
+        const int s = s0 + lane;
+        bool in = false;
+        if (s < S) {
+          const uint32_t q = pos[s];
+          in = q != kOut && linf(r, c, (int)(q >> 16), (int)(q & 0xFFFFu)) <= kVision;
+        }
+        nv += __popcll(__ballot(in));
+      }
+      const uint2 it = lane < kInv ? p.items[((size_t)e * p.P + a) * kInv + lane] : make_uint2(0u, 0u);
+      const int ninv = __builtin_ctzll(~__ballot(lane < kInv && it_type(it) != 0));  // occupied prefix
+      word = wire_count_word(min(nv, kNObs), ninv);
+    }
+    if (lane == 0) {
+      v.cnt[(size_t)e * p.P + a] = (uint16_t)word;
+      mine += wire_record_bytes(word);
+    }
+  }
+  if (lane == 0) atomicAdd(&bytes, mine);
+  __syncthreads();
+  if (tid == 0) {
+    const int nm = min(max(p.mcount[e], 0), NMMO_MARKET_ROWS);
+    v.mcount[e] = (uint16_t)nm;
+    v.env_off[e] = bytes + 32 * nm;
   }
 }
 
@@ -104,29 +121,8 @@ __global__ void __launch_bounds__(1024) wire_scan_kernel(uint8_t* wire, int n, i
     __syncthreads();
   }
   if (tid == 0) *v.total = carry;
-  const int64_t used = 8 + 8 * (int64_t)n + 2 * (int64_t)n * P + 2 * (int64_t)n;  // header pad is zero
+  const int64_t used = wire_header_used(n, P);  // header pad is zero
   if (used + tid < wire_header_bytes(n, P)) wire[used + tid] = 0;
-}
-
-// offsets of the records of env e's agents (relative to the env payload) into off[P]
-__device__ inline void record_offsets(const uint16_t* cnt, int P, int* off) {
-  const int tid = threadIdx.x;
-  if (tid < 64) {
-    int carry = 0;
-    for (int b = 0; b < P; b += 64) {
-      const int a = b + tid;
-      const int x = a < P ? wire_record_bytes(cnt[a]) : 0;
-      int inc = x;
-      for (int o = 1; o < 64; o <<= 1) {
-        const int y = __shfl_up(inc, o);
-        if (tid >= o) inc += y;
-      }
-      if (a < P) off[a] = carry + inc - x;
-      carry += __shfl(inc, 63);
-    }
-    if (tid == 0) off[P] = carry;  // listings start
-  }
-  __syncthreads();
 }
 
 constexpr int kWireAgentsPerBlock = 16;
@@ -136,7 +132,8 @@ __global__ void __launch_bounds__(256) wire_pack_kernel(const uint8_t* native, u
   __shared__ int off[129];
   const int e = blockIdx.x, g = blockIdx.y, lane = lane_id(), w = wave_id();
   const uint16_t* cnt = v.cnt + (size_t)e * P;
-  record_offsets(cnt, P, off);
+  record_offsets_wave0(cnt, P, off);
+  __syncthreads();
   const uint8_t* nenv = native + (size_t)e * wire_native_env_bytes(P);
   uint8_t* penv = v.base + v.env_off[e];
   if (g == 0) {  // listings: 32 B each, 16-B copies
@@ -172,29 +169,50 @@ __global__ void __launch_bounds__(256) wire_pack_kernel(const uint8_t* native, u
       }
       reinterpret_cast<uint32_t*>(rec + kWireHead)[lane] = bits;
     }
-    int16_t* d16 = reinterpret_cast<int16_t*>(rec + kWireHead + kWireMask);
+    int16_t* d16 = reinterpret_cast<int16_t*>(rec + kWireBody);
     for (int k = lane; k < nv * NMMO_N_ENTITY_COLS; k += 64) d16[k] = i16[kNatI16Entity + k];
     d16 += nv * NMMO_N_ENTITY_COLS;
     for (int k = lane; k < ninv * 16; k += 64) d16[k] = i16[kNatI16Inv + k];
     uint8_t* mat = reinterpret_cast<uint8_t*>(d16 + ninv * 16);
-    const int pad = wire_record_bytes(c) - (kWireHead + kWireMask + 62 * nv + 32 * ninv);
+    const int pad = wire_record_bytes(c) - (kWireBody + 62 * nv + 32 * ninv);
     for (int t = lane; t < pad; t += 64) mat[t] = t < kWireTiles ? (uint8_t)i16[kNatI16Tile + 3 * t + 2] : 0;
   }
 }
 
-// wire -> native: every byte of the native buffer is written. Each wave first copies its
-// agent's record into LDS (every load issued before the first store: vmcnt retires in issue
-// order, so loads between stores would wait for them), then writes the 9,552-B row with 16-B
-// stores computed from LDS.
-constexpr int kRecMaxU4 = (kWireHead + kWireMask + 62 * kNObs + 32 * kInv + kWireTiles + 15) / 16;  // 440
+// One wave's copy of a record into its LDS buffer: every load issued before the first store
+// (vmcnt retires in issue order, so loads between stores would wait for them), then the
+// release / wave barrier / acquire sequence that hands the bytes to the other lanes.
+__device__ __forceinline__ void record_to_lds(const uint8_t* src, int nq, uint4* lrec) {
+  const int lane = lane_id();
+  const uint4* src4 = reinterpret_cast<const uint4*>(src);
+  constexpr int kPer = (kRecMaxU4 + 63) / 64;
+  uint4 r[kPer];
+#pragma unroll
+  for (int k = 0; k < kPer; k++) r[k] = lane + 64 * k < nq ? src4[lane + 64 * k] : make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+  for (int k = 0; k < kPer; k++)
+    if (lane + 64 * k < nq) lrec[lane + 64 * k] = r[k];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+// ... and before the next record overwrites the buffer (every lane's reads of this one done)
+__device__ __forceinline__ void record_release() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
+// wire -> native: every byte of the native buffer is written. Each wave first copies its
+// agent's record into LDS, then writes the 9,552-B row with 16-B stores computed from LDS.
 __global__ void __launch_bounds__(256) wire_unpack_kernel(const uint8_t* wire, uint8_t* native, int n, int P) {
   WireView v = wire_view(const_cast<uint8_t*>(wire), n, P);
   __shared__ int off[129];
   __shared__ uint4 recbuf[4][kRecMaxU4];
   const int e = blockIdx.x, g = blockIdx.y, lane = lane_id(), w = wave_id();
   const uint16_t* cnt = v.cnt + (size_t)e * P;
-  record_offsets(cnt, P, off);
+  record_offsets_wave0(cnt, P, off);
+  __syncthreads();
   uint8_t* nenv = native + (size_t)e * wire_native_env_bytes(P);
   const uint8_t* penv = v.base + v.env_off[e];
   if (g == 0) {
@@ -215,22 +233,11 @@ __global__ void __launch_bounds__(256) wire_unpack_kernel(const uint8_t* wire, u
       for (int k = lane; k < NMMO_NATIVE_ROW_BYTES / 16; k += 64) row4[k] = make_uint4(0u, 0u, 0u, 0u);
       continue;
     }
-    const int nv = c & 127, ninv = (c >> 7) & 15, nq = wire_record_bytes(c) / 16;
-    {
-      const uint4* src4 = reinterpret_cast<const uint4*>(penv + off[a]);
-      constexpr int kPer = (kRecMaxU4 + 63) / 64;
-      uint4 r[kPer];
-#pragma unroll
-      for (int k = 0; k < kPer; k++) r[k] = lane + 64 * k < nq ? src4[lane + 64 * k] : make_uint4(0u, 0u, 0u, 0u);
-#pragma unroll
-      for (int k = 0; k < kPer; k++)
-        if (lane + 64 * k < nq) lrec[lane + 64 * k] = r[k];
-    }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    const int nv = c & 127, ninv = (c >> 7) & 15;
+    record_to_lds(penv + off[a], wire_record_bytes(c) / 16, lrec);
     const int16_t* h16 = reinterpret_cast<const int16_t*>(lb);
-    const int16_t* s16 = reinterpret_cast<const int16_t*>(lb + kWireHead + kWireMask);
-    const uint8_t* mat = lb + kWireHead + kWireMask + 62 * nv + 32 * ninv;
+    const int16_t* s16 = reinterpret_cast<const int16_t*>(lb + kWireBody);
+    const uint8_t* mat = lb + kWireBody + 62 * nv + 32 * ninv;
     const int r0 = h16[3], c0 = h16[4], task = h16[2];
     // mask bytes, 16 per lane (1,600 bytes = 100 stores)
     for (int k = lane; k < NMMO_NATIVE_MASK_BYTES / 16; k += 64) {
@@ -267,7 +274,109 @@ __global__ void __launch_bounds__(256) wire_unpack_kernel(const uint8_t* wire, u
       d4[q] = make_uint4(val(k) | val(k + 1) << 16, val(k + 2) | val(k + 3) << 16, val(k + 4) | val(k + 5) << 16,
                          val(k + 6) | val(k + 7) << 16);
     }
-    __builtin_amdgcn_wave_barrier();  // the next agent's record overwrites this one
+    record_release();
+  }
+}
+
+// Consistency of one received wire buffer of n envs x P agents (block per env): the announced
+// total (when expect_total is given), the env payload offsets against the count words and
+// listings, the counts' ranges, and every record head's AgentId / nv / ninv against its count
+// word. status bits: 1 total, 2 env offsets, 4 count ranges, 8 record heads.
+__global__ void __launch_bounds__(128) wire_check_kernel(const uint8_t* wire, int n, int P,
+                                                         const int64_t* expect_total, int* status) {
+  WireView v = wire_view(const_cast<uint8_t*>(wire), n, P);
+  __shared__ int off[129];
+  const int e = blockIdx.x, a = threadIdx.x;
+  const uint16_t* cnt = v.cnt + (size_t)e * P;
+  record_offsets_wave0(cnt, P, off);
+  __syncthreads();
+  int bad = 0;
+  const int64_t total = *v.total;
+  const int64_t base = v.env_off[e];
+  const int nm = v.mcount[e];
+  if (a == 0) {
+    if (e == 0 && expect_total && total != *expect_total) bad |= 1;
+    if (e == 0 && base != wire_header_bytes(n, P)) bad |= 2;
+    const int64_t end = e + 1 < n ? v.env_off[e + 1] : total;
+    if (end - base != (int64_t)off[P] + 32 * nm) bad |= 2;
+    if (nm > NMMO_MARKET_ROWS) bad |= 4;
+  }
+  if (a < P) {
+    const uint32_t c = cnt[a];
+    if (c & 0x8000u) {
+      const int nv = c & 127, ninv = (c >> 7) & 15;
+      if (nv > kNObs || ninv > kInv || (c & 0x7800u)) {
+        bad |= 4;
+      } else if (base + off[a] + kWireHead <= total) {
+        const int16_t* h = reinterpret_cast<const int16_t*>(v.base + base + off[a]);
+        if (h[0] <= 0 || h[5] != nv || h[6] != ninv) bad |= 8;
+      } else {
+        bad |= 2;
+      }
+    } else if (c) {
+      bad |= 4;
+    }
+  }
+  if (bad) atomicOr(status, bad);
+}
+
+// Wire records -> flat float32 rows (the pufferlib row of SPEC §8; bit-identical to
+// expand_kernel over the unpacked native layout): grid (env, 16-agent group), the env's Market
+// rows staged in LDS, one wave per agent row. row_map as in expand_kernel: flat row of agent
+// e*P + a, < 0 = not kept (the experience store decodes only the rows it keeps).
+__global__ void __launch_bounds__(256) wire_expand_kernel(ObsParams p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  int16_t* mk = reinterpret_cast<int16_t*>(smem);                         // [1024][16]
+  int* off = reinterpret_cast<int*>(smem + NMMO_MARKET_ROWS * 32);        // [P + 1]
+  uint4* recbuf = reinterpret_cast<uint4*>(smem + NMMO_MARKET_ROWS * 32 + 144 * 4);  // [4][kRecMaxU4]
+  const int P = p.P, e = blockIdx.x, g = blockIdx.y, tid = threadIdx.x, lane = lane_id(), w = wave_id();
+  WireView v = wire_view(p.wire, p.n_envs, P);
+  const uint16_t* cnt = v.cnt + (size_t)e * P;
+  record_offsets_wave0(cnt, P, off);
+  __syncthreads();
+  const uint8_t* penv = v.base + v.env_off[e];
+  {
+    const int nm = v.mcount[e];
+    const uint4* src = reinterpret_cast<const uint4*>(penv + off[P]);
+    uint4* dst = reinterpret_cast<uint4*>(mk);
+    for (int k = tid; k < NMMO_MARKET_ROWS * 2; k += blockDim.x) dst[k] = k < 2 * nm ? src[k] : make_uint4(0u, 0u, 0u, 0u);
+  }
+  __syncthreads();
+  uint4* lrec = recbuf + w * kRecMaxU4;
+  const uint8_t* lb = reinterpret_cast<const uint8_t*>(lrec);
+  for (int i = w; i < kWireAgentsPerBlock; i += 4) {
+    const int a = g * kWireAgentsPerBlock + i;
+    if (a >= P) break;
+    const int frow = p.row_map ? p.row_map[(size_t)e * P + a] : e * P + a;
+    if (frow < 0) continue;  // wave-uniform
+    float* row = p.obs + (size_t)frow * p.elems;
+    const uint32_t c = cnt[a];
+    if (!(c & 0x8000u)) {  // not in the realm: all-zero row
+      wave_zero(row, 0, p.elems);
+      continue;
+    }
+    const int nv = c & 127, ninv = (c >> 7) & 15;
+    record_to_lds(penv + off[a], wire_record_bytes(c) / 16, lrec);
+    const int16_t* h16 = reinterpret_cast<const int16_t*>(lb);
+    const uint32_t* bits = reinterpret_cast<const uint32_t*>(lb + kWireHead);
+    const int16_t* s16 = reinterpret_cast<const int16_t*>(lb + kWireBody);
+    const uint8_t* mat = lb + kWireBody + 62 * nv + 32 * ninv;
+    for (int j = lane; j < p.o_agent_id; j += 64) row[j] = (float)((bits[j >> 5] >> (j & 31)) & 1u);
+    if (lane == 0) row[p.o_agent_id] = (float)h16[0];
+    if (lane == 1) row[p.o_tick] = (float)h16[1];
+    for (int j = lane; j < kNObs * NMMO_N_ENTITY_COLS; j += 64)
+      row[p.o_entity + j] = j < nv * NMMO_N_ENTITY_COLS ? (float)s16[j] : 0.f;
+    for (int j = lane; j < kInv * 16; j += 64)
+      row[p.o_inventory + j] = j < ninv * 16 ? (float)s16[nv * NMMO_N_ENTITY_COLS + j] : 0.f;
+    for (int j = lane; j < NMMO_MARKET_ROWS * 16; j += 64) row[p.o_market + j] = (float)mk[j];
+    const float* temb = p.task + (size_t)h16[2] * p.task_dim;
+    for (int j = lane; j < p.task_dim; j += 64) row[p.o_task + j] = temb[j];
+    const int r0 = h16[3], c0 = h16[4];
+    for (int j = lane; j < 225 * 3; j += 64) {
+      const int t = j / 3, comp = j - 3 * t;
+      row[p.o_tile + j] = comp == 0 ? (float)(r0 + t / 15) : comp == 1 ? (float)(c0 + t % 15) : (float)mat[t];
+    }
+    record_release();
   }
 }
 
@@ -281,10 +390,33 @@ hipError_t launch_wire_pack(const uint16_t* counts, const int* mcount, const uin
   return hipGetLastError();
 }
 
+hipError_t launch_wire_header(const ObsParams& p, hipStream_t s) {
+  if (p.P > 128 || p.n_envs <= 0 || p.S > kMaxSlots || !p.wire) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(wire_count_kernel, dim3(p.n_envs), dim3(256), 0, s, p);
+  hipLaunchKernelGGL(wire_scan_kernel, dim3(1), dim3(1024), 0, s, p.wire, p.n_envs, p.P);
+  return hipGetLastError();
+}
+
 hipError_t launch_wire_unpack(const uint8_t* wire, uint8_t* native, int n, int P, hipStream_t s) {
   if (P > 128 || n <= 0) return hipErrorInvalidValue;
   hipLaunchKernelGGL(wire_unpack_kernel, dim3(n, (P + kWireAgentsPerBlock - 1) / kWireAgentsPerBlock), dim3(256), 0,
                      s, wire, native, n, P);
+  return hipGetLastError();
+}
+
+hipError_t launch_wire_check(const uint8_t* wire, int n, int P, const int64_t* expect_total, int* status,
+                             hipStream_t s) {
+  if (P > 128 || n <= 0 || !status) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(wire_check_kernel, dim3(n), dim3(128), 0, s, wire, n, P, expect_total, status);
+  return hipGetLastError();
+}
+
+constexpr size_t kWireExpandLds = (size_t)NMMO_MARKET_ROWS * 32 + 144 * 4 + (size_t)4 * kRecMaxU4 * 16;  // 61.4 KB
+
+hipError_t launch_wire_expand(const ObsParams& p, hipStream_t s) {
+  if (p.P > 128 || p.n_envs <= 0 || !p.wire || !p.obs) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(wire_expand_kernel, dim3(p.n_envs, (p.P + kWireAgentsPerBlock - 1) / kWireAgentsPerBlock),
+                     dim3(256), kWireExpandLds, s, p);
   return hipGetLastError();
 }
 

@@ -2,13 +2,19 @@
 
 SURVEY.md §8e: envs are independent, so each rank steps a contiguous block of envs with no
 collective on the data path; the only exchange is returning batched outputs to a single learner
-(rank 0) when the trainer is centralised. Global env indices (env_index_base = rank * n_local)
-key every random stream, so a sharded run is env-for-env identical to a single-GPU run of the
-same total envs (tests/test_distributed.py checks this on gloo).
+(rank 0) when the trainer is centralised (BASELINE config 5). Global env indices
+(env_index_base = rank * n_local) key every random stream, so a sharded run is env-for-env
+identical to a single-GPU run of the same total envs (tests/test_distributed.py checks this on
+gloo, tests/test_gpu_multirank.py on the GPU).
 
 The reference has no collective at all (single-GPU learner fed by pufferlib worker processes,
 clean_pufferl.py:106-114); this module replaces the worker-process IPC of pool.recv()/send()
 (:293, :357) with torch.distributed (RCCL over xGMI on MI355X, gloo on CPU).
+
+The learner gather moves observations as wire buffers (SPEC §8c, nmmo_amd.wire): every rank's
+handles write them straight from the state (obs_layout OBS_WIRE), ~0.8 KB per agent in the realm
+instead of 9,552 B native / 95,948 B flat. `WireExchange` is the transfer protocol and
+`WireGather` the C5 step built on it.
 """
 
 from __future__ import annotations
@@ -53,38 +59,292 @@ def scatter_from_learner(full, like: torch.Tensor, src: int = 0) -> torch.Tensor
     return out
 
 
-def gather_wire_to_learner(wire: torch.Tensor, header_bytes: int, dst: int = 0, recv_bufs=None):
-    """The learner gather of wire-encoded observations (SPEC §8c, nmmo_amd.wire): every rank's
-    packed buffer reaches rank `dst`, each peer -> root transfer carrying exactly the bytes its
-    header announces (a fixed-size header first, then the payload). Returns, on `dst`, the
-    buffers in rank order (dst's own `wire` in place, no self-copy); None elsewhere.
-    `recv_bufs[r]` (dst only) holds rank r's buffer (nmmo_wire_max_bytes of its shard); they are
-    allocated when missing. The sender reads its total size on the host (one 8-byte copy)."""
-    world, rank = dist.get_world_size(), dist.get_rank()
-    if world == 1:
-        return [wire]
+class WireExchange:
+    """Transfer protocol of the learner gather: every rank's `n_bufs` wire buffers (one per env
+    batch, SPEC §8c) and their fixed-size companions (`smalls`: reward / dones / mask) reach rank
+    `dst` each step, over point-to-point sends (RCCL over xGMI: each peer uses its own link to
+    the root; no ring, no collective on the payload).
 
-    def total_of(buf):
-        return int(buf[:8].view(torch.int64).item())
+    A wire buffer's size is known only on the device once its step has run, and a receive must
+    be posted with its exact size, so the protocol runs a step behind the compute:
+      sizes(t)   every sender's totals (8 B per buffer, read on the device from the headers)
+                 reach the root on the comm stream, and are copied into pinned host memory;
+      payload(t) posted after sizes(t) has landed (the host waits for that copy's event only, so
+                 the caller posts payload(t - 1) after queueing step t: step t computes while
+                 t - 1's buffers move); each receive is exactly the announced size.
+    No `.item()`, no stream or device synchronisation on the data path. Buffers handed to
+    sizes(t) / payload(t) must stay untouched until `done(t)` (an event on the comm stream).
+    Ring slot k = t % ring indexes the per-step state.
 
-    if rank != dst:
-        total = total_of(wire)
-        reqs = [dist.isend(wire[:header_bytes], dst)]
-        if total > header_bytes:
-            reqs.append(dist.isend(wire[header_bytes:total], dst))
-        for q in reqs:
-            q.wait()
-        return None
-    bufs = list(recv_bufs) if recv_bufs is not None else [None] * world
-    peers = [r for r in range(world) if r != dst]
-    for r in peers:
-        if bufs[r] is None:
-            bufs[r] = torch.empty_like(wire)
-    for q in [dist.irecv(bufs[r][:header_bytes], src=r) for r in peers]:
-        q.wait()
-    totals = {r: total_of(bufs[r]) for r in peers}
-    reqs = [dist.irecv(bufs[r][header_bytes:totals[r]], src=r) for r in peers if totals[r] > header_bytes]
-    for q in reqs:
-        q.wait()
-    bufs[dst] = wire
-    return [bufs[r][:totals[r]] if r != dst else wire for r in range(world)]
+    On CPU tensors (gloo, tests) every call is synchronous. With gloo and CUDA tensors (the
+    one-GPU rehearsal of a multi-rank run) transfers are staged through the host."""
+
+    def __init__(self, world: int, rank: int, n_bufs: int, recv_caps, small_bytes, device, dst: int = 0,
+                 ring: int = 3, backend: str | None = None):
+        self.world, self.rank, self.dst, self.ring = world, rank, dst, ring
+        self.n_bufs = n_bufs
+        self.device = torch.device(device)
+        self.cuda = self.device.type == "cuda"
+        self.staged = (backend or (dist.get_backend() if world > 1 else "nccl")) == "gloo" and self.cuda
+        d = self.device
+        self.sizes = torch.zeros((ring, world, n_bufs), dtype=torch.int64, device=d)
+        self.sizes_host = torch.zeros((ring, world, n_bufs), dtype=torch.int64, pin_memory=self.cuda)
+        self.comm = torch.cuda.Stream(device=d) if self.cuda else None
+        self._sized = [None] * ring
+        self._done = [None] * ring
+        self.peers = [r for r in range(world) if r != dst]
+        self.recv_wire, self.recv_small = {}, {}
+        if rank == dst:
+            for r in self.peers:
+                for j in range(n_bufs):
+                    self.recv_wire[r, j] = torch.empty(int(recv_caps[j]), dtype=torch.uint8, device=d)
+                    self.recv_small[r, j] = torch.empty(int(small_bytes[j]), dtype=torch.uint8, device=d)
+        self.payload_bytes = 0  # wire bytes received by the root (all peers, all steps)
+
+    # -- plumbing
+    def _ctx(self):
+        return torch.cuda.stream(self.comm) if self.cuda else _null()
+
+    def _p2p(self, sends, recvs):
+        """sends / recvs: [(tensor, peer)]; completes (stream-ordered on the comm stream with
+        RCCL, synchronously with gloo)."""
+        if not sends and not recvs:
+            return
+        if self.staged:  # gloo cannot read device memory: host copies, synchronously
+            self.comm.synchronize()
+            cs = [(t.cpu(), p) for t, p in sends]
+            cr = [(torch.empty(t.shape, dtype=t.dtype), p) for t, p in recvs]
+            reqs = [dist.isend(t, p) for t, p in cs] + [dist.irecv(t, p) for t, p in cr]
+            for q in reqs:
+                q.wait()
+            with torch.cuda.stream(self.comm):
+                for (t, _), (c, _) in zip(recvs, cr):
+                    t.copy_(c)
+            return
+        ops = [dist.P2POp(dist.isend, t, p) for t, p in sends] + [dist.P2POp(dist.irecv, t, p) for t, p in recvs]
+        with self._ctx():
+            for q in dist.batch_isend_irecv(ops):
+                q.wait()
+
+    # -- protocol
+    def post_sizes(self, t: int, wires, ready=()):
+        """Step t's totals: the sender's (or the root's own) buffers' first int64 into
+        sizes[k][rank]; the peers' totals into the root's sizes[k]. `ready`: events the comm
+        stream waits for (the compute that wrote `wires`)."""
+        k = t % self.ring
+        # (sizes[k] / sizes_host[k] of step t - ring were read by then: the device reads are
+        # earlier on the comm stream, the host read came before this call)
+        with self._ctx():
+            if self.cuda:
+                for ev in ready:
+                    self.comm.wait_event(ev)
+            for j, w in enumerate(wires):
+                self.sizes[k, self.rank, j].copy_(w[:8].view(torch.int64)[0])
+        if self.world > 1:
+            if self.rank == self.dst:
+                self._p2p([], [(self.sizes[k, r], r) for r in self.peers])
+            else:
+                self._p2p([(self.sizes[k, self.rank], self.dst)], [])
+        with self._ctx():
+            self.sizes_host[k].copy_(self.sizes[k], non_blocking=self.cuda)
+            if self.cuda:
+                ev = torch.cuda.Event()
+                ev.record(self.comm)
+                self._sized[k] = ev
+
+    def post_payload(self, t: int, wires, smalls):
+        """Step t's buffers: exactly the announced bytes of every wire buffer + its smalls.
+        Returns, on the root, {(rank, j): (wire bytes, small)} with the root's own buffers in
+        place (no self-copy); {} elsewhere. Everything is enqueued on the comm stream."""
+        k = t % self.ring
+        if self.cuda and self._sized[k] is not None:
+            self._sized[k].synchronize()  # the copy of sizes(t) into pinned memory (host wait only)
+        tot = self.sizes_host[k].tolist()
+        got = {}
+        if self.rank == self.dst:
+            for j in range(self.n_bufs):
+                got[self.rank, j] = (wires[j][:tot[self.rank][j]], smalls[j])
+            recvs = []
+            for r in self.peers:
+                for j in range(self.n_bufs):
+                    n = int(tot[r][j])
+                    if n < 16 or n > self.recv_wire[r, j].numel():
+                        raise RuntimeError(f"rank {r} buffer {j} announces {n} B (capacity "
+                                           f"{self.recv_wire[r, j].numel()})")
+                    w, s = self.recv_wire[r, j][:n], self.recv_small[r, j]
+                    recvs += [(w, r), (s, r)]
+                    got[r, j] = (w, s)
+                    self.payload_bytes += n
+            self._p2p([], recvs)
+        elif self.world > 1:
+            sends = []
+            for j in range(self.n_bufs):
+                sends += [(wires[j][:int(tot[self.rank][j])], self.dst), (smalls[j], self.dst)]
+            self._p2p(sends, [])
+        return got
+
+    def mark_done(self, t: int):
+        """Everything enqueued on the comm stream for step t so far (its payload and whatever
+        the caller consumed it with) is what done(t) waits for."""
+        if self.cuda:
+            ev = torch.cuda.Event()
+            ev.record(self.comm)
+            self._done[t % self.ring] = ev
+
+    def done(self, t: int):
+        return self._done[t % self.ring]
+
+
+class _null:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
+class WireGather:
+    """BASELINE config 5's step on one rank: every env batch of this rank (an NmmoEngine with
+    obs_layout OBS_WIRE on its own stream) runs the scripted policy + nmmo_step into a ring of
+    wire buffers, and the learner gather (WireExchange) moves every rank's buffers + packed
+    reward / term / trunc / mask into rank 0 one step behind, on a comm stream, so step t's
+    transfer overlaps step t + 1's compute (reference: the recv -> store loop of
+    clean_pufferl.py:293-346, fed here by every GPU of the node).
+
+    On the root, each step's buffers are validated on the device (nmmo_wire_check: sizes,
+    offsets, count words, record heads; `status` accumulates) — "delivered": every agent's
+    observation landed, checked, in the learner's HBM, in the form the experience store decodes
+    its kept rows from (nmmo_exp_store, wire input). decode=True additionally decodes every
+    rank's buffers into the native layout (nmmo_wire_unpack, the full learner-ready tensor) on
+    the comm stream. on_step(t, got) (tests) runs on the root after step t's buffers landed,
+    with the device synchronised: got = {(rank, batch): (wire bytes, smalls)}.
+
+    The compute of each (batch, ring slot) is captured once in a hipGraph (graphs=True); with
+    graphs=False, before_step(t, j, engine) (tests: per-env episode ends) runs on batch j's
+    stream ahead of its step-t compute."""
+
+    def __init__(self, engines, policy_seed: int, rank: int = 0, world: int = 1, decode: bool = False,
+                 graphs: bool = True, ring: int = 3, on_step=None, backend: str | None = None,
+                 before_step=None):
+        if before_step is not None and graphs:
+            raise ValueError("before_step needs graphs=False")
+        self.before_step = before_step
+        from . import abi, devmem
+        from . import wire as nw
+
+        self.engines = list(engines)
+        self.rank, self.world, self.decode, self.on_step = rank, world, decode, on_step
+        self.pseed = policy_seed
+        e0 = self.engines[0]
+        self.device = e0.device
+        self.P = e0.P
+        for e in self.engines:
+            if e.config.obs_layout != abi.OBS_WIRE:
+                raise ValueError("WireGather steps handles created with obs_layout OBS_WIRE")
+        nb = len(self.engines)
+        self.ring = ring
+        self.wires = [[e.obs] + [devmem.empty(tuple(e.obs.shape), torch.uint8, self.device) for _ in range(ring - 1)]
+                      for e in self.engines]
+        self.smalls = [[torch.zeros((e.n_envs, self.P, 8), dtype=torch.uint8, device=self.device) for _ in range(ring)]
+                       for e in self.engines]
+        caps = [nw.max_bytes(e.n_envs, self.P) for e in self.engines]
+        self.x = WireExchange(world, rank, nb, caps, [s[0].numel() for s in self.smalls], self.device,
+                              ring=ring, backend=backend)
+        self.streams = [torch.cuda.Stream(device=self.device) for _ in self.engines]
+        self.status = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.native = None
+        if decode and rank == 0:
+            n_envs = [e.n_envs for e in self.engines]
+            self.native = {(r, j): devmem.empty((n_envs[j], abi.native_env_bytes(self.P)), torch.uint8, self.device)
+                           for r in range(world) for j in range(nb)}
+        self.graphs = None
+        if graphs:
+            self._capture()
+        self.t = 0
+
+    def _body(self, j: int, k: int):
+        e = self.engines[j]
+        e.obs = self.wires[j][k]
+        e.scripted_actions(self.pseed)
+        e.step()
+        sm = self.smalls[j][k]
+        sm[..., 0:4] = e.rew.view(torch.uint8).view(e.n_envs, self.P, 4)
+        sm[..., 4] = e.term
+        sm[..., 5] = e.trunc
+        sm[..., 6] = e.mask
+
+    def _capture(self):
+        torch.cuda.synchronize(self.device)
+        self.graphs = {}
+        for j in range(len(self.engines)):
+            for k in range(self.ring):
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=self.streams[j]):
+                    self._body(j, k)
+                self.graphs[j, k] = g
+        torch.cuda.synchronize(self.device)
+
+    def _consume(self, s: int, got):
+        """On the comm stream, after step s's buffers landed on the root."""
+        from . import wire as nw
+
+        if self.rank != 0:
+            return
+        with torch.cuda.stream(self.x.comm):
+            for (r, j), (w, _) in got.items():
+                n = self.engines[j].n_envs
+                if r != 0:  # a received buffer against the size its sender announced
+                    nw.check_buffer(w, n, self.P, self.status, self.x.sizes[s % self.ring, r, j:j + 1])
+                if self.native is not None:
+                    nw.unpack(w, n, self.P, out=self.native[r, j])
+        if self.on_step is not None:
+            torch.cuda.synchronize(self.device)
+            self.on_step(s, got)
+
+    def step(self):
+        t, k = self.t, self.t % self.ring
+        ready = []
+        for j in range(len(self.engines)):
+            st = self.streams[j]
+            done = self.x.done(t)  # slot k's previous step (t - ring) has been sent / consumed
+            if done is not None:
+                st.wait_event(done)
+            with torch.cuda.stream(st):
+                if self.graphs is not None:
+                    self.graphs[j, k].replay()
+                else:
+                    if self.before_step is not None:
+                        self.before_step(t, j, self.engines[j])
+                    self._body(j, k)
+                ev = torch.cuda.Event()
+                ev.record(st)
+            ready.append(ev)
+        if t >= 1:  # step t - 1's payload, now that step t is queued
+            self._payload(t - 1)
+        self.x.post_sizes(t, [w[k] for w in self.wires], ready)
+        self.t += 1
+
+    def _payload(self, s: int):
+        ks = s % self.ring
+        got = self.x.post_payload(s, [w[ks] for w in self.wires], [sm[ks] for sm in self.smalls])
+        self._consume(s, got)
+        self.x.mark_done(s)
+
+    def drain(self):
+        """Post the last step's payload and make the current stream wait for every transfer."""
+        if self.t >= 1:
+            self._payload(self.t - 1)
+        cur = torch.cuda.current_stream(self.device)
+        for st in self.streams:
+            cur.wait_stream(st)
+        cur.wait_stream(self.x.comm)
+
+    def check_status(self):
+        """The accumulated nmmo_wire_check bits (0 = every received buffer was consistent)."""
+        return int(self.status.item())
+
+    def close(self):
+        torch.cuda.synchronize(self.device)
+        for j, e in enumerate(self.engines):
+            e.obs = self.wires[j][0]
+        self.graphs = None

@@ -55,6 +55,10 @@ class NmmoEngine:
             from . import devmem
 
             self.obs = devmem.empty((n, abi.native_env_bytes(P)), torch.uint8, d)
+        elif config.obs_layout == abi.OBS_WIRE:  # SPEC §8c: header + records, sized for full windows
+            from . import devmem, wire
+
+            self.obs = devmem.empty((wire.max_bytes(n, P),), torch.uint8, d)
         else:
             self.obs = None
         emb = np.zeros((1, config.TASK_EMBED_DIM), np.float32) if task is None else \
@@ -73,6 +77,10 @@ class NmmoEngine:
         if getattr(self, "h", None) is not None and self.h.value:
             torch.cuda.synchronize(self.device)
             lib().nmmo_destroy(self.h)
+            self.obs = None
+            from . import devmem
+
+            devmem.release_pending()  # the chunk-mapped buffers no tensor holds any more
         self.h = None
 
     def __del__(self):
@@ -103,12 +111,16 @@ class NmmoEngine:
         return self.obs, self.mask
 
     def end_episodes(self, env_mask):
-        """End the current episode of the envs where env_mask (host bool/u8 [n_envs]) is set: their
-        next step resets them (nmmo_end_episodes; per-env reset of an async pool)."""
-        m = np.ascontiguousarray(np.asarray(env_mask, dtype=np.uint8))
-        assert m.shape == (self.n_envs,)
+        """End the current episode of the envs where env_mask (bool/u8 [n_envs], host or device)
+        is set: their next step resets them (nmmo_end_episodes, enqueued on the current stream;
+        the per-env reset of an async pool)."""
+        m = torch.as_tensor(np.asarray(env_mask, dtype=np.uint8) if not torch.is_tensor(env_mask) else env_mask)
+        if tuple(m.shape) != (self.n_envs,):
+            raise ValueError(f"env_mask must have shape ({self.n_envs},)")
+        m = m.to(device=self.device, dtype=torch.uint8).contiguous()
         with torch.cuda.device(self.device):
-            check(lib().nmmo_end_episodes(self.h, m.ctypes.data_as(ctypes.c_void_p)), "nmmo_end_episodes")
+            check(lib().nmmo_end_episodes(self.h, self._ptr(m), self._stream()), "nmmo_end_episodes")
+        self._end_mask = m  # alive until the stream has read it
 
     def step(self, actions=None, write_obs: bool = True):
         """One tick of every env; `actions` int32 [n_envs, P, 12] on the device (default: the

@@ -94,9 +94,10 @@ class DeviceExperience:
     def store(self, o, r, d, mask, actions, logprob, value, step: int, env_id=None, env_id_base: int = 0,
               engine=None, validate: bool = False):
         """Append the learner-mask rows of one recv in row order, cut at the room left (:331-346).
-        o: flat float32 [N, obs_elems] (or [n_envs, P, obs_elems]), or the native uint8
+        o: flat float32 [N, obs_elems] (or [n_envs, P, obs_elems]), the native uint8
         [n_envs, env_bytes] buffer of `engine` (an NmmoEngine with obs_layout NATIVE), expanded
-        on store; r float32 [N]; d / mask uint8 or bool [N]; actions int [N, 12]; logprob /
+        on store, or a uint8 wire buffer (SPEC §8c) of N / P envs with `engine` an NmmoEngine
+        with obs_layout WIRE (its layout and task table), the kept rows decoded on store; r float32 [N]; d / mask uint8 or bool [N]; actions int [N, 12]; logprob /
         value float32 [N]; env_id int [N] distinct agent-slot ids (None = env_id_base + row)."""
         dev = self.device
 
@@ -118,12 +119,18 @@ class DeviceExperience:
             if torch.unique(sel).numel() != sel.numel():
                 raise ValueError("env_id must be distinct within one store")
         native = engine is not None and engine.config.obs_layout == abi.OBS_NATIVE
+        wired = engine is not None and engine.config.obs_layout == abi.OBS_WIRE
+        obs_flat = obs_nat = obs_wire = None
         if native:
             if o.dtype != torch.uint8 or o.shape[0] * engine.P != n:
                 raise ValueError("native obs must be the engine's uint8 [n_envs, env_bytes] buffer")
-            obs_flat, obs_nat = None, o.contiguous()
+            obs_nat = o.contiguous()
+        elif wired:  # a wire buffer of n / P envs (SPEC §8c): only the kept rows are decoded
+            if o.dtype != torch.uint8 or o.dim() != 1 or n % engine.P:
+                raise ValueError("wire obs must be a uint8 wire buffer of whole envs")
+            obs_wire = o
         else:
-            obs_flat, obs_nat = o.contiguous().view(n, self.obs_elems), None
+            obs_flat = o.contiguous().view(n, self.obs_elems)
             if obs_flat.dtype != torch.float32:
                 raise ValueError("flat obs must be float32")
         for t in (m_, d_, lp, v):
@@ -133,12 +140,13 @@ class DeviceExperience:
         inp = abi.NmmoStoreInput(n, int(step), obs_flat.data_ptr() if obs_flat is not None else None,
                                  obs_nat.data_ptr() if obs_nat is not None else None, r_.data_ptr(),
                                  d_.data_ptr(), m_.data_ptr(), eid.data_ptr() if eid is not None else None,
-                                 int(env_id_base), a.data_ptr(), lp.data_ptr(), v.data_ptr())
+                                 int(env_id_base), a.data_ptr(), lp.data_ptr(), v.data_ptr(),
+                                 obs_wire.data_ptr() if obs_wire is not None else None)
         with torch.cuda.device(dev):
-            check(lib().nmmo_exp_store(engine.h if native else None, ctypes.byref(self.x), ctypes.byref(inp),
-                                       _p(self.scratch), self._stream()), "nmmo_exp_store")
+            check(lib().nmmo_exp_store(engine.h if native or wired else None, ctypes.byref(self.x),
+                                       ctypes.byref(inp), _p(self.scratch), self._stream()), "nmmo_exp_store")
         # keep the inputs alive until the kernels that read them have been enqueued
-        self._inflight = (r_, d_, m_, lp, v, a, eid, obs_flat, obs_nat)
+        self._inflight = (r_, d_, m_, lp, v, a, eid, obs_flat, obs_nat, obs_wire)
 
     # -- train side (clean_pufferl.py:413-458)
     def sort(self) -> torch.Tensor:

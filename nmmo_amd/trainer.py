@@ -151,7 +151,9 @@ class DeviceTrainer:
         """One update (clean_pufferl.py:390-540): sort, GAE, flatten, PPO epochs."""
         cfg, exp, agent = self.config, self.experience, self.agent
         if cfg.anneal_lr:
-            frac = 1.0 - self.update / self.total_updates  # (data.update - 1) with 1-based updates
+            # clean_pufferl.py:409 with data.update counted from 0 and incremented after train()
+            # (:140, :557): the first update's frac is 1 + 1/total_updates, as in the reference
+            frac = 1.0 - (self.update - 1.0) / self.total_updates
             self.optimizer.param_groups[0]["lr"] = frac * cfg.learning_rate
         t0 = time.perf_counter()
         idxs = exp.sort()

@@ -97,9 +97,12 @@ class GpuVecEnv:
             raise ValueError("GpuVecEnv serves flat observations (obs_layout=OBS_FLAT)")
         self.num_envs = int(num_envs)
         if envs_per_batch not in (None, self.num_envs):
-            # lockstep GPU stepping: one batch = every env (clean_pufferl sizes buffers from
-            # envs_per_batch, so report the real value instead of silently re-batching)
-            pass
+            # lockstep GPU stepping: one batch = every env. clean_pufferl sizes its buffers from
+            # pool.envs_per_batch (clean_pufferl.py:116-119), so a caller asking for async
+            # sub-batches would silently get another batch shape: refuse instead.
+            raise ValueError(f"GpuVecEnv steps every env in lockstep: envs_per_batch must be None or "
+                             f"num_envs ({self.num_envs}), got {envs_per_batch}; run several pools for "
+                             f"env batches")
         self.envs_per_batch = self.num_envs
         self.mask_agents = mask_agents
         self.engine = NmmoEngine(self.config, self.num_envs, seed=seed, device=device,
@@ -190,6 +193,10 @@ class NmmoEnv:
         self.agents: list[int] = []
         self._obs_space = Box(-2**20, 2**20, (self.engine.obs_elems,), np.float32)
         self._act_space = MultiDiscrete(layout.ACTION_DIMS)
+        # state / realm / tasks of the current tick, read from the device once per tick
+        # (BaseStatWrapper reads env.realm once per agent per step, stat_wrapper.py:122-123);
+        # reset() and step() invalidate it
+        self._tick_cache: dict = {}
 
     def observation_space(self, agent):
         return self._obs_space
@@ -207,6 +214,7 @@ class NmmoEnv:
         return out
 
     def reset(self, seed=None, options=None):
+        self._tick_cache = {}
         self.engine.reset(None if seed is None else np.array([seed], dtype=np.uint64))
         mask = self.engine.mask[0].cpu().numpy()
         self.agents = [a for i, a in enumerate(self.possible_agents) if mask[i]]
@@ -220,6 +228,7 @@ class NmmoEnv:
             if isinstance(act, dict):
                 act = flatten_action(act)
             buf[0, a - 1] = np.asarray(act, dtype=np.int32)
+        self._tick_cache = {}
         self.engine.step(torch.from_numpy(buf).to(self.engine.device))
         e = self.engine
         mask = e.mask[0].cpu().numpy()
@@ -239,7 +248,9 @@ class NmmoEnv:
         """Realm facade: `realm.tick`, `realm.players` (id -> entity, with `dead_this_tick`),
         `realm.npcs` and `realm.event_log` — the reads of stat_wrapper.py:122-185, 216-285 and
         train_helper.py:133-166."""
-        return _Realm(self.state(), self.engine.events(0), env=self)
+        if "realm" not in self._tick_cache:
+            self._tick_cache["realm"] = _Realm(self.state(), self.engine.events(0), env=self)
+        return self._tick_cache["realm"]
 
     @property
     def max_num_agents(self) -> int:
@@ -248,17 +259,25 @@ class NmmoEnv:
     @property
     def tasks(self) -> list:
         """One Task per agent in possible_agents order (nmmo.Env.tasks)."""
-        names = getattr(self.engine, "task_names", None) or [default_spec_name(self.config)]
-        return tasks_from_state(self.state(), self.possible_agents, names, self.engine.task_table)
+        if "tasks" not in self._tick_cache:
+            names = getattr(self.engine, "task_names", None) or [default_spec_name(self.config)]
+            self._tick_cache["tasks"] = tasks_from_state(self.state(), self.possible_agents, names,
+                                                         self.engine.task_table)
+        return self._tick_cache["tasks"]
 
     @property
     def agent_task_map(self) -> dict:
         """agent id -> [Task] (nmmo.Env.agent_task_map, read at stat_wrapper.py:155)."""
-        return {t.assignee[0]: [t] for t in self.tasks}
+        if "task_map" not in self._tick_cache:
+            self._tick_cache["task_map"] = {t.assignee[0]: [t] for t in self.tasks}
+        return self._tick_cache["task_map"]
 
     def state(self) -> dict:
-        st = self.engine.get_state()
-        return parse_env_state(st, self.engine.S, self.config.PLAYER_N)
+        """The env's parsed state blob (nmmo_get_state), read once per tick."""
+        if "state" not in self._tick_cache:
+            st = self.engine.get_state()
+            self._tick_cache["state"] = parse_env_state(st, self.engine.S, self.config.PLAYER_N)
+        return self._tick_cache["state"]
 
     def record_replay(self, helper):
         """realm.record_replay(replay_helper) (train_helper.py:134): the helper is updated after

@@ -5,7 +5,9 @@ layout (9,552 B per agent + 32 KB Market per env) is mostly padding on the wire;
 (`nmmo_wire_pack`, csrc/wire.hip) keeps the 16-B record head, the ActionTargets as bits, only
 the visible Entity rows and held items, the 225 window materials and only the listed Market
 rows: ~1.3 KB per agent in C4 steady state. The receiver decodes it back to the native layout
-bit-identically (`nmmo_wire_unpack`). The transfer protocol — the fixed-size header first, then
+bit-identically (`nmmo_wire_unpack`). A handle created with obs_layout OBS_WIRE writes the same
+bytes straight from the state (nmmo_step / nmmo_observe into a wire buffer), with no native
+buffer at all. The transfer protocol — the fixed-size header first, then
 exactly the payload the header announces — is `nmmo_amd.distributed.gather_wire_to_learner`.
 """
 
@@ -59,3 +61,19 @@ def unpack(wire: torch.Tensor, n_envs: int, players: int, out: torch.Tensor | No
         check(lib().nmmo_wire_unpack(n_envs, players, ctypes.c_void_p(wire.data_ptr()),
                                      ctypes.c_void_p(out.data_ptr()), _stream(wire.device)), "nmmo_wire_unpack")
     return out
+
+
+def check_buffer(wire: torch.Tensor, n_envs: int, players: int, status: torch.Tensor,
+                 expect_total: torch.Tensor | None = None) -> torch.Tensor:
+    """Enqueue the consistency check of a (received) wire buffer (nmmo_wire_check): error bits
+    are OR-ed into `status` (device int32 [1]; 0 = valid: 1 total != expect_total, 2 offsets, 4
+    count ranges, 8 record heads). `expect_total`: device int64 [1] the sender announced."""
+    if status.dtype != torch.int32 or status.device != wire.device:
+        raise ValueError("status must be an int32 tensor on the wire buffer's device")
+    if expect_total is not None and (expect_total.dtype != torch.int64 or expect_total.device != wire.device):
+        raise ValueError("expect_total must be an int64 tensor on the wire buffer's device")
+    with torch.cuda.device(wire.device):
+        check(lib().nmmo_wire_check(ctypes.c_void_p(wire.data_ptr()), n_envs, players,
+                                    None if expect_total is None else ctypes.c_void_p(expect_total.data_ptr()),
+                                    ctypes.c_void_p(status.data_ptr()), _stream(wire.device)), "nmmo_wire_check")
+    return status

@@ -1,0 +1,109 @@
+"""One rank of the 2-rank C5 content check (tests/test_gpu_multirank.py), launched under
+torch.distributed.run with gloo, both ranks on cuda:0.
+
+Each rank steps its env batches through WireGather (wire obs, learner gather one step behind);
+rank 0 decodes every gathered buffer (its own in place, the peer's received) into the native
+layout and stores the learner-mask rows of every step into a DeviceExperience straight from the
+wire records, then writes per step and global env the sha256 of the native obs and of the
+reward / term / trunc / mask bytes, plus digests of the experience buffers, to argv[1] (JSON).
+The test compares them with one engine stepping all envs alone. Not collected by pytest."""
+
+import hashlib
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+# shared with the test's one-engine reference run
+N_PER_BATCH, BATCHES, SEED, PSEED, PREROLL, TICKS, MAP_N = 3, 2, 11, 77, 36, 18, 8
+
+
+def end_mask(ids, t):
+    """Envs (global ids) whose episode the pool ends before checked step t (staggered resets)."""
+    return (ids * 7 + t) % 11 == 0
+
+
+def preroll_mask(ids, k):
+    return ids % 12 == k if k < 12 else ids < 0
+
+
+def digest(t):
+    return hashlib.sha256(t.contiguous().cpu().numpy().tobytes()).hexdigest()[:24]
+
+
+def main():
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from nmmo_amd import abi, wire
+    from nmmo_amd.config import Config
+    from nmmo_amd.distributed import WireGather
+    from nmmo_amd.engine import NmmoEngine
+    from nmmo_amd.storage import DeviceExperience
+
+    out_path = sys.argv[1]
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("gloo")
+    n, nb = N_PER_BATCH, BATCHES
+    envs = n * nb
+    cfg = Config.preset("C4", MAP_N=MAP_N, early_stop_agent_num=8, obs_layout=abi.OBS_WIRE)
+    engs = [NmmoEngine(cfg, n, seed=SEED, device=dev, env_index_base=rank * envs + j * n) for j in range(nb)]
+    P = engs[0].P
+    for e in engs:
+        e.reset()
+    for k in range(PREROLL):
+        for j, e in enumerate(engs):
+            e.end_episodes(preroll_mask(np.arange(n) + rank * envs + j * n, k))
+            e.scripted_actions(PSEED)
+            e.step(write_obs=False)
+    torch.cuda.synchronize()
+
+    def before(t, j, e):
+        e.end_episodes(end_mask(np.arange(n) + rank * envs + j * n, t))
+
+    rec = {"native": {}, "small": {}}
+    x = DeviceExperience(TICKS * world * envs * P, engs[0].obs_elems, world * envs * P, device=dev) if rank == 0 else None
+
+    def on_step(s, got):
+        z = torch.zeros(n * P, device=dev)
+        for (r, j) in sorted(got):
+            w, sm = got[r, j]
+            nat = wire.unpack(w, n, P)
+            sm3 = sm.view(n, P, 8)
+            base = r * envs + j * n
+            for i in range(n):
+                rec["native"][f"{s}:{base + i}"] = digest(nat[i])
+                rec["small"][f"{s}:{base + i}"] = digest(sm3[i, :, :7])
+            rew = sm3[..., 0:4].contiguous().view(torch.float32).view(-1)
+            x.store(w, rew, sm3[..., 4].reshape(-1), sm3[..., 6].reshape(-1), torch.zeros((n * P, 12), dtype=torch.int32),
+                    z, z, step=s + 1, env_id_base=base * P, engine=engs[0])
+
+    g = WireGather(engs, PSEED, rank, world, graphs=False, on_step=on_step if rank == 0 else None,
+                   before_step=before, backend="gloo")
+    for _ in range(TICKS):
+        g.step()
+    g.drain()
+    torch.cuda.synchronize()
+    status = g.check_status()
+    g.close()
+    if rank == 0:
+        k = x.ptr
+        rec["status"] = status
+        rec["exp"] = {"ptr": k, "obs": digest(x.obs[:k]), "rewards": digest(x.rewards[:k]),
+                      "dones": digest(x.dones[:k]), "env_id": digest(x.env_id[:k]), "step": digest(x.step[:k])}
+        rec["payload_bytes"] = g.x.payload_bytes
+        with open(out_path, "w") as f:
+            json.dump(rec, f)
+    dist.barrier()
+    for e in engs:
+        e.close()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

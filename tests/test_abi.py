@@ -161,3 +161,31 @@ int main(void) {
 def test_set_wrapper_rejects_bad_handles(native):
     assert native.nmmo_set_wrapper(None, None, None) == abi.NMMO_E_INVALID
     assert native.nmmo_get_wrapper_state(None, None, None) == abi.NMMO_E_INVALID
+
+
+def test_storage_structs_and_wire_layout_match_c_compiler():
+    src = r"""
+#include <stdio.h>
+#include <stddef.h>
+#include "nmmo_hip.h"
+int main(void) {
+  printf("%zu %zu %zu %zu %d\n", sizeof(NmmoStoreInput), offsetof(NmmoStoreInput, values),
+         offsetof(NmmoStoreInput, wire), sizeof(NmmoExperience), NMMO_OBS_WIRE);
+  return 0;
+}
+"""
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "t.c")
+        open(c, "w").write(src)
+        exe = os.path.join(d, "t")
+        subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), c, "-o", exe])
+        got = list(map(int, subprocess.check_output([exe]).split()))
+    assert got == [ctypes.sizeof(abi.NmmoStoreInput), abi.NmmoStoreInput.values.offset,
+                   abi.NmmoStoreInput.wire.offset, ctypes.sizeof(abi.NmmoExperience), abi.OBS_WIRE]
+
+
+def test_wire_calls_report_errors(native):
+    assert native.nmmo_wire_check(None, 4, 128, None, None, None) == abi.NMMO_E_INVALID
+    assert native.nmmo_wire_pack(None, None, None, None) == abi.NMMO_E_INVALID
+    assert native.nmmo_end_episodes(None, None, None) == abi.NMMO_E_INVALID
+    assert native.nmmo_wire_header_bytes(4, 500) == abi.NMMO_E_INVALID

@@ -1,6 +1,6 @@
 """GPU-resident experience storage against the reference's storage
 restated on the CPU (oracle/storage.py): rollouts of the HIP engine are stored step by step on
-the device (flat obs, and native obs expanded on store) and on the host checker with the same
+the device (flat obs, native obs expanded on store, wire records decoded on store) and on the host checker with the same
 learner masks, actions, logprobs and values; every buffer, the (env_id, step) order, the
 advantages and the minibatch gathers must be bit-identical."""
 
@@ -38,11 +38,18 @@ def _roll(layout_kind, batch_size, n_envs, masked_policy, env_id_mode):
         v = torch.randn(n, generator=g)
         pmask = (torch.rand(n, generator=g) < 0.8) if masked_policy else torch.ones(n, dtype=torch.bool)
         learner_mask = eng.mask.view(-1).cpu().bool() & pmask
-        flat = eng.obs.view(n, -1) if layout_kind == abi.OBS_FLAT else eng.expand_obs().view(n, -1)
+        if layout_kind == abi.OBS_FLAT:
+            flat = eng.obs.view(n, -1)
+        elif layout_kind == abi.OBS_NATIVE:
+            flat = eng.expand_obs().view(n, -1)
+        else:  # wire records -> native -> flat: the checker's rows come the long way round
+            from nmmo_amd import wire
+
+            flat = eng.expand_obs(wire.unpack(eng.obs, n_envs, P)).view(n, -1)
         env_id = perm if perm is not None else torch.arange(n, dtype=torch.int32) + 3
         x.store(eng.obs, eng.rew.view(-1), eng.term.view(-1), learner_mask, a.view(n, 12), lp, v, step,
                 env_id=env_id if perm is not None else None, env_id_base=3,
-                engine=eng if layout_kind == abi.OBS_NATIVE else None)
+                engine=eng if layout_kind != abi.OBS_FLAT else None)
         ref.store(flat.cpu().numpy(), eng.rew.view(-1).cpu().numpy(), eng.term.view(-1).cpu().numpy(),
                   learner_mask.numpy(), a.view(n, 12).cpu().numpy(), lp.numpy(), v.numpy(), env_id.numpy(), step)
         assert x.ptr == ref.ptr, f"step {step}: ptr {x.ptr} != {ref.ptr}"
@@ -63,7 +70,8 @@ def _same(a, b, what):
 
 
 @pytest.mark.parametrize("layout_kind,masked_policy,env_id_mode", [
-    (abi.OBS_FLAT, False, "base"), (abi.OBS_NATIVE, True, "base"), (abi.OBS_FLAT, True, "perm")])
+    (abi.OBS_FLAT, False, "base"), (abi.OBS_NATIVE, True, "base"), (abi.OBS_FLAT, True, "perm"),
+    (abi.OBS_WIRE, True, "perm")])
 def test_storage_matches_reference(layout_kind, masked_policy, env_id_mode):
     import torch
 

@@ -141,3 +141,27 @@ def test_facade_serves_stat_wrapper_reads():
                 walked += 1
     assert walked > 0
     env.close()
+
+
+def test_realm_read_once_per_tick():
+    """BaseStatWrapper reads env.realm once per agent per step (stat_wrapper.py:122-123): over
+    the reads of a whole step for all 128 agents the facade copies the device state once."""
+    from nmmo_amd.vecenv import NmmoEnv
+    from tests.test_facade import walk_stat_wrapper_reads
+
+    env = NmmoEnv(Config.preset("C4", MAP_N=2, early_stop_agent_num=0), seed=3)
+    calls = []
+    orig = env.engine.get_state
+    env.engine.get_state = lambda: (calls.append(1), orig())[1]
+    env.reset()
+    for t in range(3):
+        calls.clear()
+        env.step({})
+        realm = env.realm
+        present = [a for a in env.possible_agents
+                   if realm.players.get(a) is not None or a in realm.players.dead_this_tick]
+        assert len(present) == 128
+        for a in present:
+            walk_stat_wrapper_reads(env.realm, env.agent_task_map, a, terminated=False)
+        assert len(calls) == 1, f"tick {t}: {len(calls)} state copies"
+    env.close()

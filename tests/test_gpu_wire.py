@@ -62,3 +62,140 @@ def test_wire_roundtrip_fullsize():
     total = wire.total_bytes(w)
     assert total * 4 < eng.obs.numel(), (total, eng.obs.numel())
     eng.close()
+
+
+def _pair(n, seed, map_n=4, wrapper=None):
+    """A native-obs engine and a wire-obs engine (NMMO_OBS_WIRE) over the same envs."""
+    from nmmo_amd import abi
+    from nmmo_amd.config import Config
+    from nmmo_amd.engine import NmmoEngine
+
+    engs = []
+    for lay in (abi.OBS_NATIVE, abi.OBS_WIRE):
+        cfg = Config.preset("C4", MAP_N=map_n, early_stop_agent_num=8, obs_layout=lay)
+        e = NmmoEngine(cfg, n, seed=seed)
+        if wrapper is not None:
+            from nmmo_amd.wrappers import wrapper_config
+
+            e.set_wrapper(wrapper_config(wrapper[0], **wrapper[1]))
+        engs.append(e)
+    return engs
+
+
+@pytest.mark.parametrize("wrapper", [None, ("yaofeng", dict(disable_give=True, donot_attack_dangerous_npc=True)),
+                                     ("neurips23_start_kit", dict(heal_bonus_weight=0.03))])
+def test_wire_layout_equals_pack_of_native(wrapper):
+    """The wire records the obs kernel writes straight from the state (NMMO_OBS_WIRE) are the
+    bytes nmmo_wire_pack makes of the native obs of the same state, tick by tick (resets,
+    staggered episodes, wrapper obs edits included)."""
+    from nmmo_amd import wire
+
+    nat, wir = _pair(4, seed=33, wrapper=wrapper)
+    for e in (nat, wir):
+        e.reset()
+    for t in range(60):
+        if t == 17:
+            for e in (nat, wir):
+                e.end_episodes(np.array([1, 0, 0, 1], bool))
+        for e in (nat, wir):
+            e.scripted_actions(900 + t)
+            e.step()
+        if t % 6 != 5:
+            continue
+        ref = wire.pack(nat)
+        total = wire.total_bytes(ref)
+        assert wire.total_bytes(wir.obs) == total, t
+        assert torch.equal(wir.obs[:total], ref[:total]), f"wire layout differs from pack(native) at tick {t}"
+        assert torch.equal(nat.rew, wir.rew) and torch.equal(nat.mask, wir.mask)
+    for e in (nat, wir):
+        e.close()
+
+
+def test_wire_layout_fullsize_roundtrip_and_check():
+    """1,024 envs with staggered episodes: the wire layout decodes to the native obs of the same
+    state, passes nmmo_wire_check, and a corrupted count word / total is flagged."""
+    from nmmo_amd import wire
+
+    n = 1024
+    nat, wir = _pair(n, seed=5, map_n=256)
+    ids = np.arange(n)
+    for e in (nat, wir):
+        e.reset()
+    for k in range(32):
+        for e in (nat, wir):
+            e.end_episodes(ids % 32 == k)
+            e.scripted_actions(300 + k)
+            e.step()
+    back = wire.unpack(wir.obs, n, wir.P)
+    assert torch.equal(back, nat.obs)
+    total = wire.total_bytes(wir.obs)
+    st = torch.zeros(1, dtype=torch.int32, device=wir.device)
+    want = torch.tensor([total], dtype=torch.int64, device=wir.device)
+    wire.check_buffer(wir.obs, n, wir.P, st, want)
+    assert int(st.item()) == 0
+    bad = wir.obs[:total].clone()
+    wire.check_buffer(bad, n, wir.P, st, want + 16)
+    assert int(st.item()) & 1
+    st.zero_()
+    hb = wire.header_bytes(n, wir.P)
+    cnt = bad[8 + 8 * n:8 + 8 * n + 2 * n * wir.P].view(torch.int16)
+    j = int(torch.nonzero(cnt < 0)[3, 0])  # bit 15: in the realm
+    cnt[j] = cnt[j] + 1  # one more visible entity than the record holds
+    wire.check_buffer(bad, n, wir.P, st)
+    assert int(st.item()) & (2 | 8), int(st.item())
+    assert hb < total
+    for e in (nat, wir):
+        e.close()
+
+
+def test_wire_store_equals_native_store():
+    """nmmo_exp_store from a wire buffer decodes exactly the kept rows into the flat experience
+    rows the native store expands (bit-exact), under a learner mask that drops rows."""
+    from nmmo_amd.storage import DeviceExperience
+
+    n = 6
+    nat, wir = _pair(n, seed=8)
+    for e in (nat, wir):
+        e.reset()
+    P = nat.P
+    xs = [DeviceExperience(700, nat.obs_elems, n * P, device=nat.device) for _ in range(2)]
+    g = torch.Generator(device="cpu").manual_seed(3)
+    for t in range(12):
+        for e in (nat, wir):
+            e.scripted_actions(40 + t)
+            e.step()
+        keep = (nat.mask.view(-1).cpu() != 0) & (torch.rand(n * P, generator=g) < 0.7)
+        m = keep.to(torch.uint8).to(nat.device)
+        z = torch.zeros(n * P, device=nat.device)
+        for x, e in zip(xs, (nat, wir)):
+            x.store(e.obs, e.rew.view(-1), e.term.view(-1), m, e.actions.view(-1, 12), z, z, step=t, engine=e)
+    torch.cuda.synchronize()
+    assert xs[0].ptr == xs[1].ptr > 0
+    k = xs[0].ptr
+    assert torch.equal(xs[0].obs[:k], xs[1].obs[:k])
+    assert torch.equal(xs[0].env_id[:k], xs[1].env_id[:k]) and torch.equal(xs[0].rewards[:k], xs[1].rewards[:k])
+    for e in (nat, wir):
+        e.close()
+
+
+def test_wire_pack_rejects_stale_native():
+    """nmmo_wire_pack refuses a native buffer a tick without an obs gather has made stale, or
+    one that is not the buffer the last gather wrote."""
+    from nmmo_amd import wire
+    from nmmo_amd._native import NativeError
+
+    eng = _engine(2, seed=4)
+    eng.reset()
+    eng.scripted_actions(1)
+    eng.step()
+    wire.pack(eng)
+    eng.scripted_actions(2)
+    eng.step(write_obs=False)
+    with pytest.raises(NativeError, match="stale"):
+        wire.pack(eng)
+    eng.observe()
+    wire.pack(eng)
+    other = torch.zeros_like(eng.obs)
+    with pytest.raises(NativeError, match="not the buffer"):
+        wire.pack(eng, native=other)
+    eng.close()

@@ -1,7 +1,7 @@
 """Wire encoding (SPEC.md §8c) on the CPU: the numpy restatement (oracle/wire.py) round-trips the
 native layout bit-exactly and shrinks it, and the learner-gather protocol
-(nmmo_amd.distributed.gather_wire_to_learner: fixed header, then exactly the announced payload)
-delivers every rank's buffer to the root over gloo (world size 2)."""
+(nmmo_amd.distributed.WireExchange: each step's sizes, then exactly the announced payload one
+step behind) delivers every rank's buffers to the root over gloo (world size 2)."""
 
 import os
 import socket
@@ -54,29 +54,59 @@ def _free_port():
     return p
 
 
+def _step_bytes(rank, t, n):
+    """What rank `rank` sends at step t: an oracle-made wire buffer (its size varies with the
+    tick) and a small companion buffer."""
+    nat, P = _native(n, 8 + 5 * t + 7 * rank, seed=9, env_index_base=rank * n)
+    small = (np.arange(n * P * 8) * (rank + 3) + t).astype(np.uint8)
+    return owire.pack(nat, P), small, P
+
+
 def _worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from nmmo_amd import distributed as nd
 
-    n = 2
-    nat, P = _native(n, 30 + 7 * rank, seed=9, env_index_base=rank * n)
-    packed = owire.pack(nat, P)
+    n, steps, ring = 2, 4, 3
+    P = Config.preset("C4").PLAYER_N
     cap = owire.header_bytes(n, P) + n * (P * 9552 + abi.NATIVE_MARKET_BYTES)
-    buf = torch.zeros(cap, dtype=torch.uint8)
-    buf[:packed.nbytes] = torch.from_numpy(packed)
-    got = nd.gather_wire_to_learner(buf, owire.header_bytes(n, P))
+    x = nd.WireExchange(world, rank, 1, [cap], [n * P * 8], torch.device("cpu"), ring=ring, backend="gloo")
+    wires = [torch.zeros(cap, dtype=torch.uint8) for _ in range(ring)]
+    smalls = [torch.zeros(n * P * 8, dtype=torch.uint8) for _ in range(ring)]
+    received = {}
+
+    def payload(s):
+        got = x.post_payload(s, [wires[s % ring]], [smalls[s % ring]])
+        for key, (w, sm) in got.items():
+            received[s, key[0]] = (w.numpy().copy(), sm.numpy().copy())
+
+    # the lagged schedule of WireGather.step: step t's sizes, step t - 1's payload
+    for t in range(steps):
+        w, sm, _ = _step_bytes(rank, t, n)
+        wires[t % ring][:w.nbytes] = torch.from_numpy(w)
+        wires[t % ring][w.nbytes:w.nbytes + 64] = 0xAB  # bytes past the total never travel
+        smalls[t % ring][:] = torch.from_numpy(sm)
+        if t >= 1:
+            payload(t - 1)
+        x.post_sizes(t, [wires[t % ring]])
+    payload(steps - 1)
     if rank == 0:
-        ok = True
-        for r in range(world):
-            ref, _ = _native(n, 30 + 7 * r, seed=9, env_index_base=r * n)
-            w = got[r].numpy()
-            ok &= np.array_equal(owire.unpack(w, n, P), ref)
+        ok = len(received) == steps * world
+        for t in range(steps):
+            for r in range(world):
+                w, sm, _ = _step_bytes(r, t, n)
+                gw, gs = received[t, r]
+                ok &= np.array_equal(gw, w) and np.array_equal(gs, sm)
+                ok &= np.array_equal(owire.unpack(gw, n, P), owire.unpack(w, n, P))
+        ok &= x.payload_bytes == sum(_step_bytes(r, t, n)[0].nbytes for t in range(steps) for r in range(1, world))
         q.put(bool(ok))
     dist.destroy_process_group()
 
 
 def test_wire_gather_protocol_gloo():
+    """WireExchange over gloo (world size 2, CPU tensors): the lagged protocol (step t's sizes,
+    then step t - 1's payload of exactly the announced bytes) delivers every rank's buffers of
+    every step to the root bit-exactly, its own in place."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()

@@ -1,0 +1,8 @@
+# round 3 GPU check: new wire / gather tests first, then the whole -m gpu suite, smoke, benches
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 400 python -u -m pytest tests/test_gpu_wire.py tests/test_gpu_storage.py tests/test_gpu_multirank.py tests/test_gpu_vecenv.py -x -v --timeout 120 --timeout-method thread > gpurun_out/gpu_new.log 2>&1 && \
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 150 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 && \
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 && \
+timeout -k 10 300 python bench.py --config C5 --steps 300 --warmup 50 --no-cpu-baseline > gpurun_out/bench_c5.json 2> gpurun_out/bench_c5.err && \
+timeout -k 10 400 python bench.py > gpurun_out/bench_default.json 2> gpurun_out/bench_default.err
