@@ -146,6 +146,8 @@ enum NmmoPredicate {
   PRED_EQUIP_ITEM, PRED_OWN_ITEM, PRED_INVENTORY_SPACE_GE, PRED_OCCUPY_TILE, PRED_CAN_SEE_TILE,
   PRED_FULLY_ARMED,
   PRED_PRACTICE_EATING, /* curriculum_generation/curriculum_tutorial.py:45-57 (EAT_FOOD count) */
+  PRED_CAN_SEE_AGENT,   /* a = target agent id; -1 / -2: the left / right team's leader */
+  PRED_CAN_SEE_GROUP,   /* a = -1 / -2: any member of the left / right team (SPEC.md §12 teams) */
   NMMO_N_PREDICATES
 };
 #define NMMO_TASK_SINGLE 0

@@ -80,7 +80,7 @@ PREDICATES = [
     "NONE", "TickGE", "CountEvent", "ScoreHit", "HarvestItem", "ConsumeItem", "ListItem", "BuyItem",
     "EarnGold", "SpendGold", "MakeProfit", "DefeatEntity", "HoardGold", "AttainSkill",
     "GainExperience", "EquipItem", "OwnItem", "InventorySpaceGE", "OccupyTile", "CanSeeTile",
-    "FullyArmed", "PracticeEating",
+    "FullyArmed", "PracticeEating", "CanSeeAgent", "CanSeeGroup",
 ]
 PRED = {n: i for i, n in enumerate(PREDICATES)}
 TASK_SINGLE, TASK_SUM, TASK_PRODUCT = 0, 1, 2

@@ -114,9 +114,19 @@ __device__ unsigned long long g_stamps[4096 * 32];
     if (threadIdx.x == 0 && blockIdx.x < 4096)                               \
       g_stamps[blockIdx.x * 32 + (k)] = __builtin_amdgcn_s_memtime();        \
   } while (0)
+// a launch's stamps start from zero: a phase a system set compiles out reads as absent
+#define NMMO_STAMP_CLEAR()                                                  \
+  do {                                                                       \
+    if (threadIdx.x < 32 && blockIdx.x < 4096) g_stamps[blockIdx.x * 32 + threadIdx.x] = 0ull; \
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");                   \
+    __builtin_amdgcn_wave_barrier();                                         \
+  } while (0)
 #else
 #define NMMO_STAMP(k) \
   do {               \
+  } while (0)
+#define NMMO_STAMP_CLEAR() \
+  do {                    \
   } while (0)
 #endif
 
@@ -1024,6 +1034,21 @@ __device__ __forceinline__ double term_progress(const Ctx& c, int p, const NmmoT
         for (int dc = -kVision; dc <= kVision; dc++)
           if (c.mat[(r + dr) * kSize + col + dc] == q.a) return 1.0;
       return 0.0;
+    }
+    case PRED_CAN_SEE_AGENT: case PRED_CAN_SEE_GROUP: {
+      // the target agent is one of the Entity obs rows of p's observation after this tick: in
+      // the realm, within the 15x15 window, and among the first 100 such entities in datastore
+      // row order (SPEC §12; teams: singletons in id order, left of agent id i is i - 1)
+      const int id = q.a > 0 ? q.a : q.a == -1 ? (p == 0 ? c.P : p) : (p + 1 == c.P ? 1 : p + 2);
+      const int t = id - 1;
+      if (t < 0 || t >= c.P || !TF(F_ALIVE, t)) return 0.0;
+      const int r = TF(F_ROW, p), col = TF(F_COL, p);
+      if (linf(r, col, TF(F_ROW, t), TF(F_COL, t)) > kVision) return 0.0;
+      const int dt = TF(F_DS_ROW, t);
+      int before = 0;
+      for (int s = 0; s < c.S; s++)
+        before += TF(F_ALIVE, s) && TF(F_DS_ROW, s) < dt && linf(r, col, TF(F_ROW, s), TF(F_COL, s)) <= kVision;
+      return before < kNObs ? 1.0 : 0.0;
     }
     case PRED_FULLY_ARMED: {
       if (q.a < 1 || q.a > 3 || !inv) return 0.0;
@@ -1984,6 +2009,7 @@ __device__ __forceinline__ void tick_body(const DevState& st, const int32_t* __r
                                           uint8_t* trunc, uint8_t* mask, int mode) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int e = blockIdx.x;
+  NMMO_STAMP_CLEAR();
   NMMO_STAMP(0);
   Ctx c = make_ctx(smem, st, e, kSys ? kSys : st.cfg.systems);
   // a step's Move / AttackStyle / AttackTarget heads of this thread's player (a valid row for

@@ -27,6 +27,25 @@ def _id(table, v):
     return v if isinstance(v, int) else table[v]
 
 
+# SPEC §12 teams (nmmo's TeamHelper for the agent-training game: every agent its own team, in id
+# order): the left team of agent i is agent i - 1 (1 -> PLAYER_N), the right one i + 1, and a
+# one-agent team's leader is that agent
+TEAM_TARGET = {"left_team_leader": -1, "right_team_leader": -2, "left_team": -1, "right_team": -2}
+
+
+def _target(eval_fn, v):
+    if eval_fn == "CanSeeAgent" and isinstance(v, int) and v > 0:
+        return v
+    if eval_fn == "CanSeeGroup" and isinstance(v, (list, tuple)) and len(v) == 1 and int(v[0]) > 0:
+        return int(v[0])
+    key = v if isinstance(v, str) else None
+    ok = key in TEAM_TARGET and key.endswith("_leader") == (eval_fn == "CanSeeAgent")
+    if not ok:
+        raise ValueError(f"{eval_fn}: target {v!r} (agent tasks: left/right team"
+                         f"{'_leader' if eval_fn == 'CanSeeAgent' else ''} or a player id)")
+    return TEAM_TARGET[key]
+
+
 def _one(kw):
     if kw.pop("num_agent", 1) != 1:
         raise ValueError("agent tasks only: num_agent must be 1 (team tasks are out of scope)")
@@ -69,6 +88,8 @@ def term(eval_fn: str, weight: float = 1.0, **kw) -> abi.NmmoTaskTerm:
         a, b = _id(SKILL, kw.pop("combat_style")), kw.pop("level")
     elif eval_fn == "PracticeEating":  # curriculum_tutorial.py:45-57 (no arguments)
         pass
+    elif eval_fn in ("CanSeeAgent", "CanSeeGroup"):  # manual_curriculum.py:157-162
+        a = _target(eval_fn, kw.pop("target"))
     else:
         raise ValueError(f"unsupported predicate {eval_fn!r}")
     if kw:
@@ -193,8 +214,9 @@ def heldout_curriculum() -> list:
 
 
 def manual_curriculum() -> list:
-    """curriculum_generation/manual_curriculum.py:53-314 (agent tasks; the four team tasks
-    CanSeeAgent/CanSeeGroup at :149-155 are out of scope), with their sampling weights."""
+    """curriculum_generation/manual_curriculum.py:53-314, every spec of the file in its order,
+    with their sampling weights (CanSeeAgent / CanSeeGroup at :157-162 target the neighbouring
+    teams, SPEC §12)."""
     event_goal = [1, 2, 3, 5, 7, 9, 12, 15, 20, 30, 50]
     infrequent, stay_alive = list(range(1, 10)), [50, 100, 150, 200, 300, 500, 700]
     level_goal, item_num = list(range(2, 10)), [1, 2, 3, 4, 5]
@@ -213,6 +235,8 @@ def manual_curriculum() -> list:
         c += [TaskSpec("PracticeSkillWithTool", {"skill": sk, "exp": e}, sampling_weight=50) for e in stay_alive]
     c += [TaskSpec("TickGE", {"num_tick": n}) for n in stay_alive]
     c += [TaskSpec("OccupyTile", {"row": 80, "col": 80})]
+    c += [TaskSpec("CanSeeAgent", {"target": t}) for t in ["left_team_leader", "right_team_leader"]]
+    c += [TaskSpec("CanSeeGroup", {"target": t}) for t in ["left_team", "right_team"]]
     c += [TaskSpec("ScoreHit", {"combat_style": st, "N": n}, sampling_weight=5)
           for st in COMBAT_SKILL for n in event_goal]
     for fn, w in [("HoardGold", 10), ("EarnGold", 10), ("SpendGold", 5), ("MakeProfit", 3)]:
@@ -240,4 +264,17 @@ def tutorial_curriculum() -> list:
          for ev in ["GO_FARTHEST", "EAT_FOOD", "DRINK_WATER", "SCORE_HIT", "HARVEST_ITEM", "LEVEL_UP"]]
     c.append(TaskSpec("PracticeEating", {}))
     c += [TaskSpec("PracticeInventoryManagement", {"space": sp, "num_tick": 500}) for sp in [2, 4, 8]]
+    return c
+
+
+def sample_eval_curriculum() -> list:
+    """The 24 sample evaluation tasks, neurips23_evaluation/sample_evaluation_task.py:12-52
+    (sample_eval_task_with_embedding.pkl holds their embeddings in this order)."""
+    c = [TaskSpec("TickGE", {"num_tick": 1024})]
+    c += [TaskSpec("CountEvent", {"event": ev, "N": 10})
+          for ev in ["EAT_FOOD", "DRINK_WATER", "SCORE_HIT", "PLAYER_KILL", "HARVEST_ITEM", "EQUIP_ITEM",
+                     "CONSUME_ITEM", "LEVEL_UP", "EARN_GOLD", "LIST_ITEM", "BUY_ITEM", "GIVE_ITEM",
+                     "DESTROY_ITEM", "GIVE_GOLD"]]
+    c += [TaskSpec("AttainSkill", {"skill": sk, "level": 10, "num_agent": 1}) for sk in COMBAT_SKILL + HARVEST_SKILL]
+    c += [TaskSpec("EarnGold", {"amount": 50})]
     return c

@@ -963,6 +963,22 @@ static double term_progress(Oracle* o, int e, int p, const NmmoTaskTerm* q, cons
           if (mat[(r + dr) * SIZE + c + dc] == q->a) return 1.0;
       return 0.0;
     }
+    case PRED_CAN_SEE_AGENT: case PRED_CAN_SEE_GROUP: {
+      /* SPEC §12: the target is in p's Entity obs after the tick (in the realm, L-inf <= 7,
+         among the first 100 visible by datastore row); singleton teams in id order */
+      const int P = o->P;
+      const int id = q->a > 0 ? q->a : q->a == -1 ? (p == 0 ? P : p) : (p + 1 == P ? 1 : p + 2);
+      const int t = id - 1;
+      if (t < 0 || t >= P || !FLD(T, F_ALIVE, t)) return 0.0;
+      const int r = FLD(T, F_ROW, p), c = FLD(T, F_COL, p);
+      if (linf(r, c, FLD(T, F_ROW, t), FLD(T, F_COL, t)) > VISION) return 0.0;
+      int before = 0;
+      for (int s = 0; s < S; s++)
+        if (FLD(T, F_ALIVE, s) && FLD(T, F_DS_ROW, s) < FLD(T, F_DS_ROW, t) &&
+            linf(r, c, FLD(T, F_ROW, s), FLD(T, F_COL, s)) <= VISION)
+          before++;
+      return before < 100 ? 1.0 : 0.0;
+    }
     case PRED_FULLY_ARMED: {
       if (q->a < 1 || q->a > 3) return 0.0;
       const int need[5] = {T_HAT, T_TOP, T_BOTTOM, T_SPEAR + q->a - 1, T_WHETSTONE + q->a - 1};

@@ -91,7 +91,7 @@ def test_event_and_predicate_enums_match_header():
     codes = dict((k.strip()[3:], int(v)) for k, v in (p.split("=") for p in ev.split(",")))
     assert codes == {k: v for k, v in vars(abi.EventCode).items() if k.isupper()}
     pr = re.search(r"enum NmmoPredicate \{(.*?)\};", text, re.S).group(1)
-    names = [p.strip().split("=")[0].strip() for p in pr.split(",")]
+    names = [p.strip().split("=")[0].strip() for p in re.sub(r"/\*.*?\*/", "", pr, flags=re.S).split(",")]
     names = [n for n in names if n.startswith("PRED_")]
     assert len(names) == len(abi.PREDICATES)
     camel = [n[5:].replace("_", "").lower() for n in names]

@@ -297,6 +297,8 @@ def _all_predicate_tasks():
         T.task("OccupyTile", row=80, col=80), T.task("CanSeeTile", tile_type="Fish"),
         T.task("FullyArmed", combat_style="Melee", level=1),
         T.practice_skill_with_tool("Fishing", 60), T.practice_inventory_management(4, 30),
+        T.task("CanSeeAgent", target="left_team_leader"), T.task("CanSeeGroup", target="right_team"),
+        T.task("CanSeeAgent", target=5),
     ]
 
 

@@ -102,7 +102,14 @@ def test_builder_rejects_team_tasks_and_unknown_predicates():
     with pytest.raises(ValueError):
         tasks.task("AttainSkill", skill="Melee", level=3, num_agent=2)
     with pytest.raises(ValueError):
-        tasks.task("CanSeeGroup", target="left_team")
+        tasks.task("CanSeeAgent", target="left_team")  # a team is a group, not an agent
+    with pytest.raises(ValueError):
+        tasks.task("CanSeeGroup", target="right_team_leader")
+    with pytest.raises(ValueError):
+        tasks.TaskSpec("TickGE", {"num_tick": 3}, reward_to="team")
+    g = tasks.task("CanSeeGroup", target="left_team").term[0]
+    assert (g.pred, g.a) == (abi.PRED["CanSeeGroup"], -1)
+    assert tasks.task("CanSeeAgent", target=7).term[0].a == 7
     t = tasks.task("HarvestItem", item="Whetstone", level=2, quantity=3)
     assert (t.term[0].pred, t.term[0].a, t.term[0].b, t.term[0].c) == (abi.PRED["HarvestItem"], 13, 2, 3)
 
@@ -157,6 +164,65 @@ def test_heldout_curriculum_matches_reference_names():
     assert progs[2].term[0].pred == abi.PRED["DefeatEntity"] and progs[2].term[0].c == 20
 
 
+def _visible(d, p, t):
+    """t is in p's Entity obs: in the realm and among the first 100 visible by datastore row."""
+    from tests.test_oracle import visible_index
+
+    if not d["ent"][0, F["alive"], t]:
+        return False
+    try:
+        return visible_index(d, p, t) < 100
+    except ValueError:
+        return False
+
+
+def test_can_see_neighbouring_team_known_answer():
+    """CanSeeAgent / CanSeeGroup (manual_curriculum.py:157-162) with SPEC §12's singleton teams
+    in id order: agent i's left team is agent i - 1 (agent 1's is agent P), its right team agent
+    i + 1 (agent P's is agent 1); progress 1 iff the target is in the agent's Entity obs after
+    the tick. Players 0 and 3 stand 3 tiles apart, the others elsewhere."""
+    from tests.test_oracle import plain
+
+    o, d = make(P=4)
+    mat = d["mat"][0]
+    r, c = find_tile(mat, plain)
+    r2, c2 = r + 3, c + 2
+    park_others(d, {0, 3}, mat)
+    place(d, 0, r, c)
+    place(d, 3, r2, c2)
+    put(o, d)
+    tl = [tasks.task("CanSeeAgent", target="left_team_leader"), tasks.task("CanSeeGroup", target="right_team"),
+          tasks.task("CanSeeAgent", target=1)]
+    assign = np.array([[0, 1, 2, 1]], np.int32)
+    o.set_tasks(tl, None, assign)
+    o.step(noop_actions(o))
+    d = split_state(o.get_state(), 1, o.S, o.P)
+    P = 4
+    target = {0: P - 1, 1: 2, 2: 0, 3: 0}  # slots: left of id 1 = id 4; right of id 2 = id 3; agent 1; right of id 4 = id 1
+    for p in range(P):
+        want = 1.0 if _visible(d, p, target[p]) else 0.0
+        assert float(o.rew[0, p]) == want, (p, want)
+    assert o.rew[0, 0] == 1.0 and o.rew[0, 3] == 1.0  # the pair that stands together
+
+
+def test_sample_eval_curriculum_matches_reference_specs():
+    """The 24 TaskSpecs of neurips23_evaluation/sample_evaluation_task.py:12-52 in the order and
+    with the arguments the reference's sample_eval_task_with_embedding.pkl holds them (read off
+    its opcode stream, tests/golden/make_task_fixtures.py), so its 24 embeddings attach in order."""
+    import json
+
+    d = np.load("tests/golden/task_embeddings.npz")
+    ref = json.loads(str(d["sample_specs"]))
+    specs = tasks.sample_eval_curriculum()
+    assert [[s.eval_fn, s.eval_fn_kwargs, s.sampling_weight] for s in specs] == ref
+    assert len(specs) == d["sample_emb"].shape[0] == 24
+    for s, e in zip(specs, d["sample_emb"]):
+        s.embedding = e
+        s.program()
+    held = json.loads(str(d["heldout_specs"]))
+    assert [[s.eval_fn, s.eval_fn_kwargs, s.sampling_weight] for s in tasks.heldout_curriculum()] == held
+
+
 def test_manual_and_tutorial_curricula_build():
     m = tasks.manual_curriculum()
     assert len(m) <= abi.MAX_TASKS
@@ -165,6 +231,12 @@ def test_manual_and_tutorial_curricula_build():
         s.program()
     names = [s.name for s in m]
     assert "Task_PracticeSkillWithTool_(skill:Fishing_exp:50)_reward_to:agent" in names
+    for t in ["left_team_leader", "right_team_leader"]:
+        assert f"Task_CanSeeAgent_(target:{t})_reward_to:agent" in names
+    for t in ["left_team", "right_team"]:
+        assert f"Task_CanSeeGroup_(target:{t})_reward_to:agent" in names
+    i = names.index("Task_OccupyTile_(row:80_col:80)_reward_to:agent")
+    assert names[i + 1].startswith("Task_CanSeeAgent") and names[i + 5].startswith("Task_ScoreHit")
     assert len(set(names)) == len(names)
 
 

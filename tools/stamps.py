@@ -1,8 +1,11 @@
 """Phase attribution of the tick kernel from in-kernel s_memtime stamps (diagnostic build).
 
-Usage (GPU box): python tools/stamps.py [C3] [envs] [warmup]
+Usage (GPU box): python tools/stamps.py [C2|C3|C4] [envs] [warmup]
 Builds nothing on the box: run `python -c "from nmmo_amd import build; build.build(stamps=True)"`
-here first (the .so travels with the snapshot). Prints median / p90 cycles per phase.
+here first (the .so travels with the snapshot). Prints median / p90 cycles per phase of the
+stepped (not reset) env-ticks. Thread 0 stamps after each phase; a launch clears its stamps
+first, so a phase its system set compiles out reads as absent (0 cycles), and phases without a
+block barrier before their stamp (respawn sub-phases) time wave 0 only.
 """
 
 import ctypes
@@ -20,8 +23,24 @@ from nmmo_amd import _native, abi  # noqa: E402
 from nmmo_amd.config import Config  # noqa: E402
 from nmmo_amd.engine import NmmoEngine  # noqa: E402
 
-PHASES = ["load", "rowslot", "decode+npc_decide", "update+harvest", "professions+items",
-          "attack rounds+loot", "move", "cull+compact", "respawn", "npc_spawn", "rewards", "store"]
+# stamp ids in execution order (tick.hip NMMO_STAMP) and the phase that ENDS at each
+STAMPS = [(0, None), (20, "state load"), (1, "prep: rowslot, positions, listings"),
+          (13, "visibility bitmap"), (12, "action decode"), (2, "npc decide + hunt BFS"),
+          (3, "update: resources, tile hash"), (15, "harvest: foilage, professions"),
+          (14, "harvest events; Use, Buy, Give, Destroy"), (4, "attack init"),
+          (5, "attack rounds, ammunition, loot"), (6, "move (+ Sell)"), (7, "cull, NPC compaction"),
+          (16, "respawn scan (wave 0)"), (18, "respawn list (wave 0)"), (19, "respawn draws, expiry (wave 0)"),
+          (8, "tick++ barrier"), (9, "npc spawn"), (10, "tasks, rewards, dones"), (11, "store")]
+
+
+def phases(st: np.ndarray) -> np.ndarray:
+    """st: [n, 32] raw stamps of stepped env-ticks -> [n, len(STAMPS)-1] cycles per phase
+    (absent stamps take the previous present one's time: 0 cycles)."""
+    ids = [k for k, _ in STAMPS]
+    t = st[:, ids].astype(np.int64)
+    for j in range(1, t.shape[1]):
+        t[:, j] = np.where(t[:, j] == 0, t[:, j - 1], t[:, j])
+    return np.diff(t, axis=1)
 
 
 def main():
@@ -37,46 +56,27 @@ def main():
         eng.end_episodes(np.arange(envs) % stagger == k)
         eng.scripted_actions(1_000_003)
         eng.step(write_obs=False)
-    totals = []
     L = _native.lib()
     L.nmmo_debug_read_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
-    rows, subs = [], []
+    rows, totals = [], []
     for t in range(warm + 10):
         eng.scripted_actions(1000 + t)
-        eng.step()
+        eng.step(write_obs=False)
         torch.cuda.synchronize()
         if t >= warm:
             buf = np.zeros(4096 * 32, np.uint64)
             assert L.nmmo_debug_read_stamps(buf.ctypes.data_as(ctypes.c_void_p), buf.size) == 0
-            st = buf.reshape(4096, 32)[:min(envs, 4096), :12].astype(np.int64)
-            fin = st[:, 11] > st[:, 0]
-            totals.append(np.stack([st[fin, 11] - st[fin, 0], (st[fin, 2] > 0).astype(np.int64)], 1))
-            ok = (st[:, 2] > 0) & (st[:, 11] > st[:, 0])  # stepped (not reset) envs
-            d = np.diff(st[ok], axis=1)
-            rows.append(d)
-            full = buf.reshape(4096, 32)[:min(envs, 4096)].astype(np.int64)[ok]
-            subs.append(np.stack([full[:, 12] - full[:, 1], full[:, 2] - full[:, 12],
-                                  full[:, 13] - full[:, 1], full[:, 15] - full[:, 3],
-                                  full[:, 14] - full[:, 15], full[:, 4] - full[:, 14],
-                                  full[:, 16] - full[:, 7], full[:, 17] - full[:, 16], full[:, 18] - full[:, 17],
-                                  full[:, 19] - full[:, 18], full[:, 8] - full[:, 19],
-                                  full[:, 20] - full[:, 0]], 1))
+            st = buf.reshape(4096, 32)[:min(envs, 4096)].astype(np.int64)
+            stepped = (st[:, 2] > 0) & (st[:, 11] > st[:, 0])  # the decode ran: not a reset
+            rows.append(phases(st[stepped]))
+            done = st[:, 11] > st[:, 0]
+            totals.append(np.stack([st[done, 11] - st[done, 0], stepped[done].astype(np.int64)], 1))
     d = np.concatenate(rows)
     tot = np.median(d.sum(1))
-    print(f"{preset} envs={envs}: median total {tot:.0f} cycles over {len(d)} env-ticks")
-    for i in range(11):
+    print(f"{preset} envs={envs}: median total {tot:.0f} cycles over {len(d)} stepped env-ticks")
+    for i, (_, name) in enumerate(STAMPS[1:]):
         med, p90 = np.median(d[:, i]), np.percentile(d[:, i], 90)
-        print(f"  {PHASES[i+1]:22s} median {med:9.0f}  p90 {p90:9.0f}  ({100*med/tot:5.1f}%)")
-    sub = np.concatenate(subs)
-    print(f"  of which player decode  median {np.median(sub[:, 0]):9.0f} (visibility bitmap "
-          f"{np.median(sub[:, 2]):9.0f}); npc decide median {np.median(sub[:, 1]):9.0f}")
-    print(f"  update+harvest = resource {np.median(d[:, 2]):9.0f} + professions "
-          f"{np.median(sub[:, 3]):9.0f}; item actions (Use..Destroy) {np.median(sub[:, 4]):9.0f}; "
-          f"attack init {np.median(sub[:, 5]):9.0f}")
-    print(f"  respawn = count {np.median(sub[:, 6]):9.0f} + prefix {np.median(sub[:, 7]):9.0f} + list "
-          f"{np.median(sub[:, 8]):9.0f} + draws {np.median(sub[:, 9]):9.0f} + expiry/tick {np.median(sub[:, 10]):9.0f}; "
-          f"groups n/a")
-    print(f"  rowslot phase: state load {np.median(sub[:, 11]):9.0f}")
+        print(f"  {name:42s} median {med:9.0f}  p90 {p90:9.0f}  ({100 * med / tot:5.1f}%)")
     tt = np.concatenate(totals)
     for name, sel in (("stepped", tt[:, 1] == 1), ("reset", tt[:, 1] == 0)):
         x = tt[sel, 0]
