@@ -115,24 +115,26 @@ def obs_bytes_per_env(S: int, P: int, elems: int, native: bool = False, wire_byt
     return rows + 33 * S * 2 + P * (225 + 12 * 8)
 
 
-def pmc_traffic(cfg_name: str, kernel: str, envs: int):
-    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary of the
-    same workload (profiles/<round>/<cfg>/pmc.json, tools/pmc_summary.py): 2 x FETCH_SIZE +
-    WRITE_SIZE, gfx950-corrected, scaled per env to a launch of `envs` envs (the summary's
-    launches covered its roofline.envs_per_launch, or its envs_per_gpu). None when no summary
-    matches this workload."""
+def pmc_traffic(cfg_name: str, kernel, envs: int):
+    """HBM bytes per launch of `kernel` (a name, or a list of kernels one launch runs: the wire
+    obs gather is wire_count + wire_scan + obs_kernel) from the newest committed rocprofv3 PMC
+    summary of the same workload (profiles/<round>/<cfg>/pmc.json, tools/pmc_summary.py):
+    2 x FETCH_SIZE + WRITE_SIZE, gfx950-corrected, scaled per env to a launch of `envs` envs (the
+    summary's launches covered its roofline.envs_per_launch, or its envs_per_gpu). None when no
+    summary matches this workload."""
     import glob
 
+    names = [kernel] if isinstance(kernel, str) else list(kernel)
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", cfg_name, "pmc.json")), reverse=True):
         try:
             d = json.load(open(path))
-            k = d["kernels"][kernel]
+            tot = sum(d["kernels"][k]["hbm_bytes_per_dispatch"] for k in names)
             b = d.get("bench", {})
             pe = b.get("roofline", {}).get("envs_per_launch") or b.get("config", {}).get("envs_per_gpu")
             if not pe:
                 continue
-            return round(k["hbm_bytes_per_dispatch"] * envs / pe), os.path.relpath(path, ROOT)
-        except (KeyError, ValueError, OSError):
+            return round(tot * envs / pe), os.path.relpath(path, ROOT)
+        except (KeyError, ValueError, OSError, TypeError):
             continue
     return None, None
 
@@ -495,9 +497,9 @@ def measure(args, name, layout_name, envs, rank, world, dev, steps, warmup, dist
     return res
 
 
-def _roofline(prof_name, kern, byts, ms, per, timing, nb, step_s, fill_gbs):
+def _roofline(prof_name, kern, byts, ms, per, timing, nb, step_s, fill_gbs, pmc_kernels=None):
     achieved = byts / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
-    traffic, traffic_src = pmc_traffic(prof_name, kern, per)
+    traffic, traffic_src = pmc_traffic(prof_name, pmc_kernels or kern, per)
     return {
         "kernel": kern, "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
@@ -594,7 +596,8 @@ def measure_gather(args, name, envs, rank, world, dev, steps, warmup, dist=None,
         "launch": f"hipGraph per step and ring slot, {nb} batches of {per} envs on {nb} streams, gather on a "
                   f"comm stream one step behind",
         "kernel_ms": {"policy": None, "tick": round(tick_avg_ms, 5), "obs": round(obs_avg_ms, 5), "wrapper": None},
-        "roofline": _roofline(name, kern, byts, ms, per, timing, nb, d["elapsed"] / steps, None),
+        "roofline": _roofline(name, kern, byts, ms, per, timing, nb, d["elapsed"] / steps, None,
+                              ["wire_count_kernel", "wire_scan_kernel", "obs_kernel"] if kern == "obs_kernel" else None),
         "batches": nb,
         "gather_bytes": d["payload_bytes_per_step"] if world > 1 else 0,
         "wire_bytes_per_agent_in_realm": round(wire_env_bytes * per * nb * steps / max(d["alive"], 1.0), 1),

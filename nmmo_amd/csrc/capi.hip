@@ -490,8 +490,9 @@ int nmmo_wire_pack(NmmoHandle* h, const void* native, void* wire, void* stream) 
   if (!h->native_fresh)
     return fail(NMMO_E_INVALID, "nmmo_wire_pack: a tick ran after the last obs gather without one (stale native obs)");
   HIP_TRY(hipSetDevice(h->device));
+  const int exch = (h->cfg.systems & NMMO_SYS_ITEM) && (h->cfg.systems & NMMO_SYS_EXCHANGE);
   HIP_TRY(launch_wire_pack(h->d_wcount, h->d_wmcount, (const uint8_t*)native, (uint8_t*)wire, h->st.n_envs, h->st.P,
-                           (hipStream_t)stream));
+                           h->d_ent, h->st.S, exch, (hipStream_t)stream));
   return NMMO_OK;
 }
 

@@ -120,7 +120,7 @@ hipError_t launch_obs(const ObsParams& p, hipStream_t stream);
 hipError_t launch_expand(const ObsParams& p, hipStream_t stream);  // native -> flat (SPEC §8b)
 // wire codec (wire.hip, SPEC §8c): native <-> compact transport records
 hipError_t launch_wire_pack(const uint16_t* counts, const int* mcount, const uint8_t* native, uint8_t* wire, int n,
-                            int P, hipStream_t s);
+                            int P, const int16_t* ent, int S, int exch, hipStream_t s);
 hipError_t launch_wire_unpack(const uint8_t* wire, uint8_t* native, int n, int P, hipStream_t s);
 // NMMO_OBS_WIRE: per-agent count words + per-env payload sizes (wire_count_kernel) and their
 // scan, ahead of obs_kernel's record writes (obs.hip launch_obs)

@@ -166,7 +166,8 @@ __device__ __forceinline__ void mask_sec_f32(const ObsParams& p, const int16_t* 
 
 // The same for a wire record (SPEC §8c): section kSec as bits of the wave's LDS bit image
 // (zeroed beforehand), one ballot per 64 entries OR-ed in at the section's bit offset (a
-// 64-bit ballot shifted by 0..31 spans 3 words: lanes 0-2 take one each).
+// 64-bit ballot shifted by 0..31 spans 3 words: lanes 0-2 take one each). Buy.MarketItem is not
+// part of a record (the decoders rebuild it from the listings, wire.h).
 template <int kSec, bool kWrap>
 __device__ __forceinline__ void mask_sec_bits(const ObsParams& p, const int16_t* T, int S, const int16_t* vis,
                                               const uint2* inv, const uint16_t* mpo, int nm, const MaskCtx& m,
@@ -178,7 +179,7 @@ __device__ __forceinline__ void mask_sec_bits(const ObsParams& p, const int16_t*
     const int k = k0 + lane;
     const uint64_t b = __ballot(k < n && mask_value<kWrap>(p, T, S, vis, inv, mpo, nm, m, kSec, k));
     if (b == 0ull) continue;
-    const int bit = lo + k0, sh = bit & 31;
+    const int bit = entry_wire_bit(lo + k0), sh = bit & 31;  // Buy.MarketItem is not sent (wire.h)
     const uint64_t lo64 = b << sh;
     const uint32_t part = lane == 0 ? (uint32_t)lo64 : lane == 1 ? (uint32_t)(lo64 >> 32)
                                                                  : (sh ? (uint32_t)(b >> (64 - sh)) : 0u);
@@ -460,7 +461,6 @@ __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
       if (alive(j + 1)) prefetch(a + kObsWaves, j + 1);  // wm is in LDS now; next agent's loads
       mask_sec_bits<0, kWrap>(p, T, S, vis, inv, mpo, nm, m, bw);
       mask_sec_bits<1, kWrap>(p, T, S, vis, inv, mpo, nm, m, bw);
-      mask_sec_bits<2, kWrap>(p, T, S, vis, inv, mpo, nm, m, bw);
       mask_sec_bits<3, kWrap>(p, T, S, vis, inv, mpo, nm, m, bw);
       mask_sec_bits<4, kWrap>(p, T, S, vis, inv, mpo, nm, m, bw);
       mask_sec_bits<5, kWrap>(p, T, S, vis, inv, mpo, nm, m, bw);
@@ -483,7 +483,7 @@ __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
       } else if (lane == kWireMask / 16) {
         *reinterpret_cast<uint4*>(rec) =
             make_uint4(i16pack(aid, tick), i16pack(__builtin_amdgcn_readlane(my_task, j), m.r - kVision),
-                       i16pack(m.c - kVision, nv), (uint32_t)ninv);
+                       i16pack(m.c - kVision, nv), i16pack(ninv | (m.exch ? 1 << 8 : 0), m.gold));
       }
       // body: nv Entity rows | ninv Inventory rows | 225 materials | pad, as int16 half-words
       // (a material half-word holds two of them), 8 per lane per 16-B store
@@ -499,9 +499,10 @@ __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
         } else if (o < ib) {
           const int i = (o - eb) >> 1;
           x = (int)item_col(inv[i >> 4], aid, i & 15);
-        } else {
-          const int t = o - ib;
-          x = (t < kWireTiles ? (int)wmat[t] : 0) | (t + 1 < kWireTiles ? (int)wmat[t + 1] << 8 : 0);
+        } else {  // tile bytes u, u + 1: materials 2u .. 2u + 3, 4 bits each
+          const int u = o - ib, t = 2 * u;
+          auto m4 = [&](int q) { return q < 225 ? (int)wmat[q] & 15 : 0; };
+          x = u < kWireTiles ? m4(t) | m4(t + 1) << 4 | (u + 1 < kWireTiles ? m4(t + 2) << 8 | m4(t + 3) << 12 : 0) : 0;
         }
         return (uint32_t)(uint16_t)x;
       };

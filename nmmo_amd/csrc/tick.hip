@@ -473,6 +473,23 @@ __device__ __forceinline__ bool receive_moved(Ctx& c, int p, uint2 w) {
   inv_insert(inv, w);
   return true;
 }
+// receive_moved without touching the item FIFO: a row stacking frees is returned in `freed`
+// (-1 if none) for the caller to append in serial order
+__device__ __forceinline__ bool receive_moved_deferred(Ctx& c, int p, uint2 w, int& freed) {
+  uint2* inv = c.inv + p * kInv;
+  const int k = inv_stack(inv, it_type(w), it_level(w));
+  if (k >= 0) {
+    inv[k].y += (uint32_t)it_qty(w);
+    freed = it_row(w);
+    return false;
+  }
+  if (inv_count(inv) >= kInv) {
+    freed = it_row(w);
+    return false;
+  }
+  inv_insert(inv, w);
+  return true;
+}
 __device__ __forceinline__ bool has_room(const Ctx& c, int p, uint2 w) {
   const uint2* inv = c.inv + p * kInv;
   return inv_stack(inv, it_type(w), it_level(w)) >= 0 || inv_count(inv) < kInv;
@@ -1549,50 +1566,106 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
     ring_append_ordered(c, freed);
     if (evon) ev_append(c, evn, u_code ? 1 : 0, [&](int i) { ev_put(c, i, s, u_code, u_type, u_lvl, u_num, 0, 0); });
 
-    // Buy (priority 20): buyers in shuffled order (key draw(tick, BUY_ORDER, id), ties by id),
-    // replayed by thread 0 against the row -> owner map of the tick-start listings
+    // Buy (priority 20): buyers in shuffled order (key draw(tick, BUY_ORDER, id), ties by id).
+    // A buy touches two players -- its buyer (gold, inventory room) and the listing's owner at
+    // tick start (gold, inventory); a later buy of a row an earlier buy took finds it unlisted in
+    // the new owner's inventory and fails, and both buys share that first owner -- so buys run
+    // in rounds like the attacks: each round executes every remaining buy that is the earliest
+    // (in shuffled order) remaining buy of both its players, all in parallel, which is the
+    // serial result. The events (BUY_ITEM + EARN_GOLD per success) and the rows freed by
+    // stacking go to the event log and the item FIFO in shuffled order: ranks by popcounts of
+    // per-position bit masks.
     if (c.exch) {
       const bool isb = s < P && c.a_buy[s] >= 0;
       int nbuy;
       block_prefix_count(isb, wtot_next(c), &nbuy);
       if (nbuy > 0) {
+        int* mi = c.ft;                                            // attack init zeroes it again
+        uint32_t* okm = reinterpret_cast<uint32_t*>(c.wtot + 20);  // [4] succeeded, by position
+        uint32_t* frm = reinterpret_cast<uint32_t*>(c.wtot + 24);  // [4] freed a row, by position
+        int16_t* frow = c.order;                                   // [128] that row, by position
+        int* anyf = c.wtot + 16;
         if (isb) c.ikey[s] = draw(seed, (uint32_t)tick, P_BUY_ORDER, (uint32_t)(s + 1), 0).x;
+        if (tid < P) mi[tid] = 0;
+        if (tid < 8) okm[tid] = 0u;  // okm and frm
+        if (tid < 3) anyf[tid] = 0;
         __syncthreads();
+        int pos = 0, owner0 = -1;
+        const int brow = isb ? c.a_buy[s] : -1;
         if (isb) {
           const uint32_t key = c.ikey[s];
-          int rank = 0;
           for (int q = 0; q < P; q++)
-            if (c.a_buy[q] >= 0) rank += (c.ikey[q] < key || (c.ikey[q] == key && q < s)) ? 1 : 0;
-          c.order[rank] = (int16_t)s;
+            if (c.a_buy[q] >= 0) pos += (c.ikey[q] < key || (c.ikey[q] == key && q < s)) ? 1 : 0;
+          owner0 = c.rmap[brow] & 255;  // a listed row at tick start (kth_listed)
         }
+        bool active = isb && acts(c, s) && owner0 != s;  // the others fail without effect
+        bool ok = false;
+        uint2 bw = make_uint2(0u, 0u);
+        int bprice = 0, bowner = -1;
+        for (int round = 1;; round++) {
+          const int key = (round << 16) | (0xFFFF - pos);
+          if (active) {
+            atomicMax(&mi[s], key);
+            atomicMax(&mi[owner0], key);
+            anyf[round % 3] = 1;
+          }
+          if (tid == 0) anyf[(round + 1) % 3] = 0;
+          __syncthreads();
+          if (!anyf[round % 3]) break;
+          if (active && mi[s] == key && mi[owner0] == key) {
+            active = false;
+            const int owner = c.rmap[brow] < 0 ? -1 : (c.rmap[brow] & 255);
+            uint2* oinv = c.inv + (owner >= 0 ? owner : 0) * kInv;
+            const int k = owner >= 0 && owner != s ? inv_find(oinv, brow) : -1;
+            if (k >= 0) {
+              uint2 w = oinv[k];
+              const int price = it_price(w);
+              if (price && TF(F_GOLD, s) >= price && has_room(c, s, w)) {
+                TF(F_GOLD, s) = (int16_t)(TF(F_GOLD, s) - price);
+                TF(F_GOLD, owner) = (int16_t)(TF(F_GOLD, owner) + price);
+                bw = w;
+                bprice = price;
+                bowner = owner;
+                ok = true;
+                w.x &= 0x1FFu;
+                inv_remove(oinv, k);
+                int freed = -1;
+                c.rmap[brow] = receive_moved_deferred(c, s, w, freed) ? (int16_t)s : (int16_t)-1;
+                atomicOr(&okm[pos >> 5], 1u << (pos & 31));
+                if (freed >= 0) {
+                  frow[pos] = (int16_t)freed;
+                  atomicOr(&frm[pos >> 5], 1u << (pos & 31));
+                }
+              }
+            }
+          }
+        }
+        // (the loop's last barrier published okm / frm / frow)
+        auto below = [&](const uint32_t* m) {
+          int n = 0;
+#pragma unroll
+          for (int i = 0; i < 4; i++)
+            n += i < (pos >> 5) ? __popc(m[i]) : i == (pos >> 5) ? __popc(m[i] & ((1u << (pos & 31)) - 1u)) : 0;
+          return n;
+        };
+        const int nok = __popc(okm[0]) + __popc(okm[1]) + __popc(okm[2]) + __popc(okm[3]);
+        const int nfr = __popc(frm[0]) + __popc(frm[1]) + __popc(frm[2]) + __popc(frm[3]);
+        if (ok) {
+          const int i = evn + 2 * below(okm);
+          if (evon) {
+            ev_put(c, i, s, EV_BUY_ITEM, it_type(bw), it_level(bw), it_qty(bw), bprice, 0);
+            ev_put(c, i + 1, bowner, EV_EARN_GOLD, 0, 0, 0, bprice, 0);
+          }
+        }
+        if (isb && ((frm[pos >> 5] >> (pos & 31)) & 1u))
+          c.iring[(c.E[E_ITEM_FREE_HEAD] + c.E[E_ITEM_FREE_COUNT] + below(frm)) % c.IC] = frow[pos];
+        if (evon) evn += 2 * nok;
         __syncthreads();
         if (tid == 0) {
-          for (int i = 0; i < nbuy; i++) {
-            const int b = c.order[i];
-            if (!acts(c, b)) continue;
-            const int row = c.a_buy[b];
-            const int owner = c.rmap[row] < 0 ? -1 : (c.rmap[row] & 255);
-            if (owner < 0 || owner == b) continue;
-            uint2* oinv = c.inv + owner * kInv;
-            const int k = inv_find(oinv, row);
-            if (k < 0) continue;
-            uint2 w = oinv[k];
-            const int price = it_price(w);
-            if (!price || TF(F_GOLD, b) < price || !has_room(c, b, w)) continue;
-            TF(F_GOLD, b) = (int16_t)(TF(F_GOLD, b) - price);
-            TF(F_GOLD, owner) = (int16_t)(TF(F_GOLD, owner) + price);
-            if (evon) {
-              ev_put(c, evn++, b, EV_BUY_ITEM, it_type(w), it_level(w), it_qty(w), price, 0);
-              ev_put(c, evn++, owner, EV_EARN_GOLD, 0, 0, 0, price, 0);
-            }
-            w.x &= 0x1FFu;
-            inv_remove(oinv, k);
-            c.rmap[row] = receive_moved(c, b, w) ? (int16_t)b : (int16_t)-1;
-          }
+          c.E[E_ITEM_FREE_COUNT] += nfr;
           c.E[E_EVENT_COUNT] = evn;
         }
         __syncthreads();
-        evn = c.E[E_EVENT_COUNT];
       }
     }
 

@@ -5,8 +5,9 @@
 // The native layout (SPEC §8b: 9,552 B per agent + 32 KB per env) is what the learner reads, but
 // most of its bytes are padding a transfer can drop: Entity rows past the visible ones, empty
 // inventory slots, Market rows past the listings, one byte per ActionTargets bit, and the Tile
-// rows/columns that follow from the window's corner. ~1.3 KB per agent in C4 steady state
-// instead of 9,552 B.
+// rows/columns that follow from the window's corner, the Buy.MarketItem mask (a function of the
+// listings, the agent's gold and id) and the high nibble of every material: ~0.55 KB per agent
+// in the realm in C4 steady state instead of 9,552 B.
 //
 // Kernels:
 //   wire_size / wire_scan / wire_pack   native -> wire (nmmo_wire_pack; counts from the native
@@ -127,7 +128,8 @@ __global__ void __launch_bounds__(1024) wire_scan_kernel(uint8_t* wire, int n, i
 
 constexpr int kWireAgentsPerBlock = 16;
 
-__global__ void __launch_bounds__(256) wire_pack_kernel(const uint8_t* native, uint8_t* wire, int n, int P) {
+__global__ void __launch_bounds__(256) wire_pack_kernel(const uint8_t* native, uint8_t* wire, int n, int P,
+                                                        const int16_t* ent, int S, int exch) {
   WireView v = wire_view(wire, n, P);
   __shared__ int off[129];
   const int e = blockIdx.x, g = blockIdx.y, lane = lane_id(), w = wave_id();
@@ -152,20 +154,18 @@ __global__ void __launch_bounds__(256) wire_pack_kernel(const uint8_t* native, u
     const int16_t* i16 = reinterpret_cast<const int16_t*>(row + NMMO_NATIVE_MASK_BYTES);
     uint8_t* rec = penv + off[a];
     if (lane == 0) {
+      const int gold = ent[((size_t)e * NMMO_NF + F_GOLD) * S + a];  // the state the obs was taken from
       const uint4 head = make_uint4((uint32_t)(uint16_t)i16[0] | (uint32_t)(uint16_t)i16[1] << 16,
                                     (uint32_t)(uint16_t)i16[kNatI16Task] | (uint32_t)(uint16_t)i16[kNatI16Tile] << 16,
                                     (uint32_t)(uint16_t)i16[kNatI16Tile + 1] | (uint32_t)nv << 16,
-                                    (uint32_t)ninv);
+                                    (uint32_t)ninv | (uint32_t)(exch ? 1 : 0) << 8 | (uint32_t)(uint16_t)gold << 16);
       *reinterpret_cast<uint4*>(rec) = head;
     }
-    if (lane < kWireMask / 4) {  // 32 mask bytes -> one word of bits (bytes past 1,586 are 0)
+    if (lane < kWireMask / 4) {  // 32 of the non-Buy mask entries -> one word of bits
       uint32_t bits = 0u;
-      if (lane < NMMO_NATIVE_MASK_BYTES / 32) {
-        const uint4 q0 = reinterpret_cast<const uint4*>(row)[2 * lane];
-        const uint4 q1 = reinterpret_cast<const uint4*>(row)[2 * lane + 1];
-        const uint32_t wd[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
-#pragma unroll
-        for (int k = 0; k < 32; k++) bits |= (((wd[k >> 2] >> (8 * (k & 3))) & 255u) != 0u ? 1u : 0u) << k;
+      for (int k = 0; k < 32; k++) {
+        const int b = 32 * lane + k;
+        if (b < kWireMaskBits && row[wire_bit_entry(b)]) bits |= 1u << k;
       }
       reinterpret_cast<uint32_t*>(rec + kWireHead)[lane] = bits;
     }
@@ -175,7 +175,8 @@ __global__ void __launch_bounds__(256) wire_pack_kernel(const uint8_t* native, u
     for (int k = lane; k < ninv * 16; k += 64) d16[k] = i16[kNatI16Inv + k];
     uint8_t* mat = reinterpret_cast<uint8_t*>(d16 + ninv * 16);
     const int pad = wire_record_bytes(c) - (kWireBody + 62 * nv + 32 * ninv);
-    for (int t = lane; t < pad; t += 64) mat[t] = t < kWireTiles ? (uint8_t)i16[kNatI16Tile + 3 * t + 2] : 0;
+    auto tile = [&](int t) { return t < 225 ? (int)i16[kNatI16Tile + 3 * t + 2] & 15 : 0; };
+    for (int u = lane; u < pad; u += 64) mat[u] = u < kWireTiles ? (uint8_t)(tile(2 * u) | tile(2 * u + 1) << 4) : 0;
   }
 }
 
@@ -204,10 +205,12 @@ __device__ __forceinline__ void record_release() {
 }
 
 // wire -> native: every byte of the native buffer is written. Each wave first copies its
-// agent's record into LDS, then writes the 9,552-B row with 16-B stores computed from LDS.
+// agent's record into LDS, then writes the 9,552-B row with 16-B stores computed from LDS; the
+// Buy.MarketItem bytes come from the env's listings (price | owner, staged once per block).
 __global__ void __launch_bounds__(256) wire_unpack_kernel(const uint8_t* wire, uint8_t* native, int n, int P) {
   WireView v = wire_view(const_cast<uint8_t*>(wire), n, P);
   __shared__ int off[129];
+  __shared__ uint32_t lpo[NMMO_MARKET_ROWS];
   __shared__ uint4 recbuf[4][kRecMaxU4];
   const int e = blockIdx.x, g = blockIdx.y, lane = lane_id(), w = wave_id();
   const uint16_t* cnt = v.cnt + (size_t)e * P;
@@ -215,13 +218,19 @@ __global__ void __launch_bounds__(256) wire_unpack_kernel(const uint8_t* wire, u
   __syncthreads();
   uint8_t* nenv = native + (size_t)e * wire_native_env_bytes(P);
   const uint8_t* penv = v.base + v.env_off[e];
+  const int nm = v.mcount[e];
+  {
+    const int16_t* lst = reinterpret_cast<const int16_t*>(penv + off[P]);
+    for (int k = threadIdx.x; k < nm; k += blockDim.x)
+      lpo[k] = (uint32_t)(uint16_t)lst[16 * k + 15] | (uint32_t)(uint16_t)lst[16 * k + 2] << 16;
+  }
   if (g == 0) {
-    const int nm = v.mcount[e];
     const uint4* src = reinterpret_cast<const uint4*>(penv + off[P]);
     uint4* dst = reinterpret_cast<uint4*>(nenv + (size_t)P * NMMO_NATIVE_ROW_BYTES);
     for (int k = threadIdx.x; k < NMMO_NATIVE_MARKET_BYTES / 16; k += blockDim.x)
       dst[k] = k < 2 * nm ? src[k] : make_uint4(0u, 0u, 0u, 0u);
   }
+  __syncthreads();
   uint4* lrec = recbuf[w];
   const uint8_t* lb = reinterpret_cast<const uint8_t*>(lrec);
   for (int i = w; i < kWireAgentsPerBlock; i += 4) {
@@ -236,17 +245,23 @@ __global__ void __launch_bounds__(256) wire_unpack_kernel(const uint8_t* wire, u
     const int nv = c & 127, ninv = (c >> 7) & 15;
     record_to_lds(penv + off[a], wire_record_bytes(c) / 16, lrec);
     const int16_t* h16 = reinterpret_cast<const int16_t*>(lb);
+    const uint32_t* bits = reinterpret_cast<const uint32_t*>(lb + kWireHead);
     const int16_t* s16 = reinterpret_cast<const int16_t*>(lb + kWireBody);
     const uint8_t* mat = lb + kWireBody + 62 * nv + 32 * ninv;
     const int r0 = h16[3], c0 = h16[4], task = h16[2];
     // mask bytes, 16 per lane (1,600 bytes = 100 stores)
     for (int k = lane; k < NMMO_NATIVE_MASK_BYTES / 16; k += 64) {
-      const uint32_t bits = (reinterpret_cast<const uint32_t*>(lb + kWireHead)[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
       uint32_t q[4];
 #pragma unroll
-      for (int j = 0; j < 4; j++)
-        q[j] = ((bits >> (4 * j)) & 1u) | ((bits >> (4 * j + 1)) & 1u) << 8 | ((bits >> (4 * j + 2)) & 1u) << 16 |
-               ((bits >> (4 * j + 3)) & 1u) << 24;
+      for (int j = 0; j < 4; j++) {
+        uint32_t wd = 0u;
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+          const int x = 16 * k + 4 * j + b;
+          wd |= (x < kMaskN && wire_mask_entry(x, bits, nm, lpo, h16) ? 1u : 0u) << (8 * b);
+        }
+        q[j] = wd;
+      }
       row4[k] = make_uint4(q[0], q[1], q[2], q[3]);
     }
     auto val = [&](int k) -> uint32_t {
@@ -261,7 +276,7 @@ __global__ void __launch_bounds__(256) wire_unpack_kernel(const uint8_t* wire, u
         x = j < ninv * 16 ? s16[nv * NMMO_N_ENTITY_COLS + j] : 0;
       } else if (k < kNatI16Task) {
         const int j = k - kNatI16Tile, t = j / 3, comp = j - 3 * t;
-        x = comp == 0 ? r0 + t / 15 : comp == 1 ? c0 + t % 15 : (int)mat[t];
+        x = comp == 0 ? r0 + t / 15 : comp == 1 ? c0 + t % 15 : wire_tile(mat, t);
       } else {
         x = k == kNatI16Task ? task : 0;
       }
@@ -309,7 +324,7 @@ __global__ void __launch_bounds__(128) wire_check_kernel(const uint8_t* wire, in
         bad |= 4;
       } else if (base + off[a] + kWireHead <= total) {
         const int16_t* h = reinterpret_cast<const int16_t*>(v.base + base + off[a]);
-        if (h[0] <= 0 || h[5] != nv || h[6] != ninv) bad |= 8;
+        if (h[0] <= 0 || h[5] != nv || (h[6] & 0xFF) != ninv || ((uint16_t)h[6] >> 8) > 1) bad |= 8;
       } else {
         bad |= 2;
       }
@@ -335,8 +350,8 @@ __global__ void __launch_bounds__(256) wire_expand_kernel(ObsParams p) {
   record_offsets_wave0(cnt, P, off);
   __syncthreads();
   const uint8_t* penv = v.base + v.env_off[e];
+  const int nm = v.mcount[e];
   {
-    const int nm = v.mcount[e];
     const uint4* src = reinterpret_cast<const uint4*>(penv + off[P]);
     uint4* dst = reinterpret_cast<uint4*>(mk);
     for (int k = tid; k < NMMO_MARKET_ROWS * 2; k += blockDim.x) dst[k] = k < 2 * nm ? src[k] : make_uint4(0u, 0u, 0u, 0u);
@@ -361,7 +376,19 @@ __global__ void __launch_bounds__(256) wire_expand_kernel(ObsParams p) {
     const uint32_t* bits = reinterpret_cast<const uint32_t*>(lb + kWireHead);
     const int16_t* s16 = reinterpret_cast<const int16_t*>(lb + kWireBody);
     const uint8_t* mat = lb + kWireBody + 62 * nv + 32 * ninv;
-    for (int j = lane; j < p.o_agent_id; j += 64) row[j] = (float)((bits[j >> 5] >> (j & 31)) & 1u);
+    const bool exch = ((uint16_t)h16[6] >> 8) != 0;
+    const int gold = h16[7], aid = h16[0];
+    for (int j = lane; j < p.o_agent_id; j += 64) {
+      bool m;
+      if (j >= kWireBuyLo && j < kWireBuyLo + kWireBuyN) {  // Buy.MarketItem from the staged listings
+        const int k = j - kWireBuyLo;
+        m = k == NMMO_MARKET_ROWS || (exch && k < nm && mk[16 * k + 15] <= gold && mk[16 * k + 2] != aid);
+      } else {
+        const int b = entry_wire_bit(j);
+        m = (bits[b >> 5] >> (b & 31)) & 1u;
+      }
+      row[j] = m ? 1.f : 0.f;
+    }
     if (lane == 0) row[p.o_agent_id] = (float)h16[0];
     if (lane == 1) row[p.o_tick] = (float)h16[1];
     for (int j = lane; j < kNObs * NMMO_N_ENTITY_COLS; j += 64)
@@ -374,19 +401,19 @@ __global__ void __launch_bounds__(256) wire_expand_kernel(ObsParams p) {
     const int r0 = h16[3], c0 = h16[4];
     for (int j = lane; j < 225 * 3; j += 64) {
       const int t = j / 3, comp = j - 3 * t;
-      row[p.o_tile + j] = comp == 0 ? (float)(r0 + t / 15) : comp == 1 ? (float)(c0 + t % 15) : (float)mat[t];
+      row[p.o_tile + j] = comp == 0 ? (float)(r0 + t / 15) : comp == 1 ? (float)(c0 + t % 15) : (float)wire_tile(mat, t);
     }
     record_release();
   }
 }
 
 hipError_t launch_wire_pack(const uint16_t* counts, const int* mcount, const uint8_t* native, uint8_t* wire, int n,
-                            int P, hipStream_t s) {
+                            int P, const int16_t* ent, int S, int exch, hipStream_t s) {
   if (P > 128 || n <= 0) return hipErrorInvalidValue;
   hipLaunchKernelGGL(wire_size_kernel, dim3(n), dim3(128), 0, s, counts, mcount, wire, n, P);
   hipLaunchKernelGGL(wire_scan_kernel, dim3(1), dim3(1024), 0, s, wire, n, P);
   hipLaunchKernelGGL(wire_pack_kernel, dim3(n, (P + kWireAgentsPerBlock - 1) / kWireAgentsPerBlock), dim3(256), 0, s,
-                     native, wire, n, P);
+                     native, wire, n, P, ent, S, exch);
   return hipGetLastError();
 }
 

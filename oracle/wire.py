@@ -3,7 +3,9 @@
 Checker for nmmo_amd/csrc/wire.hip. It derives every count from the native bytes themselves
 (an agent is in the realm iff its AgentId is non-zero; nv = Entity rows with a non-zero id;
 ninv = Inventory rows with a non-zero item row; listings = Market rows with a non-zero item
-row), where the HIP path takes them from the obs kernel. Never imported by the product path.
+row), where the HIP path takes them from the obs kernel. The record head carries the agent's
+gold and the Exchange flag (state, not native bytes: the caller passes them); Buy.MarketItem is
+not sent and unpack rebuilds it from the listings. Never imported by the product path.
 """
 
 from __future__ import annotations
@@ -12,7 +14,9 @@ import numpy as np
 
 from nmmo_amd import abi
 
-HEAD, MASK, TILES = 16, 208, 225
+HEAD, MASK, TILES = 16, 80, 113        # the mask without Buy.MarketItem; 4-bit materials
+BUY_LO, BUY_N, MASK_N = 104, 1025, 1586
+SENT = np.r_[0:BUY_LO, BUY_LO + BUY_N:MASK_N]  # flat mask entries a record carries, in bit order
 I16_ENTITY, NE = 2, 31
 I16_INV = I16_ENTITY + 100 * NE
 I16_TILE = I16_INV + 12 * 16
@@ -50,8 +54,14 @@ def counts(native: np.ndarray, P: int):
     return cnt, nm
 
 
-def pack(native: np.ndarray, P: int) -> np.ndarray:
-    """native uint8 [n, env_bytes] -> wire uint8 [total]."""
+def listing_offset(cnt_env) -> int:
+    """Offset of an env's listings in its payload: the sum of its records."""
+    return sum(record_bytes(int(c)) for c in cnt_env)
+
+
+def pack(native: np.ndarray, P: int, gold: np.ndarray, exch: bool = True) -> np.ndarray:
+    """native uint8 [n, env_bytes] -> wire uint8 [total]; gold int [n, P] = each agent's gold in
+    the state the obs was taken from."""
     n = native.shape[0]
     rows, i16, market = _rows(native, P)
     cnt, nm = counts(native, P)
@@ -73,17 +83,20 @@ def pack(native: np.ndarray, P: int) -> np.ndarray:
                 continue
             nv, ninv = c & 127, (c >> 7) & 15
             q = i16[e, a]
-            head = np.array([q[0], q[1], q[I16_TASK], q[I16_TILE], q[I16_TILE + 1], nv, ninv, 0], np.int16)
+            head = np.array([q[0], q[1], q[I16_TASK], q[I16_TILE], q[I16_TILE + 1], nv, ninv | (int(exch) << 8),
+                             gold[e, a]], np.int16)
             rec = np.zeros(record_bytes(c), np.uint8)
             rec[:HEAD] = head.view(np.uint8)
-            bits = np.packbits(rows[e, a, :abi.NATIVE_MASK_BYTES] != 0, bitorder="little")
+            bits = np.packbits(rows[e, a, SENT] != 0, bitorder="little")
             rec[HEAD:HEAD + len(bits)] = bits
             k = HEAD + MASK
             rec[k:k + 62 * nv] = q[I16_ENTITY:I16_ENTITY + NE * nv].view(np.uint8)
             k += 62 * nv
             rec[k:k + 32 * ninv] = q[I16_INV:I16_INV + 16 * ninv].view(np.uint8)
             k += 32 * ninv
-            rec[k:k + TILES] = q[I16_TILE + 2:I16_TASK:3].astype(np.uint8)
+            mats = np.zeros(2 * TILES, np.uint8)
+            mats[:225] = q[I16_TILE + 2:I16_TASK:3].astype(np.uint8) & 15
+            rec[k:k + TILES] = mats[0::2] | (mats[1::2] << 4)
             out[pos:pos + len(rec)] = rec
             pos += len(rec)
         out[pos:pos + 32 * int(nm[e])] = market[e, :int(nm[e])].reshape(-1).view(np.uint8)
@@ -108,7 +121,16 @@ def unpack(wire: np.ndarray, n: int, P: int) -> np.ndarray:
             pos += len(rec)
             head = rec[:HEAD].copy().view(np.int16)
             row = out[e, a * abi.NATIVE_ROW_BYTES:(a + 1) * abi.NATIVE_ROW_BYTES]
-            row[:abi.NATIVE_MASK_BYTES] = np.unpackbits(rec[HEAD:HEAD + MASK], bitorder="little")[:abi.NATIVE_MASK_BYTES]
+            row[SENT] = np.unpackbits(rec[HEAD:HEAD + MASK], bitorder="little")[:len(SENT)]
+            # Buy.MarketItem: listing k < nm is buyable iff Exchange, price <= gold, owner != self
+            buy = np.zeros(BUY_N, np.uint8)
+            buy[BUY_N - 1] = 1
+            nmk = int(nm[e])
+            if nmk and (int(head[6]) >> 8) & 1:
+                lo = int(env_off[e]) + listing_offset(cnt[e])
+                lst = wire[lo:lo + 32 * nmk].copy().view(np.int16).reshape(nmk, 16)
+                buy[:nmk] = (lst[:, 15] <= head[7]) & (lst[:, 2] != head[0])
+            row[BUY_LO:BUY_LO + BUY_N] = buy
             q = np.zeros(abi.NATIVE_I16, np.int16)
             q[0], q[1] = head[0], head[1]
             k = HEAD + MASK
@@ -119,7 +141,8 @@ def unpack(wire: np.ndarray, n: int, P: int) -> np.ndarray:
             t = np.arange(225)
             q[I16_TILE:I16_TASK:3] = head[3] + t // 15
             q[I16_TILE + 1:I16_TASK:3] = head[4] + t % 15
-            q[I16_TILE + 2:I16_TASK:3] = rec[k:k + TILES]
+            mats = np.stack([rec[k:k + TILES] & 15, rec[k:k + TILES] >> 4], 1).reshape(-1)[:225]
+            q[I16_TILE + 2:I16_TASK:3] = mats
             q[I16_TASK] = head[2]
             row[abi.NATIVE_MASK_BYTES:] = q.view(np.uint8)
         mk = out[e, P * abi.NATIVE_ROW_BYTES:]

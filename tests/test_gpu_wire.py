@@ -1,7 +1,8 @@
 """Wire codec (SPEC.md §8c, csrc/wire.hip) on MI355X: nmmo_wire_pack's bytes equal the numpy
 restatement's (oracle/wire.py, which derives every count from the native bytes) and
-nmmo_wire_unpack restores the native obs bit-exactly, small and at C4 size (1,024 envs,
-staggered episodes)."""
+nmmo_wire_unpack restores the native obs bit-exactly (Buy.MarketItem rebuilt from the
+listings), small and at C4 size (1,024 envs, staggered episodes); the NMMO_OBS_WIRE layout writes
+the same bytes straight from the state; the experience store decodes kept rows from it."""
 
 import numpy as np
 import pytest
@@ -22,8 +23,9 @@ def _engine(n, seed, map_n=4):
 
 
 def test_wire_pack_matches_restatement():
-    from nmmo_amd import wire
+    from nmmo_amd import abi, wire
     from oracle import wire as owire
+    from oracle.oracle import split_state
 
     eng = _engine(3, seed=21)
     eng.reset()
@@ -37,7 +39,8 @@ def test_wire_pack_matches_restatement():
         w = wire.pack(eng)
         total = wire.total_bytes(w)
         nat = eng.obs.cpu().numpy()
-        ref = owire.pack(nat, eng.P)
+        gold = split_state(eng.get_state(), eng.n_envs, eng.S, eng.P)["ent"][:, abi.F["gold"], :eng.P]
+        ref = owire.pack(nat, eng.P, gold)
         assert total == ref.nbytes, (t, total, ref.nbytes)
         assert np.array_equal(w[:total].cpu().numpy(), ref), f"wire bytes differ at tick {t}"
         back = wire.unpack(w, eng.n_envs, eng.P)

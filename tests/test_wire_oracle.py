@@ -14,23 +14,27 @@ import torch.multiprocessing as mp
 from nmmo_amd import abi
 from nmmo_amd.config import Config
 from oracle import wire as owire
-from oracle.oracle import OracleEnvs
+from oracle.oracle import OracleEnvs, split_state
 from tests.test_native_layout import encode_native
 
 
-def _native(n_envs, ticks, seed=4, env_index_base=0):
+def _native(n_envs, ticks, seed=4, env_index_base=0, with_gold=False):
     cfg = Config.preset("C4", MAP_N=4, early_stop_agent_num=8)
     orc = OracleEnvs(cfg, n_envs, seed=seed, env_index_base=env_index_base)
     orc.reset()
     for t in range(ticks):
         orc.step(orc.scripted_actions(t))
     task = np.arange(n_envs * cfg.PLAYER_N).reshape(n_envs, cfg.PLAYER_N) % 5
-    return encode_native(orc.obs, cfg.PLAYER_N, task.astype(np.int16)), cfg.PLAYER_N
+    nat = encode_native(orc.obs, cfg.PLAYER_N, task.astype(np.int16))
+    if not with_gold:
+        return nat, cfg.PLAYER_N
+    gold = split_state(orc.get_state(), n_envs, orc.S, orc.P)["ent"][:, abi.F["gold"], :orc.P]
+    return nat, cfg.PLAYER_N, gold
 
 
 def test_wire_roundtrip_and_size():
-    nat, P = _native(3, 40)
-    w = owire.pack(nat, P)
+    nat, P, gold = _native(3, 40, with_gold=True)
+    w = owire.pack(nat, P, gold)
     assert int(w[:8].view(np.int64)[0]) == w.nbytes
     back = owire.unpack(w, 3, P)
     assert np.array_equal(back, nat)
@@ -39,10 +43,29 @@ def test_wire_roundtrip_and_size():
     assert w.nbytes * 4 < nat.nbytes, (w.nbytes, nat.nbytes)
 
 
+def test_wire_buy_mask_is_rebuilt_from_the_listings():
+    """Buy.MarketItem is not sent: unpack rebuilds it from the env's listings, the head's gold
+    and the agent id (an agent can buy a listing it can afford and does not own), so a record
+    with a changed gold decodes to the mask of that gold."""
+    nat, P, gold = _native(3, 60, seed=5, with_gold=True)
+    cnt, nm = owire.counts(nat, P)
+    assert nm.max() > 0, "listings exercised"
+    e = int(np.argmax(nm))
+    rich = gold.copy()
+    rich[e] = 10_000
+    back = owire.unpack(owire.pack(nat, P, rich), 3, P)
+    rows = back[e, :P * abi.NATIVE_ROW_BYTES].reshape(P, abi.NATIVE_ROW_BYTES)
+    market = back[e, P * abi.NATIVE_ROW_BYTES:].copy().view(np.int16).reshape(abi.MARKET_ROWS, 16)
+    for a in np.nonzero(cnt[e] & 0x8000)[0]:
+        buy = rows[a, owire.BUY_LO:owire.BUY_LO + owire.BUY_N]
+        want = (np.arange(owire.BUY_N - 1) < nm[e]) & (market[:, 2] != a + 1)
+        assert np.array_equal(buy[:-1], want.astype(np.uint8)) and buy[-1] == 1
+
+
 def test_wire_all_dead_env():
-    nat, P = _native(2, 5)
+    nat, P, gold = _native(2, 5, with_gold=True)
     nat[1] = 0  # an env with nobody in the realm and no listings
-    w = owire.pack(nat, P)
+    w = owire.pack(nat, P, gold)
     assert np.array_equal(owire.unpack(w, 2, P), nat)
 
 
@@ -57,9 +80,9 @@ def _free_port():
 def _step_bytes(rank, t, n):
     """What rank `rank` sends at step t: an oracle-made wire buffer (its size varies with the
     tick) and a small companion buffer."""
-    nat, P = _native(n, 8 + 5 * t + 7 * rank, seed=9, env_index_base=rank * n)
+    nat, P, gold = _native(n, 8 + 5 * t + 7 * rank, seed=9, env_index_base=rank * n, with_gold=True)
     small = (np.arange(n * P * 8) * (rank + 3) + t).astype(np.uint8)
-    return owire.pack(nat, P), small, P
+    return owire.pack(nat, P, gold), small, P
 
 
 def _worker(rank, world, port, q):
