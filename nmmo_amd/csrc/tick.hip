@@ -980,6 +980,25 @@ __device__ __forceinline__ void fire_ammo(Ctx& c, int x, int style) {
   }
 }
 
+// fire_ammo without touching the item FIFO: the row freed by the last unit is returned (-1 if
+// none) for the caller to append in serial order
+__device__ __forceinline__ int fire_ammo_deferred(Ctx& c, int x, int style) {
+  uint2* inv = c.inv + x * kInv;
+  for (int k = 0; k < kInv; k++) {
+    const uint2 w = inv[k];
+    if (!it_type(w)) break;
+    if (!it_equipped(w) || it_type(w) != T_WHETSTONE + style) continue;
+    inv[k].y -= 1u;
+    if (it_qty(inv[k]) == 0) {
+      inv_remove(inv, k);
+      update_item_level(c, x);
+      return it_row(w);
+    }
+    break;
+  }
+  return -1;
+}
+
 // a player killed t: gold, then t's items (player) or drops (NPC) (serial; SPEC §9 Death)
 __device__ __forceinline__ void loot(Ctx& c, int x, int t, int& evn) {
   if (sys(c, NMMO_SYS_EXCHANGE)) {
@@ -1772,8 +1791,26 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
   }
   if (items || sys(c, NMMO_SYS_EXCHANGE)) {
     // ammunition and loot of the executed player attacks, in slot order (equipment sums and
-    // every attack's validity are unaffected by them, so deferring is exact)
-    const bool nd = s < P && (c.fired[s] || c.kill[s] >= 0);
+    // every attack's validity are unaffected by them, so deferring is exact). A shot touches
+    // only its shooter's inventory, and a loot its killer's and victim's: the shots of players
+    // no player killed this tick commute with every other shot and loot (their own loot comes
+    // after their shot in both orders), so they fire in parallel; only the FIFO rows a shot
+    // frees (its last unit) keep their serial place, appended by thread 0's slot-order walk
+    // with the remaining shots (of victims) and the loots.
+    uint32_t* victim = reinterpret_cast<uint32_t*>(c.misc);  // [16] slot bitmask (hunt mask: dead now)
+    if (tid < 16) victim[tid] = 0u;
+    __syncthreads();
+    if (s < P && c.kill[s] >= 0) atomicOr(&victim[c.kill[s] >> 5], 1u << (c.kill[s] & 31));
+    __syncthreads();
+    int16_t* shot_row = c.clist;  // [S] scratch (the hostile-NPC list of the decode: dead now)
+    int freed = -1;
+    const bool is_victim = s < S && ((victim[s >> 5] >> (s & 31)) & 1u);
+    if (s < P && c.fired[s] && !is_victim) {
+      freed = fire_ammo_deferred(c, s, c.asty[s]);
+      c.fired[s] = 0;  // done
+    }
+    if (s < P) shot_row[s] = (int16_t)freed;
+    const bool nd = s < P && (c.fired[s] || c.kill[s] >= 0 || freed >= 0);
     int nn;
     const int pos = block_prefix_count(nd, wtot_next(c), &nn);
     if (nd) c.order[pos] = (int16_t)s;
@@ -1781,6 +1818,7 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
     if (tid == 0) {
       for (int i = 0; i < nn; i++) {
         const int x = c.order[i];
+        if (shot_row[x] >= 0) ifree(c, shot_row[x]);
         if (c.fired[x]) fire_ammo(c, x, c.asty[x]);
         if (c.kill[x] >= 0) loot(c, x, c.kill[x], evn);
       }
