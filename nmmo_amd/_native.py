@@ -43,7 +43,25 @@ def lib():
         raise NativeError(
             f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
             " (there is no CPU fallback for the HIP stepper)")
-    L = ctypes.CDLL(LIB_PATH)
+    L = declare(ctypes.CDLL(LIB_PATH))
+    if L.nmmo_abi_version() != abi.ABI_VERSION:
+        raise NativeError(f"ABI mismatch: lib {L.nmmo_abi_version()} != python {abi.ABI_VERSION}")
+    info = build_info(L)
+    if os.environ.get("NMMO_ALLOW_STALE") != "1" and os.path.isdir(os.path.join(_PKG, "csrc")):
+        from .build import source_hash
+
+        want = source_hash()
+        if info.get("src") != want:
+            raise NativeError(
+                f"{LIB_PATH} was built from other sources (src={info.get('src')}, tree={want}): "
+                "rebuild it (`python -m nmmo_amd.build --force`)")
+    _lib = L
+    return L
+
+
+def declare(L):
+    """The ctypes signatures of include/nmmo_hip.h on a loaded library (this package's
+    libnmmo_hip.so, or any library exporting the same C-ABI)."""
     vp, i32, u64, sz = ctypes.c_void_p, ctypes.c_int32, ctypes.c_uint64, ctypes.c_size_t
     cfgp = ctypes.POINTER(abi.NmmoConfig)
     L.nmmo_default_config.argtypes = [cfgp]
@@ -91,18 +109,6 @@ def lib():
     L.nmmo_dev_alloc.argtypes = [i32, u64, ctypes.POINTER(vp)]
     L.nmmo_dev_free.argtypes = [vp]
     L.nmmo_build_info.restype = ctypes.c_char_p
-    if L.nmmo_abi_version() != abi.ABI_VERSION:
-        raise NativeError(f"ABI mismatch: lib {L.nmmo_abi_version()} != python {abi.ABI_VERSION}")
-    info = build_info(L)
-    if os.environ.get("NMMO_ALLOW_STALE") != "1" and os.path.isdir(os.path.join(_PKG, "csrc")):
-        from .build import source_hash
-
-        want = source_hash()
-        if info.get("src") != want:
-            raise NativeError(
-                f"{LIB_PATH} was built from other sources (src={info.get('src')}, tree={want}): "
-                "rebuild it (`python -m nmmo_amd.build --force`)")
-    _lib = L
     return L
 
 

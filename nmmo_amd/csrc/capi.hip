@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "kernels.h"
+#include "wire.h"
 
 
 
@@ -471,13 +472,13 @@ int nmmo_dev_free(void* ptr) {
 // ---------------------------------------------------------------- wire codec (SPEC §8c)
 int64_t nmmo_wire_header_bytes(int32_t n_envs, int32_t player_n) {
   if (n_envs <= 0 || player_n <= 0 || player_n > 128) return fail(NMMO_E_INVALID, "n_envs > 0, player_n in 1..128");
-  return ((8 + 8 * (int64_t)n_envs + 2 * (int64_t)n_envs * player_n + 2 * (int64_t)n_envs) + 15) & ~(int64_t)15;
+  return wire_header_bytes(n_envs, player_n);
 }
 
 int64_t nmmo_wire_max_bytes(int32_t n_envs, int32_t player_n) {
   const int64_t hdr = nmmo_wire_header_bytes(n_envs, player_n);
   if (hdr < 0) return hdr;
-  const int64_t rec = (16 + 208 + 62 * 100 + 32 * 12 + 225 + 15) & ~15;  // every agent in the realm, full windows
+  const int64_t rec = wire_record_bytes(wire_count_word(kNObs, kInv));  // every agent in the realm, full windows
   return hdr + (int64_t)n_envs * ((int64_t)player_n * rec + NMMO_NATIVE_MARKET_BYTES);
 }
 

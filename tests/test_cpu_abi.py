@@ -1,0 +1,102 @@
+"""The C-ABI over the CPU oracle (oracle/libnmmo_cpu.so): the same nmmo_* symbols
+as libnmmo_hip.so with host buffers, so a caller swaps backends behind one ABI. CPU only.
+
+- it exports every entry point include/nmmo_hip.h declares (the device-only ones refuse with an
+  error message instead of aborting);
+- its layout and default config equal the HIP library's host-side answers;
+- a scripted C4 rollout with staggered episode ends driven through nmmo_* equals the oracle's
+  own API (state, flat obs, rewards, flags, event log) — the same engine behind either API."""
+
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from nmmo_amd import abi
+from nmmo_amd.config import Config
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CPU_LIB = os.path.join(ROOT, "oracle", "build", "libnmmo_cpu.so")
+
+
+@pytest.fixture(scope="module")
+def cpu():
+    from nmmo_amd import _native
+    from oracle import oracle
+
+    oracle.build()
+    if not os.path.exists(CPU_LIB):
+        oracle.build(force=True)
+    return _native.declare(ctypes.CDLL(CPU_LIB))
+
+
+def test_exports_every_declared_symbol(cpu):
+    decl = set(re.findall(r"NMMO_API\s+[\w\s\*]+?\b(nmmo_\w+)\s*\(", open(os.path.join(ROOT, "include", "nmmo_hip.h")).read()))
+    out = subprocess.check_output(["nm", "-D", "--defined-only", CPU_LIB]).decode()
+    exported = set(re.findall(r"\sT\s(nmmo_\w+)", out))
+    assert decl <= exported, decl - exported
+    assert cpu.nmmo_abi_version() == abi.ABI_VERSION
+    assert cpu.nmmo_dev_alloc(0, 16, ctypes.byref(ctypes.c_void_p())) == abi.NMMO_E_INVALID
+    assert b"CPU stepper" in cpu.nmmo_last_error()
+
+
+def test_layout_and_defaults_equal_the_hip_library(cpu):
+    from nmmo_amd import _native
+
+    hip = _native.lib()
+    for preset in ("C2", "C3", "C4"):
+        cfg = Config.preset(preset).to_c()
+        a, b = abi.NmmoLayout(), abi.NmmoLayout()
+        assert cpu.nmmo_layout(ctypes.byref(cfg), ctypes.byref(a)) == 0
+        assert hip.nmmo_layout(ctypes.byref(cfg), ctypes.byref(b)) == 0
+        assert bytes(a) == bytes(b), preset
+    c1, c2 = abi.NmmoConfig(), abi.NmmoConfig()
+    cpu.nmmo_default_config(ctypes.byref(c1))
+    hip.nmmo_default_config(ctypes.byref(c2))
+    assert bytes(c1) == bytes(c2)
+    assert cpu.nmmo_wire_max_bytes(16, 128) == hip.nmmo_wire_max_bytes(16, 128)
+
+
+def test_rollout_through_the_abi_equals_the_oracle_api(cpu):
+    from oracle.oracle import OracleEnvs
+
+    n, P = 3, 128
+    cfg = Config.preset("C4", MAP_N=4, early_stop_agent_num=8)
+    c = cfg.to_c()
+    h = ctypes.c_void_p()
+    assert cpu.nmmo_create(ctypes.byref(c), n, 5, 0, None, ctypes.byref(h)) == 0, cpu.nmmo_last_error()
+    ref = OracleEnvs(cfg, n, seed=5)
+    lay = abi.NmmoLayout()
+    cpu.nmmo_layout(ctypes.byref(c), ctypes.byref(lay))
+    obs = np.zeros((n, P, lay.obs_elems), np.float32)
+    rew = np.zeros((n, P), np.float32)
+    term, trunc, mask = (np.zeros((n, P), np.uint8) for _ in range(3))
+    act = np.zeros((n, P, 12), np.int32)
+    p = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    assert cpu.nmmo_reset(h, None, p(obs), p(mask), None) == 0
+    ref.reset()
+    assert np.array_equal(obs, ref.obs)
+    for t in range(40):
+        if t in (9, 23):
+            m = (np.arange(n) % 2 == t % 2).astype(np.uint8)
+            assert cpu.nmmo_end_episodes(h, p(m), None) == 0
+            ref.end_episodes(m)
+        assert cpu.nmmo_scripted_actions(h, 100 + t, p(act), None) == 0
+        a = ref.scripted_actions(100 + t)
+        assert np.array_equal(act, a)
+        assert cpu.nmmo_step(h, p(act), p(obs), p(rew), p(term), p(trunc), p(mask), None) == 0
+        ref.step(a)
+        assert np.array_equal(rew, ref.rew) and np.array_equal(mask, ref.mask) and np.array_equal(term, ref.term)
+    assert np.array_equal(obs, ref.obs)
+    nb = lay.state_bytes_per_env * n
+    st = np.zeros(nb, np.uint8)
+    assert cpu.nmmo_get_state(h, p(st), nb) == 0
+    assert np.array_equal(st, ref.get_state())
+    rows = np.zeros((64, abi.EVENT_COLS), np.int32)
+    k = ctypes.c_int32()
+    assert cpu.nmmo_get_events(h, 1, p(rows), 64, ctypes.byref(k)) == 0
+    assert np.array_equal(rows[:k.value], ref.events(1)[-k.value:])
+    cpu.nmmo_destroy(h)
