@@ -323,7 +323,7 @@ int nmmo_reset(NmmoHandle* h, const uint64_t* env_seeds, void* obs, uint8_t* mas
   if (h->wrap_on) HIP_TRY(launch_wrap(wrap_params(h, nullptr, nullptr, nullptr, nullptr, nullptr), 0, s));
   const bool do_obs = obs && h->cfg.obs_layout != NMMO_OBS_NONE;
   if (do_obs) HIP_TRY(launch_obs(obs_params(h, obs), s));
-  h->last_native = do_obs ? obs : nullptr;
+  if (do_obs) h->last_native = obs;  // kept across a tick without obs: the pack check then says stale
   h->native_fresh = do_obs;
   return NMMO_OK;
 }
@@ -359,7 +359,7 @@ int nmmo_step(NmmoHandle* h, const int32_t* actions, void* obs, float* rew, uint
   if (rec) HIP_TRY(hipEventRecord(ev[2], s));  // wrapper span = ev[1]..ev[2] (empty when off)
   const bool do_obs = obs && h->cfg.obs_layout != NMMO_OBS_NONE;
   if (do_obs) HIP_TRY(launch_obs(obs_params(h, obs), s));
-  h->last_native = do_obs ? obs : nullptr;
+  if (do_obs) h->last_native = obs;  // kept across a tick without obs: the pack check then says stale
   h->native_fresh = do_obs;
   if (rec) {
     HIP_TRY(hipEventRecord(ev[3], s));  // obs span = ev[2]..ev[3] (empty when no obs)
