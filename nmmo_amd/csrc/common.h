@@ -160,6 +160,9 @@ __device__ __forceinline__ int wave_incl_scan(int x) {
   x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
   return x;
 }
+__host__ __device__ __forceinline__ uint32_t i16pack(int lo, int hi) {
+  return (uint32_t)(uint16_t)(int16_t)lo | ((uint32_t)(uint16_t)(int16_t)hi << 16);
+}
 // Sum over the 64 lanes of a wave (all lanes active), wave-uniform.
 __device__ __forceinline__ int wave_sum(int x) { return __builtin_amdgcn_readlane(wave_incl_scan(x), 63); }
 

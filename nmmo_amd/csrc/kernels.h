@@ -125,6 +125,8 @@ hipError_t launch_wire_unpack(const uint8_t* wire, uint8_t* native, int n, int P
 // NMMO_OBS_WIRE: per-agent count words + per-env payload sizes (wire_count_kernel) and their
 // scan, ahead of obs_kernel's record writes (obs.hip launch_obs)
 hipError_t launch_wire_header(const ObsParams& p, hipStream_t s);
+// NMMO_OBS_WIRE obs gather (wire_obs.hip): header pre-pass + wire_obs_kernel
+hipError_t launch_wire_obs(const ObsParams& p, hipStream_t s);
 // header + record-head consistency of a wire buffer; bits into *status (0 = valid)
 hipError_t launch_wire_check(const uint8_t* wire, int n, int P, const int64_t* expect_total, int* status,
                              hipStream_t s);

@@ -14,26 +14,26 @@
 // Every global load of the next agent is issued ahead of the current row's bulk stores, so the
 // store stream never waits on a load (vmcnt retires in issue order).
 #include "kernels.h"
-#include "wire.h"
 
 namespace nmmo {
 
 constexpr int kObsAgentsPerBlock = 16;
 constexpr int kObsWaves = 4;
+// agents per wave of an obs_kernel launch with `gy` workgroups per env
+__host__ __device__ inline int obs_per_wave(int P, int gy) { return (P + gy * kObsWaves - 1) / (gy * kObsWaves); }
 constexpr int kObsFields = F_DS_ROW + 1;  // 0..30 obs columns, alive, ds_row
-// output layouts of obs_kernel
-constexpr int kModeFlat = 0, kModeNative = 1, kModeWire = 2;
+// output layouts of obs_kernel (NMMO_OBS_WIRE has its own kernel, wire_obs.hip)
+constexpr int kModeFlat = 0, kModeNative = 1;
 
 // LDS: entity fields | row->slot | per-wave visible list | per-wave inventory | per-wave 15x15
 // window materials | market listings (price | owner << 8, 2 B per listing; flat rows also the
-// listed item words, 8 B) | native: per-wave ActionTargets bytes; wire: per-wave ActionTargets
-// bits + the env's record offsets. 38.8 KB (native) at S = 384: 4 workgroups (16 waves) per CU.
+// listed item words, 8 B) | native: per-wave ActionTargets bytes. 38.8 KB (native) at S = 384:
+// 4 workgroups (16 waves) per CU.
 __host__ __device__ inline size_t obs_lds_bytes(int S, int mode) {
   const size_t base = (((size_t)kObsFields * S * 2 + 15) & ~(size_t)15) + (((size_t)(S + 1) * 2 + 15) & ~(size_t)15) +
                       (size_t)kObsWaves * 128 * 2 + (size_t)kObsWaves * kInv * 8 + (size_t)kObsWaves * 256;
   if (mode == kModeFlat) return base + (size_t)NMMO_MARKET_ROWS * 10;
-  if (mode == kModeNative) return base + (size_t)NMMO_MARKET_ROWS * 2 + (size_t)kObsWaves * NMMO_NATIVE_MASK_BYTES;
-  return base + (size_t)NMMO_MARKET_ROWS * 2 + (size_t)kObsWaves * kWireMask + 132 * 4;
+  return base + (size_t)NMMO_MARKET_ROWS * 2 + (size_t)kObsWaves * NMMO_NATIVE_MASK_BYTES;
 }
 
 // Plain (temporal) stores. Measured on MI355X (same-box A/B): __builtin_nontemporal_store
@@ -63,9 +63,6 @@ constexpr int kNatEntity = 2, kNatInv = kNatEntity + kNObs * NMMO_N_ENTITY_COLS,
 static_assert(kNatTask < NMMO_NATIVE_I16, "native int16 part overflows its row");
 __host__ __device__ inline size_t native_env_bytes(int P) {
   return (size_t)P * NMMO_NATIVE_ROW_BYTES + NMMO_NATIVE_MARKET_BYTES;
-}
-__device__ __forceinline__ uint32_t i16pack(int lo, int hi) {
-  return (uint32_t)(uint16_t)(int16_t)lo | ((uint32_t)(uint16_t)(int16_t)hi << 16);
 }
 
 // One agent's view for the ActionTargets sections (SPEC §8, §9, §13 edits).
@@ -164,29 +161,6 @@ __device__ __forceinline__ void mask_sec_f32(const ObsParams& p, const int16_t* 
     obs_st(&row[lo + k], mask_value<kWrap>(p, T, S, vis, inv, mpo, nm, m, kSec, k) ? 1.f : 0.f);
 }
 
-// The same for a wire record (SPEC §8c): section kSec as bits of the wave's LDS bit image
-// (zeroed beforehand), one ballot per 64 entries OR-ed in at the section's bit offset (a
-// 64-bit ballot shifted by 0..31 spans 3 words: lanes 0-2 take one each). Buy.MarketItem is not
-// part of a record (the decoders rebuild it from the listings, wire.h).
-template <int kSec, bool kWrap>
-__device__ __forceinline__ void mask_sec_bits(const ObsParams& p, const int16_t* T, int S, const int16_t* vis,
-                                              const uint2* inv, const uint16_t* mpo, int nm, const MaskCtx& m,
-                                              uint32_t* bw) {
-  int lo, n;
-  mask_section(p, kSec, lo, n);
-  const int lane = lane_id();
-  for (int k0 = 0; k0 < n; k0 += 64) {
-    const int k = k0 + lane;
-    const uint64_t b = __ballot(k < n && mask_value<kWrap>(p, T, S, vis, inv, mpo, nm, m, kSec, k));
-    if (b == 0ull) continue;
-    const int bit = entry_wire_bit(lo + k0), sh = bit & 31;  // Buy.MarketItem is not sent (wire.h)
-    const uint64_t lo64 = b << sh;
-    const uint32_t part = lane == 0 ? (uint32_t)lo64 : lane == 1 ? (uint32_t)(lo64 >> 32)
-                                                                 : (sh ? (uint32_t)(b >> (64 - sh)) : 0u);
-    if (lane < 3 && part) atomicOr(&bw[(bit >> 5) + lane], part);
-  }
-}
-
 // Passability of the 5 move targets from the prefetched window materials: tile t of the 15x15
 // window sits in lane t & 63 of register t >> 6; the centre's 4 neighbours (t = 97, 111, 112,
 // 113, 127) are all in register 1.
@@ -208,12 +182,10 @@ constexpr int kTaskRegs = 32;  // Task embedding dwords per lane held in registe
 
 // kWrap: the wrapper's observation() edits are compiled in (SPEC §13).
 // kMode: kModeFlat = pufferlib's float32 row; kModeNative = the nmmo-dtype layout of SPEC §8b
-// (u8 masks, int16 fields, Market once per env, task index): ~10x fewer bytes per agent;
-// kModeWire = the wire records of SPEC §8c straight from the state (~1.3 KB per agent; the
-// header's count words and offsets come from wire_count_kernel + wire_scan_kernel).
+// (u8 masks, int16 fields, Market once per env, task index): ~10x fewer bytes per agent.
 template <bool kWrap, int kMode>
 __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
-  constexpr bool kNative = kMode != kModeFlat;  // native and wire share the market staging
+  constexpr bool kNative = kMode == kModeNative;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int S = p.S;
   int16_t* T = reinterpret_cast<int16_t*>(smem);
@@ -224,12 +196,9 @@ __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
   uint16_t* mpo = reinterpret_cast<uint16_t*>(kNative ? mitem : mitem + NMMO_MARKET_ROWS);  // price | owner << 8
   uint8_t* wmat_all = reinterpret_cast<uint8_t*>(mpo + NMMO_MARKET_ROWS);  // per-wave 15x15 materials
   uint8_t* mask_all = wmat_all + kObsWaves * 256;  // native: per-wave ActionTargets bytes (16-B aligned)
-  int* woff = reinterpret_cast<int*>(mask_all + kObsWaves * kWireMask);  // wire: the env's record offsets
   const int e = blockIdx.x, g = blockIdx.y;
   const int tid = threadIdx.x;
   const int nm = p.mcount[e];
-  if constexpr (kMode == kModeWire)
-    record_offsets_wave0(wire_view(p.wire, p.n_envs, p.P).cnt + (size_t)e * p.P, p.P, woff);
   if constexpr (kMode == kModeNative)
     if (p.wmcount && g == 0 && tid == 0) p.wmcount[e] = nm;  // nmmo_wire_pack reads this launch's count
   for (int j = tid; j < nm; j += blockDim.x) {  // end-of-tick listings, ascending row
@@ -256,14 +225,10 @@ __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
     if (T[F_ALIVE * S + s]) rowslot[T[F_DS_ROW * S + s]] = (int16_t)s;
   __syncthreads();
 
-  uint8_t* wenv = nullptr;  // wire: this env's payload
-  if constexpr (kMode == kModeWire) wenv = p.wire + wire_view(p.wire, p.n_envs, p.P).env_off[e];
   if constexpr (kNative) {  // the env's Market, once per env (the y == 0 workgroup)
     if (g == 0) {  // one listing row (16 int16 = two 16-B stores) per thread
-      uint4* mk = kMode == kModeWire ? reinterpret_cast<uint4*>(wenv + woff[p.P])
-                                     : reinterpret_cast<uint4*>(p.nat + (size_t)e * native_env_bytes(p.P) +
-                                                                (size_t)p.P * NMMO_NATIVE_ROW_BYTES);
-      for (int k = tid; k < (kMode == kModeWire ? min(nm, NMMO_MARKET_ROWS) : NMMO_MARKET_ROWS); k += blockDim.x) {
+      uint4* mk = reinterpret_cast<uint4*>(p.nat + (size_t)e * native_env_bytes(p.P) + (size_t)p.P * NMMO_NATIVE_ROW_BYTES);
+      for (int k = tid; k < NMMO_MARKET_ROWS; k += blockDim.x) {
         uint32_t q[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
         if (k < nm) {
           const int v = p.mlist[(size_t)e * NMMO_MARKET_ROWS + k];
@@ -290,8 +255,8 @@ __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
   m.no_give = kWrap && (p.wflags & kWrapObsNoGive);
   // this wave's agents: a_j = g * 16 + w + 4 j; lane j holds a_j's task index and (wrapper) last
   // Sell price, loaded before any store
-  constexpr int kPerWave = kObsAgentsPerBlock / kObsWaves;
-  const int abase = g * kObsAgentsPerBlock + w;
+  const int kPerWave = obs_per_wave(p.P, gridDim.y);
+  const int abase = g * kPerWave * kObsWaves + w;
   int my_task = 0, my_prev = -1;
   if (lane < kPerWave && abase + kObsWaves * lane < p.P) {
     const size_t ai = (size_t)e * p.P + abase + kObsWaves * lane;
@@ -431,93 +396,6 @@ __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
     return;
   }
 
-  if constexpr (kMode == kModeWire) {
-    const uint16_t* cnt = wire_view(p.wire, p.n_envs, p.P).cnt + (size_t)e * p.P;
-    uint32_t* bw = reinterpret_cast<uint32_t*>(mask_all + w * kWireMask);
-    for (int j = 0; j < kPerWave; j++) {
-      const int a = abase + kObsWaves * j;
-      if (a >= p.P) break;
-      if (!T[F_ALIVE * S + a]) {  // no record
-        if (alive(j + 1)) prefetch(a + kObsWaves, j + 1);
-        continue;
-      }
-      m.a = a;
-      m.r = T[F_ROW * S + a];
-      m.c = T[F_COL * S + a];
-      m.gold = T[F_GOLD * S + a];
-      m.nv = compact(m.r, m.c);
-      if (lane < kInv) inv[lane] = iv;
-#pragma unroll
-      for (int i = 0; i < 4; i++)
-        if (lane + 64 * i < 225) wmat[lane + 64 * i] = (uint8_t)wm[i];
-      if (lane < kWireMask / 4) bw[lane] = 0u;
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      m.ninv = inv_count(inv);
-      m.prev_price = kWrap ? __builtin_amdgcn_readlane(my_prev, j) : -1;
-      m.movebits = move_bits(wm[1]);
-      const int aid = T[F_ID * S + a];
-      if (alive(j + 1)) prefetch(a + kObsWaves, j + 1);  // wm is in LDS now; next agent's loads
-      mask_sec_bits<0, kWrap>(p, T, S, vis, inv, mpo, nm, m, bw);
-      mask_sec_bits<1, kWrap>(p, T, S, vis, inv, mpo, nm, m, bw);
-      mask_sec_bits<3, kWrap>(p, T, S, vis, inv, mpo, nm, m, bw);
-      mask_sec_bits<4, kWrap>(p, T, S, vis, inv, mpo, nm, m, bw);
-      mask_sec_bits<5, kWrap>(p, T, S, vis, inv, mpo, nm, m, bw);
-      mask_sec_bits<6, kWrap>(p, T, S, vis, inv, mpo, nm, m, bw);
-      mask_sec_bits<7, kWrap>(p, T, S, vis, inv, mpo, nm, m, bw);
-      mask_sec_bits<8, kWrap>(p, T, S, vis, inv, mpo, nm, m, bw);
-      mask_sec_bits<9, kWrap>(p, T, S, vis, inv, mpo, nm, m, bw);
-      mask_sec_bits<10, kWrap>(p, T, S, vis, inv, mpo, nm, m, bw);
-      mask_sec_bits<11, kWrap>(p, T, S, vis, inv, mpo, nm, m, bw);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      // the record's sizes come from its header count word (wire_count_kernel computes the same
-      // nv / ninv from the same state), so the records never overlap whatever the state holds
-      const uint32_t cw = cnt[a];
-      const int nv = cw & 127, ninv = (cw >> 7) & 15;
-      uint8_t* rec = wenv + woff[a];
-      if (lane < kWireMask / 16) {
-        reinterpret_cast<uint4*>(rec + kWireHead)[lane] = reinterpret_cast<const uint4*>(bw)[lane];
-      } else if (lane == kWireMask / 16) {
-        *reinterpret_cast<uint4*>(rec) =
-            make_uint4(i16pack(aid, tick), i16pack(__builtin_amdgcn_readlane(my_task, j), m.r - kVision),
-                       i16pack(m.c - kVision, nv), i16pack(ninv | (m.exch ? 1 << 8 : 0), m.gold));
-      }
-      // body: nv Entity rows | ninv Inventory rows | 225 materials | pad, as int16 half-words
-      // (a material half-word holds two of them), 8 per lane per 16-B store
-      const int eb = 62 * nv, ib = eb + 32 * ninv;
-      const int nq = (wire_record_bytes(cw) - kWireBody) >> 4;
-      uint4* body = reinterpret_cast<uint4*>(rec + kWireBody);
-      auto half = [&](int h) -> uint32_t {
-        const int o = 2 * h;
-        int x;
-        if (o < eb) {
-          const int k = h / NMMO_N_ENTITY_COLS, f = h - k * NMMO_N_ENTITY_COLS;
-          x = T[f * S + vis[k]];
-        } else if (o < ib) {
-          const int i = (o - eb) >> 1;
-          x = (int)item_col(inv[i >> 4], aid, i & 15);
-        } else {  // tile bytes u, u + 1: materials 2u .. 2u + 3, 4 bits each
-          const int u = o - ib, t = 2 * u;
-          auto m4 = [&](int q) { return q < 225 ? (int)wmat[q] & 15 : 0; };
-          x = u < kWireTiles ? m4(t) | m4(t + 1) << 4 | (u + 1 < kWireTiles ? m4(t + 2) << 8 | m4(t + 3) << 12 : 0) : 0;
-        }
-        return (uint32_t)(uint16_t)x;
-      };
-      for (int q = lane; q < nq; q += 64) {
-        const int h = 8 * q;
-        body[q] = make_uint4(half(h) | half(h + 1) << 16, half(h + 2) | half(h + 3) << 16,
-                             half(h + 4) | half(h + 5) << 16, half(h + 6) | half(h + 7) << 16);
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the next agent reuses vis / inv / wmat / bw
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
-    return;
-  }
-
   for (int j = 0; j < kPerWave; j++) {
     const int a = abase + kObsWaves * j;
     if (a >= p.P) break;
@@ -635,16 +513,15 @@ __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
 }
 
 hipError_t launch_obs(const ObsParams& p, hipStream_t stream) {
+  // 16 agents per workgroup: same-box A/B of the native kernel, 0.192 / 0.196 / 0.231 ms per
+  // 512-env launch at 16 / 32 / 64 (the env staging is shared by fewer agents, but more
+  // workgroups fill the CUs)
   dim3 grid(p.n_envs, (p.P + kObsAgentsPerBlock - 1) / kObsAgentsPerBlock);
   const dim3 block(64 * kObsWaves);
-  const int mode = p.wire ? kModeWire : p.nat ? kModeNative : kModeFlat;
+  if (p.wire) return launch_wire_obs(p, stream);  // wire_obs.hip
+  const int mode = p.nat ? kModeNative : kModeFlat;
   const size_t lds = obs_lds_bytes(p.S, mode);
-  if (mode == kModeWire) {
-    const hipError_t err = launch_wire_header(p, stream);  // count words, sizes, offsets
-    if (err != hipSuccess) return err;
-    if (p.wflags) hipLaunchKernelGGL((obs_kernel<true, kModeWire>), grid, block, lds, stream, p);
-    else hipLaunchKernelGGL((obs_kernel<false, kModeWire>), grid, block, lds, stream, p);
-  } else if (mode == kModeNative) {
+  if (mode == kModeNative) {
     if (p.wflags) hipLaunchKernelGGL((obs_kernel<true, kModeNative>), grid, block, lds, stream, p);
     else hipLaunchKernelGGL((obs_kernel<false, kModeNative>), grid, block, lds, stream, p);
   } else {

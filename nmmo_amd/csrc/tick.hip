@@ -1537,6 +1537,7 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
       if (e_on_nl) ev_put(c, i++, s, EV_LEVEL_UP, 5 + e_on_q, e_on_nl, 0, 0, 0);
     });
   }
+  NMMO_STAMP(21);
 
   if (items) {
     // 3. Use (priority 10): own inventory only -> parallel; consumed rows freed in slot order
@@ -1584,6 +1585,7 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
     }
     ring_append_ordered(c, freed);
     if (evon) ev_append(c, evn, u_code ? 1 : 0, [&](int i) { ev_put(c, i, s, u_code, u_type, u_lvl, u_num, 0, 0); });
+  NMMO_STAMP(22);
 
     // Buy (priority 20): buyers in shuffled order (key draw(tick, BUY_ORDER, id), ties by id).
     // A buy touches two players -- its buyer (gold, inventory room) and the listing's owner at
@@ -1688,6 +1690,7 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
       }
     }
 
+    NMMO_STAMP(23);
     // Give / GiveGold (priority 30): cross-player, replayed by thread 0 in slot order
     {
       const bool isg = s < P && (c.a_givet[s] >= 0 || c.a_ggt[s] >= 0);
@@ -1722,6 +1725,7 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
       __syncthreads();
       evn = c.E[E_EVENT_COUNT];
     }
+  NMMO_STAMP(24);
 
     // Destroy (priority 40): own inventory, rows freed in slot order
     freed = -1;
@@ -1777,6 +1781,7 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
       }
     }
   }
+  NMMO_STAMP(25);
   if (evon && combat) {  // SCORE_HIT, LEVEL_UP, PLAYER_KILL per player attacker in slot order
     const int dm = s < P ? c.ev_dmg[s] : -1, lv = s < P ? c.ev_lvl[s] : 0, kv = s < P ? c.kill[s] : -1;
     ev_append(c, evn, (dm >= 0) + (lv > 0) + (kv >= 0), [&](int i) {
@@ -1789,6 +1794,7 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
       }
     });
   }
+  NMMO_STAMP(26);
   if (items || sys(c, NMMO_SYS_EXCHANGE)) {
     // ammunition and loot of the executed player attacks, in slot order (equipment sums and
     // every attack's validity are unaffected by them, so deferring is exact). A shot touches
@@ -1815,6 +1821,7 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
     const int pos = block_prefix_count(nd, wtot_next(c), &nn);
     if (nd) c.order[pos] = (int16_t)s;
     __syncthreads();
+    NMMO_STAMP(27);
     if (tid == 0) {
       for (int i = 0; i < nn; i++) {
         const int x = c.order[i];

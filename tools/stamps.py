@@ -27,8 +27,9 @@ from nmmo_amd.engine import NmmoEngine  # noqa: E402
 STAMPS = [(0, None), (20, "state load"), (1, "prep: rowslot, positions, listings"),
           (13, "visibility bitmap"), (12, "action decode"), (2, "npc decide + hunt BFS"),
           (3, "update: resources, tile hash"), (15, "harvest: foilage, professions"),
-          (14, "harvest events; Use, Buy, Give, Destroy"), (4, "attack init"),
-          (5, "attack rounds, ammunition, loot"), (6, "move (+ Sell)"), (7, "cull, NPC compaction"),
+          (21, "harvest events"), (22, "Use"), (23, "Buy"), (24, "Give, GiveGold (serial)"),
+          (14, "Destroy"), (4, "attack init"), (25, "attack rounds"), (26, "attack events"),
+          (27, "parallel shots"), (5, "serial shots, loot"), (6, "move (+ Sell)"), (7, "cull, NPC compaction"),
           (16, "respawn scan (wave 0)"), (18, "respawn list (wave 0)"), (19, "respawn draws, expiry (wave 0)"),
           (8, "tick++ barrier"), (9, "npc spawn"), (10, "tasks, rewards, dones"), (11, "store")]
 
