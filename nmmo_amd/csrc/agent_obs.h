@@ -1,0 +1,227 @@
+// agent_obs.h — the per-agent observation pieces shared by the native (SPEC.md §8b,
+// native_obs.hip) and wire (SPEC §8c, wire_obs.hip) obs kernels.
+//
+// Per workgroup (env e, kAoAgents agents; kAoWaves waves, one agent per wave at a time):
+//  - ao_stage: the env's 31 Entity columns in LDS with an odd dword stride (a lane per field
+//    reads one slot's row conflict-free; the field-major stride of S = 384 puts all 31 fields of
+//    a slot in one bank) and one packed word per datastore row: slot | row << 10 | col << 18 |
+//    spawn-immune << 26 | dangerous << 27 | player << 28 (kAoEmpty = no entity on that row);
+//  - every lane keeps the packed words of its kAoRows datastore rows in registers, so an agent's
+//    window compaction (Entity.Query.window order) is kAoRows ballots with no LDS read;
+//  - the ActionTargets sections are wave-uniform bit fields (ballots over the visible rows and the
+//    12 inventory slots, closed forms for Style / GoldPrice / Move / SellPrice) placed into a bit
+//    image with compile-time shifts (the sections' sizes are nmmo_layout's fixed dims).
+#pragma once
+
+#include "kernels.h"
+#include "wire.h"
+
+namespace nmmo {
+
+constexpr int kAoWaves = 4;
+constexpr int kAoAgents = 16;             // agents per workgroup
+constexpr int kAoRows = kMaxSlots / 64;   // packed datastore-row words per lane
+constexpr uint32_t kAoEmpty = 0xFFFFFFFFu;
+static_assert(kSize <= 256 && kMaxSlots <= 2 * 256 && kMaxSlots % 64 == 0, "packed entity word; two slots per thread");
+__host__ __device__ inline int ao_stride(int S) { return ((S + 1) >> 1 | 1) << 1; }  // int16, odd dword count
+__host__ __device__ inline size_t ao_entity_lds(int S) {  // T | pk
+  return (((size_t)NMMO_N_ENTITY_COLS * ao_stride(S) * 2 + 15) & ~(size_t)15) + (size_t)(kMaxSlots + 64) * 4;
+}
+__device__ __forceinline__ int ao_slot(uint32_t w) { return (int)(w & 1023u); }
+__device__ __forceinline__ int ao_row(uint32_t w) { return (int)((w >> 10) & 255u); }
+__device__ __forceinline__ int ao_col(uint32_t w) { return (int)((w >> 18) & 255u); }
+
+// The 12 ActionTargets sections (nmmo_layout's dims, flat order), their flat entry offsets and
+// the wire bit offsets of the 11 sent ones (Buy.MarketItem is not sent). Launchers check a
+// handle's layout against sec_flat.
+constexpr int kSecN[12] = {3, 101, NMMO_MARKET_ROWS + 1, kInv + 1, kInv + 1, kNObs + 1, 99, kNObs + 1, 5, kInv + 1, 99, kInv + 1};
+__host__ __device__ constexpr int sec_flat(int k) { return k == 0 ? 0 : sec_flat(k - 1) + kSecN[k - 1]; }
+__host__ __device__ constexpr int sec_wire(int k) { return k < 2 ? sec_flat(k) : sec_flat(k) - kWireBuyN; }
+static_assert(sec_flat(2) == kWireBuyLo && sec_flat(12) == kMaskN && sec_wire(12) == kWireMaskBits, "sections");
+__host__ inline bool ao_layout_ok(const ObsParams& p) {
+  const int offs[12] = {p.o_style, p.o_target, p.o_buy, p.o_destroy, p.o_give_item, p.o_give_target,
+                        p.o_gg_price, p.o_gg_target, p.o_move, p.o_sell_item, p.o_sell_price, p.o_use};
+  for (int k = 0; k < 12; k++)
+    if (offs[k] != sec_flat(k)) return false;
+  return p.o_agent_id == sec_flat(12);
+}
+
+__device__ __forceinline__ uint64_t low_bits(int n) { return n >= 64 ? ~0ull : n <= 0 ? 0ull : (1ull << n) - 1ull; }
+// x with lane L's value replaced by the wave-uniform v
+__device__ __forceinline__ int writelane(int v, int L, int x) { return lane_id() == L ? v : x; }
+
+// OR the kN-bit field lo | hi << 64 (bits >= kN zero) into img at bit kOff
+template <int kOff, int kN, int kW>
+__device__ __forceinline__ void put_field(uint32_t (&img)[kW], uint64_t lo, uint64_t hi) {
+  static_assert((kOff + kN + 31) / 32 <= kW, "image size");
+#pragma unroll
+  for (int d = kOff / 32; d <= (kOff + kN - 1) / 32; d++) {
+    const int st = 32 * d - kOff;  // field bit on the dword's bit 0
+    uint32_t x;
+    if (st < 0) x = (uint32_t)(lo << (-st));
+    else if (st == 0) x = (uint32_t)lo;
+    else if (st < 64) x = (uint32_t)((lo >> st) | (hi << (64 - st)));
+    else x = (uint32_t)(hi >> (st - 64));
+    img[d] |= x;
+  }
+}
+
+// Block prologue (every thread; two barriers inside): T[f * ao_stride(S) + s] = field f (< 31)
+// of slot s, pk[row - 1] = the packed word of datastore row `row` (kAoEmpty where none).
+__device__ inline void ao_stage(const ObsParams& p, int e, int16_t* T, uint32_t* pk) {
+  const int S = p.S, P = p.P, Sp = ao_stride(S), tid = threadIdx.x;
+  const int16_t* E = p.ent + (size_t)e * NMMO_NF * S;
+  const int w4 = S / 8;  // 16-B words per field (S % 8 == 0: checked by the launchers)
+  for (int i = tid; i < NMMO_N_ENTITY_COLS * w4; i += blockDim.x) {  // 16-B loads, dword LDS writes
+    const int f = i / w4, j = i - f * w4;
+    const uint4 x = reinterpret_cast<const uint4*>(E + (size_t)f * S)[j];
+    uint32_t* d = reinterpret_cast<uint32_t*>(T + f * Sp) + 4 * j;
+    d[0] = x.x;
+    d[1] = x.y;
+    d[2] = x.z;
+    d[3] = x.w;
+  }
+  for (int k = tid; k < kMaxSlots + 64; k += blockDim.x) pk[k] = kAoEmpty;
+  int al[2], ds[2];  // alive / datastore row of slots tid and tid + 256, loaded ahead of the barrier
+#pragma unroll
+  for (int u = 0; u < 2; u++) {
+    const int s = tid + 256 * u;
+    al[u] = s < S ? E[F_ALIVE * S + s] : 0;
+    ds[u] = s < S ? E[F_DS_ROW * S + s] : 0;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < 2; u++) {
+    const int s = tid + 256 * u;
+    if (al[u] && (unsigned)(ds[u] - 1) < (unsigned)S) {
+      const bool player = s < P;
+      const bool immune = player && T[F_TIME_ALIVE * Sp + s] < p.spawn_immunity;
+      const bool danger = T[F_NPC_TYPE * Sp + s] > 1;
+      pk[ds[u] - 1] = (uint32_t)s | (uint32_t)(uint16_t)T[F_ROW * Sp + s] << 10 |
+                      (uint32_t)(uint16_t)T[F_COL * Sp + s] << 18 | (immune ? 1u << 26 : 0u) |
+                      (danger ? 1u << 27 : 0u) | (player ? 1u << 28 : 0u);
+    }
+  }
+  __syncthreads();
+}
+
+// Entity.Query.window: ascending datastore rows within L-inf <= kVision; the first kNObs packed
+// words go to visw. Returns the in-window count (uncapped).
+__device__ __forceinline__ int ao_compact(const uint32_t (&pr)[kAoRows], int S, int r, int c, uint32_t* visw) {
+  int nvis = 0;
+#pragma unroll
+  for (int i = 0; i < kAoRows; i++) {
+    if (64 * i >= S) break;
+    const uint32_t x = pr[i];
+    const bool in = x != kAoEmpty && linf(r, c, ao_row(x), ao_col(x)) <= kVision;
+    const uint64_t b = __ballot(in);
+    const int pos = nvis + __popcll(b & lanes_below());
+    if (in && pos < kNObs) visw[pos] = x;
+    nvis += __popcll(b);
+  }
+  return nvis;
+}
+
+// Passability of the 5 Move targets from the window materials (tile t in lane t & 63 of wm[t >> 6];
+// the centre's 4 neighbours are all in wm[1])
+__device__ __forceinline__ uint32_t ao_move_bits(uint32_t wm1) {
+  uint32_t b = 0u;
+#pragma unroll
+  for (int d = 0; d < 5; d++) {
+    const int t = (kVision + dir_dr(d)) * 15 + kVision + dir_dc(d);
+    if (!impassable((int)__builtin_amdgcn_readlane((int)wm1, t - 64))) b |= 1u << d;
+  }
+  return b;
+}
+
+// The 11 ActionTargets sections other than Buy.MarketItem as wave-uniform bit fields (SPEC §8,
+// §9, §13 edits): bit k = entry k of the section.
+struct AoSections {
+  uint64_t s0, s1[2], s3, s4, s5[2], s6[2], s7[2], s8, s9, s10[2], s11;
+};
+struct AoAgent {
+  int a, r, c, gold, aid, nv, ninv, prev_price;
+  uint32_t mv;
+};
+template <bool kWrap>
+__device__ __forceinline__ AoSections ao_sections(const ObsParams& p, const int16_t* T, int Sp, const uint32_t* visw,
+                                                 const AoAgent& g, uint2 it) {
+  const bool combat = (p.systems & NMMO_SYS_COMBAT) != 0;
+  const bool item = (p.systems & NMMO_SYS_ITEM) != 0;
+  const bool exch = item && (p.systems & NMMO_SYS_EXCHANGE) != 0;
+  const bool no_give = kWrap && (p.wflags & kWrapObsNoGive);
+  const bool no_danger = kWrap && (p.wflags & kWrapObsNoDangerous);
+  const int lane = lane_id();
+  AoSections x;
+  // over the visible rows: 1 AttackTarget, 5 GiveTarget, 7 GoldTarget (+ noop k = kNObs)
+  x.s1[0] = x.s1[1] = x.s5[0] = x.s5[1] = x.s7[0] = x.s7[1] = 0ull;
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    if (64 * h >= g.nv) break;
+    const int k = 64 * h + lane;
+    bool tgt = false, st = false;
+    if (k < g.nv) {
+      const uint32_t w = visw[k];
+      const int q = ao_slot(w);
+      tgt = combat && q != g.a && linf(g.r, g.c, ao_row(w), ao_col(w)) <= 3 && !((w >> 26) & 1u) &&
+            !(no_danger && ((w >> 27) & 1u));
+      st = ((w >> 28) & 1u) && q != g.a && ao_row(w) == g.r && ao_col(w) == g.c;
+    }
+    x.s1[h] = __ballot(tgt);
+    const uint64_t sb = __ballot(st);
+    if (item && !no_give) x.s5[h] = sb;
+    if (exch && !no_give) x.s7[h] = sb;
+  }
+  x.s1[1] |= 1ull << (kNObs - 64);
+  x.s5[1] |= 1ull << (kNObs - 64);
+  x.s7[1] |= 1ull << (kNObs - 64);
+  // over the inventory (lane k holds slot k's item word): 3 Destroy, 4 GiveItem, 9 SellItem,
+  // 11 Use (+ noop k = kInv)
+  const bool have = lane < g.ninv;
+  const bool fr = have && !it_equipped(it) && !it_price(it);
+  const uint64_t bfr = __ballot(fr);
+  x.s3 = (item ? bfr : 0ull) | 1ull << kInv;
+  x.s4 = (item && !no_give ? bfr : 0ull) | 1ull << kInv;
+  x.s9 = (exch ? __ballot(have && !it_equipped(it)) : 0ull) | 1ull << kInv;
+  x.s11 = (item ? __ballot(have && item_usable(T, Sp, g.a, it)) : 0ull) | 1ull << kInv;
+  // closed forms: 0 Style, 6 GoldPrice (k < gold), 8 Move, 10 SellPrice (all but the wrapper's
+  // last price)
+  x.s0 = combat ? low_bits(kSecN[0]) : 0ull;
+  x.s6[0] = x.s6[1] = x.s10[0] = x.s10[1] = 0ull;
+  if (exch) {
+    const int ng = no_give ? min(g.gold, 1) : min(g.gold, kSecN[6]);
+    x.s6[0] = low_bits(ng);
+    x.s6[1] = low_bits(ng - 64);
+    x.s10[0] = low_bits(kSecN[10]);
+    x.s10[1] = low_bits(kSecN[10] - 64);
+    if constexpr (kWrap) {
+      const int pp = g.prev_price;
+      if ((p.wflags & kWrapObsPrice) && pp >= 0 && pp < kSecN[10]) x.s10[pp >> 6] &= ~(1ull << (pp & 63));
+    }
+  }
+  x.s8 = g.mv;
+  return x;
+}
+
+// The sections into a bit image: kFlat = flat entry order (1,586 bits, Buy.MarketItem left 0),
+// else the wire order (561 bits)
+template <bool kFlat, int kW>
+__device__ __forceinline__ void ao_image(const AoSections& x, uint32_t (&img)[kW]) {
+#pragma unroll
+  for (int d = 0; d < kW; d++) img[d] = 0u;
+#define AO_PUT(k, lo, hi) put_field<kFlat ? sec_flat(k) : sec_wire(k), kSecN[k], kW>(img, lo, hi)
+  AO_PUT(0, x.s0, 0ull);
+  AO_PUT(1, x.s1[0], x.s1[1]);
+  AO_PUT(3, x.s3, 0ull);
+  AO_PUT(4, x.s4, 0ull);
+  AO_PUT(5, x.s5[0], x.s5[1]);
+  AO_PUT(6, x.s6[0], x.s6[1]);
+  AO_PUT(7, x.s7[0], x.s7[1]);
+  AO_PUT(8, x.s8, 0ull);
+  AO_PUT(9, x.s9, 0ull);
+  AO_PUT(10, x.s10[0], x.s10[1]);
+  AO_PUT(11, x.s11, 0ull);
+#undef AO_PUT
+}
+
+}  // namespace nmmo

@@ -127,6 +127,8 @@ hipError_t launch_wire_unpack(const uint8_t* wire, uint8_t* native, int n, int P
 hipError_t launch_wire_header(const ObsParams& p, hipStream_t s);
 // NMMO_OBS_WIRE obs gather (wire_obs.hip): header pre-pass + wire_obs_kernel
 hipError_t launch_wire_obs(const ObsParams& p, hipStream_t s);
+// NMMO_OBS_NATIVE obs gather (native_obs.hip)
+hipError_t launch_native_obs(const ObsParams& p, hipStream_t s);
 // header + record-head consistency of a wire buffer; bits into *status (0 = valid)
 hipError_t launch_wire_check(const uint8_t* wire, int n, int P, const int64_t* expect_total, int* status,
                              hipStream_t s);

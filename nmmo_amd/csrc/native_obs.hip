@@ -1,0 +1,253 @@
+// native_obs.hip — NMMO_OBS_NATIVE: the per-agent observation gather in the nmmo-dtype layout
+// of SPEC.md §8b (9,552 B per agent + the env's 32 KB Market), for learners that keep nmmo's
+// dtypes (the flat float32 rows are nmmo_expand_obs of it, bit-identical).
+//
+// Staging, window compaction and the ActionTargets bit fields are agent_obs.h's (shared with
+// the wire kernel). Per agent wave: the 1,586 u8 ActionTargets come from one 1,600-bit image
+// held one dword per lane (the 11 uniform sections OR-ed into their lanes, Buy.MarketItem's 32
+// entries per lane from the env's listings staged as price | owner << 8), expanded 16 bits ->
+// 16 bytes per lane (two multiply-masks per dword) into 100 16-B stores; the int16 part goes out
+// as dword stores (Entity row pairs are 31 dwords; Inventory 96 dwords; Tile + task index + pad
+// 341 dwords) and one 16-B zero run for the unseen Entity rows. Nothing of an agent passes
+// through LDS but its visible rows' packed words and its window materials.
+#include "agent_obs.h"
+
+namespace nmmo {
+
+// LDS: agent_obs.h's entity staging | listings (price | owner << 8, u16) | per-wave visible rows
+// | per-wave window materials. 31.8 KB at S = 384: 5 workgroups per CU.
+__host__ __device__ inline size_t no_lds_bytes(int S) {
+  return ao_entity_lds(S) + (size_t)NMMO_MARKET_ROWS * 2 + (size_t)kAoWaves * (128 * 4 + 256);
+}
+constexpr int kNoEntity = 2, kNoInv = kNoEntity + kNObs * NMMO_N_ENTITY_COLS, kNoTile = kNoInv + kInv * 16,
+              kNoTask = kNoTile + 225 * 3;  // int16 offsets in the int16 part (SPEC §8b)
+static_assert(kNoTask < NMMO_NATIVE_I16 && (kNoTile & 1) == 0 && (NMMO_NATIVE_I16 & 1) == 0 &&
+                  NMMO_NATIVE_MASK_BYTES % 16 == 0 && NMMO_NATIVE_ROW_BYTES % 16 == 0,
+              "native layout");
+constexpr int kNoImgWords = NMMO_NATIVE_MASK_BYTES / 32;  // 50: the mask image, one dword per lane
+
+template <bool kWrap>
+__global__ void __launch_bounds__(256) native_obs_kernel(ObsParams p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int S = p.S, P = p.P, Sp = ao_stride(S);
+  int16_t* T = reinterpret_cast<int16_t*>(smem);
+  uint32_t* pk = reinterpret_cast<uint32_t*>(smem + ao_entity_lds(S) - (size_t)(kMaxSlots + 64) * 4);
+  uint16_t* mpo = reinterpret_cast<uint16_t*>(pk + kMaxSlots + 64);           // [1024] price | owner << 8
+  uint32_t* visw_all = reinterpret_cast<uint32_t*>(mpo + NMMO_MARKET_ROWS);   // [4][128]
+  uint8_t* wmat_all = reinterpret_cast<uint8_t*>(visw_all + kAoWaves * 128);  // [4][256]
+  const int e = blockIdx.x, g = blockIdx.y, tid = threadIdx.x, lane = lane_id();
+  const int w = __builtin_amdgcn_readfirstlane(wave_id());
+  const int nm = min(max(p.mcount[e], 0), NMMO_MARKET_ROWS);
+  if (p.wmcount && g == 0 && tid == 0) p.wmcount[e] = nm;  // nmmo_wire_pack reads this launch's count
+  for (int j = tid; j < nm; j += blockDim.x) {  // end-of-tick listings, ascending row
+    const int v = p.mlist[(size_t)e * NMMO_MARKET_ROWS + j];
+    const int own = (v >> 16) & 255, slot = (v >> 24) & 15;
+    mpo[j] = (uint16_t)(it_price(p.items[((size_t)e * P + own) * kInv + slot]) | own << 8);
+  }
+  ao_stage(p, e, T, pk);  // (publishes mpo too)
+
+  uint8_t* nenv = p.nat + (size_t)e * ((size_t)P * NMMO_NATIVE_ROW_BYTES + NMMO_NATIVE_MARKET_BYTES);
+  if (g == 0) {  // the env's Market (1,024 rows of 16 int16), once per env
+    uint4* mk = reinterpret_cast<uint4*>(nenv + (size_t)P * NMMO_NATIVE_ROW_BYTES);
+    for (int k = tid; k < NMMO_MARKET_ROWS; k += blockDim.x) {
+      uint32_t q[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+      if (k < nm) {
+        const int v = p.mlist[(size_t)e * NMMO_MARKET_ROWS + k];
+        const int own = (v >> 16) & 255, slot = (v >> 24) & 15;
+        const uint2 wd = p.items[((size_t)e * P + own) * kInv + slot];
+#pragma unroll
+        for (int i = 0; i < 8; i++)
+          q[i] = i16pack((int)item_col(wd, own + 1, 2 * i), (int)item_col(wd, own + 1, 2 * i + 1));
+      }
+      mk[2 * k] = make_uint4(q[0], q[1], q[2], q[3]);
+      mk[2 * k + 1] = make_uint4(q[4], q[5], q[6], q[7]);
+    }
+  }
+
+  uint32_t pr[kAoRows];  // this lane's datastore rows 1 + lane + 64 i
+#pragma unroll
+  for (int i = 0; i < kAoRows; i++) pr[i] = pk[lane + 64 * i];
+  uint32_t* visw = visw_all + w * 128;
+  uint8_t* wmat = wmat_all + w * 256;
+  const uint8_t* mat = p.mat + (size_t)e * kTiles;
+  const int16_t* E = p.ent + (size_t)e * NMMO_NF * S;
+  const int tick = p.env[(size_t)e * NMMO_NE + E_TICK];
+  const bool exch = (p.systems & NMMO_SYS_ITEM) && (p.systems & NMMO_SYS_EXCHANGE);
+
+  const int per_wave = (kAoAgents + kAoWaves - 1) / kAoWaves;
+  const int abase = g * kAoAgents + w;
+  int my_task = 0, my_prev = -1, my_alive = 0;  // lane j: agent abase + 4 j
+  if (lane < per_wave && abase + kAoWaves * lane < P) {
+    const int aj = abase + kAoWaves * lane;
+    const size_t ai = (size_t)e * P + aj;
+    my_task = p.assign[ai];
+    my_alive = E[F_ALIVE * S + aj];
+    if constexpr (kWrap)
+      if (p.ws) my_prev = p.ws[ai].prev_price;
+  }
+  uint2 iv = make_uint2(0u, 0u);
+  uint32_t wm[4] = {0u, 0u, 0u, 0u};
+  auto prefetch = [&](int a) {
+    const int r = T[F_ROW * Sp + a], c = T[F_COL * Sp + a];
+    iv = lane < kInv ? p.items[((size_t)e * P + a) * kInv + lane] : make_uint2(0u, 0u);
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const int t = lane + 64 * i;
+      wm[i] = t < 225 ? mat[(r + t / 15 - kVision) * kSize + c + t % 15 - kVision] : 0u;
+    }
+  };
+  auto alive = [&](int j) { return j < per_wave && __builtin_amdgcn_readlane(my_alive, j) != 0; };
+  if (alive(0)) prefetch(abase);
+
+  for (int j = 0; j < per_wave; j++) {
+    const int a = abase + kAoWaves * j;
+    if (a >= P) break;
+    uint8_t* nrow = nenv + (size_t)a * NMMO_NATIVE_ROW_BYTES;
+    if (!alive(j)) {  // not in the realm: a zero row
+      if (alive(j + 1)) prefetch(a + kAoWaves);
+      if (p.wcount && lane == 0) p.wcount[(size_t)e * P + a] = 0;
+      uint4* z = reinterpret_cast<uint4*>(nrow);
+      for (int i = lane; i < NMMO_NATIVE_ROW_BYTES / 16; i += 64) z[i] = make_uint4(0u, 0u, 0u, 0u);
+      continue;
+    }
+    const int r = __builtin_amdgcn_readfirstlane(T[F_ROW * Sp + a]);
+    const int c = __builtin_amdgcn_readfirstlane(T[F_COL * Sp + a]);
+    const int gold = __builtin_amdgcn_readfirstlane(T[F_GOLD * Sp + a]);
+    const int aid = __builtin_amdgcn_readfirstlane(T[F_ID * Sp + a]);
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+      if (lane + 64 * i < 225) wmat[lane + 64 * i] = (uint8_t)wm[i];
+    const uint2 it = iv;  // this agent's item word (lanes 0..11)
+    const uint32_t mv = ao_move_bits(wm[1]);
+    const int ninv = __builtin_ctzll(~__ballot(lane < kInv && it_type(it) != 0));  // occupied prefix
+    if (alive(j + 1)) prefetch(a + kAoWaves);  // the next agent's loads, ahead of the stores
+
+    const int nv = min(ao_compact(pr, S, r, c, visw), kNObs);
+    if (p.wcount && lane == 0) p.wcount[(size_t)e * P + a] = (uint16_t)wire_count_word(nv, ninv);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+    // ActionTargets: the 1,600-bit flat image, dword d in lane d
+    {
+      AoAgent ag;
+      ag.a = a;
+      ag.r = r;
+      ag.c = c;
+      ag.gold = gold;
+      ag.aid = aid;
+      ag.nv = nv;
+      ag.ninv = ninv;
+      ag.prev_price = kWrap ? __builtin_amdgcn_readlane(my_prev, j) : -1;
+      ag.mv = mv;
+      uint32_t img[kNoImgWords];
+      ao_image<true>(ao_sections<kWrap>(p, T, Sp, visw, ag, it), img);
+      img[(kWireBuyLo + NMMO_MARKET_ROWS) / 32] |= 1u << ((kWireBuyLo + NMMO_MARKET_ROWS) & 31);  // Buy noop
+      uint32_t x = 0u;
+#pragma unroll
+      for (int d = 0; d < kNoImgWords; d++) x |= lane == d ? img[d] : 0u;
+      // Buy.MarketItem entries k = 32 d - 104 .. + 31 (a multiple of 8): listing k is buyable
+      // with exchange on, k < listings, price <= gold and not the agent's own
+      const int kb = 32 * lane - kWireBuyLo;
+      if (exch && kb + 32 > 0 && kb < nm) {
+#pragma unroll 1
+        for (int q8 = 0; q8 < 4; q8++) {
+          const int k = kb + 8 * q8;
+          if (k < 0 || k >= nm) continue;
+          const uint4 v = reinterpret_cast<const uint4*>(mpo)[k >> 3];
+          const uint32_t pw[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (int i = 0; i < 8; i++) {
+            const uint32_t po = (pw[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
+            if (k + i < nm && (int)(po & 255u) <= gold && (int)(po >> 8) != a) x |= 1u << (8 * q8 + i);
+          }
+        }
+      }
+      // 16 entries per lane -> 16 bytes: entry b of a nibble n lands in byte b by n * 0x204081
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        const int q = 64 * h + lane;  // 16-B chunk
+        const uint32_t b16 = ((uint32_t)__shfl((int)x, q >> 1) >> (16 * (q & 1))) & 0xFFFFu;
+        if (q < NMMO_NATIVE_MASK_BYTES / 16) {
+          uint32_t o[4];
+#pragma unroll
+          for (int i = 0; i < 4; i++) o[i] = (((b16 >> (4 * i)) & 15u) * 0x00204081u) & 0x01010101u;
+          reinterpret_cast<uint4*>(nrow)[q] = make_uint4(o[0], o[1], o[2], o[3]);
+        }
+      }
+    }
+    // int16 part: AgentId, CurrentTick | Entity 100 x 31 | Inventory 12 x 16 | Tile 225 x 3 | task
+    // index | zero pad (SPEC §8b)
+    uint32_t* d32 = reinterpret_cast<uint32_t*>(nrow + NMMO_NATIVE_MASK_BYTES);
+    if (lane == 0) d32[0] = i16pack(aid, tick);
+    {  // four Entity rows per pass: a row pair is 31 dwords, lanes 0-30 the pair (k, k + 1), lanes
+       // 32-62 the pair (k + 2, k + 3); the rows past the visible ones (rounded up to the pass)
+       // are one zero run
+      const int i = lane & 31, hp = lane >> 5;
+      const int c0 = 2 * i, c1 = 2 * i + 1;
+      const int r0 = c0 >= NMMO_N_ENTITY_COLS, r1 = c1 >= NMMO_N_ENTITY_COLS;
+      const int f0 = c0 - r0 * NMMO_N_ENTITY_COLS, f1 = c1 - r1 * NMMO_N_ENTITY_COLS;
+      const int nv4 = (nv + 3) & ~3;
+      uint32_t* de = d32 + kNoEntity / 2;
+#pragma unroll 1
+      for (int k0 = 0; k0 < nv4; k0 += 4) {
+        const int k = k0 + 2 * hp, ka = k + r0, kb = k + r1;
+        if (i < NMMO_N_ENTITY_COLS) {
+          const int lo = ka < nv ? T[f0 * Sp + ao_slot(visw[ka])] : 0;
+          const int hi = kb < nv ? T[f1 * Sp + ao_slot(visw[kb])] : 0;
+          de[(k >> 1) * NMMO_N_ENTITY_COLS + i] = i16pack(lo, hi);
+        }
+      }
+      uint8_t* zb = nrow + NMMO_NATIVE_MASK_BYTES + 2 * (kNoEntity + nv4 * NMMO_N_ENTITY_COLS);
+      uint8_t* ze = nrow + NMMO_NATIVE_MASK_BYTES + 2 * kNoInv;
+      // [zb, ze): 4-B aligned; dwords up to 16-B alignment, then 16-B stores, then dwords
+      const int head = (int)(((16 - (reinterpret_cast<uintptr_t>(zb) & 15)) & 15) >> 2);
+      const int nz = (int)(ze - zb) >> 2;
+      if (lane < min(head, nz)) reinterpret_cast<uint32_t*>(zb)[lane] = 0u;
+      const int body = (nz - head) >> 2;
+      uint4* z4 = reinterpret_cast<uint4*>(zb + 4 * head);
+      for (int q = lane; q < body; q += 64) z4[q] = make_uint4(0u, 0u, 0u, 0u);
+      const int t0 = head + 4 * body;
+      if (t0 + lane < nz) reinterpret_cast<uint32_t*>(zb)[t0 + lane] = 0u;
+    }
+    // Inventory: 96 dwords (item q = i >> 3, columns 2i & 15, +1), the item word from lane q
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const int i = 64 * h + lane;
+      const int q = min(i >> 3, kInv - 1);
+      const uint2 iw = make_uint2((uint32_t)__shfl((int)it.x, q), (uint32_t)__shfl((int)it.y, q));
+      if (i < kInv * 8) {
+        const int cc = (2 * i) & 15;
+        d32[kNoInv / 2 + i] =
+            (i >> 3) < ninv ? i16pack((int)item_col(iw, aid, cc), (int)item_col(iw, aid, cc + 1)) : 0u;
+      }
+    }
+    // Tile (row, col, material per window tile) | task index | zero pad, as dwords
+    {
+      const int task = __builtin_amdgcn_readlane(my_task, j);
+      auto half = [&](int h) -> int {  // int16 h of the part starting at kNoTile
+        if (h < 225 * 3) {
+          const int t = h / 3, comp = h - 3 * t;
+          return comp == 0 ? r + t / 15 - kVision : comp == 1 ? c + t % 15 - kVision : (int)wmat[t];
+        }
+        return h == 225 * 3 ? task : 0;
+      };
+      constexpr int kTileDwords = (NMMO_NATIVE_I16 - kNoTile) / 2;
+      for (int i = lane; i < kTileDwords; i += 64) d32[kNoTile / 2 + i] = i16pack(half(2 * i), half(2 * i + 1));
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the next agent reuses visw / wmat
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+}
+
+hipError_t launch_native_obs(const ObsParams& p, hipStream_t stream) {
+  if (p.S % 8 || p.S > kMaxSlots || p.P > 128 || !p.nat || !ao_layout_ok(p)) return hipErrorInvalidValue;
+  const dim3 grid(p.n_envs, (p.P + kAoAgents - 1) / kAoAgents), block(64 * kAoWaves);
+  const size_t lds = no_lds_bytes(p.S);
+  if (p.wflags) hipLaunchKernelGGL(native_obs_kernel<true>, grid, block, lds, stream, p);
+  else hipLaunchKernelGGL(native_obs_kernel<false>, grid, block, lds, stream, p);
+  return hipGetLastError();
+}
+
+}  // namespace nmmo

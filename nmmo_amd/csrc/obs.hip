@@ -19,21 +19,14 @@ namespace nmmo {
 
 constexpr int kObsAgentsPerBlock = 16;
 constexpr int kObsWaves = 4;
-// agents per wave of an obs_kernel launch with `gy` workgroups per env
-__host__ __device__ inline int obs_per_wave(int P, int gy) { return (P + gy * kObsWaves - 1) / (gy * kObsWaves); }
 constexpr int kObsFields = F_DS_ROW + 1;  // 0..30 obs columns, alive, ds_row
-// output layouts of obs_kernel (NMMO_OBS_WIRE has its own kernel, wire_obs.hip)
-constexpr int kModeFlat = 0, kModeNative = 1;
-
 // LDS: entity fields | row->slot | per-wave visible list | per-wave inventory | per-wave 15x15
-// window materials | market listings (price | owner << 8, 2 B per listing; flat rows also the
-// listed item words, 8 B) | native: per-wave ActionTargets bytes. 38.8 KB (native) at S = 384:
-// 4 workgroups (16 waves) per CU.
-__host__ __device__ inline size_t obs_lds_bytes(int S, int mode) {
-  const size_t base = (((size_t)kObsFields * S * 2 + 15) & ~(size_t)15) + (((size_t)(S + 1) * 2 + 15) & ~(size_t)15) +
-                      (size_t)kObsWaves * 128 * 2 + (size_t)kObsWaves * kInv * 8 + (size_t)kObsWaves * 256;
-  if (mode == kModeFlat) return base + (size_t)NMMO_MARKET_ROWS * 10;
-  return base + (size_t)NMMO_MARKET_ROWS * 2 + (size_t)kObsWaves * NMMO_NATIVE_MASK_BYTES;
+// window materials | market listings (item words, 8 B, then price | owner << 8, 2 B).
+// (The native and wire layouts have their own kernels: native_obs.hip, wire_obs.hip.)
+__host__ __device__ inline size_t obs_lds_bytes(int S) {
+  return (((size_t)kObsFields * S * 2 + 15) & ~(size_t)15) + (((size_t)(S + 1) * 2 + 15) & ~(size_t)15) +
+         (size_t)kObsWaves * 128 * 2 + (size_t)kObsWaves * kInv * 8 + (size_t)kObsWaves * 256 +
+         (size_t)NMMO_MARKET_ROWS * 10;
 }
 
 // Plain (temporal) stores. Measured on MI355X (same-box A/B): __builtin_nontemporal_store
@@ -138,19 +131,9 @@ __device__ __forceinline__ bool mask_value(const ObsParams& p, const int16_t* T,
   return v;
 }
 
-// Section kSec of the ActionTargets as u8 into a wave's LDS mask image: the section is a
+// Section kSec of the ActionTargets as float32 0/1 straight into a flat row: the section is a
 // template constant, so mask_section / mask_value fold to straight-line code (the generic
 // (section, chunk) loop spent ~1.3k scalar and branch instructions per agent on the dispatch).
-template <int kSec, bool kWrap>
-__device__ __forceinline__ void mask_sec_u8(const ObsParams& p, const int16_t* T, int S, const int16_t* vis,
-                                            const uint2* inv, const uint16_t* mpo, int nm, const MaskCtx& m,
-                                            uint8_t* mb) {
-  int lo, n;
-  mask_section(p, kSec, lo, n);
-  for (int k = lane_id(); k < n; k += 64) mb[lo + k] = mask_value<kWrap>(p, T, S, vis, inv, mpo, nm, m, kSec, k) ? 1 : 0;
-}
-
-// The same for a flat row: section kSec as float32 0/1 straight into the row.
 template <int kSec, bool kWrap>
 __device__ __forceinline__ void mask_sec_f32(const ObsParams& p, const int16_t* T, int S, const int16_t* vis,
                                              const uint2* inv, const uint16_t* mpo, int nm, const MaskCtx& m,
@@ -181,32 +164,26 @@ __device__ __forceinline__ uint32_t move_bits(uint32_t wm1) {
 constexpr int kTaskRegs = 32;  // Task embedding dwords per lane held in registers (2,048 per row)
 
 // kWrap: the wrapper's observation() edits are compiled in (SPEC §13).
-// kMode: kModeFlat = pufferlib's float32 row; kModeNative = the nmmo-dtype layout of SPEC §8b
-// (u8 masks, int16 fields, Market once per env, task index): ~10x fewer bytes per agent.
-template <bool kWrap, int kMode>
+template <bool kWrap>
 __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
-  constexpr bool kNative = kMode == kModeNative;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int S = p.S;
   int16_t* T = reinterpret_cast<int16_t*>(smem);
   int16_t* rowslot = reinterpret_cast<int16_t*>(smem + (((size_t)kObsFields * S * 2 + 15) & ~(size_t)15));
   int16_t* vis_all = rowslot + ((((size_t)(S + 1) * 2 + 15) & ~(size_t)15) / 2);
   uint2* inv_all = reinterpret_cast<uint2*>(vis_all + kObsWaves * 128);
-  uint2* mitem = inv_all + kObsWaves * kInv;  // flat only: listed item words
-  uint16_t* mpo = reinterpret_cast<uint16_t*>(kNative ? mitem : mitem + NMMO_MARKET_ROWS);  // price | owner << 8
+  uint2* mitem = inv_all + kObsWaves * kInv;  // listed item words
+  uint16_t* mpo = reinterpret_cast<uint16_t*>(mitem + NMMO_MARKET_ROWS);  // price | owner << 8
   uint8_t* wmat_all = reinterpret_cast<uint8_t*>(mpo + NMMO_MARKET_ROWS);  // per-wave 15x15 materials
-  uint8_t* mask_all = wmat_all + kObsWaves * 256;  // native: per-wave ActionTargets bytes (16-B aligned)
   const int e = blockIdx.x, g = blockIdx.y;
   const int tid = threadIdx.x;
   const int nm = p.mcount[e];
-  if constexpr (kMode == kModeNative)
-    if (p.wmcount && g == 0 && tid == 0) p.wmcount[e] = nm;  // nmmo_wire_pack reads this launch's count
   for (int j = tid; j < nm; j += blockDim.x) {  // end-of-tick listings, ascending row
     const int v = p.mlist[(size_t)e * NMMO_MARKET_ROWS + j];
     const int own = (v >> 16) & 255, slot = (v >> 24) & 15;
     const uint2 wd = p.items[((size_t)e * p.P + own) * kInv + slot];
     mpo[j] = (uint16_t)(it_price(wd) | own << 8);
-    if constexpr (!kNative) mitem[j] = wd;
+    mitem[j] = wd;
   }
   {
     const int16_t* src = p.ent + (size_t)e * NMMO_NF * S;
@@ -225,24 +202,6 @@ __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
     if (T[F_ALIVE * S + s]) rowslot[T[F_DS_ROW * S + s]] = (int16_t)s;
   __syncthreads();
 
-  if constexpr (kNative) {  // the env's Market, once per env (the y == 0 workgroup)
-    if (g == 0) {  // one listing row (16 int16 = two 16-B stores) per thread
-      uint4* mk = reinterpret_cast<uint4*>(p.nat + (size_t)e * native_env_bytes(p.P) + (size_t)p.P * NMMO_NATIVE_ROW_BYTES);
-      for (int k = tid; k < NMMO_MARKET_ROWS; k += blockDim.x) {
-        uint32_t q[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
-        if (k < nm) {
-          const int v = p.mlist[(size_t)e * NMMO_MARKET_ROWS + k];
-          const int own = (v >> 16) & 255, slot = (v >> 24) & 15;
-          const uint2 wd = p.items[((size_t)e * p.P + own) * kInv + slot];
-#pragma unroll
-          for (int i = 0; i < 8; i++)
-            q[i] = i16pack((int)item_col(wd, own + 1, 2 * i), (int)item_col(wd, own + 1, 2 * i + 1));
-        }
-        mk[2 * k] = make_uint4(q[0], q[1], q[2], q[3]);
-        mk[2 * k + 1] = make_uint4(q[4], q[5], q[6], q[7]);
-      }
-    }
-  }
   const int lane = lane_id(), w = wave_id();
   int16_t* vis = vis_all + w * 128;
   uint2* inv = inv_all + w * kInv;
@@ -255,8 +214,8 @@ __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
   m.no_give = kWrap && (p.wflags & kWrapObsNoGive);
   // this wave's agents: a_j = g * 16 + w + 4 j; lane j holds a_j's task index and (wrapper) last
   // Sell price, loaded before any store
-  const int kPerWave = obs_per_wave(p.P, gridDim.y);
-  const int abase = g * kPerWave * kObsWaves + w;
+  constexpr int kPerWave = kObsAgentsPerBlock / kObsWaves;
+  const int abase = g * kObsAgentsPerBlock + w;
   int my_task = 0, my_prev = -1;
   if (lane < kPerWave && abase + kObsWaves * lane < p.P) {
     const size_t ai = (size_t)e * p.P + abase + kObsWaves * lane;
@@ -297,12 +256,10 @@ __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
       const int t = lane + 64 * i;
       wm[i] = t < 225 ? mat[(r + t / 15 - kVision) * kSize + c + t % 15 - kVision] : 0u;
     }
-    if constexpr (!kNative) {
-      if (treg) {
-        const float* temb = p.task + (size_t)__builtin_amdgcn_readlane(my_task, j) * p.task_dim + lane;
+    if (treg) {
+      const float* temb = p.task + (size_t)__builtin_amdgcn_readlane(my_task, j) * p.task_dim + lane;
 #pragma unroll
-        for (int i = 0; i < kTaskRegs; i++) tv[i] = temb[64 * i];
-      }
+      for (int i = 0; i < kTaskRegs; i++) tv[i] = temb[64 * i];
     }
   };
   auto alive = [&](int j) {
@@ -311,100 +268,13 @@ __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
   };
   if (alive(0)) prefetch(abase, 0);
 
-  if constexpr (!kNative) {
-    for (int j = 0; j < kPerWave; j++) {
-      const int a = abase + kObsWaves * j;
-      if (a >= p.P) break;
-      float* row = p.obs + ((size_t)e * p.P + a) * p.elems;
-      if (!T[F_ALIVE * S + a]) {
-        if (alive(j + 1)) prefetch(a + kObsWaves, j + 1);  // ahead of this row's stores
-        wave_zero(row, 0, p.elems);
-        continue;
-      }
-      m.a = a;
-      m.r = T[F_ROW * S + a];
-      m.c = T[F_COL * S + a];
-      m.gold = T[F_GOLD * S + a];
-      m.nv = compact(m.r, m.c);
-      if (lane < kInv) inv[lane] = iv;
-#pragma unroll
-      for (int i = 0; i < 4; i++)
-        if (lane + 64 * i < 225) wmat[lane + 64 * i] = (uint8_t)wm[i];
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      m.ninv = inv_count(inv);
-      m.prev_price = kWrap ? __builtin_amdgcn_readlane(my_prev, j) : -1;
-      m.movebits = move_bits(wm[1]);
-      const int aid = T[F_ID * S + a];
-      // Task (from registers; a task_dim beyond kTaskRegs * 64 reads the rest directly)
-      {
-        const int k0 = treg ? kTaskRegs * 64 : 0;  // a shorter embedding is read in place
-        if (treg) {
-          float* dst = row + p.o_task + lane;
-#pragma unroll
-          for (int i = 0; i < kTaskRegs; i++) obs_st(&dst[64 * i], tv[i]);
-        }
-        const float* temb = p.task + (size_t)__builtin_amdgcn_readlane(my_task, j) * p.task_dim;
-        for (int k = k0 + lane; k < p.task_dim; k += 64) obs_st(&row[p.o_task + k], temb[k]);
-      }
-      // Tile (the window materials went to LDS with the inventory)
-      for (int k = lane; k < 225 * 3; k += 64) {
-        const int t = k / 3, comp = k - 3 * t;
-        const int tr = m.r + t / 15 - kVision, tc = m.c + t % 15 - kVision;
-        obs_st(&row[p.o_tile + k], comp == 0 ? (float)tr : comp == 1 ? (float)tc : (float)wmat[t]);
-      }
-      // the next agent's loads go out now, ahead of this row's remaining stores
-      if (alive(j + 1)) prefetch(a + kObsWaves, j + 1);
-      // ActionTargets, section by section
-      mask_sec_f32<0, kWrap>(p, T, S, vis, inv, mpo, nm, m, row);
-      mask_sec_f32<1, kWrap>(p, T, S, vis, inv, mpo, nm, m, row);
-      mask_sec_f32<2, kWrap>(p, T, S, vis, inv, mpo, nm, m, row);
-      mask_sec_f32<3, kWrap>(p, T, S, vis, inv, mpo, nm, m, row);
-      mask_sec_f32<4, kWrap>(p, T, S, vis, inv, mpo, nm, m, row);
-      mask_sec_f32<5, kWrap>(p, T, S, vis, inv, mpo, nm, m, row);
-      mask_sec_f32<6, kWrap>(p, T, S, vis, inv, mpo, nm, m, row);
-      mask_sec_f32<7, kWrap>(p, T, S, vis, inv, mpo, nm, m, row);
-      mask_sec_f32<8, kWrap>(p, T, S, vis, inv, mpo, nm, m, row);
-      mask_sec_f32<9, kWrap>(p, T, S, vis, inv, mpo, nm, m, row);
-      mask_sec_f32<10, kWrap>(p, T, S, vis, inv, mpo, nm, m, row);
-      mask_sec_f32<11, kWrap>(p, T, S, vis, inv, mpo, nm, m, row);
-      if (lane == 0) obs_st(&row[p.o_agent_id], (float)aid);
-      if (lane == 1) obs_st(&row[p.o_tick], (float)tick);
-      // Entity rows: two per pass (lanes 0-30 row k, lanes 32-62 row k + 1: 62 contiguous floats),
-      // the rows past the visible ones as one zero run
-      {
-        const int f = lane & 31, half = lane >> 5;
-        const int nv2 = (m.nv + 1) & ~1;
-#pragma unroll 1
-        for (int k0 = 0; k0 < nv2; k0 += 2) {
-          const int k = k0 + half;
-          if (f < NMMO_N_ENTITY_COLS)
-            obs_st(&row[p.o_entity + k * NMMO_N_ENTITY_COLS + f], k < m.nv ? (float)T[f * S + vis[k]] : 0.f);
-        }
-        wave_zero(row, p.o_entity + nv2 * NMMO_N_ENTITY_COLS, p.o_entity + kNObs * NMMO_N_ENTITY_COLS);
-      }
-      // Inventory (own items, owner = self) and Market (env listings, ascending row)
-      for (int k = lane; k < kInv * 16; k += 64) {
-        const int q = k >> 4;
-        obs_st(&row[p.o_inventory + k], q < m.ninv ? item_col(inv[q], aid, k & 15) : 0.f);
-      }
-      for (int k = lane; k < nm * 16; k += 64)
-        obs_st(&row[p.o_market + k], item_col(mitem[k >> 4], (mpo[k >> 4] >> 8) + 1, k & 15));
-      wave_zero(row, p.o_market + nm * 16, p.o_task);
-      __builtin_amdgcn_wave_barrier();
-    }
-    return;
-  }
-
   for (int j = 0; j < kPerWave; j++) {
     const int a = abase + kObsWaves * j;
     if (a >= p.P) break;
-    uint8_t* nrow = p.nat + (size_t)e * native_env_bytes(p.P) + (size_t)a * NMMO_NATIVE_ROW_BYTES;
+    float* row = p.obs + ((size_t)e * p.P + a) * p.elems;
     if (!T[F_ALIVE * S + a]) {
-      if (alive(j + 1)) prefetch(a + kObsWaves, j + 1);
-      if (p.wcount && lane == 0) p.wcount[(size_t)e * p.P + a] = 0;
-      uint4* z = reinterpret_cast<uint4*>(nrow);
-      for (int i = lane; i < NMMO_NATIVE_ROW_BYTES / 16; i += 64) z[i] = make_uint4(0u, 0u, 0u, 0u);
+      if (alive(j + 1)) prefetch(a + kObsWaves, j + 1);  // ahead of this row's stores
+      wave_zero(row, 0, p.elems);
       continue;
     }
     m.a = a;
@@ -422,112 +292,72 @@ __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
     m.prev_price = kWrap ? __builtin_amdgcn_readlane(my_prev, j) : -1;
     m.movebits = move_bits(wm[1]);
     const int aid = T[F_ID * S + a];
-    if (p.wcount && lane == 0) p.wcount[(size_t)e * p.P + a] = (uint16_t)(0x8000 | m.nv | m.ninv << 7);
-    if (alive(j + 1)) prefetch(a + kObsWaves, j + 1);  // wm is in LDS now; next agent's loads
-    // u8 ActionTargets in flat order, then pad to NMMO_NATIVE_MASK_BYTES. Buy.MarketItem (1,025
-    // entries, the longest section): four entries per lane per dword store from one 8-B LDS read
-    // of the packed listings (the section starts dword-aligned in the SPEC §8b layout; the
-    // per-byte case of mask_value covers any other offset)
-    // (built in this wave's LDS, then written out with 16-B stores: 100 instead of ~40 byte-store
-    // instructions per row)
-    uint8_t* mb = mask_all + w * NMMO_NATIVE_MASK_BYTES;
-    const bool buy4 = (p.o_buy & 3) == 0;
-    if (buy4) {
-      uint32_t* b32 = reinterpret_cast<uint32_t*>(mb + p.o_buy);
-      for (int j4 = lane; j4 < NMMO_MARKET_ROWS / 4; j4 += 64) {
-        uint32_t v = 0u;
-        if (m.exch && 4 * j4 < nm) {
-          const uint2 q = *reinterpret_cast<const uint2*>(mpo + 4 * j4);
+    // Task (from registers; a task_dim beyond kTaskRegs * 64 reads the rest directly)
+    {
+      const int k0 = treg ? kTaskRegs * 64 : 0;  // a shorter embedding is read in place
+      if (treg) {
+        float* dst = row + p.o_task + lane;
 #pragma unroll
-          for (int b = 0; b < 4; b++) {
-            const uint32_t pw = ((b < 2 ? q.x : q.y) >> (16 * (b & 1))) & 0xFFFFu;
-            if (4 * j4 + b < nm && (int)(pw & 255u) <= m.gold && (int)(pw >> 8) != a) v |= 1u << (8 * b);
-          }
-        }
-        b32[j4] = v;
+        for (int i = 0; i < kTaskRegs; i++) obs_st(&dst[64 * i], tv[i]);
       }
-      if (lane == 0) mb[p.o_buy + NMMO_MARKET_ROWS] = 1;
+      const float* temb = p.task + (size_t)__builtin_amdgcn_readlane(my_task, j) * p.task_dim;
+      for (int k = k0 + lane; k < p.task_dim; k += 64) obs_st(&row[p.o_task + k], temb[k]);
     }
-    mask_sec_u8<0, kWrap>(p, T, S, vis, inv, mpo, nm, m, mb);
-    mask_sec_u8<1, kWrap>(p, T, S, vis, inv, mpo, nm, m, mb);
-    if (!buy4) mask_sec_u8<2, kWrap>(p, T, S, vis, inv, mpo, nm, m, mb);
-    mask_sec_u8<3, kWrap>(p, T, S, vis, inv, mpo, nm, m, mb);
-    mask_sec_u8<4, kWrap>(p, T, S, vis, inv, mpo, nm, m, mb);
-    mask_sec_u8<5, kWrap>(p, T, S, vis, inv, mpo, nm, m, mb);
-    mask_sec_u8<6, kWrap>(p, T, S, vis, inv, mpo, nm, m, mb);
-    mask_sec_u8<7, kWrap>(p, T, S, vis, inv, mpo, nm, m, mb);
-    mask_sec_u8<8, kWrap>(p, T, S, vis, inv, mpo, nm, m, mb);
-    mask_sec_u8<9, kWrap>(p, T, S, vis, inv, mpo, nm, m, mb);
-    mask_sec_u8<10, kWrap>(p, T, S, vis, inv, mpo, nm, m, mb);
-    mask_sec_u8<11, kWrap>(p, T, S, vis, inv, mpo, nm, m, mb);
-    if (lane < NMMO_NATIVE_MASK_BYTES - p.o_agent_id) mb[p.o_agent_id + lane] = 0;
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    for (int k = lane; k < NMMO_NATIVE_MASK_BYTES / 16; k += 64)
-      reinterpret_cast<uint4*>(nrow)[k] = reinterpret_cast<const uint4*>(mb)[k];
-    // int16 part: AgentId, CurrentTick, Entity 100x31, Inventory 12x16, Tile 225x3, task index,
-    // zero pads (SPEC §8b)
-    int16_t* d16 = reinterpret_cast<int16_t*>(nrow + NMMO_NATIVE_MASK_BYTES);
-    if (lane == 0) d16[0] = (int16_t)aid;
-    if (lane == 1) d16[1] = (int16_t)tick;
-    {  // four entity rows per pass as dwords: a row pair is 62 int16 = 31 dwords (dword-aligned:
-       // it starts 4 + 124 j bytes into the int16 part), lanes 0-30 the pair (k, k + 1), lanes
-       // 32-62 the pair (k + 2, k + 3); lane i packs int16 2i, 2i + 1 of its pair. The rows past
-       // the visible ones (rounded up to the pass) are one zero run.
-      const int i = lane & 31, pr = lane >> 5;
-      const int nv4 = (m.nv + 3) & ~3;
-      const int c0 = 2 * i, c1 = 2 * i + 1;  // pair positions: 0-30 the first row, 31-61 the second
-      const int r0 = c0 >= NMMO_N_ENTITY_COLS, r1 = c1 >= NMMO_N_ENTITY_COLS;
-      const int f0 = c0 - r0 * NMMO_N_ENTITY_COLS, f1 = c1 - r1 * NMMO_N_ENTITY_COLS;
-      uint32_t* d32 = reinterpret_cast<uint32_t*>(d16 + kNatEntity);
+    // Tile (the window materials went to LDS with the inventory)
+    for (int k = lane; k < 225 * 3; k += 64) {
+      const int t = k / 3, comp = k - 3 * t;
+      const int tr = m.r + t / 15 - kVision, tc = m.c + t % 15 - kVision;
+      obs_st(&row[p.o_tile + k], comp == 0 ? (float)tr : comp == 1 ? (float)tc : (float)wmat[t]);
+    }
+    // the next agent's loads go out now, ahead of this row's remaining stores
+    if (alive(j + 1)) prefetch(a + kObsWaves, j + 1);
+    // ActionTargets, section by section
+    mask_sec_f32<0, kWrap>(p, T, S, vis, inv, mpo, nm, m, row);
+    mask_sec_f32<1, kWrap>(p, T, S, vis, inv, mpo, nm, m, row);
+    mask_sec_f32<2, kWrap>(p, T, S, vis, inv, mpo, nm, m, row);
+    mask_sec_f32<3, kWrap>(p, T, S, vis, inv, mpo, nm, m, row);
+    mask_sec_f32<4, kWrap>(p, T, S, vis, inv, mpo, nm, m, row);
+    mask_sec_f32<5, kWrap>(p, T, S, vis, inv, mpo, nm, m, row);
+    mask_sec_f32<6, kWrap>(p, T, S, vis, inv, mpo, nm, m, row);
+    mask_sec_f32<7, kWrap>(p, T, S, vis, inv, mpo, nm, m, row);
+    mask_sec_f32<8, kWrap>(p, T, S, vis, inv, mpo, nm, m, row);
+    mask_sec_f32<9, kWrap>(p, T, S, vis, inv, mpo, nm, m, row);
+    mask_sec_f32<10, kWrap>(p, T, S, vis, inv, mpo, nm, m, row);
+    mask_sec_f32<11, kWrap>(p, T, S, vis, inv, mpo, nm, m, row);
+    if (lane == 0) obs_st(&row[p.o_agent_id], (float)aid);
+    if (lane == 1) obs_st(&row[p.o_tick], (float)tick);
+    // Entity rows: two per pass (lanes 0-30 row k, lanes 32-62 row k + 1: 62 contiguous floats),
+    // the rows past the visible ones as one zero run
+    {
+      const int f = lane & 31, half = lane >> 5;
+      const int nv2 = (m.nv + 1) & ~1;
 #pragma unroll 1
-      for (int k0 = 0; k0 < nv4; k0 += 4) {
-        const int k = k0 + 2 * pr;
-        if (i < NMMO_N_ENTITY_COLS) {
-          const int ka = k + r0, kb = k + r1;
-          const int lo = ka < m.nv ? T[f0 * S + vis[ka]] : 0, hi = kb < m.nv ? T[f1 * S + vis[kb]] : 0;
-          d32[(k >> 1) * NMMO_N_ENTITY_COLS + i] = i16pack(lo, hi);
-        }
+      for (int k0 = 0; k0 < nv2; k0 += 2) {
+        const int k = k0 + half;
+        if (f < NMMO_N_ENTITY_COLS)
+          obs_st(&row[p.o_entity + k * NMMO_N_ENTITY_COLS + f], k < m.nv ? (float)T[f * S + vis[k]] : 0.f);
       }
-      wave_zero_bytes(nrow, NMMO_NATIVE_MASK_BYTES + 2 * (kNatEntity + nv4 * NMMO_N_ENTITY_COLS),
-                      NMMO_NATIVE_MASK_BYTES + 2 * kNatInv);
+      wave_zero(row, p.o_entity + nv2 * NMMO_N_ENTITY_COLS, p.o_entity + kNObs * NMMO_N_ENTITY_COLS);
     }
+    // Inventory (own items, owner = self) and Market (env listings, ascending row)
     for (int k = lane; k < kInv * 16; k += 64) {
       const int q = k >> 4;
-      d16[kNatInv + k] = q < m.ninv ? (int16_t)(int)item_col(inv[q], aid, k & 15) : (int16_t)0;
+      obs_st(&row[p.o_inventory + k], q < m.ninv ? item_col(inv[q], aid, k & 15) : 0.f);
     }
-#pragma unroll 1
-    for (int i = 0; i < 4; i++) {
-      const int t = lane + 64 * i;
-      if (t < 225) {
-        const int tr = m.r + t / 15 - kVision, tc = m.c + t % 15 - kVision;
-        d16[kNatTile + 3 * t] = (int16_t)tr;
-        d16[kNatTile + 3 * t + 1] = (int16_t)tc;
-        d16[kNatTile + 3 * t + 2] = (int16_t)wmat[t];
-      }
-    }
-    if (lane == 0) d16[kNatTask] = (int16_t)__builtin_amdgcn_readlane(my_task, j);
-    else if (lane < NMMO_NATIVE_I16 - kNatTask) d16[kNatTask + lane] = 0;
+    for (int k = lane; k < nm * 16; k += 64)
+      obs_st(&row[p.o_market + k], item_col(mitem[k >> 4], (mpo[k >> 4] >> 8) + 1, k & 15));
+    wave_zero(row, p.o_market + nm * 16, p.o_task);
     __builtin_amdgcn_wave_barrier();
   }
 }
 
 hipError_t launch_obs(const ObsParams& p, hipStream_t stream) {
-  // 16 agents per workgroup: same-box A/B of the native kernel, 0.192 / 0.196 / 0.231 ms per
-  // 512-env launch at 16 / 32 / 64 (the env staging is shared by fewer agents, but more
-  // workgroups fill the CUs)
-  dim3 grid(p.n_envs, (p.P + kObsAgentsPerBlock - 1) / kObsAgentsPerBlock);
-  const dim3 block(64 * kObsWaves);
   if (p.wire) return launch_wire_obs(p, stream);  // wire_obs.hip
-  const int mode = p.nat ? kModeNative : kModeFlat;
-  const size_t lds = obs_lds_bytes(p.S, mode);
-  if (mode == kModeNative) {
-    if (p.wflags) hipLaunchKernelGGL((obs_kernel<true, kModeNative>), grid, block, lds, stream, p);
-    else hipLaunchKernelGGL((obs_kernel<false, kModeNative>), grid, block, lds, stream, p);
-  } else {
-    if (p.wflags) hipLaunchKernelGGL((obs_kernel<true, kModeFlat>), grid, block, lds, stream, p);
-    else hipLaunchKernelGGL((obs_kernel<false, kModeFlat>), grid, block, lds, stream, p);
-  }
+  if (p.nat) return launch_native_obs(p, stream);  // native_obs.hip
+  const dim3 grid(p.n_envs, (p.P + kObsAgentsPerBlock - 1) / kObsAgentsPerBlock), block(64 * kObsWaves);
+  const size_t lds = obs_lds_bytes(p.S);
+  if (p.wflags) hipLaunchKernelGGL(obs_kernel<true>, grid, block, lds, stream, p);
+  else hipLaunchKernelGGL(obs_kernel<false>, grid, block, lds, stream, p);
   return hipGetLastError();
 }
 
