@@ -13,6 +13,8 @@
 //    image with compile-time shifts (the sections' sizes are nmmo_layout's fixed dims).
 #pragma once
 
+#include <utility>
+
 #include "kernels.h"
 #include "wire.h"
 
@@ -47,8 +49,26 @@ __host__ inline bool ao_layout_ok(const ObsParams& p) {
 }
 
 __device__ __forceinline__ uint64_t low_bits(int n) { return n >= 64 ? ~0ull : n <= 0 ? 0ull : (1ull << n) - 1ull; }
-// x with lane L's value replaced by the wave-uniform v
-__device__ __forceinline__ int writelane(int v, int L, int x) { return lane_id() == L ? v : x; }
+// x with lane L's value replaced by the wave-uniform v: one v_writelane_b32 (the value pinned to
+// an SGPR, the lane an inline constant; this compiler has no writelane builtin)
+template <int L>
+__device__ __forceinline__ int writelane(int v, int x) {
+  static_assert(L >= 0 && L < 64, "lane");
+  int sv = __builtin_amdgcn_readfirstlane(v);
+  asm volatile("" : "+s"(sv));
+  asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(x) : "s"(sv), "n"(L));
+  return x;
+}
+template <int kLane0, int kIdx0, int... D>
+__device__ __forceinline__ int writelanes_(const uint32_t* img, int x, std::integer_sequence<int, D...>) {
+  ((x = writelane<kLane0 + D>((int)img[kIdx0 + D], x)), ...);
+  return x;
+}
+// lanes kLane0 .. kLane0 + kN - 1 of x take img[kIdx0 ..] (wave-uniform words)
+template <int kLane0, int kIdx0, int kN>
+__device__ __forceinline__ int writelanes(const uint32_t* img, int x) {
+  return writelanes_<kLane0, kIdx0>(img, x, std::make_integer_sequence<int, kN>{});
+}
 
 // OR the kN-bit field lo | hi << 64 (bits >= kN zero) into img at bit kOff
 template <int kOff, int kN, int kW>

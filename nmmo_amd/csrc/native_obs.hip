@@ -97,6 +97,12 @@ __global__ void __launch_bounds__(256) native_obs_kernel(ObsParams p) {
     }
   };
   auto alive = [&](int j) { return j < per_wave && __builtin_amdgcn_readlane(my_alive, j) != 0; };
+  int toff[4];  // window tile lane + 64 i: (row offset) & 255 | (col offset) << 8
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const int t = lane + 64 * i;
+    toff[i] = ((t / 15 - kVision) & 255) | (t % 15 - kVision) * 256;
+  }
   if (alive(0)) prefetch(abase);
 
   for (int j = 0; j < per_wave; j++) {
@@ -143,31 +149,34 @@ __global__ void __launch_bounds__(256) native_obs_kernel(ObsParams p) {
       uint32_t img[kNoImgWords];
       ao_image<true>(ao_sections<kWrap>(p, T, Sp, visw, ag, it), img);
       img[(kWireBuyLo + NMMO_MARKET_ROWS) / 32] |= 1u << ((kWireBuyLo + NMMO_MARKET_ROWS) & 31);  // Buy noop
-      uint32_t x = 0u;
-#pragma unroll
-      for (int d = 0; d < kNoImgWords; d++) x |= lane == d ? img[d] : 0u;
-      // Buy.MarketItem entries k = 32 d - 104 .. + 31 (a multiple of 8): listing k is buyable
-      // with exchange on, k < listings, price <= gold and not the agent's own
-      const int kb = 32 * lane - kWireBuyLo;
-      if (exch && kb + 32 > 0 && kb < nm) {
-#pragma unroll 1
-        for (int q8 = 0; q8 < 4; q8++) {
-          const int k = kb + 8 * q8;
-          if (k < 0 || k >= nm) continue;
-          const uint4 v = reinterpret_cast<const uint4*>(mpo)[k >> 3];
-          const uint32_t pw[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-          for (int i = 0; i < 8; i++) {
-            const uint32_t po = (pw[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
-            if (k + i < nm && (int)(po & 255u) <= gold && (int)(po >> 8) != a) x |= 1u << (8 * q8 + i);
+      // the section words (dwords 0-3 and 35-49: Buy.MarketItem fills the ones between)
+      static_assert(sec_flat(2) / 32 == 3 && (sec_flat(3) - 1) / 32 == 35, "Buy.MarketItem dwords");
+      int x = 0;
+      x = writelanes<0, 0, 4>(img, x);
+      x = writelanes<35, 35, kNoImgWords - 35>(img, x);
+      // Buy.MarketItem entry k < listings (a lane per listing, 64 per ballot): exchange on,
+      // price <= gold, not the agent's own; the ballot of listings j0 .. j0 + 63 covers flat bits
+      // 104 + j0 .. (dwords 3 + j0 / 32 .. + 2, shifted by 8)
+      if (exch) {
+        for (int j0 = 0; j0 < nm; j0 += 64) {
+          const int k = j0 + lane;
+          bool bv = false;
+          if (k < nm) {
+            const uint32_t po = mpo[k];
+            bv = (int)(po & 255u) <= gold && (int)(po >> 8) != a;
           }
+          const uint64_t b = __ballot(bv);
+          const int d0 = (kWireBuyLo + j0) >> 5;
+          static_assert((kWireBuyLo & 31) == 8, "Buy.MarketItem bit shift");
+          const uint32_t p0 = (uint32_t)(b << 8), p1 = (uint32_t)(b >> 24), p2 = (uint32_t)(b >> 56);
+          x |= (int)(lane == d0 ? p0 : lane == d0 + 1 ? p1 : lane == d0 + 2 ? p2 : 0u);
         }
       }
       // 16 entries per lane -> 16 bytes: entry b of a nibble n lands in byte b by n * 0x204081
 #pragma unroll
       for (int h = 0; h < 2; h++) {
         const int q = 64 * h + lane;  // 16-B chunk
-        const uint32_t b16 = ((uint32_t)__shfl((int)x, q >> 1) >> (16 * (q & 1))) & 0xFFFFu;
+        const uint32_t b16 = ((uint32_t)__shfl(x, q >> 1) >> (16 * (q & 1))) & 0xFFFFu;
         if (q < NMMO_NATIVE_MASK_BYTES / 16) {
           uint32_t o[4];
 #pragma unroll
@@ -211,29 +220,36 @@ __global__ void __launch_bounds__(256) native_obs_kernel(ObsParams p) {
       if (t0 + lane < nz) reinterpret_cast<uint32_t*>(zb)[t0 + lane] = 0u;
     }
     // Inventory: 96 dwords (item q = i >> 3, columns 2i & 15, +1), the item word from lane q
+    if (ninv == 0) {
+      if (lane < kInv * 8 / 4) reinterpret_cast<uint4*>(d32 + kNoInv / 2)[lane] = make_uint4(0u, 0u, 0u, 0u);
+    } else {
 #pragma unroll
-    for (int h = 0; h < 2; h++) {
-      const int i = 64 * h + lane;
-      const int q = min(i >> 3, kInv - 1);
-      const uint2 iw = make_uint2((uint32_t)__shfl((int)it.x, q), (uint32_t)__shfl((int)it.y, q));
-      if (i < kInv * 8) {
-        const int cc = (2 * i) & 15;
-        d32[kNoInv / 2 + i] =
-            (i >> 3) < ninv ? i16pack((int)item_col(iw, aid, cc), (int)item_col(iw, aid, cc + 1)) : 0u;
+      for (int h = 0; h < 2; h++) {
+        const int i = 64 * h + lane;
+        const int q = min(i >> 3, kInv - 1);
+        const uint2 iw = make_uint2((uint32_t)__shfl((int)it.x, q), (uint32_t)__shfl((int)it.y, q));
+        if (i < kInv * 8) {
+          const int cc = (2 * i) & 15;
+          d32[kNoInv / 2 + i] =
+              (i >> 3) < ninv ? i16pack((int)item_col(iw, aid, cc), (int)item_col(iw, aid, cc + 1)) : 0u;
+        }
       }
     }
-    // Tile (row, col, material per window tile) | task index | zero pad, as dwords
+    // Tile: (row, col, material) per window tile t = lane + 64 i as three int16 stores (the
+    // lane's row / column offsets are per-wave constants), then the task index and the zero pad
     {
-      const int task = __builtin_amdgcn_readlane(my_task, j);
-      auto half = [&](int h) -> int {  // int16 h of the part starting at kNoTile
-        if (h < 225 * 3) {
-          const int t = h / 3, comp = h - 3 * t;
-          return comp == 0 ? r + t / 15 - kVision : comp == 1 ? c + t % 15 - kVision : (int)wmat[t];
+      int16_t* d16 = reinterpret_cast<int16_t*>(d32) + kNoTile;
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const int t = lane + 64 * i;
+        if (t < 225) {
+          d16[3 * t] = (int16_t)(r + ((toff[i] << 24) >> 24));
+          d16[3 * t + 1] = (int16_t)(c + (toff[i] >> 8));
+          d16[3 * t + 2] = (int16_t)wmat[t];
         }
-        return h == 225 * 3 ? task : 0;
-      };
-      constexpr int kTileDwords = (NMMO_NATIVE_I16 - kNoTile) / 2;
-      for (int i = lane; i < kTileDwords; i += 64) d32[kNoTile / 2 + i] = i16pack(half(2 * i), half(2 * i + 1));
+      }
+      if (lane < NMMO_NATIVE_I16 - kNoTask)
+        d16[225 * 3 + lane] = lane == 0 ? (int16_t)__builtin_amdgcn_readlane(my_task, j) : (int16_t)0;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the next agent reuses visw / wmat
     __builtin_amdgcn_wave_barrier();

@@ -621,6 +621,20 @@ __device__ __forceinline__ void ev_append(Ctx& c, int& evn, int n, F&& emit) {
   evn += tot;
 }
 
+// ring_append_ordered and ev_append in one prefix sum (one barrier fewer each): every thread
+// reads the FIFO tail before the scan's barrier, thread 0 moves it after.
+template <class F>
+__device__ __forceinline__ void ring_ev_append(Ctx& c, int row, int& evn, int nev, F&& emit) {
+  const int fb = c.E[E_ITEM_FREE_HEAD] + c.E[E_ITEM_FREE_COUNT];
+  int tot;
+  const int pre = block_prefix_sum((row >= 0 ? 1 : 0) | nev << 16, wtot_next(c), &tot);
+  if (row >= 0) c.iring[(fb + (pre & 0xFFFF)) % c.IC] = (int16_t)row;
+  if (nev) emit(evn + (pre >> 16));
+  evn += tot >> 16;
+  if (threadIdx.x == 0) c.E[E_ITEM_FREE_COUNT] += tot & 0xFFFF;
+  __syncthreads();
+}
+
 // ---------------------------------------------------------------- NPC spawn (SPEC §5.7)
 // 25 attempts evaluated by lanes 0..24 of wave 0; accepted in attempt order up to capacity.
 __device__ __forceinline__ void npc_spawn(Ctx& c, uint32_t tick) {
@@ -911,7 +925,9 @@ __device__ __forceinline__ int combat_level(const Ctx& c, int s) {
 }
 
 // Attack.call validity + combat.attack damage on the current LDS state; -1 = no attack.
-__device__ __forceinline__ int eval_attack(const Ctx& c, int x, int sty, int t) {
+// eq_off: x's equipment offense in this style; eq_def: t's equipment defense (both constant
+// through the attack rounds: ammunition is fired after them)
+__device__ __forceinline__ int eval_attack(const Ctx& c, int x, int sty, int t, int eq_off, int eq_def) {
   if (!TF(F_ALIVE, x) || TF(F_HEALTH, x) <= 0) return -1;
   if (!TF(F_ALIVE, t) || TF(F_HEALTH, t) <= 0 || t == x) return -1;
   if (x < c.P && t < c.P && TF(F_TIME_ALIVE, t) < c.cfg->spawn_immunity) return -1;
@@ -920,10 +936,8 @@ __device__ __forceinline__ int eval_attack(const Ctx& c, int x, int sty, int t) 
   const bool prog = sys(c, NMMO_SYS_PROGRESSION);
   int offense = prog ? 10 + 5 * TF(F_MELEE_LEVEL + 2 * sty, x) : 30;
   int defense = prog ? 5 * combat_level(c, t) : 0;
-  if (sys(c, NMMO_SYS_EQUIPMENT)) {  // players: equipped items; NPCs: spawn-time equipment
-    offense += x < c.P ? (c.items ? inv_offense(c, x, sty) : 0) : TF(F_EQUIP_OFFENSE, x);
-    defense += t < c.P ? (c.items ? inv_defense(c, t) : 0) : TF(F_EQUIP_DEFENSE, t);
-  }
+  offense += eq_off;
+  defense += eq_def;
   const int e0 = TF(F_MELEE_EXP, t), e1 = TF(F_RANGE_EXP, t), e2 = TF(F_MAGE_EXP, t);
   const int mx = max(e0, max(e1, e2)), mn = min(e0, min(e1, e2));
   int mult4 = 4;
@@ -1583,8 +1597,8 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
         }
       }
     }
-    ring_append_ordered(c, freed);
-    if (evon) ev_append(c, evn, u_code ? 1 : 0, [&](int i) { ev_put(c, i, s, u_code, u_type, u_lvl, u_num, 0, 0); });
+    ring_ev_append(c, freed, evn, evon && u_code ? 1 : 0,
+                   [&](int i) { ev_put(c, i, s, u_code, u_type, u_lvl, u_num, 0, 0); });
   NMMO_STAMP(22);
 
     // Buy (priority 20): buyers in shuffled order (key draw(tick, BUY_ORDER, id), ties by id).
@@ -1691,41 +1705,77 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
     }
 
     NMMO_STAMP(23);
-    // Give / GiveGold (priority 30): cross-player, replayed by thread 0 in slot order
+    // Give / GiveGold (priority 30), in slot order. Player p's gives touch p, its item target t
+    // and its gold target t2 (inventories and gold); like the buys, they run in rounds: each
+    // round executes every remaining give that is the lowest-slot remaining give of all its
+    // players, all in parallel, which is the serial result. Events (GIVE_ITEM, then GIVE_GOLD per
+    // player) and the rows freed by stacking go out in slot order by one prefix sum afterwards.
     {
       const bool isg = s < P && (c.a_givet[s] >= 0 || c.a_ggt[s] >= 0);
       int ng;
-      const int gpos = block_prefix_count(isg, wtot_next(c), &ng);
-      if (isg) c.order[gpos] = (int16_t)s;
-      __syncthreads();
-      if (tid == 0) {
-        for (int i = 0; i < ng; i++) {
-          const int p = c.order[i];
-          if (!acts(c, p)) continue;
-          int t = c.a_givet[p];
-          if (t >= 0 && t < P && t != p && acts(c, t) && same_tile(c, t, p)) {
-            uint2* inv = c.inv + p * kInv;
-            const int k = inv_find(inv, c.a_give[p]);
-            if (k >= 0 && !it_equipped(inv[k]) && !it_price(inv[k]) && has_room(c, t, inv[k])) {
-              const uint2 w = inv[k];
-              if (evon) ev_put(c, evn++, p, EV_GIVE_ITEM, it_type(w), it_level(w), it_qty(w), 0, TF(F_ID, t));
-              inv_remove(inv, k);
-              receive_moved(c, t, w);
+      block_prefix_count(isg, wtot_next(c), &ng);
+      if (ng > 0) {
+        int* mi = c.ft;  // attack init zeroes it again
+        int* anyf = c.wtot + 16;
+        if (tid < P) mi[tid] = 0;
+        if (tid < 3) anyf[tid] = 0;
+        __syncthreads();
+        const int tg = isg ? c.a_givet[s] : -1, tg2 = isg ? c.a_ggt[s] : -1;
+        const bool r1 = tg >= 0 && tg < P && tg != s, r2 = tg2 >= 0 && tg2 < P && tg2 != s;
+        bool active = isg && acts(c, s) && (r1 || r2);  // the others fail without effect
+        bool did_item = false, did_gold = false;
+        uint2 gw = make_uint2(0u, 0u);
+        int freed = -1;
+        for (int round = 1;; round++) {
+          const int key = (round << 16) | (0xFFFF - s);
+          if (active) {
+            atomicMax(&mi[s], key);
+            if (r1) atomicMax(&mi[tg], key);
+            if (r2) atomicMax(&mi[tg2], key);
+            anyf[round % 3] = 1;
+          }
+          if (tid == 0) anyf[(round + 1) % 3] = 0;
+          __syncthreads();
+          if (!anyf[round % 3]) break;
+          if (active && mi[s] == key && (!r1 || mi[tg] == key) && (!r2 || mi[tg2] == key)) {
+            active = false;
+            if (r1 && acts(c, tg) && same_tile(c, tg, s)) {
+              uint2* inv = c.inv + s * kInv;
+              const int k = inv_find(inv, c.a_give[s]);
+              if (k >= 0 && !it_equipped(inv[k]) && !it_price(inv[k]) && has_room(c, tg, inv[k])) {
+                gw = inv[k];
+                did_item = true;
+                inv_remove(inv, k);
+                receive_moved_deferred(c, tg, gw, freed);
+              }
+            }
+            if (r2 && acts(c, tg2) && c.a_gga[s] <= TF(F_GOLD, s) && same_tile(c, tg2, s)) {
+              TF(F_GOLD, s) = (int16_t)(TF(F_GOLD, s) - c.a_gga[s]);
+              TF(F_GOLD, tg2) = (int16_t)(TF(F_GOLD, tg2) + c.a_gga[s]);
+              did_gold = true;
             }
           }
-          t = c.a_ggt[p];
-          if (t >= 0 && t < P && t != p && acts(c, t) && c.a_gga[p] <= TF(F_GOLD, p) && same_tile(c, t, p)) {
-            TF(F_GOLD, p) = (int16_t)(TF(F_GOLD, p) - c.a_gga[p]);
-            TF(F_GOLD, t) = (int16_t)(TF(F_GOLD, t) + c.a_gga[p]);
-            if (evon) ev_put(c, evn++, p, EV_GIVE_GOLD, 0, 0, 0, c.a_gga[p], TF(F_ID, t));
-          }
         }
-        c.E[E_EVENT_COUNT] = evn;
+        // (the loop's last barrier ordered every give before these reads)
+        const int fb = c.E[E_ITEM_FREE_HEAD] + c.E[E_ITEM_FREE_COUNT];
+        const int nev = evon ? (int)did_item + (int)did_gold : 0;
+        int tot;
+        const int pre = block_prefix_sum((freed >= 0 ? 1 : 0) | nev << 16, wtot_next(c), &tot);
+        if (freed >= 0) c.iring[(fb + (pre & 0xFFFF)) % c.IC] = (int16_t)freed;
+        if (nev) {
+          int i = evn + (pre >> 16);
+          if (did_item) ev_put(c, i++, s, EV_GIVE_ITEM, it_type(gw), it_level(gw), it_qty(gw), 0, TF(F_ID, tg));
+          if (did_gold) ev_put(c, i, s, EV_GIVE_GOLD, 0, 0, 0, c.a_gga[s], TF(F_ID, tg2));
+        }
+        evn += tot >> 16;
+        if (tid == 0) {
+          c.E[E_ITEM_FREE_COUNT] += tot & 0xFFFF;
+          c.E[E_EVENT_COUNT] = evn;
+        }
+        __syncthreads();
       }
-      __syncthreads();
-      evn = c.E[E_EVENT_COUNT];
     }
-  NMMO_STAMP(24);
+    NMMO_STAMP(24);
 
     // Destroy (priority 40): own inventory, rows freed in slot order
     freed = -1;
@@ -1739,10 +1789,8 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
         inv_remove(inv, k);
       }
     }
-    ring_append_ordered(c, freed);
-    if (evon)
-      ev_append(c, evn, freed >= 0 ? 1 : 0,
-                [&](int i) { ev_put(c, i, s, EV_DESTROY_ITEM, it_type(dw), it_level(dw), it_qty(dw), 0, 0); });
+    ring_ev_append(c, freed, evn, evon && freed >= 0 ? 1 : 0,
+                   [&](int i) { ev_put(c, i, s, EV_DESTROY_ITEM, it_type(dw), it_level(dw), it_qty(dw), 0, 0); });
   }
 
   NMMO_STAMP(14);
@@ -1755,6 +1803,14 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
   int* mi = c.ft;
   for (int k = tid; k < S; k += nt) mi[k] = 0;
   if (tid < 3) c.wtot[16 + tid] = 0;  // attack-round flags
+  // equipment bonuses, once (players: equipped items; NPCs: spawn-time equipment): this slot's
+  // offense in its attack style (a register) and its defense (c.clist, read by its attackers)
+  int eq_off = 0;
+  if (sys(c, NMMO_SYS_EQUIPMENT) && s < S) {
+    const int sty0 = c.asty[s];
+    eq_off = s < P ? (items ? inv_offense(c, s, sty0) : 0) : TF(F_EQUIP_OFFENSE, s);
+    c.clist[s] = (int16_t)(s < P ? (items ? inv_defense(c, s) : 0) : TF(F_EQUIP_DEFENSE, s));
+  }
   __syncthreads();
   NMMO_STAMP(4);
   if (combat || sys(c, NMMO_SYS_NPC)) {
@@ -1775,7 +1831,7 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
       __syncthreads();
       if (!anyf[round % 3]) break;
       if (active && mi[s] == key && mi[t] == key) {
-        const int dmg = eval_attack(c, s, sty, t);
+        const int dmg = eval_attack(c, s, sty, t, eq_off, sys(c, NMMO_SYS_EQUIPMENT) ? c.clist[t] : 0);
         if (dmg >= 0) apply_attack(c, s, sty, t, dmg, tick);
         active = false;
       }
@@ -2047,21 +2103,20 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
   }
   NMMO_STAMP(19);
   __syncthreads();
-  if (tid == 0) c.E[E_TICK] = tick + 1;
-  __syncthreads();
+  if (tid == 0) c.E[E_TICK] = tick + 1;  // read only at the tick's start (and by store_env)
   NMMO_STAMP(8);
   // 7. NPC refill
   if (sys(c, NMMO_SYS_NPC)) npc_spawn(c, (uint32_t)(tick + 1));
   NMMO_STAMP(9);
 
-  // 8. rewards / dones
+  // 8. rewards / dones (every thread evaluates `done`: E_PLAYERS_ALIVE was last written before
+  // the respawn barrier)
+  const int alive_n = c.E[E_PLAYERS_ALIVE];
+  const bool done = alive_n == 0 || tick + 1 >= c.cfg->horizon || alive_n <= c.cfg->early_stop_agent_num;
   if (tid == 0) {
-    const int alive = c.E[E_PLAYERS_ALIVE];
-    const int done = alive == 0 || tick + 1 >= c.cfg->horizon || alive <= c.cfg->early_stop_agent_num;
     c.E[E_DONE] = done;
     if (c.evcap) c.E[E_EVENT_COUNT] = evn;
   }
-  __syncthreads();
   if (s < P) {  // Task.compute_rewards: progress delta, death penalty (SPEC §12)
     float rw = 0.f;
     // the prefetched task words stay opaque until here, or the compiler hoists their conversions
@@ -2085,7 +2140,7 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
     }
     rew[s] = rw;
     term[s] = c.died[s];
-    trunc[s] = (uint8_t)(c.E[E_DONE] && TF(F_ALIVE, s));
+    trunc[s] = (uint8_t)(done && TF(F_ALIVE, s));
     mask[s] = c.pres[s];
   }
 }
@@ -2176,12 +2231,12 @@ __device__ __forceinline__ void tick_body(const DevState& st, const int32_t* __r
     tick_env(c, actions + o * kHeads, a_pre, rew + o, term + o, trunc + o, mask + o);
   }
   __syncthreads();
-  if (st.counters) {  // sum(mask) of this launch (pres, or all players on a reset) + done envs
+  if (st.counters) {  // sum(mask) of this launch (pres, or all players on a reset) + done envs;
+    // one atomic per wave, no block barrier
     const bool reset = mode == 1 || reset_path;
-    int n;
-    block_prefix_count(threadIdx.x < c.P && (reset || c.pres[threadIdx.x]), wtot_next(c), &n);
+    const int n = __popcll(__ballot(threadIdx.x < c.P && (reset || c.pres[threadIdx.x])));
+    if (lane_id() == 0 && n) atomicAdd(&st.counters[0], (unsigned long long)n);
     if (threadIdx.x == 0) {
-      atomicAdd(&st.counters[0], (unsigned long long)n);
       if (!reset && c.E[E_DONE]) atomicAdd(&st.counters[1], 1ull);
       if (!reset && c.evcap) atomicAdd(&st.counters[2], (unsigned long long)(c.E[E_EVENT_COUNT] - ev_start));
     }
@@ -2189,7 +2244,9 @@ __device__ __forceinline__ void tick_body(const DevState& st, const int32_t* __r
   NMMO_STAMP(10);
   store_market(c, st, e);
   store_env(c, st, e);
+#ifdef NMMO_STAMPS
   __syncthreads();
+#endif
   NMMO_STAMP(11);
 }
 

@@ -51,35 +51,45 @@ __global__ void __launch_bounds__(128) wire_size_kernel(const uint16_t* counts, 
 // occupied inventory prefix; per env the payload bytes into env_off[e] (then wire_scan_kernel).
 __global__ void __launch_bounds__(256) wire_count_kernel(ObsParams p) {
   __shared__ uint32_t pos[kMaxSlots];  // r << 16 | c of entities in the realm, else kOut
+  __shared__ uint8_t nin[128];         // occupied inventory prefix per agent
   __shared__ int bytes;
   constexpr uint32_t kOut = 0x80008000u;
+  static_assert(kMaxSlots % 64 == 0, "rows per lane");
   WireView v = wire_view(p.wire, p.n_envs, p.P);
-  const int e = blockIdx.x, tid = threadIdx.x, lane = lane_id(), w = wave_id(), S = p.S;
+  const int e = blockIdx.x, tid = threadIdx.x, lane = lane_id(), S = p.S;
+  const int w = __builtin_amdgcn_readfirstlane(wave_id()), nw = blockDim.x >> 6;
   const int16_t* E = p.ent + (size_t)e * NMMO_NF * S;
-  for (int s = tid; s < S; s += blockDim.x)
-    pos[s] = E[F_ALIVE * S + s] ? ((uint32_t)(uint16_t)E[F_ROW * S + s] << 16) | (uint32_t)(uint16_t)E[F_COL * S + s]
-                                : kOut;
+  for (int s = tid; s < kMaxSlots; s += blockDim.x)
+    pos[s] = s < S && E[F_ALIVE * S + s] ? ((uint32_t)(uint16_t)E[F_ROW * S + s] << 16) | (uint32_t)(uint16_t)E[F_COL * S + s]
+                                         : kOut;
+  if (tid < p.P) {  // the 12 item types of agent tid, loads issued together
+    const uint2* it = p.items + ((size_t)e * p.P + tid) * kInv;
+    uint32_t ty[kInv];
+#pragma unroll
+    for (int k = 0; k < kInv; k++) ty[k] = it[k].x & 31u;
+    int n = 0;
+#pragma unroll
+    for (int k = kInv - 1; k >= 0; k--) n = ty[k] ? n + 1 : 0;  // length of the occupied prefix
+    nin[tid] = (uint8_t)n;
+  }
   if (tid == 0) bytes = 0;
   __syncthreads();
+  uint32_t pr[kMaxSlots / 64];  // this lane's slots lane + 64 i
+#pragma unroll
+  for (int i = 0; i < kMaxSlots / 64; i++) pr[i] = pos[lane + 64 * i];
   int mine = 0;
-  for (int a = w; a < p.P; a += blockDim.x >> 6) {
+  for (int a = w; a < p.P; a += nw) {
     const uint32_t pa = pos[a];
     uint32_t word = 0u;
     if (pa != kOut) {  // wave-uniform
       const int r = (int)(pa >> 16), c = (int)(pa & 0xFFFFu);
       int nv = 0;
-      for (int s0 = 0; s0 < S; s0 += 64) {
-        const int s = s0 + lane;
-        bool in = false;
-        if (s < S) {
-          const uint32_t q = pos[s];
-          in = q != kOut && linf(r, c, (int)(q >> 16), (int)(q & 0xFFFFu)) <= kVision;
-        }
-        nv += __popcll(__ballot(in));
+#pragma unroll
+      for (int i = 0; i < kMaxSlots / 64; i++) {
+        const uint32_t q = pr[i];
+        nv += __popcll(__ballot(q != kOut && linf(r, c, (int)(q >> 16), (int)(q & 0xFFFFu)) <= kVision));
       }
-      const uint2 it = lane < kInv ? p.items[((size_t)e * p.P + a) * kInv + lane] : make_uint2(0u, 0u);
-      const int ninv = __builtin_ctzll(~__ballot(lane < kInv && it_type(it) != 0));  // occupied prefix
-      word = wire_count_word(min(nv, kNObs), ninv);
+      word = wire_count_word(min(nv, kNObs), nin[a]);
     }
     if (lane == 0) {
       v.cnt[(size_t)e * p.P + a] = (uint16_t)word;

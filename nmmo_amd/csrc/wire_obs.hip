@@ -131,13 +131,11 @@ __global__ void __launch_bounds__(256) wire_obs_kernel(ObsParams p) {
     uint8_t* rec = wenv + woff[a];
     {
       const int task = __builtin_amdgcn_readlane(my_task, j);
-      int x = 0;
-      x = writelane((int)i16pack(aid, tick), 0, x);
-      x = writelane((int)i16pack(task, r - kVision), 1, x);
-      x = writelane((int)i16pack(c - kVision, nv), 2, x);
-      x = writelane((int)i16pack(ninv | (exch ? 1 << 8 : 0), gold), 3, x);
-#pragma unroll
-      for (int d = 0; d < (kWireMaskBits + 31) / 32; d++) x = writelane((int)img[d], 4 + d, x);
+      const uint32_t head[4] = {i16pack(aid, tick), i16pack(task, r - kVision), i16pack(c - kVision, nv),
+                                i16pack(ninv | (exch ? 1 << 8 : 0), gold)};
+      int x = 0;  // lanes 22, 23: the image's zero pad
+      x = writelanes<0, 0, 4>(head, x);
+      x = writelanes<4, 0, (kWireMaskBits + 31) / 32>(img, x);
       if (lane < (kWireBody >> 2)) reinterpret_cast<int*>(rec)[lane] = x;
     }
     // Entity rows, four per pass: a row pair is 31 dwords (4-B aligned: 96 + 124 j), lanes
