@@ -117,7 +117,7 @@ def obs_bytes_per_env(S: int, P: int, elems: int, native: bool = False, wire_byt
 
 def pmc_traffic(cfg_name: str, kernel, envs: int):
     """HBM bytes per launch of `kernel` (a name, or a list of kernels one launch runs: the wire
-    obs gather is wire_count + wire_scan + obs_kernel) from the newest committed rocprofv3 PMC
+    obs gather is wire_count + wire_scan + wire_obs_kernel) from the newest committed rocprofv3 PMC
     summary of the same workload (profiles/<round>/<cfg>/pmc.json, tools/pmc_summary.py):
     2 x FETCH_SIZE + WRITE_SIZE, gfx950-corrected, scaled per env to a launch of `envs` envs (the
     summary's launches covered its roofline.envs_per_launch, or its envs_per_gpu). None when no
@@ -461,8 +461,8 @@ def measure(args, name, layout_name, envs, rank, world, dev, steps, warmup, dist
     tick_b = tick_bytes_per_env(S, P, "Item" in cfg.systems, events_per_env_tick or 0.0, slim) * per
     obs_b = obs_bytes_per_env(S, P, eng.obs_elems, native) * per if wl["obs"] else 0
     if wl["obs"] and obs_avg_ms > tick_avg_ms:
-        kern, byts, ms = "obs_kernel", obs_b, obs_avg_ms
-        timing = "HIP events around each obs_kernel launch on the launch stream"
+        kern, byts, ms = "native_obs_kernel" if native else "obs_kernel", obs_b, obs_avg_ms
+        timing = f"HIP events around each {kern} launch on the launch stream"
     else:
         kern, byts, ms = "tick_kernel", tick_b, tick_avg_ms
         timing = "HIP events around each tick_kernel launch on the launch stream"
@@ -583,9 +583,9 @@ def measure_gather(args, name, envs, rank, world, dev, steps, warmup, dist=None,
     tick_b = tick_bytes_per_env(S, P, True, events_per_env_tick) * per
     obs_b = obs_bytes_per_env(S, P, eng.obs_elems, wire_bytes=wire_env_bytes) * per
     if obs_avg_ms > tick_avg_ms:
-        kern, byts, ms = "obs_kernel", obs_b, obs_avg_ms
-        timing = ("HIP events around each wire obs gather (wire_count + wire_scan + obs_kernel) on the launch "
-                  "stream")
+        kern, byts, ms = "wire_obs_kernel", obs_b, obs_avg_ms
+        timing = ("HIP events around each wire obs gather (wire_count + wire_scan + wire_obs_kernel) on the "
+                  "launch stream")
     else:
         kern, byts, ms = "tick_kernel", tick_b, tick_avg_ms
         timing = "HIP events around each tick_kernel launch on the launch stream"
@@ -597,7 +597,8 @@ def measure_gather(args, name, envs, rank, world, dev, steps, warmup, dist=None,
                   f"comm stream one step behind",
         "kernel_ms": {"policy": None, "tick": round(tick_avg_ms, 5), "obs": round(obs_avg_ms, 5), "wrapper": None},
         "roofline": _roofline(name, kern, byts, ms, per, timing, nb, d["elapsed"] / steps, None,
-                              ["wire_count_kernel", "wire_scan_kernel", "obs_kernel"] if kern == "obs_kernel" else None),
+                              ["wire_count_kernel", "wire_scan_kernel", "wire_obs_kernel"] if kern == "wire_obs_kernel"
+                              else None),
         "batches": nb,
         "gather_bytes": d["payload_bytes_per_step"] if world > 1 else 0,
         "wire_bytes_per_agent_in_realm": round(wire_env_bytes * per * nb * steps / max(d["alive"], 1.0), 1),

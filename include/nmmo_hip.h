@@ -42,7 +42,7 @@ extern "C" {
 #endif
 
 #define NMMO_API __attribute__((visibility("default")))
-#define NMMO_ABI_VERSION 7
+#define NMMO_ABI_VERSION 8
 
 /* ---- error codes ---- */
 #define NMMO_OK 0
@@ -353,20 +353,24 @@ NMMO_API int nmmo_expand_obs(NmmoHandle* h, const void* native, float* flat, int
 NMMO_API int nmmo_dev_alloc(int32_t device, uint64_t bytes, void** out);
 NMMO_API int nmmo_dev_free(void* ptr);
 
-/* ---- Wire encoding of native observations (SPEC.md §8c) ----
+/* ---- Wire encoding of native observations (SPEC.md §8c, v3) ----
  * For moving observations between GPUs (the learner gather of BASELINE config 5): the native
- * layout without its padding. A wire buffer of n_envs x player_n agents is
+ * layout without its padding and repetition. A wire buffer of n_envs x player_n agents is
  *   header: int64 total bytes | int64 env payload offset [n_envs] | u16 agent count word
  *           [n_envs][player_n] (bit 15 in the realm, bits 0-6 visible entities, 7-10 items) |
- *           u16 market listings [n_envs], padded to 16 B (nmmo_wire_header_bytes);
- *   payload: per env, one record per agent in the realm (slot order) then its listings (32 B
- *           each); a record is a 16-B head (int16 AgentId, CurrentTick, task index, tile row 0,
- *           tile col 0, nv, ninv, 0), the 1,586 ActionTargets bits in 208 B, nv Entity rows
- *           (31 int16), ninv Inventory rows (16 int16), the 225 window materials, zero pad to 16 B.
- * A sender transfers the header (fixed size) and then total - header bytes; the receiver reads
- * `total` from the header. */
+ *           u16 market listings [n_envs] | u16 entity-table rows [n_envs], padded to 16 B
+ *           (nmmo_wire_header_bytes);
+ *   payload: per env, its entity table (the distinct Entity rows its records show, 31 int16
+ *           each, ascending by the id's 16-bit pattern, padded to 16 B), one record per agent in
+ *           the realm (slot order), then its listings (32 B each); a record is a 16-B head
+ *           (int16 AgentId, CurrentTick, task index, tile row 0, tile col 0, nv, ninv | Exchange
+ *           << 8, gold), the ActionTargets bits except Buy.MarketItem (561 bits in 80 B), nv u16
+ *           entity-table indices, ninv Inventory rows (16 int16), the 225 window materials at 4
+ *           bits (113 B), zero pad to 16 B.
+ * The receiver reads `total` from the header; Buy.MarketItem is rebuilt from the listings. */
 NMMO_API int64_t nmmo_wire_header_bytes(int32_t n_envs, int32_t player_n);
-/* Upper bound of a wire buffer (every agent in the realm with 100 visible entities, 12 items). */
+/* Upper bound of a wire buffer (every agent in the realm with 100 visible entities and 12 items,
+ * full entity tables, every listing). */
 NMMO_API int64_t nmmo_wire_max_bytes(int32_t n_envs, int32_t player_n);
 /* Encodes `native` (the NMMO_OBS_NATIVE buffer of h's most recent obs gather; the per-agent
  * counts and the listing count come from that launch) into `wire` (device,
@@ -377,9 +381,10 @@ NMMO_API int64_t nmmo_wire_max_bytes(int32_t n_envs, int32_t player_n);
 NMMO_API int nmmo_wire_pack(NmmoHandle* h, const void* native, void* wire, void* stream);
 /* Consistency check of a (received) wire buffer of n_envs x player_n agents: its announced
  * total against *dev_expect_total (device int64, or NULL to skip), the env payload offsets
- * against the count words and listing counts, the count ranges, and every record head's
- * AgentId / nv / ninv against its count word. ORs error bits into *dev_status (device int32:
- * 1 total, 2 offsets, 4 count ranges, 8 record heads; 0 = valid). Enqueued; needs no handle. */
+ * against the count words, listing counts and entity tables, the count ranges, every record
+ * head's AgentId / nv / ninv against its count word and its entity-table indices against the
+ * table. ORs error bits into *dev_status (device int32: 1 total, 2 offsets, 4 count ranges,
+ * 8 record heads, 16 entity-table indices; 0 = valid). Enqueued; needs no handle. */
 NMMO_API int nmmo_wire_check(const void* wire, int32_t n_envs, int32_t player_n, const int64_t* dev_expect_total,
                              int32_t* dev_status, void* stream);
 /* Decodes a wire buffer of n_envs x player_n agents into the native layout (every byte of the

@@ -6,7 +6,7 @@ struct sizes against the compiled library and the enum values against the header
 
 import ctypes
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 NMMO_OK = 0
 NMMO_E_INVALID = -1

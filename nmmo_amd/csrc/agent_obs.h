@@ -4,10 +4,12 @@
 // Per workgroup (env e, kAoAgents agents; kAoWaves waves, one agent per wave at a time):
 //  - ao_stage: the env's 31 Entity columns in LDS with an odd dword stride (a lane per field
 //    reads one slot's row conflict-free; the field-major stride of S = 384 puts all 31 fields of
-//    a slot in one bank) and one packed word per datastore row: slot | row << 10 | col << 18 |
-//    spawn-immune << 26 | dangerous << 27 | player << 28 (kAoEmpty = no entity on that row);
+//    a slot in one bank) and one packed word per datastore row: row | slot[0:8] << 8 | col << 16
+//    | slot[8] << 24 | spawn-immune << 25 | dangerous << 26 | player << 27 (kAoEmpty = no entity
+//    on that row: row = col = 255, outside every window);
 //  - every lane keeps the packed words of its kAoRows datastore rows in registers, so an agent's
-//    window compaction (Entity.Query.window order) is kAoRows ballots with no LDS read;
+//    window compaction (Entity.Query.window order) is kAoRows ballots with no LDS read, each row
+//    tested with 16-bit packed math (row and col in the word's two halves);
 //  - the ActionTargets sections are wave-uniform bit fields (ballots over the visible rows and the
 //    12 inventory slots, closed forms for Style / GoldPrice / Move / SellPrice) placed into a bit
 //    image with compile-time shifts (the sections' sizes are nmmo_layout's fixed dims).
@@ -29,9 +31,25 @@ __host__ __device__ inline int ao_stride(int S) { return ((S + 1) >> 1 | 1) << 1
 __host__ __device__ inline size_t ao_entity_lds(int S) {  // T | pk
   return (((size_t)NMMO_N_ENTITY_COLS * ao_stride(S) * 2 + 15) & ~(size_t)15) + (size_t)(kMaxSlots + 64) * 4;
 }
-__device__ __forceinline__ int ao_slot(uint32_t w) { return (int)(w & 1023u); }
-__device__ __forceinline__ int ao_row(uint32_t w) { return (int)((w >> 10) & 255u); }
-__device__ __forceinline__ int ao_col(uint32_t w) { return (int)((w >> 18) & 255u); }
+__host__ __device__ inline uint32_t ao_pack(int slot, int row, int col, bool immune, bool danger, bool player) {
+  return (uint32_t)(row & 255) | (uint32_t)(slot & 255) << 8 | (uint32_t)(col & 255) << 16 | (uint32_t)(slot >> 8) << 24 |
+         (immune ? 1u << 25 : 0u) | (danger ? 1u << 26 : 0u) | (player ? 1u << 27 : 0u);
+}
+__device__ __forceinline__ int ao_slot(uint32_t w) { return (int)(((w >> 8) & 255u) | ((w >> 16) & 256u)); }
+__device__ __forceinline__ int ao_row(uint32_t w) { return (int)(w & 255u); }
+__device__ __forceinline__ int ao_col(uint32_t w) { return (int)((w >> 16) & 255u); }
+__device__ __forceinline__ bool ao_immune(uint32_t w) { return (w >> 25) & 1u; }
+__device__ __forceinline__ bool ao_danger(uint32_t w) { return (w >> 26) & 1u; }
+__device__ __forceinline__ bool ao_player(uint32_t w) { return (w >> 27) & 1u; }
+// L-inf distance of w's tile to (r, c) <= kVision, with rc = r | c << 16: both 16-bit halves of
+// (tile - (r, c)) + kVision in 0..2 kVision
+typedef unsigned short ao_u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ bool ao_in_window(uint32_t w, uint32_t rc) {
+  ao_u16x2 d = __builtin_bit_cast(ao_u16x2, w & 0x00FF00FFu) - __builtin_bit_cast(ao_u16x2, rc) +
+               (ao_u16x2){(unsigned short)kVision, (unsigned short)kVision};
+  return (d.x > d.y ? d.x : d.y) <= 2 * kVision;
+}
+static_assert(kMaxSlots <= 512 && kSize <= 255, "packed entity word");
 
 // The 12 ActionTargets sections (nmmo_layout's dims, flat order), their flat entry offsets and
 // the wire bit offsets of the 11 sent ones (Buy.MarketItem is not sent). Launchers check a
@@ -117,9 +135,7 @@ __device__ inline void ao_stage(const ObsParams& p, int e, int16_t* T, uint32_t*
       const bool player = s < P;
       const bool immune = player && T[F_TIME_ALIVE * Sp + s] < p.spawn_immunity;
       const bool danger = T[F_NPC_TYPE * Sp + s] > 1;
-      pk[ds[u] - 1] = (uint32_t)s | (uint32_t)(uint16_t)T[F_ROW * Sp + s] << 10 |
-                      (uint32_t)(uint16_t)T[F_COL * Sp + s] << 18 | (immune ? 1u << 26 : 0u) |
-                      (danger ? 1u << 27 : 0u) | (player ? 1u << 28 : 0u);
+      pk[ds[u] - 1] = ao_pack(s, T[F_ROW * Sp + s], T[F_COL * Sp + s], immune, danger, player);
     }
   }
   __syncthreads();
@@ -129,17 +145,33 @@ __device__ inline void ao_stage(const ObsParams& p, int e, int16_t* T, uint32_t*
 // words go to visw. Returns the in-window count (uncapped).
 __device__ __forceinline__ int ao_compact(const uint32_t (&pr)[kAoRows], int S, int r, int c, uint32_t* visw) {
   int nvis = 0;
+  const uint32_t rc = (uint32_t)r | (uint32_t)c << 16;
 #pragma unroll
   for (int i = 0; i < kAoRows; i++) {
     if (64 * i >= S) break;
     const uint32_t x = pr[i];
-    const bool in = x != kAoEmpty && linf(r, c, ao_row(x), ao_col(x)) <= kVision;
+    const bool in = ao_in_window(x, rc);  // (an empty row is at (255, 255): outside)
     const uint64_t b = __ballot(in);
     const int pos = nvis + __popcll(b & lanes_below());
     if (in && pos < kNObs) visw[pos] = x;
     nvis += __popcll(b);
   }
   return nvis;
+}
+
+// Map offsets of the window tiles t = lane + 64 i (i < 4) from the agent's tile, two int16 per
+// register (per-wave constants: an agent's 225 material loads are then one add each)
+__device__ __forceinline__ void ao_window_offsets(int (&mo)[2]) {
+  mo[0] = mo[1] = 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const int t = lane_id() + 64 * i;
+    const int o = t < 225 ? (t / 15 - kVision) * kSize + t % 15 - kVision : 0;
+    mo[i >> 1] |= (o & 0xFFFF) << (16 * (i & 1));
+  }
+}
+__device__ __forceinline__ int ao_window_off(const int (&mo)[2], int i) {
+  return (int)(int16_t)(uint16_t)((uint32_t)mo[i >> 1] >> (16 * (i & 1)));
 }
 
 // Passability of the 5 Move targets from the window materials (tile t in lane t & 63 of wm[t >> 6];
@@ -183,9 +215,9 @@ __device__ __forceinline__ AoSections ao_sections(const ObsParams& p, const int1
     if (k < g.nv) {
       const uint32_t w = visw[k];
       const int q = ao_slot(w);
-      tgt = combat && q != g.a && linf(g.r, g.c, ao_row(w), ao_col(w)) <= 3 && !((w >> 26) & 1u) &&
-            !(no_danger && ((w >> 27) & 1u));
-      st = ((w >> 28) & 1u) && q != g.a && ao_row(w) == g.r && ao_col(w) == g.c;
+      tgt = combat && q != g.a && linf(g.r, g.c, ao_row(w), ao_col(w)) <= 3 && !ao_immune(w) &&
+            !(no_danger && ao_danger(w));
+      st = ao_player(w) && q != g.a && ao_row(w) == g.r && ao_col(w) == g.c;
     }
     x.s1[h] = __ballot(tgt);
     const uint64_t sb = __ballot(st);

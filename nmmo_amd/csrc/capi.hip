@@ -60,6 +60,7 @@ struct NmmoHandle {
   NmmoTaskState* d_tstate = nullptr;
   uint16_t* d_wcount = nullptr;  // native obs: per-agent wire count words of the last obs (wire.hip)
   int32_t* d_wmcount = nullptr;  // native obs: per-env listing count of the last obs
+  uint16_t* d_wrank = nullptr;   // wire obs: per-slot entity-table index (wire_count_kernel)
   // the native buffer the last obs gather wrote, and whether no tick ran since (nmmo_wire_pack)
   const void* last_native = nullptr;
   bool native_fresh = false;
@@ -182,7 +183,7 @@ void nmmo_destroy(NmmoHandle* h) {
   void* bufs[] = {h->d_env,  h->d_ent,   h->d_ring,  h->d_mat,   h->d_dep,   h->d_bank,
                   h->d_task, h->d_seeds, h->d_items, h->d_iring, h->d_mlist, h->d_mcount,
                   h->d_events, h->d_tasks, h->d_assign, h->d_tstate, h->d_ws, h->d_uniq, h->d_wenv, h->d_wdrop, h->d_task_cum,
-                  h->d_wcount, h->d_wmcount, h->d_foreign};
+                  h->d_wcount, h->d_wmcount, h->d_wrank, h->d_foreign};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   delete h;
@@ -237,6 +238,9 @@ int nmmo_create(const NmmoConfig* cfg, int32_t n_envs, uint64_t seed, int32_t de
     ALLOC(h->d_wcount, n * P * 2);
     ALLOC(h->d_wmcount, n * 4);
   }
+  if (cfg->obs_layout == NMMO_OBS_WIRE) {
+    ALLOC(h->d_wrank, n * (size_t)kMaxSlots * 2);
+  }
 #undef ALLOC
   if (init_kernels() != hipSuccess) return cleanup_fail(fail(NMMO_E_HIP, "kernel attributes"));
   if (task_embedding && cfg->task_embed_dim > 0) {
@@ -288,6 +292,7 @@ static ObsParams obs_params(NmmoHandle* h, void* obs) {
   p.row_map = nullptr;
   p.wcount = native ? h->d_wcount : nullptr;
   p.wmcount = native ? h->d_wmcount : nullptr;
+  p.wrank = wire ? h->d_wrank : nullptr;
   p.ws = h->wrap_on ? h->d_ws : nullptr;
   p.wflags = 0;
   if (h->wrap_on) {
@@ -478,8 +483,9 @@ int64_t nmmo_wire_header_bytes(int32_t n_envs, int32_t player_n) {
 int64_t nmmo_wire_max_bytes(int32_t n_envs, int32_t player_n) {
   const int64_t hdr = nmmo_wire_header_bytes(n_envs, player_n);
   if (hdr < 0) return hdr;
-  const int64_t rec = wire_record_bytes(wire_count_word(kNObs, kInv));  // every agent in the realm, full windows
-  return hdr + (int64_t)n_envs * ((int64_t)player_n * rec + NMMO_NATIVE_MARKET_BYTES);
+  // every agent in the realm with full windows and inventories, a full entity table, every listing
+  const int64_t rec = wire_record_bytes(wire_count_word(kNObs, kInv));
+  return hdr + (int64_t)n_envs * (wire_table_bytes(kMaxSlots) + (int64_t)player_n * rec + NMMO_NATIVE_MARKET_BYTES);
 }
 
 int nmmo_wire_pack(NmmoHandle* h, const void* native, void* wire, void* stream) {

@@ -73,6 +73,8 @@ struct ObsParams {
   int wflags;
   uint16_t* wcount;     // native only, or NULL: per agent 0x8000 | nv | ninv << 7 (0 = not in the realm), wire.hip
   int* wmcount;         // native only, or NULL: [n] the listing count of this obs launch (nmmo_wire_pack)
+  uint16_t* wrank;      // wire only: [n][kMaxSlots] entity-table index of each slot (0xFFFF = none),
+                        // wire_count_kernel -> wire_obs_kernel
 };
 constexpr int kWrapObsPrice = 1, kWrapObsNoGive = 2, kWrapObsNoDangerous = 4;
 

@@ -87,14 +87,13 @@ __global__ void __launch_bounds__(256) native_obs_kernel(ObsParams p) {
   }
   uint2 iv = make_uint2(0u, 0u);
   uint32_t wm[4] = {0u, 0u, 0u, 0u};
+  int mo[2];
+  ao_window_offsets(mo);
   auto prefetch = [&](int a) {
-    const int r = T[F_ROW * Sp + a], c = T[F_COL * Sp + a];
+    const int at = T[F_ROW * Sp + a] * kSize + T[F_COL * Sp + a];
     iv = lane < kInv ? p.items[((size_t)e * P + a) * kInv + lane] : make_uint2(0u, 0u);
 #pragma unroll
-    for (int i = 0; i < 4; i++) {
-      const int t = lane + 64 * i;
-      wm[i] = t < 225 ? mat[(r + t / 15 - kVision) * kSize + c + t % 15 - kVision] : 0u;
-    }
+    for (int i = 0; i < 4; i++) wm[i] = lane + 64 * i < 225 ? mat[at + ao_window_off(mo, i)] : 0u;
   };
   auto alive = [&](int j) { return j < per_wave && __builtin_amdgcn_readlane(my_alive, j) != 0; };
   int toff[4];  // window tile lane + 64 i: (row offset) & 255 | (col offset) << 8

@@ -4,13 +4,18 @@
 //
 //   header  int64 total bytes | int64 env payload offset [n_envs] | u16 agent count word
 //           [n_envs][P] (bit 15 in the realm, bits 0-6 visible entities nv, 7-10 items ninv) |
-//           u16 market listings [n_envs]; 16-B aligned
-//   payload per env: one record per agent in the realm (slot order), then its listings
+//           u16 market listings [n_envs] | u16 entity-table rows [n_envs]; 16-B aligned
+//   payload per env: its entity table (the distinct Entity rows its records show, ascending by
+//           the 16-bit pattern of their id, 62 B each, zero pad to 16 B), one record per agent
+//           in the realm (slot order), then its listings
 //   record  16-B head (int16 AgentId, CurrentTick, task index, tile row 0, tile col 0, nv,
 //           ninv | exchange << 8, gold) | the ActionTargets as bits EXCEPT Buy.MarketItem (561
-//           bits in 80 B) | nv Entity rows (31 x int16) | ninv Inventory rows (16 x int16) | the
-//           225 window materials, 4 bits each (113 B) | zero pad to 16 B
+//           bits in 80 B) | nv u16 entity-table indices (the agent's Entity rows in order) | ninv
+//           Inventory rows (16 x int16) | the 225 window materials, 4 bits each (113 B) | zero pad
+//           to 16 B
 //   listing 16 x int16 (the native Market row)
+// An entity seen by several agents of an env (C4 steady state: 5.1 Entity rows per agent, 1.4
+// distinct entities per agent) travels once.
 // Buy.MarketItem (1,025 of the 1,586 mask entries) is a function of the env's listings, the
 // agent's gold and id: entry k < listings = exchange && price_k <= gold && owner_k != AgentId,
 // entry 1,024 (noop) = 1, the rest 0 -- the decoders rebuild it.
@@ -33,20 +38,62 @@ __host__ __device__ inline int wire_bit_entry(int b) { return b < kWireBuyLo ? b
 __host__ __device__ inline int entry_wire_bit(int j) { return j < kWireBuyLo ? j : j - kWireBuyN; }
 constexpr int kNatI16Entity = 2, kNatI16Inv = kNatI16Entity + kNObs * NMMO_N_ENTITY_COLS,
               kNatI16Tile = kNatI16Inv + kInv * 16, kNatI16Task = kNatI16Tile + 225 * 3;
-constexpr int kRecMaxU4 = (kWireBody + 62 * kNObs + 32 * kInv + kWireTiles + 15) / 16;  // 425
+constexpr int kRecMaxU4 = (kWireBody + 2 * kNObs + 32 * kInv + kWireTiles + 15) / 16;  // 50
+constexpr int kEntRow = 2 * NMMO_N_ENTITY_COLS;                                          // 62 B
 
 __host__ __device__ inline int64_t wire_header_used(int n, int P) {
-  return 8 + 8 * (int64_t)n + 2 * (int64_t)n * P + 2 * (int64_t)n;
+  return 8 + 8 * (int64_t)n + 2 * (int64_t)n * P + 4 * (int64_t)n;
 }
 __host__ __device__ inline int64_t wire_header_bytes(int n, int P) { return (wire_header_used(n, P) + 15) & ~(int64_t)15; }
 __host__ __device__ inline uint32_t wire_count_word(int nv, int ninv) { return 0x8000u | (uint32_t)nv | (uint32_t)ninv << 7; }
 __host__ __device__ inline int wire_record_bytes(uint32_t cnt) {
   if (!(cnt & 0x8000u)) return 0;
   const int nv = cnt & 127, ninv = (cnt >> 7) & 15;
-  return (kWireBody + 62 * nv + 32 * ninv + kWireTiles + 15) & ~15;
+  return (kWireBody + 2 * nv + 32 * ninv + kWireTiles + 15) & ~15;
 }
+// an env's entity table of ne rows
+__host__ __device__ inline int wire_table_bytes(int ne) { return (kEntRow * ne + 15) & ~15; }
 __host__ __device__ inline size_t wire_native_env_bytes(int P) {
   return (size_t)P * NMMO_NATIVE_ROW_BYTES + NMMO_NATIVE_MARKET_BYTES;
+}
+
+// Ranks by entity id: the env's distinct ids as a 65,536-bit set (2,048 words in LDS) and the
+// exclusive popcount prefix of its words (wave-summed, 2,048 ints); the table index of an id in
+// the set is idrank(). Every thread of the block calls the builders (barriers inside).
+constexpr int kIdWords = 65536 / 32;
+__device__ inline void idset_clear(uint32_t* ids) {
+  for (int k = threadIdx.x; k < kIdWords; k += blockDim.x) ids[k] = 0u;
+}
+__device__ inline void idset_add(uint32_t* ids, int id) {
+  const uint32_t u = (uint16_t)id;
+  atomicOr(&ids[u >> 5], 1u << (u & 31));
+}
+// pre[k] = set ids below word k; returns the set's size (every thread). Needs blockDim.x a
+// multiple of 64 dividing kIdWords; wsum >= 16 ints.
+__device__ inline int idset_prefix(const uint32_t* ids, int* pre, int* wsum) {
+  __syncthreads();
+  const int nt = blockDim.x, per = kIdWords / nt, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  int loc = 0;
+  for (int j = 0; j < per; j++) loc += __popc(ids[tid * per + j]);
+  const int inc = wave_incl_scan(loc);
+  if (lane == 63) wsum[w] = inc;
+  __syncthreads();
+  int before = 0, total = 0;
+  for (int k = 0; k < (nt >> 6); k++) {
+    before += k < w ? wsum[k] : 0;
+    total += wsum[k];
+  }
+  int run = before + inc - loc;
+  for (int j = 0; j < per; j++) {
+    pre[tid * per + j] = run;
+    run += __popc(ids[tid * per + j]);
+  }
+  __syncthreads();
+  return total;
+}
+__device__ inline int idrank(const uint32_t* ids, const int* pre, int id) {
+  const uint32_t u = (uint16_t)id;
+  return pre[u >> 5] + __popc(ids[u >> 5] & ((1u << (u & 31)) - 1u));
 }
 
 // Decoding helpers. lpo[k] = price | owner AgentId << 16 of listing k (Market row k's columns 15
@@ -71,6 +118,7 @@ struct WireView {  // the header fields of a wire buffer of n envs x P agents
   int64_t* env_off;  // [n] payload offsets (relative to the buffer start)
   uint16_t* cnt;     // [n][P]
   uint16_t* mcount;  // [n]
+  uint16_t* ecount;  // [n] entity-table rows
   uint8_t* base;
 };
 __device__ inline WireView wire_view(uint8_t* w, int n, int P) {
@@ -80,16 +128,17 @@ __device__ inline WireView wire_view(uint8_t* w, int n, int P) {
   v.env_off = v.total + 1;
   v.cnt = reinterpret_cast<uint16_t*>(v.env_off + n);
   v.mcount = v.cnt + (size_t)n * P;
+  v.ecount = v.mcount + n;
   return v;
 }
 
-// Offsets of the records of one env's agents (relative to the env payload) into off[0..P), the
-// listings' offset into off[P]. Wave 0 of the block computes them; the caller's next barrier
-// publishes them.
-__device__ inline void record_offsets_wave0(const uint16_t* cnt, int P, int* off) {
+// Offsets of the records of one env's agents (relative to the env payload, after its entity
+// table of `base` bytes) into off[0..P), the listings' offset into off[P]. Wave 0 of the block
+// computes them; the caller's next barrier publishes them.
+__device__ inline void record_offsets_wave0(const uint16_t* cnt, int P, int* off, int base) {
   if (threadIdx.x >= 64) return;
   const int lane = threadIdx.x;
-  int carry = 0;
+  int carry = base;
   for (int b = 0; b < P; b += 64) {
     const int a = b + lane;
     const int x = a < P ? wire_record_bytes(cnt[a]) : 0;

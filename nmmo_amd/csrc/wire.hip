@@ -7,7 +7,8 @@
 // inventory slots, Market rows past the listings, one byte per ActionTargets bit, and the Tile
 // rows/columns that follow from the window's corner, the Buy.MarketItem mask (a function of the
 // listings, the agent's gold and id) and the high nibble of every material: ~0.55 KB per agent
-// in the realm in C4 steady state instead of 9,552 B.
+// in the realm in C4 steady state instead of 9,552 B (v2); v3 sends each env's distinct Entity
+// rows once, in its entity table, and a 2-B table index per visible row: ~0.3 KB.
 //
 // Kernels:
 //   wire_size / wire_scan / wire_pack   native -> wire (nmmo_wire_pack; counts from the native
@@ -19,49 +20,78 @@
 //   wire_expand                         wire records -> flat float32 rows (the experience store
 //                                       decoding only the rows it keeps, clean_pufferl.py:333-346)
 // All HBM-bound byte work.
-#include "kernels.h"
-#include "wire.h"
+#include "agent_obs.h"
 
 namespace nmmo {
 
-// per env: its count words and listings into the header, its payload bytes into env_off[e]
-__global__ void __launch_bounds__(128) wire_size_kernel(const uint16_t* counts, const int* mcount, uint8_t* wire,
-                                                       int n, int P) {
+// per env (128 threads = an agent each): its count words, listings and entity-table rows (the
+// distinct ids of its records' Entity rows) into the header, its payload bytes into env_off[e]
+__global__ void __launch_bounds__(128) wire_size_kernel(const uint16_t* counts, const int* mcount,
+                                                       const uint8_t* native, uint8_t* wire, int n, int P) {
   WireView v = wire_view(wire, n, P);
-  const int e = blockIdx.x, a = threadIdx.x;
+  __shared__ uint32_t ids[kIdWords];
+  __shared__ int pre[kIdWords];
+  __shared__ int wsum[16];
   __shared__ int part[2];
+  const int e = blockIdx.x, a = threadIdx.x;
+  idset_clear(ids);
+  __syncthreads();
   int bytes = 0;
   if (a < P) {
     const uint16_t c = counts[(size_t)e * P + a];
     v.cnt[(size_t)e * P + a] = c;
     bytes = wire_record_bytes(c);
+    if (c & 0x8000u) {
+      const int16_t* ent = reinterpret_cast<const int16_t*>(native + (size_t)e * wire_native_env_bytes(P) +
+                                                            (size_t)a * NMMO_NATIVE_ROW_BYTES + NMMO_NATIVE_MASK_BYTES) +
+                           kNatI16Entity;
+      for (int k = 0; k < (int)(c & 127); k++) idset_add(ids, ent[NMMO_N_ENTITY_COLS * k]);
+    }
   }
   for (int o = 32; o > 0; o >>= 1) bytes += __shfl_xor(bytes, o);
   if ((a & 63) == 0) part[a >> 6] = bytes;
-  __syncthreads();
+  const int ne = idset_prefix(ids, pre, wsum);  // (barriers inside)
   if (a == 0) {
     const int nm = min(max(mcount[e], 0), NMMO_MARKET_ROWS);
     v.mcount[e] = (uint16_t)nm;
-    v.env_off[e] = part[0] + (blockDim.x > 64 ? part[1] : 0) + 32 * nm;
+    v.ecount[e] = (uint16_t)ne;
+    v.env_off[e] = wire_table_bytes(ne) + part[0] + (blockDim.x > 64 ? part[1] : 0) + 32 * nm;
   }
 }
 
-// NMMO_OBS_WIRE header from the env state: per agent in the realm nv = entities within the
-// L-inf <= 7 window (itself included; capped at 100, as obs_kernel's compaction), ninv = its
-// occupied inventory prefix; per env the payload bytes into env_off[e] (then wire_scan_kernel).
+// NMMO_OBS_WIRE header from the env state (block per env): per agent in the realm nv =
+// entities within the L-inf <= 7 window (itself included; the first 100 in datastore-row order,
+// as the obs kernels' compaction), ninv = its occupied inventory prefix; the env's entity table
+// (the slots some record shows, ranked by id) into p.wrank[e][slot] (0xFFFF = not in it) and
+// ecount[e]; the env's payload bytes into env_off[e] (then wire_scan_kernel).
 __global__ void __launch_bounds__(256) wire_count_kernel(ObsParams p) {
-  __shared__ uint32_t pos[kMaxSlots];  // r << 16 | c of entities in the realm, else kOut
-  __shared__ uint8_t nin[128];         // occupied inventory prefix per agent
+  __shared__ uint32_t pk[kMaxSlots];         // datastore row - 1 -> ao_pack word (agent_obs.h)
+  __shared__ uint32_t pos[kMaxSlots];        // slot -> row << 16 | col (agents' windows)
+  __shared__ uint32_t tab[kMaxSlots / 32];   // slots some record shows
+  __shared__ uint8_t nin[128];               // occupied inventory prefix per agent
+  __shared__ uint32_t ids[kIdWords];
+  __shared__ int pre[kIdWords];
+  __shared__ int wsum[16];
   __shared__ int bytes;
-  constexpr uint32_t kOut = 0x80008000u;
-  static_assert(kMaxSlots % 64 == 0, "rows per lane");
+  constexpr uint32_t kOut = 0xFFFFFFFFu;
+  static_assert(kMaxSlots % 64 == 0 && kMaxSlots <= 512, "rows per lane; two slots per thread");
   WireView v = wire_view(p.wire, p.n_envs, p.P);
   const int e = blockIdx.x, tid = threadIdx.x, lane = lane_id(), S = p.S;
   const int w = __builtin_amdgcn_readfirstlane(wave_id()), nw = blockDim.x >> 6;
   const int16_t* E = p.ent + (size_t)e * NMMO_NF * S;
-  for (int s = tid; s < kMaxSlots; s += blockDim.x)
-    pos[s] = s < S && E[F_ALIVE * S + s] ? ((uint32_t)(uint16_t)E[F_ROW * S + s] << 16) | (uint32_t)(uint16_t)E[F_COL * S + s]
-                                         : kOut;
+  int al[2], ds[2], r_[2], c_[2], id_[2];  // slots tid and tid + 256, loaded ahead of the barrier
+#pragma unroll
+  for (int u = 0; u < 2; u++) {
+    const int s = tid + 256 * u;
+    al[u] = s < S ? E[F_ALIVE * S + s] : 0;
+    ds[u] = s < S ? E[F_DS_ROW * S + s] : 0;
+    r_[u] = s < S ? E[F_ROW * S + s] : 0;
+    c_[u] = s < S ? E[F_COL * S + s] : 0;
+    id_[u] = s < S ? E[F_ID * S + s] : 0;
+  }
+  for (int k = tid; k < kMaxSlots; k += blockDim.x) pk[k] = kOut;
+  if (tid < kMaxSlots / 32) tab[tid] = 0u;
+  idset_clear(ids);
   if (tid < p.P) {  // the 12 item types of agent tid, loads issued together
     const uint2* it = p.items + ((size_t)e * p.P + tid) * kInv;
     uint32_t ty[kInv];
@@ -74,22 +104,38 @@ __global__ void __launch_bounds__(256) wire_count_kernel(ObsParams p) {
   }
   if (tid == 0) bytes = 0;
   __syncthreads();
-  uint32_t pr[kMaxSlots / 64];  // this lane's slots lane + 64 i
 #pragma unroll
-  for (int i = 0; i < kMaxSlots / 64; i++) pr[i] = pos[lane + 64 * i];
+  for (int u = 0; u < 2; u++) {
+    const int s = tid + 256 * u;
+    if (s >= kMaxSlots) continue;
+    const bool in = s < S && al[u];
+    pos[s] = in ? ((uint32_t)(uint16_t)r_[u] << 16) | (uint32_t)(uint16_t)c_[u] : kOut;
+    if (in && (unsigned)(ds[u] - 1) < (unsigned)S)
+      pk[ds[u] - 1] = ao_pack(s, r_[u], c_[u], false, false, false);
+  }
+  __syncthreads();
+  uint32_t pr[kMaxSlots / 64];  // this lane's datastore rows 1 + lane + 64 i
+#pragma unroll
+  for (int i = 0; i < kMaxSlots / 64; i++) pr[i] = pk[lane + 64 * i];
   int mine = 0;
   for (int a = w; a < p.P; a += nw) {
     const uint32_t pa = pos[a];
     uint32_t word = 0u;
     if (pa != kOut) {  // wave-uniform
-      const int r = (int)(pa >> 16), c = (int)(pa & 0xFFFFu);
-      int nv = 0;
+      const uint32_t rc = (pa >> 16) | (pa & 0xFFFFu) << 16;  // r | c << 16
+      int nvis = 0;
 #pragma unroll
       for (int i = 0; i < kMaxSlots / 64; i++) {
-        const uint32_t q = pr[i];
-        nv += __popcll(__ballot(q != kOut && linf(r, c, (int)(q >> 16), (int)(q & 0xFFFFu)) <= kVision));
+        const uint32_t x = pr[i];
+        const bool in = ao_in_window(x, rc);  // (an empty row is at (255, 255): outside)
+        const uint64_t b = __ballot(in);
+        if (in && nvis + __popcll(b & lanes_below()) < kNObs) {
+          const int q = ao_slot(x);
+          atomicOr(&tab[q >> 5], 1u << (q & 31));
+        }
+        nvis += __popcll(b);
       }
-      word = wire_count_word(min(nv, kNObs), nin[a]);
+      word = wire_count_word(min(nvis, kNObs), nin[a]);
     }
     if (lane == 0) {
       v.cnt[(size_t)e * p.P + a] = (uint16_t)word;
@@ -98,10 +144,25 @@ __global__ void __launch_bounds__(256) wire_count_kernel(ObsParams p) {
   }
   if (lane == 0) atomicAdd(&bytes, mine);
   __syncthreads();
+  bool shown[2];
+#pragma unroll
+  for (int u = 0; u < 2; u++) {
+    const int s = tid + 256 * u;
+    shown[u] = s < S && ((tab[s >> 5] >> (s & 31)) & 1u);
+    if (shown[u]) idset_add(ids, id_[u]);
+  }
+  const int ne = idset_prefix(ids, pre, wsum);  // (barriers inside)
+  uint16_t* rk = p.wrank + (size_t)e * kMaxSlots;
+#pragma unroll
+  for (int u = 0; u < 2; u++) {
+    const int s = tid + 256 * u;
+    if (s < kMaxSlots) rk[s] = shown[u] ? (uint16_t)idrank(ids, pre, id_[u]) : (uint16_t)0xFFFF;
+  }
   if (tid == 0) {
     const int nm = min(max(p.mcount[e], 0), NMMO_MARKET_ROWS);
     v.mcount[e] = (uint16_t)nm;
-    v.env_off[e] = bytes + 32 * nm;
+    v.ecount[e] = (uint16_t)ne;
+    v.env_off[e] = wire_table_bytes(ne) + bytes + 32 * nm;
   }
 }
 
@@ -142,17 +203,47 @@ __global__ void __launch_bounds__(256) wire_pack_kernel(const uint8_t* native, u
                                                         const int16_t* ent, int S, int exch) {
   WireView v = wire_view(wire, n, P);
   __shared__ int off[129];
-  const int e = blockIdx.x, g = blockIdx.y, lane = lane_id(), w = wave_id();
+  __shared__ uint32_t ids[kIdWords];
+  __shared__ int pre[kIdWords];
+  __shared__ int wsum[16];
+  const int e = blockIdx.x, g = blockIdx.y, tid = threadIdx.x, lane = lane_id(), w = wave_id();
   const uint16_t* cnt = v.cnt + (size_t)e * P;
-  record_offsets_wave0(cnt, P, off);
-  __syncthreads();
+  const int ne = v.ecount[e];
+  record_offsets_wave0(cnt, P, off, wire_table_bytes(ne));
   const uint8_t* nenv = native + (size_t)e * wire_native_env_bytes(P);
+  auto ent16 = [&](int a) {
+    return reinterpret_cast<const int16_t*>(nenv + (size_t)a * NMMO_NATIVE_ROW_BYTES + NMMO_NATIVE_MASK_BYTES) +
+           kNatI16Entity;
+  };
+  // the env's id set again (every block of the env: the table ranks)
+  idset_clear(ids);
+  __syncthreads();
+  for (int a = tid; a < P; a += blockDim.x) {
+    const uint32_t c = cnt[a];
+    if (!(c & 0x8000u)) continue;
+    const int16_t* e16 = ent16(a);
+    for (int k = 0; k < (int)(c & 127); k++) idset_add(ids, e16[NMMO_N_ENTITY_COLS * k]);
+  }
+  idset_prefix(ids, pre, wsum);  // (barriers inside; also publishes off)
   uint8_t* penv = v.base + v.env_off[e];
-  if (g == 0) {  // listings: 32 B each, 16-B copies
-    const int nm = v.mcount[e];
+  if (g == 0) {
+    const int nm = v.mcount[e];  // listings: 32 B each, 16-B copies
     const uint4* src = reinterpret_cast<const uint4*>(nenv + (size_t)P * NMMO_NATIVE_ROW_BYTES);
     uint4* dst = reinterpret_cast<uint4*>(penv + off[P]);
-    for (int k = threadIdx.x; k < 2 * nm; k += blockDim.x) dst[k] = src[k];
+    for (int k = tid; k < 2 * nm; k += blockDim.x) dst[k] = src[k];
+    // the entity table: every agent's Entity rows to their id's slot (an entity seen twice writes
+    // the same bytes twice), wave per agent, int16 per lane; then the table's zero pad
+    int16_t* tab = reinterpret_cast<int16_t*>(penv);
+    for (int a = w; a < P; a += blockDim.x >> 6) {
+      const uint32_t c = cnt[a];
+      if (!(c & 0x8000u)) continue;
+      const int16_t* e16 = ent16(a);
+      for (int j = lane; j < (int)(c & 127) * NMMO_N_ENTITY_COLS; j += 64) {
+        const int k = j / NMMO_N_ENTITY_COLS, f = j - k * NMMO_N_ENTITY_COLS;
+        tab[idrank(ids, pre, e16[NMMO_N_ENTITY_COLS * k]) * NMMO_N_ENTITY_COLS + f] = e16[j];
+      }
+    }
+    for (int b = kEntRow * ne + tid; b < wire_table_bytes(ne); b += blockDim.x) penv[b] = 0;
   }
   for (int i = w; i < kWireAgentsPerBlock; i += 4) {
     const int a = g * kWireAgentsPerBlock + i;
@@ -179,12 +270,12 @@ __global__ void __launch_bounds__(256) wire_pack_kernel(const uint8_t* native, u
       }
       reinterpret_cast<uint32_t*>(rec + kWireHead)[lane] = bits;
     }
-    int16_t* d16 = reinterpret_cast<int16_t*>(rec + kWireBody);
-    for (int k = lane; k < nv * NMMO_N_ENTITY_COLS; k += 64) d16[k] = i16[kNatI16Entity + k];
-    d16 += nv * NMMO_N_ENTITY_COLS;
-    for (int k = lane; k < ninv * 16; k += 64) d16[k] = i16[kNatI16Inv + k];
-    uint8_t* mat = reinterpret_cast<uint8_t*>(d16 + ninv * 16);
-    const int pad = wire_record_bytes(c) - (kWireBody + 62 * nv + 32 * ninv);
+    uint16_t* d16 = reinterpret_cast<uint16_t*>(rec + kWireBody);
+    for (int k = lane; k < nv; k += 64) d16[k] = (uint16_t)idrank(ids, pre, i16[kNatI16Entity + NMMO_N_ENTITY_COLS * k]);
+    int16_t* s16 = reinterpret_cast<int16_t*>(d16 + nv);
+    for (int k = lane; k < ninv * 16; k += 64) s16[k] = i16[kNatI16Inv + k];
+    uint8_t* mat = reinterpret_cast<uint8_t*>(s16 + ninv * 16);
+    const int pad = wire_record_bytes(c) - (kWireBody + 2 * nv + 32 * ninv);
     auto tile = [&](int t) { return t < 225 ? (int)i16[kNatI16Tile + 3 * t + 2] & 15 : 0; };
     for (int u = lane; u < pad; u += 64) mat[u] = u < kWireTiles ? (uint8_t)(tile(2 * u) | tile(2 * u + 1) << 4) : 0;
   }
@@ -222,13 +313,17 @@ __global__ void __launch_bounds__(256) wire_unpack_kernel(const uint8_t* wire, u
   __shared__ int off[129];
   __shared__ uint32_t lpo[NMMO_MARKET_ROWS];
   __shared__ uint4 recbuf[4][kRecMaxU4];
+  __shared__ uint4 tab4[kMaxSlots * kEntRow / 16];  // the env's entity table
   const int e = blockIdx.x, g = blockIdx.y, lane = lane_id(), w = wave_id();
   const uint16_t* cnt = v.cnt + (size_t)e * P;
-  record_offsets_wave0(cnt, P, off);
+  const int ne = min((int)v.ecount[e], kMaxSlots);
+  record_offsets_wave0(cnt, P, off, wire_table_bytes(ne));
   __syncthreads();
   uint8_t* nenv = native + (size_t)e * wire_native_env_bytes(P);
   const uint8_t* penv = v.base + v.env_off[e];
   const int nm = v.mcount[e];
+  for (int k = threadIdx.x; k < wire_table_bytes(ne) / 16; k += blockDim.x) tab4[k] = reinterpret_cast<const uint4*>(penv)[k];
+  const int16_t* tab = reinterpret_cast<const int16_t*>(tab4);
   {
     const int16_t* lst = reinterpret_cast<const int16_t*>(penv + off[P]);
     for (int k = threadIdx.x; k < nm; k += blockDim.x)
@@ -256,8 +351,9 @@ __global__ void __launch_bounds__(256) wire_unpack_kernel(const uint8_t* wire, u
     record_to_lds(penv + off[a], wire_record_bytes(c) / 16, lrec);
     const int16_t* h16 = reinterpret_cast<const int16_t*>(lb);
     const uint32_t* bits = reinterpret_cast<const uint32_t*>(lb + kWireHead);
-    const int16_t* s16 = reinterpret_cast<const int16_t*>(lb + kWireBody);
-    const uint8_t* mat = lb + kWireBody + 62 * nv + 32 * ninv;
+    const uint16_t* idx = reinterpret_cast<const uint16_t*>(lb + kWireBody);
+    const int16_t* s16 = reinterpret_cast<const int16_t*>(lb + kWireBody + 2 * nv);  // Inventory rows
+    const uint8_t* mat = lb + kWireBody + 2 * nv + 32 * ninv;
     const int r0 = h16[3], c0 = h16[4], task = h16[2];
     // mask bytes, 16 per lane (1,600 bytes = 100 stores)
     for (int k = lane; k < NMMO_NATIVE_MASK_BYTES / 16; k += 64) {
@@ -279,11 +375,11 @@ __global__ void __launch_bounds__(256) wire_unpack_kernel(const uint8_t* wire, u
       if (k < kNatI16Entity) {
         x = h16[k];
       } else if (k < kNatI16Inv) {
-        const int j = k - kNatI16Entity;
-        x = j < nv * NMMO_N_ENTITY_COLS ? s16[j] : 0;
+        const int j = k - kNatI16Entity, row = j / NMMO_N_ENTITY_COLS;
+        x = row < nv ? tab[min((int)idx[row], kMaxSlots - 1) * NMMO_N_ENTITY_COLS + j - row * NMMO_N_ENTITY_COLS] : 0;
       } else if (k < kNatI16Tile) {
         const int j = k - kNatI16Inv;
-        x = j < ninv * 16 ? s16[nv * NMMO_N_ENTITY_COLS + j] : 0;
+        x = j < ninv * 16 ? s16[j] : 0;
       } else if (k < kNatI16Task) {
         const int j = k - kNatI16Tile, t = j / 3, comp = j - 3 * t;
         x = comp == 0 ? r0 + t / 15 : comp == 1 ? c0 + t % 15 : wire_tile(mat, t);
@@ -305,15 +401,17 @@ __global__ void __launch_bounds__(256) wire_unpack_kernel(const uint8_t* wire, u
 
 // Consistency of one received wire buffer of n envs x P agents (block per env): the announced
 // total (when expect_total is given), the env payload offsets against the count words and
-// listings, the counts' ranges, and every record head's AgentId / nv / ninv against its count
-// word. status bits: 1 total, 2 env offsets, 4 count ranges, 8 record heads.
+// listings, the counts' ranges, every record head's AgentId / nv / ninv against its count word
+// and its entity-table indices against the table. status bits: 1 total, 2 env offsets, 4 count
+// ranges, 8 record heads, 16 entity-table indices.
 __global__ void __launch_bounds__(128) wire_check_kernel(const uint8_t* wire, int n, int P,
                                                          const int64_t* expect_total, int* status) {
   WireView v = wire_view(const_cast<uint8_t*>(wire), n, P);
   __shared__ int off[129];
   const int e = blockIdx.x, a = threadIdx.x;
   const uint16_t* cnt = v.cnt + (size_t)e * P;
-  record_offsets_wave0(cnt, P, off);
+  const int ne = v.ecount[e];
+  record_offsets_wave0(cnt, P, off, wire_table_bytes(ne));
   __syncthreads();
   int bad = 0;
   const int64_t total = *v.total;
@@ -324,7 +422,7 @@ __global__ void __launch_bounds__(128) wire_check_kernel(const uint8_t* wire, in
     if (e == 0 && base != wire_header_bytes(n, P)) bad |= 2;
     const int64_t end = e + 1 < n ? v.env_off[e + 1] : total;
     if (end - base != (int64_t)off[P] + 32 * nm) bad |= 2;
-    if (nm > NMMO_MARKET_ROWS) bad |= 4;
+    if (nm > NMMO_MARKET_ROWS || ne > kMaxSlots) bad |= 4;
   }
   if (a < P) {
     const uint32_t c = cnt[a];
@@ -335,6 +433,19 @@ __global__ void __launch_bounds__(128) wire_check_kernel(const uint8_t* wire, in
       } else if (base + off[a] + kWireHead <= total) {
         const int16_t* h = reinterpret_cast<const int16_t*>(v.base + base + off[a]);
         if (h[0] <= 0 || h[5] != nv || (h[6] & 0xFF) != ninv || ((uint16_t)h[6] >> 8) > 1) bad |= 8;
+        if (base + off[a] + wire_record_bytes(c) <= total) {  // entity-table indices, 8 per 16-B load
+          const uint4* ix4 = reinterpret_cast<const uint4*>(h + kWireBody / 2);
+          uint4 q[(kNObs + 7) / 8];
+#pragma unroll
+          for (int j = 0; j < (kNObs + 7) / 8; j++) q[j] = 8 * j < nv ? ix4[j] : make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+          for (int j = 0; j < (kNObs + 7) / 8; j++) {
+            const uint32_t wd[4] = {q[j].x, q[j].y, q[j].z, q[j].w};
+#pragma unroll
+            for (int i = 0; i < 8; i++)
+              if (8 * j + i < nv && ((wd[i >> 1] >> (16 * (i & 1))) & 0xFFFFu) >= (uint32_t)ne) bad |= 16;
+          }
+        }
       } else {
         bad |= 2;
       }
@@ -354,13 +465,17 @@ __global__ void __launch_bounds__(256) wire_expand_kernel(ObsParams p) {
   int16_t* mk = reinterpret_cast<int16_t*>(smem);                         // [1024][16]
   int* off = reinterpret_cast<int*>(smem + NMMO_MARKET_ROWS * 32);        // [P + 1]
   uint4* recbuf = reinterpret_cast<uint4*>(smem + NMMO_MARKET_ROWS * 32 + 144 * 4);  // [4][kRecMaxU4]
+  uint4* tab4 = recbuf + 4 * kRecMaxU4;  // the env's entity table
   const int P = p.P, e = blockIdx.x, g = blockIdx.y, tid = threadIdx.x, lane = lane_id(), w = wave_id();
   WireView v = wire_view(p.wire, p.n_envs, P);
   const uint16_t* cnt = v.cnt + (size_t)e * P;
-  record_offsets_wave0(cnt, P, off);
+  const int ne = min((int)v.ecount[e], kMaxSlots);
+  record_offsets_wave0(cnt, P, off, wire_table_bytes(ne));
   __syncthreads();
   const uint8_t* penv = v.base + v.env_off[e];
   const int nm = v.mcount[e];
+  for (int k = tid; k < wire_table_bytes(ne) / 16; k += blockDim.x) tab4[k] = reinterpret_cast<const uint4*>(penv)[k];
+  const int16_t* tab = reinterpret_cast<const int16_t*>(tab4);
   {
     const uint4* src = reinterpret_cast<const uint4*>(penv + off[P]);
     uint4* dst = reinterpret_cast<uint4*>(mk);
@@ -384,8 +499,9 @@ __global__ void __launch_bounds__(256) wire_expand_kernel(ObsParams p) {
     record_to_lds(penv + off[a], wire_record_bytes(c) / 16, lrec);
     const int16_t* h16 = reinterpret_cast<const int16_t*>(lb);
     const uint32_t* bits = reinterpret_cast<const uint32_t*>(lb + kWireHead);
-    const int16_t* s16 = reinterpret_cast<const int16_t*>(lb + kWireBody);
-    const uint8_t* mat = lb + kWireBody + 62 * nv + 32 * ninv;
+    const uint16_t* idx = reinterpret_cast<const uint16_t*>(lb + kWireBody);
+    const int16_t* s16 = reinterpret_cast<const int16_t*>(lb + kWireBody + 2 * nv);  // Inventory rows
+    const uint8_t* mat = lb + kWireBody + 2 * nv + 32 * ninv;
     const bool exch = ((uint16_t)h16[6] >> 8) != 0;
     const int gold = h16[7], aid = h16[0];
     for (int j = lane; j < p.o_agent_id; j += 64) {
@@ -401,10 +517,12 @@ __global__ void __launch_bounds__(256) wire_expand_kernel(ObsParams p) {
     }
     if (lane == 0) row[p.o_agent_id] = (float)h16[0];
     if (lane == 1) row[p.o_tick] = (float)h16[1];
-    for (int j = lane; j < kNObs * NMMO_N_ENTITY_COLS; j += 64)
-      row[p.o_entity + j] = j < nv * NMMO_N_ENTITY_COLS ? (float)s16[j] : 0.f;
-    for (int j = lane; j < kInv * 16; j += 64)
-      row[p.o_inventory + j] = j < ninv * 16 ? (float)s16[nv * NMMO_N_ENTITY_COLS + j] : 0.f;
+    for (int j = lane; j < kNObs * NMMO_N_ENTITY_COLS; j += 64) {
+      const int k = j / NMMO_N_ENTITY_COLS;
+      row[p.o_entity + j] =
+          k < nv ? (float)tab[min((int)idx[k], kMaxSlots - 1) * NMMO_N_ENTITY_COLS + j - k * NMMO_N_ENTITY_COLS] : 0.f;
+    }
+    for (int j = lane; j < kInv * 16; j += 64) row[p.o_inventory + j] = j < ninv * 16 ? (float)s16[j] : 0.f;
     for (int j = lane; j < NMMO_MARKET_ROWS * 16; j += 64) row[p.o_market + j] = (float)mk[j];
     const float* temb = p.task + (size_t)h16[2] * p.task_dim;
     for (int j = lane; j < p.task_dim; j += 64) row[p.o_task + j] = temb[j];
@@ -420,7 +538,7 @@ __global__ void __launch_bounds__(256) wire_expand_kernel(ObsParams p) {
 hipError_t launch_wire_pack(const uint16_t* counts, const int* mcount, const uint8_t* native, uint8_t* wire, int n,
                             int P, const int16_t* ent, int S, int exch, hipStream_t s) {
   if (P > 128 || n <= 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(wire_size_kernel, dim3(n), dim3(128), 0, s, counts, mcount, wire, n, P);
+  hipLaunchKernelGGL(wire_size_kernel, dim3(n), dim3(128), 0, s, counts, mcount, native, wire, n, P);
   hipLaunchKernelGGL(wire_scan_kernel, dim3(1), dim3(1024), 0, s, wire, n, P);
   hipLaunchKernelGGL(wire_pack_kernel, dim3(n, (P + kWireAgentsPerBlock - 1) / kWireAgentsPerBlock), dim3(256), 0, s,
                      native, wire, n, P, ent, S, exch);
@@ -448,7 +566,8 @@ hipError_t launch_wire_check(const uint8_t* wire, int n, int P, const int64_t* e
   return hipGetLastError();
 }
 
-constexpr size_t kWireExpandLds = (size_t)NMMO_MARKET_ROWS * 32 + 144 * 4 + (size_t)4 * kRecMaxU4 * 16;  // 61.4 KB
+constexpr size_t kWireExpandLds = (size_t)NMMO_MARKET_ROWS * 32 + 144 * 4 + (size_t)4 * kRecMaxU4 * 16 +
+                                  (size_t)kMaxSlots * kEntRow;  // 59.6 KB
 
 hipError_t launch_wire_expand(const ObsParams& p, hipStream_t s) {
   if (p.P > 128 || p.n_envs <= 0 || !p.wire || !p.obs) return hipErrorInvalidValue;

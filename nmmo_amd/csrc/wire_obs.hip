@@ -1,23 +1,25 @@
 // wire_obs.hip — NMMO_OBS_WIRE: the per-agent observation gather written straight as wire
 // records (SPEC.md §8c), the C5 sender's obs kernel.
 //
-// Same observation as obs_kernel's native layout (SPEC §8b; `nmmo_wire_pack` of it is
-// byte-identical, tests/test_gpu_wire.py), built for what a record is: ~0.55 KB per agent of
-// bits and a few rows, so the kernel is bound by the per-agent dependency chain, not bytes.
+// Same observation as the native layout (SPEC §8b; `nmmo_wire_pack` of it is byte-identical,
+// tests/test_gpu_wire.py), built for what a record is: ~0.3 KB per agent of bits, entity-table
+// indices and a few rows, so the kernel is bound by the per-agent dependency chain, not bytes.
 // Staging, window compaction and the ActionTargets bit fields are agent_obs.h's (shared with
-// the native kernel); the 561-bit image is assembled with scalar ops, and the record goes out as one dword store for head + mask, one dword store per 4 Entity rows
-//    (row pairs are 31 dwords), and u16 stores for the Inventory rows, the 4-bit materials and
-//    the zero pad.
-// The header's count words and per-env offsets come from wire_count_kernel + wire_scan_kernel
-// (wire.hip): record sizes are taken from the count words, so records never overlap.
+// the native kernel); the 561-bit image is assembled with scalar ops and goes out with the head
+// as one dword store, the Entity rows as u16 entity-table indices, then u16 stores for the
+// Inventory rows, the 4-bit materials and the zero pad. The env's entity table (the rows some
+// record shows, one 62-B row each) is written once per env from the staged columns.
+// The header's count words, entity-table ranks and per-env offsets come from wire_count_kernel +
+// wire_scan_kernel (wire.hip): record sizes are taken from the count words, so records never
+// overlap whatever the state holds.
 #include "agent_obs.h"
 
 namespace nmmo {
 
 // LDS: agent_obs.h's entity staging | per-wave visible rows | per-wave window materials | the
-// env's record offsets. 29.3 KB at S = 384: 5 workgroups per CU.
+// env's record offsets | the slots' entity-table indices. 30 KB at S = 384: 5 workgroups per CU.
 __host__ __device__ inline size_t wo_lds_bytes(int S) {
-  return ao_entity_lds(S) + (size_t)kAoWaves * (128 * 4 + 256) + (size_t)(128 + 4) * 4;
+  return ao_entity_lds(S) + (size_t)kAoWaves * (128 * 4 + 256) + (size_t)(128 + 4) * 4 + (size_t)kMaxSlots * 2;
 }
 
 template <bool kWrap>
@@ -29,12 +31,15 @@ __global__ void __launch_bounds__(256) wire_obs_kernel(ObsParams p) {
   uint32_t* visw_all = pk + kMaxSlots + 64;               // [4][128] packed words of the visible rows
   uint8_t* wmat_all = reinterpret_cast<uint8_t*>(visw_all + kAoWaves * 128);  // [4][256] window materials
   int* woff = reinterpret_cast<int*>(wmat_all + kAoWaves * 256);            // [P + 1] record offsets
+  uint16_t* rk = reinterpret_cast<uint16_t*>(woff + 128 + 4);                // [kMaxSlots] table index
   const int e = blockIdx.x, g = blockIdx.y, tid = threadIdx.x, lane = lane_id();
   const int w = __builtin_amdgcn_readfirstlane(wave_id());  // wave-uniform values in SGPRs
   const WireView v = wire_view(p.wire, p.n_envs, P);
   const uint16_t* cnt = v.cnt + (size_t)e * P;
-  record_offsets_wave0(cnt, P, woff);
-  ao_stage(p, e, T, pk);  // (publishes woff too)
+  const int ne = v.ecount[e];
+  record_offsets_wave0(cnt, P, woff, wire_table_bytes(ne));
+  for (int s = tid; s < kMaxSlots; s += blockDim.x) rk[s] = p.wrank[(size_t)e * kMaxSlots + s];
+  ao_stage(p, e, T, pk);  // (publishes woff and rk too)
 
   uint8_t* wenv = p.wire + v.env_off[e];
   const int nm = min(max(p.mcount[e], 0), NMMO_MARKET_ROWS);
@@ -51,6 +56,16 @@ __global__ void __launch_bounds__(256) wire_obs_kernel(ObsParams p) {
       mk[2 * k] = make_uint4(q[0], q[1], q[2], q[3]);
       mk[2 * k + 1] = make_uint4(q[4], q[5], q[6], q[7]);
     }
+    // the entity table: the 31 columns of each shown slot at its index (a thread per slot), then
+    // the table's zero pad
+    int16_t* tab = reinterpret_cast<int16_t*>(wenv);
+    for (int s = tid; s < S; s += blockDim.x) {
+      const int x = rk[s];
+      if (x == 0xFFFF) continue;
+#pragma unroll
+      for (int f = 0; f < NMMO_N_ENTITY_COLS; f++) tab[x * NMMO_N_ENTITY_COLS + f] = T[f * Sp + s];
+    }
+    for (int b = kEntRow * ne + tid; b < wire_table_bytes(ne); b += blockDim.x) wenv[b] = 0;
   }
 
   uint32_t pr[kAoRows];  // this lane's datastore rows 1 + lane + 64 i
@@ -75,14 +90,13 @@ __global__ void __launch_bounds__(256) wire_obs_kernel(ObsParams p) {
   }
   uint2 iv = make_uint2(0u, 0u);
   uint32_t wm[4] = {0u, 0u, 0u, 0u};
+  int mo[2];
+  ao_window_offsets(mo);
   auto prefetch = [&](int a) {
-    const int r = T[F_ROW * Sp + a], c = T[F_COL * Sp + a];
+    const int at = T[F_ROW * Sp + a] * kSize + T[F_COL * Sp + a];
     iv = lane < kInv ? p.items[((size_t)e * P + a) * kInv + lane] : make_uint2(0u, 0u);
 #pragma unroll
-    for (int i = 0; i < 4; i++) {
-      const int t = lane + 64 * i;
-      wm[i] = t < 225 ? mat[(r + t / 15 - kVision) * kSize + c + t % 15 - kVision] : 0u;
-    }
+    for (int i = 0; i < 4; i++) wm[i] = lane + 64 * i < 225 ? mat[at + ao_window_off(mo, i)] : 0u;
   };
   auto in_realm = [&](int j) {
     const int a = abase + kAoWaves * j;
@@ -138,32 +152,12 @@ __global__ void __launch_bounds__(256) wire_obs_kernel(ObsParams p) {
       x = writelanes<4, 0, (kWireMaskBits + 31) / 32>(img, x);
       if (lane < (kWireBody >> 2)) reinterpret_cast<int*>(rec)[lane] = x;
     }
-    // Entity rows, four per pass: a row pair is 31 dwords (4-B aligned: 96 + 124 j), lanes
-    // 0-30 the pair (k, k + 1), lanes 32-62 the pair (k + 2, k + 3); a pair's last dword holds
-    // the next region's first int16 when k + 1 == nv (then only its low half is stored)
-    {
-      const int i = lane & 31, hp = lane >> 5;
-      const int c0 = 2 * i, c1 = 2 * i + 1;
-      const int r0 = c0 >= NMMO_N_ENTITY_COLS, r1 = c1 >= NMMO_N_ENTITY_COLS;
-      const int f0 = c0 - r0 * NMMO_N_ENTITY_COLS, f1 = c1 - r1 * NMMO_N_ENTITY_COLS;
-#pragma unroll 1
-      for (int k0 = 0; k0 < nv; k0 += 4) {
-        const int k = k0 + 2 * hp, ka = k + r0, kb = k + r1;
-        if (i < NMMO_N_ENTITY_COLS && ka < nv) {
-          const int lo = T[f0 * Sp + ao_slot(visw[ka])];
-          uint8_t* dst = rec + kWireBody + 62 * k + 4 * i;
-          if (kb < nv) {
-            const int hi = T[f1 * Sp + ao_slot(visw[kb])];
-            *reinterpret_cast<uint32_t*>(dst) = i16pack(lo, hi);
-          } else {
-            *reinterpret_cast<int16_t*>(dst) = (int16_t)lo;
-          }
-        }
-      }
-    }
+    // Entity rows: each visible row's entity-table index
+    if (lane < nv) reinterpret_cast<uint16_t*>(rec + kWireBody)[lane] = rk[ao_slot(visw[lane])];
+    if (lane + 64 < nv) reinterpret_cast<uint16_t*>(rec + kWireBody)[lane + 64] = rk[ao_slot(visw[lane + 64])];
     // Inventory rows | materials (4 bits, 4 per int16) | zero pad, as int16 stores
     {
-      const int R = kWireBody + 62 * nv;
+      const int R = kWireBody + 2 * nv;
       const int H = (wire_record_bytes(cw) - R) >> 1;
       const int ni = 16 * ninv;
       const uint32_t* wm32 = reinterpret_cast<const uint32_t*>(wmat);

@@ -2,13 +2,15 @@
 
 BASELINE config 5 returns every rank's observations to one learner GPU over xGMI. The native
 layout (9,552 B per agent + 32 KB Market per env) is mostly padding on the wire; a wire buffer
-(`nmmo_wire_pack`, csrc/wire.hip) keeps the 16-B record head, the ActionTargets as bits, only
-the visible Entity rows and held items, the 225 window materials and only the listed Market
-rows: ~1.3 KB per agent in C4 steady state. The receiver decodes it back to the native layout
-bit-identically (`nmmo_wire_unpack`). A handle created with obs_layout OBS_WIRE writes the same
-bytes straight from the state (nmmo_step / nmmo_observe into a wire buffer), with no native
-buffer at all. The transfer protocol — the fixed-size header first, then
-exactly the payload the header announces — is `nmmo_amd.distributed.gather_wire_to_learner`.
+(`nmmo_wire_pack`, csrc/wire.hip) keeps the 16-B record head, the ActionTargets as bits except
+Buy.MarketItem (rebuilt from the listings), an entity-table index per visible Entity row (each
+env's distinct rows travel once), the held items, the 225 window materials at 4 bits and only
+the listed Market rows: ~0.3 KB per agent in the realm in C4 steady state. The receiver decodes
+it back to the native layout bit-identically (`nmmo_wire_unpack`). A handle created with
+obs_layout OBS_WIRE writes the same bytes straight from the state (nmmo_step / nmmo_observe into
+a wire buffer), with no native buffer at all. The transfer protocol — sizes a step ahead of
+their payload, then exactly the bytes the header announced — is
+`nmmo_amd.distributed.WireExchange` / `WireGather`.
 """
 
 from __future__ import annotations
@@ -67,7 +69,8 @@ def check_buffer(wire: torch.Tensor, n_envs: int, players: int, status: torch.Te
                  expect_total: torch.Tensor | None = None) -> torch.Tensor:
     """Enqueue the consistency check of a (received) wire buffer (nmmo_wire_check): error bits
     are OR-ed into `status` (device int32 [1]; 0 = valid: 1 total != expect_total, 2 offsets, 4
-    count ranges, 8 record heads). `expect_total`: device int64 [1] the sender announced."""
+    count ranges, 8 record heads, 16 entity-table indices). `expect_total`: device int64 [1] the
+    sender announced."""
     if status.dtype != torch.int32 or status.device != wire.device:
         raise ValueError("status must be an int32 tensor on the wire buffer's device")
     if expect_total is not None and (expect_total.dtype != torch.int64 or expect_total.device != wire.device):

@@ -242,13 +242,14 @@ NMMO_API int nmmo_dev_free(void* ptr) {
 }
 NMMO_API int64_t nmmo_wire_header_bytes(int32_t n_envs, int32_t player_n) {
   if (n_envs <= 0 || player_n <= 0 || player_n > 128) return fail(NMMO_E_INVALID, "n_envs > 0, player_n in 1..128");
-  return ((8 + 8 * (int64_t)n_envs + 2 * (int64_t)n_envs * player_n + 2 * (int64_t)n_envs) + 15) & ~(int64_t)15;
+  return ((8 + 8 * (int64_t)n_envs + 2 * (int64_t)n_envs * player_n + 4 * (int64_t)n_envs) + 15) & ~(int64_t)15;
 }
 NMMO_API int64_t nmmo_wire_max_bytes(int32_t n_envs, int32_t player_n) {
   const int64_t hdr = nmmo_wire_header_bytes(n_envs, player_n);
   if (hdr < 0) return hdr;
-  const int64_t rec = (96 + 62 * 100 + 32 * NMMO_INV_SLOTS + 113 + 15) & ~15; /* SPEC §8c v2 record */
-  return hdr + (int64_t)n_envs * ((int64_t)player_n * rec + NMMO_NATIVE_MARKET_BYTES);
+  const int64_t rec = (96 + 2 * 100 + 32 * NMMO_INV_SLOTS + 113 + 15) & ~15; /* SPEC §8c v3 record */
+  const int64_t table = (62 * 384 + 15) & ~15; /* a full entity table (kMaxSlots rows) */
+  return hdr + (int64_t)n_envs * (table + (int64_t)player_n * rec + NMMO_NATIVE_MARKET_BYTES);
 }
 NMMO_API int nmmo_wire_pack(NmmoHandle* h, const void* native, void* wire, void* stream) {
   (void)h; (void)native; (void)wire; (void)stream;

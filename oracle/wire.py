@@ -5,7 +5,9 @@ Checker for nmmo_amd/csrc/wire.hip. It derives every count from the native bytes
 ninv = Inventory rows with a non-zero item row; listings = Market rows with a non-zero item
 row), where the HIP path takes them from the obs kernel. The record head carries the agent's
 gold and the Exchange flag (state, not native bytes: the caller passes them); Buy.MarketItem is
-not sent and unpack rebuilds it from the listings. Never imported by the product path.
+not sent and unpack rebuilds it from the listings. Each env's distinct Entity rows travel once,
+in its entity table (ascending by the 16-bit pattern of the id), and a record holds the table
+index of each of its rows (v3). Never imported by the product path.
 """
 
 from __future__ import annotations
@@ -24,14 +26,18 @@ I16_TASK = I16_TILE + 225 * 3
 
 
 def header_bytes(n: int, P: int) -> int:
-    return (8 + 8 * n + 2 * n * P + 2 * n + 15) & ~15
+    return (8 + 8 * n + 2 * n * P + 4 * n + 15) & ~15
 
 
 def record_bytes(cnt: int) -> int:
     if not cnt & 0x8000:
         return 0
     nv, ninv = cnt & 127, (cnt >> 7) & 15
-    return (HEAD + MASK + 62 * nv + 32 * ninv + TILES + 15) & ~15
+    return (HEAD + MASK + 2 * nv + 32 * ninv + TILES + 15) & ~15
+
+
+def table_bytes(ne: int) -> int:
+    return (62 * ne + 15) & ~15
 
 
 def _rows(native: np.ndarray, P: int):
@@ -54,9 +60,24 @@ def counts(native: np.ndarray, P: int):
     return cnt, nm
 
 
-def listing_offset(cnt_env) -> int:
-    """Offset of an env's listings in its payload: the sum of its records."""
-    return sum(record_bytes(int(c)) for c in cnt_env)
+def listing_offset(cnt_env, ne: int) -> int:
+    """Offset of an env's listings in its payload: its entity table and records."""
+    return table_bytes(ne) + sum(record_bytes(int(c)) for c in cnt_env)
+
+
+def _table(i16e: np.ndarray, cnt_e: np.ndarray):
+    """One env's entity table: {id: row} over its records' Entity rows, and the ids in table
+    order (ascending by the id's 16-bit pattern)."""
+    rows = {}
+    for a, c in enumerate(cnt_e):
+        c = int(c)
+        if not c & 0x8000:
+            continue
+        ent = i16e[a, I16_ENTITY:I16_ENTITY + NE * (c & 127)].reshape(-1, NE)
+        for r in ent:
+            rows.setdefault(int(r[0]), r)
+    order = sorted(rows, key=lambda i: i & 0xFFFF)
+    return rows, order
 
 
 def pack(native: np.ndarray, P: int, gold: np.ndarray, exch: bool = True) -> np.ndarray:
@@ -65,8 +86,10 @@ def pack(native: np.ndarray, P: int, gold: np.ndarray, exch: bool = True) -> np.
     n = native.shape[0]
     rows, i16, market = _rows(native, P)
     cnt, nm = counts(native, P)
+    tables = [_table(i16[e], cnt[e]) for e in range(n)]
+    ne = np.array([len(t[1]) for t in tables], np.uint16)
     H = header_bytes(n, P)
-    env_bytes = [sum(record_bytes(int(c)) for c in cnt[e]) + 32 * int(nm[e]) for e in range(n)]
+    env_bytes = [listing_offset(cnt[e], int(ne[e])) + 32 * int(nm[e]) for e in range(n)]
     env_off = np.cumsum([H] + env_bytes)
     total = int(env_off[-1])
     out = np.zeros(total, np.uint8)
@@ -75,8 +98,14 @@ def pack(native: np.ndarray, P: int, gold: np.ndarray, exch: bool = True) -> np.
     o = 8 + 8 * n
     out[o:o + 2 * n * P] = cnt.reshape(-1).view(np.uint8)
     out[o + 2 * n * P:o + 2 * n * P + 2 * n] = nm.view(np.uint8)
+    out[o + 2 * n * P + 2 * n:o + 2 * n * P + 4 * n] = ne.view(np.uint8)
     for e in range(n):
         pos = int(env_off[e])
+        trows, order = tables[e]
+        index = {i: k for k, i in enumerate(order)}
+        if order:
+            out[pos:pos + 62 * len(order)] = np.stack([trows[i] for i in order]).astype(np.int16).view(np.uint8).reshape(-1)
+        pos += table_bytes(len(order))
         for a in range(P):
             c = int(cnt[e, a])
             if not c & 0x8000:
@@ -90,8 +119,9 @@ def pack(native: np.ndarray, P: int, gold: np.ndarray, exch: bool = True) -> np.
             bits = np.packbits(rows[e, a, SENT] != 0, bitorder="little")
             rec[HEAD:HEAD + len(bits)] = bits
             k = HEAD + MASK
-            rec[k:k + 62 * nv] = q[I16_ENTITY:I16_ENTITY + NE * nv].view(np.uint8)
-            k += 62 * nv
+            ids = q[I16_ENTITY:I16_ENTITY + NE * nv].reshape(-1, NE)[:, 0]
+            rec[k:k + 2 * nv] = np.array([index[int(i)] for i in ids], np.uint16).view(np.uint8)
+            k += 2 * nv
             rec[k:k + 32 * ninv] = q[I16_INV:I16_INV + 16 * ninv].view(np.uint8)
             k += 32 * ninv
             mats = np.zeros(2 * TILES, np.uint8)
@@ -110,8 +140,11 @@ def unpack(wire: np.ndarray, n: int, P: int) -> np.ndarray:
     o = 8 + 8 * n
     cnt = wire[o:o + 2 * n * P].copy().view(np.uint16).reshape(n, P)
     nm = wire[o + 2 * n * P:o + 2 * n * P + 2 * n].copy().view(np.uint16)
+    ne = wire[o + 2 * n * P + 2 * n:o + 2 * n * P + 4 * n].copy().view(np.uint16)
     for e in range(n):
         pos = int(env_off[e])
+        table = wire[pos:pos + 62 * int(ne[e])].copy().view(np.int16).reshape(-1, NE)
+        pos += table_bytes(int(ne[e]))
         for a in range(P):
             c = int(cnt[e, a])
             if not c & 0x8000:
@@ -127,15 +160,16 @@ def unpack(wire: np.ndarray, n: int, P: int) -> np.ndarray:
             buy[BUY_N - 1] = 1
             nmk = int(nm[e])
             if nmk and (int(head[6]) >> 8) & 1:
-                lo = int(env_off[e]) + listing_offset(cnt[e])
+                lo = int(env_off[e]) + listing_offset(cnt[e], int(ne[e]))
                 lst = wire[lo:lo + 32 * nmk].copy().view(np.int16).reshape(nmk, 16)
                 buy[:nmk] = (lst[:, 15] <= head[7]) & (lst[:, 2] != head[0])
             row[BUY_LO:BUY_LO + BUY_N] = buy
             q = np.zeros(abi.NATIVE_I16, np.int16)
             q[0], q[1] = head[0], head[1]
             k = HEAD + MASK
-            q[I16_ENTITY:I16_ENTITY + NE * nv] = rec[k:k + 62 * nv].copy().view(np.int16)
-            k += 62 * nv
+            idx = rec[k:k + 2 * nv].copy().view(np.uint16)
+            q[I16_ENTITY:I16_ENTITY + NE * nv] = table[idx].reshape(-1)
+            k += 2 * nv
             q[I16_INV:I16_INV + 16 * ninv] = rec[k:k + 32 * ninv].copy().view(np.int16)
             k += 32 * ninv
             t = np.arange(225)
