@@ -1195,7 +1195,9 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
 #pragma unroll
     for (int k = 0; k < 2; k++) c.tdesc[s * 2 + k] = make_int4(tk.term[k].pred, tk.term[k].a, tk.term[k].b, tk.term[k].c);
   }
-  __syncthreads();
+  // only the listed-row bitmap's zeroing must precede this phase's writes (its atomicOr); pres,
+  // misc and tdesc are read after the phase's closing barrier
+  if (c.exch) __syncthreads();
   // Materials around this slot's tile at tick start, loaded here so their latency hides behind
   // the decode; used after it through `nbm`. Passability and Water never change within a tick
   // (every depletion/regrowth maps passable to passable and impassable to impassable), and no
@@ -2197,6 +2199,7 @@ __device__ __forceinline__ void tick_body(const DevState& st, const int32_t* __r
   NMMO_STAMP(20);
   const size_t o = (size_t)e * c.P;
   const bool reset_path = mode == 1 || c.E[E_DONE];
+  const int alive0 = c.E[E_PLAYERS_ALIVE];  // players in the realm at tick start (sum of pres)
   const int ev_start = c.E[E_EVENT_COUNT];  // event rows this tick appends (counters[2])
   if (reset_path) {
     const int env_global = (int)(st.cfg.env_index_base + (uint64_t)e);
@@ -2231,15 +2234,14 @@ __device__ __forceinline__ void tick_body(const DevState& st, const int32_t* __r
     tick_env(c, actions + o * kHeads, a_pre, rew + o, term + o, trunc + o, mask + o);
   }
   __syncthreads();
-  if (st.counters) {  // sum(mask) of this launch (pres, or all players on a reset) + done envs;
-    // one atomic per wave, no block barrier
+  if (st.counters && threadIdx.x == 0) {  // sum(mask) of this launch + done envs + event rows, one
+    // thread (no barrier; one atomic per counter and workgroup: per-wave atomics on one address
+    // serialise in L2 and held C3 launches ~5 us longer). sum(mask) = the players present at
+    // tick start (pres = alive = E_PLAYERS_ALIVE then), or all players on a reset.
     const bool reset = mode == 1 || reset_path;
-    const int n = __popcll(__ballot(threadIdx.x < c.P && (reset || c.pres[threadIdx.x])));
-    if (lane_id() == 0 && n) atomicAdd(&st.counters[0], (unsigned long long)n);
-    if (threadIdx.x == 0) {
-      if (!reset && c.E[E_DONE]) atomicAdd(&st.counters[1], 1ull);
-      if (!reset && c.evcap) atomicAdd(&st.counters[2], (unsigned long long)(c.E[E_EVENT_COUNT] - ev_start));
-    }
+    atomicAdd(&st.counters[0], (unsigned long long)(reset ? c.P : alive0));
+    if (!reset && c.E[E_DONE]) atomicAdd(&st.counters[1], 1ull);
+    if (!reset && c.evcap) atomicAdd(&st.counters[2], (unsigned long long)(c.E[E_EVENT_COUNT] - ev_start));
   }
   NMMO_STAMP(10);
   store_market(c, st, e);

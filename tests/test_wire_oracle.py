@@ -43,6 +43,41 @@ def test_wire_roundtrip_and_size():
     assert w.nbytes * 4 < nat.nbytes, (w.nbytes, nat.nbytes)
 
 
+def test_wire_entity_table():
+    """v3: each env's entity table holds every distinct Entity row its records show exactly once,
+    ascending by the id's 16-bit pattern, and every record's indices select its own rows; an
+    entity seen by several agents makes the buffer smaller than inline rows would."""
+    nat, P, gold = _native(3, 50, seed=6, with_gold=True)
+    w = owire.pack(nat, P, gold)
+    n = 3
+    env_off = w[8:8 + 8 * n].copy().view(np.int64)
+    o = 8 + 8 * n
+    cnt = w[o:o + 2 * n * P].copy().view(np.uint16).reshape(n, P)
+    ne = w[o + 2 * n * P + 2 * n:o + 2 * n * P + 4 * n].copy().view(np.uint16)
+    _, i16, _ = owire._rows(nat, P)
+    shown = inline = 0
+    for e in range(n):
+        table = w[int(env_off[e]):int(env_off[e]) + 62 * int(ne[e])].copy().view(np.int16).reshape(-1, owire.NE)
+        ids = table[:, 0].astype(np.int64) & 0xFFFF
+        assert np.all(np.diff(ids) > 0)  # unique, ascending by the 16-bit pattern
+        pos = int(env_off[e]) + owire.table_bytes(int(ne[e]))
+        seen = set()
+        for a in range(P):
+            c = int(cnt[e, a])
+            if not c & 0x8000:
+                continue
+            nv = c & 127
+            idx = w[pos + owire.HEAD + owire.MASK:pos + owire.HEAD + owire.MASK + 2 * nv].copy().view(np.uint16)
+            rows = i16[e, a, owire.I16_ENTITY:owire.I16_ENTITY + owire.NE * nv].reshape(-1, owire.NE)
+            assert np.array_equal(table[idx], rows)
+            seen.update(idx.tolist())
+            shown += nv
+            pos += owire.record_bytes(c)
+        assert seen == set(range(int(ne[e])))  # no row the records do not show
+        inline += int(ne[e])
+    assert shown > inline  # entities shared between agents travel once
+
+
 def test_wire_buy_mask_is_rebuilt_from_the_listings():
     """Buy.MarketItem is not sent: unpack rebuilds it from the env's listings, the head's gold
     and the agent id (an agent can buy a listing it can afford and does not own), so a record
