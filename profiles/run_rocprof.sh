@@ -16,6 +16,9 @@ for c in $CONFIGS; do
   mkdir -p $OUT/$c
   case $c in
     *-native) ARGS="--config ${c%-native} --obs native" ;;
+    # C5 at one GPU: one batch and no decoded pass (the two-batch run with the decode pass on
+    # the comm stream stopped making progress under the kernel trace in round 3)
+    C5) ARGS="--config C5 --batches 1 --no-decode" ;;
     *) ARGS="--config $c" ;;
   esac
   if [ "$c" = storage ]; then  # experience-storage kernels (tools/bench_storage.py)

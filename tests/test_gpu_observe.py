@@ -88,3 +88,31 @@ def test_batches_equal_one_handle():
     whole.close()
     for h in halves:
         h.close()
+
+
+@pytest.mark.parametrize("preset", ["C2", "C3", "C4"])
+def test_counters_equal_the_outputs(preset):
+    """The device counters the bench reads (nmmo_set_counters): agent-steps = the sum of every
+    step's mask, event rows = the growth of the event count, over staggered episode ends and
+    auto-resets (the tick adds them with one atomic per workgroup)."""
+    from nmmo_amd import abi
+    from nmmo_amd.config import Config
+    from nmmo_amd.engine import NmmoEngine
+
+    cfg = Config.preset(preset, MAP_N=4, early_stop_agent_num=8, obs_layout=abi.OBS_NONE)
+    n = 12
+    eng = NmmoEngine(cfg, n, seed=17)
+    eng.reset()
+    cnt = torch.zeros(3, dtype=torch.int64, device=eng.device)
+    eng.set_counters(cnt)
+    ids = np.arange(n)
+    total = 0
+    for t in range(40):
+        eng.end_episodes(ids % 8 == t % 8)
+        eng.scripted_actions(500 + t)
+        eng.step(write_obs=False)
+        total += int(eng.mask.sum().item())
+    torch.cuda.synchronize()
+    assert int(cnt[0].item()) == total
+    assert int(cnt[1].item()) >= 0 and int(cnt[2].item()) > 0
+    eng.close()
