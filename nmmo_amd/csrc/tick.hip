@@ -1929,45 +1929,46 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
              sell_price, 0);
     evn += (tot & 0xFFFF) + (tot >> 16);
   }
-  __syncthreads();
+  // (no barrier: the cull reads only this slot's own fields, which only this thread wrote since
+  // the attack rounds' last barrier)
   NMMO_STAMP(6);
 
-  // 4. cull: rows appended to the free ring in slot order; NPC slots compacted
+  // 4. cull: rows appended to the free ring in slot order; NPC slots compacted. One prefix sum
+  // places the dead slots' rows (bits 0-9), the dead players' events (10-17) and the dead
+  // players' freed item rows (18-31); every thread reads the ring tails before its barrier and
+  // thread 0 moves them after.
   const bool dead = inslot && TF(F_ALIVE, s) && TF(F_HEALTH, s) <= 0;
-  int ndead;
-  const int dpos = block_prefix_count(dead, wtot_next(c), &ndead);
-  int npdead;
-  const int ppos = block_prefix_count(dead && s < P, wtot_next(c), &npdead);
+  const int ring_tail = c.E[E_FREE_HEAD] + c.E[E_FREE_COUNT];
+  const int iring_tail = items ? c.E[E_ITEM_FREE_HEAD] + c.E[E_ITEM_FREE_COUNT] : 0;
+  uint2* dinv = items ? c.inv + (s < P ? s : 0) * kInv : nullptr;
+  const int nitem = (items && dead && s < P) ? inv_count(dinv) : 0;
+  static_assert(kMaxSlots < 1024 && kInv * 128 < (1 << 14), "cull scan fields");
+  int ctot;
+  const int cpre = block_prefix_sum((dead ? 1 : 0) | ((dead && s < P) ? 1 << 10 : 0) | nitem << 18, wtot_next(c), &ctot);
+  const int dpos = cpre & 1023, ppos = (cpre >> 10) & 255;
+  const int ndead = ctot & 1023, npdead = (ctot >> 10) & 255;
   if (s < P) c.died[s] = dead ? 1 : 0;
   if (evon) {  // AGENT_CULLED in slot order (players are slots 0..P-1: the same prefix)
     if (dead && s < P) ev_put(c, evn + ppos, s, EV_AGENT_CULLED, 0, 0, 0, 0, 0);
     evn += npdead;
   }
   if (dead) {
-    c.ring[(c.E[E_FREE_HEAD] + c.E[E_FREE_COUNT] + dpos) % S] = TF(F_DS_ROW, s);
+    c.ring[(ring_tail + dpos) % S] = TF(F_DS_ROW, s);
     TF(F_ALIVE, s) = 0;
     if (s < P) TF(F_DIED_TICK, s) = (int16_t)(tick + 1);
   }
-  if (items) {  // unlooted items of the dead are destroyed: rows freed in (slot, inventory) order
-    uint2* inv = c.inv + (s < P ? s : 0) * kInv;
-    const int n = (dead && s < P) ? inv_count(inv) : 0;
-    int tot;
-    const int pre = block_prefix_sum(n, wtot_next(c), &tot);
-    if (n) {
-      const int base = c.E[E_ITEM_FREE_HEAD] + c.E[E_ITEM_FREE_COUNT] + pre;
-      for (int k = 0; k < n; k++) {
-        c.iring[(base + k) % c.IC] = (int16_t)it_row(inv[k]);
-        inv[k] = make_uint2(0u, 0u);
-      }
-      TF(F_ITEM_LEVEL, s) = 0;
+  if (nitem) {  // unlooted items of the dead are destroyed: rows freed in (slot, inventory) order
+    const int base = iring_tail + (cpre >> 18);
+    for (int k = 0; k < nitem; k++) {
+      c.iring[(base + k) % c.IC] = (int16_t)it_row(dinv[k]);
+      dinv[k] = make_uint2(0u, 0u);
     }
-    __syncthreads();
-    if (tid == 0) c.E[E_ITEM_FREE_COUNT] += tot;
+    TF(F_ITEM_LEVEL, s) = 0;
   }
-  __syncthreads();
   if (tid == 0) {
     c.E[E_FREE_COUNT] += ndead;
     c.E[E_PLAYERS_ALIVE] -= npdead;
+    if (items) c.E[E_ITEM_FREE_COUNT] += ctot >> 18;
   }
   if (sys(c, NMMO_SYS_NPC) && ndead > npdead) {  // compaction only when an NPC left the realm
     const bool keep = s >= P && inslot && TF(F_ALIVE, s);
