@@ -1272,7 +1272,7 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
       grid_scan(c.glist, c.gstart[kCells + g + wdw.z], c.gstart[kCells + g + wdw.w + 1], r, col, setbit);
     }
   }
-  __syncthreads();
+  if (uses_grid(c.sysm)) __syncthreads();  // (without the grid the prep's barrier ordered all)
   NMMO_STAMP(13);
   // bits 0-3: neighbour d passable; 4-7: neighbour d is Water; 8-15: own tile material
   asm volatile("" : "+v"(mw0), "+v"(mw1), "+v"(mup), "+v"(mdn));
@@ -1371,6 +1371,13 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
     c.atgt[s] = (int16_t)my_tgt;
     c.asty[s] = (int16_t)my_sty;
   }
+  const bool grid = uses_grid(c.sysm);
+  if (!grid) {  // the position hash's LDS held nothing this tick: initialised before the barrier
+    for (int k = tid; k < kHash; k += nt) {
+      c.hkey[k] = -1;
+      c.hmin[k] = 0x7FFF;
+    }
+  }
   __syncthreads();
   NMMO_STAMP(2);
   // This player's task state (when it lives in HBM) and task, for the rewards. Loaded by every
@@ -1386,11 +1393,13 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
     tsr = c.tsg[s < P ? s : 0];
     tk = c.tasks[my_task];
   }
-  for (int k = tid; k < kHash; k += nt) {  // position hash (its LDS held the decode bitmap)
-    c.hkey[k] = -1;
-    c.hmin[k] = 0x7FFF;
+  if (grid) {
+    for (int k = tid; k < kHash; k += nt) {  // position hash (its LDS held the decode bitmap and grid)
+      c.hkey[k] = -1;
+      c.hmin[k] = 0x7FFF;
+    }
+    __syncthreads();
   }
-  __syncthreads();
 
   // 2. players.update / npcs.update. Every player in the realm registers its tile in the
   // position hash (lowest slot per tile via atomicMin): first-in-slot-order harvests.
@@ -1540,7 +1549,9 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
       c.E[E_ITEM_FREE_COUNT] -= tot;
     }
   }
-  __syncthreads();
+  // Without items the next phase that touches another slot's data or the hash's LDS is behind the
+  // harvest events' scan barrier (the tile writes are read after the cull's)
+  if (c.prof || items || !evon) __syncthreads();
   NMMO_STAMP(15);
   if (evon) {
     const int n = (int)e_eat + (int)e_drink + (e_fish > 0) + (e_fish_nl > 0) + (e_on_q >= 0) + (e_on_nl > 0);
@@ -1803,17 +1814,19 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
   // is all attacks no earlier attack conflicts with. The per-entity minimum is an atomicMax of
   // round << 16 | (0xFFFF - slot), so no reset between rounds is needed.
   int* mi = c.ft;
-  for (int k = tid; k < S; k += nt) mi[k] = 0;
-  if (tid < 3) c.wtot[16 + tid] = 0;  // attack-round flags
-  // equipment bonuses, once (players: equipped items; NPCs: spawn-time equipment): this slot's
-  // offense in its attack style (a register) and its defense (c.clist, read by its attackers)
   int eq_off = 0;
-  if (sys(c, NMMO_SYS_EQUIPMENT) && s < S) {
-    const int sty0 = c.asty[s];
-    eq_off = s < P ? (items ? inv_offense(c, s, sty0) : 0) : TF(F_EQUIP_OFFENSE, s);
-    c.clist[s] = (int16_t)(s < P ? (items ? inv_defense(c, s) : 0) : TF(F_EQUIP_DEFENSE, s));
+  if (combat || sys(c, NMMO_SYS_NPC)) {
+    for (int k = tid; k < S; k += nt) mi[k] = 0;
+    if (tid < 3) c.wtot[16 + tid] = 0;  // attack-round flags
+    // equipment bonuses, once (players: equipped items; NPCs: spawn-time equipment): this slot's
+    // offense in its attack style (a register) and its defense (c.clist, read by its attackers)
+    if (sys(c, NMMO_SYS_EQUIPMENT) && s < S) {
+      const int sty0 = c.asty[s];
+      eq_off = s < P ? (items ? inv_offense(c, s, sty0) : 0) : TF(F_EQUIP_OFFENSE, s);
+      c.clist[s] = (int16_t)(s < P ? (items ? inv_defense(c, s) : 0) : TF(F_EQUIP_DEFENSE, s));
+    }
+    __syncthreads();
   }
-  __syncthreads();
   NMMO_STAMP(4);
   if (combat || sys(c, NMMO_SYS_NPC)) {
     // One barrier per round: pending attackers raise flag r % 3 before it, and thread 0 clears
@@ -2105,7 +2118,9 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
     }
   }
   NMMO_STAMP(19);
-  __syncthreads();
+  // the NPC spawn reads the respawned tiles; the rewards read nothing the respawn wrote (the
+  // store reads it after tick_env's closing barrier)
+  if (sys(c, NMMO_SYS_NPC)) __syncthreads();
   if (tid == 0) c.E[E_TICK] = tick + 1;  // read only at the tick's start (and by store_env)
   NMMO_STAMP(8);
   // 7. NPC refill
