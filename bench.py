@@ -329,6 +329,15 @@ def _write_ceiling(t, dev):
     return t.numel() * t.element_size() / (s0.elapsed_time(s1) / 10 * 1e-3) / 1e9
 
 
+_T0 = time.perf_counter()
+
+
+def _progress(msg: str) -> None:
+    """A progress line on stderr (stdout carries only the JSON line): long runs stay visibly alive."""
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(f"bench.py [{time.perf_counter() - _T0:7.1f} s] {msg}", file=sys.stderr, flush=True)
+
+
 def measure(args, name, layout_name, envs, rank, world, dev, steps, warmup, dist=None, wrapper=None):
     """Build, stagger, warm up and time one gather-free workload on this rank; returns a result
     dict.
@@ -365,7 +374,9 @@ def measure(args, name, layout_name, envs, rank, world, dev, steps, warmup, dist
             e.set_wrapper(wrapper_config(wrapper, **WRAPPER_KW.get(wrapper, {})))
         e.reset()
     pseed = args.seed * 1_000_003  # the policy's Philox counter already walks (tick, episode)
+    _progress(f"{name}: {nb} engines built and reset")
     _stagger(engs, args.stagger, per, rank * envs, pseed)
+    _progress(f"{name}: staggered over {args.stagger} ticks")
     # device counters the tick kernel adds into: [0] = sum(mask) (agent-steps), [1] = episodes,
     # [2] = event-log rows appended
     counters = [torch.zeros(3, dtype=torch.int64, device=dev) for _ in engs]
@@ -421,6 +432,7 @@ def measure(args, name, layout_name, envs, rank, world, dev, steps, warmup, dist
     alive = float(tot[0].item())
     episodes = int(tot[1].item())
     events_per_env_tick = float(tot[2].item()) / (envs * steps) if cfg.event_cap > 0 else None
+    _progress(f"{name}: timed {steps} steps in {elapsed:.3f} s")
     tick_avg_ms, obs_avg_ms, wrap_avg_ms = _kernel_timing(eng, pseed, steps)
     # The roofline's tick duration without per-kernel event overhead (which inflates a ~15 us
     # launch by ~20%): the timed step (policy + nmmo_step, graph-replayed) minus a hipGraph of
@@ -540,7 +552,9 @@ def measure_gather(args, name, envs, rank, world, dev, steps, warmup, dist=None,
     for e in engs:
         e.reset()
     pseed = args.seed * 1_000_003
+    _progress(f"{name}: {nb} engines built and reset")
     _stagger(engs, args.stagger, per, rank * envs, pseed)
+    _progress(f"{name}: staggered over {args.stagger} ticks")
     counters = [torch.zeros(3, dtype=torch.int64, device=dev) for _ in engs]
     for e, c in zip(engs, counters):
         e.set_counters(c)
@@ -570,6 +584,7 @@ def measure_gather(args, name, envs, rank, world, dev, steps, warmup, dist=None,
         status = g.check_status()
         if status:
             raise RuntimeError(f"nmmo_wire_check flagged received wire buffers (status {status})")
+        _progress(f"{name}: timed {steps} steps in {elapsed:.3f} s (decode={decode})")
         passes[decode] = {"elapsed": elapsed, "alive": float(tot[0].item()), "episodes": int(tot[1].item()),
                           "events": float(tot[2].item()),
                           "payload_bytes_per_step": (g.x.payload_bytes - b0) / steps}
@@ -682,10 +697,12 @@ def main():
     json_out = os.fdopen(os.dup(1), "w")
     sys.stdout.flush()
     os.dup2(2, 1)
+    _progress("importing torch")
     import torch
     import torch.distributed as dist
 
     from nmmo_amd import _native
+    _progress("torch imported")
 
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -707,9 +724,13 @@ def main():
     envs = args.envs or wl["envs"]
 
     def run(nm, lay, wrapper, n_envs, steps, warmup):
+        t0 = time.perf_counter()
         if WORKLOADS[nm].get("gather"):
-            return measure_gather(args, nm, n_envs, rank, world, dev, steps, warmup, dist, backend)
-        return measure(args, nm, lay, n_envs, rank, world, dev, steps, warmup, dist, wrapper)
+            r = measure_gather(args, nm, n_envs, rank, world, dev, steps, warmup, dist, backend)
+        else:
+            r = measure(args, nm, lay, n_envs, rank, world, dev, steps, warmup, dist, wrapper)
+        _progress(f"{r['name']} measured in {time.perf_counter() - t0:.1f} s")
+        return r
 
     def reduce(res, key="elapsed", alive="alive"):
         vals = torch.tensor([res[key], res[alive], res["slots"]], dtype=torch.float64, device=dev)
@@ -755,6 +776,7 @@ def main():
 
             # the CPU leg builds the flat pufferlib row when the workload has obs (the
             # reference's CPU path; the oracle has no native writer)
+            _progress("CPU baseline")
             cpu = cpu_baseline(Config.preset(wl["preset"], early_stop_agent_num=8,
                                              obs_layout=abi.OBS_FLAT if wl["obs"] else abi.OBS_NONE),
                                args.cpu_seconds)

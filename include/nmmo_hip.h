@@ -422,6 +422,16 @@ NMMO_API int nmmo_set_timing(NmmoHandle* h, int32_t enable);
  * NULL disables. The caller owns and zeroes the buffer; capture-safe. */
 NMMO_API int nmmo_set_counters(NmmoHandle* h, uint64_t* dev_counters);
 NMMO_API int nmmo_read_timing(NmmoHandle* h, double* ms /* [3] */, int32_t* n);
+/* Tick fault word: every round loop of the tick (attack, Buy and Give rounds; SPEC §9 conflict
+ * rounds) and the position-hash probe stop at a bound the serial-order argument never reaches
+ * (rounds <= the number of pending actions). A launch that hits one records its first
+ * (NMMO_FAULT_* | env << 8) here instead of hanging, and that env's tick is then not the serial
+ * result. *fault = the word (0 = none); the word is cleared. Synchronous. */
+#define NMMO_FAULT_ATTACK_ROUNDS 1
+#define NMMO_FAULT_BUY_ROUNDS 2
+#define NMMO_FAULT_GIVE_ROUNDS 3
+#define NMMO_FAULT_HASH_PROBE 4
+NMMO_API int nmmo_get_fault(NmmoHandle* h, int32_t* fault);
 
 /* The event log of env `env` (realm.event_log.get_data): copies the most recent
  * min(retained, max_rows) rows, oldest first, into host_rows [max_rows][NMMO_EVENT_COLS] and

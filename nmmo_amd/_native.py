@@ -20,7 +20,7 @@ _lib = None
 SYMBOLS = [
     "nmmo_default_config", "nmmo_layout", "nmmo_create", "nmmo_destroy", "nmmo_reset",
     "nmmo_step", "nmmo_scripted_actions", "nmmo_get_state", "nmmo_set_state",
-    "nmmo_get_map_bank", "nmmo_set_map_bank", "nmmo_set_timing", "nmmo_read_timing", "nmmo_set_counters", "nmmo_get_events", "nmmo_set_tasks",
+    "nmmo_get_map_bank", "nmmo_set_map_bank", "nmmo_set_timing", "nmmo_read_timing", "nmmo_get_fault", "nmmo_set_counters", "nmmo_get_events", "nmmo_set_tasks",
     "nmmo_set_wrapper", "nmmo_get_wrapper_state", "nmmo_expand_obs", "nmmo_exp_scratch_ints",
     "nmmo_exp_store", "nmmo_exp_sort", "nmmo_exp_gae", "nmmo_gather_rows", "nmmo_n_envs",
     "nmmo_last_error", "nmmo_abi_version", "nmmo_end_episodes", "nmmo_build_info",
@@ -78,6 +78,7 @@ def declare(L):
     L.nmmo_get_map_bank.argtypes = [vp, vp, sz]
     L.nmmo_set_map_bank.argtypes = [vp, vp, sz]
     L.nmmo_set_timing.argtypes = [vp, i32]
+    L.nmmo_get_fault.argtypes = [vp, ctypes.POINTER(i32)]
     L.nmmo_read_timing.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i32)]
     L.nmmo_set_counters.argtypes = [vp, vp]
     L.nmmo_get_events.argtypes = [vp, i32, vp, i32, ctypes.POINTER(i32)]

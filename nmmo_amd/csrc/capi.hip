@@ -222,7 +222,7 @@ int nmmo_create(const NmmoConfig* cfg, int32_t n_envs, uint64_t seed, int32_t de
   ALLOC(h->d_ring, n * S * 2);
   ALLOC(h->d_mat, n * NMMO_MAP_TILES);
   ALLOC(h->d_dep, n * kBitmapWords * 4);
-  ALLOC(h->d_foreign, 4);
+  ALLOC(h->d_foreign, 8);  // [0] DevState::foreign, [1] DevState::fault
   ALLOC(h->d_bank, (size_t)cfg->map_n * NMMO_MAP_TILES);
   ALLOC(h->d_task, (size_t)(cfg->task_embed_dim > 0 ? cfg->task_embed_dim : 1) * 4);
   ALLOC(h->d_seeds, n * 8);
@@ -252,7 +252,8 @@ int nmmo_create(const NmmoConfig* cfg, int32_t n_envs, uint64_t seed, int32_t de
   h->st = DevState{h->d_env,   h->d_ent,   h->d_ring,  h->d_mat,    h->d_dep, h->d_bank,
                    h->d_items, h->d_iring, h->d_mlist, h->d_mcount, h->d_events,
                    h->d_tasks, h->d_assign, nullptr, h->d_tstate, 1,            0,           n_envs, P,
-                   N,          S,          seed,       nullptr,     *cfg,      h->d_foreign};
+                   N,          S,          seed,       nullptr,     *cfg,      h->d_foreign,
+                   h->d_foreign + 1};
   {  // default task table: everyone runs TickGE(task_num_tick) (SPEC §12)
     NmmoTask t;
     memset(&t, 0, sizeof(t));
@@ -599,6 +600,14 @@ int nmmo_set_timing(NmmoHandle* h, int32_t enable) {
   }
   h->timing = enable != 0;
   h->t_count = 0;
+  return NMMO_OK;
+}
+
+int nmmo_get_fault(NmmoHandle* h, int32_t* fault) {
+  if (!h || !fault) return fail(NMMO_E_INVALID, "null argument");
+  HIP_TRY(hipSetDevice(h->device));
+  HIP_TRY(hipMemcpy(fault, h->d_foreign + 1, 4, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemset(h->d_foreign + 1, 0, 4));
   return NMMO_OK;
 }
 

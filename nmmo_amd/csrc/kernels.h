@@ -45,6 +45,10 @@ struct DevState {
   // nmmo_reset clears it). While 0, the tick's respawn of a system set without professions needs
   // no map-bank read: its only depletion is Foilage eaten to Scrub.
   int32_t* foreign;
+  // device int: the first bounded tick loop that hit its bound (kFault* | env << 8), 0 = none
+  // (nmmo_get_fault). Every round loop stops at a bound the serial argument never reaches, so a
+  // state outside the tick's invariants ends the launch instead of hanging it.
+  int32_t* fault;
 };
 
 struct ObsParams {

@@ -39,7 +39,7 @@ struct Ctx {
   int16_t* amove;    // [S]
   int16_t* atgt;     // [S]
   int16_t* asty;     // [S]
-  int* ft;           // [S] per-entity scratch (closest-player keys, attack-round keys)
+  int* ft;           // [2][S] per-entity scratch (closest-player keys; round keys, double-buffered)
   int16_t* clist;    // [S] scratch list (hostile NPCs searching for a target)
   int16_t* ring;     // [S]
   uint32_t* dep;     // [kBitmapWords]
@@ -88,6 +88,8 @@ struct Ctx {
   int nf;            // staged entity fields (LDS rows of T)
   const NmmoConfig* cfg;
   uint32_t sysm;     // enabled systems: a compile-time constant in the specialised kernels
+  int32_t* fault;    // DevState::fault
+  int env;           // this workgroup's env (local index)
 };
 
 // Slim entity table (system sets without Item, Equipment, Profession and Exchange, e.g. BASELINE
@@ -131,6 +133,8 @@ __device__ unsigned long long g_stamps[4096 * 32];
 #endif
 
 __device__ __forceinline__ bool sys(const Ctx& c, uint32_t b) { return (c.sysm & b) != 0; }
+// a bounded loop hit its bound (NMMO_FAULT_*): the first one of a launch is kept (nmmo_get_fault)
+__device__ __forceinline__ void tick_fault(const Ctx& c, int code) { atomicCAS(c.fault, 0, code | c.env << 8); }
 // field of LDS row `row` of T (the inverse of ent_row)
 __device__ __forceinline__ int row_field(bool slim, int row) {
   return slim ? row + (row >= 7) + 2 * (row >= 9) + 10 * (row >= 18) + 2 * (row >= 25) : row;
@@ -167,7 +171,7 @@ __host__ __device__ inline size_t union_lds_bytes(int S, bool grid) {
   auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
   size_t u = (size_t)128 * ((S + 63) / 64) * 8 + (grid ? grid_lds_bytes(S) : 0);
   u = u > 2 * kHash * 4 ? u : 2 * kHash * 4;
-  const size_t atk = al((size_t)S * 4) + al((size_t)S * 2);
+  const size_t atk = al((size_t)S * 8) + al((size_t)S * 2);  // round keys [2][S] | clist
   return u > atk ? u : atk;
 }
 
@@ -253,7 +257,7 @@ __device__ __forceinline__ Ctx make_ctx(unsigned char* smem, const DevState& st,
     c.hkey = reinterpret_cast<int*>(u);
     c.hmin = reinterpret_cast<int*>(u + kHash * 4);
     c.ft = reinterpret_cast<int*>(u);
-    c.clist = reinterpret_cast<int16_t*>(u + al((size_t)S * 4));
+    c.clist = reinterpret_cast<int16_t*>(u + al((size_t)S * 8));
     o += union_lds_bytes(S, uses_grid(sy));
   }
   c.rslot = reinterpret_cast<int16_t*>(smem + o); o += al((size_t)(S + 1) * 2);
@@ -278,6 +282,8 @@ __device__ __forceinline__ Ctx make_ctx(unsigned char* smem, const DevState& st,
   c.P = st.P;
   c.N = st.N;
   c.cfg = &st.cfg;
+  c.fault = st.fault;
+  c.env = e;
   return c;
 }
 
@@ -1147,12 +1153,13 @@ __device__ __forceinline__ int vis_kth(const Ctx& c, int s, int NW, int k) {
 // lowest player slot standing on `tile` (position hash), 0x7FFF if none
 __device__ __forceinline__ int hash_min(const Ctx& c, int tile) {
   int hh = (int)(h32((uint32_t)tile) & (kHash - 1));
-  while (true) {
+  for (int probe = 0; probe < kHash; probe++) {
     const int k = c.hkey[hh];
     if (k == tile) return c.hmin[hh];
     if (k == -1) return 0x7FFF;
     hh = (hh + 1) & (kHash - 1);
   }
+  return 0x7FFF;  // (a full table: the insertion recorded NMMO_FAULT_HASH_PROBE)
 }
 
 // system sets with a specialised tick kernel: BASELINE configs 2 and 3 (config 4 = all)
@@ -1434,7 +1441,11 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
       }
       if ((resource && (nbm >> 8) == M_FOILAGE) || c.prof) {
         int hh = (int)(h32((uint32_t)tile) & (kHash - 1));
-        while (true) {
+        for (int probe = 0;; probe++) {  // kHash >= 2 P: never full
+          if (probe == kHash) {
+            tick_fault(c, NMMO_FAULT_HASH_PROBE);
+            break;
+          }
           const int old = atomicCAS(&c.hkey[hh], -1, tile);
           if (old == -1 || old == tile) break;
           hh = (hh + 1) & (kHash - 1);
@@ -1628,13 +1639,13 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
       int nbuy;
       block_prefix_count(isb, wtot_next(c), &nbuy);
       if (nbuy > 0) {
-        int* mi = c.ft;                                            // attack init zeroes it again
+        int* mi = c.ft;  // [2][S] round keys (see the attack rounds); attack init zeroes them again
         uint32_t* okm = reinterpret_cast<uint32_t*>(c.wtot + 20);  // [4] succeeded, by position
         uint32_t* frm = reinterpret_cast<uint32_t*>(c.wtot + 24);  // [4] freed a row, by position
         int16_t* frow = c.order;                                   // [128] that row, by position
         int* anyf = c.wtot + 16;
         if (isb) c.ikey[s] = draw(seed, (uint32_t)tick, P_BUY_ORDER, (uint32_t)(s + 1), 0).x;
-        if (tid < P) mi[tid] = 0;
+        if (tid < P) mi[tid] = mi[S + tid] = 0;
         if (tid < 8) okm[tid] = 0u;  // okm and frm
         if (tid < 3) anyf[tid] = 0;
         __syncthreads();
@@ -1651,16 +1662,21 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
         uint2 bw = make_uint2(0u, 0u);
         int bprice = 0, bowner = -1;
         for (int round = 1;; round++) {
+          if (round > P + 1) {  // <= nbuy rounds (the earliest pending buy runs in every round)
+            if (tid == 0) tick_fault(c, NMMO_FAULT_BUY_ROUNDS);
+            break;
+          }
           const int key = (round << 16) | (0xFFFF - pos);
+          int* mr = mi + (round & 1) * S;
           if (active) {
-            atomicMax(&mi[s], key);
-            atomicMax(&mi[owner0], key);
+            atomicMax(&mr[s], key);
+            atomicMax(&mr[owner0], key);
             anyf[round % 3] = 1;
           }
           if (tid == 0) anyf[(round + 1) % 3] = 0;
           __syncthreads();
           if (!anyf[round % 3]) break;
-          if (active && mi[s] == key && mi[owner0] == key) {
+          if (active && mr[s] == key && mr[owner0] == key) {
             active = false;
             const int owner = c.rmap[brow] < 0 ? -1 : (c.rmap[brow] & 255);
             uint2* oinv = c.inv + (owner >= 0 ? owner : 0) * kInv;
@@ -1728,9 +1744,9 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
       int ng;
       block_prefix_count(isg, wtot_next(c), &ng);
       if (ng > 0) {
-        int* mi = c.ft;  // attack init zeroes it again
+        int* mi = c.ft;  // [2][S] round keys (see the attack rounds); attack init zeroes them again
         int* anyf = c.wtot + 16;
-        if (tid < P) mi[tid] = 0;
+        if (tid < P) mi[tid] = mi[S + tid] = 0;
         if (tid < 3) anyf[tid] = 0;
         __syncthreads();
         const int tg = isg ? c.a_givet[s] : -1, tg2 = isg ? c.a_ggt[s] : -1;
@@ -1740,17 +1756,22 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
         uint2 gw = make_uint2(0u, 0u);
         int freed = -1;
         for (int round = 1;; round++) {
+          if (round > P + 1) {  // <= ng rounds (the lowest pending give runs in every round)
+            if (tid == 0) tick_fault(c, NMMO_FAULT_GIVE_ROUNDS);
+            break;
+          }
           const int key = (round << 16) | (0xFFFF - s);
+          int* mr = mi + (round & 1) * S;
           if (active) {
-            atomicMax(&mi[s], key);
-            if (r1) atomicMax(&mi[tg], key);
-            if (r2) atomicMax(&mi[tg2], key);
+            atomicMax(&mr[s], key);
+            if (r1) atomicMax(&mr[tg], key);
+            if (r2) atomicMax(&mr[tg2], key);
             anyf[round % 3] = 1;
           }
           if (tid == 0) anyf[(round + 1) % 3] = 0;
           __syncthreads();
           if (!anyf[round % 3]) break;
-          if (active && mi[s] == key && (!r1 || mi[tg] == key) && (!r2 || mi[tg2] == key)) {
+          if (active && mr[s] == key && (!r1 || mr[tg] == key) && (!r2 || mr[tg2] == key)) {
             active = false;
             if (r1 && acts(c, tg) && same_tile(c, tg, s)) {
               uint2* inv = c.inv + s * kInv;
@@ -1812,11 +1833,15 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
   // runs every remaining attack that is the lowest-slot remaining attack on both of its
   // entities (so it follows every earlier attack it conflicts with), all in parallel; round 1
   // is all attacks no earlier attack conflicts with. The per-entity minimum is an atomicMax of
-  // round << 16 | (0xFFFF - slot), so no reset between rounds is needed.
+  // round << 16 | (0xFFFF - slot), so no reset between rounds is needed. The keys alternate
+  // between two arrays by round parity: between barriers r and r + 1 a fast wave already bids
+  // for round r + 1 while a slow one still checks round r, and with one array a check could see
+  // a round-(r + 1) key, miss its turn, and -- repeated every round -- never finish (a launch
+  // that hung on MI355X). A round-(r + 2) bid needs barrier r + 1, after every round-r check.
   int* mi = c.ft;
   int eq_off = 0;
   if (combat || sys(c, NMMO_SYS_NPC)) {
-    for (int k = tid; k < S; k += nt) mi[k] = 0;
+    for (int k = tid; k < 2 * S; k += nt) mi[k] = 0;
     if (tid < 3) c.wtot[16 + tid] = 0;  // attack-round flags
     // equipment bonuses, once (players: equipped items; NPCs: spawn-time equipment): this slot's
     // offense in its attack style (a register) and its defense (c.clist, read by its attackers)
@@ -1836,16 +1861,21 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
     bool active = inslot && t >= 0;
     const int sty = s < S ? c.asty[s] : 0;
     for (int round = 1;; round++) {
+      if (round > S + 1) {  // <= attacks rounds (the lowest pending attack runs in every round)
+        if (tid == 0) tick_fault(c, NMMO_FAULT_ATTACK_ROUNDS);
+        break;
+      }
       const int key = (round << 16) | (0xFFFF - s);
+      int* mr = mi + (round & 1) * S;
       if (active) {
-        atomicMax(&mi[s], key);
-        atomicMax(&mi[t], key);
+        atomicMax(&mr[s], key);
+        atomicMax(&mr[t], key);
         anyf[round % 3] = 1;
       }
       if (tid == 0) anyf[(round + 1) % 3] = 0;
       __syncthreads();
       if (!anyf[round % 3]) break;
-      if (active && mi[s] == key && mi[t] == key) {
+      if (active && mr[s] == key && mr[t] == key) {
         const int dmg = eval_attack(c, s, sty, t, eq_off, sys(c, NMMO_SYS_EQUIPMENT) ? c.clist[t] : 0);
         if (dmg >= 0) apply_attack(c, s, sty, t, dmg, tick);
         active = false;

@@ -210,6 +210,12 @@ class NmmoEngine:
         self._counters = counters
         check(lib().nmmo_set_counters(self.h, ptr), "nmmo_set_counters")
 
+    def get_fault(self) -> int:
+        """The tick fault word (nmmo_get_fault: NMMO_FAULT_* | env << 8, 0 = none), then cleared."""
+        f = ctypes.c_int32()
+        check(lib().nmmo_get_fault(self.h, ctypes.byref(f)), "nmmo_get_fault")
+        return f.value
+
     def read_timing(self):
         """(tick_ms_sum, obs_ms_sum, n_steps, wrapper_ms_sum) from HIP events on the launch stream."""
         ms = (ctypes.c_double * 3)()

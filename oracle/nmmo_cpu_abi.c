@@ -271,6 +271,11 @@ NMMO_API int nmmo_read_timing(NmmoHandle* h, double* ms, int32_t* n) {
   (void)h; (void)ms; (void)n;
   UNSUPPORTED("nmmo_read_timing");
 }
+NMMO_API int nmmo_get_fault(NmmoHandle* h, int32_t* fault) {  /* the serial oracle has no round loops */
+  if (!h || !fault) return fail(NMMO_E_INVALID, "null argument");
+  *fault = 0;
+  return NMMO_OK;
+}
 NMMO_API int nmmo_set_counters(NmmoHandle* h, uint64_t* c) {
   (void)h; (void)c;
   UNSUPPORTED("nmmo_set_counters");

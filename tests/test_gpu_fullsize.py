@@ -144,3 +144,27 @@ def test_run_to_run_determinism():
         digests.append(h.hexdigest())
         eng.close()
     assert digests[0] == digests[1]
+
+
+def test_long_rollout_rounds_finish():
+    """600 ticks of the bench's C4 scenario (1,024 envs, staggered): every round loop of every
+    tick ends by its serial-order bound (fault word 0). With one round-key array a wave still
+    checking round r could see round r + 1's bids and miss its turn; repeated, a launch never
+    finished (hung on MI355X at tick 184 of this scenario before the keys were double-buffered)."""
+    import torch
+
+    from nmmo_amd.engine import NmmoEngine
+
+    cfg = Config.preset("C4", early_stop_agent_num=8, obs_layout=abi.OBS_NONE)
+    eng = NmmoEngine(cfg, 1024, seed=1)
+    eng.reset()
+    assert eng.get_fault() == 0
+    for t in range(600):
+        if t < 64:
+            eng.end_episodes(np.arange(1024) % 64 == t)
+        eng.scripted_actions(1_000_003)
+        eng.step()
+        if t % 50 == 49:
+            torch.cuda.synchronize()
+            assert eng.get_fault() == 0, f"tick {t}: fault word {eng.get_fault():#x}"
+    eng.close()

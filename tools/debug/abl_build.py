@@ -1,0 +1,51 @@
+"""Ablation builds (diagnostic only): copies of the library with one piece of a kernel switched
+off by a source patch, built to nmmo_amd/lib/libnmmo_hip_<variant>.so for same-box timing A/B
+(tools/debug/abl_run.sh). Outputs are wrong by construction; only kernel times are read.
+
+Usage: python tools/debug/abl_build.py <variant> [...]   (variants: see PATCHES)
+"""
+
+import os
+import shutil
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+from nmmo_amd import build as B  # noqa: E402
+
+NEVER = "p.S == 12345"  # a run-time false the compiler cannot fold
+PATCHES = {
+    "nobuy": [("native_obs.hip", "      if (exch) {\n        for (int j0 = 0; j0 < nm; j0 += 64) {",
+               f"      if (exch && {NEVER}) {{\n        for (int j0 = 0; j0 < nm; j0 += 64) {{")],
+    "notile": [("native_obs.hip", "        if (t < 225) {\n          d16[3 * t]", f"        if (t < 225 && {NEVER}) {{\n          d16[3 * t]")],
+    "nozero": [("native_obs.hip", "for (int q = lane; q < body; q += 64) z4[q]", f"for (int q = lane; q < body && {NEVER}; q += 64) z4[q]")],
+    "nomask": [("native_obs.hip", "        if (q < NMMO_NATIVE_MASK_BYTES / 16) {", f"        if (q < NMMO_NATIVE_MASK_BYTES / 16 && {NEVER}) {{")],
+    "noent": [("native_obs.hip", "for (int k0 = 0; k0 < nv4; k0 += 4) {", f"for (int k0 = 0; k0 < nv4 && {NEVER}; k0 += 4) {{")],
+    "noinv": [("native_obs.hip", "    if (ninv == 0) {\n      if (lane < kInv * 8 / 4)", f"    if (ninv == 0 || {NEVER}) {{\n      if (lane < kInv * 8 / 4)")],
+}
+
+
+def build_variant(v: str) -> str:
+    top = os.path.join("/tmp", f"abl_{v}")
+    src = os.path.join(top, "pkg", "csrc")  # csrc includes ../../include/nmmo_hip.h
+    shutil.rmtree(top, ignore_errors=True)
+    shutil.copytree(B.CSRC, src)
+    shutil.copytree(os.path.join(ROOT, "include"), os.path.join(top, "include"))
+    for fname, old, new in PATCHES[v]:
+        p = os.path.join(src, fname)
+        s = open(p).read()
+        assert s.count(old) == 1, (v, fname, old)
+        open(p, "w").write(s.replace(old, new))
+    out = os.path.join(B.LIB_DIR, f"libnmmo_hip_{v}.so")
+    cmd = [B._hipcc(), f"--offload-arch={B.ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-fvisibility=hidden",
+           "-ffp-contract=off", f'-DNMMO_SRC_HASH="abl-{v}"', *[os.path.join(src, f) for f in B.SOURCES], "-o", out]
+    subprocess.check_call(cmd)
+    return out
+
+
+if __name__ == "__main__":
+    with ThreadPoolExecutor(4) as ex:
+        for o in ex.map(build_variant, sys.argv[1:]):
+            print(o)
