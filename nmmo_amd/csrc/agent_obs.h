@@ -141,6 +141,55 @@ __device__ inline void ao_stage(const ObsParams& p, int e, int16_t* T, uint32_t*
   __syncthreads();
 }
 
+// The window rows and item words of a workgroup's kAoAgents agents (g * kAoAgents ..), staged in
+// LDS once per workgroup (every thread; one barrier inside): ws[(la * 15 + row) * 5 + k] = the 5
+// aligned dwords holding window row `row` of agent la (its 15 materials start at byte
+// (col - kVision) & 3 of them: 160 is a multiple of 4), is[la * kInv + k] = its item word k.
+// The agent loops then issue no global load. On gfx9 vmcnt counts stores as well as loads and
+// retires them in issue order, so a load prefetched inside the loop is waited on at the loop's
+// back edge together with the stores issued after it -- as many of them as the compiler cannot
+// prove were issued on every path (the variable zero runs): one agent's row stores drained before
+// the next agent started.
+constexpr int kAoWinRowBytes = 20;
+constexpr int kAoWinAgentBytes = 15 * kAoWinRowBytes;  // 300
+__host__ __device__ inline size_t ao_win_lds() { return (size_t)kAoAgents * kAoWinAgentBytes + (size_t)kAoAgents * kInv * 8; }
+// positions of agents not in the realm are clamped so their (unused) window reads stay in the map
+__device__ __forceinline__ int ao_clamp_pos(int x) { return min(max(x, kVision), kSize - 1 - kVision); }
+__device__ inline void ao_stage_windows(const ObsParams& p, int e, int g, const int16_t* T, int Sp, uint32_t* ws, uint2* is) {
+  const int tid = threadIdx.x, P = p.P;
+  const int la = tid / 15, row = tid - 15 * la, a = g * kAoAgents + la;
+  const bool win = tid < kAoAgents * 15 && a < P;
+  uint32_t d[5] = {0u, 0u, 0u, 0u, 0u};
+  if (win) {
+    const int r = ao_clamp_pos(T[F_ROW * Sp + a]), c = ao_clamp_pos(T[F_COL * Sp + a]);
+    const int base = (r - kVision + row) * kSize + c - kVision;
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(p.mat + (size_t)e * kTiles) + (base >> 2);
+#pragma unroll
+    for (int k = 0; k < 5; k++) d[k] = src[k];
+  }
+  uint2 iw = make_uint2(0u, 0u);
+  const bool itm = tid < kAoAgents * kInv && g * kAoAgents + tid / kInv < P;
+  if (itm) iw = p.items[((size_t)e * P + g * kAoAgents) * kInv + tid];
+  if (win) {
+#pragma unroll
+    for (int k = 0; k < 5; k++) ws[tid * 5 + k] = d[k];  // tid = la * 15 + row
+  }
+  if (tid < kAoAgents * kInv) is[tid] = iw;
+  __syncthreads();
+}
+// Per-lane byte offsets of window tiles t = lane + 64 i (i < 4) in an agent's staged rows
+// (row(t) * 20 + col(t)), two 16-bit values per register
+__device__ __forceinline__ void ao_win_offsets(int (&wo)[2]) {
+  wo[0] = wo[1] = 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const int t = lane_id() + 64 * i;
+    const int o = t < 225 ? (t / 15) * kAoWinRowBytes + t % 15 : 0;
+    wo[i >> 1] |= o << (16 * (i & 1));
+  }
+}
+__device__ __forceinline__ int ao_win_off(const int (&wo)[2], int i) { return (wo[i >> 1] >> (16 * (i & 1))) & 0xFFFF; }
+
 // Entity.Query.window: ascending datastore rows within L-inf <= kVision; the first kNObs packed
 // words go to visw. Returns the in-window count (uncapped).
 __device__ __forceinline__ int ao_compact(const uint32_t (&pr)[kAoRows], int S, int r, int c, uint32_t* visw) {
@@ -160,7 +209,9 @@ __device__ __forceinline__ int ao_compact(const uint32_t (&pr)[kAoRows], int S, 
 }
 
 // Map offsets of the window tiles t = lane + 64 i (i < 4) from the agent's tile, two int16 per
-// register (per-wave constants: an agent's 225 material loads are then one add each)
+// register (per-wave constants: an agent's 225 material loads are then one add each; the wire
+// kernel's in-loop prefetch -- its few stores per record make the back-edge wait cheap, and the
+// staging's LDS cost it a workgroup per CU: 0.089 -> 0.091 ms per 512 envs)
 __device__ __forceinline__ void ao_window_offsets(int (&mo)[2]) {
   mo[0] = mo[1] = 0;
 #pragma unroll

@@ -8,16 +8,17 @@
 // entries per lane from the env's listings staged as price | owner << 8), expanded 16 bits ->
 // 16 bytes per lane (two multiply-masks per dword) into 100 16-B stores; the int16 part goes out
 // as dword stores (Entity row pairs are 31 dwords; Inventory 96 dwords; Tile + task index + pad
-// 341 dwords) and one 16-B zero run for the unseen Entity rows. Nothing of an agent passes
-// through LDS but its visible rows' packed words and its window materials.
+// 341 dwords) and one 16-B zero run for the unseen Entity rows. The workgroup's window rows and
+// item words are staged in LDS up front (agent_obs.h ao_stage_windows), so the agent loop issues
+// stores only and never waits on them.
 #include "agent_obs.h"
 
 namespace nmmo {
 
 // LDS: agent_obs.h's entity staging | listings (price | owner << 8, u16) | per-wave visible rows
-// | per-wave window materials. 31.8 KB at S = 384: 5 workgroups per CU.
+// | the workgroup's staged window rows and item words. 35.8 KB at S = 384: 4 workgroups per CU.
 __host__ __device__ inline size_t no_lds_bytes(int S) {
-  return ao_entity_lds(S) + (size_t)NMMO_MARKET_ROWS * 2 + (size_t)kAoWaves * (128 * 4 + 256);
+  return ao_entity_lds(S) + (size_t)NMMO_MARKET_ROWS * 2 + (size_t)kAoWaves * 128 * 4 + ao_win_lds();
 }
 constexpr int kNoEntity = 2, kNoInv = kNoEntity + kNObs * NMMO_N_ENTITY_COLS, kNoTile = kNoInv + kInv * 16,
               kNoTask = kNoTile + 225 * 3;  // int16 offsets in the int16 part (SPEC §8b)
@@ -36,7 +37,8 @@ __global__ void __launch_bounds__(256) native_obs_kernel(ObsParams p) {
   uint32_t* pk = reinterpret_cast<uint32_t*>(smem + ao_entity_lds(S) - (size_t)(kMaxSlots + 64) * 4);
   uint16_t* mpo = reinterpret_cast<uint16_t*>(pk + kMaxSlots + 64);           // [1024] price | owner << 8
   uint32_t* visw_all = reinterpret_cast<uint32_t*>(mpo + NMMO_MARKET_ROWS);   // [4][128]
-  uint8_t* wmat_all = reinterpret_cast<uint8_t*>(visw_all + kAoWaves * 128);  // [4][256]
+  uint32_t* wst = visw_all + kAoWaves * 128;                                  // [16][15][5] window rows
+  uint2* ist = reinterpret_cast<uint2*>(wst + kAoAgents * kAoWinAgentBytes / 4);  // [16][12] item words
   const int e = blockIdx.x, g = blockIdx.y, tid = threadIdx.x, lane = lane_id();
   const int w = __builtin_amdgcn_readfirstlane(wave_id());
   const int nm = min(max(p.mcount[e], 0), NMMO_MARKET_ROWS);
@@ -47,6 +49,7 @@ __global__ void __launch_bounds__(256) native_obs_kernel(ObsParams p) {
     mpo[j] = (uint16_t)(it_price(p.items[((size_t)e * P + own) * kInv + slot]) | own << 8);
   }
   ao_stage(p, e, T, pk);  // (publishes mpo too)
+  ao_stage_windows(p, e, g, T, Sp, wst, ist);
 
   uint8_t* nenv = p.nat + (size_t)e * ((size_t)P * NMMO_NATIVE_ROW_BYTES + NMMO_NATIVE_MARKET_BYTES);
   if (g == 0) {  // the env's Market (1,024 rows of 16 int16), once per env
@@ -70,8 +73,7 @@ __global__ void __launch_bounds__(256) native_obs_kernel(ObsParams p) {
 #pragma unroll
   for (int i = 0; i < kAoRows; i++) pr[i] = pk[lane + 64 * i];
   uint32_t* visw = visw_all + w * 128;
-  uint8_t* wmat = wmat_all + w * 256;
-  const uint8_t* mat = p.mat + (size_t)e * kTiles;
+  const uint8_t* wsb = reinterpret_cast<const uint8_t*>(wst);
   const int16_t* E = p.ent + (size_t)e * NMMO_NF * S;
   const int tick = p.env[(size_t)e * NMMO_NE + E_TICK];
   const bool exch = (p.systems & NMMO_SYS_ITEM) && (p.systems & NMMO_SYS_EXCHANGE);
@@ -87,16 +89,8 @@ __global__ void __launch_bounds__(256) native_obs_kernel(ObsParams p) {
     if constexpr (kWrap)
       if (p.ws) my_prev = p.ws[ai].prev_price;
   }
-  uint2 iv = make_uint2(0u, 0u);
-  uint32_t wm[4] = {0u, 0u, 0u, 0u};
-  int mo[2];
-  ao_window_offsets(mo);
-  auto prefetch = [&](int a) {
-    const int at = T[F_ROW * Sp + a] * kSize + T[F_COL * Sp + a];
-    iv = lane < kInv ? p.items[((size_t)e * P + a) * kInv + lane] : make_uint2(0u, 0u);
-#pragma unroll
-    for (int i = 0; i < 4; i++) wm[i] = lane + 64 * i < 225 ? mat[at + ao_window_off(mo, i)] : 0u;
-  };
+  int wo[2];
+  ao_win_offsets(wo);
   auto alive = [&](int j) { return j < per_wave && __builtin_amdgcn_readlane(my_alive, j) != 0; };
   int toff[4];  // window tile lane + 64 i: (row offset) & 255 | (col offset) << 8
 #pragma unroll
@@ -104,14 +98,12 @@ __global__ void __launch_bounds__(256) native_obs_kernel(ObsParams p) {
     const int t = lane + 64 * i;
     toff[i] = ((t / 15 - kVision) & 255) | (t % 15 - kVision) * 256;
   }
-  if (alive(0)) prefetch(abase);
 
   for (int j = 0; j < per_wave; j++) {
     const int a = abase + kAoWaves * j;
     if (a >= P) break;
     uint8_t* nrow = nenv + (size_t)a * NMMO_NATIVE_ROW_BYTES;
     if (!alive(j)) {  // not in the realm: a zero row
-      if (alive(j + 1)) prefetch(a + kAoWaves);
       if (p.wcount && lane == 0) p.wcount[(size_t)e * P + a] = 0;
       uint4* z = reinterpret_cast<uint4*>(nrow);
       for (int i = lane; i < NMMO_NATIVE_ROW_BYTES / 16; i += 64) z[i] = make_uint4(0u, 0u, 0u, 0u);
@@ -121,13 +113,14 @@ __global__ void __launch_bounds__(256) native_obs_kernel(ObsParams p) {
     const int c = __builtin_amdgcn_readfirstlane(T[F_COL * Sp + a]);
     const int gold = __builtin_amdgcn_readfirstlane(T[F_GOLD * Sp + a]);
     const int aid = __builtin_amdgcn_readfirstlane(T[F_ID * Sp + a]);
+    // window tile t = lane + 64 i and item word lane, from the workgroup's staging
+    const uint8_t* wa = wsb + (a - g * kAoAgents) * kAoWinAgentBytes + ((c - kVision) & 3);
+    uint32_t wm[4];
 #pragma unroll
-    for (int i = 0; i < 4; i++)
-      if (lane + 64 * i < 225) wmat[lane + 64 * i] = (uint8_t)wm[i];
-    const uint2 it = iv;  // this agent's item word (lanes 0..11)
+    for (int i = 0; i < 4; i++) wm[i] = lane + 64 * i < 225 ? wa[ao_win_off(wo, i)] : 0u;
+    const uint2 it = lane < kInv ? ist[(a - g * kAoAgents) * kInv + lane] : make_uint2(0u, 0u);
     const uint32_t mv = ao_move_bits(wm[1]);
     const int ninv = __builtin_ctzll(~__ballot(lane < kInv && it_type(it) != 0));  // occupied prefix
-    if (alive(j + 1)) prefetch(a + kAoWaves);  // the next agent's loads, ahead of the stores
 
     const int nv = min(ao_compact(pr, S, r, c, visw), kNObs);
     if (p.wcount && lane == 0) p.wcount[(size_t)e * P + a] = (uint16_t)wire_count_word(nv, ninv);
@@ -246,13 +239,13 @@ __global__ void __launch_bounds__(256) native_obs_kernel(ObsParams p) {
         if (t < 225) {
           d16[3 * t] = (int16_t)(r + ((toff[i] << 24) >> 24));
           d16[3 * t + 1] = (int16_t)(c + (toff[i] >> 8));
-          d16[3 * t + 2] = (int16_t)wmat[t];
+          d16[3 * t + 2] = (int16_t)wm[i];
         }
       }
       if (lane < NMMO_NATIVE_I16 - kNoTask)
         d16[225 * 3 + lane] = lane == 0 ? (int16_t)__builtin_amdgcn_readlane(my_task, j) : (int16_t)0;
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the next agent reuses visw / wmat
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the next agent reuses visw
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
