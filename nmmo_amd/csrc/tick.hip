@@ -84,6 +84,7 @@ struct Ctx {
   int S, P, N, IC;
   bool items, exch, prof, equip;
   bool foreign;      // !prof and DevState::foreign is set: respawn reads the map bank
+  bool foreign_any;  // DevState::foreign is set: a respawn may change a tile's passability
   bool slim;         // no Item/Equipment/Profession/Exchange: the fields only they change stay in HBM
   int nf;            // staged entity fields (LDS rows of T)
   const NmmoConfig* cfg;
@@ -201,7 +202,8 @@ __device__ __forceinline__ Ctx make_ctx(unsigned char* smem, const DevState& st,
   c.exch = c.items && (sy & NMMO_SYS_EXCHANGE) != 0;
   c.prof = c.items && (sy & NMMO_SYS_PROFESSION) != 0;
   c.equip = c.items && (sy & NMMO_SYS_EQUIPMENT) != 0;
-  c.foreign = !c.prof && *st.foreign != 0;  // uniform, read before any store (a scalar load)
+  c.foreign_any = *st.foreign != 0;  // uniform, read before any store (a scalar load)
+  c.foreign = !c.prof && c.foreign_any;
   c.IC = kInv * st.P;
   if (c.items) {  // 16-B aligned block first (inventories are copied with 16-B accesses)
     c.inv = reinterpret_cast<uint2*>(smem + o); o += (size_t)st.P * kInv * 8;
@@ -643,7 +645,8 @@ __device__ __forceinline__ void ring_ev_append(Ctx& c, int row, int& evn, int ne
 
 // ---------------------------------------------------------------- NPC spawn (SPEC §5.7)
 // 25 attempts evaluated by lanes 0..24 of wave 0; accepted in attempt order up to capacity.
-__device__ __forceinline__ void npc_spawn(Ctx& c, uint32_t tick) {
+// cand_mat: lane a's candidate tile material, loaded at tick start (npc_spawn_material).
+__device__ __forceinline__ void npc_spawn(Ctx& c, uint32_t tick, uint32_t cand_mat) {
   if (wave_id() == 0) {
     const int a = lane_id();
     const uint64_t seed = env_seed(c);
@@ -654,7 +657,7 @@ __device__ __forceinline__ void npc_spawn(Ctx& c, uint32_t tick) {
       const U4 u = draw(seed, tick, P_NPC_SPAWN, (uint32_t)a, 0);
       r = kLo + (int)uniform_n(u.x, kCenter);
       col = kLo + (int)uniform_n(u.y, kCenter);
-      valid = !impassable(c.mat[r * kSize + col]);
+      valid = !impassable(c.foreign_any ? (int)c.mat[r * kSize + col] : (int)cand_mat);
       int dist = r - kLo;
       dist = min(dist, kHi - r);
       dist = min(dist, col - kLo);
@@ -706,6 +709,19 @@ __device__ __forceinline__ void npc_spawn(Ctx& c, uint32_t tick) {
     }
   }
   __syncthreads();
+}
+
+// Thread a < 25 (wave 0): the material of NPC spawn attempt a's tile at tick + 1, loaded at tick
+// start: the spawn only tests passability, which no phase of the tick changes -- unless a
+// set_state / set_map_bank installed depleted tiles whose bank material is impassable
+// (DevState::foreign: the respawn before the spawn may restore it; npc_spawn reads the map then) --
+// and a load issued at the spawn waits for every tile and event store of the tick (vmcnt counts
+// stores).
+__device__ __forceinline__ uint32_t npc_spawn_material(const Ctx& c, uint32_t tick1, const uint8_t* map) {
+  if (threadIdx.x >= 25) return 0u;
+  const U4 u = draw(env_seed(c), tick1, P_NPC_SPAWN, threadIdx.x, 0);
+  const int r = kLo + (int)uniform_n(u.x, kCenter), col = kLo + (int)uniform_n(u.y, kCenter);
+  return map[r * kSize + col];
 }
 
 // ---------------------------------------------------------------- reset (SPEC §4)
@@ -773,7 +789,8 @@ __device__ __forceinline__ void reset_env(Ctx& c, uint64_t seed, int episode, in
     }
   }
   __syncthreads();
-  if (sys(c, NMMO_SYS_NPC)) npc_spawn(c, 0);
+  // (the map is the bank's copy just written: the bank holds the same material)
+  if (sys(c, NMMO_SYS_NPC)) npc_spawn(c, 0, npc_spawn_material(c, 0, c.bank + (size_t)c.E[E_MAP_ID] * kTiles));
 }
 
 // ---------------------------------------------------------------- NPC AI (SPEC §6)
@@ -1181,7 +1198,11 @@ __device__ __forceinline__ void launder(NmmoTaskState& t) {
   asm volatile("" : "+v"(t.acc[0]), "+v"(t.acc[1]), "+v"(t.acc[2]), "+v"(t.acc[3]));
 }
 
-__device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act, int3 a_pre, float* rew, uint8_t* term,
+// a player's 12 action heads (kHeads), loaded at kernel start
+struct Heads {
+  int v[kHeads];
+};
+__device__ __forceinline__ void tick_env(Ctx& c, Heads hd, float* rew, uint8_t* term,
                          uint8_t* trunc, uint8_t* mask) {
   const int tid = threadIdx.x, nt = blockDim.x, S = c.S, P = c.P;
   const int s = tid;
@@ -1281,7 +1302,11 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
   }
   if (uses_grid(c.sysm)) __syncthreads();  // (without the grid the prep's barrier ordered all)
   NMMO_STAMP(13);
-  // bits 0-3: neighbour d passable; 4-7: neighbour d is Water; 8-15: own tile material
+  // bits 0-3: neighbour d passable; 4-7: neighbour d is Water; 8-15: own tile material; 16-19:
+  // neighbour (row - 1, row + 1, col - 1, col + 1) is Fish (the professions' order). Fish and
+  // the own tile's material are read here, at tick start, by the harvest too: no harvest earlier
+  // in the tick turns a tile into or out of Fish or a profession resource, and a load after the
+  // tick's first tile store would wait for it (vmcnt counts stores).
   asm volatile("" : "+v"(mw0), "+v"(mw1), "+v"(mup), "+v"(mdn));
   const uint64_t mrow8 = (uint64_t)mw0 | ((uint64_t)mw1 << 32);
   const int msh = 8 * ((qc - 1) & 3), mcol = 8 * (qc & 3);
@@ -1293,7 +1318,9 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
   const uint32_t nbm = (impassable(m_n0) ? 0u : 1u) | (impassable(m_n1) ? 0u : 2u) |
                        (impassable(m_n2) ? 0u : 4u) | (impassable(m_n3) ? 0u : 8u) |
                        (m_n0 == M_WATER ? 16u : 0u) | (m_n1 == M_WATER ? 32u : 0u) |
-                       (m_n2 == M_WATER ? 64u : 0u) | (m_n3 == M_WATER ? 128u : 0u) | (m_own << 8);
+                       (m_n2 == M_WATER ? 64u : 0u) | (m_n3 == M_WATER ? 128u : 0u) | (m_own << 8) |
+                       (m_n0 == M_FISH ? 1u << 16 : 0u) | (m_n1 == M_FISH ? 1u << 17 : 0u) |
+                       (m_n3 == M_FISH ? 1u << 18 : 0u) | (m_n2 == M_FISH ? 1u << 19 : 0u);
   int my_move = -1, my_tgt = -1, my_sty = 0;
   int use_row = -1, destroy_row = -1, sell_row = -1, sell_price = 0;
   if (s < P) {
@@ -1307,9 +1334,10 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
     c.ev_lvl[s] = 0;
   }
   if (s < P && c.pres[s]) {
-    const int32_t* a = act + (size_t)s * kHeads;
-    asm volatile("" : "+v"(a_pre.x), "+v"(a_pre.y), "+v"(a_pre.z));  // loaded before the state
-    const int dmove = a_pre.x, dsty = a_pre.y, dk = a_pre.z;
+#pragma unroll
+    for (int k = 0; k < kHeads; k++) asm volatile("" : "+v"(hd.v[k]));  // loaded before the state
+    const int* a = hd.v;
+    const int dmove = a[8], dsty = a[0], dk = a[1];
     if (dmove >= 0 && dmove < 5) my_move = dmove;
     if (combat && dsty >= 0 && dsty < 3 && dk >= 0 && dk < kNObs) {
       my_tgt = vis_kth(c, s, NW, dk);
@@ -1363,6 +1391,10 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
     closest = best == 0x7FFFFFFF ? -1 : (best & 255);
   }
   if (npc_on && s >= P && inslot) npc_decide(c, s, closest, nbm, my_move, my_tgt, my_sty);
+  // wave 0 (players) has no NPC to decide: it draws the spawn attempts' tiles meanwhile (before
+  // the tick's first global store)
+  uint32_t spawn_mat = npc_on ? npc_spawn_material(c, (uint32_t)(tick + 1), c.mat) : 0u;
+  asm volatile("" : "+v"(spawn_mat));  // opaque: waited on at the spawn, not here
   if (npc_on) {  // hunt pathing for the NPCs that asked (block-uniform)
     __syncthreads();
     npc_bfs_phase(c);
@@ -1439,7 +1471,7 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
         TF(F_WATER, s) = (int16_t)(drink ? 100 : max(0, water - 5));
         e_drink = drink;
       }
-      if ((resource && (nbm >> 8) == M_FOILAGE) || c.prof) {
+      if ((resource && ((nbm >> 8) & 255u) == M_FOILAGE) || c.prof) {
         int hh = (int)(h32((uint32_t)tile) & (kHash - 1));
         for (int probe = 0;; probe++) {  // kHash >= 2 P: never full
           if (probe == kHash) {
@@ -1458,7 +1490,7 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
   __syncthreads();
   NMMO_STAMP(3);
   const bool first_on_tile = hslot >= 0 && c.hmin[hslot] == s;
-  if (resource && first_on_tile && (nbm >> 8) == M_FOILAGE) {
+  if (resource && first_on_tile && ((nbm >> 8) & 255u) == M_FOILAGE) {
     e_eat = true;
     TF(F_FOOD, s) = 100;
     c.mat[tile] = M_SCRUB;
@@ -1473,15 +1505,15 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
       const int nb[4] = {tile - kSize, tile + kSize, tile - 1, tile + 1};
 #pragma unroll
       for (int q = 0; q < 4; q++) {
-        if (c.mat[nb[q]] != M_FISH) continue;
+        if (!((nbm >> (16 + q)) & 1u)) continue;
         fishm |= 1 << q;
         const int f = nb[q];
         const int w = min(min(hash_min(c, f - kSize), hash_min(c, f + kSize)),
                           min(hash_min(c, f - 1), hash_min(c, f + 1)));
         got = got || w == s;
       }
-      if (first_on_tile) {
-        const int m = c.mat[tile];
+      if (first_on_tile) {  // (a tile eaten this tick was Foilage: no profession resource either way)
+        const int m = (int)((nbm >> 8) & 255u);
         q_on = m == M_HERB ? 0 : m == M_ORE ? 1 : m == M_TREE ? 2 : m == M_CRYSTAL ? 3 : -1;
       }
     }
@@ -2154,7 +2186,7 @@ __device__ __forceinline__ void tick_env(Ctx& c, const int32_t* __restrict__ act
   if (tid == 0) c.E[E_TICK] = tick + 1;  // read only at the tick's start (and by store_env)
   NMMO_STAMP(8);
   // 7. NPC refill
-  if (sys(c, NMMO_SYS_NPC)) npc_spawn(c, (uint32_t)(tick + 1));
+  if (sys(c, NMMO_SYS_NPC)) npc_spawn(c, (uint32_t)(tick + 1), spawn_mat);
   NMMO_STAMP(9);
 
   // 8. rewards / dones (every thread evaluates `done`: E_PLAYERS_ALIVE was last written before
@@ -2233,12 +2265,15 @@ __device__ __forceinline__ void tick_body(const DevState& st, const int32_t* __r
   NMMO_STAMP_CLEAR();
   NMMO_STAMP(0);
   Ctx c = make_ctx(smem, st, e, kSys ? kSys : st.cfg.systems);
-  // a step's Move / AttackStyle / AttackTarget heads of this thread's player (a valid row for
-  // every thread), loaded ahead of the state so their latency hides under its load
-  int3 a_pre = make_int3(0, 0, 0);
+  // a step's action heads of this thread's player (a valid row for every thread; Move /
+  // AttackStyle / AttackTarget, and the item heads with the Item system), loaded ahead of the
+  // state so their latency hides under its load
+  Heads hd = {};
   if (mode == 0) {
     const int32_t* a = actions + ((size_t)e * st.P + min((int)threadIdx.x, st.P - 1)) * kHeads;
-    a_pre = make_int3(a[8], a[0], a[1]);
+#pragma unroll
+    for (int k = 0; k < kHeads; k++)
+      if (k == 0 || k == 1 || k == 8 || c.items) hd.v[k] = a[k];
   }
   load_env(c, st, e);
   __syncthreads();
@@ -2277,7 +2312,7 @@ __device__ __forceinline__ void tick_body(const DevState& st, const int32_t* __r
       if (mask) mask[o + p] = 1;
     }
   } else {
-    tick_env(c, actions + o * kHeads, a_pre, rew + o, term + o, trunc + o, mask + o);
+    tick_env(c, hd, rew + o, term + o, trunc + o, mask + o);
   }
   __syncthreads();
   if (st.counters && threadIdx.x == 0) {  // sum(mask) of this launch + done envs + event rows, one
