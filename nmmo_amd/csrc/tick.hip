@@ -644,9 +644,16 @@ __device__ __forceinline__ void ring_ev_append(Ctx& c, int row, int& evn, int ne
 }
 
 // ---------------------------------------------------------------- NPC spawn (SPEC §5.7)
+// Spawn attempt a (thread a < 25 of wave 0): its draw and its tile's material, taken early in the
+// tick (npc_spawn_pre) so the spawn neither waits on HBM nor recomputes Philox on its critical path
+struct SpawnPre {
+  U4 u;          // draw(seed, tick + 1, P_NPC_SPAWN, a) (valid when `drawn`)
+  uint32_t mat;  // the tile's material
+};
 // 25 attempts evaluated by lanes 0..24 of wave 0; accepted in attempt order up to capacity.
-// cand_mat: lane a's candidate tile material, loaded at tick start (npc_spawn_material).
-__device__ __forceinline__ void npc_spawn(Ctx& c, uint32_t tick, uint32_t cand_mat) {
+// pre: lane a's early draw and tile material (npc_spawn_pre); drawn = pre.u is set (the C3
+// variant at <= 64 VGPRs does not keep it through the tick and draws again).
+__device__ __forceinline__ void npc_spawn(Ctx& c, uint32_t tick, const SpawnPre& pre, bool drawn) {
   if (wave_id() == 0) {
     const int a = lane_id();
     const uint64_t seed = env_seed(c);
@@ -654,10 +661,10 @@ __device__ __forceinline__ void npc_spawn(Ctx& c, uint32_t tick, uint32_t cand_m
     int r = 0, col = 0, type = 0, style = 0, level = 0;
     uint32_t u3 = 0;
     if (a < 25) {
-      const U4 u = draw(seed, tick, P_NPC_SPAWN, (uint32_t)a, 0);
+      const U4 u = drawn ? pre.u : draw(seed, tick, P_NPC_SPAWN, (uint32_t)a, 0);
       r = kLo + (int)uniform_n(u.x, kCenter);
       col = kLo + (int)uniform_n(u.y, kCenter);
-      valid = !impassable(c.foreign_any ? (int)c.mat[r * kSize + col] : (int)cand_mat);
+      valid = !impassable(c.foreign_any ? (int)c.mat[r * kSize + col] : (int)pre.mat);
       int dist = r - kLo;
       dist = min(dist, kHi - r);
       dist = min(dist, col - kLo);
@@ -717,11 +724,13 @@ __device__ __forceinline__ void npc_spawn(Ctx& c, uint32_t tick, uint32_t cand_m
 // (DevState::foreign: the respawn before the spawn may restore it; npc_spawn reads the map then) --
 // and a load issued at the spawn waits for every tile and event store of the tick (vmcnt counts
 // stores).
-__device__ __forceinline__ uint32_t npc_spawn_material(const Ctx& c, uint32_t tick1, const uint8_t* map) {
-  if (threadIdx.x >= 25) return 0u;
-  const U4 u = draw(env_seed(c), tick1, P_NPC_SPAWN, threadIdx.x, 0);
-  const int r = kLo + (int)uniform_n(u.x, kCenter), col = kLo + (int)uniform_n(u.y, kCenter);
-  return map[r * kSize + col];
+__device__ __forceinline__ SpawnPre npc_spawn_pre(const Ctx& c, uint32_t tick1, const uint8_t* map) {
+  SpawnPre x = {{0u, 0u, 0u, 0u}, 0u};
+  if (threadIdx.x >= 25) return x;
+  x.u = draw(env_seed(c), tick1, P_NPC_SPAWN, threadIdx.x, 0);
+  const int r = kLo + (int)uniform_n(x.u.x, kCenter), col = kLo + (int)uniform_n(x.u.y, kCenter);
+  x.mat = map[r * kSize + col];
+  return x;
 }
 
 // ---------------------------------------------------------------- reset (SPEC §4)
@@ -790,7 +799,7 @@ __device__ __forceinline__ void reset_env(Ctx& c, uint64_t seed, int episode, in
   }
   __syncthreads();
   // (the map is the bank's copy just written: the bank holds the same material)
-  if (sys(c, NMMO_SYS_NPC)) npc_spawn(c, 0, npc_spawn_material(c, 0, c.bank + (size_t)c.E[E_MAP_ID] * kTiles));
+  if (sys(c, NMMO_SYS_NPC)) npc_spawn(c, 0, npc_spawn_pre(c, 0, c.bank + (size_t)c.E[E_MAP_ID] * kTiles), true);
 }
 
 // ---------------------------------------------------------------- NPC AI (SPEC §6)
@@ -1393,8 +1402,10 @@ __device__ __forceinline__ void tick_env(Ctx& c, Heads hd, float* rew, uint8_t* 
   if (npc_on && s >= P && inslot) npc_decide(c, s, closest, nbm, my_move, my_tgt, my_sty);
   // wave 0 (players) has no NPC to decide: it draws the spawn attempts' tiles meanwhile (before
   // the tick's first global store)
-  uint32_t spawn_mat = npc_on ? npc_spawn_material(c, (uint32_t)(tick + 1), c.mat) : 0u;
-  asm volatile("" : "+v"(spawn_mat));  // opaque: waited on at the spawn, not here
+  SpawnPre spawn = {{0u, 0u, 0u, 0u}, 0u};
+  const bool spawn_drawn = c.sysm != kSysC3;
+  if (npc_on) spawn = npc_spawn_pre(c, (uint32_t)(tick + 1), c.mat);
+  asm volatile("" : "+v"(spawn.mat));  // opaque: waited on at the spawn, not here
   if (npc_on) {  // hunt pathing for the NPCs that asked (block-uniform)
     __syncthreads();
     npc_bfs_phase(c);
@@ -2186,7 +2197,7 @@ __device__ __forceinline__ void tick_env(Ctx& c, Heads hd, float* rew, uint8_t* 
   if (tid == 0) c.E[E_TICK] = tick + 1;  // read only at the tick's start (and by store_env)
   NMMO_STAMP(8);
   // 7. NPC refill
-  if (sys(c, NMMO_SYS_NPC)) npc_spawn(c, (uint32_t)(tick + 1), spawn_mat);
+  if (sys(c, NMMO_SYS_NPC)) npc_spawn(c, (uint32_t)(tick + 1), spawn, spawn_drawn);
   NMMO_STAMP(9);
 
   // 8. rewards / dones (every thread evaluates `done`: E_PLAYERS_ALIVE was last written before
