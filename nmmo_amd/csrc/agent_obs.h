@@ -26,7 +26,7 @@ constexpr int kAoWaves = 4;
 constexpr int kAoAgents = 16;             // agents per workgroup
 constexpr int kAoRows = kMaxSlots / 64;   // packed datastore-row words per lane
 constexpr uint32_t kAoEmpty = 0xFFFFFFFFu;
-static_assert(kSize <= 256 && kMaxSlots <= 2 * 256 && kMaxSlots % 64 == 0, "packed entity word; two slots per thread");
+static_assert(kSize <= 256 && kMaxSlots <= 2 * 256 && kMaxSlots % 64 == 0, "packed entity word; two slots per thread (>= 256 threads)");
 __host__ __device__ inline int ao_stride(int S) { return ((S + 1) >> 1 | 1) << 1; }  // int16, odd dword count
 __host__ __device__ inline size_t ao_entity_lds(int S) {  // T | pk
   return (((size_t)NMMO_N_ENTITY_COLS * ao_stride(S) * 2 + 15) & ~(size_t)15) + (size_t)(kMaxSlots + 64) * 4;
@@ -120,17 +120,17 @@ __device__ inline void ao_stage(const ObsParams& p, int e, int16_t* T, uint32_t*
     d[3] = x.w;
   }
   for (int k = tid; k < kMaxSlots + 64; k += blockDim.x) pk[k] = kAoEmpty;
-  int al[2], ds[2];  // alive / datastore row of slots tid and tid + 256, loaded ahead of the barrier
+  int al[2], ds[2];  // alive / datastore row of slots tid and tid + blockDim, loaded ahead of the barrier
 #pragma unroll
   for (int u = 0; u < 2; u++) {
-    const int s = tid + 256 * u;
+    const int s = tid + (int)blockDim.x * u;
     al[u] = s < S ? E[F_ALIVE * S + s] : 0;
     ds[u] = s < S ? E[F_DS_ROW * S + s] : 0;
   }
   __syncthreads();
 #pragma unroll
   for (int u = 0; u < 2; u++) {
-    const int s = tid + 256 * u;
+    const int s = tid + (int)blockDim.x * u;
     if (al[u] && (unsigned)(ds[u] - 1) < (unsigned)S) {
       const bool player = s < P;
       const bool immune = player && T[F_TIME_ALIVE * Sp + s] < p.spawn_immunity;

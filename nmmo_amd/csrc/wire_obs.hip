@@ -16,21 +16,26 @@
 
 namespace nmmo {
 
+// 32 agents per workgroup, 8 waves (the native kernel's 16 / 4): the per-workgroup prologue
+// (entity staging, record offsets, table indices) is long next to ~0.3 KB records, so twice the
+// agents per prologue: same box, 0.089 -> 0.083 ms per 512 envs, C5 at N = 1 368 -> 375 M.
+constexpr int kWoWaves = 8, kWoAgents = 32;
+
 // LDS: agent_obs.h's entity staging | per-wave visible rows | per-wave window materials | the
-// env's record offsets | the slots' entity-table indices. 30 KB at S = 384: 5 workgroups per CU.
+// env's record offsets | the slots' entity-table indices. 34 KB at S = 384.
 __host__ __device__ inline size_t wo_lds_bytes(int S) {
-  return ao_entity_lds(S) + (size_t)kAoWaves * (128 * 4 + 256) + (size_t)(128 + 4) * 4 + (size_t)kMaxSlots * 2;
+  return ao_entity_lds(S) + (size_t)kWoWaves * (128 * 4 + 256) + (size_t)(128 + 4) * 4 + (size_t)kMaxSlots * 2;
 }
 
 template <bool kWrap>
-__global__ void __launch_bounds__(256) wire_obs_kernel(ObsParams p) {
+__global__ void __launch_bounds__(64 * kWoWaves) wire_obs_kernel(ObsParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int S = p.S, P = p.P, Sp = ao_stride(S);
   int16_t* T = reinterpret_cast<int16_t*>(smem);  // [31][Sp]
   uint32_t* pk = reinterpret_cast<uint32_t*>(smem + ao_entity_lds(S) - (size_t)(kMaxSlots + 64) * 4);
-  uint32_t* visw_all = pk + kMaxSlots + 64;               // [4][128] packed words of the visible rows
-  uint8_t* wmat_all = reinterpret_cast<uint8_t*>(visw_all + kAoWaves * 128);  // [4][256] window materials
-  int* woff = reinterpret_cast<int*>(wmat_all + kAoWaves * 256);            // [P + 1] record offsets
+  uint32_t* visw_all = pk + kMaxSlots + 64;               // [kWoWaves][128] packed words of the visible rows
+  uint8_t* wmat_all = reinterpret_cast<uint8_t*>(visw_all + kWoWaves * 128);  // [kWoWaves][256] window materials
+  int* woff = reinterpret_cast<int*>(wmat_all + kWoWaves * 256);            // [P + 1] record offsets
   uint16_t* rk = reinterpret_cast<uint16_t*>(woff + 128 + 4);                // [kMaxSlots] table index
   const int e = blockIdx.x, g = blockIdx.y, tid = threadIdx.x, lane = lane_id();
   const int w = __builtin_amdgcn_readfirstlane(wave_id());  // wave-uniform values in SGPRs
@@ -79,11 +84,11 @@ __global__ void __launch_bounds__(256) wire_obs_kernel(ObsParams p) {
   const bool item = (p.systems & NMMO_SYS_ITEM) != 0;
   const bool exch = item && (p.systems & NMMO_SYS_EXCHANGE) != 0;
 
-  const int per_wave = (kAoAgents + kAoWaves - 1) / kAoWaves;
-  const int abase = g * kAoAgents + w;
+  const int per_wave = (kWoAgents + kWoWaves - 1) / kWoWaves;
+  const int abase = g * kWoAgents + w;
   int my_task = 0, my_prev = -1;  // lane j: agent abase + 4 j
-  if (lane < per_wave && abase + kAoWaves * lane < P) {
-    const size_t ai = (size_t)e * P + abase + kAoWaves * lane;
+  if (lane < per_wave && abase + kWoWaves * lane < P) {
+    const size_t ai = (size_t)e * P + abase + kWoWaves * lane;
     my_task = p.assign[ai];
     if constexpr (kWrap)
       if (p.ws) my_prev = p.ws[ai].prev_price;
@@ -99,17 +104,17 @@ __global__ void __launch_bounds__(256) wire_obs_kernel(ObsParams p) {
     for (int i = 0; i < 4; i++) wm[i] = lane + 64 * i < 225 ? mat[at + ao_window_off(mo, i)] : 0u;
   };
   auto in_realm = [&](int j) {
-    const int a = abase + kAoWaves * j;
+    const int a = abase + kWoWaves * j;
     return j < per_wave && a < P && (cnt[a] & 0x8000u);
   };
   if (in_realm(0)) prefetch(abase);
 
   for (int j = 0; j < per_wave; j++) {
-    const int a = abase + kAoWaves * j;
+    const int a = abase + kWoWaves * j;
     if (a >= P) break;
     const uint32_t cw = (uint32_t)__builtin_amdgcn_readfirstlane((int)cnt[a]);
     if (!(cw & 0x8000u)) {  // not in the realm: no record
-      if (in_realm(j + 1)) prefetch(a + kAoWaves);
+      if (in_realm(j + 1)) prefetch(a + kWoWaves);
       continue;
     }
     const int nv = cw & 127, ninv = (cw >> 7) & 15;
@@ -122,7 +127,7 @@ __global__ void __launch_bounds__(256) wire_obs_kernel(ObsParams p) {
       if (lane + 64 * i < 225) wmat[lane + 64 * i] = (uint8_t)wm[i];
     const uint2 it = iv;  // this agent's item word (lanes 0..11)
     const uint32_t mv = ao_move_bits(wm[1]);
-    if (in_realm(j + 1)) prefetch(a + kAoWaves);  // the next agent's loads, ahead of the stores
+    if (in_realm(j + 1)) prefetch(a + kWoWaves);  // the next agent's loads, ahead of the stores
 
     ao_compact(pr, S, r, c, visw);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -187,7 +192,7 @@ hipError_t launch_wire_obs(const ObsParams& p, hipStream_t stream) {
   if (!ao_layout_ok(p)) return hipErrorInvalidValue;  // the wire format's fixed sections
   const hipError_t err = launch_wire_header(p, stream);  // count words, sizes, offsets
   if (err != hipSuccess) return err;
-  const dim3 grid(p.n_envs, (p.P + kAoAgents - 1) / kAoAgents), block(64 * kAoWaves);
+  const dim3 grid(p.n_envs, (p.P + kWoAgents - 1) / kWoAgents), block(64 * kWoWaves);
   const size_t lds = wo_lds_bytes(p.S);
   if (p.wflags) hipLaunchKernelGGL(wire_obs_kernel<true>, grid, block, lds, stream, p);
   else hipLaunchKernelGGL(wire_obs_kernel<false>, grid, block, lds, stream, p);

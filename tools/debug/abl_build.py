@@ -21,6 +21,12 @@ PATCHES = {
                f"      if (exch && {NEVER}) {{\n        for (int j0 = 0; j0 < nm; j0 += 64) {{")],
     "notile": [("native_obs.hip", "        if (t < 225) {\n          d16[3 * t]", f"        if (t < 225 && {NEVER}) {{\n          d16[3 * t]")],
     "nozero": [("native_obs.hip", "for (int q = lane; q < body; q += 64) z4[q]", f"for (int q = lane; q < body && {NEVER}; q += 64) z4[q]")],
+    "ntzero": [("native_obs.hip", "for (int q = lane; q < body; q += 64) z4[q] = make_uint4(0u, 0u, 0u, 0u);",
+                "typedef unsigned int u32x4 __attribute__((ext_vector_type(4))); for (int q = lane; q < body; q += 64) __builtin_nontemporal_store((u32x4){0u, 0u, 0u, 0u}, reinterpret_cast<u32x4*>(&z4[q]));")],
+    "wg32": [("agent_obs.h", "constexpr int kAoWaves = 4;", "constexpr int kAoWaves = 8;"),
+             ("agent_obs.h", "constexpr int kAoAgents = 16; ", "constexpr int kAoAgents = 32; "),
+             ("native_obs.hip", "__launch_bounds__(256)", "__launch_bounds__(512)"),
+             ("wire_obs.hip", "__launch_bounds__(256)", "__launch_bounds__(512)")],
     "nomask": [("native_obs.hip", "        if (q < NMMO_NATIVE_MASK_BYTES / 16) {", f"        if (q < NMMO_NATIVE_MASK_BYTES / 16 && {NEVER}) {{")],
     "noent": [("native_obs.hip", "for (int k0 = 0; k0 < nv4; k0 += 4) {", f"for (int k0 = 0; k0 < nv4 && {NEVER}; k0 += 4) {{")],
     "noinv": [("native_obs.hip", "    if (ninv == 0) {\n      if (lane < kInv * 8 / 4)", f"    if (ninv == 0 || {NEVER}) {{\n      if (lane < kInv * 8 / 4)")],
