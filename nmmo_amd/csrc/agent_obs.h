@@ -141,6 +141,25 @@ __device__ inline void ao_stage(const ObsParams& p, int e, int16_t* T, uint32_t*
   __syncthreads();
 }
 
+// Workgroup -> (env, agent group) for a 1-D grid of n_envs * G workgroups. Workgroups are
+// dispatched round-robin over the 8 XCDs (id % 8), each with its own L2: the G groups of an env
+// go to one XCD back to back, so the env's staged columns come from HBM once and from that L2
+// G - 1 times (with a 2-D grid an env's groups were n_envs workgroups apart: every group fetched
+// them from HBM). Falls back to adjacent ids when n_envs % 8 != 0. Used by the wire kernel (same
+// box: C5 at N = 1 375 -> 380 M); the native kernel, whose rows are 30x larger, measured slower
+// with it (0.151 -> 0.168 ms per 512 envs) and keeps the 2-D grid.
+__device__ __forceinline__ void ao_env_group(int n_envs, int G, int& e, int& g) {
+  const int id = blockIdx.x;
+  if ((n_envs & 7) == 0) {
+    const int x = id & 7, q = id >> 3;
+    g = q % G;
+    e = (q / G) * 8 + x;
+  } else {
+    e = id / G;
+    g = id - e * G;
+  }
+}
+
 // The window rows and item words of a workgroup's kAoAgents agents (g * kAoAgents ..), staged in
 // LDS once per workgroup (every thread; one barrier inside): ws[(la * 15 + row) * 5 + k] = the 5
 // aligned dwords holding window row `row` of agent la (its 15 materials start at byte

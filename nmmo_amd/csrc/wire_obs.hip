@@ -37,7 +37,9 @@ __global__ void __launch_bounds__(64 * kWoWaves) wire_obs_kernel(ObsParams p) {
   uint8_t* wmat_all = reinterpret_cast<uint8_t*>(visw_all + kWoWaves * 128);  // [kWoWaves][256] window materials
   int* woff = reinterpret_cast<int*>(wmat_all + kWoWaves * 256);            // [P + 1] record offsets
   uint16_t* rk = reinterpret_cast<uint16_t*>(woff + 128 + 4);                // [kMaxSlots] table index
-  const int e = blockIdx.x, g = blockIdx.y, tid = threadIdx.x, lane = lane_id();
+  int e, g;
+  ao_env_group(p.n_envs, (P + kWoAgents - 1) / kWoAgents, e, g);
+  const int tid = threadIdx.x, lane = lane_id();
   const int w = __builtin_amdgcn_readfirstlane(wave_id());  // wave-uniform values in SGPRs
   const WireView v = wire_view(p.wire, p.n_envs, P);
   const uint16_t* cnt = v.cnt + (size_t)e * P;
@@ -192,7 +194,7 @@ hipError_t launch_wire_obs(const ObsParams& p, hipStream_t stream) {
   if (!ao_layout_ok(p)) return hipErrorInvalidValue;  // the wire format's fixed sections
   const hipError_t err = launch_wire_header(p, stream);  // count words, sizes, offsets
   if (err != hipSuccess) return err;
-  const dim3 grid(p.n_envs, (p.P + kWoAgents - 1) / kWoAgents), block(64 * kWoWaves);
+  const dim3 grid(p.n_envs * ((p.P + kWoAgents - 1) / kWoAgents)), block(64 * kWoWaves);  // ao_env_group
   const size_t lds = wo_lds_bytes(p.S);
   if (p.wflags) hipLaunchKernelGGL(wire_obs_kernel<true>, grid, block, lds, stream, p);
   else hipLaunchKernelGGL(wire_obs_kernel<false>, grid, block, lds, stream, p);

@@ -27,6 +27,7 @@ PATCHES = {
              ("agent_obs.h", "constexpr int kAoAgents = 16; ", "constexpr int kAoAgents = 32; "),
              ("native_obs.hip", "__launch_bounds__(256)", "__launch_bounds__(512)"),
              ("wire_obs.hip", "__launch_bounds__(256)", "__launch_bounds__(512)")],
+    "nomt": [("obs.hip", '  asm volatile("" : "+v"(my_task), "+v"(my_prev));', "")],
     "nomask": [("native_obs.hip", "        if (q < NMMO_NATIVE_MASK_BYTES / 16) {", f"        if (q < NMMO_NATIVE_MASK_BYTES / 16 && {NEVER}) {{")],
     "noent": [("native_obs.hip", "for (int k0 = 0; k0 < nv4; k0 += 4) {", f"for (int k0 = 0; k0 < nv4 && {NEVER}; k0 += 4) {{")],
     "noinv": [("native_obs.hip", "    if (ninv == 0) {\n      if (lane < kInv * 8 / 4)", f"    if (ninv == 0 || {NEVER}) {{\n      if (lane < kInv * 8 / 4)")],
