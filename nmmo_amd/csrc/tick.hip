@@ -2191,9 +2191,12 @@ __device__ __forceinline__ void tick_env(Ctx& c, Heads hd, float* rew, uint8_t* 
     }
   }
   NMMO_STAMP(19);
-  // the NPC spawn reads the respawned tiles; the rewards read nothing the respawn wrote (the
-  // store reads it after tick_env's closing barrier)
-  if (sys(c, NMMO_SYS_NPC)) __syncthreads();
+  // The NPC spawn tests its tiles' passability from their tick-start materials (npc_spawn_pre),
+  // and nothing else it touches (free ring, NPC slots, E) is written by the respawn or the
+  // expiry: it follows the respawn without a barrier, except under foreign depletion, where it
+  // reads the respawned tiles. The rewards read nothing the respawn wrote (the store reads it
+  // after tick_env's closing barrier) and follow the spawn's barrier.
+  if (sys(c, NMMO_SYS_NPC) && c.foreign_any) __syncthreads();
   if (tid == 0) c.E[E_TICK] = tick + 1;  // read only at the tick's start (and by store_env)
   NMMO_STAMP(8);
   // 7. NPC refill
