@@ -840,7 +840,8 @@ __device__ __forceinline__ uint32_t dpp_row_up(uint32_t x) {    // lane i <- lan
 __device__ __forceinline__ uint32_t dpp_row_down(uint32_t x) {  // lane i <- lane i + 1 in its row (0 at row end)
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x101, 0xF, 0xF, true);
 }
-__device__ __forceinline__ void npc_bfs_phase(Ctx& c) {
+// returns the number of requests (block-uniform: every thread counts the same LDS mask)
+__device__ __forceinline__ int npc_bfs_phase(Ctx& c) {
   constexpr int W = 2 * kVision + 1;
   constexpr uint32_t kImp = (1u << M_VOID) | (1u << M_WATER) | (1u << M_STONE) | (1u << M_OCEAN) | (1u << M_FISH);
   constexpr uint32_t kMid = 1u << kVision;
@@ -901,6 +902,7 @@ __device__ __forceinline__ void npc_bfs_phase(Ctx& c) {
     }
     if (on && row == 0) c.amove[n] = (int16_t)result;
   }
+  return nreq;
 }
 // greedy step toward (dr, dc) over the passable neighbours in nbm (SPEC §6 v1 rule)
 __device__ __forceinline__ int greedy_step(int dr, int dc, uint32_t nbm) {
@@ -1408,8 +1410,8 @@ __device__ __forceinline__ void tick_env(Ctx& c, Heads hd, float* rew, uint8_t* 
   asm volatile("" : "+v"(spawn.mat));  // opaque: waited on at the spawn, not here
   if (npc_on) {  // hunt pathing for the NPCs that asked (block-uniform)
     __syncthreads();
-    npc_bfs_phase(c);
-    __syncthreads();
+    // the results' barrier only when some NPC asked (no request: nothing was written)
+    if (npc_bfs_phase(c) > 0) __syncthreads();
     if (my_move == kBfsPending) {
       const int r = c.amove[s];
       const int ts = TF(F_TARGET_ID, s) - 1;
