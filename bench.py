@@ -167,6 +167,7 @@ def parse(argv=None):
     ap.add_argument("--no-decode", action="store_true", help="C5: skip the decoded pass")
     ap.add_argument("--dry-launch", action="store_true",
                     help="launcher check: each rank prints its RANK/WORLD_SIZE and exits (no GPU)")
+    ap.add_argument("--inject-fault", action="store_true", help=argparse.SUPPRESS)  # tests: nmmo_inject_fault
     return ap.parse_args(argv)
 
 
@@ -298,6 +299,26 @@ def _stagger(engs, L: int, per: int, base: int, pseed: int):
             e.end_episodes(ids % L == k)
             e.scripted_actions(pseed)
             e.step(write_obs=False)
+
+
+def _check_faults(args, engs, name, world, dist, dev):
+    """The tick fault word of every engine of this workload (nmmo_get_fault), max over ranks: a
+    launch that hit a loop bound did not compute the serial-order tick, so the workload fails
+    (no bench line) on every rank instead of reporting a number."""
+    import torch
+
+    from nmmo_amd.engine import TickFault
+
+    if args.inject_fault:
+        engs[0].inject_fault(1)
+    words = [e.get_fault() for e in engs]
+    word = next((w for w in words if w), 0)
+    if world > 1:
+        t = torch.tensor([word], dtype=torch.int64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        word = int(t.item())
+    if word:
+        raise TickFault(word, f"bench {name}")
 
 
 def _kernel_timing(eng, pseed: int, steps: int):
@@ -502,6 +523,7 @@ def measure(args, name, layout_name, envs, rank, world, dev, steps, warmup, dist
         "roofline": _roofline(prof_name, kern, byts, ms, per, timing, nb, elapsed / steps, fill_gbs),
         "batches": nb,
     }
+    _check_faults(args, engs, name, world, dist, dev)  # every tick of this workload ran (timed and after)
     for e in engs:
         e.close()
     del eng, engs
@@ -591,6 +613,7 @@ def measure_gather(args, name, envs, rank, world, dev, steps, warmup, dist=None,
         g.close()
     eng = engs[0]
     tick_avg_ms, obs_avg_ms, _ = _kernel_timing(eng, pseed, steps)
+    _check_faults(args, engs, name, world, dist, dev)
     wire_env_bytes = nw.total_bytes(eng.obs) / per  # this batch's last step: header + records
     S, P = eng.S, cfg.PLAYER_N
     d = passes[False]

@@ -297,6 +297,19 @@ NMMO_API int nmmo_end_episodes(NmmoHandle* h, const uint8_t* dev_env_mask, void*
 NMMO_API int nmmo_step(NmmoHandle* h, const int32_t* actions, void* obs, float* rew, uint8_t* term,
               uint8_t* trunc, uint8_t* mask, void* stream);
 
+/* One tick of the listed envs only: pool.send(actions) to the envs the last recv() returned
+ * under pufferlib's async env pool (env_pool=True, envs_per_batch < num_envs; config.yaml:35-38,
+ * clean_pufferl.py:106-114,293,357), where the other envs keep their state and their last
+ * outputs. env_ids: device int32 [n_ids], distinct ids in [0, n_envs) (an id outside the range is
+ * dropped and recorded in the fault word as NMMO_FAULT_ENV_LIST | position << 8; duplicates are
+ * a precondition violation). Every other argument has nmmo_step's full [n_envs] shape: only the
+ * listed envs' rows of actions are read and of obs / rew / term / trunc / mask written (the pool
+ * keeps each env's outputs until its next recv). Auto-reset, the wrapper layer and the counters
+ * behave as in nmmo_step for the listed envs. Flat and native obs only (NMMO_E_INVALID for a
+ * wire obs buffer: its header packs every env). Enqueued on `stream`; graph-capturable. */
+NMMO_API int nmmo_step_envs(NmmoHandle* h, const int32_t* env_ids, int32_t n_ids, const int32_t* actions, void* obs,
+                            float* rew, uint8_t* term, uint8_t* trunc, uint8_t* mask, void* stream);
+
 /* The observation gather alone, over the envs' current state (what nmmo_step's obs argument
  * writes after the tick): nmmo_step(obs = NULL) followed by nmmo_observe(obs) on the same stream
  * gives the same bytes as nmmo_step(obs). Replaces nmmo.Env._compute_observations, the second
@@ -431,7 +444,15 @@ NMMO_API int nmmo_read_timing(NmmoHandle* h, double* ms /* [3] */, int32_t* n);
 #define NMMO_FAULT_BUY_ROUNDS 2
 #define NMMO_FAULT_GIVE_ROUNDS 3
 #define NMMO_FAULT_HASH_PROBE 4
+#define NMMO_FAULT_ENV_LIST 5   /* nmmo_step_envs: an env id outside [0, n_envs) (dropped) */
 NMMO_API int nmmo_get_fault(NmmoHandle* h, int32_t* fault);
+/* The fault word without a host sync: when the word is non-zero and *dev_dst (device int32) is
+ * 0, the word is copied into it (the first fault of several handles is kept). The word is not
+ * cleared. Enqueued on `stream`; graph-capturable (the learner gather ships it with its sizes). */
+NMMO_API int nmmo_fault_into(NmmoHandle* h, int32_t* dev_dst, void* stream);
+/* Test hook: sets the fault word to `fault` (synchronous), so a caller's fault checks can be
+ * exercised without a faulting state. */
+NMMO_API int nmmo_inject_fault(NmmoHandle* h, int32_t fault);
 
 /* The event log of env `env` (realm.event_log.get_data): copies the most recent
  * min(retained, max_rows) rows, oldest first, into host_rows [max_rows][NMMO_EVENT_COLS] and

@@ -26,6 +26,7 @@ SYMBOLS = [
     "nmmo_last_error", "nmmo_abi_version", "nmmo_end_episodes", "nmmo_build_info",
     "nmmo_get_wrapper_dropped", "nmmo_set_task_weights", "nmmo_wire_header_bytes", "nmmo_wire_max_bytes",
     "nmmo_wire_pack", "nmmo_wire_unpack", "nmmo_wire_check", "nmmo_dev_alloc", "nmmo_dev_free", "nmmo_observe",
+    "nmmo_step_envs", "nmmo_inject_fault", "nmmo_fault_into",
 ]
 
 
@@ -72,6 +73,9 @@ def declare(L):
     L.nmmo_destroy.restype = None
     L.nmmo_reset.argtypes = [vp, vp, vp, vp, vp]
     L.nmmo_step.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp]
+    L.nmmo_step_envs.argtypes = [vp, vp, i32, vp, vp, vp, vp, vp, vp, vp]
+    L.nmmo_inject_fault.argtypes = [vp, i32]
+    L.nmmo_fault_into.argtypes = [vp, vp, vp]
     L.nmmo_scripted_actions.argtypes = [vp, u64, vp, vp]
     L.nmmo_get_state.argtypes = [vp, vp, sz]
     L.nmmo_set_state.argtypes = [vp, vp, sz]

@@ -14,6 +14,15 @@ NMMO_E_HIP = -2
 NMMO_E_NOMEM = -3
 NMMO_E_SIZE = -4
 
+# tick fault word (nmmo_get_fault): code | env << 8
+FAULT_ATTACK_ROUNDS = 1
+FAULT_BUY_ROUNDS = 2
+FAULT_GIVE_ROUNDS = 3
+FAULT_HASH_PROBE = 4
+FAULT_ENV_LIST = 5
+FAULT_NAMES = {1: "attack rounds", 2: "Buy rounds", 3: "Give rounds", 4: "position-hash probe",
+               5: "env id outside the handle (nmmo_step_envs)"}
+
 SYS_RESOURCE = 1 << 0
 SYS_COMBAT = 1 << 1
 SYS_NPC = 1 << 2

@@ -251,9 +251,9 @@ int nmmo_create(const NmmoConfig* cfg, int32_t n_envs, uint64_t seed, int32_t de
   }
   h->st = DevState{h->d_env,   h->d_ent,   h->d_ring,  h->d_mat,    h->d_dep, h->d_bank,
                    h->d_items, h->d_iring, h->d_mlist, h->d_mcount, h->d_events,
-                   h->d_tasks, h->d_assign, nullptr, h->d_tstate, 1,            0,           n_envs, P,
+                   h->d_tasks, h->d_assign, nullptr, h->d_tstate, 1,            0,           0, n_envs, P,
                    N,          S,          seed,       nullptr,     *cfg,      h->d_foreign,
-                   h->d_foreign + 1};
+                   h->d_foreign + 1, nullptr, 0};
   {  // default task table: everyone runs TickGE(task_num_tick) (SPEC §12)
     NmmoTask t;
     memset(&t, 0, sizeof(t));
@@ -291,6 +291,8 @@ static ObsParams obs_params(NmmoHandle* h, void* obs) {
   p.o_inventory = L.off_inventory; p.o_market = L.off_market; p.o_task = L.off_task;
   p.o_tile = L.off_tile;
   p.row_map = nullptr;
+  p.env_list = nullptr;
+  p.n_list = 0;
   p.wcount = native ? h->d_wcount : nullptr;
   p.wmcount = native ? h->d_wmcount : nullptr;
   p.wrank = wire ? h->d_wrank : nullptr;
@@ -312,6 +314,8 @@ static WrapParams wrap_params(NmmoHandle* h, const int32_t* actions, float* rew,
   p.mask = mask; p.ws = h->d_ws; p.uniq = h->d_uniq; p.wenv = h->d_wenv; p.wdrop = h->d_wdrop; p.info = h->d_info;
   p.wc = h->wc; p.n_envs = h->st.n_envs; p.P = h->st.P; p.S = h->st.S; p.evcap = h->cfg.event_cap;
   p.items_on = (h->cfg.systems & NMMO_SYS_ITEM) != 0;
+  p.env_list = nullptr;
+  p.n_list = 0;
   return p;
 }
 
@@ -349,8 +353,9 @@ int nmmo_end_episodes(NmmoHandle* h, const uint8_t* dev_env_mask, void* stream) 
   return NMMO_OK;
 }
 
-int nmmo_step(NmmoHandle* h, const int32_t* actions, void* obs, float* rew, uint8_t* term,
-              uint8_t* trunc, uint8_t* mask, void* stream) {
+// nmmo_step over every env (env_ids = NULL) or over the listed envs (nmmo_step_envs)
+static int step_impl(NmmoHandle* h, const int32_t* env_ids, int32_t n_ids, const int32_t* actions, void* obs,
+                     float* rew, uint8_t* term, uint8_t* trunc, uint8_t* mask, void* stream) {
   if (!h) return fail(NMMO_E_INVALID, "null handle");
   if (!actions || !rew || !term || !trunc || !mask)
     return fail(NMMO_E_INVALID, "actions/rew/term/trunc/mask must be device pointers");
@@ -358,19 +363,69 @@ int nmmo_step(NmmoHandle* h, const int32_t* actions, void* obs, float* rew, uint
   hipStream_t s = (hipStream_t)stream;
   const bool rec = h->timing && h->t_count < kTimingCap;
   hipEvent_t* ev = rec ? &h->ev[(size_t)h->t_count * 4] : nullptr;
+  DevState st = h->st;
+  st.env_list = env_ids;
+  st.n_list = n_ids;
   if (rec) HIP_TRY(hipEventRecord(ev[0], s));
-  HIP_TRY(launch_tick(h->st, actions, nullptr, rew, term, trunc, mask, 0, s));
+  HIP_TRY(launch_tick(st, actions, nullptr, rew, term, trunc, mask, 0, s));
   if (rec) HIP_TRY(hipEventRecord(ev[1], s));
-  if (h->wrap_on) HIP_TRY(launch_wrap(wrap_params(h, actions, rew, term, trunc, mask), 0, s));
+  if (h->wrap_on) {
+    WrapParams wp = wrap_params(h, actions, rew, term, trunc, mask);
+    wp.env_list = env_ids;
+    wp.n_list = n_ids;
+    HIP_TRY(launch_wrap(wp, 0, s));
+  }
   if (rec) HIP_TRY(hipEventRecord(ev[2], s));  // wrapper span = ev[1]..ev[2] (empty when off)
   const bool do_obs = obs && h->cfg.obs_layout != NMMO_OBS_NONE;
-  if (do_obs) HIP_TRY(launch_obs(obs_params(h, obs), s));
+  if (do_obs) {
+    ObsParams op = obs_params(h, obs);
+    op.env_list = env_ids;
+    op.n_list = n_ids;
+    HIP_TRY(launch_obs(op, s));
+  }
   if (do_obs) h->last_native = obs;  // kept across a tick without obs: the pack check then says stale
-  h->native_fresh = do_obs;
+  // a subset step leaves the other envs' native rows (and their wire counts) as they were, so the
+  // buffer describes no single state: nmmo_wire_pack refuses it until a whole-handle gather
+  h->native_fresh = do_obs && !env_ids;
   if (rec) {
     HIP_TRY(hipEventRecord(ev[3], s));  // obs span = ev[2]..ev[3] (empty when no obs)
     h->t_count++;
   }
+  return NMMO_OK;
+}
+
+int nmmo_step(NmmoHandle* h, const int32_t* actions, void* obs, float* rew, uint8_t* term,
+              uint8_t* trunc, uint8_t* mask, void* stream) {
+  return step_impl(h, nullptr, 0, actions, obs, rew, term, trunc, mask, stream);
+}
+
+int nmmo_step_envs(NmmoHandle* h, const int32_t* env_ids, int32_t n_ids, const int32_t* actions, void* obs,
+                   float* rew, uint8_t* term, uint8_t* trunc, uint8_t* mask, void* stream) {
+  if (!h || !env_ids) return fail(NMMO_E_INVALID, "null handle / env_ids");
+  if (n_ids < 0 || n_ids > h->st.n_envs) return fail(NMMO_E_INVALID, "n_ids %d not in 0..%d", n_ids, h->st.n_envs);
+  if (h->cfg.obs_layout == NMMO_OBS_WIRE && obs)
+    return fail(NMMO_E_INVALID, "nmmo_step_envs: the wire layout packs every env of the handle (use nmmo_step)");
+  return step_impl(h, env_ids, n_ids, actions, obs, rew, term, trunc, mask, stream);
+}
+
+__global__ void fault_into_kernel(const int32_t* word, int32_t* dst) {
+  const int32_t w = *word;
+  if (w) atomicCAS(dst, 0, w);
+}
+
+int nmmo_fault_into(NmmoHandle* h, int32_t* dev_dst, void* stream) {
+  if (!h || !dev_dst) return fail(NMMO_E_INVALID, "null argument");
+  HIP_TRY(hipSetDevice(h->device));
+  hipLaunchKernelGGL(fault_into_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, h->d_foreign + 1, dev_dst);
+  HIP_TRY(hipGetLastError());
+  return NMMO_OK;
+}
+
+int nmmo_inject_fault(NmmoHandle* h, int32_t fault) {
+  if (!h) return fail(NMMO_E_INVALID, "null handle");
+  HIP_TRY(hipSetDevice(h->device));
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(h->d_foreign + 1, &fault, 4, hipMemcpyHostToDevice));
   return NMMO_OK;
 }
 
@@ -734,6 +789,7 @@ int nmmo_set_state(NmmoHandle* h, const void* host_buf, size_t nbytes) {
   HIP_TRY(hipMemcpy(h->d_tstate, tstate.data(), tstate.size() * sizeof(NmmoTaskState), hipMemcpyHostToDevice));
   HIP_TRY(launch_rebuild_dep(h->st, nullptr));
   HIP_TRY(hipDeviceSynchronize());
+  h->native_fresh = false;  // the last native obs no longer describes the state (nmmo_wire_pack)
   return NMMO_OK;
 }
 
@@ -741,12 +797,13 @@ int nmmo_set_tasks(NmmoHandle* h, const NmmoTask* tasks, int32_t n_tasks, const 
                    const int32_t* assign) {
   if (!h || !tasks) return fail(NMMO_E_INVALID, "null argument");
   if (n_tasks < 1 || n_tasks > NMMO_MAX_TASKS) return fail(NMMO_E_INVALID, "n_tasks %d not in 1..%d", n_tasks, NMMO_MAX_TASKS);
-  int tev = 0;
+  int tev = 0, tmap = 0;
   for (int i = 0; i < n_tasks; i++)
     for (int k = 0; k < 2; k++) {
       const int pr = tasks[i].term[k].pred;
       if (pr < 0 || pr >= NMMO_N_PREDICATES) return fail(NMMO_E_INVALID, "task %d term %d: predicate %d", i, k, pr);
       tev |= (pr >= PRED_COUNT_EVENT && pr <= PRED_DEFEAT_ENTITY) || pr == PRED_PRACTICE_EATING;
+      tmap |= pr == PRED_CAN_SEE_TILE;
     }
   const size_t nP = (size_t)h->st.n_envs * h->st.P;
   if (assign)
@@ -780,7 +837,9 @@ int nmmo_set_tasks(NmmoHandle* h, const NmmoTask* tasks, int32_t n_tasks, const 
   h->st.tasks = d_tasks;
   h->st.n_tasks = n_tasks;
   h->st.tev = tev;
+  h->st.tmap = tmap;
   h->st.task_cum = nullptr;  // weights belong to the previous table
+  h->native_fresh = false;   // task indices of the last native obs may be out of date
   return NMMO_OK;
 }
 
@@ -911,6 +970,7 @@ int nmmo_set_map_bank(NmmoHandle* h, const uint8_t* host_buf, size_t nbytes) {
   HIP_TRY(hipMemcpy(h->d_bank, host_buf, need, hipMemcpyHostToDevice));
   HIP_TRY(launch_rebuild_dep(h->st, nullptr));
   HIP_TRY(hipDeviceSynchronize());
+  h->native_fresh = false;
   return NMMO_OK;
 }
 

@@ -36,6 +36,7 @@ struct DevState {
   const uint64_t* task_cum;  // [n_tasks] sampling thresholds (nmmo_set_task_weights) or NULL
   NmmoTaskState* tstate; // [n][P] progress / event accumulators
   int n_tasks, tev;      // tev: some task term counts events
+  int tmap;              // some task term reads the material map (CanSeeTile)
   int n_envs, P, N, S;   // N = NPC capacity (0 when the NPC system is off), S = P + N
   uint64_t seed;         // create seed (first-episode seeds)
   unsigned long long* counters;  // optional device u64 [3]: agent-steps, finished episodes, event rows
@@ -49,7 +50,13 @@ struct DevState {
   // (nmmo_get_fault). Every round loop stops at a bound the serial argument never reaches, so a
   // state outside the tick's invariants ends the launch instead of hanging it.
   int32_t* fault;
+  // launch-local env list (nmmo_step_envs): workgroup b steps env env_list[b] for b < n_list;
+  // NULL = every env (workgroup b steps env b). Ids outside [0, n_envs) are dropped (fault word).
+  const int32_t* env_list;
+  int n_list;
 };
+// grid size and env of workgroup b of a launch over an env list (NULL = all n envs)
+__host__ __device__ inline int list_grid(const int32_t* list, int n_list, int n) { return list ? n_list : n; }
 
 struct ObsParams {
   const int32_t* env;   // [n][NE]
@@ -79,6 +86,8 @@ struct ObsParams {
   int* wmcount;         // native only, or NULL: [n] the listing count of this obs launch (nmmo_wire_pack)
   uint16_t* wrank;      // wire only: [n][kMaxSlots] entity-table index of each slot (0xFFFF = none),
                         // wire_count_kernel -> wire_obs_kernel
+  const int32_t* env_list;  // flat / native obs: gather only these envs (DevState::env_list), or NULL
+  int n_list;
 };
 constexpr int kWrapObsPrice = 1, kWrapObsNoGive = 2, kWrapObsNoDangerous = 4;
 
@@ -100,6 +109,8 @@ struct WrapParams {
   NmmoAgentInfo* info;       // [n][P] caller-owned, may be NULL
   NmmoWrapperConfig wc;
   int n_envs, P, S, evcap, items_on;
+  const int32_t* env_list;   // step only: the stepped envs (DevState::env_list), or NULL
+  int n_list;
 };
 
 struct PolicyParams {

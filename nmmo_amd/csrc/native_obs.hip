@@ -39,7 +39,9 @@ __global__ void __launch_bounds__(256) native_obs_kernel(ObsParams p) {
   uint32_t* visw_all = reinterpret_cast<uint32_t*>(mpo + NMMO_MARKET_ROWS);   // [4][128]
   uint32_t* wst = visw_all + kAoWaves * 128;                                  // [16][15][5] window rows
   uint2* ist = reinterpret_cast<uint2*>(wst + kAoAgents * kAoWinAgentBytes / 4);  // [16][12] item words
-  const int e = blockIdx.x, g = blockIdx.y, tid = threadIdx.x, lane = lane_id();
+  const int e = p.env_list ? p.env_list[blockIdx.x] : (int)blockIdx.x, g = blockIdx.y, tid = threadIdx.x,
+            lane = lane_id();
+  if ((unsigned)e >= (unsigned)p.n_envs) return;  // a bad list id (the tick records it)
   const int w = __builtin_amdgcn_readfirstlane(wave_id());
   const int nm = min(max(p.mcount[e], 0), NMMO_MARKET_ROWS);
   if (p.wmcount && g == 0 && tid == 0) p.wmcount[e] = nm;  // nmmo_wire_pack reads this launch's count
@@ -253,7 +255,9 @@ __global__ void __launch_bounds__(256) native_obs_kernel(ObsParams p) {
 
 hipError_t launch_native_obs(const ObsParams& p, hipStream_t stream) {
   if (p.S % 8 || p.S > kMaxSlots || p.P > 128 || !p.nat || !ao_layout_ok(p)) return hipErrorInvalidValue;
-  const dim3 grid(p.n_envs, (p.P + kAoAgents - 1) / kAoAgents), block(64 * kAoWaves);
+  const int ne = list_grid(p.env_list, p.n_list, p.n_envs);
+  if (ne <= 0) return hipSuccess;
+  const dim3 grid(ne, (p.P + kAoAgents - 1) / kAoAgents), block(64 * kAoWaves);
   const size_t lds = no_lds_bytes(p.S);
   if (p.wflags) hipLaunchKernelGGL(native_obs_kernel<true>, grid, block, lds, stream, p);
   else hipLaunchKernelGGL(native_obs_kernel<false>, grid, block, lds, stream, p);

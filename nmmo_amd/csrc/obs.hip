@@ -175,7 +175,8 @@ __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
   uint2* mitem = inv_all + kObsWaves * kInv;  // listed item words
   uint16_t* mpo = reinterpret_cast<uint16_t*>(mitem + NMMO_MARKET_ROWS);  // price | owner << 8
   uint8_t* wmat_all = reinterpret_cast<uint8_t*>(mpo + NMMO_MARKET_ROWS);  // per-wave 15x15 materials
-  const int e = blockIdx.x, g = blockIdx.y;
+  const int e = p.env_list ? p.env_list[blockIdx.x] : (int)blockIdx.x, g = blockIdx.y;
+  if ((unsigned)e >= (unsigned)p.n_envs) return;  // a bad list id (the tick records it)
   const int tid = threadIdx.x;
   const int nm = p.mcount[e];
   for (int j = tid; j < nm; j += blockDim.x) {  // end-of-tick listings, ascending row
@@ -354,7 +355,9 @@ __global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
 hipError_t launch_obs(const ObsParams& p, hipStream_t stream) {
   if (p.wire) return launch_wire_obs(p, stream);  // wire_obs.hip
   if (p.nat) return launch_native_obs(p, stream);  // native_obs.hip
-  const dim3 grid(p.n_envs, (p.P + kObsAgentsPerBlock - 1) / kObsAgentsPerBlock), block(64 * kObsWaves);
+  const int ne = list_grid(p.env_list, p.n_list, p.n_envs);
+  if (ne <= 0) return hipSuccess;
+  const dim3 grid(ne, (p.P + kObsAgentsPerBlock - 1) / kObsAgentsPerBlock), block(64 * kObsWaves);
   const size_t lds = obs_lds_bytes(p.S);
   if (p.wflags) hipLaunchKernelGGL(obs_kernel<true>, grid, block, lds, stream, p);
   else hipLaunchKernelGGL(obs_kernel<false>, grid, block, lds, stream, p);

@@ -80,6 +80,7 @@ struct Ctx {
                         // load makes the next LDS wait (lgkmcnt) wait for HBM too
   int4* tdesc;             // LDS [128][2] (pred, a, b, c) of each player's terms (when tev)
   bool tev;
+  bool tmap;         // DevState::tmap: a task reads the material map at the rewards
   int evcap, tick1;  // ring rows (0 = no event log); tick + 1 (the events' tick column)
   int S, P, N, IC;
   bool items, exch, prof, equip;
@@ -225,6 +226,7 @@ __device__ __forceinline__ Ctx make_ctx(unsigned char* smem, const DevState& st,
     c.ikey = nullptr;
   }
   c.tev = st.tev != 0;
+  c.tmap = st.tmap != 0;
   c.tasks = st.tasks;
   c.assign = st.assign + (size_t)e * st.P;
   c.task_cum = st.task_cum;
@@ -2196,9 +2198,10 @@ __device__ __forceinline__ void tick_env(Ctx& c, Heads hd, float* rew, uint8_t* 
   // The NPC spawn tests its tiles' passability from their tick-start materials (npc_spawn_pre),
   // and nothing else it touches (free ring, NPC slots, E) is written by the respawn or the
   // expiry: it follows the respawn without a barrier, except under foreign depletion, where it
-  // reads the respawned tiles. The rewards read nothing the respawn wrote (the store reads it
-  // after tick_env's closing barrier) and follow the spawn's barrier.
-  if (sys(c, NMMO_SYS_NPC) && c.foreign_any) __syncthreads();
+  // reads the respawned tiles. The rewards read the respawned tiles only through CanSeeTile
+  // (task_progress reads c.mat, which the respawn's other waves write): with the NPC system they
+  // follow the spawn's closing barrier, without it they need this one when a task reads the map.
+  if (sys(c, NMMO_SYS_NPC) ? c.foreign_any : c.tmap) __syncthreads();
   if (tid == 0) c.E[E_TICK] = tick + 1;  // read only at the tick's start (and by store_env)
   NMMO_STAMP(8);
   // 7. NPC refill
@@ -2277,7 +2280,11 @@ __device__ __forceinline__ void tick_body(const DevState& st, const int32_t* __r
                                           const uint64_t* __restrict__ env_seeds, float* rew, uint8_t* term,
                                           uint8_t* trunc, uint8_t* mask, int mode) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int e = blockIdx.x;
+  const int e = st.env_list ? st.env_list[blockIdx.x] : (int)blockIdx.x;
+  if ((unsigned)e >= (unsigned)st.n_envs) {  // a bad id of an env list: drop it, say so
+    if (threadIdx.x == 0) atomicCAS(st.fault, 0, NMMO_FAULT_ENV_LIST | (int)blockIdx.x << 8);
+    return;
+  }
   NMMO_STAMP_CLEAR();
   NMMO_STAMP(0);
   Ctx c = make_ctx(smem, st, e, kSys ? kSys : st.cfg.systems);
@@ -2379,7 +2386,9 @@ hipError_t launch_tick(const DevState& st, const int32_t* actions, const uint64_
     case NMMO_SYS_ALL: k = tick_kernel<NMMO_SYS_ALL>; break;
     default: k = tick_kernel<0>; break;
   }
-  hipLaunchKernelGGL(k, dim3(st.n_envs), dim3(threads), lds, stream,
+  const int grid = list_grid(st.env_list, st.n_list, st.n_envs);
+  if (grid <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k, dim3(grid), dim3(threads), lds, stream,
                      st, actions, env_seeds, rew, term, trunc, mask, mode);
   return hipGetLastError();
 }

@@ -84,7 +84,8 @@ __global__ void __launch_bounds__(kWrapThreads) wrap_kernel(WrapParams p, int mo
   __shared__ int cnt[128], dmg[128], maxdist[128], earned[128], maxdmg[128], ak[128], nk[128];
   __shared__ int lvl[5][128];
   __shared__ unsigned int perf[128];
-  const int e = blockIdx.x, tid = threadIdx.x, P = p.P, S = p.S;
+  const int e = p.env_list ? p.env_list[blockIdx.x] : (int)blockIdx.x, tid = threadIdx.x, P = p.P, S = p.S;
+  if ((unsigned)e >= (unsigned)p.n_envs) return;  // a bad list id (the tick records it)
   const int32_t* E = p.env + (size_t)e * NMMO_NE;
   const int tick = E[E_TICK], evc = E[E_EVENT_COUNT];
   NmmoWrapState* ws = p.ws + (size_t)e * P;
@@ -279,7 +280,9 @@ __global__ void __launch_bounds__(kWrapThreads) wrap_kernel(WrapParams p, int mo
 
 hipError_t launch_wrap(const WrapParams& p, int mode, hipStream_t stream) {
   if (p.P > 128 || p.evcap <= 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(wrap_kernel, dim3(p.n_envs), dim3(kWrapThreads), 0, stream, p, mode);
+  const int ne = list_grid(p.env_list, p.n_list, p.n_envs);
+  if (ne <= 0) return hipSuccess;
+  hipLaunchKernelGGL(wrap_kernel, dim3(ne), dim3(kWrapThreads), 0, stream, p, mode);
   return hipGetLastError();
 }
 

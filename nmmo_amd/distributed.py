@@ -76,6 +76,12 @@ class WireExchange:
     sizes(t) / payload(t) must stay untouched until `done(t)` (an event on the comm stream).
     Ring slot k = t % ring indexes the per-step state.
 
+    Each rank's sizes row carries one more word: its tick fault word of step t (nmmo_fault_into;
+    0 = none). payload(t) raises on a rank whose own word is set and on the root for any rank's
+    word, and likewise for an announced size outside [16, capacity] — on the sender as on the root,
+    both before posting any transfer of step t, so neither side waits for a transfer the other
+    will never post.
+
     On CPU tensors (gloo, tests) every call is synchronous. With gloo and CUDA tensors (the
     one-GPU rehearsal of a multi-rank run) transfers are staged through the host."""
 
@@ -87,8 +93,10 @@ class WireExchange:
         self.cuda = self.device.type == "cuda"
         self.staged = (backend or (dist.get_backend() if world > 1 else "nccl")) == "gloo" and self.cuda
         d = self.device
-        self.sizes = torch.zeros((ring, world, n_bufs), dtype=torch.int64, device=d)
-        self.sizes_host = torch.zeros((ring, world, n_bufs), dtype=torch.int64, pin_memory=self.cuda)
+        # [.., n_bufs] = the rank's tick fault word of the step
+        self.sizes = torch.zeros((ring, world, n_bufs + 1), dtype=torch.int64, device=d)
+        self.sizes_host = torch.zeros((ring, world, n_bufs + 1), dtype=torch.int64, pin_memory=self.cuda)
+        self.caps = [int(c) for c in recv_caps]
         self.comm = torch.cuda.Stream(device=d) if self.cuda else None
         self._sized = [None] * ring
         self._done = [None] * ring
@@ -127,10 +135,11 @@ class WireExchange:
                 q.wait()
 
     # -- protocol
-    def post_sizes(self, t: int, wires, ready=()):
+    def post_sizes(self, t: int, wires, ready=(), fault=None):
         """Step t's totals: the sender's (or the root's own) buffers' first int64 into
         sizes[k][rank]; the peers' totals into the root's sizes[k]. `ready`: events the comm
-        stream waits for (the compute that wrote `wires`)."""
+        stream waits for (the compute that wrote `wires`); `fault`: a device int32 [1] holding
+        this rank's tick fault word of step t (zeroed here once copied), or None."""
         k = t % self.ring
         # (sizes[k] / sizes_host[k] of step t - ring were read by then: the device reads are
         # earlier on the comm stream, the host read came before this call)
@@ -140,6 +149,11 @@ class WireExchange:
                     self.comm.wait_event(ev)
             for j, w in enumerate(wires):
                 self.sizes[k, self.rank, j].copy_(w[:8].view(torch.int64)[0])
+            if fault is None:
+                self.sizes[k, self.rank, self.n_bufs].zero_()
+            else:
+                self.sizes[k, self.rank, self.n_bufs].copy_(fault[0])
+                fault.zero_()
         if self.world > 1:
             if self.rank == self.dst:
                 self._p2p([], [(self.sizes[k, r], r) for r in self.peers])
@@ -160,6 +174,17 @@ class WireExchange:
         if self.cuda and self._sized[k] is not None:
             self._sized[k].synchronize()  # the copy of sizes(t) into pinned memory (host wait only)
         tot = self.sizes_host[k].tolist()
+        # the same checks on both ends of every transfer, before any of step t's transfers is posted
+        ranks = range(self.world) if self.rank == self.dst else [self.rank]
+        for r in ranks:
+            if tot[r][self.n_bufs]:
+                from .engine import TickFault
+
+                raise TickFault(int(tot[r][self.n_bufs]), f"learner gather, rank {r}, step {t}")
+            for j in range(self.n_bufs):
+                n = int(tot[r][j])
+                if n < 16 or n > self.caps[j]:
+                    raise RuntimeError(f"rank {r} buffer {j} announces {n} B at step {t} (capacity {self.caps[j]})")
         got = {}
         if self.rank == self.dst:
             for j in range(self.n_bufs):
@@ -168,9 +193,6 @@ class WireExchange:
             for r in self.peers:
                 for j in range(self.n_bufs):
                     n = int(tot[r][j])
-                    if n < 16 or n > self.recv_wire[r, j].numel():
-                        raise RuntimeError(f"rank {r} buffer {j} announces {n} B (capacity "
-                                           f"{self.recv_wire[r, j].numel()})")
                     w, s = self.recv_wire[r, j][:n], self.recv_small[r, j]
                     recvs += [(w, r), (s, r)]
                     got[r, j] = (w, s)
@@ -252,6 +274,10 @@ class WireGather:
                               ring=ring, backend=backend)
         self.streams = [torch.cuda.Stream(device=self.device) for _ in self.engines]
         self.status = torch.zeros(1, dtype=torch.int32, device=self.device)
+        # per ring slot: the first tick fault word of the step's batches (nmmo_fault_into), shipped
+        # to the root with the step's sizes
+        self.faults = torch.zeros((ring, 1), dtype=torch.int32, device=self.device)
+        self._posted = -1  # the last step whose payload was posted
         self.native = None
         if decode and rank == 0:
             n_envs = [e.n_envs for e in self.engines]
@@ -267,6 +293,7 @@ class WireGather:
         e.obs = self.wires[j][k]
         e.scripted_actions(self.pseed)
         e.step()
+        e.fault_into(self.faults[k])
         sm = self.smalls[j][k]
         sm[..., 0:4] = e.rew.view(torch.uint8).view(e.n_envs, self.P, 4)
         sm[..., 4] = e.term
@@ -321,17 +348,21 @@ class WireGather:
             ready.append(ev)
         if t >= 1:  # step t - 1's payload, now that step t is queued
             self._payload(t - 1)
-        self.x.post_sizes(t, [w[k] for w in self.wires], ready)
+        self.x.post_sizes(t, [w[k] for w in self.wires], ready, fault=self.faults[k])
         self.t += 1
 
     def _payload(self, s: int):
+        if s <= self._posted:  # drain() already moved it
+            return
         ks = s % self.ring
         got = self.x.post_payload(s, [w[ks] for w in self.wires], [sm[ks] for sm in self.smalls])
+        self._posted = s
         self._consume(s, got)
         self.x.mark_done(s)
 
     def drain(self):
-        """Post the last step's payload and make the current stream wait for every transfer."""
+        """Post the last step's payload (once: the next step() does not post it again) and make
+        the current stream wait for every transfer."""
         if self.t >= 1:
             self._payload(self.t - 1)
         cur = torch.cuda.current_stream(self.device)

@@ -14,7 +14,19 @@ import numpy as np
 import torch
 
 from . import abi
-from ._native import check, layout, lib
+from ._native import NativeError, check, layout, lib
+
+
+class TickFault(NativeError):
+    """A tick launch hit one of its loop bounds (nmmo_get_fault): that env's step is not the
+    serial-order result, so nothing downstream (a learner, a bench line) may use it."""
+
+    def __init__(self, word: int, where: str = ""):
+        self.word = int(word)
+        self.code, self.env = self.word & 0xFF, self.word >> 8
+        what = abi.FAULT_NAMES.get(self.code, f"code {self.code}")
+        super().__init__(f"{where + ': ' if where else ''}tick fault word {self.word:#x}: {what} "
+                         f"(env / list position {self.env})")
 
 
 class NmmoEngine:
@@ -137,6 +149,25 @@ class NmmoEngine:
                                   self._stream()), "nmmo_step")
         return self.obs, self.rew, self.term, self.trunc, self.mask
 
+    def step_envs(self, env_ids, actions=None, write_obs: bool = True):
+        """One tick of the listed envs only (nmmo_step_envs): env_ids int32 on the device
+        (distinct, in [0, n_envs)); actions and outputs keep the full [n_envs, ...] shape, and
+        only the listed envs' rows are read / written (the async pool's send, vecenv.py)."""
+        a = self.actions if actions is None else actions
+        if a.dtype != torch.int32 or not a.is_contiguous() or a.device != self.device:
+            a = a.to(device=self.device, dtype=torch.int32).contiguous()
+        assert tuple(a.shape) == (self.n_envs, self.P, abi.N_ACTION_HEADS)
+        ids = env_ids
+        if ids.dtype != torch.int32 or ids.device != self.device or not ids.is_contiguous():
+            raise ValueError("env_ids must be a contiguous int32 tensor on the engine's device")
+        with torch.cuda.device(self.device):
+            check(lib().nmmo_step_envs(self.h, self._ptr(ids), ids.numel(), self._ptr(a),
+                                       self._ptr(self.obs if write_obs else None), self._ptr(self.rew),
+                                       self._ptr(self.term), self._ptr(self.trunc), self._ptr(self.mask),
+                                       self._stream()), "nmmo_step_envs")
+        self._ids = ids  # alive until the stream has read it
+        return self.obs, self.rew, self.term, self.trunc, self.mask
+
     def observe(self, out=None):
         """The obs gather alone over the current state into `out` (default: the engine's obs
         buffer): step(write_obs=False) + observe() == step() (nmmo_observe)."""
@@ -215,6 +246,23 @@ class NmmoEngine:
         f = ctypes.c_int32()
         check(lib().nmmo_get_fault(self.h, ctypes.byref(f)), "nmmo_get_fault")
         return f.value
+
+    def check_fault(self, where: str = ""):
+        """Raise TickFault when a launch since the last read hit a loop bound (reads and clears
+        the word; synchronous). Called at every host sync of the product paths."""
+        f = self.get_fault()
+        if f:
+            raise TickFault(f, where)
+
+    def fault_into(self, dst):
+        """Enqueue: dst (device int32 [1]) takes the fault word if it is non-zero and dst is 0
+        (nmmo_fault_into; no sync, graph-capturable)."""
+        with torch.cuda.device(self.device):
+            check(lib().nmmo_fault_into(self.h, self._ptr(dst), self._stream()), "nmmo_fault_into")
+
+    def inject_fault(self, word: int):
+        """Test hook (nmmo_inject_fault): set the fault word."""
+        check(lib().nmmo_inject_fault(self.h, int(word)), "nmmo_inject_fault")
 
     def read_timing(self):
         """(tick_ms_sum, obs_ms_sum, n_steps, wrapper_ms_sum) from HIP events on the launch stream."""

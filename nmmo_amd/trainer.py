@@ -139,6 +139,7 @@ class DeviceTrainer:
             eng.step(actions.to(torch.int32).view(eng.n_envs, eng.P, -1))
         torch.cuda.synchronize(self.device)
         elapsed = time.perf_counter() - t0
+        eng.check_fault("DeviceTrainer.evaluate")  # the batch boundary: no faulted tick reaches train()
         agent_steps = int(agent_steps.item())
         self.agent_step += agent_steps
         self.global_step += padded

@@ -10,8 +10,15 @@ Protocol 2 — what `reinforcement_learning/clean_pufferl.py` consumes:
     o, r, d, t, infos, env_id, mask = pool.recv()                          # :293
     pool.send(actions)                                                     # :357
     pool.close()                                                           # :563
-Differences by design: all envs step in lockstep on the GPU, so `envs_per_batch` is every env
-of the pool and `recv` returns device tensors for the observations (the trainer's
+The async env pool of the reference's default config (`num_envs: 15, envs_per_batch: 6,
+env_pool: True`, config.yaml:35-38) is served with a fixed ready order (SPEC §14): envs become
+ready in the order they were sent, i.e. a FIFO queue that `async_reset` fills with 0..num_envs-1;
+`recv` pops the first `envs_per_batch` envs and returns their `envs_per_batch * 128` rows, with
+`env_id` the agent slots `env * 128 + agent` of those envs (clean_pufferl.py:158,310-315,346);
+`send` steps exactly those envs (nmmo_step_envs: one launch over the listed envs, the others keep
+their state) and appends them to the queue. That is the order a pufferlib pool of equally fast
+workers produces; with `envs_per_batch == num_envs` it is plain lockstep.
+Differences by design: `recv` returns device tensors for the observations (the trainer's
 `torch.as_tensor(o).to(device)` at :302,318 is then a no-op instead of an H2D copy); `mask` is a
 host numpy bool array because the trainer combines it with host arrays (:306,334).
 
@@ -21,6 +28,9 @@ observations (the unflattened layout) like `nmmo.Env`, for wrappers such as
 """
 
 from __future__ import annotations
+
+import collections
+import ctypes
 
 import numpy as np
 import torch
@@ -85,31 +95,68 @@ def _config_from_kwargs(env_kwargs) -> Config:
     return Config()
 
 
+def _as_dict(ns) -> dict:
+    """The reward_wrapper kwargs: a dict, or the pufferlib.namespace train.py builds (:105,209)."""
+    if ns is None:
+        return {}
+    if isinstance(ns, dict):
+        return dict(ns)
+    return dict(vars(ns))
+
+
+def agent_from_creator(env_creator):
+    """The agent whose RewardWrapper `environment.make_env_creator(reward_wrapper_cls=...)`
+    closed over (environment.py:50-58, train.py:226): `agent_zoo.<agent>.reward_wrapper` ->
+    "<agent>" (None when env_creator is not such a closure). A Syllabus creator
+    (syllabus_wrapper.make_syllabus_env_creator) is refused: curricula run on the device through
+    NmmoEngine.set_curriculum instead."""
+    cells = getattr(env_creator, "__closure__", None) or ()
+    names = getattr(getattr(env_creator, "__code__", None), "co_freevars", ())
+    agent = None
+    for name, cell in zip(names, cells):
+        try:
+            v = cell.cell_contents
+        except ValueError:
+            continue
+        if name == "syllabus" and v is not None:
+            raise ValueError("a Syllabus env_creator: use NmmoEngine.set_curriculum on the pool's engine")
+        mod = getattr(v, "__module__", "") or ""
+        if isinstance(v, type) and mod.startswith("agent_zoo."):
+            agent = mod.split(".")[1]
+    return agent
+
+
 class GpuVecEnv:
-    """pufferlib-0.7.3 pool protocol over one NmmoEngine (all envs in lockstep on one GPU)."""
+    """pufferlib-0.7.3 pool protocol over one NmmoEngine: lockstep (envs_per_batch == num_envs)
+    or the async env pool (envs_per_batch < num_envs) with the FIFO ready order of SPEC §14."""
 
     def __init__(self, env_creator=None, env_kwargs=None, num_envs=1, envs_per_worker=1,
                  envs_per_batch=None, env_pool=False, mask_agents=True, *, config=None,
                  device=None, seed=0, task_embedding=None, env_index_base=0, agent=None):
-        del env_creator, envs_per_worker, env_pool  # the engine replaces workers and creators
+        del envs_per_worker  # the engine replaces workers
         self.config = config or _config_from_kwargs(env_kwargs)
+        rw = _as_dict(env_kwargs.get("reward_wrapper")) if isinstance(env_kwargs, dict) else {}
+        if config is None and "early_stop_agent_num" in rw:  # BaseStatWrapper's early stop (stat_wrapper.py:68-69)
+            self.config.early_stop_agent_num = int(rw["early_stop_agent_num"])
+        if agent is None:  # env_creator's RewardWrapper (environment.py:58), when it names one
+            agent = agent_from_creator(env_creator)
         if self.config.obs_layout != abi.OBS_FLAT:
             raise ValueError("GpuVecEnv serves flat observations (obs_layout=OBS_FLAT)")
         self.num_envs = int(num_envs)
-        if envs_per_batch not in (None, self.num_envs):
-            # lockstep GPU stepping: one batch = every env. clean_pufferl sizes its buffers from
-            # pool.envs_per_batch (clean_pufferl.py:116-119), so a caller asking for async
-            # sub-batches would silently get another batch shape: refuse instead.
-            raise ValueError(f"GpuVecEnv steps every env in lockstep: envs_per_batch must be None or "
-                             f"num_envs ({self.num_envs}), got {envs_per_batch}; run several pools for "
-                             f"env batches")
-        self.envs_per_batch = self.num_envs
+        epb = self.num_envs if envs_per_batch is None else int(envs_per_batch)
+        if not 1 <= epb <= self.num_envs:
+            raise ValueError(f"envs_per_batch must be in 1..num_envs ({self.num_envs}), got {envs_per_batch}")
+        if not env_pool and self.num_envs % epb:
+            # without the env pool, pufferlib steps fixed batches of envs_per_batch envs
+            raise ValueError(f"num_envs ({self.num_envs}) must be a multiple of envs_per_batch ({epb}) "
+                             f"unless env_pool=True")
+        self.envs_per_batch = epb
+        self.env_pool = bool(env_pool)
         self.mask_agents = mask_agents
         self.engine = NmmoEngine(self.config, self.num_envs, seed=seed, device=device,
                                  task_embedding=task_embedding, env_index_base=env_index_base)
         # env_creator's RewardWrapper (environment.py:58) with the YAML reward_wrapper kwargs,
         # run on the device (SPEC §13); agent=None keeps the bare env
-        rw = dict((env_kwargs or {}).get("reward_wrapper", {})) if isinstance(env_kwargs, dict) else {}
         self.stat_prefix = rw.get("stat_prefix")
         if agent is not None:
             from .wrappers import wrapper_config
@@ -119,10 +166,15 @@ class GpuVecEnv:
         self.driver_env = DriverEnv(self.config, self.engine.obs_elems)
         self.single_observation_space = self.driver_env.single_observation_space
         self.single_action_space = self.driver_env.single_action_space
-        self.env_id = np.arange(self.num_envs * self.agents_per_env)
         self._seed = seed
         self.env_index_base = int(env_index_base)
-        self._ready = False
+        self._ready: collections.deque | None = None  # envs whose outputs await recv, in ready order
+        self._batch: list | None = None               # envs returned by the last recv, awaiting send
+        P, d = self.agents_per_env, self.engine.device
+        if epb < self.num_envs:  # batch-shaped outputs for batches that wrap around the env range
+            self._obs_b = torch.empty((epb, P, self.engine.obs_elems), dtype=torch.float32, device=d)
+            self._ids_host = torch.empty(epb, dtype=torch.int32).pin_memory()
+            self._ids = torch.empty(epb, dtype=torch.int32, device=d)
 
     # -- protocol
     def async_reset(self, seed=None):
@@ -130,44 +182,80 @@ class GpuVecEnv:
             self.engine.reset(reset_seeds(seed, self.env_index_base, self.num_envs))
         else:
             self.engine.reset()
-        self._ready = True
+        self._ready = collections.deque(range(self.num_envs))
+        self._batch = None
 
     def recv(self):
-        if not self._ready:
-            raise RuntimeError("recv() before async_reset()/send()")
-        e = self.engine
-        N = self.num_envs * self.agents_per_env
-        o = e.obs.view(N, e.obs_elems)
-        r = e.rew.view(N)
-        d = e.term.view(N)
-        t = e.trunc.view(N)
-        mask = e.mask.view(N).to(torch.bool).cpu().numpy()
-        self._ready = False
-        return o, r, d, t, self._infos(), self.env_id, mask
+        if self._ready is None:
+            raise RuntimeError("recv() before async_reset()")
+        if self._batch is not None:
+            raise RuntimeError("recv() twice without send(): the batch it returned is still out")
+        k, P, e = self.envs_per_batch, self.agents_per_env, self.engine
+        batch = [self._ready.popleft() for _ in range(k)]
+        self._batch = batch
+        N = k * P
+        lo = batch[0]
+        if batch == list(range(lo, lo + k)):  # contiguous envs: views of the engine's buffers
+            sl = slice(lo, lo + k)
+            o = e.obs[sl].view(N, e.obs_elems)
+            r, d, t, m = (x[sl].reshape(N) for x in (e.rew, e.term, e.trunc, e.mask))
+        else:  # the batch wraps around: gather its env rows (nmmo_gather_rows)
+            idx = torch.as_tensor(batch, dtype=torch.int32).to(e.device)
+            row_bytes = P * e.obs_elems * 4
+            from ._native import check, lib
 
-    def _infos(self):
-        """Per env {agent_id: info} of the agents whose episode ended this step (BaseStatWrapper's
-        info dicts, stat_wrapper.py:128-185); empty dicts without the wrapper layer. Only the
-        records of finished agents cross to the host."""
+            with torch.cuda.device(e.device):
+                check(lib().nmmo_gather_rows(ctypes.c_void_p(e.obs.data_ptr()), row_bytes,
+                                             ctypes.c_void_p(idx.data_ptr()), k,
+                                             ctypes.c_void_p(self._obs_b.data_ptr()),
+                                             ctypes.c_void_p(torch.cuda.current_stream(e.device).cuda_stream)),
+                      "nmmo_gather_rows")
+            o = self._obs_b.view(N, e.obs_elems)
+            il = idx.long()
+            r, d, t, m = (x.index_select(0, il).reshape(N) for x in (e.rew, e.term, e.trunc, e.mask))
+        mask = m.to(torch.bool).cpu().numpy()  # the host sync of this step
+        e.check_fault("GpuVecEnv.recv")
+        env_id = (np.asarray(batch, np.int64)[:, None] * P + np.arange(P)).reshape(-1)
+        return o, r, d, t, self._infos(batch), env_id, mask
+
+    def _infos(self, batch):
+        """Per env of the batch {agent_id: info} of the agents whose episode ended this step
+        (BaseStatWrapper's info dicts, stat_wrapper.py:128-185); empty dicts without the wrapper
+        layer. Only the records of finished agents cross to the host."""
         e = self.engine
         if e.info is None:
-            return [{} for _ in range(self.num_envs)]
+            return [{} for _ in batch]
         from .wrappers import infos_from_records
 
-        done = (e.term | e.trunc).view(-1).nonzero().view(-1)
-        recs = np.zeros((self.num_envs, self.agents_per_env), abi.agent_info_dtype())
+        il = torch.as_tensor(batch, dtype=torch.long, device=e.device)
+        done = (e.term.index_select(0, il) | e.trunc.index_select(0, il)).view(-1).nonzero().view(-1)
+        recs = np.zeros((len(batch), self.agents_per_env), abi.agent_info_dtype())
         if done.numel():
-            rows = e.info.view(-1, e.info.shape[-1]).index_select(0, done).cpu().numpy()
+            info = e.info.index_select(0, il)
+            rows = info.view(-1, info.shape[-1]).index_select(0, done).cpu().numpy()
             idx = done.cpu().numpy()
             recs.reshape(-1)[idx] = rows.view(abi.agent_info_dtype()).reshape(-1)
         return infos_from_records(recs, stat_prefix=self.stat_prefix)
 
     def send(self, actions):
+        if self._batch is None:
+            raise RuntimeError("send() without a recv() batch to step")
+        batch, k, P, e = self._batch, self.envs_per_batch, self.agents_per_env, self.engine
         a = torch.as_tensor(actions)
-        a = a.to(device=self.engine.device, dtype=torch.int32).reshape(
-            self.num_envs, self.agents_per_env, abi.N_ACTION_HEADS)
-        self.engine.step(a)
-        self._ready = True
+        a = a.to(device=e.device, dtype=torch.int32).reshape(k, P, abi.N_ACTION_HEADS)
+        if k == self.num_envs:  # lockstep (every recv returns 0..num_envs-1 in order)
+            e.step(a)
+        else:
+            lo = batch[0]
+            if batch == list(range(lo, lo + k)):
+                e.actions[lo:lo + k].copy_(a)
+            else:
+                e.actions.index_copy_(0, torch.as_tensor(batch, dtype=torch.long, device=e.device), a)
+            self._ids_host.copy_(torch.as_tensor(batch, dtype=torch.int32))
+            self._ids.copy_(self._ids_host, non_blocking=True)
+            e.step_envs(self._ids)
+        self._ready.extend(batch)
+        self._batch = None
 
     def close(self):
         self.engine.close()

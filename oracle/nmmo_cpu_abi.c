@@ -25,6 +25,8 @@ int oracle_end_episodes(void* h, const uint8_t* env_mask);
 int oracle_write_obs(void* h, int env, float* obs_env);
 int oracle_step(void* h, const int32_t* actions, float* obs, float* rew, uint8_t* term, uint8_t* trunc,
                 uint8_t* mask);
+int oracle_step_range(void* h, int env_lo, int env_hi, const int32_t* actions, float* obs, float* rew,
+                      uint8_t* term, uint8_t* trunc, uint8_t* mask);
 int oracle_scripted_actions(void* h, uint64_t pseed, int32_t* actions);
 int oracle_get_state(void* h, void* buf, size_t nbytes);
 int oracle_set_state(void* h, const void* buf, size_t nbytes);
@@ -40,6 +42,7 @@ struct NmmoHandle {
   NmmoConfig cfg;
   NmmoLayout layout;
   int n_envs;
+  int32_t fault;  /* nmmo_step_envs' dropped ids, nmmo_inject_fault */
 };
 
 static _Thread_local char g_err[512];
@@ -166,6 +169,27 @@ NMMO_API int nmmo_step(NmmoHandle* h, const int32_t* actions, void* obs, float* 
   return oracle_step(h->o, actions, flat_or_null(h, obs), rew, term, trunc, mask);
 }
 
+/* host env_ids; the listed envs step in list order (envs are independent, so any order gives the
+ * same state) */
+NMMO_API int nmmo_step_envs(NmmoHandle* h, const int32_t* env_ids, int32_t n_ids, const int32_t* actions, void* obs,
+                            float* rew, uint8_t* term, uint8_t* trunc, uint8_t* mask, void* stream) {
+  (void)stream;
+  if (!h || !env_ids) return fail(NMMO_E_INVALID, "null handle / env_ids");
+  if (n_ids < 0 || n_ids > h->n_envs) return fail(NMMO_E_INVALID, "n_ids %d not in 0..%d", n_ids, h->n_envs);
+  if (!actions || !rew || !term || !trunc || !mask)
+    return fail(NMMO_E_INVALID, "actions/rew/term/trunc/mask must be host pointers");
+  for (int i = 0; i < n_ids; i++) {
+    const int e = env_ids[i];
+    if (e < 0 || e >= h->n_envs) {
+      if (!h->fault) h->fault = NMMO_FAULT_ENV_LIST | i << 8;
+      continue;
+    }
+    int rc = oracle_step_range(h->o, e, e + 1, actions, flat_or_null(h, obs), rew, term, trunc, mask);
+    if (rc) return rc;
+  }
+  return NMMO_OK;
+}
+
 NMMO_API int nmmo_observe(NmmoHandle* h, void* obs, void* stream) {
   (void)stream;
   if (!h || !obs) return fail(NMMO_E_INVALID, "null argument");
@@ -273,7 +297,19 @@ NMMO_API int nmmo_read_timing(NmmoHandle* h, double* ms, int32_t* n) {
 }
 NMMO_API int nmmo_get_fault(NmmoHandle* h, int32_t* fault) {  /* the serial oracle has no round loops */
   if (!h || !fault) return fail(NMMO_E_INVALID, "null argument");
-  *fault = 0;
+  *fault = h->fault;
+  h->fault = 0;
+  return NMMO_OK;
+}
+NMMO_API int nmmo_fault_into(NmmoHandle* h, int32_t* dst, void* stream) {  /* host dst */
+  (void)stream;
+  if (!h || !dst) return fail(NMMO_E_INVALID, "null argument");
+  if (h->fault && !*dst) *dst = h->fault;
+  return NMMO_OK;
+}
+NMMO_API int nmmo_inject_fault(NmmoHandle* h, int32_t fault) {
+  if (!h) return fail(NMMO_E_INVALID, "null handle");
+  h->fault = fault;
   return NMMO_OK;
 }
 NMMO_API int nmmo_set_counters(NmmoHandle* h, uint64_t* c) {

@@ -6,7 +6,11 @@ rank 0 decodes every gathered buffer (its own in place, the peer's received) int
 layout and stores the learner-mask rows of every step into a DeviceExperience straight from the
 wire records, then writes per step and global env the sha256 of the native obs and of the
 reward / term / trunc / mask bytes, plus digests of the experience buffers, to argv[1] (JSON).
-The test compares them with one engine stepping all envs alone. Not collected by pytest."""
+The test compares them with one engine stepping all envs alone. argv[2] = "eager" (per-step
+episode ends on each batch's stream, graphs=False) or "graphs" (the bench's mode: each (batch,
+ring slot) replayed from its hipGraph, the 3-slot ring reused across steps with cross-stream done
+events; episode phases staggered by the pre-roll only and ended by a short horizon). Not
+collected by pytest."""
 
 import hashlib
 import json
@@ -18,6 +22,11 @@ sys.path.insert(0, ROOT)
 
 # shared with the test's one-engine reference run
 N_PER_BATCH, BATCHES, SEED, PSEED, PREROLL, TICKS, MAP_N = 3, 2, 11, 77, 36, 18, 8
+
+
+def horizon(mode):
+    """graphs mode has no per-step episode ends: a horizon inside the checked window ends them"""
+    return 40 if mode == "graphs" else 1024
 
 
 def end_mask(ids, t):
@@ -45,13 +54,14 @@ def main():
     from nmmo_amd.storage import DeviceExperience
 
     out_path = sys.argv[1]
+    mode = sys.argv[2] if len(sys.argv) > 2 else "eager"
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
     dist.init_process_group("gloo")
     n, nb = N_PER_BATCH, BATCHES
     envs = n * nb
-    cfg = Config.preset("C4", MAP_N=MAP_N, early_stop_agent_num=8, obs_layout=abi.OBS_WIRE)
+    cfg = Config.preset("C4", MAP_N=MAP_N, early_stop_agent_num=8, obs_layout=abi.OBS_WIRE, HORIZON=horizon(mode))
     engs = [NmmoEngine(cfg, n, seed=SEED, device=dev, env_index_base=rank * envs + j * n) for j in range(nb)]
     P = engs[0].P
     for e in engs:
@@ -83,8 +93,9 @@ def main():
             x.store(w, rew, sm3[..., 4].reshape(-1), sm3[..., 6].reshape(-1), torch.zeros((n * P, 12), dtype=torch.int32),
                     z, z, step=s + 1, env_id_base=base * P, engine=engs[0])
 
-    g = WireGather(engs, PSEED, rank, world, graphs=False, on_step=on_step if rank == 0 else None,
-                   before_step=before, backend="gloo")
+    graphs = mode == "graphs"
+    g = WireGather(engs, PSEED, rank, world, graphs=graphs, on_step=on_step if rank == 0 else None,
+                   before_step=None if graphs else before, backend="gloo")
     for _ in range(TICKS):
         g.step()
     g.drain()

@@ -90,3 +90,28 @@ def test_val_attributes_and_task_fields():
     assert ts[0].completed is False and ts[0].reward_signal_count == 0 and ts[0]._max_progress == 0.0
     assert set(ts[0].progress_info) == {"max_progress", "completed_tick"}
     assert isinstance(realm.event_log, EventLog)
+
+
+def test_agent_from_env_creator_closure():
+    """GpuVecEnv picks the device RewardWrapper from the class environment.make_env_creator
+    closed over (environment.py:50-58, train.py:226), so the default train.py needs no extra
+    argument; a Syllabus creator is refused (curricula go through set_curriculum)."""
+    import pytest
+
+    from nmmo_amd.vecenv import _as_dict, agent_from_creator
+
+    def make_env_creator(reward_wrapper_cls, syllabus_wrapper=False, syllabus=None):  # environment.py:50
+        def env_creator(*args, **kwargs):
+            return reward_wrapper_cls, syllabus_wrapper, syllabus
+        return env_creator
+
+    RW = type("RewardWrapper", (), {"__module__": "agent_zoo.takeru.reward_wrapper"})
+    assert agent_from_creator(make_env_creator(RW)) == "takeru"
+    assert agent_from_creator(make_env_creator(type("X", (), {}))) is None
+    assert agent_from_creator(None) is None
+    with pytest.raises(ValueError, match="Syllabus"):
+        agent_from_creator(make_env_creator(RW, syllabus=object()))
+    from types import SimpleNamespace
+
+    assert _as_dict(SimpleNamespace(eval_mode=False, early_stop_agent_num=8)) == {
+        "eval_mode": False, "early_stop_agent_num": 8}

@@ -56,7 +56,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _reference(world):
+def _reference(world, mode="eager"):
     """One NATIVE-obs engine over all world x envs envs, the worker's schedule."""
     import numpy as np
     import torch
@@ -68,7 +68,8 @@ def _reference(world):
     from tests import _c5_worker as w
 
     N = world * w.N_PER_BATCH * w.BATCHES
-    cfg = Config.preset("C4", MAP_N=w.MAP_N, early_stop_agent_num=8, obs_layout=abi.OBS_NATIVE)
+    cfg = Config.preset("C4", MAP_N=w.MAP_N, early_stop_agent_num=8, obs_layout=abi.OBS_NATIVE,
+                        HORIZON=w.horizon(mode))
     eng = NmmoEngine(cfg, N, seed=w.SEED)
     P = eng.P
     eng.reset()
@@ -83,7 +84,8 @@ def _reference(world):
     cnt = torch.zeros(3, dtype=torch.int64, device=eng.device)
     eng.set_counters(cnt)
     for t in range(w.TICKS):
-        eng.end_episodes(w.end_mask(ids, t))
+        if mode == "eager":
+            eng.end_episodes(w.end_mask(ids, t))
         eng.scripted_actions(w.PSEED)
         eng.step()
         small = torch.cat([eng.rew.view(torch.uint8).view(N, P, 4), eng.term[..., None], eng.trunc[..., None],
@@ -102,16 +104,20 @@ def _reference(world):
     return rec
 
 
-def test_c5_gather_content_matches_one_rank(tmp_path):
+@pytest.mark.parametrize("mode", ["eager", "graphs"])
+def test_c5_gather_content_matches_one_rank(tmp_path, mode):
+    """eager: per-step episode ends, WireGather(graphs=False). graphs: the mode bench.py times —
+    every (batch, ring slot) replayed from its hipGraph, ring slots reused every 3 steps behind
+    cross-stream done events — with episodes ended by a horizon inside the checked window."""
     out = tmp_path / "c5.json"
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
-           os.path.join(ROOT, "tests", "_c5_worker.py"), str(out)]
+           os.path.join(ROOT, "tests", "_c5_worker.py"), str(out), mode]
     env = dict(os.environ, OMP_NUM_THREADS="1")
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=110, env=env)
     assert p.returncode == 0, p.stderr[-3000:]
     got = json.loads(out.read_text())
-    ref = _reference(2)
+    ref = _reference(2, mode)
     assert got["status"] == 0
     assert ref["episodes"] > 0  # episodes ended (and auto-reset) inside the checked window
     assert set(got["native"]) == set(ref["native"]) and len(ref["native"]) == 18 * 12

@@ -339,7 +339,43 @@ def test_task_parity_all_predicates():
     assert (st["signals"] > 0).mean() > 0.15 and (st["completed_tick"] > 0).any()
 
 
-def pathing_scenario(n=4):
+def test_can_see_tile_regrowth_parity_without_npc():
+    """CanSeeTile(Foilage) on the Resource-only system set (no NPC spawn barrier): the rewards read
+    the tiles the respawn regrows from Scrub in the same tick (tick.hip DevState::tmap barrier).
+    Most Foilage starts eaten, so windows gain and lose their Foilage tick to tick."""
+    import torch
+
+    from nmmo_amd import tasks as T
+    from oracle.oracle import join_state
+
+    n, steps = 4, 60
+    cfg = Config.preset("C2", MAP_N=4, early_stop_agent_num=0)
+    tl = [T.task("CanSeeTile", tile_type="Foilage"), T.task("TickGE", num_tick=30)]
+    assign = np.zeros((n, 128), np.int32)
+    assign[:, 1::7] = 1
+    orc = OracleEnvs(cfg, n, seed=29)
+    orc.set_tasks(tl, None, assign)
+    orc.reset()
+    d = split_state(orc.get_state(), n, orc.S, orc.P)
+    rng = np.random.default_rng(3)
+    for e in range(n):
+        rr, cc = np.nonzero(d["mat"][e] == 4)  # Foilage -> Scrub (depleted, regrows at p = 0.025)
+        pick = rng.random(rr.size) < 0.9
+        d["mat"][e, rr[pick], cc[pick]] = 3
+    orc.set_state(join_state(d))
+    eng = _engine(cfg, n, seed=0)
+    eng.set_tasks(tl, None, assign)
+    eng.set_state(orc.get_state())
+    flips = 0
+    for t in range(steps):
+        acts = orc.scripted_actions(40 + t)
+        orc.step(acts)
+        eng.step(torch.from_numpy(acts).cuda())
+        torch.cuda.synchronize()
+        _cmp_state(eng.get_state(), orc.get_state(), n, eng.S, f"CanSeeTile step {t}")
+        assert np.array_equal(eng.rew.cpu().numpy(), orc.rew), f"rewards @ {t}"
+        flips += int((orc.rew[assign == 0] != 0).sum())  # Foilage came into / went out of view
+    assert flips > 20, flips
     """SPEC §6 v2 window BFS under stress: in every env, hostile NPCs are put 2-7 tiles from live
     players and stone walls are scattered around them, so most hunts path around obstacles (and
     some targets are unreachable inside the window: greedy fallback). HIP vs oracle, bit-exact."""

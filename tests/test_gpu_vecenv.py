@@ -165,3 +165,95 @@ def test_realm_read_once_per_tick():
             walk_stat_wrapper_reads(env.realm, env.agent_task_map, a, terminated=False)
         assert len(calls) == 1, f"tick {t}: {len(calls)} state copies"
     env.close()
+
+
+def test_async_pool_15_6_clean_pufferl_loop_matches_oracle_per_env():
+    """The reference's default pool (config.yaml:35-38: num_envs 15, envs_per_batch 6,
+    env_pool True) driven in clean_pufferl.evaluate's order (recv -> per-slot state indexed by
+    env_id -> policy -> store -> send, clean_pufferl.py:287-357): the FIFO ready order of SPEC §14,
+    env_id = the batch envs' agent slots, and every env's trajectory bit-equal to the oracle
+    stepping that env alone on the same action stream (auto-resets included)."""
+    import collections
+
+    import torch
+
+    from nmmo_amd.vecenv import GpuVecEnv, reset_seeds
+    from oracle.oracle import OracleEnvs
+
+    n, k, P = 15, 6, 128
+    cfg = Config.preset("C4", MAP_N=4, early_stop_agent_num=8, HORIZON=12)
+    pool = GpuVecEnv(None, env_kwargs=None, num_envs=n, envs_per_worker=1, envs_per_batch=k,
+                     env_pool=True, mask_agents=True, config=cfg, seed=5)
+    assert pool.envs_per_batch == k and pool.agents_per_env == P
+    ref = OracleEnvs(cfg, n, seed=5)
+    pool.async_reset(1)
+    ref.reset(env_seeds=reset_seeds(1, 0, n))
+    order = collections.deque(range(n))
+    lstm = np.zeros(n * P, np.int64)  # per-slot recurrent state, indexed by env_id (:310-315)
+    stored = collections.Counter()     # sort keys (env_id, step) of stored rows (:346)
+    full = np.zeros((n, P, 12), np.int32)
+    steps = np.zeros(n, np.int64)
+    for step in range(1, 46):
+        o, r, d, t, infos, env_id, mask = pool.recv()
+        batch = [order.popleft() for _ in range(k)]
+        assert np.array_equal(env_id, (np.array(batch)[:, None] * P + np.arange(P)).reshape(-1))
+        assert o.shape == (k * P, 23987) and len(infos) == k and mask.shape == (k * P,)
+        assert np.array_equal(o.cpu().numpy(), ref.obs[batch].reshape(k * P, -1)), f"obs @ recv {step}"
+        for name, x in (("rew", r), ("term", d), ("trunc", t)):
+            assert np.array_equal(x.cpu().numpy(), getattr(ref, name)[batch].reshape(-1)), f"{name} @ {step}"
+        assert np.array_equal(mask, ref.mask[batch].reshape(-1).astype(bool))
+        lstm[env_id] += 1
+        for i in np.flatnonzero(mask):
+            stored[(int(env_id[i]), step)] += 1
+        acts = ref.scripted_actions(300 + step)[batch]          # the policy's sample for this batch
+        pool.send(acts.reshape(-1, 12).astype(np.int64))        # clean_pufferl sends int64 numpy
+        for j, e in enumerate(batch):
+            full[e] = acts[j]
+            ref.step_range(e, e + 1, full)
+        order.extend(batch)
+        steps[batch] += 1
+    torch.cuda.synchronize()
+    assert np.array_equal(pool.engine.get_state(), ref.get_state())
+    assert np.array_equal(lstm.reshape(n, P), np.repeat(steps[:, None], P, axis=1))
+    assert max(s for _, s in stored) == 45 and len(stored) > 1000
+    eps = ref.get_state().reshape(n, -1)[:, :64].copy().view(np.int32)[:, 3]  # E_EPISODE
+    assert (eps >= 1).all()  # every env auto-reset at least once (HORIZON 12, 18 steps each)
+    assert pool.engine.get_fault() == 0
+    pool.close()
+
+
+def test_pool_fault_word_raises_at_recv():
+    """A tick fault (nmmo_get_fault) surfaces at recv's host sync instead of feeding a learner."""
+    from nmmo_amd.engine import TickFault
+    from nmmo_amd.vecenv import GpuVecEnv
+
+    cfg = Config.preset("C3", MAP_N=2)
+    cfg.obs_layout = 1
+    pool = GpuVecEnv(None, num_envs=4, envs_per_batch=2, env_pool=True, config=cfg, seed=1)
+    pool.async_reset(3)
+    o, r, d, t, infos, env_id, mask = pool.recv()
+    pool.send(np.zeros((2 * 128, 12), np.int64))
+    pool.engine.inject_fault(1 | 3 << 8)
+    with pytest.raises(TickFault, match="attack rounds"):
+        pool.recv()
+    pool.close()
+
+
+def test_step_envs_drops_bad_ids_and_records_them():
+    """nmmo_step_envs with an id outside the handle: that id is dropped (no out-of-range access),
+    the listed valid env steps, and the fault word names the list position."""
+    import torch
+
+    from nmmo_amd.engine import NmmoEngine
+
+    cfg = Config.preset("C2", MAP_N=2)
+    eng = NmmoEngine(cfg, 3, seed=4)
+    eng.reset()
+    before = eng.get_state().reshape(3, -1)[:, :4].copy().view(np.int32)[:, 0]
+    ids = torch.tensor([2, 7], dtype=torch.int32, device=eng.device)
+    eng.step_envs(ids)
+    torch.cuda.synchronize()
+    after = eng.get_state().reshape(3, -1)[:, :4].copy().view(np.int32)[:, 0]
+    assert before.tolist() == [0, 0, 0] and after.tolist() == [0, 0, 1]
+    assert eng.get_fault() == 5 | 1 << 8
+    eng.close()

@@ -7,6 +7,7 @@ import os
 import socket
 
 import numpy as np
+import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
@@ -175,3 +176,58 @@ def test_wire_gather_protocol_gloo():
         p.join(timeout=300)
         assert p.exitcode == 0
     assert q.get(timeout=10)
+
+
+def _fail_worker(rank, world, port, q, mode):
+    """Rank 1 announces a tick fault word (mode "fault") or an impossible wire size (mode
+    "size") for step 1; every rank must raise at payload(1), before posting its transfers."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from nmmo_amd import distributed as nd
+    from nmmo_amd.engine import TickFault
+
+    n, ring = 2, 3
+    P = Config.preset("C4").PLAYER_N
+    cap = owire.header_bytes(n, P) + n * (P * 9552 + abi.NATIVE_MARKET_BYTES)
+    x = nd.WireExchange(world, rank, 1, [cap], [n * P * 8], torch.device("cpu"), ring=ring, backend="gloo")
+    wires = [torch.zeros(cap, dtype=torch.uint8) for _ in range(ring)]
+    smalls = [torch.zeros(n * P * 8, dtype=torch.uint8) for _ in range(ring)]
+    outcome = "no error"
+    try:
+        for t in range(3):
+            w, sm, _ = _step_bytes(rank, t, n)
+            wires[t % ring][:w.nbytes] = torch.from_numpy(w)
+            smalls[t % ring][:] = torch.from_numpy(sm)
+            fault = torch.zeros(1, dtype=torch.int32)
+            if rank == 1 and t == 1:
+                if mode == "fault":
+                    fault[0] = 1 | 5 << 8
+                else:
+                    wires[t % ring][:8] = torch.tensor([cap + 1], dtype=torch.int64).view(torch.uint8)
+            if t >= 1:
+                x.post_payload(t - 1, [wires[(t - 1) % ring]], [smalls[(t - 1) % ring]])
+            x.post_sizes(t, [wires[t % ring]], fault=fault)
+            assert not fault.any()  # zeroed once shipped
+        x.post_payload(2, [wires[2]], [smalls[2]])
+    except TickFault as err:
+        outcome = f"TickFault {err.code} {err.env} step1={'step 1' in str(err)}"
+    except RuntimeError as err:
+        outcome = f"RuntimeError step1={'step 1' in str(err)}"
+    q.put((rank, outcome))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["fault", "size"])
+def test_wire_gather_fails_on_both_ends_without_hanging(mode):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_fail_worker, args=(r, 2, port, q, mode)) for r in range(2)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(timeout=300)
+        assert p.exitcode == 0
+    got = dict(q.get(timeout=10) for _ in range(2))
+    want = "TickFault 1 5 step1=True" if mode == "fault" else "RuntimeError step1=True"
+    assert got == {0: want, 1: want}
