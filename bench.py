@@ -21,8 +21,9 @@ headline is configs[4] = C5: 1024 envs per GPU (8192 on 8), every rank's observa
 reward / dones / mask gathered into rank 0 every step (RCCL point-to-point over xGMI, wire
 records, nmmo_amd.distributed.WireGather), with gather-free C4 as the extra. C5 reports
 "delivered" (value: every agent's observation landed and validated in rank 0's HBM in the form
-the experience store decodes its kept rows from) and "decoded" (rank 0 also decodes every
-rank's buffers into the native layout each step).
+the experience store decodes its kept rows from), "stored" (rank 0 also stores every row of
+every step as experience: compact record storage, nmmo_exp_store_records) and "decoded" (rank 0
+also decodes every rank's buffers into the native layout each step).
 
 Steady state: envs start with staggered episode phases (`--stagger L`: during an untimed
 pre-roll of L ticks, the envs e = k mod L end their episode at pre-roll tick k, via
@@ -551,9 +552,10 @@ def _roofline(prof_name, kern, byts, ms, per, timing, nb, step_s, fill_gbs, pmc_
 def measure_gather(args, name, envs, rank, world, dev, steps, warmup, dist=None, backend="nccl"):
     """C5: the rank's envs as `--batches` wire-obs handles stepped by WireGather (policy +
     nmmo_step into a ring of wire buffers, hipGraph-captured, one stream per batch; the learner
-    gather into rank 0 one step behind on a comm stream). Two timed passes over the same
-    engines: "delivered" (rank 0 validates every received buffer on the device) and "decoded"
-    (rank 0 also decodes every rank's buffers into the native layout each step)."""
+    gather into rank 0 one step behind on a comm stream). Three timed passes over the same
+    engines: "delivered" (rank 0 validates every received buffer on the device), "stored" (rank 0
+    also stores every row of every step in compact record storage) and "decoded" (rank 0 also
+    decodes every rank's buffers into the native layout each step)."""
     import torch
 
     from nmmo_amd import abi
@@ -582,12 +584,24 @@ def measure_gather(args, name, envs, rank, world, dev, steps, warmup, dist=None,
         e.set_counters(c)
     torch.cuda.synchronize(dev)
     passes = {}
-    for decode in ((False,) if args.no_decode else (False, True)):
-        g = WireGather(engs, pseed, rank, world, decode=decode, graphs=not args.no_graph, backend=backend)
+    modes = ("delivered",) if args.no_decode else ("delivered", "stored", "decoded")
+    for mode in modes:
+        decode = mode == "decoded"
+        store = None
+        if mode == "stored" and rank == 0:  # compact record storage of every row of every step
+            from nmmo_amd.storage import DeviceExperience
+
+            rows = world * envs * cfg.PLAYER_N
+            store = DeviceExperience(rows, engs[0].obs_elems, rows, device=dev,
+                                     record_arena_bytes=world * nb * (nw.max_bytes(per, cfg.PLAYER_N) + 64))
+        g = WireGather(engs, pseed, rank, world, decode=decode, graphs=not args.no_graph, backend=backend,
+                       store=store)
         for _ in range(warmup):
             g.step()
         g.drain()
         torch.cuda.synchronize(dev)
+        if store is not None:
+            g.stored_rows()  # the warm-up's rows do not count
         for c in counters:
             c.zero_()
         b0 = g.x.payload_bytes
@@ -606,17 +620,21 @@ def measure_gather(args, name, envs, rank, world, dev, steps, warmup, dist=None,
         status = g.check_status()
         if status:
             raise RuntimeError(f"nmmo_wire_check flagged received wire buffers (status {status})")
-        _progress(f"{name}: timed {steps} steps in {elapsed:.3f} s (decode={decode})")
-        passes[decode] = {"elapsed": elapsed, "alive": float(tot[0].item()), "episodes": int(tot[1].item()),
-                          "events": float(tot[2].item()),
-                          "payload_bytes_per_step": (g.x.payload_bytes - b0) / steps}
+        stored = g.stored_rows() if store is not None else None
+        if store is not None and store.status:
+            raise RuntimeError(f"the root's record store dropped rows (status {store.status})")
+        _progress(f"{name}: timed {steps} steps in {elapsed:.3f} s ({mode})")
+        passes[mode] = {"elapsed": elapsed, "alive": float(tot[0].item()), "episodes": int(tot[1].item()),
+                        "events": float(tot[2].item()), "stored_rows": stored,
+                        "payload_bytes_per_step": (g.x.payload_bytes - b0) / steps}
         g.close()
+        del store
     eng = engs[0]
     tick_avg_ms, obs_avg_ms, _ = _kernel_timing(eng, pseed, steps)
     _check_faults(args, engs, name, world, dist, dev)
     wire_env_bytes = nw.total_bytes(eng.obs) / per  # this batch's last step: header + records
     S, P = eng.S, cfg.PLAYER_N
-    d = passes[False]
+    d = passes["delivered"]
     events_per_env_tick = d["events"] / (envs * steps)
     tick_b = tick_bytes_per_env(S, P, True, events_per_env_tick) * per
     obs_b = obs_bytes_per_env(S, P, eng.obs_elems, wire_bytes=wire_env_bytes) * per
@@ -640,7 +658,8 @@ def measure_gather(args, name, envs, rank, world, dev, steps, warmup, dist=None,
         "batches": nb,
         "gather_bytes": d["payload_bytes_per_step"] if world > 1 else 0,
         "wire_bytes_per_agent_in_realm": round(wire_env_bytes * per * nb * steps / max(d["alive"], 1.0), 1),
-        "decoded": passes.get(True),
+        "decoded": passes.get("decoded"),
+        "stored": passes.get("stored"),
     }
     for e in engs:
         e.close()
@@ -765,15 +784,27 @@ def main():
             return float(t_max.item()), float(sums[0].item()), float(sums[1].item())
         return res[key], res[alive], res["slots"]
 
+    def learner_passes(r, steps):
+        """The C5 line's learner-side passes (whole job, max over ranks): "stored" (rank 0 keeps
+        every row of every step in compact record storage) and "decoded"."""
+        out = {}
+        for mode, what in (("stored", "rank 0 also stores every rank's rows in the realm each step as "
+                                      "experience (nmmo_exp_store_records: the rows' fields + their wire "
+                                      "records in an arena, flat rows expanded per minibatch)"),
+                           ("decoded", "rank 0 also decodes every rank's wire buffers into the native layout "
+                                       "(nmmo_wire_unpack) each step: the full learner-ready obs tensor")):
+            if not r.get(mode):
+                continue
+            pr = dict(r, elapsed=r[mode]["elapsed"], alive=r[mode]["alive"])
+            el, al, _ = reduce(pr)
+            out[mode] = {"value": round(al / el, 1), "ms_per_step": round(el * 1e3 / steps, 4), "what": what}
+            if r[mode].get("stored_rows") is not None:
+                out[mode]["rows_stored_per_sec"] = round(r[mode]["stored_rows"] / el, 1)
+        return out
+
     res = run(name, args.obs, None, envs, args.steps, args.warmup)
     elapsed, alive_total, slots_total = reduce(res)
-    decoded = None
-    if res.get("decoded"):
-        dres = dict(res, elapsed=res["decoded"]["elapsed"], alive=res["decoded"]["alive"])
-        d_el, d_alive, d_slots = reduce(dres)
-        decoded = {"value": round(d_alive / d_el, 1), "ms_per_step": round(d_el * 1e3 / args.steps, 4),
-                   "what": "rank 0 also decodes every rank's wire buffers into the native layout "
-                           "(nmmo_wire_unpack) each step: the full learner-ready obs tensor"}
+    passes = learner_passes(res, args.steps) if res.get("gather") else {}
 
     extras = {}
     if not args.no_extras and not args.envs and args.config is None:
@@ -785,10 +816,7 @@ def main():
             line["steps"], line["warmup"] = ex_steps, ex_warm
             if r.get("gather"):
                 line.update(_gather_fields(r, world, backend, ex_steps))
-                if r.get("decoded"):
-                    dres = dict(r, elapsed=r["decoded"]["elapsed"], alive=r["decoded"]["alive"])
-                    d_el, d_al, _ = reduce(dres)
-                    line["decoded"] = {"value": round(d_al / d_el, 1), "ms_per_step": round(d_el * 1e3 / ex_steps, 4)}
+                line.update(learner_passes(r, ex_steps))
             extras[r["name"]] = line
 
     if rank == 0:
@@ -824,7 +852,7 @@ def main():
         if res["gather"]:
             line.update(_gather_fields(res, world, backend, args.steps))
             line["value_kind"] = "delivered"
-            line["decoded"] = decoded
+            line.update(passes)
         else:
             line["gather"] = None
         line["cpu_baseline"] = cpu

@@ -509,7 +509,23 @@ typedef struct NmmoStoreInput {
                              handle for the layout and task table), or NULL */
 } NmmoStoreInput;
 
-/* int32 scratch the storage calls need: max(n_rows + n_rows/512 + 2, n_slots). */
+/* Compact experience observations (the learner side of the C5 gather): a stored
+ * row's observation kept as the wire record it arrived in (SPEC.md §8c) instead of a 95,948-B
+ * flat row. nmmo_exp_store_records copies the store's wire buffer (its `total` bytes) into a byte
+ * arena behind a 16-B descriptor (int64 n_envs, int64 player_n) and records, per stored row, the
+ * descriptor's arena offset and the row's agent index (env * player_n + agent) in that buffer;
+ * nmmo_exp_gather_records expands rows to flat float32 rows when a minibatch needs them
+ * (clean_pufferl.py:439-458), bit-identical to the rows nmmo_exp_store writes from the same wire
+ * input. Every other experience field is stored as by nmmo_exp_store (x->obs may be NULL). */
+typedef struct NmmoRecordStore {
+  uint8_t* arena;        /* device bytes, 16-B aligned */
+  int64_t arena_bytes;   /* its capacity */
+  int64_t* arena_used;   /* device [1]: bytes used (zero it with the experience's ptr for a new batch) */
+  int64_t* row_buf;      /* device [capacity]: arena offset of the row's buffer descriptor */
+  int32_t* row_agent;    /* device [capacity]: env * player_n + agent in that buffer */
+} NmmoRecordStore;
+
+/* int32 scratch the storage calls need: max(n_rows + n_rows/512 + 8, n_slots). */
 NMMO_API int64_t nmmo_exp_scratch_ints(int32_t max_rows, int32_t n_slots);
 /* Appends the mask-selected rows of one recv (in row order, cut at the capacity) and advances
  * *ptr on the device; exactly one of obs / native / wire: native obs are expanded, and wire
@@ -517,6 +533,18 @@ NMMO_API int64_t nmmo_exp_scratch_ints(int32_t max_rows, int32_t n_slots);
  * whose layout and task table produced them; NULL for flat obs). Enqueued on `stream`. */
 NMMO_API int nmmo_exp_store(NmmoHandle* h, const NmmoExperience* x, const NmmoStoreInput* in,
                             int32_t* scratch, void* stream);
+/* nmmo_exp_store for a wire input (in->wire, in->obs and in->native NULL) into compact record
+ * storage: the mask-selected rows' fields as nmmo_exp_store, their observations as references
+ * into rs's arena (which receives the buffer). When the arena has no room for the buffer, the
+ * store keeps no row and ORs 2 into x->status. h: the wire handle (layout, task table).
+ * Enqueued; scratch as nmmo_exp_store. */
+NMMO_API int nmmo_exp_store_records(NmmoHandle* h, const NmmoExperience* x, const NmmoRecordStore* rs,
+                                    const NmmoStoreInput* in, int32_t* scratch, void* stream);
+/* out (device float32 [n][obs_elems]) = the flat rows of experience rows idx[0..n) (device
+ * int32) stored by nmmo_exp_store_records; h: the handle whose task table the records' task
+ * indices refer to. Enqueued. */
+NMMO_API int nmmo_exp_gather_records(NmmoHandle* h, const NmmoExperience* x, const NmmoRecordStore* rs,
+                                     const int32_t* idx, int32_t n, float* out, void* stream);
 /* idxs (device int32 [*ptr]) = the row order sorted by (env_id, step). Enqueued. */
 NMMO_API int nmmo_exp_sort(const NmmoExperience* x, int32_t* idxs, int32_t* scratch, void* stream);
 /* advantages (device f32 [batch_size]) over idxs[0..batch_size], float32, the reference's op

@@ -26,7 +26,8 @@ SYMBOLS = [
     "nmmo_last_error", "nmmo_abi_version", "nmmo_end_episodes", "nmmo_build_info",
     "nmmo_get_wrapper_dropped", "nmmo_set_task_weights", "nmmo_wire_header_bytes", "nmmo_wire_max_bytes",
     "nmmo_wire_pack", "nmmo_wire_unpack", "nmmo_wire_check", "nmmo_dev_alloc", "nmmo_dev_free", "nmmo_observe",
-    "nmmo_step_envs", "nmmo_inject_fault", "nmmo_fault_into",
+    "nmmo_step_envs", "nmmo_inject_fault", "nmmo_fault_into", "nmmo_exp_store_records",
+    "nmmo_exp_gather_records",
 ]
 
 
@@ -97,6 +98,9 @@ def declare(L):
     L.nmmo_exp_scratch_ints.restype = ctypes.c_int64
     L.nmmo_exp_store.argtypes = [vp, xp, ctypes.POINTER(abi.NmmoStoreInput), vp, vp]
     L.nmmo_exp_sort.argtypes = [xp, vp, vp, vp]
+    rsp = ctypes.POINTER(abi.NmmoRecordStore)
+    L.nmmo_exp_store_records.argtypes = [vp, xp, rsp, ctypes.POINTER(abi.NmmoStoreInput), vp, vp]
+    L.nmmo_exp_gather_records.argtypes = [vp, xp, rsp, vp, i32, vp, vp]
     L.nmmo_exp_gae.argtypes = [xp, vp, i32, ctypes.c_double, ctypes.c_double, vp, vp]
     L.nmmo_gather_rows.argtypes = [vp, ctypes.c_int64, vp, i32, vp, vp]
     L.nmmo_n_envs.argtypes = [vp]

@@ -244,6 +244,12 @@ class NmmoExperience(ctypes.Structure):
                                        "env_id", "step", "seq", "slot_count", "ptr", "status")]
 
 
+class NmmoRecordStore(ctypes.Structure):
+    """Compact experience observations (nmmo_exp_store_records / nmmo_exp_gather_records)."""
+    _fields_ = [("arena", ctypes.c_void_p), ("arena_bytes", ctypes.c_int64), ("arena_used", ctypes.c_void_p),
+                ("row_buf", ctypes.c_void_p), ("row_agent", ctypes.c_void_p)]
+
+
 class NmmoStoreInput(ctypes.Structure):
     _fields_ = [("n_rows", ctypes.c_int32), ("step", ctypes.c_int32), ("obs", ctypes.c_void_p),
                 ("native", ctypes.c_void_p), ("rewards", ctypes.c_void_p), ("dones", ctypes.c_void_p),

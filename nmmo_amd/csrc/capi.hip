@@ -576,17 +576,54 @@ int nmmo_wire_unpack(int32_t n_envs, int32_t player_n, const void* wire, void* n
 
 // ---------------------------------------------------------------- experience storage (§8f row 3)
 int64_t nmmo_exp_scratch_ints(int32_t max_rows, int32_t n_slots) {
-  const int64_t a = (int64_t)max_rows + store_blocks(max_rows) + 2;
+  const int64_t a = (int64_t)max_rows + store_blocks(max_rows) + 8;
   return a > n_slots ? a : (int64_t)n_slots;
 }
 
-static int check_exp(const NmmoExperience* x) {
+static int check_exp(const NmmoExperience* x, bool need_obs = true) {
   if (!x) return fail(NMMO_E_INVALID, "null experience");
   if (x->capacity <= 0 || x->obs_elems <= 0 || x->n_slots <= 0)
     return fail(NMMO_E_INVALID, "capacity/obs_elems/n_slots must be > 0");
-  if (!x->obs || !x->actions || !x->logprobs || !x->rewards || !x->dones || !x->values || !x->env_id ||
+  if ((need_obs && !x->obs) || !x->actions || !x->logprobs || !x->rewards || !x->dones || !x->values || !x->env_id ||
       !x->step || !x->seq || !x->slot_count || !x->ptr)
     return fail(NMMO_E_INVALID, "experience buffers must be device pointers");
+  return NMMO_OK;
+}
+
+static int check_records(const NmmoRecordStore* rs) {
+  if (!rs || !rs->arena || !rs->arena_used || !rs->row_buf || !rs->row_agent)
+    return fail(NMMO_E_INVALID, "record store buffers must be device pointers");
+  if (rs->arena_bytes <= 0 || ((uintptr_t)rs->arena & 15)) return fail(NMMO_E_INVALID, "arena must be 16-B aligned, > 0 bytes");
+  return NMMO_OK;
+}
+
+int nmmo_exp_store_records(NmmoHandle* h, const NmmoExperience* x, const NmmoRecordStore* rs, const NmmoStoreInput* in,
+                           int32_t* scratch, void* stream) {
+  if (int rc = check_exp(x, false)) return rc;
+  if (int rc = check_records(rs)) return rc;
+  if (!h || !in || !scratch) return fail(NMMO_E_INVALID, "null handle/input/scratch");
+  if (!in->wire || in->obs || in->native) return fail(NMMO_E_INVALID, "record storage takes a wire input only");
+  if (in->n_rows <= 0 || in->n_rows % h->st.P) return fail(NMMO_E_SIZE, "n_rows must be whole envs of player_n rows");
+  if (!in->rewards || !in->dones || !in->mask || !in->actions || !in->logprobs || !in->values)
+    return fail(NMMO_E_INVALID, "store inputs must be device pointers");
+  if (!in->env_id && (in->env_id_base < 0 || (int64_t)in->env_id_base + in->n_rows > x->n_slots))
+    return fail(NMMO_E_INVALID, "env_id_base + n_rows exceeds n_slots");
+  if (((uintptr_t)in->wire & 15)) return fail(NMMO_E_INVALID, "wire buffer must be 16-B aligned");
+  HIP_TRY(hipSetDevice(h->device));
+  const int64_t cap = nmmo_wire_max_bytes(in->n_rows / h->st.P, h->st.P);
+  HIP_TRY(launch_store_records(*x, *rs, *in, h->st.P, cap, scratch, (hipStream_t)stream));
+  return NMMO_OK;
+}
+
+int nmmo_exp_gather_records(NmmoHandle* h, const NmmoExperience* x, const NmmoRecordStore* rs, const int32_t* idx,
+                            int32_t n, float* out, void* stream) {
+  if (int rc = check_exp(x, false)) return rc;
+  if (int rc = check_records(rs)) return rc;
+  if (!h || !idx || !out) return fail(NMMO_E_INVALID, "null handle/idx/out");
+  if (n < 0) return fail(NMMO_E_INVALID, "n must be >= 0");
+  if (x->obs_elems != h->layout.obs_elems) return fail(NMMO_E_SIZE, "obs_elems != the handle's layout");
+  HIP_TRY(hipSetDevice(h->device));
+  HIP_TRY(launch_record_gather(obs_params(h, nullptr), *rs, idx, n, out, (hipStream_t)stream));
   return NMMO_OK;
 }
 

@@ -153,6 +153,12 @@ hipError_t launch_wire_check(const uint8_t* wire, int n, int P, const int64_t* e
 hipError_t launch_wire_expand(const ObsParams& p, hipStream_t s);
 hipError_t launch_store(const NmmoExperience& x, const NmmoStoreInput& in, const ObsParams* native,
                         int* scratch, hipStream_t stream);  // storage.hip
+// compact record storage (storage.hip): the store's wire buffer into rs's arena, row references
+hipError_t launch_store_records(const NmmoExperience& x, const NmmoRecordStore& rs, const NmmoStoreInput& in,
+                                int P, int64_t wire_cap, int* scratch, hipStream_t stream);
+// flat rows of stored record rows (wire.hip)
+hipError_t launch_record_gather(const ObsParams& p, const NmmoRecordStore& rs, const int32_t* idx, int n,
+                                float* out, hipStream_t stream);
 int store_blocks(int n_rows);
 hipError_t launch_sort(const NmmoExperience& x, int32_t* idxs, int* scratch, hipStream_t stream);
 hipError_t launch_gae(const NmmoExperience& x, const int32_t* idxs, int B, float g, float gl, float* adv,

@@ -12,7 +12,10 @@
 // the native layout (SPEC §8b: 9,552 B read per row) or decoded from its wire record (SPEC §8c,
 // ~1.3 KB read per row; wire.hip wire_expand_kernel) into its experience slot; every other
 // field is a few bytes per row.
+#include <algorithm>
+
 #include "kernels.h"
+#include "wire.h"
 
 namespace nmmo {
 
@@ -46,8 +49,13 @@ __global__ void __launch_bounds__(kStoreBlock) store_count_kernel(NmmoExperience
 // Pass 2: each alive row's rank in row order (clean_pufferl.py:333 torch.where(learner_mask)),
 // its experience slot ptr + rank if that is below the capacity (the [: batch_size - ptr + 1]
 // cut, :333), and the small per-row fields. dst[r] = slot or -1 (read by store_rows).
+// gate: NULL, or a device int that is 0 when the store keeps no row (record storage without arena
+// room); rs.row_buf non-NULL: record storage, each stored row's buffer descriptor (at arena offset
+// *rbase) and agent index are recorded.
 __global__ void __launch_bounds__(kStoreBlock) store_place_kernel(NmmoExperience x, NmmoStoreInput in,
-                                                                  const int* blk_cnt, int* dst, int* total) {
+                                                                  const int* blk_cnt, int* dst, int* total,
+                                                                  const int* gate, NmmoRecordStore rs,
+                                                                  const int64_t* rbase) {
   __shared__ int wt[2][8];
   const int b = blockIdx.x, tid = threadIdx.x, r = b * kStoreBlock + tid;
   int part = 0;  // rows of the blocks before this one
@@ -58,7 +66,7 @@ __global__ void __launch_bounds__(kStoreBlock) store_place_kernel(NmmoExperience
   int blk_total;
   const int rank = base_total + block_prefix_count(alive, wt[1], &blk_total);
   const int ptr0 = *x.ptr;
-  const int room = x.capacity - ptr0;
+  const int room = gate && !*gate ? 0 : x.capacity - ptr0;
   if (r < in.n_rows) dst[r] = (alive && rank < room) ? ptr0 + rank : -1;
   if (alive && rank < room) {
     const int s = ptr0 + rank;
@@ -73,12 +81,16 @@ __global__ void __launch_bounds__(kStoreBlock) store_place_kernel(NmmoExperience
     for (int h = 0; h < kHeads; h++) o[h] = a[h];
     x.env_id[s] = eid;
     x.step[s] = in.step;
+    if (rs.row_buf) {
+      rs.row_buf[s] = *rbase;
+      rs.row_agent[s] = r;
+    }
     // rank of this row among its env_id's rows (stores arrive in step order). Env ids are
     // distinct within one store (ABI precondition), so the counter has one writer; the atomic
     // keeps a violating caller's rows at distinct sorted positions instead of corrupting them.
     x.seq[s] = atomicAdd(&x.slot_count[eid], 1);
   }
-  if (b == gridDim.x - 1 && tid == 0) *total = base_total + blk_total;
+  if (b == gridDim.x - 1 && tid == 0) *total = min(base_total + blk_total, room);  // rows placed
 }
 
 // Pass 3 (flat obs): one wave copies one 95,948-B row (4-B aligned rows, so dword accesses;
@@ -197,7 +209,8 @@ hipError_t launch_store(const NmmoExperience& x, const NmmoStoreInput& in, const
   int* blk = scratch + in.n_rows;    // [nb]
   int* total = blk + nb;             // [1]
   hipLaunchKernelGGL(store_count_kernel, dim3(nb), dim3(kStoreBlock), 0, stream, x, in, blk);
-  hipLaunchKernelGGL(store_place_kernel, dim3(nb), dim3(kStoreBlock), 0, stream, x, in, blk, dst, total);
+  hipLaunchKernelGGL(store_place_kernel, dim3(nb), dim3(kStoreBlock), 0, stream, x, in, blk, dst, total,
+                     (const int*)nullptr, NmmoRecordStore{}, (const int64_t*)nullptr);
   if (native) {
     ObsParams p = *native;
     p.obs = x.obs;
@@ -208,6 +221,61 @@ hipError_t launch_store(const NmmoExperience& x, const NmmoStoreInput& in, const
     hipLaunchKernelGGL(store_rows_kernel, dim3((in.n_rows + 3) / 4), dim3(256), 0, stream, in.obs, in.n_rows,
                        x.obs_elems, dst, x.obs);
   }
+  hipLaunchKernelGGL(store_commit_kernel, dim3(1), dim3(1), 0, stream, x.ptr, total, x.capacity);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- compact record storage
+// One thread: the wire buffer's announced total, its place in the arena (16-B aligned, after a
+// 16-B descriptor n_envs | player_n) if it fits and is a plausible buffer (>= its header, <= the
+// caller's capacity bound). gate[0] = fits; rbase[0] = descriptor offset; the arena grows.
+__global__ void record_reserve_kernel(NmmoExperience x, NmmoRecordStore rs, const uint8_t* wire, int n_envs, int P,
+                                      int64_t wire_cap, int* gate, int64_t* rbase) {
+  const int64_t total = *reinterpret_cast<const int64_t*>(wire);
+  const int64_t base = (*rs.arena_used + 15) & ~(int64_t)15;
+  const bool ok = total >= wire_header_bytes(n_envs, P) && total <= wire_cap && (total & 15) == 0 &&
+                  base + 16 + total <= rs.arena_bytes;
+  *gate = ok;
+  *rbase = base;
+  if (ok) {
+    int64_t* d = reinterpret_cast<int64_t*>(rs.arena + base);
+    d[0] = n_envs;
+    d[1] = P;
+    *rs.arena_used = base + 16 + total;
+  } else if (x.status) {
+    atomicOr(x.status, 2);
+  }
+}
+
+// the buffer's `total` bytes behind its descriptor, 16 B per lane, grid-stride (the length is read
+// on the device)
+__global__ void __launch_bounds__(256) record_copy_kernel(NmmoRecordStore rs, const uint4* __restrict__ wire,
+                                                         const int* gate, const int64_t* rbase) {
+  if (!*gate) return;
+  const int64_t words = *reinterpret_cast<const int64_t*>(wire) / 16;
+  uint4* dst = reinterpret_cast<uint4*>(rs.arena + *rbase + 16);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += (int64_t)gridDim.x * blockDim.x)
+    dst[i] = wire[i];
+}
+
+hipError_t launch_store_records(const NmmoExperience& x, const NmmoRecordStore& rs, const NmmoStoreInput& in,
+                                int P, int64_t wire_cap, int* scratch, hipStream_t stream) {
+  const int nb = store_blocks(in.n_rows);
+  int* dst = scratch;                // [n_rows]
+  int* blk = scratch + in.n_rows;    // [nb]
+  int* total = blk + nb;             // [1]
+  int* gate = total + 1;             // [1]
+  int64_t* rbase = reinterpret_cast<int64_t*>(scratch + ((in.n_rows + nb + 2 + 1) & ~1));  // [1], 8-B aligned
+  const uint8_t* wire = (const uint8_t*)in.wire;
+  hipLaunchKernelGGL(record_reserve_kernel, dim3(1), dim3(1), 0, stream, x, rs, wire, in.n_rows / P, P, wire_cap,
+                     gate, rbase);
+  hipLaunchKernelGGL(store_count_kernel, dim3(nb), dim3(kStoreBlock), 0, stream, x, in, blk);
+  hipLaunchKernelGGL(store_place_kernel, dim3(nb), dim3(kStoreBlock), 0, stream, x, in, blk, dst, total,
+                     (const int*)gate, rs, (const int64_t*)rbase);
+  const int64_t words = wire_cap / 16;
+  const int grid = (int)std::min<int64_t>((words + 255) / 256, 4096);
+  hipLaunchKernelGGL(record_copy_kernel, dim3(grid > 0 ? grid : 1), dim3(256), 0, stream, rs,
+                     (const uint4*)wire, (const int*)gate, (const int64_t*)rbase);
   hipLaunchKernelGGL(store_commit_kernel, dim3(1), dim3(1), 0, stream, x.ptr, total, x.capacity);
   return hipGetLastError();
 }

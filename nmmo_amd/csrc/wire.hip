@@ -535,6 +535,92 @@ __global__ void __launch_bounds__(256) wire_expand_kernel(ObsParams p) {
   }
 }
 
+// Flat rows of record-stored experience rows (nmmo_exp_gather_records): one wave per output row,
+// whose record may sit in any stored buffer and env, so nothing is staged per workgroup: the
+// wave finds the record (its env's count words -> offsets), copies it into its LDS slot and
+// writes the row with every value exactly as wire_expand_kernel computes it (entity-table rows,
+// listings and the Task embedding read through L2).
+__global__ void __launch_bounds__(256) record_gather_kernel(ObsParams p, NmmoRecordStore rs, const int32_t* idx, int n,
+                                                            float* out) {
+  __shared__ uint4 recbuf[4][kRecMaxU4];
+  const int k = blockIdx.x * 4 + wave_id(), lane = lane_id();
+  if (k >= n) return;
+  const int s = idx[k];
+  const uint8_t* d = rs.arena + rs.row_buf[s];
+  const int n_envs = (int)reinterpret_cast<const int64_t*>(d)[0], P = (int)reinterpret_cast<const int64_t*>(d)[1];
+  const int ra = rs.row_agent[s], e = ra / P, a = ra - e * P;
+  WireView v = wire_view(const_cast<uint8_t*>(d + 16), n_envs, P);
+  const uint16_t* cnt = v.cnt + (size_t)e * P;
+  const int ne = min((int)v.ecount[e], kMaxSlots), nm = v.mcount[e];
+  const uint8_t* penv = v.base + v.env_off[e];
+  float* row = out + (size_t)k * p.elems;
+  const uint32_t c = cnt[a];
+  if (!(c & 0x8000u)) {  // not in the realm: all-zero row
+    wave_zero(row, 0, p.elems);
+    return;
+  }
+  // record offset (agents before a) and the listings' offset (all agents), after the table
+  int before = 0, all = 0;
+  for (int b = 0; b < P; b += 64) {
+    const int q = b + lane;
+    const int x = q < P ? wire_record_bytes(cnt[q]) : 0;
+    before += q < a ? x : 0;
+    all += x;
+  }
+  before = wave_sum(before);
+  all = wave_sum(all);
+  const int tb = wire_table_bytes(ne);
+  const int16_t* tab = reinterpret_cast<const int16_t*>(penv);
+  const int16_t* mk = reinterpret_cast<const int16_t*>(penv + tb + all);  // listings, 16 int16 each
+  uint4* lrec = recbuf[wave_id()];
+  const uint8_t* lb = reinterpret_cast<const uint8_t*>(lrec);
+  const int nv = c & 127, ninv = (c >> 7) & 15;
+  record_to_lds(penv + tb + before, wire_record_bytes(c) / 16, lrec);
+  const int16_t* h16 = reinterpret_cast<const int16_t*>(lb);
+  const uint32_t* bits = reinterpret_cast<const uint32_t*>(lb + kWireHead);
+  const uint16_t* ix = reinterpret_cast<const uint16_t*>(lb + kWireBody);
+  const int16_t* s16 = reinterpret_cast<const int16_t*>(lb + kWireBody + 2 * nv);  // Inventory rows
+  const uint8_t* mat = lb + kWireBody + 2 * nv + 32 * ninv;
+  const bool exch = ((uint16_t)h16[6] >> 8) != 0;
+  const int gold = h16[7], aid = h16[0];
+  for (int j = lane; j < p.o_agent_id; j += 64) {
+    bool m;
+    if (j >= kWireBuyLo && j < kWireBuyLo + kWireBuyN) {  // Buy.MarketItem from the listings
+      const int q = j - kWireBuyLo;
+      m = q == NMMO_MARKET_ROWS || (exch && q < nm && mk[16 * q + 15] <= gold && mk[16 * q + 2] != aid);
+    } else {
+      const int b = entry_wire_bit(j);
+      m = (bits[b >> 5] >> (b & 31)) & 1u;
+    }
+    row[j] = m ? 1.f : 0.f;
+  }
+  if (lane == 0) row[p.o_agent_id] = (float)h16[0];
+  if (lane == 1) row[p.o_tick] = (float)h16[1];
+  for (int j = lane; j < kNObs * NMMO_N_ENTITY_COLS; j += 64) {
+    const int q = j / NMMO_N_ENTITY_COLS;
+    row[p.o_entity + j] =
+        q < nv ? (float)tab[min((int)ix[q], kMaxSlots - 1) * NMMO_N_ENTITY_COLS + j - q * NMMO_N_ENTITY_COLS] : 0.f;
+  }
+  for (int j = lane; j < kInv * 16; j += 64) row[p.o_inventory + j] = j < ninv * 16 ? (float)s16[j] : 0.f;
+  for (int j = lane; j < nm * 16; j += 64) row[p.o_market + j] = (float)mk[j];
+  wave_zero(row, p.o_market + nm * 16, p.o_task);
+  const float* temb = p.task + (size_t)h16[2] * p.task_dim;
+  for (int j = lane; j < p.task_dim; j += 64) row[p.o_task + j] = temb[j];
+  const int r0 = h16[3], c0 = h16[4];
+  for (int j = lane; j < 225 * 3; j += 64) {
+    const int t = j / 3, comp = j - 3 * t;
+    row[p.o_tile + j] = comp == 0 ? (float)(r0 + t / 15) : comp == 1 ? (float)(c0 + t % 15) : (float)wire_tile(mat, t);
+  }
+}
+
+hipError_t launch_record_gather(const ObsParams& p, const NmmoRecordStore& rs, const int32_t* idx, int n, float* out,
+                                hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  if (p.o_task != p.o_market + NMMO_MARKET_ROWS * 16) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(record_gather_kernel, dim3((n + 3) / 4), dim3(256), 0, s, p, rs, idx, n, out);
+  return hipGetLastError();
+}
+
 hipError_t launch_wire_pack(const uint16_t* counts, const int* mcount, const uint8_t* native, uint8_t* wire, int n,
                             int P, const int16_t* ent, int S, int exch, hipStream_t s) {
   if (P > 128 || n <= 0) return hipErrorInvalidValue;

@@ -238,8 +238,11 @@ class WireGather:
     observation landed, checked, in the learner's HBM, in the form the experience store decodes
     its kept rows from (nmmo_exp_store, wire input). decode=True additionally decodes every
     rank's buffers into the native layout (nmmo_wire_unpack, the full learner-ready tensor) on
-    the comm stream. on_step(t, got) (tests) runs on the root after step t's buffers landed,
-    with the device synchronised: got = {(rank, batch): (wire bytes, smalls)}.
+    the comm stream. store=DeviceExperience (root; compact record storage) stores every step's
+    learner rows (the agents in the realm) from every received buffer on the comm stream — the
+    root's real work per step, clean_pufferl.py:331-346 — as a batch of its own (reset each step).
+    on_step(t, got) (tests) runs on the root after step t's buffers landed, with the device
+    synchronised: got = {(rank, batch): (wire bytes, smalls)}.
 
     The compute of each (batch, ring slot) is captured once in a hipGraph (graphs=True); with
     graphs=False, before_step(t, j, engine) (tests: per-env episode ends) runs on batch j's
@@ -247,7 +250,7 @@ class WireGather:
 
     def __init__(self, engines, policy_seed: int, rank: int = 0, world: int = 1, decode: bool = False,
                  graphs: bool = True, ring: int = 3, on_step=None, backend: str | None = None,
-                 before_step=None):
+                 before_step=None, store=None):
         if before_step is not None and graphs:
             raise ValueError("before_step needs graphs=False")
         self.before_step = before_step
@@ -256,6 +259,8 @@ class WireGather:
 
         self.engines = list(engines)
         self.rank, self.world, self.decode, self.on_step = rank, world, decode, on_step
+        self.store = store if rank == 0 else None
+        self._stored = torch.zeros((), dtype=torch.int64, device=engines[0].device)  # rows the root stored
         self.pseed = policy_seed
         e0 = self.engines[0]
         self.device = e0.device
@@ -283,6 +288,7 @@ class WireGather:
             n_envs = [e.n_envs for e in self.engines]
             self.native = {(r, j): devmem.empty((n_envs[j], abi.native_env_bytes(self.P)), torch.uint8, self.device)
                            for r in range(world) for j in range(nb)}
+        self._zeros = self._acts = None
         self.graphs = None
         if graphs:
             self._capture()
@@ -318,12 +324,27 @@ class WireGather:
         if self.rank != 0:
             return
         with torch.cuda.stream(self.x.comm):
-            for (r, j), (w, _) in got.items():
+            if self.store is not None:
+                self.store.reset()
+            nb = len(self.engines)
+            for (r, j), (w, sm) in got.items():
                 n = self.engines[j].n_envs
                 if r != 0:  # a received buffer against the size its sender announced
                     nw.check_buffer(w, n, self.P, self.status, self.x.sizes[s % self.ring, r, j:j + 1])
                 if self.native is not None:
                     nw.unpack(w, n, self.P, out=self.native[r, j])
+                if self.store is not None:  # learner mask = in the realm; no policy outputs modelled
+                    st = sm.view(n * self.P, 8)
+                    if self._zeros is None or self._zeros.numel() < n * self.P:
+                        self._zeros = torch.zeros(n * self.P, device=self.device)
+                        self._acts = torch.zeros((n * self.P, 12), dtype=torch.int32, device=self.device)
+                    z = self._zeros[:n * self.P]
+                    base = (r * nb * n + j * n) * self.P  # global agent slot of the buffer's first row
+                    self.store.store(w, st[:, 0:4].contiguous().view(torch.float32).view(-1), st[:, 4], st[:, 6],
+                                     self._acts[:n * self.P], z, z, step=s + 1, env_id_base=base,
+                                     engine=self.engines[j])
+            if self.store is not None:
+                self._stored += self.store.ptr_dev[0].to(torch.int64)
         if self.on_step is not None:
             torch.cuda.synchronize(self.device)
             self.on_step(s, got)
@@ -369,6 +390,13 @@ class WireGather:
         for st in self.streams:
             cur.wait_stream(st)
         cur.wait_stream(self.x.comm)
+
+    def stored_rows(self) -> int:
+        """Rows the root's store pass kept since the last call (synchronising read)."""
+        torch.cuda.synchronize(self.device)
+        n = int(self._stored.item())
+        self._stored.zero_()
+        return n
 
     def check_status(self):
         """The accumulated nmmo_wire_check bits (0 = every received buffer was consistent)."""

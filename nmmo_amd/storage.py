@@ -29,9 +29,12 @@ def _p(t):
 
 
 class DeviceExperience:
-    def __init__(self, batch_size: int, obs_elems: int, n_slots: int, device=None):
+    def __init__(self, batch_size: int, obs_elems: int, n_slots: int, device=None, record_arena_bytes: int = 0):
         """batch_size: rows trained on per update (the buffers hold batch_size + 1, :182);
-        n_slots: the env_id range = num_envs x agents_per_env (:119)."""
+        n_slots: the env_id range = num_envs x agents_per_env (:119). record_arena_bytes > 0:
+        compact storage (nmmo_exp_store_records) — observations stay the wire records they came
+        in as (~0.3 KB per row instead of 95,948 B), in an arena of that many bytes, and are
+        expanded to flat rows per minibatch (gather_obs)."""
         self.device = torch.device("cuda", torch.cuda.current_device()) if device is None \
             else torch.device(device)
         self.batch_size = int(batch_size)
@@ -43,8 +46,19 @@ class DeviceExperience:
         i32 = dict(dtype=torch.int32, device=d)
         from . import devmem
 
-        self.obs = devmem.empty((cap, self.obs_elems), torch.float32, d)  # chunk-mapped when large
-        self.obs.zero_()
+        self.records = None
+        if record_arena_bytes > 0:
+            self.obs = None
+            self.arena = devmem.empty((int(record_arena_bytes),), torch.uint8, d)
+            self.arena_used = torch.zeros(1, dtype=torch.int64, device=d)
+            self.row_buf = torch.zeros(cap, dtype=torch.int64, device=d)
+            self.row_agent = torch.zeros(cap, **i32)
+            self.records = abi.NmmoRecordStore(self.arena.data_ptr(), int(record_arena_bytes),
+                                               self.arena_used.data_ptr(), self.row_buf.data_ptr(),
+                                               self.row_agent.data_ptr())
+        else:
+            self.obs = devmem.empty((cap, self.obs_elems), torch.float32, d)  # chunk-mapped when large
+            self.obs.zero_()
         self.actions = torch.zeros((cap, abi.N_ACTION_HEADS), dtype=torch.int64, device=d)
         self.logprobs = torch.zeros(cap, **f32)
         self.rewards = torch.zeros(cap, **f32)
@@ -60,7 +74,7 @@ class DeviceExperience:
         self._scratch_rows = 0
         self.scratch = torch.zeros(0, **i32)
         self.x = abi.NmmoExperience(cap, self.obs_elems, self.n_slots, *[
-            t.data_ptr() for t in (self.obs, self.actions, self.logprobs, self.rewards, self.dones,
+            None if t is None else t.data_ptr() for t in (self.obs, self.actions, self.logprobs, self.rewards, self.dones,
                                    self.truncateds, self.values, self.env_id, self.step, self.seq,
                                    self.slot_count, self.ptr_dev, self.status_dev)])
 
@@ -77,6 +91,8 @@ class DeviceExperience:
         """Start a new batch: ptr = 0 (:200) and empty sort keys (:415)."""
         self.ptr_dev.zero_()
         self.slot_count.zero_()
+        if self.records is not None:
+            self.arena_used.zero_()
 
     @property
     def status(self) -> int:
@@ -120,6 +136,8 @@ class DeviceExperience:
                 raise ValueError("env_id must be distinct within one store")
         native = engine is not None and engine.config.obs_layout == abi.OBS_NATIVE
         wired = engine is not None and engine.config.obs_layout == abi.OBS_WIRE
+        if self.records is not None and not wired:
+            raise ValueError("compact (record) storage stores wire buffers: pass the wire engine")
         obs_flat = obs_nat = obs_wire = None
         if native:
             if o.dtype != torch.uint8 or o.shape[0] * engine.P != n:
@@ -143,8 +161,14 @@ class DeviceExperience:
                                  int(env_id_base), a.data_ptr(), lp.data_ptr(), v.data_ptr(),
                                  obs_wire.data_ptr() if obs_wire is not None else None)
         with torch.cuda.device(dev):
-            check(lib().nmmo_exp_store(engine.h if native or wired else None, ctypes.byref(self.x),
-                                       ctypes.byref(inp), _p(self.scratch), self._stream()), "nmmo_exp_store")
+            if self.records is not None:
+                self._engine = engine  # its task table decodes the records (gather_obs)
+                check(lib().nmmo_exp_store_records(engine.h, ctypes.byref(self.x), ctypes.byref(self.records),
+                                                   ctypes.byref(inp), _p(self.scratch), self._stream()),
+                      "nmmo_exp_store_records")
+            else:
+                check(lib().nmmo_exp_store(engine.h if native or wired else None, ctypes.byref(self.x),
+                                           ctypes.byref(inp), _p(self.scratch), self._stream()), "nmmo_exp_store")
         # keep the inputs alive until the kernels that read them have been enqueued
         self._inflight = (r_, d_, m_, lp, v, a, eid, obs_flat, obs_nat, obs_wire)
 
@@ -185,9 +209,23 @@ class DeviceExperience:
         """Minibatch `mb` of the flattened batch (:456-462): obs [batch_rows, bptt, obs_elems],
         actions, logprobs, dones, values gathered straight from the experience rows."""
         idx = b_idxs[mb]
-        return {"obs": self.gather(self.obs, idx), "actions": self.gather(self.actions, idx),
+        return {"obs": self.gather_obs(idx), "actions": self.gather(self.actions, idx),
                 "logprobs": self.gather(self.logprobs, idx), "dones": self.gather(self.dones, idx),
                 "values": self.gather(self.values, idx)}
+
+    def gather_obs(self, idx: torch.Tensor, engine=None) -> torch.Tensor:
+        """Flat float32 obs rows of experience rows idx (any shape): a row gather, or with compact
+        storage the records expanded on the device (nmmo_exp_gather_records; `engine` = the wire
+        handle whose task table the records use, default the one the stores came from)."""
+        if self.records is None:
+            return self.gather(self.obs, idx)
+        eng = engine or self._engine
+        flat_idx = idx.reshape(-1).to(torch.int32).contiguous()
+        out = torch.empty((flat_idx.numel(), self.obs_elems), dtype=torch.float32, device=self.device)
+        with torch.cuda.device(self.device):
+            check(lib().nmmo_exp_gather_records(eng.h, ctypes.byref(self.x), ctypes.byref(self.records), _p(flat_idx),
+                                                flat_idx.numel(), _p(out), self._stream()), "nmmo_exp_gather_records")
+        return out.view(tuple(idx.shape) + (self.obs_elems,))
 
     def gather(self, src: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
         """src[idx] on the device through nmmo_gather_rows (rows of src's trailing dims)."""

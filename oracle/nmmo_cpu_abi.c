@@ -301,6 +301,16 @@ NMMO_API int nmmo_get_fault(NmmoHandle* h, int32_t* fault) {  /* the serial orac
   h->fault = 0;
   return NMMO_OK;
 }
+NMMO_API int nmmo_exp_store_records(NmmoHandle* h, const NmmoExperience* x, const NmmoRecordStore* rs,
+                                    const NmmoStoreInput* in, int32_t* scratch, void* stream) {
+  (void)h; (void)x; (void)rs; (void)in; (void)scratch; (void)stream;
+  UNSUPPORTED("nmmo_exp_store_records");
+}
+NMMO_API int nmmo_exp_gather_records(NmmoHandle* h, const NmmoExperience* x, const NmmoRecordStore* rs,
+                                     const int32_t* idx, int32_t n, float* out, void* stream) {
+  (void)h; (void)x; (void)rs; (void)idx; (void)n; (void)out; (void)stream;
+  UNSUPPORTED("nmmo_exp_gather_records");
+}
 NMMO_API int nmmo_fault_into(NmmoHandle* h, int32_t* dst, void* stream) {  /* host dst */
   (void)stream;
   if (!h || !dst) return fail(NMMO_E_INVALID, "null argument");

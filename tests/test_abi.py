@@ -169,8 +169,9 @@ def test_storage_structs_and_wire_layout_match_c_compiler():
 #include <stddef.h>
 #include "nmmo_hip.h"
 int main(void) {
-  printf("%zu %zu %zu %zu %d\n", sizeof(NmmoStoreInput), offsetof(NmmoStoreInput, values),
-         offsetof(NmmoStoreInput, wire), sizeof(NmmoExperience), NMMO_OBS_WIRE);
+  printf("%zu %zu %zu %zu %d %zu %zu\n", sizeof(NmmoStoreInput), offsetof(NmmoStoreInput, values),
+         offsetof(NmmoStoreInput, wire), sizeof(NmmoExperience), NMMO_OBS_WIRE, sizeof(NmmoRecordStore),
+         offsetof(NmmoRecordStore, row_agent));
   return 0;
 }
 """
@@ -181,7 +182,8 @@ int main(void) {
         subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), c, "-o", exe])
         got = list(map(int, subprocess.check_output([exe]).split()))
     assert got == [ctypes.sizeof(abi.NmmoStoreInput), abi.NmmoStoreInput.values.offset,
-                   abi.NmmoStoreInput.wire.offset, ctypes.sizeof(abi.NmmoExperience), abi.OBS_WIRE]
+                   abi.NmmoStoreInput.wire.offset, ctypes.sizeof(abi.NmmoExperience), abi.OBS_WIRE,
+                   ctypes.sizeof(abi.NmmoRecordStore), abi.NmmoRecordStore.row_agent.offset]
 
 
 def test_wire_calls_report_errors(native):

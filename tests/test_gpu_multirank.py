@@ -45,7 +45,10 @@ def test_two_ranks_c4():
 def test_two_ranks_c5_is_the_default_multi_gpu_line():
     d = _run("--envs", "8")  # no --config: N > 1 measures C5
     assert d["n_gpus"] == 2 and d["config"]["workload"].startswith("C5")
-    assert d["value_kind"] == "delivered" and d["decoded"]["value"] > 0
+    assert d["value_kind"] == "delivered" and d["decoded"]["value"] > 0 and d["stored"]["value"] > 0
+    # the root stored every row in the realm of both ranks: the rows/s equal the alive agent-steps/s
+    # of the stored pass (env side), within timing rounding
+    assert d["stored"]["rows_stored_per_sec"] == pytest.approx(d["stored"]["value"], rel=0.02)
     assert d["gather_bytes_per_step"] > 0 and "B/step" in d["gather"]
     assert 0 < d["value"] * d["ms_per_step"] / 1e3 <= 2 * 8 * 128 * 1.01
 

@@ -376,6 +376,9 @@ def test_can_see_tile_regrowth_parity_without_npc():
         assert np.array_equal(eng.rew.cpu().numpy(), orc.rew), f"rewards @ {t}"
         flips += int((orc.rew[assign == 0] != 0).sum())  # Foilage came into / went out of view
     assert flips > 20, flips
+
+
+def pathing_scenario(n=4):
     """SPEC §6 v2 window BFS under stress: in every env, hostile NPCs are put 2-7 tiles from live
     players and stone walls are scattered around them, so most hunts path around obstacles (and
     some targets are unreachable inside the window: greedy fallback). HIP vs oracle, bit-exact."""

@@ -181,6 +181,50 @@ def test_wire_store_equals_native_store():
         e.close()
 
 
+def test_record_store_gathers_the_flat_store_rows():
+    """Compact storage (nmmo_exp_store_records): the kept rows' observations stay wire records in
+    an arena and expand per gather; every row equals the flat store's row from the same wire
+    buffers (bit-exact, in a shuffled gather order), the small fields are identical, and a store
+    the arena has no room for keeps no row and raises status bit 2."""
+    from nmmo_amd.storage import DeviceExperience
+
+    from nmmo_amd import abi
+    from nmmo_amd.config import Config
+    from nmmo_amd.engine import NmmoEngine
+
+    n = 5
+    wir = NmmoEngine(Config.preset("C4", MAP_N=4, early_stop_agent_num=8, obs_layout=abi.OBS_WIRE), n, seed=9)
+    wir.reset()
+    P = wir.P
+    flat = DeviceExperience(900, wir.obs_elems, n * P, device=wir.device)
+    rec = DeviceExperience(900, wir.obs_elems, n * P, device=wir.device, record_arena_bytes=64 << 20)
+    g = torch.Generator(device="cpu").manual_seed(4)
+    for t in range(10):
+        wir.scripted_actions(70 + t)
+        wir.step()
+        keep = (wir.mask.view(-1).cpu() != 0) & (torch.rand(n * P, generator=g) < 0.6)
+        m = keep.to(torch.uint8).to(wir.device)
+        lp = torch.randn(n * P, generator=g).to(wir.device)
+        for x in (flat, rec):
+            x.store(wir.obs, wir.rew.view(-1), wir.term.view(-1), m, wir.actions.view(-1, 12), lp, lp, step=t,
+                    engine=wir)
+    torch.cuda.synchronize()
+    k = flat.ptr
+    assert rec.ptr == k == 901 and rec.status == 0
+    for name in ("actions", "rewards", "dones", "logprobs", "values", "env_id", "step", "seq"):
+        assert torch.equal(getattr(flat, name)[:k], getattr(rec, name)[:k]), name
+    order = torch.randperm(k, generator=g).to(torch.int32).to(wir.device)
+    got = rec.gather_obs(order)
+    assert torch.equal(got, flat.obs[order.long()])
+    assert int(rec.arena_used.item()) < 4 << 20  # a few MB of records, not 900 x 96 KB
+    small = DeviceExperience(900, wir.obs_elems, n * P, device=wir.device, record_arena_bytes=4096)
+    small.store(wir.obs, wir.rew.view(-1), wir.term.view(-1), m, wir.actions.view(-1, 12), lp, lp, step=0,
+                engine=wir)
+    torch.cuda.synchronize()
+    assert small.ptr == 0 and small.status & 2
+    wir.close()
+
+
 def test_wire_pack_rejects_stale_native():
     """nmmo_wire_pack refuses a native buffer a tick without an obs gather has made stale, or
     one that is not the buffer the last gather wrote."""

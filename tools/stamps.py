@@ -78,6 +78,17 @@ def main():
     for i, (_, name) in enumerate(STAMPS[1:]):
         med, p90 = np.median(d[:, i]), np.percentile(d[:, i], 90)
         print(f"  {name:42s} median {med:9.0f}  p90 {p90:9.0f}  ({100 * med / tot:5.1f}%)")
+    # the tail: a launch lasts as long as its slowest env, so what makes the slowest env-ticks
+    # slow matters more than the median. Per phase: p99, and the mean over the slowest 5% of
+    # env-ticks (by total) against the mean over all of them.
+    tot_each = d.sum(1)
+    slow = tot_each >= np.percentile(tot_each, 95)
+    print(f"  tail: slowest 5% of stepped env-ticks ({int(slow.sum())}): total mean {tot_each[slow].mean():.0f} "
+          f"vs {tot_each.mean():.0f} overall, p99 {np.percentile(tot_each, 99):.0f}, max {tot_each.max():.0f}")
+    excess = d[slow].mean(0) - d.mean(0)
+    for i in np.argsort(-excess)[:10]:
+        print(f"    {STAMPS[i + 1][1]:42s} slow-5% mean {d[slow, i].mean():9.0f}  all mean {d[:, i].mean():9.0f}  "
+              f"p99 {np.percentile(d[:, i], 99):9.0f}  excess {excess[i]:8.0f}")
     tt = np.concatenate(totals)
     for name, sel in (("stepped", tt[:, 1] == 1), ("reset", tt[:, 1] == 0)):
         x = tt[sel, 0]
