@@ -22,8 +22,12 @@
 
 namespace nmmo {
 
-constexpr int kAoWaves = 4;
-constexpr int kAoAgents = 16;             // agents per workgroup
+#ifndef NMMO_AO_WAVES  // (A/B builds of the native kernel's workgroup shape: tools/debug/ab_native.sh)
+#define NMMO_AO_WAVES 4
+#define NMMO_AO_AGENTS 16
+#endif
+constexpr int kAoWaves = NMMO_AO_WAVES;
+constexpr int kAoAgents = NMMO_AO_AGENTS;  // agents per workgroup
 constexpr int kAoRows = kMaxSlots / 64;   // packed datastore-row words per lane
 constexpr uint32_t kAoEmpty = 0xFFFFFFFFu;
 static_assert(kSize <= 256 && kMaxSlots <= 2 * 256 && kMaxSlots % 64 == 0, "packed entity word; two slots per thread (>= 256 threads)");

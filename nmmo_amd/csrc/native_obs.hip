@@ -30,7 +30,7 @@ constexpr int kNoImgWords = NMMO_NATIVE_MASK_BYTES / 32;  // 50: the mask image,
 // (Capped at 96 VGPRs for a fifth wave per SIMD it measured 0.155 ms per 512 envs against 0.143
 // uncapped at 109 VGPRs / 4 waves.)
 template <bool kWrap>
-__global__ void __launch_bounds__(256) native_obs_kernel(ObsParams p) {
+__global__ void __launch_bounds__(64 * kAoWaves) native_obs_kernel(ObsParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int S = p.S, P = p.P, Sp = ao_stride(S);
   int16_t* T = reinterpret_cast<int16_t*>(smem);
@@ -39,8 +39,13 @@ __global__ void __launch_bounds__(256) native_obs_kernel(ObsParams p) {
   uint32_t* visw_all = reinterpret_cast<uint32_t*>(mpo + NMMO_MARKET_ROWS);   // [4][128]
   uint32_t* wst = visw_all + kAoWaves * 128;                                  // [16][15][5] window rows
   uint2* ist = reinterpret_cast<uint2*>(wst + kAoAgents * kAoWinAgentBytes / 4);  // [16][12] item words
-  const int e = p.env_list ? p.env_list[blockIdx.x] : (int)blockIdx.x, g = blockIdx.y, tid = threadIdx.x,
-            lane = lane_id();
+#ifdef NMMO_NO_XCD  // 1-D grid, an env's groups back to back on one XCD (agent_obs.h ao_env_group)
+  int el, g;
+  ao_env_group(p.env_list ? p.n_list : p.n_envs, (p.P + kAoAgents - 1) / kAoAgents, el, g);
+#else
+  const int el = blockIdx.x, g = blockIdx.y;
+#endif
+  const int e = p.env_list ? p.env_list[el] : el, tid = threadIdx.x, lane = lane_id();
   if ((unsigned)e >= (unsigned)p.n_envs) return;  // a bad list id (the tick records it)
   const int w = __builtin_amdgcn_readfirstlane(wave_id());
   const int nm = min(max(p.mcount[e], 0), NMMO_MARKET_ROWS);
@@ -257,7 +262,11 @@ hipError_t launch_native_obs(const ObsParams& p, hipStream_t stream) {
   if (p.S % 8 || p.S > kMaxSlots || p.P > 128 || !p.nat || !ao_layout_ok(p)) return hipErrorInvalidValue;
   const int ne = list_grid(p.env_list, p.n_list, p.n_envs);
   if (ne <= 0) return hipSuccess;
+#ifdef NMMO_NO_XCD
+  const dim3 grid(ne * ((p.P + kAoAgents - 1) / kAoAgents)), block(64 * kAoWaves);
+#else
   const dim3 grid(ne, (p.P + kAoAgents - 1) / kAoAgents), block(64 * kAoWaves);
+#endif
   const size_t lds = no_lds_bytes(p.S);
   if (p.wflags) hipLaunchKernelGGL(native_obs_kernel<true>, grid, block, lds, stream, p);
   else hipLaunchKernelGGL(native_obs_kernel<false>, grid, block, lds, stream, p);

@@ -161,11 +161,18 @@ __device__ __forceinline__ uint32_t move_bits(uint32_t wm1) {
 // embedding) are issued before the previous agent's remaining ~130 stores (vmcnt retires in
 // issue order, so a load issued after a store stream waits for all of it; issued ahead of >= 63
 // younger stores it costs no wait at all).
-constexpr int kTaskRegs = 32;  // Task embedding dwords per lane held in registers (2,048 per row)
+#ifndef NMMO_OBS_TASK_REGS  // (A/B knobs: tools/debug/variants.py)
+#define NMMO_OBS_TASK_REGS 32
+#endif
+constexpr int kTaskRegs = NMMO_OBS_TASK_REGS;  // Task embedding dwords per lane held in registers (2,048 per row)
 
 // kWrap: the wrapper's observation() edits are compiled in (SPEC §13).
 template <bool kWrap>
-__global__ void __launch_bounds__(256) obs_kernel(ObsParams p) {
+__global__ void __launch_bounds__(256)
+#ifdef NMMO_OBS_WPE
+__attribute__((amdgpu_waves_per_eu(NMMO_OBS_WPE, NMMO_OBS_WPE)))
+#endif
+obs_kernel(ObsParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int S = p.S;
   int16_t* T = reinterpret_cast<int16_t*>(smem);
