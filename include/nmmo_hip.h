@@ -540,6 +540,15 @@ NMMO_API int nmmo_exp_store(NmmoHandle* h, const NmmoExperience* x, const NmmoSt
  * Enqueued; scratch as nmmo_exp_store. */
 NMMO_API int nmmo_exp_store_records(NmmoHandle* h, const NmmoExperience* x, const NmmoRecordStore* rs,
                                     const NmmoStoreInput* in, int32_t* scratch, void* stream);
+/* nmmo_exp_store_records over n_inputs (1..16) wire inputs at once, stored in input order as
+ * one store (the learner storing every rank's buffers of a step: a fixed number of launches
+ * whatever the input count). field_stride > 0: each input's rewards / dones / mask are read
+ * field_stride bytes apart per row (float at rewards, u8 at dones and mask; e.g. an 8-B packed
+ * per-agent record), 0: packed arrays as in nmmo_exp_store. scratch: nmmo_exp_scratch_ints of
+ * the inputs' summed rows. Enqueued. */
+NMMO_API int nmmo_exp_store_records_many(NmmoHandle* h, const NmmoExperience* x, const NmmoRecordStore* rs,
+                                         const NmmoStoreInput* ins, int32_t n_inputs, int32_t field_stride,
+                                         int32_t* scratch, void* stream);
 /* out (device float32 [n][obs_elems]) = the flat rows of experience rows idx[0..n) (device
  * int32) stored by nmmo_exp_store_records; h: the handle whose task table the records' task
  * indices refer to. Enqueued. */

@@ -27,7 +27,7 @@ SYMBOLS = [
     "nmmo_get_wrapper_dropped", "nmmo_set_task_weights", "nmmo_wire_header_bytes", "nmmo_wire_max_bytes",
     "nmmo_wire_pack", "nmmo_wire_unpack", "nmmo_wire_check", "nmmo_dev_alloc", "nmmo_dev_free", "nmmo_observe",
     "nmmo_step_envs", "nmmo_inject_fault", "nmmo_fault_into", "nmmo_exp_store_records",
-    "nmmo_exp_gather_records",
+    "nmmo_exp_gather_records", "nmmo_exp_store_records_many",
 ]
 
 
@@ -101,6 +101,7 @@ def declare(L):
     rsp = ctypes.POINTER(abi.NmmoRecordStore)
     L.nmmo_exp_store_records.argtypes = [vp, xp, rsp, ctypes.POINTER(abi.NmmoStoreInput), vp, vp]
     L.nmmo_exp_gather_records.argtypes = [vp, xp, rsp, vp, i32, vp, vp]
+    L.nmmo_exp_store_records_many.argtypes = [vp, xp, rsp, ctypes.POINTER(abi.NmmoStoreInput), i32, i32, vp, vp]
     L.nmmo_exp_gae.argtypes = [xp, vp, i32, ctypes.c_double, ctypes.c_double, vp, vp]
     L.nmmo_gather_rows.argtypes = [vp, ctypes.c_int64, vp, i32, vp, vp]
     L.nmmo_n_envs.argtypes = [vp]

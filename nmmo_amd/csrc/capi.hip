@@ -615,6 +615,36 @@ int nmmo_exp_store_records(NmmoHandle* h, const NmmoExperience* x, const NmmoRec
   return NMMO_OK;
 }
 
+int nmmo_exp_store_records_many(NmmoHandle* h, const NmmoExperience* x, const NmmoRecordStore* rs,
+                                const NmmoStoreInput* ins, int32_t n_inputs, int32_t field_stride, int32_t* scratch,
+                                void* stream) {
+  if (int rc = check_exp(x, false)) return rc;
+  if (int rc = check_records(rs)) return rc;
+  if (!h || !ins || !scratch) return fail(NMMO_E_INVALID, "null handle/inputs/scratch");
+  if (n_inputs < 1 || n_inputs > kMaxStoreInputs) return fail(NMMO_E_INVALID, "n_inputs %d not in 1..%d", n_inputs, kMaxStoreInputs);
+  if (field_stride < 0) return fail(NMMO_E_INVALID, "field_stride < 0");
+  StoreBatch b;
+  memset(&b, 0, sizeof(b));
+  b.n = n_inputs;
+  b.P = h->st.P;
+  b.stride = field_stride;
+  for (int i = 0; i < n_inputs; i++) {
+    const NmmoStoreInput& in = ins[i];
+    if (!in.wire || in.obs || in.native) return fail(NMMO_E_INVALID, "input %d: record storage takes a wire input only", i);
+    if (in.n_rows <= 0 || in.n_rows % h->st.P) return fail(NMMO_E_SIZE, "input %d: n_rows must be whole envs", i);
+    if (!in.rewards || !in.dones || !in.mask || !in.actions || !in.logprobs || !in.values)
+      return fail(NMMO_E_INVALID, "input %d: store inputs must be device pointers", i);
+    if (!in.env_id && (in.env_id_base < 0 || (int64_t)in.env_id_base + in.n_rows > x->n_slots))
+      return fail(NMMO_E_INVALID, "input %d: env_id_base + n_rows exceeds n_slots", i);
+    if (((uintptr_t)in.wire & 15)) return fail(NMMO_E_INVALID, "input %d: wire buffer must be 16-B aligned", i);
+    b.in[i] = in;
+    b.wire_cap[i] = nmmo_wire_max_bytes(in.n_rows / h->st.P, h->st.P);
+  }
+  HIP_TRY(hipSetDevice(h->device));
+  HIP_TRY(launch_store_records_many(*x, *rs, b, scratch, (hipStream_t)stream));
+  return NMMO_OK;
+}
+
 int nmmo_exp_gather_records(NmmoHandle* h, const NmmoExperience* x, const NmmoRecordStore* rs, const int32_t* idx,
                             int32_t n, float* out, void* stream) {
   if (int rc = check_exp(x, false)) return rc;

@@ -156,6 +156,17 @@ hipError_t launch_store(const NmmoExperience& x, const NmmoStoreInput& in, const
 // compact record storage (storage.hip): the store's wire buffer into rs's arena, row references
 hipError_t launch_store_records(const NmmoExperience& x, const NmmoRecordStore& rs, const NmmoStoreInput& in,
                                 int P, int64_t wire_cap, int* scratch, hipStream_t stream);
+// several wire buffers in one record store (storage.hip)
+constexpr int kMaxStoreInputs = 16;
+struct StoreBatch {
+  NmmoStoreInput in[kMaxStoreInputs];
+  int64_t wire_cap[kMaxStoreInputs];  // each buffer's capacity bound (nmmo_wire_max_bytes)
+  int n, P;
+  int stride;  // bytes between consecutive rows' reward / done / mask (0: packed float / u8 arrays)
+};
+int store_many_scratch_ints(int n_inputs, int max_rows);
+hipError_t launch_store_records_many(const NmmoExperience& x, const NmmoRecordStore& rs, const StoreBatch& b,
+                                     int* scratch, hipStream_t stream);
 // flat rows of stored record rows (wire.hip)
 hipError_t launch_record_gather(const ObsParams& p, const NmmoRecordStore& rs, const int32_t* idx, int n,
                                 float* out, hipStream_t stream);

@@ -280,6 +280,135 @@ hipError_t launch_store_records(const NmmoExperience& x, const NmmoRecordStore& 
   return hipGetLastError();
 }
 
+// ---- several wire buffers in one store (the root of the C5 gather: every rank's buffers of a
+// step, kept as one batch of rows in input order; five launches whatever the input count)
+__device__ __forceinline__ int sb_mask(const StoreBatch& b, const NmmoStoreInput& in, int r) {
+  return b.stride ? in.mask[(size_t)r * b.stride] : in.mask[r];
+}
+__device__ __forceinline__ bool sb_selected(const NmmoExperience& x, const StoreBatch& b, int i, const int* gates,
+                                            int r) {
+  const NmmoStoreInput& in = b.in[i];
+  if (r >= in.n_rows || !gates[i] || sb_mask(b, in, r) == 0) return false;
+  const int eid = in.env_id ? in.env_id[r] : in.env_id_base + r;
+  if (eid >= 0 && eid < x.n_slots) return true;
+  if (x.status) atomicOr(x.status, 1);
+  return false;
+}
+
+__global__ void record_reserve_many_kernel(NmmoExperience x, NmmoRecordStore rs, StoreBatch b, int* gates,
+                                           int64_t* rbase) {
+  int64_t used = *rs.arena_used;
+  for (int i = 0; i < b.n; i++) {
+    const NmmoStoreInput& in = b.in[i];
+    const int n_envs = in.n_rows / b.P;
+    const int64_t total = *reinterpret_cast<const int64_t*>(in.wire);
+    const int64_t base = (used + 15) & ~(int64_t)15;
+    const bool ok = total >= wire_header_bytes(n_envs, b.P) && total <= b.wire_cap[i] && (total & 15) == 0 &&
+                    base + 16 + total <= rs.arena_bytes;
+    gates[i] = ok;
+    rbase[i] = base;
+    if (ok) {
+      int64_t* d = reinterpret_cast<int64_t*>(rs.arena + base);
+      d[0] = n_envs;
+      d[1] = b.P;
+      used = base + 16 + total;
+    } else if (x.status) {
+      atomicOr(x.status, 2);
+    }
+  }
+  *rs.arena_used = used;
+}
+
+__global__ void __launch_bounds__(kStoreBlock) store_count_many_kernel(NmmoExperience x, StoreBatch b,
+                                                                       const int* gates, int* blk_cnt) {
+  __shared__ int wt[8];
+  const int i = blockIdx.y, r = blockIdx.x * kStoreBlock + threadIdx.x;
+  const uint64_t m = __ballot(sb_selected(x, b, i, gates, r));
+  if (lane_id() == 0) wt[wave_id()] = __popcll(m);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int s = 0;
+    for (int k = 0; k < kStoreBlock / 64; k++) s += wt[k];
+    blk_cnt[i * gridDim.x + blockIdx.x] = s;
+  }
+}
+
+__global__ void __launch_bounds__(kStoreBlock) store_place_many_kernel(NmmoExperience x, NmmoRecordStore rs,
+                                                                       StoreBatch b, const int* gates,
+                                                                       const int64_t* rbase, const int* blk_cnt,
+                                                                       int* total) {
+  __shared__ int wt[2][8];
+  const int i = blockIdx.y, tid = threadIdx.x, r = blockIdx.x * kStoreBlock + tid;
+  const int gb = i * gridDim.x + blockIdx.x;  // this block's place in input order
+  int part = 0;
+  for (int k = tid; k < gb; k += kStoreBlock) part += blk_cnt[k];
+  int base_total;
+  (void)block_prefix_sum(part, wt[0], &base_total);
+  const bool alive = sb_selected(x, b, i, gates, r);
+  int blk_total;
+  const int rank = base_total + block_prefix_count(alive, wt[1], &blk_total);
+  const int ptr0 = *x.ptr;
+  const int room = x.capacity - ptr0;
+  if (alive && rank < room) {
+    const NmmoStoreInput& in = b.in[i];
+    const int s = ptr0 + rank;
+    const int eid = in.env_id ? in.env_id[r] : in.env_id_base + r;
+    const uint8_t* rw = reinterpret_cast<const uint8_t*>(in.rewards);
+    x.rewards[s] = b.stride ? *reinterpret_cast<const float*>(rw + (size_t)r * b.stride) : in.rewards[r];
+    x.dones[s] = (float)(b.stride ? in.dones[(size_t)r * b.stride] : in.dones[r]);
+    x.logprobs[s] = in.logprobs[r];
+    x.values[s] = in.values[r];
+    const int32_t* a = in.actions + (size_t)r * kHeads;
+    long long* o = reinterpret_cast<long long*>(x.actions) + (size_t)s * kHeads;
+#pragma unroll
+    for (int h = 0; h < kHeads; h++) o[h] = a[h];
+    x.env_id[s] = eid;
+    x.step[s] = in.step;
+    x.seq[s] = atomicAdd(&x.slot_count[eid], 1);
+    rs.row_buf[s] = rbase[i];
+    rs.row_agent[s] = r;
+  }
+  if (gb == (int)(gridDim.x * gridDim.y) - 1 && tid == 0) *total = min(base_total + blk_total, room);
+}
+
+__global__ void __launch_bounds__(256) record_copy_many_kernel(NmmoRecordStore rs, StoreBatch b, const int* gates,
+                                                              const int64_t* rbase) {
+  const int i = blockIdx.y;
+  if (!gates[i]) return;
+  const uint4* wire = reinterpret_cast<const uint4*>(b.in[i].wire);
+  const int64_t words = *reinterpret_cast<const int64_t*>(wire) / 16;
+  uint4* dst = reinterpret_cast<uint4*>(rs.arena + rbase[i] + 16);
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < words; k += (int64_t)gridDim.x * blockDim.x)
+    dst[k] = wire[k];
+}
+
+int store_many_scratch_ints(int n_inputs, int max_rows) {
+  return n_inputs * store_blocks(max_rows) + 1 + n_inputs + 2 * n_inputs + 4;
+}
+
+hipError_t launch_store_records_many(const NmmoExperience& x, const NmmoRecordStore& rs, const StoreBatch& b,
+                                     int* scratch, hipStream_t stream) {
+  int max_rows = 0;
+  for (int i = 0; i < b.n; i++) max_rows = max(max_rows, b.in[i].n_rows);
+  const int nb = store_blocks(max_rows);
+  int* blk = scratch;              // [n][nb]
+  int* total = blk + b.n * nb;     // [1]
+  int* gates = total + 1;          // [n]
+  int64_t* rbase = reinterpret_cast<int64_t*>(scratch + ((b.n * nb + 1 + b.n + 1) & ~1));  // [n], 8-B aligned
+  hipLaunchKernelGGL(record_reserve_many_kernel, dim3(1), dim3(1), 0, stream, x, rs, b, gates, rbase);
+  hipLaunchKernelGGL(store_count_many_kernel, dim3(nb, b.n), dim3(kStoreBlock), 0, stream, x, b, (const int*)gates,
+                     blk);
+  hipLaunchKernelGGL(store_place_many_kernel, dim3(nb, b.n), dim3(kStoreBlock), 0, stream, x, rs, b,
+                     (const int*)gates, (const int64_t*)rbase, (const int*)blk, total);
+  int64_t words = 0;
+  for (int i = 0; i < b.n; i++) words = std::max(words, b.wire_cap[i] / 16);
+  const int grid = (int)std::min<int64_t>((words + 255) / 256, 1024);
+  hipLaunchKernelGGL(record_copy_many_kernel, dim3(grid > 0 ? grid : 1, b.n), dim3(256), 0, stream, rs, b,
+                     (const int*)gates, (const int64_t*)rbase);
+  hipLaunchKernelGGL(store_commit_kernel, dim3(1), dim3(1), 0, stream, x.ptr, total, x.capacity);
+  return hipGetLastError();
+}
+
 hipError_t launch_sort(const NmmoExperience& x, int32_t* idxs, int* scratch, hipStream_t stream) {
   hipLaunchKernelGGL(sort_scan_kernel, dim3(1), dim3(512), 0, stream, x.slot_count, x.n_slots, scratch);
   hipLaunchKernelGGL(sort_scatter_kernel, dim3((x.capacity + 255) / 256), dim3(256), 0, stream, x, scratch, idxs);

@@ -324,9 +324,8 @@ class WireGather:
         if self.rank != 0:
             return
         with torch.cuda.stream(self.x.comm):
-            if self.store is not None:
-                self.store.reset()
             nb = len(self.engines)
+            batch = []
             for (r, j), (w, sm) in got.items():
                 n = self.engines[j].n_envs
                 if r != 0:  # a received buffer against the size its sender announced
@@ -334,16 +333,17 @@ class WireGather:
                 if self.native is not None:
                     nw.unpack(w, n, self.P, out=self.native[r, j])
                 if self.store is not None:  # learner mask = in the realm; no policy outputs modelled
-                    st = sm.view(n * self.P, 8)
                     if self._zeros is None or self._zeros.numel() < n * self.P:
                         self._zeros = torch.zeros(n * self.P, device=self.device)
                         self._acts = torch.zeros((n * self.P, 12), dtype=torch.int32, device=self.device)
                     z = self._zeros[:n * self.P]
                     base = (r * nb * n + j * n) * self.P  # global agent slot of the buffer's first row
-                    self.store.store(w, st[:, 0:4].contiguous().view(torch.float32).view(-1), st[:, 4], st[:, 6],
-                                     self._acts[:n * self.P], z, z, step=s + 1, env_id_base=base,
-                                     engine=self.engines[j])
-            if self.store is not None:
+                    st = sm.view(-1)  # 8 B per agent: reward f32 | term | trunc | mask | pad
+                    batch.append((w, st, st[4:], st[6:], self._acts[:n * self.P], z, z, base))
+            if self.store is not None:  # every buffer of the step as one store (fixed launch count)
+                self.store.reset()
+                for k in range(0, len(batch), 16):
+                    self.store.store_many(batch[k:k + 16], s + 1, self.engines[0], field_stride=8)
                 self._stored += self.store.ptr_dev[0].to(torch.int64)
         if self.on_step is not None:
             torch.cuda.synchronize(self.device)

@@ -172,6 +172,33 @@ class DeviceExperience:
         # keep the inputs alive until the kernels that read them have been enqueued
         self._inflight = (r_, d_, m_, lp, v, a, eid, obs_flat, obs_nat, obs_wire)
 
+    def store_many(self, inputs, step: int, engine, field_stride: int = 0):
+        """Several wire buffers stored as one store, in input order (compact storage only;
+        nmmo_exp_store_records_many: a fixed number of launches for up to 16 buffers, e.g. every
+        rank's buffers of a step at the learner). inputs: (wire, rewards, dones, mask, actions,
+        logprobs, values, env_id_base) per buffer, all device tensors already in their final
+        dtype; field_stride > 0: rewards / dones / mask are byte views read field_stride bytes
+        apart per row (the gather's packed 8-B per-agent smalls)."""
+        if self.records is None:
+            raise ValueError("store_many needs compact (record) storage")
+        n = len(inputs)
+        arr = (abi.NmmoStoreInput * n)()
+        rows = 0
+        keep = []
+        for i, (w, r, d, m, a, lp, v, base) in enumerate(inputs):
+            nr = a.shape[0]
+            rows += nr
+            arr[i] = abi.NmmoStoreInput(nr, int(step), None, None, r.data_ptr(), d.data_ptr(), m.data_ptr(), None,
+                                        int(base), a.data_ptr(), lp.data_ptr(), v.data_ptr(), w.data_ptr())
+            keep.append((w, r, d, m, a, lp, v))
+        self._ensure_scratch(rows)
+        self._engine = engine
+        with torch.cuda.device(self.device):
+            check(lib().nmmo_exp_store_records_many(engine.h, ctypes.byref(self.x), ctypes.byref(self.records), arr, n,
+                                                    int(field_stride), _p(self.scratch), self._stream()),
+                  "nmmo_exp_store_records_many")
+        self._inflight = keep
+
     # -- train side (clean_pufferl.py:413-458)
     def sort(self) -> torch.Tensor:
         """idxs: the stored rows sorted by (env_id, step) (:414), device int32 [ptr]."""

@@ -225,6 +225,52 @@ def test_record_store_gathers_the_flat_store_rows():
     wir.close()
 
 
+def test_record_store_many_equals_sequential_stores():
+    """nmmo_exp_store_records_many (every buffer of a step in one store, the gather root's call,
+    rewards / dones / mask read from 8-B packed per-agent records) keeps exactly the rows, fields
+    and gathered observations of one nmmo_exp_store_records call per buffer in the same order."""
+    from nmmo_amd import abi
+    from nmmo_amd.config import Config
+    from nmmo_amd.engine import NmmoEngine
+    from nmmo_amd.storage import DeviceExperience
+
+    cfg = Config.preset("C4", MAP_N=4, early_stop_agent_num=8, obs_layout=abi.OBS_WIRE)
+    engs = [NmmoEngine(cfg, 3, seed=12, env_index_base=3 * i) for i in range(2)]
+    P = engs[0].P
+    for e in engs:
+        e.reset()
+    n = 3 * P
+    seq = DeviceExperience(1500, engs[0].obs_elems, 2 * n, device=engs[0].device, record_arena_bytes=64 << 20)
+    many = DeviceExperience(1500, engs[0].obs_elems, 2 * n, device=engs[0].device, record_arena_bytes=64 << 20)
+    g = torch.Generator(device="cpu").manual_seed(6)
+    acts = torch.zeros((n, 12), dtype=torch.int32, device=engs[0].device)
+    for t in range(8):
+        batch = []
+        for i, e in enumerate(engs):
+            e.scripted_actions(90 + t)
+            e.step()
+            keep = (e.mask.view(-1) != 0) & (torch.rand(n, generator=g) < 0.7).to(e.device)
+            lp = torch.randn(n, generator=g).to(e.device)
+            sm = torch.zeros((n, 8), dtype=torch.uint8, device=e.device)
+            sm[:, 0:4] = e.rew.view(-1).view(torch.uint8).view(n, 4)
+            sm[:, 4] = e.term.view(-1)
+            sm[:, 6] = keep.to(torch.uint8)
+            seq.store(e.obs, e.rew.view(-1), e.term.view(-1), keep, acts, lp, lp, step=t, env_id_base=i * n,
+                      engine=e)
+            st = sm.view(-1)
+            batch.append((e.obs.clone(), st, st[4:], st[6:], acts, lp, lp, i * n))
+        many.store_many(batch, t, engs[0], field_stride=8)
+    torch.cuda.synchronize()
+    k = seq.ptr
+    assert many.ptr == k == 1501 and many.status == 0 and seq.status == 0
+    for name in ("actions", "rewards", "dones", "logprobs", "values", "env_id", "step", "seq", "row_agent"):
+        assert torch.equal(getattr(seq, name)[:k], getattr(many, name)[:k]), name
+    idx = torch.arange(k, dtype=torch.int32, device=engs[0].device)
+    assert torch.equal(seq.gather_obs(idx), many.gather_obs(idx))
+    for e in engs:
+        e.close()
+
+
 def test_wire_pack_rejects_stale_native():
     """nmmo_wire_pack refuses a native buffer a tick without an obs gather has made stale, or
     one that is not the buffer the last gather wrote."""
