@@ -19,7 +19,11 @@ namespace nmmo {
 // 32 agents per workgroup, 8 waves (the native kernel's 16 / 4): the per-workgroup prologue
 // (entity staging, record offsets, table indices) is long next to ~0.3 KB records, so twice the
 // agents per prologue: same box, 0.089 -> 0.083 ms per 512 envs, C5 at N = 1 368 -> 375 M.
-constexpr int kWoWaves = 8, kWoAgents = 32;
+#ifndef NMMO_WO_WAVES  // (A/B knobs: tools/debug/variants.py)
+#define NMMO_WO_WAVES 8
+#define NMMO_WO_AGENTS 32
+#endif
+constexpr int kWoWaves = NMMO_WO_WAVES, kWoAgents = NMMO_WO_AGENTS;
 
 // LDS: agent_obs.h's entity staging | per-wave visible rows | per-wave window materials | the
 // env's record offsets | the slots' entity-table indices. 34 KB at S = 384.
@@ -111,6 +115,9 @@ __global__ void __launch_bounds__(64 * kWoWaves) wire_obs_kernel(ObsParams p) {
   };
   if (in_realm(0)) prefetch(abase);
 
+#ifdef NMMO_WO_ABLATE_LOOP  // diagnostic timing only (no records written): the prologue alone
+  if (p.S != 12345) return;
+#endif
   for (int j = 0; j < per_wave; j++) {
     const int a = abase + kWoWaves * j;
     if (a >= P) break;

@@ -21,3 +21,7 @@ if [ "$1" = "abflat" ]; then
 L=nmmo_amd/lib
 timeout -k 10 900 bash tools/ab_obs.sh C4 $L/libnmmo_hip.so,$L/libnmmo_hip_obsw4.so,$L/libnmmo_hip_obst16.so,$L/libnmmo_hip_obst16w4.so > gpurun_out/ab_flat.txt 2>&1
 fi
+if [ "$1" = "abwire" ]; then
+L=nmmo_amd/lib
+timeout -k 10 900 bash tools/ab_obs.sh C5 $L/libnmmo_hip.so,$L/libnmmo_hip_wo16w64.so,$L/libnmmo_hip_wo16w128.so,$L/libnmmo_hip_wonoloop.so --no-decode > gpurun_out/ab_wire.txt 2>&1
+fi
