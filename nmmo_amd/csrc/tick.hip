@@ -169,14 +169,11 @@ constexpr size_t kPlayerArrBytes = 4 * 256 + 128;  // kill, order, ev_dmg, ev_lv
 __host__ __device__ inline bool uses_grid(uint32_t systems) {
   return (systems & (NMMO_SYS_COMBAT | NMMO_SYS_ITEM | NMMO_SYS_NPC)) != 0;
 }
-// the Buy / Give rounds' per-player scratch, after the round keys and clist: position, first
-// owner / targets (int16 x 2), the bought item word, price | owner << 16
-constexpr size_t kRoundScratch = 128 * 2 * 2 + 128 * 8 + 128 * 4;
 __host__ __device__ inline size_t union_lds_bytes(int S, bool grid) {
   auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
   size_t u = (size_t)128 * ((S + 63) / 64) * 8 + (grid ? grid_lds_bytes(S) : 0);
   u = u > 2 * kHash * 4 ? u : 2 * kHash * 4;
-  const size_t atk = al((size_t)S * 8) + al((size_t)S * 2) + kRoundScratch;  // round keys [2][S] | clist | scratch
+  const size_t atk = al((size_t)S * 8) + al((size_t)S * 2);  // round keys [2][S] | clist
   return u > atk ? u : atk;
 }
 
@@ -1060,14 +1057,35 @@ __device__ __forceinline__ void loot(Ctx& c, int x, int t, int& evn) {
   }
   if (!c.items) return;
   if (t < c.P) {
-    uint2* inv = c.inv + t * kInv;
-    while (it_type(inv[0])) {
-      uint2 w = inv[0];
-      if (c.evcap) ev_put(c, evn++, x, EV_LOOT_ITEM, it_type(w), it_level(w), it_qty(w), 0, TF(F_ID, t));
+    // the victim's items in slot order into the killer's inventory (receive_moved each), both
+    // inventories in registers (common.h InvR): the slot loops' dependent LDS reads made a
+    // 12-item loot ~30k cycles of the serial phase
+    uint2* vinv = c.inv + t * kInv;
+    uint2* kinv = c.inv + x * kInv;
+    const InvR vi = invr_load(vinv);
+    InvR ki = invr_load(kinv);
+    const int tid_t = TF(F_ID, t);
+#pragma unroll
+    for (int j = 0; j < kInv; j++) {
+      uint2 w = vi.w[j];
+      if (!it_type(w)) break;  // (the occupied prefix)
+      if (c.evcap) ev_put(c, evn++, x, EV_LOOT_ITEM, it_type(w), it_level(w), it_qty(w), 0, tid_t);
       w.x &= 0x1FFu;  // unequipped, unlisted
-      inv_remove(inv, 0);
-      receive_moved(c, x, w);
+      const int stk = invr_stack(ki, it_type(w), it_level(w));
+      if (stk >= 0) {
+        invr_add_qty(ki, stk, (uint32_t)it_qty(w));
+        ifree(c, it_row(w));
+      } else if (invr_count(ki) >= kInv) {
+        ifree(c, it_row(w));
+      } else {
+        invr_insert(ki, w);
+      }
     }
+    invr_save(kinv, ki);
+    InvR empty;
+#pragma unroll
+    for (int j = 0; j < kInv; j++) empty.w[j] = make_uint2(0u, 0u);
+    invr_save(vinv, empty);
     update_item_level(c, t);
   } else {
     const int lvl = TF(F_NPC_LEVEL, t) > 0 ? TF(F_NPC_LEVEL, t) : 1;
@@ -1699,90 +1717,75 @@ __device__ __forceinline__ void tick_env(Ctx& c, Heads hd, float* rew, uint8_t* 
         if (tid < 8) okm[tid] = 0u;  // okm and frm
         if (tid < 3) anyf[tid] = 0;
         __syncthreads();
-        // per-player scratch after the round keys (union_lds_bytes): shuffled position, first owner,
-        // and the bought item word / price | owner of each successful buy
-        int16_t* bpos = c.clist + S + ((8 - (S & 7)) & 7);  // (16-B aligned: clist is S int16)
-        int16_t* bown = bpos + 128;
-        uint2* bwl = reinterpret_cast<uint2*>(bown + 128);
-        int* bpo = reinterpret_cast<int*>(bwl + 128);
-        int pos = 0;
+        int pos = 0, owner0 = -1;
+        const int brow = isb ? c.a_buy[s] : -1;
         if (isb) {
           const uint32_t key = c.ikey[s];
           for (int q = 0; q < P; q++)
             if (c.a_buy[q] >= 0) pos += (c.ikey[q] < key || (c.ikey[q] == key && q < s)) ? 1 : 0;
-          bpos[s] = (int16_t)pos;
-          bown[s] = (int16_t)(c.rmap[c.a_buy[s]] & 255);  // a listed row at tick start (kth_listed)
+          owner0 = c.rmap[brow] & 255;  // a listed row at tick start (kth_listed)
         }
-        __syncthreads();
-        // The rounds run in wave 0 alone, two players per lane (slots lane, lane + 64): a round is
-        // then one ballot and wave-ordered LDS accesses instead of a block barrier (a hot seller's
-        // buyers chain one round each: the slowest envs spent 7.5k cycles here, p99 27k).
-        if (wave_id() == 0) {
-          const int lane = lane_id();
-          bool act[2];
-          int ps[2], ow[2];
-#pragma unroll
-          for (int h = 0; h < 2; h++) {
-            const int q = lane + 64 * h;
-            const bool b = q < P && c.a_buy[q] >= 0;
-            ps[h] = b ? bpos[q] : 0;
-            ow[h] = b ? bown[q] : -1;
-            act[h] = b && acts(c, q) && ow[h] != q;  // the others fail without effect
-            if (q < P) bpo[q] = -1;
+        bool active = isb && acts(c, s) && owner0 != s;  // the others fail without effect
+        bool ok = false;
+        uint2 bw = make_uint2(0u, 0u);
+        int bprice = 0, bowner = -1;
+        for (int round = 1;; round++) {
+          if (round > P + 1) {  // <= nbuy rounds (the earliest pending buy runs in every round)
+            if (tid == 0) tick_fault(c, NMMO_FAULT_BUY_ROUNDS);
+            break;
           }
-          for (int round = 1;; round++) {
-            if (round > P + 1) {  // <= nbuy rounds (the earliest pending buy runs in every round)
-              if (lane == 0) tick_fault(c, NMMO_FAULT_BUY_ROUNDS);
-              break;
-            }
-            int* mr = mi + (round & 1) * S;
-#pragma unroll
-            for (int h = 0; h < 2; h++)
-              if (act[h]) {
-                const int key = (round << 16) | (0xFFFF - ps[h]);
-                atomicMax(&mr[lane + 64 * h], key);
-                atomicMax(&mr[ow[h]], key);
-              }
-            if (__ballot(act[0] || act[1]) == 0) break;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-            for (int h = 0; h < 2; h++) {
-              const int q = lane + 64 * h, key = (round << 16) | (0xFFFF - ps[h]);
-              if (!(act[h] && mr[q] == key && mr[ow[h]] == key)) continue;
-              act[h] = false;
-              const int brow = c.a_buy[q];
-              const int owner = c.rmap[brow] < 0 ? -1 : (c.rmap[brow] & 255);
-              uint2* oinv = c.inv + (owner >= 0 ? owner : 0) * kInv;
-              const int k = owner >= 0 && owner != q ? inv_find(oinv, brow) : -1;
-              if (k < 0) continue;
-              uint2 w = oinv[k];
+          const int key = (round << 16) | (0xFFFF - pos);
+          int* mr = mi + (round & 1) * S;
+          if (active) {
+            atomicMax(&mr[s], key);
+            atomicMax(&mr[owner0], key);
+            anyf[round % 3] = 1;
+          }
+          if (tid == 0) anyf[(round + 1) % 3] = 0;
+          __syncthreads();
+          if (!anyf[round % 3]) break;
+          if (active && mr[s] == key && mr[owner0] == key) {
+            active = false;
+            const int owner = c.rmap[brow] < 0 ? -1 : (c.rmap[brow] & 255);
+            // both inventories in registers (inv_find / has_room / inv_remove /
+            // receive_moved_deferred on them: common.h InvR)
+            uint2* oinv = c.inv + (owner >= 0 ? owner : 0) * kInv;
+            uint2* binv = c.inv + s * kInv;
+            InvR oi = invr_load(oinv), bi = invr_load(binv);
+            const int k = owner >= 0 && owner != s ? invr_find(oi, brow) : -1;
+            if (k >= 0) {
+              uint2 w = invr_get(oi, k);
               const int price = it_price(w);
-              if (!(price && TF(F_GOLD, q) >= price && has_room(c, q, w))) continue;
-              TF(F_GOLD, q) = (int16_t)(TF(F_GOLD, q) - price);
-              TF(F_GOLD, owner) = (int16_t)(TF(F_GOLD, owner) + price);
-              bwl[q] = w;
-              bpo[q] = price | owner << 16;
-              w.x &= 0x1FFu;
-              inv_remove(oinv, k);
-              int freed = -1;
-              c.rmap[brow] = receive_moved_deferred(c, q, w, freed) ? (int16_t)q : (int16_t)-1;
-              atomicOr(&okm[ps[h] >> 5], 1u << (ps[h] & 31));
-              if (freed >= 0) {
-                frow[ps[h]] = (int16_t)freed;
-                atomicOr(&frm[ps[h] >> 5], 1u << (ps[h] & 31));
+              const int stk = invr_stack(bi, it_type(w), it_level(w));
+              if (price && TF(F_GOLD, s) >= price && (stk >= 0 || invr_count(bi) < kInv)) {
+                TF(F_GOLD, s) = (int16_t)(TF(F_GOLD, s) - price);
+                TF(F_GOLD, owner) = (int16_t)(TF(F_GOLD, owner) + price);
+                bw = w;
+                bprice = price;
+                bowner = owner;
+                ok = true;
+                w.x &= 0x1FFu;
+                invr_remove(oi, k);
+                invr_save(oinv, oi);
+                int freed = -1;
+                if (stk >= 0) {  // stacks onto the buyer's ammunition: the row is freed
+                  invr_add_qty(bi, stk, (uint32_t)it_qty(w));
+                  freed = it_row(w);
+                } else {
+                  invr_insert(bi, w);
+                }
+                invr_save(binv, bi);
+                c.rmap[brow] = stk < 0 ? (int16_t)s : (int16_t)-1;
+                atomicOr(&okm[pos >> 5], 1u << (pos & 31));
+                if (freed >= 0) {
+                  frow[pos] = (int16_t)freed;
+                  atomicOr(&frm[pos >> 5], 1u << (pos & 31));
+                }
               }
             }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
           }
         }
-        __syncthreads();  // publishes okm / frm / frow and the per-player results
-        const bool ok = isb && bpo[s] >= 0;
-        const uint2 bw = ok ? bwl[s] : make_uint2(0u, 0u);
-        const int bprice = ok ? (bpo[s] & 0xFFFF) : 0, bowner = ok ? (bpo[s] >> 16) : -1;
+        // (the loop's last barrier published okm / frm / frow)
         auto below = [&](const uint32_t* m) {
           int n = 0;
 #pragma unroll
@@ -1828,79 +1831,58 @@ __device__ __forceinline__ void tick_env(Ctx& c, Heads hd, float* rew, uint8_t* 
         if (tid < 3) anyf[tid] = 0;
         __syncthreads();
         const int tg = isg ? c.a_givet[s] : -1, tg2 = isg ? c.a_ggt[s] : -1;
-        // the rounds run in wave 0 alone, two players per lane (as the Buy rounds), results per
-        // player in the scratch after the round keys: the given item word, and freed row + 1 |
-        // item given << 16 | gold given << 17
-        uint2* gwl = reinterpret_cast<uint2*>(c.clist + S + ((8 - (S & 7)) & 7) + 256);
-        int* gres = reinterpret_cast<int*>(gwl + 128);
-        if (wave_id() == 0) {
-          const int lane = lane_id();
-          bool act[2], r1[2], r2[2];
-          int t1[2], t2[2];
-#pragma unroll
-          for (int h = 0; h < 2; h++) {
-            const int q = lane + 64 * h;
-            const bool g = q < P && (c.a_givet[q] >= 0 || c.a_ggt[q] >= 0);
-            t1[h] = g ? c.a_givet[q] : -1;
-            t2[h] = g ? c.a_ggt[q] : -1;
-            r1[h] = t1[h] >= 0 && t1[h] < P && t1[h] != q;
-            r2[h] = t2[h] >= 0 && t2[h] < P && t2[h] != q;
-            act[h] = g && acts(c, q) && (r1[h] || r2[h]);  // the others fail without effect
-            if (q < P) gres[q] = 0;
+        const bool r1 = tg >= 0 && tg < P && tg != s, r2 = tg2 >= 0 && tg2 < P && tg2 != s;
+        bool active = isg && acts(c, s) && (r1 || r2);  // the others fail without effect
+        bool did_item = false, did_gold = false;
+        uint2 gw = make_uint2(0u, 0u);
+        int freed = -1;
+        for (int round = 1;; round++) {
+          if (round > P + 1) {  // <= ng rounds (the lowest pending give runs in every round)
+            if (tid == 0) tick_fault(c, NMMO_FAULT_GIVE_ROUNDS);
+            break;
           }
-          for (int round = 1;; round++) {
-            if (round > P + 1) {  // <= ng rounds (the lowest pending give runs in every round)
-              if (lane == 0) tick_fault(c, NMMO_FAULT_GIVE_ROUNDS);
-              break;
-            }
-            int* mr = mi + (round & 1) * S;
-#pragma unroll
-            for (int h = 0; h < 2; h++)
-              if (act[h]) {
-                const int q = lane + 64 * h, key = (round << 16) | (0xFFFF - q);
-                atomicMax(&mr[q], key);
-                if (r1[h]) atomicMax(&mr[t1[h]], key);
-                if (r2[h]) atomicMax(&mr[t2[h]], key);
-              }
-            if (__ballot(act[0] || act[1]) == 0) break;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-            for (int h = 0; h < 2; h++) {
-              const int q = lane + 64 * h, key = (round << 16) | (0xFFFF - q);
-              if (!(act[h] && mr[q] == key && (!r1[h] || mr[t1[h]] == key) && (!r2[h] || mr[t2[h]] == key)))
-                continue;
-              act[h] = false;
-              int res = 0, fr = -1;
-              if (r1[h] && acts(c, t1[h]) && same_tile(c, t1[h], q)) {
-                uint2* inv = c.inv + q * kInv;
-                const int k = inv_find(inv, c.a_give[q]);
-                if (k >= 0 && !it_equipped(inv[k]) && !it_price(inv[k]) && has_room(c, t1[h], inv[k])) {
-                  const uint2 w = inv[k];
-                  gwl[q] = w;
-                  res |= 1 << 16;
-                  inv_remove(inv, k);
-                  receive_moved_deferred(c, t1[h], w, fr);
+          const int key = (round << 16) | (0xFFFF - s);
+          int* mr = mi + (round & 1) * S;
+          if (active) {
+            atomicMax(&mr[s], key);
+            if (r1) atomicMax(&mr[tg], key);
+            if (r2) atomicMax(&mr[tg2], key);
+            anyf[round % 3] = 1;
+          }
+          if (tid == 0) anyf[(round + 1) % 3] = 0;
+          __syncthreads();
+          if (!anyf[round % 3]) break;
+          if (active && mr[s] == key && (!r1 || mr[tg] == key) && (!r2 || mr[tg2] == key)) {
+            active = false;
+            if (r1 && acts(c, tg) && same_tile(c, tg, s)) {  // both inventories in registers (InvR)
+              uint2* inv = c.inv + s * kInv;
+              uint2* tinv = c.inv + tg * kInv;
+              InvR gi = invr_load(inv), ti = invr_load(tinv);
+              const int k = invr_find(gi, c.a_give[s]);
+              const uint2 w = invr_get(gi, k);
+              const int stk = k >= 0 ? invr_stack(ti, it_type(w), it_level(w)) : -1;
+              if (k >= 0 && !it_equipped(w) && !it_price(w) && (stk >= 0 || invr_count(ti) < kInv)) {
+                gw = w;
+                did_item = true;
+                invr_remove(gi, k);
+                invr_save(inv, gi);
+                if (stk >= 0) {  // stacks onto the target's ammunition: the row is freed
+                  invr_add_qty(ti, stk, (uint32_t)it_qty(w));
+                  freed = it_row(w);
+                } else {
+                  invr_insert(ti, w);
                 }
+                invr_save(tinv, ti);
               }
-              if (r2[h] && acts(c, t2[h]) && c.a_gga[q] <= TF(F_GOLD, q) && same_tile(c, t2[h], q)) {
-                TF(F_GOLD, q) = (int16_t)(TF(F_GOLD, q) - c.a_gga[q]);
-                TF(F_GOLD, t2[h]) = (int16_t)(TF(F_GOLD, t2[h]) + c.a_gga[q]);
-                res |= 1 << 17;
-              }
-              gres[q] = res | (fr + 1);
             }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (r2 && acts(c, tg2) && c.a_gga[s] <= TF(F_GOLD, s) && same_tile(c, tg2, s)) {
+              TF(F_GOLD, s) = (int16_t)(TF(F_GOLD, s) - c.a_gga[s]);
+              TF(F_GOLD, tg2) = (int16_t)(TF(F_GOLD, tg2) + c.a_gga[s]);
+              did_gold = true;
+            }
           }
         }
-        __syncthreads();  // publishes every give's result
-        const int gr = isg ? gres[s] : 0;
-        const bool did_item = (gr >> 16) & 1, did_gold = (gr >> 17) & 1;
-        const int freed = (gr & 0xFFFF) - 1;
-        const uint2 gw = did_item ? gwl[s] : make_uint2(0u, 0u);
+        // (the loop's last barrier ordered every give before these reads)
         const int fb = c.E[E_ITEM_FREE_HEAD] + c.E[E_ITEM_FREE_COUNT];
         const int nev = evon ? (int)did_item + (int)did_gold : 0;
         int tot;
