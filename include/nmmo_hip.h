@@ -445,6 +445,7 @@ NMMO_API int nmmo_read_timing(NmmoHandle* h, double* ms /* [3] */, int32_t* n);
 #define NMMO_FAULT_GIVE_ROUNDS 3
 #define NMMO_FAULT_HASH_PROBE 4
 #define NMMO_FAULT_ENV_LIST 5   /* nmmo_step_envs: an env id outside [0, n_envs) (dropped) */
+#define NMMO_FAULT_WIRE_SCAN 6  /* NMMO_OBS_WIRE: an env's payload offset never resolved (bounded wait) */
 NMMO_API int nmmo_get_fault(NmmoHandle* h, int32_t* fault);
 /* The fault word without a host sync: when the word is non-zero and *dev_dst (device int32) is
  * 0, the word is copied into it (the first fault of several handles is kept). The word is not

@@ -20,8 +20,9 @@ FAULT_BUY_ROUNDS = 2
 FAULT_GIVE_ROUNDS = 3
 FAULT_HASH_PROBE = 4
 FAULT_ENV_LIST = 5
+FAULT_WIRE_SCAN = 6
 FAULT_NAMES = {1: "attack rounds", 2: "Buy rounds", 3: "Give rounds", 4: "position-hash probe",
-               5: "env id outside the handle (nmmo_step_envs)"}
+               5: "env id outside the handle (nmmo_step_envs)", 6: "wire payload offset scan"}
 
 SYS_RESOURCE = 1 << 0
 SYS_COMBAT = 1 << 1
