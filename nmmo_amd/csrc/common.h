@@ -238,92 +238,6 @@ __device__ inline int inv_stack(const uint2* inv, int type, int level) {  // amm
   return -1;
 }
 
-// An inventory held in registers: six 16-B LDS reads in flight instead of the slot-by-slot
-// dependent reads of the helpers above (each ~LDS latency), and every query / edit as unrolled
-// selects (no dynamic register indexing). A Buy / Give chains its buyer's and seller's inventory
-// queries serially; with the slot loops one executed buy cost ~4k cycles.
-struct InvR {
-  uint2 w[kInv];
-};
-static_assert(kInv == 12, "six 16-B words per inventory");
-__device__ __forceinline__ InvR invr_load(const uint2* inv) {  // inv: 16-B aligned
-  InvR r;
-  const uint4* p = reinterpret_cast<const uint4*>(inv);
-#pragma unroll
-  for (int i = 0; i < kInv / 2; i++) {
-    const uint4 q = p[i];
-    r.w[2 * i] = make_uint2(q.x, q.y);
-    r.w[2 * i + 1] = make_uint2(q.z, q.w);
-  }
-  return r;
-}
-__device__ __forceinline__ void invr_save(uint2* inv, const InvR& r) {
-  uint4* p = reinterpret_cast<uint4*>(inv);
-#pragma unroll
-  for (int i = 0; i < kInv / 2; i++) p[i] = make_uint4(r.w[2 * i].x, r.w[2 * i].y, r.w[2 * i + 1].x, r.w[2 * i + 1].y);
-}
-__device__ __forceinline__ int invr_count(const InvR& r) {
-  int n = 0;
-  bool run = true;
-#pragma unroll
-  for (int j = 0; j < kInv; j++) {
-    run = run && it_type(r.w[j]) != 0;
-    n += run ? 1 : 0;
-  }
-  return n;
-}
-__device__ __forceinline__ int invr_find(const InvR& r, int row) {  // inv_find
-  int k = -1;
-  bool run = true;
-#pragma unroll
-  for (int j = 0; j < kInv; j++) {
-    run = run && it_type(r.w[j]) != 0;
-    if (run && k < 0 && it_row(r.w[j]) == row) k = j;
-  }
-  return k;
-}
-__device__ __forceinline__ int invr_stack(const InvR& r, int type, int level) {  // inv_stack
-  if (type < T_WHETSTONE || type > T_RUNES) return -1;
-  int k = -1;
-  bool run = true;
-#pragma unroll
-  for (int j = 0; j < kInv; j++) {
-    run = run && it_type(r.w[j]) != 0;
-    if (run && k < 0 && it_type(r.w[j]) == type && it_level(r.w[j]) == level) k = j;
-  }
-  return k;
-}
-__device__ __forceinline__ uint2 invr_get(const InvR& r, int k) {
-  uint2 x = make_uint2(0u, 0u);
-#pragma unroll
-  for (int j = 0; j < kInv; j++)
-    if (j == k) x = r.w[j];
-  return x;
-}
-__device__ __forceinline__ void invr_add_qty(InvR& r, int k, uint32_t q) {
-#pragma unroll
-  for (int j = 0; j < kInv; j++)
-    if (j == k) r.w[j].y += q;
-}
-__device__ __forceinline__ void invr_remove(InvR& r, int k) {  // inv_remove
-#pragma unroll
-  for (int j = 0; j < kInv - 1; j++) r.w[j] = j >= k ? r.w[j + 1] : r.w[j];
-  r.w[kInv - 1] = make_uint2(0u, 0u);
-}
-__device__ __forceinline__ void invr_insert(InvR& r, uint2 w) {  // inv_insert (the caller checked room)
-  // its place: after every occupied slot whose row is below w's (the slots ascend by row)
-  int p = 0;
-  bool run = true;
-#pragma unroll
-  for (int j = 0; j < kInv; j++) {
-    run = run && it_type(r.w[j]) != 0;
-    p += run && it_row(r.w[j]) < it_row(w) ? 1 : 0;
-  }
-#pragma unroll
-  for (int j = kInv - 1; j > 0; j--) r.w[j] = j > p ? r.w[j - 1] : j == p ? w : r.w[j];
-  if (p == 0) r.w[0] = w;
-}
-
 // lane `lane` of `old` <- the wave-uniform `val`: v_cmp + v_cndmask. (An inline-asm
 // v_writelane_b32 with the lane select in M0 is one op cheaper but mis-set ~1 in 10^3 masks on
 // gfx950 — a hazard the compiler's recognizer cannot see inside asm — so it is not used.)

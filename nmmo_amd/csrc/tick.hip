@@ -1057,35 +1057,14 @@ __device__ __forceinline__ void loot(Ctx& c, int x, int t, int& evn) {
   }
   if (!c.items) return;
   if (t < c.P) {
-    // the victim's items in slot order into the killer's inventory (receive_moved each), both
-    // inventories in registers (common.h InvR): the slot loops' dependent LDS reads made a
-    // 12-item loot ~30k cycles of the serial phase
-    uint2* vinv = c.inv + t * kInv;
-    uint2* kinv = c.inv + x * kInv;
-    const InvR vi = invr_load(vinv);
-    InvR ki = invr_load(kinv);
-    const int tid_t = TF(F_ID, t);
-#pragma unroll
-    for (int j = 0; j < kInv; j++) {
-      uint2 w = vi.w[j];
-      if (!it_type(w)) break;  // (the occupied prefix)
-      if (c.evcap) ev_put(c, evn++, x, EV_LOOT_ITEM, it_type(w), it_level(w), it_qty(w), 0, tid_t);
+    uint2* inv = c.inv + t * kInv;
+    while (it_type(inv[0])) {
+      uint2 w = inv[0];
+      if (c.evcap) ev_put(c, evn++, x, EV_LOOT_ITEM, it_type(w), it_level(w), it_qty(w), 0, TF(F_ID, t));
       w.x &= 0x1FFu;  // unequipped, unlisted
-      const int stk = invr_stack(ki, it_type(w), it_level(w));
-      if (stk >= 0) {
-        invr_add_qty(ki, stk, (uint32_t)it_qty(w));
-        ifree(c, it_row(w));
-      } else if (invr_count(ki) >= kInv) {
-        ifree(c, it_row(w));
-      } else {
-        invr_insert(ki, w);
-      }
+      inv_remove(inv, 0);
+      receive_moved(c, x, w);
     }
-    invr_save(kinv, ki);
-    InvR empty;
-#pragma unroll
-    for (int j = 0; j < kInv; j++) empty.w[j] = make_uint2(0u, 0u);
-    invr_save(vinv, empty);
     update_item_level(c, t);
   } else {
     const int lvl = TF(F_NPC_LEVEL, t) > 0 ? TF(F_NPC_LEVEL, t) : 1;
@@ -1747,17 +1726,12 @@ __device__ __forceinline__ void tick_env(Ctx& c, Heads hd, float* rew, uint8_t* 
           if (active && mr[s] == key && mr[owner0] == key) {
             active = false;
             const int owner = c.rmap[brow] < 0 ? -1 : (c.rmap[brow] & 255);
-            // both inventories in registers (inv_find / has_room / inv_remove /
-            // receive_moved_deferred on them: common.h InvR)
             uint2* oinv = c.inv + (owner >= 0 ? owner : 0) * kInv;
-            uint2* binv = c.inv + s * kInv;
-            InvR oi = invr_load(oinv), bi = invr_load(binv);
-            const int k = owner >= 0 && owner != s ? invr_find(oi, brow) : -1;
+            const int k = owner >= 0 && owner != s ? inv_find(oinv, brow) : -1;
             if (k >= 0) {
-              uint2 w = invr_get(oi, k);
+              uint2 w = oinv[k];
               const int price = it_price(w);
-              const int stk = invr_stack(bi, it_type(w), it_level(w));
-              if (price && TF(F_GOLD, s) >= price && (stk >= 0 || invr_count(bi) < kInv)) {
+              if (price && TF(F_GOLD, s) >= price && has_room(c, s, w)) {
                 TF(F_GOLD, s) = (int16_t)(TF(F_GOLD, s) - price);
                 TF(F_GOLD, owner) = (int16_t)(TF(F_GOLD, owner) + price);
                 bw = w;
@@ -1765,17 +1739,9 @@ __device__ __forceinline__ void tick_env(Ctx& c, Heads hd, float* rew, uint8_t* 
                 bowner = owner;
                 ok = true;
                 w.x &= 0x1FFu;
-                invr_remove(oi, k);
-                invr_save(oinv, oi);
+                inv_remove(oinv, k);
                 int freed = -1;
-                if (stk >= 0) {  // stacks onto the buyer's ammunition: the row is freed
-                  invr_add_qty(bi, stk, (uint32_t)it_qty(w));
-                  freed = it_row(w);
-                } else {
-                  invr_insert(bi, w);
-                }
-                invr_save(binv, bi);
-                c.rmap[brow] = stk < 0 ? (int16_t)s : (int16_t)-1;
+                c.rmap[brow] = receive_moved_deferred(c, s, w, freed) ? (int16_t)s : (int16_t)-1;
                 atomicOr(&okm[pos >> 5], 1u << (pos & 31));
                 if (freed >= 0) {
                   frow[pos] = (int16_t)freed;
@@ -1854,25 +1820,14 @@ __device__ __forceinline__ void tick_env(Ctx& c, Heads hd, float* rew, uint8_t* 
           if (!anyf[round % 3]) break;
           if (active && mr[s] == key && (!r1 || mr[tg] == key) && (!r2 || mr[tg2] == key)) {
             active = false;
-            if (r1 && acts(c, tg) && same_tile(c, tg, s)) {  // both inventories in registers (InvR)
+            if (r1 && acts(c, tg) && same_tile(c, tg, s)) {
               uint2* inv = c.inv + s * kInv;
-              uint2* tinv = c.inv + tg * kInv;
-              InvR gi = invr_load(inv), ti = invr_load(tinv);
-              const int k = invr_find(gi, c.a_give[s]);
-              const uint2 w = invr_get(gi, k);
-              const int stk = k >= 0 ? invr_stack(ti, it_type(w), it_level(w)) : -1;
-              if (k >= 0 && !it_equipped(w) && !it_price(w) && (stk >= 0 || invr_count(ti) < kInv)) {
-                gw = w;
+              const int k = inv_find(inv, c.a_give[s]);
+              if (k >= 0 && !it_equipped(inv[k]) && !it_price(inv[k]) && has_room(c, tg, inv[k])) {
+                gw = inv[k];
                 did_item = true;
-                invr_remove(gi, k);
-                invr_save(inv, gi);
-                if (stk >= 0) {  // stacks onto the target's ammunition: the row is freed
-                  invr_add_qty(ti, stk, (uint32_t)it_qty(w));
-                  freed = it_row(w);
-                } else {
-                  invr_insert(ti, w);
-                }
-                invr_save(tinv, ti);
+                inv_remove(inv, k);
+                receive_moved_deferred(c, tg, gw, freed);
               }
             }
             if (r2 && acts(c, tg2) && c.a_gga[s] <= TF(F_GOLD, s) && same_tile(c, tg2, s)) {

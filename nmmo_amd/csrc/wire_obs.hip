@@ -204,6 +204,12 @@ __global__ void __launch_bounds__(64 * kWoWaves) wire_obs_kernel(ObsParams p) {
 // two launches); then the table, the listings and the records. An A/B with the prologue alone
 // (tools/debug/variants.py wonoloop) put the three-kernel path's staging and header passes at 57%
 // of its time. kWeWaves waves, kWeWaves / 128 of the agents each.
+// Measured slower, so it is built only with -DNMMO_WIRE_FUSED (same box, C5, 512-env launches,
+// profiles/r04/ab/ab_wire_fused.txt): 0.167 ms per launch at 16 waves, 0.222 at 8, 0.255 at 4,
+// against 0.086 for count + scan + records. One workgroup per env holds the whole env's
+// critical path (staging, 128 compactions, the id set's prefix, the look-back, 128 records) on
+// one CU, where the record kernel spreads an env over 4 workgroups; at 16 waves LDS and VGPRs
+// leave one workgroup per CU, so 512 envs run in two rounds.
 #ifndef NMMO_WE_WAVES
 #define NMMO_WE_WAVES 16
 #endif
@@ -477,7 +483,7 @@ __global__ void __launch_bounds__(64 * kWeWaves) wire_env_kernel(ObsParams p) {
 hipError_t launch_wire_obs(const ObsParams& p, hipStream_t stream) {
   if (p.S % 8 || p.S > kMaxSlots || p.P > 128 || !p.wire) return hipErrorInvalidValue;
   if (!ao_layout_ok(p)) return hipErrorInvalidValue;  // the wire format's fixed sections
-#ifdef NMMO_WIRE_SPLIT  // the three-kernel path (A/B)
+#ifndef NMMO_WIRE_FUSED  // the three-kernel path (the fused one-kernel path is an A/B variant)
   const hipError_t err = launch_wire_header(p, stream);  // count words, sizes, offsets
   if (err != hipSuccess) return err;
   const dim3 grid(p.n_envs * ((p.P + kWoAgents - 1) / kWoAgents)), block(64 * kWoWaves);  // ao_env_group

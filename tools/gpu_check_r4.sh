@@ -25,3 +25,24 @@ if [ "$1" = "abwire" ]; then
 L=nmmo_amd/lib
 timeout -k 10 900 bash tools/ab_obs.sh C5 $L/libnmmo_hip.so,$L/libnmmo_hip_wo16w64.so,$L/libnmmo_hip_wo16w128.so,$L/libnmmo_hip_wonoloop.so --no-decode > gpurun_out/ab_wire.txt 2>&1
 fi
+if [ "$1" = "quick" ]; then
+timeout -k 10 400 python -u -m pytest tests/test_gpu_wire.py tests/test_gpu_multirank.py tests/test_gpu_faults.py -x -v --timeout 150 --timeout-method thread > gpurun_out/gpu_new.log 2>&1 && \
+timeout -k 10 300 python bench.py --config C5 > gpurun_out/bench_c5.json 2> gpurun_out/bench_c5.err && \
+timeout -k 10 300 python bench.py > gpurun_out/bench_default.json 2> gpurun_out/bench_default.err && \
+STAMPS_STAGGER=64 timeout -k 10 200 python tools/stamps.py C4 512 40 > gpurun_out/stamps_C4.txt 2>&1
+fi
+if [ "$1" = "abwe" ]; then
+L=nmmo_amd/lib
+timeout -k 10 900 bash tools/ab_obs.sh C5 $L/libnmmo_hip.so,$L/libnmmo_hip_wsplit.so,$L/libnmmo_hip_we8.so,$L/libnmmo_hip_we4.so --no-decode > gpurun_out/ab_we.txt 2>&1 && \
+STAMPS_STAGGER=64 timeout -k 10 200 python tools/stamps.py C4 512 40 > gpurun_out/stamps_C4.txt 2>&1 && \
+STAMPS_STAGGER=64 timeout -k 10 200 python tools/stamps.py C3 512 40 > gpurun_out/stamps_C3.txt 2>&1 && \
+STAMPS_STAGGER=64 timeout -k 10 200 python tools/stamps.py C2 128 40 > gpurun_out/stamps_C2.txt 2>&1
+fi
+if [ "$1" = "abtick" ]; then
+L=nmmo_amd/lib
+timeout -k 10 600 bash tools/ab_obs.sh C4 $L/libnmmo_hip.so,$L/libnmmo_hip_tprev.so --obs native > gpurun_out/ab_tick.txt 2>&1 && \
+STAMPS_STAGGER=64 timeout -k 10 200 python tools/stamps.py C4 512 40 > gpurun_out/stamps_C4.txt 2>&1 && \
+NMMO_LIB=$L/libnmmo_hip_tprev_stamps.so NMMO_ALLOW_STALE=1 STAMPS_STAGGER=64 timeout -k 10 200 python tools/stamps.py C4 512 40 > gpurun_out/stamps_C4_prev.txt 2>&1 && \
+STAMPS_STAGGER=64 timeout -k 10 200 python tools/stamps.py C4 512 40 > gpurun_out/stamps_C4_b.txt 2>&1 && \
+timeout -k 10 300 python bench.py --config C5 --no-cpu-baseline > gpurun_out/bench_c5.json 2> gpurun_out/bench_c5.err
+fi

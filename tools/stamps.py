@@ -14,7 +14,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-os.environ["NMMO_LIB"] = os.path.join(ROOT, "nmmo_amd", "lib", "libnmmo_hip_stamps.so")
+os.environ.setdefault("NMMO_LIB", os.path.join(ROOT, "nmmo_amd", "lib", "libnmmo_hip_stamps.so"))
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
