@@ -266,7 +266,7 @@ struct AoSections {
   uint64_t s0, s1[2], s3, s4, s5[2], s6[2], s7[2], s8, s9, s10[2], s11;
 };
 struct AoAgent {
-  int a, r, c, gold, aid, nv, ninv, prev_price;
+  int a, ti, r, c, gold, aid, nv, ninv, prev_price;  // ti: the agent's column index in T
   uint32_t mv;
 };
 template <bool kWrap>
@@ -309,7 +309,7 @@ __device__ __forceinline__ AoSections ao_sections(const ObsParams& p, const int1
   x.s3 = (item ? bfr : 0ull) | 1ull << kInv;
   x.s4 = (item && !no_give ? bfr : 0ull) | 1ull << kInv;
   x.s9 = (exch ? __ballot(have && !it_equipped(it)) : 0ull) | 1ull << kInv;
-  x.s11 = (item ? __ballot(have && item_usable(T, Sp, g.a, it)) : 0ull) | 1ull << kInv;
+  x.s11 = (item ? __ballot(have && item_usable(T, Sp, g.ti, it)) : 0ull) | 1ull << kInv;
   // closed forms: 0 Style, 6 GoldPrice (k < gold), 8 Move, 10 SellPrice (all but the wrapper's
   // last price)
   x.s0 = combat ? low_bits(kSecN[0]) : 0ull;

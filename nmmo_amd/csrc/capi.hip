@@ -61,7 +61,7 @@ struct NmmoHandle {
   uint16_t* d_wcount = nullptr;  // native obs: per-agent wire count words of the last obs (wire.hip)
   int32_t* d_wmcount = nullptr;  // native obs: per-env listing count of the last obs
   uint16_t* d_wrank = nullptr;   // wire obs: per-slot entity-table index (wire_count_kernel)
-  unsigned long long* d_wlook = nullptr;  // wire obs: look-back words of the fused kernel (wire_obs.hip)
+  uint32_t* d_wpk = nullptr;     // wire obs: per-env packed datastore-row words (wire_count_kernel)
   // the native buffer the last obs gather wrote, and whether no tick ran since (nmmo_wire_pack)
   const void* last_native = nullptr;
   bool native_fresh = false;
@@ -184,7 +184,7 @@ void nmmo_destroy(NmmoHandle* h) {
   void* bufs[] = {h->d_env,  h->d_ent,   h->d_ring,  h->d_mat,   h->d_dep,   h->d_bank,
                   h->d_task, h->d_seeds, h->d_items, h->d_iring, h->d_mlist, h->d_mcount,
                   h->d_events, h->d_tasks, h->d_assign, h->d_tstate, h->d_ws, h->d_uniq, h->d_wenv, h->d_wdrop, h->d_task_cum,
-                  h->d_wcount, h->d_wmcount, h->d_wrank, h->d_wlook, h->d_foreign};
+                  h->d_wcount, h->d_wmcount, h->d_wrank, h->d_wpk, h->d_foreign};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   delete h;
@@ -241,7 +241,7 @@ int nmmo_create(const NmmoConfig* cfg, int32_t n_envs, uint64_t seed, int32_t de
   }
   if (cfg->obs_layout == NMMO_OBS_WIRE) {
     ALLOC(h->d_wrank, n * (size_t)kMaxSlots * 2);
-    ALLOC(h->d_wlook, n * 8);
+    ALLOC(h->d_wpk, n * (size_t)kMaxSlots * 4);
   }
 #undef ALLOC
   if (init_kernels() != hipSuccess) return cleanup_fail(fail(NMMO_E_HIP, "kernel attributes"));
@@ -298,7 +298,7 @@ static ObsParams obs_params(NmmoHandle* h, void* obs) {
   p.wcount = native ? h->d_wcount : nullptr;
   p.wmcount = native ? h->d_wmcount : nullptr;
   p.wrank = wire ? h->d_wrank : nullptr;
-  p.wlook = wire ? h->d_wlook : nullptr;
+  p.wpk = wire ? h->d_wpk : nullptr;
   p.fault = h->d_foreign + 1;
   p.ws = h->wrap_on ? h->d_ws : nullptr;
   p.wflags = 0;

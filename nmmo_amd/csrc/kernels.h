@@ -88,7 +88,8 @@ struct ObsParams {
                         // wire_count_kernel -> wire_obs_kernel
   const int32_t* env_list;  // flat / native obs: gather only these envs (DevState::env_list), or NULL
   int n_list;
-  unsigned long long* wlook;  // wire only: [n] the fused kernel's look-back words (zeroed per launch)
+  uint32_t* wpk;        // wire only: [n][kMaxSlots] packed datastore-row words (agent_obs.h ao_pack),
+                        // wire_count_kernel -> wire_obs_kernel
   int32_t* fault;             // DevState::fault (a look-back that never resolves records kFaultWireScan)
 };
 constexpr int kWrapObsPrice = 1, kWrapObsNoGive = 2, kWrapObsNoDangerous = 4;

@@ -139,6 +139,7 @@ __global__ void __launch_bounds__(64 * kAoWaves) native_obs_kernel(ObsParams p) 
     {
       AoAgent ag;
       ag.a = a;
+      ag.ti = a;
       ag.r = r;
       ag.c = c;
       ag.gold = gold;

@@ -63,7 +63,10 @@ __global__ void __launch_bounds__(128) wire_size_kernel(const uint16_t* counts, 
 // entities within the L-inf <= 7 window (itself included; the first 100 in datastore-row order,
 // as the obs kernels' compaction), ninv = its occupied inventory prefix; the env's entity table
 // (the slots some record shows, ranked by id) into p.wrank[e][slot] (0xFFFF = not in it) and
-// ecount[e]; the env's payload bytes into env_off[e] (then wire_scan_kernel).
+// ecount[e]; the env's payload bytes into env_off[e] (then wire_scan_kernel); the packed word of
+// every datastore row (agent_obs.h ao_pack, with the spawn-immune / dangerous / player bits) into
+// p.wpk[e], so the record kernel's workgroups load 2 KB of row words instead of staging the env's
+// 24 KB of Entity columns each.
 __global__ void __launch_bounds__(256) wire_count_kernel(ObsParams p) {
   __shared__ uint32_t pk[kMaxSlots];         // datastore row - 1 -> ao_pack word (agent_obs.h)
   __shared__ uint32_t pos[kMaxSlots];        // slot -> row << 16 | col (agents' windows)
@@ -79,7 +82,7 @@ __global__ void __launch_bounds__(256) wire_count_kernel(ObsParams p) {
   const int e = blockIdx.x, tid = threadIdx.x, lane = lane_id(), S = p.S;
   const int w = __builtin_amdgcn_readfirstlane(wave_id()), nw = blockDim.x >> 6;
   const int16_t* E = p.ent + (size_t)e * NMMO_NF * S;
-  int al[2], ds[2], r_[2], c_[2], id_[2];  // slots tid and tid + 256, loaded ahead of the barrier
+  int al[2], ds[2], r_[2], c_[2], id_[2], ta_[2], nt_[2];  // slots tid and tid + 256, loaded ahead of the barrier
 #pragma unroll
   for (int u = 0; u < 2; u++) {
     const int s = tid + 256 * u;
@@ -88,6 +91,8 @@ __global__ void __launch_bounds__(256) wire_count_kernel(ObsParams p) {
     r_[u] = s < S ? E[F_ROW * S + s] : 0;
     c_[u] = s < S ? E[F_COL * S + s] : 0;
     id_[u] = s < S ? E[F_ID * S + s] : 0;
+    ta_[u] = s < S ? E[F_TIME_ALIVE * S + s] : 0;
+    nt_[u] = s < S ? E[F_NPC_TYPE * S + s] : 0;
   }
   for (int k = tid; k < kMaxSlots; k += blockDim.x) pk[k] = kOut;
   if (tid < kMaxSlots / 32) tab[tid] = 0u;
@@ -110,13 +115,18 @@ __global__ void __launch_bounds__(256) wire_count_kernel(ObsParams p) {
     if (s >= kMaxSlots) continue;
     const bool in = s < S && al[u];
     pos[s] = in ? ((uint32_t)(uint16_t)r_[u] << 16) | (uint32_t)(uint16_t)c_[u] : kOut;
-    if (in && (unsigned)(ds[u] - 1) < (unsigned)S)
-      pk[ds[u] - 1] = ao_pack(s, r_[u], c_[u], false, false, false);
+    if (in && (unsigned)(ds[u] - 1) < (unsigned)S) {
+      const bool player = s < p.P;  // (the flags as agent_obs.h ao_stage)
+      pk[ds[u] - 1] = ao_pack(s, r_[u], c_[u], player && ta_[u] < p.spawn_immunity, nt_[u] > 1, player);
+    }
   }
   __syncthreads();
   uint32_t pr[kMaxSlots / 64];  // this lane's datastore rows 1 + lane + 64 i
 #pragma unroll
-  for (int i = 0; i < kMaxSlots / 64; i++) pr[i] = pk[lane + 64 * i];
+  for (int i = 0; i < kMaxSlots / 64; i++) {
+    pr[i] = pk[lane + 64 * i];
+    if (w == 0) p.wpk[(size_t)e * kMaxSlots + lane + 64 * i] = pr[i];
+  }
   int mine = 0;
   for (int a = w; a < p.P; a += nw) {
     const uint32_t pa = pos[a];

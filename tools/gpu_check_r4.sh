@@ -46,3 +46,14 @@ NMMO_LIB=$L/libnmmo_hip_tprev_stamps.so NMMO_ALLOW_STALE=1 STAMPS_STAGGER=64 tim
 STAMPS_STAGGER=64 timeout -k 10 200 python tools/stamps.py C4 512 40 > gpurun_out/stamps_C4_b.txt 2>&1 && \
 timeout -k 10 300 python bench.py --config C5 --no-cpu-baseline > gpurun_out/bench_c5.json 2> gpurun_out/bench_c5.err
 fi
+if [ "$1" = "wire2" ]; then
+L=nmmo_amd/lib
+timeout -k 10 300 python -u -m pytest tests/test_gpu_wire.py tests/test_gpu_multirank.py -x -v --timeout 150 --timeout-method thread > gpurun_out/gpu_wire.log 2>&1 && \
+timeout -k 10 900 bash tools/ab_obs.sh C5 $L/libnmmo_hip.so,$L/libnmmo_hip_wbase.so,$L/libnmmo_hip_wo16w4.so,$L/libnmmo_hip_wo64w8.so --no-decode > gpurun_out/ab_wire2.txt 2>&1
+fi
+if [ "$1" = "wire3" ]; then
+L=nmmo_amd/lib
+timeout -k 10 300 python -u -m pytest tests/test_gpu_wire.py -x -v --timeout 150 --timeout-method thread > gpurun_out/gpu_wire.log 2>&1 && \
+timeout -k 10 900 bash tools/ab_obs.sh C5 $L/libnmmo_hip.so,$L/libnmmo_hip_wo8w2.so,$L/libnmmo_hip_wo16w8.so,$L/libnmmo_hip_wo32w4.so --no-decode > gpurun_out/ab_wire3.txt 2>&1 && \
+bash profiles/run_rocprof.sh r04 C5 > gpurun_out/prof_c5.log 2>&1
+fi
