@@ -57,3 +57,10 @@ timeout -k 10 300 python -u -m pytest tests/test_gpu_wire.py -x -v --timeout 150
 timeout -k 10 900 bash tools/ab_obs.sh C5 $L/libnmmo_hip.so,$L/libnmmo_hip_wo8w2.so,$L/libnmmo_hip_wo16w8.so,$L/libnmmo_hip_wo32w4.so --no-decode > gpurun_out/ab_wire3.txt 2>&1 && \
 bash profiles/run_rocprof.sh r04 C5 > gpurun_out/prof_c5.log 2>&1
 fi
+if [ "$1" = "cusplit" ]; then
+B="python bench.py --steps 200 --warmup 30 --no-cpu-baseline --no-extras"
+for a in "" "--no-graph" "--cu-split 16" "--cu-split 32" "--cu-split 64" "" "--cu-split 32"; do
+  timeout -k 10 200 $B $a > gpurun_out/cs.json 2> gpurun_out/cs.err || { echo "FAIL $a"; tail -5 gpurun_out/cs.err; exit 1; }
+  python -c "import json,sys; d=json.loads(open('gpurun_out/cs.json').read().strip().splitlines()[-1]); print(repr(sys.argv[1]), round(d['value']/1e6,2), d['ms_per_step'], d['kernel_ms'])" "$a"
+done > gpurun_out/cusplit.txt 2>&1
+fi
