@@ -56,6 +56,22 @@ __global__ void __launch_bounds__(64 * kWoWaves) wire_obs_kernel(ObsParams p) {
   const int ne = v.ecount[e];
   const int a0 = g * kWoAgents;  // the workgroup's first agent
   const int16_t* E = p.ent + (size_t)e * NMMO_NF * S;
+  // Every global load of the kernel is issued here or in the agent loop's prefetch, ahead of any
+  // store (vmcnt counts stores too and retires in issue order: a load after a store waits for
+  // it). Lane j of a wave holds its agent abase + kWoWaves j's count word, task and last price.
+  int my_task = 0, my_prev = -1, my_cnt = 0;
+  {
+    const int aj = g * kWoAgents + wave_id() + kWoWaves * lane;
+    if (lane < (kWoAgents + kWoWaves - 1) / kWoWaves && aj < P) {
+      const size_t ai = (size_t)e * P + aj;
+      my_cnt = cnt[aj];
+      my_task = p.assign[ai];
+      if constexpr (kWrap)
+        if (p.ws) my_prev = p.ws[ai].prev_price;
+    }
+  }
+  const int tick = p.env[(size_t)e * NMMO_NE + E_TICK];
+  uint8_t* const wenv = p.wire + v.env_off[e];
   record_offsets_wave0(cnt, P, woff, wire_table_bytes(ne));
   for (int s = tid; s < kMaxSlots; s += blockDim.x) rk[s] = p.wrank[(size_t)e * kMaxSlots + s];
   for (int i = tid; i < NMMO_N_ENTITY_COLS * kWoAgents; i += blockDim.x) {
@@ -67,53 +83,15 @@ __global__ void __launch_bounds__(64 * kWoWaves) wire_obs_kernel(ObsParams p) {
   for (int i = 0; i < kAoRows; i++) pr[i] = p.wpk[(size_t)e * kMaxSlots + lane + 64 * i];
   __syncthreads();
 
-  uint8_t* wenv = p.wire + v.env_off[e];
-  const int nm = min(max(p.mcount[e], 0), NMMO_MARKET_ROWS);
-  if (g == 0) {  // the env's listings (Market rows), one 32-B row per thread
-    uint4* mk = reinterpret_cast<uint4*>(wenv + woff[P]);
-    for (int k = tid; k < nm; k += blockDim.x) {
-      const int x = p.mlist[(size_t)e * NMMO_MARKET_ROWS + k];
-      const int own = (x >> 16) & 255, slot = (x >> 24) & 15;
-      const uint2 wd = p.items[((size_t)e * P + own) * kInv + slot];
-      uint32_t q[8];
-#pragma unroll
-      for (int i = 0; i < 8; i++)
-        q[i] = i16pack((int)item_col(wd, own + 1, 2 * i), (int)item_col(wd, own + 1, 2 * i + 1));
-      mk[2 * k] = make_uint4(q[0], q[1], q[2], q[3]);
-      mk[2 * k + 1] = make_uint4(q[4], q[5], q[6], q[7]);
-    }
-    // the entity table: the 31 columns of each shown slot at its index (a thread per slot, the
-    // columns from HBM), then the table's zero pad
-    int16_t* tab = reinterpret_cast<int16_t*>(wenv);
-    for (int s = tid; s < S; s += blockDim.x) {
-      const int x = rk[s];
-      if (x == 0xFFFF) continue;
-      int16_t col[NMMO_N_ENTITY_COLS];
-#pragma unroll
-      for (int f = 0; f < NMMO_N_ENTITY_COLS; f++) col[f] = E[f * S + s];
-#pragma unroll
-      for (int f = 0; f < NMMO_N_ENTITY_COLS; f++) tab[x * NMMO_N_ENTITY_COLS + f] = col[f];
-    }
-    for (int b = kEntRow * ne + tid; b < wire_table_bytes(ne); b += blockDim.x) wenv[b] = 0;
-  }
-
   uint32_t* visw = visw_all + w * 128;
   uint8_t* wmat = wmat_all + w * 256;
   if (lane < 256 - 225) wmat[225 + lane] = 0;  // materials 225.. read as zero nibbles
   const uint8_t* mat = p.mat + (size_t)e * kTiles;
-  const int tick = p.env[(size_t)e * NMMO_NE + E_TICK];
   const bool item = (p.systems & NMMO_SYS_ITEM) != 0;
   const bool exch = item && (p.systems & NMMO_SYS_EXCHANGE) != 0;
 
   const int per_wave = (kWoAgents + kWoWaves - 1) / kWoWaves;
   const int abase = g * kWoAgents + w;
-  int my_task = 0, my_prev = -1;  // lane j: agent abase + 4 j
-  if (lane < per_wave && abase + kWoWaves * lane < P) {
-    const size_t ai = (size_t)e * P + abase + kWoWaves * lane;
-    my_task = p.assign[ai];
-    if constexpr (kWrap)
-      if (p.ws) my_prev = p.ws[ai].prev_price;
-  }
   uint2 iv = make_uint2(0u, 0u);
   uint32_t wm[4] = {0u, 0u, 0u, 0u};
   int mo[2];
@@ -126,7 +104,7 @@ __global__ void __launch_bounds__(64 * kWoWaves) wire_obs_kernel(ObsParams p) {
   };
   auto in_realm = [&](int j) {
     const int a = abase + kWoWaves * j;
-    return j < per_wave && a < P && (cnt[a] & 0x8000u);
+    return j < per_wave && a < P && (__builtin_amdgcn_readlane(my_cnt, j) & 0x8000);
   };
   if (in_realm(0)) prefetch(abase);
 
@@ -136,7 +114,7 @@ __global__ void __launch_bounds__(64 * kWoWaves) wire_obs_kernel(ObsParams p) {
   for (int j = 0; j < per_wave; j++) {
     const int a = abase + kWoWaves * j;
     if (a >= P) break;
-    const uint32_t cw = (uint32_t)__builtin_amdgcn_readfirstlane((int)cnt[a]);
+    const uint32_t cw = (uint32_t)__builtin_amdgcn_readlane(my_cnt, j);
     if (!(cw & 0x8000u)) {  // not in the realm: no record
       if (in_realm(j + 1)) prefetch(a + kWoWaves);
       continue;
@@ -209,6 +187,35 @@ __global__ void __launch_bounds__(64 * kWoWaves) wire_obs_kernel(ObsParams p) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the next agent reuses visw / wmat
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  // the env's listings (Market rows, one 32-B row per thread) and its entity table (the 31
+  // columns of each shown slot at its index, a thread per slot, the columns from HBM; then the
+  // table's zero pad): workgroup 0, after its records, so no record waits on these stores
+  if (g == 0) {
+    const int nm = min(max(p.mcount[e], 0), NMMO_MARKET_ROWS);
+    uint4* mk = reinterpret_cast<uint4*>(wenv + woff[P]);
+    for (int k = tid; k < nm; k += blockDim.x) {
+      const int x = p.mlist[(size_t)e * NMMO_MARKET_ROWS + k];
+      const int own = (x >> 16) & 255, slot = (x >> 24) & 15;
+      const uint2 wd = p.items[((size_t)e * P + own) * kInv + slot];
+      uint32_t q[8];
+#pragma unroll
+      for (int i = 0; i < 8; i++)
+        q[i] = i16pack((int)item_col(wd, own + 1, 2 * i), (int)item_col(wd, own + 1, 2 * i + 1));
+      mk[2 * k] = make_uint4(q[0], q[1], q[2], q[3]);
+      mk[2 * k + 1] = make_uint4(q[4], q[5], q[6], q[7]);
+    }
+    int16_t* tab = reinterpret_cast<int16_t*>(wenv);
+    for (int s = tid; s < S; s += blockDim.x) {
+      const int x = rk[s];
+      if (x == 0xFFFF) continue;
+      int16_t col[NMMO_N_ENTITY_COLS];
+#pragma unroll
+      for (int f = 0; f < NMMO_N_ENTITY_COLS; f++) col[f] = E[f * S + s];
+#pragma unroll
+      for (int f = 0; f < NMMO_N_ENTITY_COLS; f++) tab[x * NMMO_N_ENTITY_COLS + f] = col[f];
+    }
+    for (int b = kEntRow * ne + tid; b < wire_table_bytes(ne); b += blockDim.x) wenv[b] = 0;
   }
 }
 

@@ -64,3 +64,8 @@ for a in "" "--no-graph" "--cu-split 16" "--cu-split 32" "--cu-split 64" "" "--c
   python -c "import json,sys; d=json.loads(open('gpurun_out/cs.json').read().strip().splitlines()[-1]); print(repr(sys.argv[1]), round(d['value']/1e6,2), d['ms_per_step'], d['kernel_ms'])" "$a"
 done > gpurun_out/cusplit.txt 2>&1
 fi
+if [ "$1" = "wire4" ]; then
+L=nmmo_amd/lib
+timeout -k 10 300 python -u -m pytest tests/test_gpu_wire.py tests/test_gpu_multirank.py -x -v --timeout 150 --timeout-method thread > gpurun_out/gpu_wire.log 2>&1 && \
+timeout -k 10 900 bash tools/ab_obs.sh C5 $L/libnmmo_hip.so,$L/libnmmo_hip_wbase.so --no-decode > gpurun_out/ab_wire4.txt 2>&1
+fi
