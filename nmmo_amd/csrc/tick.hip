@@ -1696,13 +1696,14 @@ __device__ __forceinline__ void tick_env(Ctx& c, Heads hd, float* rew, uint8_t* 
         if (tid < 8) okm[tid] = 0u;  // okm and frm
         if (tid < 3) anyf[tid] = 0;
         __syncthreads();
-        int pos = 0, owner0 = -1;
+        int pos = 0, owner0 = -1, rm0 = -1;
         const int brow = isb ? c.a_buy[s] : -1;
         if (isb) {
           const uint32_t key = c.ikey[s];
           for (int q = 0; q < P; q++)
             if (c.a_buy[q] >= 0) pos += (c.ikey[q] < key || (c.ikey[q] == key && q < s)) ? 1 : 0;
-          owner0 = c.rmap[brow] & 255;  // a listed row at tick start (kth_listed)
+          rm0 = c.rmap[brow];
+          owner0 = rm0 & 255;  // a listed row at tick start (kth_listed)
         }
         bool active = isb && acts(c, s) && owner0 != s;  // the others fail without effect
         bool ok = false;
@@ -1723,6 +1724,12 @@ __device__ __forceinline__ void tick_env(Ctx& c, Heads hd, float* rew, uint8_t* 
           if (tid == 0) anyf[(round + 1) % 3] = 0;
           __syncthreads();
           if (!anyf[round % 3]) break;
+          // A buy whose row has left its tick-start owner fails whenever its turn comes: only a
+          // buy of the same row moves it, that buy shares owner0 and so ran earlier in the order,
+          // and it leaves the row unlisted. Such a buy retires now instead of taking a round of
+          // owner0's (the buyers of one popular listing used to chain one round each: p99 26k
+          // cycles). A row moved in this round's executions is seen now or next round.
+          if (active && c.rmap[brow] != rm0 && !(mr[s] == key && mr[owner0] == key)) active = false;
           if (active && mr[s] == key && mr[owner0] == key) {
             active = false;
             const int owner = c.rmap[brow] < 0 ? -1 : (c.rmap[brow] & 255);

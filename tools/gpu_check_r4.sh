@@ -69,3 +69,10 @@ L=nmmo_amd/lib
 timeout -k 10 300 python -u -m pytest tests/test_gpu_wire.py tests/test_gpu_multirank.py -x -v --timeout 150 --timeout-method thread > gpurun_out/gpu_wire.log 2>&1 && \
 timeout -k 10 900 bash tools/ab_obs.sh C5 $L/libnmmo_hip.so,$L/libnmmo_hip_wbase.so --no-decode > gpurun_out/ab_wire4.txt 2>&1
 fi
+if [ "$1" = "tick" ]; then
+L=nmmo_amd/lib
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fullsize.py -x -v --timeout 200 --timeout-method thread > gpurun_out/gpu_tick.log 2>&1 && \
+STAMPS_STAGGER=64 timeout -k 10 200 python tools/stamps.py C4 512 40 > gpurun_out/stamps_C4.txt 2>&1 && \
+timeout -k 10 600 bash tools/ab_obs.sh C5 $L/libnmmo_hip.so,$L/libnmmo_hip_tbase.so --no-decode > gpurun_out/ab_tick.txt 2>&1 && \
+timeout -k 10 600 bash tools/ab_obs.sh C3 $L/libnmmo_hip.so,$L/libnmmo_hip_tbase.so > gpurun_out/ab_tick_c3.txt 2>&1
+fi
