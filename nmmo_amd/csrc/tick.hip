@@ -1685,30 +1685,59 @@ __device__ __forceinline__ void tick_env(Ctx& c, Heads hd, float* rew, uint8_t* 
       const bool isb = s < P && c.a_buy[s] >= 0;
       int nbuy;
       block_prefix_count(isb, wtot_next(c), &nbuy);
+      NMMO_STAMP(28);
       if (nbuy > 0) {
         int* mi = c.ft;  // [2][S] round keys (see the attack rounds); attack init zeroes them again
         uint32_t* okm = reinterpret_cast<uint32_t*>(c.wtot + 20);  // [4] succeeded, by position
         uint32_t* frm = reinterpret_cast<uint32_t*>(c.wtot + 24);  // [4] freed a row, by position
         int16_t* frow = c.order;                                   // [128] that row, by position
+        uint32_t* tgm = reinterpret_cast<uint32_t*>(c.wtot + 28);  // [4] owners of some buy's row
         int* anyf = c.wtot + 16;
-        if (isb) c.ikey[s] = draw(seed, (uint32_t)tick, P_BUY_ORDER, (uint32_t)(s + 1), 0).x;
+        // sort keys, ~0 for the slots without a buy (up to a multiple of 4: read as uint4 below)
+        if (s < ((P + 3) & ~3)) c.ikey[s] = isb ? draw(seed, (uint32_t)tick, P_BUY_ORDER, (uint32_t)(s + 1), 0).x : ~0u;
         if (tid < P) mi[tid] = mi[S + tid] = 0;
-        if (tid < 8) okm[tid] = 0u;  // okm and frm
+        if (tid < 12) okm[tid] = 0u;  // okm, frm and tgm
         if (tid < 3) anyf[tid] = 0;
         __syncthreads();
         int pos = 0, owner0 = -1, rm0 = -1;
         const int brow = isb ? c.a_buy[s] : -1;
         if (isb) {
+          // pos = buys with a smaller (key, slot): the keys below this one, 4 per LDS read; only
+          // when another slot holds the same key (a ~0 key, or a 32-bit draw collision) the
+          // exact per-slot count
           const uint32_t key = c.ikey[s];
-          for (int q = 0; q < P; q++)
-            if (c.a_buy[q] >= 0) pos += (c.ikey[q] < key || (c.ikey[q] == key && q < s)) ? 1 : 0;
+          const uint4* k4 = reinterpret_cast<const uint4*>(c.ikey);
+          int eq = 0;
+          for (int q4 = 0; q4 < ((P + 3) >> 2); q4++) {
+            const uint4 v = k4[q4];
+            pos += (v.x < key) + (v.y < key) + (v.z < key) + (v.w < key);
+            eq += (v.x == key) + (v.y == key) + (v.z == key) + (v.w == key);
+          }
+          if (eq > 1) {
+            pos = 0;
+            for (int q = 0; q < P; q++)
+              if (c.a_buy[q] >= 0) pos += (c.ikey[q] < key || (c.ikey[q] == key && q < s)) ? 1 : 0;
+          }
           rm0 = c.rmap[brow];
           owner0 = rm0 & 255;  // a listed row at tick start (kth_listed)
         }
         bool active = isb && acts(c, s) && owner0 != s;  // the others fail without effect
+        // Whether the buy would succeed on the tick-start state (no buy has run yet: every thread
+        // passes round 1's barrier before any executes). A buyer whose own row no buy targets
+        // keeps its gold and inventory through the phase, so if it fails now it fails at its turn.
+        bool elig0 = false;
+        if (active) {
+          const uint2* oinv = c.inv + owner0 * kInv;
+          const int k = inv_find(oinv, brow);
+          if (k >= 0) {
+            const uint2 w = oinv[k];
+            elig0 = it_price(w) && TF(F_GOLD, s) >= it_price(w) && has_room(c, s, w);
+          }
+        }
         bool ok = false;
         uint2 bw = make_uint2(0u, 0u);
         int bprice = 0, bowner = -1;
+        NMMO_STAMP(29);
         for (int round = 1;; round++) {
           if (round > P + 1) {  // <= nbuy rounds (the earliest pending buy runs in every round)
             if (tid == 0) tick_fault(c, NMMO_FAULT_BUY_ROUNDS);
@@ -1720,10 +1749,15 @@ __device__ __forceinline__ void tick_env(Ctx& c, Heads hd, float* rew, uint8_t* 
             atomicMax(&mr[s], key);
             atomicMax(&mr[owner0], key);
             anyf[round % 3] = 1;
+            if (round == 1) atomicOr(&tgm[owner0 >> 5], 1u << (owner0 & 31));
           }
           if (tid == 0) anyf[(round + 1) % 3] = 0;
           __syncthreads();
           if (!anyf[round % 3]) break;
+          // (round 1) the buys that fail on the tick-start state and whose buyer owns no bought
+          // row fail at their turn too: they retire without a round of owner0's (a full
+          // inventory or short gold chained one round per buyer of a popular seller)
+          if (round == 1 && active && !elig0 && !((tgm[s >> 5] >> (s & 31)) & 1u)) active = false;
           // A buy whose row has left its tick-start owner fails whenever its turn comes: only a
           // buy of the same row moves it, that buy shares owner0 and so ran earlier in the order,
           // and it leaves the row unlisted. Such a buy retires now instead of taking a round of
@@ -1758,6 +1792,7 @@ __device__ __forceinline__ void tick_env(Ctx& c, Heads hd, float* rew, uint8_t* 
             }
           }
         }
+        NMMO_STAMP(30);
         // (the loop's last barrier published okm / frm / frow)
         auto below = [&](const uint32_t* m) {
           int n = 0;

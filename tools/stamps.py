@@ -27,7 +27,8 @@ from nmmo_amd.engine import NmmoEngine  # noqa: E402
 STAMPS = [(0, None), (20, "state load"), (1, "prep: rowslot, positions, listings"),
           (13, "visibility bitmap"), (12, "action decode"), (2, "npc decide + hunt BFS"),
           (3, "update: resources, tile hash"), (15, "harvest: foilage, professions"),
-          (21, "harvest events"), (22, "Use"), (23, "Buy"), (24, "Give, GiveGold (serial)"),
+          (21, "harvest events"), (22, "Use"), (28, "Buy: count"), (29, "Buy: order, eligibility"),
+          (30, "Buy: rounds"), (23, "Buy: events, freed rows"), (24, "Give, GiveGold (serial)"),
           (14, "Destroy"), (4, "attack init"), (25, "attack rounds"), (26, "attack events"),
           (27, "parallel shots"), (5, "serial shots, loot"), (6, "move (+ Sell)"), (7, "cull, NPC compaction"),
           (16, "respawn scan (wave 0)"), (18, "respawn list (wave 0)"), (19, "respawn draws, expiry (wave 0)"),
