@@ -30,6 +30,7 @@ PATCHES = {
     "nomt": [("obs.hip", '  asm volatile("" : "+v"(my_task), "+v"(my_prev));', "")],
     "nomask": [("native_obs.hip", "        if (q < NMMO_NATIVE_MASK_BYTES / 16) {", f"        if (q < NMMO_NATIVE_MASK_BYTES / 16 && {NEVER}) {{")],
     "noent": [("native_obs.hip", "for (int k0 = 0; k0 < nv4; k0 += 4) {", f"for (int k0 = 0; k0 < nv4 && {NEVER}; k0 += 4) {{")],
+    "nnoloop": [("native_obs.hip", "  for (int j = 0; j < per_wave; j++) {", f"  for (int j = 0; j < per_wave && {NEVER}; j++) {{")],
     "noinv": [("native_obs.hip", "    if (ninv == 0) {\n      if (lane < kInv * 8 / 4)", f"    if (ninv == 0 || {NEVER}) {{\n      if (lane < kInv * 8 / 4)")],
 }
 

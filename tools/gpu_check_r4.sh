@@ -76,3 +76,7 @@ STAMPS_STAGGER=64 timeout -k 10 200 python tools/stamps.py C4 512 40 > gpurun_ou
 timeout -k 10 600 bash tools/ab_obs.sh C5 $L/libnmmo_hip.so,$L/libnmmo_hip_tbase.so --no-decode > gpurun_out/ab_tick.txt 2>&1 && \
 timeout -k 10 600 bash tools/ab_obs.sh C3 $L/libnmmo_hip.so,$L/libnmmo_hip_tbase.so > gpurun_out/ab_tick_c3.txt 2>&1
 fi
+if [ "$1" = "ablnat" ]; then
+L=nmmo_amd/lib
+timeout -k 10 900 bash tools/ab_obs.sh C4 $L/libnmmo_hip.so,$L/libnmmo_hip_nnoloop.so,$L/libnmmo_hip_notile.so,$L/libnmmo_hip_nozero.so --obs native > gpurun_out/abl_nat.txt 2>&1
+fi
