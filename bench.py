@@ -73,7 +73,7 @@ WORKLOADS = {
 }
 # (config, obs layout, wrapper) measured beside the headline
 EXTRAS = [("C2", None, None), ("C3", None, None), ("C4", "native", None), ("C5", None, None),
-          ("C4", None, "neurips23_start_kit")]
+          ("C4", None, "neurips23_start_kit"), ("C4", "flat-rezero", None)]
 EXTRAS_MULTI = [("C4", None, None)]
 
 # the agent sections' reward_wrapper weights (config.yaml:103-106, 118-126, 137-140)
@@ -101,19 +101,27 @@ def tick_bytes_per_env(S: int, P: int, items: bool, events_per_env: float = 0.0,
     return int(2 * state + P * 4 + P * 12 * 4 + P * (4 + 1 + 1 + 1) + P * 6 + events_per_env * EVENT_ROW_BYTES)
 
 
-def obs_bytes_per_env(S: int, P: int, elems: int, native: bool = False, wire_bytes: float | None = None) -> float:
+def obs_bytes_per_env(S: int, P: int, elems: int, native: bool = False, wire_bytes: float | None = None,
+                      stored: float | None = None, alive_frac: float = 1.0) -> float:
     """Algorithmic bytes of one env's obs gather, each byte counted once:
     the rows written (flat fp32: 23,987 x 4 B per agent; native, SPEC §8b: 9,552 B per agent +
     the env's 32 KB Market once; wire, SPEC §8c: the measured record + header bytes per env)
     + the env's 33 obs-relevant int16 entity columns read once + each agent's 15x15 window
-    materials and 12 item words read."""
+    materials and 12 item words read. stored: the bytes one env's rows took in stores, as the
+    kernel counted them (nmmo_set_obs_counter: a flat row stores only what differs from what
+    the buffer holds already, nmmo_hip.h nmmo_obs_invalidate); alive_frac: the fraction of agents
+    in the realm (whose windows and items are read)."""
     from nmmo_amd import abi
 
     if wire_bytes is not None:
         rows = wire_bytes
+    elif stored is not None:
+        rows = stored + (abi.native_env_bytes(P) - P * abi.NATIVE_ROW_BYTES if native else 0)  # + Market
+    elif native:
+        rows = abi.native_env_bytes(P)
     else:
-        rows = abi.native_env_bytes(P) if native else P * elems * 4
-    return rows + 33 * S * 2 + P * (225 + 12 * 8)
+        rows = P * elems * 4
+    return rows + 33 * S * 2 + P * (225 + 12 * 8) * alive_frac
 
 
 def pmc_traffic(cfg_name: str, kernel, envs: int):
@@ -386,8 +394,17 @@ def measure(args, name, layout_name, envs, rank, world, dev, steps, warmup, dist
     if envs % nb:
         raise SystemExit(f"--batches {nb} must divide the {envs} envs per GPU")
     per = envs // nb
-    engs = [NmmoEngine(cfg, per, seed=args.seed, device=dev, task_embedding=task,
-                       env_index_base=rank * envs + i * per) for i in range(nb)]
+    # "flat-rezero": every obs row written in full every step (NMMO_OBS_REZERO, nmmo_hip.h
+    # nmmo_obs_invalidate), beside the headline's incremental rows
+    rezero = layout_name == "flat-rezero"
+    if rezero:
+        os.environ["NMMO_OBS_REZERO"] = "1"
+    try:
+        engs = [NmmoEngine(cfg, per, seed=args.seed, device=dev, task_embedding=task,
+                           env_index_base=rank * envs + i * per) for i in range(nb)]
+    finally:
+        if rezero:
+            del os.environ["NMMO_OBS_REZERO"]
     eng = engs[0]
     for e in engs:
         if wrapper != "none":
@@ -402,8 +419,11 @@ def measure(args, name, layout_name, envs, rank, world, dev, steps, warmup, dist
     # device counters the tick kernel adds into: [0] = sum(mask) (agent-steps), [1] = episodes,
     # [2] = event-log rows appended
     counters = [torch.zeros(3, dtype=torch.int64, device=dev) for _ in engs]
-    for e, c in zip(engs, counters):
+    obs_rows = [torch.zeros(2, dtype=torch.int64, device=dev) for _ in engs]  # rows / bytes the gathers wrote
+    for e, c, r in zip(engs, counters, obs_rows):
         e.set_counters(c)
+        if wl["obs"]:
+            e.set_obs_counter(r)
     # nb > 1: all side streams (a capture cannot run on the legacy default stream)
     streams = [torch.cuda.current_stream(dev)] if nb == 1 else [torch.cuda.Stream(device=dev) for _ in engs]
 
@@ -433,7 +453,7 @@ def measure(args, name, layout_name, envs, rank, world, dev, steps, warmup, dist
                 graphs[n] = g
             plans.append([graphs[g_n]] * q + ([graphs[r]] if r else []))
         torch.cuda.synchronize(dev)
-    for c in counters:
+    for c in counters + obs_rows:
         c.zero_()
     if world > 1:
         dist.barrier()
@@ -453,6 +473,8 @@ def measure(args, name, layout_name, envs, rank, world, dev, steps, warmup, dist
     tot = torch.stack(counters).sum(0)
     alive = float(tot[0].item())
     episodes = int(tot[1].item())
+    obs_cnt = torch.stack(obs_rows).sum(0)
+    rows_written, bytes_stored = float(obs_cnt[0].item()), float(obs_cnt[1].item())
     events_per_env_tick = float(tot[2].item()) / (envs * steps) if cfg.event_cap > 0 else None
     _progress(f"{name}: timed {steps} steps in {elapsed:.3f} s")
     tick_avg_ms, obs_avg_ms, wrap_avg_ms = _kernel_timing(eng, pseed, steps)
@@ -493,7 +515,9 @@ def measure(args, name, layout_name, envs, rank, world, dev, steps, warmup, dist
     S, P = eng.S, cfg.PLAYER_N
     slim = not any(x in cfg.systems for x in ("Item", "Equipment", "Profession", "Exchange"))
     tick_b = tick_bytes_per_env(S, P, "Item" in cfg.systems, events_per_env_tick or 0.0, slim) * per
-    obs_b = obs_bytes_per_env(S, P, eng.obs_elems, native) * per if wl["obs"] else 0
+    row_frac = rows_written / (envs * P * steps)  # the timed steps' rows written per agent row
+    obs_b = obs_bytes_per_env(S, P, eng.obs_elems, native, stored=bytes_stored / (envs * steps),
+                              alive_frac=alive / (envs * P * steps)) * per if wl["obs"] else 0
     if wl["obs"] and obs_avg_ms > tick_avg_ms:
         kern, byts, ms = "native_obs_kernel" if native else "obs_kernel", obs_b, obs_avg_ms
         timing = f"HIP events around each {kern} launch on the launch stream"
@@ -510,7 +534,8 @@ def measure(args, name, layout_name, envs, rank, world, dev, steps, warmup, dist
                 timing = (f"one batch alone after the timed region: a {batch}-step hipGraph (policy + "
                           f"tick) minus a {batch}-launch policy-only hipGraph, HIP events on the "
                           f"launch stream")
-    prof_name = name + ("-native" if native else "") + ("" if wrapper == "none" else "+" + wrapper)
+    prof_name = name + ("-native" if native else "-rezero" if rezero else "") + \
+        ("" if wrapper == "none" else "+" + wrapper)
     launch = "eager" if not plans else f"hipGraph x{min(args.graph_steps, steps)} ticks"
     if nb > 1:
         launch += f", {nb} batches of {per} envs on {nb} streams"
@@ -523,6 +548,8 @@ def measure(args, name, layout_name, envs, rank, world, dev, steps, warmup, dist
                       "wrapper": round(wrap_avg_ms, 5) if wrapper != "none" else None},
         "roofline": _roofline(prof_name, kern, byts, ms, per, timing, nb, elapsed / steps, fill_gbs),
         "batches": nb,
+        "obs_rows_written_frac": round(row_frac, 4) if wl["obs"] else None,
+        "obs_bytes_stored_per_agent_row": round(bytes_stored / (envs * P * steps), 1) if wl["obs"] else None,
     }
     _check_faults(args, engs, name, world, dist, dev)  # every tick of this workload ran (timed and after)
     for e in engs:
@@ -699,6 +726,11 @@ def result_line(res, args, world, steps, alive_total, slots_total, elapsed, warm
         "launch": res["launch"],
         "roofline": res["roofline"],
     }
+    if res.get("obs_rows_written_frac") is not None:
+        # the obs rows are written incrementally: the buffer's bytes after every step equal a full
+        # write (nmmo_hip.h nmmo_obs_invalidate, tests/test_gpu_zero_rows.py)
+        line["obs_rows_written_frac"] = res["obs_rows_written_frac"]
+        line["obs_bytes_stored_per_agent_row"] = res["obs_bytes_stored_per_agent_row"]
     if res["gather"]:
         line["wire_bytes_per_agent_in_realm"] = res["wire_bytes_per_agent_in_realm"]
     return line

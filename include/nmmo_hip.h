@@ -317,6 +317,29 @@ NMMO_API int nmmo_step_envs(NmmoHandle* h, const int32_t* env_ids, int32_t n_ids
  * HBM-bound gathers apart from their ticks (bench.py --batches). Graph-capturable. */
 NMMO_API int nmmo_observe(NmmoHandle* h, void* obs, void* stream);
 
+/* Incremental obs rows. Most of a flat row is zero runs: rows of agents out of the realm (dead,
+ * or not yet spawned) are all-zero (pufferlib's pad_agent_data), and an agent's row holds ~5 of
+ * its 100 Entity rows, a few of the 1,024 Market rows and Buy.MarketItem entries, and a Task
+ * embedding that changes only with its task. nmmo_obs_bind makes `obs` the handle's own obs
+ * buffer: for it the handle remembers, per agent row, what it last wrote there (row all-zero;
+ * the Entity rows, Market rows and Buy entries past which the row is zero; the task whose
+ * embedding it holds) and stores only what differs from that. The buffer's bytes after every
+ * call are the same as when every row is written in full (tests/test_gpu_zero_rows.py checks
+ * them against such a handle). Native rows skip only all-zero rows. Any other buffer passed to
+ * nmmo_reset / nmmo_step / nmmo_step_envs / nmmo_observe gets every row written in full. A bound
+ * buffer is the handle's until it is unbound (obs = NULL) or the handle destroyed: a caller that
+ * writes into it calls nmmo_obs_invalidate first (the next gather then writes every row in
+ * full). Binding synchronises the device and forgets the previous binding; nmmo_set_tasks
+ * forgets the Task sections itself. NMMO_OBS_REZERO=1 in the environment at nmmo_create turns
+ * the tracking off (A/B). nmmo_set_obs_counter: when set, every obs gather adds into
+ * dev_counter (device u64 [2]): [0] += rows it wrote (rows of agents in the realm + rows
+ * zeroed), [1] += bytes it stored (flat: the sections written; native: whole rows); NULL
+ * disables. nmmo_obs_invalidate and nmmo_set_obs_counter are enqueued on / capture-safe for
+ * `stream`. */
+NMMO_API int nmmo_obs_bind(NmmoHandle* h, const void* obs);
+NMMO_API int nmmo_obs_invalidate(NmmoHandle* h, void* stream);
+NMMO_API int nmmo_set_obs_counter(NmmoHandle* h, uint64_t* dev_counter);
+
 /* Task table and per-player assignment (SPEC.md §12; nmmo.Env.reset(make_task_fn) /
  * agent_task_map). tasks: host [n_tasks] (1..NMMO_MAX_TASKS); embeddings: host fp16
  * [n_tasks][task_embed_dim] used as each player's Task obs (NULL = keep the create-time

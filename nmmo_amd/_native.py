@@ -27,7 +27,8 @@ SYMBOLS = [
     "nmmo_get_wrapper_dropped", "nmmo_set_task_weights", "nmmo_wire_header_bytes", "nmmo_wire_max_bytes",
     "nmmo_wire_pack", "nmmo_wire_unpack", "nmmo_wire_check", "nmmo_dev_alloc", "nmmo_dev_free", "nmmo_observe",
     "nmmo_step_envs", "nmmo_inject_fault", "nmmo_fault_into", "nmmo_exp_store_records",
-    "nmmo_exp_gather_records", "nmmo_exp_store_records_many",
+    "nmmo_exp_gather_records", "nmmo_exp_store_records_many", "nmmo_obs_invalidate", "nmmo_set_obs_counter",
+    "nmmo_obs_bind",
 ]
 
 
@@ -93,6 +94,9 @@ def declare(L):
     L.nmmo_get_wrapper_state.argtypes = [vp, vp, vp]
     L.nmmo_expand_obs.argtypes = [vp, vp, vp, i32, vp]
     L.nmmo_observe.argtypes = [vp, vp, vp]
+    L.nmmo_obs_invalidate.argtypes = [vp, vp]
+    L.nmmo_obs_bind.argtypes = [vp, vp]
+    L.nmmo_set_obs_counter.argtypes = [vp, vp]
     xp = ctypes.POINTER(abi.NmmoExperience)
     L.nmmo_exp_scratch_ints.argtypes = [i32, i32]
     L.nmmo_exp_scratch_ints.restype = ctypes.c_int64

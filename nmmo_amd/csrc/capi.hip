@@ -2,6 +2,7 @@
 // device state (SoA over env x slot in HBM), enqueues the gfx950 kernels on the caller's
 // stream, never synchronises inside nmmo_step (graph-capturable, no allocation).
 #include <math.h>
+#include <stdlib.h>
 #include <stdarg.h>
 #include <stdio.h>
 #include <string.h>
@@ -62,6 +63,13 @@ struct NmmoHandle {
   int32_t* d_wmcount = nullptr;  // native obs: per-env listing count of the last obs
   uint16_t* d_wrank = nullptr;   // wire obs: per-slot entity-table index (wire_count_kernel)
   uint32_t* d_wpk = nullptr;     // wire obs: per-env packed datastore-row words (wire_count_kernel)
+  // flat / native obs: per agent row, the tag of the buffer the row state describes and the state
+  // (ObsParams::zrow / zst); NMMO_OBS_REZERO=1 at create time writes every row in full
+  uint64_t* d_zrow = nullptr;
+  bool zskip = true;
+  const void* zbuf = nullptr;  // the bound obs buffer (nmmo_obs_bind) and its tag
+  uint64_t ztag = 0;
+  unsigned long long* d_rows_out = nullptr;  // nmmo_set_obs_counter
   // the native buffer the last obs gather wrote, and whether no tick ran since (nmmo_wire_pack)
   const void* last_native = nullptr;
   bool native_fresh = false;
@@ -184,7 +192,7 @@ void nmmo_destroy(NmmoHandle* h) {
   void* bufs[] = {h->d_env,  h->d_ent,   h->d_ring,  h->d_mat,   h->d_dep,   h->d_bank,
                   h->d_task, h->d_seeds, h->d_items, h->d_iring, h->d_mlist, h->d_mcount,
                   h->d_events, h->d_tasks, h->d_assign, h->d_tstate, h->d_ws, h->d_uniq, h->d_wenv, h->d_wdrop, h->d_task_cum,
-                  h->d_wcount, h->d_wmcount, h->d_wrank, h->d_wpk, h->d_foreign};
+                  h->d_wcount, h->d_wmcount, h->d_wrank, h->d_wpk, h->d_foreign, h->d_zrow};  // d_zst lives in d_zrow's allocation
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   delete h;
@@ -238,6 +246,13 @@ int nmmo_create(const NmmoConfig* cfg, int32_t n_envs, uint64_t seed, int32_t de
   if (cfg->obs_layout == NMMO_OBS_NATIVE) {
     ALLOC(h->d_wcount, n * P * 2);
     ALLOC(h->d_wmcount, n * 4);
+  }
+  if (cfg->obs_layout == NMMO_OBS_FLAT || cfg->obs_layout == NMMO_OBS_NATIVE) {
+    ALLOC(h->d_zrow, n * P * 16);  // (two statements)
+  }
+  {
+    const char* rz = getenv("NMMO_OBS_REZERO");  // A/B: rewrite the zero rows every launch
+    h->zskip = !(rz && rz[0] == '1');
   }
   if (cfg->obs_layout == NMMO_OBS_WIRE) {
     ALLOC(h->d_wrank, n * (size_t)kMaxSlots * 2);
@@ -300,6 +315,11 @@ static ObsParams obs_params(NmmoHandle* h, void* obs) {
   p.wrank = wire ? h->d_wrank : nullptr;
   p.wpk = wire ? h->d_wpk : nullptr;
   p.fault = h->d_foreign + 1;
+  // only the bound buffer (nmmo_obs_bind) is written incrementally
+  p.zrow = h->d_zrow;
+  p.zst = h->d_zrow ? h->d_zrow + (size_t)h->st.n_envs * h->st.P : nullptr;
+  p.ztag = h->d_zrow && h->zskip && obs && obs == h->zbuf ? h->ztag : 0;
+  p.rows_out = h->d_rows_out;
   p.ws = h->wrap_on ? h->d_ws : nullptr;
   p.wflags = 0;
   if (h->wrap_on) {
@@ -531,6 +551,31 @@ int nmmo_dev_free(void* ptr) {
   HIP_TRY(hipMemUnmap(ptr, a.bytes));
   for (auto c : a.chunks) HIP_TRY(hipMemRelease(c));
   HIP_TRY(hipMemAddressFree(ptr, a.bytes));
+  return NMMO_OK;
+}
+
+int nmmo_obs_bind(NmmoHandle* h, const void* obs) {
+  if (!h) return fail(NMMO_E_INVALID, "null handle");
+  if (!h->d_zrow) return obs ? fail(NMMO_E_INVALID, "nmmo_obs_bind: flat or native obs layouts only") : NMMO_OK;
+  HIP_TRY(hipSetDevice(h->device));
+  HIP_TRY(hipDeviceSynchronize());  // no gather of the previous binding is in flight
+  HIP_TRY(hipMemset(h->d_zrow, 0, (size_t)h->st.n_envs * h->st.P * 8));
+  h->zbuf = obs;
+  h->ztag = obs ? h->ztag + 1 : h->ztag;  // never 0 for a bound buffer
+  return NMMO_OK;
+}
+
+int nmmo_obs_invalidate(NmmoHandle* h, void* stream) {
+  if (!h) return fail(NMMO_E_INVALID, "null handle");
+  if (!h->d_zrow) return NMMO_OK;
+  HIP_TRY(hipSetDevice(h->device));
+  HIP_TRY(hipMemsetAsync(h->d_zrow, 0, (size_t)h->st.n_envs * h->st.P * 8, (hipStream_t)stream));  // the tags
+  return NMMO_OK;
+}
+
+int nmmo_set_obs_counter(NmmoHandle* h, uint64_t* dev_rows) {
+  if (!h) return fail(NMMO_E_INVALID, "null handle");
+  h->d_rows_out = reinterpret_cast<unsigned long long*>(dev_rows);
   return NMMO_OK;
 }
 
@@ -911,6 +956,8 @@ int nmmo_set_tasks(NmmoHandle* h, const NmmoTask* tasks, int32_t n_tasks, const 
   h->st.tmap = tmap;
   h->st.task_cum = nullptr;  // weights belong to the previous table
   h->native_fresh = false;   // task indices of the last native obs may be out of date
+  // flat rows keep a task's embedding by index (ObsParams::zst): the new table may differ
+  if (h->d_zrow) HIP_TRY(hipMemset(h->d_zrow, 0, (size_t)h->st.n_envs * h->st.P * 8));
   return NMMO_OK;
 }
 

@@ -91,7 +91,29 @@ struct ObsParams {
   uint32_t* wpk;        // wire only: [n][kMaxSlots] packed datastore-row words (agent_obs.h ao_pack),
                         // wire_count_kernel -> wire_obs_kernel
   int32_t* fault;             // DevState::fault (a look-back that never resolves records kFaultWireScan)
+  // flat / native obs row state (nmmo_hip.h nmmo_obs_invalidate). zrow[e * P + a] holds the tag
+  // of the buffer that zst[e * P + a] describes row (e, a) of (0 = none); a launch whose buffer has
+  // tag ztag (nmmo_dev_alloc serial | offset, capi.hip obs_zero_tag; 0 = untracked buffer: every
+  // row written in full, the state untouched) leaves alone what the state says is there already:
+  // an all-zero row (kZsZero) of an agent out of the realm; in flat rows also the zero Entity rows
+  // >= zs_hv, the zero Market rows and Buy.MarketItem entries >= zs_hm, and the Task embedding of
+  // task zs_task.
+  uint64_t* zrow;
+  uint64_t* zst;
+  uint64_t ztag;
+  unsigned long long* rows_out;  // optional [2]: += rows this launch wrote, bytes it stored
 };
+constexpr uint64_t kZsZero = 1ull << 20;
+__host__ __device__ inline int zs_hv(uint64_t s) { return (int)(s & 255u); }
+__host__ __device__ inline int zs_hm(uint64_t s) { return (int)((s >> 8) & 4095u); }
+__host__ __device__ inline int zs_task(uint64_t s) { return (int)(uint32_t)(s >> 32); }
+__host__ __device__ inline uint64_t zs_pack(int hv, int hm, int task) {
+  return (uint64_t)hv | (uint64_t)hm << 8 | (uint64_t)(uint32_t)task << 32;
+}
+__device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int j) {
+  return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, j) |
+         (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), j) << 32;
+}
 constexpr int kWrapObsPrice = 1, kWrapObsNoGive = 2, kWrapObsNoDangerous = 4;
 
 struct WrapParams {

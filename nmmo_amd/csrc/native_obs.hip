@@ -88,14 +88,23 @@ __global__ void __launch_bounds__(64 * kAoWaves) native_obs_kernel(ObsParams p) 
   const int per_wave = (kAoAgents + kAoWaves - 1) / kAoWaves;
   const int abase = g * kAoAgents + w;
   int my_task = 0, my_prev = -1, my_alive = 0;  // lane j: agent abase + 4 j
+  uint64_t my_z = 0, my_s = 0;                  // its row state tag and word (ObsParams::zrow / zst)
   if (lane < per_wave && abase + kAoWaves * lane < P) {
     const int aj = abase + kAoWaves * lane;
     const size_t ai = (size_t)e * P + aj;
     my_task = p.assign[ai];
     my_alive = E[F_ALIVE * S + aj];
+    if (p.ztag) {
+      my_z = p.zrow[ai];
+      my_s = p.zst[ai];
+    }
     if constexpr (kWrap)
       if (p.ws) my_prev = p.ws[ai].prev_price;
   }
+  // bit j: agent j's row is all-zero in this buffer already (native rows track nothing else)
+  const uint64_t zknown = __ballot(p.ztag && my_z == p.ztag && (my_s & kZsZero));
+  int nrows = 0;                  // rows this wave wrote (rows_out[0])
+  unsigned long long nbytes = 0;  // bytes this wave stored (rows_out[1])
   int wo[2];
   ao_win_offsets(wo);
   auto alive = [&](int j) { return j < per_wave && __builtin_amdgcn_readlane(my_alive, j) != 0; };
@@ -112,10 +121,20 @@ __global__ void __launch_bounds__(64 * kAoWaves) native_obs_kernel(ObsParams p) 
     uint8_t* nrow = nenv + (size_t)a * NMMO_NATIVE_ROW_BYTES;
     if (!alive(j)) {  // not in the realm: a zero row
       if (p.wcount && lane == 0) p.wcount[(size_t)e * P + a] = 0;
+      if ((zknown >> j) & 1) continue;  // zeroed by an earlier launch into this buffer
       uint4* z = reinterpret_cast<uint4*>(nrow);
       for (int i = lane; i < NMMO_NATIVE_ROW_BYTES / 16; i += 64) z[i] = make_uint4(0u, 0u, 0u, 0u);
+      if (p.ztag && lane == 0) {
+        p.zrow[(size_t)e * P + a] = p.ztag;
+        p.zst[(size_t)e * P + a] = kZsZero;
+      }
+      nrows++;
+      nbytes += NMMO_NATIVE_ROW_BYTES;
       continue;
     }
+    nrows++;
+    nbytes += NMMO_NATIVE_ROW_BYTES;
+    if (((zknown >> j) & 1) && lane == 0) p.zst[(size_t)e * P + a] = 0;  // the row is written now
     const int r = __builtin_amdgcn_readfirstlane(T[F_ROW * Sp + a]);
     const int c = __builtin_amdgcn_readfirstlane(T[F_COL * Sp + a]);
     const int gold = __builtin_amdgcn_readfirstlane(T[F_GOLD * Sp + a]);
@@ -256,6 +275,10 @@ __global__ void __launch_bounds__(64 * kAoWaves) native_obs_kernel(ObsParams p) 
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the next agent reuses visw
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  if (p.rows_out && lane == 0 && nrows) {
+    atomicAdd(p.rows_out, (unsigned long long)nrows);
+    atomicAdd(p.rows_out + 1, nbytes);
   }
 }
 

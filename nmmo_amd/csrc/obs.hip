@@ -225,12 +225,30 @@ obs_kernel(ObsParams p) {
   constexpr int kPerWave = kObsAgentsPerBlock / kObsWaves;
   const int abase = g * kObsAgentsPerBlock + w;
   int my_task = 0, my_prev = -1;
+  // the row's state (ObsParams::zrow / zst): its Entity rows >= hv, its Market rows and
+  // Buy.MarketItem entries >= hm are zero already (my_h = hv | hm << 12; a row of unknown content:
+  // nothing is known zero, an all-zero row: everything)
+  int my_h = kNObs | NMMO_MARKET_ROWS << 12;
+  bool zv = false, zz = false, zt = false;
   if (lane < kPerWave && abase + kObsWaves * lane < p.P) {
     const size_t ai = (size_t)e * p.P + abase + kObsWaves * lane;
     my_task = p.assign[ai];
+    if (p.ztag && p.zrow[ai] == p.ztag) {
+      const uint64_t zs = p.zst[ai];
+      zv = true;
+      zz = (zs & kZsZero) != 0;
+      zt = !zz && zs_task(zs) == my_task;
+      my_h = zz ? 0 : zs_hv(zs) | zs_hm(zs) << 12;
+    }
     if constexpr (kWrap)
       if (p.ws) my_prev = p.ws[ai].prev_price;
   }
+  // bit j: agent j's row state describes this buffer / the row is all-zero / its Task section
+  // holds agent j's task embedding already
+  const uint64_t zvalid = __ballot(zv), zzero = __ballot(zz), zknown_task = __ballot(zt);
+  auto task_known = [&](int j) { return ((zknown_task >> j) & 1) != 0; };
+  int nrows = 0;             // rows this wave wrote (rows_out[0])
+  unsigned long long nbytes = 0;  // bytes this wave stored (rows_out[1])
   // Entity.Query.window: ascending datastore rows within L-inf <= 7, first 100 -> vis, returns nv
   auto compact = [&](int r, int c) {
     int nv = 0;
@@ -264,7 +282,7 @@ obs_kernel(ObsParams p) {
       const int t = lane + 64 * i;
       wm[i] = t < 225 ? mat[(r + t / 15 - kVision) * kSize + c + t % 15 - kVision] : 0u;
     }
-    if (treg) {
+    if (treg && !task_known(j)) {
       const float* temb = p.task + (size_t)__builtin_amdgcn_readlane(my_task, j) * p.task_dim + lane;
 #pragma unroll
       for (int i = 0; i < kTaskRegs; i++) tv[i] = temb[64 * i];
@@ -280,11 +298,31 @@ obs_kernel(ObsParams p) {
     const int a = abase + kObsWaves * j;
     if (a >= p.P) break;
     float* row = p.obs + ((size_t)e * p.P + a) * p.elems;
-    if (!T[F_ALIVE * S + a]) {
+    const bool zv = (zvalid >> j) & 1;
+    const int hj = __builtin_amdgcn_readlane(my_h, j);
+    const int hv = hj & 4095, hm = hj >> 12;
+    if (!T[F_ALIVE * S + a]) {  // not in the realm: an all-zero row
       if (alive(j + 1)) prefetch(a + kObsWaves, j + 1);  // ahead of this row's stores
-      wave_zero(row, 0, p.elems);
+      if ((zzero >> j) & 1) continue;  // zeroed by an earlier launch into this buffer
+      if (zv) {  // zero what the last write left nonzero
+        wave_zero(row, 0, p.o_entity + hv * NMMO_N_ENTITY_COLS);
+        wave_zero(row, p.o_inventory, p.o_market + hm * 16);
+        wave_zero(row, p.o_task, p.elems);
+        nbytes += 4ull * (p.o_entity + hv * NMMO_N_ENTITY_COLS + p.o_market + hm * 16 - p.o_inventory +
+                          p.elems - p.o_task);
+      } else {
+        wave_zero(row, 0, p.elems);
+        nbytes += 4ull * p.elems;
+      }
+      if (p.ztag && lane == 0) {
+        p.zrow[(size_t)e * p.P + a] = p.ztag;
+        p.zst[(size_t)e * p.P + a] = kZsZero;
+      }
+      nrows++;
       continue;
     }
+    nrows++;
+    const bool tknown = task_known(j);
     m.a = a;
     m.r = T[F_ROW * S + a];
     m.c = T[F_COL * S + a];
@@ -300,8 +338,10 @@ obs_kernel(ObsParams p) {
     m.prev_price = kWrap ? __builtin_amdgcn_readlane(my_prev, j) : -1;
     m.movebits = move_bits(wm[1]);
     const int aid = T[F_ID * S + a];
-    // Task (from registers; a task_dim beyond kTaskRegs * 64 reads the rest directly)
-    {
+    // Task (from registers; a task_dim beyond kTaskRegs * 64 reads the rest directly), unless the
+    // row holds this task's embedding already
+    if (!tknown) {
+      nbytes += 4ull * p.task_dim;
       const int k0 = treg ? kTaskRegs * 64 : 0;  // a shorter embedding is read in place
       if (treg) {
         float* dst = row + p.o_task + lane;
@@ -322,7 +362,13 @@ obs_kernel(ObsParams p) {
     // ActionTargets, section by section
     mask_sec_f32<0, kWrap>(p, T, S, vis, inv, mpo, nm, m, row);
     mask_sec_f32<1, kWrap>(p, T, S, vis, inv, mpo, nm, m, row);
-    mask_sec_f32<2, kWrap>(p, T, S, vis, inv, mpo, nm, m, row);
+    {  // Buy.MarketItem: the listings' entries, the zero entries up to hm, and the no-op entry
+      const int n = max(nm, hm);
+      for (int k = lane; k < n; k += 64)
+        obs_st(&row[p.o_buy + k], mask_value<kWrap>(p, T, S, vis, inv, mpo, nm, m, 2, k) ? 1.f : 0.f);
+      if (lane == 0) obs_st(&row[p.o_buy + NMMO_MARKET_ROWS], 1.f);
+      nbytes += 4ull * (p.o_agent_id + 2 - NMMO_MARKET_ROWS + n);  // every mask but Buy's tail, id, tick
+    }
     mask_sec_f32<3, kWrap>(p, T, S, vis, inv, mpo, nm, m, row);
     mask_sec_f32<4, kWrap>(p, T, S, vis, inv, mpo, nm, m, row);
     mask_sec_f32<5, kWrap>(p, T, S, vis, inv, mpo, nm, m, row);
@@ -345,7 +391,13 @@ obs_kernel(ObsParams p) {
         if (f < NMMO_N_ENTITY_COLS)
           obs_st(&row[p.o_entity + k * NMMO_N_ENTITY_COLS + f], k < m.nv ? (float)T[f * S + vis[k]] : 0.f);
       }
-      wave_zero(row, p.o_entity + nv2 * NMMO_N_ENTITY_COLS, p.o_entity + kNObs * NMMO_N_ENTITY_COLS);
+      const int hz = max(nv2, hv);  // the rows past the visible ones not known zero
+      wave_zero(row, p.o_entity + nv2 * NMMO_N_ENTITY_COLS, p.o_entity + hz * NMMO_N_ENTITY_COLS);
+      nbytes += 4ull * (hz * NMMO_N_ENTITY_COLS + kInv * 16 + max(nm, hm) * 16 + 225 * 3);
+      if (p.ztag && lane == 0) {
+        if (!zv) p.zrow[(size_t)e * p.P + a] = p.ztag;
+        p.zst[(size_t)e * p.P + a] = zs_pack(nv2, nm, __builtin_amdgcn_readlane(my_task, j));
+      }
     }
     // Inventory (own items, owner = self) and Market (env listings, ascending row)
     for (int k = lane; k < kInv * 16; k += 64) {
@@ -354,8 +406,12 @@ obs_kernel(ObsParams p) {
     }
     for (int k = lane; k < nm * 16; k += 64)
       obs_st(&row[p.o_market + k], item_col(mitem[k >> 4], (mpo[k >> 4] >> 8) + 1, k & 15));
-    wave_zero(row, p.o_market + nm * 16, p.o_task);
+    wave_zero(row, p.o_market + nm * 16, p.o_market + max(nm, hm) * 16);
     __builtin_amdgcn_wave_barrier();
+  }
+  if (p.rows_out && lane == 0 && nrows) {
+    atomicAdd(p.rows_out, (unsigned long long)nrows);
+    atomicAdd(p.rows_out + 1, nbytes);
   }
 }
 

@@ -73,6 +73,9 @@ class NmmoEngine:
             self.obs = devmem.empty((wire.max_bytes(n, P),), torch.uint8, d)
         else:
             self.obs = None
+        if self.obs is not None and config.obs_layout in (abi.OBS_FLAT, abi.OBS_NATIVE):
+            # the engine's own buffer: obs rows are written incrementally (nmmo_obs_bind)
+            check(lib().nmmo_obs_bind(self.h, self._ptr(self.obs)), "nmmo_obs_bind")
         emb = np.zeros((1, config.TASK_EMBED_DIM), np.float32) if task is None else \
             task.view(np.float16).astype(np.float32).reshape(1, -1)
         self.task_table = emb  # Task obs per task index (native-layout decoding)
@@ -240,6 +243,22 @@ class NmmoEngine:
         ptr = None if counters is None else ctypes.c_void_p(counters.data_ptr())
         self._counters = counters
         check(lib().nmmo_set_counters(self.h, ptr), "nmmo_set_counters")
+
+    def set_obs_counter(self, counter):
+        """Device u64 [2] (torch int64 tensor on this device) every obs gather adds into: [0] the
+        rows it wrote (rows of agents in the realm + rows zeroed), [1] the bytes it stored
+        (nmmo_set_obs_counter); None disables."""
+        if counter is not None and (counter.numel() < 2 or counter.dtype != torch.int64
+                                    or counter.device != self.device):
+            raise ValueError("counter must be an int64 tensor of >= 2 elements on the engine's device")
+        self._obs_counter = counter
+        check(lib().nmmo_set_obs_counter(self.h, None if counter is None else ctypes.c_void_p(counter.data_ptr())),
+              "nmmo_set_obs_counter")
+
+    def obs_invalidate(self):
+        """Forget what the obs rows hold (nmmo_obs_invalidate): call after writing into self.obs;
+        the next gather writes every row in full."""
+        check(lib().nmmo_obs_invalidate(self.h, self._stream()), "nmmo_obs_invalidate")
 
     def get_fault(self) -> int:
         """The tick fault word (nmmo_get_fault: NMMO_FAULT_* | env << 8, 0 = none), then cleared."""

@@ -328,6 +328,20 @@ NMMO_API int nmmo_inject_fault(NmmoHandle* h, int32_t fault) {
   h->fault = fault;
   return NMMO_OK;
 }
+NMMO_API int nmmo_obs_bind(NmmoHandle* h, const void* obs) {
+  (void)obs;
+  if (!h) return fail(NMMO_E_INVALID, "null handle");
+  return NMMO_OK;  /* every obs call writes every row here */
+}
+NMMO_API int nmmo_obs_invalidate(NmmoHandle* h, void* stream) {
+  (void)stream;
+  if (!h) return fail(NMMO_E_INVALID, "null handle");
+  return NMMO_OK;  /* every obs call writes every row here */
+}
+NMMO_API int nmmo_set_obs_counter(NmmoHandle* h, uint64_t* c) {
+  (void)h; (void)c;
+  UNSUPPORTED("nmmo_set_obs_counter");
+}
 NMMO_API int nmmo_set_counters(NmmoHandle* h, uint64_t* c) {
   (void)h; (void)c;
   UNSUPPORTED("nmmo_set_counters");
