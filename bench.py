@@ -419,7 +419,7 @@ def measure(args, name, layout_name, envs, rank, world, dev, steps, warmup, dist
     # device counters the tick kernel adds into: [0] = sum(mask) (agent-steps), [1] = episodes,
     # [2] = event-log rows appended
     counters = [torch.zeros(3, dtype=torch.int64, device=dev) for _ in engs]
-    obs_rows = [torch.zeros(2, dtype=torch.int64, device=dev) for _ in engs]  # rows / bytes the gathers wrote
+    obs_rows = [torch.zeros((per, 2), dtype=torch.int64, device=dev) for _ in engs]  # rows / bytes per env
     for e, c, r in zip(engs, counters, obs_rows):
         e.set_counters(c)
         if wl["obs"]:
@@ -473,7 +473,7 @@ def measure(args, name, layout_name, envs, rank, world, dev, steps, warmup, dist
     tot = torch.stack(counters).sum(0)
     alive = float(tot[0].item())
     episodes = int(tot[1].item())
-    obs_cnt = torch.stack(obs_rows).sum(0)
+    obs_cnt = torch.stack(obs_rows).sum((0, 1))
     rows_written, bytes_stored = float(obs_cnt[0].item()), float(obs_cnt[1].item())
     events_per_env_tick = float(tot[2].item()) / (envs * steps) if cfg.event_cap > 0 else None
     _progress(f"{name}: timed {steps} steps in {elapsed:.3f} s")

@@ -332,9 +332,9 @@ NMMO_API int nmmo_observe(NmmoHandle* h, void* obs, void* stream);
  * full). Binding synchronises the device and forgets the previous binding; nmmo_set_tasks
  * forgets the Task sections itself. NMMO_OBS_REZERO=1 in the environment at nmmo_create turns
  * the tracking off (A/B). nmmo_set_obs_counter: when set, every obs gather adds into
- * dev_counter (device u64 [2]): [0] += rows it wrote (rows of agents in the realm + rows
- * zeroed), [1] += bytes it stored (flat: the sections written; native: whole rows); NULL
- * disables. nmmo_obs_invalidate and nmmo_set_obs_counter are enqueued on / capture-safe for
+ * dev_counter (device u64 [n_envs][2], one pair per env so the adds do not contend): [e][0] +=
+ * rows it wrote for env e (rows of agents in the realm + rows zeroed), [e][1] += bytes it stored
+ * for env e (flat: the sections written; native: whole rows); NULL disables. nmmo_obs_invalidate and nmmo_set_obs_counter are enqueued on / capture-safe for
  * `stream`. */
 NMMO_API int nmmo_obs_bind(NmmoHandle* h, const void* obs);
 NMMO_API int nmmo_obs_invalidate(NmmoHandle* h, void* stream);

@@ -548,9 +548,15 @@ int nmmo_dev_free(void* ptr) {
     g_vmm.erase(it);
   }
   HIP_TRY(hipDeviceSynchronize());  // no kernel may still use the range
-  HIP_TRY(hipMemUnmap(ptr, a.bytes));
+  // Unmapped chunk by chunk as it was mapped, and the physical chunks released; the virtual range
+  // itself stays reserved for the life of the process. Measured on MI355X: a range freed with
+  // hipMemAddressFree came back from the next hipMemAddressReserve of the same size, mapped to new
+  // chunks, and a buffer filled there read back other contents in 4 of 48 alloc / fill / check /
+  // free cycles (tools/debug/dbg_zero_rows.py) -- stale translations of the reused addresses. A
+  // range that is never reused cannot have them; the address space is 128 TB.
+  const size_t chunk = a.chunks.empty() ? a.bytes : a.bytes / a.chunks.size();
+  for (size_t i = 0; i < a.chunks.size(); i++) HIP_TRY(hipMemUnmap((char*)ptr + i * chunk, chunk));
   for (auto c : a.chunks) HIP_TRY(hipMemRelease(c));
-  HIP_TRY(hipMemAddressFree(ptr, a.bytes));
   return NMMO_OK;
 }
 

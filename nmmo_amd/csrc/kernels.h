@@ -101,7 +101,7 @@ struct ObsParams {
   uint64_t* zrow;
   uint64_t* zst;
   uint64_t ztag;
-  unsigned long long* rows_out;  // optional [2]: += rows this launch wrote, bytes it stored
+  unsigned long long* rows_out;  // optional [n][2]: += rows this launch wrote, bytes it stored, per env
 };
 constexpr uint64_t kZsZero = 1ull << 20;
 __host__ __device__ inline int zs_hv(uint64_t s) { return (int)(s & 255u); }

@@ -276,9 +276,9 @@ __global__ void __launch_bounds__(64 * kAoWaves) native_obs_kernel(ObsParams p) 
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
-  if (p.rows_out && lane == 0 && nrows) {
-    atomicAdd(p.rows_out, (unsigned long long)nrows);
-    atomicAdd(p.rows_out + 1, nbytes);
+  if (p.rows_out && lane == 0 && nrows) {  // per env: one address per env keeps the atomics uncontended
+    atomicAdd(&p.rows_out[2 * e], (unsigned long long)nrows);
+    atomicAdd(&p.rows_out[2 * e + 1], nbytes);
   }
 }
 

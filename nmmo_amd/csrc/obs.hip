@@ -409,9 +409,9 @@ obs_kernel(ObsParams p) {
     wave_zero(row, p.o_market + nm * 16, p.o_market + max(nm, hm) * 16);
     __builtin_amdgcn_wave_barrier();
   }
-  if (p.rows_out && lane == 0 && nrows) {
-    atomicAdd(p.rows_out, (unsigned long long)nrows);
-    atomicAdd(p.rows_out + 1, nbytes);
+  if (p.rows_out && lane == 0 && nrows) {  // per env: one address per env keeps the atomics uncontended
+    atomicAdd(&p.rows_out[2 * e], (unsigned long long)nrows);
+    atomicAdd(&p.rows_out[2 * e + 1], nbytes);
   }
 }
 

@@ -245,12 +245,13 @@ class NmmoEngine:
         check(lib().nmmo_set_counters(self.h, ptr), "nmmo_set_counters")
 
     def set_obs_counter(self, counter):
-        """Device u64 [2] (torch int64 tensor on this device) every obs gather adds into: [0] the
-        rows it wrote (rows of agents in the realm + rows zeroed), [1] the bytes it stored
-        (nmmo_set_obs_counter); None disables."""
-        if counter is not None and (counter.numel() < 2 or counter.dtype != torch.int64
-                                    or counter.device != self.device):
-            raise ValueError("counter must be an int64 tensor of >= 2 elements on the engine's device")
+        """Device u64 [n_envs, 2] (torch int64 tensor on this device) every obs gather adds
+        into, per env: [e, 0] the rows it wrote (rows of agents in the realm + rows zeroed),
+        [e, 1] the bytes it stored (nmmo_set_obs_counter); None disables."""
+        if counter is not None and (counter.numel() < 2 * self.n_envs or counter.dtype != torch.int64
+                                    or counter.device != self.device or not counter.is_contiguous()):
+            raise ValueError("counter must be a contiguous int64 tensor of >= 2 * n_envs elements on the "
+                             "engine's device")
         self._obs_counter = counter
         check(lib().nmmo_set_obs_counter(self.h, None if counter is None else ctypes.c_void_p(counter.data_ptr())),
               "nmmo_set_obs_counter")

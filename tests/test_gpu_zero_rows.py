@@ -42,8 +42,8 @@ def _rows(eng):
 def test_zero_row_skip_equals_full_write(layout):
     n = 4
     a, b = _engines(layout, n, seed=21)
-    ca = torch.zeros(2, dtype=torch.int64, device=a.device)
-    cb = torch.zeros(2, dtype=torch.int64, device=b.device)
+    ca = torch.zeros((n, 2), dtype=torch.int64, device=a.device)
+    cb = torch.zeros((n, 2), dtype=torch.int64, device=b.device)
     a.set_obs_counter(ca)
     b.set_obs_counter(cb)
     a.reset()
@@ -65,6 +65,7 @@ def test_zero_row_skip_equals_full_write(layout):
             assert torch.equal(a.obs.view(torch.uint8), b.obs.view(torch.uint8)), f"tick {t}"
     torch.cuda.synchronize()
     assert torch.equal(a.obs.view(torch.uint8), b.obs.view(torch.uint8))
+    ca, cb = ca.sum(0), cb.sum(0)
     total = launches * n * a.P
     assert int(cb[0].item()) == total  # every row, every launch
     assert int(ca[0].item()) < total, "no zero row was skipped (buffer not tracked?)"

@@ -1,4 +1,4 @@
-"""Debug: chunk-mapped buffer lifetime (devmem) — do live tensors keep their DeviceBuffer?"""
+"""Debug: chunk-mapped buffer reuse (devmem): allocate, fill, check, free, over and over."""
 import os
 import sys
 
@@ -9,12 +9,17 @@ from nmmo_amd import devmem  # noqa: E402
 
 devmem.MIN_BYTES = 4 << 20
 dev = torch.device("cuda", 0)
-for it in range(6):
-    bufs = []
-    for k in range(4):
-        bufs.append(devmem.empty(((8 + 7 * k + it) << 18,), torch.float32, dev))
-        print(it, k, hex(bufs[-1].data_ptr()), "pending", len(devmem._pending), flush=True)
-    ptrs = [b.data_ptr() for b in bufs]
-    print("distinct", len(set(ptrs)) == len(ptrs), flush=True)
-    del bufs
+bad, seen = 0, set()
+for it in range(24):
+    bufs = [devmem.empty(((8 + 7 * k + it % 12) << 18,), torch.float32, dev) for k in range(4)]
+    for k, b in enumerate(bufs):
+        seen.add(b.data_ptr())
+        b.fill_(float(it * 10 + k))
+    torch.cuda.synchronize()
+    for k, b in enumerate(bufs):
+        if not bool((b == float(it * 10 + k)).all()):
+            bad += 1
+            print("iteration", it, "buffer", k, "ptr", hex(b.data_ptr()), "wrong content", flush=True)
+    del bufs, b
     devmem.release_pending()
+print("vmm reuse check done: bad buffers", bad, "distinct ranges", len(seen), flush=True)
