@@ -20,8 +20,8 @@ namespace nmmo {
 constexpr int kObsAgentsPerBlock = 16;
 constexpr int kObsWaves = 4;
 constexpr int kObsFields = F_DS_ROW + 1;  // 0..30 obs columns, alive, ds_row
-// LDS: entity fields | row->slot | per-wave visible list | per-wave inventory | per-wave 15x15
-// window materials | market listings (item words, 8 B, then price | owner << 8, 2 B).
+// LDS: entity fields | row->slot | per-wave visible list | per-wave inventory | market listings
+// (item words, 8 B, then price | owner << 8, 2 B) | per-wave 15x15 window materials.
 // (The native and wire layouts have their own kernels: native_obs.hip, wire_obs.hip.)
 __host__ __device__ inline size_t obs_lds_bytes(int S) {
   return (((size_t)kObsFields * S * 2 + 15) & ~(size_t)15) + (((size_t)(S + 1) * 2 + 15) & ~(size_t)15) +
@@ -162,7 +162,7 @@ __device__ __forceinline__ uint32_t move_bits(uint32_t wm1) {
 // issue order, so a load issued after a store stream waits for all of it; issued ahead of >= 63
 // younger stores it costs no wait at all).
 #ifndef NMMO_OBS_TASK_REGS  // (A/B knobs: tools/debug/variants.py)
-#define NMMO_OBS_TASK_REGS 32
+#define NMMO_OBS_TASK_REGS 0  // (32 before the Task section was kept across steps: 156 VGPRs)
 #endif
 constexpr int kTaskRegs = NMMO_OBS_TASK_REGS;  // Task embedding dwords per lane held in registers (2,048 per row)
 
@@ -271,8 +271,9 @@ obs_kernel(ObsParams p) {
   // lane + 64 i in wm[i]) and, for flat rows, the first kTaskRegs * 64 Task embedding floats
   uint2 iv;
   uint32_t wm[4];
-  float tv[kTaskRegs];
-  const bool treg = p.task_dim >= kTaskRegs * 64;  // the first kTaskRegs * 64 Task floats prefetched
+  float tv[kTaskRegs > 0 ? kTaskRegs : 1];
+  // the first kTaskRegs * 64 Task floats prefetched
+  const bool treg = kTaskRegs > 0 && p.task_dim >= kTaskRegs * 64;
   uint8_t* wmat = wmat_all + w * 256;
   auto prefetch = [&](int a, int j) {
     const int r = T[F_ROW * S + a], c = T[F_COL * S + a];
@@ -327,16 +328,28 @@ obs_kernel(ObsParams p) {
     m.r = T[F_ROW * S + a];
     m.c = T[F_COL * S + a];
     m.gold = T[F_GOLD * S + a];
-    m.nv = compact(m.r, m.c);
-    if (lane < kInv) inv[lane] = iv;
+    // Tile: lane-per-tile (tile t = lane + 64 i): its row, column and material as three floats
+    // 12 B apart (the pass's three stores fill the same lines); the materials go through LDS so
+    // the prefetch registers are free before the compaction
 #pragma unroll
     for (int i = 0; i < 4; i++)
       if (lane + 64 * i < 225) wmat[lane + 64 * i] = (uint8_t)wm[i];
+    m.movebits = move_bits(wm[1]);
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+#pragma unroll 1
+    for (int t = lane; t < 225; t += 64) {
+      float* d = &row[p.o_tile + 3 * t];
+      obs_st(&d[0], (float)(m.r + t / 15 - kVision));
+      obs_st(&d[1], (float)(m.c + t % 15 - kVision));
+      obs_st(&d[2], (float)wmat[t]);
+    }
+    m.nv = compact(m.r, m.c);
+    if (lane < kInv) inv[lane] = iv;
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     m.ninv = inv_count(inv);
     m.prev_price = kWrap ? __builtin_amdgcn_readlane(my_prev, j) : -1;
-    m.movebits = move_bits(wm[1]);
     const int aid = T[F_ID * S + a];
     // Task (from registers; a task_dim beyond kTaskRegs * 64 reads the rest directly), unless the
     // row holds this task's embedding already
@@ -350,12 +363,6 @@ obs_kernel(ObsParams p) {
       }
       const float* temb = p.task + (size_t)__builtin_amdgcn_readlane(my_task, j) * p.task_dim;
       for (int k = k0 + lane; k < p.task_dim; k += 64) obs_st(&row[p.o_task + k], temb[k]);
-    }
-    // Tile (the window materials went to LDS with the inventory)
-    for (int k = lane; k < 225 * 3; k += 64) {
-      const int t = k / 3, comp = k - 3 * t;
-      const int tr = m.r + t / 15 - kVision, tc = m.c + t % 15 - kVision;
-      obs_st(&row[p.o_tile + k], comp == 0 ? (float)tr : comp == 1 ? (float)tc : (float)wmat[t]);
     }
     // the next agent's loads go out now, ahead of this row's remaining stores
     if (alive(j + 1)) prefetch(a + kObsWaves, j + 1);
