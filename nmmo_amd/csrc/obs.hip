@@ -17,15 +17,20 @@
 
 namespace nmmo {
 
-constexpr int kObsAgentsPerBlock = 16;
+constexpr int kObsAgentsPerBlock = 16;  // expand_kernel's shape
 constexpr int kObsWaves = 4;
+#ifndef NMMO_OBS_FLAT_APB  // (A/B knob: tools/debug/variants.py)
+#define NMMO_OBS_FLAT_APB 16
+#endif
+// obs_kernel: agents per workgroup, 4 per wave; the env's staged columns are shared by them
+constexpr int kFlatAgents = NMMO_OBS_FLAT_APB, kFlatWaves = kFlatAgents / 4;
 constexpr int kObsFields = F_DS_ROW + 1;  // 0..30 obs columns, alive, ds_row
 // LDS: entity fields | row->slot | per-wave visible list | per-wave inventory | market listings
 // (item words, 8 B, then price | owner << 8, 2 B) | per-wave 15x15 window materials.
 // (The native and wire layouts have their own kernels: native_obs.hip, wire_obs.hip.)
 __host__ __device__ inline size_t obs_lds_bytes(int S) {
   return (((size_t)kObsFields * S * 2 + 15) & ~(size_t)15) + (((size_t)(S + 1) * 2 + 15) & ~(size_t)15) +
-         (size_t)kObsWaves * 128 * 2 + (size_t)kObsWaves * kInv * 8 + (size_t)kObsWaves * 256 +
+         (size_t)kFlatWaves * 128 * 2 + (size_t)kFlatWaves * kInv * 8 + (size_t)kFlatWaves * 256 +
          (size_t)NMMO_MARKET_ROWS * 10;
 }
 
@@ -168,7 +173,7 @@ constexpr int kTaskRegs = NMMO_OBS_TASK_REGS;  // Task embedding dwords per lane
 
 // kWrap: the wrapper's observation() edits are compiled in (SPEC §13).
 template <bool kWrap>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(64 * kFlatWaves)
 #ifdef NMMO_OBS_WPE
 __attribute__((amdgpu_waves_per_eu(NMMO_OBS_WPE, NMMO_OBS_WPE)))
 #endif
@@ -178,11 +183,25 @@ obs_kernel(ObsParams p) {
   int16_t* T = reinterpret_cast<int16_t*>(smem);
   int16_t* rowslot = reinterpret_cast<int16_t*>(smem + (((size_t)kObsFields * S * 2 + 15) & ~(size_t)15));
   int16_t* vis_all = rowslot + ((((size_t)(S + 1) * 2 + 15) & ~(size_t)15) / 2);
-  uint2* inv_all = reinterpret_cast<uint2*>(vis_all + kObsWaves * 128);
-  uint2* mitem = inv_all + kObsWaves * kInv;  // listed item words
+  uint2* inv_all = reinterpret_cast<uint2*>(vis_all + kFlatWaves * 128);
+  uint2* mitem = inv_all + kFlatWaves * kInv;  // listed item words
   uint16_t* mpo = reinterpret_cast<uint16_t*>(mitem + NMMO_MARKET_ROWS);  // price | owner << 8
   uint8_t* wmat_all = reinterpret_cast<uint8_t*>(mpo + NMMO_MARKET_ROWS);  // per-wave 15x15 materials
+#ifdef NMMO_OBS_XCD  // A/B knob: 1-D grid, an env's groups on one XCD (as agent_obs.h ao_env_group)
+  const int G = (p.P + kFlatAgents - 1) / kFlatAgents, ne = p.env_list ? p.n_list : p.n_envs;
+  int el, g;
+  if ((ne & 7) == 0) {
+    const int x = blockIdx.x & 7, q = blockIdx.x >> 3;
+    g = q % G;
+    el = (q / G) * 8 + x;
+  } else {
+    el = blockIdx.x / G;
+    g = blockIdx.x - el * G;
+  }
+  const int e = p.env_list ? p.env_list[el] : el;
+#else
   const int e = p.env_list ? p.env_list[blockIdx.x] : (int)blockIdx.x, g = blockIdx.y;
+#endif
   if ((unsigned)e >= (unsigned)p.n_envs) return;  // a bad list id (the tick records it)
   const int tid = threadIdx.x;
   const int nm = p.mcount[e];
@@ -222,16 +241,16 @@ obs_kernel(ObsParams p) {
   m.no_give = kWrap && (p.wflags & kWrapObsNoGive);
   // this wave's agents: a_j = g * 16 + w + 4 j; lane j holds a_j's task index and (wrapper) last
   // Sell price, loaded before any store
-  constexpr int kPerWave = kObsAgentsPerBlock / kObsWaves;
-  const int abase = g * kObsAgentsPerBlock + w;
+  constexpr int kPerWave = kFlatAgents / kFlatWaves;
+  const int abase = g * kFlatAgents + w;
   int my_task = 0, my_prev = -1;
   // the row's state (ObsParams::zrow / zst): its Entity rows >= hv, its Market rows and
   // Buy.MarketItem entries >= hm are zero already (my_h = hv | hm << 12; a row of unknown content:
   // nothing is known zero, an all-zero row: everything)
   int my_h = kNObs | NMMO_MARKET_ROWS << 12;
   bool zv = false, zz = false, zt = false;
-  if (lane < kPerWave && abase + kObsWaves * lane < p.P) {
-    const size_t ai = (size_t)e * p.P + abase + kObsWaves * lane;
+  if (lane < kPerWave && abase + kFlatWaves * lane < p.P) {
+    const size_t ai = (size_t)e * p.P + abase + kFlatWaves * lane;
     my_task = p.assign[ai];
     if (p.ztag && p.zrow[ai] == p.ztag) {
       const uint64_t zs = p.zst[ai];
@@ -290,20 +309,20 @@ obs_kernel(ObsParams p) {
     }
   };
   auto alive = [&](int j) {
-    const int a = abase + kObsWaves * j;
+    const int a = abase + kFlatWaves * j;
     return j < kPerWave && a < p.P && T[F_ALIVE * S + a] != 0;
   };
   if (alive(0)) prefetch(abase, 0);
 
   for (int j = 0; j < kPerWave; j++) {
-    const int a = abase + kObsWaves * j;
+    const int a = abase + kFlatWaves * j;
     if (a >= p.P) break;
     float* row = p.obs + ((size_t)e * p.P + a) * p.elems;
     const bool zv = (zvalid >> j) & 1;
     const int hj = __builtin_amdgcn_readlane(my_h, j);
     const int hv = hj & 4095, hm = hj >> 12;
     if (!T[F_ALIVE * S + a]) {  // not in the realm: an all-zero row
-      if (alive(j + 1)) prefetch(a + kObsWaves, j + 1);  // ahead of this row's stores
+      if (alive(j + 1)) prefetch(a + kFlatWaves, j + 1);  // ahead of this row's stores
       if ((zzero >> j) & 1) continue;  // zeroed by an earlier launch into this buffer
       if (zv) {  // zero what the last write left nonzero
         wave_zero(row, 0, p.o_entity + hv * NMMO_N_ENTITY_COLS);
@@ -365,7 +384,7 @@ obs_kernel(ObsParams p) {
       for (int k = k0 + lane; k < p.task_dim; k += 64) obs_st(&row[p.o_task + k], temb[k]);
     }
     // the next agent's loads go out now, ahead of this row's remaining stores
-    if (alive(j + 1)) prefetch(a + kObsWaves, j + 1);
+    if (alive(j + 1)) prefetch(a + kFlatWaves, j + 1);
     // ActionTargets, section by section
     mask_sec_f32<0, kWrap>(p, T, S, vis, inv, mpo, nm, m, row);
     mask_sec_f32<1, kWrap>(p, T, S, vis, inv, mpo, nm, m, row);
@@ -427,7 +446,11 @@ hipError_t launch_obs(const ObsParams& p, hipStream_t stream) {
   if (p.nat) return launch_native_obs(p, stream);  // native_obs.hip
   const int ne = list_grid(p.env_list, p.n_list, p.n_envs);
   if (ne <= 0) return hipSuccess;
-  const dim3 grid(ne, (p.P + kObsAgentsPerBlock - 1) / kObsAgentsPerBlock), block(64 * kObsWaves);
+#ifdef NMMO_OBS_XCD
+  const dim3 grid(ne * ((p.P + kFlatAgents - 1) / kFlatAgents)), block(64 * kFlatWaves);
+#else
+  const dim3 grid(ne, (p.P + kFlatAgents - 1) / kFlatAgents), block(64 * kFlatWaves);
+#endif
   const size_t lds = obs_lds_bytes(p.S);
   if (p.wflags) hipLaunchKernelGGL(obs_kernel<true>, grid, block, lds, stream, p);
   else hipLaunchKernelGGL(obs_kernel<false>, grid, block, lds, stream, p);
