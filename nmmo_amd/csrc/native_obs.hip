@@ -101,8 +101,11 @@ __global__ void __launch_bounds__(64 * kAoWaves) native_obs_kernel(ObsParams p) 
     if constexpr (kWrap)
       if (p.ws) my_prev = p.ws[ai].prev_price;
   }
-  // bit j: agent j's row is all-zero in this buffer already (native rows track nothing else)
-  const uint64_t zknown = __ballot(p.ztag && my_z == p.ztag && (my_s & kZsZero));
+  // bit j: agent j's row state describes this buffer / the row is all-zero already; my_h: the
+  // Entity rows past which the row is zero (all 100 unknown, 0 for an all-zero row)
+  const bool zvl = p.ztag && my_z == p.ztag;
+  const uint64_t zvalid = __ballot(zvl), zknown = __ballot(zvl && (my_s & kZsZero));
+  const int my_h = !zvl ? kNObs : (my_s & kZsZero) ? 0 : zs_hv(my_s);
   int nrows = 0;                  // rows this wave wrote (rows_out[0])
   unsigned long long nbytes = 0;  // bytes this wave stored (rows_out[1])
   int wo[2];
@@ -133,8 +136,7 @@ __global__ void __launch_bounds__(64 * kAoWaves) native_obs_kernel(ObsParams p) 
       continue;
     }
     nrows++;
-    nbytes += NMMO_NATIVE_ROW_BYTES;
-    if (((zknown >> j) & 1) && lane == 0) p.zst[(size_t)e * P + a] = 0;  // the row is written now
+    const int hv = __builtin_amdgcn_readlane(my_h, j);
     const int r = __builtin_amdgcn_readfirstlane(T[F_ROW * Sp + a]);
     const int c = __builtin_amdgcn_readfirstlane(T[F_COL * Sp + a]);
     const int gold = __builtin_amdgcn_readfirstlane(T[F_GOLD * Sp + a]);
@@ -218,6 +220,7 @@ __global__ void __launch_bounds__(64 * kAoWaves) native_obs_kernel(ObsParams p) 
       const int r0 = c0 >= NMMO_N_ENTITY_COLS, r1 = c1 >= NMMO_N_ENTITY_COLS;
       const int f0 = c0 - r0 * NMMO_N_ENTITY_COLS, f1 = c1 - r1 * NMMO_N_ENTITY_COLS;
       const int nv4 = (nv + 3) & ~3;
+      const int hz = max(nv4, hv);  // the rows past the visible ones not known zero
       uint32_t* de = d32 + kNoEntity / 2;
 #pragma unroll 1
       for (int k0 = 0; k0 < nv4; k0 += 4) {
@@ -229,11 +232,16 @@ __global__ void __launch_bounds__(64 * kAoWaves) native_obs_kernel(ObsParams p) 
         }
       }
       uint8_t* zb = nrow + NMMO_NATIVE_MASK_BYTES + 2 * (kNoEntity + nv4 * NMMO_N_ENTITY_COLS);
-      uint8_t* ze = nrow + NMMO_NATIVE_MASK_BYTES + 2 * kNoInv;
+      uint8_t* ze = nrow + NMMO_NATIVE_MASK_BYTES + 2 * (kNoEntity + hz * NMMO_N_ENTITY_COLS);
+      nbytes += NMMO_NATIVE_ROW_BYTES - 2 * (kNObs - hz) * NMMO_N_ENTITY_COLS;
+      if (p.ztag && lane == 0) {
+        if (!((zvalid >> j) & 1)) p.zrow[(size_t)e * P + a] = p.ztag;
+        p.zst[(size_t)e * P + a] = zs_pack(nv4, 0, 0);
+      }
       // [zb, ze): 4-B aligned; dwords up to 16-B alignment, then 16-B stores, then dwords
-      const int head = (int)(((16 - (reinterpret_cast<uintptr_t>(zb) & 15)) & 15) >> 2);
       const int nz = (int)(ze - zb) >> 2;
-      if (lane < min(head, nz)) reinterpret_cast<uint32_t*>(zb)[lane] = 0u;
+      const int head = min((int)(((16 - (reinterpret_cast<uintptr_t>(zb) & 15)) & 15) >> 2), nz);
+      if (lane < head) reinterpret_cast<uint32_t*>(zb)[lane] = 0u;
       const int body = (nz - head) >> 2;
       uint4* z4 = reinterpret_cast<uint4*>(zb + 4 * head);
       for (int q = lane; q < body; q += 64) z4[q] = make_uint4(0u, 0u, 0u, 0u);
