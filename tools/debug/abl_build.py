@@ -31,6 +31,16 @@ PATCHES = {
     "nomask": [("native_obs.hip", "        if (q < NMMO_NATIVE_MASK_BYTES / 16) {", f"        if (q < NMMO_NATIVE_MASK_BYTES / 16 && {NEVER}) {{")],
     "noent": [("native_obs.hip", "for (int k0 = 0; k0 < nv4; k0 += 4) {", f"for (int k0 = 0; k0 < nv4 && {NEVER}; k0 += 4) {{")],
     "nnoloop": [("native_obs.hip", "  for (int j = 0; j < per_wave; j++) {", f"  for (int j = 0; j < per_wave && {NEVER}; j++) {{")],
+    # flat obs kernel (obs.hip)
+    "fnomask": [("obs.hip", "  for (int k = lane_id(); k < n; k += 64)\n    obs_st(&row[lo + k]",
+                 f"  for (int k = lane_id(); k < n && {NEVER}; k += 64)\n    obs_st(&row[lo + k]"),
+                ("obs.hip", "      for (int k = lane; k < n; k += 64)\n        obs_st(&row[p.o_buy + k]",
+                 f"      for (int k = lane; k < n && {NEVER}; k += 64)\n        obs_st(&row[p.o_buy + k]")],
+    "fnotile": [("obs.hip", "    for (int t = lane; t < 225; t += 64) {", f"    for (int t = lane; t < 225 && {NEVER}; t += 64) {{")],
+    "fnocomp": [("obs.hip", "    m.nv = compact(m.r, m.c);", f"    m.nv = {NEVER} ? compact(m.r, m.c) : 0;")],
+    "fnoent": [("obs.hip", "      for (int k0 = 0; k0 < nv2; k0 += 2) {", f"      for (int k0 = 0; k0 < nv2 && {NEVER}; k0 += 2) {{")],
+    "fnoinv": [("obs.hip", "    for (int k = lane; k < kInv * 16; k += 64) {", f"    for (int k = lane; k < kInv * 16 && {NEVER}; k += 64) {{")],
+    "fnoloop": [("obs.hip", "  for (int j = 0; j < kPerWave; j++) {", f"  for (int j = 0; j < kPerWave && {NEVER}; j++) {{")],
     "noinv": [("native_obs.hip", "    if (ninv == 0) {\n      if (lane < kInv * 8 / 4)", f"    if (ninv == 0 || {NEVER}) {{\n      if (lane < kInv * 8 / 4)")],
 }
 
