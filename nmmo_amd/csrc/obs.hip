@@ -39,9 +39,7 @@ __host__ __device__ inline size_t obs_lds_bytes(int S) {
 // from 16-byte stores (4 consecutive elements per lane) was 54% slower (3.25 vs 2.11 ms: the
 // per-element section dispatch doubled the VGPRs and halved occupancy).
 __device__ __forceinline__ void obs_st(float* p, float v) { *p = v; }
-struct Tile3 {  // one window tile of the flat Tile section: 12 B, 4-B aligned
-  float r, c, m;
-};
+
 __device__ __forceinline__ void obs_st4(float4* p, float4 v) { *p = v; }
 
 // zero bytes [lo, hi) of a row (lo, hi even): int16 stores up to 16-B alignment, then 16-B stores
@@ -177,9 +175,10 @@ constexpr int kTaskRegs = NMMO_OBS_TASK_REGS;  // Task embedding dwords per lane
 // kWrap: the wrapper's observation() edits are compiled in (SPEC §13).
 template <bool kWrap>
 __global__ void __launch_bounds__(64 * kFlatWaves)
-#ifdef NMMO_OBS_WPE
-__attribute__((amdgpu_waves_per_eu(NMMO_OBS_WPE, NMMO_OBS_WPE)))
+#ifndef NMMO_OBS_WPE  // 4 waves per SIMD: the wrapper variant would take 129 VGPRs (3 waves) and
+#define NMMO_OBS_WPE 4  // fits 128 with a 20-B spill instead; the plain one is 128 either way
 #endif
+__attribute__((amdgpu_waves_per_eu(NMMO_OBS_WPE, NMMO_OBS_WPE)))
 obs_kernel(ObsParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int S = p.S;
@@ -362,16 +361,17 @@ obs_kernel(ObsParams p) {
     m.movebits = move_bits(wm[1]);
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    // lane-per-tile: one 12-B store per window tile (a pass covers 768 contiguous bytes; measured
-    // 0.174 vs 0.196 ms per launch against contiguous dword stores with the index arithmetic)
+    // lane-per-tile: three dword stores 12 B apart per window tile (the pass's three stores fill
+    // the same 768 bytes; measured 0.174 vs 0.196 ms per launch against contiguous stores with the
+    // index arithmetic, and equal to one 12-B store, which costs the wrapper variant a VGPR over
+    // the 4-wave limit)
 #pragma unroll 1
     for (int t = lane; t < 225; t += 64) {
       const int tr = (t * 0x1112u) >> 16;  // t / 15 for t < 225
-      Tile3 v;
-      v.r = (float)(m.r + tr - kVision);
-      v.c = (float)(m.c + t - 15 * tr - kVision);
-      v.m = (float)wmat[t];
-      *reinterpret_cast<Tile3*>(&row[p.o_tile + 3 * t]) = v;
+      float* d = &row[p.o_tile + 3 * t];
+      obs_st(&d[0], (float)(m.r + tr - kVision));
+      obs_st(&d[1], (float)(m.c + t - 15 * tr - kVision));
+      obs_st(&d[2], (float)wmat[t]);
     }
     m.nv = compact(m.r, m.c);
     if (lane < kInv) inv[lane] = iv;
