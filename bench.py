@@ -534,6 +534,9 @@ def measure(args, name, layout_name, envs, rank, world, dev, steps, warmup, dist
                 timing = (f"one batch alone after the timed region: a {batch}-step hipGraph (policy + "
                           f"tick) minus a {batch}-launch policy-only hipGraph, HIP events on the "
                           f"launch stream")
+    full_b = None  # §8(d)'s model: every row written in full
+    if wl["obs"] and kern != "tick_kernel" and not rezero:
+        full_b = obs_bytes_per_env(S, P, eng.obs_elems, native, alive_frac=alive / (envs * P * steps)) * per
     prof_name = name + ("-native" if native else "-rezero" if rezero else "") + \
         ("" if wrapper == "none" else "+" + wrapper)
     launch = "eager" if not plans else f"hipGraph x{min(args.graph_steps, steps)} ticks"
@@ -546,8 +549,15 @@ def measure(args, name, layout_name, envs, rank, world, dev, steps, warmup, dist
         "kernel_ms": {"policy": round(policy_avg_ms, 5), "tick": round(tick_avg_ms, 5),
                       "obs": round(obs_avg_ms, 5) if wl["obs"] else None,
                       "wrapper": round(wrap_avg_ms, 5) if wrapper != "none" else None},
-        "roofline": _roofline(prof_name, kern, byts, ms, per, timing, nb, elapsed / steps, fill_gbs),
+        "roofline": _roofline(prof_name, kern, byts, ms, per, timing, nb, elapsed / steps, fill_gbs, full_b=full_b,
+                              byte_model=None if not wl["obs"] or kern == "tick_kernel" else
+                              "full rows" if rezero else "stored bytes"),
         "batches": nb,
+        "obs_contract": None if not wl["obs"] else
+        ("every row written in full each step (what GpuVecEnv's default obs_readonly=False gives a consumer that "
+         "may edit its rows in place)" if rezero else
+         "incremental rows into the engine's bound buffer: a row stores only what differs from what the buffer "
+         "holds (DESIGN.md §3.2c); valid for a read-only consumer (GpuVecEnv obs_readonly=True)"),
         "obs_rows_written_frac": round(row_frac, 4) if wl["obs"] else None,
         "obs_bytes_stored_per_agent_row": round(bytes_stored / (envs * P * steps), 1) if wl["obs"] else None,
     }
@@ -559,11 +569,22 @@ def measure(args, name, layout_name, envs, rank, world, dev, steps, warmup, dist
     return res
 
 
-def _roofline(prof_name, kern, byts, ms, per, timing, nb, step_s, fill_gbs, pmc_kernels=None):
+def _roofline(prof_name, kern, byts, ms, per, timing, nb, step_s, fill_gbs, pmc_kernels=None, full_b=None,
+              byte_model=None):
+    """The dominant kernel's roofline entry. byte_model names what `achieved` counts: "stored
+    bytes" for the incremental obs rows (the bytes the kernel stored, counted on the device, plus
+    its reads: DESIGN.md §3.2c), "full rows" for every row written in full (§8(d)'s model). With
+    stored bytes, `full_row_model` puts §8(d)'s full-row bytes over the same launch beside it: a
+    frac > 1 there says the launch stores far less than a full write, not that it beats HBM."""
     achieved = byts / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
     traffic, traffic_src = pmc_traffic(prof_name, pmc_kernels or kern, per)
+    full = None
+    if full_b is not None and ms > 0:
+        fa = full_b / (ms * 1e-3) / 1e9
+        full = {"bytes_per_launch": round(full_b), "achieved": round(fa, 1), "frac": round(fa / HBM_PEAK_GBS, 4)}
     return {
-        "kernel": kern, "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+        "kernel": kern, "bound": "hbm", "byte_model": byte_model, "full_row_model": full,
+        "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
         "traffic_source": traffic_src, "bytes_per_launch": round(byts), "envs_per_launch": per,
         "avg_launch_ms": round(ms, 5), "timing": timing,
@@ -726,6 +747,8 @@ def result_line(res, args, world, steps, alive_total, slots_total, elapsed, warm
         "launch": res["launch"],
         "roofline": res["roofline"],
     }
+    if res.get("obs_contract"):
+        line["config"]["obs_contract"] = res["obs_contract"]
     if res.get("obs_rows_written_frac") is not None:
         # the obs rows are written incrementally: the buffer's bytes after every step equal a full
         # write (nmmo_hip.h nmmo_obs_invalidate, tests/test_gpu_zero_rows.py)
@@ -888,6 +911,12 @@ def main():
         else:
             line["gather"] = None
         line["cpu_baseline"] = cpu
+        fw = extras.get("C4-rezero") if res["name"] == "C4" else None
+        if fw:  # the headline's full-write figure (a consumer that may edit its rows) beside it
+            line["full_write"] = {"value": fw["value"], "ms_per_step": fw["ms_per_step"],
+                                  "obs_ms": fw["kernel_ms"]["obs"], "roofline_frac": fw["roofline"]["frac"],
+                                  "frac_of_write_ceiling": fw["roofline"]["frac_of_write_ceiling"],
+                                  "see": "extra_configs.C4-rezero"}
         line["extra_configs"] = extras or None
         line["build"] = _native.build_info()
         print(json.dumps(line), file=json_out, flush=True)

@@ -329,15 +329,21 @@ NMMO_API int nmmo_observe(NmmoHandle* h, void* obs, void* stream);
  * nmmo_reset / nmmo_step / nmmo_step_envs / nmmo_observe gets every row written in full. A bound
  * buffer is the handle's until it is unbound (obs = NULL) or the handle destroyed: a caller that
  * writes into it calls nmmo_obs_invalidate first (the next gather then writes every row in
- * full). Binding synchronises the device and forgets the previous binding; nmmo_set_tasks
- * forgets the Task sections itself. NMMO_OBS_REZERO=1 in the environment at nmmo_create turns
- * the tracking off (A/B). nmmo_set_obs_counter: when set, every obs gather adds into
- * dev_counter (device u64 [n_envs][2], one pair per env so the adds do not contend): [e][0] +=
+ * full); nmmo_obs_invalidate_envs forgets only the rows of the listed envs (device int32
+ * [n_ids], ids in [0, n_envs); ids outside are ignored) -- what a pool that handed those envs'
+ * rows to a consumer that may edit them in place calls before their next gather (the
+ * reference's start-kit TileEncoder edits its Tile input in place, baseline_policy.py:96-97;
+ * nmmo_amd.vecenv.GpuVecEnv with obs_readonly=False). Binding synchronises the device and
+ * forgets the previous binding; nmmo_set_tasks forgets the Task sections itself.
+ * NMMO_OBS_REZERO=1 in the environment at nmmo_create turns the tracking off (A/B).
+ * nmmo_set_obs_counter: when set, every obs gather adds into dev_counter (device u64
+ * [n_envs][2] on the handle's device, one pair per env so the adds do not contend): [e][0] +=
  * rows it wrote for env e (rows of agents in the realm + rows zeroed), [e][1] += bytes it stored
- * for env e (flat: the sections written; native: whole rows); NULL disables. nmmo_obs_invalidate and nmmo_set_obs_counter are enqueued on / capture-safe for
- * `stream`. */
+ * for env e (flat: the sections written; native: whole rows); NULL disables.
+ * nmmo_obs_invalidate / nmmo_obs_invalidate_envs are enqueued on `stream` and capture-safe. */
 NMMO_API int nmmo_obs_bind(NmmoHandle* h, const void* obs);
 NMMO_API int nmmo_obs_invalidate(NmmoHandle* h, void* stream);
+NMMO_API int nmmo_obs_invalidate_envs(NmmoHandle* h, const int32_t* env_ids, int32_t n_ids, void* stream);
 NMMO_API int nmmo_set_obs_counter(NmmoHandle* h, uint64_t* dev_counter);
 
 /* Task table and per-player assignment (SPEC.md §12; nmmo.Env.reset(make_task_fn) /

@@ -13,7 +13,7 @@ CSRC = os.path.join(HERE, "csrc")
 LIB_DIR = os.path.join(HERE, "lib")
 LIB_PATH = os.path.join(LIB_DIR, "libnmmo_hip.so")
 STAMPS_PATH = os.path.join(LIB_DIR, "libnmmo_hip_stamps.so")
-SOURCES = ["mapgen.hip", "tick.hip", "obs.hip", "wrap.hip", "storage.hip", "wire.hip", "wire_obs.hip", "native_obs.hip", "capi.hip"]
+SOURCES = ["mapgen.hip", "tick.hip", "obs.hip", "wrap.hip", "storage.hip", "wire.hip", "wire_obs.hip", "native_obs.hip", "flat_obs.hip", "capi.hip"]
 HEADERS = ["agent_obs.h", "common.h", "kernels.h", "wire.h"]
 ARCH = os.environ.get("NMMO_OFFLOAD_ARCH", "gfx950")
 

@@ -507,8 +507,9 @@ int nmmo_dev_alloc(int32_t device, uint64_t bytes, void** out) {
   void* va = nullptr;
   HIP_TRY(hipMemAddressReserve(&va, total, chunk, nullptr, 0));
   VmmAlloc a{total, {}};
-  auto undo = [&]() {
-    (void)hipMemUnmap(va, total);
+  size_t mapped = 0;  // chunks mapped so far
+  auto undo = [&]() {  // one unmap per mapped chunk, as they were mapped (and as nmmo_dev_free does)
+    for (size_t i = 0; i < mapped; i++) (void)hipMemUnmap((char*)va + i * chunk, chunk);
     for (auto c : a.chunks) (void)hipMemRelease(c);
     (void)hipMemAddressFree(va, total);
   };
@@ -523,6 +524,7 @@ int nmmo_dev_alloc(int32_t device, uint64_t bytes, void** out) {
       undo();
       return fail(NMMO_E_HIP, "hipMemMap at offset %zu", off);
     }
+    mapped++;
   }
   hipMemAccessDesc acc = {};
   acc.location = prop.location;
@@ -579,8 +581,36 @@ int nmmo_obs_invalidate(NmmoHandle* h, void* stream) {
   return NMMO_OK;
 }
 
+// the row-state tags of the listed envs' rows (zrow[e * P + a] = 0: nothing known about the row)
+__global__ void obs_forget_envs_kernel(uint64_t* zrow, const int32_t* ids, int n_ids, int n_envs, int P) {
+  const int i = blockIdx.x, e = ids[i];
+  if ((unsigned)e >= (unsigned)n_envs) return;
+  for (int a = threadIdx.x; a < P; a += blockDim.x) zrow[(size_t)e * P + a] = 0;
+}
+
+int nmmo_obs_invalidate_envs(NmmoHandle* h, const int32_t* env_ids, int32_t n_ids, void* stream) {
+  if (!h) return fail(NMMO_E_INVALID, "null handle");
+  if (n_ids < 0 || n_ids > h->st.n_envs) return fail(NMMO_E_INVALID, "n_ids %d not in 0..%d", n_ids, h->st.n_envs);
+  if (n_ids > 0 && !env_ids) return fail(NMMO_E_INVALID, "null env_ids");
+  if (!h->d_zrow || n_ids == 0) return NMMO_OK;
+  HIP_TRY(hipSetDevice(h->device));
+  hipLaunchKernelGGL(obs_forget_envs_kernel, dim3(n_ids), dim3(128), 0, (hipStream_t)stream, h->d_zrow, env_ids,
+                     n_ids, h->st.n_envs, h->st.P);
+  HIP_TRY(hipGetLastError());
+  return NMMO_OK;
+}
+
 int nmmo_set_obs_counter(NmmoHandle* h, uint64_t* dev_rows) {
   if (!h) return fail(NMMO_E_INVALID, "null handle");
+  if (dev_rows) {  // the kernels add into it: it must be device memory of the handle's device
+    HIP_TRY(hipSetDevice(h->device));
+    hipPointerAttribute_t at;
+    if (hipPointerGetAttributes(&at, dev_rows) != hipSuccess || at.type != hipMemoryTypeDevice ||
+        at.device != h->device) {
+      (void)hipGetLastError();
+      return fail(NMMO_E_INVALID, "nmmo_set_obs_counter: not device memory of device %d", h->device);
+    }
+  }
   h->d_rows_out = reinterpret_cast<unsigned long long*>(dev_rows);
   return NMMO_OK;
 }

@@ -1,0 +1,363 @@
+// flat_obs.hip — the pufferlib-flat float32 obs rows (23,987 per agent, SPEC.md §8) written
+// incrementally into the handle's bound buffer (nmmo_obs_bind): a row stores only
+// what differs from what the buffer already holds (ObsParams::zrow / zst). Replaces
+// Env._compute_observations + pufferlib's flatten/pad (the rows the reference's learner decodes with
+// unpack_batched_obs, baseline_policy.py:41) for the bound buffer; an unbound or untracked buffer
+// gets every row in full from obs.hip's obs_kernel<kWrap, true>.
+//
+// Round 5 rewrite on agent_obs.h's pieces (the native kernel's staging, compaction and section bit
+// fields). The round-4 flat kernel was issue-bound (per agent row 760 VALU, 524 SALU, 146 branch
+// for 33 stores; profiles/r04/pmc_flat): one predicate per mask entry, index arithmetic per store,
+// 31-way LDS bank conflicts on the Entity gathers and SGPR spills. Here, per agent wave:
+//  - ActionTargets: 25 chunks of 64 entries; chunk c's 64-bit mask is the OR of the sections' bit
+//    fields at compile-time shifts (the Buy.MarketItem part from one ballot per 64 listings), and
+//    lane L stores bit L of it as 0.f / 1.f -- one v_cndmask on the SGPR pair
+//    (__builtin_amdgcn_inverse_ballot_w64) and one store per chunk. Chunks holding only Buy entries
+//    at or past the row's known-zero threshold are skipped. AgentId / CurrentTick ride in the last
+//    chunk's lanes 50 and 51;
+//  - the env's Entity columns staged with an odd dword stride (conflict-free lane-per-field reads),
+//    the window compaction from packed datastore-row words held in registers, and the workgroup's
+//    window rows and item words staged in LDS up front, so the agent loop issues no global load
+//    (except a Task section to rewrite, once per task change, and listings past the staged 256);
+//  - every store goes to the row's wave-uniform base (SGPRs) plus a per-lane constant offset.
+#include "agent_obs.h"
+
+namespace nmmo {
+
+constexpr int kFoStagedListings = 256;  // listings whose item words are staged (Market rows)
+constexpr int kFoChunks = 25;           // 64-entry chunks over the 1,586 mask entries (+ id, tick)
+static_assert(kFoChunks * 64 >= kMaskN + 2 && (kFoChunks - 1) * 64 < kMaskN, "mask chunks");
+static_assert(sec_flat(2) == 104 && sec_flat(3) == 104 + NMMO_MARKET_ROWS + 1, "Buy.MarketItem bits");
+constexpr int kFoBuyLo = sec_flat(2);
+// the flat row's section offsets (nmmo_layout; launch_flat_obs checks the handle's): compile-time,
+// so the agent loop keeps few uniform values live (every runtime offset was an SGPR the loop spilled)
+constexpr int kFoId = kMaskN, kFoEntity = kFoId + 2, kFoInv = kFoEntity + kNObs * NMMO_N_ENTITY_COLS,
+              kFoMarket = kFoInv + kInv * 16, kFoTask = kFoMarket + NMMO_MARKET_ROWS * 16;
+
+// LDS: agent_obs.h's entity staging | listings (price | owner << 8, u16) | the first 256 listings'
+// item words | per-wave visible rows | the workgroup's staged window rows and item words.
+// 38.7 KB at S = 384: 4 workgroups per CU.
+__host__ __device__ inline size_t fo_lds_bytes(int S) {
+  return ao_entity_lds(S) + (size_t)NMMO_MARKET_ROWS * 2 + (size_t)kFoStagedListings * 8 +
+         (size_t)kAoWaves * 128 * 4 + ao_win_lds();
+}
+
+// Low 64 bits of the 128-bit field (hi:lo) shifted left by kSh (right when negative): the part of a
+// section whose bit 0 sits at chunk bit kSh.
+template <int kSh>
+__device__ __forceinline__ uint64_t fo_shift(uint64_t lo, uint64_t hi) {
+  if constexpr (kSh >= 64) {
+    return 0ull;
+  } else if constexpr (kSh > 0) {
+    return lo << kSh;
+  } else if constexpr (kSh == 0) {
+    return lo;
+  } else if constexpr (-kSh < 64) {
+    return (lo >> (-kSh)) | (hi << (64 + kSh));
+  } else if constexpr (-kSh < 128) {
+    return hi >> (-kSh - 64);
+  } else {
+    return 0ull;
+  }
+}
+// Section k's contribution to chunk kC (entries 64 kC .. 64 kC + 63 of the flat mask part)
+template <int kK, int kC>
+__device__ __forceinline__ uint64_t fo_sec(uint64_t lo, uint64_t hi) {
+  constexpr int off = sec_flat(kK), n = kSecN[kK];
+  if constexpr (off >= 64 * kC + 64 || off + n <= 64 * kC) return 0ull;
+  else return fo_shift<off - 64 * kC>(lo, hi);
+}
+// The 11 section fields (every section but Buy.MarketItem) in chunk kC
+template <int kC>
+__device__ __forceinline__ uint64_t fo_chunk(const AoSections& x) {
+  return fo_sec<0, kC>(x.s0, 0ull) | fo_sec<1, kC>(x.s1[0], x.s1[1]) | fo_sec<3, kC>(x.s3, 0ull) |
+         fo_sec<4, kC>(x.s4, 0ull) | fo_sec<5, kC>(x.s5[0], x.s5[1]) | fo_sec<6, kC>(x.s6[0], x.s6[1]) |
+         fo_sec<7, kC>(x.s7[0], x.s7[1]) | fo_sec<8, kC>(x.s8, 0ull) | fo_sec<9, kC>(x.s9, 0ull) |
+         fo_sec<10, kC>(x.s10[0], x.s10[1]) | fo_sec<11, kC>(x.s11, 0ull);
+}
+__device__ __forceinline__ float fo_bit(uint64_t m) { return __builtin_amdgcn_inverse_ballot_w64(m) ? 1.f : 0.f; }
+
+// Chunks kC .. kFoChunks - 1 (past Buy.MarketItem's entries; chunk 17 also holds Buy's last 40
+// entries and its no-op): lane L of chunk kC stores entry 64 kC + L. buy17: Buy's bits in chunk 17.
+template <int kC>
+__device__ __forceinline__ void fo_tail_chunks(float* row, const AoSections& x, uint64_t buy17, float aid, float tick) {
+  if constexpr (kC < kFoChunks) {
+    uint64_t m = fo_chunk<kC>(x);
+    if constexpr (kC == (kFoBuyLo + NMMO_MARKET_ROWS) / 64) m |= buy17 | 1ull << ((kFoBuyLo + NMMO_MARKET_ROWS) & 63);
+    const int lane = lane_id();
+    if constexpr (kC == kFoChunks - 1) {  // + AgentId, CurrentTick right after the mask entries
+      constexpr int n = kMaskN - 64 * kC;
+      if (lane < n + 2) row[64 * kC + lane] = lane < n ? fo_bit(m) : lane == n ? aid : tick;
+    } else {
+      row[64 * kC + lane] = fo_bit(m);
+    }
+    fo_tail_chunks<kC + 1>(row, x, buy17, aid, tick);
+  }
+}
+
+// Window compaction as agent_obs.h's ao_compact over all kAoRows register words (the rows past S
+// hold kAoEmpty, outside every window): no bound on S to keep live across the agent loop
+__device__ __forceinline__ int fo_compact(const uint32_t (&pr)[kAoRows], int r, int c, uint32_t* visw) {
+  int nvis = 0;
+  const uint32_t rc = (uint32_t)r | (uint32_t)c << 16;
+#pragma unroll
+  for (int i = 0; i < kAoRows; i++) {
+    const bool in = ao_in_window(pr[i], rc);
+    const uint64_t b = __ballot(in);
+    const int pos = nvis + __popcll(b & lanes_below());
+    if (in && pos < kNObs) visw[pos] = pr[i];
+    nvis += __popcll(b);
+  }
+  return nvis;
+}
+
+// kS: the slot count when known at compile time (C3 / C4: 128 players + 256 NPCs), 0 = p.S. With
+// it the staged-column offsets are immediates instead of uniform values the agent loop keeps live.
+template <bool kWrap, int kS>
+__global__ void __launch_bounds__(64 * kAoWaves) flat_obs_kernel(ObsParams p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int S = kS ? kS : p.S, P = p.P, Sp = ao_stride(S), tdim = p.task_dim, elems = kFoTask + tdim + 225 * 3;
+  int16_t* T = reinterpret_cast<int16_t*>(smem);
+  uint32_t* pk = reinterpret_cast<uint32_t*>(smem + ao_entity_lds(S) - (size_t)(kMaxSlots + 64) * 4);
+  uint16_t* mpo = reinterpret_cast<uint16_t*>(pk + kMaxSlots + 64);            // [1024] price | owner << 8
+  uint2* mitem = reinterpret_cast<uint2*>(mpo + NMMO_MARKET_ROWS);            // [256] listed item words
+  uint32_t* visw_all = reinterpret_cast<uint32_t*>(mitem + kFoStagedListings);  // [4][128]
+  uint32_t* wst = visw_all + kAoWaves * 128;                                   // [16][15][5] window rows
+  uint2* ist = reinterpret_cast<uint2*>(wst + kAoAgents * kAoWinAgentBytes / 4);  // [16][12] item words
+  const int el = blockIdx.x, g = blockIdx.y;
+  const int e = p.env_list ? p.env_list[el] : el, tid = threadIdx.x, lane = lane_id();
+  if ((unsigned)e >= (unsigned)p.n_envs) return;  // a bad list id (the tick records it)
+  const int w = __builtin_amdgcn_readfirstlane(wave_id());
+  const int nm = min(max(p.mcount[e], 0), NMMO_MARKET_ROWS);
+  for (int j = tid; j < nm; j += blockDim.x) {  // end-of-tick listings, ascending row
+    const int v = p.mlist[(size_t)e * NMMO_MARKET_ROWS + j];
+    const int own = (v >> 16) & 255, slot = (v >> 24) & 15;
+    const uint2 wd = p.items[((size_t)e * P + own) * kInv + slot];
+    mpo[j] = (uint16_t)(it_price(wd) | own << 8);
+    if (j < kFoStagedListings) mitem[j] = wd;
+  }
+  ao_stage(p, e, T, pk);  // (publishes mpo / mitem too)
+  ao_stage_windows(p, e, g, T, Sp, wst, ist);
+
+  uint32_t pr[kAoRows];  // this lane's datastore rows 1 + lane + 64 i
+#pragma unroll
+  for (int i = 0; i < kAoRows; i++) pr[i] = pk[lane + 64 * i];
+  uint32_t* visw = visw_all + w * 128;
+  const uint8_t* wsb = reinterpret_cast<const uint8_t*>(wst);
+  const int16_t* E = p.ent + (size_t)e * NMMO_NF * S;
+  const float tickf = (float)p.env[(size_t)e * NMMO_NE + E_TICK];
+  const bool exch = (p.systems & NMMO_SYS_ITEM) && (p.systems & NMMO_SYS_EXCHANGE);
+
+  constexpr int kPerWave = kAoAgents / kAoWaves;
+  const int abase = g * kAoAgents + w;
+  int my_task = 0, my_prev = -1, my_alive = 0;  // lane j: agent abase + 4 j
+  uint64_t my_z = 0, my_s = 0;                  // its row state tag and word
+  if (lane < kPerWave && abase + kAoWaves * lane < P) {
+    const int aj = abase + kAoWaves * lane;
+    const size_t ai = (size_t)e * P + aj;
+    my_task = p.assign[ai];
+    my_alive = E[F_ALIVE * S + aj];
+    my_z = p.zrow[ai];
+    my_s = p.zst[ai];
+    if constexpr (kWrap)
+      if (p.ws) my_prev = p.ws[ai].prev_price;
+  }
+  // bit j: agent j's row state describes this buffer / the row is all-zero / its Task section holds
+  // its task's embedding; my_h = hv | hm << 12: its Entity rows >= hv and its Market rows and Buy
+  // entries >= hm are zero (a row of unknown content: nothing known zero)
+  const bool zvl = p.ztag && my_z == p.ztag;
+  const bool zzl = zvl && (my_s & kZsZero);
+  const uint64_t zvalid = __ballot(zvl), zzero = __ballot(zzl), ztask = __ballot(zvl && !zzl && zs_task(my_s) == my_task);
+  const int my_h = !zvl ? (kNObs | NMMO_MARKET_ROWS << 12) : zzl ? 0 : (zs_hv(my_s) | zs_hm(my_s) << 12);
+  int nrows = 0;                  // rows this wave wrote (rows_out[0])
+  unsigned long long nbytes = 0;  // bytes this wave stored (rows_out[1])
+  int wo[2];
+  ao_win_offsets(wo);
+  int toff[4];  // window tile lane + 64 i: (row offset) & 255 | (col offset) << 8
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const int t = lane + 64 * i;
+    toff[i] = ((t / 15 - kVision) & 255) | (t % 15 - kVision) * 256;
+  }
+  const int ef = lane & 31, eh = lane >> 5;  // Entity: field, row of the pair
+  const int icol = lane & 15, iq = lane >> 4;  // Inventory / Market: column, item of the chunk
+
+#pragma unroll 1
+  for (int j = 0; j < kPerWave; j++) {
+    const int a = abase + kAoWaves * j;
+    if (a >= P) break;
+    float* row = p.obs + ((size_t)e * P + a) * elems;
+    const bool zv = (zvalid >> j) & 1;
+    const int hj = __builtin_amdgcn_readlane(my_h, j);
+    const int hv = hj & 4095, hm = hj >> 12;
+    if (!__builtin_amdgcn_readlane(my_alive, j)) {  // not in the realm: an all-zero row
+      if ((zzero >> j) & 1) continue;  // zeroed by an earlier launch into this buffer
+      if (zv) {  // zero what the last write left nonzero
+        wave_zero(row, 0, kFoEntity + hv * NMMO_N_ENTITY_COLS);
+        wave_zero(row, kFoInv, kFoMarket + hm * 16);
+        wave_zero(row, kFoTask, elems);
+        nbytes += 4ull * (kFoEntity + hv * NMMO_N_ENTITY_COLS + kFoMarket + hm * 16 - kFoInv + elems - kFoTask);
+      } else {
+        wave_zero(row, 0, elems);
+        nbytes += 4ull * elems;
+      }
+      if (lane == 0) {
+        p.zrow[(size_t)e * P + a] = p.ztag;
+        p.zst[(size_t)e * P + a] = kZsZero;
+      }
+      nrows++;
+      continue;
+    }
+    nrows++;
+    const int la = a - g * kAoAgents;
+    const int r = __builtin_amdgcn_readfirstlane(T[F_ROW * Sp + a]);
+    const int c = __builtin_amdgcn_readfirstlane(T[F_COL * Sp + a]);
+    const int gold = __builtin_amdgcn_readfirstlane(T[F_GOLD * Sp + a]);
+    const int aid = __builtin_amdgcn_readfirstlane(T[F_ID * Sp + a]);
+    const uint8_t* wa = wsb + la * kAoWinAgentBytes + ((c - kVision) & 3);
+    uint32_t wm[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) wm[i] = lane + 64 * i < 225 ? wa[ao_win_off(wo, i)] : 0u;
+    const uint2 it = lane < kInv ? ist[la * kInv + lane] : make_uint2(0u, 0u);
+    const uint32_t mv = ao_move_bits(wm[1]);
+    const int ninv = __builtin_ctzll(~__ballot(lane < kInv && it_type(it) != 0));  // occupied prefix
+    const int nv = min(fo_compact(pr, r, c, visw), kNObs);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+    // ActionTargets (+ AgentId, CurrentTick)
+    {
+      AoAgent ag;
+      ag.a = a;
+      ag.ti = a;
+      ag.r = r;
+      ag.c = c;
+      ag.gold = gold;
+      ag.aid = aid;
+      ag.nv = nv;
+      ag.ninv = ninv;
+      ag.prev_price = kWrap ? __builtin_amdgcn_readlane(my_prev, j) : -1;
+      ag.mv = mv;
+      const AoSections x = ao_sections<kWrap>(p, T, Sp, visw, ag, it);
+      row[lane] = fo_bit(fo_chunk<0>(x));
+      // Buy.MarketItem entry k < listings: exchange on, price <= gold, not the agent's own. buy_word
+      // m = the ballot over listings 64 m + lane; chunk c holds words c - 1 (from bit 40) and c - 2
+      // (its top 40 bits). Chunks 2..16 hold Buy entries only: written up to the known-zero
+      // threshold max(nm, hm) (their entries past nm are zero).
+      auto buy_word = [&](int m) {
+        const int k = 64 * m + lane;
+        bool bv = false;
+        if (exch && k < nm) {
+          const uint32_t po = mpo[k];
+          bv = (int)(po & 255u) <= gold && (int)(po >> 8) != a;
+        }
+        return __ballot(bv);
+      };
+      const int nbuy = max(nm, hm);
+      const int clast = max(1, min((kFoBuyLo + nbuy - 1) >> 6, 16));
+      uint64_t bprev = 0ull;
+      const uint64_t c1 = fo_chunk<1>(x);
+#pragma unroll 1
+      for (int cc = 1; cc <= clast; cc++) {
+        const uint64_t bcur = 64 * (cc - 1) < nm ? buy_word(cc - 1) : 0ull;
+        const uint64_t m = (cc == 1 ? c1 : 0ull) | bcur << (kFoBuyLo & 63) | bprev >> (64 - (kFoBuyLo & 63));
+        row[64 * cc + lane] = fo_bit(m);
+        bprev = bcur;
+      }
+      // chunk 17: Buy entries 984..1023 (word 15, only when nm > 960: the loop then ran to 16)
+      const uint64_t buy17 = nm > 15 * 64 ? bprev >> (64 - (kFoBuyLo & 63)) : 0ull;
+      fo_tail_chunks<(kFoBuyLo + NMMO_MARKET_ROWS) / 64>(row, x, buy17, (float)aid, tickf);
+      nbytes += 4ull * (64 * (1 + clast) + 64 * (kFoChunks - 1 - (kFoBuyLo + NMMO_MARKET_ROWS) / 64) +
+                        (kMaskN - 64 * (kFoChunks - 1)) + 2);
+    }
+    // Entity rows: two per pass (lanes 0-30 row k, lanes 32-62 row k + 1: 62 contiguous floats),
+    // the rows past the visible ones not known zero as one zero run
+    const int nv2 = (nv + 1) & ~1;
+    {
+      float* de = row + kFoEntity + (lane - eh);
+#pragma unroll 1
+      for (int k0 = 0; k0 < nv2; k0 += 2) {
+        const int k = k0 + eh;
+        if (ef < NMMO_N_ENTITY_COLS)
+          de[k0 * NMMO_N_ENTITY_COLS] = k < nv ? (float)T[ef * Sp + ao_slot(visw[k])] : 0.f;
+      }
+      const int hz = max(nv2, hv);
+      wave_zero(row, kFoEntity + nv2 * NMMO_N_ENTITY_COLS, kFoEntity + hz * NMMO_N_ENTITY_COLS);
+      nbytes += 4ull * (hz * NMMO_N_ENTITY_COLS + kInv * 16 + max(nm, hm) * 16 + 225 * 3);
+    }
+    // Inventory: item q = 4 h + lane / 16, column lane % 16 (own items, owner = self)
+#pragma unroll
+    for (int h = 0; h < kInv * 16 / 64; h++) {
+      const int q = 4 * h + iq;
+      float v = 0.f;
+      if (q < ninv) v = item_col(ist[la * kInv + q], aid, icol);
+      row[kFoInv + 64 * h + lane] = v;
+    }
+    // Market (the env's listings, ascending row; owner = lister) and its zero run down to hm
+    for (int k = lane; k < nm * 16; k += 64) {
+      const int q = k >> 4;
+      const uint2 wd = q < kFoStagedListings ? mitem[q] : [&]() {
+        const int v = p.mlist[(size_t)e * NMMO_MARKET_ROWS + q];
+        return p.items[((size_t)e * P + ((v >> 16) & 255)) * kInv + ((v >> 24) & 15)];
+      }();
+      row[kFoMarket + k] = item_col(wd, (mpo[q] >> 8) + 1, icol);
+    }
+    wave_zero(row, kFoMarket + nm * 16, kFoMarket + max(nm, hm) * 16);
+    // Task: only when the row does not hold this task's embedding yet (read in place)
+    const int task = __builtin_amdgcn_readlane(my_task, j);
+    if (!((ztask >> j) & 1)) {
+      const float* temb = p.task + (size_t)task * tdim;
+      for (int k = lane; k < tdim; k += 64) row[kFoTask + k] = temb[k];
+      nbytes += 4ull * tdim;
+    }
+    // Tile: (row, column, material) per window tile t = lane + 64 i, three stores 12 B apart
+    {
+      float* dt = row + kFoTask + tdim + 3 * lane;
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        if (lane + 64 * i < 225) {
+          dt[192 * i] = (float)(r + ((toff[i] << 24) >> 24));
+          dt[192 * i + 1] = (float)(c + (toff[i] >> 8));
+          dt[192 * i + 2] = (float)wm[i];
+        }
+      }
+    }
+    if (lane == 0) {
+      if (!zv) p.zrow[(size_t)e * P + a] = p.ztag;
+      p.zst[(size_t)e * P + a] = zs_pack(nv2, nm, task);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the next agent reuses visw
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  if (p.rows_out && lane == 0 && nrows) {  // per env: one address per env keeps the atomics uncontended
+    atomicAdd(&p.rows_out[2 * e], (unsigned long long)nrows);
+    atomicAdd(&p.rows_out[2 * e + 1], nbytes);
+  }
+}
+
+bool flat_obs_ok(const ObsParams& p) {  // agent_obs.h's staging: S a multiple of 8 (16-B column loads)
+  return p.S % 8 == 0 && p.S <= kMaxSlots && p.P <= 128 && p.obs && p.ztag && p.zrow && ao_layout_ok(p) &&
+         p.o_agent_id == kFoId && p.o_tick == kFoId + 1 && p.o_entity == kFoEntity && p.o_inventory == kFoInv &&
+         p.o_market == kFoMarket && p.o_task == kFoTask && p.o_tile == kFoTask + p.task_dim &&
+         p.elems == p.o_tile + 225 * 3;
+}
+
+hipError_t launch_flat_obs(const ObsParams& p, hipStream_t stream) {
+  if (!flat_obs_ok(p)) return hipErrorInvalidValue;
+  const int ne = list_grid(p.env_list, p.n_list, p.n_envs);
+  if (ne <= 0) return hipSuccess;
+  const dim3 grid(ne, (p.P + kAoAgents - 1) / kAoAgents), block(64 * kAoWaves);
+  const size_t lds = fo_lds_bytes(p.S);
+  if (p.S == kMaxSlots) {
+    if (p.wflags) hipLaunchKernelGGL((flat_obs_kernel<true, kMaxSlots>), grid, block, lds, stream, p);
+    else hipLaunchKernelGGL((flat_obs_kernel<false, kMaxSlots>), grid, block, lds, stream, p);
+  } else {
+    if (p.wflags) hipLaunchKernelGGL((flat_obs_kernel<true, 0>), grid, block, lds, stream, p);
+    else hipLaunchKernelGGL((flat_obs_kernel<false, 0>), grid, block, lds, stream, p);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace nmmo

@@ -169,6 +169,9 @@ hipError_t launch_wire_unpack(const uint8_t* wire, uint8_t* native, int n, int P
 hipError_t launch_wire_header(const ObsParams& p, hipStream_t s);
 // NMMO_OBS_WIRE obs gather (wire_obs.hip): header pre-pass + wire_obs_kernel
 hipError_t launch_wire_obs(const ObsParams& p, hipStream_t s);
+// flat obs rows into the handle's bound buffer, incrementally (flat_obs.hip; p.ztag != 0)
+hipError_t launch_flat_obs(const ObsParams& p, hipStream_t s);
+bool flat_obs_ok(const ObsParams& p);  // launch_flat_obs takes p (else obs_kernel<kWrap, false>)
 // NMMO_OBS_NATIVE obs gather (native_obs.hip)
 hipError_t launch_native_obs(const ObsParams& p, hipStream_t s);
 // header + record-head consistency of a wire buffer; bits into *status (0 = valid)

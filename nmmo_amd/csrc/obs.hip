@@ -170,16 +170,28 @@ __device__ __forceinline__ uint32_t move_bits(uint32_t wm1) {
 #ifndef NMMO_OBS_TASK_REGS  // (A/B knobs: tools/debug/variants.py)
 #define NMMO_OBS_TASK_REGS 0  // (32 before the Task section was kept across steps: 156 VGPRs)
 #endif
-constexpr int kTaskRegs = NMMO_OBS_TASK_REGS;  // Task embedding dwords per lane held in registers (2,048 per row)
+// Task embedding dwords per lane held in registers (2,048 per row): the incremental variant writes
+// a Task section once per episode and reads it in place; the full-write variant (every row every
+// launch: an unbound or untracked buffer, NMMO_OBS_REZERO) prefetches its first 2,048 floats with
+// the agent's other loads, so its Task stores never wait behind the Tile stores issued before them.
+#ifndef NMMO_OBS_FULL_TREGS  // (A/B knobs: 0 and 4 = the round-4 full write)
+#define NMMO_OBS_FULL_TREGS 32
+#endif
+#ifndef NMMO_OBS_FULL_WPE
+#define NMMO_OBS_FULL_WPE 3
+#endif
+constexpr int kTaskRegsFull = NMMO_OBS_FULL_TREGS;
 
-// kWrap: the wrapper's observation() edits are compiled in (SPEC §13).
-template <bool kWrap>
-__global__ void __launch_bounds__(64 * kFlatWaves)
+// kWrap: the wrapper's observation() edits are compiled in (SPEC §13). kFull: no row state (every
+// row written in full, Task from registers); 3 waves per SIMD (the registers take it past 128).
 #ifndef NMMO_OBS_WPE  // 4 waves per SIMD: the wrapper variant would take 129 VGPRs (3 waves) and
 #define NMMO_OBS_WPE 4  // fits 128 with a 20-B spill instead; the plain one is 128 either way
 #endif
-__attribute__((amdgpu_waves_per_eu(NMMO_OBS_WPE, NMMO_OBS_WPE)))
+template <bool kWrap, bool kFull>
+__global__ void __launch_bounds__(64 * kFlatWaves)
+__attribute__((amdgpu_waves_per_eu(kFull ? NMMO_OBS_FULL_WPE : NMMO_OBS_WPE, kFull ? NMMO_OBS_FULL_WPE : NMMO_OBS_WPE)))
 obs_kernel(ObsParams p) {
+  constexpr int kTaskRegs = kFull ? kTaskRegsFull : NMMO_OBS_TASK_REGS;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int S = p.S;
   int16_t* T = reinterpret_cast<int16_t*>(smem);
@@ -462,8 +474,17 @@ hipError_t launch_obs(const ObsParams& p, hipStream_t stream) {
   const dim3 grid(ne, (p.P + kFlatAgents - 1) / kFlatAgents), block(64 * kFlatWaves);
 #endif
   const size_t lds = obs_lds_bytes(p.S);
-  if (p.wflags) hipLaunchKernelGGL(obs_kernel<true>, grid, block, lds, stream, p);
-  else hipLaunchKernelGGL(obs_kernel<false>, grid, block, lds, stream, p);
+  if (p.ztag) {  // the bound buffer: incremental rows (flat_obs.hip; here the round-4 kernel for slot
+                 // counts that are not a multiple of 8, and under NMMO_FLAT_V1)
+#ifndef NMMO_FLAT_V1
+    if (flat_obs_ok(p)) return launch_flat_obs(p, stream);
+#endif
+    if (p.wflags) hipLaunchKernelGGL((obs_kernel<true, false>), grid, block, lds, stream, p);
+    else hipLaunchKernelGGL((obs_kernel<false, false>), grid, block, lds, stream, p);
+  } else {  // every row in full
+    if (p.wflags) hipLaunchKernelGGL((obs_kernel<true, true>), grid, block, lds, stream, p);
+    else hipLaunchKernelGGL((obs_kernel<false, true>), grid, block, lds, stream, p);
+  }
   return hipGetLastError();
 }
 

@@ -261,6 +261,17 @@ class NmmoEngine:
         the next gather writes every row in full."""
         check(lib().nmmo_obs_invalidate(self.h, self._stream()), "nmmo_obs_invalidate")
 
+    def obs_invalidate_envs(self, env_ids):
+        """Forget what the listed envs' obs rows hold (nmmo_obs_invalidate_envs; env_ids a
+        contiguous int32 tensor on the device): their next gather writes those rows in full.
+        Enqueued on the current stream."""
+        if env_ids.dtype != torch.int32 or env_ids.device != self.device or not env_ids.is_contiguous():
+            raise ValueError("env_ids must be a contiguous int32 tensor on the engine's device")
+        with torch.cuda.device(self.device):
+            check(lib().nmmo_obs_invalidate_envs(self.h, self._ptr(env_ids), env_ids.numel(), self._stream()),
+                  "nmmo_obs_invalidate_envs")
+        self._inv_ids = env_ids  # alive until the stream has read it
+
     def get_fault(self) -> int:
         """The tick fault word (nmmo_get_fault: NMMO_FAULT_* | env << 8, 0 = none), then cleared."""
         f = ctypes.c_int32()

@@ -22,6 +22,19 @@ Differences by design: `recv` returns device tensors for the observations (the t
 `torch.as_tensor(o).to(device)` at :302,318 is then a no-op instead of an H2D copy); `mask` is a
 host numpy bool array because the trainer combines it with host arrays (:306,334).
 
+The obs contract at this boundary. `recv` hands out views of the engine's own obs buffer (a
+batch of contiguous envs), which the engine writes incrementally (nmmo_obs_bind: a row stores only
+what differs from what the buffer already holds). In the reference the trainer's `.to(device)`
+copies the shared-memory rows, so a policy may edit its input in place -- the start-kit's
+TileEncoder does (`tile[:, :, :2] -= ...; += 7`, baseline_policy.py:96-97, on
+unpack_batched_obs views). So by default (`obs_readonly=False`) `send` forgets the row state of
+the envs whose rows the last `recv` handed out (nmmo_obs_invalidate_envs) before it steps them:
+their next gather rewrites those rows in full, and every `recv` returns the bytes of a full write
+whatever the consumer did to the previous ones. `obs_readonly=True` is the consumer's promise not
+to write into the returned rows (a policy that copies first, a learner that only reads): the rows
+stay incremental, ~6 KB stored per 96-KB row. A batch that wraps around the env
+range is returned as a copy and needs neither.
+
 Protocol 1 — `NmmoEnv` exposes `reset(seed)` / `step(actions)` with per-agent dict
 observations (the unflattened layout) like `nmmo.Env`, for wrappers such as
 `reinforcement_learning/stat_wrapper.py` (the realm facade is partial: see `NmmoEnv.realm`).
@@ -132,8 +145,13 @@ class GpuVecEnv:
 
     def __init__(self, env_creator=None, env_kwargs=None, num_envs=1, envs_per_worker=1,
                  envs_per_batch=None, env_pool=False, mask_agents=True, *, config=None,
-                 device=None, seed=0, task_embedding=None, env_index_base=0, agent=None):
+                 device=None, seed=0, task_embedding=None, env_index_base=0, agent=None,
+                 obs_readonly=False):
+        """obs_readonly: the consumer never writes into the obs rows recv() returns (module
+        docstring); False (default) keeps in-place edits from reaching later recv() outputs."""
         del envs_per_worker  # the engine replaces workers
+        self.obs_readonly = bool(obs_readonly)
+        self._views_out = False  # the last recv() handed out views of the engine's obs buffer
         self.config = config or _config_from_kwargs(env_kwargs)
         rw = _as_dict(env_kwargs.get("reward_wrapper")) if isinstance(env_kwargs, dict) else {}
         if config is None and "early_stop_agent_num" in rw:  # BaseStatWrapper's early stop (stat_wrapper.py:68-69)
@@ -198,6 +216,7 @@ class GpuVecEnv:
         if batch == list(range(lo, lo + k)):  # contiguous envs: views of the engine's buffers
             sl = slice(lo, lo + k)
             o = e.obs[sl].view(N, e.obs_elems)
+            self._views_out = True
             r, d, t, m = (x[sl].reshape(N) for x in (e.rew, e.term, e.trunc, e.mask))
         else:  # the batch wraps around: gather its env rows (nmmo_gather_rows)
             idx = torch.as_tensor(batch, dtype=torch.int32).to(e.device)
@@ -211,6 +230,7 @@ class GpuVecEnv:
                                              ctypes.c_void_p(torch.cuda.current_stream(e.device).cuda_stream)),
                       "nmmo_gather_rows")
             o = self._obs_b.view(N, e.obs_elems)
+            self._views_out = False  # a copy: the engine's rows were not handed out
             il = idx.long()
             r, d, t, m = (x.index_select(0, il).reshape(N) for x in (e.rew, e.term, e.trunc, e.mask))
         mask = m.to(torch.bool).cpu().numpy()  # the host sync of this step
@@ -243,7 +263,10 @@ class GpuVecEnv:
         batch, k, P, e = self._batch, self.envs_per_batch, self.agents_per_env, self.engine
         a = torch.as_tensor(actions)
         a = a.to(device=e.device, dtype=torch.int32).reshape(k, P, abi.N_ACTION_HEADS)
+        forget = self._views_out and not self.obs_readonly  # the consumer may have edited the rows
         if k == self.num_envs:  # lockstep (every recv returns 0..num_envs-1 in order)
+            if forget:
+                e.obs_invalidate()
             e.step(a)
         else:
             lo = batch[0]
@@ -253,7 +276,10 @@ class GpuVecEnv:
                 e.actions.index_copy_(0, torch.as_tensor(batch, dtype=torch.long, device=e.device), a)
             self._ids_host.copy_(torch.as_tensor(batch, dtype=torch.int32))
             self._ids.copy_(self._ids_host, non_blocking=True)
+            if forget:
+                e.obs_invalidate_envs(self._ids)
             e.step_envs(self._ids)
+        self._views_out = False
         self._ready.extend(batch)
         self._batch = None
 
