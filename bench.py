@@ -174,6 +174,9 @@ def parse(argv=None):
                     help="run env_creator's RewardWrapper on the device (SPEC §13) with the "
                          "config.yaml weights")
     ap.add_argument("--no-decode", action="store_true", help="C5: skip the decoded pass")
+    ap.add_argument("--root-rehearsal", type=int, default=7,
+                    help="C5 at N = 1: a root_loaded pass in which rank 0 also validates and stores this many "
+                         "phantom peers' buffers each step (0 = off)")
     ap.add_argument("--dry-launch", action="store_true",
                     help="launcher check: each rank prints its RANK/WORLD_SIZE and exits (no GPU)")
     ap.add_argument("--inject-fault", action="store_true", help=argparse.SUPPRESS)  # tests: nmmo_inject_fault
@@ -633,17 +636,21 @@ def measure_gather(args, name, envs, rank, world, dev, steps, warmup, dist=None,
     torch.cuda.synchronize(dev)
     passes = {}
     modes = ("delivered",) if args.no_decode else ("delivered", "stored", "decoded")
+    rh = args.root_rehearsal if world == 1 and not args.no_decode else 0
+    if rh > 0:
+        modes += ("root_loaded",)
     for mode in modes:
         decode = mode == "decoded"
         store = None
-        if mode == "stored" and rank == 0:  # compact record storage of every row of every step
+        ranks = world + (rh if mode == "root_loaded" else 0)  # ranks whose rows the root stores
+        if mode in ("stored", "root_loaded") and rank == 0:  # compact record storage of every row of every step
             from nmmo_amd.storage import DeviceExperience
 
-            rows = world * envs * cfg.PLAYER_N
+            rows = ranks * envs * cfg.PLAYER_N
             store = DeviceExperience(rows, engs[0].obs_elems, rows, device=dev,
-                                     record_arena_bytes=world * nb * (nw.max_bytes(per, cfg.PLAYER_N) + 64))
+                                     record_arena_bytes=ranks * nb * (nw.max_bytes(per, cfg.PLAYER_N) + 64))
         g = WireGather(engs, pseed, rank, world, decode=decode, graphs=not args.no_graph, backend=backend,
-                       store=store)
+                       store=store, rehearse=rh if mode == "root_loaded" else 0)
         for _ in range(warmup):
             g.step()
         g.drain()
@@ -708,6 +715,8 @@ def measure_gather(args, name, envs, rank, world, dev, steps, warmup, dist=None,
         "wire_bytes_per_agent_in_realm": round(wire_env_bytes * per * nb * steps / max(d["alive"], 1.0), 1),
         "decoded": passes.get("decoded"),
         "stored": passes.get("stored"),
+        "root_loaded": passes.get("root_loaded"),
+        "root_rehearsal": rh,
     }
     for e in engs:
         e.close()
@@ -843,11 +852,18 @@ def main():
         """The C5 line's learner-side passes (whole job, max over ranks): "stored" (rank 0 keeps
         every row of every step in compact record storage) and "decoded"."""
         out = {}
+        rh = r.get("root_rehearsal") or 0
         for mode, what in (("stored", "rank 0 also stores every rank's rows in the realm each step as "
                                       "experience (nmmo_exp_store_records: the rows' fields + their wire "
                                       "records in an arena, flat rows expanded per minibatch)"),
                            ("decoded", "rank 0 also decodes every rank's wire buffers into the native layout "
-                                       "(nmmo_wire_unpack) each step: the full learner-ready obs tensor")):
+                                       "(nmmo_wire_unpack) each step: the full learner-ready obs tensor"),
+                           ("root_loaded", f"the stored pass with the root's load of an N = {rh + 1} node: each "
+                                           f"step rank 0 also copies its own buffers into {rh} phantom peers' "
+                                           f"receive buffers (the incoming transfers' HBM writes), validates "
+                                           f"(nmmo_wire_check) and stores them as those peers' rows on its comm "
+                                           f"stream; value counts only rank 0's own agents (the xGMI links are "
+                                           f"not modelled)")):
             if not r.get(mode):
                 continue
             pr = dict(r, elapsed=r[mode]["elapsed"], alive=r[mode]["alive"])

@@ -555,8 +555,12 @@ typedef struct NmmoRecordStore {
   int32_t* row_agent;    /* device [capacity]: env * player_n + agent in that buffer */
 } NmmoRecordStore;
 
-/* int32 scratch the storage calls need: max(n_rows + n_rows/512 + 8, n_slots). */
+/* int32 scratch the storage calls need: max(n_rows + n_rows/512 + 8, n_slots).
+ * nmmo_exp_scratch_ints_many: what nmmo_exp_store_records_many over n_inputs inputs of at most
+ * max_rows rows each needs (its per-input block counts take more than the summed rows' count when
+ * many small inputs meet few slots); NMMO_E_INVALID (< 0) for n_inputs outside 1..16. */
 NMMO_API int64_t nmmo_exp_scratch_ints(int32_t max_rows, int32_t n_slots);
+NMMO_API int64_t nmmo_exp_scratch_ints_many(int32_t n_inputs, int32_t max_rows, int32_t n_slots);
 /* Appends the mask-selected rows of one recv (in row order, cut at the capacity) and advances
  * *ptr on the device; exactly one of obs / native / wire: native obs are expanded, and wire
  * records decoded, straight into the flat experience rows of the kept rows only (h = a handle
@@ -574,8 +578,8 @@ NMMO_API int nmmo_exp_store_records(NmmoHandle* h, const NmmoExperience* x, cons
  * one store (the learner storing every rank's buffers of a step: a fixed number of launches
  * whatever the input count). field_stride > 0: each input's rewards / dones / mask are read
  * field_stride bytes apart per row (float at rewards, u8 at dones and mask; e.g. an 8-B packed
- * per-agent record), 0: packed arrays as in nmmo_exp_store. scratch: nmmo_exp_scratch_ints of
- * the inputs' summed rows. Enqueued. */
+ * per-agent record), 0: packed arrays as in nmmo_exp_store. scratch: nmmo_exp_scratch_ints_many
+ * ints. Enqueued. */
 NMMO_API int nmmo_exp_store_records_many(NmmoHandle* h, const NmmoExperience* x, const NmmoRecordStore* rs,
                                          const NmmoStoreInput* ins, int32_t n_inputs, int32_t field_stride,
                                          int32_t* scratch, void* stream);

@@ -28,7 +28,7 @@ SYMBOLS = [
     "nmmo_wire_pack", "nmmo_wire_unpack", "nmmo_wire_check", "nmmo_dev_alloc", "nmmo_dev_free", "nmmo_observe",
     "nmmo_step_envs", "nmmo_inject_fault", "nmmo_fault_into", "nmmo_exp_store_records",
     "nmmo_exp_gather_records", "nmmo_exp_store_records_many", "nmmo_obs_invalidate", "nmmo_set_obs_counter",
-    "nmmo_obs_bind", "nmmo_obs_invalidate_envs",
+    "nmmo_obs_bind", "nmmo_obs_invalidate_envs", "nmmo_exp_scratch_ints_many",
 ]
 
 
@@ -101,6 +101,8 @@ def declare(L):
     xp = ctypes.POINTER(abi.NmmoExperience)
     L.nmmo_exp_scratch_ints.argtypes = [i32, i32]
     L.nmmo_exp_scratch_ints.restype = ctypes.c_int64
+    L.nmmo_exp_scratch_ints_many.argtypes = [i32, i32, i32]
+    L.nmmo_exp_scratch_ints_many.restype = ctypes.c_int64
     L.nmmo_exp_store.argtypes = [vp, xp, ctypes.POINTER(abi.NmmoStoreInput), vp, vp]
     L.nmmo_exp_sort.argtypes = [xp, vp, vp, vp]
     rsp = ctypes.POINTER(abi.NmmoRecordStore)

@@ -7,6 +7,7 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <algorithm>
 #include <map>
 #include <mutex>
 #include <string>
@@ -663,6 +664,14 @@ int nmmo_wire_unpack(int32_t n_envs, int32_t player_n, const void* wire, void* n
 int64_t nmmo_exp_scratch_ints(int32_t max_rows, int32_t n_slots) {
   const int64_t a = (int64_t)max_rows + store_blocks(max_rows) + 8;
   return a > n_slots ? a : (int64_t)n_slots;
+}
+
+int64_t nmmo_exp_scratch_ints_many(int32_t n_inputs, int32_t max_rows, int32_t n_slots) {
+  if (n_inputs < 1 || n_inputs > kMaxStoreInputs || max_rows < 0)
+    return fail(NMMO_E_INVALID, "n_inputs %d not in 1..%d / max_rows < 0", n_inputs, kMaxStoreInputs);
+  const int64_t a = nmmo_exp_scratch_ints((int32_t)std::min<int64_t>((int64_t)n_inputs * max_rows, INT32_MAX), n_slots);
+  const int64_t b = store_many_scratch_ints(n_inputs, max_rows);
+  return a > b ? a : b;
 }
 
 static int check_exp(const NmmoExperience* x, bool need_obs = true) {

@@ -24,6 +24,9 @@
 
 namespace nmmo {
 
+#ifndef NMMO_FO_ABL  // diagnostic ablation (timing attribution only, wrong rows): bit 1 masks, 2 Entity,
+#define NMMO_FO_ABL 0  // 4 Inventory, 8 Market, 16 Tile, 32 compaction (tools/debug/variants.py)
+#endif
 constexpr int kFoStagedListings = 256;  // listings whose item words are staged (Market rows)
 constexpr int kFoChunks = 25;           // 64-entry chunks over the 1,586 mask entries (+ id, tick)
 static_assert(kFoChunks * 64 >= kMaskN + 2 && (kFoChunks - 1) * 64 < kMaskN, "mask chunks");
@@ -94,6 +97,51 @@ __device__ __forceinline__ void fo_tail_chunks(float* row, const AoSections& x, 
     fo_tail_chunks<kC + 1>(row, x, buy17, aid, tick);
   }
 }
+
+// item_col (common.h) for a column fixed per lane (Inventory / Market chunks: lane L holds
+// column L % 16 of every item it writes): a per-lane descriptor built once, so an entry is one
+// bit-field extract plus a type-mask term instead of a 16-way select per entry.
+//   value = bfe(x or y, sh, wd) + own * owner + mult * level + (mult ? b : 0),
+//   mult = bit(type) of tmA * aA + bit(type) of tmB * aB
+struct IcDesc {
+  uint32_t tmA, tmB;
+  uint32_t f;  // sel | sh << 1 | wd << 6 | own << 11 | aA << 12 | aB << 16 | b << 20
+};
+__device__ __forceinline__ IcDesc ic_desc(int col) {
+  auto bits = [](int lo, int hi) { return ((2u << hi) - 1u) & ~((1u << lo) - 1u); };
+  IcDesc d{0u, 0u, 0u};
+  auto bf = [&](int sel, int sh, int wd) { d.f = (uint32_t)(sel | sh << 1 | wd << 6); };
+  switch (col) {
+    case 0: bf(1, 16, 16); break;  // row
+    case 1: bf(0, 0, 5); break;    // type
+    case 2: d.f = 1u << 11; break; // owner
+    case 3: bf(0, 5, 4); break;    // level
+    case 5: bf(1, 0, 16); break;   // quantity
+    case 6: case 7: case 8:        // melee / range / mage attack
+      d.tmA = 1u << (T_SPEAR + col - 6) | 1u << (T_WHETSTONE + col - 6);
+      d.f = 5u << 12 | 5u << 20;
+      break;
+    case 9: case 10: case 11:      // defense
+      d.tmA = bits(T_HAT, T_BOTTOM);
+      d.tmB = bits(T_ROD, T_CHISEL);
+      d.f = 3u << 12 | 2u << 16;
+      break;
+    case 12: d.tmA = 1u << T_POTION; d.f = 5u << 12 | 50u << 20; break;
+    case 13: d.tmA = 1u << T_RATION; d.f = 5u << 12 | 50u << 20; break;
+    case 14: bf(0, 9, 1); break;   // equipped
+    case 15: bf(0, 10, 7); break;  // listed price
+    default: break;                // 4: zero
+  }
+  return d;
+}
+__device__ __forceinline__ float ic_value(uint2 w, int owner, const IcDesc& d) {
+  const int type = (int)(w.x & 31u), lvl = (int)((w.x >> 5) & 15u);
+  const uint32_t bfv = __builtin_amdgcn_ubfe((d.f & 1u) ? w.y : w.x, (d.f >> 1) & 31u, (d.f >> 6) & 31u);
+  const int ta = (int)((d.tmA >> type) & 1u), tb = (int)((d.tmB >> type) & 1u);
+  const int mult = ta * (int)((d.f >> 12) & 15u) + tb * (int)((d.f >> 16) & 15u);
+  return (float)((int)bfv + (int)((d.f >> 11) & 1u) * owner + mult * lvl + ((ta | tb) ? (int)(d.f >> 20) : 0));
+}
+static_assert(T_POTION < 32 && T_RATION < 32 && T_WHETSTONE + 2 < 32, "item type masks");
 
 // Window compaction as agent_obs.h's ao_compact over all kAoRows register words (the rows past S
 // hold kAoEmpty, outside every window): no bound on S to keep live across the agent loop
@@ -180,7 +228,8 @@ __global__ void __launch_bounds__(64 * kAoWaves) flat_obs_kernel(ObsParams p) {
     toff[i] = ((t / 15 - kVision) & 255) | (t % 15 - kVision) * 256;
   }
   const int ef = lane & 31, eh = lane >> 5;  // Entity: field, row of the pair
-  const int icol = lane & 15, iq = lane >> 4;  // Inventory / Market: column, item of the chunk
+  const int iq = lane >> 4;                  // Inventory: item of the chunk
+  const IcDesc icd = ic_desc(lane & 15);      // Inventory / Market: column lane % 16
 
 #pragma unroll 1
   for (int j = 0; j < kPerWave; j++) {
@@ -221,13 +270,13 @@ __global__ void __launch_bounds__(64 * kAoWaves) flat_obs_kernel(ObsParams p) {
     const uint2 it = lane < kInv ? ist[la * kInv + lane] : make_uint2(0u, 0u);
     const uint32_t mv = ao_move_bits(wm[1]);
     const int ninv = __builtin_ctzll(~__ballot(lane < kInv && it_type(it) != 0));  // occupied prefix
-    const int nv = min(fo_compact(pr, r, c, visw), kNObs);
+    const int nv = (NMMO_FO_ABL & 32) ? 0 : min(fo_compact(pr, r, c, visw), kNObs);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
     // ActionTargets (+ AgentId, CurrentTick)
-    {
+    if (!(NMMO_FO_ABL & 1)) {
       AoAgent ag;
       ag.a = a;
       ag.ti = a;
@@ -274,7 +323,7 @@ __global__ void __launch_bounds__(64 * kAoWaves) flat_obs_kernel(ObsParams p) {
     // Entity rows: two per pass (lanes 0-30 row k, lanes 32-62 row k + 1: 62 contiguous floats),
     // the rows past the visible ones not known zero as one zero run
     const int nv2 = (nv + 1) & ~1;
-    {
+    if (!(NMMO_FO_ABL & 2)) {
       float* de = row + kFoEntity + (lane - eh);
 #pragma unroll 1
       for (int k0 = 0; k0 < nv2; k0 += 2) {
@@ -288,20 +337,20 @@ __global__ void __launch_bounds__(64 * kAoWaves) flat_obs_kernel(ObsParams p) {
     }
     // Inventory: item q = 4 h + lane / 16, column lane % 16 (own items, owner = self)
 #pragma unroll
-    for (int h = 0; h < kInv * 16 / 64; h++) {
+    for (int h = 0; h < ((NMMO_FO_ABL & 4) ? 0 : kInv * 16 / 64); h++) {
       const int q = 4 * h + iq;
       float v = 0.f;
-      if (q < ninv) v = item_col(ist[la * kInv + q], aid, icol);
+      if (4 * h < ninv && q < ninv) v = ic_value(ist[la * kInv + q], aid, icd);  // (a uniform skip first)
       row[kFoInv + 64 * h + lane] = v;
     }
     // Market (the env's listings, ascending row; owner = lister) and its zero run down to hm
-    for (int k = lane; k < nm * 16; k += 64) {
+    for (int k = lane; k < ((NMMO_FO_ABL & 8) ? 0 : nm * 16); k += 64) {
       const int q = k >> 4;
       const uint2 wd = q < kFoStagedListings ? mitem[q] : [&]() {
         const int v = p.mlist[(size_t)e * NMMO_MARKET_ROWS + q];
         return p.items[((size_t)e * P + ((v >> 16) & 255)) * kInv + ((v >> 24) & 15)];
       }();
-      row[kFoMarket + k] = item_col(wd, (mpo[q] >> 8) + 1, icol);
+      row[kFoMarket + k] = ic_value(wd, (mpo[q] >> 8) + 1, icd);
     }
     wave_zero(row, kFoMarket + nm * 16, kFoMarket + max(nm, hm) * 16);
     // Task: only when the row does not hold this task's embedding yet (read in place)
@@ -312,7 +361,7 @@ __global__ void __launch_bounds__(64 * kAoWaves) flat_obs_kernel(ObsParams p) {
       nbytes += 4ull * tdim;
     }
     // Tile: (row, column, material) per window tile t = lane + 64 i, three stores 12 B apart
-    {
+    if (!(NMMO_FO_ABL & 16)) {
       float* dt = row + kFoTask + tdim + 3 * lane;
 #pragma unroll
       for (int i = 0; i < 4; i++) {

@@ -250,7 +250,12 @@ class WireGather:
 
     def __init__(self, engines, policy_seed: int, rank: int = 0, world: int = 1, decode: bool = False,
                  graphs: bool = True, ring: int = 3, on_step=None, backend: str | None = None,
-                 before_step=None, store=None):
+                 before_step=None, store=None, rehearse: int = 0):
+        """rehearse = R > 0 (root): after its real buffers, the root also treats R phantom peers'
+        buffers each step -- its own step's buffers copied into receive buffers (the HBM writes of
+        the incoming transfers), validated (nmmo_wire_check), decoded / stored as a peer's -- so a
+        one-GPU run carries the root's compute load of an N = R + 1 node (bench.py
+        --root-rehearsal; the xGMI links themselves are not modelled)."""
         if before_step is not None and graphs:
             raise ValueError("before_step needs graphs=False")
         self.before_step = before_step
@@ -265,10 +270,33 @@ class WireGather:
         e0 = self.engines[0]
         self.device = e0.device
         self.P = e0.P
+        import numpy as np
+
         for e in self.engines:
             if e.config.obs_layout != abi.OBS_WIRE:
                 raise ValueError("WireGather steps handles created with obs_layout OBS_WIRE")
+            if not np.array_equal(e.task_table, e0.task_table):
+                raise ValueError("WireGather: the batches' task tables differ (records decode with one table)")
         nb = len(self.engines)
+        # the root sizes its receive buffers from its own batches, places buffer (r, j)'s rows at
+        # global agent slot (r * envs + env offset of batch j) * P and decodes every buffer with its
+        # own task table: every rank must have the same batches and task table (checked once here)
+        self._env0 = [0]
+        for e in self.engines:
+            self._env0.append(self._env0[-1] + e.n_envs)
+        if world > 1:
+            import zlib
+
+            shape = np.asarray([e.n_envs for e in self.engines], np.int64)
+            sig = torch.tensor([nb, int(shape.sum()), zlib.crc32(shape.tobytes()),
+                                zlib.crc32(np.ascontiguousarray(e0.task_table, np.float32).tobytes())],
+                               dtype=torch.int64, device=self.device)
+            lo, hi = sig.clone(), sig.clone()
+            dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+            dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+            if not torch.equal(lo, hi):
+                raise ValueError("WireGather: ranks differ in their env batches or task table (the root receives "
+                                 "and decodes every rank's buffers with its own)")
         self.ring = ring
         self.wires = [[e.obs] + [devmem.empty(tuple(e.obs.shape), torch.uint8, self.device) for _ in range(ring - 1)]
                       for e in self.engines]
@@ -289,6 +317,14 @@ class WireGather:
             self.native = {(r, j): devmem.empty((n_envs[j], abi.native_env_bytes(self.P)), torch.uint8, self.device)
                            for r in range(world) for j in range(nb)}
         self._zeros = self._acts = None
+        self.rehearse = int(rehearse) if rank == 0 else 0
+        if self.rehearse:  # the phantom peers' receive buffers, one set per phantom as a real root's
+            self._rh_wire = {(q, j): devmem.empty((caps[j],), torch.uint8, self.device)
+                             for q in range(self.rehearse) for j in range(nb)}
+            self._rh_small = {(q, j): torch.empty_like(self.smalls[j][0]) for q in range(self.rehearse) for j in range(nb)}
+            self._rh_native = None if not decode else \
+                {(q, j): devmem.empty((e.n_envs, abi.native_env_bytes(self.P)), torch.uint8, self.device)
+                 for q in range(self.rehearse) for j, e in enumerate(self.engines)}
         self.graphs = None
         if graphs:
             self._capture()
@@ -326,18 +362,28 @@ class WireGather:
         with torch.cuda.stream(self.x.comm):
             nb = len(self.engines)
             batch = []
-            for (r, j), (w, sm) in got.items():
+            items = list(got.items())
+            for q in range(1, self.rehearse + 1):  # phantom peer q: the root's own buffers, copied in
+                for j in range(nb):
+                    w0, sm0 = got[0, j]
+                    w, sm = self._rh_wire[q - 1, j][:w0.numel()], self._rh_small[q - 1, j]
+                    w.copy_(w0)
+                    sm.copy_(sm0)
+                    items.append(((self.world - 1 + q, j), (w, sm)))
+            for (r, j), (w, sm) in items:
                 n = self.engines[j].n_envs
                 if r != 0:  # a received buffer against the size its sender announced
-                    nw.check_buffer(w, n, self.P, self.status, self.x.sizes[s % self.ring, r, j:j + 1])
+                    nw.check_buffer(w, n, self.P, self.status,
+                                    self.x.sizes[s % self.ring, r if r < self.world else 0, j:j + 1])
                 if self.native is not None:
-                    nw.unpack(w, n, self.P, out=self.native[r, j])
+                    nw.unpack(w, n, self.P, out=self.native[r, j] if r < self.world else
+                              self._rh_native[r - self.world, j])
                 if self.store is not None:  # learner mask = in the realm; no policy outputs modelled
                     if self._zeros is None or self._zeros.numel() < n * self.P:
                         self._zeros = torch.zeros(n * self.P, device=self.device)
                         self._acts = torch.zeros((n * self.P, 12), dtype=torch.int32, device=self.device)
                     z = self._zeros[:n * self.P]
-                    base = (r * nb * n + j * n) * self.P  # global agent slot of the buffer's first row
+                    base = (r * self._env0[-1] + self._env0[j]) * self.P  # global slot of the buffer's first row
                     st = sm.view(-1)  # 8 B per agent: reward f32 | term | trunc | mask | pad
                     batch.append((w, st, st[4:], st[6:], self._acts[:n * self.P], z, z, base))
             if self.store is not None:  # every buffer of the step as one store (fixed launch count)

@@ -81,8 +81,12 @@ class DeviceExperience:
     def _stream(self):
         return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
 
-    def _ensure_scratch(self, n_rows: int):
+    def _ensure_scratch(self, n_rows: int, n_inputs: int = 0, max_rows: int = 0):
+        """n_rows: the rows of one store; n_inputs > 0: a store_many over n_inputs inputs of at most
+        max_rows rows (nmmo_exp_scratch_ints_many)."""
         need = int(lib().nmmo_exp_scratch_ints(max(n_rows, 1), self.n_slots))
+        if n_inputs:
+            need = max(need, int(lib().nmmo_exp_scratch_ints_many(n_inputs, max(max_rows, 1), self.n_slots)))
         if self.scratch.numel() < need:
             self.scratch = torch.zeros(need, dtype=torch.int32, device=self.device)
 
@@ -191,7 +195,7 @@ class DeviceExperience:
             arr[i] = abi.NmmoStoreInput(nr, int(step), None, None, r.data_ptr(), d.data_ptr(), m.data_ptr(), None,
                                         int(base), a.data_ptr(), lp.data_ptr(), v.data_ptr(), w.data_ptr())
             keep.append((w, r, d, m, a, lp, v))
-        self._ensure_scratch(rows)
+        self._ensure_scratch(rows, n, max(a.shape[0] for _, _, _, _, a, _, _, _ in inputs))
         self._engine = engine
         with torch.cuda.device(self.device):
             check(lib().nmmo_exp_store_records_many(engine.h, ctypes.byref(self.x), ctypes.byref(self.records), arr, n,

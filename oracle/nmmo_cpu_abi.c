@@ -355,6 +355,10 @@ NMMO_API int64_t nmmo_exp_scratch_ints(int32_t max_rows, int32_t n_slots) {
   (void)max_rows; (void)n_slots;
   UNSUPPORTED("nmmo_exp_scratch_ints");
 }
+NMMO_API int64_t nmmo_exp_scratch_ints_many(int32_t n_inputs, int32_t max_rows, int32_t n_slots) {
+  (void)n_inputs; (void)max_rows; (void)n_slots;
+  UNSUPPORTED("nmmo_exp_scratch_ints_many");
+}
 NMMO_API int nmmo_exp_store(NmmoHandle* h, const NmmoExperience* x, const NmmoStoreInput* in, int32_t* s, void* st) {
   (void)h; (void)x; (void)in; (void)s; (void)st;
   UNSUPPORTED("nmmo_exp_store");
