@@ -260,6 +260,38 @@ __device__ __forceinline__ uint32_t ao_move_bits(uint32_t wm1) {
   return b;
 }
 
+// Use.InventoryItem over the inventory (lane k holds slot k's item word; `have`: slot k occupied):
+// common.h item_usable without its per-lane branches. Lane i < 8 reads skill level i (melee,
+// range, mage, fishing, herbalism, prospecting, carving, alchemy: F_MELEE_LEVEL + 2 i), lane 8 the
+// max of the combat levels; an item's requirement is the lane its type maps to (a 4-bit table,
+// requirement_level's cases), fetched with one cross-lane read.
+static_assert(F_ALCHEMY_LEVEL == F_MELEE_LEVEL + 14 && F_FISHING_LEVEL == F_MELEE_LEVEL + 6 &&
+                  F_HERBALISM_LEVEL == F_MELEE_LEVEL + 8, "skill level fields");
+__host__ __device__ constexpr uint64_t ao_req_lut() {  // type -> requirement lane (types 0..15)
+  uint64_t m = 0;
+  for (int t = 0; t < 16; t++) {
+    const int k = (t >= T_SPEAR && t <= T_WAND) ? t - T_SPEAR : (t >= T_WHETSTONE && t <= T_RUNES) ? t - T_WHETSTONE
+                  : (t >= T_ROD && t <= T_CHISEL) ? 3 + t - T_ROD : 8;
+    m |= (uint64_t)k << (4 * t);
+  }
+  return m;
+}
+static_assert(T_RATION == 16 && T_POTION == 17, "requirement table: ration -> fishing, potion -> herbalism");
+__device__ __forceinline__ uint64_t ao_usable_ballot(const int16_t* T, int Sp, int ti, uint2 it, bool have) {
+  const int lane = lane_id();
+  int lv = 0;
+  if (lane < 8) {
+    lv = T[(F_MELEE_LEVEL + 2 * lane) * Sp + ti];
+  } else if (lane == 8) {
+    lv = max((int)T[F_MELEE_LEVEL * Sp + ti], max((int)T[F_RANGE_LEVEL * Sp + ti], (int)T[F_MAGE_LEVEL * Sp + ti]));
+  }
+  const int type = it_type(it);
+  const int k = type < 16 ? (int)((ao_req_lut() >> (4 * type)) & 15u) : type == T_RATION ? 3 : type == T_POTION ? 4 : 8;
+  const int req = __shfl(lv, k);
+  const bool eq = type >= T_HAT && type <= T_RUNES && it_equipped(it);  // equip_slot(type) >= 0
+  return __ballot(have && !it_price(it) && (eq || it_level(it) <= req));
+}
+
 // The 11 ActionTargets sections other than Buy.MarketItem as wave-uniform bit fields (SPEC §8,
 // §9, §13 edits): bit k = entry k of the section.
 struct AoSections {
@@ -309,7 +341,7 @@ __device__ __forceinline__ AoSections ao_sections(const ObsParams& p, const int1
   x.s3 = (item ? bfr : 0ull) | 1ull << kInv;
   x.s4 = (item && !no_give ? bfr : 0ull) | 1ull << kInv;
   x.s9 = (exch ? __ballot(have && !it_equipped(it)) : 0ull) | 1ull << kInv;
-  x.s11 = (item ? __ballot(have && item_usable(T, Sp, g.ti, it)) : 0ull) | 1ull << kInv;
+  x.s11 = (item ? ao_usable_ballot(T, Sp, g.ti, it, have) : 0ull) | 1ull << kInv;
   // closed forms: 0 Style, 6 GoldPrice (k < gold), 8 Move, 10 SellPrice (all but the wrapper's
   // last price)
   x.s0 = combat ? low_bits(kSecN[0]) : 0ull;

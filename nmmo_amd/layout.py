@@ -96,6 +96,21 @@ def unflatten(flat, task_dim: int = 2048) -> dict:
     return out
 
 
+def unpack_batched_obs(batched_obs, unflatten_context) -> dict:
+    """pufferlib.emulation.unpack_batched_obs with the reference's call signature
+    (baseline_policy.py:7,41: `unpack_batched_obs(flat_observations, self.unflatten_context)`),
+    for the context GpuVecEnv's driver_env hands the policy (`flat_layout`, an OrderedDict of
+    Segments): the nested dict of views the policy indexes -- Tile, Entity, AgentId, Inventory,
+    Market, Task and ActionTargets[head][arg] (baseline_policy.py:42-76, 230-262). With pufferlib
+    absent the policy's one change is importing this name from here. (pufferlib 0.7.3's own
+    decoder is not importable in this image: that it accepts this context is unpinned.)"""
+    total = unflatten_context["__total__"].offset
+    if batched_obs.shape[-1] != total:
+        raise ValueError(f"flat obs have {batched_obs.shape[-1]} elements, the context {total}")
+    task = unflatten_context["Task"].shape[0]
+    return unflatten(batched_obs, task)
+
+
 # ---------------------------------------------------------------- native layout (SPEC.md §8b)
 NATIVE_I16_FIELDS = [("AgentId", (1,)), ("CurrentTick", (1,)), ("Entity", (PLAYER_N_OBS, ENTITY_COLS)),
                      ("Inventory", (INVENTORY_N_OBS, ITEM_COLS)), ("Tile", (TILE_ROWS, TILE_COLS)),

@@ -187,3 +187,25 @@ def test_ids_and_materials(rollout):
     bank = o.map_bank()
     assert bank.shape == (4, 160, 160) and bank.max() <= 15  # MAP_CENTER 128 + border
     assert np.all(bank[:, :16, :] == 0) and np.all(bank[:, 144:, :] == 0)
+
+
+def test_unpack_batched_obs_serves_the_reference_policy_reads():
+    """layout.unpack_batched_obs(flat, driver_env.unflatten_context) -- the reference's call at
+    baseline_policy.py:41 -- yields what encode_observations / ActionDecoder index (:42-76,
+    :230-262), as views of the flat batch (the start-kit's in-place Tile edit lands in it)."""
+    import torch
+
+    from nmmo_amd.layout import ACTION_HEADS, flat_layout, unpack_batched_obs
+
+    ctx = flat_layout(2048)
+    flat = torch.arange(3 * 23987, dtype=torch.float32).reshape(3, 23987)
+    d = unpack_batched_obs(flat, ctx)
+    assert d["Tile"].shape == (3, 225, 3) and d["Entity"].shape == (3, 100, 31)
+    assert d["AgentId"][:, 0].shape == (3,) and d["Inventory"].shape == (3, 12, 16)
+    assert d["Market"].shape == (3, 1024, 16) and d["Task"].shape == (3, 2048)
+    for (a, b), n in ACTION_HEADS:
+        assert d["ActionTargets"][a][b].shape == (3, n)
+    d["Tile"][:, :, :2] += 7  # baseline_policy.py:97, on the views
+    assert float(flat[0, ctx["Tile"].offset]) == ctx["Tile"].offset + 7
+    with pytest.raises(ValueError):
+        unpack_batched_obs(flat[:, :-1], ctx)

@@ -20,7 +20,7 @@ bench)  # the default bench line (N = 1)
   ;;
 flat)  # the flat-obs parity tests, then the C4 A/B (this tree vs the round-4 flat kernel)
   timeout -k 10 600 $PYT tests/test_gpu_parity.py tests/test_gpu_zero_rows.py tests/test_gpu_obs_contract.py \
-    tests/test_gpu_wrapper.py tests/test_gpu_fullsize.py > gpurun_out/gpu_flat.log 2>&1 && \
+    tests/test_gpu_wrapper.py tests/test_gpu_fullsize.py tests/test_gpu_native_obs.py tests/test_gpu_wire.py > gpurun_out/gpu_flat.log 2>&1 && \
   timeout -k 10 600 bash tools/ab_obs.sh C4 $L/libnmmo_hip.so,$L/libnmmo_hip_flatv1.so > gpurun_out/ab_flat.txt 2>&1 && \
   timeout -k 10 900 bash tools/ab_obs.sh C4 $L/libnmmo_hip.so,$L/libnmmo_hip_fa1.so,$L/libnmmo_hip_fa2.so,$L/libnmmo_hip_fa4.so,$L/libnmmo_hip_fa16.so,$L/libnmmo_hip_fa32.so > gpurun_out/abl_flat.txt 2>&1
   ;;
