@@ -354,7 +354,13 @@ __device__ __forceinline__ AoSections ao_sections(const ObsParams& p, const int1
     x.s10[1] = low_bits(kSecN[10] - 64);
     if constexpr (kWrap) {
       const int pp = g.prev_price;
-      if ((p.wflags & kWrapObsPrice) && pp >= 0 && pp < kSecN[10]) x.s10[pp >> 6] &= ~(1ull << (pp & 63));
+      if ((p.wflags & kWrapObsPrice) && pp >= 0 && pp < kSecN[10]) {
+        // (no runtime index into x: one put the whole struct in scratch, whose loads then waited
+        // for every store the kernel had issued)
+        const uint64_t clr = ~(1ull << (pp & 63));
+        if (pp < 64) x.s10[0] &= clr;
+        else x.s10[1] &= clr;
+      }
     }
   }
   x.s8 = g.mv;

@@ -344,13 +344,18 @@ __global__ void __launch_bounds__(64 * kAoWaves) flat_obs_kernel(ObsParams p) {
       row[kFoInv + 64 * h + lane] = v;
     }
     // Market (the env's listings, ascending row; owner = lister) and its zero run down to hm
-    for (int k = lane; k < ((NMMO_FO_ABL & 8) ? 0 : nm * 16); k += 64) {
-      const int q = k >> 4;
-      const uint2 wd = q < kFoStagedListings ? mitem[q] : [&]() {
+    // (the listings past the staged ones in a loop of their own: a global load in the common loop
+    // made every iteration wait for all of the row's stores -- vmcnt counts stores and retires in
+    // order -- whether or not it took the load)
+    const int nms = (NMMO_FO_ABL & 8) ? 0 : min(nm, kFoStagedListings);
+    for (int k = lane; k < nms * 16; k += 64) row[kFoMarket + k] = ic_value(mitem[k >> 4], (mpo[k >> 4] >> 8) + 1, icd);
+    if (nm > nms && !(NMMO_FO_ABL & 8)) {
+      for (int k = nms * 16 + lane; k < nm * 16; k += 64) {
+        const int q = k >> 4;
         const int v = p.mlist[(size_t)e * NMMO_MARKET_ROWS + q];
-        return p.items[((size_t)e * P + ((v >> 16) & 255)) * kInv + ((v >> 24) & 15)];
-      }();
-      row[kFoMarket + k] = ic_value(wd, (mpo[q] >> 8) + 1, icd);
+        const uint2 wd = p.items[((size_t)e * P + ((v >> 16) & 255)) * kInv + ((v >> 24) & 15)];
+        row[kFoMarket + k] = ic_value(wd, (mpo[q] >> 8) + 1, icd);
+      }
     }
     wave_zero(row, kFoMarket + nm * 16, kFoMarket + max(nm, hm) * 16);
     // Task: only when the row does not hold this task's embedding yet (read in place)
