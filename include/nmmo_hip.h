@@ -429,6 +429,14 @@ NMMO_API int nmmo_wire_pack(NmmoHandle* h, const void* native, void* wire, void*
  * 8 record heads, 16 entity-table indices; 0 = valid). Enqueued; needs no handle. */
 NMMO_API int nmmo_wire_check(const void* wire, int32_t n_envs, int32_t player_n, const int64_t* dev_expect_total,
                              int32_t* dev_status, void* stream);
+/* nmmo_wire_check over n_bufs (1..16) buffers in one launch (the learner root validating every
+ * buffer a step received): wires / n_envs / dev_expect_totals are host arrays of n_bufs entries
+ * (device buffers, their env counts, device int64 announced totals; dev_expect_totals NULL or an
+ * entry NULL skips that comparison); the bits of all of them are OR-ed into *dev_status.
+ * Enqueued; needs no handle. */
+NMMO_API int nmmo_wire_check_many(const void* const* wires, const int32_t* n_envs,
+                                  const int64_t* const* dev_expect_totals, int32_t n_bufs,
+                                  int32_t player_n, int32_t* dev_status, void* stream);
 /* Decodes a wire buffer of n_envs x player_n agents into the native layout (every byte of the
  * n_envs x (player_n x NMMO_NATIVE_ROW_BYTES + NMMO_NATIVE_MARKET_BYTES) buffer is written;
  * bit-identical to what the sender's nmmo_step wrote). Enqueued; needs no handle. */

@@ -551,15 +551,17 @@ int nmmo_dev_free(void* ptr) {
     g_vmm.erase(it);
   }
   HIP_TRY(hipDeviceSynchronize());  // no kernel may still use the range
-  // Unmapped chunk by chunk as it was mapped, and the physical chunks released; the virtual range
-  // itself stays reserved for the life of the process. Measured on MI355X: a range freed with
-  // hipMemAddressFree came back from the next hipMemAddressReserve of the same size, mapped to new
-  // chunks, and a buffer filled there read back other contents in 4 of 48 alloc / fill / check /
-  // free cycles (tools/debug/dbg_zero_rows.py) -- stale translations of the reused addresses. A
-  // range that is never reused cannot have them; the address space is 128 TB.
+  // Unmapped chunk by chunk as it was mapped, the physical chunks released, the virtual range
+  // freed. (Round 4 kept freed ranges reserved after a reused range read back other contents in
+  // 4 of 48 cycles of tools/debug/dbg_vmm.py, under the old single hipMemUnmap over the whole
+  // multi-chunk range; the standalone reproducer tools/vmm_repro.hip -- this exact call sequence,
+  // no build code -- found no wrong word in 4 x 192 allocations with 187 of 192 ranges reused, either
+  // unmap form, profiles/r05/vmm_repro.txt. NMMO_DEVMEM_KEEP_VA=1 keeps ranges reserved, for A/B.)
   const size_t chunk = a.chunks.empty() ? a.bytes : a.bytes / a.chunks.size();
   for (size_t i = 0; i < a.chunks.size(); i++) HIP_TRY(hipMemUnmap((char*)ptr + i * chunk, chunk));
   for (auto c : a.chunks) HIP_TRY(hipMemRelease(c));
+  const char* keep = getenv("NMMO_DEVMEM_KEEP_VA");
+  if (!(keep && keep[0] == '1')) HIP_TRY(hipMemAddressFree(ptr, a.bytes));
   return NMMO_OK;
 }
 
@@ -650,6 +652,24 @@ int nmmo_wire_check(const void* wire, int32_t n_envs, int32_t player_n, const in
   if (!wire || !dev_status) return fail(NMMO_E_INVALID, "null argument");
   if (n_envs <= 0 || player_n <= 0 || player_n > 128) return fail(NMMO_E_INVALID, "n_envs > 0, player_n in 1..128");
   HIP_TRY(launch_wire_check((const uint8_t*)wire, n_envs, player_n, dev_expect_total, dev_status, (hipStream_t)stream));
+  return NMMO_OK;
+}
+
+int nmmo_wire_check_many(const void* const* wires, const int32_t* n_envs, const int64_t* const* dev_expect_totals,
+                         int32_t n_bufs, int32_t player_n, int32_t* dev_status, void* stream) {
+  if (!wires || !n_envs || !dev_status) return fail(NMMO_E_INVALID, "null argument");
+  if (n_bufs < 1 || n_bufs > kMaxCheckBufs) return fail(NMMO_E_INVALID, "n_bufs %d not in 1..%d", n_bufs, kMaxCheckBufs);
+  if (player_n <= 0 || player_n > 128) return fail(NMMO_E_INVALID, "player_n in 1..128");
+  WireCheckBatch b;
+  memset(&b, 0, sizeof(b));
+  b.count = n_bufs;
+  for (int i = 0; i < n_bufs; i++) {
+    if (!wires[i] || n_envs[i] <= 0) return fail(NMMO_E_INVALID, "buffer %d: null wire / n_envs <= 0", i);
+    b.wire[i] = (const uint8_t*)wires[i];
+    b.n[i] = n_envs[i];
+    b.expect[i] = dev_expect_totals ? dev_expect_totals[i] : nullptr;
+  }
+  HIP_TRY(launch_wire_check_many(b, player_n, dev_status, (hipStream_t)stream));
   return NMMO_OK;
 }
 

@@ -177,6 +177,15 @@ hipError_t launch_native_obs(const ObsParams& p, hipStream_t s);
 // header + record-head consistency of a wire buffer; bits into *status (0 = valid)
 hipError_t launch_wire_check(const uint8_t* wire, int n, int P, const int64_t* expect_total, int* status,
                              hipStream_t s);
+// several buffers' checks as one launch (nmmo_wire_check_many)
+constexpr int kMaxCheckBufs = 16;
+struct WireCheckBatch {
+  const uint8_t* wire[kMaxCheckBufs];
+  const int64_t* expect[kMaxCheckBufs];
+  int n[kMaxCheckBufs];
+  int count;
+};
+hipError_t launch_wire_check_many(const WireCheckBatch& b, int P, int* status, hipStream_t s);
 // wire records -> flat float32 rows (p.wire, p.obs, p.row_map as in launch_expand)
 hipError_t launch_wire_expand(const ObsParams& p, hipStream_t s);
 hipError_t launch_store(const NmmoExperience& x, const NmmoStoreInput& in, const ObsParams* native,

@@ -414,11 +414,11 @@ __global__ void __launch_bounds__(256) wire_unpack_kernel(const uint8_t* wire, u
 // listings, the counts' ranges, every record head's AgentId / nv / ninv against its count word
 // and its entity-table indices against the table. status bits: 1 total, 2 env offsets, 4 count
 // ranges, 8 record heads, 16 entity-table indices.
-__global__ void __launch_bounds__(128) wire_check_kernel(const uint8_t* wire, int n, int P,
-                                                         const int64_t* expect_total, int* status) {
+__device__ __forceinline__ void wire_check_env(const uint8_t* wire, int n, int P, const int64_t* expect_total,
+                                               int* status, int e) {
   WireView v = wire_view(const_cast<uint8_t*>(wire), n, P);
   __shared__ int off[129];
-  const int e = blockIdx.x, a = threadIdx.x;
+  const int a = threadIdx.x;
   const uint16_t* cnt = v.cnt + (size_t)e * P;
   const int ne = v.ecount[e];
   record_offsets_wave0(cnt, P, off, wire_table_bytes(ne));
@@ -464,6 +464,16 @@ __global__ void __launch_bounds__(128) wire_check_kernel(const uint8_t* wire, in
     }
   }
   if (bad) atomicOr(status, bad);
+}
+__global__ void __launch_bounds__(128) wire_check_kernel(const uint8_t* wire, int n, int P,
+                                                         const int64_t* expect_total, int* status) {
+  wire_check_env(wire, n, P, expect_total, status, blockIdx.x);
+}
+// Every received buffer of a step in one launch: grid (max envs, buffers)
+__global__ void __launch_bounds__(128) wire_check_many_kernel(WireCheckBatch b, int P, int* status) {
+  const int i = blockIdx.y;
+  if ((int)blockIdx.x >= b.n[i]) return;
+  wire_check_env(b.wire[i], b.n[i], P, b.expect[i], status, blockIdx.x);
 }
 
 // Wire records -> flat float32 rows (the pufferlib row of SPEC §8; bit-identical to
@@ -652,6 +662,14 @@ hipError_t launch_wire_unpack(const uint8_t* wire, uint8_t* native, int n, int P
   if (P > 128 || n <= 0) return hipErrorInvalidValue;
   hipLaunchKernelGGL(wire_unpack_kernel, dim3(n, (P + kWireAgentsPerBlock - 1) / kWireAgentsPerBlock), dim3(256), 0,
                      s, wire, native, n, P);
+  return hipGetLastError();
+}
+
+hipError_t launch_wire_check_many(const WireCheckBatch& b, int P, int* status, hipStream_t s) {
+  int mx = 0;
+  for (int i = 0; i < b.count; i++) mx = max(mx, b.n[i]);
+  if (b.count <= 0 || mx <= 0) return hipSuccess;
+  hipLaunchKernelGGL(wire_check_many_kernel, dim3(mx, b.count), dim3(128), 0, s, b, P, status);
   return hipGetLastError();
 }
 

@@ -370,11 +370,13 @@ class WireGather:
                     w.copy_(w0)
                     sm.copy_(sm0)
                     items.append(((self.world - 1 + q, j), (w, sm)))
+            # every received buffer against the size its sender announced, up to 16 per launch
+            recv = [(w, self.engines[j].n_envs, self.x.sizes[s % self.ring, r if r < self.world else 0, j:j + 1])
+                    for (r, j), (w, sm) in items if r != 0]
+            for k in range(0, len(recv), 16):
+                nw.check_buffers(recv[k:k + 16], self.P, self.status)
             for (r, j), (w, sm) in items:
                 n = self.engines[j].n_envs
-                if r != 0:  # a received buffer against the size its sender announced
-                    nw.check_buffer(w, n, self.P, self.status,
-                                    self.x.sizes[s % self.ring, r if r < self.world else 0, j:j + 1])
                 if self.native is not None:
                     nw.unpack(w, n, self.P, out=self.native[r, j] if r < self.world else
                               self._rh_native[r - self.world, j])

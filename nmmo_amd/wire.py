@@ -65,6 +65,26 @@ def unpack(wire: torch.Tensor, n_envs: int, players: int, out: torch.Tensor | No
     return out
 
 
+def check_buffers(bufs, players: int, status: torch.Tensor) -> torch.Tensor:
+    """check_buffer over up to 16 buffers in one launch (nmmo_wire_check_many): bufs = [(wire,
+    n_envs, expect_total or None)], all on status's device."""
+    n = len(bufs)
+    if not 1 <= n <= 16:
+        raise ValueError("check_buffers takes 1..16 buffers")
+    if status.dtype != torch.int32:
+        raise ValueError("status must be an int32 tensor")
+    for w, _, x in bufs:
+        if w.device != status.device or (x is not None and (x.dtype != torch.int64 or x.device != status.device)):
+            raise ValueError("wire buffers / expect_totals must be on status's device (expect_total int64)")
+    wires = (ctypes.c_void_p * n)(*[w.data_ptr() for w, _, _ in bufs])
+    envs = (ctypes.c_int32 * n)(*[int(ne) for _, ne, _ in bufs])
+    exp = (ctypes.c_void_p * n)(*[None if x is None else x.data_ptr() for _, _, x in bufs])
+    with torch.cuda.device(status.device):
+        check(lib().nmmo_wire_check_many(wires, envs, exp, n, players, ctypes.c_void_p(status.data_ptr()),
+                                         _stream(status.device)), "nmmo_wire_check_many")
+    return status
+
+
 def check_buffer(wire: torch.Tensor, n_envs: int, players: int, status: torch.Tensor,
                  expect_total: torch.Tensor | None = None) -> torch.Tensor:
     """Enqueue the consistency check of a (received) wire buffer (nmmo_wire_check): error bits

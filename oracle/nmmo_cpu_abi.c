@@ -287,6 +287,11 @@ NMMO_API int nmmo_wire_check(const void* wire, int32_t n, int32_t p, const int64
   (void)wire; (void)n; (void)p; (void)e; (void)s; (void)stream;
   UNSUPPORTED("nmmo_wire_check");
 }
+NMMO_API int nmmo_wire_check_many(const void* const* w, const int32_t* n, const int64_t* const* e, int32_t nb,
+                                  int32_t p, int32_t* s, void* stream) {
+  (void)w; (void)n; (void)e; (void)nb; (void)p; (void)s; (void)stream;
+  UNSUPPORTED("nmmo_wire_check_many");
+}
 NMMO_API int nmmo_set_timing(NmmoHandle* h, int32_t enable) {
   (void)h; (void)enable;
   UNSUPPORTED("nmmo_set_timing");

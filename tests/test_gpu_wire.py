@@ -147,6 +147,17 @@ def test_wire_layout_fullsize_roundtrip_and_check():
     wire.check_buffer(bad, n, wir.P, st)
     assert int(st.item()) & (2 | 8), int(st.item())
     assert hb < total
+    # the batched form (nmmo_wire_check_many, one launch): clean buffers stay clean, and a bad one
+    # among good ones sets the same bits
+    good = wir.obs[:total]
+    st.zero_()
+    wire.check_buffers([(good, n, want), (good, n, None), (good, n, want)], wir.P, st)
+    assert int(st.item()) == 0
+    wire.check_buffers([(good, n, want), (bad, n, None)], wir.P, st)
+    assert int(st.item()) & (2 | 8), int(st.item())
+    st.zero_()
+    wire.check_buffers([(good, n, want + 16)], wir.P, st)
+    assert int(st.item()) & 1
     for e in (nat, wir):
         e.close()
 

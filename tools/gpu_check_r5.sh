@@ -47,6 +47,11 @@ fix1)  # flat obs fixes (Market loop vmcnt, wrapper scratch) vs HEAD, parity fir
   timeout -k 10 600 bash tools/ab_obs.sh C4 $L/libnmmo_hip.so,$L/libnmmo_hip_head.so --wrapper neurips23_start_kit > gpurun_out/ab_fix1_wrap.txt 2>&1 && \
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c5 -o run -- python3 bench.py --config C5 --steps 60 --warmup 10 --no-cpu-baseline > gpurun_out/prof_c5.json 2> gpurun_out/prof_c5.err
   ;;
+c5)  # devmem with freed ranges, wire + multirank tests (batched check), then C5 at N = 1 (root_loaded pass)
+  timeout -k 10 600 $PYT tests/test_gpu_devmem.py tests/test_gpu_wire.py tests/test_gpu_multirank.py tests/test_gpu_storage.py > gpurun_out/gpu_c5.log 2>&1 && \
+  timeout -k 10 200 python tools/debug/dbg_vmm.py > gpurun_out/dbg_vmm.txt 2>&1 && \
+  timeout -k 10 300 python bench.py --config C5 --no-cpu-baseline > gpurun_out/bench_c5.json 2> gpurun_out/bench_c5.err
+  ;;
 ab)  # same-box A/B of variant libraries: ab <config> <lib,lib,...> [bench args]
   CFG=$2; LIBS=$3; shift 3
   timeout -k 10 900 bash tools/ab_obs.sh $CFG $LIBS "$@" > gpurun_out/ab_$CFG.txt 2>&1
