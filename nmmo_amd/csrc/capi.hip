@@ -551,17 +551,18 @@ int nmmo_dev_free(void* ptr) {
     g_vmm.erase(it);
   }
   HIP_TRY(hipDeviceSynchronize());  // no kernel may still use the range
-  // Unmapped chunk by chunk as it was mapped, the physical chunks released, the virtual range
-  // freed. (Round 4 kept freed ranges reserved after a reused range read back other contents in
-  // 4 of 48 cycles of tools/debug/dbg_vmm.py, under the old single hipMemUnmap over the whole
-  // multi-chunk range; the standalone reproducer tools/vmm_repro.hip -- this exact call sequence,
-  // no build code -- found no wrong word in 4 x 192 allocations with 187 of 192 ranges reused, either
-  // unmap form, profiles/r05/vmm_repro.txt. NMMO_DEVMEM_KEEP_VA=1 keeps ranges reserved, for A/B.)
+  // Unmapped chunk by chunk as it was mapped and the physical chunks released; the virtual range
+  // stays reserved for the life of the process (NMMO_DEVMEM_FREE_VA=1 frees it, for A/B). A
+  // freed range handed out again by hipMemAddressReserve read back other contents through torch
+  // (tests/test_gpu_devmem.py with free: cycle 1, one-chunk buffers, so not the unmap form), while
+  // the same HIP call sequence alone (tools/vmm_repro.hip) found no wrong word with 187 of 192
+  // ranges reused: profiles/r05/vmm_repro.txt. A range never reused cannot hit it; the address
+  // space is 128 TB.
   const size_t chunk = a.chunks.empty() ? a.bytes : a.bytes / a.chunks.size();
   for (size_t i = 0; i < a.chunks.size(); i++) HIP_TRY(hipMemUnmap((char*)ptr + i * chunk, chunk));
   for (auto c : a.chunks) HIP_TRY(hipMemRelease(c));
-  const char* keep = getenv("NMMO_DEVMEM_KEEP_VA");
-  if (!(keep && keep[0] == '1')) HIP_TRY(hipMemAddressFree(ptr, a.bytes));
+  const char* fr = getenv("NMMO_DEVMEM_FREE_VA");
+  if (fr && fr[0] == '1') HIP_TRY(hipMemAddressFree(ptr, a.bytes));
   return NMMO_OK;
 }
 

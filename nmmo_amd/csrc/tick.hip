@@ -180,8 +180,7 @@ __host__ __device__ inline size_t union_lds_bytes(int S, bool grid) {
 __host__ __device__ inline size_t tick_lds_bytes(int S, int P, bool items, bool tev, bool grid, bool slim) {
   auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
   // task state is staged in LDS only when events feed its accumulators (else read in place)
-  size_t b = (items ? item_lds_bytes(P) : 0) + kPlayerArrBytes +
-             (tev ? 128 * 2 * 16 + al((size_t)P * sizeof(NmmoTaskState)) : 0);
+  size_t b = (items ? item_lds_bytes(P) : 0) + kPlayerArrBytes;
   b += al((size_t)(slim ? kSlimNF : kNFLive) * S * 2);  // T
   b += union_lds_bytes(S, grid);     // vism + grid | hkey,hmin | ft,clist
   b += al((size_t)(S + 1) * 2);      // rslot
@@ -190,13 +189,17 @@ __host__ __device__ inline size_t tick_lds_bytes(int S, int P, bool items, bool 
   b += al((size_t)S * 2);            // ring
   b += (size_t)kBitmapWords * 4;     // dep
   b += NMMO_NE * 4 + 32 * 4 + 16 * 4 + 128 + 128;
+  // task state staging last (make_ctx): 16-B aligned
+  if (tev) b = al(b) + al((size_t)P * sizeof(NmmoTaskState)) + 128 * 2 * 16;
   return b;
 }
 
+// kS / kP: the slot / player counts when known at compile time (0 = st's)
+template <int kS = 0, int kP = 0>
 __device__ __forceinline__ Ctx make_ctx(unsigned char* smem, const DevState& st, int e, uint32_t sy) {
   auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
   Ctx c;
-  const int S = st.S;
+  const int S = kS ? kS : st.S, P = kP ? kP : st.P;
   size_t o = 0;
   c.sysm = sy;
   c.items = (sy & NMMO_SYS_ITEM) != 0;
@@ -205,9 +208,9 @@ __device__ __forceinline__ Ctx make_ctx(unsigned char* smem, const DevState& st,
   c.equip = c.items && (sy & NMMO_SYS_EQUIPMENT) != 0;
   c.foreign_any = *st.foreign != 0;  // uniform, read before any store (a scalar load)
   c.foreign = !c.prof && c.foreign_any;
-  c.IC = kInv * st.P;
+  c.IC = kInv * P;
   if (c.items) {  // 16-B aligned block first (inventories are copied with 16-B accesses)
-    c.inv = reinterpret_cast<uint2*>(smem + o); o += (size_t)st.P * kInv * 8;
+    c.inv = reinterpret_cast<uint2*>(smem + o); o += (size_t)P * kInv * 8;
     c.iring = reinterpret_cast<int16_t*>(smem + o); o += al((size_t)c.IC * 2);
     c.rmap = reinterpret_cast<int16_t*>(smem + o); o += al((size_t)(c.IC + 1) * 2);
     c.lbits = reinterpret_cast<uint64_t*>(smem + o); o += kLWords * 8;
@@ -228,19 +231,10 @@ __device__ __forceinline__ Ctx make_ctx(unsigned char* smem, const DevState& st,
   c.tev = st.tev != 0;
   c.tmap = st.tmap != 0;
   c.tasks = st.tasks;
-  c.assign = st.assign + (size_t)e * st.P;
+  c.assign = st.assign + (size_t)e * P;
   c.task_cum = st.task_cum;
   c.n_tasks = st.n_tasks;
-  c.tsl = reinterpret_cast<NmmoTaskState*>(smem + o);  // an LDS address either way (copy_segs)
-  c.tsg = st.tstate + (size_t)e * st.P;
-  if (c.tev) {
-    c.ts = c.tsl;
-    o += al((size_t)st.P * sizeof(NmmoTaskState));
-    c.tdesc = reinterpret_cast<int4*>(smem + o); o += 128 * 2 * 16;
-  } else {
-    c.ts = st.tstate + (size_t)e * st.P;  // HBM, touched once per player at the rewards
-    c.tdesc = nullptr;
-  }
+  c.tsg = st.tstate + (size_t)e * P;
   c.kill = reinterpret_cast<int16_t*>(smem + o); o += 256;
   c.order = reinterpret_cast<int16_t*>(smem + o); o += 256;
   c.ev_dmg = reinterpret_cast<int16_t*>(smem + o); o += 256;
@@ -277,13 +271,25 @@ __device__ __forceinline__ Ctx make_ctx(unsigned char* smem, const DevState& st,
   c.misc = reinterpret_cast<int*>(smem + o); o += 16 * 4;
   c.pres = smem + o; o += 128;
   c.died = smem + o; o += 128;
+  // task state last: its LDS staging exists only with task events (a run-time flag), so every
+  // offset above is a compile-time constant in the specialised kernels
+  o = al(o);  // (16-B words: copy_segs)
+  c.tsl = reinterpret_cast<NmmoTaskState*>(smem + o);  // an LDS address either way
+  if (c.tev) {
+    c.ts = c.tsl;
+    o += al((size_t)P * sizeof(NmmoTaskState));
+    c.tdesc = reinterpret_cast<int4*>(smem + o); o += 128 * 2 * 16;
+  } else {
+    c.ts = c.tsg;  // HBM, touched once per player at the rewards
+    c.tdesc = nullptr;
+  }
   c.mat = st.mat + (size_t)e * kTiles;
   c.bank = st.bank;
   c.evcap = st.cfg.event_cap > 0 ? st.cfg.event_cap : 0;
   c.evg = c.evcap ? st.events + (size_t)e * c.evcap * NMMO_EVENT_COLS : nullptr;
   c.tick1 = 0;
   c.S = S;
-  c.P = st.P;
+  c.P = P;
   c.N = st.N;
   c.cfg = &st.cfg;
   c.fault = st.fault;
@@ -2317,7 +2323,7 @@ __device__ __forceinline__ void store_market(Ctx& c, const DevState& st, int e) 
 // mode 0: step (auto-reset envs that are done); mode 1: reset every env.
 // kSys != 0: specialised for exactly that system set (launch_tick dispatches on
 // cfg.systems), so disabled systems compile out; kSys == 0 reads the set at run time.
-template <uint32_t kSys>
+template <uint32_t kSys, int kS, int kP>
 __device__ __forceinline__ void tick_body(const DevState& st, const int32_t* __restrict__ actions,
                                           const uint64_t* __restrict__ env_seeds, float* rew, uint8_t* term,
                                           uint8_t* trunc, uint8_t* mask, int mode) {
@@ -2329,13 +2335,13 @@ __device__ __forceinline__ void tick_body(const DevState& st, const int32_t* __r
   }
   NMMO_STAMP_CLEAR();
   NMMO_STAMP(0);
-  Ctx c = make_ctx(smem, st, e, kSys ? kSys : st.cfg.systems);
+  Ctx c = make_ctx<kS, kP>(smem, st, e, kSys ? kSys : st.cfg.systems);
   // a step's action heads of this thread's player (a valid row for every thread; Move /
   // AttackStyle / AttackTarget, and the item heads with the Item system), loaded ahead of the
   // state so their latency hides under its load
   Heads hd = {};
   if (mode == 0) {
-    const int32_t* a = actions + ((size_t)e * st.P + min((int)threadIdx.x, st.P - 1)) * kHeads;
+    const int32_t* a = actions + ((size_t)e * c.P + min((int)threadIdx.x, c.P - 1)) * kHeads;
 #pragma unroll
     for (int k = 0; k < kHeads; k++)
       if (k == 0 || k == 1 || k == 8 || c.items) hd.v[k] = a[k];
@@ -2398,19 +2404,22 @@ __device__ __forceinline__ void tick_body(const DevState& st, const int32_t* __r
   NMMO_STAMP(11);
 }
 
-template <uint32_t kSys>
+// kS / kP != 0: specialised for that slot / player count too (the bench configs: C2 128 / 128,
+// C3 and C4 384 / 128), so the staged arrays' LDS offsets are immediates rather than uniform values
+// held across the whole tick (the generic C4 kernel spilled 960 SGPRs to VGPR lanes)
+template <uint32_t kSys, int kS = 0, int kP = 0>
 __global__ void tick_kernel(DevState st, const int32_t* __restrict__ actions,
                             const uint64_t* __restrict__ env_seeds, float* rew, uint8_t* term,
                             uint8_t* trunc, uint8_t* mask, int mode) {
-  tick_body<kSys>(st, actions, env_seeds, rew, term, trunc, mask, mode);
+  tick_body<kSys, kS, kP>(st, actions, env_seeds, rew, term, trunc, mask, mode);
 }
 // The C3 specialisation at <= 64 VGPRs: a 6-wave workgroup puts 2 waves on two SIMDs, so 4
 // workgroups per CU (the 1,024 envs of C3 in one round on 256 CUs) need 8 wave slots there.
-template <uint32_t kSys>
+template <uint32_t kSys, int kS = 0, int kP = 0>
 __global__ void __attribute__((amdgpu_waves_per_eu(8, 8)))
 tick_kernel_w8(DevState st, const int32_t* __restrict__ actions, const uint64_t* __restrict__ env_seeds,
                float* rew, uint8_t* term, uint8_t* trunc, uint8_t* mask, int mode) {
-  tick_body<kSys>(st, actions, env_seeds, rew, term, trunc, mask, mode);
+  tick_body<kSys, kS, kP>(st, actions, env_seeds, rew, term, trunc, mask, mode);
 }
 
 
@@ -2422,10 +2431,11 @@ hipError_t launch_tick(const DevState& st, const int32_t* actions, const uint64_
   const size_t lds = tick_lds_bytes(st.S, st.P, (st.cfg.systems & NMMO_SYS_ITEM) != 0, st.tev != 0,
                                     uses_grid(st.cfg.systems), slim_systems(st.cfg.systems));
   void (*k)(DevState, const int32_t*, const uint64_t*, float*, uint8_t*, uint8_t*, uint8_t*, int);
+  const bool s128 = st.S == 128 && st.P == 128, s384 = st.S == 384 && st.P == 128;
   switch (st.cfg.systems) {
-    case kSysC2: k = tick_kernel<kSysC2>; break;
-    case kSysC3: k = tick_kernel_w8<kSysC3>; break;
-    case NMMO_SYS_ALL: k = tick_kernel<NMMO_SYS_ALL>; break;
+    case kSysC2: k = s128 ? tick_kernel<kSysC2, 128, 128> : tick_kernel<kSysC2>; break;
+    case kSysC3: k = s384 ? tick_kernel_w8<kSysC3, 384, 128> : tick_kernel_w8<kSysC3>; break;
+    case NMMO_SYS_ALL: k = s384 ? tick_kernel<NMMO_SYS_ALL, 384, 128> : tick_kernel<NMMO_SYS_ALL>; break;
     default: k = tick_kernel<0>; break;
   }
   const int grid = list_grid(st.env_list, st.n_list, st.n_envs);
@@ -2437,10 +2447,13 @@ hipError_t launch_tick(const DevState& st, const int32_t* actions, const uint64_
 
 hipError_t init_kernels() {
   // dynamic LDS may use what the kernel's static LDS leaves of 160 KB
-  const void* ks[4] = {reinterpret_cast<const void*>(tick_kernel<kSysC2>),
+  const void* ks[7] = {reinterpret_cast<const void*>(tick_kernel<kSysC2>),
                        reinterpret_cast<const void*>(tick_kernel_w8<kSysC3>),
                        reinterpret_cast<const void*>(tick_kernel<NMMO_SYS_ALL>),
-                       reinterpret_cast<const void*>(tick_kernel<0>)};
+                       reinterpret_cast<const void*>(tick_kernel<0>),
+                       reinterpret_cast<const void*>(tick_kernel<kSysC2, 128, 128>),
+                       reinterpret_cast<const void*>(tick_kernel_w8<kSysC3, 384, 128>),
+                       reinterpret_cast<const void*>(tick_kernel<NMMO_SYS_ALL, 384, 128>)};
   for (const void* k : ks) {
     hipFuncAttributes fa;
     hipError_t err = hipFuncGetAttributes(&fa, k);

@@ -25,7 +25,7 @@ flat)  # the flat-obs parity tests, then the C4 A/B (this tree vs the round-4 fl
   timeout -k 10 900 bash tools/ab_obs.sh C4 $L/libnmmo_hip.so,$L/libnmmo_hip_fa1.so,$L/libnmmo_hip_fa2.so,$L/libnmmo_hip_fa4.so,$L/libnmmo_hip_fa16.so,$L/libnmmo_hip_fa32.so > gpurun_out/abl_flat.txt 2>&1
   ;;
 vmm)  # the standalone VMM reproducer (tools/vmm_repro.hip), four variants; rc 1 = wrong contents seen
-  for v in "unmap=whole free=1" "unmap=chunk free=1" "unmap=chunk sync=1 free=1" "unmap=chunk free=0"; do
+  for v in "unmap=whole free=1 tmp=1" "unmap=chunk free=1 attrs=1 tmp=1" "unmap=chunk free=0 attrs=1 tmp=1"; do
     timeout -k 10 120 tools/vmm_repro $v cycles=48 >> gpurun_out/vmm_repro.txt 2>&1; rc=$?
     [ $rc -le 1 ] || { echo "vmm_repro $v: rc $rc" >> gpurun_out/vmm_repro.txt; exit $rc; }
   done
@@ -47,10 +47,16 @@ fix1)  # flat obs fixes (Market loop vmcnt, wrapper scratch) vs HEAD, parity fir
   timeout -k 10 600 bash tools/ab_obs.sh C4 $L/libnmmo_hip.so,$L/libnmmo_hip_head.so --wrapper neurips23_start_kit > gpurun_out/ab_fix1_wrap.txt 2>&1 && \
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c5 -o run -- python3 bench.py --config C5 --steps 60 --warmup 10 --no-cpu-baseline > gpurun_out/prof_c5.json 2> gpurun_out/prof_c5.err
   ;;
-c5)  # devmem with freed ranges, wire + multirank tests (batched check), then C5 at N = 1 (root_loaded pass)
+c5)  # devmem (kept ranges), wire + multirank tests (batched check), then C5 at N = 1 (root_loaded pass)
   timeout -k 10 600 $PYT tests/test_gpu_devmem.py tests/test_gpu_wire.py tests/test_gpu_multirank.py tests/test_gpu_storage.py > gpurun_out/gpu_c5.log 2>&1 && \
-  timeout -k 10 200 python tools/debug/dbg_vmm.py > gpurun_out/dbg_vmm.txt 2>&1 && \
+  NMMO_DEVMEM_FREE_VA=1 timeout -k 10 200 python tools/debug/dbg_vmm.py > gpurun_out/dbg_vmm.txt 2>&1 && \
   timeout -k 10 300 python bench.py --config C5 --no-cpu-baseline > gpurun_out/bench_c5.json 2> gpurun_out/bench_c5.err
+  ;;
+tick1)  # tick parity with compile-time S/P, then same-box C2 / C3 / C4 against HEAD's library
+  timeout -k 10 600 $PYT tests/test_gpu_parity.py tests/test_gpu_fullsize.py > gpurun_out/gpu_tick1.log 2>&1 && \
+  timeout -k 10 300 bash tools/ab_obs.sh C2 $L/libnmmo_hip.so,$L/libnmmo_hip_head.so > gpurun_out/ab_tick_c2.txt 2>&1 && \
+  timeout -k 10 300 bash tools/ab_obs.sh C3 $L/libnmmo_hip.so,$L/libnmmo_hip_head.so > gpurun_out/ab_tick_c3.txt 2>&1 && \
+  timeout -k 10 300 bash tools/ab_obs.sh C4 $L/libnmmo_hip.so,$L/libnmmo_hip_head.so > gpurun_out/ab_tick_c4.txt 2>&1
   ;;
 ab)  # same-box A/B of variant libraries: ab <config> <lib,lib,...> [bench args]
   CFG=$2; LIBS=$3; shift 3

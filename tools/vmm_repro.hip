@@ -11,6 +11,10 @@
 //   sync=0|1            hipDeviceSynchronize between the unmaps and the releases
 //   free=1|0            hipMemAddressFree the range (0: keep it reserved, as nmmo_dev_free does)
 //   cycles=N
+//   attrs=1             hipPointerGetAttributes on each new range (what torch does when it wraps a
+//                       foreign device pointer: torch.as_tensor over __cuda_array_interface__)
+//   tmp=1               each check also hipMallocs a quarter-size temporary, written by a kernel and
+//                       kept until the end (torch's caching allocator holding the `b == v` results)
 // Prints one line per variant run: cycles, buffers with wrong contents, ranges handed out again.
 //   hipcc --offload-arch=gfx950 -O2 tools/vmm_repro.hip -o tools/vmm_repro && tools/vmm_repro unmap=whole
 #include <hip/hip_runtime.h>
@@ -86,13 +90,15 @@ static void free_buf(Buf& b, bool whole, bool sync, bool free_va) {
 }
 
 int main(int argc, char** argv) {
-  bool whole = true, sync = false, free_va = true;
+  bool whole = true, sync = false, free_va = true, attrs = false, tmp = false;
   int cycles = 48;
   for (int i = 1; i < argc; i++) {
     if (!strcmp(argv[i], "unmap=chunk")) whole = false;
     else if (!strcmp(argv[i], "unmap=whole")) whole = true;
     else if (!strcmp(argv[i], "sync=1")) sync = true;
     else if (!strcmp(argv[i], "free=0")) free_va = false;
+    else if (!strcmp(argv[i], "attrs=1")) attrs = true;
+    else if (!strcmp(argv[i], "tmp=1")) tmp = true;
     else if (!strncmp(argv[i], "cycles=", 7)) cycles = atoi(argv[i] + 7);
   }
   int dev = 0, vmm = 0;
@@ -107,12 +113,17 @@ int main(int argc, char** argv) {
   int bad_bufs = 0, reused = 0;
   unsigned long long bad_words = 0;
   std::set<void*> seen;
+  std::vector<void*> temps;
   for (int it = 0; it < cycles; it++) {
     Buf bufs[4];
     for (int k = 0; k < 4; k++) {  // the sizes of dbg_vmm.py: (8 + 7 k + it % 12) << 18 floats
       const size_t bytes = (size_t)(8 + 7 * k + it % 12) << 20;
       bufs[k] = alloc_buf(dev, bytes);
       if (!seen.insert(bufs[k].va).second) reused++;
+      if (attrs) {
+        hipPointerAttribute_t at;
+        CHECK(hipPointerGetAttributes(&at, bufs[k].va));
+      }
       hipLaunchKernelGGL(fill_kernel, dim3(1024), dim3(256), 0, 0, (uint32_t*)bufs[k].va, bytes / 4,
                          (uint32_t)(it * 10 + k) * 2654435761u);
     }
@@ -120,6 +131,13 @@ int main(int argc, char** argv) {
     for (int k = 0; k < 4; k++) {
       const size_t bytes = (size_t)(8 + 7 * k + it % 12) << 20;
       CHECK(hipMemset(d_bad, 0, 8));
+      if (tmp) {
+        void* t = nullptr;
+        const size_t tb = ((bytes / 4) + ((size_t)2 << 20) - 1) & ~(((size_t)2 << 20) - 1);
+        CHECK(hipMalloc(&t, tb));
+        hipLaunchKernelGGL(fill_kernel, dim3(256), dim3(256), 0, 0, (uint32_t*)t, tb / 4, 0x5A5A5A5Au);
+        temps.push_back(t);
+      }
       hipLaunchKernelGGL(check_kernel, dim3(1024), dim3(256), 0, 0, (const uint32_t*)bufs[k].va, bytes / 4,
                          (uint32_t)(it * 10 + k) * 2654435761u, d_bad);
       unsigned long long b = 0;
@@ -132,9 +150,10 @@ int main(int argc, char** argv) {
     }
     for (int k = 0; k < 4; k++) free_buf(bufs[k], whole, sync, free_va);
   }
-  printf("vmm_repro unmap=%s sync=%d free=%d cycles=%d: buffers with wrong contents %d (%llu words), "
+  printf("vmm_repro unmap=%s sync=%d free=%d attrs=%d tmp=%d cycles=%d: buffers with wrong contents %d (%llu words), "
          "ranges handed out again %d of %d\n",
-         whole ? "whole" : "chunk", (int)sync, (int)free_va, cycles, bad_bufs, bad_words, reused, 4 * cycles);
+         whole ? "whole" : "chunk", (int)sync, (int)free_va, (int)attrs, (int)tmp, cycles, bad_bufs, bad_words, reused, 4 * cycles);
+  for (void* t : temps) CHECK(hipFree(t));
   CHECK(hipFree(d_bad));
   return bad_bufs ? 1 : 0;
 }
