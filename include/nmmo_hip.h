@@ -587,7 +587,9 @@ NMMO_API int nmmo_exp_store_records(NmmoHandle* h, const NmmoExperience* x, cons
  * whatever the input count). field_stride > 0: each input's rewards / dones / mask are read
  * field_stride bytes apart per row (float at rewards, u8 at dones and mask; e.g. an 8-B packed
  * per-agent record), 0: packed arrays as in nmmo_exp_store. scratch: nmmo_exp_scratch_ints_many
- * ints. Enqueued. */
+ * ints. Enqueued. An input whose buffer already lies where it would be copied to (wire == arena +
+ * the 16-B-aligned end of the arena's used part + 16 at its turn: received straight into the
+ * arena) is stored in place, not copied; nmmo_exp_store_records likewise. */
 NMMO_API int nmmo_exp_store_records_many(NmmoHandle* h, const NmmoExperience* x, const NmmoRecordStore* rs,
                                          const NmmoStoreInput* ins, int32_t n_inputs, int32_t field_stride,
                                          int32_t* scratch, void* stream);

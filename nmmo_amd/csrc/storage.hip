@@ -235,7 +235,7 @@ __global__ void record_reserve_kernel(NmmoExperience x, NmmoRecordStore rs, cons
   const int64_t base = (*rs.arena_used + 15) & ~(int64_t)15;
   const bool ok = total >= wire_header_bytes(n_envs, P) && total <= wire_cap && (total & 15) == 0 &&
                   base + 16 + total <= rs.arena_bytes;
-  *gate = ok;
+  *gate = ok ? (wire == rs.arena + base + 16 ? 2 : 1) : 0;  // 2: the buffer is in place already
   *rbase = base;
   if (ok) {
     int64_t* d = reinterpret_cast<int64_t*>(rs.arena + base);
@@ -251,7 +251,7 @@ __global__ void record_reserve_kernel(NmmoExperience x, NmmoRecordStore rs, cons
 // on the device)
 __global__ void __launch_bounds__(256) record_copy_kernel(NmmoRecordStore rs, const uint4* __restrict__ wire,
                                                          const int* gate, const int64_t* rbase) {
-  if (!*gate) return;
+  if (*gate != 1) return;  // not stored, or received in place
   const int64_t words = *reinterpret_cast<const int64_t*>(wire) / 16;
   uint4* dst = reinterpret_cast<uint4*>(rs.arena + *rbase + 16);
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += (int64_t)gridDim.x * blockDim.x)
@@ -305,7 +305,8 @@ __global__ void record_reserve_many_kernel(NmmoExperience x, NmmoRecordStore rs,
     const int64_t base = (used + 15) & ~(int64_t)15;
     const bool ok = total >= wire_header_bytes(n_envs, b.P) && total <= b.wire_cap[i] && (total & 15) == 0 &&
                     base + 16 + total <= rs.arena_bytes;
-    gates[i] = ok;
+    // 2: the buffer already sits where it is to be stored (received straight into the arena)
+    gates[i] = ok ? (reinterpret_cast<const uint8_t*>(in.wire) == rs.arena + base + 16 ? 2 : 1) : 0;
     rbase[i] = base;
     if (ok) {
       int64_t* d = reinterpret_cast<int64_t*>(rs.arena + base);
@@ -374,7 +375,7 @@ __global__ void __launch_bounds__(kStoreBlock) store_place_many_kernel(NmmoExper
 __global__ void __launch_bounds__(256) record_copy_many_kernel(NmmoRecordStore rs, StoreBatch b, const int* gates,
                                                               const int64_t* rbase) {
   const int i = blockIdx.y;
-  if (!gates[i]) return;
+  if (gates[i] != 1) return;  // not stored, or received in place
   const uint4* wire = reinterpret_cast<const uint4*>(b.in[i].wire);
   const int64_t words = *reinterpret_cast<const int64_t*>(wire) / 16;
   uint4* dst = reinterpret_cast<uint4*>(rs.arena + rbase[i] + 16);

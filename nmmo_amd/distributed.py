@@ -166,14 +166,21 @@ class WireExchange:
                 ev.record(self.comm)
                 self._sized[k] = ev
 
-    def post_payload(self, t: int, wires, smalls):
-        """Step t's buffers: exactly the announced bytes of every wire buffer + its smalls.
-        Returns, on the root, {(rank, j): (wire bytes, small)} with the root's own buffers in
-        place (no self-copy); {} elsewhere. Everything is enqueued on the comm stream."""
+    def totals(self, t: int):
+        """Step t's announced totals on the host ([rank][buffer], + the fault word), once sizes(t)
+        has reached pinned memory (host wait on that copy only)."""
         k = t % self.ring
         if self.cuda and self._sized[k] is not None:
-            self._sized[k].synchronize()  # the copy of sizes(t) into pinned memory (host wait only)
-        tot = self.sizes_host[k].tolist()
+            self._sized[k].synchronize()
+        return self.sizes_host[k].tolist()
+
+    def post_payload(self, t: int, wires, smalls, recv_into=None):
+        """Step t's buffers: exactly the announced bytes of every wire buffer + its smalls.
+        Returns, on the root, {(rank, j): (wire bytes, small)} with the root's own buffers in
+        place (no self-copy); {} elsewhere. recv_into (root): {(rank, j): uint8 tensor} to receive
+        those buffers into instead of the exchange's own receive buffers (the learner's record
+        arena). Everything is enqueued on the comm stream."""
+        tot = self.totals(t)
         # the same checks on both ends of every transfer, before any of step t's transfers is posted
         ranks = range(self.world) if self.rank == self.dst else [self.rank]
         for r in ranks:
@@ -193,7 +200,8 @@ class WireExchange:
             for r in self.peers:
                 for j in range(self.n_bufs):
                     n = int(tot[r][j])
-                    w, s = self.recv_wire[r, j][:n], self.recv_small[r, j]
+                    dst = self.recv_wire[r, j] if recv_into is None or (r, j) not in recv_into else recv_into[r, j]
+                    w, s = dst[:n], self.recv_small[r, j]
                     recvs += [(w, r), (s, r)]
                     got[r, j] = (w, s)
                     self.payload_bytes += n
@@ -353,7 +361,7 @@ class WireGather:
                 self.graphs[j, k] = g
         torch.cuda.synchronize(self.device)
 
-    def _consume(self, s: int, got):
+    def _consume(self, s: int, got, plan=None):
         """On the comm stream, after step s's buffers landed on the root."""
         from . import wire as nw
 
@@ -366,10 +374,12 @@ class WireGather:
             for q in range(1, self.rehearse + 1):  # phantom peer q: the root's own buffers, copied in
                 for j in range(nb):
                     w0, sm0 = got[0, j]
-                    w, sm = self._rh_wire[q - 1, j][:w0.numel()], self._rh_small[q - 1, j]
+                    key = (self.world - 1 + q, j)
+                    w = plan[key] if plan is not None else self._rh_wire[q - 1, j][:w0.numel()]
+                    sm = self._rh_small[q - 1, j]
                     w.copy_(w0)
                     sm.copy_(sm0)
-                    items.append(((self.world - 1 + q, j), (w, sm)))
+                    items.append((key, (w, sm)))
             # every received buffer against the size its sender announced, up to 16 per launch
             recv = [(w, self.engines[j].n_envs, self.x.sizes[s % self.ring, r if r < self.world else 0, j:j + 1])
                     for (r, j), (w, sm) in items if r != 0]
@@ -420,13 +430,43 @@ class WireGather:
         self.x.post_sizes(t, [w[k] for w in self.wires], ready, fault=self.faults[k])
         self.t += 1
 
+    def _arena_plan(self, s: int):
+        """The root's record arena layout of step s, on the host: the store writes its inputs in
+        batch order (the root's own buffers, every peer's, the rehearsal's phantoms), each at the
+        16-B-aligned end of the last plus a 16-B descriptor (storage.hip record_reserve_many_kernel;
+        the arena restarts every step). Received buffers go straight to their positions, so the
+        store finds them in place and copies only the root's own -- instead of receiving into the
+        exchange's buffers and copying every one into the arena. None when the step does not fit
+        (the store then copies, and flags what does not fit, as without a plan)."""
+        if self.store is None or self.store.records is None:
+            return None
+        tot = self.x.totals(s)
+        nb = len(self.engines)
+        keys = [(0, j) for j in range(nb)] + [(r, j) for r in range(1, self.world) for j in range(nb)] + \
+               [(self.world - 1 + q, j) for q in range(1, self.rehearse + 1) for j in range(nb)]
+        used, plan = 0, {}
+        cap = self.store.arena.numel()
+        for (r, j) in keys:
+            n = int(tot[r if r < self.world else 0][j])
+            if n & 15 or n > self.x.caps[j]:
+                return None
+            base = (used + 15) & ~15
+            if base + 16 + n > cap:
+                return None
+            if r != 0:
+                plan[r, j] = self.store.arena[base + 16:base + 16 + n]
+            used = base + 16 + n
+        return plan
+
     def _payload(self, s: int):
         if s <= self._posted:  # drain() already moved it
             return
         ks = s % self.ring
-        got = self.x.post_payload(s, [w[ks] for w in self.wires], [sm[ks] for sm in self.smalls])
+        plan = self._arena_plan(s) if self.rank == 0 else None
+        got = self.x.post_payload(s, [w[ks] for w in self.wires], [sm[ks] for sm in self.smalls],
+                                  recv_into=plan)
         self._posted = s
-        self._consume(s, got)
+        self._consume(s, got, plan)
         self.x.mark_done(s)
 
     def drain(self):
