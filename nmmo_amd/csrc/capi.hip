@@ -67,6 +67,7 @@ struct NmmoHandle {
   // flat / native obs: per agent row, the tag of the buffer the row state describes and the state
   // (ObsParams::zrow / zst); NMMO_OBS_REZERO=1 at create time writes every row in full
   uint64_t* d_zrow = nullptr;
+  uint64_t* d_zext = nullptr;  // flat rows' extended state (ObsParams::zext)
   bool zskip = true;
   const void* zbuf = nullptr;  // the bound obs buffer (nmmo_obs_bind) and its tag
   uint64_t ztag = 0;
@@ -193,7 +194,7 @@ void nmmo_destroy(NmmoHandle* h) {
   void* bufs[] = {h->d_env,  h->d_ent,   h->d_ring,  h->d_mat,   h->d_dep,   h->d_bank,
                   h->d_task, h->d_seeds, h->d_items, h->d_iring, h->d_mlist, h->d_mcount,
                   h->d_events, h->d_tasks, h->d_assign, h->d_tstate, h->d_ws, h->d_uniq, h->d_wenv, h->d_wdrop, h->d_task_cum,
-                  h->d_wcount, h->d_wmcount, h->d_wrank, h->d_wpk, h->d_foreign, h->d_zrow};  // d_zst lives in d_zrow's allocation
+                  h->d_wcount, h->d_wmcount, h->d_wrank, h->d_wpk, h->d_foreign, h->d_zrow, h->d_zext};  // d_zst lives in d_zrow's allocation
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   delete h;
@@ -250,6 +251,9 @@ int nmmo_create(const NmmoConfig* cfg, int32_t n_envs, uint64_t seed, int32_t de
   }
   if (cfg->obs_layout == NMMO_OBS_FLAT || cfg->obs_layout == NMMO_OBS_NATIVE) {
     ALLOC(h->d_zrow, n * P * 16);  // (two statements)
+  }
+  if (cfg->obs_layout == NMMO_OBS_FLAT) {
+    ALLOC(h->d_zext, n * P * kZext * 8);
   }
   {
     const char* rz = getenv("NMMO_OBS_REZERO");  // A/B: rewrite the zero rows every launch
@@ -319,6 +323,7 @@ static ObsParams obs_params(NmmoHandle* h, void* obs) {
   // only the bound buffer (nmmo_obs_bind) is written incrementally
   p.zrow = h->d_zrow;
   p.zst = h->d_zrow ? h->d_zrow + (size_t)h->st.n_envs * h->st.P : nullptr;
+  p.zext = h->d_zext;
   p.ztag = h->d_zrow && h->zskip && obs && obs == h->zbuf ? h->ztag : 0;
   p.rows_out = h->d_rows_out;
   p.ws = h->wrap_on ? h->d_ws : nullptr;
@@ -552,12 +557,13 @@ int nmmo_dev_free(void* ptr) {
   }
   HIP_TRY(hipDeviceSynchronize());  // no kernel may still use the range
   // Unmapped chunk by chunk as it was mapped and the physical chunks released; the virtual range
-  // stays reserved for the life of the process (NMMO_DEVMEM_FREE_VA=1 frees it, for A/B). A
-  // freed range handed out again by hipMemAddressReserve read back other contents through torch
-  // (tests/test_gpu_devmem.py with free: cycle 1, one-chunk buffers, so not the unmap form), while
-  // the same HIP call sequence alone (tools/vmm_repro.hip) found no wrong word with 187 of 192
-  // ranges reused: profiles/r05/vmm_repro.txt. A range never reused cannot hit it; the address
-  // space is 128 TB.
+  // stays reserved for the life of the process (NMMO_DEVMEM_FREE_VA=1 frees it, for A/B). Cause,
+  // isolated with no build code (tools/vmm_repro.hip, profiles/r05/vmm_repro.txt): after
+  // hipMemAddressFree, hipMemAddressReserve hands the same range out again, and a later hipMalloc
+  // (torch's caching allocator, here) can return addresses inside it too -- the two allocations
+  // alias, so a buffer reads back what the other wrote (187 of 187 reused ranges with hipMalloc'd
+  // temporaries alive, either unmap form; 0 of 192 with ranges kept reserved). A range never
+  // reused cannot alias; the address space is 128 TB.
   const size_t chunk = a.chunks.empty() ? a.bytes : a.bytes / a.chunks.size();
   for (size_t i = 0; i < a.chunks.size(); i++) HIP_TRY(hipMemUnmap((char*)ptr + i * chunk, chunk));
   for (auto c : a.chunks) HIP_TRY(hipMemRelease(c));

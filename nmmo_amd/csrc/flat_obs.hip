@@ -80,21 +80,55 @@ __device__ __forceinline__ uint64_t fo_chunk(const AoSections& x) {
 }
 __device__ __forceinline__ float fo_bit(uint64_t m) { return __builtin_amdgcn_inverse_ballot_w64(m) ? 1.f : 0.f; }
 
-// Chunks kC .. kFoChunks - 1 (past Buy.MarketItem's entries; chunk 17 also holds Buy's last 40
-// entries and its no-op): lane L of chunk kC stores entry 64 kC + L. buy17: Buy's bits in chunk 17.
+// The row's tracked ActionTargets chunks (ObsParams::zext): chunks 0 and 1 (Style, Attack.Target,
+// Buy's first 24 entries) and 17..24 (Buy's last 40 entries and no-op, then every other section,
+// AgentId, CurrentTick) as slots 0..9. A chunk whose mask equals the one the row was last written
+// with is not stored again: per tick an agent's Move and Attack.Target bits change, while the
+// gold-, inventory- and same-tile-driven sections mostly do not.
+constexpr int kFoTail0 = (kFoBuyLo + NMMO_MARKET_ROWS) / 64;  // 17
+__host__ __device__ constexpr int fo_slot(int c) { return c < 2 ? c : c - kFoTail0 + 2; }
+static_assert(fo_slot(kFoChunks - 1) == 9 && kZext == 10 + 1 + 12, "tracked chunks | position | items");
+struct FoImg {
+  bool ext;        // the row's extended state is valid (else every chunk is stored)
+  uint32_t lo, hi; // the wave's loaded masks: lane 10 j + slot = agent j's chunk `slot`
+  int j10;         // 10 j
+  int nimg;        // the new masks: lane 2 slot / 2 slot + 1 = slot's lo / hi word
+  int nst;         // mask entries (+ id, tick) stored
+};
+__device__ __forceinline__ uint64_t fo_prev(const FoImg& g, int slot) {
+  return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)g.lo, g.j10 + slot) |
+         (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)g.hi, g.j10 + slot) << 32;
+}
+// chunk kC with mask m: stored unless the row holds it already; its mask goes into the new image
 template <int kC>
-__device__ __forceinline__ void fo_tail_chunks(float* row, const AoSections& x, uint64_t buy17, float aid, float tick) {
+__device__ __forceinline__ void fo_put(float* row, FoImg& g, uint64_t m, float aid, float tick) {
+  constexpr int sl = fo_slot(kC);
+  const int lane = lane_id();
+  const bool same = g.ext && m == fo_prev(g, sl);
+  if constexpr (kC == kFoChunks - 1) {  // + AgentId, CurrentTick right after the mask entries
+    constexpr int n = kMaskN - 64 * kC;
+    if (!same) {
+      if (lane < n + 2) row[64 * kC + lane] = lane < n ? fo_bit(m) : lane == n ? aid : tick;
+      g.nst += n + 2;
+    } else {
+      if (lane == n + 1) row[64 * kC + lane] = tick;  // the tick changes every step
+      g.nst += 1;
+    }
+  } else if (!same) {
+    row[64 * kC + lane] = fo_bit(m);
+    g.nst += 64;
+  }
+  g.nimg = writelane<2 * sl>((int)(uint32_t)m, g.nimg);
+  g.nimg = writelane<2 * sl + 1>((int)(uint32_t)(m >> 32), g.nimg);
+}
+template <int kC>
+__device__ __forceinline__ void fo_tail_chunks(float* row, FoImg& g, const AoSections& x, uint64_t buy17, float aid,
+                                               float tick) {
   if constexpr (kC < kFoChunks) {
     uint64_t m = fo_chunk<kC>(x);
-    if constexpr (kC == (kFoBuyLo + NMMO_MARKET_ROWS) / 64) m |= buy17 | 1ull << ((kFoBuyLo + NMMO_MARKET_ROWS) & 63);
-    const int lane = lane_id();
-    if constexpr (kC == kFoChunks - 1) {  // + AgentId, CurrentTick right after the mask entries
-      constexpr int n = kMaskN - 64 * kC;
-      if (lane < n + 2) row[64 * kC + lane] = lane < n ? fo_bit(m) : lane == n ? aid : tick;
-    } else {
-      row[64 * kC + lane] = fo_bit(m);
-    }
-    fo_tail_chunks<kC + 1>(row, x, buy17, aid, tick);
+    if constexpr (kC == kFoTail0) m |= buy17 | 1ull << ((kFoBuyLo + NMMO_MARKET_ROWS) & 63);
+    fo_put<kC>(row, g, m, aid, tick);
+    fo_tail_chunks<kC + 1>(row, g, x, buy17, aid, tick);
   }
 }
 
@@ -211,11 +245,23 @@ __global__ void __launch_bounds__(64 * kAoWaves) flat_obs_kernel(ObsParams p) {
       if (p.ws) my_prev = p.ws[ai].prev_price;
   }
   // bit j: agent j's row state describes this buffer / the row is all-zero / its Task section holds
-  // its task's embedding; my_h = hv | hm << 12: its Entity rows >= hv and its Market rows and Buy
-  // entries >= hm are zero (a row of unknown content: nothing known zero)
+  // its task's embedding / its extended state is valid; my_h = hv | hm << 12: its Entity rows >= hv
+  // and its Market rows and Buy entries >= hm are zero (a row of unknown content: nothing known zero)
   const bool zvl = p.ztag && my_z == p.ztag;
   const bool zzl = zvl && (my_s & kZsZero);
   const uint64_t zvalid = __ballot(zvl), zzero = __ballot(zzl), ztask = __ballot(zvl && !zzl && zs_task(my_s) == my_task);
+  const uint64_t zextv = __ballot(zvl && !zzl && (my_s & kZsExt));
+  // the extended state (ObsParams::zext): lane 10 j + slot = agent j's tracked chunk `slot`, lane
+  // 40 + j its Tile position; lane 12 j + k (inv) its item word k
+  uint2 img = make_uint2(0u, 0u), pinv = make_uint2(0u, 0u);
+  {
+    const int ja = lane < 40 ? lane / 10 : lane - 40, ji = lane / 12;
+    const int aa = abase + kAoWaves * ja, ai = abase + kAoWaves * ji;
+    if (lane < 44 && aa < P && ((zextv >> ja) & 1))
+      img = reinterpret_cast<const uint2*>(p.zext)[((size_t)e * P + aa) * kZext + (lane < 40 ? lane % 10 : 10)];
+    if (lane < 48 && ai < P && ((zextv >> ji) & 1))
+      pinv = reinterpret_cast<const uint2*>(p.zext)[((size_t)e * P + ai) * kZext + 11 + lane % 12];
+  }
   const int my_h = !zvl ? (kNObs | NMMO_MARKET_ROWS << 12) : zzl ? 0 : (zs_hv(my_s) | zs_hm(my_s) << 12);
   int nrows = 0;                  // rows this wave wrote (rows_out[0])
   unsigned long long nbytes = 0;  // bytes this wave stored (rows_out[1])
@@ -275,6 +321,8 @@ __global__ void __launch_bounds__(64 * kAoWaves) flat_obs_kernel(ObsParams p) {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
+    const bool ext = (zextv >> j) & 1;  // the row's extended state is valid
+    FoImg fg{ext, img.x, img.y, 10 * j, 0, 0};
     // ActionTargets (+ AgentId, CurrentTick)
     if (!(NMMO_FO_ABL & 1)) {
       AoAgent ag;
@@ -289,7 +337,8 @@ __global__ void __launch_bounds__(64 * kAoWaves) flat_obs_kernel(ObsParams p) {
       ag.prev_price = kWrap ? __builtin_amdgcn_readlane(my_prev, j) : -1;
       ag.mv = mv;
       const AoSections x = ao_sections<kWrap>(p, T, Sp, visw, ag, it);
-      row[lane] = fo_bit(fo_chunk<0>(x));
+      fg.ext = ext;
+      fo_put<0>(row, fg, fo_chunk<0>(x), 0.f, 0.f);
       // Buy.MarketItem entry k < listings: exchange on, price <= gold, not the agent's own. buy_word
       // m = the ballot over listings 64 m + lane; chunk c holds words c - 1 (from bit 40) and c - 2
       // (its top 40 bits). Chunks 2..16 hold Buy entries only: written up to the known-zero
@@ -305,20 +354,18 @@ __global__ void __launch_bounds__(64 * kAoWaves) flat_obs_kernel(ObsParams p) {
       };
       const int nbuy = max(nm, hm);
       const int clast = max(1, min((kFoBuyLo + nbuy - 1) >> 6, 16));
-      uint64_t bprev = 0ull;
-      const uint64_t c1 = fo_chunk<1>(x);
+      uint64_t bprev = nm > 0 ? buy_word(0) : 0ull;  // chunk 1: Attack.Target's tail, Buy's first 24
+      fo_put<1>(row, fg, fo_chunk<1>(x) | bprev << (kFoBuyLo & 63), 0.f, 0.f);
 #pragma unroll 1
-      for (int cc = 1; cc <= clast; cc++) {
+      for (int cc = 2; cc <= clast; cc++) {  // Buy-only chunks, not tracked
         const uint64_t bcur = 64 * (cc - 1) < nm ? buy_word(cc - 1) : 0ull;
-        const uint64_t m = (cc == 1 ? c1 : 0ull) | bcur << (kFoBuyLo & 63) | bprev >> (64 - (kFoBuyLo & 63));
-        row[64 * cc + lane] = fo_bit(m);
+        row[64 * cc + lane] = fo_bit(bcur << (kFoBuyLo & 63) | bprev >> (64 - (kFoBuyLo & 63)));
         bprev = bcur;
       }
       // chunk 17: Buy entries 984..1023 (word 15, only when nm > 960: the loop then ran to 16)
       const uint64_t buy17 = nm > 15 * 64 ? bprev >> (64 - (kFoBuyLo & 63)) : 0ull;
-      fo_tail_chunks<(kFoBuyLo + NMMO_MARKET_ROWS) / 64>(row, x, buy17, (float)aid, tickf);
-      nbytes += 4ull * (64 * (1 + clast) + 64 * (kFoChunks - 1 - (kFoBuyLo + NMMO_MARKET_ROWS) / 64) +
-                        (kMaskN - 64 * (kFoChunks - 1)) + 2);
+      fo_tail_chunks<kFoTail0>(row, fg, x, buy17, (float)aid, tickf);
+      nbytes += 4ull * (fg.nst + 64 * (clast - 1));
     }
     // Entity rows: two per pass (lanes 0-30 row k, lanes 32-62 row k + 1: 62 contiguous floats),
     // the rows past the visible ones not known zero as one zero run
@@ -333,15 +380,22 @@ __global__ void __launch_bounds__(64 * kAoWaves) flat_obs_kernel(ObsParams p) {
       }
       const int hz = max(nv2, hv);
       wave_zero(row, kFoEntity + nv2 * NMMO_N_ENTITY_COLS, kFoEntity + hz * NMMO_N_ENTITY_COLS);
-      nbytes += 4ull * (hz * NMMO_N_ENTITY_COLS + kInv * 16 + max(nm, hm) * 16 + 225 * 3);
+      nbytes += 4ull * (hz * NMMO_N_ENTITY_COLS + max(nm, hm) * 16);
     }
-    // Inventory: item q = 4 h + lane / 16, column lane % 16 (own items, owner = self)
+    // Inventory: item q = 4 h + lane / 16, column lane % 16 (own items, owner = self); not stored
+    // when the row was last written from the same 12 item words (its only inputs besides AgentId)
+    const int jl = (12 * j + lane) & 63;
+    const uint32_t px = (uint32_t)__shfl((int)pinv.x, jl), py = (uint32_t)__shfl((int)pinv.y, jl);
+    const bool inv_same = ext && __ballot(lane < kInv && (px != it.x || py != it.y)) == 0ull;
+    if (!inv_same) {
 #pragma unroll
-    for (int h = 0; h < ((NMMO_FO_ABL & 4) ? 0 : kInv * 16 / 64); h++) {
-      const int q = 4 * h + iq;
-      float v = 0.f;
-      if (4 * h < ninv && q < ninv) v = ic_value(ist[la * kInv + q], aid, icd);  // (a uniform skip first)
-      row[kFoInv + 64 * h + lane] = v;
+      for (int h = 0; h < ((NMMO_FO_ABL & 4) ? 0 : kInv * 16 / 64); h++) {
+        const int q = 4 * h + iq;
+        float v = 0.f;
+        if (4 * h < ninv && q < ninv) v = ic_value(ist[la * kInv + q], aid, icd);  // (a uniform skip first)
+        row[kFoInv + 64 * h + lane] = v;
+      }
+      nbytes += 4ull * kInv * 16;
     }
     // Market (the env's listings, ascending row; owner = lister) and its zero run down to hm
     // (the listings past the staged ones in a loop of their own: a global load in the common loop
@@ -365,21 +419,34 @@ __global__ void __launch_bounds__(64 * kAoWaves) flat_obs_kernel(ObsParams p) {
       for (int k = lane; k < tdim; k += 64) row[kFoTask + k] = temb[k];
       nbytes += 4ull * tdim;
     }
-    // Tile: (row, column, material) per window tile t = lane + 64 i, three stores 12 B apart
+    // Tile: (row, column, material) per window tile t = lane + 64 i, three stores 12 B apart; the
+    // row (column) components are not stored when the row was last written at the same agent row
+    // (column): a move changes one of the two, staying neither
+    const uint32_t ppos = (uint32_t)__builtin_amdgcn_readlane((int)img.x, 40 + j);
+    const bool same_r = ext && (int)(ppos & 255u) == r, same_c = ext && (int)((ppos >> 8) & 255u) == c;
     if (!(NMMO_FO_ABL & 16)) {
       float* dt = row + kFoTask + tdim + 3 * lane;
 #pragma unroll
       for (int i = 0; i < 4; i++) {
         if (lane + 64 * i < 225) {
-          dt[192 * i] = (float)(r + ((toff[i] << 24) >> 24));
-          dt[192 * i + 1] = (float)(c + (toff[i] >> 8));
+          if (!same_r) dt[192 * i] = (float)(r + ((toff[i] << 24) >> 24));
+          if (!same_c) dt[192 * i + 1] = (float)(c + (toff[i] >> 8));
           dt[192 * i + 2] = (float)wm[i];
         }
       }
+      nbytes += 4ull * 225 * (1 + !same_r + !same_c);
     }
-    if (lane == 0) {
-      if (!zv) p.zrow[(size_t)e * P + a] = p.ztag;
-      p.zst[(size_t)e * P + a] = zs_pack(nv2, nm, task);
+    {  // the row's state: tag, zero thresholds and task, then the extended state
+      uint32_t* zx = reinterpret_cast<uint32_t*>(p.zext + ((size_t)e * P + a) * kZext);
+      int wv = fg.nimg;  // lanes 0..19 the tracked masks, lanes 20 / 21 the position
+      if (lane == 20) wv = r | c << 8;
+      if (lane == 21) wv = 0;
+      if (lane < 22) zx[lane] = (uint32_t)wv;
+      if (!inv_same && lane < kInv) reinterpret_cast<uint2*>(zx + 22)[lane] = it;
+      if (lane == 0) {
+        if (!zv) p.zrow[(size_t)e * P + a] = p.ztag;
+        p.zst[(size_t)e * P + a] = zs_pack(nv2, nm, task) | kZsExt;
+      }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the next agent reuses visw
     __builtin_amdgcn_wave_barrier();

@@ -1,8 +1,8 @@
 """Chunk-mapped device buffers (nmmo_dev_alloc / nmmo_dev_free, nmmo_amd/devmem.py) on MI355X:
 buffers allocated, filled, checked and freed over and over keep their contents. Freed virtual
-ranges stay reserved (a reused range read back other contents through torch, capi.hip
-nmmo_dev_free; tools/vmm_repro.hip is the standalone reproducer), so every allocation gets
-addresses never used before."""
+ranges stay reserved: a range freed with hipMemAddressFree and reserved again can alias a later
+hipMalloc (torch's allocator) and read back what that wrote (tools/vmm_repro.hip, the standalone
+reproducer; capi.hip nmmo_dev_free), so every allocation gets addresses never used before."""
 
 import pytest
 import torch

@@ -58,6 +58,12 @@ tick1)  # tick parity with compile-time S/P, then same-box C2 / C3 / C4 against 
   timeout -k 10 300 bash tools/ab_obs.sh C3 $L/libnmmo_hip.so,$L/libnmmo_hip_head.so > gpurun_out/ab_tick_c3.txt 2>&1 && \
   timeout -k 10 300 bash tools/ab_obs.sh C4 $L/libnmmo_hip.so,$L/libnmmo_hip_head.so > gpurun_out/ab_tick_c4.txt 2>&1
   ;;
+ext)  # flat rows' extended state (tracked chunks, inventory, Tile position): parity, then C4 / start-kit A/B vs HEAD
+  timeout -k 10 600 $PYT tests/test_gpu_parity.py tests/test_gpu_zero_rows.py tests/test_gpu_obs_contract.py tests/test_gpu_wrapper.py \
+    tests/test_gpu_fullsize.py tests/test_gpu_vecenv.py > gpurun_out/gpu_ext.log 2>&1 && \
+  timeout -k 10 600 bash tools/ab_obs.sh C4 $L/libnmmo_hip.so,$L/libnmmo_hip_head.so > gpurun_out/ab_ext.txt 2>&1 && \
+  timeout -k 10 600 bash tools/ab_obs.sh C4 $L/libnmmo_hip.so,$L/libnmmo_hip_head.so --wrapper neurips23_start_kit > gpurun_out/ab_ext_wrap.txt 2>&1
+  ;;
 ab)  # same-box A/B of variant libraries: ab <config> <lib,lib,...> [bench args]
   CFG=$2; LIBS=$3; shift 3
   timeout -k 10 900 bash tools/ab_obs.sh $CFG $LIBS "$@" > gpurun_out/ab_$CFG.txt 2>&1
