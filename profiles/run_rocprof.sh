@@ -21,6 +21,8 @@ for c in $CONFIGS; do
     C5) ARGS="--config C5 --batches 1 --no-decode" ;;
     *) ARGS="--config $c" ;;
   esac
+  # C4-rezero: every obs row written in full (the flat full-write kernel, bench.py's extra of the name)
+  if [ "$c" = C4-rezero ]; then ARGS="--config C4"; export NMMO_OBS_REZERO=1; else unset NMMO_OBS_REZERO; fi
   if [ "$c" = storage ]; then  # experience-storage kernels (tools/bench_storage.py)
     timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/$c/trace -o run -- \
       python3 tools/bench_storage.py > $OUT/$c/bench_storage.json

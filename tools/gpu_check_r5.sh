@@ -64,6 +64,11 @@ ext)  # flat rows' extended state (tracked chunks, inventory, Tile position): pa
   timeout -k 10 600 bash tools/ab_obs.sh C4 $L/libnmmo_hip.so,$L/libnmmo_hip_head.so > gpurun_out/ab_ext.txt 2>&1 && \
   timeout -k 10 600 bash tools/ab_obs.sh C4 $L/libnmmo_hip.so,$L/libnmmo_hip_head.so --wrapper neurips23_start_kit > gpurun_out/ab_ext_wrap.txt 2>&1
   ;;
+prof)  # round-5 rocprofv3 summaries, then env batches per GPU (2 vs 4) on C4
+  timeout -k 10 1000 bash profiles/run_rocprof.sh r05 C4 C4-native C4-rezero C5 C2 C3 > gpurun_out/prof_r05.log 2>&1 && \
+  for b in 2 4 2 4; do timeout -k 10 120 python bench.py --batches $b --steps 200 --warmup 30 --no-cpu-baseline --no-extras > gpurun_out/bat_$b.json 2>/dev/null && \
+    python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], round(d['value']/1e6,2), d['ms_per_step'], d['kernel_ms'])" gpurun_out/bat_$b.json $b >> gpurun_out/batches.txt || exit 1; done
+  ;;
 ab)  # same-box A/B of variant libraries: ab <config> <lib,lib,...> [bench args]
   CFG=$2; LIBS=$3; shift 3
   timeout -k 10 900 bash tools/ab_obs.sh $CFG $LIBS "$@" > gpurun_out/ab_$CFG.txt 2>&1
