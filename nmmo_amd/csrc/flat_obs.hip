@@ -87,8 +87,7 @@ __device__ __forceinline__ float fo_bit(uint64_t m) { return __builtin_amdgcn_in
 // gold-, inventory- and same-tile-driven sections mostly do not.
 constexpr int kFoTail0 = (kFoBuyLo + NMMO_MARKET_ROWS) / 64;  // 17
 __host__ __device__ constexpr int fo_slot(int c) { return c < 2 ? c : c - kFoTail0 + 2; }
-static_assert(fo_slot(kFoChunks - 1) == 9 && kZext == 10 + 1 + 12 + 16, "tracked chunks | position | items | materials");
-static_assert(M_FISH < 16, "Tile materials as 4-bit codes");
+static_assert(fo_slot(kFoChunks - 1) == 9 && kZext == 10 + 1 + 12, "tracked chunks | position | items");
 struct FoImg {
   bool ext;        // the row's extended state is valid (else every chunk is stored)
   uint32_t lo, hi; // the wave's loaded masks: lane 10 j + slot = agent j's chunk `slot`
@@ -197,7 +196,7 @@ __device__ __forceinline__ int fo_compact(const uint32_t (&pr)[kAoRows], int r, 
 // kS: the slot count when known at compile time (C3 / C4: 128 players + 256 NPCs), 0 = p.S. With
 // it the staged-column offsets are immediates instead of uniform values the agent loop keeps live.
 template <bool kWrap, int kS>
-__global__ void __launch_bounds__(64 * kAoWaves) __attribute__((amdgpu_waves_per_eu(4, 4))) flat_obs_kernel(ObsParams p) {
+__global__ void __launch_bounds__(64 * kAoWaves) flat_obs_kernel(ObsParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int S = kS ? kS : p.S, P = p.P, Sp = ao_stride(S), tdim = p.task_dim, elems = kFoTask + tdim + 225 * 3;
   int16_t* T = reinterpret_cast<int16_t*>(smem);
@@ -263,26 +262,16 @@ __global__ void __launch_bounds__(64 * kAoWaves) __attribute__((amdgpu_waves_per
     if (lane < 48 && ai < P && ((zextv >> ji) & 1))
       pinv = reinterpret_cast<const uint2*>(p.zext)[((size_t)e * P + ai) * kZext + 11 + lane % 12];
   }
-  // the Tile materials each row was last written with: lane L's 4-bit codes of tiles L + 64 i,
-  // agent j's in bits 16 (j & 1) of pmat[j >> 1]
-  uint32_t pmat[2] = {0u, 0u};
-#pragma unroll
-  for (int jj = 0; jj < kPerWave; jj++) {
-    const int aj = abase + kAoWaves * jj;
-    if (aj < P && ((zextv >> jj) & 1))
-      pmat[jj >> 1] |= (uint32_t)reinterpret_cast<const uint16_t*>(p.zext + ((size_t)e * P + aj) * kZext + 23)[lane]
-                       << (16 * (jj & 1));
-  }
   const int my_h = !zvl ? (kNObs | NMMO_MARKET_ROWS << 12) : zzl ? 0 : (zs_hv(my_s) | zs_hm(my_s) << 12);
   int nrows = 0;                  // rows this wave wrote (rows_out[0])
   unsigned long long nbytes = 0;  // bytes this wave stored (rows_out[1])
   int wo[2];
   ao_win_offsets(wo);
-  uint32_t toff[2] = {0u, 0u};  // window tile lane + 64 i: (row offset) & 255 | (col offset & 255) << 8, 16 bits each
+  int toff[4];  // window tile lane + 64 i: (row offset) & 255 | (col offset) << 8
 #pragma unroll
   for (int i = 0; i < 4; i++) {
     const int t = lane + 64 * i;
-    toff[i >> 1] |= (uint32_t)(((t / 15 - kVision) & 255) | ((t % 15 - kVision) & 255) << 8) << (16 * (i & 1));
+    toff[i] = ((t / 15 - kVision) & 255) | (t % 15 - kVision) * 256;
   }
   const int ef = lane & 31, eh = lane >> 5;  // Entity: field, row of the pair
   const int iq = lane >> 4;                  // Inventory: item of the chunk
@@ -430,27 +419,22 @@ __global__ void __launch_bounds__(64 * kAoWaves) __attribute__((amdgpu_waves_per
       for (int k = lane; k < tdim; k += 64) row[kFoTask + k] = temb[k];
       nbytes += 4ull * tdim;
     }
-    // Tile: (row, column, material) per window tile t = lane + 64 i, three stores 12 B apart; not
-    // stored at all when the row was last written at the same position with the same materials.
-    // (Storing only the components that changed left partly written lines -- every third dword --
-    // which the memory writes back as masked partial-line writes: WRITE_SIZE 1.9x the stored bytes.)
+    // Tile: (row, column, material) per window tile t = lane + 64 i, three stores 12 B apart; the
+    // row (column) components are not stored when the row was last written at the same agent row
+    // (column): a move changes one of the two, staying neither
     const uint32_t ppos = (uint32_t)__builtin_amdgcn_readlane((int)img.x, 40 + j);
-    const uint32_t mcode = (wm[0] & 15u) | (wm[1] & 15u) << 4 | (wm[2] & 15u) << 8 | (wm[3] & 15u) << 12;
-    const uint32_t pm = (((j >> 1) ? pmat[1] : pmat[0]) >> (16 * (j & 1))) & 0xFFFFu;
-    const bool mat_same = ext && __ballot(mcode != pm) == 0ull;
-    const bool tile_same = mat_same && (int)(ppos & 255u) == r && (int)((ppos >> 8) & 255u) == c;
-    if (!(NMMO_FO_ABL & 16) && !tile_same) {
+    const bool same_r = ext && (int)(ppos & 255u) == r, same_c = ext && (int)((ppos >> 8) & 255u) == c;
+    if (!(NMMO_FO_ABL & 16)) {
       float* dt = row + kFoTask + tdim + 3 * lane;
 #pragma unroll
       for (int i = 0; i < 4; i++) {
         if (lane + 64 * i < 225) {
-          const uint32_t to = toff[i >> 1] >> (16 * (i & 1));
-          dt[192 * i] = (float)(r + (int)(int8_t)(to & 255u));
-          dt[192 * i + 1] = (float)(c + (int)(int8_t)((to >> 8) & 255u));
+          if (!same_r) dt[192 * i] = (float)(r + ((toff[i] << 24) >> 24));
+          if (!same_c) dt[192 * i + 1] = (float)(c + (toff[i] >> 8));
           dt[192 * i + 2] = (float)wm[i];
         }
       }
-      nbytes += 4ull * 225 * 3;
+      nbytes += 4ull * 225 * (1 + !same_r + !same_c);
     }
     {  // the row's state: tag, zero thresholds and task, then the extended state
       uint32_t* zx = reinterpret_cast<uint32_t*>(p.zext + ((size_t)e * P + a) * kZext);
@@ -459,7 +443,6 @@ __global__ void __launch_bounds__(64 * kAoWaves) __attribute__((amdgpu_waves_per
       if (lane == 21) wv = 0;
       if (lane < 22) zx[lane] = (uint32_t)wv;
       if (!inv_same && lane < kInv) reinterpret_cast<uint2*>(zx + 22)[lane] = it;
-      if (!mat_same) reinterpret_cast<uint16_t*>(zx + 46)[lane] = (uint16_t)mcode;
       if (lane == 0) {
         if (!zv) p.zrow[(size_t)e * P + a] = p.ztag;
         p.zst[(size_t)e * P + a] = zs_pack(nv2, nm, task) | kZsExt;

@@ -103,14 +103,13 @@ struct ObsParams {
   uint64_t ztag;
   // flat rows (flat_obs.hip), per row kZext u64 (valid when zst has kZsExt): the 64-bit masks of
   // the 10 tracked ActionTargets chunks, the position (row | col << 8) the Tile section was written
-  // for, the 12 item words the Inventory section was written from, and the Tile materials (4 bits
-  // per tile, lane L's 4 tiles L + 64 i as one u16 per lane)
+  // for, and the 12 item words the Inventory section was written from
   uint64_t* zext;
   unsigned long long* rows_out;  // optional [n][2]: += rows this launch wrote, bytes it stored, per env
 };
 constexpr uint64_t kZsZero = 1ull << 20;
 constexpr uint64_t kZsExt = 1ull << 21;  // the row's extended state (ObsParams::zext) is valid
-constexpr int kZext = 10 + 1 + 12 + 16;  // u64 per row: chunk masks | position | item words | materials
+constexpr int kZext = 10 + 1 + 12;       // u64 per row: chunk masks | position | item words
 __host__ __device__ inline int zs_hv(uint64_t s) { return (int)(s & 255u); }
 __host__ __device__ inline int zs_hm(uint64_t s) { return (int)((s >> 8) & 4095u); }
 __host__ __device__ inline int zs_task(uint64_t s) { return (int)(uint32_t)(s >> 32); }
