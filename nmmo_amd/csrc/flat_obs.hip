@@ -25,8 +25,9 @@
 namespace nmmo {
 
 #ifndef NMMO_FO_ABL  // diagnostic ablation (timing attribution only, wrong rows): bit 1 masks, 2 Entity,
-#define NMMO_FO_ABL 0  // 4 Inventory, 8 Market, 16 Tile, 32 compaction (tools/debug/variants.py)
-#endif
+#define NMMO_FO_ABL 0  // 4 Inventory, 8 Market, 16 Tile, 32 compaction, 64 the agent loop (prologue only),
+#endif                 // 128 everything (an empty launch), 256 rows aliased onto 128 per XCD (stores L2-resident)
+                       // (tools/debug/variants.py)
 constexpr int kFoStagedListings = 256;  // listings whose item words are staged (Market rows)
 constexpr int kFoChunks = 25;           // 64-entry chunks over the 1,586 mask entries (+ id, tick)
 static_assert(kFoChunks * 64 >= kMaskN + 2 && (kFoChunks - 1) * 64 < kMaskN, "mask chunks");
@@ -209,6 +210,7 @@ __global__ void __launch_bounds__(64 * kAoWaves) flat_obs_kernel(ObsParams p) {
   const int el = blockIdx.x, g = blockIdx.y;
   const int e = p.env_list ? p.env_list[el] : el, tid = threadIdx.x, lane = lane_id();
   if ((unsigned)e >= (unsigned)p.n_envs) return;  // a bad list id (the tick records it)
+  if (NMMO_FO_ABL & 128) return;
   const int w = __builtin_amdgcn_readfirstlane(wave_id());
   const int nm = min(max(p.mcount[e], 0), NMMO_MARKET_ROWS);
   for (int j = tid; j < nm; j += blockDim.x) {  // end-of-tick listings, ascending row
@@ -262,6 +264,10 @@ __global__ void __launch_bounds__(64 * kAoWaves) flat_obs_kernel(ObsParams p) {
     if (lane < 48 && ai < P && ((zextv >> ji) & 1))
       pinv = reinterpret_cast<const uint2*>(p.zext)[((size_t)e * P + ai) * kZext + 11 + lane % 12];
   }
+  // Wait for the prologue's loads here, once: vmcnt counts stores too and retires in order, so a
+  // first use of img / pinv / my_prev inside the agent loop (under a branch the waitcnt pass cannot
+  // see through) waited for every store the row had issued -- one full drain per tracked chunk.
+  asm volatile("" : "+v"(img.x), "+v"(img.y), "+v"(pinv.x), "+v"(pinv.y), "+v"(my_prev));
   const int my_h = !zvl ? (kNObs | NMMO_MARKET_ROWS << 12) : zzl ? 0 : (zs_hv(my_s) | zs_hm(my_s) << 12);
   int nrows = 0;                  // rows this wave wrote (rows_out[0])
   unsigned long long nbytes = 0;  // bytes this wave stored (rows_out[1])
@@ -278,10 +284,10 @@ __global__ void __launch_bounds__(64 * kAoWaves) flat_obs_kernel(ObsParams p) {
   const IcDesc icd = ic_desc(lane & 15);      // Inventory / Market: column lane % 16
 
 #pragma unroll 1
-  for (int j = 0; j < kPerWave; j++) {
+  for (int j = 0; j < ((NMMO_FO_ABL & 64) ? 0 : kPerWave); j++) {
     const int a = abase + kAoWaves * j;
     if (a >= P) break;
-    float* row = p.obs + ((size_t)e * P + a) * elems;
+    float* row = p.obs + ((NMMO_FO_ABL & 256) ? (size_t)(((e * P + a) & 15) + 16 * (blockIdx.x & 7)) : (size_t)e * P + a) * elems;
     const bool zv = (zvalid >> j) & 1;
     const int hj = __builtin_amdgcn_readlane(my_h, j);
     const int hv = hj & 4095, hm = hj >> 12;
