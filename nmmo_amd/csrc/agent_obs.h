@@ -70,6 +70,15 @@ __host__ inline bool ao_layout_ok(const ObsParams& p) {
   return p.o_agent_id == sec_flat(12);
 }
 
+// The lane index, opaque to the optimiser: per-lane predicates built from it are recomputed where
+// they are used instead of hoisted out of the agent loops as lane masks (an SGPR pair each), which
+// the loops then spilled to VGPR lanes and reloaded (two v_readlane each).
+__device__ __forceinline__ int ao_lane() {
+  int l = (int)(threadIdx.x & 63u);
+  asm volatile("" : "+v"(l));
+  return l;
+}
+
 __device__ __forceinline__ uint64_t low_bits(int n) { return n >= 64 ? ~0ull : n <= 0 ? 0ull : (1ull << n) - 1ull; }
 // x with lane L's value replaced by the wave-uniform v: one v_writelane_b32 (the value pinned to
 // an SGPR, the lane an inline constant; this compiler has no writelane builtin)
@@ -278,7 +287,7 @@ __host__ __device__ constexpr uint64_t ao_req_lut() {  // type -> requirement la
 }
 static_assert(T_RATION == 16 && T_POTION == 17, "requirement table: ration -> fishing, potion -> herbalism");
 __device__ __forceinline__ uint64_t ao_usable_ballot(const int16_t* T, int Sp, int ti, uint2 it, bool have) {
-  const int lane = lane_id();
+  const int lane = ao_lane();
   int lv = 0;
   if (lane < 8) {
     lv = T[(F_MELEE_LEVEL + 2 * lane) * Sp + ti];
@@ -309,7 +318,7 @@ __device__ __forceinline__ AoSections ao_sections(const ObsParams& p, const int1
   const bool exch = item && (p.systems & NMMO_SYS_EXCHANGE) != 0;
   const bool no_give = kWrap && (p.wflags & kWrapObsNoGive);
   const bool no_danger = kWrap && (p.wflags & kWrapObsNoDangerous);
-  const int lane = lane_id();
+  const int lane = ao_lane();
   AoSections x;
   // over the visible rows: 1 AttackTarget, 5 GiveTarget, 7 GoldTarget (+ noop k = kNObs)
   x.s1[0] = x.s1[1] = x.s5[0] = x.s5[1] = x.s7[0] = x.s7[1] = 0ull;

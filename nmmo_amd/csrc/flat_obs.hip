@@ -28,6 +28,18 @@ namespace nmmo {
 #define NMMO_FO_ABL 0  // 4 Inventory, 8 Market, 16 Tile, 32 compaction, 64 the agent loop (prologue only),
 #endif                 // 128 everything (an empty launch), 256 rows aliased onto 128 per XCD (stores L2-resident)
                        // (tools/debug/variants.py)
+#ifndef NMMO_FO_STAMPS  // diagnostic: s_memtime per section of every alive row (tools/debug/fo_stamps.py)
+#define NMMO_FO_STAMPS 0
+#endif
+#if NMMO_FO_STAMPS
+constexpr int kFoStamps = 12;  // loop top, compaction, sections, chunks 0-1, Buy-only chunks, tail chunks,
+                              // Entity, Inventory, Market, Task, Tile, state
+__device__ uint64_t fo_stamp_buf[1 << 17][kFoStamps];
+__device__ uint64_t fo_wave_buf[1 << 15][6];  // per wave: entry, staged, windows, loop start, loop end, env
+#define FO_STAMP(k) fst[k] = __builtin_amdgcn_s_memtime()
+#else
+#define FO_STAMP(k) (void)0
+#endif
 constexpr int kFoStagedListings = 256;  // listings whose item words are staged (Market rows)
 constexpr int kFoChunks = 25;           // 64-entry chunks over the 1,586 mask entries (+ id, tick)
 static_assert(kFoChunks * 64 >= kMaskN + 2 && (kFoChunks - 1) * 64 < kMaskN, "mask chunks");
@@ -104,7 +116,7 @@ __device__ __forceinline__ uint64_t fo_prev(const FoImg& g, int slot) {
 template <int kC>
 __device__ __forceinline__ void fo_put(float* row, FoImg& g, uint64_t m, float aid, float tick) {
   constexpr int sl = fo_slot(kC);
-  const int lane = lane_id();
+  const int lane = ao_lane();
   const bool same = g.ext && m == fo_prev(g, sl);
   if constexpr (kC == kFoChunks - 1) {  // + AgentId, CurrentTick right after the mask entries
     constexpr int n = kMaskN - 64 * kC;
@@ -194,6 +206,8 @@ __device__ __forceinline__ int fo_compact(const uint32_t (&pr)[kAoRows], int r, 
   return nvis;
 }
 
+typedef const __attribute__((address_space(4))) ObsParams* FoArgs;  // the kernel's argument segment
+
 // kS: the slot count when known at compile time (C3 / C4: 128 players + 256 NPCs), 0 = p.S. With
 // it the staged-column offsets are immediates instead of uniform values the agent loop keeps live.
 template <bool kWrap, int kS>
@@ -211,6 +225,10 @@ __global__ void __launch_bounds__(64 * kAoWaves) flat_obs_kernel(ObsParams p) {
   const int e = p.env_list ? p.env_list[el] : el, tid = threadIdx.x, lane = lane_id();
   if ((unsigned)e >= (unsigned)p.n_envs) return;  // a bad list id (the tick records it)
   if (NMMO_FO_ABL & 128) return;
+#if NMMO_FO_STAMPS
+  uint64_t wst_[6];
+  wst_[0] = __builtin_amdgcn_s_memtime();
+#endif
   const int w = __builtin_amdgcn_readfirstlane(wave_id());
   const int nm = min(max(p.mcount[e], 0), NMMO_MARKET_ROWS);
   for (int j = tid; j < nm; j += blockDim.x) {  // end-of-tick listings, ascending row
@@ -221,7 +239,13 @@ __global__ void __launch_bounds__(64 * kAoWaves) flat_obs_kernel(ObsParams p) {
     if (j < kFoStagedListings) mitem[j] = wd;
   }
   ao_stage(p, e, T, pk);  // (publishes mpo / mitem too)
+#if NMMO_FO_STAMPS
+  wst_[1] = __builtin_amdgcn_s_memtime();
+#endif
   ao_stage_windows(p, e, g, T, Sp, wst, ist);
+#if NMMO_FO_STAMPS
+  wst_[2] = __builtin_amdgcn_s_memtime();
+#endif
 
   uint32_t pr[kAoRows];  // this lane's datastore rows 1 + lane + 64 i
 #pragma unroll
@@ -283,11 +307,24 @@ __global__ void __launch_bounds__(64 * kAoWaves) flat_obs_kernel(ObsParams p) {
   const int iq = lane >> 4;                  // Inventory: item of the chunk
   const IcDesc icd = ic_desc(lane & 15);      // Inventory / Market: column lane % 16
 
+#if NMMO_FO_STAMPS
+  wst_[3] = __builtin_amdgcn_s_memtime();
+#endif
 #pragma unroll 1
   for (int j = 0; j < ((NMMO_FO_ABL & 64) ? 0 : kPerWave); j++) {
     const int a = abase + kAoWaves * j;
     if (a >= P) break;
-    float* row = p.obs + ((NMMO_FO_ABL & 256) ? (size_t)(((e * P + a) & 15) + 16 * (blockIdx.x & 7)) : (size_t)e * P + a) * elems;
+    const int lane = ao_lane();  // (per iteration: lane predicates are not hoisted and spilled)
+    // the kernel arguments the row's stores use, read from the argument segment per agent (scalar
+    // loads) instead of held in SGPRs across the loop, which spilled them
+    FoArgs kp = (FoArgs)__builtin_amdgcn_kernarg_segment_ptr();  // p is the only argument
+    asm volatile("" : "+s"(kp));
+    // the row pointer opaque per agent (its global address space kept), so the section bases are
+    // computed from it in the loop instead of hoisted out of it (and spilled)
+    auto grow = (__attribute__((address_space(1))) float*)(p.obs + ((NMMO_FO_ABL & 256)
+        ? (size_t)(((e * P + a) & 15) + 16 * (blockIdx.x & 7)) : (size_t)e * P + a) * elems);
+    asm volatile("" : "+s"(grow));
+    float* row = (float*)grow;
     const bool zv = (zvalid >> j) & 1;
     const int hj = __builtin_amdgcn_readlane(my_h, j);
     const int hv = hj & 4095, hm = hj >> 12;
@@ -303,13 +340,17 @@ __global__ void __launch_bounds__(64 * kAoWaves) flat_obs_kernel(ObsParams p) {
         nbytes += 4ull * elems;
       }
       if (lane == 0) {
-        p.zrow[(size_t)e * P + a] = p.ztag;
-        p.zst[(size_t)e * P + a] = kZsZero;
+        kp->zrow[(size_t)e * P + a] = kp->ztag;
+        kp->zst[(size_t)e * P + a] = kZsZero;
       }
       nrows++;
       continue;
     }
     nrows++;
+#if NMMO_FO_STAMPS
+    uint64_t fst[kFoStamps];
+#endif
+    FO_STAMP(0);
     const int la = a - g * kAoAgents;
     const int r = __builtin_amdgcn_readfirstlane(T[F_ROW * Sp + a]);
     const int c = __builtin_amdgcn_readfirstlane(T[F_COL * Sp + a]);
@@ -327,6 +368,7 @@ __global__ void __launch_bounds__(64 * kAoWaves) flat_obs_kernel(ObsParams p) {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
+    FO_STAMP(1);
     const bool ext = (zextv >> j) & 1;  // the row's extended state is valid
     FoImg fg{ext, img.x, img.y, 10 * j, 0, 0};
     // ActionTargets (+ AgentId, CurrentTick)
@@ -343,6 +385,7 @@ __global__ void __launch_bounds__(64 * kAoWaves) flat_obs_kernel(ObsParams p) {
       ag.prev_price = kWrap ? __builtin_amdgcn_readlane(my_prev, j) : -1;
       ag.mv = mv;
       const AoSections x = ao_sections<kWrap>(p, T, Sp, visw, ag, it);
+      FO_STAMP(2);
       fg.ext = ext;
       fo_put<0>(row, fg, fo_chunk<0>(x), 0.f, 0.f);
       // Buy.MarketItem entry k < listings: exchange on, price <= gold, not the agent's own. buy_word
@@ -362,6 +405,7 @@ __global__ void __launch_bounds__(64 * kAoWaves) flat_obs_kernel(ObsParams p) {
       const int clast = max(1, min((kFoBuyLo + nbuy - 1) >> 6, 16));
       uint64_t bprev = nm > 0 ? buy_word(0) : 0ull;  // chunk 1: Attack.Target's tail, Buy's first 24
       fo_put<1>(row, fg, fo_chunk<1>(x) | bprev << (kFoBuyLo & 63), 0.f, 0.f);
+      FO_STAMP(3);
 #pragma unroll 1
       for (int cc = 2; cc <= clast; cc++) {  // Buy-only chunks, not tracked
         const uint64_t bcur = 64 * (cc - 1) < nm ? buy_word(cc - 1) : 0ull;
@@ -369,10 +413,12 @@ __global__ void __launch_bounds__(64 * kAoWaves) flat_obs_kernel(ObsParams p) {
         bprev = bcur;
       }
       // chunk 17: Buy entries 984..1023 (word 15, only when nm > 960: the loop then ran to 16)
+      FO_STAMP(4);
       const uint64_t buy17 = nm > 15 * 64 ? bprev >> (64 - (kFoBuyLo & 63)) : 0ull;
       fo_tail_chunks<kFoTail0>(row, fg, x, buy17, (float)aid, tickf);
       nbytes += 4ull * (fg.nst + 64 * (clast - 1));
     }
+    FO_STAMP(5);
     // Entity rows: two per pass (lanes 0-30 row k, lanes 32-62 row k + 1: 62 contiguous floats),
     // the rows past the visible ones not known zero as one zero run
     const int nv2 = (nv + 1) & ~1;
@@ -388,6 +434,7 @@ __global__ void __launch_bounds__(64 * kAoWaves) flat_obs_kernel(ObsParams p) {
       wave_zero(row, kFoEntity + nv2 * NMMO_N_ENTITY_COLS, kFoEntity + hz * NMMO_N_ENTITY_COLS);
       nbytes += 4ull * (hz * NMMO_N_ENTITY_COLS + max(nm, hm) * 16);
     }
+    FO_STAMP(6);
     // Inventory: item q = 4 h + lane / 16, column lane % 16 (own items, owner = self); not stored
     // when the row was last written from the same 12 item words (its only inputs besides AgentId)
     const int jl = (12 * j + lane) & 63;
@@ -403,6 +450,7 @@ __global__ void __launch_bounds__(64 * kAoWaves) flat_obs_kernel(ObsParams p) {
       }
       nbytes += 4ull * kInv * 16;
     }
+    FO_STAMP(7);
     // Market (the env's listings, ascending row; owner = lister) and its zero run down to hm
     // (the listings past the staged ones in a loop of their own: a global load in the common loop
     // made every iteration wait for all of the row's stores -- vmcnt counts stores and retires in
@@ -412,19 +460,21 @@ __global__ void __launch_bounds__(64 * kAoWaves) flat_obs_kernel(ObsParams p) {
     if (nm > nms && !(NMMO_FO_ABL & 8)) {
       for (int k = nms * 16 + lane; k < nm * 16; k += 64) {
         const int q = k >> 4;
-        const int v = p.mlist[(size_t)e * NMMO_MARKET_ROWS + q];
-        const uint2 wd = p.items[((size_t)e * P + ((v >> 16) & 255)) * kInv + ((v >> 24) & 15)];
+        const int v = kp->mlist[(size_t)e * NMMO_MARKET_ROWS + q];
+        const uint2 wd = kp->items[((size_t)e * P + ((v >> 16) & 255)) * kInv + ((v >> 24) & 15)];
         row[kFoMarket + k] = ic_value(wd, (mpo[q] >> 8) + 1, icd);
       }
     }
     wave_zero(row, kFoMarket + nm * 16, kFoMarket + max(nm, hm) * 16);
+    FO_STAMP(8);
     // Task: only when the row does not hold this task's embedding yet (read in place)
     const int task = __builtin_amdgcn_readlane(my_task, j);
     if (!((ztask >> j) & 1)) {
-      const float* temb = p.task + (size_t)task * tdim;
+      const float* temb = kp->task + (size_t)task * tdim;
       for (int k = lane; k < tdim; k += 64) row[kFoTask + k] = temb[k];
       nbytes += 4ull * tdim;
     }
+    FO_STAMP(9);
     // Tile: (row, column, material) per window tile t = lane + 64 i, three stores 12 B apart; the
     // row (column) components are not stored when the row was last written at the same agent row
     // (column): a move changes one of the two, staying neither
@@ -442,22 +492,37 @@ __global__ void __launch_bounds__(64 * kAoWaves) flat_obs_kernel(ObsParams p) {
       }
       nbytes += 4ull * 225 * (1 + !same_r + !same_c);
     }
+    FO_STAMP(10);
     {  // the row's state: tag, zero thresholds and task, then the extended state
-      uint32_t* zx = reinterpret_cast<uint32_t*>(p.zext + ((size_t)e * P + a) * kZext);
+      uint32_t* zx = reinterpret_cast<uint32_t*>(kp->zext + ((size_t)e * P + a) * kZext);
       int wv = fg.nimg;  // lanes 0..19 the tracked masks, lanes 20 / 21 the position
       if (lane == 20) wv = r | c << 8;
       if (lane == 21) wv = 0;
       if (lane < 22) zx[lane] = (uint32_t)wv;
       if (!inv_same && lane < kInv) reinterpret_cast<uint2*>(zx + 22)[lane] = it;
       if (lane == 0) {
-        if (!zv) p.zrow[(size_t)e * P + a] = p.ztag;
-        p.zst[(size_t)e * P + a] = zs_pack(nv2, nm, task) | kZsExt;
+        if (!zv) kp->zrow[(size_t)e * P + a] = kp->ztag;
+        kp->zst[(size_t)e * P + a] = zs_pack(nv2, nm, task) | kZsExt;
       }
     }
+#if NMMO_FO_STAMPS
+    FO_STAMP(11);
+    if (lane == 0 && (size_t)e * P + a < (1u << 17))
+      for (int k = 0; k < kFoStamps; k++) fo_stamp_buf[(size_t)e * P + a][k] = fst[k];
+#endif
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the next agent reuses visw
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
+#if NMMO_FO_STAMPS
+  wst_[4] = __builtin_amdgcn_s_memtime();
+  wst_[5] = (uint64_t)e | (uint64_t)nrows << 32;
+  {
+    const size_t wi = ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * kAoWaves + w;
+    if (lane == 0 && wi < (1u << 15))
+      for (int k = 0; k < 6; k++) fo_wave_buf[wi][k] = wst_[k];
+  }
+#endif
   if (p.rows_out && lane == 0 && nrows) {  // per env: one address per env keeps the atomics uncontended
     atomicAdd(&p.rows_out[2 * e], (unsigned long long)nrows);
     atomicAdd(&p.rows_out[2 * e + 1], nbytes);
@@ -488,3 +553,23 @@ hipError_t launch_flat_obs(const ObsParams& p, hipStream_t stream) {
 }
 
 }  // namespace nmmo
+
+#if NMMO_FO_STAMPS
+// diagnostic export of the stamp variant only: copy the stamps out, then zero them
+extern "C" __attribute__((visibility("default"))) int nmmo_debug_fo_stamps(void* host, size_t bytes) {
+  if (bytes > sizeof(nmmo::fo_stamp_buf)) bytes = sizeof(nmmo::fo_stamp_buf);
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(nmmo::fo_stamp_buf), bytes) != hipSuccess) return -1;
+  void* d = nullptr;
+  if (hipGetSymbolAddress(&d, HIP_SYMBOL(nmmo::fo_stamp_buf)) != hipSuccess) return -1;
+  return hipMemset(d, 0, sizeof(nmmo::fo_stamp_buf)) == hipSuccess && hipDeviceSynchronize() == hipSuccess ? 0 : -1;
+}
+extern "C" __attribute__((visibility("default"))) int nmmo_debug_fo_wave_stamps(void* host, size_t bytes) {
+  if (bytes > sizeof(nmmo::fo_wave_buf)) bytes = sizeof(nmmo::fo_wave_buf);
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(nmmo::fo_wave_buf), bytes) != hipSuccess) return -1;
+  void* d = nullptr;
+  if (hipGetSymbolAddress(&d, HIP_SYMBOL(nmmo::fo_wave_buf)) != hipSuccess) return -1;
+  return hipMemset(d, 0, sizeof(nmmo::fo_wave_buf)) == hipSuccess && hipDeviceSynchronize() == hipSuccess ? 0 : -1;
+}
+#endif

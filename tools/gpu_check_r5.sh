@@ -47,6 +47,9 @@ pmcflat2)  # the flat obs kernel's SQ counters only (passes 1-3)
   timeout -k 10 180 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SMEM SQ_BUSY_CYCLES SQ_INSTS_BRANCH --output-format csv -d gpurun_out/pmf/p2 -o run -- $B > gpurun_out/pmf/p2.log 2>&1 && \
   timeout -k 10 180 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC SQ_INST_LEVEL_LDS SQ_LDS_BANK_CONFLICT --output-format csv -d gpurun_out/pmf/p3 -o run -- $B > gpurun_out/pmf/p3.log 2>&1
   ;;
+fost)  # per-section stamps of the flat obs kernel (the NMMO_FO_STAMPS variant)
+  NMMO_LIB=nmmo_amd/lib/libnmmo_hip_fost.so NMMO_ALLOW_STALE=1 timeout -k 10 300 python tools/debug/fo_stamps.py > gpurun_out/fo_stamps.txt 2>&1
+  ;;
 fix1)  # flat obs fixes (Market loop vmcnt, wrapper scratch) vs HEAD, parity first; then the C5 kernel stats
   export TMPDIR=/tmp
   timeout -k 10 600 $PYT tests/test_gpu_parity.py tests/test_gpu_wrapper.py tests/test_gpu_native_obs.py tests/test_gpu_wire.py tests/test_gpu_zero_rows.py > gpurun_out/gpu_fix1.log 2>&1 && \
