@@ -437,6 +437,16 @@ NMMO_API int nmmo_wire_check(const void* wire, int32_t n_envs, int32_t player_n,
 NMMO_API int nmmo_wire_check_many(const void* const* wires, const int32_t* n_envs,
                                   const int64_t* const* dev_expect_totals, int32_t n_bufs,
                                   int32_t player_n, int32_t* dev_status, void* stream);
+/* The per-agent step records the learner gather ships beside each wire buffer: with dev_records
+ * set (device, n_envs x player_n x 8 B; NULL = off), every nmmo_step that writes NMMO_OBS_WIRE obs
+ * also writes, per agent, its reward (f32) | terminated | truncated | mask | 0 -- the step's rew /
+ * term / trunc / mask outputs in one 8-B record, from the wire gather's own launch (instead of four
+ * strided copies after it). dev_fault (device int32, or NULL): the same launch also does what
+ * nmmo_fault_into(h, dev_fault) would after the step (a nonzero tick fault word is stored there
+ * unless it already holds one). The pointers are read when each step is enqueued (a captured
+ * step keeps the ones it saw). Replaces the caller-side packing of pufferlib's per-agent rewards /
+ * dones / masks (clean_pufferl.py:305-318 consumes them per step). */
+NMMO_API int nmmo_set_step_records(NmmoHandle* h, uint8_t* dev_records, int32_t* dev_fault);
 /* Decodes a wire buffer of n_envs x player_n agents into the native layout (every byte of the
  * n_envs x (player_n x NMMO_NATIVE_ROW_BYTES + NMMO_NATIVE_MARKET_BYTES) buffer is written;
  * bit-identical to what the sender's nmmo_step wrote). Enqueued; needs no handle. */

@@ -28,7 +28,7 @@ SYMBOLS = [
     "nmmo_wire_pack", "nmmo_wire_unpack", "nmmo_wire_check", "nmmo_dev_alloc", "nmmo_dev_free", "nmmo_observe",
     "nmmo_step_envs", "nmmo_inject_fault", "nmmo_fault_into", "nmmo_exp_store_records",
     "nmmo_exp_gather_records", "nmmo_exp_store_records_many", "nmmo_obs_invalidate", "nmmo_set_obs_counter",
-    "nmmo_obs_bind", "nmmo_obs_invalidate_envs", "nmmo_exp_scratch_ints_many",
+    "nmmo_obs_bind", "nmmo_obs_invalidate_envs", "nmmo_exp_scratch_ints_many", "nmmo_set_step_records",
     "nmmo_wire_check_many",
 ]
 
@@ -99,6 +99,7 @@ def declare(L):
     L.nmmo_obs_bind.argtypes = [vp, vp]
     L.nmmo_obs_invalidate_envs.argtypes = [vp, vp, i32, vp]
     L.nmmo_set_obs_counter.argtypes = [vp, vp]
+    L.nmmo_set_step_records.argtypes = [vp, vp, vp]
     xp = ctypes.POINTER(abi.NmmoExperience)
     L.nmmo_exp_scratch_ints.argtypes = [i32, i32]
     L.nmmo_exp_scratch_ints.restype = ctypes.c_int64

@@ -72,6 +72,8 @@ struct NmmoHandle {
   const void* zbuf = nullptr;  // the bound obs buffer (nmmo_obs_bind) and its tag
   uint64_t ztag = 0;
   unsigned long long* d_rows_out = nullptr;  // nmmo_set_obs_counter
+  uint8_t* d_recs = nullptr;                 // nmmo_set_step_records
+  int32_t* d_recs_fault = nullptr;
   // the native buffer the last obs gather wrote, and whether no tick ran since (nmmo_wire_pack)
   const void* last_native = nullptr;
   bool native_fresh = false;
@@ -326,6 +328,10 @@ static ObsParams obs_params(NmmoHandle* h, void* obs) {
   p.zext = h->d_zext;
   p.ztag = h->d_zrow && h->zskip && obs && obs == h->zbuf ? h->ztag : 0;
   p.rows_out = h->d_rows_out;
+  p.recs = nullptr;  // (a step's outputs: step_impl sets them)
+  p.fault_dst = nullptr;
+  p.rew = nullptr;
+  p.term = p.trunc = p.mask = nullptr;
   p.ws = h->wrap_on ? h->d_ws : nullptr;
   p.wflags = 0;
   if (h->wrap_on) {
@@ -411,6 +417,14 @@ static int step_impl(NmmoHandle* h, const int32_t* env_ids, int32_t n_ids, const
     ObsParams op = obs_params(h, obs);
     op.env_list = env_ids;
     op.n_list = n_ids;
+    if (op.wire && h->d_recs) {
+      op.recs = h->d_recs;
+      op.fault_dst = h->d_recs_fault;
+      op.rew = rew;
+      op.term = term;
+      op.trunc = trunc;
+      op.mask = mask;
+    }
     HIP_TRY(launch_obs(op, s));
   }
   if (do_obs) h->last_native = obs;  // kept across a tick without obs: the pack check then says stale
@@ -569,6 +583,16 @@ int nmmo_dev_free(void* ptr) {
   for (auto c : a.chunks) HIP_TRY(hipMemRelease(c));
   const char* fr = getenv("NMMO_DEVMEM_FREE_VA");
   if (fr && fr[0] == '1') HIP_TRY(hipMemAddressFree(ptr, a.bytes));
+  return NMMO_OK;
+}
+
+int nmmo_set_step_records(NmmoHandle* h, uint8_t* dev_records, int32_t* dev_fault) {
+  if (!h) return fail(NMMO_E_INVALID, "null handle");
+  if (dev_records && h->cfg.obs_layout != NMMO_OBS_WIRE)
+    return fail(NMMO_E_INVALID, "nmmo_set_step_records: step records come with the wire obs layout");
+  if (dev_fault && !dev_records) return fail(NMMO_E_INVALID, "nmmo_set_step_records: dev_fault without records");
+  h->d_recs = dev_records;
+  h->d_recs_fault = dev_fault;
   return NMMO_OK;
 }
 

@@ -105,6 +105,14 @@ struct ObsParams {
   // the 10 tracked ActionTargets chunks, the position (row | col << 8) the Tile section was written
   // for, and the 12 item words the Inventory section was written from
   uint64_t* zext;
+  // wire layout only (nmmo_set_step_records): per agent 8 B reward | term | trunc | mask | 0,
+  // written by wire_count_kernel from the step's outputs (NULL = off)
+  uint8_t* recs;
+  int32_t* fault_dst;  // with recs: *fault's nonzero word CAS-ed into it (nmmo_fault_into's effect)
+  const float* rew;
+  const uint8_t* term;
+  const uint8_t* trunc;
+  const uint8_t* mask;
   unsigned long long* rows_out;  // optional [n][2]: += rows this launch wrote, bytes it stored, per env
 };
 constexpr uint64_t kZsZero = 1ull << 20;

@@ -174,6 +174,16 @@ __global__ void __launch_bounds__(256) wire_count_kernel(ObsParams p) {
     v.ecount[e] = (uint16_t)ne;
     v.env_off[e] = wire_table_bytes(ne) + bytes + 32 * nm;
   }
+  if (p.fault_dst && e == 0 && tid == 0) {  // nmmo_fault_into's effect (the tick ran before this launch)
+    const int32_t fw = *p.fault;
+    if (fw) atomicCAS(p.fault_dst, 0, fw);
+  }
+  if (p.recs && tid < p.P) {  // the step record (nmmo_set_step_records): reward | term | trunc | mask | 0
+    const size_t ai = (size_t)e * p.P + tid;
+    const uint2 rec = make_uint2(__float_as_uint(p.rew[ai]),
+                                 (uint32_t)p.term[ai] | (uint32_t)p.trunc[ai] << 8 | (uint32_t)p.mask[ai] << 16);
+    reinterpret_cast<uint2*>(p.recs)[ai] = rec;
+  }
 }
 
 // exclusive scan of the per-env payload bytes (one workgroup): env_off[e] becomes the offset of

@@ -341,14 +341,10 @@ class WireGather:
     def _body(self, j: int, k: int):
         e = self.engines[j]
         e.obs = self.wires[j][k]
+        # reward | term | trunc | mask | 0 per agent and the tick fault word, by the step's wire gather
+        e.set_step_records(self.smalls[j][k], self.faults[k])
         e.scripted_actions(self.pseed)
         e.step()
-        e.fault_into(self.faults[k])
-        sm = self.smalls[j][k]
-        sm[..., 0:4] = e.rew.view(torch.uint8).view(e.n_envs, self.P, 4)
-        sm[..., 4] = e.term
-        sm[..., 5] = e.trunc
-        sm[..., 6] = e.mask
 
     def _capture(self):
         torch.cuda.synchronize(self.device)

@@ -256,6 +256,22 @@ class NmmoEngine:
         check(lib().nmmo_set_obs_counter(self.h, None if counter is None else ctypes.c_void_p(counter.data_ptr())),
               "nmmo_set_obs_counter")
 
+    def set_step_records(self, records, fault=None):
+        """uint8 [n_envs, P, 8] device tensor (or None = off) every following step() with wire obs
+        fills, per agent, with reward f32 | term | trunc | mask | 0 (nmmo_set_step_records); read
+        when a step is enqueued, so a captured step keeps the tensor it saw. fault: a device int32
+        tensor the same launch stores a nonzero tick fault word into (fault_into()'s effect)."""
+        if records is not None and (records.dtype != torch.uint8 or records.device != self.device
+                                    or not records.is_contiguous() or records.numel() < 8 * self.n_envs * self.P):
+            raise ValueError("records must be a contiguous uint8 tensor of >= 8 * n_envs * P bytes on the "
+                             "engine's device")
+        if fault is not None and (fault.dtype != torch.int32 or fault.device != self.device):
+            raise ValueError("fault must be an int32 tensor on the engine's device")
+        self._step_records = (records, fault)
+        check(lib().nmmo_set_step_records(self.h, None if records is None else ctypes.c_void_p(records.data_ptr()),
+                                          None if fault is None else ctypes.c_void_p(fault.data_ptr())),
+              "nmmo_set_step_records")
+
     def obs_invalidate(self):
         """Forget what the obs rows hold (nmmo_obs_invalidate): call after writing into self.obs;
         the next gather writes every row in full."""

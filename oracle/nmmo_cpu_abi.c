@@ -352,6 +352,10 @@ NMMO_API int nmmo_set_obs_counter(NmmoHandle* h, uint64_t* c) {
   (void)h; (void)c;
   UNSUPPORTED("nmmo_set_obs_counter");
 }
+NMMO_API int nmmo_set_step_records(NmmoHandle* h, uint8_t* r, int32_t* f) {
+  (void)h; (void)r; (void)f;
+  UNSUPPORTED("nmmo_set_step_records");
+}
 NMMO_API int nmmo_set_counters(NmmoHandle* h, uint64_t* c) {
   (void)h; (void)c;
   UNSUPPORTED("nmmo_set_counters");

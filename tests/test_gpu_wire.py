@@ -114,6 +114,48 @@ def test_wire_layout_equals_pack_of_native(wrapper):
         e.close()
 
 
+def test_step_records_equal_step_outputs():
+    """nmmo_set_step_records: every wire-obs step writes, per agent, reward f32 | term | trunc |
+    mask | 0 -- the bytes of the step's own outputs (over deaths and an episode end); a step
+    after records are switched off leaves the buffer alone; the native layout refuses them."""
+    from nmmo_amd._native import NativeError
+
+    nat, wir = _pair(4, seed=41)
+    with pytest.raises(NativeError):
+        nat.set_step_records(torch.zeros((4, nat.P, 8), dtype=torch.uint8, device=nat.device))
+    wir.reset()
+    rec = torch.full((4, wir.P, 8), 0xAB, dtype=torch.uint8, device=wir.device)
+    wir.set_step_records(rec)
+    ended = 0
+    for t in range(40):
+        if t == 13:
+            wir.end_episodes(np.array([0, 1, 0, 0], bool))
+        wir.scripted_actions(300 + t)
+        wir.step()
+        want = torch.cat([wir.rew.view(torch.uint8).view(4, wir.P, 4), wir.term[..., None], wir.trunc[..., None],
+                          wir.mask[..., None], torch.zeros_like(wir.mask[..., None])], -1)
+        assert torch.equal(rec, want), f"step records differ from the step outputs at tick {t}"
+        ended += int(wir.trunc.sum()) + int(wir.term.sum())
+    assert ended > 0  # dones were among the records
+    fault = torch.zeros(1, dtype=torch.int32, device=wir.device)
+    wir.set_step_records(rec, fault)
+    wir.scripted_actions(500)
+    wir.step()
+    assert int(fault.item()) == 0
+    wir.inject_fault(4)  # the tick's fault word, as a loop bound would set it
+    wir.scripted_actions(501)
+    wir.step()
+    assert int(fault.item()) == 4  # what fault_into() would have stored
+    wir.inject_fault(0)
+    wir.set_step_records(None)
+    before = rec.clone()
+    wir.scripted_actions(999)
+    wir.step()
+    assert torch.equal(rec, before)
+    for e in (nat, wir):
+        e.close()
+
+
 def test_wire_layout_fullsize_roundtrip_and_check():
     """1,024 envs with staggered episodes: the wire layout decodes to the native obs of the same
     state, passes nmmo_wire_check, and a corrupted count word / total is flagged."""
