@@ -92,6 +92,11 @@ __device__ __forceinline__ uint64_t fo_chunk(const AoSections& x) {
          fo_sec<10, kC>(x.s10[0], x.s10[1]) | fo_sec<11, kC>(x.s11, 0ull);
 }
 __device__ __forceinline__ float fo_bit(uint64_t m) { return __builtin_amdgcn_inverse_ballot_w64(m) ? 1.f : 0.f; }
+// row[idx] = v as base + zero-extended 32-bit byte offset: the store's SGPR-base (saddr) form, one
+// offset VGPR, instead of a sign-extended 64-bit address built per store (4 VALU each)
+__device__ __forceinline__ void fo_st(float* row, uint32_t idx, float v) {
+  *reinterpret_cast<float*>(reinterpret_cast<char*>(row) + (idx << 2)) = v;
+}
 
 // The row's tracked ActionTargets chunks (ObsParams::zext): chunks 0 and 1 (Style, Attack.Target,
 // Buy's first 24 entries) and 17..24 (Buy's last 40 entries and no-op, then every other section,
@@ -121,14 +126,14 @@ __device__ __forceinline__ void fo_put(float* row, FoImg& g, uint64_t m, float a
   if constexpr (kC == kFoChunks - 1) {  // + AgentId, CurrentTick right after the mask entries
     constexpr int n = kMaskN - 64 * kC;
     if (!same) {
-      if (lane < n + 2) row[64 * kC + lane] = lane < n ? fo_bit(m) : lane == n ? aid : tick;
+      if (lane < n + 2) fo_st(row, 64 * kC + lane, lane < n ? fo_bit(m) : lane == n ? aid : tick);
       g.nst += n + 2;
     } else {
-      if (lane == n + 1) row[64 * kC + lane] = tick;  // the tick changes every step
+      if (lane == n + 1) fo_st(row, 64 * kC + lane, tick);  // the tick changes every step
       g.nst += 1;
     }
   } else if (!same) {
-    row[64 * kC + lane] = fo_bit(m);
+    fo_st(row, 64 * kC + lane, fo_bit(m));
     g.nst += 64;
   }
   g.nimg = writelane<2 * sl>((int)(uint32_t)m, g.nimg);
@@ -409,7 +414,7 @@ __global__ void __launch_bounds__(64 * kAoWaves) flat_obs_kernel(ObsParams p) {
 #pragma unroll 1
       for (int cc = 2; cc <= clast; cc++) {  // Buy-only chunks, not tracked
         const uint64_t bcur = 64 * (cc - 1) < nm ? buy_word(cc - 1) : 0ull;
-        row[64 * cc + lane] = fo_bit(bcur << (kFoBuyLo & 63) | bprev >> (64 - (kFoBuyLo & 63)));
+        fo_st(row, 64 * cc + lane, fo_bit(bcur << (kFoBuyLo & 63) | bprev >> (64 - (kFoBuyLo & 63))));
         bprev = bcur;
       }
       // chunk 17: Buy entries 984..1023 (word 15, only when nm > 960: the loop then ran to 16)
@@ -423,12 +428,12 @@ __global__ void __launch_bounds__(64 * kAoWaves) flat_obs_kernel(ObsParams p) {
     // the rows past the visible ones not known zero as one zero run
     const int nv2 = (nv + 1) & ~1;
     if (!(NMMO_FO_ABL & 2)) {
-      float* de = row + kFoEntity + (lane - eh);
+      const uint32_t de = kFoEntity + (lane - eh);
 #pragma unroll 1
       for (int k0 = 0; k0 < nv2; k0 += 2) {
         const int k = k0 + eh;
         if (ef < NMMO_N_ENTITY_COLS)
-          de[k0 * NMMO_N_ENTITY_COLS] = k < nv ? (float)T[ef * Sp + ao_slot(visw[k])] : 0.f;
+          fo_st(row, de + k0 * NMMO_N_ENTITY_COLS, k < nv ? (float)T[ef * Sp + ao_slot(visw[k])] : 0.f);
       }
       const int hz = max(nv2, hv);
       wave_zero(row, kFoEntity + nv2 * NMMO_N_ENTITY_COLS, kFoEntity + hz * NMMO_N_ENTITY_COLS);
@@ -446,7 +451,7 @@ __global__ void __launch_bounds__(64 * kAoWaves) flat_obs_kernel(ObsParams p) {
         const int q = 4 * h + iq;
         float v = 0.f;
         if (4 * h < ninv && q < ninv) v = ic_value(ist[la * kInv + q], aid, icd);  // (a uniform skip first)
-        row[kFoInv + 64 * h + lane] = v;
+        fo_st(row, kFoInv + 64 * h + lane, v);
       }
       nbytes += 4ull * kInv * 16;
     }
@@ -456,13 +461,13 @@ __global__ void __launch_bounds__(64 * kAoWaves) flat_obs_kernel(ObsParams p) {
     // made every iteration wait for all of the row's stores -- vmcnt counts stores and retires in
     // order -- whether or not it took the load)
     const int nms = (NMMO_FO_ABL & 8) ? 0 : min(nm, kFoStagedListings);
-    for (int k = lane; k < nms * 16; k += 64) row[kFoMarket + k] = ic_value(mitem[k >> 4], (mpo[k >> 4] >> 8) + 1, icd);
+    for (int k = lane; k < nms * 16; k += 64) fo_st(row, kFoMarket + k, ic_value(mitem[k >> 4], (mpo[k >> 4] >> 8) + 1, icd));
     if (nm > nms && !(NMMO_FO_ABL & 8)) {
       for (int k = nms * 16 + lane; k < nm * 16; k += 64) {
         const int q = k >> 4;
         const int v = kp->mlist[(size_t)e * NMMO_MARKET_ROWS + q];
         const uint2 wd = kp->items[((size_t)e * P + ((v >> 16) & 255)) * kInv + ((v >> 24) & 15)];
-        row[kFoMarket + k] = ic_value(wd, (mpo[q] >> 8) + 1, icd);
+        fo_st(row, kFoMarket + k, ic_value(wd, (mpo[q] >> 8) + 1, icd));
       }
     }
     wave_zero(row, kFoMarket + nm * 16, kFoMarket + max(nm, hm) * 16);
@@ -471,7 +476,7 @@ __global__ void __launch_bounds__(64 * kAoWaves) flat_obs_kernel(ObsParams p) {
     const int task = __builtin_amdgcn_readlane(my_task, j);
     if (!((ztask >> j) & 1)) {
       const float* temb = kp->task + (size_t)task * tdim;
-      for (int k = lane; k < tdim; k += 64) row[kFoTask + k] = temb[k];
+      for (int k = lane; k < tdim; k += 64) fo_st(row, kFoTask + k, temb[k]);
       nbytes += 4ull * tdim;
     }
     FO_STAMP(9);
