@@ -522,7 +522,9 @@ def measure(args, name, layout_name, envs, rank, world, dev, steps, warmup, dist
     obs_b = obs_bytes_per_env(S, P, eng.obs_elems, native, stored=bytes_stored / (envs * steps),
                               alive_frac=alive / (envs * P * steps)) * per if wl["obs"] else 0
     if wl["obs"] and obs_avg_ms > tick_avg_ms:
-        kern, byts, ms = "native_obs_kernel" if native else "obs_kernel", obs_b, obs_avg_ms
+        # incremental flat rows: flat_obs_kernel; every row in full (rezero): obs_kernel
+        kern = "native_obs_kernel" if native else "obs_kernel" if rezero else "flat_obs_kernel"
+        byts, ms = obs_b, obs_avg_ms
         timing = f"HIP events around each {kern} launch on the launch stream"
     else:
         kern, byts, ms = "tick_kernel", tick_b, tick_avg_ms
