@@ -67,7 +67,12 @@ __global__ void __launch_bounds__(128) wire_size_kernel(const uint16_t* counts, 
 // every datastore row (agent_obs.h ao_pack, with the spawn-immune / dangerous / player bits) into
 // p.wpk[e], so the record kernel's workgroups load 2 KB of row words instead of staging the env's
 // 24 KB of Entity columns each.
-__global__ void __launch_bounds__(256) wire_count_kernel(ObsParams p) {
+#ifndef NMMO_COUNT_THREADS  // (A/B knob: tools/debug/variants.py)
+#define NMMO_COUNT_THREADS 512
+#endif
+constexpr int kCountThreads = NMMO_COUNT_THREADS;  // a workgroup per env; its agents split over the waves
+constexpr int kCountU = (kMaxSlots + kCountThreads - 1) / kCountThreads;  // slots per thread
+__global__ void __launch_bounds__(kCountThreads) wire_count_kernel(ObsParams p) {
   __shared__ uint32_t pk[kMaxSlots];         // datastore row - 1 -> ao_pack word (agent_obs.h)
   __shared__ uint32_t pos[kMaxSlots];        // slot -> row << 16 | col (agents' windows)
   __shared__ uint32_t tab[kMaxSlots / 32];   // slots some record shows
@@ -77,15 +82,15 @@ __global__ void __launch_bounds__(256) wire_count_kernel(ObsParams p) {
   __shared__ int wsum[16];
   __shared__ int bytes;
   constexpr uint32_t kOut = 0xFFFFFFFFu;
-  static_assert(kMaxSlots % 64 == 0 && kMaxSlots <= 512, "rows per lane; two slots per thread");
+  static_assert(kMaxSlots % 64 == 0 && kMaxSlots <= 512 && kIdWords % kCountThreads == 0, "rows per lane; idset");
   WireView v = wire_view(p.wire, p.n_envs, p.P);
   const int e = blockIdx.x, tid = threadIdx.x, lane = lane_id(), S = p.S;
   const int w = __builtin_amdgcn_readfirstlane(wave_id()), nw = blockDim.x >> 6;
   const int16_t* E = p.ent + (size_t)e * NMMO_NF * S;
-  int al[2], ds[2], r_[2], c_[2], id_[2], ta_[2], nt_[2];  // slots tid and tid + 256, loaded ahead of the barrier
-#pragma unroll
-  for (int u = 0; u < 2; u++) {
-    const int s = tid + 256 * u;
+  int al[kCountU], ds[kCountU], r_[kCountU], c_[kCountU], id_[kCountU], ta_[kCountU], nt_[kCountU];  // slots tid +
+#pragma unroll  // kCountThreads u, loaded ahead of the barrier
+  for (int u = 0; u < kCountU; u++) {
+    const int s = tid + kCountThreads * u;
     al[u] = s < S ? E[F_ALIVE * S + s] : 0;
     ds[u] = s < S ? E[F_DS_ROW * S + s] : 0;
     r_[u] = s < S ? E[F_ROW * S + s] : 0;
@@ -110,8 +115,8 @@ __global__ void __launch_bounds__(256) wire_count_kernel(ObsParams p) {
   if (tid == 0) bytes = 0;
   __syncthreads();
 #pragma unroll
-  for (int u = 0; u < 2; u++) {
-    const int s = tid + 256 * u;
+  for (int u = 0; u < kCountU; u++) {
+    const int s = tid + kCountThreads * u;
     if (s >= kMaxSlots) continue;
     const bool in = s < S && al[u];
     pos[s] = in ? ((uint32_t)(uint16_t)r_[u] << 16) | (uint32_t)(uint16_t)c_[u] : kOut;
@@ -154,18 +159,18 @@ __global__ void __launch_bounds__(256) wire_count_kernel(ObsParams p) {
   }
   if (lane == 0) atomicAdd(&bytes, mine);
   __syncthreads();
-  bool shown[2];
+  bool shown[kCountU];
 #pragma unroll
-  for (int u = 0; u < 2; u++) {
-    const int s = tid + 256 * u;
+  for (int u = 0; u < kCountU; u++) {
+    const int s = tid + kCountThreads * u;
     shown[u] = s < S && ((tab[s >> 5] >> (s & 31)) & 1u);
     if (shown[u]) idset_add(ids, id_[u]);
   }
   const int ne = idset_prefix(ids, pre, wsum);  // (barriers inside)
   uint16_t* rk = p.wrank + (size_t)e * kMaxSlots;
 #pragma unroll
-  for (int u = 0; u < 2; u++) {
-    const int s = tid + 256 * u;
+  for (int u = 0; u < kCountU; u++) {
+    const int s = tid + kCountThreads * u;
     if (s < kMaxSlots) rk[s] = shown[u] ? (uint16_t)idrank(ids, pre, id_[u]) : (uint16_t)0xFFFF;
   }
   if (tid == 0) {
@@ -663,7 +668,7 @@ hipError_t launch_wire_pack(const uint16_t* counts, const int* mcount, const uin
 
 hipError_t launch_wire_header(const ObsParams& p, hipStream_t s) {
   if (p.P > 128 || p.n_envs <= 0 || p.S > kMaxSlots || !p.wire) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(wire_count_kernel, dim3(p.n_envs), dim3(256), 0, s, p);
+  hipLaunchKernelGGL(wire_count_kernel, dim3(p.n_envs), dim3(kCountThreads), 0, s, p);
   hipLaunchKernelGGL(wire_scan_kernel, dim3(1), dim3(1024), 0, s, p.wire, p.n_envs, p.P);
   return hipGetLastError();
 }
