@@ -2426,8 +2426,13 @@ tick_kernel_w8(DevState st, const int32_t* __restrict__ actions, const uint64_t*
 hipError_t launch_tick(const DevState& st, const int32_t* actions, const uint64_t* env_seeds,
                        float* rew, uint8_t* term, uint8_t* trunc, uint8_t* mask, int mode,
                        hipStream_t stream) {
-  // >= 4 waves so the block-wide loops (state copies, respawn draws) use all four SIMDs
-  const int threads = max(((st.S + 63) / 64) * 64, 256);
+  // >= 8 waves: the block-wide loops (state copies, respawn draws, the wave-split phases) get two
+  // waves per SIMD; slot phases leave threads >= S idle (same box: C2 tick 15.3 -> 14.9 us, C3
+  // 34.9 -> 34.3, C4 58.9 -> 58.1 against >= 4 waves)
+#ifndef NMMO_TICK_MIN_THREADS  // (A/B knob: tools/debug/variants.py; at most 8 waves: wtot)
+#define NMMO_TICK_MIN_THREADS 512
+#endif
+  const int threads = max(((st.S + 63) / 64) * 64, NMMO_TICK_MIN_THREADS);
   const size_t lds = tick_lds_bytes(st.S, st.P, (st.cfg.systems & NMMO_SYS_ITEM) != 0, st.tev != 0,
                                     uses_grid(st.cfg.systems), slim_systems(st.cfg.systems));
   void (*k)(DevState, const int32_t*, const uint64_t*, float*, uint8_t*, uint8_t*, uint8_t*, int);
