@@ -18,7 +18,11 @@
 
 namespace nmmo {
 
-constexpr int kWrapThreads = 128;
+#ifndef NMMO_WRAP_THREADS  // (A/B knob: tools/debug/variants.py; >= 128 = the player cap)
+#define NMMO_WRAP_THREADS 256  // (same box: wrapper 16.4 -> 16.0 us per 512 envs against 128)
+#endif
+constexpr int kWrapThreads = NMMO_WRAP_THREADS;
+static_assert(kWrapThreads >= 128 && kWrapThreads % 64 == 0, "thread a owns agent a");
 
 // event code -> dense index 0..16 (SPEC §11 code list), -1 otherwise
 __host__ __device__ inline int ev_index(int code) {
