@@ -2415,8 +2415,11 @@ __global__ void tick_kernel(DevState st, const int32_t* __restrict__ actions,
 }
 // The C3 specialisation at <= 64 VGPRs: a 6-wave workgroup puts 2 waves on two SIMDs, so 4
 // workgroups per CU (the 1,024 envs of C3 in one round on 256 CUs) need 8 wave slots there.
+#ifndef NMMO_TICK_C3_WPE  // (A/B knob: tools/debug/variants.py)
+#define NMMO_TICK_C3_WPE 8
+#endif
 template <uint32_t kSys, int kS = 0, int kP = 0>
-__global__ void __attribute__((amdgpu_waves_per_eu(8, 8)))
+__global__ void __attribute__((amdgpu_waves_per_eu(NMMO_TICK_C3_WPE, NMMO_TICK_C3_WPE)))
 tick_kernel_w8(DevState st, const int32_t* __restrict__ actions, const uint64_t* __restrict__ env_seeds,
                float* rew, uint8_t* term, uint8_t* trunc, uint8_t* mask, int mode) {
   tick_body<kSys, kS, kP>(st, actions, env_seeds, rew, term, trunc, mask, mode);
