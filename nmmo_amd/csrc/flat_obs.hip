@@ -475,8 +475,18 @@ __global__ void __launch_bounds__(64 * kAoWaves) flat_obs_kernel(ObsParams p) {
     // Task: only when the row does not hold this task's embedding yet (read in place)
     const int task = __builtin_amdgcn_readlane(my_task, j);
     if (!((ztask >> j) & 1)) {
+      // 8 loads in flight before their stores: each load waits for every store issued before it
+      // (vmcnt retires in order), so a load-store loop drained the queue once per 64 floats
       const float* temb = kp->task + (size_t)task * tdim;
-      for (int k = lane; k < tdim; k += 64) fo_st(row, kFoTask + k, temb[k]);
+      int k0 = 0;
+      for (; k0 + 8 * 64 <= tdim; k0 += 8 * 64) {
+        float t[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++) t[i] = temb[k0 + 64 * i + lane];
+#pragma unroll
+        for (int i = 0; i < 8; i++) fo_st(row, kFoTask + k0 + 64 * i + lane, t[i]);
+      }
+      for (int k = k0 + lane; k < tdim; k += 64) fo_st(row, kFoTask + k, temb[k]);
       nbytes += 4ull * tdim;
     }
     FO_STAMP(9);
