@@ -1089,6 +1089,40 @@ __device__ __forceinline__ void loot(Ctx& c, int x, int t, int& evn) {
 __device__ __forceinline__ double per_d(int num, int den) { return (double)num / (double)(den > 0 ? den : 1); }
 __device__ __forceinline__ double clip01(double x) { return x < 0.0 ? 0.0 : x > 1.0 ? 1.0 : x; }
 
+// Is material `m` on any tile of the 15x15 window around (r, col) (this tick's materials, in
+// HBM)? The window rows are loaded as aligned dwords, 5 rows (25 loads) before their tests: a
+// byte-by-byte early-exit scan waited, per byte, for every store the tick had queued before it
+// (vmcnt counts stores too and retires in order). Bytes 0..14 of a row come out of its 5 dwords
+// by v_alignbyte; a zero byte of row ^ (m x 4) is a match.
+__device__ __forceinline__ bool can_see_tile(const Ctx& c, int r, int col, int m) {
+  if ((unsigned)m > 255u) return false;  // no tile byte holds it
+  const uint32_t* m32 = reinterpret_cast<const uint32_t*>(c.mat);
+  const uint32_t rep = (uint32_t)(m & 255) * 0x01010101u;
+  auto zero_byte = [](uint32_t x) { return ((x - 0x01010101u) & ~x & 0x80808080u) != 0u; };
+  bool hit = false;
+  for (int r0 = 0; r0 < 15; r0 += 5) {
+    uint32_t w[5][5];
+    int off[5];
+#pragma unroll
+    for (int i = 0; i < 5; i++) {
+      const int b = (r - kVision + r0 + i) * kSize + col - kVision;  // the row's first window byte
+      off[i] = b & 3;
+#pragma unroll
+      for (int k = 0; k < 5; k++) w[i][k] = m32[min(max((b >> 2) + k, 0), kTiles / 4 - 1)];
+    }
+#pragma unroll
+    for (int i = 0; i < 5; i++) {
+      uint32_t v[4];
+#pragma unroll
+      for (int k = 0; k < 4; k++) v[k] = __builtin_amdgcn_alignbyte(w[i][k + 1], w[i][k], off[i]) ^ rep;
+      // (byte 15 lies outside the window: forced nonzero)
+      hit = hit || zero_byte(v[0]) || zero_byte(v[1]) || zero_byte(v[2]) || zero_byte(v[3] | 0xFF000000u);
+    }
+    if (hit) break;
+  }
+  return hit;
+}
+
 __device__ __forceinline__ double term_progress(const Ctx& c, int p, const NmmoTaskTerm& q, const int* acc) {
   const int sk = q.a >= 1 && q.a <= 8 ? q.a - 1 : -1;
   const uint2* inv = c.items ? c.inv + p * kInv : nullptr;
@@ -1120,13 +1154,7 @@ __device__ __forceinline__ double term_progress(const Ctx& c, int p, const NmmoT
     }
     case PRED_INVENTORY_SPACE_GE: return kInv - (inv ? inv_count(inv) : 0) >= q.a ? 1.0 : 0.0;
     case PRED_OCCUPY_TILE: return TF(F_ROW, p) == q.a && TF(F_COL, p) == q.b ? 1.0 : 0.0;
-    case PRED_CAN_SEE_TILE: {
-      const int r = TF(F_ROW, p), col = TF(F_COL, p);
-      for (int dr = -kVision; dr <= kVision; dr++)
-        for (int dc = -kVision; dc <= kVision; dc++)
-          if (c.mat[(r + dr) * kSize + col + dc] == q.a) return 1.0;
-      return 0.0;
-    }
+    case PRED_CAN_SEE_TILE: return can_see_tile(c, TF(F_ROW, p), TF(F_COL, p), q.a) ? 1.0 : 0.0;
     case PRED_CAN_SEE_AGENT: case PRED_CAN_SEE_GROUP: {
       // the target agent is one of the Entity obs rows of p's observation after this tick: in
       // the realm, within the 15x15 window, and among the first 100 such entities in datastore
