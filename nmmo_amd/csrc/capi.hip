@@ -275,7 +275,7 @@ int nmmo_create(const NmmoConfig* cfg, int32_t n_envs, uint64_t seed, int32_t de
   }
   h->st = DevState{h->d_env,   h->d_ent,   h->d_ring,  h->d_mat,    h->d_dep, h->d_bank,
                    h->d_items, h->d_iring, h->d_mlist, h->d_mcount, h->d_events,
-                   h->d_tasks, h->d_assign, nullptr, h->d_tstate, 1,            0,           0, n_envs, P,
+                   h->d_tasks, h->d_assign, nullptr, h->d_tstate, 1,            0,           0, 0, n_envs, P,
                    N,          S,          seed,       nullptr,     *cfg,      h->d_foreign,
                    h->d_foreign + 1, nullptr, 0};
   {  // default task table: everyone runs TickGE(task_num_tick) (SPEC §12)
@@ -1009,13 +1009,14 @@ int nmmo_set_tasks(NmmoHandle* h, const NmmoTask* tasks, int32_t n_tasks, const 
                    const int32_t* assign) {
   if (!h || !tasks) return fail(NMMO_E_INVALID, "null argument");
   if (n_tasks < 1 || n_tasks > NMMO_MAX_TASKS) return fail(NMMO_E_INVALID, "n_tasks %d not in 1..%d", n_tasks, NMMO_MAX_TASKS);
-  int tev = 0, tmap = 0;
+  int tev = 0, tmap = 0, tsee = 0;
   for (int i = 0; i < n_tasks; i++)
     for (int k = 0; k < 2; k++) {
       const int pr = tasks[i].term[k].pred;
       if (pr < 0 || pr >= NMMO_N_PREDICATES) return fail(NMMO_E_INVALID, "task %d term %d: predicate %d", i, k, pr);
       tev |= (pr >= PRED_COUNT_EVENT && pr <= PRED_DEFEAT_ENTITY) || pr == PRED_PRACTICE_EATING;
       tmap |= pr == PRED_CAN_SEE_TILE;
+      tsee |= pr == PRED_CAN_SEE_AGENT || pr == PRED_CAN_SEE_GROUP;
     }
   const size_t nP = (size_t)h->st.n_envs * h->st.P;
   if (assign)
@@ -1050,6 +1051,7 @@ int nmmo_set_tasks(NmmoHandle* h, const NmmoTask* tasks, int32_t n_tasks, const 
   h->st.n_tasks = n_tasks;
   h->st.tev = tev;
   h->st.tmap = tmap;
+  h->st.tsee = tsee;
   h->st.task_cum = nullptr;  // weights belong to the previous table
   h->native_fresh = false;   // task indices of the last native obs may be out of date
   // flat rows keep a task's embedding by index (ObsParams::zst): the new table may differ

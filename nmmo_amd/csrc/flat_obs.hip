@@ -40,6 +40,10 @@ __device__ uint64_t fo_wave_buf[1 << 15][6];  // per wave: entry, staged, window
 #else
 #define FO_STAMP(k) (void)0
 #endif
+#ifndef NMMO_FO_TASK_BATCH  // (A/B knob: tools/debug/variants.py)
+#define NMMO_FO_TASK_BATCH 8
+#endif
+constexpr int kFoTaskBatch = NMMO_FO_TASK_BATCH;  // Task floats per lane loaded before their stores
 constexpr int kFoStagedListings = 256;  // listings whose item words are staged (Market rows)
 constexpr int kFoChunks = 25;           // 64-entry chunks over the 1,586 mask entries (+ id, tick)
 static_assert(kFoChunks * 64 >= kMaskN + 2 && (kFoChunks - 1) * 64 < kMaskN, "mask chunks");
@@ -475,16 +479,16 @@ __global__ void __launch_bounds__(64 * kAoWaves) flat_obs_kernel(ObsParams p) {
     // Task: only when the row does not hold this task's embedding yet (read in place)
     const int task = __builtin_amdgcn_readlane(my_task, j);
     if (!((ztask >> j) & 1)) {
-      // 8 loads in flight before their stores: each load waits for every store issued before it
-      // (vmcnt retires in order), so a load-store loop drained the queue once per 64 floats
+      // kFoTaskBatch loads in flight before their stores: each load waits for every store issued
+      // before it (vmcnt retires in order), so a load-store loop drained the queue per 64 floats
       const float* temb = kp->task + (size_t)task * tdim;
       int k0 = 0;
-      for (; k0 + 8 * 64 <= tdim; k0 += 8 * 64) {
-        float t[8];
+      for (; k0 + kFoTaskBatch * 64 <= tdim; k0 += kFoTaskBatch * 64) {
+        float t[kFoTaskBatch];
 #pragma unroll
-        for (int i = 0; i < 8; i++) t[i] = temb[k0 + 64 * i + lane];
+        for (int i = 0; i < kFoTaskBatch; i++) t[i] = temb[k0 + 64 * i + lane];
 #pragma unroll
-        for (int i = 0; i < 8; i++) fo_st(row, kFoTask + k0 + 64 * i + lane, t[i]);
+        for (int i = 0; i < kFoTaskBatch; i++) fo_st(row, kFoTask + k0 + 64 * i + lane, t[i]);
       }
       for (int k = k0 + lane; k < tdim; k += 64) fo_st(row, kFoTask + k, temb[k]);
       nbytes += 4ull * tdim;

@@ -37,6 +37,7 @@ struct DevState {
   NmmoTaskState* tstate; // [n][P] progress / event accumulators
   int n_tasks, tev;      // tev: some task term counts events
   int tmap;              // some task term reads the material map (CanSeeTile)
+  int tsee;              // some task term counts window entities (CanSeeAgent / CanSeeGroup)
   int n_envs, P, N, S;   // N = NPC capacity (0 when the NPC system is off), S = P + N
   uint64_t seed;         // create seed (first-episode seeds)
   unsigned long long* counters;  // optional device u64 [3]: agent-steps, finished episodes, event rows

@@ -81,6 +81,7 @@ struct Ctx {
   int4* tdesc;             // LDS [128][2] (pred, a, b, c) of each player's terms (when tev)
   bool tev;
   bool tmap;         // DevState::tmap: a task reads the material map at the rewards
+  bool tsee;         // DevState::tsee: a task counts window entities (the rewards' slot words in ft)
   int evcap, tick1;  // ring rows (0 = no event log); tick + 1 (the events' tick column)
   int S, P, N, IC;
   bool items, exch, prof, equip;
@@ -230,6 +231,7 @@ __device__ __forceinline__ Ctx make_ctx(unsigned char* smem, const DevState& st,
   }
   c.tev = st.tev != 0;
   c.tmap = st.tmap != 0;
+  c.tsee = st.tsee != 0;
   c.tasks = st.tasks;
   c.assign = st.assign + (size_t)e * P;
   c.task_cum = st.task_cum;
@@ -1165,9 +1167,18 @@ __device__ __forceinline__ double term_progress(const Ctx& c, int p, const NmmoT
       const int r = TF(F_ROW, p), col = TF(F_COL, p);
       if (linf(r, col, TF(F_ROW, t), TF(F_COL, t)) > kVision) return 0.0;
       const int dt = TF(F_DS_ROW, t);
+      // over the slots' packed words (ds_row << 16 | row << 8 | col, dead: ds_row 511; built once
+      // per tick in c.ft when a task counts window entities), four per LDS read: the per-slot
+      // loop read four staged fields per slot, and one player's scan was most of a tick
+      const uint4* sw = reinterpret_cast<const uint4*>(c.ft);
       int before = 0;
-      for (int s = 0; s < c.S; s++)
-        before += TF(F_ALIVE, s) && TF(F_DS_ROW, s) < dt && linf(r, col, TF(F_ROW, s), TF(F_COL, s)) <= kVision;
+      for (int s4 = 0; s4 < (c.S + 3) >> 2; s4++) {
+        const uint4 q4 = sw[s4];
+        const uint32_t qs[4] = {q4.x, q4.y, q4.z, q4.w};
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+          before += (int)(qs[k] >> 16) < dt && linf(r, col, (int)((qs[k] >> 8) & 255u), (int)(qs[k] & 255u)) <= kVision;
+      }
       return before < kNObs ? 1.0 : 0.0;
     }
     case PRED_FULLY_ARMED: {
@@ -2291,6 +2302,14 @@ __device__ __forceinline__ void tick_env(Ctx& c, Heads hd, float* rew, uint8_t* 
   if (tid == 0) {
     c.E[E_DONE] = done;
     if (c.evcap) c.E[E_EVENT_COUNT] = evn;
+  }
+  if (c.tsee) {  // the slots' packed words for CanSeeAgent / CanSeeGroup (the union region is free here)
+    uint32_t* sw = reinterpret_cast<uint32_t*>(c.ft);
+    for (int k = tid; k < ((c.S + 3) & ~3); k += blockDim.x)
+      sw[k] = k < c.S && TF(F_ALIVE, k) ? (uint32_t)(TF(F_DS_ROW, k) & 511) << 16 | (uint32_t)(TF(F_ROW, k) & 255) << 8 |
+                                              (uint32_t)(TF(F_COL, k) & 255)
+                                        : 511u << 16;
+    __syncthreads();
   }
   if (s < P) {  // Task.compute_rewards: progress delta, death penalty (SPEC §12)
     float rw = 0.f;

@@ -52,6 +52,11 @@ def main():
     cfg = Config.preset(preset, early_stop_agent_num=8,
                         obs_layout=abi.OBS_FLAT if preset == "C4" else abi.OBS_NONE)
     eng = NmmoEngine(cfg, envs, seed=1)
+    cur = os.environ.get("STAMPS_CURRICULUM")  # e.g. manual / heldout: nmmo_amd.tasks' curricula
+    if cur:
+        from nmmo_amd import tasks
+
+        eng.set_curriculum(getattr(tasks, cur + "_curriculum")())
     eng.reset()
     stagger = int(os.environ.get("STAMPS_STAGGER", "0"))  # bench.py's staggered pre-roll
     for k in range(stagger):
