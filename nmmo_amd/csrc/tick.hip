@@ -1096,24 +1096,29 @@ __device__ __forceinline__ double clip01(double x) { return x < 0.0 ? 0.0 : x > 
 // byte-by-byte early-exit scan waited, per byte, for every store the tick had queued before it
 // (vmcnt counts stores too and retires in order). Bytes 0..14 of a row come out of its 5 dwords
 // by v_alignbyte; a zero byte of row ^ (m x 4) is a match.
+#ifndef NMMO_SEE_ROWS  // window rows loaded per batch (A/B knob; divides 15)
+#define NMMO_SEE_ROWS 5
+#endif
+constexpr int kSeeRows = NMMO_SEE_ROWS;
+static_assert(15 % kSeeRows == 0, "window rows per batch");
 __device__ __forceinline__ bool can_see_tile(const Ctx& c, int r, int col, int m) {
   if ((unsigned)m > 255u) return false;  // no tile byte holds it
   const uint32_t* m32 = reinterpret_cast<const uint32_t*>(c.mat);
   const uint32_t rep = (uint32_t)(m & 255) * 0x01010101u;
   auto zero_byte = [](uint32_t x) { return ((x - 0x01010101u) & ~x & 0x80808080u) != 0u; };
   bool hit = false;
-  for (int r0 = 0; r0 < 15; r0 += 5) {
-    uint32_t w[5][5];
-    int off[5];
+  for (int r0 = 0; r0 < 15; r0 += kSeeRows) {
+    uint32_t w[kSeeRows][5];
+    int off[kSeeRows];
 #pragma unroll
-    for (int i = 0; i < 5; i++) {
+    for (int i = 0; i < kSeeRows; i++) {
       const int b = (r - kVision + r0 + i) * kSize + col - kVision;  // the row's first window byte
       off[i] = b & 3;
 #pragma unroll
       for (int k = 0; k < 5; k++) w[i][k] = m32[min(max((b >> 2) + k, 0), kTiles / 4 - 1)];
     }
 #pragma unroll
-    for (int i = 0; i < 5; i++) {
+    for (int i = 0; i < kSeeRows; i++) {
       uint32_t v[4];
 #pragma unroll
       for (int k = 0; k < 4; k++) v[k] = __builtin_amdgcn_alignbyte(w[i][k + 1], w[i][k], off[i]) ^ rep;
