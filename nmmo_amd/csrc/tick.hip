@@ -1092,12 +1092,12 @@ __device__ __forceinline__ double per_d(int num, int den) { return (double)num /
 __device__ __forceinline__ double clip01(double x) { return x < 0.0 ? 0.0 : x > 1.0 ? 1.0 : x; }
 
 // Is material `m` on any tile of the 15x15 window around (r, col) (this tick's materials, in
-// HBM)? The window rows are loaded as aligned dwords, 5 rows (25 loads) before their tests: a
+// HBM)? The window rows are loaded as aligned dwords, a row's 5 loads before its tests: a
 // byte-by-byte early-exit scan waited, per byte, for every store the tick had queued before it
 // (vmcnt counts stores too and retires in order). Bytes 0..14 of a row come out of its 5 dwords
 // by v_alignbyte; a zero byte of row ^ (m x 4) is a match.
 #ifndef NMMO_SEE_ROWS  // window rows loaded per batch (A/B knob; divides 15)
-#define NMMO_SEE_ROWS 5
+#define NMMO_SEE_ROWS 1  // (5 rows: same curricula times, more spills in every tick variant: C3 tick +1.3%)
 #endif
 constexpr int kSeeRows = NMMO_SEE_ROWS;
 static_assert(15 % kSeeRows == 0, "window rows per batch");
