@@ -293,7 +293,7 @@ constexpr int kGrid = (kSize + (1 << kCellShift) - 1) >> kCellShift;  // 10
 constexpr int kCells = kGrid * kGrid;
 constexpr int kGridCells = 2 * kCells;
 constexpr int kWinRows = (14 + (1 << kCellShift) - 1) / (1 << kCellShift) + 1;  // 2
-__host__ __device__ inline size_t grid_lds_bytes(int S) {  // gstart | glist
+__host__ __device__ constexpr size_t grid_lds_bytes(int S) {  // gstart | glist
   return (((size_t)(kGridCells + 1) * 4 + 15) & ~(size_t)15) + (((size_t)S * 4 + 15) & ~(size_t)15);
 }
 // first / last grid row and first / last grid column of the window around (r, c)

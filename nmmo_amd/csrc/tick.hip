@@ -78,7 +78,8 @@ struct Ctx {
   NmmoTaskState* tsg;   // this env's task state in HBM. Accessed through tsl/tsg, never ts, on the
                         // hot path: ts may point to either, so its accesses are flat, and a flat
                         // load makes the next LDS wait (lgkmcnt) wait for HBM too
-  int4* tdesc;             // LDS [128][2] (pred, a, b, c) of each player's terms (when tev)
+  int2* tdesc;             // LDS [128][2] (pred | a << 8, b) of each player's terms (when tev): what
+                           // task_accumulate reads; 8 B, so C4's task staging keeps 2 workgroups per CU
   bool tev;
   bool tmap;         // DevState::tmap: a task reads the material map at the rewards
   bool tsee;         // DevState::tsee: a task counts window entities (the rewards' slot words in ft)
@@ -159,7 +160,7 @@ constexpr int kHash = 256;  // >= 2x players: open addressing never fills
 constexpr int kLWords = 32;  // listed-row bitmap words (rows 1..12*128)
 
 // item system: inventories, item FIFO, row map, listed bitmap, decoded Buy/Give actions
-__host__ __device__ inline size_t item_lds_bytes(int P) {
+__host__ __device__ constexpr size_t item_lds_bytes(int P) {
   auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
   const size_t ic = (size_t)kInv * P;
   return (size_t)P * kInv * 8 + al(ic * 2) + al((ic + 1) * 2) + kLWords * 8 + 5 * 256 + 512;
@@ -170,7 +171,7 @@ constexpr size_t kPlayerArrBytes = 4 * 256 + 128;  // kill, order, ev_dmg, ev_lv
 __host__ __device__ inline bool uses_grid(uint32_t systems) {
   return (systems & (NMMO_SYS_COMBAT | NMMO_SYS_ITEM | NMMO_SYS_NPC)) != 0;
 }
-__host__ __device__ inline size_t union_lds_bytes(int S, bool grid) {
+__host__ __device__ constexpr size_t union_lds_bytes(int S, bool grid) {
   auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
   size_t u = (size_t)128 * ((S + 63) / 64) * 8 + (grid ? grid_lds_bytes(S) : 0);
   u = u > 2 * kHash * 4 ? u : 2 * kHash * 4;
@@ -178,7 +179,7 @@ __host__ __device__ inline size_t union_lds_bytes(int S, bool grid) {
   return u > atk ? u : atk;
 }
 
-__host__ __device__ inline size_t tick_lds_bytes(int S, int P, bool items, bool tev, bool grid, bool slim) {
+__host__ __device__ constexpr size_t tick_lds_bytes(int S, int P, bool items, bool tev, bool grid, bool slim) {
   auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
   // task state is staged in LDS only when events feed its accumulators (else read in place)
   size_t b = (items ? item_lds_bytes(P) : 0) + kPlayerArrBytes;
@@ -191,9 +192,12 @@ __host__ __device__ inline size_t tick_lds_bytes(int S, int P, bool items, bool 
   b += (size_t)kBitmapWords * 4;     // dep
   b += NMMO_NE * 4 + 32 * 4 + 16 * 4 + 128 + 128;
   // task state staging last (make_ctx): 16-B aligned
-  if (tev) b = al(b) + al((size_t)P * sizeof(NmmoTaskState)) + 128 * 2 * 16;
+  if (tev) b = al(b) + al((size_t)P * sizeof(NmmoTaskState)) + 128 * 2 * 8;
   return b;
 }
+// C4 (384 slots, items) with task events staged (a curriculum with event-counting terms) must keep
+// two workgroups per CU: at 82,000 B (80 B over half the CU's LDS) it ran one, and a tick took twice as long
+static_assert(tick_lds_bytes(384, 128, true, true, true, false) <= 80 * 1024, "C4 tick LDS: 2 workgroups per CU");
 
 // kS / kP: the slot / player counts when known at compile time (0 = st's)
 template <int kS = 0, int kP = 0>
@@ -280,7 +284,7 @@ __device__ __forceinline__ Ctx make_ctx(unsigned char* smem, const DevState& st,
   if (c.tev) {
     c.ts = c.tsl;
     o += al((size_t)P * sizeof(NmmoTaskState));
-    c.tdesc = reinterpret_cast<int4*>(smem + o); o += 128 * 2 * 16;
+    c.tdesc = reinterpret_cast<int2*>(smem + o); o += 128 * 2 * 8;
   } else {
     c.ts = c.tsg;  // HBM, touched once per player at the rewards
     c.tdesc = nullptr;
@@ -582,7 +586,8 @@ __device__ __forceinline__ void task_accumulate(const Ctx& c, int p, int code, i
                                                 int gold, int target) {
 #pragma unroll
   for (int k = 0; k < 2; k++) {
-    const int4 q = c.tdesc[p * 2 + k];  // pred, a, b, c
+    const int2 qd = c.tdesc[p * 2 + k];
+    const int4 q = make_int4(qd.x & 255, qd.x >> 8, qd.y, 0);  // pred, a, b (c: not read here)
     int* acc = c.tsl[p].acc + 2 * k;  // called only when tev (staged)
     int add0 = 0, add1 = 0;
     switch (q.x) {
@@ -1284,7 +1289,7 @@ __device__ __forceinline__ void tick_env(Ctx& c, Heads hd, float* rew, uint8_t* 
   if (c.tev && s < P) {  // this player's task terms and event accumulators
     const NmmoTask& tk = c.tasks[c.assign[s]];
 #pragma unroll
-    for (int k = 0; k < 2; k++) c.tdesc[s * 2 + k] = make_int4(tk.term[k].pred, tk.term[k].a, tk.term[k].b, tk.term[k].c);
+    for (int k = 0; k < 2; k++) c.tdesc[s * 2 + k] = make_int2((tk.term[k].pred & 255) | tk.term[k].a * 256, tk.term[k].b);
   }
   // only the listed-row bitmap's zeroing must precede this phase's writes (its atomicOr); pres,
   // misc and tdesc are read after the phase's closing barrier
