@@ -84,9 +84,11 @@ __host__ __device__ inline int level_at_exp(int exp) {
   for (int i = 0; i < 10; i++) l += exp >= thr[i];
   return l;
 }
+// (a select chain: a runtime index into a constant array is a global load on the device, and in
+// the tick it came after the phase's stores -- vmcnt retires in order -- so it drained them)
 __host__ __device__ inline int exp_at_level(int level) {
-  const int thr[10] = {0, 90, 250, 500, 900, 1500, 2400, 3700, 5500, 8000};
-  return thr[level - 1];
+  return level <= 1 ? 0 : level == 2 ? 90 : level == 3 ? 250 : level == 4 ? 500 : level == 5 ? 900
+       : level == 6 ? 1500 : level == 7 ? 2400 : level == 8 ? 3700 : level == 9 ? 5500 : 8000;
 }
 
 __host__ __device__ inline int dir_dr(int d) { return d == 0 ? -1 : d == 1 ? 1 : 0; }
