@@ -174,9 +174,17 @@ def parse(argv=None):
                     help="run env_creator's RewardWrapper on the device (SPEC §13) with the "
                          "config.yaml weights")
     ap.add_argument("--no-decode", action="store_true", help="C5: skip the decoded pass")
-    ap.add_argument("--root-rehearsal", type=int, default=7,
-                    help="C5 at N = 1: a root_loaded pass in which rank 0 also validates and stores this many "
-                         "phantom peers' buffers each step (0 = off)")
+    ap.add_argument("--root-rehearsal", type=int, default=8,
+                    help="C5 at N = 1: model the node of this many GPUs from measured pieces (a peer's step at "
+                         "its share, rank 0's step at its share with the other ranks' buffers received, checked "
+                         "and stored: measure_root_model); 0 = off")
+    ap.add_argument("--root-envs", type=int, default=None,
+                    help="C5: envs on rank 0 (the learner) at N GPUs; the other ranks split the rest of "
+                         "1024 x N (default: ROOT_ENVS[N])")
+    ap.add_argument("--rehearse-copy", action="store_true",
+                    help="C5 model: also time the root with the phantom transfers as copies (read + write)")
+    ap.add_argument("--no-c5-reference", action="store_true",
+                    help="N > 1: skip the one-GPU C5 reference pass (the like-for-like scaling base)")
     ap.add_argument("--dry-launch", action="store_true",
                     help="launcher check: each rank prints its RANK/WORLD_SIZE and exits (no GPU)")
     ap.add_argument("--inject-fault", action="store_true", help=argparse.SUPPRESS)  # tests: nmmo_inject_fault
@@ -602,93 +610,130 @@ def _roofline(prof_name, kern, byts, ms, per, timing, nb, step_s, fill_gbs, pmc_
     }
 
 
-def measure_gather(args, name, envs, rank, world, dev, steps, warmup, dist=None, backend="nccl"):
-    """C5: the rank's envs as `--batches` wire-obs handles stepped by WireGather (policy +
-    nmmo_step into a ring of wire buffers, hipGraph-captured, one stream per batch; the learner
-    gather into rank 0 one step behind on a comm stream). Three timed passes over the same
-    engines: "delivered" (rank 0 validates every received buffer on the device), "stored" (rank 0
-    also stores every row of every step in compact record storage) and "decoded" (rank 0 also
-    decodes every rank's buffers into the native layout each step)."""
+# C5's learner share (distributed.env_shares): envs on rank 0 at N GPUs (8 * 1024 envs on 8),
+# the other ranks split the rest. The root validates and stores every peer's buffers each step
+# besides its own compute, so it holds fewer envs; DESIGN.md §5 derives the shares from the
+# measured root and peer steps (bench C5 extra at N = 1: root_loaded / peer passes).
+ROOT_ENVS = {2: 1024, 4: 1024, 8: 1024}
+XGMI_LINK_GBS = 153.6   # per xGMI link (task brief: 7 links x ~153 GB/s per GPU)
+LINK_EFF = 0.75         # the share of it the N = 8 model assumes a point-to-point send gets
+
+
+def c5_shares(args, world: int, nb: int):
+    """Per-rank env counts of C5 at `world` ranks (1024 per GPU in total)."""
+    from nmmo_amd.distributed import env_shares
+
+    total = (args.envs or WORKLOADS["C5"]["envs"]) * world
+    k = args.root_envs if args.root_envs is not None else ROOT_ENVS.get(world) if args.envs is None else None
+    return env_shares(total, world, None if world == 1 else k, granule=nb)
+
+
+def _wire_engines(args, cfg, task, envs, base, nb, dev, pseed):
+    from nmmo_amd.engine import NmmoEngine
+
+    if envs % nb:
+        raise SystemExit(f"--batches {nb} must divide the {envs} envs of this rank")
+    per = envs // nb
+    engs = [NmmoEngine(cfg, per, seed=args.seed, device=dev, task_embedding=_task_embedding(),
+                       env_index_base=base + i * per) for i in range(nb)]
+    for e in engs:
+        e.reset()
+    _stagger(engs, args.stagger, per, base, pseed)
+    return engs
+
+
+def _gather_pass(args, engs, g, steps, warmup, world, dist, dev, counters, store=None):
+    """Warm up, then time `steps` steps of WireGather g (barrier + device sync on both sides)."""
+    import torch
+
+    for _ in range(warmup):
+        g.step()
+    g.drain()
+    torch.cuda.synchronize(dev)
+    if store is not None:
+        g.stored_rows()  # the warm-up's rows do not count
+    for c in counters:
+        c.zero_()
+    b0 = g.x.payload_bytes
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        g.step()
+    g.drain()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    tot = torch.stack(counters).sum(0)
+    status = g.check_status()
+    if status:
+        raise RuntimeError(f"the received-buffer check flagged wire buffers (status {status})")
+    stored = g.stored_rows() if store is not None else None
+    if store is not None and store.status:
+        raise RuntimeError(f"the root's record store dropped rows (status {store.status})")
+    return {"elapsed": elapsed, "alive": float(tot[0].item()), "episodes": int(tot[1].item()),
+            "events": float(tot[2].item()), "stored_rows": stored,
+            "payload_bytes_per_step": (g.x.payload_bytes - b0) / steps}
+
+
+def _record_store(per_list, dev, P):
+    """Compact record storage for every row of one step of buffers of per_list envs (rank 0)."""
+    from nmmo_amd import wire as nw
+    from nmmo_amd.storage import DeviceExperience
+
+    rows = sum(per_list) * P
+    arena = sum(nw.max_bytes(n, P) + 64 for n in per_list)
+    return DeviceExperience(rows, 23987, rows, device=dev, record_arena_bytes=arena)
+
+
+def measure_gather(args, name, envs, rank, world, dev, steps, warmup, dist=None, backend="nccl", shares=None,
+                   modes=None):
+    """C5: the rank's envs (its share of the node) as `--batches` wire-obs handles stepped by
+    WireGather (policy + nmmo_step into a ring of wire buffers, hipGraph-captured, one stream per
+    batch; the learner gather into rank 0 one step behind on a comm stream). Timed passes over
+    the same engines: "delivered" (rank 0 validates every received buffer on the device),
+    "stored" (rank 0 also stores every row of every step in compact record storage, the check
+    fused into the store) and "decoded" (rank 0 also decodes every rank's buffers into the native
+    layout each step)."""
     import torch
 
     from nmmo_amd import abi
-    from nmmo_amd import wire as nw
     from nmmo_amd.config import Config
     from nmmo_amd.distributed import WireGather
-    from nmmo_amd.engine import NmmoEngine
 
     wl = WORKLOADS[name]
     cfg = Config.preset(wl["preset"], early_stop_agent_num=8, obs_layout=abi.OBS_WIRE)
     nb = max(1, args.batches)
-    if envs % nb:
-        raise SystemExit(f"--batches {nb} must divide the {envs} envs per GPU")
-    per = envs // nb
-    task = _task_embedding()
-    engs = [NmmoEngine(cfg, per, seed=args.seed, device=dev, task_embedding=task,
-                       env_index_base=rank * envs + i * per) for i in range(nb)]
-    for e in engs:
-        e.reset()
+    shares = shares or [envs]
+    envs = shares[rank]
+    base = sum(shares[:rank])
     pseed = args.seed * 1_000_003
-    _progress(f"{name}: {nb} engines built and reset")
-    _stagger(engs, args.stagger, per, rank * envs, pseed)
-    _progress(f"{name}: staggered over {args.stagger} ticks")
+    engs = _wire_engines(args, cfg, None, envs, base, nb, dev, pseed)
+    per = envs // nb
+    _progress(f"{name}: {nb} engines of {per} envs built, reset and staggered over {args.stagger} ticks")
     counters = [torch.zeros(3, dtype=torch.int64, device=dev) for _ in engs]
     for e, c in zip(engs, counters):
         e.set_counters(c)
     torch.cuda.synchronize(dev)
     passes = {}
-    modes = ("delivered",) if args.no_decode else ("delivered", "stored", "decoded")
-    rh = args.root_rehearsal if world == 1 and not args.no_decode else 0
-    if rh > 0:
-        modes += ("root_loaded",)
+    modes = modes or (("delivered",) if args.no_decode else ("delivered", "stored", "decoded"))
     for mode in modes:
-        decode = mode == "decoded"
         store = None
-        ranks = world + (rh if mode == "root_loaded" else 0)  # ranks whose rows the root stores
-        if mode in ("stored", "root_loaded") and rank == 0:  # compact record storage of every row of every step
-            from nmmo_amd.storage import DeviceExperience
-
-            rows = ranks * envs * cfg.PLAYER_N
-            store = DeviceExperience(rows, engs[0].obs_elems, rows, device=dev,
-                                     record_arena_bytes=ranks * nb * (nw.max_bytes(per, cfg.PLAYER_N) + 64))
-        g = WireGather(engs, pseed, rank, world, decode=decode, graphs=not args.no_graph, backend=backend,
-                       store=store, rehearse=rh if mode == "root_loaded" else 0)
-        for _ in range(warmup):
-            g.step()
-        g.drain()
-        torch.cuda.synchronize(dev)
-        if store is not None:
-            g.stored_rows()  # the warm-up's rows do not count
-        for c in counters:
-            c.zero_()
-        b0 = g.x.payload_bytes
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize(dev)
-        t0 = time.perf_counter()
-        for _ in range(steps):
-            g.step()
-        g.drain()
-        torch.cuda.synchronize(dev)
-        if world > 1:
-            dist.barrier()
-        elapsed = time.perf_counter() - t0
-        tot = torch.stack(counters).sum(0)
-        status = g.check_status()
-        if status:
-            raise RuntimeError(f"nmmo_wire_check flagged received wire buffers (status {status})")
-        stored = g.stored_rows() if store is not None else None
-        if store is not None and store.status:
-            raise RuntimeError(f"the root's record store dropped rows (status {store.status})")
-        _progress(f"{name}: timed {steps} steps in {elapsed:.3f} s ({mode})")
-        passes[mode] = {"elapsed": elapsed, "alive": float(tot[0].item()), "episodes": int(tot[1].item()),
-                        "events": float(tot[2].item()), "stored_rows": stored,
-                        "payload_bytes_per_step": (g.x.payload_bytes - b0) / steps}
+        if mode == "stored" and rank == 0:  # compact record storage of every row of every step
+            store = _record_store([n // nb for n in shares for _ in range(nb)], dev, cfg.PLAYER_N)
+        g = WireGather(engs, pseed, rank, world, decode=mode == "decoded", graphs=not args.no_graph,
+                       backend=backend, store=store)
+        passes[mode] = _gather_pass(args, engs, g, steps, warmup, world, dist, dev, counters, store)
+        _progress(f"{name}: timed {steps} steps in {passes[mode]['elapsed']:.3f} s ({mode})")
         g.close()
         del store
     eng = engs[0]
     tick_avg_ms, obs_avg_ms, _ = _kernel_timing(eng, pseed, steps)
     _check_faults(args, engs, name, world, dist, dev)
+    from nmmo_amd import wire as nw
+
     wire_env_bytes = nw.total_bytes(eng.obs) / per  # this batch's last step: header + records
     S, P = eng.S, cfg.PLAYER_N
     d = passes["delivered"]
@@ -713,18 +758,117 @@ def measure_gather(args, name, envs, rank, world, dev, steps, warmup, dist=None,
                               ["wire_count_kernel", "wire_scan_kernel", "wire_obs_kernel"] if kern == "wire_obs_kernel"
                               else None),
         "batches": nb,
+        "shares": list(shares),
         "gather_bytes": d["payload_bytes_per_step"] if world > 1 else 0,
+        "wire_bytes_per_env": round(wire_env_bytes, 1),
         "wire_bytes_per_agent_in_realm": round(wire_env_bytes * per * nb * steps / max(d["alive"], 1.0), 1),
         "decoded": passes.get("decoded"),
         "stored": passes.get("stored"),
-        "root_loaded": passes.get("root_loaded"),
-        "root_rehearsal": rh,
     }
     for e in engs:
         e.close()
     del eng, engs
     torch.cuda.empty_cache()
     return res
+
+
+def measure_root_model(args, dev, steps, warmup, n_model: int = 8):
+    """The N = n_model node of C5 from its measured pieces on one GPU:
+      peer: one peer's step at its share of the node (C5 delivered, world 1, peer-share envs);
+      root_loaded: rank 0's step at its share with n_model - 1 phantom peers' buffers received
+        (write-only fills of their bytes), validated and stored every step (the fused checked
+        store): the root's whole load (WireGather rehearse, phantom = the peer pass's buffers);
+      link: the bytes one peer sends per step over its own xGMI link at LINK_EFF of XGMI_LINK_GBS.
+    The node delivers (root's + peers' agents in the realm per step) / max(root, peer, link)."""
+    import torch
+
+    from nmmo_amd import abi
+    from nmmo_amd.config import Config
+    from nmmo_amd.distributed import WireGather
+
+    nb = max(1, args.batches)
+    shares = c5_shares(args, n_model, nb)
+    k_root, e_peer = shares[0], shares[1]
+    cfg = Config.preset("C4", early_stop_agent_num=8, obs_layout=abi.OBS_WIRE)
+    P = cfg.PLAYER_N
+    pseed = args.seed * 1_000_003
+    # 1. a peer's share, stepped alone (rank 1's env block); its last buffers become the phantoms
+    engs = _wire_engines(args, cfg, None, e_peer, shares[0], nb, dev, pseed)
+    counters = [torch.zeros(3, dtype=torch.int64, device=dev) for _ in engs]
+    for e, c in zip(engs, counters):
+        e.set_counters(c)
+    g = WireGather(engs, pseed, 0, 1, graphs=not args.no_graph)
+    peer = _gather_pass(args, engs, g, steps, warmup, 1, None, dev, counters)
+    _progress(f"C5 model: peer share {e_peer} envs, {peer['elapsed'] * 1e3 / steps:.4f} ms/step")
+    from nmmo_amd import wire as nw
+
+    # the phantoms = the peer's last step: its wire buffers (the announced bytes) and step records
+    k = (g.t - 1) % g.ring
+    phantom, peer_bytes = [], 0
+    for j, e in enumerate(engs):
+        w = g.wires[j][k]
+        tot = nw.total_bytes(w)
+        peer_bytes += tot + g.smalls[j][k].numel()  # what a peer sends per step: wire bytes + step records
+        phantom.append((w[:tot].clone(), g.smalls[j][k].clone(), e.n_envs))
+    g.close()
+    for e in engs:
+        e.close()
+    del engs, g
+    torch.cuda.empty_cache()
+    # 2. the root's share with n_model - 1 phantom peers received, checked and stored each step
+    engs = _wire_engines(args, cfg, None, k_root, 0, nb, dev, pseed)
+    counters = [torch.zeros(3, dtype=torch.int64, device=dev) for _ in engs]
+    for e, c in zip(engs, counters):
+        e.set_counters(c)
+    R = n_model - 1
+    store = _record_store([k_root // nb] * nb + [n for _, _, n in phantom] * R, dev, P)
+    out = {}
+    for mode in ("fill", "copy") if args.rehearse_copy else ("fill",):
+        store.reset()
+        g = WireGather(engs, pseed, 0, 1, graphs=not args.no_graph, store=store, rehearse=R, phantom=phantom,
+                       rehearse_mode=mode)
+        out[mode] = _gather_pass(args, engs, g, steps, warmup, 1, None, dev, counters, store)
+        _progress(f"C5 model: root share {k_root} envs + {R} phantom peers ({mode}), "
+                  f"{out[mode]['elapsed'] * 1e3 / steps:.4f} ms/step")
+        g.close()
+    for e in engs:
+        e.close()
+    del engs, g, store
+    torch.cuda.empty_cache()
+    root = out["fill"]
+    root_ms = root["elapsed"] * 1e3 / steps
+    peer_ms = peer["elapsed"] * 1e3 / steps
+    link_ms = peer_bytes / (LINK_EFF * XGMI_LINK_GBS * 1e9) * 1e3
+    alive_step = root["alive"] / steps + R * peer["alive"] / steps
+    step_ms = max(root_ms, peer_ms, link_ms)
+    res = {
+        "n_gpus": n_model, "shares": shares,
+        "root_loaded": {"envs": k_root, "phantom_peers": R, "ms_per_step": round(root_ms, 4),
+                        "stored_rows_per_step": round((root["stored_rows"] or 0) / steps, 1),
+                        "what": f"rank 0's step at its share ({k_root} envs) with {R} phantom peers' buffers "
+                                f"({e_peer} envs each) received (write-only fills of their bytes), validated and "
+                                f"stored every step (nmmo_exp_store_records_checked)"},
+        "peer": {"envs": e_peer, "ms_per_step": round(peer_ms, 4), "bytes_per_step": int(peer_bytes),
+                 "what": f"one peer's step at its share ({e_peer} envs), gather-free"},
+        "link": {"ms_per_step": round(link_ms, 4), "gbs": round(LINK_EFF * XGMI_LINK_GBS, 1),
+                 "what": f"a peer's wire buffers + step records over its own xGMI link at {LINK_EFF:.0%} of "
+                         f"{XGMI_LINK_GBS} GB/s"},
+        "step_ms": round(step_ms, 4),
+        "bound": "root" if step_ms == root_ms else "peer" if step_ms == peer_ms else "link",
+        "value": round(alive_step / (step_ms * 1e-3), 1),
+    }
+    if "copy" in out:
+        res["root_loaded"]["copy_ms_per_step"] = round(out["copy"]["elapsed"] * 1e3 / steps, 4)
+    return res
+
+
+def _node_model(m, one_gpu_value):
+    m = dict(m)
+    m["ratio_vs_one_gpu"] = round(m["value"] / one_gpu_value, 3)
+    m["what"] = (f"the N = {m['n_gpus']} C5 node from pieces measured here (DESIGN.md §5): agents in the realm per "
+                 f"step of the root's and the peers' shares / max(root_loaded, peer, link); ratio_vs_one_gpu against "
+                 f"C5 at N = 1 measured in this run")
+    return m
 
 
 def result_line(res, args, world, steps, alive_total, slots_total, elapsed, warmup):
@@ -834,7 +978,10 @@ def main():
     def run(nm, lay, wrapper, n_envs, steps, warmup):
         t0 = time.perf_counter()
         if WORKLOADS[nm].get("gather"):
-            r = measure_gather(args, nm, n_envs, rank, world, dev, steps, warmup, dist, backend)
+            shares = c5_shares(args, world, max(1, args.batches))
+            r = measure_gather(args, nm, n_envs, rank, world, dev, steps, warmup, dist, backend, shares=shares)
+            if world == 1 and args.root_rehearsal > 1 and args.envs is None:
+                r["n_model"] = measure_root_model(args, dev, steps, warmup, args.root_rehearsal)
         else:
             r = measure(args, nm, lay, n_envs, rank, world, dev, steps, warmup, dist, wrapper)
         _progress(f"{r['name']} measured in {time.perf_counter() - t0:.1f} s")
@@ -854,18 +1001,12 @@ def main():
         """The C5 line's learner-side passes (whole job, max over ranks): "stored" (rank 0 keeps
         every row of every step in compact record storage) and "decoded"."""
         out = {}
-        rh = r.get("root_rehearsal") or 0
         for mode, what in (("stored", "rank 0 also stores every rank's rows in the realm each step as "
                                       "experience (nmmo_exp_store_records: the rows' fields + their wire "
                                       "records in an arena, flat rows expanded per minibatch)"),
                            ("decoded", "rank 0 also decodes every rank's wire buffers into the native layout "
                                        "(nmmo_wire_unpack) each step: the full learner-ready obs tensor"),
-                           ("root_loaded", f"the stored pass with the root's load of an N = {rh + 1} node: each "
-                                           f"step rank 0 also copies its own buffers into {rh} phantom peers' "
-                                           f"receive buffers (the incoming transfers' HBM writes), validates "
-                                           f"(nmmo_wire_check) and stores them as those peers' rows on its comm "
-                                           f"stream; value counts only rank 0's own agents (the xGMI links are "
-                                           f"not modelled)")):
+                           ):
             if not r.get(mode):
                 continue
             pr = dict(r, elapsed=r[mode]["elapsed"], alive=r[mode]["alive"])
@@ -878,6 +1019,19 @@ def main():
     res = run(name, args.obs, None, envs, args.steps, args.warmup)
     elapsed, alive_total, slots_total = reduce(res)
     passes = learner_passes(res, args.steps) if res.get("gather") else {}
+    one_gpu = None
+    if res.get("gather") and world > 1 and not args.no_c5_reference:
+        # the like-for-like scaling base: C5 at N = 1 (1024 envs, the root's own buffers in place,
+        # nothing sent) on rank 0's GPU in this run, while the other ranks wait
+        if rank == 0:
+            n1 = args.envs or WORKLOADS["C5"]["envs"]
+            r1 = measure_gather(args, "C5", n1, 0, 1, dev, args.steps, args.warmup, None, backend, shares=[n1],
+                                modes=("delivered",))
+            one_gpu = {"value": round(r1["alive"] / r1["elapsed"], 1),
+                       "ms_per_step": round(r1["elapsed"] * 1e3 / args.steps, 4), "envs": n1,
+                       "what": "C5 at N = 1 measured in this run on rank 0's GPU (its own wire buffers in place, "
+                               "nothing sent): the base of a like-for-like N > 1 scaling ratio"}
+        dist.barrier()
 
     extras = {}
     if not args.no_extras and not args.envs and args.config is None:
@@ -890,6 +1044,8 @@ def main():
             if r.get("gather"):
                 line.update(_gather_fields(r, world, backend, ex_steps))
                 line.update(learner_passes(r, ex_steps))
+                if r.get("n_model"):
+                    line["node_model"] = _node_model(r["n_model"], line["value"])
             extras[r["name"]] = line
 
     if rank == 0:
@@ -926,6 +1082,16 @@ def main():
             line.update(_gather_fields(res, world, backend, args.steps))
             line["value_kind"] = "delivered"
             line.update(passes)
+            line["config"]["envs_per_rank"] = res["shares"]
+            if res.get("n_model"):
+                line["node_model"] = _node_model(res["n_model"], line["value"])
+            if one_gpu:
+                line["c5_one_gpu"] = one_gpu
+                line["scaling_vs_c5_one_gpu"] = round(line["value"] / one_gpu["value"], 3)
+                line["like_for_like"] = ("scaling_vs_c5_one_gpu divides this line's value by C5 at N = 1 measured in "
+                                         "the same run; the N = 1 headline (bench.py --gpus 1) is C4 with flat obs, a "
+                                         "different workload, so value(N) / value(1) across the two lines is not a "
+                                         "scaling ratio")
         else:
             line["gather"] = None
         line["cpu_baseline"] = cpu

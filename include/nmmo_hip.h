@@ -537,7 +537,10 @@ typedef struct NmmoExperience {
   int32_t* ptr;         /* [1] rows stored (clean_pufferl.py:200 ptr) */
   int32_t* status;      /* [1] or NULL: bit 0 set when a store met a selected row whose env_id is
                            outside [0, n_slots) (the row is dropped, nothing out of range is
-                           written). Env ids must be distinct within one store (precondition). */
+                           written). Env ids must be distinct within one store (precondition).
+                           Record storage: bit 1 a wire buffer without arena room or with an
+                           implausible total, bit 3 one that failed the fused check, bit 4 one
+                           inside the arena but not at its slot (each keeps no row). */
 } NmmoExperience;
 
 typedef struct NmmoStoreInput {
@@ -603,6 +606,22 @@ NMMO_API int nmmo_exp_store_records(NmmoHandle* h, const NmmoExperience* x, cons
 NMMO_API int nmmo_exp_store_records_many(NmmoHandle* h, const NmmoExperience* x, const NmmoRecordStore* rs,
                                          const NmmoStoreInput* ins, int32_t n_inputs, int32_t field_stride,
                                          int32_t* scratch, void* stream);
+/* nmmo_exp_store_records_many with the received-buffer check fused into its reservation pass (the
+ * learner root of the C5 gather: one launch validates every input as nmmo_wire_check_many does and
+ * reserves the arena): each input's check bits (1 total vs *dev_expect_totals[i], 2 offsets, 4
+ * count ranges, 8 record heads, 16 entity-table indices) are OR-ed into *dev_check_status (device
+ * int32, or NULL), and an input with any bit set keeps no row (x->status bit 3). dev_expect_totals:
+ * host array of n_inputs device int64 pointers (an entry or the array NULL skips that comparison).
+ * check_mask: bit i set = check input i (an unchecked input, e.g. the root's own buffers, counts as
+ * clean). dev_ctl: device int32 [NMMO_STORE_CTL_INTS], zero before the first call; every call leaves it
+ * zero (one per stream: calls sharing it must not overlap). Any store of a buffer that lies inside
+ * the arena but not at its reserved slot is refused (x->status bit 4), never copied. */
+#define NMMO_STORE_CTL_INTS 17
+NMMO_API int nmmo_exp_store_records_checked(NmmoHandle* h, const NmmoExperience* x, const NmmoRecordStore* rs,
+                                            const NmmoStoreInput* ins, int32_t n_inputs, int32_t field_stride,
+                                            const int64_t* const* dev_expect_totals, uint32_t check_mask,
+                                            int32_t* dev_check_status, int32_t* dev_ctl, int32_t* scratch,
+                                            void* stream);
 /* out (device float32 [n][obs_elems]) = the flat rows of experience rows idx[0..n) (device
  * int32) stored by nmmo_exp_store_records; h: the handle whose task table the records' task
  * indices refer to. Enqueued. */

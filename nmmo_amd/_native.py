@@ -29,7 +29,7 @@ SYMBOLS = [
     "nmmo_step_envs", "nmmo_inject_fault", "nmmo_fault_into", "nmmo_exp_store_records",
     "nmmo_exp_gather_records", "nmmo_exp_store_records_many", "nmmo_obs_invalidate", "nmmo_set_obs_counter",
     "nmmo_obs_bind", "nmmo_obs_invalidate_envs", "nmmo_exp_scratch_ints_many", "nmmo_set_step_records",
-    "nmmo_wire_check_many",
+    "nmmo_wire_check_many", "nmmo_exp_store_records_checked",
 ]
 
 
@@ -111,6 +111,8 @@ def declare(L):
     L.nmmo_exp_store_records.argtypes = [vp, xp, rsp, ctypes.POINTER(abi.NmmoStoreInput), vp, vp]
     L.nmmo_exp_gather_records.argtypes = [vp, xp, rsp, vp, i32, vp, vp]
     L.nmmo_exp_store_records_many.argtypes = [vp, xp, rsp, ctypes.POINTER(abi.NmmoStoreInput), i32, i32, vp, vp]
+    L.nmmo_exp_store_records_checked.argtypes = [vp, xp, rsp, ctypes.POINTER(abi.NmmoStoreInput), i32, i32, vp,
+                                                 ctypes.c_uint32, vp, vp, vp, vp]
     L.nmmo_exp_gae.argtypes = [xp, vp, i32, ctypes.c_double, ctypes.c_double, vp, vp]
     L.nmmo_gather_rows.argtypes = [vp, ctypes.c_int64, vp, i32, vp, vp]
     L.nmmo_n_envs.argtypes = [vp]

@@ -53,18 +53,27 @@ def build(force: bool = False, verbose: bool = False, stamps: bool = False) -> s
         return LIB_PATH
     os.makedirs(LIB_DIR, exist_ok=True)
     tmp = out + ".tmp"
-    cmd = [
-        _hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-        "-fvisibility=hidden", "-Wall", "-Werror",
+    flags = [
+        f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden", "-Wall", "-Werror",
         # no FMA contraction: hipcc contracts even __dadd_rn(__dmul_rn(..)) pairs, and the float /
         # double reward, wrapper and advantage arithmetic must round op by op like the oracle
         "-ffp-contract=off", *(["-DNMMO_STAMPS"] if stamps else []),
         f'-DNMMO_SRC_HASH="{source_hash()}"',
-        *[os.path.join(CSRC, f) for f in SOURCES], "-o", tmp,
     ]
-    if verbose:
-        print(" ".join(cmd), file=sys.stderr)
-    subprocess.check_call(cmd)
+    # one hipcc per source in parallel (every kernel lives in its own translation unit), then link
+    import concurrent.futures
+    import tempfile
+
+    with tempfile.TemporaryDirectory(prefix="nmmo_build_") as d:
+        objs = [os.path.join(d, f + ".o") for f in SOURCES]
+        cmds = [[_hipcc(), *flags, "-c", os.path.join(CSRC, f), "-o", o] for f, o in zip(SOURCES, objs)]
+        if verbose:
+            print("\n".join(" ".join(c) for c in cmds), file=sys.stderr)
+        jobs = max(1, min(len(cmds), os.cpu_count() or 1, int(os.environ.get("MAX_JOBS", "8"))))
+        with concurrent.futures.ThreadPoolExecutor(jobs) as ex:
+            for f in [ex.submit(subprocess.check_call, c) for c in cmds]:
+                f.result()
+        subprocess.check_call([_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", tmp])
     os.replace(tmp, out)
     return out
 

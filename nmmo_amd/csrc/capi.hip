@@ -760,9 +760,9 @@ int nmmo_exp_store_records(NmmoHandle* h, const NmmoExperience* x, const NmmoRec
   return NMMO_OK;
 }
 
-int nmmo_exp_store_records_many(NmmoHandle* h, const NmmoExperience* x, const NmmoRecordStore* rs,
-                                const NmmoStoreInput* ins, int32_t n_inputs, int32_t field_stride, int32_t* scratch,
-                                void* stream) {
+static int store_records_many(NmmoHandle* h, const NmmoExperience* x, const NmmoRecordStore* rs, const NmmoStoreInput* ins,
+                              int32_t n_inputs, int32_t field_stride, int32_t* scratch, void* stream,
+                              const StoreCheck* chk) {
   if (int rc = check_exp(x, false)) return rc;
   if (int rc = check_records(rs)) return rc;
   if (!h || !ins || !scratch) return fail(NMMO_E_INVALID, "null handle/inputs/scratch");
@@ -786,8 +786,28 @@ int nmmo_exp_store_records_many(NmmoHandle* h, const NmmoExperience* x, const Nm
     b.wire_cap[i] = nmmo_wire_max_bytes(in.n_rows / h->st.P, h->st.P);
   }
   HIP_TRY(hipSetDevice(h->device));
-  HIP_TRY(launch_store_records_many(*x, *rs, b, scratch, (hipStream_t)stream));
+  HIP_TRY(launch_store_records_many(*x, *rs, b, scratch, (hipStream_t)stream, chk));
   return NMMO_OK;
+}
+
+int nmmo_exp_store_records_many(NmmoHandle* h, const NmmoExperience* x, const NmmoRecordStore* rs,
+                                const NmmoStoreInput* ins, int32_t n_inputs, int32_t field_stride, int32_t* scratch,
+                                void* stream) {
+  return store_records_many(h, x, rs, ins, n_inputs, field_stride, scratch, stream, nullptr);
+}
+
+int nmmo_exp_store_records_checked(NmmoHandle* h, const NmmoExperience* x, const NmmoRecordStore* rs,
+                                   const NmmoStoreInput* ins, int32_t n_inputs, int32_t field_stride,
+                                   const int64_t* const* dev_expect_totals, uint32_t check_mask,
+                                   int32_t* dev_check_status, int32_t* dev_ctl, int32_t* scratch, void* stream) {
+  if (!dev_ctl) return fail(NMMO_E_INVALID, "dev_ctl must be a device int32 [%d]", NMMO_STORE_CTL_INTS);
+  StoreCheck chk;
+  memset(&chk, 0, sizeof(chk));
+  for (int i = 0; i < n_inputs && i < kMaxStoreInputs; i++) chk.expect[i] = dev_expect_totals ? dev_expect_totals[i] : nullptr;
+  chk.status = dev_check_status;
+  chk.ctl = dev_ctl;
+  chk.mask = check_mask;
+  return store_records_many(h, x, rs, ins, n_inputs, field_stride, scratch, stream, &chk);
 }
 
 int nmmo_exp_gather_records(NmmoHandle* h, const NmmoExperience* x, const NmmoRecordStore* rs, const int32_t* idx,

@@ -216,9 +216,16 @@ struct StoreBatch {
   int n, P;
   int stride;  // bytes between consecutive rows' reward / done / mask (0: packed float / u8 arrays)
 };
+// the fused received-buffer check of the learner root's store (nmmo_exp_store_records_checked)
+struct StoreCheck {
+  const int64_t* expect[kMaxStoreInputs];  // each input's announced total (device), or NULL
+  int* status;                             // the check bits of every input (nmmo_wire_check's), or NULL
+  int* ctl;                                // [1 + kMaxStoreInputs]: ticket, per-input bits; zero, left zero
+  uint32_t mask;                           // bit i: check input i (an unchecked input counts as clean)
+};
 int store_many_scratch_ints(int n_inputs, int max_rows);
 hipError_t launch_store_records_many(const NmmoExperience& x, const NmmoRecordStore& rs, const StoreBatch& b,
-                                     int* scratch, hipStream_t stream);
+                                     int* scratch, hipStream_t stream, const StoreCheck* chk = nullptr);
 // flat rows of stored record rows (wire.hip)
 hipError_t launch_record_gather(const ObsParams& p, const NmmoRecordStore& rs, const int32_t* idx, int n,
                                 float* out, hipStream_t stream);

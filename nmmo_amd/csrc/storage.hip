@@ -233,9 +233,12 @@ __global__ void record_reserve_kernel(NmmoExperience x, NmmoRecordStore rs, cons
                                       int64_t wire_cap, int* gate, int64_t* rbase) {
   const int64_t total = *reinterpret_cast<const int64_t*>(wire);
   const int64_t base = (*rs.arena_used + 15) & ~(int64_t)15;
-  const bool ok = total >= wire_header_bytes(n_envs, P) && total <= wire_cap && (total & 15) == 0 &&
-                  base + 16 + total <= rs.arena_bytes;
-  *gate = ok ? (wire == rs.arena + base + 16 ? 2 : 1) : 0;  // 2: the buffer is in place already
+  const bool sane = total >= wire_header_bytes(n_envs, P) && total <= wire_cap && (total & 15) == 0 &&
+                    base + 16 + total <= rs.arena_bytes;
+  // a buffer inside the arena is stored only at its own slot (record_reserve_serial)
+  const bool inside = wire >= rs.arena && wire < rs.arena + rs.arena_bytes, placed = wire == rs.arena + base + 16;
+  const bool ok = sane && (!inside || placed);
+  *gate = ok ? (placed ? 2 : 1) : 0;  // 2: the buffer is in place already
   *rbase = base;
   if (ok) {
     int64_t* d = reinterpret_cast<int64_t*>(rs.arena + base);
@@ -243,7 +246,7 @@ __global__ void record_reserve_kernel(NmmoExperience x, NmmoRecordStore rs, cons
     d[1] = P;
     *rs.arena_used = base + 16 + total;
   } else if (x.status) {
-    atomicOr(x.status, 2);
+    atomicOr(x.status, sane ? 16 : 2);
   }
 }
 
@@ -295,18 +298,30 @@ __device__ __forceinline__ bool sb_selected(const NmmoExperience& x, const Store
   return false;
 }
 
-__global__ void record_reserve_many_kernel(NmmoExperience x, NmmoRecordStore rs, StoreBatch b, int* gates,
-                                           int64_t* rbase) {
+// The serial reservation of every input, in input order (one thread). An input is stored when its
+// announced total is a plausible buffer (>= its header, <= its capacity bound, 16-B multiple), it
+// fits, and (ist, the fused check's per-input bits, when given) it passed its check. gates[i]: 2 =
+// the buffer already sits where it is to be stored (received straight into the arena), 1 = copy
+// it there, 0 = not stored (x.status bit 2: no room / not plausible; bit 3: failed its check;
+// bit 4: the buffer lies inside the arena but not at its reserved slot -- a copy would read arena
+// bytes that earlier inputs of this store overwrite, so it is refused, never copied).
+__device__ void record_reserve_serial(const NmmoExperience& x, const NmmoRecordStore& rs, const StoreBatch& b,
+                                      int* gates, int64_t* rbase, const int* ist) {
   int64_t used = *rs.arena_used;
+  const uint8_t* a0 = rs.arena;
   for (int i = 0; i < b.n; i++) {
     const NmmoStoreInput& in = b.in[i];
     const int n_envs = in.n_rows / b.P;
-    const int64_t total = *reinterpret_cast<const int64_t*>(in.wire);
+    const uint8_t* w = reinterpret_cast<const uint8_t*>(in.wire);
+    const int64_t total = *reinterpret_cast<const int64_t*>(w);
     const int64_t base = (used + 15) & ~(int64_t)15;
-    const bool ok = total >= wire_header_bytes(n_envs, b.P) && total <= b.wire_cap[i] && (total & 15) == 0 &&
-                    base + 16 + total <= rs.arena_bytes;
-    // 2: the buffer already sits where it is to be stored (received straight into the arena)
-    gates[i] = ok ? (reinterpret_cast<const uint8_t*>(in.wire) == rs.arena + base + 16 ? 2 : 1) : 0;
+    const bool sane = total >= wire_header_bytes(n_envs, b.P) && total <= b.wire_cap[i] && (total & 15) == 0 &&
+                      base + 16 + total <= rs.arena_bytes;
+    const bool checked = !ist || __hip_atomic_load(&ist[i], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0;
+    const bool inside = w >= a0 && w < a0 + rs.arena_bytes;
+    const bool placed = w == a0 + base + 16;
+    const bool ok = sane && checked && (!inside || placed);
+    gates[i] = ok ? (placed ? 2 : 1) : 0;
     rbase[i] = base;
     if (ok) {
       int64_t* d = reinterpret_cast<int64_t*>(rs.arena + base);
@@ -314,10 +329,45 @@ __global__ void record_reserve_many_kernel(NmmoExperience x, NmmoRecordStore rs,
       d[1] = b.P;
       used = base + 16 + total;
     } else if (x.status) {
-      atomicOr(x.status, 2);
+      atomicOr(x.status, !sane ? 2 : !checked ? 8 : 16);
     }
   }
   *rs.arena_used = used;
+}
+
+__global__ void record_reserve_many_kernel(NmmoExperience x, NmmoRecordStore rs, StoreBatch b, int* gates,
+                                           int64_t* rbase) {
+  record_reserve_serial(x, rs, b, gates, rbase, nullptr);
+}
+
+// The fused root pass (nmmo_exp_store_records_checked): block (env, input) runs the received-buffer
+// check of one env (wire_check_env, the bits of nmmo_wire_check_many) into the input's status word
+// and the caller's; the launch's last block to finish (an agent-scope ticket) then reserves every
+// input, storing only the ones whose check came back clean. ctl = [ticket, ist[16]], zero on entry
+// and left zero.
+__global__ void __launch_bounds__(128) record_check_reserve_kernel(NmmoExperience x, NmmoRecordStore rs, StoreBatch b,
+                                                                   StoreCheck c, int* gates, int64_t* rbase) {
+  const int i = blockIdx.y, e = blockIdx.x;
+  const int n_envs = b.in[i].n_rows / b.P;
+  int* ist = c.ctl + 1;
+  if (e < n_envs && ((c.mask >> i) & 1u)) {  // block-uniform: the check's barriers see every thread
+    const int bad = wire_check_env(reinterpret_cast<const uint8_t*>(b.in[i].wire), n_envs, b.P, c.expect[i], e);
+    if (bad) {
+      __hip_atomic_fetch_or(&ist[i], bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (c.status) atomicOr(c.status, bad);
+    }
+  }
+  __shared__ int last;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  __syncthreads();
+  if (threadIdx.x == 0)
+    last = __hip_atomic_fetch_add(c.ctl, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
+           (int)(gridDim.x * gridDim.y) - 1;
+  __syncthreads();
+  if (!last || threadIdx.x != 0) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  record_reserve_serial(x, rs, b, gates, rbase, ist);
+  for (int k = 0; k <= kMaxStoreInputs; k++) __hip_atomic_store(&c.ctl[k], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __global__ void __launch_bounds__(kStoreBlock) store_count_many_kernel(NmmoExperience x, StoreBatch b,
@@ -372,15 +422,18 @@ __global__ void __launch_bounds__(kStoreBlock) store_place_many_kernel(NmmoExper
   if (gb == (int)(gridDim.x * gridDim.y) - 1 && tid == 0) *total = min(base_total + blk_total, room);
 }
 
+// The inputs with gate 1, each copied behind its descriptor (16 B per lane, grid-stride over a 1-D
+// grid that walks every input: a store whose inputs are all in place costs one short launch).
 __global__ void __launch_bounds__(256) record_copy_many_kernel(NmmoRecordStore rs, StoreBatch b, const int* gates,
                                                               const int64_t* rbase) {
-  const int i = blockIdx.y;
-  if (gates[i] != 1) return;  // not stored, or received in place
-  const uint4* wire = reinterpret_cast<const uint4*>(b.in[i].wire);
-  const int64_t words = *reinterpret_cast<const int64_t*>(wire) / 16;
-  uint4* dst = reinterpret_cast<uint4*>(rs.arena + rbase[i] + 16);
-  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < words; k += (int64_t)gridDim.x * blockDim.x)
-    dst[k] = wire[k];
+  const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (int64_t)gridDim.x * blockDim.x;
+  for (int i = 0; i < b.n; i++) {
+    if (gates[i] != 1) continue;  // not stored, or received in place
+    const uint4* wire = reinterpret_cast<const uint4*>(b.in[i].wire);
+    const int64_t words = *reinterpret_cast<const int64_t*>(wire) / 16;
+    uint4* dst = reinterpret_cast<uint4*>(rs.arena + rbase[i] + 16);
+    for (int64_t k = t0; k < words; k += stride) dst[k] = wire[k];
+  }
 }
 
 int store_many_scratch_ints(int n_inputs, int max_rows) {
@@ -388,7 +441,7 @@ int store_many_scratch_ints(int n_inputs, int max_rows) {
 }
 
 hipError_t launch_store_records_many(const NmmoExperience& x, const NmmoRecordStore& rs, const StoreBatch& b,
-                                     int* scratch, hipStream_t stream) {
+                                     int* scratch, hipStream_t stream, const StoreCheck* chk) {
   int max_rows = 0;
   for (int i = 0; i < b.n; i++) max_rows = max(max_rows, b.in[i].n_rows);
   const int nb = store_blocks(max_rows);
@@ -396,15 +449,20 @@ hipError_t launch_store_records_many(const NmmoExperience& x, const NmmoRecordSt
   int* total = blk + b.n * nb;     // [1]
   int* gates = total + 1;          // [n]
   int64_t* rbase = reinterpret_cast<int64_t*>(scratch + ((b.n * nb + 1 + b.n + 1) & ~1));  // [n], 8-B aligned
-  hipLaunchKernelGGL(record_reserve_many_kernel, dim3(1), dim3(1), 0, stream, x, rs, b, gates, rbase);
+  if (chk) {
+    hipLaunchKernelGGL(record_check_reserve_kernel, dim3(max_rows / b.P, b.n), dim3(128), 0, stream, x, rs, b, *chk,
+                       gates, rbase);
+  } else {
+    hipLaunchKernelGGL(record_reserve_many_kernel, dim3(1), dim3(1), 0, stream, x, rs, b, gates, rbase);
+  }
   hipLaunchKernelGGL(store_count_many_kernel, dim3(nb, b.n), dim3(kStoreBlock), 0, stream, x, b, (const int*)gates,
                      blk);
   hipLaunchKernelGGL(store_place_many_kernel, dim3(nb, b.n), dim3(kStoreBlock), 0, stream, x, rs, b,
                      (const int*)gates, (const int64_t*)rbase, (const int*)blk, total);
   int64_t words = 0;
   for (int i = 0; i < b.n; i++) words = std::max(words, b.wire_cap[i] / 16);
-  const int grid = (int)std::min<int64_t>((words + 255) / 256, 1024);
-  hipLaunchKernelGGL(record_copy_many_kernel, dim3(grid > 0 ? grid : 1, b.n), dim3(256), 0, stream, rs, b,
+  const int grid = (int)std::min<int64_t>((words + 255) / 256, 2048);
+  hipLaunchKernelGGL(record_copy_many_kernel, dim3(grid > 0 ? grid : 1), dim3(256), 0, stream, rs, b,
                      (const int*)gates, (const int64_t*)rbase);
   hipLaunchKernelGGL(store_commit_kernel, dim3(1), dim3(1), 0, stream, x.ptr, total, x.capacity);
   return hipGetLastError();

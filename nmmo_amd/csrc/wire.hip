@@ -424,71 +424,17 @@ __global__ void __launch_bounds__(256) wire_unpack_kernel(const uint8_t* wire, u
   }
 }
 
-// Consistency of one received wire buffer of n envs x P agents (block per env): the announced
-// total (when expect_total is given), the env payload offsets against the count words and
-// listings, the counts' ranges, every record head's AgentId / nv / ninv against its count word
-// and its entity-table indices against the table. status bits: 1 total, 2 env offsets, 4 count
-// ranges, 8 record heads, 16 entity-table indices.
-__device__ __forceinline__ void wire_check_env(const uint8_t* wire, int n, int P, const int64_t* expect_total,
-                                               int* status, int e) {
-  WireView v = wire_view(const_cast<uint8_t*>(wire), n, P);
-  __shared__ int off[129];
-  const int a = threadIdx.x;
-  const uint16_t* cnt = v.cnt + (size_t)e * P;
-  const int ne = v.ecount[e];
-  record_offsets_wave0(cnt, P, off, wire_table_bytes(ne));
-  __syncthreads();
-  int bad = 0;
-  const int64_t total = *v.total;
-  const int64_t base = v.env_off[e];
-  const int nm = v.mcount[e];
-  if (a == 0) {
-    if (e == 0 && expect_total && total != *expect_total) bad |= 1;
-    if (e == 0 && base != wire_header_bytes(n, P)) bad |= 2;
-    const int64_t end = e + 1 < n ? v.env_off[e + 1] : total;
-    if (end - base != (int64_t)off[P] + 32 * nm) bad |= 2;
-    if (nm > NMMO_MARKET_ROWS || ne > kMaxSlots) bad |= 4;
-  }
-  if (a < P) {
-    const uint32_t c = cnt[a];
-    if (c & 0x8000u) {
-      const int nv = c & 127, ninv = (c >> 7) & 15;
-      if (nv > kNObs || ninv > kInv || (c & 0x7800u)) {
-        bad |= 4;
-      } else if (base + off[a] + kWireHead <= total) {
-        const int16_t* h = reinterpret_cast<const int16_t*>(v.base + base + off[a]);
-        if (h[0] <= 0 || h[5] != nv || (h[6] & 0xFF) != ninv || ((uint16_t)h[6] >> 8) > 1) bad |= 8;
-        if (base + off[a] + wire_record_bytes(c) <= total) {  // entity-table indices, 8 per 16-B load
-          const uint4* ix4 = reinterpret_cast<const uint4*>(h + kWireBody / 2);
-          uint4 q[(kNObs + 7) / 8];
-#pragma unroll
-          for (int j = 0; j < (kNObs + 7) / 8; j++) q[j] = 8 * j < nv ? ix4[j] : make_uint4(0u, 0u, 0u, 0u);
-#pragma unroll
-          for (int j = 0; j < (kNObs + 7) / 8; j++) {
-            const uint32_t wd[4] = {q[j].x, q[j].y, q[j].z, q[j].w};
-#pragma unroll
-            for (int i = 0; i < 8; i++)
-              if (8 * j + i < nv && ((wd[i >> 1] >> (16 * (i & 1))) & 0xFFFFu) >= (uint32_t)ne) bad |= 16;
-          }
-        }
-      } else {
-        bad |= 2;
-      }
-    } else if (c) {
-      bad |= 4;
-    }
-  }
-  if (bad) atomicOr(status, bad);
-}
 __global__ void __launch_bounds__(128) wire_check_kernel(const uint8_t* wire, int n, int P,
                                                          const int64_t* expect_total, int* status) {
-  wire_check_env(wire, n, P, expect_total, status, blockIdx.x);
+  const int bad = wire_check_env(wire, n, P, expect_total, blockIdx.x);
+  if (bad) atomicOr(status, bad);
 }
 // Every received buffer of a step in one launch: grid (max envs, buffers)
 __global__ void __launch_bounds__(128) wire_check_many_kernel(WireCheckBatch b, int P, int* status) {
   const int i = blockIdx.y;
   if ((int)blockIdx.x >= b.n[i]) return;
-  wire_check_env(b.wire[i], b.n[i], P, b.expect[i], status, blockIdx.x);
+  const int bad = wire_check_env(b.wire[i], b.n[i], P, b.expect[i], blockIdx.x);
+  if (bad) atomicOr(status, bad);
 }
 
 // Wire records -> flat float32 rows (the pufferlib row of SPEC §8; bit-identical to

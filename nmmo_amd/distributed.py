@@ -31,6 +31,27 @@ def shard(total_envs: int, world: int, rank: int):
     return rank * n, n
 
 
+def env_shares(total_envs: int, world: int, root_envs: int | None = None, granule: int = 1):
+    """Env counts per rank for a learner gather (BASELINE config 5): `root_envs` on rank 0 (the
+    learner, which also validates and stores every peer's buffers each step, so it steps fewer
+    envs of its own; None = an even split) and the rest over ranks 1..world-1 as evenly as
+    possible, every count a multiple of `granule` (the env batches per rank). Contiguous blocks in
+    rank order: rank r's env_index_base is the sum of the counts before it."""
+    if world == 1:
+        return [total_envs]
+    if root_envs is None:
+        if total_envs % world:
+            raise ValueError(f"{total_envs} envs do not split evenly over {world} ranks")
+        root_envs = total_envs // world
+    rest = total_envs - root_envs
+    if root_envs < granule or root_envs % granule or rest % granule:
+        raise ValueError(f"root_envs {root_envs} and the {rest} other envs must be positive multiples of {granule}")
+    units, extra = divmod(rest // granule, world - 1)
+    if units == 0:
+        raise ValueError(f"{rest} envs cannot give each of {world - 1} peers {granule}")
+    return [root_envs] + [(units + (1 if r < extra else 0)) * granule for r in range(world - 1)]
+
+
 def gather_to_learner(t: torch.Tensor, dst: int = 0):
     """Gather the rank-local batch `t` ([n_local, ...]) to rank `dst` as [world*n_local, ...].
     Each peer -> root transfer is a point-to-point xGMI link under RCCL (no ring)."""
@@ -87,8 +108,14 @@ class WireExchange:
 
     def __init__(self, world: int, rank: int, n_bufs: int, recv_caps, small_bytes, device, dst: int = 0,
                  ring: int = 3, backend: str | None = None):
+        """recv_caps / small_bytes: per rank a list of n_bufs sizes (each rank's buffer j may hold a
+        different env count), or one list of n_bufs sizes shared by every rank."""
         self.world, self.rank, self.dst, self.ring = world, rank, dst, ring
         self.n_bufs = n_bufs
+        if recv_caps and not isinstance(recv_caps[0], (list, tuple)):
+            recv_caps = [list(recv_caps)] * world
+        if small_bytes and not isinstance(small_bytes[0], (list, tuple)):
+            small_bytes = [list(small_bytes)] * world
         self.device = torch.device(device)
         self.cuda = self.device.type == "cuda"
         self.staged = (backend or (dist.get_backend() if world > 1 else "nccl")) == "gloo" and self.cuda
@@ -96,7 +123,7 @@ class WireExchange:
         # [.., n_bufs] = the rank's tick fault word of the step
         self.sizes = torch.zeros((ring, world, n_bufs + 1), dtype=torch.int64, device=d)
         self.sizes_host = torch.zeros((ring, world, n_bufs + 1), dtype=torch.int64, pin_memory=self.cuda)
-        self.caps = [int(c) for c in recv_caps]
+        self.caps = [[int(c) for c in row] for row in recv_caps]  # [rank][buffer] capacity bound
         self.comm = torch.cuda.Stream(device=d) if self.cuda else None
         self._sized = [None] * ring
         self._done = [None] * ring
@@ -105,8 +132,8 @@ class WireExchange:
         if rank == dst:
             for r in self.peers:
                 for j in range(n_bufs):
-                    self.recv_wire[r, j] = torch.empty(int(recv_caps[j]), dtype=torch.uint8, device=d)
-                    self.recv_small[r, j] = torch.empty(int(small_bytes[j]), dtype=torch.uint8, device=d)
+                    self.recv_wire[r, j] = torch.empty(int(recv_caps[r][j]), dtype=torch.uint8, device=d)
+                    self.recv_small[r, j] = torch.empty(int(small_bytes[r][j]), dtype=torch.uint8, device=d)
         self.payload_bytes = 0  # wire bytes received by the root (all peers, all steps)
 
     # -- plumbing
@@ -190,8 +217,8 @@ class WireExchange:
                 raise TickFault(int(tot[r][self.n_bufs]), f"learner gather, rank {r}, step {t}")
             for j in range(self.n_bufs):
                 n = int(tot[r][j])
-                if n < 16 or n > self.caps[j]:
-                    raise RuntimeError(f"rank {r} buffer {j} announces {n} B at step {t} (capacity {self.caps[j]})")
+                if n < 16 or n > self.caps[r][j]:
+                    raise RuntimeError(f"rank {r} buffer {j} announces {n} B at step {t} (capacity {self.caps[r][j]})")
         got = {}
         if self.rank == self.dst:
             for j in range(self.n_bufs):
@@ -241,6 +268,10 @@ class WireGather:
     transfer overlaps step t + 1's compute (reference: the recv -> store loop of
     clean_pufferl.py:293-346, fed here by every GPU of the node).
 
+    Ranks may hold different env counts (`env_shares`: the learner root fewer, the peers the
+    rest); every rank has the same number of batches and the same task table, and the root learns
+    each rank's batch sizes once at construction. Global env ids are contiguous in rank order.
+
     On the root, each step's buffers are validated on the device (nmmo_wire_check: sizes,
     offsets, count words, record heads; `status` accumulates) — "delivered": every agent's
     observation landed, checked, in the learner's HBM, in the form the experience store decodes
@@ -248,7 +279,9 @@ class WireGather:
     rank's buffers into the native layout (nmmo_wire_unpack, the full learner-ready tensor) on
     the comm stream. store=DeviceExperience (root; compact record storage) stores every step's
     learner rows (the agents in the realm) from every received buffer on the comm stream — the
-    root's real work per step, clean_pufferl.py:331-346 — as a batch of its own (reset each step).
+    root's real work per step, clean_pufferl.py:331-346 — as a batch of its own (reset each step),
+    with the check fused into the store's reservation pass (nmmo_exp_store_records_checked: a
+    buffer that fails keeps no row), the peers' buffers received straight into their arena slots.
     on_step(t, got) (tests) runs on the root after step t's buffers landed, with the device
     synchronised: got = {(rank, batch): (wire bytes, smalls)}.
 
@@ -258,14 +291,20 @@ class WireGather:
 
     def __init__(self, engines, policy_seed: int, rank: int = 0, world: int = 1, decode: bool = False,
                  graphs: bool = True, ring: int = 3, on_step=None, backend: str | None = None,
-                 before_step=None, store=None, rehearse: int = 0):
-        """rehearse = R > 0 (root): after its real buffers, the root also treats R phantom peers'
-        buffers each step -- its own step's buffers copied into receive buffers (the HBM writes of
-        the incoming transfers), validated (nmmo_wire_check), decoded / stored as a peer's -- so a
-        one-GPU run carries the root's compute load of an N = R + 1 node (bench.py
-        --root-rehearsal; the xGMI links themselves are not modelled)."""
+                 before_step=None, store=None, rehearse: int = 0, phantom=None, rehearse_mode: str = "fill"):
+        """rehearse = R > 0 (root, one GPU): the root also takes R phantom peers' buffers every
+        step, so a one-GPU run carries the root's load of an N = world + R node. phantom: per batch
+        j a (wire bytes, smalls, n_envs) snapshot of a peer's buffers (e.g. a rank of the node's
+        peer share stepped beforehand); each phantom peer q "receives" that content every step:
+        rehearse_mode "fill" stands in for the incoming transfers with write-only fills of the
+        same bytes (the received data's HBM writes; the content sits in the record arena once,
+        so the check and store read valid buffers in place), "copy" copies the snapshot into its
+        arena slot every step (read + write: what a receive through an intermediate buffer costs).
+        The phantoms are validated and stored like real peers (the xGMI links are not modelled)."""
         if before_step is not None and graphs:
             raise ValueError("before_step needs graphs=False")
+        if rehearse_mode not in ("fill", "copy"):
+            raise ValueError("rehearse_mode: fill or copy")
         self.before_step = before_step
         from . import abi, devmem
         from . import wire as nw
@@ -286,33 +325,41 @@ class WireGather:
             if not np.array_equal(e.task_table, e0.task_table):
                 raise ValueError("WireGather: the batches' task tables differ (records decode with one table)")
         nb = len(self.engines)
-        # the root sizes its receive buffers from its own batches, places buffer (r, j)'s rows at
-        # global agent slot (r * envs + env offset of batch j) * P and decodes every buffer with its
-        # own task table: every rank must have the same batches and task table (checked once here)
-        self._env0 = [0]
-        for e in self.engines:
-            self._env0.append(self._env0[-1] + e.n_envs)
+        # every rank's batch sizes (the root sizes its receive buffers and places each buffer's
+        # rows from them) and one task table for all (the root decodes every buffer with its own)
+        mine = [e.n_envs for e in self.engines]
+        self.counts = [mine]
         if world > 1:
             import zlib
 
-            shape = np.asarray([e.n_envs for e in self.engines], np.int64)
-            sig = torch.tensor([nb, int(shape.sum()), zlib.crc32(shape.tobytes()),
-                                zlib.crc32(np.ascontiguousarray(e0.task_table, np.float32).tobytes())],
-                               dtype=torch.int64, device=self.device)
+            crc = zlib.crc32(np.ascontiguousarray(e0.task_table, np.float32).tobytes())
+            sig = torch.tensor([nb, crc], dtype=torch.int64, device=self.device)
             lo, hi = sig.clone(), sig.clone()
             dist.all_reduce(lo, op=dist.ReduceOp.MIN)
             dist.all_reduce(hi, op=dist.ReduceOp.MAX)
             if not torch.equal(lo, hi):
-                raise ValueError("WireGather: ranks differ in their env batches or task table (the root receives "
-                                 "and decodes every rank's buffers with its own)")
+                raise ValueError("WireGather: ranks differ in their number of env batches or task table (the root "
+                                 "receives every rank's buffers and decodes them with its own table)")
+            row = torch.zeros(world, nb, dtype=torch.int64, device=self.device)
+            row[rank] = torch.tensor(mine, dtype=torch.int64)
+            dist.all_reduce(row, op=dist.ReduceOp.SUM)
+            self.counts = row.tolist()
+        self.counts = [[int(c) for c in r] for r in self.counts]
+        # global env id of (rank r, batch j)'s first env: contiguous blocks in rank order
+        self.env_base = {}
+        acc = 0
+        for r in range(world):
+            for j in range(nb):
+                self.env_base[r, j] = acc
+                acc += self.counts[r][j]
         self.ring = ring
         self.wires = [[e.obs] + [devmem.empty(tuple(e.obs.shape), torch.uint8, self.device) for _ in range(ring - 1)]
                       for e in self.engines]
         self.smalls = [[torch.zeros((e.n_envs, self.P, 8), dtype=torch.uint8, device=self.device) for _ in range(ring)]
                        for e in self.engines]
-        caps = [nw.max_bytes(e.n_envs, self.P) for e in self.engines]
-        self.x = WireExchange(world, rank, nb, caps, [s[0].numel() for s in self.smalls], self.device,
-                              ring=ring, backend=backend)
+        caps = [[nw.max_bytes(c, self.P) for c in row] for row in self.counts]
+        self.x = WireExchange(world, rank, nb, caps, [[c * self.P * 8 for c in row] for row in self.counts],
+                              self.device, ring=ring, backend=backend)
         self.streams = [torch.cuda.Stream(device=self.device) for _ in self.engines]
         self.status = torch.zeros(1, dtype=torch.int32, device=self.device)
         # per ring slot: the first tick fault word of the step's batches (nmmo_fault_into), shipped
@@ -321,22 +368,61 @@ class WireGather:
         self._posted = -1  # the last step whose payload was posted
         self.native = None
         if decode and rank == 0:
-            n_envs = [e.n_envs for e in self.engines]
-            self.native = {(r, j): devmem.empty((n_envs[j], abi.native_env_bytes(self.P)), torch.uint8, self.device)
-                           for r in range(world) for j in range(nb)}
+            self.native = {(r, j): devmem.empty((self.counts[r][j], abi.native_env_bytes(self.P)), torch.uint8,
+                                                self.device) for r in range(world) for j in range(nb)}
         self._zeros = self._acts = None
         self.rehearse = int(rehearse) if rank == 0 else 0
-        if self.rehearse:  # the phantom peers' receive buffers, one set per phantom as a real root's
-            self._rh_wire = {(q, j): devmem.empty((caps[j],), torch.uint8, self.device)
-                             for q in range(self.rehearse) for j in range(nb)}
-            self._rh_small = {(q, j): torch.empty_like(self.smalls[j][0]) for q in range(self.rehearse) for j in range(nb)}
-            self._rh_native = None if not decode else \
-                {(q, j): devmem.empty((e.n_envs, abi.native_env_bytes(self.P)), torch.uint8, self.device)
-                 for q in range(self.rehearse) for j, e in enumerate(self.engines)}
+        self.rehearse_mode = rehearse_mode
+        self._ph = []  # phantom peers' buffers: (key, arena slot or buffer, smalls, n_envs, expect)
+        if self.rehearse:
+            self._setup_phantoms(phantom, acc)
         self.graphs = None
         if graphs:
             self._capture()
         self.t = 0
+
+    def _setup_phantoms(self, phantom, env0):
+        """The rehearsal's phantom peers (see __init__): their content placed once, at the front of
+        the record arena (fixed slots, so the store finds them in place every step), or in buffers
+        of their own without a store. Phantom q's batch j takes global envs after the real ranks'."""
+        from . import abi, devmem
+
+        nb = len(self.engines)
+        if phantom is None or len(phantom) != nb:
+            raise ValueError("rehearse needs phantom = one (wire bytes, smalls, n_envs) per batch")
+        d = self.device
+        used = 0
+        arena = self.store.arena if self.store is not None else None
+        keys = [(self.world - 1 + q, j) for q in range(1, self.rehearse + 1) for j in range(nb)]
+        self._rh_src = []
+        sink = 0
+        for (r, j) in keys:
+            w0, sm0, n = phantom[j]
+            w0 = w0.view(-1)
+            tot = int(w0[:8].view(torch.int64)[0].item())
+            if tot != w0.numel() or tot & 15:
+                raise ValueError("phantom wire bytes must be one whole buffer (its announced total)")
+            if arena is not None:
+                base = (used + 15) & ~15
+                if base + 16 + tot > arena.numel():
+                    raise ValueError("the record arena cannot hold the phantom peers' buffers")
+                w = arena[base + 16:base + 16 + tot]
+                used = base + 16 + tot
+            else:
+                w = devmem.empty((tot,), torch.uint8, d)
+            w.copy_(w0)
+            sm = sm0.clone()
+            expect = torch.tensor([tot], dtype=torch.int64, device=d)
+            self._ph.append(((r, j), w, sm, int(n), expect))
+            self._rh_src.append(w0.clone() if self.rehearse_mode == "copy" else None)
+            sink += tot + sm.numel()
+            self.env_base[r, j] = env0
+            env0 += int(n)
+        self._ph_arena_end = used
+        # "fill": one write-only region as large as a step's phantom transfers
+        self._sink = torch.empty(sink, dtype=torch.uint8, device=d) if self.rehearse_mode == "fill" else None
+        self._rh_native = None if not self.decode else \
+            {key: devmem.empty((n, abi.native_env_bytes(self.P)), torch.uint8, d) for key, _, _, n, _ in self._ph}
 
     def _body(self, j: int, k: int):
         e = self.engines[j]
@@ -355,7 +441,14 @@ class WireGather:
                 with torch.cuda.graph(g, stream=self.streams[j]):
                     self._body(j, k)
                 self.graphs[j, k] = g
+        # each graph keeps the step-record pointers it captured; the handles forget them, so an
+        # eager step later cannot write into a ring slot the comm stream may still be sending
+        for e in self.engines:
+            e.set_step_records(None)
         torch.cuda.synchronize(self.device)
+
+    def _n_envs(self, r, j):
+        return self.counts[r][j] if r < self.world else next(n for key, _, _, n, _ in self._ph if key == (r, j))
 
     def _consume(self, s: int, got, plan=None):
         """On the comm stream, after step s's buffers landed on the root."""
@@ -365,39 +458,41 @@ class WireGather:
             return
         with torch.cuda.stream(self.x.comm):
             nb = len(self.engines)
+            items = []  # (key, (wire, smalls), expect or None, check?) in the arena's store order
+            if self._ph:  # the phantom peers' transfers of this step, then their buffers in place
+                if self._sink is not None:
+                    self._sink.fill_(s & 0xFF)
+                for (key, w, sm, n, expect), src in zip(self._ph, self._rh_src):
+                    if src is not None:
+                        w.copy_(src)
+                    items.append((key, (w, sm), expect, True))
+            items += [((0, j), got[0, j], None, False) for j in range(nb)]
+            items += [((r, j), got[r, j], self.x.sizes[s % self.ring, r, j:j + 1], True)
+                      for r in range(1, self.world) for j in range(nb)]
+            if self.store is None:  # every received buffer against its announced size, up to 16 per launch
+                recv = [(w, self._n_envs(*key), ex) for key, (w, sm), ex, chk in items if chk]
+                for k in range(0, len(recv), 16):
+                    nw.check_buffers(recv[k:k + 16], self.P, self.status)
             batch = []
-            items = list(got.items())
-            for q in range(1, self.rehearse + 1):  # phantom peer q: the root's own buffers, copied in
-                for j in range(nb):
-                    w0, sm0 = got[0, j]
-                    key = (self.world - 1 + q, j)
-                    w = plan[key] if plan is not None else self._rh_wire[q - 1, j][:w0.numel()]
-                    sm = self._rh_small[q - 1, j]
-                    w.copy_(w0)
-                    sm.copy_(sm0)
-                    items.append((key, (w, sm)))
-            # every received buffer against the size its sender announced, up to 16 per launch
-            recv = [(w, self.engines[j].n_envs, self.x.sizes[s % self.ring, r if r < self.world else 0, j:j + 1])
-                    for (r, j), (w, sm) in items if r != 0]
-            for k in range(0, len(recv), 16):
-                nw.check_buffers(recv[k:k + 16], self.P, self.status)
-            for (r, j), (w, sm) in items:
-                n = self.engines[j].n_envs
+            for key, (w, sm), ex, chk in items:
+                n = self._n_envs(*key)
                 if self.native is not None:
-                    nw.unpack(w, n, self.P, out=self.native[r, j] if r < self.world else
-                              self._rh_native[r - self.world, j])
+                    nw.unpack(w, n, self.P, out=self.native[key] if key[0] < self.world else self._rh_native[key])
                 if self.store is not None:  # learner mask = in the realm; no policy outputs modelled
                     if self._zeros is None or self._zeros.numel() < n * self.P:
                         self._zeros = torch.zeros(n * self.P, device=self.device)
                         self._acts = torch.zeros((n * self.P, 12), dtype=torch.int32, device=self.device)
                     z = self._zeros[:n * self.P]
-                    base = (r * self._env0[-1] + self._env0[j]) * self.P  # global slot of the buffer's first row
                     st = sm.view(-1)  # 8 B per agent: reward f32 | term | trunc | mask | pad
-                    batch.append((w, st, st[4:], st[6:], self._acts[:n * self.P], z, z, base))
-            if self.store is not None:  # every buffer of the step as one store (fixed launch count)
+                    batch.append(((w, st, st[4:], st[6:], self._acts[:n * self.P], z, z, self.env_base[key] * self.P),
+                                  ex, chk))
+            if self.store is not None:  # every buffer of the step as one store, checked in its reservation
                 self.store.reset()
                 for k in range(0, len(batch), 16):
-                    self.store.store_many(batch[k:k + 16], s + 1, self.engines[0], field_stride=8)
+                    part = batch[k:k + 16]
+                    self.store.store_many([b for b, _, _ in part], s + 1, self.engines[0], field_stride=8,
+                                          expect=[ex for _, ex, _ in part], check_status=self.status,
+                                          check=[c for _, _, c in part])
                 self._stored += self.store.ptr_dev[0].to(torch.int64)
         if self.on_step is not None:
             torch.cuda.synchronize(self.device)
@@ -427,24 +522,26 @@ class WireGather:
         self.t += 1
 
     def _arena_plan(self, s: int):
-        """The root's record arena layout of step s, on the host: the store writes its inputs in
-        batch order (the root's own buffers, every peer's, the rehearsal's phantoms), each at the
-        16-B-aligned end of the last plus a 16-B descriptor (storage.hip record_reserve_many_kernel;
-        the arena restarts every step). Received buffers go straight to their positions, so the
-        store finds them in place and copies only the root's own -- instead of receiving into the
-        exchange's buffers and copying every one into the arena. None when the step does not fit
-        (the store then copies, and flags what does not fit, as without a plan)."""
+        """The root's record arena layout of step s, on the host: the store reserves its inputs in
+        order (the rehearsal's phantoms at their fixed slots, the root's own buffers, every peer's),
+        each at the 16-B-aligned end of the last plus a 16-B descriptor, with the plausibility rules
+        of storage.hip record_reserve_serial (the arena restarts every step). Received buffers go
+        straight to their slots, so the store finds them in place and copies only the root's own —
+        instead of receiving into the exchange's buffers and copying every one into the arena.
+        None when any buffer would not be reserved (implausible size, no room): the step is then
+        received into the exchange's buffers and copied, and the store flags what it refuses —
+        a plan that shifted later slots would have them refused as misplaced."""
+        from . import wire as nw
+
         if self.store is None or self.store.records is None:
             return None
         tot = self.x.totals(s)
         nb = len(self.engines)
-        keys = [(0, j) for j in range(nb)] + [(r, j) for r in range(1, self.world) for j in range(nb)] + \
-               [(self.world - 1 + q, j) for q in range(1, self.rehearse + 1) for j in range(nb)]
-        used, plan = 0, {}
+        used, plan = (self._ph_arena_end if self._ph else 0), {}
         cap = self.store.arena.numel()
-        for (r, j) in keys:
-            n = int(tot[r if r < self.world else 0][j])
-            if n & 15 or n > self.x.caps[j]:
+        for (r, j) in [(0, j) for j in range(nb)] + [(r, j) for r in range(1, self.world) for j in range(nb)]:
+            n = int(tot[r][j])
+            if n & 15 or n > self.x.caps[r][j] or n < nw.header_bytes(self.counts[r][j], self.P):
                 return None
             base = (used + 15) & ~15
             if base + 16 + n > cap:
@@ -483,7 +580,7 @@ class WireGather:
         return n
 
     def check_status(self):
-        """The accumulated nmmo_wire_check bits (0 = every received buffer was consistent)."""
+        """The accumulated received-buffer check bits (0 = every received buffer was consistent)."""
         return int(self.status.item())
 
     def close(self):

@@ -176,13 +176,20 @@ class DeviceExperience:
         # keep the inputs alive until the kernels that read them have been enqueued
         self._inflight = (r_, d_, m_, lp, v, a, eid, obs_flat, obs_nat, obs_wire)
 
-    def store_many(self, inputs, step: int, engine, field_stride: int = 0):
+    def store_many(self, inputs, step: int, engine, field_stride: int = 0, expect=None, check_status=None,
+                   check=None):
         """Several wire buffers stored as one store, in input order (compact storage only;
         nmmo_exp_store_records_many: a fixed number of launches for up to 16 buffers, e.g. every
         rank's buffers of a step at the learner). inputs: (wire, rewards, dones, mask, actions,
         logprobs, values, env_id_base) per buffer, all device tensors already in their final
         dtype; field_stride > 0: rewards / dones / mask are byte views read field_stride bytes
-        apart per row (the gather's packed 8-B per-agent smalls)."""
+        apart per row (the gather's packed 8-B per-agent smalls).
+
+        check_status (device int32 [1]) fuses the received-buffer check into the store
+        (nmmo_exp_store_records_checked): every input is validated as nmmo_wire_check_many does,
+        its bits OR-ed into check_status, and an input that fails keeps no row. expect: per
+        input a device int64 [1] announced total, or None; check: per input whether to check it
+        (default all; an unchecked input, e.g. the root's own buffer, counts as clean)."""
         if self.records is None:
             raise ValueError("store_many needs compact (record) storage")
         n = len(inputs)
@@ -198,9 +205,26 @@ class DeviceExperience:
         self._ensure_scratch(rows, n, max(a.shape[0] for _, _, _, _, a, _, _, _ in inputs))
         self._engine = engine
         with torch.cuda.device(self.device):
-            check(lib().nmmo_exp_store_records_many(engine.h, ctypes.byref(self.x), ctypes.byref(self.records), arr, n,
-                                                    int(field_stride), _p(self.scratch), self._stream()),
-                  "nmmo_exp_store_records_many")
+            if check_status is None:
+                check(lib().nmmo_exp_store_records_many(engine.h, ctypes.byref(self.x), ctypes.byref(self.records), arr,
+                                                        n, int(field_stride), _p(self.scratch), self._stream()),
+                      "nmmo_exp_store_records_many")
+            else:
+                if check_status.dtype != torch.int32 or check_status.device != self.device:
+                    raise ValueError("check_status must be a device int32 tensor on the store's device")
+                ex = list(expect) if expect is not None else [None] * n
+                if len(ex) != n or any(e is not None and (e.dtype != torch.int64 or e.device != self.device)
+                                       for e in ex):
+                    raise ValueError("expect: one device int64 [1] (or None) per input")
+                exp_arr = (ctypes.c_void_p * n)(*[None if e is None else e.data_ptr() for e in ex])
+                mask = sum(1 << i for i in range(n) if check is None or check[i])
+                if getattr(self, "_ctl", None) is None:  # zero; every call leaves it zero
+                    self._ctl = torch.zeros(abi.STORE_CTL_INTS, dtype=torch.int32, device=self.device)
+                check(lib().nmmo_exp_store_records_checked(engine.h, ctypes.byref(self.x), ctypes.byref(self.records),
+                                                           arr, n, int(field_stride), exp_arr, mask, _p(check_status),
+                                                           _p(self._ctl), _p(self.scratch), self._stream()),
+                      "nmmo_exp_store_records_checked")
+                keep.append(ex)
         self._inflight = keep
 
     # -- train side (clean_pufferl.py:413-458)

@@ -317,6 +317,14 @@ NMMO_API int nmmo_exp_store_records_many(NmmoHandle* h, const NmmoExperience* x,
   (void)h; (void)x; (void)rs; (void)ins; (void)n_inputs; (void)field_stride; (void)scratch; (void)stream;
   UNSUPPORTED("nmmo_exp_store_records_many");
 }
+NMMO_API int nmmo_exp_store_records_checked(NmmoHandle* h, const NmmoExperience* x, const NmmoRecordStore* rs,
+                                            const NmmoStoreInput* ins, int32_t n_inputs, int32_t field_stride,
+                                            const int64_t* const* e, uint32_t m, int32_t* cs, int32_t* ctl,
+                                            int32_t* scratch, void* stream) {
+  (void)h; (void)x; (void)rs; (void)ins; (void)n_inputs; (void)field_stride; (void)e; (void)m; (void)cs; (void)ctl;
+  (void)scratch; (void)stream;
+  UNSUPPORTED("nmmo_exp_store_records_checked");
+}
 NMMO_API int nmmo_exp_gather_records(NmmoHandle* h, const NmmoExperience* x, const NmmoRecordStore* rs,
                                      const int32_t* idx, int32_t n, float* out, void* stream) {
   (void)h; (void)x; (void)rs; (void)idx; (void)n; (void)out; (void)stream;

@@ -9,7 +9,12 @@ reward / term / trunc / mask bytes, plus digests of the experience buffers, to a
 The test compares them with one engine stepping all envs alone. argv[2] = "eager" (per-step
 episode ends on each batch's stream, graphs=False) or "graphs" (the bench's mode: each (batch,
 ring slot) replayed from its hipGraph, the 3-slot ring reused across steps with cross-stream done
-events; episode phases staggered by the pre-roll only and ended by a short horizon). Not
+events; episode phases staggered by the pre-roll only and ended by a short horizon). argv[3] =
+"even" (N_PER_BATCH envs per batch on both ranks) or "uneven" (the learner's smaller share,
+bench.py --root-envs: SPLIT envs per batch by rank). argv[4] = "store" also gives rank 0 the
+gather's own compact record store (WireGather store=: the fused checked store, peers received
+straight into their arena slots) and records each step's stored rows; "store-noplan" the same
+with the arena receive off (peers received into the exchange's buffers and copied). Not
 collected by pytest."""
 
 import hashlib
@@ -22,6 +27,7 @@ sys.path.insert(0, ROOT)
 
 # shared with the test's one-engine reference run
 N_PER_BATCH, BATCHES, SEED, PSEED, PREROLL, TICKS, MAP_N = 3, 2, 11, 77, 36, 18, 8
+SPLIT = {"even": (N_PER_BATCH, N_PER_BATCH), "uneven": (1, 5)}  # envs per batch on rank 0, rank 1
 
 
 def horizon(mode):
@@ -55,47 +61,67 @@ def main():
 
     out_path = sys.argv[1]
     mode = sys.argv[2] if len(sys.argv) > 2 else "eager"
+    split = sys.argv[3] if len(sys.argv) > 3 else "even"
+    store_mode = sys.argv[4] if len(sys.argv) > 4 else ""
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
     dist.init_process_group("gloo")
-    n, nb = N_PER_BATCH, BATCHES
+    nb = BATCHES
+    per_rank = SPLIT[split]
+    n = per_rank[rank]
     envs = n * nb
+    base0 = sum(p * nb for p in per_rank[:rank])  # this rank's first global env
+    total = sum(p * nb for p in per_rank)
     cfg = Config.preset("C4", MAP_N=MAP_N, early_stop_agent_num=8, obs_layout=abi.OBS_WIRE, HORIZON=horizon(mode))
-    engs = [NmmoEngine(cfg, n, seed=SEED, device=dev, env_index_base=rank * envs + j * n) for j in range(nb)]
+    engs = [NmmoEngine(cfg, n, seed=SEED, device=dev, env_index_base=base0 + j * n) for j in range(nb)]
     P = engs[0].P
     for e in engs:
         e.reset()
     for k in range(PREROLL):
         for j, e in enumerate(engs):
-            e.end_episodes(preroll_mask(np.arange(n) + rank * envs + j * n, k))
+            e.end_episodes(preroll_mask(np.arange(n) + base0 + j * n, k))
             e.scripted_actions(PSEED)
             e.step(write_obs=False)
     torch.cuda.synchronize()
 
     def before(t, j, e):
-        e.end_episodes(end_mask(np.arange(n) + rank * envs + j * n, t))
+        e.end_episodes(end_mask(np.arange(n) + base0 + j * n, t))
 
-    rec = {"native": {}, "small": {}}
-    x = DeviceExperience(TICKS * world * envs * P, engs[0].obs_elems, world * envs * P, device=dev) if rank == 0 else None
+    rec = {"native": {}, "small": {}, "stored": {}}
+    x = DeviceExperience(TICKS * total * P, engs[0].obs_elems, total * P, device=dev) if rank == 0 else None
+    gs = None
+    if store_mode and rank == 0:  # the gather's own record store: every row of every step, reset per step
+        from nmmo_amd import wire as nw
+
+        gs = DeviceExperience(total * P, engs[0].obs_elems, total * P, device=dev,
+                              record_arena_bytes=sum(nw.max_bytes(p, P) + 64 for p in per_rank for _ in range(nb)))
 
     def on_step(s, got):
-        z = torch.zeros(n * P, device=dev)
         for (r, j) in sorted(got):
             w, sm = got[r, j]
-            nat = wire.unpack(w, n, P)
-            sm3 = sm.view(n, P, 8)
-            base = r * envs + j * n
-            for i in range(n):
+            m = g.counts[r][j]
+            z = torch.zeros(m * P, device=dev)
+            nat = wire.unpack(w, m, P)
+            sm3 = sm.view(m, P, 8)
+            base = g.env_base[r, j]
+            for i in range(m):
                 rec["native"][f"{s}:{base + i}"] = digest(nat[i])
                 rec["small"][f"{s}:{base + i}"] = digest(sm3[i, :, :7])
             rew = sm3[..., 0:4].contiguous().view(torch.float32).view(-1)
-            x.store(w, rew, sm3[..., 4].reshape(-1), sm3[..., 6].reshape(-1), torch.zeros((n * P, 12), dtype=torch.int32),
+            x.store(w, rew, sm3[..., 4].reshape(-1), sm3[..., 6].reshape(-1), torch.zeros((m * P, 12), dtype=torch.int32),
                     z, z, step=s + 1, env_id_base=base * P, engine=engs[0])
+        if gs is not None:  # the step's rows as the gather stored them (global env order)
+            k = gs.ptr
+            idx = torch.arange(k, dtype=torch.int32, device=dev)
+            rec["stored"][str(s)] = {"ptr": k, "obs": digest(gs.gather_obs(idx)), "rewards": digest(gs.rewards[:k]),
+                                     "dones": digest(gs.dones[:k]), "env_id": digest(gs.env_id[:k])}
 
     graphs = mode == "graphs"
     g = WireGather(engs, PSEED, rank, world, graphs=graphs, on_step=on_step if rank == 0 else None,
-                   before_step=None if graphs else before, backend="gloo")
+                   before_step=None if graphs else before, backend="gloo", store=gs)
+    if store_mode == "store-noplan" and rank == 0:
+        g._arena_plan = lambda s: None  # received into the exchange's buffers, then copied by the store
     for _ in range(TICKS):
         g.step()
     g.drain()
@@ -108,6 +134,7 @@ def main():
         rec["exp"] = {"ptr": k, "obs": digest(x.obs[:k]), "rewards": digest(x.rewards[:k]),
                       "dones": digest(x.dones[:k]), "env_id": digest(x.env_id[:k]), "step": digest(x.step[:k])}
         rec["payload_bytes"] = g.x.payload_bytes
+        rec["store_status"] = gs.status if gs is not None else 0
         with open(out_path, "w") as f:
             json.dump(rec, f)
     dist.barrier()

@@ -52,7 +52,8 @@ def test_enums_match_header():
     enames = [n.strip().split("=")[0].strip() for n in env.split(",")]
     assert [n[2:].lower() for n in enames if n.startswith("E_")] == abi.ENV_FIELDS
     for macro, val in [("NMMO_SYS_RESOURCE", abi.SYS_RESOURCE), ("NMMO_SYS_EXCHANGE", abi.SYS_EXCHANGE),
-                       ("NMMO_OBS_FLAT", abi.OBS_FLAT), ("NMMO_ABI_VERSION", abi.ABI_VERSION)]:
+                       ("NMMO_OBS_FLAT", abi.OBS_FLAT), ("NMMO_ABI_VERSION", abi.ABI_VERSION),
+                       ("NMMO_STORE_CTL_INTS", abi.STORE_CTL_INTS)]:
         m = re.search(rf"#define {macro} (.*?)(?:/\*|$)", text, re.M)
         assert eval(m.group(1).replace("u", "").strip()) == val, macro
 

@@ -95,3 +95,19 @@ def test_shard_bounds():
         pass
     else:
         raise AssertionError("uneven split must raise")
+
+
+def test_env_shares_learner_split():
+    """C5's learner share (bench.py --root-envs): rank 0 holds root_envs, the peers split the rest
+    as evenly as possible in whole env batches, and the node still steps every env."""
+    assert nd.env_shares(8192, 8, 512, granule=2) == [512] + [1098] * 4 + [1096] * 3
+    for world, k in ((2, 896), (4, 640), (8, 256), (8, 1024)):
+        sh = nd.env_shares(1024 * world, world, k, granule=2)
+        assert sh[0] == k and sum(sh) == 1024 * world
+        assert all(n % 2 == 0 for n in sh) and max(sh[1:]) - min(sh[1:]) <= 2
+    assert nd.env_shares(4096, 4, None) == [1024] * 4
+    assert nd.env_shares(1024, 1, 100) == [1024]
+    with pytest.raises(ValueError):
+        nd.env_shares(1024 * 8, 8, 511, granule=2)
+    with pytest.raises(ValueError):
+        nd.env_shares(16, 8, 14, granule=2)

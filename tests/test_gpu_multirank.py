@@ -70,7 +70,7 @@ def _reference(world, mode="eager"):
     from nmmo_amd.storage import DeviceExperience
     from tests import _c5_worker as w
 
-    N = world * w.N_PER_BATCH * w.BATCHES
+    N = world * w.N_PER_BATCH * w.BATCHES  # the same 12 global envs for every split
     cfg = Config.preset("C4", MAP_N=w.MAP_N, early_stop_agent_num=8, obs_layout=abi.OBS_NATIVE,
                         HORIZON=w.horizon(mode))
     eng = NmmoEngine(cfg, N, seed=w.SEED)
@@ -82,7 +82,8 @@ def _reference(world, mode="eager"):
         eng.scripted_actions(w.PSEED)
         eng.step(write_obs=False)
     x = DeviceExperience(w.TICKS * N * P, eng.obs_elems, N * P, device=eng.device)
-    rec = {"native": {}, "small": {}}
+    xs = DeviceExperience(N * P, eng.obs_elems, N * P, device=eng.device)  # one step's rows
+    rec = {"native": {}, "small": {}, "stored": {}}
     z = torch.zeros(N * P, device=eng.device)
     cnt = torch.zeros(3, dtype=torch.int64, device=eng.device)
     eng.set_counters(cnt)
@@ -98,6 +99,12 @@ def _reference(world, mode="eager"):
             rec["small"][f"{t}:{i}"] = w.digest(small[i])
         x.store(eng.obs, eng.rew.view(-1), eng.term.view(-1), eng.mask.view(-1),
                 torch.zeros((N * P, 12), dtype=torch.int32), z, z, step=t + 1, engine=eng)
+        xs.reset()
+        xs.store(eng.obs, eng.rew.view(-1), eng.term.view(-1), eng.mask.view(-1),
+                 torch.zeros((N * P, 12), dtype=torch.int32), z, z, step=t + 1, engine=eng)
+        k = xs.ptr
+        rec["stored"][str(t)] = {"ptr": k, "obs": w.digest(xs.obs[:k]), "rewards": w.digest(xs.rewards[:k]),
+                                 "dones": w.digest(xs.dones[:k]), "env_id": w.digest(xs.env_id[:k])}
     torch.cuda.synchronize()
     k = x.ptr
     rec["exp"] = {"ptr": k, "obs": w.digest(x.obs[:k]), "rewards": w.digest(x.rewards[:k]),
@@ -107,15 +114,21 @@ def _reference(world, mode="eager"):
     return rec
 
 
-@pytest.mark.parametrize("mode", ["eager", "graphs"])
-def test_c5_gather_content_matches_one_rank(tmp_path, mode):
+@pytest.mark.parametrize("mode,split,store", [("eager", "even", ""), ("graphs", "even", ""),
+                                              ("eager", "uneven", "store"), ("graphs", "uneven", "store"),
+                                              ("graphs", "uneven", "store-noplan")])
+def test_c5_gather_content_matches_one_rank(tmp_path, mode, split, store):
     """eager: per-step episode ends, WireGather(graphs=False). graphs: the mode bench.py times —
     every (batch, ring slot) replayed from its hipGraph, ring slots reused every 3 steps behind
-    cross-stream done events — with episodes ended by a horizon inside the checked window."""
+    cross-stream done events — with episodes ended by a horizon inside the checked window.
+    uneven: the learner's smaller share (rank 0 1 env per batch, rank 1 5). store: rank 0's
+    gather also keeps every step's rows in its compact record store (the fused checked store, the
+    peer received straight into its arena slot; store-noplan: received into the exchange's buffers
+    and copied), and each step's stored rows equal one engine's rows of that step."""
     out = tmp_path / "c5.json"
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
-           os.path.join(ROOT, "tests", "_c5_worker.py"), str(out), mode]
+           os.path.join(ROOT, "tests", "_c5_worker.py"), str(out), mode, split, store]
     env = dict(os.environ, OMP_NUM_THREADS="1")
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=110, env=env)
     assert p.returncode == 0, p.stderr[-3000:]
@@ -130,3 +143,8 @@ def test_c5_gather_content_matches_one_rank(tmp_path, mode):
     assert not bad, f"reward/dones/mask differ at (tick:env) {bad[:8]}"
     assert got["exp"] == ref["exp"]
     assert got["payload_bytes"] > 0
+    if store:
+        assert got["store_status"] == 0
+        assert set(got["stored"]) == set(ref["stored"])
+        bad = [k for k in ref["stored"] if got["stored"][k] != ref["stored"][k]]
+        assert not bad, f"the gather's stored rows differ at steps {bad[:8]}"

@@ -324,6 +324,159 @@ def test_record_store_many_equals_sequential_stores():
         e.close()
 
 
+def test_checked_store_refuses_bad_and_misplaced_buffers():
+    """nmmo_exp_store_records_checked (the gather root's store with the received-buffer check fused
+    into its reservation): a corrupt input among good ones sets the check bits and keeps no row
+    while the good ones are stored exactly as unchecked stores keep them; a buffer already at its
+    arena slot is stored in place; one inside the arena but not at its slot is refused (status
+    bit 4), never copied over the rows before it."""
+    from nmmo_amd import abi, wire
+    from nmmo_amd.config import Config
+    from nmmo_amd.engine import NmmoEngine
+    from nmmo_amd.storage import DeviceExperience
+
+    cfg = Config.preset("C4", MAP_N=4, early_stop_agent_num=8, obs_layout=abi.OBS_WIRE)
+    engs = [NmmoEngine(cfg, 3, seed=14, env_index_base=3 * i) for i in range(3)]
+    P = engs[0].P
+    dev = engs[0].device
+    for e in engs:
+        e.reset()
+    for t in range(6):
+        for e in engs:
+            e.scripted_actions(30 + t)
+            e.step()
+    n = 3 * P
+    acts = torch.zeros((n, 12), dtype=torch.int32, device=dev)
+    z = torch.zeros(n, device=dev)
+
+    def inp(e, i, w=None):
+        sm = torch.zeros((n, 8), dtype=torch.uint8, device=dev)
+        sm[:, 0:4] = e.rew.view(-1).view(torch.uint8).view(n, 4)
+        sm[:, 6] = e.mask.view(-1)
+        st = sm.view(-1)
+        return (e.obs if w is None else w, st, st[4:], st[6:], acts, z, z, i * n)
+
+    tots = [wire.total_bytes(e.obs) for e in engs]
+    bad = engs[1].obs[:tots[1]].clone()
+    cnt = bad[8 + 8 * 3:8 + 8 * 3 + 2 * 3 * P].view(torch.int16)
+    j = int(torch.nonzero(cnt < 0)[2, 0])
+    cnt[j] = cnt[j] + 1  # one more visible entity than the record holds
+    ref = DeviceExperience(2000, engs[0].obs_elems, 3 * n, device=dev, record_arena_bytes=64 << 20)
+    ref.store_many([inp(engs[0], 0), inp(engs[2], 2)], 1, engs[0], field_stride=8)
+    chk = DeviceExperience(2000, engs[0].obs_elems, 3 * n, device=dev, record_arena_bytes=64 << 20)
+    cs = torch.zeros(1, dtype=torch.int32, device=dev)
+    exp = [torch.tensor([t], dtype=torch.int64, device=dev) for t in tots]
+    chk.store_many([inp(engs[0], 0), inp(engs[1], 1, bad), inp(engs[2], 2)], 1, engs[0], field_stride=8,
+                   expect=exp, check_status=cs)
+    torch.cuda.synchronize()
+    assert int(cs.item()) & (2 | 8) and chk.status & 8, (int(cs.item()), chk.status)
+    k = ref.ptr
+    assert chk.ptr == k > 0
+    for name in ("rewards", "dones", "env_id", "step", "seq", "row_agent"):
+        assert torch.equal(getattr(ref, name)[:k], getattr(chk, name)[:k]), name
+    idx = torch.arange(k, dtype=torch.int32, device=dev)
+    assert torch.equal(ref.gather_obs(idx), chk.gather_obs(idx))
+    assert int(chk._ctl.abs().sum().item()) == 0  # the control words are left zero
+    # clean inputs: no bits; the announced total is compared
+    cs.zero_()
+    chk.reset()
+    chk.status_dev.zero_()
+    chk.store_many([inp(engs[0], 0), inp(engs[2], 2)], 2, engs[0], field_stride=8, expect=[exp[0], exp[2]],
+                   check_status=cs)
+    torch.cuda.synchronize()
+    assert int(cs.item()) == 0 and chk.status == 0 and chk.ptr == k
+    chk.reset()
+    chk.store_many([inp(engs[0], 0)], 3, engs[0], field_stride=8, expect=[exp[0] + 16], check_status=cs)
+    torch.cuda.synchronize()
+    assert int(cs.item()) & 1 and chk.status & 8 and chk.ptr == 0
+    # a buffer already at its slot is stored in place; one elsewhere in the arena is refused
+    for ok_slot in (True, False):
+        x = DeviceExperience(2000, engs[0].obs_elems, 3 * n, device=dev, record_arena_bytes=64 << 20)
+        off = 16 if ok_slot else 4096 + 16
+        w = x.arena[off:off + tots[0]]
+        w.copy_(engs[0].obs[:tots[0]])
+        x.store_many([inp(engs[0], 0, w)], 1, engs[0], field_stride=8)
+        torch.cuda.synchronize()
+        if ok_slot:
+            assert x.status == 0 and x.ptr > 0
+            m = x.ptr
+            assert torch.equal(x.gather_obs(idx[:m]), ref.gather_obs(idx[:m]))
+        else:
+            assert x.status & 16 and x.ptr == 0
+    for e in engs:
+        e.close()
+
+
+def test_wire_gather_rehearsal_stores_phantom_peers():
+    """The one-GPU rehearsal of an N-rank root (WireGather rehearse=R, bench.py's C5 node model):
+    every step the root stores its own rows and R phantom peers' rows, each phantom's records and
+    fields equal to a plain store of the phantom buffer, with the fused check clean, in both the
+    write-only fill and the copy mode."""
+    from nmmo_amd import abi, wire
+    from nmmo_amd.config import Config
+    from nmmo_amd.distributed import WireGather
+    from nmmo_amd.engine import NmmoEngine
+    from nmmo_amd.storage import DeviceExperience
+
+    cfg = Config.preset("C4", MAP_N=4, early_stop_agent_num=8, obs_layout=abi.OBS_WIRE)
+    dev = torch.device("cuda", 0)
+    peer = [NmmoEngine(cfg, 3, seed=5, env_index_base=100 + 3 * i) for i in range(2)]
+    for e in peer:
+        e.reset()
+    g = WireGather(peer, 11, graphs=False)
+    for _ in range(5):
+        g.step()
+    g.drain()
+    torch.cuda.synchronize()
+    k = (g.t - 1) % g.ring
+    phantom = []
+    for j, e in enumerate(peer):
+        tot = wire.total_bytes(g.wires[j][k])
+        phantom.append((g.wires[j][k][:tot].clone(), g.smalls[j][k].clone(), e.n_envs))
+    g.close()
+    P = peer[0].P
+    ph_rows = sum(int(sm.view(-1, 8)[:, 6].sum().item()) for _, sm, _ in phantom)
+    # a plain store of the phantom buffers: the rows every phantom peer must add
+    one = DeviceExperience(4000, 23987, 12 * P, device=dev, record_arena_bytes=64 << 20)
+    acts = torch.zeros((3 * P, 12), dtype=torch.int32, device=dev)
+    zz = torch.zeros(3 * P, device=dev)
+    one.store_many([(w, sm.view(-1), sm.view(-1)[4:], sm.view(-1)[6:], acts, zz, zz, j * 3 * P)
+                    for j, (w, sm, _) in enumerate(phantom)], 1, peer[0], field_stride=8)
+    torch.cuda.synchronize()
+    assert one.ptr == ph_rows > 0
+    want = one.gather_obs(torch.arange(ph_rows, dtype=torch.int32, device=dev))
+    root = [NmmoEngine(cfg, 2, seed=5, env_index_base=2 * i) for i in range(2)]
+    for e in root:
+        e.reset()
+    R = 2
+    for mode in ("fill", "copy"):
+        rows = []
+        store = DeviceExperience(4000, 23987, 16 * P, device=dev, record_arena_bytes=64 << 20)
+
+        def on_step(s, got):
+            rows.append((store.ptr, store.gather_obs(torch.arange(store.ptr, dtype=torch.int32, device=dev)),
+                         store.env_id[:store.ptr].clone()))
+
+        g = WireGather(root, 11, graphs=False, store=store, rehearse=R, phantom=phantom, rehearse_mode=mode,
+                       on_step=on_step)
+        for _ in range(4):
+            g.step()
+        g.drain()
+        torch.cuda.synchronize()
+        assert g.check_status() == 0 and store.status == 0
+        assert len(rows) == 4
+        for ptr, obs, eid in rows:
+            assert ptr > R * ph_rows
+            # the phantoms come first in the arena, in peer order: each equals the plain store
+            for q in range(R):
+                assert torch.equal(obs[q * ph_rows:(q + 1) * ph_rows], want), (mode, q)
+            # env ids: phantom q's rows sit after the real ranks' 4 envs
+            assert int(eid[:R * ph_rows].min()) >= 4 * P
+        g.close()
+    for e in peer + root:
+        e.close()
+
+
 def test_wire_pack_rejects_stale_native():
     """nmmo_wire_pack refuses a native buffer a tick without an obs gather has made stale, or
     one that is not the buffer the last gather wrote."""
