@@ -492,7 +492,7 @@ class WireGather:
                     part = batch[k:k + 16]
                     self.store.store_many([b for b, _, _ in part], s + 1, self.engines[0], field_stride=8,
                                           expect=[ex for _, ex, _ in part], check_status=self.status,
-                                          check=[c for _, _, c in part])
+                                          checked=[c for _, _, c in part])
                 self._stored += self.store.ptr_dev[0].to(torch.int64)
         if self.on_step is not None:
             torch.cuda.synchronize(self.device)

@@ -177,7 +177,7 @@ class DeviceExperience:
         self._inflight = (r_, d_, m_, lp, v, a, eid, obs_flat, obs_nat, obs_wire)
 
     def store_many(self, inputs, step: int, engine, field_stride: int = 0, expect=None, check_status=None,
-                   check=None):
+                   checked=None):
         """Several wire buffers stored as one store, in input order (compact storage only;
         nmmo_exp_store_records_many: a fixed number of launches for up to 16 buffers, e.g. every
         rank's buffers of a step at the learner). inputs: (wire, rewards, dones, mask, actions,
@@ -188,7 +188,7 @@ class DeviceExperience:
         check_status (device int32 [1]) fuses the received-buffer check into the store
         (nmmo_exp_store_records_checked): every input is validated as nmmo_wire_check_many does,
         its bits OR-ed into check_status, and an input that fails keeps no row. expect: per
-        input a device int64 [1] announced total, or None; check: per input whether to check it
+        input a device int64 [1] announced total, or None; checked: per input whether to check it
         (default all; an unchecked input, e.g. the root's own buffer, counts as clean)."""
         if self.records is None:
             raise ValueError("store_many needs compact (record) storage")
@@ -217,7 +217,7 @@ class DeviceExperience:
                                        for e in ex):
                     raise ValueError("expect: one device int64 [1] (or None) per input")
                 exp_arr = (ctypes.c_void_p * n)(*[None if e is None else e.data_ptr() for e in ex])
-                mask = sum(1 << i for i in range(n) if check is None or check[i])
+                mask = sum(1 << i for i in range(n) if checked is None or checked[i])
                 if getattr(self, "_ctl", None) is None:  # zero; every call leaves it zero
                     self._ctl = torch.zeros(abi.STORE_CTL_INTS, dtype=torch.int32, device=self.device)
                 check(lib().nmmo_exp_store_records_checked(engine.h, ctypes.byref(self.x), ctypes.byref(self.records),
