@@ -606,9 +606,9 @@ NMMO_API int nmmo_exp_store_records(NmmoHandle* h, const NmmoExperience* x, cons
 NMMO_API int nmmo_exp_store_records_many(NmmoHandle* h, const NmmoExperience* x, const NmmoRecordStore* rs,
                                          const NmmoStoreInput* ins, int32_t n_inputs, int32_t field_stride,
                                          int32_t* scratch, void* stream);
-/* nmmo_exp_store_records_many with the received-buffer check fused into its reservation pass (the
- * learner root of the C5 gather: one launch validates every input as nmmo_wire_check_many does and
- * reserves the arena): each input's check bits (1 total vs *dev_expect_totals[i], 2 offsets, 4
+/* nmmo_exp_store_records_many with the received-buffer check in front of its reservation pass (the
+ * learner root of the C5 gather: one call validates every input as nmmo_wire_check_many does and
+ * stores only the clean ones): each input's check bits (1 total vs *dev_expect_totals[i], 2 offsets, 4
  * count ranges, 8 record heads, 16 entity-table indices) are OR-ed into *dev_check_status (device
  * int32, or NULL), and an input with any bit set keeps no row (x->status bit 3). dev_expect_totals:
  * host array of n_inputs device int64 pointers (an entry or the array NULL skips that comparison).
@@ -616,7 +616,7 @@ NMMO_API int nmmo_exp_store_records_many(NmmoHandle* h, const NmmoExperience* x,
  * clean). dev_ctl: device int32 [NMMO_STORE_CTL_INTS], zero before the first call; every call leaves it
  * zero (one per stream: calls sharing it must not overlap). Any store of a buffer that lies inside
  * the arena but not at its reserved slot is refused (x->status bit 4), never copied. */
-#define NMMO_STORE_CTL_INTS 17
+#define NMMO_STORE_CTL_INTS 16
 NMMO_API int nmmo_exp_store_records_checked(NmmoHandle* h, const NmmoExperience* x, const NmmoRecordStore* rs,
                                             const NmmoStoreInput* ins, int32_t n_inputs, int32_t field_stride,
                                             const int64_t* const* dev_expect_totals, uint32_t check_mask,

@@ -37,7 +37,7 @@ SYS_ALL = 0xFF
 OBS_NONE = 0
 OBS_FLAT = 1
 OBS_NATIVE = 2
-STORE_CTL_INTS = 17  # nmmo_exp_store_records_checked's device control words (ticket + 16 per-input)
+STORE_CTL_INTS = 16  # nmmo_exp_store_records_checked's device words (per-input check bits)
 OBS_WIRE = 3  # SPEC.md §8c wire records straight from the state (the learner-gather transport)
 # native layout (SPEC.md §8b)
 NATIVE_MASK_BYTES = 1600

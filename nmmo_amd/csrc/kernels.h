@@ -220,7 +220,7 @@ struct StoreBatch {
 struct StoreCheck {
   const int64_t* expect[kMaxStoreInputs];  // each input's announced total (device), or NULL
   int* status;                             // the check bits of every input (nmmo_wire_check's), or NULL
-  int* ctl;                                // [1 + kMaxStoreInputs]: ticket, per-input bits; zero, left zero
+  int* ctl;                                // [kMaxStoreInputs] per-input check bits; zero, left zero
   uint32_t mask;                           // bit i: check input i (an unchecked input counts as clean)
 };
 int store_many_scratch_ints(int n_inputs, int max_rows);

@@ -317,7 +317,7 @@ __device__ void record_reserve_serial(const NmmoExperience& x, const NmmoRecordS
     const int64_t base = (used + 15) & ~(int64_t)15;
     const bool sane = total >= wire_header_bytes(n_envs, b.P) && total <= b.wire_cap[i] && (total & 15) == 0 &&
                       base + 16 + total <= rs.arena_bytes;
-    const bool checked = !ist || __hip_atomic_load(&ist[i], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0;
+    const bool checked = !ist || ist[i] == 0;
     const bool inside = w >= a0 && w < a0 + rs.arena_bytes;
     const bool placed = w == a0 + base + 16;
     const bool ok = sane && checked && (!inside || placed);
@@ -340,34 +340,27 @@ __global__ void record_reserve_many_kernel(NmmoExperience x, NmmoRecordStore rs,
   record_reserve_serial(x, rs, b, gates, rbase, nullptr);
 }
 
-// The fused root pass (nmmo_exp_store_records_checked): block (env, input) runs the received-buffer
-// check of one env (wire_check_env, the bits of nmmo_wire_check_many) into the input's status word
-// and the caller's; the launch's last block to finish (an agent-scope ticket) then reserves every
-// input, storing only the ones whose check came back clean. ctl = [ticket, ist[16]], zero on entry
-// and left zero.
-__global__ void __launch_bounds__(128) record_check_reserve_kernel(NmmoExperience x, NmmoRecordStore rs, StoreBatch b,
-                                                                   StoreCheck c, int* gates, int64_t* rbase) {
+// The root's received-buffer check inside its store (nmmo_exp_store_records_checked): block (env,
+// input) runs the check of one env (wire_check_env, the bits of nmmo_wire_check_many) and ORs
+// what it finds into the input's status word c.ctl[i] and the caller's; the reservation that
+// follows (record_reserve_checked_kernel) stores only the inputs whose word stayed 0 and zeroes
+// the words again. (A last-block ticket that reserved inside this launch measured ~1 ms per step
+// at C5's 16 inputs x 512 envs: one agent-scope atomic per block on a single word.)
+__global__ void __launch_bounds__(128) record_check_kernel(StoreBatch b, StoreCheck c) {
   const int i = blockIdx.y, e = blockIdx.x;
   const int n_envs = b.in[i].n_rows / b.P;
-  int* ist = c.ctl + 1;
-  if (e < n_envs && ((c.mask >> i) & 1u)) {  // block-uniform: the check's barriers see every thread
-    const int bad = wire_check_env(reinterpret_cast<const uint8_t*>(b.in[i].wire), n_envs, b.P, c.expect[i], e);
-    if (bad) {
-      __hip_atomic_fetch_or(&ist[i], bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (c.status) atomicOr(c.status, bad);
-    }
+  if (e >= n_envs || !((c.mask >> i) & 1u)) return;  // block-uniform
+  const int bad = wire_check_env(reinterpret_cast<const uint8_t*>(b.in[i].wire), n_envs, b.P, c.expect[i], e);
+  if (bad) {
+    atomicOr(&c.ctl[i], bad);
+    if (c.status) atomicOr(c.status, bad);
   }
-  __shared__ int last;
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-  __syncthreads();
-  if (threadIdx.x == 0)
-    last = __hip_atomic_fetch_add(c.ctl, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
-           (int)(gridDim.x * gridDim.y) - 1;
-  __syncthreads();
-  if (!last || threadIdx.x != 0) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  record_reserve_serial(x, rs, b, gates, rbase, ist);
-  for (int k = 0; k <= kMaxStoreInputs; k++) __hip_atomic_store(&c.ctl[k], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ void record_reserve_checked_kernel(NmmoExperience x, NmmoRecordStore rs, StoreBatch b, StoreCheck c,
+                                              int* gates, int64_t* rbase) {
+  record_reserve_serial(x, rs, b, gates, rbase, c.ctl);
+  for (int k = 0; k < kMaxStoreInputs; k++) c.ctl[k] = 0;
 }
 
 __global__ void __launch_bounds__(kStoreBlock) store_count_many_kernel(NmmoExperience x, StoreBatch b,
@@ -450,8 +443,8 @@ hipError_t launch_store_records_many(const NmmoExperience& x, const NmmoRecordSt
   int* gates = total + 1;          // [n]
   int64_t* rbase = reinterpret_cast<int64_t*>(scratch + ((b.n * nb + 1 + b.n + 1) & ~1));  // [n], 8-B aligned
   if (chk) {
-    hipLaunchKernelGGL(record_check_reserve_kernel, dim3(max_rows / b.P, b.n), dim3(128), 0, stream, x, rs, b, *chk,
-                       gates, rbase);
+    hipLaunchKernelGGL(record_check_kernel, dim3(max_rows / b.P, b.n), dim3(128), 0, stream, b, *chk);
+    hipLaunchKernelGGL(record_reserve_checked_kernel, dim3(1), dim3(1), 0, stream, x, rs, b, *chk, gates, rbase);
   } else {
     hipLaunchKernelGGL(record_reserve_many_kernel, dim3(1), dim3(1), 0, stream, x, rs, b, gates, rbase);
   }
