@@ -404,11 +404,16 @@ NMMO_API int nmmo_dev_free(void* ptr);
  *           (nmmo_wire_header_bytes);
  *   payload: per env, its entity table (the distinct Entity rows its records show, 31 int16
  *           each, ascending by the id's 16-bit pattern, padded to 16 B), one record per agent in
- *           the realm (slot order), then its listings (32 B each); a record is a 16-B head
- *           (int16 AgentId, CurrentTick, task index, tile row 0, tile col 0, nv, ninv | Exchange
- *           << 8, gold), the ActionTargets bits except Buy.MarketItem (561 bits in 80 B), nv u16
+ *           the realm (slot order), then its listings (32 B each); a record (v4) is a 16-B head
+ *           (int16 AgentId, CurrentTick, task index, tile row 0, tile col 0, m5, m6, gold), nv u16
  *           entity-table indices, ninv Inventory rows (16 int16), the 225 window materials at 4
- *           bits (113 B), zero pad to 16 B.
+ *           bits (114 B), the mask bit stream, zero pad to 16 B. The ActionTargets travel as what
+ *           they are made of: m5 = nv | ninv << 7 | Exchange << 11 | (pp1 & 15) << 12, m6 = Style
+ *           | Move (5 bits) << 1 | GoldPrice's count of leading ones << 6 | (pp1 >> 4) << 13 (pp1
+ *           = 1 + the SellPrice entry the wrapper cleared, 0 = none), and the stream holds
+ *           AttackTarget, GiveTarget, GoldTarget entries < nv then Destroy, GiveItem, SellItem,
+ *           Use entries < ninv (3 nv + 4 ninv bits in whole u16 words; every later entry is 0,
+ *           each noop 1).
  * The receiver reads `total` from the header; Buy.MarketItem is rebuilt from the listings. */
 NMMO_API int64_t nmmo_wire_header_bytes(int32_t n_envs, int32_t player_n);
 /* Upper bound of a wire buffer (every agent in the realm with 100 visible entities and 12 items,

@@ -55,13 +55,17 @@ __device__ __forceinline__ bool ao_in_window(uint32_t w, uint32_t rc) {
 }
 static_assert(kMaxSlots <= 512 && kSize <= 255, "packed entity word");
 
-// The 12 ActionTargets sections (nmmo_layout's dims, flat order), their flat entry offsets and
-// the wire bit offsets of the 11 sent ones (Buy.MarketItem is not sent). Launchers check a
-// handle's layout against sec_flat.
+// The 12 ActionTargets sections (nmmo_layout's dims, flat order) and their flat entry offsets
+// (sec_wire: offsets with Buy.MarketItem left out). Launchers check a handle's layout against
+// sec_flat.
 constexpr int kSecN[12] = {3, 101, NMMO_MARKET_ROWS + 1, kInv + 1, kInv + 1, kNObs + 1, 99, kNObs + 1, 5, kInv + 1, 99, kInv + 1};
 __host__ __device__ constexpr int sec_flat(int k) { return k == 0 ? 0 : sec_flat(k - 1) + kSecN[k - 1]; }
 __host__ __device__ constexpr int sec_wire(int k) { return k < 2 ? sec_flat(k) : sec_flat(k) - kWireBuyN; }
-static_assert(sec_flat(2) == kWireBuyLo && sec_flat(12) == kMaskN && sec_wire(12) == kWireMaskBits, "sections");
+static_assert(sec_flat(2) == kWireBuyLo && sec_flat(12) == kMaskN && sec_flat(1) == kMkAttackT &&
+                  sec_flat(3) == kMkDestroy && sec_flat(4) == kMkGiveI && sec_flat(5) == kMkGiveT &&
+                  sec_flat(6) == kMkGoldP && sec_flat(7) == kMkGoldT && sec_flat(8) == kMkMove &&
+                  sec_flat(9) == kMkSellI && sec_flat(10) == kMkSellP && sec_flat(11) == kMkUse,
+              "sections (wire.h)");
 __host__ inline bool ao_layout_ok(const ObsParams& p) {
   const int offs[12] = {p.o_style, p.o_target, p.o_buy, p.o_destroy, p.o_give_item, p.o_give_target,
                         p.o_gg_price, p.o_gg_target, p.o_move, p.o_sell_item, p.o_sell_price, p.o_use};

@@ -1,5 +1,5 @@
 // wire.h — the wire format of native observations (SPEC.md §8c), shared by the codec kernels
-// (wire.hip), the wire-writing observation gather (obs.hip, NMMO_OBS_WIRE) and the experience
+// (wire.hip), the wire-writing observation gather (wire_obs.hip, NMMO_OBS_WIRE) and the experience
 // store that decodes wire records straight into flat rows (wire.hip).
 //
 //   header  int64 total bytes | int64 env payload offset [n_envs] | u16 agent count word
@@ -8,17 +8,25 @@
 //   payload per env: its entity table (the distinct Entity rows its records show, ascending by
 //           the 16-bit pattern of their id, 62 B each, zero pad to 16 B), one record per agent
 //           in the realm (slot order), then its listings
-//   record  16-B head (int16 AgentId, CurrentTick, task index, tile row 0, tile col 0, nv,
-//           ninv | exchange << 8, gold) | the ActionTargets as bits EXCEPT Buy.MarketItem (561
-//           bits in 80 B) | nv u16 entity-table indices (the agent's Entity rows in order) | ninv
-//           Inventory rows (16 x int16) | the 225 window materials, 4 bits each (113 B) | zero pad
+//   record  16-B head (int16 AgentId, CurrentTick, task index, tile row 0, tile col 0, m5, m6,
+//           gold) | nv u16 entity-table indices (the agent's Entity rows in order) | ninv
+//           Inventory rows (16 x int16) | the 225 window materials, 4 bits each (114 B, the last
+//           byte zero) | the mask bit stream (3 nv + 4 ninv bits in whole u16 words) | zero pad
 //           to 16 B
 //   listing 16 x int16 (the native Market row)
+// The ActionTargets (1,586 entries) travel as what they are made of (v4):
+//   m5 = nv | ninv << 7 | Exchange << 11 | (pp1 & 15) << 12
+//   m6 = Style (its 3 entries are all 1 or all 0) | Move (5 bits) << 1 | GoldPrice ones (a
+//        prefix: count) << 6 | (pp1 >> 4) << 13
+//   pp1 = 1 + the SellPrice entry the wrapper cleared (0 = none); SellPrice = Exchange ? every
+//        entry but that one : none
+//   the stream: AttackTarget, GiveTarget, GoldTarget entries 0..nv-1, then Destroy, GiveItem,
+//        SellItem, Use entries 0..ninv-1 (every later entry is 0 and each section's noop 1)
+//   Buy.MarketItem (1,025 entries) is a function of the env's listings, the agent's gold and id:
+//        entry k < listings = Exchange && price_k <= gold && owner_k != AgentId, entry 1,024
+//        (noop) = 1, the rest 0 -- the decoders rebuild it.
 // An entity seen by several agents of an env (C4 steady state: 5.1 Entity rows per agent, 1.4
 // distinct entities per agent) travels once.
-// Buy.MarketItem (1,025 of the 1,586 mask entries) is a function of the env's listings, the
-// agent's gold and id: entry k < listings = exchange && price_k <= gold && owner_k != AgentId,
-// entry 1,024 (noop) = 1, the rest 0 -- the decoders rebuild it.
 #pragma once
 
 #include "common.h"
@@ -28,18 +36,32 @@ namespace nmmo {
 constexpr int kWireHead = 16;
 constexpr int kWireBuyLo = 104, kWireBuyN = NMMO_MARKET_ROWS + 1;  // the Buy section's flat mask entries
 constexpr int kMaskN = 1586;                                       // ActionTargets entries (flat offset of AgentId)
-constexpr int kWireMaskBits = kMaskN - kWireBuyN;                  // 561 sent
-constexpr int kWireMask = 80;                                      // their bytes, zero-padded
-constexpr int kWireTiles = 113;                                    // 225 materials, two per byte
-constexpr int kWireBody = kWireHead + kWireMask;  // 96: Entity rows start 16-B aligned
-static_assert(kWireMaskBits <= 8 * kWireMask && kWireBody % 16 == 0, "wire record head");
-// flat mask entry of wire bit b (b < kWireMaskBits), and the wire bit of a non-Buy entry
-__host__ __device__ inline int wire_bit_entry(int b) { return b < kWireBuyLo ? b : b + kWireBuyN; }
-__host__ __device__ inline int entry_wire_bit(int j) { return j < kWireBuyLo ? j : j - kWireBuyN; }
+constexpr int kWireTiles = 114;                                    // 225 materials, two per byte (+ a zero byte)
+// flat offsets of the ActionTargets sections (nmmo_layout order)
+constexpr int kMkStyle = 0, kMkAttackT = 3, kMkDestroy = 1129, kMkGiveI = 1142, kMkGiveT = 1155, kMkGoldP = 1256,
+              kMkGoldT = 1355, kMkMove = 1456, kMkSellI = 1461, kMkSellP = 1474, kMkUse = 1573;
 constexpr int kNatI16Entity = 2, kNatI16Inv = kNatI16Entity + kNObs * NMMO_N_ENTITY_COLS,
               kNatI16Tile = kNatI16Inv + kInv * 16, kNatI16Task = kNatI16Tile + 225 * 3;
-constexpr int kRecMaxU4 = (kWireBody + 2 * kNObs + 32 * kInv + kWireTiles + 15) / 16;  // 50
+// the mask bit stream: 3 nv + 4 ninv bits in whole u16 words
+__host__ __device__ inline int wire_stream_bytes(int nv, int ninv) { return 2 * ((3 * nv + 4 * ninv + 15) >> 4); }
+// record offsets (bytes from the record start)
+__host__ __device__ inline int wire_off_inv(int nv) { return kWireHead + 2 * nv; }
+__host__ __device__ inline int wire_off_mat(int nv, int ninv) { return kWireHead + 2 * nv + 32 * ninv; }
+__host__ __device__ inline int wire_off_stream(int nv, int ninv) { return wire_off_mat(nv, ninv) + kWireTiles; }
+constexpr int kRecMaxU4 = (kWireHead + 2 * kNObs + 32 * kInv + kWireTiles + 2 * ((3 * kNObs + 4 * kInv + 15) >> 4) +
+                           15) / 16;  // 48
 constexpr int kEntRow = 2 * NMMO_N_ENTITY_COLS;                                          // 62 B
+// head words 5 and 6 (m5, m6 above)
+__host__ __device__ inline uint32_t wire_m5(int nv, int ninv, bool exch, int pp1) {
+  return (uint32_t)nv | (uint32_t)ninv << 7 | (exch ? 1u << 11 : 0u) | (uint32_t)(pp1 & 15) << 12;
+}
+__host__ __device__ inline uint32_t wire_m6(bool style, uint32_t move, int ng, int pp1) {
+  return (style ? 1u : 0u) | (move & 31u) << 1 | (uint32_t)ng << 6 | (uint32_t)(pp1 >> 4) << 13;
+}
+__host__ __device__ inline bool wire_exch(const int16_t* head) { return ((uint16_t)head[5] >> 11) & 1u; }
+__host__ __device__ inline int wire_pp1(const int16_t* head) {
+  return ((uint16_t)head[5] >> 12) | ((uint16_t)head[6] >> 13) << 4;
+}
 
 __host__ __device__ inline int64_t wire_header_used(int n, int P) {
   return 8 + 8 * (int64_t)n + 2 * (int64_t)n * P + 4 * (int64_t)n;
@@ -49,7 +71,7 @@ __host__ __device__ inline uint32_t wire_count_word(int nv, int ninv) { return 0
 __host__ __device__ inline int wire_record_bytes(uint32_t cnt) {
   if (!(cnt & 0x8000u)) return 0;
   const int nv = cnt & 127, ninv = (cnt >> 7) & 15;
-  return (kWireBody + 2 * nv + 32 * ninv + kWireTiles + 15) & ~15;
+  return (wire_off_stream(nv, ninv) + wire_stream_bytes(nv, ninv) + 15) & ~15;
 }
 // an env's entity table of ne rows
 __host__ __device__ inline int wire_table_bytes(int ne) { return (kEntRow * ne + 15) & ~15; }
@@ -100,15 +122,33 @@ __device__ inline int idrank(const uint32_t* ids, const int* pre, int id) {
 // and 2); head = the record's 8 int16.
 __device__ inline bool wire_buy_entry(int k, int nm, const uint32_t* lpo, const int16_t* head) {
   if (k == NMMO_MARKET_ROWS) return true;  // noop
-  if (k >= nm || !((uint16_t)head[6] >> 8)) return false;
+  if (k >= nm || !wire_exch(head)) return false;
   const uint32_t v = lpo[k];
   return (int)(v & 0xFFFFu) <= head[7] && (int)(v >> 16) != head[0];
 }
-// flat ActionTargets entry j (< kMaskN) of a record whose mask bits are `bits`
-__device__ inline bool wire_mask_entry(int j, const uint32_t* bits, int nm, const uint32_t* lpo, const int16_t* head) {
+// flat ActionTargets entry j (< kMaskN, not in Buy.MarketItem) of a record: head, its mask bit
+// stream (byte pointer), nv, ninv
+__device__ inline bool wire_mask_entry(int j, const int16_t* head, const uint8_t* st, int nv, int ninv) {
+  const uint32_t m6 = (uint16_t)head[6];
+  auto bit = [&](int i) { return ((st[i >> 3] >> (i & 7)) & 1u) != 0; };
+  // list sections: entries < n from the stream at s0, the noop (last entry) 1, the rest 0
+  auto list = [&](int k, int n, int noop, int s0) { return k == noop ? true : k < n ? bit(s0 + k) : false; };
+  if (j < kMkAttackT) return m6 & 1u;                                  // Style
+  if (j < kWireBuyLo) return list(j - kMkAttackT, nv, kNObs, 0);       // AttackTarget
+  if (j < kMkGiveI) return list(j - kMkDestroy, ninv, kInv, 3 * nv);   // Destroy
+  if (j < kMkGiveT) return list(j - kMkGiveI, ninv, kInv, 3 * nv + ninv);  // GiveItem
+  if (j < kMkGoldP) return list(j - kMkGiveT, nv, kNObs, nv);          // GiveTarget
+  if (j < kMkGoldT) return j - kMkGoldP < (int)((m6 >> 6) & 127u);     // GoldPrice: a prefix of ones
+  if (j < kMkMove) return list(j - kMkGoldT, nv, kNObs, 2 * nv);       // GoldTarget
+  if (j < kMkSellI) return (m6 >> (1 + j - kMkMove)) & 1u;             // Move
+  if (j < kMkSellP) return list(j - kMkSellI, ninv, kInv, 3 * nv + 2 * ninv);  // SellItem
+  if (j < kMkUse) return wire_exch(head) && j - kMkSellP + 1 != wire_pp1(head);  // SellPrice
+  return list(j - kMkUse, ninv, kInv, 3 * nv + 3 * ninv);             // Use
+}
+__device__ inline bool wire_mask_entry_any(int j, const int16_t* head, const uint8_t* st, int nv, int ninv, int nm,
+                                           const uint32_t* lpo) {
   if (j >= kWireBuyLo && j < kWireBuyLo + kWireBuyN) return wire_buy_entry(j - kWireBuyLo, nm, lpo, head);
-  const int b = entry_wire_bit(j);
-  return (bits[b >> 5] >> (b & 31)) & 1u;
+  return wire_mask_entry(j, head, st, nv, ninv);
 }
 // window material t (< 225) of a record's 4-bit tile bytes
 __device__ inline int wire_tile(const uint8_t* mat, int t) { return (mat[t >> 1] >> (4 * (t & 1))) & 15; }
@@ -182,9 +222,11 @@ __device__ __forceinline__ int wire_check_env(const uint8_t* wire, int n, int P,
         bad |= 4;
       } else if (base + off[a] + kWireHead <= total) {
         const int16_t* h = reinterpret_cast<const int16_t*>(v.base + base + off[a]);
-        if (h[0] <= 0 || h[5] != nv || (h[6] & 0xFF) != ninv || ((uint16_t)h[6] >> 8) > 1) bad |= 8;
+        if (h[0] <= 0 || ((uint16_t)h[5] & 0x7FFu) != (c & 0x7FFu) || wire_pp1(h) > 99 ||
+            (((uint16_t)h[6] >> 6) & 127u) > 99)
+          bad |= 8;
         if (base + off[a] + wire_record_bytes(c) <= total) {  // entity-table indices, 8 per 16-B load
-          const uint4* ix4 = reinterpret_cast<const uint4*>(h + kWireBody / 2);
+          const uint4* ix4 = reinterpret_cast<const uint4*>(h + kWireHead / 2);
           uint4 q[(kNObs + 7) / 8];
 #pragma unroll
           for (int j = 0; j < (kNObs + 7) / 8; j++) q[j] = 8 * j < nv ? ix4[j] : make_uint4(0u, 0u, 0u, 0u);

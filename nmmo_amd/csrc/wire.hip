@@ -279,30 +279,54 @@ __global__ void __launch_bounds__(256) wire_pack_kernel(const uint8_t* native, u
     const uint8_t* row = nenv + (size_t)a * NMMO_NATIVE_ROW_BYTES;
     const int16_t* i16 = reinterpret_cast<const int16_t*>(row + NMMO_NATIVE_MASK_BYTES);
     uint8_t* rec = penv + off[a];
+    // the ActionTargets as wire.h v4 builds them: head words m5 / m6 from the closed-form
+    // sections, the target / inventory entries as a bit stream (ballots over the native bytes)
+    const bool style = row[kMkStyle] != 0;
+    uint32_t move = 0u;
+    for (int k = 0; k < 5; k++) move |= row[kMkMove + k] ? 1u << k : 0u;
+    const int ng = __popcll(__ballot(lane < 64 && row[kMkGoldP + lane])) +
+                   __popcll(__ballot(lane + 64 < kSecN[6] && row[kMkGoldP + 64 + lane]));
+    int pp1 = 0;
+    if (exch) {
+      const uint64_t z0 = __ballot(!row[kMkSellP + lane]);
+      const uint64_t z1 = __ballot(lane + 64 < kSecN[10] && !row[kMkSellP + 64 + lane]);
+      pp1 = z0 ? __builtin_ctzll(z0) + 1 : z1 ? 65 + __builtin_ctzll(z1) : 0;
+    }
     if (lane == 0) {
       const int gold = ent[((size_t)e * NMMO_NF + F_GOLD) * S + a];  // the state the obs was taken from
       const uint4 head = make_uint4((uint32_t)(uint16_t)i16[0] | (uint32_t)(uint16_t)i16[1] << 16,
                                     (uint32_t)(uint16_t)i16[kNatI16Task] | (uint32_t)(uint16_t)i16[kNatI16Tile] << 16,
-                                    (uint32_t)(uint16_t)i16[kNatI16Tile + 1] | (uint32_t)nv << 16,
-                                    (uint32_t)ninv | (uint32_t)(exch ? 1 : 0) << 8 | (uint32_t)(uint16_t)gold << 16);
+                                    (uint32_t)(uint16_t)i16[kNatI16Tile + 1] | wire_m5(nv, ninv, exch, pp1) << 16,
+                                    wire_m6(style, move, ng, pp1) | (uint32_t)(uint16_t)gold << 16);
       *reinterpret_cast<uint4*>(rec) = head;
     }
-    if (lane < kWireMask / 4) {  // 32 of the non-Buy mask entries -> one word of bits
-      uint32_t bits = 0u;
-      for (int k = 0; k < 32; k++) {
-        const int b = 32 * lane + k;
-        if (b < kWireMaskBits && row[wire_bit_entry(b)]) bits |= 1u << k;
-      }
-      reinterpret_cast<uint32_t*>(rec + kWireHead)[lane] = bits;
-    }
-    uint16_t* d16 = reinterpret_cast<uint16_t*>(rec + kWireBody);
+    uint16_t* d16 = reinterpret_cast<uint16_t*>(rec + kWireHead);
     for (int k = lane; k < nv; k += 64) d16[k] = (uint16_t)idrank(ids, pre, i16[kNatI16Entity + NMMO_N_ENTITY_COLS * k]);
     int16_t* s16 = reinterpret_cast<int16_t*>(d16 + nv);
     for (int k = lane; k < ninv * 16; k += 64) s16[k] = i16[kNatI16Inv + k];
     uint8_t* mat = reinterpret_cast<uint8_t*>(s16 + ninv * 16);
-    const int pad = wire_record_bytes(c) - (kWireBody + 2 * nv + 32 * ninv);
     auto tile = [&](int t) { return t < 225 ? (int)i16[kNatI16Tile + 3 * t + 2] & 15 : 0; };
-    for (int u = lane; u < pad; u += 64) mat[u] = u < kWireTiles ? (uint8_t)(tile(2 * u) | tile(2 * u + 1) << 4) : 0;
+    for (int u = lane; u < kWireTiles; u += 64) mat[u] = (uint8_t)(tile(2 * u) | tile(2 * u + 1) << 4);
+    // the stream: bit i of AttackTarget / GiveTarget / GoldTarget (i < nv), then Destroy / GiveItem /
+    // SellItem / Use (i < ninv); a lane per bit, a byte per 8 lanes, then the zero pad
+    uint8_t* st = mat + kWireTiles;
+    const int B = 3 * nv + 4 * ninv, pad = wire_record_bytes(c) - wire_off_stream(nv, ninv);
+    for (int i0 = 0; i0 < 8 * pad; i0 += 64) {
+      const int i = i0 + lane;
+      int k = i, sec;
+      if (k < 3 * nv) {
+        sec = k / max(nv, 1);
+        k -= sec * nv;
+        sec = sec == 0 ? kMkAttackT : sec == 1 ? kMkGiveT : kMkGoldT;
+      } else {
+        k -= 3 * nv;
+        const int q = min(k / max(ninv, 1), 3);
+        k -= q * ninv;
+        sec = q == 0 ? kMkDestroy : q == 1 ? kMkGiveI : q == 2 ? kMkSellI : kMkUse;
+      }
+      const uint64_t b = __ballot(i < B && row[sec + k] != 0);
+      if ((lane & 7) == 0 && i < 8 * pad) st[i >> 3] = (uint8_t)(b >> lane);
+    }
   }
 }
 
@@ -375,10 +399,10 @@ __global__ void __launch_bounds__(256) wire_unpack_kernel(const uint8_t* wire, u
     const int nv = c & 127, ninv = (c >> 7) & 15;
     record_to_lds(penv + off[a], wire_record_bytes(c) / 16, lrec);
     const int16_t* h16 = reinterpret_cast<const int16_t*>(lb);
-    const uint32_t* bits = reinterpret_cast<const uint32_t*>(lb + kWireHead);
-    const uint16_t* idx = reinterpret_cast<const uint16_t*>(lb + kWireBody);
-    const int16_t* s16 = reinterpret_cast<const int16_t*>(lb + kWireBody + 2 * nv);  // Inventory rows
-    const uint8_t* mat = lb + kWireBody + 2 * nv + 32 * ninv;
+    const uint16_t* idx = reinterpret_cast<const uint16_t*>(lb + kWireHead);
+    const int16_t* s16 = reinterpret_cast<const int16_t*>(lb + wire_off_inv(nv));  // Inventory rows
+    const uint8_t* mat = lb + wire_off_mat(nv, ninv);
+    const uint8_t* st = lb + wire_off_stream(nv, ninv);  // the mask bit stream
     const int r0 = h16[3], c0 = h16[4], task = h16[2];
     // mask bytes, 16 per lane (1,600 bytes = 100 stores)
     for (int k = lane; k < NMMO_NATIVE_MASK_BYTES / 16; k += 64) {
@@ -389,7 +413,7 @@ __global__ void __launch_bounds__(256) wire_unpack_kernel(const uint8_t* wire, u
 #pragma unroll
         for (int b = 0; b < 4; b++) {
           const int x = 16 * k + 4 * j + b;
-          wd |= (x < kMaskN && wire_mask_entry(x, bits, nm, lpo, h16) ? 1u : 0u) << (8 * b);
+          wd |= (x < kMaskN && wire_mask_entry_any(x, h16, st, nv, ninv, nm, lpo) ? 1u : 0u) << (8 * b);
         }
         q[j] = wd;
       }
@@ -479,11 +503,11 @@ __global__ void __launch_bounds__(256) wire_expand_kernel(ObsParams p) {
     const int nv = c & 127, ninv = (c >> 7) & 15;
     record_to_lds(penv + off[a], wire_record_bytes(c) / 16, lrec);
     const int16_t* h16 = reinterpret_cast<const int16_t*>(lb);
-    const uint32_t* bits = reinterpret_cast<const uint32_t*>(lb + kWireHead);
-    const uint16_t* idx = reinterpret_cast<const uint16_t*>(lb + kWireBody);
-    const int16_t* s16 = reinterpret_cast<const int16_t*>(lb + kWireBody + 2 * nv);  // Inventory rows
-    const uint8_t* mat = lb + kWireBody + 2 * nv + 32 * ninv;
-    const bool exch = ((uint16_t)h16[6] >> 8) != 0;
+    const uint16_t* idx = reinterpret_cast<const uint16_t*>(lb + kWireHead);
+    const int16_t* s16 = reinterpret_cast<const int16_t*>(lb + wire_off_inv(nv));  // Inventory rows
+    const uint8_t* mat = lb + wire_off_mat(nv, ninv);
+    const uint8_t* st = lb + wire_off_stream(nv, ninv);
+    const bool exch = wire_exch(h16);
     const int gold = h16[7], aid = h16[0];
     for (int j = lane; j < p.o_agent_id; j += 64) {
       bool m;
@@ -491,8 +515,7 @@ __global__ void __launch_bounds__(256) wire_expand_kernel(ObsParams p) {
         const int k = j - kWireBuyLo;
         m = k == NMMO_MARKET_ROWS || (exch && k < nm && mk[16 * k + 15] <= gold && mk[16 * k + 2] != aid);
       } else {
-        const int b = entry_wire_bit(j);
-        m = (bits[b >> 5] >> (b & 31)) & 1u;
+        m = wire_mask_entry(j, h16, st, nv, ninv);
       }
       row[j] = m ? 1.f : 0.f;
     }
@@ -558,11 +581,11 @@ __global__ void __launch_bounds__(256) record_gather_kernel(ObsParams p, NmmoRec
   const int nv = c & 127, ninv = (c >> 7) & 15;
   record_to_lds(penv + tb + before, wire_record_bytes(c) / 16, lrec);
   const int16_t* h16 = reinterpret_cast<const int16_t*>(lb);
-  const uint32_t* bits = reinterpret_cast<const uint32_t*>(lb + kWireHead);
-  const uint16_t* ix = reinterpret_cast<const uint16_t*>(lb + kWireBody);
-  const int16_t* s16 = reinterpret_cast<const int16_t*>(lb + kWireBody + 2 * nv);  // Inventory rows
-  const uint8_t* mat = lb + kWireBody + 2 * nv + 32 * ninv;
-  const bool exch = ((uint16_t)h16[6] >> 8) != 0;
+  const uint16_t* ix = reinterpret_cast<const uint16_t*>(lb + kWireHead);
+  const int16_t* s16 = reinterpret_cast<const int16_t*>(lb + wire_off_inv(nv));  // Inventory rows
+  const uint8_t* mat = lb + wire_off_mat(nv, ninv);
+  const uint8_t* st = lb + wire_off_stream(nv, ninv);
+  const bool exch = wire_exch(h16);
   const int gold = h16[7], aid = h16[0];
   for (int j = lane; j < p.o_agent_id; j += 64) {
     bool m;
@@ -570,8 +593,7 @@ __global__ void __launch_bounds__(256) record_gather_kernel(ObsParams p, NmmoRec
       const int q = j - kWireBuyLo;
       m = q == NMMO_MARKET_ROWS || (exch && q < nm && mk[16 * q + 15] <= gold && mk[16 * q + 2] != aid);
     } else {
-      const int b = entry_wire_bit(j);
-      m = (bits[b >> 5] >> (b & 31)) & 1u;
+      m = wire_mask_entry(j, h16, st, nv, ninv);
     }
     row[j] = m ? 1.f : 0.f;
   }

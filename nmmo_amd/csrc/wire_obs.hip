@@ -5,9 +5,10 @@
 // tests/test_gpu_wire.py), built for what a record is: ~0.3 KB per agent of bits, entity-table
 // indices and a few rows, so the kernel is bound by the per-agent dependency chain, not bytes.
 // Window compaction (over wire_count_kernel's packed row words) and the ActionTargets bit fields
-// are agent_obs.h's (shared with the native kernel); the 561-bit image is assembled with scalar ops and goes out with the head
-// as one dword store, the Entity rows as u16 entity-table indices, then u16 stores for the
-// Inventory rows, the 4-bit materials and the zero pad. The env's entity table (the rows some
+// are agent_obs.h's (shared with the native kernel); the head (with the Style / Move / GoldPrice /
+// SellPrice sections folded into two of its words) goes out as one dword store, the Entity rows as
+// u16 entity-table indices, then u16 stores for the Inventory rows, the 4-bit materials, the
+// mask bit stream (3 nv + 4 ninv bits from ballots) and the zero pad. The env's entity table (the rows some
 // record shows, one 62-B row each) is written once per env from the columns in HBM.
 // The header's count words, entity-table ranks and per-env offsets come from wire_count_kernel +
 // wire_scan_kernel (wire.hip): record sizes are taken from the count words, so records never
@@ -147,41 +148,75 @@ __global__ void __launch_bounds__(64 * kWoWaves) wire_obs_kernel(ObsParams p) {
     ag.ninv = ninv;
     ag.prev_price = kWrap ? __builtin_amdgcn_readlane(my_prev, j) : -1;
     ag.mv = mv;
-    uint32_t img[(kWireMaskBits + 31) / 32];  // the 561-bit image, wave-uniform
-    ao_image<false>(ao_sections<kWrap>(p, T, Sp, visw, ag, it), img);
-    // record: head (4 dwords) | mask image (18 + 2 zero dwords): lane i holds dword i, one store
+    // the ActionTargets as what they are made of (wire.h v4): head words m5 / m6 and a bit stream
+    // of the first nv entries of the 3 target sections and the first ninv of the 4 inventory ones
+    const AoSections x = ao_sections<kWrap>(p, T, Sp, visw, ag, it);
+    int pp1 = 0;  // 1 + the SellPrice entry the wrapper cleared
+    if (exch) {
+      const uint64_t z0 = ~x.s10[0], z1 = ~x.s10[1] & low_bits(kSecN[10] - 64);
+      pp1 = z0 ? __builtin_ctzll(z0) + 1 : z1 ? 65 + __builtin_ctzll(z1) : 0;
+    }
+    const int ng = __popcll(x.s6[0]) + __popcll(x.s6[1]);
+    const int B = 3 * nv + 4 * ninv;  // stream bits
+    uint64_t W[6];                    // the stream, 64 bits per ballot (B <= 348)
+#pragma unroll
+    for (int q = 0; q < 6; q++) {
+      W[q] = 0ull;
+      if (64 * q >= B) continue;  // wave-uniform
+      int k = 64 * q + lane;
+      uint64_t lo = 0ull, hi = 0ull;
+      if (k < nv) {
+        lo = x.s1[0], hi = x.s1[1];
+      } else if ((k -= nv) < nv) {
+        lo = x.s5[0], hi = x.s5[1];
+      } else if ((k -= nv) < nv) {
+        lo = x.s7[0], hi = x.s7[1];
+      } else {
+        k -= nv;
+        lo = k < ninv ? x.s3 : k < 2 * ninv ? x.s4 : k < 3 * ninv ? x.s9 : x.s11;
+        k -= k < ninv ? 0 : k < 2 * ninv ? ninv : k < 3 * ninv ? 2 * ninv : 3 * ninv;
+      }
+      const uint64_t wd = k < 64 ? lo : hi;
+      W[q] = __ballot(64 * q + lane < B && ((wd >> (k & 63)) & 1ull));
+    }
     uint8_t* rec = wenv + woff[a];
     {
       const int task = __builtin_amdgcn_readlane(my_task, j);
-      const uint32_t head[4] = {i16pack(aid, tick), i16pack(task, r - kVision), i16pack(c - kVision, nv),
-                                i16pack(ninv | (exch ? 1 << 8 : 0), gold)};
-      int x = 0;  // lanes 22, 23: the image's zero pad
-      x = writelanes<0, 0, 4>(head, x);
-      x = writelanes<4, 0, (kWireMaskBits + 31) / 32>(img, x);
-      if (lane < (kWireBody >> 2)) reinterpret_cast<int*>(rec)[lane] = x;
+      const uint32_t head[4] = {i16pack(aid, tick), i16pack(task, r - kVision),
+                                i16pack(c - kVision, (int)wire_m5(nv, ninv, exch, pp1)),
+                                i16pack((int)wire_m6(x.s0 != 0ull, x.s8, ng, pp1), gold)};
+      int hx = 0;
+      hx = writelanes<0, 0, 4>(head, hx);
+      if (lane < 4) reinterpret_cast<int*>(rec)[lane] = hx;
     }
     // Entity rows: each visible row's entity-table index
-    if (lane < nv) reinterpret_cast<uint16_t*>(rec + kWireBody)[lane] = rk[ao_slot(visw[lane])];
-    if (lane + 64 < nv) reinterpret_cast<uint16_t*>(rec + kWireBody)[lane + 64] = rk[ao_slot(visw[lane + 64])];
-    // Inventory rows | materials (4 bits, 4 per int16) | zero pad, as int16 stores
+    if (lane < nv) reinterpret_cast<uint16_t*>(rec + kWireHead)[lane] = rk[ao_slot(visw[lane])];
+    if (lane + 64 < nv) reinterpret_cast<uint16_t*>(rec + kWireHead)[lane + 64] = rk[ao_slot(visw[lane + 64])];
+    // Inventory rows | materials (4 bits, 4 per int16) | the mask stream | zero pad, as int16 stores
     {
-      const int R = kWireBody + 2 * nv;
+      const int R = wire_off_inv(nv);
       const int H = (wire_record_bytes(cw) - R) >> 1;
-      const int ni = 16 * ninv;
+      const int ni = 16 * ninv, nt = kWireTiles / 2, ns = wire_stream_bytes(nv, ninv) / 2;
       const uint32_t* wm32 = reinterpret_cast<const uint32_t*>(wmat);
       int16_t* dst = reinterpret_cast<int16_t*>(rec + R);
       for (int h0 = 0; h0 < H; h0 += 64) {
         const int h = h0 + lane;
         const int q = min(h >> 4, kInv - 1);
         const uint2 iw = make_uint2((uint32_t)__shfl((int)it.x, q), (uint32_t)__shfl((int)it.y, q));
-        int x = 0;
+        int v16 = 0;
         if (h < ni) {
-          x = (int)item_col(iw, aid, h & 15);
-        } else if (h - ni < (kWireTiles + 1) / 2) {
+          v16 = (int)item_col(iw, aid, h & 15);
+        } else if (h - ni < nt) {
           const uint32_t m4 = wm32[h - ni] & 0x0F0F0F0Fu;
-          x = (int)((m4 & 15u) | (m4 >> 4 & 0xF0u) | (m4 >> 8 & 0xF00u) | (m4 >> 12 & 0xF000u));
+          v16 = (int)((m4 & 15u) | (m4 >> 4 & 0xF0u) | (m4 >> 8 & 0xF00u) | (m4 >> 12 & 0xF000u));
+        } else if (h - ni - nt < ns) {
+          const int m = h - ni - nt;
+          uint64_t wv = W[0];
+#pragma unroll
+          for (int u = 1; u < 6; u++) wv = (m >> 2) == u ? W[u] : wv;
+          v16 = (int)((wv >> (16 * (m & 3))) & 0xFFFFu);
         }
-        if (h < H) dst[h] = (int16_t)x;
+        if (h < H) dst[h] = (int16_t)v16;
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the next agent reuses visw / wmat

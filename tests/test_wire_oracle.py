@@ -68,7 +68,7 @@ def test_wire_entity_table():
             if not c & 0x8000:
                 continue
             nv = c & 127
-            idx = w[pos + owire.HEAD + owire.MASK:pos + owire.HEAD + owire.MASK + 2 * nv].copy().view(np.uint16)
+            idx = w[pos + owire.HEAD:pos + owire.HEAD + 2 * nv].copy().view(np.uint16)
             rows = i16[e, a, owire.I16_ENTITY:owire.I16_ENTITY + owire.NE * nv].reshape(-1, owire.NE)
             assert np.array_equal(table[idx], rows)
             seen.update(idx.tolist())
