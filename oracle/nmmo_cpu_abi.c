@@ -271,7 +271,8 @@ NMMO_API int64_t nmmo_wire_header_bytes(int32_t n_envs, int32_t player_n) {
 NMMO_API int64_t nmmo_wire_max_bytes(int32_t n_envs, int32_t player_n) {
   const int64_t hdr = nmmo_wire_header_bytes(n_envs, player_n);
   if (hdr < 0) return hdr;
-  const int64_t rec = (96 + 2 * 100 + 32 * NMMO_INV_SLOTS + 113 + 15) & ~15; /* SPEC §8c v3 record */
+  /* SPEC §8c v4 record: head, 100 indices, 12 Inventory rows, 114 B of materials, the mask stream */
+  const int64_t rec = (16 + 2 * 100 + 32 * NMMO_INV_SLOTS + 114 + 2 * ((3 * 100 + 4 * NMMO_INV_SLOTS + 15) / 16) + 15) & ~15;
   const int64_t table = (62 * 384 + 15) & ~15; /* a full entity table (kMaxSlots rows) */
   return hdr + (int64_t)n_envs * (table + (int64_t)player_n * rec + NMMO_NATIVE_MARKET_BYTES);
 }
