@@ -235,7 +235,7 @@ __global__ void record_reserve_kernel(NmmoExperience x, NmmoRecordStore rs, cons
   const int64_t base = (*rs.arena_used + 15) & ~(int64_t)15;
   const bool sane = total >= wire_header_bytes(n_envs, P) && total <= wire_cap && (total & 15) == 0 &&
                     base + 16 + total <= rs.arena_bytes;
-  // a buffer inside the arena is stored only at its own slot (record_reserve_serial)
+  // a buffer inside the arena is stored only at its own slot (record_reserve_wave)
   const bool inside = wire >= rs.arena && wire < rs.arena + rs.arena_bytes, placed = wire == rs.arena + base + 16;
   const bool ok = sane && (!inside || placed);
   *gate = ok ? (placed ? 2 : 1) : 0;  // 2: the buffer is in place already
@@ -298,26 +298,38 @@ __device__ __forceinline__ bool sb_selected(const NmmoExperience& x, const Store
   return false;
 }
 
-// The serial reservation of every input, in input order (one thread). An input is stored when its
-// announced total is a plausible buffer (>= its header, <= its capacity bound, 16-B multiple), it
-// fits, and (ist, the fused check's per-input bits, when given) it passed its check. gates[i]: 2 =
-// the buffer already sits where it is to be stored (received straight into the arena), 1 = copy
-// it there, 0 = not stored (x.status bit 2: no room / not plausible; bit 3: failed its check;
-// bit 4: the buffer lies inside the arena but not at its reserved slot -- a copy would read arena
-// bytes that earlier inputs of this store overwrite, so it is refused, never copied).
-__device__ void record_reserve_serial(const NmmoExperience& x, const NmmoRecordStore& rs, const StoreBatch& b,
-                                      int* gates, int64_t* rbase, const int* ist) {
+// The reservation of every input, in input order, by one wave: lane i loads input i's announced
+// total and check word (every load in flight at once -- one thread walking 16 inputs waited a
+// memory round trip per input), then lane 0 places them serially from registers. An input is
+// stored when its announced total is a plausible buffer (>= its header, <= its capacity bound,
+// 16-B multiple), it fits, and (ist, the check's per-input bits, when given) it passed its check.
+// gates[i]: 2 = the buffer already sits where it is to be stored (received straight into the
+// arena), 1 = copy it there, 0 = not stored (x.status bit 1: no room / not plausible; bit 3:
+// failed its check; bit 4: the buffer lies inside the arena but not at its reserved slot -- a
+// copy would read arena bytes that earlier inputs of this store overwrite, so it is refused,
+// never copied).
+__device__ void record_reserve_wave(const NmmoExperience& x, const NmmoRecordStore& rs, const StoreBatch& b,
+                                    int* gates, int64_t* rbase, const int* ist) {
+  const int lane = threadIdx.x;
+  int64_t tot = 0;
+  int chk = 0;
+  if (lane < b.n) {
+    tot = *reinterpret_cast<const int64_t*>(b.in[lane].wire);
+    chk = ist ? ist[lane] : 0;
+  }
   int64_t used = *rs.arena_used;
+  if (lane != 0) return;
   const uint8_t* a0 = rs.arena;
   for (int i = 0; i < b.n; i++) {
     const NmmoStoreInput& in = b.in[i];
     const int n_envs = in.n_rows / b.P;
     const uint8_t* w = reinterpret_cast<const uint8_t*>(in.wire);
-    const int64_t total = *reinterpret_cast<const int64_t*>(w);
+    const int64_t total = (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)tot, i) |
+                          (int64_t)__builtin_amdgcn_readlane((int)(tot >> 32), i) << 32;
     const int64_t base = (used + 15) & ~(int64_t)15;
     const bool sane = total >= wire_header_bytes(n_envs, b.P) && total <= b.wire_cap[i] && (total & 15) == 0 &&
                       base + 16 + total <= rs.arena_bytes;
-    const bool checked = !ist || ist[i] == 0;
+    const bool checked = __builtin_amdgcn_readlane(chk, i) == 0;
     const bool inside = w >= a0 && w < a0 + rs.arena_bytes;
     const bool placed = w == a0 + base + 16;
     const bool ok = sane && checked && (!inside || placed);
@@ -335,9 +347,9 @@ __device__ void record_reserve_serial(const NmmoExperience& x, const NmmoRecordS
   *rs.arena_used = used;
 }
 
-__global__ void record_reserve_many_kernel(NmmoExperience x, NmmoRecordStore rs, StoreBatch b, int* gates,
-                                           int64_t* rbase) {
-  record_reserve_serial(x, rs, b, gates, rbase, nullptr);
+__global__ void __launch_bounds__(64) record_reserve_many_kernel(NmmoExperience x, NmmoRecordStore rs, StoreBatch b,
+                                                                  int* gates, int64_t* rbase) {
+  record_reserve_wave(x, rs, b, gates, rbase, nullptr);
 }
 
 // The root's received-buffer check inside its store (nmmo_exp_store_records_checked): block (env,
@@ -357,10 +369,10 @@ __global__ void __launch_bounds__(128) record_check_kernel(StoreBatch b, StoreCh
   }
 }
 
-__global__ void record_reserve_checked_kernel(NmmoExperience x, NmmoRecordStore rs, StoreBatch b, StoreCheck c,
-                                              int* gates, int64_t* rbase) {
-  record_reserve_serial(x, rs, b, gates, rbase, c.ctl);
-  for (int k = 0; k < kMaxStoreInputs; k++) c.ctl[k] = 0;
+__global__ void __launch_bounds__(64) record_reserve_checked_kernel(NmmoExperience x, NmmoRecordStore rs, StoreBatch b,
+                                                                     StoreCheck c, int* gates, int64_t* rbase) {
+  record_reserve_wave(x, rs, b, gates, rbase, c.ctl);
+  if (threadIdx.x < kMaxStoreInputs) c.ctl[threadIdx.x] = 0;  // (every lane read its word above)
 }
 
 __global__ void __launch_bounds__(kStoreBlock) store_count_many_kernel(NmmoExperience x, StoreBatch b,
@@ -444,9 +456,9 @@ hipError_t launch_store_records_many(const NmmoExperience& x, const NmmoRecordSt
   int64_t* rbase = reinterpret_cast<int64_t*>(scratch + ((b.n * nb + 1 + b.n + 1) & ~1));  // [n], 8-B aligned
   if (chk) {
     hipLaunchKernelGGL(record_check_kernel, dim3(max_rows / b.P, b.n), dim3(128), 0, stream, b, *chk);
-    hipLaunchKernelGGL(record_reserve_checked_kernel, dim3(1), dim3(1), 0, stream, x, rs, b, *chk, gates, rbase);
+    hipLaunchKernelGGL(record_reserve_checked_kernel, dim3(1), dim3(64), 0, stream, x, rs, b, *chk, gates, rbase);
   } else {
-    hipLaunchKernelGGL(record_reserve_many_kernel, dim3(1), dim3(1), 0, stream, x, rs, b, gates, rbase);
+    hipLaunchKernelGGL(record_reserve_many_kernel, dim3(1), dim3(64), 0, stream, x, rs, b, gates, rbase);
   }
   hipLaunchKernelGGL(store_count_many_kernel, dim3(nb, b.n), dim3(kStoreBlock), 0, stream, x, b, (const int*)gates,
                      blk);

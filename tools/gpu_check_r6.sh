@@ -6,11 +6,20 @@ mkdir -p $out
 case "$1" in
 scale)  # the checked store, the rehearsal, the uneven 2-rank gather; then the C5 node model by root share
   timeout -k 10 900 python -u -m pytest -x -v --timeout 170 --timeout-method thread \
-    tests/test_gpu_wire.py tests/test_gpu_multirank.py > $out/tests_scale.log 2>&1 || exit 1
+    tests/test_gpu_wire.py tests/test_gpu_multirank.py tests/test_gpu_storage.py tests/test_gpu_faults.py \
+    > $out/tests_scale.log 2>&1 || exit 1
   for k in ${KS:-1024 768 512 256}; do
     timeout -k 10 400 python bench.py --config C5 --no-cpu-baseline --no-decode --steps 100 --warmup 20 \
       --root-envs $k --rehearse-copy > $out/c5_k$k.json 2> $out/c5_k$k.err || exit 1
   done
+  ;;
+rootprof)  # kernel trace of the C5 passes incl. the N = 8 root rehearsal at one root share
+  export TMPDIR=/tmp
+  timeout -k 10 240 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_wire.py \
+    > $out/tests_wire.log 2>&1 || exit 1
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/rootprof -o run -- \
+    python3 bench.py --config C5 --no-decode --root-envs ${K:-512} --steps 100 --warmup 20 --no-cpu-baseline \
+    > $out/rootprof.json 2> $out/rootprof.err || exit 1
   ;;
 *) echo "unknown step $1"; exit 2 ;;
 esac
