@@ -442,6 +442,12 @@ NMMO_API int nmmo_wire_check(const void* wire, int32_t n_envs, int32_t player_n,
 NMMO_API int nmmo_wire_check_many(const void* const* wires, const int32_t* n_envs,
                                   const int64_t* const* dev_expect_totals, int32_t n_bufs,
                                   int32_t player_n, int32_t* dev_status, void* stream);
+/* The learner gather's sizes row of one step (nmmo_amd.distributed.WireExchange.post_sizes):
+ * dev_row[j] = the announced total (first int64) of wires[j] for j < n_bufs (1..16 device wire
+ * buffers), dev_row[n_bufs] = *dev_fault (a device int32 tick fault word, or 0 when NULL), and
+ * *dev_fault is cleared. One launch, enqueued; graph-capturable; needs no handle. */
+NMMO_API int nmmo_sizes_row(const void* const* wires, int32_t n_bufs, int32_t* dev_fault, int64_t* dev_row,
+                            void* stream);
 /* The per-agent step records the learner gather ships beside each wire buffer: with dev_records
  * set (device, n_envs x player_n x 8 B; NULL = off), every nmmo_step that writes NMMO_OBS_WIRE obs
  * also writes, per agent, its reward (f32) | terminated | truncated | mask | 0 -- the step's rew /

@@ -29,7 +29,7 @@ SYMBOLS = [
     "nmmo_step_envs", "nmmo_inject_fault", "nmmo_fault_into", "nmmo_exp_store_records",
     "nmmo_exp_gather_records", "nmmo_exp_store_records_many", "nmmo_obs_invalidate", "nmmo_set_obs_counter",
     "nmmo_obs_bind", "nmmo_obs_invalidate_envs", "nmmo_exp_scratch_ints_many", "nmmo_set_step_records",
-    "nmmo_wire_check_many", "nmmo_exp_store_records_checked",
+    "nmmo_wire_check_many", "nmmo_exp_store_records_checked", "nmmo_sizes_row",
 ]
 
 
@@ -128,6 +128,7 @@ def declare(L):
     L.nmmo_wire_unpack.argtypes = [i32, i32, vp, vp, vp]
     L.nmmo_wire_check.argtypes = [vp, i32, i32, vp, vp, vp]
     L.nmmo_wire_check_many.argtypes = [vp, vp, vp, i32, i32, vp, vp]
+    L.nmmo_sizes_row.argtypes = [vp, i32, vp, vp, vp]
     L.nmmo_dev_alloc.argtypes = [i32, u64, ctypes.POINTER(vp)]
     L.nmmo_dev_free.argtypes = [vp]
     L.nmmo_build_info.restype = ctypes.c_char_p

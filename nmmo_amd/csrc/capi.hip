@@ -704,6 +704,36 @@ int nmmo_wire_check_many(const void* const* wires, const int32_t* n_envs, const 
   return NMMO_OK;
 }
 
+// the learner gather's sizes row of one step (nmmo_sizes_row): one launch instead of a copy per
+// buffer, a copy and a zero for the fault word
+struct SizesRowArgs {
+  const int64_t* w[kMaxCheckBufs];
+  int n;
+};
+__global__ void sizes_row_kernel(SizesRowArgs a, int32_t* fault, int64_t* row) {
+  const int j = threadIdx.x;
+  if (j < a.n) row[j] = *a.w[j];
+  if (j == a.n) {
+    row[j] = fault ? *fault : 0;
+    if (fault) *fault = 0;
+  }
+}
+
+int nmmo_sizes_row(const void* const* wires, int32_t n_bufs, int32_t* dev_fault, int64_t* dev_row, void* stream) {
+  if (!wires || !dev_row) return fail(NMMO_E_INVALID, "null argument");
+  if (n_bufs < 1 || n_bufs > kMaxCheckBufs) return fail(NMMO_E_INVALID, "n_bufs %d not in 1..%d", n_bufs, kMaxCheckBufs);
+  SizesRowArgs a;
+  memset(&a, 0, sizeof(a));
+  a.n = n_bufs;
+  for (int j = 0; j < n_bufs; j++) {
+    if (!wires[j] || ((uintptr_t)wires[j] & 7)) return fail(NMMO_E_INVALID, "buffer %d: null / not 8-B aligned", j);
+    a.w[j] = (const int64_t*)wires[j];
+  }
+  hipLaunchKernelGGL(sizes_row_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, a, dev_fault, dev_row);
+  HIP_TRY(hipGetLastError());
+  return NMMO_OK;
+}
+
 int nmmo_wire_unpack(int32_t n_envs, int32_t player_n, const void* wire, void* native, void* stream) {
   if (!wire || !native) return fail(NMMO_E_INVALID, "null argument");
   if (n_envs <= 0 || player_n <= 0 || player_n > 128) return fail(NMMO_E_INVALID, "n_envs > 0, player_n in 1..128");

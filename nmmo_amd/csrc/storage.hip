@@ -352,16 +352,16 @@ __global__ void __launch_bounds__(64) record_reserve_many_kernel(NmmoExperience 
   record_reserve_wave(x, rs, b, gates, rbase, nullptr);
 }
 
-// The root's received-buffer check inside its store (nmmo_exp_store_records_checked): block (env,
+// The root's received-buffer check inside its store (nmmo_exp_store_records_checked): wave (env,
 // input) runs the check of one env (wire_check_env, the bits of nmmo_wire_check_many) and ORs
 // what it finds into the input's status word c.ctl[i] and the caller's; the reservation that
 // follows (record_reserve_checked_kernel) stores only the inputs whose word stayed 0 and zeroes
 // the words again. (A last-block ticket that reserved inside this launch measured ~1 ms per step
 // at C5's 16 inputs x 512 envs: one agent-scope atomic per block on a single word.)
-__global__ void __launch_bounds__(128) record_check_kernel(StoreBatch b, StoreCheck c) {
-  const int i = blockIdx.y, e = blockIdx.x;
+__global__ void __launch_bounds__(64 * kCheckEnvsPerBlock) record_check_kernel(StoreBatch b, StoreCheck c) {
+  const int i = blockIdx.y, e = blockIdx.x * kCheckEnvsPerBlock + wave_id();
   const int n_envs = b.in[i].n_rows / b.P;
-  if (e >= n_envs || !((c.mask >> i) & 1u)) return;  // block-uniform
+  if (e >= n_envs || !((c.mask >> i) & 1u)) return;  // wave-uniform
   const int bad = wire_check_env(reinterpret_cast<const uint8_t*>(b.in[i].wire), n_envs, b.P, c.expect[i], e);
   if (bad) {
     atomicOr(&c.ctl[i], bad);
@@ -420,7 +420,11 @@ __global__ void __launch_bounds__(kStoreBlock) store_place_many_kernel(NmmoExper
     for (int h = 0; h < kHeads; h++) o[h] = a[h];
     x.env_id[s] = eid;
     x.step[s] = in.step;
-    x.seq[s] = atomicAdd(&x.slot_count[eid], 1);
+    // env ids are distinct within one store (nmmo_hip.h precondition): a plain read and write, no
+    // atomic round trip per row
+    const int q = x.slot_count[eid];
+    x.seq[s] = q;
+    x.slot_count[eid] = q + 1;
     rs.row_buf[s] = rbase[i];
     rs.row_agent[s] = r;
   }
@@ -455,7 +459,8 @@ hipError_t launch_store_records_many(const NmmoExperience& x, const NmmoRecordSt
   int* gates = total + 1;          // [n]
   int64_t* rbase = reinterpret_cast<int64_t*>(scratch + ((b.n * nb + 1 + b.n + 1) & ~1));  // [n], 8-B aligned
   if (chk) {
-    hipLaunchKernelGGL(record_check_kernel, dim3(max_rows / b.P, b.n), dim3(128), 0, stream, b, *chk);
+    hipLaunchKernelGGL(record_check_kernel, dim3((max_rows / b.P + kCheckEnvsPerBlock - 1) / kCheckEnvsPerBlock, b.n),
+                       dim3(64 * kCheckEnvsPerBlock), 0, stream, b, *chk);
     hipLaunchKernelGGL(record_reserve_checked_kernel, dim3(1), dim3(64), 0, stream, x, rs, b, *chk, gates, rbase);
   } else {
     hipLaunchKernelGGL(record_reserve_many_kernel, dim3(1), dim3(64), 0, stream, x, rs, b, gates, rbase);

@@ -189,43 +189,46 @@ __device__ inline void record_offsets_wave0(const uint16_t* cnt, int P, int* off
   if (lane == 0) off[P] = carry;
 }
 
-// Consistency of one received wire buffer of n envs x P agents (block per env): the announced
-// total (when expect_total is given), the env payload offsets against the count words and
-// listings, the counts' ranges, every record head's AgentId / nv / ninv against its count word
-// and its entity-table indices against the table. status bits: 1 total, 2 env offsets, 4 count
-// ranges, 8 record heads, 16 entity-table indices; returns this thread's bits (every thread of the
-// block calls it: barrier inside).
+// Consistency of one received wire buffer of n envs x P agents, one wave per env (lane l holds
+// agents l and l + 64: the record offsets are two wave scans in registers, no LDS, no barrier):
+// the announced total (when expect_total is given), the env payload offsets against the count
+// words and listings, the counts' ranges, every record head's AgentId / nv / ninv / closed-form
+// mask fields against its count word and its entity-table indices against the table. Returns
+// this lane's bits: 1 total, 2 env offsets, 4 count ranges, 8 record heads, 16 entity-table
+// indices.
 __device__ __forceinline__ int wire_check_env(const uint8_t* wire, int n, int P, const int64_t* expect_total, int e) {
   WireView v = wire_view(const_cast<uint8_t*>(wire), n, P);
-  __shared__ int off[129];
-  const int a = threadIdx.x;
+  const int lane = threadIdx.x & 63;
   const uint16_t* cnt = v.cnt + (size_t)e * P;
+  const uint32_t c0 = lane < P ? cnt[lane] : 0u, c1 = lane + 64 < P ? cnt[lane + 64] : 0u;
   const int ne = v.ecount[e];
-  record_offsets_wave0(cnt, P, off, wire_table_bytes(ne));
-  __syncthreads();
-  int bad = 0;
   const int64_t total = *v.total;
   const int64_t base = v.env_off[e];
   const int nm = v.mcount[e];
-  if (a == 0) {
+  const int x0 = wire_record_bytes(c0), x1 = wire_record_bytes(c1);
+  const int i0 = wave_incl_scan(x0), i1 = wave_incl_scan(x1);
+  const int tb = wire_table_bytes(ne), t0 = __builtin_amdgcn_readlane(i0, 63);
+  const int all = tb + t0 + __builtin_amdgcn_readlane(i1, 63);  // the listings' offset
+  int bad = 0;
+  if (lane == 0) {
     if (e == 0 && expect_total && total != *expect_total) bad |= 1;
     if (e == 0 && base != wire_header_bytes(n, P)) bad |= 2;
     const int64_t end = e + 1 < n ? v.env_off[e + 1] : total;
-    if (end - base != (int64_t)off[P] + 32 * nm) bad |= 2;
+    if (end - base != (int64_t)all + 32 * nm) bad |= 2;
     if (nm > NMMO_MARKET_ROWS || ne > kMaxSlots) bad |= 4;
   }
-  if (a < P) {
-    const uint32_t c = cnt[a];
+  auto agent = [&](uint32_t c, int off) {
+    int b = 0;
     if (c & 0x8000u) {
       const int nv = c & 127, ninv = (c >> 7) & 15;
       if (nv > kNObs || ninv > kInv || (c & 0x7800u)) {
-        bad |= 4;
-      } else if (base + off[a] + kWireHead <= total) {
-        const int16_t* h = reinterpret_cast<const int16_t*>(v.base + base + off[a]);
+        b |= 4;
+      } else if (base + off + kWireHead <= total) {
+        const int16_t* h = reinterpret_cast<const int16_t*>(v.base + base + off);
         if (h[0] <= 0 || ((uint16_t)h[5] & 0x7FFu) != (c & 0x7FFu) || wire_pp1(h) > 99 ||
             (((uint16_t)h[6] >> 6) & 127u) > 99)
-          bad |= 8;
-        if (base + off[a] + wire_record_bytes(c) <= total) {  // entity-table indices, 8 per 16-B load
+          b |= 8;
+        if (base + off + wire_record_bytes(c) <= total) {  // entity-table indices, 8 per 16-B load
           const uint4* ix4 = reinterpret_cast<const uint4*>(h + kWireHead / 2);
           uint4 q[(kNObs + 7) / 8];
 #pragma unroll
@@ -235,16 +238,21 @@ __device__ __forceinline__ int wire_check_env(const uint8_t* wire, int n, int P,
             const uint32_t wd[4] = {q[j].x, q[j].y, q[j].z, q[j].w};
 #pragma unroll
             for (int i = 0; i < 8; i++)
-              if (8 * j + i < nv && ((wd[i >> 1] >> (16 * (i & 1))) & 0xFFFFu) >= (uint32_t)ne) bad |= 16;
+              if (8 * j + i < nv && ((wd[i >> 1] >> (16 * (i & 1))) & 0xFFFFu) >= (uint32_t)ne) b |= 16;
           }
         }
       } else {
-        bad |= 2;
+        b |= 2;
       }
     } else if (c) {
-      bad |= 4;
+      b |= 4;
     }
-  }
+    return b;
+  };
+  bad |= agent(c0, tb + i0 - x0);
+  bad |= agent(c1, tb + t0 + i1 - x1);
   return bad;
 }
+constexpr int kCheckEnvsPerBlock = 4;  // one wave per env
+
 }  // namespace nmmo

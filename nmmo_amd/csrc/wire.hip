@@ -448,16 +448,19 @@ __global__ void __launch_bounds__(256) wire_unpack_kernel(const uint8_t* wire, u
   }
 }
 
-__global__ void __launch_bounds__(128) wire_check_kernel(const uint8_t* wire, int n, int P,
-                                                         const int64_t* expect_total, int* status) {
-  const int bad = wire_check_env(wire, n, P, expect_total, blockIdx.x);
+__global__ void __launch_bounds__(64 * kCheckEnvsPerBlock) wire_check_kernel(const uint8_t* wire, int n, int P,
+                                                                            const int64_t* expect_total, int* status) {
+  const int e = blockIdx.x * kCheckEnvsPerBlock + wave_id();
+  if (e >= n) return;
+  const int bad = wire_check_env(wire, n, P, expect_total, e);
   if (bad) atomicOr(status, bad);
 }
 // Every received buffer of a step in one launch: grid (max envs, buffers)
-__global__ void __launch_bounds__(128) wire_check_many_kernel(WireCheckBatch b, int P, int* status) {
-  const int i = blockIdx.y;
-  if ((int)blockIdx.x >= b.n[i]) return;
-  const int bad = wire_check_env(b.wire[i], b.n[i], P, b.expect[i], blockIdx.x);
+__global__ void __launch_bounds__(64 * kCheckEnvsPerBlock) wire_check_many_kernel(WireCheckBatch b, int P,
+                                                                                 int* status) {
+  const int i = blockIdx.y, e = blockIdx.x * kCheckEnvsPerBlock + wave_id();
+  if (e >= b.n[i]) return;
+  const int bad = wire_check_env(b.wire[i], b.n[i], P, b.expect[i], e);
   if (bad) atomicOr(status, bad);
 }
 
@@ -652,14 +655,16 @@ hipError_t launch_wire_check_many(const WireCheckBatch& b, int P, int* status, h
   int mx = 0;
   for (int i = 0; i < b.count; i++) mx = max(mx, b.n[i]);
   if (b.count <= 0 || mx <= 0) return hipSuccess;
-  hipLaunchKernelGGL(wire_check_many_kernel, dim3(mx, b.count), dim3(128), 0, s, b, P, status);
+  hipLaunchKernelGGL(wire_check_many_kernel, dim3((mx + kCheckEnvsPerBlock - 1) / kCheckEnvsPerBlock, b.count),
+                     dim3(64 * kCheckEnvsPerBlock), 0, s, b, P, status);
   return hipGetLastError();
 }
 
 hipError_t launch_wire_check(const uint8_t* wire, int n, int P, const int64_t* expect_total, int* status,
                              hipStream_t s) {
   if (P > 128 || n <= 0 || !status) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(wire_check_kernel, dim3(n), dim3(128), 0, s, wire, n, P, expect_total, status);
+  hipLaunchKernelGGL(wire_check_kernel, dim3((n + kCheckEnvsPerBlock - 1) / kCheckEnvsPerBlock),
+                     dim3(64 * kCheckEnvsPerBlock), 0, s, wire, n, P, expect_total, status);
   return hipGetLastError();
 }
 

@@ -174,13 +174,15 @@ class WireExchange:
             if self.cuda:
                 for ev in ready:
                     self.comm.wait_event(ev)
-            for j, w in enumerate(wires):
-                self.sizes[k, self.rank, j].copy_(w[:8].view(torch.int64)[0])
-            if fault is None:
-                self.sizes[k, self.rank, self.n_bufs].zero_()
+                _sizes_row(wires, fault, self.sizes[k, self.rank], self.comm)  # one launch (nmmo_sizes_row)
             else:
-                self.sizes[k, self.rank, self.n_bufs].copy_(fault[0])
-                fault.zero_()
+                for j, w in enumerate(wires):
+                    self.sizes[k, self.rank, j].copy_(w[:8].view(torch.int64)[0])
+                if fault is None:
+                    self.sizes[k, self.rank, self.n_bufs].zero_()
+                else:
+                    self.sizes[k, self.rank, self.n_bufs].copy_(fault[0])
+                    fault.zero_()
         if self.world > 1:
             if self.rank == self.dst:
                 self._p2p([], [(self.sizes[k, r], r) for r in self.peers])
@@ -250,6 +252,18 @@ class WireExchange:
 
     def done(self, t: int):
         return self._done[t % self.ring]
+
+
+def _sizes_row(wires, fault, row, stream):
+    """row[j] = wires[j]'s announced total, row[n] = *fault (then cleared): nmmo_sizes_row."""
+    import ctypes
+
+    from ._native import check, lib
+
+    n = len(wires)
+    ptrs = (ctypes.c_void_p * n)(*[w.data_ptr() for w in wires])
+    check(lib().nmmo_sizes_row(ptrs, n, None if fault is None else ctypes.c_void_p(fault.data_ptr()),
+                               ctypes.c_void_p(row.data_ptr()), ctypes.c_void_p(stream.cuda_stream)), "nmmo_sizes_row")
 
 
 class _null:

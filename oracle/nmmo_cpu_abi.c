@@ -280,6 +280,10 @@ NMMO_API int nmmo_wire_pack(NmmoHandle* h, const void* native, void* wire, void*
   (void)h; (void)native; (void)wire; (void)stream;
   UNSUPPORTED("nmmo_wire_pack");
 }
+NMMO_API int nmmo_sizes_row(const void* const* w, int32_t n, int32_t* f, int64_t* row, void* stream) {
+  (void)w; (void)n; (void)f; (void)row; (void)stream;
+  UNSUPPORTED("nmmo_sizes_row");
+}
 NMMO_API int nmmo_wire_unpack(int32_t n, int32_t p, const void* wire, void* native, void* stream) {
   (void)n; (void)p; (void)wire; (void)native; (void)stream;
   UNSUPPORTED("nmmo_wire_unpack");

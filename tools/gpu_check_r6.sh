@@ -21,5 +21,18 @@ rootprof)  # kernel trace of the C5 passes incl. the N = 8 root rehearsal at one
     python3 bench.py --config C5 --no-decode --root-envs ${K:-512} --steps 100 --warmup 20 --no-cpu-baseline \
     > $out/rootprof.json 2> $out/rootprof.err || exit 1
   ;;
+scale2)  # tests, then the root's kernel trace, then the model by root share
+  export TMPDIR=/tmp
+  timeout -k 10 900 python -u -m pytest -x -v --timeout 170 --timeout-method thread \
+    tests/test_gpu_wire.py tests/test_gpu_multirank.py tests/test_gpu_storage.py tests/test_gpu_faults.py \
+    > $out/tests_scale.log 2>&1 || exit 1
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/rootprof -o run -- \
+    python3 bench.py --config C5 --no-decode --root-envs ${K:-512} --steps 100 --warmup 20 --no-cpu-baseline \
+    > $out/rootprof.json 2> $out/rootprof.err || exit 1
+  for k in ${KS:-1024 512 256}; do
+    timeout -k 10 400 python bench.py --config C5 --no-cpu-baseline --no-decode --steps 100 --warmup 20 \
+      --root-envs $k > $out/c5_k$k.json 2> $out/c5_k$k.err || exit 1
+  done
+  ;;
 *) echo "unknown step $1"; exit 2 ;;
 esac
