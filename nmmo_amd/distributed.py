@@ -487,30 +487,74 @@ class WireGather:
                 recv = [(w, self._n_envs(*key), ex) for key, (w, sm), ex, chk in items if chk]
                 for k in range(0, len(recv), 16):
                     nw.check_buffers(recv[k:k + 16], self.P, self.status)
-            batch = []
-            for key, (w, sm), ex, chk in items:
-                n = self._n_envs(*key)
-                if self.native is not None:
-                    nw.unpack(w, n, self.P, out=self.native[key] if key[0] < self.world else self._rh_native[key])
-                if self.store is not None:  # learner mask = in the realm; no policy outputs modelled
-                    if self._zeros is None or self._zeros.numel() < n * self.P:
-                        self._zeros = torch.zeros(n * self.P, device=self.device)
-                        self._acts = torch.zeros((n * self.P, 12), dtype=torch.int32, device=self.device)
-                    z = self._zeros[:n * self.P]
-                    st = sm.view(-1)  # 8 B per agent: reward f32 | term | trunc | mask | pad
-                    batch.append(((w, st, st[4:], st[6:], self._acts[:n * self.P], z, z, self.env_base[key] * self.P),
-                                  ex, chk))
+            if self.native is not None:
+                for key, (w, sm), ex, chk in items:
+                    nw.unpack(w, self._n_envs(*key), self.P,
+                              out=self.native[key] if key[0] < self.world else self._rh_native[key])
             if self.store is not None:  # every buffer of the step as one store, checked in its reservation
                 self.store.reset()
-                for k in range(0, len(batch), 16):
-                    part = batch[k:k + 16]
-                    self.store.store_many([b for b, _, _ in part], s + 1, self.engines[0], field_stride=8,
-                                          expect=[ex for _, ex, _ in part], check_status=self.status,
-                                          checked=[c for _, _, c in part])
+                self._store_step(s, items)
                 self._stored += self.store.ptr_dev[0].to(torch.int64)
         if self.on_step is not None:
             torch.cuda.synchronize(self.device)
             self.on_step(s, got)
+
+    def _store_step(self, s: int, items):
+        """The root's store of step s's buffers (learner mask = in the realm; no policy outputs
+        modelled) as nmmo_exp_store_records_checked calls of up to 16 inputs, from ctypes input
+        arrays built once per ring slot: per step only the step number and the peers' buffer
+        pointers (their arena slots move with the announced sizes) are patched, so the host's
+        per-step work stays a few field writes and one call per 16 inputs."""
+        import ctypes
+
+        from . import abi
+        from ._native import check, lib
+
+        k = s % self.ring
+        plan = self._store_plans.get(k) if hasattr(self, "_store_plans") else None
+        if plan is None:
+            if not hasattr(self, "_store_plans"):
+                self._store_plans = {}
+            n_max = max(self._n_envs(*key) for key, _, _, _ in items)
+            if self._zeros is None or self._zeros.numel() < n_max * self.P:
+                self._zeros = torch.zeros(n_max * self.P, device=self.device)
+                self._acts = torch.zeros((n_max * self.P, 12), dtype=torch.int32, device=self.device)
+            chunks = []
+            for c0 in range(0, len(items), 16):
+                part = items[c0:c0 + 16]
+                arr = (abi.NmmoStoreInput * len(part))()
+                exp = (ctypes.c_void_p * len(part))()
+                mask = 0
+                for i, (key, (w, sm), ex, chk) in enumerate(part):
+                    n = self._n_envs(*key) * self.P
+                    st = sm.data_ptr()  # 8 B per agent: reward f32 | term | trunc | mask | pad
+                    arr[i] = abi.NmmoStoreInput(n, 0, None, None, st, st + 4, st + 6, None, self.env_base[key] * self.P,
+                                                self._acts.data_ptr(), self._zeros.data_ptr(), self._zeros.data_ptr(),
+                                                w.data_ptr())
+                    exp[i] = None if ex is None else ex.data_ptr()
+                    mask |= (1 << i) if chk else 0
+                chunks.append((arr, exp, mask, len(part)))
+            self.store._ensure_scratch(sum(self._n_envs(*key) for key, _, _, _ in items) * self.P,
+                                       min(16, len(items)), n_max * self.P)
+            if getattr(self.store, "_ctl", None) is None:
+                self.store._ctl = torch.zeros(abi.STORE_CTL_INTS, dtype=torch.int32, device=self.device)
+            self.store._engine = self.engines[0]
+            plan = self._store_plans[k] = chunks
+        st = self.store
+        stream = ctypes.c_void_p(self.x.comm.cuda_stream)
+        i0 = 0
+        for arr, exp, mask, n in plan:
+            for i in range(n):
+                key, (w, _), _, _ = items[i0 + i]
+                arr[i].step = s + 1
+                if key[0] > 0 and key[0] < self.world:  # a peer's buffer: where this step received it
+                    arr[i].wire = w.data_ptr()
+            i0 += n
+            check(lib().nmmo_exp_store_records_checked(self.engines[0].h, ctypes.byref(st.x), ctypes.byref(st.records),
+                                                       arr, n, 8, exp, mask, ctypes.c_void_p(self.status.data_ptr()),
+                                                       ctypes.c_void_p(st._ctl.data_ptr()),
+                                                       ctypes.c_void_p(st.scratch.data_ptr()), stream),
+                  "nmmo_exp_store_records_checked")
 
     def step(self):
         t, k = self.t, self.t % self.ring
