@@ -34,5 +34,12 @@ scale2)  # tests, then the root's kernel trace, then the model by root share
       --root-envs $k > $out/c5_k$k.json 2> $out/c5_k$k.err || exit 1
   done
   ;;
+shares)  # the C5 node model at N = 2, 4, 8 with the default and neighbouring root shares
+  for nk in ${NKS:-2:984 4:832 8:512 8:640}; do
+    n=${nk%%:*}; k=${nk##*:}
+    timeout -k 10 400 python bench.py --config C5 --no-cpu-baseline --no-decode --steps 200 --warmup 30 \
+      --root-rehearsal $n --root-envs $k > $out/model_n${n}_k$k.json 2> $out/model_n${n}_k$k.err || exit 1
+  done
+  ;;
 *) echo "unknown step $1"; exit 2 ;;
 esac
