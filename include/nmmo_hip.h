@@ -344,6 +344,18 @@ NMMO_API int nmmo_observe(NmmoHandle* h, void* obs, void* stream);
 NMMO_API int nmmo_obs_bind(NmmoHandle* h, const void* obs);
 NMMO_API int nmmo_obs_invalidate(NmmoHandle* h, void* stream);
 NMMO_API int nmmo_obs_invalidate_envs(NmmoHandle* h, const int32_t* env_ids, int32_t n_ids, void* stream);
+/* nmmo_obs_invalidate_envs scoped to the sections a consumer writes (`sections`, a mask of
+ * NMMO_OBS_SEC_*): with NMMO_OBS_SEC_TILE alone only the listed envs' rows' Tile sections are
+ * forgotten -- the next gather rewrites every Tile entry of those rows (and re-zeroes the Tile of
+ * rows out of the realm) and stays incremental everywhere else: what the start-kit policy's
+ * in-place edit of Tile[:, :, :2] needs (baseline_policy.py:96-97). Any other mask, or a handle
+ * whose rows do not track the Tile section (native layout, slot counts not a multiple of 8),
+ * forgets the listed envs' whole rows. env_ids NULL = every env (n_ids ignored). Enqueued on
+ * `stream`; capture-safe. */
+#define NMMO_OBS_SEC_TILE 1u
+#define NMMO_OBS_SEC_ALL 0xFFFFFFFFu
+NMMO_API int nmmo_obs_invalidate_sections(NmmoHandle* h, const int32_t* env_ids, int32_t n_ids, uint32_t sections,
+                                          void* stream);
 NMMO_API int nmmo_set_obs_counter(NmmoHandle* h, uint64_t* dev_counter);
 
 /* Task table and per-player assignment (SPEC.md §12; nmmo.Env.reset(make_task_fn) /

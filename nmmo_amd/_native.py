@@ -30,6 +30,7 @@ SYMBOLS = [
     "nmmo_exp_gather_records", "nmmo_exp_store_records_many", "nmmo_obs_invalidate", "nmmo_set_obs_counter",
     "nmmo_obs_bind", "nmmo_obs_invalidate_envs", "nmmo_exp_scratch_ints_many", "nmmo_set_step_records",
     "nmmo_wire_check_many", "nmmo_exp_store_records_checked", "nmmo_sizes_row",
+    "nmmo_obs_invalidate_sections",
 ]
 
 
@@ -98,6 +99,7 @@ def declare(L):
     L.nmmo_obs_invalidate.argtypes = [vp, vp]
     L.nmmo_obs_bind.argtypes = [vp, vp]
     L.nmmo_obs_invalidate_envs.argtypes = [vp, vp, i32, vp]
+    L.nmmo_obs_invalidate_sections.argtypes = [vp, vp, i32, ctypes.c_uint32, vp]
     L.nmmo_set_obs_counter.argtypes = [vp, vp]
     L.nmmo_set_step_records.argtypes = [vp, vp, vp]
     xp = ctypes.POINTER(abi.NmmoExperience)

@@ -37,6 +37,8 @@ SYS_ALL = 0xFF
 OBS_NONE = 0
 OBS_FLAT = 1
 OBS_NATIVE = 2
+OBS_SEC_TILE = 1  # nmmo_obs_invalidate_sections: the Tile section
+OBS_SEC_ALL = 0xFFFFFFFF
 STORE_CTL_INTS = 16  # nmmo_exp_store_records_checked's device words (per-input check bits)
 OBS_WIRE = 3  # SPEC.md §8c wire records straight from the state (the learner-gather transport)
 # native layout (SPEC.md §8b)

@@ -634,6 +634,36 @@ int nmmo_obs_invalidate_envs(NmmoHandle* h, const int32_t* env_ids, int32_t n_id
   return NMMO_OK;
 }
 
+// the Tile sections of the listed envs' rows (all envs when ids is NULL): kZsTile in their state
+__global__ void obs_forget_tile_kernel(uint64_t* zst, const int32_t* ids, int n_envs, int P) {
+  const int e = ids ? ids[blockIdx.x] : (int)blockIdx.x;
+  if ((unsigned)e >= (unsigned)n_envs) return;
+  for (int a = threadIdx.x; a < P; a += blockDim.x) zst[(size_t)e * P + a] |= kZsTile;
+}
+
+int nmmo_obs_invalidate_sections(NmmoHandle* h, const int32_t* env_ids, int32_t n_ids, uint32_t sections,
+                                 void* stream) {
+  if (!h) return fail(NMMO_E_INVALID, "null handle");
+  if (!env_ids) n_ids = h->st.n_envs;
+  if (n_ids < 0 || n_ids > h->st.n_envs) return fail(NMMO_E_INVALID, "n_ids %d not in 0..%d", n_ids, h->st.n_envs);
+  if (!h->d_zrow || n_ids == 0 || sections == 0) return NMMO_OK;
+  HIP_TRY(hipSetDevice(h->device));
+  // the Tile section alone is tracked per row by the flat rows of flat_obs.hip (slots a multiple of
+  // 8); any other section, layout or kernel forgets the listed envs' whole rows
+  const bool tile_only = sections == NMMO_OBS_SEC_TILE && h->cfg.obs_layout == NMMO_OBS_FLAT && h->st.S % 8 == 0;
+  if (!tile_only) {
+    if (!env_ids) {
+      HIP_TRY(hipMemsetAsync(h->d_zrow, 0, (size_t)h->st.n_envs * h->st.P * 8, (hipStream_t)stream));
+      return NMMO_OK;
+    }
+    return nmmo_obs_invalidate_envs(h, env_ids, n_ids, stream);
+  }
+  hipLaunchKernelGGL(obs_forget_tile_kernel, dim3(n_ids), dim3(128), 0, (hipStream_t)stream,
+                     h->d_zrow + (size_t)h->st.n_envs * h->st.P, env_ids, h->st.n_envs, h->st.P);
+  HIP_TRY(hipGetLastError());
+  return NMMO_OK;
+}
+
 int nmmo_set_obs_counter(NmmoHandle* h, uint64_t* dev_rows) {
   if (!h) return fail(NMMO_E_INVALID, "null handle");
   if (dev_rows) {  // the kernels add into it: it must be device memory of the handle's device

@@ -286,6 +286,7 @@ __global__ void __launch_bounds__(64 * kAoWaves) flat_obs_kernel(ObsParams p) {
   const bool zzl = zvl && (my_s & kZsZero);
   const uint64_t zvalid = __ballot(zvl), zzero = __ballot(zzl), ztask = __ballot(zvl && !zzl && zs_task(my_s) == my_task);
   const uint64_t zextv = __ballot(zvl && !zzl && (my_s & kZsExt));
+  const uint64_t ztile = __ballot(zvl && (my_s & kZsTile));  // its Tile section was written by a consumer
   // the extended state (ObsParams::zext): lane 10 j + slot = agent j's tracked chunk `slot`, lane
   // 40 + j its Tile position; lane 12 j + k (inv) its item word k
   uint2 img = make_uint2(0u, 0u), pinv = make_uint2(0u, 0u);
@@ -338,7 +339,15 @@ __global__ void __launch_bounds__(64 * kAoWaves) flat_obs_kernel(ObsParams p) {
     const int hj = __builtin_amdgcn_readlane(my_h, j);
     const int hv = hj & 4095, hm = hj >> 12;
     if (!__builtin_amdgcn_readlane(my_alive, j)) {  // not in the realm: an all-zero row
-      if ((zzero >> j) & 1) continue;  // zeroed by an earlier launch into this buffer
+      if ((zzero >> j) & 1) {  // zeroed by an earlier launch into this buffer
+        if ((ztile >> j) & 1) {  // ... but a consumer wrote into its Tile section since
+          wave_zero(row, kFoTask + tdim, elems);
+          nbytes += 4ull * (elems - kFoTask - tdim);
+          if (lane == 0) kp->zst[(size_t)e * P + a] = kZsZero;
+          nrows++;
+        }
+        continue;
+      }
       if (zv) {  // zero what the last write left nonzero
         wave_zero(row, 0, kFoEntity + hv * NMMO_N_ENTITY_COLS);
         wave_zero(row, kFoInv, kFoMarket + hm * 16);
@@ -498,7 +507,8 @@ __global__ void __launch_bounds__(64 * kAoWaves) flat_obs_kernel(ObsParams p) {
     // row (column) components are not stored when the row was last written at the same agent row
     // (column): a move changes one of the two, staying neither
     const uint32_t ppos = (uint32_t)__builtin_amdgcn_readlane((int)img.x, 40 + j);
-    const bool same_r = ext && (int)(ppos & 255u) == r, same_c = ext && (int)((ppos >> 8) & 255u) == c;
+    const bool tkn = ext && !((ztile >> j) & 1);  // the Tile section holds what this kernel wrote
+    const bool same_r = tkn && (int)(ppos & 255u) == r, same_c = tkn && (int)((ppos >> 8) & 255u) == c;
     if (!(NMMO_FO_ABL & 16)) {
       float* dt = row + kFoTask + tdim + 3 * lane;
 #pragma unroll

@@ -118,6 +118,9 @@ struct ObsParams {
 };
 constexpr uint64_t kZsZero = 1ull << 20;
 constexpr uint64_t kZsExt = 1ull << 21;  // the row's extended state (ObsParams::zext) is valid
+// the row's Tile section holds unknown values (a consumer wrote into it, nmmo_obs_invalidate_sections):
+// the next flat gather rewrites the whole section (an all-zero row: zeroes it), and forgets the bit
+constexpr uint64_t kZsTile = 1ull << 22;
 constexpr int kZext = 10 + 1 + 12;       // u64 per row: chunk masks | position | item words
 __host__ __device__ inline int zs_hv(uint64_t s) { return (int)(s & 255u); }
 __host__ __device__ inline int zs_hm(uint64_t s) { return (int)((s >> 8) & 4095u); }

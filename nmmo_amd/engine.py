@@ -288,6 +288,20 @@ class NmmoEngine:
                   "nmmo_obs_invalidate_envs")
         self._inv_ids = env_ids  # alive until the stream has read it
 
+    def obs_invalidate_sections(self, sections: int, env_ids=None):
+        """Forget only the given sections (abi.OBS_SEC_*) of the listed envs' obs rows
+        (nmmo_obs_invalidate_sections; env_ids a contiguous int32 tensor on the device, None =
+        every env): OBS_SEC_TILE alone makes the next gather rewrite those rows' Tile sections and
+        stay incremental elsewhere. Enqueued on the current stream."""
+        if env_ids is not None and (env_ids.dtype != torch.int32 or env_ids.device != self.device
+                                    or not env_ids.is_contiguous()):
+            raise ValueError("env_ids must be a contiguous int32 tensor on the engine's device")
+        with torch.cuda.device(self.device):
+            check(lib().nmmo_obs_invalidate_sections(self.h, None if env_ids is None else self._ptr(env_ids),
+                                                     0 if env_ids is None else env_ids.numel(), int(sections),
+                                                     self._stream()), "nmmo_obs_invalidate_sections")
+        self._inv_ids = env_ids
+
     def get_fault(self) -> int:
         """The tick fault word (nmmo_get_fault: NMMO_FAULT_* | env << 8, 0 = none), then cleared."""
         f = ctypes.c_int32()

@@ -27,13 +27,17 @@ batch of contiguous envs), which the engine writes incrementally (nmmo_obs_bind:
 what differs from what the buffer already holds). In the reference the trainer's `.to(device)`
 copies the shared-memory rows, so a policy may edit its input in place -- the start-kit's
 TileEncoder does (`tile[:, :, :2] -= ...; += 7`, baseline_policy.py:96-97, on
-unpack_batched_obs views). So by default (`obs_readonly=False`) `send` forgets the row state of
-the envs whose rows the last `recv` handed out (nmmo_obs_invalidate_envs) before it steps them:
-their next gather rewrites those rows in full, and every `recv` returns the bytes of a full write
-whatever the consumer did to the previous ones. `obs_readonly=True` is the consumer's promise not
-to write into the returned rows (a policy that copies first, a learner that only reads): the rows
-stay incremental, ~6 KB stored per 96-KB row. A batch that wraps around the env
-range is returned as a copy and needs neither.
+unpack_batched_obs views); the takeru and yaofeng policies only read theirs. `obs_writes` names
+the sections a consumer writes into: before `send` steps the envs whose rows the last `recv`
+handed out, their state for those sections is forgotten, so every `recv` returns the bytes of a
+full write whatever the consumer did to the previous ones:
+  - `{"Tile"}`: only the Tile sections are rewritten in full next step (nmmo_obs_invalidate_sections);
+    every other section stays incremental;
+  - `set()` (or `obs_readonly=True`): the consumer writes nothing; the rows stay incremental;
+  - `"all"`: whole rows are rewritten (nmmo_obs_invalidate_envs; the full-write cost).
+The default (`obs_writes=None`) is what the policy of the agent env_creator names writes
+(`AGENT_OBS_WRITES`: the start-kit `{"Tile"}`, takeru / yaofeng nothing), and `"all"` when no agent
+is named. A batch that wraps around the env range is returned as a copy and needs none of it.
 
 Protocol 1 — `NmmoEnv` exposes `reset(seed)` / `step(actions)` with per-agent dict
 observations (the unflattened layout) like `nmmo.Env`, for wrappers such as
@@ -117,6 +121,31 @@ def _as_dict(ns) -> dict:
     return dict(vars(ns))
 
 
+# What each reference agent's Policy writes into its observation input in place (agent_zoo/<agent>):
+# the start-kit TileEncoder edits Tile[:, :, :2] (neurips23_start_kit/baseline_policy.py:96-97); the
+# takeru (ReducedTileEncoder slices, policy.py:85-97) and yaofeng (policy.py:91-106) policies only read.
+AGENT_OBS_WRITES = {"neurips23_start_kit": frozenset({"Tile"}), "takeru": frozenset(), "yaofeng": frozenset()}
+OBS_SECTIONS = {"Tile": abi.OBS_SEC_TILE}
+
+
+def resolve_obs_writes(agent, obs_writes=None, obs_readonly=False):
+    """GpuVecEnv's obs_writes: frozenset of section names or "all" (module docstring)."""
+    if obs_readonly:
+        return frozenset()
+    if obs_writes is None:
+        return AGENT_OBS_WRITES.get(agent, "all")
+    if obs_writes == "all":
+        return "all"
+    if isinstance(obs_writes, str):
+        raise ValueError('obs_writes: a set of section names (e.g. {"Tile"}), "all" or None')
+    names = frozenset(obs_writes)
+    known = {k for k in layout.flat_layout() if k != "__total__"} | {"ActionTargets"}
+    unknown = names - known
+    if unknown:
+        raise ValueError(f"obs_writes: unknown obs sections {sorted(unknown)}")
+    return names
+
+
 def agent_from_creator(env_creator):
     """The agent whose RewardWrapper `environment.make_env_creator(reward_wrapper_cls=...)`
     closed over (environment.py:50-58, train.py:226): `agent_zoo.<agent>.reward_wrapper` ->
@@ -146,11 +175,11 @@ class GpuVecEnv:
     def __init__(self, env_creator=None, env_kwargs=None, num_envs=1, envs_per_worker=1,
                  envs_per_batch=None, env_pool=False, mask_agents=True, *, config=None,
                  device=None, seed=0, task_embedding=None, env_index_base=0, agent=None,
-                 obs_readonly=False):
-        """obs_readonly: the consumer never writes into the obs rows recv() returns (module
-        docstring); False (default) keeps in-place edits from reaching later recv() outputs."""
+                 obs_readonly=False, obs_writes=None):
+        """obs_writes: the obs sections the consumer writes into in place (module docstring): a set
+        of section names, "all", or None = what the named agent's policy writes (AGENT_OBS_WRITES;
+        "all" without an agent). obs_readonly=True is obs_writes=set()."""
         del envs_per_worker  # the engine replaces workers
-        self.obs_readonly = bool(obs_readonly)
         self._views_out = False  # the last recv() handed out views of the engine's obs buffer
         self.config = config or _config_from_kwargs(env_kwargs)
         rw = _as_dict(env_kwargs.get("reward_wrapper")) if isinstance(env_kwargs, dict) else {}
@@ -158,6 +187,8 @@ class GpuVecEnv:
             self.config.early_stop_agent_num = int(rw["early_stop_agent_num"])
         if agent is None:  # env_creator's RewardWrapper (environment.py:58), when it names one
             agent = agent_from_creator(env_creator)
+        self.obs_writes = resolve_obs_writes(agent, obs_writes, obs_readonly)
+        self.obs_readonly = self.obs_writes == frozenset()
         if self.config.obs_layout != abi.OBS_FLAT:
             raise ValueError("GpuVecEnv serves flat observations (obs_layout=OBS_FLAT)")
         self.num_envs = int(num_envs)
@@ -195,7 +226,23 @@ class GpuVecEnv:
             self._ids = torch.empty(epb, dtype=torch.int32, device=d)
 
     # -- protocol
+    def _forget(self, ids=None):
+        """Forget what the consumer may have written into the rows the last recv() handed out
+        (ids: their envs on the device; None = every env), as obs_writes says."""
+        e = self.engine
+        if not self._views_out or self.obs_readonly:
+            return
+        if self.obs_writes == "all" or any(s not in OBS_SECTIONS for s in self.obs_writes):
+            if ids is None:
+                e.obs_invalidate()
+            else:
+                e.obs_invalidate_envs(ids)
+        else:
+            e.obs_invalidate_sections(sum(OBS_SECTIONS[s] for s in self.obs_writes), ids)
+
     def async_reset(self, seed=None):
+        self._forget()  # the reset writes into the same rows (ADVICE r05)
+        self._views_out = False
         if seed is not None:
             self.engine.reset(reset_seeds(seed, self.env_index_base, self.num_envs))
         else:
@@ -263,10 +310,8 @@ class GpuVecEnv:
         batch, k, P, e = self._batch, self.envs_per_batch, self.agents_per_env, self.engine
         a = torch.as_tensor(actions)
         a = a.to(device=e.device, dtype=torch.int32).reshape(k, P, abi.N_ACTION_HEADS)
-        forget = self._views_out and not self.obs_readonly  # the consumer may have edited the rows
         if k == self.num_envs:  # lockstep (every recv returns 0..num_envs-1 in order)
-            if forget:
-                e.obs_invalidate()
+            self._forget()  # the consumer may have edited the rows recv handed out
             e.step(a)
         else:
             lo = batch[0]
@@ -276,8 +321,7 @@ class GpuVecEnv:
                 e.actions.index_copy_(0, torch.as_tensor(batch, dtype=torch.long, device=e.device), a)
             self._ids_host.copy_(torch.as_tensor(batch, dtype=torch.int32))
             self._ids.copy_(self._ids_host, non_blocking=True)
-            if forget:
-                e.obs_invalidate_envs(self._ids)
+            self._forget(self._ids)
             e.step_envs(self._ids)
         self._views_out = False
         self._ready.extend(batch)

@@ -361,6 +361,12 @@ NMMO_API int nmmo_obs_invalidate_envs(NmmoHandle* h, const int32_t* env_ids, int
   if (!h) return fail(NMMO_E_INVALID, "null handle");
   return NMMO_OK;  /* every obs call writes every row here */
 }
+NMMO_API int nmmo_obs_invalidate_sections(NmmoHandle* h, const int32_t* env_ids, int32_t n_ids, uint32_t sections,
+                                          void* stream) {
+  (void)env_ids; (void)n_ids; (void)sections; (void)stream;
+  if (!h) return fail(NMMO_E_INVALID, "null handle");
+  return NMMO_OK;  /* every obs call writes every row here */
+}
 NMMO_API int nmmo_set_obs_counter(NmmoHandle* h, uint64_t* c) {
   (void)h; (void)c;
   UNSUPPORTED("nmmo_set_obs_counter");

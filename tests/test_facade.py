@@ -115,3 +115,23 @@ def test_agent_from_env_creator_closure():
 
     assert _as_dict(SimpleNamespace(eval_mode=False, early_stop_agent_num=8)) == {
         "eval_mode": False, "early_stop_agent_num": 8}
+
+
+def test_obs_writes_follow_the_agent_policy():
+    """GpuVecEnv's obs contract defaults to what the named agent's policy writes into its input in
+    place: the start-kit TileEncoder's Tile edit (baseline_policy.py:96-97) scopes the rewrite to the
+    Tile sections; takeru / yaofeng write nothing; without an agent every row is rewritten."""
+    from nmmo_amd.vecenv import resolve_obs_writes
+
+    assert resolve_obs_writes("neurips23_start_kit") == frozenset({"Tile"})
+    assert resolve_obs_writes("takeru") == resolve_obs_writes("yaofeng") == frozenset()
+    assert resolve_obs_writes(None) == "all"
+    assert resolve_obs_writes(None, obs_readonly=True) == frozenset()
+    assert resolve_obs_writes("takeru", obs_writes="all") == "all"
+    assert resolve_obs_writes(None, obs_writes={"Tile", "Entity"}) == frozenset({"Tile", "Entity"})
+    import pytest
+
+    with pytest.raises(ValueError):
+        resolve_obs_writes(None, obs_writes={"Tiles"})
+    with pytest.raises(ValueError):
+        resolve_obs_writes(None, obs_writes="Tile")

@@ -1,13 +1,15 @@
 """The obs contract at the pool boundary (nmmo_amd.vecenv module docstring, nmmo_hip.h
-nmmo_obs_invalidate_envs). recv() hands out views of the engine's incrementally written obs
-buffer; the reference's default policy edits its input in place (the start-kit TileEncoder,
-agent_zoo/neurips23_start_kit/baseline_policy.py:96-97, on unpack_batched_obs views). With the
-default obs_readonly=False every recv() must still equal the oracle's full-write obs whatever the
-consumer did to the previous ones: here a consumer edits every recv() output in place -- the
-start-kit's Tile edit (idempotent) or a non-idempotent one that touches every region the
+nmmo_obs_invalidate_envs / nmmo_obs_invalidate_sections). recv() hands out views of the engine's
+incrementally written obs buffer; the reference's start-kit policy edits its input in place (the
+TileEncoder, agent_zoo/neurips23_start_kit/baseline_policy.py:96-97, on unpack_batched_obs views).
+Under the pool's obs_writes contract every recv() must still equal the oracle's full-write obs
+whatever the consumer did to the previous ones: here a consumer edits every recv() output in place
+-- the start-kit's Tile edit (idempotent) or a non-idempotent one that touches every region the
 incremental gather skips (Entity and Market zero tails, Buy entries, Task, rows of agents out of
 the realm) -- in the reference's default 15/6 async pool and in lockstep, over deaths and
-auto-resets. obs_readonly=True under the same edit diverges (the flag is what keeps it exact)."""
+auto-resets. obs_writes="all" rewrites whole rows; obs_writes={"Tile"} rewrites only the Tile
+sections and is exact for the start-kit edit; an edit outside the declared sections, or any edit
+under obs_readonly=True, diverges (the declaration is what keeps it exact)."""
 
 import collections
 
@@ -40,7 +42,7 @@ def non_idempotent_edit(o):
 EDITS = {"start_kit_tile": start_kit_tile_edit, "non_idempotent": non_idempotent_edit}
 
 
-def _run_pool(n, k, edit, readonly, steps, seed=5):
+def _run_pool(n, k, edit, readonly, steps, seed=5, writes=None, reset_at=None):
     """Drive GpuVecEnv like clean_pufferl.evaluate (recv -> policy -> send) against the oracle
     stepping each env on the same action stream; returns the recv() indices whose obs differed."""
     import torch
@@ -52,7 +54,7 @@ def _run_pool(n, k, edit, readonly, steps, seed=5):
     # deaths from tick ~22, early-stop resets from ~30 (oracle rollout of these seeds)
     cfg = Config.preset("C4", MAP_N=4, early_stop_agent_num=8)
     pool = GpuVecEnv(None, env_kwargs=None, num_envs=n, envs_per_batch=k, env_pool=k < n, config=cfg,
-                     seed=seed, obs_readonly=readonly)
+                     seed=seed, obs_readonly=readonly, obs_writes=writes)
     ref = OracleEnvs(cfg, n, seed=seed)
     pool.async_reset(1)
     ref.reset(env_seeds=reset_seeds(1, 0, n))
@@ -67,6 +69,11 @@ def _run_pool(n, k, edit, readonly, steps, seed=5):
             bad.append(step)
         dead_rows += int((~mask).sum())
         EDITS[edit](o)  # the consumer's in-place edit of what recv handed out
+        if step == reset_at:  # the pool resets right after a recv whose rows the consumer edited
+            pool.async_reset(2)
+            ref.reset(env_seeds=reset_seeds(2, 0, n))
+            order = collections.deque(range(n))
+            continue
         acts = ref.scripted_actions(500 + step)[batch]
         pool.send(acts.reshape(-1, 12).astype(np.int64))
         for j, e in enumerate(batch):
@@ -75,8 +82,9 @@ def _run_pool(n, k, edit, readonly, steps, seed=5):
         order.extend(batch)
     torch.cuda.synchronize()
     assert np.array_equal(pool.engine.get_state(), ref.get_state())
-    eps = ref.get_state().reshape(n, -1)[:, :64].copy().view(np.int32)[:, 3]  # E_EPISODE
-    assert (eps >= 1).all(), "every env auto-reset at least once"
+    if reset_at is None:
+        eps = ref.get_state().reshape(n, -1)[:, :64].copy().view(np.int32)[:, 3]  # E_EPISODE
+        assert (eps >= 1).all(), "every env auto-reset at least once"
     assert dead_rows > 0, "no agent out of the realm in the window"
     assert pool.engine.get_fault() == 0
     pool.close()
@@ -88,6 +96,33 @@ def _run_pool(n, k, edit, readonly, steps, seed=5):
 def test_mutating_consumer_gets_full_write_obs(edit, shape):
     n, k = shape
     bad = _run_pool(n, k, edit, readonly=False, steps=130 if k < n else 45)
+    assert not bad, f"recv() obs differ from the oracle at steps {bad}"
+
+
+@pytest.mark.parametrize("shape", [(15, 6), (4, 4)], ids=["pool15x6", "lockstep4"])
+def test_start_kit_edit_under_tile_writes_stays_exact(shape):
+    """obs_writes={"Tile"} (the start-kit agent's default): only the handed-out rows' Tile sections
+    are rewritten next step (nmmo_obs_invalidate_sections), including the Tile of rows out of the
+    realm the edit made nonzero, and every recv() equals the oracle."""
+    n, k = shape
+    bad = _run_pool(n, k, "start_kit_tile", readonly=False, steps=130 if k < n else 45, writes={"Tile"})
+    assert not bad, f"recv() obs differ from the oracle at steps {bad}"
+
+
+def test_edit_outside_the_declared_sections_diverges():
+    """The declaration is what keeps it exact: an edit of sections other than Tile under
+    obs_writes={"Tile"} leaves stale bytes in later recv() outputs."""
+    bad = _run_pool(4, 4, "non_idempotent", readonly=False, steps=45, writes={"Tile"})
+    assert bad, "an undeclared edit should leave stale bytes"
+
+
+@pytest.mark.parametrize("writes", [None, {"Tile"}], ids=["all", "tile"])
+def test_reset_after_an_edited_recv(writes):
+    """async_reset after a recv() whose rows the consumer edited: the reset's gather forgets what
+    the consumer may have written (the rows of every env), and the recv() after it equals the
+    oracle's reset obs."""
+    edit = "non_idempotent" if writes is None else "start_kit_tile"
+    bad = _run_pool(4, 4, edit, readonly=False, steps=40, writes=writes, reset_at=20)
     assert not bad, f"recv() obs differ from the oracle at steps {bad}"
 
 
