@@ -73,7 +73,8 @@ WORKLOADS = {
 }
 # (config, obs layout, wrapper) measured beside the headline
 EXTRAS = [("C2", None, None), ("C3", None, None), ("C4", "native", None), ("C5", None, None),
-          ("C4", None, "neurips23_start_kit"), ("C4", "flat-rezero", None)]
+          ("C4", None, "neurips23_start_kit"), ("C4", "flat-tile-writer", "neurips23_start_kit"),
+          ("C4", "flat-rezero", None)]
 EXTRAS_MULTI = [("C4", None, None)]
 
 # the agent sections' reward_wrapper weights (config.yaml:103-106, 118-126, 137-140)
@@ -408,6 +409,10 @@ def measure(args, name, layout_name, envs, rank, world, dev, steps, warmup, dist
     # "flat-rezero": every obs row written in full every step (NMMO_OBS_REZERO, nmmo_hip.h
     # nmmo_obs_invalidate), beside the headline's incremental rows
     rezero = layout_name == "flat-rezero"
+    # "flat-tile-writer": the start-kit consumer's contract (GpuVecEnv obs_writes={"Tile"}): every
+    # step first forgets every row's Tile section (nmmo_obs_invalidate_sections), as the pool does
+    # for rows whose Tile[:, :, :2] the start-kit TileEncoder edited in place (baseline_policy.py:96-97)
+    tile_writer = layout_name == "flat-tile-writer"
     if rezero:
         os.environ["NMMO_OBS_REZERO"] = "1"
     try:
@@ -446,6 +451,8 @@ def measure(args, name, layout_name, envs, rank, world, dev, steps, warmup, dist
             with torch.cuda.stream(streams[j]) if nb > 1 else contextlib.nullcontext():
                 for _ in range(k):
                     engs[j].scripted_actions(pseed)
+                    if tile_writer:
+                        engs[j].obs_invalidate_sections(abi.OBS_SEC_TILE)
                     engs[j].step()
 
     torch.cuda.synchronize(dev)  # the pre-roll ran on the default stream
@@ -550,7 +557,7 @@ def measure(args, name, layout_name, envs, rank, world, dev, steps, warmup, dist
     full_b = None  # §8(d)'s model: every row written in full
     if wl["obs"] and kern != "tick_kernel" and not rezero:
         full_b = obs_bytes_per_env(S, P, eng.obs_elems, native, alive_frac=alive / (envs * P * steps)) * per
-    prof_name = name + ("-native" if native else "-rezero" if rezero else "") + \
+    prof_name = name + ("-native" if native else "-rezero" if rezero else "-tilewriter" if tile_writer else "") + \
         ("" if wrapper == "none" else "+" + wrapper)
     launch = "eager" if not plans else f"hipGraph x{min(args.graph_steps, steps)} ticks"
     if nb > 1:
@@ -567,10 +574,13 @@ def measure(args, name, layout_name, envs, rank, world, dev, steps, warmup, dist
                               "full rows" if rezero else "stored bytes"),
         "batches": nb,
         "obs_contract": None if not wl["obs"] else
-        ("every row written in full each step (what GpuVecEnv's default obs_readonly=False gives a consumer that "
-         "may edit its rows in place)" if rezero else
+        ("every row written in full each step (GpuVecEnv obs_writes=\"all\": a consumer that may edit any "
+         "section in place)" if rezero else
+         "incremental rows with every Tile section rewritten each step (GpuVecEnv obs_writes={\"Tile\"}, the "
+         "start-kit agent's default: its TileEncoder edits Tile[:, :, :2] in place)" if tile_writer else
          "incremental rows into the engine's bound buffer: a row stores only what differs from what the buffer "
-         "holds (DESIGN.md §3.2c); valid for a read-only consumer (GpuVecEnv obs_readonly=True)"),
+         "holds (DESIGN.md §3.2c); valid for a read-only consumer (GpuVecEnv obs_writes=set(): the takeru and "
+         "yaofeng agents' default)"),
         "obs_rows_written_frac": round(row_frac, 4) if wl["obs"] else None,
         "obs_bytes_stored_per_agent_row": round(bytes_stored / (envs * P * steps), 1) if wl["obs"] else None,
     }
@@ -1101,6 +1111,11 @@ def main():
                                   "obs_ms": fw["kernel_ms"]["obs"], "roofline_frac": fw["roofline"]["frac"],
                                   "frac_of_write_ceiling": fw["roofline"]["frac_of_write_ceiling"],
                                   "see": "extra_configs.C4-rezero"}
+        tw = extras.get("C4-tilewriter+neurips23_start_kit") if res["name"] == "C4" else None
+        if tw:  # the reference's start-kit loop: its wrapper, its policy's Tile edit (obs_writes={"Tile"})
+            line["start_kit_consumer"] = {"value": tw["value"], "ms_per_step": tw["ms_per_step"],
+                                          "obs_ms": tw["kernel_ms"]["obs"], "see": "extra_configs.C4-tilewriter"
+                                          "+neurips23_start_kit"}
         line["extra_configs"] = extras or None
         line["build"] = _native.build_info()
         print(json.dumps(line), file=json_out, flush=True)

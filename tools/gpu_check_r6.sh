@@ -41,5 +41,12 @@ shares)  # the C5 node model at N = 2, 4, 8 with the default and neighbouring ro
       --root-rehearsal $n --root-envs $k > $out/model_n${n}_k$k.json 2> $out/model_n${n}_k$k.err || exit 1
   done
   ;;
+contract)  # the scoped obs contract: pool tests, zero-row tests, then the start-kit consumer's rate
+  timeout -k 10 900 python -u -m pytest -x -v --timeout 170 --timeout-method thread \
+    tests/test_gpu_obs_contract.py tests/test_gpu_zero_rows.py tests/test_gpu_vecenv.py \
+    > $out/tests_contract.log 2>&1 || exit 1
+  timeout -k 10 400 python bench.py --no-cpu-baseline --steps 100 --warmup 20 > $out/bench_default.json \
+    2> $out/bench_default.err || exit 1
+  ;;
 *) echo "unknown step $1"; exit 2 ;;
 esac
