@@ -122,7 +122,7 @@ def test_reset_after_an_edited_recv(writes):
     the consumer may have written (the rows of every env), and the recv() after it equals the
     oracle's reset obs."""
     edit = "non_idempotent" if writes is None else "start_kit_tile"
-    bad = _run_pool(4, 4, edit, readonly=False, steps=40, writes=writes, reset_at=20)
+    bad = _run_pool(4, 4, edit, readonly=False, steps=60, writes=writes, reset_at=35)
     assert not bad, f"recv() obs differ from the oracle at steps {bad}"
 
 
