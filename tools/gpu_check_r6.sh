@@ -48,5 +48,9 @@ contract)  # the scoped obs contract: pool tests, zero-row tests, then the start
   timeout -k 10 400 python bench.py --no-cpu-baseline --steps 100 --warmup 20 > $out/bench_default.json \
     2> $out/bench_default.err || exit 1
   ;;
+longrun)  # the row state at full size over 300 ticks (tracked vs full write; sampled envs vs the oracle)
+  timeout -k 10 400 python -u -m pytest -x -v --timeout 180 --timeout-method thread tests/test_gpu_longrun.py \
+    > $out/tests_longrun.log 2>&1 || exit 1
+  ;;
 *) echo "unknown step $1"; exit 2 ;;
 esac
