@@ -102,6 +102,11 @@ def tick_bytes_per_env(S: int, P: int, items: bool, events_per_env: float = 0.0,
     return int(2 * state + P * 4 + P * 12 * 4 + P * (4 + 1 + 1 + 1) + P * 6 + events_per_env * EVENT_ROW_BYTES)
 
 
+ROW_STATE_READ = 16 + 8 * 23   # per agent row: zrow + zst, then the extended state (ObsParams::zext, kZext u64)
+ROW_STATE_WRITE = 16 + 88      # per row written in the realm: zrow + zst, the 10 chunk masks + position (the
+                               # 12 item words, 96 B more, only when they changed: not counted)
+
+
 def obs_bytes_per_env(S: int, P: int, elems: int, native: bool = False, wire_bytes: float | None = None,
                       stored: float | None = None, alive_frac: float = 1.0) -> float:
     """Algorithmic bytes of one env's obs gather, each byte counted once:
@@ -111,18 +116,23 @@ def obs_bytes_per_env(S: int, P: int, elems: int, native: bool = False, wire_byt
     materials and 12 item words read. stored: the bytes one env's rows took in stores, as the
     kernel counted them (nmmo_set_obs_counter: a flat row stores only what differs from what
     the buffer holds already, nmmo_hip.h nmmo_obs_invalidate); alive_frac: the fraction of agents
-    in the realm (whose windows and items are read)."""
+    in the realm (whose windows and items are read). The incremental flat rows also read each
+    row's state and write it back for the rows in the realm (ROW_STATE_READ / ROW_STATE_WRITE,
+    flat_obs.hip: what lets a row store only what differs)."""
     from nmmo_amd import abi
 
+    state = 0.0
     if wire_bytes is not None:
         rows = wire_bytes
     elif stored is not None:
         rows = stored + (abi.native_env_bytes(P) - P * abi.NATIVE_ROW_BYTES if native else 0)  # + Market
+        if not native:
+            state = P * (ROW_STATE_READ + ROW_STATE_WRITE * alive_frac)
     elif native:
         rows = abi.native_env_bytes(P)
     else:
         rows = P * elems * 4
-    return rows + 33 * S * 2 + P * (225 + 12 * 8) * alive_frac
+    return rows + state + 33 * S * 2 + P * (225 + 12 * 8) * alive_frac
 
 
 def pmc_traffic(cfg_name: str, kernel, envs: int):

@@ -40,6 +40,9 @@ __device__ uint64_t fo_wave_buf[1 << 15][6];  // per wave: entry, staged, window
 #else
 #define FO_STAMP(k) (void)0
 #endif
+#ifndef NMMO_FO_TILE_SKIP  // (A/B knob: 1 = round 5's Tile component skip, tools/debug/variants.py)
+#define NMMO_FO_TILE_SKIP 0
+#endif
 #ifndef NMMO_FO_TASK_BATCH  // (A/B knob: tools/debug/variants.py)
 #define NMMO_FO_TASK_BATCH 8
 #endif
@@ -503,11 +506,13 @@ __global__ void __launch_bounds__(64 * kAoWaves) flat_obs_kernel(ObsParams p) {
       nbytes += 4ull * tdim;
     }
     FO_STAMP(9);
-    // Tile: (row, column, material) per window tile t = lane + 64 i, three stores 12 B apart; the
-    // row (column) components are not stored when the row was last written at the same agent row
-    // (column): a move changes one of the two, staying neither
+    // Tile: (row, column, material) per window tile t = lane + 64 i, three stores 12 B apart, all
+    // three every step: the three stores of a pass fill 768 contiguous bytes, so the section goes out
+    // as whole lines. (Round 5 skipped the row / column components when the agent had not moved: a
+    // third of the stores, but every line of the section was still written in part, which HBM writes
+    // as whole sectors -- WRITE_SIZE 1.9x the stored bytes; NMMO_FO_TILE_SKIP=1 keeps that variant.)
     const uint32_t ppos = (uint32_t)__builtin_amdgcn_readlane((int)img.x, 40 + j);
-    const bool tkn = ext && !((ztile >> j) & 1);  // the Tile section holds what this kernel wrote
+    const bool tkn = NMMO_FO_TILE_SKIP && ext && !((ztile >> j) & 1);  // the Tile section holds what this kernel wrote
     const bool same_r = tkn && (int)(ppos & 255u) == r, same_c = tkn && (int)((ppos >> 8) & 255u) == c;
     if (!(NMMO_FO_ABL & 16)) {
       float* dt = row + kFoTask + tdim + 3 * lane;

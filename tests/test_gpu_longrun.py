@@ -69,6 +69,11 @@ def test_tracked_rows_full_size_long_horizon(wrapper, monkeypatch):
             orcs.append((lo, n, o))
     ids = np.arange(N)
     checked = 0
+    listed = False
+    from nmmo_amd import layout
+
+    mk = layout.flat_layout()["Market"]
+    mk_lo = mk.offset
     for t in range(TICKS):
         if t < STAGGER:
             m = ids % STAGGER == t
@@ -88,6 +93,7 @@ def test_tracked_rows_full_size_long_horizon(wrapper, monkeypatch):
             torch.cuda.synchronize()
             assert torch.equal(a.obs.view(torch.int32), b.obs.view(torch.int32)), f"tracked != full write at tick {tick}"
             checked += 1
+            listed = listed or bool((a.obs[:, 0, mk_lo:mk_lo + 16] != 0).any())
         if orcs and tick in ORACLE_TICKS:
             for lo, n, o in orcs:
                 for k in range(n):
@@ -97,8 +103,11 @@ def test_tracked_rows_full_size_long_horizon(wrapper, monkeypatch):
                         bad = np.argwhere(g != want)[:5]
                         raise AssertionError(f"tick {tick} env {lo + k}: obs differ at {bad.tolist()}")
     assert checked >= TICKS // CHECK_EVERY
+    assert listed, "no market listing appeared in the window"
     st = a.get_state().reshape(N, -1)[:, :abi.NE * 4].copy().view(np.int32)
-    assert int(st[:, abi.ENV_FIELDS.index("episode")].min()) >= 1, "every env reset inside the window"
+    eps = st[:, abi.ENV_FIELDS.index("episode")]
+    assert int(eps.min()) >= 1, "every env reset inside the window"
+    assert int(eps.sum()) > N + N // 4, "episodes ended on their own after the staggered ends"
     assert a.get_fault() == 0 and b.get_fault() == 0
     # incremental: far fewer bytes stored than full rows
     stored = int(rows[:, 1].sum().item())

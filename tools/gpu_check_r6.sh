@@ -52,5 +52,20 @@ longrun)  # the row state at full size over 300 ticks (tracked vs full write; sa
   timeout -k 10 400 python -u -m pytest -x -v --timeout 180 --timeout-method thread tests/test_gpu_longrun.py \
     > $out/tests_longrun.log 2>&1 || exit 1
   ;;
+tile)  # dense Tile stores: long-horizon parity, then same-box A/B against the component skip + WRITE_SIZE
+  export TMPDIR=/tmp
+  timeout -k 10 400 python -u -m pytest -x -v --timeout 180 --timeout-method thread tests/test_gpu_longrun.py \
+    tests/test_gpu_zero_rows.py > $out/tests_tile.log 2>&1 || exit 1
+  timeout -k 10 600 bash tools/debug/ab_lib.sh "--steps 200 --warmup 30" base tileskip > $out/ab_tile.txt 2>&1 || exit 1
+  for v in base tileskip; do
+    L=nmmo_amd/lib/libnmmo_hip.so; [ $v = base ] || L=nmmo_amd/lib/libnmmo_hip_$v.so
+    NMMO_LIB=$L NMMO_ALLOW_STALE=1 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv \
+      -d $out/pmc_tile_$v -o run -- python3 bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-extras \
+      > /dev/null 2>&1 || exit 1
+    NMMO_LIB=$L NMMO_ALLOW_STALE=1 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv \
+      -d $out/kt_tile_$v -o run -- python3 bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-extras \
+      > $out/kt_tile_$v.json 2>/dev/null || exit 1
+  done
+  ;;
 *) echo "unknown step $1"; exit 2 ;;
 esac
