@@ -519,9 +519,16 @@ __global__ void __launch_bounds__(64 * kAoWaves) flat_obs_kernel(ObsParams p) {
 #pragma unroll
       for (int i = 0; i < 4; i++) {
         if (lane + 64 * i < 225) {
-          if (!same_r) dt[192 * i] = (float)(r + ((toff[i] << 24) >> 24));
-          if (!same_c) dt[192 * i + 1] = (float)(c + (toff[i] >> 8));
-          dt[192 * i + 2] = (float)wm[i];
+          const float vr = (float)(r + ((toff[i] << 24) >> 24)), vc = (float)(c + (toff[i] >> 8)), vm = (float)wm[i];
+          if (NMMO_FO_TILE_SKIP) {
+            if (!same_r) dt[192 * i] = vr;
+            if (!same_c) dt[192 * i + 1] = vc;
+            dt[192 * i + 2] = vm;
+          } else {  // the tile's 12 bytes as one 3-dword store (rows are 4-B aligned)
+            typedef float f3 __attribute__((ext_vector_type(3)));
+            const f3 v = {vr, vc, vm};
+            __builtin_memcpy(dt + 192 * i, &v, 12);
+          }
         }
       }
       nbytes += 4ull * 225 * (1 + !same_r + !same_c);
