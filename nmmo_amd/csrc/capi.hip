@@ -1094,6 +1094,8 @@ int nmmo_set_tasks(NmmoHandle* h, const NmmoTask* tasks, int32_t n_tasks, const 
     for (int k = 0; k < 2; k++) {
       const int pr = tasks[i].term[k].pred;
       if (pr < 0 || pr >= NMMO_N_PREDICATES) return fail(NMMO_E_INVALID, "task %d term %d: predicate %d", i, k, pr);
+      const int64_t ta = tasks[i].term[k].a;  // the tick's 8-B descriptor holds a in 24 bits
+      if (ta < -(1 << 23) || ta >= (1 << 23)) return fail(NMMO_E_INVALID, "task %d term %d: a %lld outside +/-2^23", i, k, (long long)ta);
       tev |= (pr >= PRED_COUNT_EVENT && pr <= PRED_DEFEAT_ENTITY) || pr == PRED_PRACTICE_EATING;
       tmap |= pr == PRED_CAN_SEE_TILE;
       tsee |= pr == PRED_CAN_SEE_AGENT || pr == PRED_CAN_SEE_GROUP;

@@ -582,6 +582,7 @@ __device__ __forceinline__ int kth_listed(const Ctx& c, int k) {
 // ---------------------------------------------------------------- event log (SPEC §11)
 // Row of the episode's event `idx` (0-based) for player p.
 // an event of player p feeds the event accumulators of p's task terms (SPEC §12)
+static_assert(NMMO_N_PREDICATES <= 256, "the 8-B task descriptor packs the predicate in 8 bits");
 __device__ __forceinline__ void task_accumulate(const Ctx& c, int p, int code, int type, int level, int number,
                                                 int gold, int target) {
 #pragma unroll
@@ -1289,7 +1290,9 @@ __device__ __forceinline__ void tick_env(Ctx& c, Heads hd, float* rew, uint8_t* 
   if (c.tev && s < P) {  // this player's task terms and event accumulators
     const NmmoTask& tk = c.tasks[c.assign[s]];
 #pragma unroll
-    for (int k = 0; k < 2; k++) c.tdesc[s * 2 + k] = make_int2((tk.term[k].pred & 255) | tk.term[k].a * 256, tk.term[k].b);
+    // pred | a << 8 as unsigned bits (nmmo_set_tasks keeps |a| < 2^23), decoded by an arithmetic shift
+    for (int k = 0; k < 2; k++)
+      c.tdesc[s * 2 + k] = make_int2((int)((uint32_t)(tk.term[k].pred & 255) | (uint32_t)tk.term[k].a << 8), tk.term[k].b);
   }
   // only the listed-row bitmap's zeroing must precede this phase's writes (its atomicOr); pres,
   // misc and tdesc are read after the phase's closing barrier

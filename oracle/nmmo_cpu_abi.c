@@ -227,6 +227,10 @@ NMMO_API int nmmo_set_tasks(NmmoHandle* h, const NmmoTask* tasks, int32_t n_task
                             const int32_t* assign) {
   if (!h || !tasks) return fail(NMMO_E_INVALID, "null argument");
   if (n_tasks < 1 || n_tasks > NMMO_MAX_TASKS) return fail(NMMO_E_INVALID, "n_tasks %d", n_tasks);
+  for (int i = 0; i < n_tasks; i++)  /* the HIP tick packs a term's a in 24 bits (capi.hip nmmo_set_tasks) */
+    for (int k = 0; k < 2; k++)
+      if (tasks[i].term[k].a < -(1 << 23) || tasks[i].term[k].a >= (1 << 23))
+        return fail(NMMO_E_INVALID, "task %d term %d: a outside +/-2^23", i, k);
   return oracle_set_tasks(h->o, tasks, n_tasks, embeddings, assign);
 }
 NMMO_API int nmmo_set_task_weights(NmmoHandle* h, const double* weights, int32_t n_tasks) {

@@ -100,3 +100,20 @@ def test_rollout_through_the_abi_equals_the_oracle_api(cpu):
     assert cpu.nmmo_get_events(h, 1, p(rows), 64, ctypes.byref(k)) == 0
     assert np.array_equal(rows[:k.value], ref.events(1)[-k.value:])
     cpu.nmmo_destroy(h)
+
+
+def test_set_tasks_refuses_terms_the_tick_cannot_pack(cpu):
+    """nmmo_set_tasks bounds a term's `a` to +/-2^23: the tick stages each term as an 8-B
+    descriptor pred | a << 8; both libraries refuse the same tables."""
+    cfg = Config.preset("C4", MAP_N=4, early_stop_agent_num=8)
+    c = cfg.to_c()
+    h = ctypes.c_void_p()
+    assert cpu.nmmo_create(ctypes.byref(c), 1, 5, 0, None, ctypes.byref(h)) == 0, cpu.nmmo_last_error()
+    t = abi.NmmoTask()
+    t.term[0].pred = abi.PRED["CountEvent"]
+    t.term[0].weight = 1.0
+    for a, ok in ((3, True), ((1 << 23) - 1, True), (-(1 << 23), True), (1 << 23, False), (-(1 << 23) - 1, False)):
+        t.term[0].a = a
+        rc = cpu.nmmo_set_tasks(h, ctypes.byref(t), 1, None, None)
+        assert (rc == 0) == ok, (a, rc)
+    cpu.nmmo_destroy(h)
