@@ -30,7 +30,8 @@ SYMBOLS = [
     "nmmo_exp_gather_records", "nmmo_exp_store_records_many", "nmmo_obs_invalidate", "nmmo_set_obs_counter",
     "nmmo_obs_bind", "nmmo_obs_invalidate_envs", "nmmo_exp_scratch_ints_many", "nmmo_set_step_records",
     "nmmo_wire_check_many", "nmmo_exp_store_records_checked", "nmmo_sizes_row",
-    "nmmo_obs_invalidate_sections",
+    "nmmo_obs_invalidate_sections", "nmmo_p2p_load", "nmmo_p2p_unique_id", "nmmo_p2p_init", "nmmo_p2p_group",
+    "nmmo_p2p_destroy",
 ]
 
 
@@ -131,6 +132,11 @@ def declare(L):
     L.nmmo_wire_check.argtypes = [vp, i32, i32, vp, vp, vp]
     L.nmmo_wire_check_many.argtypes = [vp, vp, vp, i32, i32, vp, vp]
     L.nmmo_sizes_row.argtypes = [vp, i32, vp, vp, vp]
+    L.nmmo_p2p_load.argtypes = [ctypes.c_char_p]
+    L.nmmo_p2p_unique_id.argtypes = [vp]
+    L.nmmo_p2p_init.argtypes = [vp, i32, i32, ctypes.POINTER(vp)]
+    L.nmmo_p2p_group.argtypes = [vp, ctypes.POINTER(abi.NmmoP2POp), i32, vp]
+    L.nmmo_p2p_destroy.argtypes = [vp]
     L.nmmo_dev_alloc.argtypes = [i32, u64, ctypes.POINTER(vp)]
     L.nmmo_dev_free.argtypes = [vp]
     L.nmmo_build_info.restype = ctypes.c_char_p

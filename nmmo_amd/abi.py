@@ -254,6 +254,13 @@ class NmmoRecordStore(ctypes.Structure):
                 ("row_buf", ctypes.c_void_p), ("row_agent", ctypes.c_void_p)]
 
 
+P2P_ID_BYTES = 128  # nmmo_p2p_unique_id
+
+
+class NmmoP2POp(ctypes.Structure):
+    _fields_ = [("buf", ctypes.c_void_p), ("bytes", ctypes.c_int64), ("peer", ctypes.c_int32), ("recv", ctypes.c_int32)]
+
+
 class NmmoStoreInput(ctypes.Structure):
     _fields_ = [("n_rows", ctypes.c_int32), ("step", ctypes.c_int32), ("obs", ctypes.c_void_p),
                 ("native", ctypes.c_void_p), ("rewards", ctypes.c_void_p), ("dones", ctypes.c_void_p),

@@ -13,7 +13,8 @@ CSRC = os.path.join(HERE, "csrc")
 LIB_DIR = os.path.join(HERE, "lib")
 LIB_PATH = os.path.join(LIB_DIR, "libnmmo_hip.so")
 STAMPS_PATH = os.path.join(LIB_DIR, "libnmmo_hip_stamps.so")
-SOURCES = ["mapgen.hip", "tick.hip", "obs.hip", "wrap.hip", "storage.hip", "wire.hip", "wire_obs.hip", "native_obs.hip", "flat_obs.hip", "capi.hip"]
+SOURCES = ["mapgen.hip", "tick.hip", "obs.hip", "wrap.hip", "storage.hip", "wire.hip", "wire_obs.hip", "native_obs.hip",
+           "flat_obs.hip", "p2p.hip", "capi.hip"]
 HEADERS = ["agent_obs.h", "common.h", "kernels.h", "wire.h"]
 ARCH = os.environ.get("NMMO_OFFLOAD_ARCH", "gfx950")
 
@@ -73,7 +74,7 @@ def build(force: bool = False, verbose: bool = False, stamps: bool = False) -> s
         with concurrent.futures.ThreadPoolExecutor(jobs) as ex:
             for f in [ex.submit(subprocess.check_call, c) for c in cmds]:
                 f.result()
-        subprocess.check_call([_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", tmp])
+        subprocess.check_call([_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-ldl", "-o", tmp])
     os.replace(tmp, out)
     return out
 

@@ -764,6 +764,38 @@ int nmmo_sizes_row(const void* const* wires, int32_t n_bufs, int32_t* dev_fault,
   return NMMO_OK;
 }
 
+// ---------------------------------------------------------------- gather point-to-point (p2p.hip)
+int nmmo_p2p_load(const char* librccl_path) {
+  char err[512];
+  if (p2p_load(librccl_path, err, sizeof(err))) return fail(NMMO_E_INVALID, "%s", err);
+  return NMMO_OK;
+}
+int nmmo_p2p_unique_id(void* id) {
+  char err[512];
+  if (!id) return fail(NMMO_E_INVALID, "null id");
+  if (p2p_load(nullptr, err, sizeof(err))) return fail(NMMO_E_INVALID, "nmmo_p2p_load first");
+  if (p2p_unique_id(id, err, sizeof(err))) return fail(NMMO_E_HIP, "%s", err);
+  return NMMO_OK;
+}
+int nmmo_p2p_init(const void* id, int32_t world, int32_t rank, void** comm) {
+  char err[512];
+  if (!id || !comm) return fail(NMMO_E_INVALID, "null argument");
+  if (world < 1 || rank < 0 || rank >= world) return fail(NMMO_E_INVALID, "rank %d of %d", rank, world);
+  if (p2p_load(nullptr, err, sizeof(err))) return fail(NMMO_E_INVALID, "nmmo_p2p_load first");
+  if (p2p_init(id, world, rank, comm, err, sizeof(err))) return fail(NMMO_E_HIP, "%s", err);
+  return NMMO_OK;
+}
+int nmmo_p2p_group(void* comm, const NmmoP2POp* ops, int32_t n_ops, void* stream) {
+  char err[512];
+  if (!comm || (n_ops > 0 && !ops) || n_ops < 0) return fail(NMMO_E_INVALID, "null communicator / ops");
+  for (int i = 0; i < n_ops; i++)
+    if (!ops[i].buf || ops[i].bytes < 0 || ops[i].peer < 0) return fail(NMMO_E_INVALID, "op %d: buffer / size / peer", i);
+  if (n_ops == 0) return NMMO_OK;
+  if (p2p_group(comm, ops, n_ops, (hipStream_t)stream, err, sizeof(err))) return fail(NMMO_E_HIP, "%s", err);
+  return NMMO_OK;
+}
+int nmmo_p2p_destroy(void* comm) { return p2p_destroy(comm) ? fail(NMMO_E_HIP, "ncclCommDestroy") : NMMO_OK; }
+
 int nmmo_wire_unpack(int32_t n_envs, int32_t player_n, const void* wire, void* native, void* stream) {
   if (!wire || !native) return fail(NMMO_E_INVALID, "null argument");
   if (n_envs <= 0 || player_n <= 0 || player_n > 128) return fail(NMMO_E_INVALID, "n_envs > 0, player_n in 1..128");

@@ -226,6 +226,12 @@ struct StoreCheck {
   int* ctl;                                // [kMaxStoreInputs] per-input check bits; zero, left zero
   uint32_t mask;                           // bit i: check input i (an unchecked input counts as clean)
 };
+// the learner gather's native point-to-point groups (p2p.hip; RCCL resolved at run time)
+int p2p_load(const char* path, char* err, size_t n);
+int p2p_unique_id(void* id, char* err, size_t n);
+int p2p_init(const void* id, int world, int rank, void** comm, char* err, size_t n);
+int p2p_group(void* comm, const NmmoP2POp* ops, int n_ops, hipStream_t stream, char* err, size_t n);
+int p2p_destroy(void* comm);
 int store_many_scratch_ints(int n_inputs, int max_rows);
 hipError_t launch_store_records_many(const NmmoExperience& x, const NmmoRecordStore& rs, const StoreBatch& b,
                                      int* scratch, hipStream_t stream, const StoreCheck* chk = nullptr);

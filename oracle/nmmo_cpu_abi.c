@@ -288,6 +288,17 @@ NMMO_API int nmmo_sizes_row(const void* const* w, int32_t n, int32_t* f, int64_t
   (void)w; (void)n; (void)f; (void)row; (void)stream;
   UNSUPPORTED("nmmo_sizes_row");
 }
+NMMO_API int nmmo_p2p_load(const char* path) { (void)path; UNSUPPORTED("nmmo_p2p_load"); }
+NMMO_API int nmmo_p2p_unique_id(void* id) { (void)id; UNSUPPORTED("nmmo_p2p_unique_id"); }
+NMMO_API int nmmo_p2p_init(const void* id, int32_t world, int32_t rank, void** comm) {
+  (void)id; (void)world; (void)rank; (void)comm;
+  UNSUPPORTED("nmmo_p2p_init");
+}
+NMMO_API int nmmo_p2p_group(void* comm, const NmmoP2POp* ops, int32_t n_ops, void* stream) {
+  (void)comm; (void)ops; (void)n_ops; (void)stream;
+  UNSUPPORTED("nmmo_p2p_group");
+}
+NMMO_API int nmmo_p2p_destroy(void* comm) { (void)comm; UNSUPPORTED("nmmo_p2p_destroy"); }
 NMMO_API int nmmo_wire_unpack(int32_t n, int32_t p, const void* wire, void* native, void* stream) {
   (void)n; (void)p; (void)wire; (void)native; (void)stream;
   UNSUPPORTED("nmmo_wire_unpack");

@@ -53,7 +53,8 @@ def test_enums_match_header():
     assert [n[2:].lower() for n in enames if n.startswith("E_")] == abi.ENV_FIELDS
     for macro, val in [("NMMO_SYS_RESOURCE", abi.SYS_RESOURCE), ("NMMO_SYS_EXCHANGE", abi.SYS_EXCHANGE),
                        ("NMMO_OBS_FLAT", abi.OBS_FLAT), ("NMMO_ABI_VERSION", abi.ABI_VERSION),
-                       ("NMMO_STORE_CTL_INTS", abi.STORE_CTL_INTS)]:
+                       ("NMMO_STORE_CTL_INTS", abi.STORE_CTL_INTS), ("NMMO_P2P_ID_BYTES", abi.P2P_ID_BYTES),
+                       ("NMMO_OBS_SEC_TILE", abi.OBS_SEC_TILE)]:
         m = re.search(rf"#define {macro} (.*?)(?:/\*|$)", text, re.M)
         assert eval(m.group(1).replace("u", "").strip()) == val, macro
 
@@ -64,10 +65,11 @@ def test_struct_layout_matches_c_compiler():
 #include <stddef.h>
 #include "nmmo_hip.h"
 int main(void) {
-  printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(NmmoConfig), offsetof(NmmoConfig, map_seed),
+  printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(NmmoConfig), offsetof(NmmoConfig, map_seed),
          sizeof(NmmoLayout), offsetof(NmmoLayout, off_tile), offsetof(NmmoLayout, state_bytes_per_env),
          offsetof(NmmoConfig, event_cap), sizeof(NmmoTaskTerm), sizeof(NmmoTask), offsetof(NmmoTask, combine),
-         sizeof(NmmoTaskState), offsetof(NmmoTaskState, acc));
+         sizeof(NmmoTaskState), offsetof(NmmoTaskState, acc), sizeof(NmmoP2POp), offsetof(NmmoP2POp, peer),
+         sizeof(NmmoStoreInput));
   return 0;
 }
 """
@@ -81,7 +83,8 @@ int main(void) {
             ctypes.sizeof(abi.NmmoLayout), abi.NmmoLayout.off_tile.offset,
             abi.NmmoLayout.state_bytes_per_env.offset, abi.NmmoConfig.event_cap.offset,
             ctypes.sizeof(abi.NmmoTaskTerm), ctypes.sizeof(abi.NmmoTask), abi.NmmoTask.combine.offset,
-            ctypes.sizeof(abi.NmmoTaskState), abi.NmmoTaskState.acc.offset]
+            ctypes.sizeof(abi.NmmoTaskState), abi.NmmoTaskState.acc.offset, ctypes.sizeof(abi.NmmoP2POp),
+            abi.NmmoP2POp.peer.offset, ctypes.sizeof(abi.NmmoStoreInput)]
     assert got == want
     assert ctypes.sizeof(abi.NmmoTaskState) == abi.TASK_STATE_BYTES == abi.task_state_dtype().itemsize
 

@@ -67,5 +67,9 @@ tile)  # dense Tile stores: long-horizon parity, then same-box A/B against the c
       > $out/kt_tile_$v.json 2>/dev/null || exit 1
   done
   ;;
+p2p)  # the native RCCL group (one GPU, self point-to-point) and the multi-rank gather tests
+  timeout -k 10 300 python -u -m pytest -x -v -s --timeout 120 --timeout-method thread tests/test_gpu_p2p.py \
+    tests/test_gpu_multirank.py > $out/tests_p2p.log 2>&1 || exit 1
+  ;;
 *) echo "unknown step $1"; exit 2 ;;
 esac
