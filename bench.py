@@ -678,9 +678,11 @@ def _gather_pass(args, engs, g, steps, warmup, world, dist, dev, counters, store
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
+    g.host_s = g.x.wait_s = 0.0
     t0 = time.perf_counter()
     for _ in range(steps):
         g.step()
+    host_work = (g.host_s - g.x.wait_s) / steps
     g.drain()
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -695,7 +697,7 @@ def _gather_pass(args, engs, g, steps, warmup, world, dist, dev, counters, store
         raise RuntimeError(f"the root's record store dropped rows (status {store.status})")
     return {"elapsed": elapsed, "alive": float(tot[0].item()), "episodes": int(tot[1].item()),
             "events": float(tot[2].item()), "stored_rows": stored,
-            "payload_bytes_per_step": (g.x.payload_bytes - b0) / steps}
+            "payload_bytes_per_step": (g.x.payload_bytes - b0) / steps, "host_ms_per_step": host_work * 1e3}
 
 
 def _record_store(per_list, dev, P):
@@ -780,6 +782,7 @@ def measure_gather(args, name, envs, rank, world, dev, steps, warmup, dist=None,
         "batches": nb,
         "shares": list(shares),
         "gather_bytes": d["payload_bytes_per_step"] if world > 1 else 0,
+        "host_ms_per_step": round(d["host_ms_per_step"], 4),
         "wire_bytes_per_env": round(wire_env_bytes, 1),
         "wire_bytes_per_agent_in_realm": round(wire_env_bytes * per * nb * steps / max(d["alive"], 1.0), 1),
         "decoded": passes.get("decoded"),
@@ -864,6 +867,7 @@ def measure_root_model(args, dev, steps, warmup, n_model: int = 8):
     res = {
         "n_gpus": n_model, "shares": shares,
         "root_loaded": {"envs": k_root, "phantom_peers": R, "ms_per_step": round(root_ms, 4),
+                        "host_ms_per_step": round(root["host_ms_per_step"], 4),
                         "stored_rows_per_step": round((root["stored_rows"] or 0) / steps, 1),
                         "what": f"rank 0's step at its share ({k_root} envs) with {R} phantom peers' buffers "
                                 f"({e_peer} envs each) received (write-only fills of their bytes), validated and "
@@ -931,6 +935,7 @@ def result_line(res, args, world, steps, alive_total, slots_total, elapsed, warm
         line["obs_bytes_stored_per_agent_row"] = res["obs_bytes_stored_per_agent_row"]
     if res["gather"]:
         line["wire_bytes_per_agent_in_realm"] = res["wire_bytes_per_agent_in_realm"]
+        line["host_ms_per_step"] = res["host_ms_per_step"]  # rank 0's host work per step (no waits)
     return line
 
 

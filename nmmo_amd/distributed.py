@@ -172,6 +172,7 @@ class WireExchange:
                     self.recv_wire[r, j] = torch.empty(int(recv_caps[r][j]), dtype=torch.uint8, device=d)
                     self.recv_small[r, j] = torch.empty(int(small_bytes[r][j]), dtype=torch.uint8, device=d)
         self.payload_bytes = 0  # wire bytes received by the root (all peers, all steps)
+        self.wait_s = 0.0  # host seconds blocked on size rows (totals)
 
     # -- plumbing
     def _ctx(self):
@@ -249,7 +250,11 @@ class WireExchange:
         has reached pinned memory (host wait on that copy only)."""
         k = t % self.ring
         if self.cuda and self._sized[k] is not None:
+            import time
+
+            w0 = time.perf_counter()
             self._sized[k].synchronize()
+            self.wait_s += time.perf_counter() - w0
         return self.sizes_host[k].tolist()
 
     def post_payload(self, t: int, wires, smalls, recv_into=None):
@@ -443,6 +448,7 @@ class WireGather:
         if graphs:
             self._capture()
         self.t = 0
+        self.host_s = 0.0  # host seconds inside step() (WireExchange.totals' wait for step t - 1's sizes included)
 
     def _setup_phantoms(self, phantom, env0):
         """The rehearsal's phantom peers (see __init__): their content placed once, at the front of
@@ -606,7 +612,14 @@ class WireGather:
                   "nmmo_exp_store_records_checked")
 
     def step(self):
-        t, k = self.t, self.t % self.ring
+        import time
+
+        h0 = time.perf_counter()
+        self._step(self.t)
+        self.host_s += time.perf_counter() - h0  # the host's own time per step (posting, not waiting)
+
+    def _step(self, t):
+        k = t % self.ring
         ready = []
         for j in range(len(self.engines)):
             st = self.streams[j]
