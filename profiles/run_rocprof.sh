@@ -18,7 +18,7 @@ for c in $CONFIGS; do
     *-native) ARGS="--config ${c%-native} --obs native" ;;
     # C5 at one GPU: one batch and no decoded pass (the two-batch run with the decode pass on
     # the comm stream stopped making progress under the kernel trace in round 3)
-    C5) ARGS="--config C5 --batches 1 --no-decode" ;;
+    C5) ARGS="--config C5 --batches 1 --no-decode --root-rehearsal 0" ;;
     *) ARGS="--config $c" ;;
   esac
   # C4-rezero: every obs row written in full (the flat full-write kernel, bench.py's extra of the name)
