@@ -158,11 +158,18 @@ __global__ void __launch_bounds__(64 * kWoWaves) wire_obs_kernel(ObsParams p) {
     }
     const int ng = __popcll(x.s6[0]) + __popcll(x.s6[1]);
     const int B = 3 * nv + 4 * ninv;  // stream bits
-    uint64_t W[6];                    // the stream, 64 bits per ballot (B <= 348)
+    uint64_t W[6];                    // the stream, 64 bits per word (B <= 348)
+#pragma unroll
+    for (int q = 0; q < 6; q++) W[q] = 0ull;
+    if (B <= 64) {  // the common case (nv <= 21 with ninv <= 0, ...): one word, scalar shifts and ors
+      const uint64_t mv = low_bits(nv), mi = low_bits(ninv);
+      const int o = 3 * nv;
+      W[0] = (x.s1[0] & mv) | (x.s5[0] & mv) << nv | (x.s7[0] & mv) << (2 * nv) | (x.s3 & mi) << o |
+             (x.s4 & mi) << (o + ninv) | (x.s9 & mi) << (o + 2 * ninv) | (x.s11 & mi) << (o + 3 * ninv);
+    }
 #pragma unroll
     for (int q = 0; q < 6; q++) {
-      W[q] = 0ull;
-      if (64 * q >= B) continue;  // wave-uniform
+      if (B <= 64 || 64 * q >= B) continue;  // wave-uniform: the long streams a lane per bit
       int k = 64 * q + lane;
       uint64_t lo = 0ull, hi = 0ull;
       if (k < nv) {

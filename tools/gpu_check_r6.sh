@@ -71,5 +71,11 @@ p2p)  # the native RCCL group (one GPU, self point-to-point) and the multi-rank 
   timeout -k 10 300 python -u -m pytest -x -v -s --timeout 120 --timeout-method thread tests/test_gpu_p2p.py \
     tests/test_gpu_multirank.py > $out/tests_p2p.log 2>&1 || exit 1
   ;;
+abc5)  # same-box A/B of library variants on the C5 line (N = 1, no model passes): VARIANTS="base name ..."
+  timeout -k 10 200 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_wire.py \
+    > $out/tests_abc5.log 2>&1 || exit 1
+  timeout -k 10 900 bash tools/debug/ab_lib.sh "--config C5 --steps 300 --warmup 30 --no-decode --root-rehearsal 0" \
+    ${VARIANTS:-base} > $out/ab_c5.txt 2>&1 || exit 1
+  ;;
 *) echo "unknown step $1"; exit 2 ;;
 esac
