@@ -33,10 +33,12 @@ constexpr int kWoWaves = NMMO_WO_WAVES, kWoAgents = NMMO_WO_AGENTS;
 // col, flags), loaded straight into registers, and the entity table (workgroup 0) is written from
 // the columns in HBM: the kernel used to stage all 24 KB of the env's columns in LDS per
 // workgroup, once for each of an env's 4 workgroups, and that prologue was over half its time.
+// + the workgroup's staged window rows and item words (agent_obs.h ao_stage_windows): 15.9 KB.
 __host__ __device__ inline size_t wo_lds_bytes() {
   return (size_t)NMMO_N_ENTITY_COLS * kWoAgents * 2 + (size_t)kWoWaves * (128 * 4 + 256) + (size_t)(128 + 4) * 4 +
-         (size_t)kMaxSlots * 2;
+         (size_t)kMaxSlots * 2 + ao_win_lds();
 }
+static_assert(kWoAgents == kAoAgents, "ao_stage_windows stages kAoAgents agents per workgroup");
 
 template <bool kWrap>
 __global__ void __launch_bounds__(64 * kWoWaves) wire_obs_kernel(ObsParams p) {
@@ -48,6 +50,8 @@ __global__ void __launch_bounds__(64 * kWoWaves) wire_obs_kernel(ObsParams p) {
   uint8_t* wmat_all = reinterpret_cast<uint8_t*>(visw_all + kWoWaves * 128);  // [kWoWaves][256] window materials
   int* woff = reinterpret_cast<int*>(wmat_all + kWoWaves * 256);            // [P + 1] record offsets
   uint16_t* rk = reinterpret_cast<uint16_t*>(woff + 128 + 4);                // [kMaxSlots] table index
+  uint32_t* wst = reinterpret_cast<uint32_t*>(rk + kMaxSlots);                 // [16][15][5] window rows
+  uint2* ist = reinterpret_cast<uint2*>(wst + kAoAgents * kAoWinAgentBytes / 4);  // [16][12] item words
   int e, g;
   ao_env_group(p.n_envs, (P + kWoAgents - 1) / kWoAgents, e, g);
   const int tid = threadIdx.x, lane = lane_id();
@@ -83,31 +87,22 @@ __global__ void __launch_bounds__(64 * kWoWaves) wire_obs_kernel(ObsParams p) {
 #pragma unroll
   for (int i = 0; i < kAoRows; i++) pr[i] = p.wpk[(size_t)e * kMaxSlots + lane + 64 * i];
   __syncthreads();
+  // the workgroup's window rows and item words into LDS (T is per workgroup: agent a at a - a0),
+  // so the agent loop issues no global load: an in-loop prefetch after the previous record's
+  // stores waited for them (vmcnt retires in order)
+  ao_stage_windows(p, e, g, T - a0, Sp, wst, ist);  // (barrier inside)
+  const uint8_t* wsb = reinterpret_cast<const uint8_t*>(wst);
 
   uint32_t* visw = visw_all + w * 128;
   uint8_t* wmat = wmat_all + w * 256;
   if (lane < 256 - 225) wmat[225 + lane] = 0;  // materials 225.. read as zero nibbles
-  const uint8_t* mat = p.mat + (size_t)e * kTiles;
   const bool item = (p.systems & NMMO_SYS_ITEM) != 0;
   const bool exch = item && (p.systems & NMMO_SYS_EXCHANGE) != 0;
 
   const int per_wave = (kWoAgents + kWoWaves - 1) / kWoWaves;
   const int abase = g * kWoAgents + w;
-  uint2 iv = make_uint2(0u, 0u);
-  uint32_t wm[4] = {0u, 0u, 0u, 0u};
-  int mo[2];
-  ao_window_offsets(mo);
-  auto prefetch = [&](int a) {
-    const int at = T[F_ROW * Sp + a - a0] * kSize + T[F_COL * Sp + a - a0];
-    iv = lane < kInv ? p.items[((size_t)e * P + a) * kInv + lane] : make_uint2(0u, 0u);
-#pragma unroll
-    for (int i = 0; i < 4; i++) wm[i] = lane + 64 * i < 225 ? mat[at + ao_window_off(mo, i)] : 0u;
-  };
-  auto in_realm = [&](int j) {
-    const int a = abase + kWoWaves * j;
-    return j < per_wave && a < P && (__builtin_amdgcn_readlane(my_cnt, j) & 0x8000);
-  };
-  if (in_realm(0)) prefetch(abase);
+  int wo[2];
+  ao_win_offsets(wo);
 
 #ifdef NMMO_WO_ABLATE_LOOP  // diagnostic timing only (no records written): the prologue alone
   if (p.S != 12345) return;
@@ -116,21 +111,22 @@ __global__ void __launch_bounds__(64 * kWoWaves) wire_obs_kernel(ObsParams p) {
     const int a = abase + kWoWaves * j;
     if (a >= P) break;
     const uint32_t cw = (uint32_t)__builtin_amdgcn_readlane(my_cnt, j);
-    if (!(cw & 0x8000u)) {  // not in the realm: no record
-      if (in_realm(j + 1)) prefetch(a + kWoWaves);
-      continue;
-    }
+    if (!(cw & 0x8000u)) continue;  // not in the realm: no record
     const int nv = cw & 127, ninv = (cw >> 7) & 15;
-    const int r = __builtin_amdgcn_readfirstlane(T[F_ROW * Sp + a - a0]);
-    const int c = __builtin_amdgcn_readfirstlane(T[F_COL * Sp + a - a0]);
-    const int gold = __builtin_amdgcn_readfirstlane(T[F_GOLD * Sp + a - a0]);
-    const int aid = __builtin_amdgcn_readfirstlane(T[F_ID * Sp + a - a0]);
+    const int la = a - a0;
+    const int r = __builtin_amdgcn_readfirstlane(T[F_ROW * Sp + la]);
+    const int c = __builtin_amdgcn_readfirstlane(T[F_COL * Sp + la]);
+    const int gold = __builtin_amdgcn_readfirstlane(T[F_GOLD * Sp + la]);
+    const int aid = __builtin_amdgcn_readfirstlane(T[F_ID * Sp + la]);
+    const uint8_t* wa = wsb + la * kAoWinAgentBytes + ((c - kVision) & 3);
+    uint32_t wm[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) wm[i] = lane + 64 * i < 225 ? wa[ao_win_off(wo, i)] : 0u;
 #pragma unroll
     for (int i = 0; i < 4; i++)
       if (lane + 64 * i < 225) wmat[lane + 64 * i] = (uint8_t)wm[i];
-    const uint2 it = iv;  // this agent's item word (lanes 0..11)
+    const uint2 it = lane < kInv ? ist[la * kInv + lane] : make_uint2(0u, 0u);  // lanes 0..11
     const uint32_t mv = ao_move_bits(wm[1]);
-    if (in_realm(j + 1)) prefetch(a + kWoWaves);  // the next agent's loads, ahead of the stores
 
     ao_compact(pr, S, r, c, visw);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
