@@ -127,23 +127,46 @@ __device__ inline void ao_stage(const ObsParams& p, int e, int16_t* T, uint32_t*
   const int S = p.S, P = p.P, Sp = ao_stride(S), tid = threadIdx.x;
   const int16_t* E = p.ent + (size_t)e * NMMO_NF * S;
   const int w4 = S / 8;  // 16-B words per field (S % 8 == 0: checked by the launchers)
-  for (int i = tid; i < NMMO_N_ENTITY_COLS * w4; i += blockDim.x) {  // 16-B loads, dword LDS writes
-    const int f = i / w4, j = i - f * w4;
-    const uint4 x = reinterpret_cast<const uint4*>(E + (size_t)f * S)[j];
-    uint32_t* d = reinterpret_cast<uint32_t*>(T + f * Sp) + 4 * j;
-    d[0] = x.x;
-    d[1] = x.y;
-    d[2] = x.z;
-    d[3] = x.w;
-  }
-  for (int k = tid; k < kMaxSlots + 64; k += blockDim.x) pk[k] = kAoEmpty;
+  const int nw = NMMO_N_ENTITY_COLS * w4;
+  // every load of the thread in flight before the first LDS write: a load -> write loop waited one
+  // memory round trip per 16-B word (6 per thread at S = 384, blockDim 256)
+  constexpr int kIt = (NMMO_N_ENTITY_COLS * (kMaxSlots / 8) + 255) / 256;
+  uint4 x[kIt];
   int al[2], ds[2];  // alive / datastore row of slots tid and tid + blockDim, loaded ahead of the barrier
+#pragma unroll
+  for (int k = 0; k < kIt; k++) {
+    const int i = tid + (int)blockDim.x * k;
+    const int f = i / w4, j = i - f * w4;
+    x[k] = i < nw ? reinterpret_cast<const uint4*>(E + (size_t)f * S)[j] : make_uint4(0u, 0u, 0u, 0u);
+  }
 #pragma unroll
   for (int u = 0; u < 2; u++) {
     const int s = tid + (int)blockDim.x * u;
     al[u] = s < S ? E[F_ALIVE * S + s] : 0;
     ds[u] = s < S ? E[F_DS_ROW * S + s] : 0;
   }
+#pragma unroll
+  for (int k = 0; k < kIt; k++) {
+    const int i = tid + (int)blockDim.x * k;
+    if (i < nw) {
+      const int f = i / w4, j = i - f * w4;
+      uint32_t* d = reinterpret_cast<uint32_t*>(T + f * Sp) + 4 * j;
+      d[0] = x[k].x;
+      d[1] = x[k].y;
+      d[2] = x[k].z;
+      d[3] = x[k].w;
+    }
+  }
+  for (int i = tid + (int)blockDim.x * kIt; i < nw; i += blockDim.x) {  // (blocks under 256 threads)
+    const int f = i / w4, j = i - f * w4;
+    const uint4 y = reinterpret_cast<const uint4*>(E + (size_t)f * S)[j];
+    uint32_t* d = reinterpret_cast<uint32_t*>(T + f * Sp) + 4 * j;
+    d[0] = y.x;
+    d[1] = y.y;
+    d[2] = y.z;
+    d[3] = y.w;
+  }
+  for (int k = tid; k < kMaxSlots + 64; k += blockDim.x) pk[k] = kAoEmpty;
   __syncthreads();
 #pragma unroll
   for (int u = 0; u < 2; u++) {
