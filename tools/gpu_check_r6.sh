@@ -77,5 +77,12 @@ abc5)  # same-box A/B of library variants on the C5 line (N = 1, no model passes
   timeout -k 10 900 bash tools/debug/ab_lib.sh "--config C5 --steps 300 --warmup 30 --no-decode --root-rehearsal 0" \
     ${VARIANTS:-base} > $out/ab_c5.txt 2>&1 || exit 1
   ;;
+abc4)  # parity of the obs kernels, then same-box A/B on the C4 headline and C4-native: VARIANTS="base name ..."
+  timeout -k 10 400 python -u -m pytest -x -q --timeout 170 --timeout-method thread tests/test_gpu_longrun.py \
+    tests/test_gpu_zero_rows.py tests/test_gpu_native_obs.py tests/test_gpu_parity.py > $out/tests_abc4.log 2>&1 || exit 1
+  timeout -k 10 600 bash tools/debug/ab_lib.sh "--steps 200 --warmup 30" ${VARIANTS:-base} > $out/ab_c4.txt 2>&1 || exit 1
+  timeout -k 10 600 bash tools/debug/ab_lib.sh "--obs native --steps 200 --warmup 30" ${VARIANTS:-base} \
+    > $out/ab_c4native.txt 2>&1 || exit 1
+  ;;
 *) echo "unknown step $1"; exit 2 ;;
 esac
