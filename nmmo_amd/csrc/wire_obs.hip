@@ -77,12 +77,28 @@ __global__ void __launch_bounds__(64 * kWoWaves) wire_obs_kernel(ObsParams p) {
   }
   const int tick = p.env[(size_t)e * NMMO_NE + E_TICK];
   uint8_t* const wenv = p.wire + v.env_off[e];
-  record_offsets_wave0(cnt, P, woff, wire_table_bytes(ne));
-  for (int s = tid; s < kMaxSlots; s += blockDim.x) rk[s] = p.wrank[(size_t)e * kMaxSlots + s];
-  for (int i = tid; i < NMMO_N_ENTITY_COLS * kWoAgents; i += blockDim.x) {
-    const int f = i / kWoAgents, la = i - f * kWoAgents;
-    T[i] = a0 + la < P ? E[f * S + a0 + la] : (int16_t)0;
+  // the table ranks and the agents' columns: every load of the thread before its LDS writes
+  constexpr int kRk = (kMaxSlots + 64 * kWoWaves - 1) / (64 * kWoWaves);
+  constexpr int kTc = (NMMO_N_ENTITY_COLS * kWoAgents + 64 * kWoWaves - 1) / (64 * kWoWaves);
+  uint16_t rkv[kRk];
+  int16_t tcv[kTc];
+#pragma unroll
+  for (int k = 0; k < kRk; k++) {
+    const int sl = tid + 64 * kWoWaves * k;
+    rkv[k] = sl < kMaxSlots ? p.wrank[(size_t)e * kMaxSlots + sl] : (uint16_t)0;
   }
+#pragma unroll
+  for (int k = 0; k < kTc; k++) {
+    const int i = tid + 64 * kWoWaves * k, f = i / kWoAgents, la = i - f * kWoAgents;
+    tcv[k] = i < NMMO_N_ENTITY_COLS * kWoAgents && a0 + la < P ? E[f * S + a0 + la] : (int16_t)0;
+  }
+  record_offsets_wave0(cnt, P, woff, wire_table_bytes(ne));
+#pragma unroll
+  for (int k = 0; k < kRk; k++)
+    if (tid + 64 * kWoWaves * k < kMaxSlots) rk[tid + 64 * kWoWaves * k] = rkv[k];
+#pragma unroll
+  for (int k = 0; k < kTc; k++)
+    if (tid + 64 * kWoWaves * k < NMMO_N_ENTITY_COLS * kWoAgents) T[tid + 64 * kWoWaves * k] = tcv[k];
   uint32_t pr[kAoRows];  // this lane's datastore rows 1 + lane + 64 i
 #pragma unroll
   for (int i = 0; i < kAoRows; i++) pr[i] = p.wpk[(size_t)e * kMaxSlots + lane + 64 * i];
