@@ -111,13 +111,16 @@ static_assert(slim_row(F_DROP_TOOL) == kSlimNF - 1, "slim rows");
 __device__ __forceinline__ int ent_row(bool slim, int f) { return slim ? slim_row(f) : f; }
 #define TF(f, s) c.T[ent_row(c.slim, (f)) * c.S + (s)]
 
-// Diagnostic build only (-DNMMO_STAMPS, tools/stamps.py): thread 0 stamps the shader clock right
-// after phase barriers; never compiled into the product library.
+// Diagnostic build only (-DNMMO_STAMPS, tools/stamps.py): thread NMMO_STAMP_TID (0) stamps the
+// shader clock right after phase barriers; never compiled into the product library.
 #ifdef NMMO_STAMPS
+#ifndef NMMO_STAMP_TID  // the stamping thread (64: wave 1's timeline)
+#define NMMO_STAMP_TID 0
+#endif
 __device__ unsigned long long g_stamps[4096 * 32];
 #define NMMO_STAMP(k)                                                        \
   do {                                                                       \
-    if (threadIdx.x == 0 && blockIdx.x < 4096)                               \
+    if (threadIdx.x == NMMO_STAMP_TID && blockIdx.x < 4096)                  \
       g_stamps[blockIdx.x * 32 + (k)] = __builtin_amdgcn_s_memtime();        \
   } while (0)
 // a launch's stamps start from zero: a phase a system set compiles out reads as absent
@@ -343,12 +346,18 @@ __device__ __forceinline__ void copy_segs(const Seg16 (&sg)[6], int tid, int nt,
   // remainder (the whole copy at C2/C3: 3.7 and 6.3 words per thread) goes in batches of 4 whose
   // loads read a clamped index instead of branching around them, so 4 loads are in flight at once
   // at a quarter of the full batch's registers.
+  // The loaded words pass through an empty asm before any LDS store: without it the compiler sank
+  // each load into its store's branch (the segment selects lower to branches), and the batch
+  // became load, wait, store, load, wait, ... -- one HBM round trip per word.
+  auto hold = [](uint4& v) { asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w)); };
   constexpr int U = 8;
   int b = tid;
   for (; b + (U - 1) * nt < total; b += U * nt) {
     uint4 r[U];
 #pragma unroll
     for (int k = 0; k < U; k++) r[k] = *src(b + k * nt);
+#pragma unroll
+    for (int k = 0; k < U; k++) hold(r[k]);
 #pragma unroll
     for (int k = 0; k < U; k++) *dst(b + k * nt) = r[k];
   }
@@ -358,27 +367,51 @@ __device__ __forceinline__ void copy_segs(const Seg16 (&sg)[6], int tid, int nt,
 #pragma unroll
     for (int k = 0; k < T; k++) r[k] = *src(min(b + k * nt, total - 1));
 #pragma unroll
+    for (int k = 0; k < T; k++) hold(r[k]);
+#pragma unroll
     for (int k = 0; k < T; k++)
       if (b + k * nt < total) *dst(b + k * nt) = r[k];
   }
 }
 
-__device__ __forceinline__ void load_env_arrays(Ctx& c, const DevState& st, int e);
-__device__ __forceinline__ void load_env(Ctx& c, const DevState& st, int e) {
-  const int tid = threadIdx.x;
+// The depleted-tile bitmap (3.2 KB of a C2 env's 11 KB of state) held in registers from the
+// state load until the update phase, when the C2 tick defers it (defer_dep): the tick's first
+// barrier then waits on the entity table alone, and the bitmap, first touched by the harvest,
+// arrives behind it.
+constexpr int kDepU4 = kBitmapWords / 4;
+struct DepQ {
+  uint4 v0, v1;
+};
+// every state segment a whole number of 16-B words (task state: 40 B per player)
+__device__ __forceinline__ bool state_v16(const Ctx& c) { return (c.S & 7) == 0 && (c.IC & 7) == 0 && (c.P & 1) == 0; }
+__device__ __forceinline__ bool defer_dep(const Ctx& c, uint32_t ksys) {
+  return ksys == NMMO_SYS_RESOURCE && state_v16(c) && 2 * (int)blockDim.x >= kDepU4;
+}
+
+__device__ __forceinline__ void load_env_arrays(Ctx& c, const DevState& st, int e, bool defer);
+// may_defer: a compile-time constant (the C2 kernel), so the bitmap loads are unconditional: a
+// conditional load leaves a register merge at the branch join that waits on it
+__device__ __forceinline__ DepQ load_env(Ctx& c, const DevState& st, int e, bool may_defer, bool defer) {
+  const int tid = threadIdx.x, nt = blockDim.x;
   // env scalars: loaded first, written to LDS after the copy has issued its loads (stored right
   // away, their wait put a whole HBM round trip ahead of the state copy)
   int ev = st.env[(size_t)e * NMMO_NE + min(tid, NMMO_NE - 1)];  // every thread: no branch join
-  load_env_arrays(c, st, e);
+  load_env_arrays(c, st, e, defer);
+  DepQ dq = {};
+  if (may_defer) {  // clamped indices: the tick writes only the in-range words, and only if defer
+    const uint4* dep4 = reinterpret_cast<const uint4*>(st.dep + (size_t)e * kBitmapWords);
+    dq.v0 = dep4[min(tid, kDepU4 - 1)];
+    dq.v1 = dep4[min(tid + nt, kDepU4 - 1)];
+  }
   asm volatile("" : "+v"(ev));
   if (tid < NMMO_NE) c.E[tid] = ev;
+  return dq;
 }
 
-__device__ __forceinline__ void load_env_arrays(Ctx& c, const DevState& st, int e) {
+__device__ __forceinline__ void load_env_arrays(Ctx& c, const DevState& st, int e, bool defer) {
   const int tid = threadIdx.x, nt = blockDim.x, S = c.S;
   const int16_t* src = st.ent + (size_t)e * NMMO_NF * S;
-  // every segment a whole number of 16-B words (task state: 40 B per player)
-  const bool v16 = (S & 7) == 0 && (c.IC & 7) == 0 && (c.P & 1) == 0;
+  const bool v16 = state_v16(c);
   NmmoTaskState* tsg = st.tstate + (size_t)e * c.P;
   const uint4* ring4 = reinterpret_cast<const uint4*>(st.ring + (size_t)e * S);
   const uint4* dep4 = reinterpret_cast<const uint4*>(st.dep + (size_t)e * kBitmapWords);
@@ -387,7 +420,7 @@ __device__ __forceinline__ void load_env_arrays(Ctx& c, const DevState& st, int 
     Seg16 sg[6] = {
         {reinterpret_cast<uint4*>(c.T), reinterpret_cast<const uint4*>(src), c.nf * S / 8},
         {reinterpret_cast<uint4*>(c.ring), ring4, S / 8},
-        {reinterpret_cast<uint4*>(c.dep), dep4, kBitmapWords / 4},
+        {reinterpret_cast<uint4*>(c.dep), dep4, defer ? 0 : kDepU4},
         {reinterpret_cast<uint4*>(c.inv), reinterpret_cast<const uint4*>(st.items + (size_t)e * c.P * kInv),
          c.items ? c.P * kInv / 2 : 0},
         {reinterpret_cast<uint4*>(c.iring), reinterpret_cast<const uint4*>(st.iring + (size_t)e * c.IC),
@@ -1271,7 +1304,7 @@ __device__ __forceinline__ void launder(NmmoTaskState& t) {
 struct Heads {
   int v[kHeads];
 };
-__device__ __forceinline__ void tick_env(Ctx& c, Heads hd, float* rew, uint8_t* term,
+__device__ __forceinline__ void tick_env(Ctx& c, Heads hd, bool defer, DepQ dq, float* rew, uint8_t* term,
                          uint8_t* trunc, uint8_t* mask) {
   const int tid = threadIdx.x, nt = blockDim.x, S = c.S, P = c.P;
   const int s = tid;
@@ -1560,8 +1593,20 @@ __device__ __forceinline__ void tick_env(Ctx& c, Heads hd, float* rew, uint8_t* 
       }
     }
   }
+  if (defer) {  // the deferred bitmap into LDS, ahead of the harvest's first atomicOr
+    uint4* d4 = reinterpret_cast<uint4*>(c.dep);
+    if (tid < kDepU4) d4[tid] = dq.v0;
+    if (tid + nt < kDepU4) d4[tid + nt] = dq.v1;
+  }
   __syncthreads();
   NMMO_STAMP(3);
+  // The prefetched task words are waited on here, before the tick's first global store (the
+  // harvest's depletion): gfx9 counts stores in vmcnt, so waited on at the rewards, behind the
+  // harvest and respawn stores, they held each tick a store round trip longer.
+  if (task_early) {
+    launder(tk);
+    launder(tsr);
+  }
   const bool first_on_tile = hslot >= 0 && c.hmin[hslot] == s;
   if (resource && first_on_tile && ((nbm >> 8) & 255u) == M_FOILAGE) {
     e_eat = true;
@@ -2406,7 +2451,8 @@ __device__ __forceinline__ void tick_body(const DevState& st, const int32_t* __r
     for (int k = 0; k < kHeads; k++)
       if (k == 0 || k == 1 || k == 8 || c.items) hd.v[k] = a[k];
   }
-  load_env(c, st, e);
+  const bool defer = defer_dep(c, kSys);
+  const DepQ dq = load_env(c, st, e, kSys == NMMO_SYS_RESOURCE, defer);
   __syncthreads();
   NMMO_STAMP(20);
   const size_t o = (size_t)e * c.P;
@@ -2443,7 +2489,7 @@ __device__ __forceinline__ void tick_body(const DevState& st, const int32_t* __r
       if (mask) mask[o + p] = 1;
     }
   } else {
-    tick_env(c, hd, rew + o, term + o, trunc + o, mask + o);
+    tick_env(c, hd, defer, dq, rew + o, term + o, trunc + o, mask + o);
   }
   __syncthreads();
   if (st.counters && threadIdx.x == 0) {  // sum(mask) of this launch + done envs + event rows, one
