@@ -121,40 +121,58 @@ __device__ __forceinline__ void put_field(uint32_t (&img)[kW], uint64_t lo, uint
   }
 }
 
-// Block prologue (every thread; two barriers inside): T[f * ao_stride(S) + s] = field f (< 31)
-// of slot s, pk[row - 1] = the packed word of datastore row `row` (kAoEmpty where none).
-__device__ inline void ao_stage(const ObsParams& p, int e, int16_t* T, uint32_t* pk) {
-  const int S = p.S, P = p.P, Sp = ao_stride(S), tid = threadIdx.x;
+// Block prologue, in two parts so a kernel can issue its other independent loads between them:
+// ao_stage_load issues the loads (the Entity columns, alive / datastore row of slots tid and
+// tid + blockDim, the listing count and listing tid's mlist word), ao_stage_store writes LDS
+// (every thread; two barriers inside): T[f * ao_stride(S) + s] = field f (< 31) of slot s,
+// pk[row - 1] = the packed word of datastore row `row` (kAoEmpty where none).
+// Every load of the thread is in flight before the first LDS write: a load -> write loop waited
+// one memory round trip per 16-B word (6 per thread at S = 384, blockDim 256), and the listings'
+// count -> mlist -> item chain ahead of the stage was three more.
+constexpr int kAoStageIt = (NMMO_N_ENTITY_COLS * (kMaxSlots / 8) + 255) / 256;
+struct AoStage {
+  uint4 x[kAoStageIt];
+  int al[2], ds[2];
+  int nm, mv;  // the env's listing count (as stored) and listing tid's mlist word (any when >= nm)
+};
+__device__ __forceinline__ void ao_stage_load(const ObsParams& p, int e, AoStage& r) {
+  const int S = p.S, tid = threadIdx.x;
   const int16_t* E = p.ent + (size_t)e * NMMO_NF * S;
   const int w4 = S / 8;  // 16-B words per field (S % 8 == 0: checked by the launchers)
   const int nw = NMMO_N_ENTITY_COLS * w4;
-  // every load of the thread in flight before the first LDS write: a load -> write loop waited one
-  // memory round trip per 16-B word (6 per thread at S = 384, blockDim 256)
-  constexpr int kIt = (NMMO_N_ENTITY_COLS * (kMaxSlots / 8) + 255) / 256;
-  uint4 x[kIt];
-  int al[2], ds[2];  // alive / datastore row of slots tid and tid + blockDim, loaded ahead of the barrier
+  r.nm = p.mcount[e];
+  r.mv = p.mlist[(size_t)e * NMMO_MARKET_ROWS + min(tid, NMMO_MARKET_ROWS - 1)];
 #pragma unroll
-  for (int k = 0; k < kIt; k++) {
+  for (int k = 0; k < kAoStageIt; k++) {
     const int i = tid + (int)blockDim.x * k;
     const int f = i / w4, j = i - f * w4;
-    x[k] = i < nw ? reinterpret_cast<const uint4*>(E + (size_t)f * S)[j] : make_uint4(0u, 0u, 0u, 0u);
+    r.x[k] = i < nw ? reinterpret_cast<const uint4*>(E + (size_t)f * S)[j] : make_uint4(0u, 0u, 0u, 0u);
   }
 #pragma unroll
-  for (int u = 0; u < 2; u++) {
-    const int s = tid + (int)blockDim.x * u;
-    al[u] = s < S ? E[F_ALIVE * S + s] : 0;
-    ds[u] = s < S ? E[F_DS_ROW * S + s] : 0;
+  for (int u = 0; u < 2; u++) {  // (a clamped slot: a conditional load is waited on at its branch's join)
+    const int s = min(tid + (int)blockDim.x * u, S - 1);
+    r.al[u] = E[F_ALIVE * S + s];
+    r.ds[u] = E[F_DS_ROW * S + s];
   }
+}
+__device__ __forceinline__ void ao_stage_store(const ObsParams& p, int e, int16_t* T, uint32_t* pk, const AoStage& r) {
+  const int S = p.S, P = p.P, Sp = ao_stride(S), tid = threadIdx.x;
+  const int16_t* E = p.ent + (size_t)e * NMMO_NF * S;
+  const int w4 = S / 8;
+  const int nw = NMMO_N_ENTITY_COLS * w4;
+  constexpr int kIt = kAoStageIt;
+  const int(&al)[2] = r.al;
+  const int(&ds)[2] = r.ds;
 #pragma unroll
   for (int k = 0; k < kIt; k++) {
     const int i = tid + (int)blockDim.x * k;
     if (i < nw) {
       const int f = i / w4, j = i - f * w4;
       uint32_t* d = reinterpret_cast<uint32_t*>(T + f * Sp) + 4 * j;
-      d[0] = x[k].x;
-      d[1] = x[k].y;
-      d[2] = x[k].z;
-      d[3] = x[k].w;
+      d[0] = r.x[k].x;
+      d[1] = r.x[k].y;
+      d[2] = r.x[k].z;
+      d[3] = r.x[k].w;
     }
   }
   for (int i = tid + (int)blockDim.x * kIt; i < nw; i += blockDim.x) {  // (blocks under 256 threads)
@@ -171,7 +189,7 @@ __device__ inline void ao_stage(const ObsParams& p, int e, int16_t* T, uint32_t*
 #pragma unroll
   for (int u = 0; u < 2; u++) {
     const int s = tid + (int)blockDim.x * u;
-    if (al[u] && (unsigned)(ds[u] - 1) < (unsigned)S) {
+    if (s < S && al[u] && (unsigned)(ds[u] - 1) < (unsigned)S) {
       const bool player = s < P;
       const bool immune = player && T[F_TIME_ALIVE * Sp + s] < p.spawn_immunity;
       const bool danger = T[F_NPC_TYPE * Sp + s] > 1;
@@ -179,6 +197,11 @@ __device__ inline void ao_stage(const ObsParams& p, int e, int16_t* T, uint32_t*
     }
   }
   __syncthreads();
+}
+// listing tid's item word (a valid address whatever the mlist word: used only below the count)
+__device__ __forceinline__ uint2 ao_listing_load(const ObsParams& p, int e, const AoStage& r) {
+  const int own = min((r.mv >> 16) & 255, p.P - 1), slot = min((r.mv >> 24) & 15, kInv - 1);
+  return p.items[((size_t)e * p.P + own) * kInv + slot];
 }
 
 // Workgroup -> (env, agent group) for a 1-D grid of n_envs * G workgroups. Workgroups are
@@ -214,7 +237,13 @@ constexpr int kAoWinAgentBytes = 15 * kAoWinRowBytes;  // 300
 __host__ __device__ inline size_t ao_win_lds() { return (size_t)kAoAgents * kAoWinAgentBytes + (size_t)kAoAgents * kInv * 8; }
 // positions of agents not in the realm are clamped so their (unused) window reads stay in the map
 __device__ __forceinline__ int ao_clamp_pos(int x) { return min(max(x, kVision), kSize - 1 - kVision); }
-__device__ inline void ao_stage_windows(const ObsParams& p, int e, int g, const int16_t* T, int Sp, uint32_t* ws, uint2* is) {
+// `before_barrier` runs after the LDS writes (every thread), ahead of the barrier that publishes them.
+struct AoNoop {
+  __device__ void operator()() const {}
+};
+template <typename F = AoNoop>
+__device__ inline void ao_stage_windows(const ObsParams& p, int e, int g, const int16_t* T, int Sp, uint32_t* ws, uint2* is,
+                                        F before_barrier = F()) {
   const int tid = threadIdx.x, P = p.P;
   const int la = tid / 15, row = tid - 15 * la, a = g * kAoAgents + la;
   const bool win = tid < kAoAgents * 15 && a < P;
@@ -234,6 +263,7 @@ __device__ inline void ao_stage_windows(const ObsParams& p, int e, int g, const 
     for (int k = 0; k < 5; k++) ws[tid * 5 + k] = d[k];  // tid = la * 15 + row
   }
   if (tid < kAoAgents * kInv) is[tid] = iw;
+  before_barrier();
   __syncthreads();
 }
 // Per-lane byte offsets of window tiles t = lane + 64 i (i < 4) in an agent's staged rows

@@ -242,21 +242,37 @@ __global__ void __launch_bounds__(64 * kAoWaves) flat_obs_kernel(ObsParams p) {
   wst_[0] = __builtin_amdgcn_s_memtime();
 #endif
   const int w = __builtin_amdgcn_readfirstlane(wave_id());
-  const int nm = min(max(p.mcount[e], 0), NMMO_MARKET_ROWS);
-  for (int j = tid; j < nm; j += blockDim.x) {  // end-of-tick listings, ascending row
-    const int v = p.mlist[(size_t)e * NMMO_MARKET_ROWS + j];
-    const int own = (v >> 16) & 255, slot = (v >> 24) & 15;
-    const uint2 wd = p.items[((size_t)e * P + own) * kInv + slot];
-    mpo[j] = (uint16_t)(it_price(wd) | own << 8);
-    if (j < kFoStagedListings) mitem[j] = wd;
+  // The prologue in two memory round trips: (1) the stage's loads, the listings' count and mlist
+  // words and this wave's agents' words; (2) after the stage's LDS writes, the listed items, the
+  // agents' extended row state and the workgroup's windows. (Issued where each was first needed,
+  // the count -> mlist -> item chain, the stage, the windows and the extended state were six.)
+  AoStage sg;
+  ao_stage_load(p, e, sg);
+  const int16_t* E = p.ent + (size_t)e * NMMO_NF * S;
+  constexpr int kPerWave = kAoAgents / kAoWaves;
+  const int abase = g * kAoAgents + w;
+  int my_task = 0, my_prev = -1, my_alive = 0;  // lane j: agent abase + 4 j
+  uint64_t my_z = 0, my_s = 0;                  // its row state tag and word
+  const bool mine = lane < kPerWave && abase + kAoWaves * lane < P;
+  {  // every lane loads (a clamped agent), the values kept for its own agent below
+    const int aj = min(abase + kAoWaves * min(lane, kPerWave - 1), P - 1);
+    const size_t ai = (size_t)e * P + aj;
+    my_task = p.assign[ai];
+    my_alive = E[F_ALIVE * S + aj];
+    if (p.zrow) {
+      my_z = p.zrow[ai];
+      my_s = p.zst[ai];
+    }
+    if constexpr (kWrap)
+      if (p.ws) my_prev = p.ws[ai].prev_price;
   }
-  ao_stage(p, e, T, pk);  // (publishes mpo / mitem too)
+  ao_stage_store(p, e, T, pk, sg);
+  if (!mine) {
+    my_task = 0, my_prev = -1, my_alive = 0;
+    my_z = my_s = 0;
+  }
 #if NMMO_FO_STAMPS
   wst_[1] = __builtin_amdgcn_s_memtime();
-#endif
-  ao_stage_windows(p, e, g, T, Sp, wst, ist);
-#if NMMO_FO_STAMPS
-  wst_[2] = __builtin_amdgcn_s_memtime();
 #endif
 
   uint32_t pr[kAoRows];  // this lane's datastore rows 1 + lane + 64 i
@@ -264,24 +280,9 @@ __global__ void __launch_bounds__(64 * kAoWaves) flat_obs_kernel(ObsParams p) {
   for (int i = 0; i < kAoRows; i++) pr[i] = pk[lane + 64 * i];
   uint32_t* visw = visw_all + w * 128;
   const uint8_t* wsb = reinterpret_cast<const uint8_t*>(wst);
-  const int16_t* E = p.ent + (size_t)e * NMMO_NF * S;
   const float tickf = (float)p.env[(size_t)e * NMMO_NE + E_TICK];
   const bool exch = (p.systems & NMMO_SYS_ITEM) && (p.systems & NMMO_SYS_EXCHANGE);
 
-  constexpr int kPerWave = kAoAgents / kAoWaves;
-  const int abase = g * kAoAgents + w;
-  int my_task = 0, my_prev = -1, my_alive = 0;  // lane j: agent abase + 4 j
-  uint64_t my_z = 0, my_s = 0;                  // its row state tag and word
-  if (lane < kPerWave && abase + kAoWaves * lane < P) {
-    const int aj = abase + kAoWaves * lane;
-    const size_t ai = (size_t)e * P + aj;
-    my_task = p.assign[ai];
-    my_alive = E[F_ALIVE * S + aj];
-    my_z = p.zrow[ai];
-    my_s = p.zst[ai];
-    if constexpr (kWrap)
-      if (p.ws) my_prev = p.ws[ai].prev_price;
-  }
   // bit j: agent j's row state describes this buffer / the row is all-zero / its Task section holds
   // its task's embedding / its extended state is valid; my_h = hv | hm << 12: its Entity rows >= hv
   // and its Market rows and Buy entries >= hm are zero (a row of unknown content: nothing known zero)
@@ -292,19 +293,43 @@ __global__ void __launch_bounds__(64 * kAoWaves) flat_obs_kernel(ObsParams p) {
   const uint64_t ztile = __ballot(zvl && (my_s & kZsTile));  // its Tile section was written by a consumer
   // the extended state (ObsParams::zext): lane 10 j + slot = agent j's tracked chunk `slot`, lane
   // 40 + j its Tile position; lane 12 j + k (inv) its item word k
+  // (loaded by every lane from a valid address, with the listings' items and ahead of the
+  // windows, and kept only where the state is valid)
   uint2 img = make_uint2(0u, 0u), pinv = make_uint2(0u, 0u);
-  {
-    const int ja = lane < 40 ? lane / 10 : lane - 40, ji = lane / 12;
-    const int aa = abase + kAoWaves * ja, ai = abase + kAoWaves * ji;
-    if (lane < 44 && aa < P && ((zextv >> ja) & 1))
-      img = reinterpret_cast<const uint2*>(p.zext)[((size_t)e * P + aa) * kZext + (lane < 40 ? lane % 10 : 10)];
-    if (lane < 48 && ai < P && ((zextv >> ji) & 1))
-      pinv = reinterpret_cast<const uint2*>(p.zext)[((size_t)e * P + ai) * kZext + 11 + lane % 12];
+  const int ja = lane < 40 ? lane / 10 : lane - 40, ji = lane / 12;
+  const bool img_ok = lane < 44 && abase + kAoWaves * ja < P && ((zextv >> ja) & 1);
+  const bool pinv_ok = lane < 48 && abase + kAoWaves * ji < P && ((zextv >> ji) & 1);
+  if (p.zext) {
+    const int aa = min(abase + kAoWaves * min(ja, kPerWave - 1), P - 1);
+    const int ai = min(abase + kAoWaves * min(ji, kPerWave - 1), P - 1);
+    img = reinterpret_cast<const uint2*>(p.zext)[((size_t)e * P + aa) * kZext + (lane < 40 ? lane % 10 : 10)];
+    pinv = reinterpret_cast<const uint2*>(p.zext)[((size_t)e * P + ai) * kZext + 11 + min(lane, 47) % 12];
   }
-  // Wait for the prologue's loads here, once: vmcnt counts stores too and retires in order, so a
-  // first use of img / pinv / my_prev inside the agent loop (under a branch the waitcnt pass cannot
-  // see through) waited for every store the row had issued -- one full drain per tracked chunk.
+  const int nm = min(max(sg.nm, 0), NMMO_MARKET_ROWS);
+  const uint2 lwd = ao_listing_load(p, e, sg);
+  // the listings (ascending row) into LDS ahead of the windows' barrier, which publishes them
+  ao_stage_windows(p, e, g, T, Sp, wst, ist, [&]() {
+    if (tid < nm) {
+      mpo[tid] = (uint16_t)(it_price(lwd) | ((sg.mv >> 16) & 255) << 8);
+      if (tid < kFoStagedListings) mitem[tid] = lwd;
+    }
+    for (int j = tid + (int)blockDim.x; j < nm; j += blockDim.x) {  // (more listings than threads)
+      const int v = p.mlist[(size_t)e * NMMO_MARKET_ROWS + j];
+      const int own = (v >> 16) & 255, slot = (v >> 24) & 15;
+      const uint2 wd = p.items[((size_t)e * P + own) * kInv + slot];
+      mpo[j] = (uint16_t)(it_price(wd) | own << 8);
+      if (j < kFoStagedListings) mitem[j] = wd;
+    }
+  });
+#if NMMO_FO_STAMPS
+  wst_[2] = __builtin_amdgcn_s_memtime();
+#endif
+  // Every prologue load has been waited on (the windows' LDS writes): a first use of img / pinv /
+  // my_prev inside the agent loop (under a branch the waitcnt pass cannot see through) waited for
+  // every store the row had issued -- one full drain per tracked chunk.
   asm volatile("" : "+v"(img.x), "+v"(img.y), "+v"(pinv.x), "+v"(pinv.y), "+v"(my_prev));
+  if (!img_ok) img = make_uint2(0u, 0u);
+  if (!pinv_ok) pinv = make_uint2(0u, 0u);
   const int my_h = !zvl ? (kNObs | NMMO_MARKET_ROWS << 12) : zzl ? 0 : (zs_hv(my_s) | zs_hm(my_s) << 12);
   int nrows = 0;                  // rows this wave wrote (rows_out[0])
   unsigned long long nbytes = 0;  // bytes this wave stored (rows_out[1])

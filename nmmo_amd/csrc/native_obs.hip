@@ -48,15 +48,45 @@ __global__ void __launch_bounds__(64 * kAoWaves) native_obs_kernel(ObsParams p) 
   const int e = p.env_list ? p.env_list[el] : el, tid = threadIdx.x, lane = lane_id();
   if ((unsigned)e >= (unsigned)p.n_envs) return;  // a bad list id (the tick records it)
   const int w = __builtin_amdgcn_readfirstlane(wave_id());
-  const int nm = min(max(p.mcount[e], 0), NMMO_MARKET_ROWS);
-  if (p.wmcount && g == 0 && tid == 0) p.wmcount[e] = nm;  // nmmo_wire_pack reads this launch's count
-  for (int j = tid; j < nm; j += blockDim.x) {  // end-of-tick listings, ascending row
-    const int v = p.mlist[(size_t)e * NMMO_MARKET_ROWS + j];
-    const int own = (v >> 16) & 255, slot = (v >> 24) & 15;
-    mpo[j] = (uint16_t)(it_price(p.items[((size_t)e * P + own) * kInv + slot]) | own << 8);
+  // the prologue in two memory round trips (as flat_obs.hip): the stage's loads with the
+  // listings' count / mlist words and this wave's agents' words, then the listed items with the
+  // windows
+  AoStage sg;
+  ao_stage_load(p, e, sg);
+  const int16_t* E = p.ent + (size_t)e * NMMO_NF * S;
+  const int per_wave = (kAoAgents + kAoWaves - 1) / kAoWaves;
+  const int abase = g * kAoAgents + w;
+  int my_task = 0, my_prev = -1, my_alive = 0;  // lane j: agent abase + 4 j
+  uint64_t my_z = 0, my_s = 0;                  // its row state tag and word (ObsParams::zrow / zst)
+  const bool mine = lane < per_wave && abase + kAoWaves * lane < P;
+  {  // every lane loads (a clamped agent), the values kept for its own agent below
+    const int aj = min(abase + kAoWaves * min(lane, per_wave - 1), P - 1);
+    const size_t ai = (size_t)e * P + aj;
+    my_task = p.assign[ai];
+    my_alive = E[F_ALIVE * S + aj];
+    if (p.ztag) {
+      my_z = p.zrow[ai];
+      my_s = p.zst[ai];
+    }
+    if constexpr (kWrap)
+      if (p.ws) my_prev = p.ws[ai].prev_price;
   }
-  ao_stage(p, e, T, pk);  // (publishes mpo too)
-  ao_stage_windows(p, e, g, T, Sp, wst, ist);
+  ao_stage_store(p, e, T, pk, sg);
+  if (!mine) {
+    my_task = 0, my_prev = -1, my_alive = 0;
+    my_z = my_s = 0;
+  }
+  const int nm = min(max(sg.nm, 0), NMMO_MARKET_ROWS);
+  if (p.wmcount && g == 0 && tid == 0) p.wmcount[e] = nm;  // nmmo_wire_pack reads this launch's count
+  const uint2 lwd = ao_listing_load(p, e, sg);
+  ao_stage_windows(p, e, g, T, Sp, wst, ist, [&]() {  // the listings, ascending row (published by its barrier)
+    if (tid < nm) mpo[tid] = (uint16_t)(it_price(lwd) | ((sg.mv >> 16) & 255) << 8);
+    for (int j = tid + (int)blockDim.x; j < nm; j += blockDim.x) {  // (more listings than threads)
+      const int v = p.mlist[(size_t)e * NMMO_MARKET_ROWS + j];
+      const int own = (v >> 16) & 255, slot = (v >> 24) & 15;
+      mpo[j] = (uint16_t)(it_price(p.items[((size_t)e * P + own) * kInv + slot]) | own << 8);
+    }
+  });
 
   uint8_t* nenv = p.nat + (size_t)e * ((size_t)P * NMMO_NATIVE_ROW_BYTES + NMMO_NATIVE_MARKET_BYTES);
   if (g == 0) {  // the env's Market (1,024 rows of 16 int16), once per env
@@ -81,26 +111,8 @@ __global__ void __launch_bounds__(64 * kAoWaves) native_obs_kernel(ObsParams p) 
   for (int i = 0; i < kAoRows; i++) pr[i] = pk[lane + 64 * i];
   uint32_t* visw = visw_all + w * 128;
   const uint8_t* wsb = reinterpret_cast<const uint8_t*>(wst);
-  const int16_t* E = p.ent + (size_t)e * NMMO_NF * S;
   const int tick = p.env[(size_t)e * NMMO_NE + E_TICK];
   const bool exch = (p.systems & NMMO_SYS_ITEM) && (p.systems & NMMO_SYS_EXCHANGE);
-
-  const int per_wave = (kAoAgents + kAoWaves - 1) / kAoWaves;
-  const int abase = g * kAoAgents + w;
-  int my_task = 0, my_prev = -1, my_alive = 0;  // lane j: agent abase + 4 j
-  uint64_t my_z = 0, my_s = 0;                  // its row state tag and word (ObsParams::zrow / zst)
-  if (lane < per_wave && abase + kAoWaves * lane < P) {
-    const int aj = abase + kAoWaves * lane;
-    const size_t ai = (size_t)e * P + aj;
-    my_task = p.assign[ai];
-    my_alive = E[F_ALIVE * S + aj];
-    if (p.ztag) {
-      my_z = p.zrow[ai];
-      my_s = p.zst[ai];
-    }
-    if constexpr (kWrap)
-      if (p.ws) my_prev = p.ws[ai].prev_price;
-  }
   // bit j: agent j's row state describes this buffer / the row is all-zero already; my_h: the
   // Entity rows past which the row is zero (all 100 unknown, 0 for an all-zero row)
   const bool zvl = p.ztag && my_z == p.ztag;
