@@ -40,6 +40,9 @@ __device__ uint64_t fo_wave_buf[1 << 15][6];  // per wave: entry, staged, window
 #else
 #define FO_STAMP(k) (void)0
 #endif
+#ifndef NMMO_FO_XCD  // (A/B knob: 1 = a 1-D grid with an env's groups on one XCD, agent_obs.h ao_env_group)
+#define NMMO_FO_XCD 0
+#endif
 #ifndef NMMO_FO_TILE_SKIP  // (A/B knob: 1 = round 5's Tile component skip, tools/debug/variants.py)
 #define NMMO_FO_TILE_SKIP 0
 #endif
@@ -233,7 +236,12 @@ __global__ void __launch_bounds__(64 * kAoWaves) flat_obs_kernel(ObsParams p) {
   uint32_t* visw_all = reinterpret_cast<uint32_t*>(mitem + kFoStagedListings);  // [4][128]
   uint32_t* wst = visw_all + kAoWaves * 128;                                   // [16][15][5] window rows
   uint2* ist = reinterpret_cast<uint2*>(wst + kAoAgents * kAoWinAgentBytes / 4);  // [16][12] item words
+#if NMMO_FO_XCD  // 1-D grid, an env's groups back to back on one XCD (agent_obs.h ao_env_group)
+  int el, g;
+  ao_env_group(p.env_list ? p.n_list : p.n_envs, (p.P + kAoAgents - 1) / kAoAgents, el, g);
+#else
   const int el = blockIdx.x, g = blockIdx.y;
+#endif
   const int e = p.env_list ? p.env_list[el] : el, tid = threadIdx.x, lane = lane_id();
   if ((unsigned)e >= (unsigned)p.n_envs) return;  // a bad list id (the tick records it)
   if (NMMO_FO_ABL & 128) return;
@@ -606,7 +614,11 @@ hipError_t launch_flat_obs(const ObsParams& p, hipStream_t stream) {
   if (!flat_obs_ok(p)) return hipErrorInvalidValue;
   const int ne = list_grid(p.env_list, p.n_list, p.n_envs);
   if (ne <= 0) return hipSuccess;
+#if NMMO_FO_XCD
+  const dim3 grid(ne * ((p.P + kAoAgents - 1) / kAoAgents)), block(64 * kAoWaves);
+#else
   const dim3 grid(ne, (p.P + kAoAgents - 1) / kAoAgents), block(64 * kAoWaves);
+#endif
   const size_t lds = fo_lds_bytes(p.S);
   if (p.S == kMaxSlots) {
     if (p.wflags) hipLaunchKernelGGL((flat_obs_kernel<true, kMaxSlots>), grid, block, lds, stream, p);
