@@ -209,8 +209,10 @@ __device__ __forceinline__ uint2 ao_listing_load(const ObsParams& p, int e, cons
 // go to one XCD back to back, so the env's staged columns come from HBM once and from that L2
 // G - 1 times (with a 2-D grid an env's groups were n_envs workgroups apart: every group fetched
 // them from HBM). Falls back to adjacent ids when n_envs % 8 != 0. Used by the wire kernel (same
-// box: C5 at N = 1 375 -> 380 M); the native kernel, whose rows are 30x larger, measured slower
-// with it (0.151 -> 0.168 ms per 512 envs) and keeps the 2-D grid.
+// box: C5 at N = 1 375 -> 380 M) and the flat kernel (round 6: C4 308 -> 312 M same box, the
+// kernel alone 1 % slower but the overlapped tick gets the HBM reads it no longer makes); the
+// native kernel measured slower with it (round 6 again: C4-native 341 -> 339 M) and keeps the 2-D
+// grid.
 __device__ __forceinline__ void ao_env_group(int n_envs, int G, int& e, int& g) {
   const int id = blockIdx.x;
   if ((n_envs & 7) == 0) {

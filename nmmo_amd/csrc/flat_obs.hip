@@ -41,7 +41,7 @@ __device__ uint64_t fo_wave_buf[1 << 15][6];  // per wave: entry, staged, window
 #define FO_STAMP(k) (void)0
 #endif
 #ifndef NMMO_FO_XCD  // (A/B knob: 1 = a 1-D grid with an env's groups on one XCD, agent_obs.h ao_env_group)
-#define NMMO_FO_XCD 0
+#define NMMO_FO_XCD 1
 #endif
 #ifndef NMMO_FO_TILE_SKIP  // (A/B knob: 1 = round 5's Tile component skip, tools/debug/variants.py)
 #define NMMO_FO_TILE_SKIP 0
