@@ -69,6 +69,7 @@ struct NmmoHandle {
   uint64_t* d_zrow = nullptr;
   uint64_t* d_zext = nullptr;  // flat rows' extended state (ObsParams::zext)
   bool zskip = true;
+  bool wire_fuse = true;  // the tick writes the wire count words (DevState::wf); NMMO_WIRE_FUSE=0 at create: off
   const void* zbuf = nullptr;  // the bound obs buffer (nmmo_obs_bind) and its tag
   uint64_t ztag = 0;
   unsigned long long* d_rows_out = nullptr;  // nmmo_set_obs_counter
@@ -260,6 +261,8 @@ int nmmo_create(const NmmoConfig* cfg, int32_t n_envs, uint64_t seed, int32_t de
   {
     const char* rz = getenv("NMMO_OBS_REZERO");  // A/B: rewrite the zero rows every launch
     h->zskip = !(rz && rz[0] == '1');
+    const char* wf = getenv("NMMO_WIRE_FUSE");  // A/B: the count kernel instead of the tick-fused count
+    h->wire_fuse = !(wf && wf[0] == '0');
   }
   if (cfg->obs_layout == NMMO_OBS_WIRE) {
     ALLOC(h->d_wrank, n * (size_t)kMaxSlots * 2);
@@ -328,6 +331,7 @@ static ObsParams obs_params(NmmoHandle* h, void* obs) {
   p.zext = h->d_zext;
   p.ztag = h->d_zrow && h->zskip && obs && obs == h->zbuf ? h->ztag : 0;
   p.rows_out = h->d_rows_out;
+  p.counted = 0;
   p.recs = nullptr;  // (a step's outputs: step_impl sets them)
   p.fault_dst = nullptr;
   p.rew = nullptr;
@@ -402,6 +406,18 @@ static int step_impl(NmmoHandle* h, const int32_t* env_ids, int32_t n_ids, const
   DevState st = h->st;
   st.env_list = env_ids;
   st.n_list = n_ids;
+  const bool do_obs = obs && h->cfg.obs_layout != NMMO_OBS_NONE;
+  // a whole-handle step into a wire buffer without the wrapper (which rewrites the rewards the
+  // records carry after the tick): the C4 tick writes the count words itself (tick.hip
+  // wire_count_fused, the 384-slot / 128-player specialisation launch_tick picks for these shapes)
+  if (do_obs && h->cfg.obs_layout == NMMO_OBS_WIRE && !env_ids && !h->wrap_on && h->wire_fuse &&
+      st.cfg.systems == NMMO_SYS_ALL && st.S == 384 && st.P == 128) {
+    st.wf.wire = (uint8_t*)obs;
+    st.wf.wrank = h->d_wrank;
+    st.wf.wpk = h->d_wpk;
+    st.wf.n_envs = st.n_envs;
+    st.wf.spawn_immunity = h->cfg.spawn_immunity;
+  }
   if (rec) HIP_TRY(hipEventRecord(ev[0], s));
   HIP_TRY(launch_tick(st, actions, nullptr, rew, term, trunc, mask, 0, s));
   if (rec) HIP_TRY(hipEventRecord(ev[1], s));
@@ -412,11 +428,11 @@ static int step_impl(NmmoHandle* h, const int32_t* env_ids, int32_t n_ids, const
     HIP_TRY(launch_wrap(wp, 0, s));
   }
   if (rec) HIP_TRY(hipEventRecord(ev[2], s));  // wrapper span = ev[1]..ev[2] (empty when off)
-  const bool do_obs = obs && h->cfg.obs_layout != NMMO_OBS_NONE;
   if (do_obs) {
     ObsParams op = obs_params(h, obs);
     op.env_list = env_ids;
     op.n_list = n_ids;
+    op.counted = st.wf.wire != nullptr;
     if (op.wire && h->d_recs) {
       op.recs = h->d_recs;
       op.fault_dst = h->d_recs_fault;

@@ -55,6 +55,16 @@ struct DevState {
   // NULL = every env (workgroup b steps env b). Ids outside [0, n_envs) are dropped (fault word).
   const int32_t* env_list;
   int n_list;
+  // The wire header's count words written by the tick (wire_count_kernel's outputs from the
+  // workgroup's LDS state after the store, tick_kernel<NMMO_SYS_ALL, 384, 128> only): set by a
+  // whole-handle nmmo_step into a wire buffer without the wrapper layer; wire == NULL = off
+  struct WireFuse {
+    uint8_t* wire;
+    uint16_t* wrank;  // [n][kMaxSlots] (ObsParams::wrank)
+    uint32_t* wpk;    // [n][kMaxSlots] (ObsParams::wpk)
+    int n_envs;
+    int spawn_immunity;
+  } wf;
 };
 // grid size and env of workgroup b of a launch over an env list (NULL = all n envs)
 __host__ __device__ inline int list_grid(const int32_t* list, int n_list, int n) { return list ? n_list : n; }
@@ -107,7 +117,7 @@ struct ObsParams {
   // for, and the 12 item words the Inventory section was written from
   uint64_t* zext;
   // wire layout only (nmmo_set_step_records): per agent 8 B reward | term | trunc | mask | 0,
-  // written by wire_count_kernel from the step's outputs (NULL = off)
+  // written by wire_obs_kernel from the step's outputs (NULL = off)
   uint8_t* recs;
   int32_t* fault_dst;  // with recs: *fault's nonzero word CAS-ed into it (nmmo_fault_into's effect)
   const float* rew;
@@ -115,6 +125,7 @@ struct ObsParams {
   const uint8_t* trunc;
   const uint8_t* mask;
   unsigned long long* rows_out;  // optional [n][2]: += rows this launch wrote, bytes it stored, per env
+  int counted;  // wire layout: the tick wrote the header's count words (DevState::wf), no count launch
 };
 constexpr uint64_t kZsZero = 1ull << 20;
 constexpr uint64_t kZsExt = 1ull << 21;  // the row's extended state (ObsParams::zext) is valid

@@ -22,6 +22,7 @@
 //     steps (Buy in shuffled order, Give/GiveGold, and ammunition + loot of executed attacks,
 //     deferred to after the attack phase — equipment sums cannot change inside it) are
 //     replayed by thread 0 in serial order.
+#include "agent_obs.h"  // ao_pack / ao_in_window / ao_slot, wire.h (the tick-fused wire count)
 #include "kernels.h"
 
 namespace nmmo {
@@ -2397,6 +2398,111 @@ __device__ __forceinline__ void tick_env(Ctx& c, Heads hd, bool defer, DepQ dq, 
   }
 }
 
+// The tick-fused wire count (DevState::wf): wire.hip wire_count_kernel's outputs -- per agent in
+// the realm its count word (visible entities, the first kNObs, and its occupied inventory prefix),
+// the env's entity-table ranks and size, its listing count and payload bytes, the packed word of
+// every datastore row into wf.wpk -- computed the same way from the workgroup's LDS state after
+// the store instead of from HBM by a launch of its own (C5: the count kernel was ~14 us per 512
+// envs, most of it loading what the tick held). Scratch: the item ring and row map (free after the
+// store) hold the packed rows, positions, shown set and prefixes; the union .. died range holds
+// the id set and its prefix.
+template <int kS, int kP>
+__device__ __forceinline__ void wire_count_fused(Ctx& c, const DevState& st, int e) {
+  static_assert(kS > 0 && kS <= kMaxSlots && kP > 0 && kP <= 128, "a specialised shape");
+  auto al16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
+  constexpr size_t kIdBytes = (size_t)kIdWords * 4 * 2;  // ids | pre
+  constexpr size_t kRegion = union_lds_bytes(kS, true) + al16((size_t)(kS + 1) * 2) + 128 * 4 + 4 * al16((size_t)kS * 2) +
+                             (size_t)kBitmapWords * 4 + NMMO_NE * 4 + 32 * 4 + 16 * 4 + 128 + 128;
+  static_assert(kRegion >= kIdBytes, "the id set fits the union .. died range");
+  constexpr size_t kSmall = (size_t)kMaxSlots * 8 + kMaxSlots / 8 + 128 + 16 * 4 + 4;
+  static_assert(kSmall <= al16((size_t)kInv * kP * 2) + al16((size_t)(kInv * kP + 1) * 2), "the item ring and row map");
+  constexpr uint32_t kOut = 0xFFFFFFFFu;
+  const int tid = threadIdx.x, lane = lane_id(), S = kS, P = kP;
+  const int w = __builtin_amdgcn_readfirstlane(wave_id()), nw = blockDim.x >> 6;
+  int nm = 0;  // store_market's listing count
+  if (c.exch && tid == 0) {
+    for (int j = 0; j < kLWords; j++) nm += __popcll(c.lbits[j]);
+    nm = min(nm, NMMO_MARKET_ROWS);
+  }
+  // this thread's slot (blockDim >= S), read before the barrier that frees the scratch
+  const int s = tid;
+  const bool in = s < S && TF(F_ALIVE, s);
+  const int ds = s < S ? TF(F_DS_ROW, s) : 0, r = s < S ? TF(F_ROW, s) : 0, col = s < S ? TF(F_COL, s) : 0;
+  const int id = s < S ? TF(F_ID, s) : 0, ta = s < S ? TF(F_TIME_ALIVE, s) : 0, npc = s < S ? TF(F_NPC_TYPE, s) : 0;
+  int ninv = 0;
+  if (tid < P) {  // the occupied inventory prefix
+    const uint2* inv = c.inv + tid * kInv;
+#pragma unroll
+    for (int k = kInv - 1; k >= 0; k--) ninv = it_type(inv[k]) ? ninv + 1 : 0;
+  }
+  __syncthreads();  // the store's LDS reads are done: the scratch below overwrites what they read
+  uint32_t* pk = reinterpret_cast<uint32_t*>(c.iring);  // datastore row - 1 -> ao_pack word
+  uint32_t* pos = pk + kMaxSlots;                       // slot -> row << 16 | col
+  uint32_t* tab = pos + kMaxSlots;                      // slots some record shows
+  uint8_t* nin = reinterpret_cast<uint8_t*>(tab + kMaxSlots / 32);
+  int* wsum = reinterpret_cast<int*>(nin + 128);
+  int* bytes = wsum + 16;
+  uint32_t* ids = reinterpret_cast<uint32_t*>(c.vism);
+  int* pre = reinterpret_cast<int*>(ids + kIdWords);
+  for (int k = tid; k < kMaxSlots; k += blockDim.x) pk[k] = kOut;
+  if (tid < kMaxSlots / 32) tab[tid] = 0u;
+  idset_clear(ids);
+  if (tid < P) nin[tid] = (uint8_t)ninv;
+  if (tid == 0) *bytes = 0;
+  __syncthreads();
+  if (s < kMaxSlots) {
+    pos[s] = in ? ((uint32_t)(uint16_t)r << 16) | (uint32_t)(uint16_t)col : kOut;
+    if (in && (unsigned)(ds - 1) < (unsigned)S) {
+      const bool player = s < P;
+      pk[ds - 1] = ao_pack(s, r, col, player && ta < st.wf.spawn_immunity, npc > 1, player);
+    }
+  }
+  __syncthreads();
+  const WireView v = wire_view(st.wf.wire, st.wf.n_envs, P);
+  uint32_t pr[kMaxSlots / 64];  // this lane's datastore rows 1 + lane + 64 i
+#pragma unroll
+  for (int i = 0; i < kMaxSlots / 64; i++) {
+    pr[i] = pk[lane + 64 * i];
+    if (w == 0) st.wf.wpk[(size_t)e * kMaxSlots + lane + 64 * i] = pr[i];
+  }
+  int mine = 0;
+  for (int a = w; a < P; a += nw) {
+    const uint32_t pa = pos[a];
+    uint32_t word = 0u;
+    if (pa != kOut) {  // wave-uniform
+      const uint32_t rc = (pa >> 16) | (pa & 0xFFFFu) << 16;  // r | c << 16
+      int nvis = 0;
+#pragma unroll
+      for (int i = 0; i < kMaxSlots / 64; i++) {
+        const uint32_t x = pr[i];
+        const bool iw = ao_in_window(x, rc);  // (an empty row is at (255, 255): outside)
+        const uint64_t b = __ballot(iw);
+        if (iw && nvis + __popcll(b & lanes_below()) < kNObs) {
+          const int q = ao_slot(x);
+          atomicOr(&tab[q >> 5], 1u << (q & 31));
+        }
+        nvis += __popcll(b);
+      }
+      word = wire_count_word(min(nvis, kNObs), nin[a]);
+    }
+    if (lane == 0) {
+      v.cnt[(size_t)e * P + a] = (uint16_t)word;
+      mine += wire_record_bytes(word);
+    }
+  }
+  if (lane == 0) atomicAdd(bytes, mine);
+  __syncthreads();
+  const bool shown = s < S && ((tab[s >> 5] >> (s & 31)) & 1u);
+  if (shown) idset_add(ids, id);
+  const int ne = idset_prefix(ids, pre, wsum);  // (barriers inside)
+  if (s < kMaxSlots) st.wf.wrank[(size_t)e * kMaxSlots + s] = shown ? (uint16_t)idrank(ids, pre, id) : (uint16_t)0xFFFF;
+  if (tid == 0) {
+    v.mcount[e] = (uint16_t)nm;
+    v.ecount[e] = (uint16_t)ne;
+    v.env_off[e] = wire_table_bytes(ne) + *bytes + 32 * nm;
+  }
+}
+
 // End-of-tick listings for the obs and policy kernels (Market rows, Buy mask): ascending row.
 __device__ __forceinline__ void store_market(Ctx& c, const DevState& st, int e) {
   const int tid = threadIdx.x;
@@ -2504,6 +2610,8 @@ __device__ __forceinline__ void tick_body(const DevState& st, const int32_t* __r
   NMMO_STAMP(10);
   store_market(c, st, e);
   store_env(c, st, e);
+  if constexpr (kSys == NMMO_SYS_ALL && kS > 0 && kP > 0)
+    if (st.wf.wire) wire_count_fused<kS, kP>(c, st, e);
 #ifdef NMMO_STAMPS
   __syncthreads();
 #endif

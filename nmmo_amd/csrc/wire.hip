@@ -179,16 +179,6 @@ __global__ void __launch_bounds__(kCountThreads) wire_count_kernel(ObsParams p) 
     v.ecount[e] = (uint16_t)ne;
     v.env_off[e] = wire_table_bytes(ne) + bytes + 32 * nm;
   }
-  if (p.fault_dst && e == 0 && tid == 0) {  // nmmo_fault_into's effect (the tick ran before this launch)
-    const int32_t fw = *p.fault;
-    if (fw) atomicCAS(p.fault_dst, 0, fw);
-  }
-  if (p.recs && tid < p.P) {  // the step record (nmmo_set_step_records): reward | term | trunc | mask | 0
-    const size_t ai = (size_t)e * p.P + tid;
-    const uint2 rec = make_uint2(__float_as_uint(p.rew[ai]),
-                                 (uint32_t)p.term[ai] | (uint32_t)p.trunc[ai] << 8 | (uint32_t)p.mask[ai] << 16);
-    reinterpret_cast<uint2*>(p.recs)[ai] = rec;
-  }
 }
 
 // exclusive scan of the per-env payload bytes (one workgroup): env_off[e] becomes the offset of
@@ -639,7 +629,7 @@ hipError_t launch_wire_pack(const uint16_t* counts, const int* mcount, const uin
 
 hipError_t launch_wire_header(const ObsParams& p, hipStream_t s) {
   if (p.P > 128 || p.n_envs <= 0 || p.S > kMaxSlots || !p.wire) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(wire_count_kernel, dim3(p.n_envs), dim3(kCountThreads), 0, s, p);
+  if (!p.counted) hipLaunchKernelGGL(wire_count_kernel, dim3(p.n_envs), dim3(kCountThreads), 0, s, p);
   hipLaunchKernelGGL(wire_scan_kernel, dim3(1), dim3(1024), 0, s, p.wire, p.n_envs, p.P);
   return hipGetLastError();
 }

@@ -65,14 +65,19 @@ __global__ void __launch_bounds__(64 * kWoWaves) wire_obs_kernel(ObsParams p) {
   // store (vmcnt counts stores too and retires in issue order: a load after a store waits for
   // it). Lane j of a wave holds its agent abase + kWoWaves j's count word, task and last price.
   int my_task = 0, my_prev = -1, my_cnt = 0;
+  uint2 my_rec = make_uint2(0u, 0u);  // its step record (nmmo_set_step_records), stored after the loop
+  const int my_a = g * kWoAgents + wave_id() + kWoWaves * lane;
+  const bool my_on = lane < (kWoAgents + kWoWaves - 1) / kWoWaves && my_a < P;
   {
-    const int aj = g * kWoAgents + wave_id() + kWoWaves * lane;
-    if (lane < (kWoAgents + kWoWaves - 1) / kWoWaves && aj < P) {
-      const size_t ai = (size_t)e * P + aj;
-      my_cnt = cnt[aj];
+    if (my_on) {
+      const size_t ai = (size_t)e * P + my_a;
+      my_cnt = cnt[my_a];
       my_task = p.assign[ai];
       if constexpr (kWrap)
         if (p.ws) my_prev = p.ws[ai].prev_price;
+      if (p.recs)  // reward | term | trunc | mask | 0
+        my_rec = make_uint2(__float_as_uint(p.rew[ai]),
+                            (uint32_t)p.term[ai] | (uint32_t)p.trunc[ai] << 8 | (uint32_t)p.mask[ai] << 16);
     }
   }
   const int tick = p.env[(size_t)e * NMMO_NE + E_TICK];
@@ -241,6 +246,11 @@ __global__ void __launch_bounds__(64 * kWoWaves) wire_obs_kernel(ObsParams p) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the next agent reuses visw / wmat
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  if (p.recs && my_on) reinterpret_cast<uint2*>(p.recs)[(size_t)e * P + my_a] = my_rec;
+  if (p.fault_dst && e == 0 && g == 0 && tid == 0) {  // nmmo_fault_into's effect (the tick ran before)
+    const int32_t fw = *p.fault;
+    if (fw) atomicCAS(p.fault_dst, 0, fw);
   }
   // the env's listings (Market rows, one 32-B row per thread) and its entity table (the 31
   // columns of each shown slot at its index, a thread per slot, the columns from HBM; then the

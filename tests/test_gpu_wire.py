@@ -114,6 +114,41 @@ def test_wire_layout_equals_pack_of_native(wrapper):
         e.close()
 
 
+def test_tick_fused_count_equals_count_kernel(monkeypatch):
+    """A whole-handle C4 step into a wire buffer has the tick write the header's count words
+    (tick.hip wire_count_fused): the buffers, step records included, equal those of a handle whose
+    count kernel runs (NMMO_WIRE_FUSE=0 at create), tick by tick over resets and episode ends."""
+    from nmmo_amd import abi, wire
+    from nmmo_amd.config import Config
+    from nmmo_amd.engine import NmmoEngine
+
+    engs = []
+    for fuse in ("1", "0"):
+        monkeypatch.setenv("NMMO_WIRE_FUSE", fuse)
+        cfg = Config.preset("C4", MAP_N=4, early_stop_agent_num=8, obs_layout=abi.OBS_WIRE)
+        engs.append(NmmoEngine(cfg, 8, seed=57))
+    monkeypatch.delenv("NMMO_WIRE_FUSE")
+    assert engs[0].S == 384 and engs[0].P == 128  # the fused specialisation's shape
+    recs = [torch.zeros((8, e.P, 8), dtype=torch.uint8, device=e.device) for e in engs]
+    for e, r in zip(engs, recs):
+        e.reset()
+        e.set_step_records(r)
+    for t in range(48):
+        if t == 11:
+            for e in engs:
+                e.end_episodes(np.array([1, 0, 0, 1, 0, 0, 1, 0], bool))
+        for e in engs:
+            e.scripted_actions(700 + t)
+            e.step()
+        total = wire.total_bytes(engs[1].obs)
+        assert wire.total_bytes(engs[0].obs) == total, t
+        assert torch.equal(engs[0].obs[:total], engs[1].obs[:total]), f"fused count differs at tick {t}"
+        assert torch.equal(recs[0], recs[1]), t
+    for e in engs:
+        e.set_step_records(None)
+        e.close()
+
+
 def test_step_records_equal_step_outputs():
     """nmmo_set_step_records: every wire-obs step writes, per agent, reward f32 | term | trunc |
     mask | 0 -- the bytes of the step's own outputs (over deaths and an episode end); a step
