@@ -137,7 +137,9 @@ def obs_bytes_per_env(S: int, P: int, elems: int, native: bool = False, wire_byt
 
 def pmc_traffic(cfg_name: str, kernel, envs: int):
     """HBM bytes per launch of `kernel` (a name, or a list of kernels one launch runs: the wire
-    obs gather is wire_count + wire_scan + wire_obs_kernel) from the newest committed rocprofv3 PMC
+    obs gather is wire_scan + wire_obs_kernel, after wire_count_kernel where the tick does not
+    write the count words itself; a name ending in "?" counts when the summary has it) from the
+    newest committed rocprofv3 PMC
     summary of the same workload (profiles/<round>/<cfg>/pmc.json, tools/pmc_summary.py):
     2 x FETCH_SIZE + WRITE_SIZE, gfx950-corrected, scaled per env to a launch of `envs` envs (the
     summary's launches covered its roofline.envs_per_launch, or its envs_per_gpu). None when no
@@ -148,7 +150,9 @@ def pmc_traffic(cfg_name: str, kernel, envs: int):
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", cfg_name, "pmc.json")), reverse=True):
         try:
             d = json.load(open(path))
-            tot = sum(d["kernels"][k]["hbm_bytes_per_dispatch"] for k in names)
+            ks = d["kernels"]
+            tot = sum(ks[k]["hbm_bytes_per_dispatch"] for k in names if not k.endswith("?")) + \
+                sum(ks[k[:-1]]["hbm_bytes_per_dispatch"] for k in names if k.endswith("?") and k[:-1] in ks)
             b = d.get("bench", {})
             pe = b.get("roofline", {}).get("envs_per_launch") or b.get("config", {}).get("envs_per_gpu")
             if not pe:
@@ -764,8 +768,8 @@ def measure_gather(args, name, envs, rank, world, dev, steps, warmup, dist=None,
     obs_b = obs_bytes_per_env(S, P, eng.obs_elems, wire_bytes=wire_env_bytes) * per
     if obs_avg_ms > tick_avg_ms:
         kern, byts, ms = "wire_obs_kernel", obs_b, obs_avg_ms
-        timing = ("HIP events around each wire obs gather (wire_count + wire_scan + wire_obs_kernel) on the "
-                  "launch stream")
+        timing = ("HIP events around each wire obs gather (wire_scan + wire_obs_kernel; the count words come "
+                  "from the tick, tick.hip wire_count_fused) on the launch stream")
     else:
         kern, byts, ms = "tick_kernel", tick_b, tick_avg_ms
         timing = "HIP events around each tick_kernel launch on the launch stream"
@@ -777,7 +781,7 @@ def measure_gather(args, name, envs, rank, world, dev, steps, warmup, dist=None,
                   f"comm stream one step behind",
         "kernel_ms": {"policy": None, "tick": round(tick_avg_ms, 5), "obs": round(obs_avg_ms, 5), "wrapper": None},
         "roofline": _roofline(name, kern, byts, ms, per, timing, nb, d["elapsed"] / steps, None,
-                              ["wire_count_kernel", "wire_scan_kernel", "wire_obs_kernel"] if kern == "wire_obs_kernel"
+                              ["wire_count_kernel?", "wire_scan_kernel", "wire_obs_kernel"] if kern == "wire_obs_kernel"
                               else None),
         "batches": nb,
         "shares": list(shares),
