@@ -1,8 +1,10 @@
 #!/usr/bin/env python3
 """Summarise rocprofv3 output of profiles/run_rocprof.sh into one JSON per config.
 
-Per kernel: dispatch count and mean duration (kernel trace), mean FETCH_SIZE / WRITE_SIZE per
-dispatch (separate --pmc passes) and the HBM bytes per dispatch corrected as
+Per kernel: dispatch count and mean duration (kernel trace), FETCH_SIZE / WRITE_SIZE per dispatch
+(separate --pmc passes; the median, which is the steady state: the mean also counts the few
+launches that write every obs row in full -- the first launch into a bound buffer, the resets --
+and is reported beside it) and the HBM bytes per dispatch corrected as
 MI355X_MICROARCH.md §HBM prescribes: rocprofv3 reports both counters in KiB; on gfx950
 FETCH_SIZE counts half the bytes of wide coalesced reads (doubled here), WRITE_SIZE is exact
 for 16-B-per-lane stores.
@@ -59,7 +61,10 @@ def summarise(d):
             if r.get("Counter_Name") == ctr:
                 acc[_short(r["Kernel_Name"])].append(float(r["Counter_Value"]))
         for k, v in acc.items():
-            out[k][ctr.lower() + "_kib_per_dispatch"] = sum(v) / len(v)
+            sv = sorted(v)
+            med = sv[len(sv) // 2] if len(sv) % 2 else (sv[len(sv) // 2 - 1] + sv[len(sv) // 2]) / 2
+            out[k][ctr.lower() + "_kib_per_dispatch"] = med
+            out[k][ctr.lower() + "_kib_mean"] = sum(v) / len(v)
             out[k][ctr.lower() + "_dispatches"] = len(v)
     for k, v in out.items():
         if "fetch_size_kib_per_dispatch" in v and "write_size_kib_per_dispatch" in v:
