@@ -215,8 +215,11 @@ __device__ __forceinline__ Ctx make_ctx(unsigned char* smem, const DevState& st,
   c.exch = c.items && (sy & NMMO_SYS_EXCHANGE) != 0;
   c.prof = c.items && (sy & NMMO_SYS_PROFESSION) != 0;
   c.equip = c.items && (sy & NMMO_SYS_EQUIPMENT) != 0;
-  c.foreign_any = *st.foreign != 0;  // uniform, read before any store (a scalar load)
-  c.foreign = !c.prof && c.foreign_any;
+  // DevState::foreign is loaded with the env state (load_env): a scalar load of it here was
+  // waited on by the next kernel-argument wait (SMEM returns out of order, so the compiler waits
+  // lgkmcnt(0)), one HBM round trip ahead of the state copy
+  c.foreign_any = false;
+  c.foreign = false;
   c.IC = kInv * P;
   if (c.items) {  // 16-B aligned block first (inventories are copied with 16-B accesses)
     c.inv = reinterpret_cast<uint2*>(smem + o); o += (size_t)P * kInv * 8;
@@ -397,6 +400,7 @@ __device__ __forceinline__ DepQ load_env(Ctx& c, const DevState& st, int e, bool
   // env scalars: loaded first, written to LDS after the copy has issued its loads (stored right
   // away, their wait put a whole HBM round trip ahead of the state copy)
   int ev = st.env[(size_t)e * NMMO_NE + min(tid, NMMO_NE - 1)];  // every thread: no branch join
+  int fg = *st.foreign;  // (a vector load: vmcnt retires in order, waited with the copy's loads)
   load_env_arrays(c, st, e, defer);
   DepQ dq = {};
   if (may_defer) {  // clamped indices: the tick writes only the in-range words, and only if defer
@@ -404,8 +408,10 @@ __device__ __forceinline__ DepQ load_env(Ctx& c, const DevState& st, int e, bool
     dq.v0 = dep4[min(tid, kDepU4 - 1)];
     dq.v1 = dep4[min(tid + nt, kDepU4 - 1)];
   }
-  asm volatile("" : "+v"(ev));
+  asm volatile("" : "+v"(ev), "+v"(fg));
   if (tid < NMMO_NE) c.E[tid] = ev;
+  c.foreign_any = __builtin_amdgcn_readfirstlane(fg) != 0;  // uniform, read before any store
+  c.foreign = !c.prof && c.foreign_any;
   return dq;
 }
 
