@@ -638,7 +638,7 @@ def _roofline(prof_name, kern, byts, ms, per, timing, nb, step_s, fill_gbs, pmc_
 # the other ranks split the rest. The root validates and stores every peer's buffers each step
 # besides its own compute, so it holds fewer envs; DESIGN.md §5 derives the shares from the
 # measured root and peer steps (bench C5 extra at N = 1: root_loaded / peer passes).
-ROOT_ENVS = {2: 984, 4: 832, 8: 512}
+ROOT_ENVS = {2: 984, 4: 832, 8: 448}
 XGMI_LINK_GBS = 153.6   # per xGMI link (task brief: 7 links x ~153 GB/s per GPU)
 LINK_EFF = 0.75         # the share of it the N = 8 model assumes a point-to-point send gets
 
