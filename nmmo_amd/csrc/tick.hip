@@ -470,18 +470,34 @@ __device__ __forceinline__ void store_env(const Ctx& c, const DevState& st, int 
       dst[row_field(c.slim, row) * S + i - row * S] = c.T[i];
     }
   }
-  for (int i = tid; i < S; i += nt) st.ring[(size_t)e * S + i] = c.ring[i];
-  for (int i = tid; i < kBitmapWords; i += nt) st.dep[(size_t)e * kBitmapWords + i] = c.dep[i];
+  if (state_v16(c)) {  // the ring, bitmap and item ring as 16-B words too (2-B stores wrote partial lines)
+    auto copy16 = [&](void* d, const void* s, int n) {
+      for (int i = tid; i < n; i += nt) reinterpret_cast<uint4*>(d)[i] = reinterpret_cast<const uint4*>(s)[i];
+    };
+    copy16(st.ring + (size_t)e * S, c.ring, S / 8);
+    copy16(st.dep + (size_t)e * kBitmapWords, c.dep, kDepU4);
+    if (c.items) copy16(st.iring + (size_t)e * c.IC, c.iring, c.IC / 8);
+  } else {
+    for (int i = tid; i < S; i += nt) st.ring[(size_t)e * S + i] = c.ring[i];
+    for (int i = tid; i < kBitmapWords; i += nt) st.dep[(size_t)e * kBitmapWords + i] = c.dep[i];
+    if (c.items)
+      for (int i = tid; i < c.IC; i += nt) st.iring[(size_t)e * c.IC + i] = c.iring[i];
+  }
   if (c.items) {
     const uint4* s4 = reinterpret_cast<const uint4*>(c.inv);
     uint4* d4 = reinterpret_cast<uint4*>(st.items + (size_t)e * c.P * kInv);
     for (int i = tid; i < c.P * kInv / 2; i += nt) d4[i] = s4[i];
-    for (int i = tid; i < c.IC; i += nt) st.iring[(size_t)e * c.IC + i] = c.iring[i];
   }
   if (c.tev) {  // task state (SPEC §12), when staged
-    int* dsti = reinterpret_cast<int*>(st.tstate + (size_t)e * c.P);
-    const int* srci = reinterpret_cast<const int*>(c.tsl);
-    for (int i = tid; i < c.P * (int)sizeof(NmmoTaskState) / 4; i += nt) dsti[i] = srci[i];
+    if (state_v16(c)) {
+      uint4* d4 = reinterpret_cast<uint4*>(st.tstate + (size_t)e * c.P);
+      const uint4* s4 = reinterpret_cast<const uint4*>(c.tsl);
+      for (int i = tid; i < c.P * (int)sizeof(NmmoTaskState) / 16; i += nt) d4[i] = s4[i];
+    } else {
+      int* dsti = reinterpret_cast<int*>(st.tstate + (size_t)e * c.P);
+      const int* srci = reinterpret_cast<const int*>(c.tsl);
+      for (int i = tid; i < c.P * (int)sizeof(NmmoTaskState) / 4; i += nt) dsti[i] = srci[i];
+    }
   }
 }
 
