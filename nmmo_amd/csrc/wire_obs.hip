@@ -40,9 +40,27 @@ __host__ __device__ inline size_t wo_lds_bytes() {
 }
 static_assert(kWoAgents == kAoAgents, "ao_stage_windows stages kAoAgents agents per workgroup");
 
+#ifndef NMMO_WO_STAMPS  // diagnostic: s_memtime per wave phase and per record section (tools/debug/wo_stamps.py)
+#define NMMO_WO_STAMPS 0
+#endif
+#if NMMO_WO_STAMPS
+constexpr int kWoStamps = 6;  // record: start, window materials, compaction, sections, stream, stores
+__device__ uint64_t wo_stamp_buf[1 << 17][kWoStamps];
+__device__ uint64_t wo_wave_buf[1 << 15][6];  // wave: start, prologue, windows, loop, end, env | records << 32
+#define WO_STAMP(arr, k) arr[k] = __builtin_amdgcn_s_memtime()
+#else
+#define WO_STAMP(arr, k) \
+  do {                   \
+  } while (0)
+#endif
 template <bool kWrap>
 __global__ void __launch_bounds__(64 * kWoWaves) wire_obs_kernel(ObsParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+#if NMMO_WO_STAMPS
+  uint64_t wv_[6], rs_[kWoStamps];
+  int nrec = 0;
+  WO_STAMP(wv_, 0);
+#endif
   const int S = p.S, P = p.P;
   constexpr int Sp = kWoAgents;  // T's stride: column f of the workgroup's agent la at T[f * Sp + la]
   int16_t* T = reinterpret_cast<int16_t*>(smem);  // [31][kWoAgents]
@@ -111,7 +129,13 @@ __global__ void __launch_bounds__(64 * kWoWaves) wire_obs_kernel(ObsParams p) {
   // the workgroup's window rows and item words into LDS (T is per workgroup: agent a at a - a0),
   // so the agent loop issues no global load: an in-loop prefetch after the previous record's
   // stores waited for them (vmcnt retires in order)
+#if NMMO_WO_STAMPS
+  WO_STAMP(wv_, 1);
+#endif
   ao_stage_windows(p, e, g, T - a0, Sp, wst, ist);  // (barrier inside)
+#if NMMO_WO_STAMPS
+  WO_STAMP(wv_, 2);
+#endif
   const uint8_t* wsb = reinterpret_cast<const uint8_t*>(wst);
 
   uint32_t* visw = visw_all + w * 128;
@@ -149,6 +173,11 @@ __global__ void __launch_bounds__(64 * kWoWaves) wire_obs_kernel(ObsParams p) {
     const uint2 it = lane < kInv ? ist[la * kInv + lane] : make_uint2(0u, 0u);  // lanes 0..11
     const uint32_t mv = ao_move_bits(wm[1]);
 
+#if NMMO_WO_STAMPS
+    WO_STAMP(rs_, 0);
+    asm volatile("" ::"v"(wm[0]), "v"(wm[3]));
+    WO_STAMP(rs_, 1);
+#endif
     ao_compact(pr, S, r, c, visw);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -167,7 +196,14 @@ __global__ void __launch_bounds__(64 * kWoWaves) wire_obs_kernel(ObsParams p) {
     ag.mv = mv;
     // the ActionTargets as what they are made of (wire.h v4): head words m5 / m6 and a bit stream
     // of the first nv entries of the 3 target sections and the first ninv of the 4 inventory ones
+#if NMMO_WO_STAMPS
+    WO_STAMP(rs_, 2);
+#endif
     const AoSections x = ao_sections<kWrap>(p, T, Sp, visw, ag, it);
+#if NMMO_WO_STAMPS
+    asm volatile("" ::"s"(x.s0), "s"(x.s3));
+    WO_STAMP(rs_, 3);
+#endif
     int pp1 = 0;  // 1 + the SellPrice entry the wrapper cleared
     if (exch) {
       const uint64_t z0 = ~x.s10[0], z1 = ~x.s10[1] & low_bits(kSecN[10] - 64);
@@ -203,6 +239,10 @@ __global__ void __launch_bounds__(64 * kWoWaves) wire_obs_kernel(ObsParams p) {
       const uint64_t wd = k < 64 ? lo : hi;
       W[q] = __ballot(64 * q + lane < B && ((wd >> (k & 63)) & 1ull));
     }
+#if NMMO_WO_STAMPS
+    asm volatile("" ::"s"(W[0]), "s"(W[5]));
+    WO_STAMP(rs_, 4);
+#endif
     uint8_t* rec = wenv + woff[a];
     {
       const int task = __builtin_amdgcn_readlane(my_task, j);
@@ -243,10 +283,21 @@ __global__ void __launch_bounds__(64 * kWoWaves) wire_obs_kernel(ObsParams p) {
         if (h < H) dst[h] = (int16_t)v16;
       }
     }
+#if NMMO_WO_STAMPS
+    WO_STAMP(rs_, 5);
+    if (lane == 0) {
+#pragma unroll
+      for (int k = 0; k < kWoStamps; k++) wo_stamp_buf[(size_t)e * P + a][k] = rs_[k];
+    }
+    nrec++;
+#endif
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the next agent reuses visw / wmat
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
+#if NMMO_WO_STAMPS
+  WO_STAMP(wv_, 3);
+#endif
   if (p.recs && my_on) reinterpret_cast<uint2*>(p.recs)[(size_t)e * P + my_a] = my_rec;
   if (p.fault_dst && e == 0 && g == 0 && tid == 0) {  // nmmo_fault_into's effect (the tick ran before)
     const int32_t fw = *p.fault;
@@ -281,6 +332,15 @@ __global__ void __launch_bounds__(64 * kWoWaves) wire_obs_kernel(ObsParams p) {
     }
     for (int b = kEntRow * ne + tid; b < wire_table_bytes(ne); b += blockDim.x) wenv[b] = 0;
   }
+#if NMMO_WO_STAMPS
+  WO_STAMP(wv_, 4);
+  wv_[5] = (uint64_t)e | (uint64_t)nrec << 32;
+  if (lane == 0) {
+    const int wi = blockIdx.x * kWoWaves + w;
+    if (wi < (1 << 15))
+      for (int k = 0; k < 6; k++) wo_wave_buf[wi][k] = wv_[k];
+  }
+#endif
 }
 
 hipError_t launch_wire_obs(const ObsParams& p, hipStream_t stream) {
@@ -296,3 +356,19 @@ hipError_t launch_wire_obs(const ObsParams& p, hipStream_t stream) {
 }
 
 }  // namespace nmmo
+
+#if NMMO_WO_STAMPS
+extern "C" __attribute__((visibility("default"))) int nmmo_debug_wo_stamps(void* rec, size_t rec_bytes, void* wave,
+                                                                         size_t wave_bytes) {
+  if (rec_bytes > sizeof(nmmo::wo_stamp_buf)) rec_bytes = sizeof(nmmo::wo_stamp_buf);
+  if (wave_bytes > sizeof(nmmo::wo_wave_buf)) wave_bytes = sizeof(nmmo::wo_wave_buf);
+  if (hipMemcpyFromSymbol(rec, HIP_SYMBOL(nmmo::wo_stamp_buf), rec_bytes) != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(wave, HIP_SYMBOL(nmmo::wo_wave_buf), wave_bytes) != hipSuccess) return -1;
+  void* d = nullptr;
+  if (hipGetSymbolAddress(&d, HIP_SYMBOL(nmmo::wo_stamp_buf)) != hipSuccess || hipMemset(d, 0, sizeof(nmmo::wo_stamp_buf)) != hipSuccess)
+    return -1;
+  if (hipGetSymbolAddress(&d, HIP_SYMBOL(nmmo::wo_wave_buf)) != hipSuccess || hipMemset(d, 0, sizeof(nmmo::wo_wave_buf)) != hipSuccess)
+    return -1;
+  return hipDeviceSynchronize() == hipSuccess ? 0 : -1;
+}
+#endif
