@@ -236,19 +236,21 @@ __device__ __forceinline__ void ao_env_group(int n_envs, int G, int& e, int& g) 
 // the next agent started.
 constexpr int kAoWinRowBytes = 20;
 constexpr int kAoWinAgentBytes = 15 * kAoWinRowBytes;  // 300
-__host__ __device__ inline size_t ao_win_lds() { return (size_t)kAoAgents * kAoWinAgentBytes + (size_t)kAoAgents * kInv * 8; }
+__host__ __device__ inline size_t ao_win_lds(int agents = kAoAgents) {
+  return (size_t)agents * kAoWinAgentBytes + (size_t)agents * kInv * 8;
+}
 // positions of agents not in the realm are clamped so their (unused) window reads stay in the map
 __device__ __forceinline__ int ao_clamp_pos(int x) { return min(max(x, kVision), kSize - 1 - kVision); }
 // `before_barrier` runs after the LDS writes (every thread), ahead of the barrier that publishes them.
 struct AoNoop {
   __device__ void operator()() const {}
 };
-template <typename F = AoNoop>
+template <int kAgents = kAoAgents, typename F = AoNoop>
 __device__ inline void ao_stage_windows(const ObsParams& p, int e, int g, const int16_t* T, int Sp, uint32_t* ws, uint2* is,
                                         F before_barrier = F()) {
   const int tid = threadIdx.x, P = p.P;
-  const int la = tid / 15, row = tid - 15 * la, a = g * kAoAgents + la;
-  const bool win = tid < kAoAgents * 15 && a < P;
+  const int la = tid / 15, row = tid - 15 * la, a = g * kAgents + la;
+  const bool win = tid < kAgents * 15 && a < P;
   uint32_t d[5] = {0u, 0u, 0u, 0u, 0u};
   if (win) {
     const int r = ao_clamp_pos(T[F_ROW * Sp + a]), c = ao_clamp_pos(T[F_COL * Sp + a]);
@@ -258,13 +260,13 @@ __device__ inline void ao_stage_windows(const ObsParams& p, int e, int g, const 
     for (int k = 0; k < 5; k++) d[k] = src[k];
   }
   uint2 iw = make_uint2(0u, 0u);
-  const bool itm = tid < kAoAgents * kInv && g * kAoAgents + tid / kInv < P;
-  if (itm) iw = p.items[((size_t)e * P + g * kAoAgents) * kInv + tid];
+  const bool itm = tid < kAgents * kInv && g * kAgents + tid / kInv < P;
+  if (itm) iw = p.items[((size_t)e * P + g * kAgents) * kInv + tid];
   if (win) {
 #pragma unroll
     for (int k = 0; k < 5; k++) ws[tid * 5 + k] = d[k];  // tid = la * 15 + row
   }
-  if (tid < kAoAgents * kInv) is[tid] = iw;
+  if (tid < kAgents * kInv) is[tid] = iw;
   before_barrier();
   __syncthreads();
 }

@@ -15,10 +15,21 @@
 
 namespace nmmo {
 
+// The native kernel's workgroup: 32 agents on 8 waves (4 per wave, as agent_obs.h's 16 on 4), so
+// the env's staged columns serve twice the rows per workgroup (round 6, same box: C4-native
+// 359 -> 363 M, the kernel alone 0.093 -> 0.096 ms but overlapping the other batch's tick better;
+// the flat and wire kernels measured slower with it and keep 16 on 4)
+#ifndef NMMO_NO_WAVES  // (A/B knob: tools/debug/variants.py)
+#define NMMO_NO_WAVES 8
+#define NMMO_NO_AGENTS 32
+#endif
+constexpr int kNoWaves = NMMO_NO_WAVES, kNoAgents = NMMO_NO_AGENTS;
+static_assert(kNoAgents / kNoWaves == kAoAgents / kAoWaves, "agents per wave: agent_obs.h's lane layouts");
+
 // LDS: agent_obs.h's entity staging | listings (price | owner << 8, u16) | per-wave visible rows
-// | the workgroup's staged window rows and item words. 35.8 KB at S = 384: 4 workgroups per CU.
+// | the workgroup's staged window rows and item words. ~44 KB at S = 384 with 32 agents.
 __host__ __device__ inline size_t no_lds_bytes(int S) {
-  return ao_entity_lds(S) + (size_t)NMMO_MARKET_ROWS * 2 + (size_t)kAoWaves * 128 * 4 + ao_win_lds();
+  return ao_entity_lds(S) + (size_t)NMMO_MARKET_ROWS * 2 + (size_t)kNoWaves * 128 * 4 + ao_win_lds(kNoAgents);
 }
 constexpr int kNoEntity = 2, kNoInv = kNoEntity + kNObs * NMMO_N_ENTITY_COLS, kNoTile = kNoInv + kInv * 16,
               kNoTask = kNoTile + 225 * 3;  // int16 offsets in the int16 part (SPEC §8b)
@@ -30,18 +41,18 @@ constexpr int kNoImgWords = NMMO_NATIVE_MASK_BYTES / 32;  // 50: the mask image,
 // (Capped at 96 VGPRs for a fifth wave per SIMD it measured 0.155 ms per 512 envs against 0.143
 // uncapped at 109 VGPRs / 4 waves.)
 template <bool kWrap>
-__global__ void __launch_bounds__(64 * kAoWaves) native_obs_kernel(ObsParams p) {
+__global__ void __launch_bounds__(64 * kNoWaves) native_obs_kernel(ObsParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int S = p.S, P = p.P, Sp = ao_stride(S);
   int16_t* T = reinterpret_cast<int16_t*>(smem);
   uint32_t* pk = reinterpret_cast<uint32_t*>(smem + ao_entity_lds(S) - (size_t)(kMaxSlots + 64) * 4);
   uint16_t* mpo = reinterpret_cast<uint16_t*>(pk + kMaxSlots + 64);           // [1024] price | owner << 8
   uint32_t* visw_all = reinterpret_cast<uint32_t*>(mpo + NMMO_MARKET_ROWS);   // [4][128]
-  uint32_t* wst = visw_all + kAoWaves * 128;                                  // [16][15][5] window rows
-  uint2* ist = reinterpret_cast<uint2*>(wst + kAoAgents * kAoWinAgentBytes / 4);  // [16][12] item words
+  uint32_t* wst = visw_all + kNoWaves * 128;                                  // [16][15][5] window rows
+  uint2* ist = reinterpret_cast<uint2*>(wst + kNoAgents * kAoWinAgentBytes / 4);  // [16][12] item words
 #ifdef NMMO_NO_XCD  // 1-D grid, an env's groups back to back on one XCD (agent_obs.h ao_env_group)
   int el, g;
-  ao_env_group(p.env_list ? p.n_list : p.n_envs, (p.P + kAoAgents - 1) / kAoAgents, el, g);
+  ao_env_group(p.env_list ? p.n_list : p.n_envs, (p.P + kNoAgents - 1) / kNoAgents, el, g);
 #else
   const int el = blockIdx.x, g = blockIdx.y;
 #endif
@@ -54,13 +65,13 @@ __global__ void __launch_bounds__(64 * kAoWaves) native_obs_kernel(ObsParams p) 
   AoStage sg;
   ao_stage_load(p, e, sg);
   const int16_t* E = p.ent + (size_t)e * NMMO_NF * S;
-  const int per_wave = (kAoAgents + kAoWaves - 1) / kAoWaves;
-  const int abase = g * kAoAgents + w;
+  const int per_wave = (kNoAgents + kNoWaves - 1) / kNoWaves;
+  const int abase = g * kNoAgents + w;
   int my_task = 0, my_prev = -1, my_alive = 0;  // lane j: agent abase + 4 j
   uint64_t my_z = 0, my_s = 0;                  // its row state tag and word (ObsParams::zrow / zst)
-  const bool mine = lane < per_wave && abase + kAoWaves * lane < P;
+  const bool mine = lane < per_wave && abase + kNoWaves * lane < P;
   {  // every lane loads (a clamped agent), the values kept for its own agent below
-    const int aj = min(abase + kAoWaves * min(lane, per_wave - 1), P - 1);
+    const int aj = min(abase + kNoWaves * min(lane, per_wave - 1), P - 1);
     const size_t ai = (size_t)e * P + aj;
     my_task = p.assign[ai];
     my_alive = E[F_ALIVE * S + aj];
@@ -79,7 +90,7 @@ __global__ void __launch_bounds__(64 * kAoWaves) native_obs_kernel(ObsParams p) 
   const int nm = min(max(sg.nm, 0), NMMO_MARKET_ROWS);
   if (p.wmcount && g == 0 && tid == 0) p.wmcount[e] = nm;  // nmmo_wire_pack reads this launch's count
   const uint2 lwd = ao_listing_load(p, e, sg);
-  ao_stage_windows(p, e, g, T, Sp, wst, ist, [&]() {  // the listings, ascending row (published by its barrier)
+  ao_stage_windows<kNoAgents>(p, e, g, T, Sp, wst, ist, [&]() {  // the listings, ascending row (published by its barrier)
     if (tid < nm) mpo[tid] = (uint16_t)(it_price(lwd) | ((sg.mv >> 16) & 255) << 8);
     for (int j = tid + (int)blockDim.x; j < nm; j += blockDim.x) {  // (more listings than threads)
       const int v = p.mlist[(size_t)e * NMMO_MARKET_ROWS + j];
@@ -131,7 +142,7 @@ __global__ void __launch_bounds__(64 * kAoWaves) native_obs_kernel(ObsParams p) 
   }
 
   for (int j = 0; j < per_wave; j++) {
-    const int a = abase + kAoWaves * j;
+    const int a = abase + kNoWaves * j;
     if (a >= P) break;
     uint8_t* nrow = nenv + (size_t)a * NMMO_NATIVE_ROW_BYTES;
     if (!alive(j)) {  // not in the realm: a zero row
@@ -154,11 +165,11 @@ __global__ void __launch_bounds__(64 * kAoWaves) native_obs_kernel(ObsParams p) 
     const int gold = __builtin_amdgcn_readfirstlane(T[F_GOLD * Sp + a]);
     const int aid = __builtin_amdgcn_readfirstlane(T[F_ID * Sp + a]);
     // window tile t = lane + 64 i and item word lane, from the workgroup's staging
-    const uint8_t* wa = wsb + (a - g * kAoAgents) * kAoWinAgentBytes + ((c - kVision) & 3);
+    const uint8_t* wa = wsb + (a - g * kNoAgents) * kAoWinAgentBytes + ((c - kVision) & 3);
     uint32_t wm[4];
 #pragma unroll
     for (int i = 0; i < 4; i++) wm[i] = lane + 64 * i < 225 ? wa[ao_win_off(wo, i)] : 0u;
-    const uint2 it = lane < kInv ? ist[(a - g * kAoAgents) * kInv + lane] : make_uint2(0u, 0u);
+    const uint2 it = lane < kInv ? ist[(a - g * kNoAgents) * kInv + lane] : make_uint2(0u, 0u);
     const uint32_t mv = ao_move_bits(wm[1]);
     const int ninv = __builtin_ctzll(~__ballot(lane < kInv && it_type(it) != 0));  // occupied prefix
 
@@ -307,9 +318,9 @@ hipError_t launch_native_obs(const ObsParams& p, hipStream_t stream) {
   const int ne = list_grid(p.env_list, p.n_list, p.n_envs);
   if (ne <= 0) return hipSuccess;
 #ifdef NMMO_NO_XCD
-  const dim3 grid(ne * ((p.P + kAoAgents - 1) / kAoAgents)), block(64 * kAoWaves);
+  const dim3 grid(ne * ((p.P + kNoAgents - 1) / kNoAgents)), block(64 * kNoWaves);
 #else
-  const dim3 grid(ne, (p.P + kAoAgents - 1) / kAoAgents), block(64 * kAoWaves);
+  const dim3 grid(ne, (p.P + kNoAgents - 1) / kNoAgents), block(64 * kNoWaves);
 #endif
   const size_t lds = no_lds_bytes(p.S);
   if (p.wflags) hipLaunchKernelGGL(native_obs_kernel<true>, grid, block, lds, stream, p);
